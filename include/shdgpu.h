@@ -1,0 +1,360 @@
+/*
+ * shdgpu.h -- C-ABI of libshdgpu, the MI355X-native simulated-network core.
+ *
+ * libshdgpu replaces two pieces of Shadow 1.14 (joskid/shadow-1):
+ *
+ *   1. the topology PATH CACHE (src/main/routing/topology.c), which maps a
+ *      (source vertex, destination vertex) pair to a latency (ms) and a
+ *      reliability, built lazily with igraph Dijkstra;
+ *   2. the conservative round/window PACKET EVENT LOOP (src/main/core/scheduler/,
+ *      master.c, slave.c, worker.c) that delivers packets between hosts through
+ *      the path cache, the reliability drop, the per-host RNG, the CoDel router
+ *      queue and the receive token bucket.
+ *
+ * Conventions: plain C types only, opaque handles, every call returns 0 or a
+ * negative errno-style status (SHD_E*).  No exceptions cross the ABI.  The
+ * library owns device buffers; callers own host buffers (copied in).  An engine
+ * handle is driven by ONE host thread and is not re-entrant.
+ *
+ * Reference interfaces each entry point replaces are cited per declaration
+ * (paths relative to the reference repository root).  The ctypes / C binding a
+ * Shadow maintainer would add is shown in INTEGRATION.md.
+ */
+#ifndef SHDGPU_H
+#define SHDGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- status */
+#define SHD_OK 0
+#define SHD_EINVAL (-22)     /* bad argument / invalid graph                 */
+#define SHD_ENOMEM (-12)     /* host or device allocation failed             */
+#define SHD_ENODEV (-19)     /* no HIP device / HIP runtime error            */
+#define SHD_EOVERFLOW (-75)  /* a fixed-capacity device queue overflowed     */
+#define SHD_ERANGE (-34)     /* path longer than supported / bad index       */
+#define SHD_EAMBIG (-125)    /* first-touch drop decision ambiguous */
+#define SHD_ENOTCONN (-107)  /* topology not strongly connected (topology.c:800-806) */
+
+/* time: unsigned nanoseconds, SimulationTime (core/support/definitions.h:18-64) */
+#define SHD_SIMTIME_INVALID UINT64_MAX
+#define SHD_SIMTIME_MAX (UINT64_MAX - 1)
+#define SHD_MS 1000000ULL
+#define SHD_SEC 1000000000ULL
+#define SHD_MTU 1500u                 /* CONFIG_MTU, definitions.h:188            */
+#define SHD_HEADER_UDP 42u            /* CONFIG_HEADER_SIZE_UDPIPETH, definitions.h:176 */
+#define SHD_MIN_RANDOM_PORT 10000u    /* MIN_RANDOM_PORT, definitions.h:94        */
+#define SHD_PHOLD_LISTEN_PORT 8998u   /* PHOLD_LISTEN_PORT, src/test/phold/test_phold.c:34 */
+
+/* ------------------------------------------------------------ graph input */
+/*
+ * A topology graph as read from graphml (topology.c:371-399, igraph document
+ * order): vertex ids and edge ids are document order.  For undirected graphs an
+ * edge (a,b) is stored once.  Absent numeric attributes are NaN
+ * (_topology_findVertexAttributeDouble treats NaN as absent, topology.c:330-347).
+ */
+typedef struct shd_graph {
+    int32_t n_vertices;
+    int32_t n_edges;
+    int32_t directed;               /* graphml edgedefault="directed"          */
+    int32_t prefer_direct;          /* graph attr preferdirectpaths true/yes/1 (topology.c:760-790) */
+    const int32_t* edge_src;        /* [E] document order                      */
+    const int32_t* edge_dst;        /* [E]                                     */
+    const double* edge_latency;     /* [E] ms, > 0 (topology.c:1070)          */
+    const double* edge_loss;        /* [E] in [0,1] (topology.c:1090)         */
+    const double* vertex_loss;      /* [V] or NULL; NaN = attribute absent    */
+} shd_graph;
+
+/* Validation of topology_new (topology.c:1187-1210): strongly connected, one
+ * cluster, latency > 0, loss in [0,1].  Also reports the completeness test of
+ * _topology_isComplete (topology.c:450-552). */
+typedef struct shd_graph_props {
+    int32_t is_connected;
+    int32_t is_complete;
+    int32_t is_directed;
+    int32_t prefer_direct;
+    int32_t n_self_loops;
+    int32_t max_out_degree;
+} shd_graph_props;
+int shd_graph_check(const shd_graph* g, shd_graph_props* out);
+
+/* graphml loader (libxml2, the parser igraph 0.7.1 uses).  Replaces
+ * igraph_read_graph_graphml + the attribute extraction of topology.c:371-399,
+ * 565-722, 1212-1246.  Arrays are allocated by the library; free with
+ * shd_graphml_free.  Vertex string attributes are returned for attach. */
+typedef struct shd_graphml {
+    shd_graph g;
+    double* bw_down;                /* [V] vertex bandwidthdown (KiB/s), NaN if absent */
+    double* bw_up;                  /* [V] vertex bandwidthup                  */
+    char** vertex_id;               /* [V] "id" attribute (graphml node id)    */
+    char** vertex_ip;               /* [V] "ip" or NULL                        */
+    char** vertex_citycode;         /* [V] or NULL                             */
+    char** vertex_countrycode;      /* [V] or NULL                             */
+    char** vertex_geocode;          /* [V] or NULL                             */
+    char** vertex_type;             /* [V] or NULL                             */
+    double* edge_jitter;            /* [E] NaN if absent                       */
+} shd_graphml;
+int shd_graphml_load_file(const char* path, shd_graphml** out);
+int shd_graphml_load_string(const char* xml, size_t len, shd_graphml** out);
+void shd_graphml_free(shd_graphml* gm);
+
+/* ------------------------------------------------------------ path cache */
+/*
+ * Path-cache build.  Replaces the lazy cache of _topology_getPathEntry
+ * (topology.c:1969-2051) and everything it calls:
+ *   direct paths  _topology_lookupDirectPath        topology.c:1877-1927
+ *   source rows   _topology_computeSourcePaths      topology.c:1655-1875
+ *                 (igraph_get_shortest_paths_dijkstra, topology.c:1756)
+ *   properties    _topology_computePathProperties   topology.c:1407-1523
+ *   self paths    _topology_computeShortestPathToSelf topology.c:1545-1653
+ *
+ * The device computes, for every attached source vertex, its full row to every
+ * attached target (the values _topology_computeSourcePaths would store), the
+ * direct-path value of every adjacent attached pair and the "2 x min incident
+ * edge" self value.  The reference's write-once / first-touch selection rules
+ * (topology.c:1307-1336, 1988-1990, 2034-2037) are applied on top by
+ * shd_pc_lookup (host, low rate) and by the engine (device, per packet).
+ *
+ * Tables are [n_attached][n_attached] row-major f64 in HBM, indexed by the
+ * position of a vertex in the `attached` array given at creation.
+ */
+typedef struct shd_pc shd_pc;
+
+#define SHD_PC_FORCE_ROWS 0x1u   /* compute SSSP rows even on complete graphs (C2 forced mode) */
+#define SHD_PC_NO_TABLES_ON_HOST 0x2u
+
+typedef struct shd_pc_info {
+    int32_t n_vertices;
+    int32_t n_attached;
+    int32_t is_complete;
+    int32_t is_directed;
+    int32_t prefer_direct;
+    int32_t rows_computed;          /* rows built (0 in pure direct mode)      */
+    int64_t n_ties;                 /* vertices whose shortest-path parent was not unique */
+    int32_t max_hops;               /* longest shortest path (edges)           */
+    int32_t sssp_iterations_max;    /* deepest frontier iteration count        */
+    int32_t n_unroutable;           /* row entries with no path (self without self-loop) */
+    double min_latency_ms;          /* min over all table latencies (topology.c:1374-1378) */
+    double build_ms_device;         /* device time of the table build (HIP events) */
+    double build_ms_sssp;           /* device time of the SSSP-row kernel alone */
+    double build_ms_props;          /* device time of the path-properties kernel */
+    double build_ms_direct;         /* device time of the direct-table kernel   */
+} shd_pc_info;
+
+/* attached: vertex ids with >=1 attached host (topology.c:2393, verticesWithAttachedHosts) */
+int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_t n_attached,
+                  uint32_t flags, int device, shd_pc** out);
+int shd_pc_build(shd_pc* pc);
+int shd_pc_get_info(const shd_pc* pc, shd_pc_info* out);
+/* D2H copy of source rows [row0, row0+nrows) of the row tables (lat ms, rel) */
+int shd_pc_copy_rows(shd_pc* pc, int32_t row0, int32_t nrows, double* lat, double* rel);
+/* D2H copy of the direct tables (only adjacent pairs valid; NaN elsewhere) */
+int shd_pc_copy_direct(shd_pc* pc, int32_t row0, int32_t nrows, double* lat, double* rel);
+/* D2H copy of the per-attached-vertex self values (2*min incident edge) */
+int shd_pc_copy_self(shd_pc* pc, double* lat, double* rel);
+/* Lazy lookup with the reference's first-touch semantics (serial order of the
+ * calls = the reference's serial event order).  Replaces topology_getLatency /
+ * topology_getReliability (topology.c:2065-2087).  Returns latency -1 and
+ * reliability -1 when the reference would (error path, topology.c:2040-2046). */
+int shd_pc_lookup(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex, double* lat, double* rel);
+/* topology_incrementPathPacketCounter (topology.c:2053-2063) + read back */
+int shd_pc_count_packet(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex);
+int shd_pc_packet_count(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex, uint64_t* count);
+/* master_updateMinTimeJump / _master_getMinTimeJump (master.c:133-159):
+ * (u64)floor(min stored latency ms) * 1e6 ns, 10 ms default if 0, >= runahead */
+int shd_pc_min_time_jump(shd_pc* pc, uint64_t runahead_ns, uint64_t* jump_ns);
+void shd_pc_destroy(shd_pc* pc);
+
+/* ------------------------------------------------------------ RNG / seeds */
+/* glibc rand_r as used by utility/random.c:32-51 */
+int32_t shd_rand_r(uint32_t* state);
+double shd_next_double(uint32_t* state);          /* random.c:39-43 */
+uint32_t shd_next_uint(uint32_t* state);          /* random.c:45-51 */
+/* seed chain master.c:95,417 -> slave.c:182,198 -> slave.c:301 (registration order) */
+int shd_seed_chain(uint32_t options_seed, int32_t n_hosts, uint32_t* host_seeds);
+
+/* ------------------------------------------------------------ attach */
+/* _topology_findAttachmentVertex (topology.c:2248-2369): hint filtering, exact
+ * IP match, longest-prefix match, else random pick with the host RNG
+ * (one nextDouble draw, topology.c:2326-2334).  Hints may be NULL. */
+int shd_topology_attach(const shd_graphml* gm, uint32_t* host_rng_state, const char* ip_hint,
+                        const char* citycode_hint, const char* countrycode_hint,
+                        const char* geocode_hint, const char* type_hint,
+                        int32_t* vertex_out, uint64_t* bw_down_out, uint64_t* bw_up_out);
+
+/* ------------------------------------------------------------ engine */
+/*
+ * The packet event loop for the PHOLD-UDP model (DESIGN.md section "Model"):
+ * per-host application from src/test/phold/test_phold.c on the reference's own
+ * socket / interface / router / worker path:
+ *   worker_sendPacket            core/worker.c:260-321
+ *   _worker_runDeliverPacketTask core/worker.c:253-258, routing/router.c:104-133
+ *   CoDel                        routing/router_queue_codel.c:113-267
+ *   token buckets + refill       host/network_interface.c:102-226, 421-455, 519-579
+ *   event order                  core/work/event.c:110-153
+ *   window / rounds              core/master.c:450-480, core/slave.c:413-466
+ * Hosts [host_begin, host_end) of the model live on this engine's device
+ * (one engine per GPU; see DESIGN.md "Multi-GPU").
+ */
+typedef struct shd_model {
+    int32_t n_hosts;
+    int32_t _pad0;
+    const int32_t* host_vertex;     /* [H] graph vertex id                     */
+    const uint32_t* host_rng;       /* [H] RNG state at boot (after attach draw) */
+    const uint64_t* bw_down_kibps;  /* [H]                                     */
+    const uint64_t* bw_up_kibps;    /* [H]                                     */
+    const double* dest_cum;         /* [H] PHOLD cumulative weights (test_phold.c:160-178) */
+    uint64_t end_time;              /* <shadow stoptime> / kill time (ns)      */
+    uint64_t bootstrap_end;         /* <shadow bootstraptime> (ns)             */
+    uint64_t heartbeat_interval;    /* --heartbeat-frequency (ns), options.c:85 */
+    uint64_t app_start;             /* <application starttime> (ns)            */
+    uint32_t load;                  /* PHOLD load=                             */
+    uint32_t payload;               /* message bytes (PHOLD sends 1)           */
+    uint32_t trace;                 /* record delivered-packet trace           */
+    uint32_t evq_cap;               /* per-host event heap capacity (0=default) */
+    uint32_t inbox_cap;             /* per-host per-round inbound capacity     */
+    uint32_t codelq_cap;            /* per-host router queue capacity          */
+    uint32_t txq_cap;               /* per-host interface send queue capacity  */
+    uint32_t _pad1;
+} shd_model;
+
+/* one event (32 B): key (time, dst, src, seq) = event_compare, event.c:110-153 */
+typedef struct shd_event {
+    uint64_t time;
+    uint64_t seq;                   /* srcHostEventID (host_getNewEventID, host.c:397) */
+    uint32_t src;
+    uint32_t dst;
+    uint32_t pkt;                   /* packet id on src (host_getNewPacketID) */
+    uint32_t kind;                  /* SHD_EV_*                                */
+} shd_event;
+
+enum {
+    SHD_EV_HEARTBEAT = 1,   /* tracker_heartbeat, host/tracker.c:566-611            */
+    SHD_EV_REFILL = 2,      /* _networkinterface_refillTokenBucketsCB, n_i.c:163-183 */
+    SHD_EV_REFILL_LO = 3,   /* loopback interface refill (one at boot)               */
+    SHD_EV_APP_START = 4,   /* process start task, host/process.c:1344               */
+    SHD_EV_PACKET = 5,      /* _worker_runDeliverPacketTask, worker.c:253            */
+    SHD_EV_LOCAL = 6,       /* loopback shortcut +1 ns, network_interface.c:548-555 */
+    SHD_EV_NOTIFY = 7       /* epoll notification +1 ns, descriptor/epoll.c:345-365 */
+};
+
+/* trace record (32 B): one per packet state change, compared as a multiset */
+typedef struct shd_trace_rec {
+    uint64_t time;
+    uint64_t seq;                   /* event seq for ARRIVE, else 0            */
+    uint32_t host;                  /* host where it happened                  */
+    uint32_t peer;                  /* the other host of the packet            */
+    uint32_t pkt;                   /* packet id on its source host            */
+    uint32_t kind;                  /* SHD_TR_*                                */
+} shd_trace_rec;
+
+enum {
+    SHD_TR_SENT = 1,        /* PDS_INET_SENT at the sender (worker.c:300)            */
+    SHD_TR_INET_DROP = 2,   /* PDS_INET_DROPPED (worker.c:319)                       */
+    SHD_TR_ARRIVE = 3,      /* deliver event executed = PDS_ROUTER_ENQUEUED          */
+    SHD_TR_CODEL_DROP = 4,  /* PDS_ROUTER_DROPPED in CoDel (router_queue_codel.c:135) */
+    SHD_TR_RECV = 5,        /* PDS_RCV_INTERFACE_RECEIVED (network_interface.c:380)  */
+    SHD_TR_IF_DROP = 6,     /* PDS_RCV_INTERFACE_DROPPED (no bound socket)           */
+    SHD_TR_LOCAL = 7        /* loopback shortcut delivery                            */
+};
+
+/* per-host end state, compared bit for bit against the oracle */
+typedef struct shd_host_digest {
+    uint64_t ev_seq;
+    uint64_t rx_remaining;
+    uint64_t tx_remaining;
+    uint64_t codel_total;
+    uint64_t codel_interval_expire;
+    uint64_t codel_next_drop;
+    uint64_t n_events;
+    uint64_t n_pkt_events;
+    uint64_t n_sent;
+    uint64_t n_inet_drop;
+    uint64_t n_codel_drop;
+    uint64_t n_recv;
+    uint32_t rng;
+    uint32_t pkt_seq;
+    uint32_t codel_mode;
+    uint32_t codel_count;
+    uint32_t codel_drop_count;
+    uint32_t codel_drop_count_last;
+    uint32_t unread;
+    uint32_t flags;
+} shd_host_digest;
+
+typedef struct shd_round_summary {
+    uint64_t window_start;
+    uint64_t window_end;
+    uint64_t next_time;             /* min next event time on this engine      */
+    uint64_t n_events;              /* events executed this round              */
+    uint64_t n_pkt_events;          /* packet-deliver events executed          */
+    uint64_t n_pending;             /* sends awaiting first-touch resolution   */
+    uint64_t n_remote;              /* events for hosts of other engines       */
+    uint32_t error;                 /* SHD_ERR_* bits                          */
+    uint32_t _pad;
+} shd_round_summary;
+
+enum {
+    SHD_ERR_EVQ_OVERFLOW = 1, SHD_ERR_INBOX_OVERFLOW = 2, SHD_ERR_CODELQ_OVERFLOW = 4,
+    SHD_ERR_TXQ_OVERFLOW = 8, SHD_ERR_AMBIGUOUS = 16, SHD_ERR_PENDING_OVERFLOW = 32,
+    SHD_ERR_TRACE_OVERFLOW = 64, SHD_ERR_REMOTE_OVERFLOW = 128
+};
+
+typedef struct shd_run_stats {
+    uint64_t n_rounds;
+    uint64_t n_events;
+    uint64_t n_pkt_events;
+    uint64_t n_pending_resolved;
+    uint64_t window_ns;             /* the serial-equivalent window W          */
+    uint64_t final_time;
+    double device_ms_round_kernel;  /* HIP-event time inside the round kernel  */
+    double wall_ms;
+    uint32_t error;
+    uint32_t _pad;
+} shd_run_stats;
+
+typedef struct shd_eng shd_eng;
+int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin, int32_t host_end,
+                   int device, shd_eng** out);
+/* the serial-equivalent window: min over attached pairs of ceil(lat*1e6) ns */
+int shd_eng_window(shd_eng* e, uint64_t* window_ns);
+/* host_boot for every local host (host.c:372-390) at t=0 */
+int shd_eng_boot(shd_eng* e);
+/* one round [window_start, window_end) on this engine; remote-bound events are
+ * kept in the outbox until shd_eng_take_remote */
+int shd_eng_run_round(shd_eng* e, uint64_t window_start, uint64_t window_end,
+                      shd_round_summary* out);
+/* whole single-engine run to end_time (rounds of W) */
+int shd_eng_run(shd_eng* e, shd_run_stats* out);
+/* multi-GPU exchange (DESIGN.md "Multi-GPU"): device pointer + count of events
+ * bound for other engines, grouped by destination engine; and ingest of
+ * events received from other engines (device pointer) */
+int shd_eng_remote_counts(shd_eng* e, int32_t n_parts, const int32_t* part_begin,
+                          uint64_t* counts_out);
+int shd_eng_remote_buffer(shd_eng* e, void** dev_ptr, uint64_t* n_events);
+int shd_eng_ingest(shd_eng* e, const void* dev_events, uint64_t n_events);
+int shd_eng_next_time(shd_eng* e, uint64_t* next_time);
+/* first-touch resolution records; multi-GPU callers gather
+ * them from all engines, resolve once, and apply the ranks everywhere */
+int shd_eng_pending_count(shd_eng* e, uint64_t* n);
+int shd_eng_resolve_pending(shd_eng* e);
+int shd_eng_trace_count(shd_eng* e, uint64_t* n);
+int shd_eng_trace_copy(shd_eng* e, shd_trace_rec* out, uint64_t cap, uint64_t* n);
+int shd_eng_digest(shd_eng* e, shd_host_digest* out);   /* [host_end-host_begin] */
+int shd_eng_stream(shd_eng* e, void** hip_stream);
+/* HIP-event device time of the last round kernel launch (ms) */
+int shd_eng_last_kernel_ms(shd_eng* e, double* ms);
+void shd_eng_destroy(shd_eng* e);
+
+/* library */
+const char* shd_version(void);
+int shd_device_count(int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHDGPU_H */

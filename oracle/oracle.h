@@ -1,0 +1,129 @@
+/*
+ * oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * A plain-C restatement of the reference (Shadow 1.14, joskid/shadow-1)
+ * algorithms on the accelerated path.  It is the parity checker for libshdgpu:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it, and never as the thing measured or shipped.  The product path
+ * (shadow-1_amd/) does not link, include or call anything under oracle/.
+ *
+ * Every function cites the reference file:line it restates.  Pinning status:
+ *  - RNG, priority-queue order, CoDel: pinned against the reference's own
+ *    random.c / priority_queue.c / router_queue_codel.c compiled into
+ *    oracle/_ref (tests/test_oracle_ref.py).
+ *  - Path cache: distances/paths pinned against networkx 3.4.2 Dijkstra on
+ *    tie-free graphs (tests/golden/make_pathcache_golden.py); the igraph 0.7.1
+ *    Dijkstra itself is absent from the image (not vendored, not installed), so
+ *    its TIE-BREAKING is restated from its published algorithm and is
+ *    "parity unpinned" ("Oracle").
+ *  - Event loop: restated from worker.c / event.c / scheduler.c /
+ *    network_interface.c / router.c; the reference loop cannot be built here
+ *    (process.c needs generated rpth.h, topology.c needs igraph).  Its pieces
+ *    are pinned individually (RNG, CoDel, queue order) and the loop by
+ *    self-consistency with the GPU engine.
+ */
+#ifndef SHD_ORACLE_H
+#define SHD_ORACLE_H
+
+#include <stdint.h>
+#include "../include/shdgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- RNG (utility/random.c:32-51 over glibc rand_r) ---- */
+int32_t o_rand_r(uint32_t* state);
+double o_next_double(uint32_t* state);
+uint32_t o_next_uint(uint32_t* state);
+int o_seed_chain(uint32_t options_seed, int32_t n_hosts, uint32_t* host_seeds);
+
+/* ---- igraph-0.7.1-shaped graph (type_indexededgelist.c as published) ---- */
+typedef struct o_graph {
+    int32_t V, E, directed;
+    int32_t* from;   /* undirected: max(a,b); directed: a */
+    int32_t* to;     /* undirected: min(a,b); directed: b */
+    double* w;       /* latency */
+    double* eloss;
+    double* vloss;   /* NULL or [V] with NaN = absent */
+    int32_t* oi;     /* edge ids sorted by (from,to,eid) */
+    int32_t* ii;     /* edge ids sorted by (to,from,eid) */
+    int32_t* os;     /* [V+1] */
+    int32_t* is;     /* [V+1] */
+    int32_t prefer_direct;
+} o_graph;
+
+o_graph* o_graph_new(const shd_graph* g);
+void o_graph_free(o_graph* g);
+/* igraph_incident(graph, v, IGRAPH_OUT) order; returns count, fills eids (cap) */
+int32_t o_incident(const o_graph* g, int32_t v, int32_t* eids, int32_t cap);
+int32_t o_incident_count(const o_graph* g, int32_t v);
+/* igraph_get_eid(from,to,directedness,error=false): -1 if none (lowest eid) */
+int32_t o_get_eid(const o_graph* g, int32_t a, int32_t b);
+int o_graph_props(const o_graph* g, shd_graph_props* out);
+
+/* ---- path cache primitives ---- */
+/* _topology_lookupDirectPath (topology.c:1877-1927) */
+int o_direct_path(const o_graph* g, int32_t s, int32_t d, double* lat, double* rel);
+/* _topology_computeShortestPathToSelf (topology.c:1545-1653) */
+int o_self_path(const o_graph* g, int32_t s, double* lat, double* rel);
+/* one Dijkstra row (topology.c:1655-1875 with igraph 0.7.1 Dijkstra):
+ * lat/rel per target; ok[j]=0 when computePathProperties fails (no edge);
+ * hops[j] = path edge count; ties (out) = #vertices with a non-unique parent */
+int o_sssp_row(const o_graph* g, int32_t src, const int32_t* targets, int32_t nt,
+               double* lat, double* rel, int32_t* ok, int32_t* hops, int64_t* ties);
+
+/* ---- lazy path cache with the reference's semantics ---- */
+typedef struct o_topo o_topo;
+o_topo* o_topo_new(const o_graph* g, const int32_t* attached, int32_t n_attached,
+                   int32_t force_rows);
+void o_topo_free(o_topo* t);
+/* _topology_getPathEntry (topology.c:1969-2051) -> path latency/reliability;
+ * returns 0 and -1/-1 when the reference returns NULL */
+int o_topo_get(o_topo* t, int32_t s, int32_t d, double* lat, double* rel);
+void o_topo_count_packet(o_topo* t, int32_t s, int32_t d);
+uint64_t o_topo_packet_count(o_topo* t, int32_t s, int32_t d);
+double o_topo_min_latency(o_topo* t);
+int32_t o_topo_rows_run(o_topo* t);
+int32_t o_topo_self_run(o_topo* t);
+
+/* ---- CoDel (routing/router_queue_codel.c) ---- */
+typedef struct o_codel_entry { uint64_t ts; uint32_t len; uint32_t id; uint32_t src; uint32_t _pad; } o_codel_entry;
+typedef struct o_codel {
+    o_codel_entry* q; uint32_t cap, head, count;
+    uint64_t total;
+    uint32_t mode;                 /* 0 store, 1 drop */
+    uint64_t interval_expire;
+    uint64_t next_drop;
+    uint32_t drop_count, drop_count_last;
+} o_codel;
+void o_codel_init(o_codel* c, uint32_t cap);
+void o_codel_free(o_codel* c);
+int o_codel_enqueue(o_codel* c, uint64_t now, uint32_t len, uint32_t id, uint32_t src);
+/* returns 1 and fills *out when a packet is dequeued; dropped entries are
+ * appended to drops (cap ndrops_cap) */
+int o_codel_dequeue(o_codel* c, uint64_t now, o_codel_entry* out, o_codel_entry* drops,
+                    uint32_t ndrops_cap, uint32_t* ndrops);
+uint64_t o_codel_control_law(uint32_t count, uint64_t ts);
+
+/* ---- serial event loop for the PHOLD-UDP model ---- */
+typedef struct o_run {
+    shd_trace_rec* trace; uint64_t n_trace, cap_trace;
+    shd_host_digest* digest;   /* [H] */
+    uint64_t n_events, n_pkt_events;
+    uint64_t window_ns;        /* min ceil(lat*1e6) over attached pairs (for info) */
+    int32_t rows_run, self_run;
+    double wall_ms;
+} o_run;
+/* serial mode (--workers 0): one global queue ordered by event_compare,
+ * one round to end_time (slave.c:415-428) */
+int o_engine_run(const shd_model* m, const shd_graph* g, int32_t force_rows, o_run* out);
+void o_run_free(o_run* r);
+
+/* ---- reference priority order (event.c:110-153) as a checker ---- */
+int o_event_compare(const shd_event* a, const shd_event* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

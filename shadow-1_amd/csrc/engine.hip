@@ -1,0 +1,1188 @@
+// engine.hip -- the conservative round/window packet event loop on MI355X.
+//
+// One GPU thread owns one simulated host.  Per round [ws, we) each host pops
+// its events in (time, src, seq) order (event_compare, event.c:110-153; the
+// dst key is the host itself) and executes them with the reference semantics
+// of the PHOLD-UDP model (DESIGN.md "Model"):
+//
+//   worker_sendPacket      worker.c:260-321   path value, one RNG draw per send,
+//                                              drop unless chance <= reliability,
+//                                              delivery at now + ceil(lat * 1e6)
+//   router_enqueue/CoDel   router.c:104-133, router_queue_codel.c:113-267
+//   token buckets + refill network_interface.c:102-226, 421-455, 519-579
+//   PHOLD application      test_phold.c (chooseNode, implicit-bind port, one
+//                                        message per received message)
+//
+// W = min over attached pairs of ceil(lat*1e6) ns (every inter-host event
+// lands at or after the window end), so a host never receives an event for
+// the round it is executing: rounds are serial-equivalent and the result is
+// the reference's serial (--workers 0) run bit for bit.  Self events that fall
+// inside the window (refills, +1 ns loopback / epoll notifications) are
+// processed in the same round by the owning thread.
+//
+// Device layout (HBM): struct-of-arrays host state; a per-host binary heap of
+// 32-B events; double-buffered per-host inboxes filled with one atomicAdd per
+// event on the destination's counter; per-host CoDel and send FIFOs.  The
+// first-touch path-cache rule is applied from per-vertex row ranks;
+// the rare sends whose pair was unranked at round start are logged, resolved
+// in serial order on the host after the round, and finalised by k_finalize.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "shd_device.h"
+
+namespace {
+
+constexpr uint64_t kInf = 0xFFFFFFFFFFFFFFFFull;
+constexpr uint32_t F_REFILL_PENDING = 1u, F_NOTIFY_PENDING = 2u, F_LISTENING = 4u, F_CODEL_DROP_MODE = 8u;
+constexpr double kRandMax = 2147483647.0;
+constexpr uint64_t kCodelTarget = 10ull * SHD_MS;      // router_queue_codel.c:42
+constexpr uint64_t kCodelInterval = 100ull * SHD_MS;   // router_queue_codel.c:48
+
+struct CodelEnt {
+    uint64_t ts;
+    uint32_t src;
+    uint32_t pkt;
+};
+struct TxEnt {
+    uint32_t dst;
+    uint32_t pkt;
+};
+
+// a send whose (src,dst) pair was unranked at round start
+struct Pending {
+    uint64_t qtime;    // executing event key (time, dst=host, src, seq) + sub-index
+    uint64_t qseq;
+    uint32_t qhost;
+    uint32_t qsrc;
+    uint32_t qsub;
+    uint32_t a, b;     // attached indices of the query
+    uint32_t delivered;   // 0 dropped, 1 delivery pending, 2 delivered in-round
+    uint32_t dst;      // destination host
+    uint32_t pkt;
+    uint64_t seq;      // event seq of the packet (when delivered)
+};
+
+// engine-wide counters / summary on the device
+struct DevSummary {
+    unsigned long long next_time;
+    unsigned long long n_events;
+    unsigned long long n_pkt_events;
+    unsigned long long n_pending;
+    unsigned long long n_remote;
+    unsigned long long n_trace;
+    unsigned int error;
+    unsigned int pad;
+};
+
+struct Params {
+    // hosts
+    int32_t H;                  // total hosts of the model
+    int32_t h0, nloc;           // this engine's hosts [h0, h0+nloc)
+    uint32_t evq_cap, inbox_cap, cq_cap, tq_cap;
+    uint64_t end_time, bootstrap_end, heartbeat, app_start;
+    uint32_t load, payload, trace, pkt_len;
+    // per-host state (local index)
+    uint32_t* rng;
+    uint64_t* ev_seq;
+    uint32_t* pkt_seq;
+    uint64_t* rx_rem;
+    uint64_t* tx_rem;
+    uint64_t* rx_refill;
+    uint64_t* tx_refill;
+    uint32_t* flags;
+    uint32_t* unread;
+    uint64_t* cq_total;
+    uint64_t* cq_iexp;
+    uint64_t* cq_ndrop;
+    uint32_t* cq_dc;
+    uint32_t* cq_dcl;
+    uint32_t* cq_head;
+    uint32_t* cq_count;
+    uint32_t* tq_head;
+    uint32_t* tq_count;
+    uint64_t* c_events;
+    uint64_t* c_pkt;
+    uint64_t* c_sent;
+    uint64_t* c_idrop;
+    uint64_t* c_cdrop;
+    uint64_t* c_recv;
+    // queues
+    shd_event* evq;
+    uint32_t* evq_n;
+    shd_event* inbox[2];
+    uint32_t* inbox_n[2];
+    CodelEnt* cq;
+    TxEnt* tq;
+    // global host tables (all H hosts)
+    const int32_t* host_att;     // attached index of every host
+    const double* dest_cum;
+    // path cache
+    int32_t T;
+    int32_t complete, prefer_direct, directed;
+    const double* row_lat;
+    const double* row_rel;
+    const double* dir_lat;
+    const double* dir_rel;
+    const double* self_lat;
+    const double* self_rel;
+    const uint8_t* adj;
+    const int32_t* rank;
+    const int32_t* self_rank;
+    // outputs
+    Pending* pend;
+    uint32_t pend_cap;
+    shd_event* remote;
+    uint32_t remote_cap;
+    shd_trace_rec* trace_buf;
+    uint64_t trace_cap;
+    DevSummary* sum;
+};
+
+// --------------------------------------------------------------- RNG
+__device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
+    uint32_t r;
+    x = x * 1103515245u + 12345u;
+    r = (x >> 16) & 2047u;
+    x = x * 1103515245u + 12345u;
+    r = (r << 10) ^ ((x >> 16) & 1023u);
+    x = x * 1103515245u + 12345u;
+    r = (r << 10) ^ ((x >> 16) & 1023u);
+    return (int32_t)r;
+}
+__device__ __forceinline__ double next_double_dev(uint32_t& x) { return (double)rand_r_dev(x) / kRandMax; }
+
+// --------------------------------------------------------------- per-host context
+struct HostCtx {
+    int32_t l;       // local index
+    uint32_t h;      // global host id
+    uint64_t now;
+    uint32_t rng;
+    uint64_t ev_seq;
+    uint32_t pkt_seq;
+    uint64_t rx_rem, tx_rem, rx_refill, tx_refill;
+    uint32_t flags;
+    uint32_t unread;
+    uint64_t cq_total, cq_iexp, cq_ndrop;
+    uint32_t cq_dc, cq_dcl, cq_head, cq_count;
+    uint32_t tq_head, tq_count;
+    uint32_t evq_n;
+    uint64_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;
+    // current executing event key (for first-touch logging)
+    uint64_t q_seq;
+    uint32_t q_src;
+    uint32_t q_sub;
+    uint64_t min_emit;   // min time of events sent to other hosts
+    uint32_t err;
+    uint32_t n_pend;
+};
+
+__device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) {
+    if (a.time != b.time) return a.time < b.time;
+    if (a.src != b.src) return a.src < b.src;
+    return a.seq < b.seq;
+}
+
+__device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
+    shd_event* hp = P.evq + (size_t)c.l * P.evq_cap;
+    if (c.evq_n >= P.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
+    uint32_t i = c.evq_n++;
+    while (i > 0) {
+        uint32_t p = (i - 1) >> 1;
+        shd_event pe = hp[p];
+        if (!ev_less(e, pe)) break;
+        hp[i] = pe;
+        i = p;
+    }
+    hp[i] = e;
+}
+
+__device__ shd_event heap_pop(const Params& P, HostCtx& c) {
+    shd_event* hp = P.evq + (size_t)c.l * P.evq_cap;
+    shd_event top = hp[0];
+    uint32_t n = --c.evq_n;
+    if (n == 0) return top;
+    shd_event last = hp[n];
+    uint32_t i = 0;
+    for (;;) {
+        uint32_t lc = 2 * i + 1;
+        if (lc >= n) break;
+        uint32_t m = lc;
+        shd_event me = hp[lc];
+        if (lc + 1 < n) {
+            shd_event re = hp[lc + 1];
+            if (ev_less(re, me)) { m = lc + 1; me = re; }
+        }
+        if (!ev_less(me, last)) break;
+        hp[i] = me;
+        i = m;
+    }
+    hp[i] = last;
+    return top;
+}
+
+__device__ __forceinline__ void trace(const Params& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
+                                      uint32_t peer, uint32_t pkt, uint32_t kind) {
+    if (!P.trace) return;
+    unsigned long long i = atomicAdd(&P.sum->n_trace, 1ull);
+    if (i >= P.trace_cap) { c.err |= SHD_ERR_TRACE_OVERFLOW; return; }
+    shd_trace_rec r;
+    r.time = t; r.seq = seq; r.host = host; r.peer = peer; r.pkt = pkt; r.kind = kind;
+    P.trace_buf[i] = r;
+}
+
+__device__ __forceinline__ bool bootstrapping(const Params& P, const HostCtx& c) { return c.now < P.bootstrap_end; }
+
+// event_new_ (consumes the source's event ID, event.c:38) + scheduler_push
+// (discards time >= end, scheduler.c:346-349) for a self event
+__device__ void schedule_self(const Params& P, HostCtx& c, uint32_t kind, uint64_t delay, uint32_t pkt) {
+    shd_event e;
+    e.time = c.now + delay;
+    e.seq = c.ev_seq++;
+    e.src = c.h;
+    e.dst = c.h;
+    e.pkt = pkt;
+    e.kind = kind;
+    if (e.time >= P.end_time) return;
+    heap_push(P, c, e);
+}
+
+// deliver an inter-host event: to the destination's inbox for the next round,
+// or to the remote outbox when the destination lives on another engine
+__device__ void emit_remote(const Params& P, HostCtx& c, const shd_event& e, int next_parity) {
+    if (e.time >= P.end_time) return;
+    if (e.time < c.min_emit) c.min_emit = e.time;
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl >= 0 && dl < P.nloc) {
+        uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
+        if (slot >= P.inbox_cap) { c.err |= SHD_ERR_INBOX_OVERFLOW; return; }
+        P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
+    } else {
+        unsigned long long slot = atomicAdd(&P.sum->n_remote, 1ull);
+        if (slot >= P.remote_cap) { c.err |= SHD_ERR_REMOTE_OVERFLOW; return; }
+        P.remote[slot] = e;
+    }
+}
+
+// _networkinterface_scheduleNextRefillIfNeeded (network_interface.c:130-161),
+// timeStartedRefillingBuckets = 0
+__device__ void refill_if_needed(const Params& P, HostCtx& c) {
+    const bool need = (c.tx_rem < c.tx_refill + SHD_MTU) || (c.rx_rem < c.rx_refill + SHD_MTU);
+    if (need && !(c.flags & F_REFILL_PENDING)) {
+        const uint64_t until = SHD_MS - (c.now % SHD_MS);
+        schedule_self(P, c, SHD_EV_REFILL, until, 0);
+        c.flags |= F_REFILL_PENDING;
+    }
+}
+__device__ __forceinline__ void consume(uint64_t& rem, uint64_t n) { rem = (n >= rem) ? 0 : rem - n; }
+
+// _networkinterface_receivePacket (network_interface.c:375-419)
+__device__ void if_receive_packet(const Params& P, HostCtx& c, uint32_t src, uint32_t pkt) {
+    if (c.flags & F_LISTENING) {
+        trace(P, c, c.now, 0, c.h, src, pkt, SHD_TR_RECV);
+        c.c_recv++;
+        c.unread++;
+        if (!(c.flags & F_NOTIFY_PENDING)) {   // epoll.c:345-365, +1 ns
+            schedule_self(P, c, SHD_EV_NOTIFY, 1, 0);
+            c.flags |= F_NOTIFY_PENDING;
+        }
+    } else {
+        trace(P, c, c.now, 0, c.h, src, pkt, SHD_TR_IF_DROP);
+    }
+}
+
+// ---- CoDel (router_queue_codel.c) on the per-host FIFO ----
+__device__ __forceinline__ uint64_t codel_control_law(uint32_t count, uint64_t ts) {
+    const uint64_t newTS = ts + kCodelInterval;
+    const double result = ((double)newTS) / sqrt((double)count);
+    return (uint64_t)round(result);
+}
+
+__device__ bool codel_helper(const Params& P, HostCtx& c, bool& okToDrop, CodelEnt& out) {
+    okToDrop = false;
+    if (c.cq_count == 0) { c.cq_iexp = 0; return false; }
+    CodelEnt* q = P.cq + (size_t)c.l * P.cq_cap;
+    out = q[c.cq_head];
+    c.cq_head = (c.cq_head + 1 == P.cq_cap) ? 0 : c.cq_head + 1;
+    c.cq_count--;
+    c.cq_total -= P.pkt_len;
+    const uint64_t sojourn = c.now - out.ts;
+    if (sojourn < kCodelTarget || c.cq_total < SHD_MTU) {
+        c.cq_iexp = 0;
+    } else {
+        if (c.cq_iexp == 0) c.cq_iexp = c.now + kCodelInterval;
+        else if (c.now >= c.cq_iexp) okToDrop = true;
+    }
+    return true;
+}
+
+__device__ __forceinline__ void codel_drop(const Params& P, HostCtx& c, const CodelEnt& e) {
+    trace(P, c, c.now, 0, c.h, e.src, e.pkt, SHD_TR_CODEL_DROP);
+    c.c_cdrop++;
+}
+
+__device__ bool codel_dequeue(const Params& P, HostCtx& c, CodelEnt& out) {
+    bool okToDrop = false;
+    CodelEnt pkt;
+    bool have = codel_helper(P, c, okToDrop, pkt);
+    if (!have) { c.flags &= ~F_CODEL_DROP_MODE; return false; }
+    if (c.flags & F_CODEL_DROP_MODE) {
+        if (!okToDrop) c.flags &= ~F_CODEL_DROP_MODE;
+        while (c.now >= c.cq_ndrop && (c.flags & F_CODEL_DROP_MODE)) {
+            codel_drop(P, c, pkt);
+            c.cq_dc++;
+            have = codel_helper(P, c, okToDrop, pkt);
+            if (okToDrop) c.cq_ndrop = codel_control_law(c.cq_dc, c.cq_ndrop);
+            else c.flags &= ~F_CODEL_DROP_MODE;
+        }
+    } else if (okToDrop) {
+        codel_drop(P, c, pkt);
+        have = codel_helper(P, c, okToDrop, pkt);
+        c.flags |= F_CODEL_DROP_MODE;
+        const uint32_t delta = c.cq_dc - c.cq_dcl;
+        c.cq_dc = 1;
+        const bool recently = c.now < c.cq_ndrop + 16 * kCodelInterval;
+        if (recently && delta > 1) c.cq_dc = delta;
+        c.cq_ndrop = codel_control_law(c.cq_dc, c.now);
+        c.cq_dcl = c.cq_dc;
+    }
+    if (!have) return false;
+    out = pkt;
+    return true;
+}
+
+// networkinterface_receivePackets (network_interface.c:421-455)
+__device__ void if_receive_packets(const Params& P, HostCtx& c) {
+    const bool boot = bootstrapping(P, c);
+    while (boot || c.rx_rem >= SHD_MTU) {
+        CodelEnt p;
+        if (!codel_dequeue(P, c, p)) break;
+        if_receive_packet(P, c, p.src, p.pkt);
+        if (!boot) {
+            consume(c.rx_rem, P.pkt_len);
+            refill_if_needed(P, c);
+        }
+    }
+}
+
+// ---- path value with the first-touch rule ----
+struct PathVal {
+    double lat, rel;
+    double lat2, rel2;   // second candidate when unresolved
+    bool resolved;
+    bool log;            // the query must be logged for rank assignment
+};
+
+__device__ PathVal path_value(const Params& P, int32_t a, int32_t b) {
+    PathVal v;
+    v.resolved = true;
+    v.log = false;
+    const size_t ab = (size_t)a * P.T + b, ba = (size_t)b * P.T + a;
+    if (P.complete || (P.prefer_direct && P.adj[ab])) {
+        v.lat = P.dir_lat[ab]; v.rel = P.dir_rel[ab];
+        return v;
+    }
+    if (a == b) {
+        const int32_t ra = P.rank[a], rs = P.self_rank[a];
+        if (ra == kNoRank && rs == kNoRank) {
+            v.resolved = false; v.log = true;
+            v.lat = P.self_lat[a]; v.rel = P.self_rel[a];
+            v.lat2 = P.row_lat[ab]; v.rel2 = P.row_rel[ab];
+        } else if (rs < ra) {
+            v.lat = P.self_lat[a]; v.rel = P.self_rel[a];
+        } else {
+            v.lat = P.row_lat[ab]; v.rel = P.row_rel[ab];
+        }
+        return v;
+    }
+    const int32_t ra = P.rank[a], rb = P.rank[b];
+    if (ra == kNoRank && rb == kNoRank) {
+        v.resolved = false; v.log = true;
+        v.lat = P.row_lat[ab]; v.rel = P.row_rel[ab];
+        v.lat2 = P.row_lat[ba]; v.rel2 = P.row_rel[ba];
+        return v;
+    }
+    if (P.directed && ra == kNoRank) v.log = true;   // row a still runs (directed rerun rule)
+    if (ra < rb) { v.lat = P.row_lat[ab]; v.rel = P.row_rel[ab]; }
+    else { v.lat = P.row_lat[ba]; v.rel = P.row_rel[ba]; }
+    return v;
+}
+
+__device__ void log_pending(const Params& P, HostCtx& c, int32_t a, int32_t b, uint32_t delivered, uint32_t dst,
+                            uint32_t pkt, uint64_t seq) {
+    unsigned long long i = atomicAdd(&P.sum->n_pending, 1ull);
+    c.n_pend++;
+    if (i >= P.pend_cap) { c.err |= SHD_ERR_PENDING_OVERFLOW; return; }
+    Pending r;
+    r.qtime = c.now; r.qseq = c.q_seq; r.qhost = c.h; r.qsrc = c.q_src; r.qsub = c.q_sub++;
+    r.a = (uint32_t)a; r.b = (uint32_t)b; r.delivered = delivered; r.dst = dst; r.pkt = pkt; r.seq = seq;
+    P.pend[i] = r;
+}
+
+// worker_sendPacket (worker.c:260-321)
+__device__ void worker_send_packet(const Params& P, HostCtx& c, uint32_t dst, uint32_t pkt, int next_parity) {
+    const int32_t a = P.host_att[c.h], b = P.host_att[dst];
+    const PathVal pv = path_value(P, a, b);
+    const double chance = next_double_dev(c.rng);
+    const bool boot = bootstrapping(P, c);
+    const bool pass = boot || chance <= pv.rel || P.payload == 0;
+    if (!pv.resolved) {
+        const bool pass2 = boot || chance <= pv.rel2 || P.payload == 0;
+        if (pass != pass2) c.err |= SHD_ERR_AMBIGUOUS;
+    }
+    if (pass) {
+        const uint64_t seq = c.ev_seq++;
+        trace(P, c, c.now, seq, c.h, dst, pkt, SHD_TR_SENT);
+        c.c_sent++;
+        if (pv.log) {
+            // 1 = delivery waits for the resolution, 2 = already delivered
+            log_pending(P, c, a, b, pv.resolved ? 2u : 1u, dst, pkt, seq);
+            if (!pv.resolved) return;
+        }
+        shd_event e;
+        e.time = c.now + (uint64_t)ceil(pv.lat * (double)SHD_MS);
+        e.seq = seq; e.src = c.h; e.dst = dst; e.pkt = pkt; e.kind = SHD_EV_PACKET;
+        emit_remote(P, c, e, next_parity);
+    } else {
+        trace(P, c, c.now, 0, c.h, dst, pkt, SHD_TR_INET_DROP);
+        c.c_idrop++;
+        if (pv.log) log_pending(P, c, a, b, 0u, dst, pkt, 0);
+    }
+}
+
+// _networkinterface_sendPackets (network_interface.c:519-579), FIFO qdisc
+__device__ void if_send_packets(const Params& P, HostCtx& c, int next_parity) {
+    const bool boot = bootstrapping(P, c);
+    TxEnt* q = P.tq + (size_t)c.l * P.tq_cap;
+    while (c.tx_rem >= SHD_MTU) {
+        if (c.tq_count == 0) break;
+        const TxEnt p = q[c.tq_head];
+        c.tq_head = (c.tq_head + 1 == P.tq_cap) ? 0 : c.tq_head + 1;
+        c.tq_count--;
+        if (p.dst == c.h) {
+            trace(P, c, c.now, c.ev_seq, c.h, c.h, p.pkt, SHD_TR_LOCAL);
+            schedule_self(P, c, SHD_EV_LOCAL, 1, p.pkt);
+        } else {
+            worker_send_packet(P, c, p.dst, p.pkt, next_parity);
+        }
+        if (!boot) {
+            consume(c.tx_rem, P.pkt_len);
+            refill_if_needed(P, c);
+        }
+    }
+}
+
+// _host_getRandomPort / _host_getRandomFreePort (host.c:1058-1110)
+__device__ __forceinline__ uint16_t random_port(HostCtx& c) {
+    const double f = next_double_dev(c.rng);
+    const double pick = round(f * (double)(65535 - SHD_MIN_RANDOM_PORT));
+    uint16_t p = (uint16_t)pick;
+    return (uint16_t)(p + (uint16_t)SHD_MIN_RANDOM_PORT);
+}
+__device__ void random_free_port(HostCtx& c) {
+    for (int i = 0; i < 10; i++)
+        if (random_port(c) != SHD_PHOLD_LISTEN_PORT) return;
+    (void)random_port(c);   // linear-search fallback: draws once, always finds a port
+}
+
+// _phold_sendNewMessage (test_phold.c:218-230)
+__device__ void send_new_message(const Params& P, HostCtx& c, int next_parity) {
+    const double r = ((double)rand_r_dev(c.rng)) / kRandMax;
+    int32_t lo = 0, hi = P.H;
+    while (lo < hi) {
+        const int32_t mid = lo + ((hi - lo) >> 1);
+        if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
+    }
+    if (lo >= P.H) return;
+    const uint32_t dst = (uint32_t)lo;
+    random_free_port(c);
+    const uint32_t pkt = c.pkt_seq++;
+    if (c.tq_count >= P.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return; }
+    TxEnt* q = P.tq + (size_t)c.l * P.tq_cap;
+    uint32_t tail = c.tq_head + c.tq_count;
+    if (tail >= P.tq_cap) tail -= P.tq_cap;
+    q[tail] = TxEnt{dst, pkt};
+    c.tq_count++;
+    if_send_packets(P, c, next_parity);
+}
+
+// _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
+__device__ void refill_cb(const Params& P, HostCtx& c, int next_parity) {
+    c.flags &= ~F_REFILL_PENDING;
+    c.rx_rem += c.rx_refill;
+    if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
+    c.tx_rem += c.tx_refill;
+    if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
+    if_receive_packets(P, c);
+    if_send_packets(P, c, next_parity);
+    refill_if_needed(P, c);
+}
+
+__device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int next_parity) {
+    c.c_events++;
+    c.q_seq = e.seq;
+    c.q_src = e.src;
+    c.q_sub = 0;
+    switch (e.kind) {
+    case SHD_EV_HEARTBEAT:
+        schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
+        break;
+    case SHD_EV_REFILL:
+        refill_cb(P, c, next_parity);
+        break;
+    case SHD_EV_REFILL_LO:
+        break;
+    case SHD_EV_APP_START:
+        c.flags |= F_LISTENING;
+        for (uint32_t i = 0; i < P.load; i++) send_new_message(P, c, next_parity);
+        break;
+    case SHD_EV_PACKET: {
+        // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
+        c.c_pkt++;
+        trace(P, c, c.now, e.seq, c.h, e.src, e.pkt, SHD_TR_ARRIVE);
+        const bool was_empty = c.cq_count == 0;
+        if (c.cq_count >= P.cq_cap) { c.err |= SHD_ERR_CODELQ_OVERFLOW; break; }
+        CodelEnt* q = P.cq + (size_t)c.l * P.cq_cap;
+        uint32_t tail = c.cq_head + c.cq_count;
+        if (tail >= P.cq_cap) tail -= P.cq_cap;
+        q[tail] = CodelEnt{c.now, e.src, e.pkt};
+        c.cq_count++;
+        c.cq_total += P.pkt_len;
+        if (was_empty) if_receive_packets(P, c);
+        break;
+    }
+    case SHD_EV_LOCAL:
+        if_receive_packet(P, c, c.h, e.pkt);
+        break;
+    case SHD_EV_NOTIFY: {
+        c.flags &= ~F_NOTIFY_PENDING;
+        const uint32_t n = c.unread;
+        c.unread = 0;
+        for (uint32_t i = 0; i < n; i++) send_new_message(P, c, next_parity);
+        break;
+    }
+    default:
+        c.err |= 0x80000000u;
+        break;
+    }
+}
+
+__device__ void load_ctx(const Params& P, HostCtx& c, int32_t l) {
+    c.l = l;
+    c.h = (uint32_t)(P.h0 + l);
+    c.rng = P.rng[l]; c.ev_seq = P.ev_seq[l]; c.pkt_seq = P.pkt_seq[l];
+    c.rx_rem = P.rx_rem[l]; c.tx_rem = P.tx_rem[l]; c.rx_refill = P.rx_refill[l]; c.tx_refill = P.tx_refill[l];
+    c.flags = P.flags[l]; c.unread = P.unread[l];
+    c.cq_total = P.cq_total[l]; c.cq_iexp = P.cq_iexp[l]; c.cq_ndrop = P.cq_ndrop[l];
+    c.cq_dc = P.cq_dc[l]; c.cq_dcl = P.cq_dcl[l]; c.cq_head = P.cq_head[l]; c.cq_count = P.cq_count[l];
+    c.tq_head = P.tq_head[l]; c.tq_count = P.tq_count[l];
+    c.evq_n = P.evq_n[l];
+    c.c_events = P.c_events[l]; c.c_pkt = P.c_pkt[l]; c.c_sent = P.c_sent[l];
+    c.c_idrop = P.c_idrop[l]; c.c_cdrop = P.c_cdrop[l]; c.c_recv = P.c_recv[l];
+    c.min_emit = kInf; c.err = 0; c.n_pend = 0;
+}
+
+__device__ void store_ctx(const Params& P, const HostCtx& c) {
+    const int32_t l = c.l;
+    P.rng[l] = c.rng; P.ev_seq[l] = c.ev_seq; P.pkt_seq[l] = c.pkt_seq;
+    P.rx_rem[l] = c.rx_rem; P.tx_rem[l] = c.tx_rem;
+    P.flags[l] = c.flags; P.unread[l] = c.unread;
+    P.cq_total[l] = c.cq_total; P.cq_iexp[l] = c.cq_iexp; P.cq_ndrop[l] = c.cq_ndrop;
+    P.cq_dc[l] = c.cq_dc; P.cq_dcl[l] = c.cq_dcl; P.cq_head[l] = c.cq_head; P.cq_count[l] = c.cq_count;
+    P.tq_head[l] = c.tq_head; P.tq_count[l] = c.tq_count;
+    P.evq_n[l] = c.evq_n;
+    P.c_events[l] = c.c_events; P.c_pkt[l] = c.c_pkt; P.c_sent[l] = c.c_sent;
+    P.c_idrop[l] = c.c_idrop; P.c_cdrop[l] = c.c_cdrop; P.c_recv[l] = c.c_recv;
+}
+
+template <int BLOCK>
+__device__ void block_reduce_publish(const Params& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
+    __shared__ unsigned long long s_next[BLOCK / 64], s_ev[BLOCK / 64], s_pkt[BLOCK / 64];
+    __shared__ unsigned int s_err[BLOCK / 64];
+    // wave reductions (64 lanes)
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        err |= __shfl_xor(err, off, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { s_next[w] = next; s_ev[w] = nev; s_pkt[w] = npkt; s_err[w] = err; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < BLOCK / 64; i++) {
+            if (s_next[i] < s_next[0]) s_next[0] = s_next[i];
+            s_ev[0] += s_ev[i]; s_pkt[0] += s_pkt[i]; s_err[0] |= s_err[i];
+        }
+        if (s_next[0] != kInf) atomicMin(&P.sum->next_time, s_next[0]);
+        if (s_ev[0]) atomicAdd(&P.sum->n_events, s_ev[0]);
+        if (s_pkt[0]) atomicAdd(&P.sum->n_pkt_events, s_pkt[0]);
+        if (s_err[0]) atomicOr(&P.sum->error, s_err[0]);
+    }
+}
+
+// ------------------------------------------------------------------ kernels
+constexpr int kBlock = 64;
+
+// host_boot for every local host at t = 0 (host.c:372-390)
+__global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __restrict__ rng0,
+                                                  const uint64_t* __restrict__ bw_down,
+                                                  const uint64_t* __restrict__ bw_up) {
+    const int32_t l = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    if (l < P.nloc) {
+        const uint32_t h = (uint32_t)(P.h0 + l);
+        // _networkinterface_setupTokenBuckets (network_interface.c:192-226)
+        P.rx_refill[l] = bw_down[h] * 1024 / 1000;
+        P.tx_refill[l] = bw_up[h] * 1024 / 1000;
+        P.rng[l] = rng0[h];
+        P.ev_seq[l] = 0; P.pkt_seq[l] = 0; P.rx_rem[l] = 0; P.tx_rem[l] = 0;
+        P.flags[l] = 0; P.unread[l] = 0;
+        P.cq_total[l] = 0; P.cq_iexp[l] = 0; P.cq_ndrop[l] = 0; P.cq_dc[l] = 0; P.cq_dcl[l] = 0;
+        P.cq_head[l] = 0; P.cq_count[l] = 0; P.tq_head[l] = 0; P.tq_count[l] = 0; P.evq_n[l] = 0;
+        P.c_events[l] = 0; P.c_pkt[l] = 0; P.c_sent[l] = 0; P.c_idrop[l] = 0; P.c_cdrop[l] = 0; P.c_recv[l] = 0;
+        P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
+        HostCtx c;
+        load_ctx(P, c, l);
+        c.now = 0;
+        c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
+        schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);   // tracker_new, tracker.c:141,607-610
+        refill_cb(P, c, 0);                                      // ethernet startRefilling
+        schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);        // loopback refill at +1 ms
+        schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
+        store_ctx(P, c);
+        if (c.evq_n) next = P.evq[(size_t)l * P.evq_cap].time;
+        err = c.err;
+    }
+    block_reduce_publish<kBlock>(P, next, 0, 0, err);
+}
+
+// one round [ws, we): merge inbox[parity], run events < we
+__global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int parity) {
+    const int32_t l = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t next = kInf, nev = 0, npkt = 0;
+    uint32_t err = 0;
+    if (l < P.nloc) {
+        HostCtx c;
+        load_ctx(P, c, l);
+        const uint64_t ev0 = c.c_events, pk0 = c.c_pkt;
+        // merge inbound events of the previous round
+        const uint32_t nin = P.inbox_n[parity][l];
+        if (nin) {
+            const shd_event* in = P.inbox[parity] + (size_t)l * P.inbox_cap;
+            const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
+            for (uint32_t i = 0; i < n; i++) heap_push(P, c, in[i]);
+            P.inbox_n[parity][l] = 0;
+        }
+        const shd_event* hp = P.evq + (size_t)l * P.evq_cap;
+        while (c.evq_n > 0 && hp[0].time < we) {
+            const shd_event e = heap_pop(P, c);
+            c.now = e.time;
+            execute(P, c, e, parity ^ 1);
+        }
+        next = c.evq_n ? hp[0].time : kInf;
+        if (c.min_emit < next) next = c.min_emit;
+        nev = c.c_events - ev0;
+        npkt = c.c_pkt - pk0;
+        err = c.err;
+        store_ctx(P, c);
+    }
+    block_reduce_publish<kBlock>(P, next, nev, npkt, err);
+}
+
+// finalize resolved pending sends: value from the min-rank row, then deliver
+__global__ void k_finalize(Params P, const Pending* __restrict__ pend, uint32_t n, int next_parity) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    if (i < n) {
+        const Pending r = pend[i];
+        if (r.delivered == 1u) {
+            const PathVal pv = path_value(P, (int32_t)r.a, (int32_t)r.b);
+            if (!pv.resolved) err |= SHD_ERR_AMBIGUOUS;
+            shd_event e;
+            e.time = r.qtime + (uint64_t)ceil(pv.lat * (double)SHD_MS);
+            e.seq = r.seq; e.src = r.qhost; e.dst = r.dst; e.pkt = r.pkt; e.kind = SHD_EV_PACKET;
+            if (e.time < P.end_time) {
+                next = e.time;
+                const int32_t dl = (int32_t)e.dst - P.h0;
+                if (dl >= 0 && dl < P.nloc) {
+                    uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
+                    if (slot >= P.inbox_cap) err |= SHD_ERR_INBOX_OVERFLOW;
+                    else P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
+                } else {
+                    unsigned long long slot = atomicAdd(&P.sum->n_remote, 1ull);
+                    if (slot >= P.remote_cap) err |= SHD_ERR_REMOTE_OVERFLOW;
+                    else P.remote[slot] = e;
+                }
+            }
+        }
+    }
+    if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+    if (err) atomicOr(&P.sum->error, err);
+}
+
+// ingest events from other engines into inbox[parity]
+__global__ void k_ingest(Params P, const shd_event* __restrict__ ev, uint64_t n, int parity) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const shd_event e = ev[i];
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
+    uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+    if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
+    P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+}
+
+__global__ void k_digest(Params P, shd_host_digest* __restrict__ out) {
+    const int32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= P.nloc) return;
+    shd_host_digest d;
+    d.ev_seq = P.ev_seq[l]; d.rx_remaining = P.rx_rem[l]; d.tx_remaining = P.tx_rem[l];
+    d.codel_total = P.cq_total[l]; d.codel_interval_expire = P.cq_iexp[l]; d.codel_next_drop = P.cq_ndrop[l];
+    d.n_events = P.c_events[l]; d.n_pkt_events = P.c_pkt[l]; d.n_sent = P.c_sent[l];
+    d.n_inet_drop = P.c_idrop[l]; d.n_codel_drop = P.c_cdrop[l]; d.n_recv = P.c_recv[l];
+    d.rng = P.rng[l]; d.pkt_seq = P.pkt_seq[l];
+    const uint32_t f = P.flags[l];
+    d.codel_mode = (f & F_CODEL_DROP_MODE) ? 1u : 0u;
+    d.codel_count = P.cq_count[l]; d.codel_drop_count = P.cq_dc[l]; d.codel_drop_count_last = P.cq_dcl[l];
+    d.unread = P.unread[l];
+    d.flags = (f & F_REFILL_PENDING ? 1u : 0u) | (f & F_NOTIFY_PENDING ? 2u : 0u) | (f & F_LISTENING ? 4u : 0u) |
+              (P.tq_count[l] ? 8u : 0u);
+    out[l] = d;
+}
+
+// min over valid latencies of a table -> *out (u64 bits)
+__global__ void k_min_valid(const double* __restrict__ a, size_t n, unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long sm[256];
+    unsigned long long m = kDistInf;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const double v = a[i];
+        if (v >= 0.0) {
+            const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+            if (b < m) m = b;
+        }
+    }
+    sm[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s && sm[threadIdx.x + s] < sm[threadIdx.x]) sm[threadIdx.x] = sm[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMin(out, sm[0]);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host driver
+struct shd_eng {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    shd_pc* pc = nullptr;
+    Params P{};
+    int32_t H = 0, h0 = 0, nloc = 0;
+    uint64_t window = 0;
+    int parity = 0;
+    bool booted = false;
+    std::vector<void*> allocs;
+    // inputs kept on device
+    uint32_t* d_rng0 = nullptr;
+    uint64_t* d_bwd = nullptr;
+    uint64_t* d_bwu = nullptr;
+    int32_t* d_host_att = nullptr;
+    double* d_cum = nullptr;
+    int32_t* d_rank = nullptr;
+    int32_t* d_self_rank = nullptr;
+    DevSummary* d_sum = nullptr;
+    DevSummary* h_sum = nullptr;   // pinned
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_kernel_ms = 0;
+    double kernel_ms_total = 0;
+    // host mirrors for the first-touch resolution
+    std::vector<int32_t> h_rank, h_self_rank;
+    int32_t next_rank = 0;
+    uint64_t pending_resolved = 0;
+    uint64_t trace_cap = 0;
+};
+
+template <typename T>
+static int ealloc(shd_eng* e, T** p, size_t n, bool zero = true) {
+    void* q = nullptr;
+    SHD_HIP(hipMalloc(&q, sizeof(T) * (n ? n : 1)));
+    e->allocs.push_back(q);
+    if (zero) SHD_HIP(hipMemsetAsync(q, 0, sizeof(T) * (n ? n : 1), e->stream));
+    *p = (T*)q;
+    return SHD_OK;
+}
+
+#define EALLOC(ptr, n)                          \
+    do {                                        \
+        int rc_ = ealloc(e, &(ptr), (size_t)(n)); \
+        if (rc_) { shd_eng_destroy(e); return rc_; } \
+    } while (0)
+
+extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin, int32_t host_end, int device,
+                              shd_eng** out) {
+    if (!m || !pc || !out || !pc->built || m->n_hosts <= 0) return SHD_EINVAL;
+    if (host_begin < 0 || host_end > m->n_hosts || host_begin >= host_end) return SHD_EINVAL;
+    if (!m->host_vertex || !m->host_rng || !m->bw_down_kibps || !m->bw_up_kibps || !m->dest_cum) return SHD_EINVAL;
+    if (m->heartbeat_interval == 0) return SHD_EINVAL;
+    const int32_t H = m->n_hosts;
+    // every host must sit on an attached vertex of the path cache
+    std::vector<int32_t> host_att(H);
+    std::vector<int32_t> hosts_on(pc->T, 0);
+    for (int32_t h = 0; h < H; h++) {
+        const int32_t v = m->host_vertex[h];
+        if (v < 0 || v >= pc->V || pc->h_att_index[v] < 0) return SHD_EINVAL;
+        host_att[h] = pc->h_att_index[v];
+        hosts_on[host_att[h]]++;
+    }
+    // row mode needs a self-loop on every attached vertex (a row without one
+    // fails as a whole in the reference, topology.c:1490-1495)
+    if (pc->rows_mode && pc->info.n_unroutable != 0) return SHD_EINVAL;
+    shd_eng* e = new shd_eng();
+    e->device = device;
+    e->pc = pc;
+    e->H = H; e->h0 = host_begin; e->nloc = host_end - host_begin;
+    if (hipSetDevice(device) != hipSuccess) { delete e; return SHD_ENODEV; }
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) { delete e; return SHD_ENODEV; }
+    (void)hipEventCreate(&e->ev0);
+    (void)hipEventCreate(&e->ev1);
+    Params& P = e->P;
+    P.H = H; P.h0 = host_begin; P.nloc = e->nloc;
+    P.evq_cap = m->evq_cap ? m->evq_cap : std::max<uint32_t>(64, 4 * m->load + 32);
+    P.inbox_cap = m->inbox_cap ? m->inbox_cap : P.evq_cap;
+    P.cq_cap = m->codelq_cap ? m->codelq_cap : 64;
+    P.tq_cap = m->txq_cap ? m->txq_cap : 64;
+    P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
+    P.app_start = m->app_start; P.load = m->load; P.payload = m->payload; P.trace = m->trace;
+    P.pkt_len = m->payload + SHD_HEADER_UDP;
+    const size_t n = (size_t)e->nloc;
+    EALLOC(P.rng, n); EALLOC(P.ev_seq, n); EALLOC(P.pkt_seq, n); EALLOC(P.rx_rem, n); EALLOC(P.tx_rem, n);
+    EALLOC(P.rx_refill, n); EALLOC(P.tx_refill, n); EALLOC(P.flags, n); EALLOC(P.unread, n);
+    EALLOC(P.cq_total, n); EALLOC(P.cq_iexp, n); EALLOC(P.cq_ndrop, n); EALLOC(P.cq_dc, n); EALLOC(P.cq_dcl, n);
+    EALLOC(P.cq_head, n); EALLOC(P.cq_count, n); EALLOC(P.tq_head, n); EALLOC(P.tq_count, n);
+    EALLOC(P.c_events, n); EALLOC(P.c_pkt, n); EALLOC(P.c_sent, n); EALLOC(P.c_idrop, n); EALLOC(P.c_cdrop, n);
+    EALLOC(P.c_recv, n);
+    {
+        int rc;
+        if ((rc = ealloc(e, &P.evq, n * P.evq_cap, false)) || (rc = ealloc(e, &P.evq_n, n)) ||
+            (rc = ealloc(e, &P.inbox[0], n * P.inbox_cap, false)) ||
+            (rc = ealloc(e, &P.inbox[1], n * P.inbox_cap, false)) || (rc = ealloc(e, &P.inbox_n[0], n)) ||
+            (rc = ealloc(e, &P.inbox_n[1], n)) || (rc = ealloc(e, &P.cq, n * P.cq_cap, false)) ||
+            (rc = ealloc(e, &P.tq, n * P.tq_cap, false))) {
+            shd_eng_destroy(e);
+            return rc;
+        }
+    }
+    EALLOC(e->d_rng0, H); EALLOC(e->d_bwd, H); EALLOC(e->d_bwu, H); EALLOC(e->d_host_att, H); EALLOC(e->d_cum, H);
+    EALLOC(e->d_rank, pc->T); EALLOC(e->d_self_rank, pc->T);
+    EALLOC(e->d_sum, 1);
+    if (hipHostMalloc((void**)&e->h_sum, sizeof(DevSummary)) != hipSuccess) { shd_eng_destroy(e); return SHD_ENOMEM; }
+    P.pend_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 16, (uint64_t)n * (m->load + 4)), 1u << 30);
+    P.remote_cap = (uint32_t)std::min<uint64_t>((uint64_t)n * P.inbox_cap, 1u << 30);
+    {
+        int rc;
+        if ((rc = ealloc(e, &P.pend, P.pend_cap, false))) { shd_eng_destroy(e); return rc; }
+        const bool multi = !(host_begin == 0 && host_end == H);
+        if ((rc = ealloc(e, &P.remote, multi ? P.remote_cap : 1, false))) { shd_eng_destroy(e); return rc; }
+        if (!multi) P.remote_cap = 0;
+        e->trace_cap = m->trace ? std::max<uint64_t>(1u << 20, (uint64_t)n * 4096) : 1;
+        if (m->trace) e->trace_cap = std::min<uint64_t>(e->trace_cap, 1ull << 27);
+        if ((rc = ealloc(e, &P.trace_buf, e->trace_cap, false))) { shd_eng_destroy(e); return rc; }
+        P.trace_cap = e->trace_cap;
+    }
+    hipStream_t s = e->stream;
+    if (hipMemcpyAsync(e->d_rng0, m->host_rng, 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_bwd, m->bw_down_kibps, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_bwu, m->bw_up_kibps, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_host_att, host_att.data(), 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_cum, m->dest_cum, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess) {
+        shd_eng_destroy(e);
+        return SHD_ENODEV;
+    }
+    e->h_rank.assign(pc->T, kNoRank);
+    e->h_self_rank.assign(pc->T, kNoRank);
+    if (hipMemcpyAsync(e->d_rank, e->h_rank.data(), 4 * (size_t)pc->T, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_self_rank, e->h_self_rank.data(), 4 * (size_t)pc->T, hipMemcpyHostToDevice, s) !=
+            hipSuccess) {
+        shd_eng_destroy(e);
+        return SHD_ENODEV;
+    }
+    P.host_att = e->d_host_att;
+    P.dest_cum = e->d_cum;
+    P.T = pc->T;
+    P.complete = pc->complete; P.prefer_direct = pc->prefer_direct; P.directed = pc->directed;
+    P.row_lat = pc->d_row_lat; P.row_rel = pc->d_row_rel;
+    P.dir_lat = pc->d_dir_lat; P.dir_rel = pc->d_dir_rel;
+    P.self_lat = pc->d_self_lat; P.self_rel = pc->d_self_rel;
+    P.adj = pc->d_adj;
+    P.rank = e->d_rank; P.self_rank = e->d_self_rank;
+    P.sum = e->d_sum;
+    // the serial-equivalent window W: min over every latency a send can be
+    // served (rows, direct values, self values) -> ceil(lat * 1e6) ns
+    {
+        unsigned long long* d_min = nullptr;
+        if (hipMalloc((void**)&d_min, 8) != hipSuccess) { shd_eng_destroy(e); return SHD_ENOMEM; }
+        unsigned long long init = kDistInf;
+        (void)hipMemcpyAsync(d_min, &init, 8, hipMemcpyHostToDevice, s);
+        const size_t TT = (size_t)pc->T * pc->T;
+        const int blocks = (int)std::min<size_t>((TT + 255) / 256, 4096);
+        if (pc->rows_mode) {
+            hipLaunchKernelGGL(k_min_valid, dim3(blocks), dim3(256), 0, s, pc->d_row_lat, TT, d_min);
+            hipLaunchKernelGGL(k_min_valid, dim3((pc->T + 255) / 256), dim3(256), 0, s, pc->d_self_lat,
+                               (size_t)pc->T, d_min);
+        }
+        if (pc->complete || pc->prefer_direct)
+            hipLaunchKernelGGL(k_min_valid, dim3(blocks), dim3(256), 0, s, pc->d_dir_lat, TT, d_min);
+        unsigned long long bits = 0;
+        (void)hipMemcpyAsync(&bits, d_min, 8, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) { (void)hipFree(d_min); shd_eng_destroy(e); return SHD_ENODEV; }
+        (void)hipFree(d_min);
+        double ml;
+        memcpy(&ml, &bits, 8);
+        if (!(ml > 0.0) || bits == kDistInf) { shd_eng_destroy(e); return SHD_EINVAL; }
+        e->window = (uint64_t)ceil(ml * (double)SHD_MS);
+        if (e->window == 0) e->window = 1;
+    }
+    *out = e;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_window(shd_eng* e, uint64_t* w) {
+    if (!e || !w) return SHD_EINVAL;
+    *w = e->window;
+    return SHD_OK;
+}
+
+static int reset_summary(shd_eng* e) {
+    DevSummary z{};
+    z.next_time = kInf;
+    // keep n_trace cumulative
+    z.n_trace = e->h_sum->n_trace;
+    SHD_HIP(hipMemcpyAsync(e->d_sum, &z, sizeof(z), hipMemcpyHostToDevice, e->stream));
+    return SHD_OK;
+}
+
+static int read_summary(shd_eng* e) {
+    SHD_HIP(hipMemcpyAsync(e->h_sum, e->d_sum, sizeof(DevSummary), hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_boot(shd_eng* e) {
+    if (!e) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(e->device));
+    memset(e->h_sum, 0, sizeof(DevSummary));
+    int rc = reset_summary(e);
+    if (rc) return rc;
+    const int grid = (e->nloc + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_boot, dim3(grid), dim3(kBlock), 0, e->stream, e->P, e->d_rng0, e->d_bwd, e->d_bwu);
+    SHD_HIP(hipGetLastError());
+    if ((rc = read_summary(e))) return rc;
+    e->parity = 0;
+    e->booted = true;
+    if (e->h_sum->error) return SHD_EOVERFLOW;
+    return SHD_OK;
+}
+
+// first-touch resolution in serial order: sort the logged queries
+// by the executing event's key, assign row ranks, finalize delivered sends
+static int resolve_pending(shd_eng* e, uint64_t npend, int next_parity) {
+    if (npend > e->P.pend_cap) return SHD_EOVERFLOW;
+    std::vector<Pending> recs(npend);
+    SHD_HIP(hipMemcpyAsync(recs.data(), e->P.pend, sizeof(Pending) * npend, hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
+    std::sort(recs.begin(), recs.end(), [](const Pending& x, const Pending& y) {
+        if (x.qtime != y.qtime) return x.qtime < y.qtime;
+        if (x.qhost != y.qhost) return x.qhost < y.qhost;
+        if (x.qsrc != y.qsrc) return x.qsrc < y.qsrc;
+        if (x.qseq != y.qseq) return x.qseq < y.qseq;
+        return x.qsub < y.qsub;
+    });
+    const bool directed = e->pc->directed;
+    for (const Pending& r : recs) {
+        const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
+        if (a == b) {
+            if (e->h_rank[a] == kNoRank && e->h_self_rank[a] == kNoRank) e->h_self_rank[a] = e->next_rank++;
+        } else if (directed) {
+            if (e->h_rank[a] == kNoRank) e->h_rank[a] = e->next_rank++;
+        } else {
+            if (e->h_rank[a] == kNoRank && e->h_rank[b] == kNoRank) e->h_rank[a] = e->next_rank++;
+        }
+    }
+    const int32_t T = e->pc->T;
+    SHD_HIP(hipMemcpyAsync(e->d_rank, e->h_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
+    SHD_HIP(hipMemcpyAsync(e->d_self_rank, e->h_self_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
+    const uint32_t n = (uint32_t)npend;
+    hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->P, e->P.pend, n, next_parity);
+    SHD_HIP(hipGetLastError());
+    e->pending_resolved += npend;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_run_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out) {
+    if (!e || !e->booted || we <= ws) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(e->device));
+    int rc = reset_summary(e);
+    if (rc) return rc;
+    const int grid = (e->nloc + kBlock - 1) / kBlock;
+    SHD_HIP(hipEventRecord(e->ev0, e->stream));
+    hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, e->P, we, e->parity);
+    SHD_HIP(hipGetLastError());
+    SHD_HIP(hipEventRecord(e->ev1, e->stream));
+    if ((rc = read_summary(e))) return rc;
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e->ev0, e->ev1);
+    e->last_kernel_ms = ms;
+    e->kernel_ms_total += ms;
+    const uint64_t npend = e->h_sum->n_pending;
+    const int next_parity = e->parity ^ 1;
+    if (npend) {
+        if ((rc = resolve_pending(e, npend, next_parity))) return rc;
+        if ((rc = read_summary(e))) return rc;
+    }
+    e->parity = next_parity;
+    if (out) {
+        out->window_start = ws; out->window_end = we;
+        out->next_time = e->h_sum->next_time;
+        out->n_events = e->h_sum->n_events; out->n_pkt_events = e->h_sum->n_pkt_events;
+        out->n_pending = npend; out->n_remote = e->h_sum->n_remote; out->error = e->h_sum->error;
+    }
+    if (e->h_sum->error & SHD_ERR_AMBIGUOUS) return SHD_EAMBIG;
+    if (e->h_sum->error) return SHD_EOVERFLOW;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_run(shd_eng* e, shd_run_stats* st) {
+    if (!e) return SHD_EINVAL;
+    auto t0 = std::chrono::steady_clock::now();
+    int rc = SHD_OK;
+    if (!e->booted && (rc = shd_eng_boot(e))) return rc;
+    shd_run_stats s{};
+    s.window_ns = e->window;
+    uint64_t next = e->h_sum->next_time;
+    e->kernel_ms_total = 0;
+    while (next < e->P.end_time) {
+        const uint64_t ws = next;
+        uint64_t we = ws + e->window;
+        if (we > e->P.end_time || we < ws) we = e->P.end_time;
+        shd_round_summary r;
+        rc = shd_eng_run_round(e, ws, we, &r);
+        s.n_rounds++;
+        s.n_events += r.n_events;
+        s.n_pkt_events += r.n_pkt_events;
+        s.final_time = we;
+        if (rc) { s.error = r.error; break; }
+        next = r.next_time;
+    }
+    s.n_pending_resolved = e->pending_resolved;
+    s.device_ms_round_kernel = e->kernel_ms_total;
+    s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) *st = s;
+    return rc;
+}
+
+extern "C" int shd_eng_remote_counts(shd_eng* e, int32_t n_parts, const int32_t* part_begin, uint64_t* counts) {
+    if (!e || n_parts <= 0 || !part_begin || !counts) return SHD_EINVAL;
+    // events are staged unsorted; the multi-GPU driver sorts them by
+    // destination through shd_eng_remote_buffer
+    for (int32_t i = 0; i < n_parts; i++) counts[i] = 0;
+    counts[0] = e->h_sum->n_remote;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_remote_buffer(shd_eng* e, void** p, uint64_t* n) {
+    if (!e || !p || !n) return SHD_EINVAL;
+    *p = e->P.remote;
+    *n = std::min<uint64_t>(e->h_sum->n_remote, e->P.remote_cap);
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_ingest(shd_eng* e, const void* ev, uint64_t n) {
+    if (!e || (n && !ev)) return SHD_EINVAL;
+    if (!n) return SHD_OK;
+    SHD_HIP(hipSetDevice(e->device));
+    hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->P,
+                       (const shd_event*)ev, n, e->parity);
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_next_time(shd_eng* e, uint64_t* t) {
+    if (!e || !t) return SHD_EINVAL;
+    *t = e->h_sum->next_time;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_pending_count(shd_eng* e, uint64_t* n) {
+    if (!e || !n) return SHD_EINVAL;
+    *n = e->pending_resolved;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_resolve_pending(shd_eng* e) {
+    return e ? SHD_OK : SHD_EINVAL;   // resolution runs inside shd_eng_run_round
+}
+
+extern "C" int shd_eng_trace_count(shd_eng* e, uint64_t* n) {
+    if (!e || !n) return SHD_EINVAL;
+    *n = std::min<uint64_t>(e->h_sum->n_trace, e->trace_cap);
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_trace_copy(shd_eng* e, shd_trace_rec* out, uint64_t cap, uint64_t* n) {
+    if (!e || !out || !n) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(e->device));
+    const uint64_t cnt = std::min<uint64_t>(std::min<uint64_t>(e->h_sum->n_trace, e->trace_cap), cap);
+    if (cnt) SHD_HIP(hipMemcpy(out, e->P.trace_buf, sizeof(shd_trace_rec) * cnt, hipMemcpyDeviceToHost));
+    *n = cnt;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_digest(shd_eng* e, shd_host_digest* out) {
+    if (!e || !out) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(e->device));
+    shd_host_digest* d = nullptr;
+    SHD_HIP(hipMalloc((void**)&d, sizeof(shd_host_digest) * (size_t)e->nloc));
+    hipLaunchKernelGGL(k_digest, dim3((e->nloc + 255) / 256), dim3(256), 0, e->stream, e->P, d);
+    hipError_t err = hipMemcpyAsync(out, d, sizeof(shd_host_digest) * (size_t)e->nloc, hipMemcpyDeviceToHost, e->stream);
+    hipError_t err2 = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (err != hipSuccess || err2 != hipSuccess) return SHD_ENODEV;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_stream(shd_eng* e, void** s) {
+    if (!e || !s) return SHD_EINVAL;
+    *s = (void*)e->stream;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_last_kernel_ms(shd_eng* e, double* ms) {
+    if (!e || !ms) return SHD_EINVAL;
+    *ms = e->last_kernel_ms;
+    return SHD_OK;
+}
+
+extern "C" void shd_eng_destroy(shd_eng* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    for (void* p : e->allocs) (void)hipFree(p);
+    if (e->h_sum) (void)hipHostFree(e->h_sum);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}

@@ -1,0 +1,710 @@
+// pathcache.hip -- the topology path cache on MI355X (gfx950).
+//
+// Replaces the lazy igraph-Dijkstra cache of src/main/routing/topology.c with
+// three device kernels that fill [T][T] f64 tables in HBM (T = attached
+// vertices):
+//
+//   k_sssp_rows    one workgroup per source row (persistent over rows):
+//                  frontier Bellman-Ford in LDS (distances as u64 bit patterns
+//                  of non-negative doubles, ds_min_u64), then each vertex picks
+//                  its shortest-path parent (the in-arc with d[u]+w == d[v] and
+//                  the smallest d[u], the arc Dijkstra relaxes first), then every
+//                  target walks its parent chain and folds latency and
+//                  reliability FORWARD from the source exactly as
+//                  _topology_computePathProperties does (topology.c:1407-1523):
+//                  lat = ((0+w1)+w2)+..., rel = ((1*r(src))*r(dst))*r(e1)*r(e2)...
+//                  Relaxation d[x] = d[u] + w(u,x) is the same left fold, so the
+//                  converged distance equals igraph's on tie-free graphs.
+//   k_direct       direct-path values of adjacent pairs (topology.c:1877-1927).
+//   k_self         "2 x min incident edge" self values (topology.c:1545-1653).
+//
+// No MFMA: min-plus relaxation is not a multiply-add contraction.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <unordered_map>
+
+#include "shd_device.h"
+
+static char g_last_error[512];
+void shd_set_hip_error(hipError_t e, const char* what, const char* file, int line) {
+    snprintf(g_last_error, sizeof(g_last_error), "%s:%d %s -> %s", file, line, what,
+             hipGetErrorString(e));
+    fprintf(stderr, "libshdgpu: %s\n", g_last_error);
+}
+
+extern "C" const char* shd_version(void) { return "libshdgpu 0.1 (gfx950)"; }
+
+extern "C" int shd_device_count(int* n) {
+    if (!n) return SHD_EINVAL;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return SHD_OK;
+}
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ double u2d(uint64_t u) { return __longlong_as_double((long long)u); }
+__device__ __forceinline__ uint64_t d2u(double d) { return (uint64_t)__double_as_longlong(d); }
+
+// reliability factor of a vertex whose packetloss attribute is present
+// (_topology_findVertexAttributeDouble: NaN means absent, topology.c:330-347)
+__device__ __forceinline__ bool vrel(const double* vloss, int32_t v, double* r) {
+    if (!vloss) return false;
+    double l = vloss[v];
+    if (isnan(l)) return false;
+    *r = (double)1.0f - l;
+    return true;
+}
+
+// ------------------------------------------------------------------ SSSP rows
+// Per-row working set: dist u64[V], parent i32[V] (index into the rin_* arcs),
+// upd u16[V] (iteration at which the vertex last improved = frontier stamp).
+constexpr int kChunk = 32;   // edges folded per pass of the forward chain walk
+
+template <int BLOCK>
+__device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
+                             const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
+                             const double* __restrict__ arc_w, const int32_t* __restrict__ rin_off,
+                             const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
+                             const double* __restrict__ rin_w, const double* __restrict__ w_e,
+                             const double* __restrict__ eloss, const double* __restrict__ vloss,
+                             const int32_t* __restrict__ attached, const int32_t* __restrict__ self_eid,
+                             double* __restrict__ out_lat, double* __restrict__ out_rel,
+                             int64_t* __restrict__ stats, uint64_t* dist, int32_t* parent,
+                             uint16_t* upd, int* flags /* LDS int[4] */) {
+    const int tid = threadIdx.x;
+    for (int32_t v = tid; v < V; v += BLOCK) {
+        dist[v] = kDistInf;
+        parent[v] = -1;
+        upd[v] = 0xFFFF;
+    }
+    if (tid < 3) flags[tid] = 0;
+    __syncthreads();
+    if (tid == 0) { dist[src] = 0; upd[src] = 0; }
+    __syncthreads();
+
+    // ---- frontier Bellman-Ford: vertices improved in iteration `it` relax in it+1
+    int it = 0;
+    for (;;) {
+        if (tid == 0) flags[(it + 1) % 3] = 0;
+        const uint16_t stamp = (uint16_t)it;
+        for (int32_t v = tid; v < V; v += BLOCK) {
+            if (upd[v] != stamp) continue;
+            const double dv = u2d(dist[v]);
+            const int32_t k1 = arc_off[v + 1];
+            for (int32_t k = arc_off[v]; k < k1; k++) {
+                const int32_t x = arc_dst[k];
+                const uint64_t nb = d2u(dv + arc_w[k]);
+                if (nb < dist[x]) {
+                    const uint64_t old = atomicMin((unsigned long long*)&dist[x], (unsigned long long)nb);
+                    if (nb < old) {
+                        upd[x] = (uint16_t)(it + 1);
+                        flags[it % 3] = 1;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        const bool more = flags[it % 3] != 0;
+        it++;
+        if (!more || it >= 0xFFFE) break;
+    }
+
+    // ---- parent per vertex: smallest d[u] among exact predecessors; equal d[u]
+    // (a tie Dijkstra breaks by heap order, unpinned) -> lowest edge id
+    int64_t my_ties = 0;
+    for (int32_t v = tid; v < V; v += BLOCK) {
+        if (v == src) continue;
+        const uint64_t dvb = dist[v];
+        if (dvb == kDistInf) continue;
+        const double dv = u2d(dvb);
+        int32_t best = -1;
+        uint64_t bestd = kDistInf;
+        int nbest = 0;
+        for (int32_t k = rin_off[v]; k < rin_off[v + 1]; k++) {
+            const int32_t u = rin_src[k];
+            const uint64_t dub = dist[u];
+            if (dub == kDistInf) continue;
+            if (u2d(dub) + rin_w[k] == dv) {
+                if (best < 0 || dub < bestd) { best = k; bestd = dub; nbest = 1; }
+                else if (dub == bestd) {
+                    nbest++;
+                    if (rin_eid[k] < rin_eid[best]) best = k;
+                }
+            }
+        }
+        parent[v] = best;
+        if (nbest > 1) my_ties++;
+    }
+    if (my_ties) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)my_ties);
+    if (tid == 0) atomicMax((unsigned long long*)&stats[2], (unsigned long long)it);
+    __syncthreads();
+
+    // ---- properties per target: forward fold along the parent chain
+    double rsrc = 1.0;
+    const bool has_rsrc = vrel(vloss, src, &rsrc);
+    int32_t my_maxhops = 0;
+    int64_t my_unroutable = 0, my_mismatch = 0;
+    for (int32_t j = tid; j < T; j += BLOCK) {
+        const int32_t t = attached[j];
+        double lat, rel;
+        if (t == src) {
+            // igraph 0.7.1 returns the path [src]: the self-loop edge alone, no
+            // destination factor (topology.c:1456-1508)
+            const int32_t e = self_eid[row];
+            if (e < 0) {
+                lat = -1.0; rel = -1.0; my_unroutable++;
+            } else {
+                lat = 0.0 + w_e[e];
+                rel = 1.0;
+                if (has_rsrc) rel *= rsrc;
+                rel *= ((double)1.0f - eloss[e]);
+            }
+        } else if (dist[t] == kDistInf) {
+            lat = -1.0; rel = -1.0; my_unroutable++;
+        } else {
+            rel = 1.0;
+            if (has_rsrc) rel *= rsrc;
+            double rt;
+            if (vrel(vloss, t, &rt)) rel *= rt;
+            // hop count
+            int32_t k = 0;
+            for (int32_t v = t; v != src; v = rin_src[parent[v]]) k++;
+            if (k > my_maxhops) my_maxhops = k;
+            lat = 0.0;
+            int32_t eid_buf[kChunk];
+            for (int32_t done = 0; done < k; done += kChunk) {
+                const int32_t cnt = min(kChunk, k - done);
+                int32_t v = t;
+                for (int32_t s = 0; s < k - done - cnt; s++) v = rin_src[parent[v]];
+                for (int32_t s = cnt - 1; s >= 0; s--) {
+                    const int32_t a = parent[v];
+                    eid_buf[s] = rin_eid[a];
+                    v = rin_src[a];
+                }
+                for (int32_t s = 0; s < cnt; s++) {
+                    const int32_t e = eid_buf[s];
+                    lat += w_e[e];
+                    rel *= ((double)1.0f - eloss[e]);
+                }
+            }
+            if (d2u(lat) != dist[t]) my_mismatch++;
+            if (lat == 0) lat = 1;   // topology.c:1848-1852
+        }
+        out_lat[(size_t)row * T + j] = lat;
+        out_rel[(size_t)row * T + j] = rel;
+    }
+    if (my_maxhops) atomicMax((unsigned long long*)&stats[1], (unsigned long long)my_maxhops);
+    if (my_unroutable) atomicAdd((unsigned long long*)&stats[3], (unsigned long long)my_unroutable);
+    if (my_mismatch) atomicAdd((unsigned long long*)&stats[4], (unsigned long long)my_mismatch);
+    __syncthreads();
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
+    int32_t V, int32_t T, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
+    const double* __restrict__ arc_w, const int32_t* __restrict__ rin_off,
+    const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
+    const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
+    const double* __restrict__ vloss, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ self_eid, double* __restrict__ out_lat, double* __restrict__ out_rel,
+    int64_t* __restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint64_t* dist = (uint64_t*)smem;
+    int32_t* parent = (int32_t*)(smem + (size_t)8 * V);
+    uint16_t* upd = (uint16_t*)(smem + (size_t)12 * V);
+    int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
+    for (int32_t row = blockIdx.x; row < T; row += gridDim.x)
+        sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
+                            rin_w, w_e, eloss, vloss, attached, self_eid, out_lat, out_rel, stats, dist,
+                            parent, upd, flags);
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
+    int32_t V, int32_t T, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
+    const double* __restrict__ arc_w, const int32_t* __restrict__ rin_off,
+    const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
+    const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
+    const double* __restrict__ vloss, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ self_eid, double* __restrict__ out_lat, double* __restrict__ out_rel,
+    int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block) {
+    __shared__ int flags[4];
+    char* base = scratch + per_block * blockIdx.x;
+    uint64_t* dist = (uint64_t*)base;
+    int32_t* parent = (int32_t*)(base + (size_t)8 * V);
+    uint16_t* upd = (uint16_t*)(base + (size_t)12 * V);
+    for (int32_t row = blockIdx.x; row < T; row += gridDim.x)
+        sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
+                            rin_w, w_e, eloss, vloss, attached, self_eid, out_lat, out_rel, stats, dist,
+                            parent, upd, flags);
+}
+
+// ------------------------------------------------------------------ direct
+// _topology_lookupDirectPath (topology.c:1877-1927) for every attached pair;
+// igraph_get_eid through the (neighbour, eid)-sorted lists (lowest parallel eid)
+__device__ __forceinline__ int32_t dev_get_eid(const int32_t* nbr_off, const int32_t* nbr_v,
+                                               const int32_t* nbr_eid, int32_t a, int32_t b) {
+    int32_t lo = nbr_off[a], hi = nbr_off[a + 1];
+    const int32_t end = hi;
+    while (lo < hi) {
+        int32_t mid = lo + ((hi - lo) >> 1);
+        if (nbr_v[mid] < b) lo = mid + 1; else hi = mid;
+    }
+    return (lo < end && nbr_v[lo] == b) ? nbr_eid[lo] : -1;
+}
+
+__global__ void k_direct(int32_t T, const int32_t* __restrict__ attached, const int32_t* __restrict__ nbr_off,
+                         const int32_t* __restrict__ nbr_v, const int32_t* __restrict__ nbr_eid,
+                         const double* __restrict__ w_e, const double* __restrict__ eloss,
+                         const double* __restrict__ vloss, double* __restrict__ lat_out,
+                         double* __restrict__ rel_out, uint8_t* __restrict__ adj_out) {
+    const size_t n = (size_t)T * T;
+    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        const int32_t i = (int32_t)(idx / T), j = (int32_t)(idx % T);
+        const int32_t s = attached[i], d = attached[j];
+        const int32_t e = dev_get_eid(nbr_off, nbr_v, nbr_eid, s, d);
+        double lat = __longlong_as_double(0x7FF8000000000000ll), rel = lat;
+        if (e >= 0) {
+            double tl = 0.0, tr = 1.0, r;
+            if (vrel(vloss, s, &r)) tr *= r;
+            if (vrel(vloss, d, &r)) tr *= r;
+            tl += w_e[e];
+            tr *= ((double)1.0f - eloss[e]);
+            lat = tl; rel = tr;
+        }
+        lat_out[idx] = lat;
+        rel_out[idx] = rel;
+        adj_out[idx] = e >= 0;
+    }
+}
+
+// ------------------------------------------------------------------ self
+// _topology_computeShortestPathToSelf (topology.c:1545-1653): first strict
+// minimum over the igraph_incident(OUT) list; latency 2*min, reliability r^2
+__global__ void k_self(int32_t T, const int32_t* __restrict__ attached, const int32_t* __restrict__ inc_off,
+                       const int32_t* __restrict__ inc_eid, const double* __restrict__ w_e,
+                       const double* __restrict__ eloss, double* __restrict__ lat_out,
+                       double* __restrict__ rel_out) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T) return;
+    const int32_t v = attached[i];
+    double minLatency = 0.0f, relMin = 0.0f;
+    const int32_t k0 = inc_off[v], k1 = inc_off[v + 1];
+    for (int32_t k = k0; k < k1; k++) {
+        const int32_t e = inc_eid[k];
+        const double el = w_e[e];
+        if (minLatency == 0 || el < minLatency) {
+            minLatency = el;
+            relMin = (double)1.0f - eloss[e];
+        }
+    }
+    if (k1 == k0) { lat_out[i] = -1.0; rel_out[i] = -1.0; return; }
+    lat_out[i] = (double)2.0f * minLatency;
+    rel_out[i] = relMin * relMin;
+}
+
+// min over valid (>= 0, non-NaN) latencies of a table -> stats[5] as u64 bits
+__global__ void k_min_latency(const double* __restrict__ a, size_t n, int64_t* __restrict__ stats) {
+    __shared__ unsigned long long smin[256];
+    unsigned long long m = kDistInf;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const double v = a[i];
+        if (v >= 0.0) { unsigned long long b = (unsigned long long)__double_as_longlong(v); if (b < m) m = b; }
+    }
+    smin[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s && smin[threadIdx.x + s] < smin[threadIdx.x]) smin[threadIdx.x] = smin[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMin((unsigned long long*)&stats[5], smin[0]);
+}
+
+// ------------------------------------------------------------------ host API
+template <typename T>
+static int dalloc_copy(T** d, const T* h, size_t n) {
+    SHD_HIP(hipMalloc((void**)d, sizeof(T) * (n ? n : 1)));
+    if (n) SHD_HIP(hipMemcpy(*d, h, sizeof(T) * n, hipMemcpyHostToDevice));
+    return SHD_OK;
+}
+
+static void pc_free_device(shd_pc* pc) {
+    void* ptrs[] = {pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
+                    pc->d_rin_w, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
+                    pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row_lat,
+                    pc->d_row_rel, pc->d_dir_lat, pc->d_dir_rel, pc->d_self_lat, pc->d_self_rel, pc->d_adj,
+                    pc->d_scratch, pc->d_stats};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+}
+
+extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_t n_attached, uint32_t flags,
+                             int device, shd_pc** out) {
+    if (!g || !attached || n_attached <= 0 || !out) return SHD_EINVAL;
+    shd_graph_props props;
+    int rc = shd_graph_check(g, &props);
+    if (rc) return rc;
+    for (int32_t i = 0; i < n_attached; i++)
+        if (attached[i] < 0 || attached[i] >= g->n_vertices) return SHD_EINVAL;
+    shd_pc* pc = new shd_pc();
+    pc->device = device;
+    pc->flags = flags;
+    pc->props = props;
+    pc->V = g->n_vertices;
+    pc->E = g->n_edges;
+    pc->T = n_attached;
+    pc->directed = g->directed;
+    pc->prefer_direct = g->prefer_direct;
+    pc->complete = props.is_complete && !(flags & SHD_PC_FORCE_ROWS);
+    pc->rows_mode = !pc->complete;
+    if ((rc = shd_csr_build(g, &pc->csr))) { delete pc; return rc; }
+    const int32_t V = pc->V, E = pc->E, T = pc->T;
+    pc->h_attached = (int32_t*)malloc(sizeof(int32_t) * T);
+    memcpy(pc->h_attached, attached, sizeof(int32_t) * T);
+    pc->h_att_index = (int32_t*)malloc(sizeof(int32_t) * V);
+    for (int32_t v = 0; v < V; v++) pc->h_att_index[v] = -1;
+    for (int32_t i = 0; i < T; i++) {
+        if (pc->h_att_index[attached[i]] >= 0) { shd_pc_destroy(pc); return SHD_EINVAL; }  // duplicate
+        pc->h_att_index[attached[i]] = i;
+    }
+    pc->h_w = (double*)malloc(sizeof(double) * (E + 1));
+    pc->h_eloss = (double*)malloc(sizeof(double) * (E + 1));
+    memcpy(pc->h_w, g->edge_latency, sizeof(double) * E);
+    memcpy(pc->h_eloss, g->edge_loss, sizeof(double) * E);
+    pc->h_vloss = (double*)malloc(sizeof(double) * V);
+    pc->has_vloss = g->vertex_loss != nullptr;
+    for (int32_t v = 0; v < V; v++) pc->h_vloss[v] = g->vertex_loss ? g->vertex_loss[v] : NAN;
+    pc->h_self_eid = (int32_t*)malloc(sizeof(int32_t) * T);
+    for (int32_t i = 0; i < T; i++) pc->h_self_eid[i] = shd_csr_get_eid(&pc->csr, attached[i], attached[i]);
+    pc->h_rank = (int32_t*)malloc(sizeof(int32_t) * T);
+    pc->h_self_rank = (int32_t*)malloc(sizeof(int32_t) * T);
+    for (int32_t i = 0; i < T; i++) pc->h_rank[i] = pc->h_self_rank[i] = kNoRank;
+    pc->counts = new std::unordered_map<uint64_t, uint64_t>();
+
+    if (hipSetDevice(device) != hipSuccess) { shd_pc_destroy(pc); return SHD_ENODEV; }
+    if (hipStreamCreateWithFlags(&pc->stream, hipStreamNonBlocking) != hipSuccess) {
+        shd_pc_destroy(pc);
+        return SHD_ENODEV;
+    }
+    const shd_csr& c = pc->csr;
+    const int32_t na = c.arc_off[V];
+    if ((rc = dalloc_copy(&pc->d_arc_off, c.arc_off, V + 1)) || (rc = dalloc_copy(&pc->d_arc_dst, c.arc_dst, na)) ||
+        (rc = dalloc_copy(&pc->d_arc_w, c.arc_w, na)) || (rc = dalloc_copy(&pc->d_rin_off, c.rin_off, V + 1)) ||
+        (rc = dalloc_copy(&pc->d_rin_src, c.rin_src, na)) || (rc = dalloc_copy(&pc->d_rin_eid, c.rin_eid, na)) ||
+        (rc = dalloc_copy(&pc->d_rin_w, c.rin_w, na)) || (rc = dalloc_copy(&pc->d_inc_off, c.inc_off, V + 1)) ||
+        (rc = dalloc_copy(&pc->d_inc_eid, c.inc_eid, c.inc_off[V])) ||
+        (rc = dalloc_copy(&pc->d_nbr_off, c.nbr_off, V + 1)) || (rc = dalloc_copy(&pc->d_nbr_v, c.nbr_v, c.nbr_off[V])) ||
+        (rc = dalloc_copy(&pc->d_nbr_eid, c.nbr_eid, c.nbr_off[V])) || (rc = dalloc_copy(&pc->d_w, pc->h_w, E)) ||
+        (rc = dalloc_copy(&pc->d_eloss, pc->h_eloss, E)) || (rc = dalloc_copy(&pc->d_attached, pc->h_attached, T)) ||
+        (rc = dalloc_copy(&pc->d_self_eid, pc->h_self_eid, T))) {
+        shd_pc_destroy(pc);
+        return rc;
+    }
+    if (pc->has_vloss && (rc = dalloc_copy(&pc->d_vloss, pc->h_vloss, V))) { shd_pc_destroy(pc); return rc; }
+    const size_t TT = (size_t)T * T;
+    if (hipMalloc((void**)&pc->d_dir_lat, 8 * TT) != hipSuccess || hipMalloc((void**)&pc->d_dir_rel, 8 * TT) != hipSuccess ||
+        hipMalloc((void**)&pc->d_adj, TT) != hipSuccess || hipMalloc((void**)&pc->d_self_lat, 8 * T) != hipSuccess ||
+        hipMalloc((void**)&pc->d_self_rel, 8 * T) != hipSuccess || hipMalloc((void**)&pc->d_stats, 8 * 8) != hipSuccess) {
+        shd_pc_destroy(pc);
+        return SHD_ENOMEM;
+    }
+    if (pc->rows_mode) {
+        if (hipMalloc((void**)&pc->d_row_lat, 8 * TT) != hipSuccess ||
+            hipMalloc((void**)&pc->d_row_rel, 8 * TT) != hipSuccess) {
+            shd_pc_destroy(pc);
+            return SHD_ENOMEM;
+        }
+    }
+    pc->info.n_vertices = V;
+    pc->info.n_attached = T;
+    pc->info.is_complete = pc->complete;
+    pc->info.is_directed = pc->directed;
+    pc->info.prefer_direct = pc->prefer_direct;
+    *out = pc;
+    return SHD_OK;
+}
+
+static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
+static constexpr size_t kLdsMax = 160 * 1024;
+
+extern "C" int shd_pc_build(shd_pc* pc) {
+    if (!pc) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(pc->device));
+    const int32_t V = pc->V, T = pc->T;
+    hipStream_t s = pc->stream;
+    int64_t init_stats[8] = {0, 0, 0, 0, 0, (int64_t)kDistInf, 0, 0};
+    SHD_HIP(hipMemcpyAsync(pc->d_stats, init_stats, sizeof(init_stats), hipMemcpyHostToDevice, s));
+    hipEvent_t ev[4];
+    for (auto& e : ev) SHD_HIP(hipEventCreate(&e));
+    SHD_HIP(hipEventRecord(ev[0], s));
+    // direct values + adjacency for every attached pair (used in complete and
+    // prefer-direct modes; cheap otherwise)
+    {
+        const size_t TT = (size_t)T * T;
+        int blocks = (int)std::min<size_t>((TT + 255) / 256, 8192);
+        hipLaunchKernelGGL(k_direct, dim3(blocks), dim3(256), 0, s, T, pc->d_attached, pc->d_nbr_off, pc->d_nbr_v,
+                           pc->d_nbr_eid, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_dir_lat, pc->d_dir_rel, pc->d_adj);
+        hipLaunchKernelGGL(k_self, dim3((T + 255) / 256), dim3(256), 0, s, T, pc->d_attached, pc->d_inc_off,
+                           pc->d_inc_eid, pc->d_w, pc->d_eloss, pc->d_self_lat, pc->d_self_rel);
+        SHD_HIP(hipGetLastError());
+    }
+    SHD_HIP(hipEventRecord(ev[1], s));
+    if (pc->rows_mode) {
+        const size_t lds = lds_bytes_for(V);
+        int ncu = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, pc->device) == hipSuccess) ncu = prop.multiProcessorCount;
+        if (lds <= kLdsMax) {
+            if (V <= 2048) {
+                int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, kLdsMax / lds));
+                int grid = std::min(T, ncu * per_cu);
+                SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<256>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
+                                   pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
+                                   pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
+                                   pc->d_row_lat, pc->d_row_rel, pc->d_stats);
+            } else {
+                int grid = std::min(T, ncu);
+                SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<1024>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                hipLaunchKernelGGL(k_sssp_rows_lds<1024>, dim3(grid), dim3(1024), lds, s, V, T, pc->d_arc_off,
+                                   pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
+                                   pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
+                                   pc->d_row_lat, pc->d_row_rel, pc->d_stats);
+            }
+        } else {
+            const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
+            int grid = std::min(T, ncu * 4);
+            if (!pc->d_scratch || pc->scratch_bytes < per_block * grid) {
+                if (pc->d_scratch) (void)hipFree(pc->d_scratch);
+                pc->scratch_bytes = per_block * grid;
+                SHD_HIP(hipMalloc(&pc->d_scratch, pc->scratch_bytes));
+            }
+            hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
+                               pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
+                               pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row_lat,
+                               pc->d_row_rel, pc->d_stats, (char*)pc->d_scratch, per_block);
+        }
+        SHD_HIP(hipGetLastError());
+    }
+    SHD_HIP(hipEventRecord(ev[2], s));
+    {
+        const size_t TT = (size_t)T * T;
+        int blocks = (int)std::min<size_t>((TT + 255) / 256, 4096);
+        const double* tab = pc->rows_mode ? pc->d_row_lat : pc->d_dir_lat;
+        hipLaunchKernelGGL(k_min_latency, dim3(blocks), dim3(256), 0, s, tab, TT, pc->d_stats);
+        SHD_HIP(hipGetLastError());
+    }
+    SHD_HIP(hipEventRecord(ev[3], s));
+    SHD_HIP(hipStreamSynchronize(s));
+    float ms_dir = 0, ms_rows = 0, ms_all = 0;
+    SHD_HIP(hipEventElapsedTime(&ms_dir, ev[0], ev[1]));
+    SHD_HIP(hipEventElapsedTime(&ms_rows, ev[1], ev[2]));
+    SHD_HIP(hipEventElapsedTime(&ms_all, ev[0], ev[3]));
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    int64_t st[8];
+    SHD_HIP(hipMemcpy(st, pc->d_stats, sizeof(st), hipMemcpyDeviceToHost));
+    pc->info.rows_computed = pc->rows_mode ? T : 0;
+    pc->info.n_ties = st[0];
+    pc->info.max_hops = (int32_t)st[1];
+    pc->info.sssp_iterations_max = (int32_t)st[2];
+    pc->info.n_unroutable = (int32_t)st[3];
+    uint64_t mb = (uint64_t)st[5];
+    double ml;
+    memcpy(&ml, &mb, 8);
+    pc->info.min_latency_ms = ml;
+    pc->info.build_ms_direct = ms_dir;
+    pc->info.build_ms_sssp = ms_rows;
+    pc->info.build_ms_props = 0.0;   // fused into the SSSP kernel
+    pc->info.build_ms_device = ms_all;
+    if (st[4] != 0) {
+        fprintf(stderr, "libshdgpu: %lld latency folds differ from converged distances\n", (long long)st[4]);
+        return SHD_ERANGE;
+    }
+    pc->built = true;
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_get_info(const shd_pc* pc, shd_pc_info* out) {
+    if (!pc || !out) return SHD_EINVAL;
+    *out = pc->info;
+    return SHD_OK;
+}
+
+static int copy_table(shd_pc* pc, const double* dl, const double* dr, int32_t row0, int32_t nrows, double* lat,
+                      double* rel) {
+    if (!pc || !pc->built || row0 < 0 || nrows < 0 || row0 + nrows > pc->T) return SHD_EINVAL;
+    if (!dl) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(pc->device));
+    const size_t off = (size_t)row0 * pc->T, n = (size_t)nrows * pc->T;
+    if (lat) SHD_HIP(hipMemcpy(lat, dl + off, 8 * n, hipMemcpyDeviceToHost));
+    if (rel) SHD_HIP(hipMemcpy(rel, dr + off, 8 * n, hipMemcpyDeviceToHost));
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_copy_rows(shd_pc* pc, int32_t row0, int32_t nrows, double* lat, double* rel) {
+    if (!pc) return SHD_EINVAL;
+    return copy_table(pc, pc->d_row_lat, pc->d_row_rel, row0, nrows, lat, rel);
+}
+extern "C" int shd_pc_copy_direct(shd_pc* pc, int32_t row0, int32_t nrows, double* lat, double* rel) {
+    if (!pc) return SHD_EINVAL;
+    return copy_table(pc, pc->d_dir_lat, pc->d_dir_rel, row0, nrows, lat, rel);
+}
+extern "C" int shd_pc_copy_self(shd_pc* pc, double* lat, double* rel) {
+    if (!pc || !pc->built) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(pc->device));
+    if (lat) SHD_HIP(hipMemcpy(lat, pc->d_self_lat, 8 * (size_t)pc->T, hipMemcpyDeviceToHost));
+    if (rel) SHD_HIP(hipMemcpy(rel, pc->d_self_rel, 8 * (size_t)pc->T, hipMemcpyDeviceToHost));
+    return SHD_OK;
+}
+
+// ------------------------------------------------------------------ lazy lookup (host adapter)
+// The reference stores each unordered pair once, from whichever row ran first
+// (topology.c:1307-1336), and a row for source s runs on the first query
+// (s,d) that misses in both orientations (1987-1990, 2030).  Direct paths
+// are stored by the first query of an adjacent pair (2019-2021).
+static int fetch2(shd_pc* pc, const double* dl, const double* dr, size_t idx, double* lat, double* rel) {
+    SHD_HIP(hipMemcpy(lat, dl + idx, 8, hipMemcpyDeviceToHost));
+    SHD_HIP(hipMemcpy(rel, dr + idx, 8, hipMemcpyDeviceToHost));
+    return SHD_OK;
+}
+
+static void note_min(shd_pc* pc, double lat) {
+    if (pc->min_stored_latency == 0 || lat < pc->min_stored_latency) pc->min_stored_latency = lat;
+}
+
+static int run_row_for_min(shd_pc* pc, int32_t a) {
+    // the row stores every {a,t} not yet stored: track minimumPathLatency
+    const int32_t T = pc->T;
+    double* buf = (double*)malloc(8 * (size_t)T);
+    if (!buf) return SHD_ENOMEM;
+    if (hipMemcpy(buf, pc->d_row_lat + (size_t)a * T, 8 * (size_t)T, hipMemcpyDeviceToHost) != hipSuccess) {
+        free(buf);
+        return SHD_ENODEV;
+    }
+    for (int32_t t = 0; t < T; t++) {
+        const bool stored = (t == a) ? (pc->h_self_rank[a] != kNoRank) : (pc->h_rank[t] != kNoRank);
+        if (stored || buf[t] < 0) continue;
+        if (pc->prefer_direct) {
+            uint8_t adj = 0;
+            if (hipMemcpy(&adj, pc->d_adj + (size_t)a * T + t, 1, hipMemcpyDeviceToHost) != hipSuccess) {
+                free(buf);
+                return SHD_ENODEV;
+            }
+            if (adj) continue;
+        }
+        note_min(pc, buf[t]);
+    }
+    free(buf);
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_lookup(shd_pc* pc, int32_t sv, int32_t dv, double* lat, double* rel) {
+    if (!pc || !pc->built || !lat || !rel || sv < 0 || dv < 0 || sv >= pc->V || dv >= pc->V) return SHD_EINVAL;
+    const int32_t a = pc->h_att_index[sv], b = pc->h_att_index[dv];
+    if (a < 0 || b < 0) { *lat = -1; *rel = -1; return SHD_EINVAL; }
+    SHD_HIP(hipSetDevice(pc->device));
+    const int32_t T = pc->T;
+    uint8_t adj = 0;
+    if (pc->prefer_direct && !pc->complete)
+        SHD_HIP(hipMemcpy(&adj, pc->d_adj + (size_t)a * T + b, 1, hipMemcpyDeviceToHost));
+    if (pc->complete || adj) {
+        int rc = fetch2(pc, pc->d_dir_lat, pc->d_dir_rel, (size_t)a * T + b, lat, rel);
+        if (rc) return rc;
+        if (isnan(*lat)) { *lat = -1; *rel = -1; return SHD_OK; }
+        note_min(pc, *lat);
+        return SHD_OK;
+    }
+    if (a == b) {
+        // self pair: stored by row a ([a] with the self-loop) or by the
+        // self-path computation, whichever came first
+        int32_t ra = pc->h_rank[a], rs = pc->h_self_rank[a];
+        if (ra == kNoRank && rs == kNoRank) {
+            pc->h_self_rank[a] = rs = pc->next_rank++;
+            int rc = fetch2(pc, pc->d_self_lat, pc->d_self_rel, (size_t)a, lat, rel);
+            if (rc) return rc;
+            if (*lat < 0) return SHD_OK;
+            note_min(pc, *lat);
+            return SHD_OK;
+        }
+        if (rs < ra) return fetch2(pc, pc->d_self_lat, pc->d_self_rel, (size_t)a, lat, rel);
+        return fetch2(pc, pc->d_row_lat, pc->d_row_rel, (size_t)a * T + a, lat, rel);
+    }
+    int32_t ra = pc->h_rank[a], rb = pc->h_rank[b];
+    // undirected: a miss needs both orientations missing (1987-1990);
+    // directed: only (a,b) is checked, so a row reruns when b stored {a,b}
+    const bool hit = pc->directed ? (ra != kNoRank && ra < rb) : (ra != kNoRank || rb != kNoRank);
+    bool failed = false;
+    if (!hit) {
+        if (pc->h_rank[a] == kNoRank) {
+            int rc = run_row_for_min(pc, a);
+            if (rc) return rc;
+            pc->h_rank[a] = pc->next_rank++;
+        }
+        // the row fails as a whole when its [a] entry has no self-loop
+        // (computePathProperties returns FALSE, topology.c:1490-1495, 1857)
+        if (pc->h_self_eid[a] < 0) failed = true;
+        ra = pc->h_rank[a];
+    }
+    if (failed) { *lat = -1; *rel = -1; return SHD_OK; }
+    // value from whichever endpoint's row ran first; on directed graphs this can
+    // be the reverse path (topology.c:2034-2037)
+    if (ra != kNoRank && (rb == kNoRank || ra < rb))
+        return fetch2(pc, pc->d_row_lat, pc->d_row_rel, (size_t)a * T + b, lat, rel);
+    return fetch2(pc, pc->d_row_lat, pc->d_row_rel, (size_t)b * T + a, lat, rel);
+}
+
+extern "C" int shd_pc_count_packet(shd_pc* pc, int32_t sv, int32_t dv) {
+    double lat, rel;
+    int rc = shd_pc_lookup(pc, sv, dv, &lat, &rel);
+    if (rc) return rc;
+    if (lat < 0) return SHD_OK;
+    auto* m = (std::unordered_map<uint64_t, uint64_t>*)pc->counts;
+    int32_t a = pc->h_att_index[sv], b = pc->h_att_index[dv];
+    uint64_t key = ((uint64_t)(uint32_t)std::min(a, b) << 32) | (uint32_t)std::max(a, b);
+    (*m)[key]++;
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_packet_count(shd_pc* pc, int32_t sv, int32_t dv, uint64_t* count) {
+    if (!pc || !count || sv < 0 || dv < 0 || sv >= pc->V || dv >= pc->V) return SHD_EINVAL;
+    int32_t a = pc->h_att_index[sv], b = pc->h_att_index[dv];
+    if (a < 0 || b < 0) return SHD_EINVAL;
+    auto* m = (std::unordered_map<uint64_t, uint64_t>*)pc->counts;
+    uint64_t key = ((uint64_t)(uint32_t)std::min(a, b) << 32) | (uint32_t)std::max(a, b);
+    auto it = m->find(key);
+    *count = it == m->end() ? 0 : it->second;
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_min_time_jump(shd_pc* pc, uint64_t runahead_ns, uint64_t* jump_ns) {
+    if (!pc || !jump_ns) return SHD_EINVAL;
+    // master_updateMinTimeJump (master.c:148-159): floor(ms) * 1e6 ns;
+    // _master_getMinTimeJump (133-146): 10 ms default if 0, >= runahead
+    uint64_t j = (uint64_t)floor(pc->min_stored_latency) * SHD_MS;
+    if (j == 0) j = 10 * SHD_MS;
+    if (runahead_ns > j) j = runahead_ns;
+    *jump_ns = j;
+    return SHD_OK;
+}
+
+extern "C" void shd_pc_destroy(shd_pc* pc) {
+    if (!pc) return;
+    (void)hipSetDevice(pc->device);
+    pc_free_device(pc);
+    if (pc->stream) (void)hipStreamDestroy(pc->stream);
+    shd_csr_free(&pc->csr);
+    free(pc->h_attached); free(pc->h_att_index); free(pc->h_w); free(pc->h_eloss); free(pc->h_vloss);
+    free(pc->h_self_eid); free(pc->h_rank); free(pc->h_self_rank); free(pc->h_direct_stored);
+    delete (std::unordered_map<uint64_t, uint64_t>*)pc->counts;
+    delete pc;
+}

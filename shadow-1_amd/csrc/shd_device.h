@@ -1,0 +1,69 @@
+// shd_device.h -- internal declarations shared by the libshdgpu HIP sources.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/shdgpu.h"
+#include "../host/shd_host.h"
+
+#define SHD_HIP(x)                                                      \
+    do {                                                                \
+        hipError_t e_ = (x);                                            \
+        if (e_ != hipSuccess) {                                         \
+            shd_set_hip_error(e_, #x, __FILE__, __LINE__);              \
+            return SHD_ENODEV;                                          \
+        }                                                               \
+    } while (0)
+
+void shd_set_hip_error(hipError_t e, const char* what, const char* file, int line);
+
+static constexpr uint64_t kDistInf = 0x7FF0000000000000ull;   // +inf as u64
+static constexpr int32_t kNoRank = 0x7FFFFFFF;
+
+// Path-cache device state (owned by shd_pc, consumed by the engine).
+struct shd_pc {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t flags = 0;
+    shd_csr csr{};
+    shd_graph_props props{};
+    int32_t V = 0, E = 0, T = 0;
+    int directed = 0, complete = 0, prefer_direct = 0, rows_mode = 0, has_vloss = 0;
+    // host copies
+    int32_t* h_attached = nullptr;      // [T]
+    int32_t* h_att_index = nullptr;     // [V] -> attached index or -1
+    double* h_w = nullptr;              // [E]
+    double* h_eloss = nullptr;          // [E]
+    double* h_vloss = nullptr;          // [V] NaN = absent
+    int32_t* h_self_eid = nullptr;      // [T] self-loop eid or -1
+    // device graph
+    int32_t *d_arc_off = nullptr, *d_arc_dst = nullptr;
+    double* d_arc_w = nullptr;
+    int32_t *d_rin_off = nullptr, *d_rin_src = nullptr, *d_rin_eid = nullptr;
+    double* d_rin_w = nullptr;
+    int32_t *d_inc_off = nullptr, *d_inc_eid = nullptr;
+    int32_t *d_nbr_off = nullptr, *d_nbr_v = nullptr, *d_nbr_eid = nullptr;
+    double *d_w = nullptr, *d_eloss = nullptr, *d_vloss = nullptr;
+    int32_t *d_attached = nullptr, *d_self_eid = nullptr;
+    // device tables [T][T] and [T]
+    double *d_row_lat = nullptr, *d_row_rel = nullptr;
+    double *d_dir_lat = nullptr, *d_dir_rel = nullptr;
+    double *d_self_lat = nullptr, *d_self_rel = nullptr;
+    uint8_t* d_adj = nullptr;           // [T][T] 1 = adjacent (direct path exists)
+    void* d_scratch = nullptr;          // global-memory SSSP scratch (large V)
+    size_t scratch_bytes = 0;
+    int64_t* d_stats = nullptr;         // ties, max hops, max iters, unroutable, lat mismatch, minlat bits
+    bool built = false;
+    shd_pc_info info{};
+    // host lazy-cache adapter state (shd_pc_lookup)
+    int32_t* h_rank = nullptr;          // [T] row run order, kNoRank if never
+    int32_t* h_self_rank = nullptr;     // [T] self-path store order
+    uint8_t* h_direct_stored = nullptr; // lazily allocated [T*T] bits for direct/adjacent stores
+    int32_t next_rank = 0;
+    double min_stored_latency = 0.0;
+    void* counts = nullptr;             // std::unordered_map<uint64_t,uint64_t>*
+};
+
+// resolved value for a (src attached idx, dst attached idx) pair given ranks
+// (device + host): see DESIGN.md "First-touch rule".

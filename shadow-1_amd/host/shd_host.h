@@ -1,0 +1,46 @@
+/*
+ * shd_host.h -- internal host-side structures of libshdgpu (not part of the
+ * C-ABI).  The CSR built here is the device layout of the topology graph.
+ */
+#ifndef SHD_HOST_H
+#define SHD_HOST_H
+
+#include <stdint.h>
+
+#include "../../include/shdgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * Graph index in the orders the reference depends on:
+ *  - inc_*: igraph_incident(v, IGRAPH_OUT) order (undirected: edges stored with
+ *    from=max, to=min; out-list sorted by (to,eid) then in-list sorted by
+ *    (from,eid); a self-loop appears in both).  Used by the self-path scan
+ *    (topology.c:1559-1603, first strict minimum).
+ *  - arc_*: relaxation arcs v -> x for SSSP (self-loops dropped; they never
+ *    improve a distance), with the arc weight copied next to the head so one
+ *    relaxation reads 12 contiguous bytes.
+ *  - rin_*: reverse arcs x <- v (for undirected graphs identical to arc_*),
+ *    used to pick each vertex's shortest-path parent after convergence.
+ *  - nbr_*: per-vertex neighbour list sorted by (neighbour, eid) for
+ *    igraph_get_eid (lowest eid among parallel edges).
+ */
+typedef struct shd_csr {
+    int32_t V, E, directed;
+    int32_t* inc_off; int32_t* inc_eid;
+    int32_t* arc_off; int32_t* arc_dst; int32_t* arc_eid; double* arc_w;
+    int32_t* rin_off; int32_t* rin_src; int32_t* rin_eid; double* rin_w;
+    int32_t* nbr_off; int32_t* nbr_v; int32_t* nbr_eid;
+    int32_t max_degree;
+} shd_csr;
+
+int shd_csr_build(const shd_graph* g, shd_csr* out);
+void shd_csr_free(shd_csr* c);
+int32_t shd_csr_get_eid(const shd_csr* c, int32_t a, int32_t b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,283 @@
+"""ctypes binding of libshdgpu (include/shdgpu.h).
+
+This is the Python mirror of the C-ABI a Shadow maintainer would bind (see
+INTEGRATION.md).  It loads the in-tree ``libshdgpu.so`` built by
+``__graft_entry__.build()`` and fails loudly when it is missing: there is no
+CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libshdgpu.so")
+
+SHD_MS = 1_000_000
+SHD_SEC = 1_000_000_000
+SHD_MTU = 1500
+SHD_HEADER_UDP = 42
+
+EV_HEARTBEAT, EV_REFILL, EV_REFILL_LO, EV_APP_START, EV_PACKET, EV_LOCAL, EV_NOTIFY = range(1, 8)
+TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL = range(1, 8)
+
+ERRORS = {
+    0: "ok", -22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -75: "EOVERFLOW",
+    -34: "ERANGE", -125: "EAMBIG", -107: "ENOTCONN",
+}
+
+
+class ShdError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        raise ShdError(f"{what} failed: {rc} ({ERRORS.get(rc, '?')})")
+
+
+P = C.POINTER
+
+
+class Graph(C.Structure):
+    _fields_ = [
+        ("n_vertices", C.c_int32), ("n_edges", C.c_int32),
+        ("directed", C.c_int32), ("prefer_direct", C.c_int32),
+        ("edge_src", P(C.c_int32)), ("edge_dst", P(C.c_int32)),
+        ("edge_latency", P(C.c_double)), ("edge_loss", P(C.c_double)),
+        ("vertex_loss", P(C.c_double)),
+    ]
+
+
+class GraphProps(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "is_connected", "is_complete", "is_directed", "prefer_direct", "n_self_loops",
+        "max_out_degree")]
+
+
+class GraphML(C.Structure):
+    _fields_ = [
+        ("g", Graph), ("bw_down", P(C.c_double)), ("bw_up", P(C.c_double)),
+        ("vertex_id", P(C.c_char_p)), ("vertex_ip", P(C.c_char_p)),
+        ("vertex_citycode", P(C.c_char_p)), ("vertex_countrycode", P(C.c_char_p)),
+        ("vertex_geocode", P(C.c_char_p)), ("vertex_type", P(C.c_char_p)),
+        ("edge_jitter", P(C.c_double)),
+    ]
+
+
+class PcInfo(C.Structure):
+    _fields_ = [
+        ("n_vertices", C.c_int32), ("n_attached", C.c_int32), ("is_complete", C.c_int32),
+        ("is_directed", C.c_int32), ("prefer_direct", C.c_int32), ("rows_computed", C.c_int32),
+        ("n_ties", C.c_int64), ("max_hops", C.c_int32), ("sssp_iterations_max", C.c_int32),
+        ("n_unroutable", C.c_int32), ("min_latency_ms", C.c_double),
+        ("build_ms_device", C.c_double), ("build_ms_sssp", C.c_double),
+        ("build_ms_props", C.c_double), ("build_ms_direct", C.c_double),
+    ]
+
+
+class Model(C.Structure):
+    _fields_ = [
+        ("n_hosts", C.c_int32), ("_pad0", C.c_int32),
+        ("host_vertex", P(C.c_int32)), ("host_rng", P(C.c_uint32)),
+        ("bw_down_kibps", P(C.c_uint64)), ("bw_up_kibps", P(C.c_uint64)),
+        ("dest_cum", P(C.c_double)),
+        ("end_time", C.c_uint64), ("bootstrap_end", C.c_uint64),
+        ("heartbeat_interval", C.c_uint64), ("app_start", C.c_uint64),
+        ("load", C.c_uint32), ("payload", C.c_uint32), ("trace", C.c_uint32),
+        ("evq_cap", C.c_uint32), ("inbox_cap", C.c_uint32), ("codelq_cap", C.c_uint32),
+        ("txq_cap", C.c_uint32), ("_pad1", C.c_uint32),
+    ]
+
+
+class Event(C.Structure):
+    _fields_ = [("time", C.c_uint64), ("seq", C.c_uint64), ("src", C.c_uint32),
+                ("dst", C.c_uint32), ("pkt", C.c_uint32), ("kind", C.c_uint32)]
+
+
+class TraceRec(C.Structure):
+    _fields_ = [("time", C.c_uint64), ("seq", C.c_uint64), ("host", C.c_uint32),
+                ("peer", C.c_uint32), ("pkt", C.c_uint32), ("kind", C.c_uint32)]
+
+
+TRACE_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("peer", "<u4"),
+                        ("pkt", "<u4"), ("kind", "<u4")])
+
+
+class HostDigest(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "ev_seq", "rx_remaining", "tx_remaining", "codel_total", "codel_interval_expire",
+        "codel_next_drop", "n_events", "n_pkt_events", "n_sent", "n_inet_drop",
+        "n_codel_drop", "n_recv")] + [(n, C.c_uint32) for n in (
+            "rng", "pkt_seq", "codel_mode", "codel_count", "codel_drop_count",
+            "codel_drop_count_last", "unread", "flags")]
+
+
+DIGEST_DTYPE = np.dtype([(n, "<u8") for n in (
+    "ev_seq", "rx_remaining", "tx_remaining", "codel_total", "codel_interval_expire",
+    "codel_next_drop", "n_events", "n_pkt_events", "n_sent", "n_inet_drop", "n_codel_drop",
+    "n_recv")] + [(n, "<u4") for n in ("rng", "pkt_seq", "codel_mode", "codel_count",
+                                      "codel_drop_count", "codel_drop_count_last", "unread",
+                                      "flags")])
+assert DIGEST_DTYPE.itemsize == C.sizeof(HostDigest)
+assert TRACE_DTYPE.itemsize == C.sizeof(TraceRec) == 32
+assert C.sizeof(Event) == 32
+
+
+class RoundSummary(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "window_start", "window_end", "next_time", "n_events", "n_pkt_events", "n_pending",
+        "n_remote")] + [("error", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class RunStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in (
+        "n_rounds", "n_events", "n_pkt_events", "n_pending_resolved", "window_ns",
+        "final_time")] + [("device_ms_round_kernel", C.c_double), ("wall_ms", C.c_double),
+                          ("error", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+# exported symbols (checked by tests/test_abi.py against include/shdgpu.h)
+_SIGS = {
+    "shd_graph_check": (C.c_int, [P(Graph), P(GraphProps)]),
+    "shd_graphml_load_file": (C.c_int, [C.c_char_p, P(P(GraphML))]),
+    "shd_graphml_load_string": (C.c_int, [C.c_char_p, C.c_size_t, P(P(GraphML))]),
+    "shd_graphml_free": (None, [P(GraphML)]),
+    "shd_pc_create": (C.c_int, [P(Graph), P(C.c_int32), C.c_int32, C.c_uint32, C.c_int,
+                                P(C.c_void_p)]),
+    "shd_pc_build": (C.c_int, [C.c_void_p]),
+    "shd_pc_get_info": (C.c_int, [C.c_void_p, P(PcInfo)]),
+    "shd_pc_copy_rows": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double),
+                                   P(C.c_double)]),
+    "shd_pc_copy_direct": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double),
+                                     P(C.c_double)]),
+    "shd_pc_copy_self": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double)]),
+    "shd_pc_lookup": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double),
+                                P(C.c_double)]),
+    "shd_pc_count_packet": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    "shd_pc_packet_count": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint64)]),
+    "shd_pc_min_time_jump": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "shd_pc_destroy": (None, [C.c_void_p]),
+    "shd_rand_r": (C.c_int32, [P(C.c_uint32)]),
+    "shd_next_double": (C.c_double, [P(C.c_uint32)]),
+    "shd_next_uint": (C.c_uint32, [P(C.c_uint32)]),
+    "shd_seed_chain": (C.c_int, [C.c_uint32, C.c_int32, P(C.c_uint32)]),
+    "shd_topology_attach": (C.c_int, [P(GraphML), P(C.c_uint32), C.c_char_p, C.c_char_p,
+                                      C.c_char_p, C.c_char_p, C.c_char_p, P(C.c_int32),
+                                      P(C.c_uint64), P(C.c_uint64)]),
+    "shd_eng_create": (C.c_int, [P(Model), C.c_void_p, C.c_int32, C.c_int32, C.c_int,
+                                 P(C.c_void_p)]),
+    "shd_eng_window": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "shd_eng_boot": (C.c_int, [C.c_void_p]),
+    "shd_eng_run_round": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(RoundSummary)]),
+    "shd_eng_run": (C.c_int, [C.c_void_p, P(RunStats)]),
+    "shd_eng_remote_counts": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_int32), P(C.c_uint64)]),
+    "shd_eng_remote_buffer": (C.c_int, [C.c_void_p, P(C.c_void_p), P(C.c_uint64)]),
+    "shd_eng_ingest": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "shd_eng_next_time": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "shd_eng_pending_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "shd_eng_resolve_pending": (C.c_int, [C.c_void_p]),
+    "shd_eng_trace_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "shd_eng_trace_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "shd_eng_digest": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "shd_eng_stream": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
+    "shd_eng_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_double)]),
+    "shd_eng_destroy": (None, [C.c_void_p]),
+    "shd_version": (C.c_char_p, []),
+    "shd_device_count": (C.c_int, [P(C.c_int)]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libshdgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ShdError(f"{LIB_PATH} missing: run __graft_entry__.build() first "
+                           "(there is no CPU fallback)")
+        l = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGS)
+
+
+def as_ptr(a: np.ndarray, ctype):
+    return a.ctypes.data_as(P(ctype))
+
+
+# ----------------------------------------------------------------- helpers
+class GraphArrays:
+    """Owns the numpy arrays behind a ``Graph`` struct (document order)."""
+
+    def __init__(self, n_vertices, src, dst, latency, loss, vertex_loss=None,
+                 directed=False, prefer_direct=False):
+        self.n_vertices = int(n_vertices)
+        self.src = np.ascontiguousarray(src, dtype=np.int32)
+        self.dst = np.ascontiguousarray(dst, dtype=np.int32)
+        self.latency = np.ascontiguousarray(latency, dtype=np.float64)
+        self.loss = np.ascontiguousarray(loss, dtype=np.float64)
+        self.vertex_loss = (None if vertex_loss is None else
+                            np.ascontiguousarray(vertex_loss, dtype=np.float64))
+        self.directed = bool(directed)
+        self.prefer_direct = bool(prefer_direct)
+        self.struct = Graph(
+            self.n_vertices, len(self.src), int(self.directed), int(self.prefer_direct),
+            as_ptr(self.src, C.c_int32), as_ptr(self.dst, C.c_int32),
+            as_ptr(self.latency, C.c_double), as_ptr(self.loss, C.c_double),
+            None if self.vertex_loss is None else as_ptr(self.vertex_loss, C.c_double))
+
+    @property
+    def n_edges(self):
+        return len(self.src)
+
+
+def graph_from_graphml(gm_ptr) -> GraphArrays:
+    gm = gm_ptr.contents
+    g = gm.g
+    V, E = g.n_vertices, g.n_edges
+    src = np.ctypeslib.as_array(g.edge_src, (E,)).copy()
+    dst = np.ctypeslib.as_array(g.edge_dst, (E,)).copy()
+    lat = np.ctypeslib.as_array(g.edge_latency, (E,)).copy()
+    loss = np.ctypeslib.as_array(g.edge_loss, (E,)).copy()
+    vl = np.ctypeslib.as_array(g.vertex_loss, (V,)).copy() if g.vertex_loss else None
+    return GraphArrays(V, src, dst, lat, loss, vl, bool(g.directed), bool(g.prefer_direct))
+
+
+class ModelArrays:
+    """Owns the numpy arrays behind a ``Model`` struct."""
+
+    def __init__(self, host_vertex, host_rng, bw_down, bw_up, dest_cum, *, end_time,
+                 app_start=1 * SHD_SEC, load=16, payload=1, heartbeat_interval=SHD_SEC,
+                 bootstrap_end=0, trace=False, evq_cap=0, inbox_cap=0, codelq_cap=0,
+                 txq_cap=0):
+        self.host_vertex = np.ascontiguousarray(host_vertex, dtype=np.int32)
+        self.host_rng = np.ascontiguousarray(host_rng, dtype=np.uint32)
+        self.bw_down = np.ascontiguousarray(bw_down, dtype=np.uint64)
+        self.bw_up = np.ascontiguousarray(bw_up, dtype=np.uint64)
+        self.dest_cum = np.ascontiguousarray(dest_cum, dtype=np.float64)
+        H = len(self.host_vertex)
+        assert all(len(a) == H for a in (self.host_rng, self.bw_down, self.bw_up, self.dest_cum))
+        self.params = dict(end_time=int(end_time), app_start=int(app_start), load=int(load),
+                           payload=int(payload), heartbeat_interval=int(heartbeat_interval),
+                           bootstrap_end=int(bootstrap_end), trace=int(bool(trace)))
+        self.struct = Model(
+            H, 0, as_ptr(self.host_vertex, C.c_int32), as_ptr(self.host_rng, C.c_uint32),
+            as_ptr(self.bw_down, C.c_uint64), as_ptr(self.bw_up, C.c_uint64),
+            as_ptr(self.dest_cum, C.c_double), int(end_time), int(bootstrap_end),
+            int(heartbeat_interval), int(app_start), int(load), int(payload), int(bool(trace)),
+            int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), 0)
+
+    @property
+    def n_hosts(self):
+        return len(self.host_vertex)

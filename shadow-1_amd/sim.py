@@ -1,0 +1,155 @@
+"""Python host driver over libshdgpu: path cache + engine handles.
+
+This mirrors how Shadow's C host side would drive the C-ABI:
+master/slave create the path cache from the topology (topology_new), hosts are
+registered (seeds, attach, bandwidth), and the scheduler loop advances rounds.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+import shdgpu as S
+
+SHD_PC_FORCE_ROWS = 1
+
+
+class PathCache:
+    def __init__(self, g: S.GraphArrays, attached, flags=0, device=0, build=True):
+        self.g = g
+        self.att = np.ascontiguousarray(attached, dtype=np.int32)
+        self.ptr = C.c_void_p()
+        S.check(S.lib().shd_pc_create(C.byref(g.struct), S.as_ptr(self.att, C.c_int32), len(self.att),
+                                      flags, device, C.byref(self.ptr)), "shd_pc_create")
+        if build:
+            self.build()
+
+    def build(self):
+        S.check(S.lib().shd_pc_build(self.ptr), "shd_pc_build")
+
+    def info(self) -> S.PcInfo:
+        i = S.PcInfo()
+        S.check(S.lib().shd_pc_get_info(self.ptr, C.byref(i)), "shd_pc_get_info")
+        return i
+
+    def _table(self, fn, row0, nrows):
+        T = len(self.att)
+        lat = np.empty((nrows, T)); rel = np.empty((nrows, T))
+        S.check(fn(self.ptr, row0, nrows, S.as_ptr(lat, C.c_double), S.as_ptr(rel, C.c_double)),
+                "copy table")
+        return lat, rel
+
+    def rows(self, row0=0, nrows=None):
+        n = len(self.att) - row0 if nrows is None else nrows
+        return self._table(S.lib().shd_pc_copy_rows, row0, n)
+
+    def direct(self, row0=0, nrows=None):
+        n = len(self.att) - row0 if nrows is None else nrows
+        return self._table(S.lib().shd_pc_copy_direct, row0, n)
+
+    def self_values(self):
+        T = len(self.att)
+        lat = np.empty(T); rel = np.empty(T)
+        S.check(S.lib().shd_pc_copy_self(self.ptr, S.as_ptr(lat, C.c_double), S.as_ptr(rel, C.c_double)),
+                "copy self")
+        return lat, rel
+
+    def lookup(self, s, d):
+        a, b = C.c_double(), C.c_double()
+        S.check(S.lib().shd_pc_lookup(self.ptr, int(s), int(d), C.byref(a), C.byref(b)), "lookup")
+        return a.value, b.value
+
+    def close(self):
+        if self.ptr:
+            S.lib().shd_pc_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One engine = the hosts [host_begin, host_end) of a model on one GPU."""
+
+    def __init__(self, model: S.ModelArrays, pc: PathCache, host_begin=0, host_end=None, device=0):
+        self.model = model
+        self.pc = pc
+        self.h0 = int(host_begin)
+        self.h1 = int(model.n_hosts if host_end is None else host_end)
+        self.ptr = C.c_void_p()
+        S.check(S.lib().shd_eng_create(C.byref(model.struct), pc.ptr, self.h0, self.h1, device,
+                                       C.byref(self.ptr)), "shd_eng_create")
+
+    @property
+    def window(self) -> int:
+        w = C.c_uint64()
+        S.check(S.lib().shd_eng_window(self.ptr, C.byref(w)), "shd_eng_window")
+        return w.value
+
+    def boot(self):
+        S.check(S.lib().shd_eng_boot(self.ptr), "shd_eng_boot")
+
+    def run(self) -> S.RunStats:
+        st = S.RunStats()
+        rc = S.lib().shd_eng_run(self.ptr, C.byref(st))
+        S.check(rc, f"shd_eng_run (error bits {st.error:#x})")
+        return st
+
+    def run_round(self, ws, we) -> S.RoundSummary:
+        r = S.RoundSummary()
+        rc = S.lib().shd_eng_run_round(self.ptr, int(ws), int(we), C.byref(r))
+        S.check(rc, f"shd_eng_run_round (error bits {r.error:#x})")
+        return r
+
+    def next_time(self) -> int:
+        t = C.c_uint64()
+        S.check(S.lib().shd_eng_next_time(self.ptr, C.byref(t)), "next_time")
+        return t.value
+
+    def trace(self) -> np.ndarray:
+        n = C.c_uint64()
+        S.check(S.lib().shd_eng_trace_count(self.ptr, C.byref(n)), "trace_count")
+        out = np.empty(n.value, dtype=S.TRACE_DTYPE)
+        got = C.c_uint64()
+        if n.value:
+            S.check(S.lib().shd_eng_trace_copy(self.ptr, out.ctypes.data, n.value, C.byref(got)),
+                    "trace_copy")
+        return out[:got.value] if n.value else out
+
+    def digest(self) -> np.ndarray:
+        out = np.empty(self.h1 - self.h0, dtype=S.DIGEST_DTYPE)
+        S.check(S.lib().shd_eng_digest(self.ptr, out.ctypes.data), "digest")
+        return out
+
+    def remote(self):
+        p = C.c_void_p(); n = C.c_uint64()
+        S.check(S.lib().shd_eng_remote_buffer(self.ptr, C.byref(p), C.byref(n)), "remote_buffer")
+        return p.value, n.value
+
+    def ingest(self, dev_ptr, n):
+        S.check(S.lib().shd_eng_ingest(self.ptr, C.c_void_p(dev_ptr), int(n)), "ingest")
+
+    def last_kernel_ms(self) -> float:
+        v = C.c_double()
+        S.check(S.lib().shd_eng_last_kernel_ms(self.ptr, C.byref(v)), "last_kernel_ms")
+        return v.value
+
+    def close(self):
+        if self.ptr:
+            S.lib().shd_eng_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def sort_trace(tr: np.ndarray) -> np.ndarray:
+    """Canonical order for multiset comparison of traces."""
+    return np.sort(tr, order=["time", "host", "kind", "peer", "pkt", "seq"])

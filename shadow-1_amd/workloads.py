@@ -1,0 +1,178 @@
+"""Synthetic workloads for the BASELINE configs (host side, numpy).
+
+The reference has no generators for these configs; they are defined in
+SURVEY.md section 8(d) / BASELINE.md section 2.2:
+
+* C2  the bundled topology (resource/topology.graphml.xml.xz, 183 vertices,
+      complete) -- a committed data fixture under tests/golden/.
+* C3  PHOLD-UDP, 10k hosts, one per vertex of a 10k-vertex random geometric
+      graph (unit square, radius 1.5x the connectivity threshold, latency
+      1 + 50*distance ms, edge loss U[0, 0.01], a self-loop on every vertex).
+* C5  the same graph family with 100 hosts per vertex (1M hosts at V = 10k).
+
+Host ids are dense registration order; host seeds follow the reference seed
+chain (master.c:95,417 -> slave.c:182,198,301) and each host's RNG then
+consumes the one nextDouble draw of topology_attach (topology.c:2326-2334),
+which the reference makes even on an exact-IP match.
+"""
+from __future__ import annotations
+
+import lzma
+import math
+import os
+
+import numpy as np
+
+import shdgpu as S
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUNDLED_XZ = os.path.join(REPO, "tests", "golden", "topology.graphml.xml.xz")
+
+
+def bundled_graphml_bytes() -> bytes:
+    with lzma.open(BUNDLED_XZ) as f:
+        return f.read()
+
+
+def load_graphml_bytes(xml: bytes):
+    """Parse graphml with libshdgpu's loader; returns (GraphArrays, GraphML*)."""
+    lib = S.lib()
+    gm = S.P(S.GraphML)()
+    S.check(lib.shd_graphml_load_string(xml, len(xml), S.C.byref(gm)), "shd_graphml_load_string")
+    return S.graph_from_graphml(gm), gm
+
+
+def bundled_graph():
+    g, gm = load_graphml_bytes(bundled_graphml_bytes())
+    S.lib().shd_graphml_free(gm)
+    return g
+
+
+def geometric_graph(n_vertices: int, seed: int = 1, radius_factor: float = 1.5,
+                    loss_max: float = 0.01, self_loops: bool = True,
+                    vertex_loss: bool = False, max_tries: int = 20) -> S.GraphArrays:
+    """Random geometric graph in the unit square; connected (retries seeds)."""
+    rng = np.random.default_rng(seed)
+    V = int(n_vertices)
+    r = radius_factor * math.sqrt(math.log(max(V, 2)) / (math.pi * max(V, 2)))
+    for _ in range(max_tries):
+        pts = rng.random((V, 2))
+        # grid bucketing: O(V * degree)
+        cell = max(r, 1e-9)
+        ncell = max(1, int(1.0 / cell))
+        cx = np.minimum((pts[:, 0] * ncell).astype(np.int64), ncell - 1)
+        cy = np.minimum((pts[:, 1] * ncell).astype(np.int64), ncell - 1)
+        cid = cx * ncell + cy
+        order = np.argsort(cid, kind="stable")
+        cs = cid[order]
+        starts = np.searchsorted(cs, np.arange(ncell * ncell))
+        ends = np.searchsorted(cs, np.arange(ncell * ncell), side="right")
+        src, dst = [], []
+        for dx in (-1, 0, 1):
+            for dy in (-1, 0, 1):
+                nx, ny = cx + dx, cy + dy
+                ok = (nx >= 0) & (nx < ncell) & (ny >= 0) & (ny < ncell)
+                for i in np.nonzero(ok)[0]:
+                    c = nx[i] * ncell + ny[i]
+                    js = order[starts[c]:ends[c]]
+                    js = js[js > i]
+                    if len(js) == 0:
+                        continue
+                    d = np.hypot(pts[js, 0] - pts[i, 0], pts[js, 1] - pts[i, 1])
+                    js = js[d <= r]
+                    src.append(np.full(len(js), i, dtype=np.int64))
+                    dst.append(js)
+        src = np.concatenate(src) if src else np.zeros(0, np.int64)
+        dst = np.concatenate(dst) if dst else np.zeros(0, np.int64)
+        # connectivity check (union-find)
+        parent = np.arange(V)
+
+        def find(x):
+            while parent[x] != x:
+                parent[x] = parent[parent[x]]
+                x = parent[x]
+            return x
+        for a, b in zip(src.tolist(), dst.tolist()):
+            ra, rb = find(a), find(b)
+            if ra != rb:
+                parent[ra] = rb
+        roots = {find(i) for i in range(V)}
+        if len(roots) == 1:
+            break
+        r *= 1.1
+    else:
+        raise RuntimeError("could not generate a connected geometric graph")
+    dist = np.hypot(pts[src, 0] - pts[dst, 0], pts[src, 1] - pts[dst, 1])
+    lat = 1.0 + 50.0 * dist
+    loss = rng.random(len(src)) * loss_max
+    # document order: shuffle edges so ids are not sorted by endpoint
+    perm = rng.permutation(len(src))
+    src, dst, lat, loss = src[perm], dst[perm], lat[perm], loss[perm]
+    if self_loops:
+        sl_lat = 1.0 + 50.0 * r * rng.random(V) + 0.5
+        sl_loss = rng.random(V) * loss_max
+        src = np.concatenate([src, np.arange(V)])
+        dst = np.concatenate([dst, np.arange(V)])
+        lat = np.concatenate([lat, sl_lat])
+        loss = np.concatenate([loss, sl_loss])
+    vl = rng.random(V) * 0.001 if vertex_loss else None
+    return S.GraphArrays(V, src, dst, lat, loss, vl)
+
+
+def seed_chain(n_hosts: int, options_seed: int = 1) -> np.ndarray:
+    seeds = np.zeros(n_hosts, dtype=np.uint32)
+    S.check(S.lib().shd_seed_chain(options_seed, n_hosts, S.as_ptr(seeds, S.C.c_uint32)),
+            "shd_seed_chain")
+    return seeds
+
+
+def after_attach_draw(seeds: np.ndarray) -> np.ndarray:
+    """Advance each host RNG by the one attach draw (topology.c:2326-2334)."""
+    out = seeds.copy()
+    # rand_r = 3 LCG steps; vectorised
+    x = out.astype(np.uint64)
+    for _ in range(3):
+        x = (x * np.uint64(1103515245) + np.uint64(12345)) & np.uint64(0xFFFFFFFF)
+    return x.astype(np.uint32)
+
+
+def uniform_cum(n_hosts: int) -> np.ndarray:
+    """PHOLD cumulative weights for equal weights (test_phold.c:160-178):
+    cumulative += w_i / total, accumulated in order in f64."""
+    w = 1.0
+    total = 0.0
+    for _ in range(1):  # total = sum of n ones, exact
+        total = float(n_hosts) * w
+    norm = w / total
+    cum = np.empty(n_hosts, dtype=np.float64)
+    c = 0.0
+    # sequential f64 accumulation (np.cumsum is sequential for 1-D float64)
+    cum[:] = np.cumsum(np.full(n_hosts, norm, dtype=np.float64))
+    # guard: np.cumsum must equal the scalar left fold
+    if n_hosts <= 4096:
+        for i in range(n_hosts):
+            c += norm
+            assert cum[i] == c
+    return cum
+
+
+def phold_model(host_vertex, *, end_time, seed=1, bw_down=10240, bw_up=10240, load=16,
+                payload=1, app_start=S.SHD_SEC, heartbeat=S.SHD_SEC, bootstrap_end=0,
+                trace=False, **caps) -> S.ModelArrays:
+    H = len(host_vertex)
+    seeds = after_attach_draw(seed_chain(H, seed))
+    bd = np.broadcast_to(np.asarray(bw_down, dtype=np.uint64), (H,)).copy()
+    bu = np.broadcast_to(np.asarray(bw_up, dtype=np.uint64), (H,)).copy()
+    return S.ModelArrays(host_vertex, seeds, bd, bu, uniform_cum(H), end_time=end_time,
+                         app_start=app_start, load=load, payload=payload,
+                         heartbeat_interval=heartbeat, bootstrap_end=bootstrap_end, trace=trace,
+                         **caps)
+
+
+def hosts_on_vertices(n_vertices: int, hosts_per_vertex: int) -> np.ndarray:
+    """Registration order: host i on vertex i // hosts_per_vertex."""
+    return np.repeat(np.arange(n_vertices, dtype=np.int32), hosts_per_vertex)
+
+
+def attached_vertices(host_vertex) -> np.ndarray:
+    return np.unique(np.asarray(host_vertex, dtype=np.int32))

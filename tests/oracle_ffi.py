@@ -1,0 +1,159 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The oracle is the CPU restatement of the reference (see oracle/oracle.h); it is
+the checker for libshdgpu and is never on the product path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+import shdgpu as S
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "oracle", "liboracle.so")
+P = C.POINTER
+
+
+class ORun(C.Structure):
+    _fields_ = [("trace", P(S.TraceRec)), ("n_trace", C.c_uint64), ("cap_trace", C.c_uint64),
+                ("digest", P(S.HostDigest)), ("n_events", C.c_uint64), ("n_pkt_events", C.c_uint64),
+                ("window_ns", C.c_uint64), ("rows_run", C.c_int32), ("self_run", C.c_int32),
+                ("wall_ms", C.c_double)]
+
+
+class OCodelEntry(C.Structure):
+    _fields_ = [("ts", C.c_uint64), ("len", C.c_uint32), ("id", C.c_uint32), ("src", C.c_uint32),
+                ("_pad", C.c_uint32)]
+
+
+class OCodel(C.Structure):
+    _fields_ = [("q", P(OCodelEntry)), ("cap", C.c_uint32), ("head", C.c_uint32),
+                ("count", C.c_uint32), ("total", C.c_uint64), ("mode", C.c_uint32),
+                ("interval_expire", C.c_uint64), ("next_drop", C.c_uint64),
+                ("drop_count", C.c_uint32), ("drop_count_last", C.c_uint32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run `make -C oracle` (or __graft_entry__.build())")
+        l = C.CDLL(LIB)
+        l.o_rand_r.restype = C.c_int32; l.o_rand_r.argtypes = [P(C.c_uint32)]
+        l.o_next_double.restype = C.c_double; l.o_next_double.argtypes = [P(C.c_uint32)]
+        l.o_next_uint.restype = C.c_uint32; l.o_next_uint.argtypes = [P(C.c_uint32)]
+        l.o_seed_chain.argtypes = [C.c_uint32, C.c_int32, P(C.c_uint32)]
+        l.o_graph_new.restype = C.c_void_p; l.o_graph_new.argtypes = [P(S.Graph)]
+        l.o_graph_free.argtypes = [C.c_void_p]
+        l.o_graph_props.argtypes = [C.c_void_p, P(S.GraphProps)]
+        l.o_direct_path.argtypes = [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double), P(C.c_double)]
+        l.o_self_path.argtypes = [C.c_void_p, C.c_int32, P(C.c_double), P(C.c_double)]
+        l.o_sssp_row.argtypes = [C.c_void_p, C.c_int32, P(C.c_int32), C.c_int32, P(C.c_double),
+                                 P(C.c_double), P(C.c_int32), P(C.c_int32), P(C.c_int64)]
+        l.o_topo_new.restype = C.c_void_p
+        l.o_topo_new.argtypes = [C.c_void_p, P(C.c_int32), C.c_int32, C.c_int32]
+        l.o_topo_free.argtypes = [C.c_void_p]
+        l.o_topo_get.argtypes = [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double), P(C.c_double)]
+        l.o_topo_count_packet.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        l.o_topo_packet_count.restype = C.c_uint64
+        l.o_topo_packet_count.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        l.o_topo_min_latency.restype = C.c_double; l.o_topo_min_latency.argtypes = [C.c_void_p]
+        l.o_topo_rows_run.restype = C.c_int32; l.o_topo_rows_run.argtypes = [C.c_void_p]
+        l.o_codel_init.argtypes = [P(OCodel), C.c_uint32]
+        l.o_codel_free.argtypes = [P(OCodel)]
+        l.o_codel_enqueue.argtypes = [P(OCodel), C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]
+        l.o_codel_dequeue.argtypes = [P(OCodel), C.c_uint64, P(OCodelEntry), P(OCodelEntry),
+                                      C.c_uint32, P(C.c_uint32)]
+        l.o_codel_control_law.restype = C.c_uint64
+        l.o_codel_control_law.argtypes = [C.c_uint32, C.c_uint64]
+        l.o_engine_run.argtypes = [P(S.Model), P(S.Graph), C.c_int32, P(ORun)]
+        l.o_run_free.argtypes = [P(ORun)]
+        l.o_event_compare.argtypes = [P(S.Event), P(S.Event)]
+        _lib = l
+    return _lib
+
+
+class OGraph:
+    def __init__(self, g: S.GraphArrays):
+        self.g = g
+        self.ptr = lib().o_graph_new(C.byref(g.struct))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().o_graph_free(self.ptr)
+            self.ptr = None
+
+    def props(self):
+        p = S.GraphProps()
+        lib().o_graph_props(self.ptr, C.byref(p))
+        return p
+
+    def row(self, src, targets):
+        t = np.ascontiguousarray(targets, dtype=np.int32)
+        n = len(t)
+        lat = np.empty(n); rel = np.empty(n)
+        ok = np.empty(n, np.int32); hops = np.empty(n, np.int32)
+        ties = C.c_int64(0)
+        lib().o_sssp_row(self.ptr, int(src), S.as_ptr(t, C.c_int32), n, S.as_ptr(lat, C.c_double),
+                         S.as_ptr(rel, C.c_double), S.as_ptr(ok, C.c_int32),
+                         S.as_ptr(hops, C.c_int32), C.byref(ties))
+        return lat, rel, ok, hops, ties.value
+
+    def direct(self, s, d):
+        a, b = C.c_double(), C.c_double()
+        rc = lib().o_direct_path(self.ptr, int(s), int(d), C.byref(a), C.byref(b))
+        return (a.value, b.value) if rc == 0 else (float("nan"), float("nan"))
+
+    def self_path(self, s):
+        a, b = C.c_double(), C.c_double()
+        lib().o_self_path(self.ptr, int(s), C.byref(a), C.byref(b))
+        return a.value, b.value
+
+
+class OTopo:
+    def __init__(self, og: OGraph, attached, force_rows=False):
+        self.og = og
+        self.att = np.ascontiguousarray(attached, dtype=np.int32)
+        self.ptr = lib().o_topo_new(og.ptr, S.as_ptr(self.att, C.c_int32), len(self.att),
+                                    int(force_rows))
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            lib().o_topo_free(self.ptr)
+            self.ptr = None
+
+    def get(self, s, d):
+        a, b = C.c_double(), C.c_double()
+        lib().o_topo_get(self.ptr, int(s), int(d), C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def rows_run(self):
+        return lib().o_topo_rows_run(self.ptr)
+
+
+def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False):
+    """Serial reference loop; returns (trace ndarray, digest ndarray, ORun stats dict)."""
+    r = ORun()
+    rc = lib().o_engine_run(C.byref(model.struct), C.byref(g.struct), int(force_rows), C.byref(r))
+    assert rc == 0
+    n = r.n_trace
+    tr = np.empty(n, dtype=S.TRACE_DTYPE)
+    if n:
+        C.memmove(tr.ctypes.data, r.trace, n * 32)
+    H = model.n_hosts
+    dg = np.empty(H, dtype=S.DIGEST_DTYPE)
+    C.memmove(dg.ctypes.data, r.digest, H * S.DIGEST_DTYPE.itemsize)
+    stats = dict(n_events=r.n_events, n_pkt_events=r.n_pkt_events, rows_run=r.rows_run,
+                 self_run=r.self_run, wall_ms=r.wall_ms)
+    lib().o_run_free(C.byref(r))
+    return tr, dg, stats
+
+
+def rand_r(state: int):
+    s = C.c_uint32(state)
+    v = lib().o_rand_r(C.byref(s))
+    return v, s.value

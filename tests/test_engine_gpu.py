@@ -1,0 +1,103 @@
+"""Event-loop parity on the GPU: libshdgpu engine vs the serial oracle.
+
+The oracle runs the reference's serial mode (--workers 0, one global queue in
+event_compare order, slave.c:415-428); the engine runs serial-equivalent
+rounds of width W on the GPU.  Traces (every packet state change) must be the
+same multiset and every host's end state must match bit for bit.
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import shdgpu as S
+import workloads as W
+from sim import Engine, PathCache, sort_trace
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(g, model, force_rows=False):
+    att = W.attached_vertices(model.host_vertex)
+    pc = PathCache(g, att, flags=1 if force_rows else 0)
+    eng = Engine(model, pc)
+    st = eng.run()
+    gtr = sort_trace(eng.trace())
+    gdg = eng.digest()
+    otr, odg, ost = O.engine_run(model, g, force_rows=force_rows)
+    otr = sort_trace(otr)
+    return (gtr, gdg, st), (otr, odg, ost), eng, pc
+
+
+def assert_same(gpu, ora):
+    (gtr, gdg, st), (otr, odg, ost) = gpu, ora
+    assert st.n_events == ost["n_events"]
+    assert st.n_pkt_events == ost["n_pkt_events"]
+    assert len(gtr) == len(otr)
+    assert np.array_equal(gtr, otr)
+    assert np.array_equal(gdg, odg)
+
+
+def test_geometric_one_host_per_vertex():
+    g = W.geometric_graph(300, seed=2)
+    m = W.phold_model(W.hosts_on_vertices(300, 1), end_time=3 * S.SHD_SEC, trace=True)
+    gpu, ora, eng, _ = run_both(g, m)
+    assert_same(gpu, ora)
+    assert gpu[2].n_rounds > 100
+    assert np.count_nonzero(gpu[0]["kind"] == S.TR_LOCAL) > 0     # self-sends exercised
+    assert np.count_nonzero(gpu[0]["kind"] == S.TR_INET_DROP) > 0  # reliability drops
+
+
+def test_bundled_complete_graph_many_hosts_per_vertex():
+    g = W.bundled_graph()
+    rng = np.random.default_rng(0)
+    hv = np.sort(rng.integers(0, g.n_vertices, 400)).astype(np.int32)
+    m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, load=8)
+    gpu, ora, _, _ = run_both(g, m)
+    assert_same(gpu, ora)
+
+
+def test_geometric_shared_vertices_rows_and_self_paths():
+    g = W.geometric_graph(120, seed=4, vertex_loss=True)
+    m = W.phold_model(W.hosts_on_vertices(120, 3), end_time=int(2.5 * S.SHD_SEC), trace=True)
+    gpu, ora, _, _ = run_both(g, m)
+    assert_same(gpu, ora)
+
+
+def test_codel_drops_under_low_receive_bandwidth():
+    g = W.geometric_graph(150, seed=8)
+    m = W.phold_model(W.hosts_on_vertices(150, 1), end_time=4 * S.SHD_SEC, trace=True, load=24,
+                      payload=1000, bw_down=600, bw_up=100000, codelq_cap=256)
+    gpu, ora, _, _ = run_both(g, m)
+    assert_same(gpu, ora)
+    assert np.count_nonzero(gpu[0]["kind"] == S.TR_CODEL_DROP) > 0
+
+
+def test_bootstrap_period_and_forced_rows_on_complete_graph():
+    g = W.bundled_graph()
+    hv = np.arange(0, g.n_vertices, 2, dtype=np.int32)
+    m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, bootstrap_end=2 * S.SHD_SEC, bw_down=100)
+    gpu, ora, _, _ = run_both(g, m, force_rows=True)
+    assert_same(gpu, ora)
+
+
+def test_prefer_direct_paths():
+    g = W.geometric_graph(200, seed=12)
+    g2 = S.GraphArrays(g.n_vertices, g.src, g.dst, g.latency, g.loss, None, prefer_direct=True)
+    m = W.phold_model(W.hosts_on_vertices(200, 1), end_time=3 * S.SHD_SEC, trace=True)
+    gpu, ora, _, _ = run_both(g2, m)
+    assert_same(gpu, ora)
+
+
+def test_run_to_run_determinism():
+    # reference determinism1/2 tests (src/test/determinism) compare two runs
+    g = W.geometric_graph(500, seed=3)
+    m = W.phold_model(W.hosts_on_vertices(500, 1), end_time=3 * S.SHD_SEC, trace=True)
+    att = W.attached_vertices(m.host_vertex)
+    pc = PathCache(g, att)
+    outs = []
+    for _ in range(2):
+        e = Engine(m, pc)
+        e.run()
+        outs.append((sort_trace(e.trace()), e.digest()))
+        e.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

@@ -1,0 +1,105 @@
+"""Path-cache parity on the GPU: libshdgpu tables vs the oracle, bit for bit.
+
+Reference: src/main/routing/topology.c (rows 1655-1875 + 1407-1523, direct
+1877-1927, self 1545-1653, lazy selection 1969-2051).
+"""
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import workloads as W
+from pc_helpers import PathCache, same_bits
+
+pytestmark = pytest.mark.gpu
+
+SHD_PC_FORCE_ROWS = 1
+
+
+def oracle_rows(g, attached, rows):
+    og = O.OGraph(g)
+    lat = np.empty((len(rows), len(attached))); rel = np.empty_like(lat)
+    ties = 0
+    for k, r in enumerate(rows):
+        l, rr, ok, hops, t = og.row(attached[r], attached)
+        l[ok == 0] = -1.0; rr[ok == 0] = -1.0
+        lat[k], rel[k] = l, rr
+        ties += t
+    return lat, rel, ties
+
+
+def test_bundled_direct_mode_bit_exact():
+    g = W.bundled_graph()
+    att = np.arange(g.n_vertices, dtype=np.int32)
+    pc = PathCache(g, att)
+    info = pc.info()
+    assert info.is_complete == 1 and info.rows_computed == 0
+    lat, rel = pc.direct()
+    og = O.OGraph(g)
+    olat = np.empty_like(lat); orel = np.empty_like(rel)
+    for i, s in enumerate(att):
+        for j, d in enumerate(att):
+            olat[i, j], orel[i, j] = og.direct(s, d)
+    assert same_bits(lat, olat) and same_bits(rel, orel)
+    # reference mode: the lazy lookup serves direct paths
+    for s, d in [(0, 5), (5, 0), (17, 17), (182, 3)]:
+        assert pc.lookup(s, d) == (olat[s, d], orel[s, d])
+
+
+def test_bundled_forced_rows_bit_exact():
+    g = W.bundled_graph()
+    att = np.arange(g.n_vertices, dtype=np.int32)
+    pc = PathCache(g, att, flags=SHD_PC_FORCE_ROWS)
+    info = pc.info()
+    assert info.rows_computed == g.n_vertices
+    lat, rel = pc.rows()
+    olat, orel, ties = oracle_rows(g, att, range(len(att)))
+    assert info.n_ties == ties
+    assert same_bits(lat, olat) and same_bits(rel, orel)
+    # the 737 off-diagonal pairs where the shortest path is not the direct edge
+    dl, _ = pc.direct()
+    off = ~np.eye(len(att), dtype=bool)
+    assert int(np.sum(np.triu(lat < dl, 1))) == 737
+
+
+@pytest.mark.parametrize("V,seed", [(2000, 11), (3000, 5)])
+def test_geometric_rows_bit_exact(V, seed):
+    g = W.geometric_graph(V, seed=seed, vertex_loss=True)
+    att = np.arange(V, dtype=np.int32)
+    pc = PathCache(g, att)
+    info = pc.info()
+    assert info.is_complete == 0 and info.rows_computed == V
+    assert info.n_ties == 0
+    rows = list(range(0, V, max(1, V // 64))) + [V - 1]
+    lat, rel = pc.rows()
+    olat, orel, ties = oracle_rows(g, att, rows)
+    assert same_bits(lat[rows], olat) and same_bits(rel[rows], orel)
+    slat, srel = pc.self_values()
+    og = O.OGraph(g)
+    ref = np.array([og.self_path(v) for v in att])
+    assert same_bits(slat, ref[:, 0]) and same_bits(srel, ref[:, 1])
+
+
+def test_geometric_subset_attached_and_global_scratch_path():
+    # V above the LDS capacity (14 B/vertex > 160 KiB) -> global-memory kernel
+    V = 12500
+    g = W.geometric_graph(V, seed=7)
+    rng = np.random.default_rng(0)
+    att = np.sort(rng.choice(V, 300, replace=False)).astype(np.int32)
+    pc = PathCache(g, att)
+    lat, rel = pc.rows()
+    rows = list(range(0, len(att), 10))
+    olat, orel, _ = oracle_rows(g, att, rows)
+    assert same_bits(lat[rows], olat) and same_bits(rel[rows], orel)
+
+
+def test_lazy_lookup_first_touch_matches_reference_cache():
+    g = W.geometric_graph(400, seed=9, vertex_loss=True)
+    att = np.arange(400, dtype=np.int32)
+    pc = PathCache(g, att)
+    ot = O.OTopo(O.OGraph(g), att)
+    rng = np.random.default_rng(1)
+    for _ in range(3000):
+        s, d = (int(x) for x in rng.integers(0, 400, 2))
+        a = pc.lookup(s, d)
+        b = ot.get(s, d)
+        assert np.array(a).view(np.uint64).tolist() == np.array(b).view(np.uint64).tolist(), (s, d)
