@@ -330,18 +330,38 @@ int shd_eng_run_round(shd_eng* e, uint64_t window_start, uint64_t window_end,
                       shd_round_summary* out);
 /* whole single-engine run to end_time (rounds of W) */
 int shd_eng_run(shd_eng* e, shd_run_stats* out);
-/* multi-GPU exchange (DESIGN.md "Multi-GPU"): device pointer + count of events
- * bound for other engines, grouped by destination engine; and ingest of
- * events received from other engines (device pointer) */
-int shd_eng_remote_counts(shd_eng* e, int32_t n_parts, const int32_t* part_begin,
-                          uint64_t* counts_out);
-int shd_eng_remote_buffer(shd_eng* e, void** dev_ptr, uint64_t* n_events);
+/* rounds while the next event time is below t_stop (rounds never cross t_stop);
+ * stats cover this call only */
+int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* out);
+/* A round split into its phases, for drivers that own several engines (one
+ * per GPU, DESIGN.md "Multi-GPU").  shd_eng_run_round = round_kernel, then,
+ * if the round logged first-touch queries, pending_copy + resolve with this
+ * engine's records, then end_round. */
+typedef struct shd_pending {
+    uint64_t qtime;                 /* key of the executing event: time, seq */
+    uint64_t qseq;
+    uint32_t qhost;                 /*   its destination host (the sender)   */
+    uint32_t qsrc;                  /*   its source host                     */
+    uint32_t qsub;                  /*   position of the query in the event  */
+    uint32_t a, b;                  /* attached indices (src, dst) queried   */
+    uint32_t delivered;             /* 0 dropped, 1 awaiting resolution, 2 sent */
+    uint32_t dst;                   /* destination host of the packet        */
+    uint32_t pkt;
+    uint64_t seq;                   /* packet event seq                      */
+} shd_pending;
+int shd_eng_round_kernel(shd_eng* e, uint64_t window_start, uint64_t window_end,
+                         shd_round_summary* out);
+int shd_eng_pending_copy(shd_eng* e, shd_pending* out, uint64_t cap, uint64_t* n);
+/* `all` = the pending records of EVERY engine this round (any order): row
+ * ranks are assigned in serial event order, then this engine's sends are
+ * finalized (delivery time from the min-rank row) */
+int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_all);
+int shd_eng_end_round(shd_eng* e, shd_round_summary* out);
+/* events this engine produced for hosts of other engines (device to device
+ * copy into dev_dst, capacity cap events) and ingest of received events */
+int shd_eng_remote_copy(shd_eng* e, void* dev_dst, uint64_t cap, uint64_t* n);
 int shd_eng_ingest(shd_eng* e, const void* dev_events, uint64_t n_events);
 int shd_eng_next_time(shd_eng* e, uint64_t* next_time);
-/* first-touch resolution records; multi-GPU callers gather
- * them from all engines, resolve once, and apply the ranks everywhere */
-int shd_eng_pending_count(shd_eng* e, uint64_t* n);
-int shd_eng_resolve_pending(shd_eng* e);
 int shd_eng_trace_count(shd_eng* e, uint64_t* n);
 int shd_eng_trace_copy(shd_eng* e, shd_trace_rec* out, uint64_t cap, uint64_t* n);
 int shd_eng_digest(shd_eng* e, shd_host_digest* out);   /* [host_end-host_begin] */

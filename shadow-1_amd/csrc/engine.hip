@@ -57,19 +57,9 @@ struct TxEnt {
     uint32_t pkt;
 };
 
-// a send whose (src,dst) pair was unranked at round start
-struct Pending {
-    uint64_t qtime;    // executing event key (time, dst=host, src, seq) + sub-index
-    uint64_t qseq;
-    uint32_t qhost;
-    uint32_t qsrc;
-    uint32_t qsub;
-    uint32_t a, b;     // attached indices of the query
-    uint32_t delivered;   // 0 dropped, 1 delivery pending, 2 delivered in-round
-    uint32_t dst;      // destination host
-    uint32_t pkt;
-    uint64_t seq;      // event seq of the packet (when delivered)
-};
+// a send whose (src,dst) pair was unranked at round start (include/shdgpu.h)
+using Pending = shd_pending;
+static_assert(sizeof(Pending) == 56, "pending record layout");
 
 // engine-wide counters / summary on the device
 struct DevSummary {
@@ -812,6 +802,7 @@ struct shd_eng {
     std::vector<int32_t> h_rank, h_self_rank;
     int32_t next_rank = 0;
     uint64_t pending_resolved = 0;
+    uint64_t round_ws = 0, round_we = 0, round_pending = 0, round_events = 0, round_pkt = 0;
     uint64_t trace_cap = 0;
 };
 
@@ -860,8 +851,12 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     (void)hipEventCreate(&e->ev1);
     Params& P = e->P;
     P.H = H; P.h0 = host_begin; P.nloc = e->nloc;
-    P.evq_cap = m->evq_cap ? m->evq_cap : std::max<uint32_t>(64, 4 * m->load + 32);
-    P.inbox_cap = m->inbox_cap ? m->inbox_cap : P.evq_cap;
+    // default capacities: packets in flight TO a host are ~ load x (mean latency
+    // of its inbound paths / global mean latency), up to ~10x load on the
+    // bundled topology (5 - 2294 ms edges); one round's arrivals peak at the
+    // application start (every host sends `load` messages at once)
+    P.evq_cap = m->evq_cap ? m->evq_cap : std::max<uint32_t>(64, 16 * m->load + 64);
+    P.inbox_cap = m->inbox_cap ? m->inbox_cap : std::max<uint32_t>(64, 4 * m->load + 32);
     P.cq_cap = m->codelq_cap ? m->codelq_cap : 64;
     P.tq_cap = m->txq_cap ? m->txq_cap : 64;
     P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
@@ -998,40 +993,20 @@ extern "C" int shd_eng_boot(shd_eng* e) {
 
 // first-touch resolution in serial order: sort the logged queries
 // by the executing event's key, assign row ranks, finalize delivered sends
-static int resolve_pending(shd_eng* e, uint64_t npend, int next_parity) {
-    if (npend > e->P.pend_cap) return SHD_EOVERFLOW;
-    std::vector<Pending> recs(npend);
-    SHD_HIP(hipMemcpyAsync(recs.data(), e->P.pend, sizeof(Pending) * npend, hipMemcpyDeviceToHost, e->stream));
-    SHD_HIP(hipStreamSynchronize(e->stream));
-    std::sort(recs.begin(), recs.end(), [](const Pending& x, const Pending& y) {
+// first-touch resolution in serial order (DESIGN.md "First-touch rule"): sort
+// the logged queries of ALL engines by the executing event's key, assign row
+// ranks (identically on every engine), then finalize this engine's sends
+static void sort_pending(std::vector<shd_pending>& recs) {
+    std::sort(recs.begin(), recs.end(), [](const shd_pending& x, const shd_pending& y) {
         if (x.qtime != y.qtime) return x.qtime < y.qtime;
         if (x.qhost != y.qhost) return x.qhost < y.qhost;
         if (x.qsrc != y.qsrc) return x.qsrc < y.qsrc;
         if (x.qseq != y.qseq) return x.qseq < y.qseq;
         return x.qsub < y.qsub;
     });
-    const bool directed = e->pc->directed;
-    for (const Pending& r : recs) {
-        const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
-        if (a == b) {
-            if (e->h_rank[a] == kNoRank && e->h_self_rank[a] == kNoRank) e->h_self_rank[a] = e->next_rank++;
-        } else if (directed) {
-            if (e->h_rank[a] == kNoRank) e->h_rank[a] = e->next_rank++;
-        } else {
-            if (e->h_rank[a] == kNoRank && e->h_rank[b] == kNoRank) e->h_rank[a] = e->next_rank++;
-        }
-    }
-    const int32_t T = e->pc->T;
-    SHD_HIP(hipMemcpyAsync(e->d_rank, e->h_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
-    SHD_HIP(hipMemcpyAsync(e->d_self_rank, e->h_self_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
-    const uint32_t n = (uint32_t)npend;
-    hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->P, e->P.pend, n, next_parity);
-    SHD_HIP(hipGetLastError());
-    e->pending_resolved += npend;
-    return SHD_OK;
 }
 
-extern "C" int shd_eng_run_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out) {
+extern "C" int shd_eng_round_kernel(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out) {
     if (!e || !e->booted || we <= ws) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(e->device));
     int rc = reset_summary(e);
@@ -1046,25 +1021,94 @@ extern "C" int shd_eng_run_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round
     (void)hipEventElapsedTime(&ms, e->ev0, e->ev1);
     e->last_kernel_ms = ms;
     e->kernel_ms_total += ms;
-    const uint64_t npend = e->h_sum->n_pending;
-    const int next_parity = e->parity ^ 1;
-    if (npend) {
-        if ((rc = resolve_pending(e, npend, next_parity))) return rc;
-        if ((rc = read_summary(e))) return rc;
-    }
-    e->parity = next_parity;
+    e->round_ws = ws;
+    e->round_we = we;
+    e->round_pending = e->h_sum->n_pending;
+    e->round_events = e->h_sum->n_events;
+    e->round_pkt = e->h_sum->n_pkt_events;
     if (out) {
         out->window_start = ws; out->window_end = we;
         out->next_time = e->h_sum->next_time;
         out->n_events = e->h_sum->n_events; out->n_pkt_events = e->h_sum->n_pkt_events;
-        out->n_pending = npend; out->n_remote = e->h_sum->n_remote; out->error = e->h_sum->error;
+        out->n_pending = e->h_sum->n_pending; out->n_remote = e->h_sum->n_remote; out->error = e->h_sum->error;
+    }
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_pending_copy(shd_eng* e, shd_pending* out, uint64_t cap, uint64_t* n) {
+    if (!e || !n || (cap && !out)) return SHD_EINVAL;
+    const uint64_t cnt = e->round_pending;
+    if (cnt > e->P.pend_cap) return SHD_EOVERFLOW;
+    if (cnt > cap) { *n = cnt; return SHD_ERANGE; }
+    SHD_HIP(hipSetDevice(e->device));
+    if (cnt) {
+        SHD_HIP(hipMemcpyAsync(out, e->P.pend, sizeof(shd_pending) * cnt, hipMemcpyDeviceToHost, e->stream));
+        SHD_HIP(hipStreamSynchronize(e->stream));
+    }
+    *n = cnt;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_all) {
+    if (!e || (n_all && !all)) return SHD_EINVAL;
+    if (!n_all) return SHD_OK;
+    SHD_HIP(hipSetDevice(e->device));
+    std::vector<shd_pending> recs(all, all + n_all);
+    sort_pending(recs);
+    const bool directed = e->pc->directed;
+    for (const shd_pending& r : recs) {
+        const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
+        if (a < 0 || b < 0 || a >= e->pc->T || b >= e->pc->T) return SHD_EINVAL;
+        if (a == b) {
+            if (e->h_rank[a] == kNoRank && e->h_self_rank[a] == kNoRank) e->h_self_rank[a] = e->next_rank++;
+        } else if (directed) {
+            if (e->h_rank[a] == kNoRank) e->h_rank[a] = e->next_rank++;
+        } else {
+            if (e->h_rank[a] == kNoRank && e->h_rank[b] == kNoRank) e->h_rank[a] = e->next_rank++;
+        }
+    }
+    const int32_t T = e->pc->T;
+    SHD_HIP(hipMemcpyAsync(e->d_rank, e->h_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
+    SHD_HIP(hipMemcpyAsync(e->d_self_rank, e->h_self_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
+    const uint32_t n = (uint32_t)e->round_pending;
+    if (n) {
+        hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->P,
+                           (const Pending*)e->P.pend, n, e->parity ^ 1);
+        SHD_HIP(hipGetLastError());
+    }
+    e->pending_resolved += n;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_end_round(shd_eng* e, shd_round_summary* out) {
+    if (!e) return SHD_EINVAL;
+    int rc = read_summary(e);
+    if (rc) return rc;
+    e->parity ^= 1;
+    if (out) {
+        out->window_start = e->round_ws; out->window_end = e->round_we;
+        out->next_time = e->h_sum->next_time;
+        out->n_events = e->round_events; out->n_pkt_events = e->round_pkt;
+        out->n_pending = e->round_pending; out->n_remote = e->h_sum->n_remote; out->error = e->h_sum->error;
     }
     if (e->h_sum->error & SHD_ERR_AMBIGUOUS) return SHD_EAMBIG;
     if (e->h_sum->error) return SHD_EOVERFLOW;
     return SHD_OK;
 }
 
-extern "C" int shd_eng_run(shd_eng* e, shd_run_stats* st) {
+extern "C" int shd_eng_run_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out) {
+    int rc = shd_eng_round_kernel(e, ws, we, out);
+    if (rc) return rc;
+    if (e->round_pending) {
+        std::vector<shd_pending> recs(e->round_pending);
+        uint64_t n = 0;
+        if ((rc = shd_eng_pending_copy(e, recs.data(), recs.size(), &n))) return rc;
+        if ((rc = shd_eng_resolve(e, recs.data(), n))) return rc;
+    }
+    return shd_eng_end_round(e, out);
+}
+
+extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;
     auto t0 = std::chrono::steady_clock::now();
     int rc = SHD_OK;
@@ -1072,11 +1116,13 @@ extern "C" int shd_eng_run(shd_eng* e, shd_run_stats* st) {
     shd_run_stats s{};
     s.window_ns = e->window;
     uint64_t next = e->h_sum->next_time;
+    const uint64_t stop = std::min<uint64_t>(t_stop, e->P.end_time);
     e->kernel_ms_total = 0;
-    while (next < e->P.end_time) {
+    const uint64_t pend0 = e->pending_resolved;
+    while (next < stop) {
         const uint64_t ws = next;
         uint64_t we = ws + e->window;
-        if (we > e->P.end_time || we < ws) we = e->P.end_time;
+        if (we > stop || we < ws) we = stop;
         shd_round_summary r;
         rc = shd_eng_run_round(e, ws, we, &r);
         s.n_rounds++;
@@ -1086,26 +1132,29 @@ extern "C" int shd_eng_run(shd_eng* e, shd_run_stats* st) {
         if (rc) { s.error = r.error; break; }
         next = r.next_time;
     }
-    s.n_pending_resolved = e->pending_resolved;
+    s.n_pending_resolved = e->pending_resolved - pend0;
     s.device_ms_round_kernel = e->kernel_ms_total;
     s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (st) *st = s;
     return rc;
 }
 
-extern "C" int shd_eng_remote_counts(shd_eng* e, int32_t n_parts, const int32_t* part_begin, uint64_t* counts) {
-    if (!e || n_parts <= 0 || !part_begin || !counts) return SHD_EINVAL;
-    // events are staged unsorted; the multi-GPU driver sorts them by
-    // destination through shd_eng_remote_buffer
-    for (int32_t i = 0; i < n_parts; i++) counts[i] = 0;
-    counts[0] = e->h_sum->n_remote;
-    return SHD_OK;
+extern "C" int shd_eng_run(shd_eng* e, shd_run_stats* st) {
+    if (!e) return SHD_EINVAL;
+    return shd_eng_run_until(e, e->P.end_time, st);
 }
 
-extern "C" int shd_eng_remote_buffer(shd_eng* e, void** p, uint64_t* n) {
-    if (!e || !p || !n) return SHD_EINVAL;
-    *p = e->P.remote;
-    *n = std::min<uint64_t>(e->h_sum->n_remote, e->P.remote_cap);
+extern "C" int shd_eng_remote_copy(shd_eng* e, void* dev_dst, uint64_t cap, uint64_t* n) {
+    if (!e || !n) return SHD_EINVAL;
+    const uint64_t cnt = std::min<uint64_t>(e->h_sum->n_remote, e->P.remote_cap);
+    if (cnt > cap) { *n = cnt; return SHD_ERANGE; }
+    SHD_HIP(hipSetDevice(e->device));
+    if (cnt) {
+        if (!dev_dst) return SHD_EINVAL;
+        SHD_HIP(hipMemcpyAsync(dev_dst, e->P.remote, sizeof(shd_event) * cnt, hipMemcpyDeviceToDevice, e->stream));
+        SHD_HIP(hipStreamSynchronize(e->stream));
+    }
+    *n = cnt;
     return SHD_OK;
 }
 
@@ -1116,6 +1165,7 @@ extern "C" int shd_eng_ingest(shd_eng* e, const void* ev, uint64_t n) {
     hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->P,
                        (const shd_event*)ev, n, e->parity);
     SHD_HIP(hipGetLastError());
+    SHD_HIP(hipStreamSynchronize(e->stream));
     return SHD_OK;
 }
 
@@ -1123,16 +1173,6 @@ extern "C" int shd_eng_next_time(shd_eng* e, uint64_t* t) {
     if (!e || !t) return SHD_EINVAL;
     *t = e->h_sum->next_time;
     return SHD_OK;
-}
-
-extern "C" int shd_eng_pending_count(shd_eng* e, uint64_t* n) {
-    if (!e || !n) return SHD_EINVAL;
-    *n = e->pending_resolved;
-    return SHD_OK;
-}
-
-extern "C" int shd_eng_resolve_pending(shd_eng* e) {
-    return e ? SHD_OK : SHD_EINVAL;   // resolution runs inside shd_eng_run_round
 }
 
 extern "C" int shd_eng_trace_count(shd_eng* e, uint64_t* n) {

@@ -36,9 +36,9 @@ typedef struct shd_csr {
     int32_t max_degree;
 } shd_csr;
 
-int shd_csr_build(const shd_graph* g, shd_csr* out);
-void shd_csr_free(shd_csr* c);
-int32_t shd_csr_get_eid(const shd_csr* c, int32_t a, int32_t b);
+__attribute__((visibility("hidden"))) int shd_csr_build(const shd_graph* g, shd_csr* out);
+__attribute__((visibility("hidden"))) void shd_csr_free(shd_csr* c);
+__attribute__((visibility("hidden"))) int32_t shd_csr_get_eid(const shd_csr* c, int32_t a, int32_t b);
 
 #ifdef __cplusplus
 }

@@ -126,6 +126,14 @@ assert TRACE_DTYPE.itemsize == C.sizeof(TraceRec) == 32
 assert C.sizeof(Event) == 32
 
 
+PENDING_DTYPE = np.dtype([("qtime", "<u8"), ("qseq", "<u8"), ("qhost", "<u4"), ("qsrc", "<u4"),
+                          ("qsub", "<u4"), ("a", "<u4"), ("b", "<u4"), ("delivered", "<u4"),
+                          ("dst", "<u4"), ("pkt", "<u4"), ("seq", "<u8")])
+assert PENDING_DTYPE.itemsize == 56
+EVENT_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("src", "<u4"), ("dst", "<u4"),
+                        ("pkt", "<u4"), ("kind", "<u4")])
+
+
 class RoundSummary(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in (
         "window_start", "window_end", "next_time", "n_events", "n_pkt_events", "n_pending",
@@ -173,12 +181,14 @@ _SIGS = {
     "shd_eng_boot": (C.c_int, [C.c_void_p]),
     "shd_eng_run_round": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(RoundSummary)]),
     "shd_eng_run": (C.c_int, [C.c_void_p, P(RunStats)]),
-    "shd_eng_remote_counts": (C.c_int, [C.c_void_p, C.c_int32, P(C.c_int32), P(C.c_uint64)]),
-    "shd_eng_remote_buffer": (C.c_int, [C.c_void_p, P(C.c_void_p), P(C.c_uint64)]),
+    "shd_eng_run_until": (C.c_int, [C.c_void_p, C.c_uint64, P(RunStats)]),
+    "shd_eng_round_kernel": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(RoundSummary)]),
+    "shd_eng_pending_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "shd_eng_resolve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "shd_eng_end_round": (C.c_int, [C.c_void_p, P(RoundSummary)]),
+    "shd_eng_remote_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_ingest": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "shd_eng_next_time": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
-    "shd_eng_pending_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
-    "shd_eng_resolve_pending": (C.c_int, [C.c_void_p]),
     "shd_eng_trace_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "shd_eng_trace_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_digest": (C.c_int, [C.c_void_p, C.c_void_p]),

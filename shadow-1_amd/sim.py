@@ -99,6 +99,12 @@ class Engine:
         S.check(rc, f"shd_eng_run (error bits {st.error:#x})")
         return st
 
+    def run_until(self, t_stop) -> S.RunStats:
+        st = S.RunStats()
+        rc = S.lib().shd_eng_run_until(self.ptr, int(t_stop), C.byref(st))
+        S.check(rc, f"shd_eng_run_until (error bits {st.error:#x})")
+        return st
+
     def run_round(self, ws, we) -> S.RoundSummary:
         r = S.RoundSummary()
         rc = S.lib().shd_eng_run_round(self.ptr, int(ws), int(we), C.byref(r))

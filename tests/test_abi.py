@@ -1,0 +1,51 @@
+"""The C-ABI library loads and exports exactly what include/shdgpu.h declares
+(no compute calls: runs on CPU)."""
+import os
+import re
+import subprocess
+
+import shdgpu as S
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared():
+    h = open(os.path.join(REPO, "include", "shdgpu.h")).read()
+    return set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(shd_[a-z_0-9]+)\(", h, re.M))
+
+
+def exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", S.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    return {l.split()[-1] for l in out.splitlines() if l.split()[-1].startswith("shd_")}
+
+
+def test_library_loads(shd):
+    assert b"gfx950" in shd.lib().shd_version()
+
+
+def test_every_declared_symbol_is_exported_and_bound():
+    d, e = declared(), exported()
+    assert d, "no declarations parsed"
+    assert d == e, (d - e, e - d)
+    assert d == set(S.exported_symbols())
+
+
+def test_code_object_targets_gfx950():
+    blob = open(S.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"sm_"):
+        assert other not in blob
+
+
+def test_no_oracle_on_product_path():
+    # the product library never links or embeds the oracle
+    out = subprocess.run(["nm", "-D", S.LIB_PATH], capture_output=True, text=True).stdout
+    assert " o_" not in out
+    ldd = subprocess.run(["ldd", S.LIB_PATH], capture_output=True, text=True).stdout
+    assert "oracle" not in ldd
+    for root, _, files in os.walk(os.path.join(REPO, "shadow-1_amd")):
+        for f in files:
+            if f.endswith((".py", ".c", ".h", ".hip", ".cpp")):
+                src = open(os.path.join(root, f), errors="ignore").read()
+                assert "oracle_ffi" not in src and "liboracle" not in src, f
