@@ -1,0 +1,238 @@
+#!/usr/bin/env python3
+"""bench.py -- simulated packet events/s of libshdgpu (BASELINE.json metric).
+
+Workload (N = --gpus, weak scaling): PHOLD-UDP on a V-vertex random geometric
+topology (BASELINE.md C3 at N = 1: 10k hosts, one per vertex, load 16, 1-byte
+messages; N x 10k hosts, N per vertex, at N > 1, toward C5).  One "step" is one
+second of simulated time on the loaded model; W warmup steps (boot, the
+application start at t = 1 s and the lazy path-cache warm-up) are untimed, then
+K steps are timed between a barrier + synchronize on both sides; the reported
+time is the max over ranks.  value = packet events (executed deliver-packet
+events, worker.c:253) of all ranks / time.
+
+Also reported: the APSP path-cache build time for the same 10k-vertex topology
+(BASELINE metric 2), a roofline object for the round kernel (HIP-event device
+time on the engine's stream; algorithmic bytes defined in DESIGN.md), and the
+oracle's serial CPU loop as cpu_baseline (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "shadow-1_amd")]
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8 TB/s HBM3E (spec)
+BYTES_PER_EVENT = 64             # event record stored once + loaded once
+BYTES_PER_PKT_EVENT = 16 + 32    # path entry (lat+rel f64) + router-queue entry in/out
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--vertices", type=int, default=10000)
+    ap.add_argument("--hosts-per-gpu", type=int, default=10000)
+    ap.add_argument("--load", type=int, default=16)
+    ap.add_argument("--payload", type=int, default=1)
+    ap.add_argument("--step-ms", type=int, default=1000)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--edge-loss-max", type=float, default=0.0005,
+                    help="edge loss ~ U[0, x]; paths are ~20 hops, so the default keeps the per-path "
+                         "loss near U[0,1%%] and the PHOLD population alive for the whole run")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-seconds", type=float, default=1.0,
+                    help="steady-state simulated seconds the oracle is timed over")
+    ap.add_argument("--cpu-sample-hosts", type=int, default=2000,
+                    help="hosts (= vertices) of the CPU sample instance of the same workload")
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args()
+
+
+def log(rank, *a):
+    if rank == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = args.gpus
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = local_rank if world > 1 else 0
+
+    import shdgpu as S
+    import workloads as W
+    from sim import Engine, PathCache
+    from driver import DistCluster, partition
+
+    t_setup = time.perf_counter()
+    V = args.vertices
+    H = args.hosts_per_gpu * max(world, 1)
+    g = W.geometric_graph(V, seed=args.seed, loss_max=args.edge_loss_max)
+    hpv = max(1, H // V)
+    host_vertex = (np.arange(H, dtype=np.int64) * V // H).astype(np.int32) if H != V * hpv else \
+        W.hosts_on_vertices(V, hpv)
+    step = args.step_ms * S.SHD_MS
+    end_time = (args.warmup + args.steps) * step
+    model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load,
+                          payload=args.payload)
+    att = W.attached_vertices(host_vertex)
+    pc = PathCache(g, att, device=dev)
+    builds = []
+    for _ in range(2):
+        pc.build()
+        builds.append(pc.info().build_ms_device)
+    info = pc.info()
+    pb = partition(H, max(world, 1))
+    eng = Engine(model, pc, pb[rank], pb[rank + 1], device=dev)
+    log(rank, f"setup {time.perf_counter() - t_setup:.1f}s  V={V} E={g.n_edges} H={H} W={eng.window}ns "
+              f"apsp={min(builds):.1f}ms iters={info.sssp_iterations_max} hops={info.max_hops}")
+
+    if world > 1:
+        cl = DistCluster(eng, pb, rank, world, dist, torch)
+        cl.boot()
+        run = lambda t: cl.run_until(t)  # noqa: E731
+    else:
+        eng.boot()
+        run = lambda t: eng.run_until(t)  # noqa: E731
+
+    # warmup
+    tw = time.perf_counter()
+    run(args.warmup * step)
+    torch.cuda.synchronize()
+    log(rank, f"warmup {time.perf_counter() - tw:.1f}s")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    st = run(end_time)
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        pkt, evs, rounds, kms = st.pkt_events, st.events, st.rounds, st.kernel_ms
+    else:
+        pkt, evs, rounds, kms = st.n_pkt_events, st.n_events, st.n_rounds, st.device_ms_round_kernel
+    tot = torch.tensor([float(pkt), float(evs), float(kms)], dtype=torch.float64, device="cuda")
+    mx = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(tot)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    pkt_all, ev_all, kms_all = tot.tolist()
+    elapsed = mx.item()
+    value = pkt_all / elapsed
+
+    # roofline of the round kernel (per launch = per rank-round)
+    launches = rounds * max(world, 1)
+    alg_bytes = BYTES_PER_EVENT * ev_all + BYTES_PER_PKT_EVENT * pkt_all
+    avg_launch_ms = kms_all / max(launches, 1)
+    achieved = (alg_bytes / max(launches, 1)) / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                "kernel": "k_round", "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+                "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1)}
+
+    cpu_baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_baseline = cpu_leg(args, S, W)
+
+    if rank == 0:
+        out = {
+            "metric": "simulated packet events/sec",
+            "value": round(value, 1),
+            "unit": "packet events/s",
+            "n_gpus": n_gpus,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (random geometric topology + PHOLD-UDP traffic, seed %d)" % args.seed,
+            "config": {"workload": "C3 PHOLD-UDP (N x %d hosts, %d-vertex geometric topology)"
+                                   % (args.hosts_per_gpu, V),
+                       "edge_loss": "U[0,%g]" % args.edge_loss_max,
+                       "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
+                       "payload_bytes": args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
+                       "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1)},
+            "all_events_per_s": round(ev_all / elapsed, 1),
+            "rounds": int(rounds),
+            "apsp": {"rows": int(info.rows_computed), "vertices": V, "build_ms": round(min(builds), 3),
+                     "sssp_kernel_ms": round(info.build_ms_sssp, 3), "iterations": int(info.sssp_iterations_max),
+                     "max_hops": int(info.max_hops), "ties": int(info.n_ties)},
+            "roofline": roofline,
+            "cpu_baseline": cpu_baseline,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    pc.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_leg(args, S, W):
+    """The oracle's serial loop (the reference's --workers 0 semantics) timed
+    on this host, one core, on a bounded sample of the same workload family:
+    a --cpu-sample-hosts instance (hosts = vertices, same load and message
+    size), timed over --cpu-sample-seconds of steady state after the warm-up
+    (which includes the reference's lazy Dijkstra rows)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    try:
+        import oracle_ffi as O
+        O.lib()
+    except Exception as ex:   # the checker is absent: report it, never substitute
+        return {"value": None, "unit": "packet events/s", "cores": 1, "kind": "port",
+                "sample": f"oracle unavailable: {ex}"}
+    step = args.step_ms * S.SHD_MS
+    n = min(args.cpu_sample_hosts, args.vertices)
+    g = W.geometric_graph(n, seed=args.seed, loss_max=args.edge_loss_max)
+    hv = W.hosts_on_vertices(n, 1)
+    mark = args.warmup * step
+    end = mark + int(args.cpu_sample_seconds * S.SHD_SEC)
+    m = W.phold_model(hv, end_time=end, seed=args.seed, load=args.load, payload=args.payload)
+    _, _, st = O.engine_run(m, g, mark=mark)
+    dt = (st["wall_ms"] - st["mark_wall_ms"]) * 1e-3
+    pkt = st["n_pkt_events"] - st["mark_pkt_events"]
+    # APSP CPU rate on the full-size topology: restated igraph Dijkstra rows, 1 core
+    gfull = W.geometric_graph(args.vertices, seed=args.seed, loss_max=args.edge_loss_max)
+    og = O.OGraph(gfull)
+    att = np.arange(args.vertices, dtype=np.int32)
+    t0 = time.perf_counter()
+    nrows = 16
+    for s in att[:nrows]:
+        og.row(int(s), att, count_ties=False)
+    ms_row = (time.perf_counter() - t0) * 1e3 / nrows
+    return {"value": round(pkt / dt, 1) if dt > 0 else None, "unit": "packet events/s", "cores": 1,
+            "kind": "port",
+            "sample": "oracle serial loop (reference --workers 0 semantics) on a %d-host instance of the "
+                      "same PHOLD-UDP workload (load %d), steady state over simulated [%.1f s, %.1f s): "
+                      "%d packet events in %.2f s (all events %d)"
+                      % (n, args.load, mark / 1e9, end / 1e9, pkt, dt, st["n_events"] - st["mark_events"]),
+            "warmup_wall_s": round(st["mark_wall_ms"] * 1e-3, 2),
+            "apsp_ms_per_row": round(ms_row, 3),
+            "apsp_rows": int(args.vertices),
+            "apsp_all_rows_s_extrapolated": round(ms_row * args.vertices / 1e3, 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -336,6 +336,9 @@ static void boot(ctx_t* c, uint32_t h) {
     (void)H;
 }
 
+static uint64_t g_mark = UINT64_MAX;
+void o_engine_set_mark(uint64_t t) { g_mark = t; }
+
 int o_engine_run(const shd_model* m, const shd_graph* gin, int32_t force_rows, o_run* out) {
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
@@ -364,9 +367,17 @@ int o_engine_run(const shd_model* m, const shd_graph* gin, int32_t force_rows, o
         H->txq_cap = 16; H->txq = malloc(sizeof(txent) * 16);
     }
     for (int32_t h = 0; h < m->n_hosts; h++) boot(&c, (uint32_t)h);
+    int marked = 0;
     while (c.q.n) {
         shd_event e = eh_pop(&c.q);
         c.now = e.time;
+        if (!marked && c.now >= g_mark) {
+            struct timespec tm;
+            clock_gettime(CLOCK_MONOTONIC, &tm);
+            out->mark_events = out->n_events; out->mark_pkt_events = out->n_pkt_events;
+            out->mark_wall_ms = (tm.tv_sec - t0.tv_sec) * 1e3 + (tm.tv_nsec - t0.tv_nsec) * 1e-6;
+            marked = 1;
+        }
         execute(&c, &e);
         out->n_events++;
         if (e.kind == SHD_EV_PACKET) out->n_pkt_events++;

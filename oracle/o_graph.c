@@ -76,14 +76,17 @@ int32_t o_incident(const o_graph* g, int32_t v, int32_t* eids, int32_t cap) {
 }
 
 int32_t o_get_eid(const o_graph* g, int32_t a, int32_t b) {
+    /* binary search in the (from,to,eid)-sorted index, as igraph_get_eid does;
+     * the first match is the lowest eid among parallel edges */
     int32_t from = a, to = b;
     if (!g->directed && a < b) { from = b; to = a; }
-    int32_t best = -1;
-    for (int32_t i = g->os[from]; i < g->os[from + 1]; i++) {
-        int32_t e = g->oi[i];
-        if (g->to[e] == to && (best < 0 || e < best)) best = e;
+    int32_t lo = g->os[from], hi = g->os[from + 1];
+    while (lo < hi) {
+        int32_t mid = lo + (hi - lo) / 2;
+        if (g->to[g->oi[mid]] < to) lo = mid + 1; else hi = mid;
     }
-    return best;
+    if (lo < g->os[from + 1] && g->to[g->oi[lo]] == to) return g->oi[lo];
+    return -1;
 }
 
 /* strongly connected with one cluster (topology.c:738-806) and the

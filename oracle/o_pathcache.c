@@ -203,18 +203,16 @@ int o_sssp_row(const o_graph* g, int32_t src, const int32_t* targets, int32_t nt
     /* count vertices whose final distance is reached by more than one
      * predecessor with the minimal predecessor distance (unpinned ties) */
     int64_t nties = 0;
-    for (int32_t v = 0; v < V; v++) {
+    int32_t* inc = ties ? malloc(sizeof(int32_t) * (2 * (size_t)(maxdeg + 1) + 1)) : NULL;
+    for (int32_t v = 0; v < V && ties; v++) {
         if (v == src || dists[v] < 0) continue;
         double bestd = -1; int32_t nbest = 0;
-        for (int32_t u = 0; u < 1; u++) (void)u;
-        /* scan in-arcs: for undirected graphs the incident list */
-        int32_t n = o_incident_count(g, v);
-        int32_t* inc = malloc(sizeof(int32_t) * (n + g->is[v + 1] - g->is[v] + 1));
+        /* scan in-arcs: the incident list for undirected graphs */
         int32_t m = 0;
         if (g->directed) {
-            for (int32_t i = g->is[v]; i < g->is[v + 1]; i++) inc[m++] = g->ii[i];
+            for (int32_t i = g->is[v]; i < g->is[v + 1] && m < 2 * (maxdeg + 1); i++) inc[m++] = g->ii[i];
         } else {
-            m = o_incident(g, v, inc, n);
+            m = o_incident(g, v, inc, 2 * (maxdeg + 1));
         }
         for (int32_t i = 0; i < m; i++) {
             int32_t e = inc[i];
@@ -226,8 +224,8 @@ int o_sssp_row(const o_graph* g, int32_t src, const int32_t* targets, int32_t nt
             }
         }
         if (nbest > 1) nties++;
-        free(inc);
     }
+    free(inc);
     if (ties) *ties = nties;
     /* paths (igraph 0.7.1: walk parent eids; path to the source = [source]) */
     int32_t* pv = malloc(sizeof(int32_t) * (V + 1));

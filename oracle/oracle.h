@@ -114,7 +114,12 @@ typedef struct o_run {
     uint64_t window_ns;        /* min ceil(lat*1e6) over attached pairs (for info) */
     int32_t rows_run, self_run;
     double wall_ms;
+    /* state when simulated time first reached the mark (o_engine_set_mark) */
+    uint64_t mark_events, mark_pkt_events;
+    double mark_wall_ms;
 } o_run;
+/* steady-state timing: record counters/wall time when sim time reaches t */
+void o_engine_set_mark(uint64_t t);
 /* serial mode (--workers 0): one global queue ordered by event_compare,
  * one round to end_time (slave.c:415-428) */
 int o_engine_run(const shd_model* m, const shd_graph* g, int32_t force_rows, o_run* out);

@@ -209,6 +209,14 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ShdError(f"{LIB_PATH} missing: run __graft_entry__.build() first "
                            "(there is no CPU fallback)")
+        # One HIP runtime per process: the torch wheel bundles its own
+        # libamdhip64.so.7.  Loading torch first makes libshdgpu's NEEDED
+        # libamdhip64.so.7 resolve to that same copy (same SONAME), so device
+        # pointers can flow between torch tensors (RCCL exchange) and libshdgpu.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         l = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(l, name)

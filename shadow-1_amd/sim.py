@@ -111,6 +111,40 @@ class Engine:
         S.check(rc, f"shd_eng_run_round (error bits {r.error:#x})")
         return r
 
+    # ---- phases of a round for multi-engine drivers (driver.py) ----
+    def round_kernel(self, ws, we) -> S.RoundSummary:
+        r = S.RoundSummary()
+        S.check(S.lib().shd_eng_round_kernel(self.ptr, int(ws), int(we), C.byref(r)), "round_kernel")
+        return r
+
+    def pending_records(self) -> np.ndarray:
+        n = C.c_uint64()
+        cap = 4096
+        buf = np.empty(cap, dtype=S.PENDING_DTYPE)
+        rc = S.lib().shd_eng_pending_copy(self.ptr, buf.ctypes.data, cap, C.byref(n))
+        if rc == -34:   # ERANGE: more than cap
+            buf = np.empty(n.value, dtype=S.PENDING_DTYPE)
+            rc = S.lib().shd_eng_pending_copy(self.ptr, buf.ctypes.data, n.value, C.byref(n))
+        S.check(rc, "shd_eng_pending_copy")
+        return buf[:n.value]
+
+    def resolve(self, recs: np.ndarray):
+        recs = np.ascontiguousarray(recs, dtype=S.PENDING_DTYPE)
+        S.check(S.lib().shd_eng_resolve(self.ptr, recs.ctypes.data if len(recs) else None, len(recs)),
+                "shd_eng_resolve")
+
+    def end_round(self) -> S.RoundSummary:
+        r = S.RoundSummary()
+        rc = S.lib().shd_eng_end_round(self.ptr, C.byref(r))
+        S.check(rc, f"shd_eng_end_round (error bits {r.error:#x})")
+        return r
+
+    def remote_copy(self, dev_ptr: int, cap_events: int) -> int:
+        n = C.c_uint64()
+        S.check(S.lib().shd_eng_remote_copy(self.ptr, C.c_void_p(dev_ptr), int(cap_events), C.byref(n)),
+                "shd_eng_remote_copy")
+        return n.value
+
     def next_time(self) -> int:
         t = C.c_uint64()
         S.check(S.lib().shd_eng_next_time(self.ptr, C.byref(t)), "next_time")

@@ -19,7 +19,8 @@ class ORun(C.Structure):
     _fields_ = [("trace", P(S.TraceRec)), ("n_trace", C.c_uint64), ("cap_trace", C.c_uint64),
                 ("digest", P(S.HostDigest)), ("n_events", C.c_uint64), ("n_pkt_events", C.c_uint64),
                 ("window_ns", C.c_uint64), ("rows_run", C.c_int32), ("self_run", C.c_int32),
-                ("wall_ms", C.c_double)]
+                ("wall_ms", C.c_double), ("mark_events", C.c_uint64),
+                ("mark_pkt_events", C.c_uint64), ("mark_wall_ms", C.c_double)]
 
 
 class OCodelEntry(C.Structure):
@@ -73,6 +74,7 @@ def lib():
         l.o_engine_run.argtypes = [P(S.Model), P(S.Graph), C.c_int32, P(ORun)]
         l.o_run_free.argtypes = [P(ORun)]
         l.o_event_compare.argtypes = [P(S.Event), P(S.Event)]
+        l.o_engine_set_mark.argtypes = [C.c_uint64]
         _lib = l
     return _lib
 
@@ -92,7 +94,7 @@ class OGraph:
         lib().o_graph_props(self.ptr, C.byref(p))
         return p
 
-    def row(self, src, targets):
+    def row(self, src, targets, count_ties=True):
         t = np.ascontiguousarray(targets, dtype=np.int32)
         n = len(t)
         lat = np.empty(n); rel = np.empty(n)
@@ -100,7 +102,7 @@ class OGraph:
         ties = C.c_int64(0)
         lib().o_sssp_row(self.ptr, int(src), S.as_ptr(t, C.c_int32), n, S.as_ptr(lat, C.c_double),
                          S.as_ptr(rel, C.c_double), S.as_ptr(ok, C.c_int32),
-                         S.as_ptr(hops, C.c_int32), C.byref(ties))
+                         S.as_ptr(hops, C.c_int32), C.byref(ties) if count_ties else None)
         return lat, rel, ok, hops, ties.value
 
     def direct(self, s, d):
@@ -135,8 +137,9 @@ class OTopo:
         return lib().o_topo_rows_run(self.ptr)
 
 
-def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False):
+def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None):
     """Serial reference loop; returns (trace ndarray, digest ndarray, ORun stats dict)."""
+    lib().o_engine_set_mark((1 << 64) - 1 if mark is None else int(mark))
     r = ORun()
     rc = lib().o_engine_run(C.byref(model.struct), C.byref(g.struct), int(force_rows), C.byref(r))
     assert rc == 0
@@ -148,7 +151,8 @@ def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False):
     dg = np.empty(H, dtype=S.DIGEST_DTYPE)
     C.memmove(dg.ctypes.data, r.digest, H * S.DIGEST_DTYPE.itemsize)
     stats = dict(n_events=r.n_events, n_pkt_events=r.n_pkt_events, rows_run=r.rows_run,
-                 self_run=r.self_run, wall_ms=r.wall_ms)
+                 self_run=r.self_run, wall_ms=r.wall_ms, mark_events=r.mark_events,
+                 mark_pkt_events=r.mark_pkt_events, mark_wall_ms=r.mark_wall_ms)
     lib().o_run_free(C.byref(r))
     return tr, dg, stats
 

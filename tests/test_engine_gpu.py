@@ -101,3 +101,26 @@ def test_run_to_run_determinism():
         outs.append((sort_trace(e.trace()), e.digest()))
         e.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_sharded_engines_match_oracle(parts):
+    """Hosts partitioned over several engines (DESIGN.md "Multi-GPU"): the
+    exchanged events and the global first-touch resolution reproduce the
+    serial run exactly."""
+    from driver import LocalCluster, partition
+    g = W.geometric_graph(240, seed=6)
+    m = W.phold_model(W.hosts_on_vertices(240, 1), end_time=3 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    pb = partition(m.n_hosts, parts)
+    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
+    cl = LocalCluster(engines, pb)
+    cl.boot()
+    res = cl.run_until(m.params["end_time"])
+    assert res.exchanged > 0 and res.pending > 0
+    tr = sort_trace(np.concatenate([e.trace() for e in engines]))
+    dg = np.concatenate([e.digest() for e in engines])
+    otr, odg, ost = O.engine_run(m, g)
+    assert res.pkt_events == ost["n_pkt_events"]
+    assert np.array_equal(tr, sort_trace(otr))
+    assert np.array_equal(dg, odg)
