@@ -662,7 +662,17 @@ __global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int par
     const int32_t l = blockIdx.x * kBlock + threadIdx.x;
     uint64_t next = kInf, nev = 0, npkt = 0;
     uint32_t err = 0;
+    // hosts with nothing due this round touch 2-3 words, not their whole state
+    bool idle = false;
     if (l < P.nloc) {
+        const uint32_t nin0 = P.inbox_n[parity][l];
+        const uint32_t nq0 = P.evq_n[l];
+        if (nin0 == 0) {
+            const uint64_t t0 = nq0 ? P.evq[(size_t)l * P.evq_cap].time : kInf;
+            if (t0 >= we) { idle = true; next = t0; }
+        }
+    }
+    if (l < P.nloc && !idle) {
         HostCtx c;
         load_ctx(P, c, l);
         const uint64_t ev0 = c.c_events, pk0 = c.c_pkt;
