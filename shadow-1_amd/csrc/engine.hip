@@ -68,7 +68,6 @@ struct DevSummary {
     unsigned long long n_pkt_events;
     unsigned long long n_pending;
     unsigned long long n_remote;
-    unsigned long long n_trace;
     unsigned int error;
     unsigned int pad;
 };
@@ -134,7 +133,10 @@ struct Params {
     uint32_t remote_cap;
     shd_trace_rec* trace_buf;
     uint64_t trace_cap;
-    DevSummary* sum;
+    unsigned long long* trace_n;   // cumulative trace records
+    DevSummary* sum;               // this round's summary
+    int32_t* next_rank;            // row-rank counter (device is the source of truth)
+    uint32_t* halt;                // set when a round needs host-side resolution
 };
 
 // --------------------------------------------------------------- RNG
@@ -222,7 +224,7 @@ __device__ shd_event heap_pop(const Params& P, HostCtx& c) {
 __device__ __forceinline__ void trace(const Params& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
                                       uint32_t peer, uint32_t pkt, uint32_t kind) {
     if (!P.trace) return;
-    unsigned long long i = atomicAdd(&P.sum->n_trace, 1ull);
+    unsigned long long i = atomicAdd(P.trace_n, 1ull);
     if (i >= P.trace_cap) { c.err |= SHD_ERR_TRACE_OVERFLOW; return; }
     shd_trace_rec r;
     r.time = t; r.seq = seq; r.host = host; r.peer = peer; r.pkt = pkt; r.kind = kind;
@@ -658,7 +660,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
 }
 
 // one round [ws, we): merge inbox[parity], run events < we
-__global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int parity) {
+__device__ __forceinline__ void round_body(const Params& P, uint64_t we, int parity) {
     const int32_t l = blockIdx.x * kBlock + threadIdx.x;
     uint64_t next = kInf, nev = 0, npkt = 0;
     uint32_t err = 0;
@@ -700,34 +702,120 @@ __global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int par
     block_reduce_publish<kBlock>(P, next, nev, npkt, err);
 }
 
+__global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int parity) {
+    round_body(P, we, parity);
+}
+
+// device-driven round: the window start is the previous round's next event
+// time (read on the device), so rounds are enqueued back to back with no host
+// round trip; a round past `stop` only forwards the time.  `init` is the next
+// round's summary, initialised here (nothing else touches it this round).
+__global__ __launch_bounds__(kBlock) void k_round_dev(Params P, const DevSummary* __restrict__ prev,
+                                                       DevSummary* __restrict__ init, uint64_t window,
+                                                       uint64_t stop, int parity) {
+    if (*P.halt) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        DevSummary z{};
+        z.next_time = kInf;
+        *init = z;
+    }
+    const uint64_t ws = prev->next_time;
+    if (ws >= stop) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&P.sum->next_time, (unsigned long long)ws);
+        return;
+    }
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    round_body(P, we, parity);
+}
+
 // finalize resolved pending sends: value from the min-rank row, then deliver
+__device__ void finalize_one(const Params& P, const Pending& r, int next_parity, uint64_t& next, uint32_t& err) {
+    if (r.delivered != 1u) return;
+    const PathVal pv = path_value(P, (int32_t)r.a, (int32_t)r.b);
+    if (!pv.resolved) err |= SHD_ERR_AMBIGUOUS;
+    shd_event e;
+    e.time = r.qtime + (uint64_t)ceil(pv.lat * (double)SHD_MS);
+    e.seq = r.seq; e.src = r.qhost; e.dst = r.dst; e.pkt = r.pkt; e.kind = SHD_EV_PACKET;
+    if (e.time >= P.end_time) return;
+    if (e.time < next) next = e.time;
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl >= 0 && dl < P.nloc) {
+        uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
+        if (slot >= P.inbox_cap) err |= SHD_ERR_INBOX_OVERFLOW;
+        else P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
+    } else {
+        unsigned long long slot = atomicAdd(&P.sum->n_remote, 1ull);
+        if (slot >= P.remote_cap) err |= SHD_ERR_REMOTE_OVERFLOW;
+        else P.remote[slot] = e;
+    }
+}
+
 __global__ void k_finalize(Params P, const Pending* __restrict__ pend, uint32_t n, int next_parity) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t next = kInf;
     uint32_t err = 0;
-    if (i < n) {
-        const Pending r = pend[i];
-        if (r.delivered == 1u) {
-            const PathVal pv = path_value(P, (int32_t)r.a, (int32_t)r.b);
-            if (!pv.resolved) err |= SHD_ERR_AMBIGUOUS;
-            shd_event e;
-            e.time = r.qtime + (uint64_t)ceil(pv.lat * (double)SHD_MS);
-            e.seq = r.seq; e.src = r.qhost; e.dst = r.dst; e.pkt = r.pkt; e.kind = SHD_EV_PACKET;
-            if (e.time < P.end_time) {
-                next = e.time;
-                const int32_t dl = (int32_t)e.dst - P.h0;
-                if (dl >= 0 && dl < P.nloc) {
-                    uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
-                    if (slot >= P.inbox_cap) err |= SHD_ERR_INBOX_OVERFLOW;
-                    else P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
-                } else {
-                    unsigned long long slot = atomicAdd(&P.sum->n_remote, 1ull);
-                    if (slot >= P.remote_cap) err |= SHD_ERR_REMOTE_OVERFLOW;
-                    else P.remote[slot] = e;
-                }
+    if (i < n) finalize_one(P, pend[i], next_parity, next, err);
+    if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+    if (err) atomicOr(&P.sum->error, err);
+}
+
+// device-side first-touch resolution for rounds with few logged queries (the
+// common case after warm-up): one workgroup ranks the records by serial key
+// (counting sort: keys are unique), one lane assigns row ranks in that order,
+// every lane finalizes its record.  Larger rounds halt the pipeline for the
+// host path (shd_eng_resolve).
+constexpr int kResolveMax = 256;
+__device__ __forceinline__ bool pend_less(const Pending& x, const Pending& y) {
+    if (x.qtime != y.qtime) return x.qtime < y.qtime;
+    if (x.qhost != y.qhost) return x.qhost < y.qhost;
+    if (x.qsrc != y.qsrc) return x.qsrc < y.qsrc;
+    if (x.qseq != y.qseq) return x.qseq < y.qseq;
+    return x.qsub < y.qsub;
+}
+
+__global__ __launch_bounds__(kResolveMax) void k_resolve_dev(Params P, int next_parity) {
+    __shared__ Pending recs[kResolveMax];
+    __shared__ int16_t order[kResolveMax];
+    if (*P.halt) return;
+    const unsigned long long n = P.sum->n_pending;
+    if (n == 0) return;
+    if (n > (unsigned long long)kResolveMax) {
+        if (threadIdx.x == 0) *P.halt = 1u;
+        return;
+    }
+    const int i = threadIdx.x;
+    if (i < (int)n) recs[i] = P.pend[i];
+    __syncthreads();
+    if (i < (int)n) {
+        int pos = 0;
+        for (int j = 0; j < (int)n; j++) pos += pend_less(recs[j], recs[i]) ? 1 : 0;
+        order[pos] = (int16_t)i;
+    }
+    __syncthreads();
+    if (i == 0) {
+        int32_t nr = *P.next_rank;
+        int32_t* rank = (int32_t*)P.rank;
+        int32_t* srank = (int32_t*)P.self_rank;
+        for (int k = 0; k < (int)n; k++) {
+            const Pending& r = recs[order[k]];
+            const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
+            if (a == b) {
+                if (rank[a] == kNoRank && srank[a] == kNoRank) srank[a] = nr++;
+            } else if (P.directed) {
+                if (rank[a] == kNoRank) rank[a] = nr++;
+            } else {
+                if (rank[a] == kNoRank && rank[b] == kNoRank) rank[a] = nr++;
             }
         }
+        *P.next_rank = nr;
+        __threadfence();
     }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // drop L1 lines of the rank arrays
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    if (i < (int)n) finalize_one(P, recs[i], next_parity, next, err);
     if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
     if (err) atomicOr(&P.sum->error, err);
 }
@@ -813,6 +901,16 @@ struct shd_eng {
     int32_t next_rank = 0;
     uint64_t pending_resolved = 0;
     uint64_t round_ws = 0, round_we = 0, round_pending = 0, round_events = 0, round_pkt = 0;
+    uint64_t round = 0;                     // rounds executed (parity = round & 1)
+    // device-driven pipeline
+    static constexpr int kBatch = 64;
+    static constexpr int kRing = 2 * kBatch + 2;
+    DevSummary* d_ring = nullptr;
+    DevSummary* h_ring = nullptr;           // pinned
+    uint32_t* d_halt = nullptr;
+    int32_t* d_next_rank = nullptr;
+    unsigned long long* d_trace_n = nullptr;
+    hipEvent_t bev[2 * kBatch] = {};
     uint64_t trace_cap = 0;
 };
 
@@ -894,6 +992,15 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     EALLOC(e->d_rank, pc->T); EALLOC(e->d_self_rank, pc->T);
     EALLOC(e->d_sum, 1);
     if (hipHostMalloc((void**)&e->h_sum, sizeof(DevSummary)) != hipSuccess) { shd_eng_destroy(e); return SHD_ENOMEM; }
+    memset(e->h_sum, 0, sizeof(DevSummary));
+    EALLOC(e->d_ring, shd_eng::kRing);
+    if (hipHostMalloc((void**)&e->h_ring, sizeof(DevSummary) * shd_eng::kRing) != hipSuccess) {
+        shd_eng_destroy(e);
+        return SHD_ENOMEM;
+    }
+    EALLOC(e->d_halt, 1); EALLOC(e->d_next_rank, 1); EALLOC(e->d_trace_n, 1);
+    for (auto& ev : e->bev) (void)hipEventCreate(&ev);
+    P.halt = e->d_halt; P.next_rank = e->d_next_rank; P.trace_n = e->d_trace_n;
     P.pend_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 16, (uint64_t)n * (m->load + 4)), 1u << 30);
     P.remote_cap = (uint32_t)std::min<uint64_t>((uint64_t)n * P.inbox_cap, 1u << 30);
     {
@@ -973,9 +1080,8 @@ extern "C" int shd_eng_window(shd_eng* e, uint64_t* w) {
 static int reset_summary(shd_eng* e) {
     DevSummary z{};
     z.next_time = kInf;
-    // keep n_trace cumulative
-    z.n_trace = e->h_sum->n_trace;
     SHD_HIP(hipMemcpyAsync(e->d_sum, &z, sizeof(z), hipMemcpyHostToDevice, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
     return SHD_OK;
 }
 
@@ -1022,6 +1128,7 @@ extern "C" int shd_eng_round_kernel(shd_eng* e, uint64_t ws, uint64_t we, shd_ro
     int rc = reset_summary(e);
     if (rc) return rc;
     const int grid = (e->nloc + kBlock - 1) / kBlock;
+    e->P.sum = e->d_sum;
     SHD_HIP(hipEventRecord(e->ev0, e->stream));
     hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, e->P, we, e->parity);
     SHD_HIP(hipGetLastError());
@@ -1063,6 +1170,12 @@ extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_al
     if (!e || (n_all && !all)) return SHD_EINVAL;
     if (!n_all) return SHD_OK;
     SHD_HIP(hipSetDevice(e->device));
+    // the device is the source of truth for ranks (k_resolve_dev assigns them too)
+    SHD_HIP(hipMemcpyAsync(e->h_rank.data(), e->d_rank, 4 * (size_t)e->pc->T, hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipMemcpyAsync(e->h_self_rank.data(), e->d_self_rank, 4 * (size_t)e->pc->T, hipMemcpyDeviceToHost,
+                           e->stream));
+    SHD_HIP(hipMemcpyAsync(&e->next_rank, e->d_next_rank, 4, hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
     std::vector<shd_pending> recs(all, all + n_all);
     sort_pending(recs);
     const bool directed = e->pc->directed;
@@ -1080,6 +1193,7 @@ extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_al
     const int32_t T = e->pc->T;
     SHD_HIP(hipMemcpyAsync(e->d_rank, e->h_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
     SHD_HIP(hipMemcpyAsync(e->d_self_rank, e->h_self_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
+    SHD_HIP(hipMemcpyAsync(e->d_next_rank, &e->next_rank, 4, hipMemcpyHostToDevice, e->stream));
     const uint32_t n = (uint32_t)e->round_pending;
     if (n) {
         hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->P,
@@ -1095,6 +1209,7 @@ extern "C" int shd_eng_end_round(shd_eng* e, shd_round_summary* out) {
     int rc = read_summary(e);
     if (rc) return rc;
     e->parity ^= 1;
+    e->round++;
     if (out) {
         out->window_start = e->round_ws; out->window_end = e->round_we;
         out->next_time = e->h_sum->next_time;
@@ -1118,30 +1233,98 @@ extern "C" int shd_eng_run_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round
     return shd_eng_end_round(e, out);
 }
 
+// Device-driven rounds (single engine): batches of kBatch rounds are enqueued
+// back to back, each k_round_dev reading its window start from the previous
+// round's summary on the device and k_resolve_dev resolving small first-touch
+// logs in place.  The host reads the batch's summaries once per batch.  A
+// round whose first-touch log is too large for the device path halts the
+// batch; the host resolves it (shd_eng_resolve) and resumes after it.
 extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;
     auto t0 = std::chrono::steady_clock::now();
     int rc = SHD_OK;
     if (!e->booted && (rc = shd_eng_boot(e))) return rc;
+    SHD_HIP(hipSetDevice(e->device));
     shd_run_stats s{};
     s.window_ns = e->window;
-    uint64_t next = e->h_sum->next_time;
     const uint64_t stop = std::min<uint64_t>(t_stop, e->P.end_time);
+    uint64_t next = e->h_sum->next_time;
     e->kernel_ms_total = 0;
     const uint64_t pend0 = e->pending_resolved;
-    while (next < stop) {
-        const uint64_t ws = next;
-        uint64_t we = ws + e->window;
-        if (we > stop || we < ws) we = stop;
-        shd_round_summary r;
-        rc = shd_eng_run_round(e, ws, we, &r);
-        s.n_rounds++;
-        s.n_events += r.n_events;
-        s.n_pkt_events += r.n_pkt_events;
-        s.final_time = we;
-        if (rc) { s.error = r.error; break; }
-        next = r.next_time;
+    const int grid = (e->nloc + kBlock - 1) / kBlock;
+    constexpr int B = shd_eng::kBatch, R = shd_eng::kRing;
+    while (next < stop && rc == SHD_OK) {
+        // slot 0 carries the window start; rounds use slots 1..B
+        DevSummary seed{};
+        seed.next_time = next;
+        DevSummary first{};
+        first.next_time = kInf;
+        SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &seed, sizeof(seed), hipMemcpyHostToDevice, e->stream));
+        SHD_HIP(hipMemcpyAsync(&e->d_ring[1], &first, sizeof(first), hipMemcpyHostToDevice, e->stream));
+        SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
+        for (int i = 0; i < B; i++) {
+            Params P = e->P;
+            P.sum = &e->d_ring[i + 1];
+            const int parity = (int)((e->round + i) & 1);
+            SHD_HIP(hipEventRecord(e->bev[2 * i], e->stream));
+            hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, P,
+                               (const DevSummary*)&e->d_ring[i], &e->d_ring[i + 2], e->window, stop, parity);
+            SHD_HIP(hipEventRecord(e->bev[2 * i + 1], e->stream));
+            hipLaunchKernelGGL(k_resolve_dev, dim3(1), dim3(kResolveMax), 0, e->stream, P, parity ^ 1);
+        }
+        SHD_HIP(hipGetLastError());
+        uint32_t halt = 0;
+        SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost, e->stream));
+        SHD_HIP(hipMemcpyAsync(&halt, e->d_halt, 4, hipMemcpyDeviceToHost, e->stream));
+        SHD_HIP(hipStreamSynchronize(e->stream));
+        static_assert(R >= B + 2, "summary ring");
+        for (int i = 0; i < B; i++) {
+            const DevSummary& r = e->h_ring[i + 1];
+            const uint64_t ws = e->h_ring[i].next_time;
+            if (ws >= stop) { next = ws; break; }   // the rest only forwarded the time
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e->bev[2 * i], e->bev[2 * i + 1]);
+            e->kernel_ms_total += ms;
+            e->last_kernel_ms = ms;
+            const bool halted_here = halt && r.n_pending > (unsigned long long)kResolveMax;
+            s.n_rounds++;
+            s.n_events += r.n_events;
+            s.n_pkt_events += r.n_pkt_events;
+            uint64_t we = ws + e->window;
+            if (we > stop || we < ws) we = stop;
+            s.final_time = we;
+            e->round++;
+            e->parity = (int)(e->round & 1);
+            if (halted_here) {
+                // host resolution of this round's log, then resume after it
+                e->round_pending = r.n_pending;
+                *e->h_sum = r;
+                SHD_HIP(hipMemcpyAsync(e->d_sum, &r, sizeof(r), hipMemcpyHostToDevice, e->stream));
+                std::vector<shd_pending> recs(r.n_pending);
+                uint64_t n = 0;
+                const int saved_parity = e->parity;
+                e->parity = (int)((e->round - 1) & 1);   // the halted round's parity
+                e->P.sum = e->d_sum;
+                if ((rc = shd_eng_pending_copy(e, recs.data(), recs.size(), &n)) ||
+                    (rc = shd_eng_resolve(e, recs.data(), n)) || (rc = read_summary(e))) {
+                    e->parity = saved_parity;
+                    break;
+                }
+                e->parity = saved_parity;
+                next = e->h_sum->next_time;
+                if (e->h_sum->error) { s.error = e->h_sum->error; rc = SHD_EOVERFLOW; }
+                break;
+            }
+            if (r.n_pending) e->pending_resolved += r.n_pending;
+            if (r.error) {
+                s.error = r.error;
+                rc = (r.error & SHD_ERR_AMBIGUOUS) ? SHD_EAMBIG : SHD_EOVERFLOW;
+                break;
+            }
+            next = r.next_time;
+        }
     }
+    e->h_sum->next_time = next;
     s.n_pending_resolved = e->pending_resolved - pend0;
     s.device_ms_round_kernel = e->kernel_ms_total;
     s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1185,16 +1368,23 @@ extern "C" int shd_eng_next_time(shd_eng* e, uint64_t* t) {
     return SHD_OK;
 }
 
+static uint64_t trace_total(shd_eng* e) {
+    unsigned long long t = 0;
+    if (hipMemcpy(&t, e->d_trace_n, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+    return t;
+}
+
 extern "C" int shd_eng_trace_count(shd_eng* e, uint64_t* n) {
     if (!e || !n) return SHD_EINVAL;
-    *n = std::min<uint64_t>(e->h_sum->n_trace, e->trace_cap);
+    SHD_HIP(hipSetDevice(e->device));
+    *n = std::min<uint64_t>(trace_total(e), e->trace_cap);
     return SHD_OK;
 }
 
 extern "C" int shd_eng_trace_copy(shd_eng* e, shd_trace_rec* out, uint64_t cap, uint64_t* n) {
     if (!e || !out || !n) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(e->device));
-    const uint64_t cnt = std::min<uint64_t>(std::min<uint64_t>(e->h_sum->n_trace, e->trace_cap), cap);
+    const uint64_t cnt = std::min<uint64_t>(std::min<uint64_t>(trace_total(e), e->trace_cap), cap);
     if (cnt) SHD_HIP(hipMemcpy(out, e->P.trace_buf, sizeof(shd_trace_rec) * cnt, hipMemcpyDeviceToHost));
     *n = cnt;
     return SHD_OK;
@@ -1231,6 +1421,9 @@ extern "C" void shd_eng_destroy(shd_eng* e) {
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_sum) (void)hipHostFree(e->h_sum);
+    if (e->h_ring) (void)hipHostFree(e->h_ring);
+    for (auto& ev : e->bev)
+        if (ev) (void)hipEventDestroy(ev);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
