@@ -301,7 +301,8 @@ typedef struct shd_round_summary {
 enum {
     SHD_ERR_EVQ_OVERFLOW = 1, SHD_ERR_INBOX_OVERFLOW = 2, SHD_ERR_CODELQ_OVERFLOW = 4,
     SHD_ERR_TXQ_OVERFLOW = 8, SHD_ERR_AMBIGUOUS = 16, SHD_ERR_PENDING_OVERFLOW = 32,
-    SHD_ERR_TRACE_OVERFLOW = 64, SHD_ERR_REMOTE_OVERFLOW = 128
+    SHD_ERR_TRACE_OVERFLOW = 64, SHD_ERR_REMOTE_OVERFLOW = 128,
+    SHD_ERR_INTERNAL = 0x80000000u  /* engine invariant broken (bad event kind, timer slot reuse) */
 };
 
 typedef struct shd_run_stats {

@@ -72,10 +72,20 @@ struct DevSummary {
     unsigned int pad;
 };
 
+// destination-pick guide: for bucket k, i = the first index with
+// dest_cum[i] >= k / H, and the next three cumulative weights inline, so an
+// even-weight pick resolves in one 32-B load
+struct DestGuide {
+    int32_t i;
+    int32_t pad;
+    double cum[3];   // dest_cum[i .. i+2], 2.0 past the end
+};
+
 struct Params {
     // hosts
     int32_t H;                  // total hosts of the model
     int32_t h0, nloc;           // this engine's hosts [h0, h0+nloc)
+    int32_t hpw;                // hosts per wave in the round kernel (lanes >= hpw idle)
     uint32_t evq_cap, inbox_cap, cq_cap, tq_cap;
     uint64_t end_time, bootstrap_end, heartbeat, app_start;
     uint32_t load, payload, trace, pkt_len;
@@ -104,9 +114,15 @@ struct Params {
     uint64_t* c_idrop;
     uint64_t* c_cdrop;
     uint64_t* c_recv;
-    // queues
-    shd_event* evq;
+    // timer slots: the self events with at most one pending instance per host
+    // (heartbeat, token-bucket refill, epoll notification) as (time, seq)
+    uint64_t* tm_time[3];
+    uint64_t* tm_seq[3];
+    uint64_t* hnext;             // per-host earliest pending event (timers, heap)
+    // queues: per-host 4-ary heap of the other events (packets, loopback, boot one-shots)
+    shd_event* evq;              // slab of evq_stride entries per host, heap at +3
     uint32_t* evq_n;
+    uint32_t evq_stride;
     shd_event* inbox[2];
     uint32_t* inbox_n[2];
     CodelEnt* cq;
@@ -114,15 +130,13 @@ struct Params {
     // global host tables (all H hosts)
     const int32_t* host_att;     // attached index of every host
     const double* dest_cum;
+    const struct DestGuide* dest_guide;   // [H]: bucket k -> first i with dest_cum[i] >= k / H
     // path cache
     int32_t T;
     int32_t complete, prefer_direct, directed;
-    const double* row_lat;
-    const double* row_rel;
-    const double* dir_lat;
-    const double* dir_rel;
-    const double* self_lat;
-    const double* self_rel;
+    const shd_pv* row;           // [T][T] (lat, rel)
+    const shd_pv* dir;           // [T][T] direct-edge values
+    const shd_pv* self;          // [T] self-path values
     const uint8_t* adj;
     const int32_t* rank;
     const int32_t* self_rank;
@@ -138,6 +152,29 @@ struct Params {
     int32_t* next_rank;            // row-rank counter (device is the source of truth)
     uint32_t* halt;                // set when a round needs host-side resolution
 };
+
+// --------------------------------------------------------------- profiling
+// Built with -DSHD_PROF (make prof -> libshdgpu_prof.so, scripts/prof_round.py):
+// per-thread shader-clock totals per phase, summed and max-reduced into g_prof.
+enum {
+    PR_TOTAL, PR_LOAD, PR_MERGE, PR_POP, PR_EXEC_PKT, PR_EXEC_NOTIFY, PR_EXEC_REFILL, PR_EXEC_OTHER, PR_PICK,
+    PR_SEND, PR_STORE, PR_NEV, PR_N
+};
+#ifdef SHD_PROF
+__device__ unsigned long long g_prof[2 * PR_N + 2];
+// per-round wave timing (100 MHz wall clock), 128 round slots keyed by the
+// summary address: min start, max end, max wave duration, sum of durations,
+// waves, max events of a lane, sum over waves of the wave's max lane events
+__device__ unsigned long long g_wave[128][8];
+struct ProfAcc {
+    unsigned long long v[PR_N] = {};
+};
+#define PROF_T0(name) const unsigned long long name = clock64();
+#define PROF_ADD(c, i, t0) (c).prof.v[i] += clock64() - (t0);
+#else
+#define PROF_T0(name)
+#define PROF_ADD(c, i, t0)
+#endif
 
 // --------------------------------------------------------------- RNG
 __device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
@@ -167,6 +204,13 @@ struct HostCtx {
     uint32_t cq_dc, cq_dcl, cq_head, cq_count;
     uint32_t tq_head, tq_count;
     uint32_t evq_n;
+    shd_event top;              // heap root (valid when evq_n > 0)
+    uint64_t tt0, tt1, tt2;     // timer times (kInf = empty): heartbeat, refill, notify
+    uint64_t ts0, ts1, ts2;     // timer event IDs
+    CodelEnt cq_hint;           // CoDel head entry held in registers (not yet stored)
+    TxEnt tq_hint;              // send FIFO head entry held in registers
+    bool cq_hv, tq_hv;
+    int32_t att;                // this host's attached-vertex index
     uint64_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;
     // current executing event key (for first-touch logging)
     uint64_t q_seq;
@@ -175,6 +219,9 @@ struct HostCtx {
     uint64_t min_emit;   // min time of events sent to other hosts
     uint32_t err;
     uint32_t n_pend;
+#ifdef SHD_PROF
+    ProfAcc prof;
+#endif
 };
 
 __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) {
@@ -183,13 +230,22 @@ __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) 
     return a.seq < b.seq;
 }
 
+// 4-ary min-heap; the slab's entry 3 is the root, so the four children of
+// node i (4i+1 .. 4i+4) fill one aligned 128-B line.  The root is cached in
+// c.top: peeking never touches memory.
+__device__ __forceinline__ shd_event* heap_base(const Params& P, const HostCtx& c) {
+    return P.evq + (size_t)c.l * P.evq_stride + 3;
+}
+
 __device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
-    shd_event* hp = P.evq + (size_t)c.l * P.evq_cap;
+    shd_event* hp = heap_base(P, c);
     if (c.evq_n >= P.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
     uint32_t i = c.evq_n++;
+    if (i == 0) { hp[0] = e; c.top = e; return; }
+    if (ev_less(e, c.top)) c.top = e;   // it will end at the root
     while (i > 0) {
-        uint32_t p = (i - 1) >> 1;
-        shd_event pe = hp[p];
+        const uint32_t p = (i - 1) >> 2;
+        const shd_event pe = hp[p];
         if (!ev_less(e, pe)) break;
         hp[i] = pe;
         i = p;
@@ -197,28 +253,32 @@ __device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
     hp[i] = e;
 }
 
-__device__ shd_event heap_pop(const Params& P, HostCtx& c) {
-    shd_event* hp = P.evq + (size_t)c.l * P.evq_cap;
-    shd_event top = hp[0];
-    uint32_t n = --c.evq_n;
-    if (n == 0) return top;
-    shd_event last = hp[n];
+// remove the root (c.top); the new root is re-cached
+__device__ void heap_pop(const Params& P, HostCtx& c) {
+    shd_event* hp = heap_base(P, c);
+    const uint32_t n = --c.evq_n;
+    if (n == 0) return;
+    const shd_event last = hp[n];
     uint32_t i = 0;
     for (;;) {
-        uint32_t lc = 2 * i + 1;
-        if (lc >= n) break;
-        uint32_t m = lc;
-        shd_event me = hp[lc];
-        if (lc + 1 < n) {
-            shd_event re = hp[lc + 1];
-            if (ev_less(re, me)) { m = lc + 1; me = re; }
-        }
+        const uint32_t c1 = 4 * i + 1;
+        if (c1 >= n) break;
+        shd_event ch[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (c1 + k < n) ch[k] = hp[c1 + k];
+        uint32_t m = c1;
+        shd_event me = ch[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++)
+            if (c1 + k < n && ev_less(ch[k], me)) { me = ch[k]; m = c1 + k; }
         if (!ev_less(me, last)) break;
         hp[i] = me;
+        if (i == 0) c.top = me;
         i = m;
     }
     hp[i] = last;
-    return top;
+    if (i == 0) c.top = last;
 }
 
 __device__ __forceinline__ void trace(const Params& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
@@ -244,7 +304,22 @@ __device__ void schedule_self(const Params& P, HostCtx& c, uint32_t kind, uint64
     e.pkt = pkt;
     e.kind = kind;
     if (e.time >= P.end_time) return;
-    heap_push(P, c, e);
+    switch (kind) {   // at most one pending instance each (flags / self-rescheduling)
+    case SHD_EV_HEARTBEAT:
+        if (c.tt0 != kInf) c.err |= SHD_ERR_INTERNAL;
+        c.tt0 = e.time; c.ts0 = e.seq;
+        break;
+    case SHD_EV_REFILL:
+        if (c.tt1 != kInf) c.err |= SHD_ERR_INTERNAL;
+        c.tt1 = e.time; c.ts1 = e.seq;
+        break;
+    case SHD_EV_NOTIFY:
+        if (c.tt2 != kInf) c.err |= SHD_ERR_INTERNAL;
+        c.tt2 = e.time; c.ts2 = e.seq;
+        break;
+    default:
+        heap_push(P, c, e);
+    }
 }
 
 // deliver an inter-host event: to the destination's inbox for the next round,
@@ -301,8 +376,12 @@ __device__ __forceinline__ uint64_t codel_control_law(uint32_t count, uint64_t t
 __device__ bool codel_helper(const Params& P, HostCtx& c, bool& okToDrop, CodelEnt& out) {
     okToDrop = false;
     if (c.cq_count == 0) { c.cq_iexp = 0; return false; }
-    CodelEnt* q = P.cq + (size_t)c.l * P.cq_cap;
-    out = q[c.cq_head];
+    if (c.cq_hv) {
+        out = c.cq_hint;
+        c.cq_hv = false;
+    } else {
+        out = P.cq[(size_t)c.l * P.cq_cap + c.cq_head];
+    }
     c.cq_head = (c.cq_head + 1 == P.cq_cap) ? 0 : c.cq_head + 1;
     c.cq_count--;
     c.cq_total -= P.pkt_len;
@@ -379,32 +458,37 @@ __device__ PathVal path_value(const Params& P, int32_t a, int32_t b) {
     v.log = false;
     const size_t ab = (size_t)a * P.T + b, ba = (size_t)b * P.T + a;
     if (P.complete || (P.prefer_direct && P.adj[ab])) {
-        v.lat = P.dir_lat[ab]; v.rel = P.dir_rel[ab];
+        const shd_pv d = P.dir[ab];
+        v.lat = d.lat; v.rel = d.rel;
         return v;
     }
+    // every candidate is loaded in one round trip; the rank rule picks after
+    const int32_t ra = P.rank[a];
     if (a == b) {
-        const int32_t ra = P.rank[a], rs = P.self_rank[a];
+        const int32_t rs = P.self_rank[a];
+        const shd_pv s = P.self[a], r = P.row[ab];
         if (ra == kNoRank && rs == kNoRank) {
             v.resolved = false; v.log = true;
-            v.lat = P.self_lat[a]; v.rel = P.self_rel[a];
-            v.lat2 = P.row_lat[ab]; v.rel2 = P.row_rel[ab];
+            v.lat = s.lat; v.rel = s.rel;
+            v.lat2 = r.lat; v.rel2 = r.rel;
         } else if (rs < ra) {
-            v.lat = P.self_lat[a]; v.rel = P.self_rel[a];
+            v.lat = s.lat; v.rel = s.rel;
         } else {
-            v.lat = P.row_lat[ab]; v.rel = P.row_rel[ab];
+            v.lat = r.lat; v.rel = r.rel;
         }
         return v;
     }
-    const int32_t ra = P.rank[a], rb = P.rank[b];
+    const int32_t rb = P.rank[b];
+    const shd_pv vab = P.row[ab], vba = P.row[ba];
     if (ra == kNoRank && rb == kNoRank) {
         v.resolved = false; v.log = true;
-        v.lat = P.row_lat[ab]; v.rel = P.row_rel[ab];
-        v.lat2 = P.row_lat[ba]; v.rel2 = P.row_rel[ba];
+        v.lat = vab.lat; v.rel = vab.rel;
+        v.lat2 = vba.lat; v.rel2 = vba.rel;
         return v;
     }
     if (P.directed && ra == kNoRank) v.log = true;   // row a still runs (directed rerun rule)
-    if (ra < rb) { v.lat = P.row_lat[ab]; v.rel = P.row_rel[ab]; }
-    else { v.lat = P.row_lat[ba]; v.rel = P.row_rel[ba]; }
+    const shd_pv& w = ra < rb ? vab : vba;
+    v.lat = w.lat; v.rel = w.rel;
     return v;
 }
 
@@ -421,7 +505,7 @@ __device__ void log_pending(const Params& P, HostCtx& c, int32_t a, int32_t b, u
 
 // worker_sendPacket (worker.c:260-321)
 __device__ void worker_send_packet(const Params& P, HostCtx& c, uint32_t dst, uint32_t pkt, int next_parity) {
-    const int32_t a = P.host_att[c.h], b = P.host_att[dst];
+    const int32_t a = c.att, b = P.host_att[dst];
     const PathVal pv = path_value(P, a, b);
     const double chance = next_double_dev(c.rng);
     const bool boot = bootstrapping(P, c);
@@ -453,17 +537,24 @@ __device__ void worker_send_packet(const Params& P, HostCtx& c, uint32_t dst, ui
 // _networkinterface_sendPackets (network_interface.c:519-579), FIFO qdisc
 __device__ void if_send_packets(const Params& P, HostCtx& c, int next_parity) {
     const bool boot = bootstrapping(P, c);
-    TxEnt* q = P.tq + (size_t)c.l * P.tq_cap;
     while (c.tx_rem >= SHD_MTU) {
         if (c.tq_count == 0) break;
-        const TxEnt p = q[c.tq_head];
+        TxEnt p;
+        if (c.tq_hv) {
+            p = c.tq_hint;
+            c.tq_hv = false;
+        } else {
+            p = P.tq[(size_t)c.l * P.tq_cap + c.tq_head];
+        }
         c.tq_head = (c.tq_head + 1 == P.tq_cap) ? 0 : c.tq_head + 1;
         c.tq_count--;
         if (p.dst == c.h) {
             trace(P, c, c.now, c.ev_seq, c.h, c.h, p.pkt, SHD_TR_LOCAL);
             schedule_self(P, c, SHD_EV_LOCAL, 1, p.pkt);
         } else {
+            PROF_T0(ts)
             worker_send_packet(P, c, p.dst, p.pkt, next_parity);
+            PROF_ADD(c, PR_SEND, ts)
         }
         if (!boot) {
             consume(c.tx_rem, P.pkt_len);
@@ -485,25 +576,47 @@ __device__ void random_free_port(HostCtx& c) {
     (void)random_port(c);   // linear-search fallback: draws once, always finds a port
 }
 
-// _phold_sendNewMessage (test_phold.c:218-230)
-__device__ void send_new_message(const Params& P, HostCtx& c, int next_parity) {
+// _phold_sendNewMessage (test_phold.c:218-230) up to the socket send: pick
+// the destination, bind, queue the datagram; false when nothing was queued
+__device__ bool enqueue_new_message(const Params& P, HostCtx& c) {
+    PROF_T0(tp)
     const double r = ((double)rand_r_dev(c.rng)) / kRandMax;
-    int32_t lo = 0, hi = P.H;
-    while (lo < hi) {
-        const int32_t mid = lo + ((hi - lo) >> 1);
-        if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
+    // first i with dest_cum[i] >= r.  guide[k] is a lower bound of it for any
+    // k <= r*H - 1 (DESIGN.md "Destination pick"); for even weights the answer
+    // is within the next few entries, else a binary search finishes the job.
+    int32_t k = (int32_t)(r * (double)P.H) - 1;
+    k = k < 0 ? 0 : (k > P.H - 1 ? P.H - 1 : k);
+    const DestGuide g = P.dest_guide[k];
+    int32_t lo = g.i;
+    {
+        const int32_t f = g.cum[0] >= r ? 0 : g.cum[1] >= r ? 1 : g.cum[2] >= r ? 2 : 3;
+        if (f < 3 || lo + 3 >= P.H) {
+            lo = f < 3 ? lo + f : P.H;
+        } else {
+            int32_t hi = P.H;
+            lo += 3;
+            while (lo < hi) {
+                const int32_t mid = lo + ((hi - lo) >> 1);
+                if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
+            }
+        }
     }
-    if (lo >= P.H) return;
+    PROF_ADD(c, PR_PICK, tp)
+    if (lo >= P.H) return false;
     const uint32_t dst = (uint32_t)lo;
     random_free_port(c);
     const uint32_t pkt = c.pkt_seq++;
-    if (c.tq_count >= P.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return; }
-    TxEnt* q = P.tq + (size_t)c.l * P.tq_cap;
-    uint32_t tail = c.tq_head + c.tq_count;
-    if (tail >= P.tq_cap) tail -= P.tq_cap;
-    q[tail] = TxEnt{dst, pkt};
+    if (c.tq_count >= P.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
+    if (c.tq_count == 0) {
+        c.tq_hint = TxEnt{dst, pkt};
+        c.tq_hv = true;
+    } else {
+        uint32_t tail = c.tq_head + c.tq_count;
+        if (tail >= P.tq_cap) tail -= P.tq_cap;
+        P.tq[(size_t)c.l * P.tq_cap + tail] = TxEnt{dst, pkt};
+    }
     c.tq_count++;
-    if_send_packets(P, c, next_parity);
+    return true;
 }
 
 // _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
@@ -518,23 +631,41 @@ __device__ void refill_cb(const Params& P, HostCtx& c, int next_parity) {
     refill_if_needed(P, c);
 }
 
+// One event.  The kind-specific part only sets up work; the expensive shared
+// steps (CoDel dequeue + receive, message generation, the send loop with its
+// path lookups) run once below for every kind that needs them, so the lanes
+// of a wave that execute different kinds in the same iteration converge on
+// them instead of running them one kind after the other.  Per kind, the
+// steps and their order are the reference's:
+//   REFILL    refill_cb: top up, receive, send, schedule next refill
+//   PACKET    router_enqueue, receive if the queue was empty
+//   NOTIFY    one new message per unread datagram, each sent right away
+//   APP_START `load` new messages
 __device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int next_parity) {
     c.c_events++;
     c.q_seq = e.seq;
     c.q_src = e.src;
     c.q_sub = 0;
+    uint32_t msgs = 0;
+    bool rx = false, tx = false, refill_chk = false;
     switch (e.kind) {
     case SHD_EV_HEARTBEAT:
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
         break;
     case SHD_EV_REFILL:
-        refill_cb(P, c, next_parity);
+        // _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
+        c.flags &= ~F_REFILL_PENDING;
+        c.rx_rem += c.rx_refill;
+        if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
+        c.tx_rem += c.tx_refill;
+        if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
+        rx = tx = refill_chk = true;
         break;
     case SHD_EV_REFILL_LO:
         break;
     case SHD_EV_APP_START:
         c.flags |= F_LISTENING;
-        for (uint32_t i = 0; i < P.load; i++) send_new_message(P, c, next_parity);
+        msgs = P.load;
         break;
     case SHD_EV_PACKET: {
         // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
@@ -542,29 +673,44 @@ __device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int nex
         trace(P, c, c.now, e.seq, c.h, e.src, e.pkt, SHD_TR_ARRIVE);
         const bool was_empty = c.cq_count == 0;
         if (c.cq_count >= P.cq_cap) { c.err |= SHD_ERR_CODELQ_OVERFLOW; break; }
-        CodelEnt* q = P.cq + (size_t)c.l * P.cq_cap;
-        uint32_t tail = c.cq_head + c.cq_count;
-        if (tail >= P.cq_cap) tail -= P.cq_cap;
-        q[tail] = CodelEnt{c.now, e.src, e.pkt};
+        const CodelEnt ent{c.now, e.src, e.pkt};
+        if (was_empty) {   // the head stays in registers; stored only if still queued at round end
+            c.cq_hint = ent;
+            c.cq_hv = true;
+        } else {
+            uint32_t tail = c.cq_head + c.cq_count;
+            if (tail >= P.cq_cap) tail -= P.cq_cap;
+            P.cq[(size_t)c.l * P.cq_cap + tail] = ent;
+        }
         c.cq_count++;
         c.cq_total += P.pkt_len;
-        if (was_empty) if_receive_packets(P, c);
+        rx = was_empty;
         break;
     }
     case SHD_EV_LOCAL:
         if_receive_packet(P, c, c.h, e.pkt);
         break;
-    case SHD_EV_NOTIFY: {
+    case SHD_EV_NOTIFY:
         c.flags &= ~F_NOTIFY_PENDING;
-        const uint32_t n = c.unread;
+        msgs = c.unread;
         c.unread = 0;
-        for (uint32_t i = 0; i < n; i++) send_new_message(P, c, next_parity);
         break;
-    }
     default:
-        c.err |= 0x80000000u;
+        c.err |= SHD_ERR_INTERNAL;
         break;
     }
+    if (rx) if_receive_packets(P, c);
+    while (msgs || tx) {
+        bool go = true;
+        if (msgs) {
+            go = enqueue_new_message(P, c);
+            msgs--;
+        } else {
+            tx = false;
+        }
+        if (go) if_send_packets(P, c, next_parity);
+    }
+    if (refill_chk) refill_if_needed(P, c);
 }
 
 __device__ void load_ctx(const Params& P, HostCtx& c, int32_t l) {
@@ -577,9 +723,49 @@ __device__ void load_ctx(const Params& P, HostCtx& c, int32_t l) {
     c.cq_dc = P.cq_dc[l]; c.cq_dcl = P.cq_dcl[l]; c.cq_head = P.cq_head[l]; c.cq_count = P.cq_count[l];
     c.tq_head = P.tq_head[l]; c.tq_count = P.tq_count[l];
     c.evq_n = P.evq_n[l];
+    c.top = P.evq[(size_t)l * P.evq_stride + 3];   // garbage when empty, never used then
+    c.tt0 = P.tm_time[0][l]; c.tt1 = P.tm_time[1][l]; c.tt2 = P.tm_time[2][l];
+    c.ts0 = P.tm_seq[0][l]; c.ts1 = P.tm_seq[1][l]; c.ts2 = P.tm_seq[2][l];
+    c.cq_hv = false; c.tq_hv = false;
+    c.att = P.host_att[c.h];
     c.c_events = P.c_events[l]; c.c_pkt = P.c_pkt[l]; c.c_sent = P.c_sent[l];
     c.c_idrop = P.c_idrop[l]; c.c_cdrop = P.c_cdrop[l]; c.c_recv = P.c_recv[l];
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
+}
+
+// earliest pending event of the host (timers and heap)
+__device__ __forceinline__ uint64_t host_next(const HostCtx& c) {
+    uint64_t t = c.evq_n ? c.top.time : kInf;
+    t = c.tt0 < t ? c.tt0 : t;
+    t = c.tt1 < t ? c.tt1 : t;
+    return c.tt2 < t ? c.tt2 : t;
+}
+
+// the host's next event in (time, src, seq) order if it is before `we`:
+// the earliest timer (src = the host) against the heap root
+__device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t we, shd_event& e) {
+    uint64_t bt = c.tt0, bs = c.ts0;
+    uint32_t kind = SHD_EV_HEARTBEAT;
+    int slot = 0;
+    if (c.tt1 < bt || (c.tt1 == bt && c.tt1 != kInf && c.ts1 < bs)) { bt = c.tt1; bs = c.ts1; kind = SHD_EV_REFILL; slot = 1; }
+    if (c.tt2 < bt || (c.tt2 == bt && c.tt2 != kInf && c.ts2 < bs)) { bt = c.tt2; bs = c.ts2; kind = SHD_EV_NOTIFY; slot = 2; }
+    bool timer = bt != kInf;
+    if (c.evq_n) {
+        const shd_event& t = c.top;
+        if (!timer || t.time < bt || (t.time == bt && (t.src < c.h || (t.src == c.h && t.seq < bs)))) timer = false;
+    }
+    if (timer) {
+        if (bt >= we) return false;
+        e.time = bt; e.seq = bs; e.src = c.h; e.dst = c.h; e.pkt = 0; e.kind = kind;
+        if (slot == 0) c.tt0 = kInf;
+        else if (slot == 1) c.tt1 = kInf;
+        else c.tt2 = kInf;
+        return true;
+    }
+    if (!c.evq_n || c.top.time >= we) return false;
+    e = c.top;
+    heap_pop(P, c);
+    return true;
 }
 
 __device__ void store_ctx(const Params& P, const HostCtx& c) {
@@ -591,6 +777,11 @@ __device__ void store_ctx(const Params& P, const HostCtx& c) {
     P.cq_dc[l] = c.cq_dc; P.cq_dcl[l] = c.cq_dcl; P.cq_head[l] = c.cq_head; P.cq_count[l] = c.cq_count;
     P.tq_head[l] = c.tq_head; P.tq_count[l] = c.tq_count;
     P.evq_n[l] = c.evq_n;
+    P.tm_time[0][l] = c.tt0; P.tm_time[1][l] = c.tt1; P.tm_time[2][l] = c.tt2;
+    P.tm_seq[0][l] = c.ts0; P.tm_seq[1][l] = c.ts1; P.tm_seq[2][l] = c.ts2;
+    if (c.cq_hv) P.cq[(size_t)l * P.cq_cap + c.cq_head] = c.cq_hint;
+    if (c.tq_hv) P.tq[(size_t)l * P.tq_cap + c.tq_head] = c.tq_hint;
+    P.hnext[l] = host_next(c);
     P.c_events[l] = c.c_events; P.c_pkt[l] = c.c_pkt; P.c_sent[l] = c.c_sent;
     P.c_idrop[l] = c.c_idrop; P.c_cdrop[l] = c.c_cdrop; P.c_recv[l] = c.c_recv;
 }
@@ -642,6 +833,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
         P.flags[l] = 0; P.unread[l] = 0;
         P.cq_total[l] = 0; P.cq_iexp[l] = 0; P.cq_ndrop[l] = 0; P.cq_dc[l] = 0; P.cq_dcl[l] = 0;
         P.cq_head[l] = 0; P.cq_count[l] = 0; P.tq_head[l] = 0; P.tq_count[l] = 0; P.evq_n[l] = 0;
+        for (int k = 0; k < 3; k++) { P.tm_time[k][l] = kInf; P.tm_seq[k][l] = 0; }
         P.c_events[l] = 0; P.c_pkt[l] = 0; P.c_sent[l] = 0; P.c_idrop[l] = 0; P.c_cdrop[l] = 0; P.c_recv[l] = 0;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
         HostCtx c;
@@ -653,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
         schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);        // loopback refill at +1 ms
         schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
         store_ctx(P, c);
-        if (c.evq_n) next = P.evq[(size_t)l * P.evq_cap].time;
+        next = host_next(c);
         err = c.err;
     }
     block_reduce_publish<kBlock>(P, next, 0, 0, err);
@@ -661,24 +853,30 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
 
 // one round [ws, we): merge inbox[parity], run events < we
 __device__ __forceinline__ void round_body(const Params& P, uint64_t we, int parity) {
-    const int32_t l = blockIdx.x * kBlock + threadIdx.x;
+    const int32_t l = (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
+#ifdef SHD_PROF
+    const unsigned long long w0 = wall_clock64();
+#endif
     uint64_t next = kInf, nev = 0, npkt = 0;
     uint32_t err = 0;
     // hosts with nothing due this round touch 2-3 words, not their whole state
     bool idle = false;
     if (l < P.nloc) {
         const uint32_t nin0 = P.inbox_n[parity][l];
-        const uint32_t nq0 = P.evq_n[l];
-        if (nin0 == 0) {
-            const uint64_t t0 = nq0 ? P.evq[(size_t)l * P.evq_cap].time : kInf;
-            if (t0 >= we) { idle = true; next = t0; }
-        }
+        const uint64_t t0 = P.hnext[l];
+        if (nin0 == 0 && t0 >= we) { idle = true; next = t0; }
     }
     if (l < P.nloc && !idle) {
+        PROF_T0(t_all)
         HostCtx c;
         load_ctx(P, c, l);
+#ifdef SHD_PROF
+        c.prof = ProfAcc{};
+#endif
+        PROF_ADD(c, PR_LOAD, t_all)
         const uint64_t ev0 = c.c_events, pk0 = c.c_pkt;
         // merge inbound events of the previous round
+        PROF_T0(t_m)
         const uint32_t nin = P.inbox_n[parity][l];
         if (nin) {
             const shd_event* in = P.inbox[parity] + (size_t)l * P.inbox_cap;
@@ -686,19 +884,60 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t we, int par
             for (uint32_t i = 0; i < n; i++) heap_push(P, c, in[i]);
             P.inbox_n[parity][l] = 0;
         }
-        const shd_event* hp = P.evq + (size_t)l * P.evq_cap;
-        while (c.evq_n > 0 && hp[0].time < we) {
-            const shd_event e = heap_pop(P, c);
+        PROF_ADD(c, PR_MERGE, t_m)
+        for (;;) {
+            PROF_T0(t_p)
+            shd_event e;
+            const bool more = take_next(P, c, we, e);
+            PROF_ADD(c, PR_POP, t_p)
+            if (!more) break;
             c.now = e.time;
+            PROF_T0(t_x)
             execute(P, c, e, parity ^ 1);
+#ifdef SHD_PROF
+            const int k = e.kind == SHD_EV_PACKET ? PR_EXEC_PKT : e.kind == SHD_EV_NOTIFY ? PR_EXEC_NOTIFY
+                        : e.kind == SHD_EV_REFILL ? PR_EXEC_REFILL : PR_EXEC_OTHER;
+            PROF_ADD(c, k, t_x)
+#endif
         }
-        next = c.evq_n ? hp[0].time : kInf;
+        next = host_next(c);
         if (c.min_emit < next) next = c.min_emit;
         nev = c.c_events - ev0;
         npkt = c.c_pkt - pk0;
         err = c.err;
+        PROF_T0(t_s)
         store_ctx(P, c);
+        PROF_ADD(c, PR_STORE, t_s)
+        PROF_ADD(c, PR_TOTAL, t_all)
+#ifdef SHD_PROF
+        c.prof.v[PR_NEV] = nev;
+        for (int i = 0; i < PR_N; i++) {
+            atomicAdd(&g_prof[i], c.prof.v[i]);
+            atomicMax(&g_prof[PR_N + i], c.prof.v[i]);
+        }
+        atomicAdd(&g_prof[2 * PR_N], 1ull);
+#endif
     }
+#ifdef SHD_PROF
+    {
+        uint64_t mx = nev;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        const unsigned long long w1 = wall_clock64();
+        if (threadIdx.x == 0) {
+            unsigned long long* g = g_wave[((uintptr_t)P.sum / sizeof(DevSummary)) & 127];
+            atomicMin(&g[0], w0);
+            atomicMax(&g[1], w1);
+            atomicMax(&g[2], w1 - w0);
+            atomicAdd(&g[3], w1 - w0);
+            atomicAdd(&g[4], 1ull);
+            atomicMax(&g[5], (unsigned long long)mx);
+            atomicAdd(&g[6], (unsigned long long)mx);
+        }
+    }
+#endif
     block_reduce_publish<kBlock>(P, next, nev, npkt, err);
 }
 
@@ -851,11 +1090,11 @@ __global__ void k_digest(Params P, shd_host_digest* __restrict__ out) {
 }
 
 // min over valid latencies of a table -> *out (u64 bits)
-__global__ void k_min_valid(const double* __restrict__ a, size_t n, unsigned long long* __restrict__ out) {
+__global__ void k_min_valid(const shd_pv* __restrict__ a, size_t n, unsigned long long* __restrict__ out) {
     __shared__ unsigned long long sm[256];
     unsigned long long m = kDistInf;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const double v = a[i];
+        const double v = a[i].lat;
         if (v >= 0.0) {
             const unsigned long long b = (unsigned long long)__double_as_longlong(v);
             if (b < m) m = b;
@@ -889,6 +1128,7 @@ struct shd_eng {
     uint64_t* d_bwu = nullptr;
     int32_t* d_host_att = nullptr;
     double* d_cum = nullptr;
+    DestGuide* d_guide = nullptr;
     int32_t* d_rank = nullptr;
     int32_t* d_self_rank = nullptr;
     DevSummary* d_sum = nullptr;
@@ -959,6 +1199,8 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     (void)hipEventCreate(&e->ev1);
     Params& P = e->P;
     P.H = H; P.h0 = host_begin; P.nloc = e->nloc;
+    P.hpw = 64;
+    if (const char* s = getenv("SHD_HPW")) P.hpw = std::min(64, std::max(1, atoi(s)));
     // default capacities: packets in flight TO a host are ~ load x (mean latency
     // of its inbound paths / global mean latency), up to ~10x load on the
     // bundled topology (5 - 2294 ms edges); one round's arrivals peak at the
@@ -979,7 +1221,11 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     EALLOC(P.c_recv, n);
     {
         int rc;
-        if ((rc = ealloc(e, &P.evq, n * P.evq_cap, false)) || (rc = ealloc(e, &P.evq_n, n)) ||
+        P.evq_stride = ((P.evq_cap + 3) & ~3u) + 4;   // heap root at +3: child groups 128-B aligned
+        if ((rc = ealloc(e, &P.evq, n * P.evq_stride, false)) || (rc = ealloc(e, &P.evq_n, n)) ||
+            (rc = ealloc(e, &P.tm_time[0], n)) || (rc = ealloc(e, &P.tm_time[1], n)) ||
+            (rc = ealloc(e, &P.tm_time[2], n)) || (rc = ealloc(e, &P.tm_seq[0], n)) ||
+            (rc = ealloc(e, &P.tm_seq[1], n)) || (rc = ealloc(e, &P.tm_seq[2], n)) || (rc = ealloc(e, &P.hnext, n)) ||
             (rc = ealloc(e, &P.inbox[0], n * P.inbox_cap, false)) ||
             (rc = ealloc(e, &P.inbox[1], n * P.inbox_cap, false)) || (rc = ealloc(e, &P.inbox_n[0], n)) ||
             (rc = ealloc(e, &P.inbox_n[1], n)) || (rc = ealloc(e, &P.cq, n * P.cq_cap, false)) ||
@@ -989,6 +1235,18 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         }
     }
     EALLOC(e->d_rng0, H); EALLOC(e->d_bwd, H); EALLOC(e->d_bwu, H); EALLOC(e->d_host_att, H); EALLOC(e->d_cum, H);
+    EALLOC(e->d_guide, H);
+    // destination guide table: guide[k] = first i with cum[i] >= k / H (H if none)
+    std::vector<DestGuide> guide(H);
+    for (int32_t k = 0, i = 0; k < H; k++) {
+        const double t = (double)k / (double)H;
+        while (i < H && !(m->dest_cum[i] >= t)) i++;
+        guide[k].i = i;
+        guide[k].pad = 0;
+        for (int j = 0; j < 3; j++) guide[k].cum[j] = i + j < H ? m->dest_cum[i + j] : 2.0;
+    }
+    for (int32_t i = 1; i < H; i++)
+        if (!(m->dest_cum[i] >= m->dest_cum[i - 1])) { shd_eng_destroy(e); return SHD_EINVAL; }
     EALLOC(e->d_rank, pc->T); EALLOC(e->d_self_rank, pc->T);
     EALLOC(e->d_sum, 1);
     if (hipHostMalloc((void**)&e->h_sum, sizeof(DevSummary)) != hipSuccess) { shd_eng_destroy(e); return SHD_ENOMEM; }
@@ -1019,7 +1277,9 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         hipMemcpyAsync(e->d_bwd, m->bw_down_kibps, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(e->d_bwu, m->bw_up_kibps, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(e->d_host_att, host_att.data(), 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(e->d_cum, m->dest_cum, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess) {
+        hipMemcpyAsync(e->d_cum, m->dest_cum, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_guide, guide.data(), sizeof(DestGuide) * (size_t)H, hipMemcpyHostToDevice, s) !=
+            hipSuccess) {
         shd_eng_destroy(e);
         return SHD_ENODEV;
     }
@@ -1033,11 +1293,10 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     }
     P.host_att = e->d_host_att;
     P.dest_cum = e->d_cum;
+    P.dest_guide = e->d_guide;
     P.T = pc->T;
     P.complete = pc->complete; P.prefer_direct = pc->prefer_direct; P.directed = pc->directed;
-    P.row_lat = pc->d_row_lat; P.row_rel = pc->d_row_rel;
-    P.dir_lat = pc->d_dir_lat; P.dir_rel = pc->d_dir_rel;
-    P.self_lat = pc->d_self_lat; P.self_rel = pc->d_self_rel;
+    P.row = pc->d_row; P.dir = pc->d_dir; P.self = pc->d_self;
     P.adj = pc->d_adj;
     P.rank = e->d_rank; P.self_rank = e->d_self_rank;
     P.sum = e->d_sum;
@@ -1051,12 +1310,12 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         const size_t TT = (size_t)pc->T * pc->T;
         const int blocks = (int)std::min<size_t>((TT + 255) / 256, 4096);
         if (pc->rows_mode) {
-            hipLaunchKernelGGL(k_min_valid, dim3(blocks), dim3(256), 0, s, pc->d_row_lat, TT, d_min);
-            hipLaunchKernelGGL(k_min_valid, dim3((pc->T + 255) / 256), dim3(256), 0, s, pc->d_self_lat,
+            hipLaunchKernelGGL(k_min_valid, dim3(blocks), dim3(256), 0, s, pc->d_row, TT, d_min);
+            hipLaunchKernelGGL(k_min_valid, dim3((pc->T + 255) / 256), dim3(256), 0, s, pc->d_self,
                                (size_t)pc->T, d_min);
         }
         if (pc->complete || pc->prefer_direct)
-            hipLaunchKernelGGL(k_min_valid, dim3(blocks), dim3(256), 0, s, pc->d_dir_lat, TT, d_min);
+            hipLaunchKernelGGL(k_min_valid, dim3(blocks), dim3(256), 0, s, pc->d_dir, TT, d_min);
         unsigned long long bits = 0;
         (void)hipMemcpyAsync(&bits, d_min, 8, hipMemcpyDeviceToHost, s);
         if (hipStreamSynchronize(s) != hipSuccess) { (void)hipFree(d_min); shd_eng_destroy(e); return SHD_ENODEV; }
@@ -1127,7 +1386,7 @@ extern "C" int shd_eng_round_kernel(shd_eng* e, uint64_t ws, uint64_t we, shd_ro
     SHD_HIP(hipSetDevice(e->device));
     int rc = reset_summary(e);
     if (rc) return rc;
-    const int grid = (e->nloc + kBlock - 1) / kBlock;
+    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     e->P.sum = e->d_sum;
     SHD_HIP(hipEventRecord(e->ev0, e->stream));
     hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, e->P, we, e->parity);
@@ -1251,7 +1510,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     uint64_t next = e->h_sum->next_time;
     e->kernel_ms_total = 0;
     const uint64_t pend0 = e->pending_resolved;
-    const int grid = (e->nloc + kBlock - 1) / kBlock;
+    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     constexpr int B = shd_eng::kBatch, R = shd_eng::kRing;
     while (next < stop && rc == SHD_OK) {
         // slot 0 carries the window start; rounds use slots 1..B
@@ -1331,6 +1590,30 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     if (st) *st = s;
     return rc;
 }
+
+#ifdef SHD_PROF
+// profiling build only: read (and clear) the per-phase clock totals
+extern "C" int shd_debug_waves(uint64_t* out) {   // 128 x 8, then reset
+    SHD_HIP(hipDeviceSynchronize());
+    SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave), sizeof(g_wave)));
+    static unsigned long long z[128][8];
+    for (int i = 0; i < 128; i++) {
+        for (int k = 0; k < 8; k++) z[i][k] = 0;
+        z[i][0] = ~0ull;
+    }
+    SHD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_wave), z, sizeof(z)));
+    return SHD_OK;
+}
+
+extern "C" int shd_debug_prof(uint64_t* out, int n) {
+    if (n < 2 * PR_N + 2) return SHD_EINVAL;
+    SHD_HIP(hipDeviceSynchronize());
+    SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * (2 * PR_N + 2)));
+    unsigned long long z[2 * PR_N + 2] = {};
+    SHD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+    return SHD_OK;
+}
+#endif
 
 extern "C" int shd_eng_run(shd_eng* e, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;

@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <vector>
 #include <unordered_map>
 
 #include "shd_device.h"
@@ -75,7 +76,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              const double* __restrict__ rin_w, const double* __restrict__ w_e,
                              const double* __restrict__ eloss, const double* __restrict__ vloss,
                              const int32_t* __restrict__ attached, const int32_t* __restrict__ self_eid,
-                             double* __restrict__ out_lat, double* __restrict__ out_rel,
+                             shd_pv* __restrict__ out,
                              int64_t* __restrict__ stats, uint64_t* dist, int32_t* parent,
                              uint16_t* upd, int* flags /* LDS int[4] */) {
     const int tid = threadIdx.x;
@@ -197,8 +198,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             if (d2u(lat) != dist[t]) my_mismatch++;
             if (lat == 0) lat = 1;   // topology.c:1848-1852
         }
-        out_lat[(size_t)row * T + j] = lat;
-        out_rel[(size_t)row * T + j] = rel;
+        out[(size_t)row * T + j] = shd_pv{lat, rel};
     }
     if (my_maxhops) atomicMax((unsigned long long*)&stats[1], (unsigned long long)my_maxhops);
     if (my_unroutable) atomicAdd((unsigned long long*)&stats[3], (unsigned long long)my_unroutable);
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
     const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
-    const int32_t* __restrict__ self_eid, double* __restrict__ out_lat, double* __restrict__ out_rel,
+    const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint64_t* dist = (uint64_t*)smem;
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
     for (int32_t row = blockIdx.x; row < T; row += gridDim.x)
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
-                            rin_w, w_e, eloss, vloss, attached, self_eid, out_lat, out_rel, stats, dist,
+                            rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
 }
 
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
     const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
-    const int32_t* __restrict__ self_eid, double* __restrict__ out_lat, double* __restrict__ out_rel,
+    const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block) {
     __shared__ int flags[4];
     char* base = scratch + per_block * blockIdx.x;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     uint16_t* upd = (uint16_t*)(base + (size_t)12 * V);
     for (int32_t row = blockIdx.x; row < T; row += gridDim.x)
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
-                            rin_w, w_e, eloss, vloss, attached, self_eid, out_lat, out_rel, stats, dist,
+                            rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
 }
 
@@ -263,8 +263,8 @@ __device__ __forceinline__ int32_t dev_get_eid(const int32_t* nbr_off, const int
 __global__ void k_direct(int32_t T, const int32_t* __restrict__ attached, const int32_t* __restrict__ nbr_off,
                          const int32_t* __restrict__ nbr_v, const int32_t* __restrict__ nbr_eid,
                          const double* __restrict__ w_e, const double* __restrict__ eloss,
-                         const double* __restrict__ vloss, double* __restrict__ lat_out,
-                         double* __restrict__ rel_out, uint8_t* __restrict__ adj_out) {
+                         const double* __restrict__ vloss, shd_pv* __restrict__ out,
+                         uint8_t* __restrict__ adj_out) {
     const size_t n = (size_t)T * T;
     for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < n;
          idx += (size_t)gridDim.x * blockDim.x) {
@@ -280,8 +280,7 @@ __global__ void k_direct(int32_t T, const int32_t* __restrict__ attached, const 
             tr *= ((double)1.0f - eloss[e]);
             lat = tl; rel = tr;
         }
-        lat_out[idx] = lat;
-        rel_out[idx] = rel;
+        out[idx] = shd_pv{lat, rel};
         adj_out[idx] = e >= 0;
     }
 }
@@ -291,8 +290,7 @@ __global__ void k_direct(int32_t T, const int32_t* __restrict__ attached, const 
 // minimum over the igraph_incident(OUT) list; latency 2*min, reliability r^2
 __global__ void k_self(int32_t T, const int32_t* __restrict__ attached, const int32_t* __restrict__ inc_off,
                        const int32_t* __restrict__ inc_eid, const double* __restrict__ w_e,
-                       const double* __restrict__ eloss, double* __restrict__ lat_out,
-                       double* __restrict__ rel_out) {
+                       const double* __restrict__ eloss, shd_pv* __restrict__ out) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= T) return;
     const int32_t v = attached[i];
@@ -306,17 +304,16 @@ __global__ void k_self(int32_t T, const int32_t* __restrict__ attached, const in
             relMin = (double)1.0f - eloss[e];
         }
     }
-    if (k1 == k0) { lat_out[i] = -1.0; rel_out[i] = -1.0; return; }
-    lat_out[i] = (double)2.0f * minLatency;
-    rel_out[i] = relMin * relMin;
+    if (k1 == k0) { out[i] = shd_pv{-1.0, -1.0}; return; }
+    out[i] = shd_pv{(double)2.0f * minLatency, relMin * relMin};
 }
 
 // min over valid (>= 0, non-NaN) latencies of a table -> stats[5] as u64 bits
-__global__ void k_min_latency(const double* __restrict__ a, size_t n, int64_t* __restrict__ stats) {
+__global__ void k_min_latency(const shd_pv* __restrict__ a, size_t n, int64_t* __restrict__ stats) {
     __shared__ unsigned long long smin[256];
     unsigned long long m = kDistInf;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const double v = a[i];
+        const double v = a[i].lat;
         if (v >= 0.0) { unsigned long long b = (unsigned long long)__double_as_longlong(v); if (b < m) m = b; }
     }
     smin[threadIdx.x] = m;
@@ -339,8 +336,8 @@ static int dalloc_copy(T** d, const T* h, size_t n) {
 static void pc_free_device(shd_pc* pc) {
     void* ptrs[] = {pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                     pc->d_rin_w, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
-                    pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row_lat,
-                    pc->d_row_rel, pc->d_dir_lat, pc->d_dir_rel, pc->d_self_lat, pc->d_self_rel, pc->d_adj,
+                    pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
+                    pc->d_dir, pc->d_self, pc->d_adj,
                     pc->d_scratch, pc->d_stats};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -410,15 +407,14 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
     }
     if (pc->has_vloss && (rc = dalloc_copy(&pc->d_vloss, pc->h_vloss, V))) { shd_pc_destroy(pc); return rc; }
     const size_t TT = (size_t)T * T;
-    if (hipMalloc((void**)&pc->d_dir_lat, 8 * TT) != hipSuccess || hipMalloc((void**)&pc->d_dir_rel, 8 * TT) != hipSuccess ||
-        hipMalloc((void**)&pc->d_adj, TT) != hipSuccess || hipMalloc((void**)&pc->d_self_lat, 8 * T) != hipSuccess ||
-        hipMalloc((void**)&pc->d_self_rel, 8 * T) != hipSuccess || hipMalloc((void**)&pc->d_stats, 8 * 8) != hipSuccess) {
+    if (hipMalloc((void**)&pc->d_dir, sizeof(shd_pv) * TT) != hipSuccess ||
+        hipMalloc((void**)&pc->d_adj, TT) != hipSuccess || hipMalloc((void**)&pc->d_self, sizeof(shd_pv) * T) != hipSuccess ||
+        hipMalloc((void**)&pc->d_stats, 8 * 8) != hipSuccess) {
         shd_pc_destroy(pc);
         return SHD_ENOMEM;
     }
     if (pc->rows_mode) {
-        if (hipMalloc((void**)&pc->d_row_lat, 8 * TT) != hipSuccess ||
-            hipMalloc((void**)&pc->d_row_rel, 8 * TT) != hipSuccess) {
+        if (hipMalloc((void**)&pc->d_row, sizeof(shd_pv) * TT) != hipSuccess) {
             shd_pc_destroy(pc);
             return SHD_ENOMEM;
         }
@@ -451,9 +447,9 @@ extern "C" int shd_pc_build(shd_pc* pc) {
         const size_t TT = (size_t)T * T;
         int blocks = (int)std::min<size_t>((TT + 255) / 256, 8192);
         hipLaunchKernelGGL(k_direct, dim3(blocks), dim3(256), 0, s, T, pc->d_attached, pc->d_nbr_off, pc->d_nbr_v,
-                           pc->d_nbr_eid, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_dir_lat, pc->d_dir_rel, pc->d_adj);
+                           pc->d_nbr_eid, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_dir, pc->d_adj);
         hipLaunchKernelGGL(k_self, dim3((T + 255) / 256), dim3(256), 0, s, T, pc->d_attached, pc->d_inc_off,
-                           pc->d_inc_eid, pc->d_w, pc->d_eloss, pc->d_self_lat, pc->d_self_rel);
+                           pc->d_inc_eid, pc->d_w, pc->d_eloss, pc->d_self);
         SHD_HIP(hipGetLastError());
     }
     SHD_HIP(hipEventRecord(ev[1], s));
@@ -471,7 +467,7 @@ extern "C" int shd_pc_build(shd_pc* pc) {
                 hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
-                                   pc->d_row_lat, pc->d_row_rel, pc->d_stats);
+                                   pc->d_row, pc->d_stats);
             } else {
                 int grid = std::min(T, ncu);
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<1024>,
@@ -479,7 +475,7 @@ extern "C" int shd_pc_build(shd_pc* pc) {
                 hipLaunchKernelGGL(k_sssp_rows_lds<1024>, dim3(grid), dim3(1024), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
-                                   pc->d_row_lat, pc->d_row_rel, pc->d_stats);
+                                   pc->d_row, pc->d_stats);
             }
         } else {
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -491,8 +487,8 @@ extern "C" int shd_pc_build(shd_pc* pc) {
             }
             hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
-                               pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row_lat,
-                               pc->d_row_rel, pc->d_stats, (char*)pc->d_scratch, per_block);
+                               pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
+                               pc->d_stats, (char*)pc->d_scratch, per_block);
         }
         SHD_HIP(hipGetLastError());
     }
@@ -500,7 +496,7 @@ extern "C" int shd_pc_build(shd_pc* pc) {
     {
         const size_t TT = (size_t)T * T;
         int blocks = (int)std::min<size_t>((TT + 255) / 256, 4096);
-        const double* tab = pc->rows_mode ? pc->d_row_lat : pc->d_dir_lat;
+        const shd_pv* tab = pc->rows_mode ? pc->d_row : pc->d_dir;
         hipLaunchKernelGGL(k_min_latency, dim3(blocks), dim3(256), 0, s, tab, TT, pc->d_stats);
         SHD_HIP(hipGetLastError());
     }
@@ -540,31 +536,41 @@ extern "C" int shd_pc_get_info(const shd_pc* pc, shd_pc_info* out) {
     return SHD_OK;
 }
 
-static int copy_table(shd_pc* pc, const double* dl, const double* dr, int32_t row0, int32_t nrows, double* lat,
-                      double* rel) {
+// device (lat, rel) pairs -> the caller's two arrays, in bounded chunks
+static int split_copy(const shd_pv* src, size_t n, double* lat, double* rel) {
+    constexpr size_t kChunk = 1u << 20;
+    std::vector<shd_pv> buf(std::min(n, kChunk));
+    for (size_t i = 0; i < n; i += kChunk) {
+        const size_t m = std::min(kChunk, n - i);
+        SHD_HIP(hipMemcpy(buf.data(), src + i, sizeof(shd_pv) * m, hipMemcpyDeviceToHost));
+        for (size_t k = 0; k < m; k++) {
+            if (lat) lat[i + k] = buf[k].lat;
+            if (rel) rel[i + k] = buf[k].rel;
+        }
+    }
+    return SHD_OK;
+}
+
+static int copy_table(shd_pc* pc, const shd_pv* d, int32_t row0, int32_t nrows, double* lat, double* rel) {
     if (!pc || !pc->built || row0 < 0 || nrows < 0 || row0 + nrows > pc->T) return SHD_EINVAL;
-    if (!dl) return SHD_EINVAL;
+    if (!d) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(pc->device));
     const size_t off = (size_t)row0 * pc->T, n = (size_t)nrows * pc->T;
-    if (lat) SHD_HIP(hipMemcpy(lat, dl + off, 8 * n, hipMemcpyDeviceToHost));
-    if (rel) SHD_HIP(hipMemcpy(rel, dr + off, 8 * n, hipMemcpyDeviceToHost));
-    return SHD_OK;
+    return split_copy(d + off, n, lat, rel);
 }
 
 extern "C" int shd_pc_copy_rows(shd_pc* pc, int32_t row0, int32_t nrows, double* lat, double* rel) {
     if (!pc) return SHD_EINVAL;
-    return copy_table(pc, pc->d_row_lat, pc->d_row_rel, row0, nrows, lat, rel);
+    return copy_table(pc, pc->d_row, row0, nrows, lat, rel);
 }
 extern "C" int shd_pc_copy_direct(shd_pc* pc, int32_t row0, int32_t nrows, double* lat, double* rel) {
     if (!pc) return SHD_EINVAL;
-    return copy_table(pc, pc->d_dir_lat, pc->d_dir_rel, row0, nrows, lat, rel);
+    return copy_table(pc, pc->d_dir, row0, nrows, lat, rel);
 }
 extern "C" int shd_pc_copy_self(shd_pc* pc, double* lat, double* rel) {
     if (!pc || !pc->built) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(pc->device));
-    if (lat) SHD_HIP(hipMemcpy(lat, pc->d_self_lat, 8 * (size_t)pc->T, hipMemcpyDeviceToHost));
-    if (rel) SHD_HIP(hipMemcpy(rel, pc->d_self_rel, 8 * (size_t)pc->T, hipMemcpyDeviceToHost));
-    return SHD_OK;
+    return split_copy(pc->d_self, (size_t)pc->T, lat, rel);
 }
 
 // ------------------------------------------------------------------ lazy lookup (host adapter)
@@ -572,9 +578,11 @@ extern "C" int shd_pc_copy_self(shd_pc* pc, double* lat, double* rel) {
 // (topology.c:1307-1336), and a row for source s runs on the first query
 // (s,d) that misses in both orientations (1987-1990, 2030).  Direct paths
 // are stored by the first query of an adjacent pair (2019-2021).
-static int fetch2(shd_pc* pc, const double* dl, const double* dr, size_t idx, double* lat, double* rel) {
-    SHD_HIP(hipMemcpy(lat, dl + idx, 8, hipMemcpyDeviceToHost));
-    SHD_HIP(hipMemcpy(rel, dr + idx, 8, hipMemcpyDeviceToHost));
+static int fetch2(shd_pc* pc, const shd_pv* d, size_t idx, double* lat, double* rel) {
+    shd_pv v;
+    SHD_HIP(hipMemcpy(&v, d + idx, sizeof(v), hipMemcpyDeviceToHost));
+    *lat = v.lat;
+    *rel = v.rel;
     return SHD_OK;
 }
 
@@ -587,7 +595,7 @@ static int run_row_for_min(shd_pc* pc, int32_t a) {
     const int32_t T = pc->T;
     double* buf = (double*)malloc(8 * (size_t)T);
     if (!buf) return SHD_ENOMEM;
-    if (hipMemcpy(buf, pc->d_row_lat + (size_t)a * T, 8 * (size_t)T, hipMemcpyDeviceToHost) != hipSuccess) {
+    if (split_copy(pc->d_row + (size_t)a * T, (size_t)T, buf, nullptr) != SHD_OK) {
         free(buf);
         return SHD_ENODEV;
     }
@@ -618,7 +626,7 @@ extern "C" int shd_pc_lookup(shd_pc* pc, int32_t sv, int32_t dv, double* lat, do
     if (pc->prefer_direct && !pc->complete)
         SHD_HIP(hipMemcpy(&adj, pc->d_adj + (size_t)a * T + b, 1, hipMemcpyDeviceToHost));
     if (pc->complete || adj) {
-        int rc = fetch2(pc, pc->d_dir_lat, pc->d_dir_rel, (size_t)a * T + b, lat, rel);
+        int rc = fetch2(pc, pc->d_dir, (size_t)a * T + b, lat, rel);
         if (rc) return rc;
         if (isnan(*lat)) { *lat = -1; *rel = -1; return SHD_OK; }
         note_min(pc, *lat);
@@ -630,14 +638,14 @@ extern "C" int shd_pc_lookup(shd_pc* pc, int32_t sv, int32_t dv, double* lat, do
         int32_t ra = pc->h_rank[a], rs = pc->h_self_rank[a];
         if (ra == kNoRank && rs == kNoRank) {
             pc->h_self_rank[a] = rs = pc->next_rank++;
-            int rc = fetch2(pc, pc->d_self_lat, pc->d_self_rel, (size_t)a, lat, rel);
+            int rc = fetch2(pc, pc->d_self, (size_t)a, lat, rel);
             if (rc) return rc;
             if (*lat < 0) return SHD_OK;
             note_min(pc, *lat);
             return SHD_OK;
         }
-        if (rs < ra) return fetch2(pc, pc->d_self_lat, pc->d_self_rel, (size_t)a, lat, rel);
-        return fetch2(pc, pc->d_row_lat, pc->d_row_rel, (size_t)a * T + a, lat, rel);
+        if (rs < ra) return fetch2(pc, pc->d_self, (size_t)a, lat, rel);
+        return fetch2(pc, pc->d_row, (size_t)a * T + a, lat, rel);
     }
     int32_t ra = pc->h_rank[a], rb = pc->h_rank[b];
     // undirected: a miss needs both orientations missing (1987-1990);
@@ -659,8 +667,8 @@ extern "C" int shd_pc_lookup(shd_pc* pc, int32_t sv, int32_t dv, double* lat, do
     // value from whichever endpoint's row ran first; on directed graphs this can
     // be the reverse path (topology.c:2034-2037)
     if (ra != kNoRank && (rb == kNoRank || ra < rb))
-        return fetch2(pc, pc->d_row_lat, pc->d_row_rel, (size_t)a * T + b, lat, rel);
-    return fetch2(pc, pc->d_row_lat, pc->d_row_rel, (size_t)b * T + a, lat, rel);
+        return fetch2(pc, pc->d_row, (size_t)a * T + b, lat, rel);
+    return fetch2(pc, pc->d_row, (size_t)b * T + a, lat, rel);
 }
 
 extern "C" int shd_pc_count_packet(shd_pc* pc, int32_t sv, int32_t dv) {

@@ -22,6 +22,11 @@ static constexpr uint64_t kDistInf = 0x7FF0000000000000ull;   // +inf as u64
 static constexpr int32_t kNoRank = 0x7FFFFFFF;
 
 // Path-cache device state (owned by shd_pc, consumed by the engine).
+// path value as stored: latency (ms) and reliability, interleaved
+struct shd_pv {
+    double lat, rel;
+};
+
 struct shd_pc {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -46,10 +51,11 @@ struct shd_pc {
     int32_t *d_nbr_off = nullptr, *d_nbr_v = nullptr, *d_nbr_eid = nullptr;
     double *d_w = nullptr, *d_eloss = nullptr, *d_vloss = nullptr;
     int32_t *d_attached = nullptr, *d_self_eid = nullptr;
-    // device tables [T][T] and [T]
-    double *d_row_lat = nullptr, *d_row_rel = nullptr;
-    double *d_dir_lat = nullptr, *d_dir_rel = nullptr;
-    double *d_self_lat = nullptr, *d_self_rel = nullptr;
+    // device tables [T][T] and [T] of (latency, reliability) pairs: one 16-B
+    // load per lookup in the event loop
+    shd_pv* d_row = nullptr;
+    shd_pv* d_dir = nullptr;
+    shd_pv* d_self = nullptr;
     uint8_t* d_adj = nullptr;           // [T][T] 1 = adjacent (direct path exists)
     void* d_scratch = nullptr;          // global-memory SSSP scratch (large V)
     size_t scratch_bytes = 0;

@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libshdgpu.so")
+LIB_PATH = os.environ.get("SHDGPU_LIB") or os.path.join(HERE, "libshdgpu.so")   # override: profiling build
 
 SHD_MS = 1_000_000
 SHD_SEC = 1_000_000_000
