@@ -50,6 +50,11 @@ def parse():
                     help="steady-state simulated seconds the oracle is timed over")
     ap.add_argument("--cpu-sample-hosts", type=int, default=2000,
                     help="hosts (= vertices) of the CPU sample instance of the same workload")
+    ap.add_argument("--exchange", choices=["rccl", "torch"], default="rccl",
+                    help="N > 1: rccl = shd_xgroup (device-driven rounds, one fixed-size RCCL all-to-all "
+                         "per round); torch = driver.DistCluster (host-driven, torch.distributed)")
+    ap.add_argument("--group", action="store_true",
+                    help="run the shd_xgroup path even at N = 1 (a one-rank RCCL group)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -103,7 +108,17 @@ def main():
     log(rank, f"setup {time.perf_counter() - t_setup:.1f}s  V={V} E={g.n_edges} H={H} W={eng.window}ns "
               f"apsp={min(builds):.1f}ms iters={info.sssp_iterations_max} hops={info.max_hops}")
 
-    if world > 1:
+    use_group = args.group or (world > 1 and args.exchange == "rccl")
+    if use_group:
+        from sim import XGroup
+        uid = torch.zeros(S.SHD_XID_BYTES, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(XGroup.unique_id()), dtype=torch.uint8))
+        if world > 1:
+            dist.broadcast(uid, 0)
+        grp = XGroup.rccl(eng, bytes(uid.cpu().numpy().tobytes()), max(world, 1), rank)
+        run = lambda t: grp.run_until(t)  # noqa: E731
+    elif world > 1:
         cl = DistCluster(eng, pb, rank, world, dist, torch)
         cl.boot()
         run = lambda t: cl.run_until(t)  # noqa: E731
@@ -128,7 +143,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if world > 1 and not use_group:
         pkt, evs, rounds, kms = st.pkt_events, st.events, st.rounds, st.kernel_ms
     else:
         pkt, evs, rounds, kms = st.n_pkt_events, st.n_events, st.n_rounds, st.device_ms_round_kernel
@@ -174,7 +189,9 @@ def main():
                        "edge_loss": "U[0,%g]" % args.edge_loss_max,
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
                        "payload_bytes": args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
-                       "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1)},
+                       "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1),
+                       "exchange": ("shd_xgroup/RCCL all-to-all" if use_group else
+                                    "torch.distributed" if world > 1 else "none (single engine)")},
             "all_events_per_s": round(ev_all / elapsed, 1),
             "rounds": int(rounds),
             "apsp": {"rows": int(info.rows_computed), "vertices": V, "build_ms": round(min(builds), 3),
@@ -184,6 +201,8 @@ def main():
             "cpu_baseline": cpu_baseline,
         }
         print(json.dumps(out), flush=True)
+    if use_group:
+        grp.close()
     eng.close()
     pc.close()
     if world > 1:

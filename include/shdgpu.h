@@ -371,6 +371,32 @@ int shd_eng_stream(shd_eng* e, void** hip_stream);
 int shd_eng_last_kernel_ms(shd_eng* e, double* ms);
 void shd_eng_destroy(shd_eng* e);
 
+/* ---- engine groups (DESIGN.md "Multi-GPU") ----
+ * One engine per rank; rank p owns hosts [(H*p)/N, (H*(p+1))/N).  Every round
+ * is one fixed-size all-to-all whose per-peer blocks carry a header (the
+ * sender's next event time and flags) and the events for that peer, so the
+ * next window start (the min over the headers), the halt decision and the
+ * delivery need no host round trip: the round loop of slave.c:413-466 /
+ * master.c:148-192 across GPUs.  Rounds run in device-driven batches; a
+ * round with first-touch queries, a block overflow or an error anywhere in
+ * the group halts the batch on every rank alike, the host resolves it and
+ * the batch resumes.  Transports: RCCL (one engine per process; the
+ * multi-GPU path) or local (several engines driven by one host thread,
+ * device-to-device copies). */
+#define SHD_XID_BYTES 128
+typedef struct shd_xgroup shd_xgroup;
+/* RCCL unique id: rank 0 makes it, every rank passes the same bytes */
+int shd_xgroup_unique_id(uint8_t id[SHD_XID_BYTES]);
+/* block_events: events per peer block per round (0 = default) */
+int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
+                           uint32_t block_events, shd_xgroup** out);
+int shd_xgroup_create_local(shd_eng* const* engines, int n, uint32_t block_events, shd_xgroup** out);
+/* boots the engines if needed, then rounds while the group's next event time
+ * is below t_stop; stats: this process's engines, this call */
+int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stats* out);
+int shd_xgroup_next_time(shd_xgroup* g, uint64_t* next_time);
+void shd_xgroup_destroy(shd_xgroup* g);
+
 /* library */
 const char* shd_version(void);
 int shd_device_count(int* n);

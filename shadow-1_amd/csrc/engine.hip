@@ -27,6 +27,7 @@
 // the rare sends whose pair was unranked at round start are logged, resolved
 // in serial order on the host after the round, and finalised by k_finalize.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <math.h>
 #include <stdio.h>
@@ -69,8 +70,41 @@ struct DevSummary {
     unsigned long long n_pending;
     unsigned long long n_remote;
     unsigned int error;
+    unsigned int flags;            // exchange mode: 1 = this round halted the batch, 2 = skipped
+    unsigned long long ws;         // the round's window start (device-driven rounds)
+    unsigned long long t_first;    // device wall clock: first block start, last block end
+    unsigned long long t_last;
+    unsigned int done;             // blocks finished (last-block ticket)
     unsigned int pad;
 };
+
+__device__ __forceinline__ DevSummary fresh_summary() {
+    DevSummary z{};
+    z.next_time = ~0ull;
+    z.t_first = ~0ull;
+    return z;
+}
+
+// per-batch inputs of the device-driven rounds (device memory, so that a
+// captured batch graph is replayed unchanged): round i of the batch has
+// parity (round_base + i) & 1
+struct DevCtl {
+    unsigned long long stop;
+    unsigned long long round_base;
+};
+
+// Exchange mode (shd_xgroup): the per-peer blocks of the fixed-size
+// all-to-all buffers start with one header slot, then `xcap` events.
+struct XHeader {
+    unsigned long long next_time;  // sender's earliest pending event (its hosts + its sends in flight)
+    uint32_t count;                // events in this block (<= xcap)
+    uint32_t flags;                // XF_* of the sender's round
+    unsigned long long n_pending;  // sender's first-touch log of the round
+    uint32_t error;
+    uint32_t pad;
+};
+static_assert(sizeof(XHeader) == sizeof(shd_event), "header fills one event slot");
+constexpr uint32_t XF_PENDING = 1u, XF_OVERFLOW = 2u, XF_ERROR = 4u;
 
 // destination-pick guide: for bucket k, i = the first index with
 // dest_cum[i] >= k / H, and the next three cumulative weights inline, so an
@@ -151,7 +185,21 @@ struct Params {
     DevSummary* sum;               // this round's summary
     int32_t* next_rank;            // row-rank counter (device is the source of truth)
     uint32_t* halt;                // set when a round needs host-side resolution
+    // exchange mode (null xsend: remote events go to `remote`)
+    shd_event* xsend;              // [xworld][xcap + 1]
+    uint32_t* xcount;              // [xworld] events queued per peer this round
+    uint32_t xcap;
+    int32_t xworld;                // engines of the group; host partition (H*p)/xworld
 };
+
+// engine of the group that owns host h: the partition is b[p] = (H*p)/N
+__device__ __forceinline__ int32_t owner_of(const Params& P, uint32_t h) {
+    const uint64_t H = (uint64_t)P.H, N = (uint64_t)P.xworld;
+    int64_t p = (int64_t)(((uint64_t)h * N) / H);
+    while (p + 1 < (int64_t)N && (H * (uint64_t)(p + 1)) / N <= h) p++;
+    while (p > 0 && (H * (uint64_t)p) / N > h) p--;
+    return (int32_t)p;
+}
 
 // --------------------------------------------------------------- profiling
 // Built with -DSHD_PROF (make prof -> libshdgpu_prof.so, scripts/prof_round.py):
@@ -333,6 +381,16 @@ __device__ void emit_remote(const Params& P, HostCtx& c, const shd_event& e, int
         if (slot >= P.inbox_cap) { c.err |= SHD_ERR_INBOX_OVERFLOW; return; }
         P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
     } else {
+        if (P.xsend) {   // exchange mode: straight into the peer's all-to-all block
+            const int32_t peer = owner_of(P, e.dst);
+            const uint32_t s = atomicAdd(&P.xcount[peer], 1u);
+            if (s < P.xcap) {
+                P.xsend[(size_t)peer * (P.xcap + 1) + 1 + s] = e;
+                return;
+            }
+            // block full: spill to the remote buffer (the header says so, the
+            // group halts after the exchange and the host delivers the spill)
+        }
         unsigned long long slot = atomicAdd(&P.sum->n_remote, 1ull);
         if (slot >= P.remote_cap) { c.err |= SHD_ERR_REMOTE_OVERFLOW; return; }
         P.remote[slot] = e;
@@ -945,29 +1003,6 @@ __global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int par
     round_body(P, we, parity);
 }
 
-// device-driven round: the window start is the previous round's next event
-// time (read on the device), so rounds are enqueued back to back with no host
-// round trip; a round past `stop` only forwards the time.  `init` is the next
-// round's summary, initialised here (nothing else touches it this round).
-__global__ __launch_bounds__(kBlock) void k_round_dev(Params P, const DevSummary* __restrict__ prev,
-                                                       DevSummary* __restrict__ init, uint64_t window,
-                                                       uint64_t stop, int parity) {
-    if (*P.halt) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        DevSummary z{};
-        z.next_time = kInf;
-        *init = z;
-    }
-    const uint64_t ws = prev->next_time;
-    if (ws >= stop) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) atomicMin(&P.sum->next_time, (unsigned long long)ws);
-        return;
-    }
-    uint64_t we = ws + window;
-    if (we > stop || we < ws) we = stop;
-    round_body(P, we, parity);
-}
-
 // finalize resolved pending sends: value from the min-rank row, then deliver
 __device__ void finalize_one(const Params& P, const Pending& r, int next_parity, uint64_t& next, uint32_t& err) {
     if (r.delivered != 1u) return;
@@ -1000,10 +1035,10 @@ __global__ void k_finalize(Params P, const Pending* __restrict__ pend, uint32_t 
 }
 
 // device-side first-touch resolution for rounds with few logged queries (the
-// common case after warm-up): one workgroup ranks the records by serial key
-// (counting sort: keys are unique), one lane assigns row ranks in that order,
-// every lane finalizes its record.  Larger rounds halt the pipeline for the
-// host path (shd_eng_resolve).
+// common case after warm-up), run by the last block of the round: rank the
+// records by serial key (counting sort: keys are unique), one lane assigns
+// row ranks in that order, every lane finalizes its records.  Larger rounds
+// halt the batch for the host path (shd_eng_resolve).
 constexpr int kResolveMax = 256;
 __device__ __forceinline__ bool pend_less(const Pending& x, const Pending& y) {
     if (x.qtime != y.qtime) return x.qtime < y.qtime;
@@ -1013,30 +1048,29 @@ __device__ __forceinline__ bool pend_less(const Pending& x, const Pending& y) {
     return x.qsub < y.qsub;
 }
 
-__global__ __launch_bounds__(kResolveMax) void k_resolve_dev(Params P, int next_parity) {
+__device__ void resolve_block(const Params& P, int next_parity) {
     __shared__ Pending recs[kResolveMax];
     __shared__ int16_t order[kResolveMax];
-    if (*P.halt) return;
     const unsigned long long n = P.sum->n_pending;
     if (n == 0) return;
     if (n > (unsigned long long)kResolveMax) {
         if (threadIdx.x == 0) *P.halt = 1u;
         return;
     }
-    const int i = threadIdx.x;
-    if (i < (int)n) recs[i] = P.pend[i];
+    const int cnt = (int)n;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) recs[i] = P.pend[i];
     __syncthreads();
-    if (i < (int)n) {
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
         int pos = 0;
-        for (int j = 0; j < (int)n; j++) pos += pend_less(recs[j], recs[i]) ? 1 : 0;
+        for (int j = 0; j < cnt; j++) pos += pend_less(recs[j], recs[i]) ? 1 : 0;
         order[pos] = (int16_t)i;
     }
     __syncthreads();
-    if (i == 0) {
+    if (threadIdx.x == 0) {
         int32_t nr = *P.next_rank;
         int32_t* rank = (int32_t*)P.rank;
         int32_t* srank = (int32_t*)P.self_rank;
-        for (int k = 0; k < (int)n; k++) {
+        for (int k = 0; k < cnt; k++) {
             const Pending& r = recs[order[k]];
             const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
             if (a == b) {
@@ -1054,9 +1088,62 @@ __global__ __launch_bounds__(kResolveMax) void k_resolve_dev(Params P, int next_
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // drop L1 lines of the rank arrays
     uint64_t next = kInf;
     uint32_t err = 0;
-    if (i < (int)n) finalize_one(P, recs[i], next_parity, next, err);
-    if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
-    if (err) atomicOr(&P.sum->error, err);
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) finalize_one(P, recs[i], next_parity, next, err);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0) {
+        if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+        if (err) atomicOr(&P.sum->error, err);
+    }
+}
+
+// last-block ticket: true in the one block that finishes the round last; all
+// blocks' summary atomics and logged records are then visible to it
+__device__ __forceinline__ bool last_block(const Params& P) {
+    __shared__ int s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();   // release this block's stores (pending records, inbox)
+        const unsigned t = atomicAdd(&P.sum->done, 1u);
+        s_last = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return true;
+}
+
+// device-driven round i of a batch (single engine): the window start is the
+// previous round's next event time (read on the device), so rounds run back
+// to back from one batch launch (or graph) with no host round trip; the last
+// block resolves the round's first-touch log.  A round past `stop` only
+// forwards the time.  `init` is the next round's summary, initialised here.
+__global__ __launch_bounds__(kBlock) void k_round_dev(Params P, const DevSummary* __restrict__ prev,
+                                                       DevSummary* __restrict__ init,
+                                                       const DevCtl* __restrict__ ctl, int i, uint64_t window) {
+    if (*P.halt) return;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (lead) {
+        atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+        *init = fresh_summary();
+    }
+    const uint64_t stop = ctl->stop;
+    const int parity = (int)((ctl->round_base + (uint64_t)i) & 1);
+    const uint64_t ws = prev->next_time;
+    if (ws >= stop) {
+        if (lead) atomicMin(&P.sum->next_time, (unsigned long long)ws);
+        return;
+    }
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    round_body(P, we, parity);
+    if (!last_block(P)) return;
+    if (threadIdx.x == 0) P.sum->ws = ws;
+    resolve_block(P, parity ^ 1);
+    if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
 }
 
 // ingest events from other engines into inbox[parity]
@@ -1067,6 +1154,123 @@ __global__ void k_ingest(Params P, const shd_event* __restrict__ ev, uint64_t n,
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
     uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+    if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
+    P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+}
+
+// ---- exchange mode kernels (shd_xgroup) ----
+// local transport: block d of sender s -> block s of receiver d, header plus
+// the counted events only; grid (slots, receiver, sender)
+struct XPtrs {
+    const shd_event* send[64];
+    shd_event* recv[64];
+};
+__global__ void k_xcopy_local(XPtrs X, uint64_t stride) {
+    const int s = blockIdx.z, d = blockIdx.y;
+    const shd_event* src = X.send[s] + (size_t)d * stride;
+    shd_event* dst = X.recv[d] + (size_t)s * stride;
+    const uint32_t n = ((const XHeader*)src)->count;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
+// headers of this engine's blocks, one lane per peer: the engine's next event
+// time and the round's flags; `clean` after a host recovery (the recovered
+// round's flags are not repeated).  Resets the per-peer counters.
+__device__ void xpack_block(const Params& P, const DevSummary* sum, int clean, uint64_t next_time) {
+    const int32_t p = threadIdx.x;
+    if (p >= P.xworld) return;
+    const uint32_t cnt = P.xcount[p];
+    XHeader h;
+    h.next_time = next_time;
+    h.count = cnt < P.xcap ? cnt : P.xcap;
+    uint32_t fl = 0;
+    if (!clean) {
+        if (sum->n_pending) fl |= XF_PENDING;
+        if (sum->n_remote) fl |= XF_OVERFLOW;
+        if (sum->error) fl |= XF_ERROR;
+    }
+    h.flags = fl;
+    h.n_pending = clean ? 0 : sum->n_pending;
+    h.error = sum->error;
+    h.pad = 0;
+    *(XHeader*)(P.xsend + (size_t)p * (P.xcap + 1)) = h;
+    P.xcount[p] = 0;
+}
+
+__global__ void k_xpack(Params P, const DevSummary* __restrict__ sum, int clean) {
+    if (*P.halt) return;
+    xpack_block(P, sum, clean, sum->next_time);
+}
+
+// one round of an engine group: the window start is the min over the
+// headers of the last exchange; any flagged header (a first-touch log, a
+// spill or an error anywhere in the group) halts the batch on every engine
+// alike.  The last block writes this engine's headers for the next exchange.
+__global__ __launch_bounds__(kBlock) void k_round_x(Params P, const shd_event* __restrict__ xrecv,
+                                                    XHeader* __restrict__ halt_hdr, DevSummary* __restrict__ init,
+                                                    const DevCtl* __restrict__ ctl, int i, uint64_t window) {
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (*P.halt) {
+        if (lead) P.sum->flags = 2u;
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+        *init = fresh_summary();
+    }
+    const uint64_t stop = ctl->stop;
+    const int parity = (int)((ctl->round_base + (uint64_t)i) & 1);
+    const size_t stride = (size_t)P.xcap + 1;
+    uint64_t ws = kInf;
+    uint32_t fl = 0;
+    for (int32_t p = 0; p < P.xworld; p++) {
+        const XHeader h = *(const XHeader*)(xrecv + (size_t)p * stride);
+        ws = h.next_time < ws ? h.next_time : ws;
+        fl |= h.flags;
+    }
+    if (fl) {
+        if (blockIdx.x == 0) {
+            if ((int32_t)threadIdx.x < P.xworld) halt_hdr[threadIdx.x] = *(const XHeader*)(xrecv + threadIdx.x * stride);
+            if (threadIdx.x == 0) {
+                *P.halt = 1u;
+                P.sum->flags = 1u;
+            }
+        }
+        return;
+    }
+    if (ws >= stop) {   // only forwards the time
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) {
+                P.sum->ws = ws;
+                atomicMin(&P.sum->next_time, (unsigned long long)ws);
+            }
+            xpack_block(P, P.sum, 1, ws);
+        }
+        return;
+    }
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    round_body(P, we, parity);
+    if (!last_block(P)) return;
+    if (threadIdx.x == 0) P.sum->ws = ws;
+    xpack_block(P, P.sum, 0, P.sum->next_time);
+    if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
+}
+
+// events received in the exchange -> inbox[parity] of the next round
+__global__ void k_ingest_x(Params P, const shd_event* __restrict__ xrecv, const DevCtl* __restrict__ ctl, int ri) {
+    if (*P.halt) return;
+    const int parity = (int)((ctl->round_base + (uint64_t)ri + 1) & 1);   // the next round's inbox
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p = t / P.xcap, s = t % P.xcap;
+    if (p >= (uint64_t)P.xworld) return;
+    const shd_event* blk = xrecv + p * ((uint64_t)P.xcap + 1);
+    if (s >= ((const XHeader*)blk)->count) return;
+    const shd_event e = blk[1 + s];
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
+    const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
     if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
 }
@@ -1151,6 +1355,11 @@ struct shd_eng {
     int32_t* d_next_rank = nullptr;
     unsigned long long* d_trace_n = nullptr;
     hipEvent_t bev[2 * kBatch] = {};
+    DevCtl* d_ctl = nullptr;                // per-batch inputs (device) and their pinned staging
+    DevCtl* h_ctl = nullptr;
+    DevSummary* h_seed = nullptr;           // pinned: ring slots 0 and 1 at a batch start
+    hipGraphExec_t batch_graph = nullptr;   // captured batch of kBatch device-driven rounds
+    double wall_khz = 100000.0;             // device wall clock (wall_clock64) rate
     uint64_t trace_cap = 0;
 };
 
@@ -1256,7 +1465,17 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         shd_eng_destroy(e);
         return SHD_ENOMEM;
     }
-    EALLOC(e->d_halt, 1); EALLOC(e->d_next_rank, 1); EALLOC(e->d_trace_n, 1);
+    EALLOC(e->d_halt, 1); EALLOC(e->d_next_rank, 1); EALLOC(e->d_trace_n, 1); EALLOC(e->d_ctl, 1);
+    if (hipHostMalloc((void**)&e->h_ctl, sizeof(DevCtl)) != hipSuccess ||
+        hipHostMalloc((void**)&e->h_seed, 2 * sizeof(DevSummary)) != hipSuccess) {
+        shd_eng_destroy(e);
+        return SHD_ENOMEM;
+    }
+    {
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+            e->wall_khz = khz;
+    }
     for (auto& ev : e->bev) (void)hipEventCreate(&ev);
     P.halt = e->d_halt; P.next_rank = e->d_next_rank; P.trace_n = e->d_trace_n;
     P.pend_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 16, (uint64_t)n * (m->load + 4)), 1u << 30);
@@ -1336,9 +1555,21 @@ extern "C" int shd_eng_window(shd_eng* e, uint64_t* w) {
     return SHD_OK;
 }
 
-static int reset_summary(shd_eng* e) {
+static DevSummary host_fresh_summary() {
     DevSummary z{};
     z.next_time = kInf;
+    z.t_first = kInf;
+    return z;
+}
+
+// device time of a round kernel from its summary's wall-clock stamps
+static double round_kernel_ms(const shd_eng* e, const DevSummary& r) {
+    if (r.t_first == kInf || r.t_last < r.t_first) return 0.0;
+    return (double)(r.t_last - r.t_first) / e->wall_khz;
+}
+
+static int reset_summary(shd_eng* e) {
+    DevSummary z = host_fresh_summary();
     SHD_HIP(hipMemcpyAsync(e->d_sum, &z, sizeof(z), hipMemcpyHostToDevice, e->stream));
     SHD_HIP(hipStreamSynchronize(e->stream));
     return SHD_OK;
@@ -1492,12 +1723,44 @@ extern "C" int shd_eng_run_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round
     return shd_eng_end_round(e, out);
 }
 
-// Device-driven rounds (single engine): batches of kBatch rounds are enqueued
-// back to back, each k_round_dev reading its window start from the previous
-// round's summary on the device and k_resolve_dev resolving small first-touch
-// logs in place.  The host reads the batch's summaries once per batch.  A
-// round whose first-touch log is too large for the device path halts the
-// batch; the host resolves it (shd_eng_resolve) and resumes after it.
+// Device-driven rounds (single engine): a batch of kBatch rounds is one
+// captured graph of k_round_dev launches, each reading its window start from
+// the previous round's summary on the device, its stop time and parity from
+// the batch control block, and resolving small first-touch logs in its last
+// block.  The host reads the batch's summaries once per batch.  A round whose
+// first-touch log is too large for the device path halts the batch; the host
+// resolves it (shd_eng_resolve) and resumes after it.
+static int enqueue_batch(shd_eng* e) {
+    constexpr int B = shd_eng::kBatch;
+    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
+    for (int i = 0; i < B; i++) {
+        Params P = e->P;
+        P.sum = &e->d_ring[i + 1];
+        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, P, (const DevSummary*)&e->d_ring[i],
+                           &e->d_ring[i + 2], (const DevCtl*)e->d_ctl, i, e->window);
+    }
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
+static int launch_batch(shd_eng* e) {
+    static const bool no_graph = getenv("SHD_NO_GRAPH") != nullptr;
+    if (no_graph) return enqueue_batch(e);
+    if (!e->batch_graph) {
+        hipGraph_t gr = nullptr;
+        SHD_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        const int rc = enqueue_batch(e);
+        const hipError_t ec = hipStreamEndCapture(e->stream, &gr);
+        if (rc) return rc;
+        SHD_HIP(ec);
+        const hipError_t ei = hipGraphInstantiate(&e->batch_graph, gr, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(gr);
+        SHD_HIP(ei);
+    }
+    SHD_HIP(hipGraphLaunch(e->batch_graph, e->stream));
+    return SHD_OK;
+}
+
 extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;
     auto t0 = std::chrono::steady_clock::now();
@@ -1510,39 +1773,28 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     uint64_t next = e->h_sum->next_time;
     e->kernel_ms_total = 0;
     const uint64_t pend0 = e->pending_resolved;
-    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     constexpr int B = shd_eng::kBatch, R = shd_eng::kRing;
+    static_assert(R >= B + 2, "summary ring");
     while (next < stop && rc == SHD_OK) {
         // slot 0 carries the window start; rounds use slots 1..B
-        DevSummary seed{};
-        seed.next_time = next;
-        DevSummary first{};
-        first.next_time = kInf;
-        SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &seed, sizeof(seed), hipMemcpyHostToDevice, e->stream));
-        SHD_HIP(hipMemcpyAsync(&e->d_ring[1], &first, sizeof(first), hipMemcpyHostToDevice, e->stream));
+        e->h_seed[0] = host_fresh_summary();
+        e->h_seed[0].next_time = next;
+        e->h_seed[1] = host_fresh_summary();
+        e->h_ctl->stop = stop;
+        e->h_ctl->round_base = e->round;
+        SHD_HIP(hipMemcpyAsync(e->d_ring, e->h_seed, 2 * sizeof(DevSummary), hipMemcpyHostToDevice, e->stream));
+        SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
-        for (int i = 0; i < B; i++) {
-            Params P = e->P;
-            P.sum = &e->d_ring[i + 1];
-            const int parity = (int)((e->round + i) & 1);
-            SHD_HIP(hipEventRecord(e->bev[2 * i], e->stream));
-            hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, P,
-                               (const DevSummary*)&e->d_ring[i], &e->d_ring[i + 2], e->window, stop, parity);
-            SHD_HIP(hipEventRecord(e->bev[2 * i + 1], e->stream));
-            hipLaunchKernelGGL(k_resolve_dev, dim3(1), dim3(kResolveMax), 0, e->stream, P, parity ^ 1);
-        }
-        SHD_HIP(hipGetLastError());
+        if ((rc = launch_batch(e))) break;
         uint32_t halt = 0;
         SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost, e->stream));
         SHD_HIP(hipMemcpyAsync(&halt, e->d_halt, 4, hipMemcpyDeviceToHost, e->stream));
         SHD_HIP(hipStreamSynchronize(e->stream));
-        static_assert(R >= B + 2, "summary ring");
         for (int i = 0; i < B; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
             if (ws >= stop) { next = ws; break; }   // the rest only forwarded the time
-            float ms = 0;
-            (void)hipEventElapsedTime(&ms, e->bev[2 * i], e->bev[2 * i + 1]);
+            const double ms = round_kernel_ms(e, r);
             e->kernel_ms_total += ms;
             e->last_kernel_ms = ms;
             const bool halted_here = halt && r.n_pending > (unsigned long long)kResolveMax;
@@ -1705,10 +1957,573 @@ extern "C" void shd_eng_destroy(shd_eng* e) {
     for (void* p : e->allocs) (void)hipFree(p);
     if (e->h_sum) (void)hipHostFree(e->h_sum);
     if (e->h_ring) (void)hipHostFree(e->h_ring);
+    if (e->h_ctl) (void)hipHostFree(e->h_ctl);
+    if (e->h_seed) (void)hipHostFree(e->h_seed);
+    if (e->batch_graph) (void)hipGraphExecDestroy(e->batch_graph);
     for (auto& ev : e->bev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
+}
+
+// ===================================================================== engine groups
+// shd_xgroup (include/shdgpu.h): rounds across engines with one fixed-size
+// all-to-all per round.  DESIGN.md "Multi-GPU" describes the protocol.
+#define SHD_NCCL(x)                                                                                  \
+    do {                                                                                             \
+        ncclResult_t r_ = (x);                                                                       \
+        if (r_ != ncclSuccess) {                                                                     \
+            fprintf(stderr, "libshdgpu: %s: %s (%s:%d)\n", #x, ncclGetErrorString(r_), __FILE__, __LINE__); \
+            return SHD_ENODEV;                                                                       \
+        }                                                                                            \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == SHD_XID_BYTES, "RCCL unique id size");
+
+struct shd_xgroup {
+    bool rccl = false;
+    ncclComm_t comm = nullptr;
+    int world = 1;                     // engines in the group
+    int rank0 = 0;                     // group rank of local engine 0
+    std::vector<shd_eng*> engs;        // this process's engines, rank order
+    uint32_t xcap = 0;                 // events per peer block
+    size_t stride = 0;                 // event slots per peer block (header + xcap)
+    uint64_t window = 0, end_time = 0;
+    struct Loc {
+        shd_event* xsend = nullptr;
+        shd_event* xrecv[2] = {nullptr, nullptr};
+        uint32_t* xcount = nullptr;
+        XHeader* halt_hdr = nullptr;
+    };
+    std::vector<Loc> loc;
+    uint64_t xseq = 0;                 // exchanges done: the latest headers are in xrecv[(xseq - 1) & 1]
+    bool started = false;
+    hipStream_t xs = nullptr;          // local transport: the copy stream
+    hipEvent_t xev = nullptr;
+    std::vector<hipEvent_t> eev;
+    uint64_t next = kInf;              // group next event time (host view)
+    bool fixed_cap = false;            // block size given by the caller
+    uint64_t last_spill_batch = ~0ull; // batch index of the last spill halt
+    uint64_t batches = 0;
+};
+
+static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
+    Params P = g->engs[k]->P;
+    P.xsend = g->loc[k].xsend;
+    P.xcount = g->loc[k].xcount;
+    P.xcap = g->xcap;
+    P.xworld = g->world;
+    P.sum = sum;
+    return P;
+}
+
+// the fixed-size all-to-all: block d of every sender's xsend -> block s of
+// receiver d's xrecv[xseq & 1]
+static int x_exchange(shd_xgroup* g) {
+    const size_t bytes = g->stride * sizeof(shd_event);
+    const int wi = (int)(g->xseq & 1);
+    if (g->rccl) {
+        shd_eng* e = g->engs[0];
+        SHD_NCCL(ncclAllToAll(g->loc[0].xsend, g->loc[0].xrecv[wi], bytes, ncclUint8, g->comm, e->stream));
+    } else {
+        const int n = g->world;
+        for (int k = 0; k < n; k++) {
+            SHD_HIP(hipEventRecord(g->eev[k], g->engs[k]->stream));
+            SHD_HIP(hipStreamWaitEvent(g->xs, g->eev[k], 0));
+        }
+        XPtrs X;
+        for (int k = 0; k < n; k++) {
+            X.send[k] = g->loc[k].xsend;
+            X.recv[k] = g->loc[k].xrecv[wi];
+        }
+        hipLaunchKernelGGL(k_xcopy_local, dim3(8, n, n), dim3(256), 0, g->xs, X, (uint64_t)g->stride);
+        SHD_HIP(hipGetLastError());
+        SHD_HIP(hipEventRecord(g->xev, g->xs));
+        for (int k = 0; k < n; k++) SHD_HIP(hipStreamWaitEvent(g->engs[k]->stream, g->xev, 0));
+    }
+    g->xseq++;
+    return SHD_OK;
+}
+
+// headers of the latest exchange as seen by local engine 0
+static int x_headers(shd_xgroup* g, std::vector<XHeader>& h) {
+    shd_eng* e = g->engs[0];
+    h.resize(g->world);
+    const shd_event* src = g->loc[0].xrecv[(g->xseq - 1) & 1];
+    SHD_HIP(hipMemcpy2DAsync(h.data(), sizeof(XHeader), src, g->stride * sizeof(shd_event), sizeof(XHeader),
+                             g->world, hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
+    return SHD_OK;
+}
+
+static int x_read_next(shd_xgroup* g) {
+    std::vector<XHeader> h;
+    int rc = x_headers(g, h);
+    if (rc) return rc;
+    uint64_t t = kInf;
+    for (const XHeader& x : h) t = std::min<uint64_t>(t, x.next_time);
+    g->next = t;
+    return SHD_OK;
+}
+
+// every engine's first-touch records of the flagged round, in any order
+static int x_gather_pending(shd_xgroup* g, std::vector<shd_pending>& all) {
+    std::vector<shd_pending> mine;
+    for (shd_eng* e : g->engs) {
+        const uint64_t n = e->round_pending;
+        if (n > e->P.pend_cap) return SHD_EOVERFLOW;
+        const size_t at = mine.size();
+        mine.resize(at + n);
+        if (n) SHD_HIP(hipMemcpy(mine.data() + at, e->P.pend, sizeof(shd_pending) * n, hipMemcpyDeviceToHost));
+    }
+    if (!g->rccl) {
+        all.swap(mine);
+        return SHD_OK;
+    }
+    shd_eng* e = g->engs[0];
+    unsigned long long* d_cnt = nullptr;
+    SHD_HIP(hipMalloc((void**)&d_cnt, 8 * (size_t)(g->world + 1)));
+    const unsigned long long my = mine.size();
+    std::vector<unsigned long long> cnt(g->world);
+    SHD_HIP(hipMemcpyAsync(d_cnt + g->world, &my, 8, hipMemcpyHostToDevice, e->stream));
+    ncclResult_t nr = ncclAllGather(d_cnt + g->world, d_cnt, 1, ncclUint64, g->comm, e->stream);
+    if (nr == ncclSuccess) {
+        (void)hipMemcpyAsync(cnt.data(), d_cnt, 8 * (size_t)g->world, hipMemcpyDeviceToHost, e->stream);
+        (void)hipStreamSynchronize(e->stream);
+    }
+    (void)hipFree(d_cnt);
+    if (nr != ncclSuccess) return SHD_ENODEV;
+    const unsigned long long mx = *std::max_element(cnt.begin(), cnt.end());
+    if (mx == 0) {
+        all.clear();
+        return SHD_OK;
+    }
+    const size_t blk = mx * sizeof(shd_pending);
+    char* d_buf = nullptr;
+    SHD_HIP(hipMalloc((void**)&d_buf, blk * (size_t)(g->world + 1)));
+    (void)hipMemsetAsync(d_buf + blk * g->world, 0, blk, e->stream);
+    if (!mine.empty())
+        (void)hipMemcpyAsync(d_buf + blk * g->world, mine.data(), sizeof(shd_pending) * mine.size(),
+                             hipMemcpyHostToDevice, e->stream);
+    std::vector<char> h(blk * (size_t)g->world);
+    nr = ncclAllGather(d_buf + blk * g->world, d_buf, blk, ncclUint8, g->comm, e->stream);
+    if (nr == ncclSuccess) {
+        (void)hipMemcpyAsync(h.data(), d_buf, h.size(), hipMemcpyDeviceToHost, e->stream);
+        (void)hipStreamSynchronize(e->stream);
+    }
+    (void)hipFree(d_buf);
+    if (nr != ncclSuccess) return SHD_ENODEV;
+    all.clear();
+    for (int r = 0; r < g->world; r++) {
+        const shd_pending* p = (const shd_pending*)(h.data() + blk * r);
+        all.insert(all.end(), p, p + cnt[r]);
+    }
+    return SHD_OK;
+}
+
+static int x_ingest(shd_eng* e, const Params& P, const shd_event* d_ev, uint64_t n, int parity) {
+    if (!n) return SHD_OK;
+    hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, P, d_ev, n, parity);
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
+// deliver the remote buffers (block spills and finalized first-touch sends of
+// the flagged round, whose summary is ring slot `slot`) with a variable-size
+// exchange; the receivers' next round merges them (inbox[round & 1])
+static int x_exchange_remote(shd_xgroup* g, int slot) {
+    const int nl = (int)g->engs.size();
+    std::vector<std::vector<std::vector<shd_event>>> out(nl);   // [local sender][peer]
+    for (int k = 0; k < nl; k++) {
+        shd_eng* e = g->engs[k];
+        DevSummary r;
+        SHD_HIP(hipMemcpy(&r, &e->d_ring[slot], sizeof(r), hipMemcpyDeviceToHost));
+        const uint64_t n = std::min<uint64_t>(r.n_remote, e->P.remote_cap);
+        std::vector<shd_event> ev(n);
+        if (n) SHD_HIP(hipMemcpy(ev.data(), e->P.remote, sizeof(shd_event) * n, hipMemcpyDeviceToHost));
+        out[k].assign(g->world, {});
+        const uint64_t H = (uint64_t)e->P.H, N = (uint64_t)g->world;
+        for (const shd_event& x : ev) {
+            int64_t p = (int64_t)(((uint64_t)x.dst * N) / H);
+            while (p + 1 < (int64_t)N && (H * (uint64_t)(p + 1)) / N <= x.dst) p++;
+            while (p > 0 && (H * (uint64_t)p) / N > x.dst) p--;
+            out[k][p].push_back(x);
+        }
+        const unsigned long long z = 0;   // the spill is consumed
+        SHD_HIP(hipMemcpy(&e->d_ring[slot].n_remote, &z, 8, hipMemcpyHostToDevice));
+    }
+    if (!g->rccl) {
+        for (int d = 0; d < nl; d++) {
+            std::vector<shd_event> in;
+            for (int s = 0; s < nl; s++) in.insert(in.end(), out[s][d].begin(), out[s][d].end());
+            if (in.empty()) continue;
+            shd_eng* e = g->engs[d];
+            shd_event* d_ev = nullptr;
+            SHD_HIP(hipMalloc((void**)&d_ev, sizeof(shd_event) * in.size()));
+            int rc = SHD_OK;
+            if (hipMemcpy(d_ev, in.data(), sizeof(shd_event) * in.size(), hipMemcpyHostToDevice) != hipSuccess)
+                rc = SHD_ENODEV;
+            if (!rc) rc = x_ingest(e, xparams(g, d, &e->d_ring[slot]), d_ev, in.size(), (int)(e->round & 1));
+            if (!rc && hipStreamSynchronize(e->stream) != hipSuccess) rc = SHD_ENODEV;
+            (void)hipFree(d_ev);
+            if (rc) return rc;
+        }
+        return SHD_OK;
+    }
+    // RCCL: counts matrix, then one all-to-allv of the bucketed events
+    shd_eng* e = g->engs[0];
+    const int W = g->world;
+    std::vector<unsigned long long> sc(W), all((size_t)W * W);
+    for (int p = 0; p < W; p++) sc[p] = out[0][p].size();
+    unsigned long long* d_c = nullptr;
+    SHD_HIP(hipMalloc((void**)&d_c, 8 * (size_t)W * (W + 1)));
+    (void)hipMemcpyAsync(d_c + (size_t)W * W, sc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream);
+    ncclResult_t nr = ncclAllGather(d_c + (size_t)W * W, d_c, W, ncclUint64, g->comm, e->stream);
+    if (nr == ncclSuccess) {
+        (void)hipMemcpyAsync(all.data(), d_c, 8 * (size_t)W * W, hipMemcpyDeviceToHost, e->stream);
+        (void)hipStreamSynchronize(e->stream);
+    }
+    (void)hipFree(d_c);
+    if (nr != ncclSuccess) return SHD_ENODEV;
+    const int me = g->rank0;
+    std::vector<size_t> scount(W), sdisp(W), rcount(W), rdisp(W);
+    size_t ns = 0, nrcv = 0;
+    for (int p = 0; p < W; p++) {
+        scount[p] = sc[p] * sizeof(shd_event);
+        sdisp[p] = ns;
+        ns += scount[p];
+        rcount[p] = all[(size_t)p * W + me] * sizeof(shd_event);
+        rdisp[p] = nrcv;
+        nrcv += rcount[p];
+    }
+    std::vector<shd_event> flat;
+    flat.reserve(ns / sizeof(shd_event));
+    for (int p = 0; p < W; p++) flat.insert(flat.end(), out[0][p].begin(), out[0][p].end());
+    char *d_s = nullptr, *d_r = nullptr;
+    SHD_HIP(hipMalloc((void**)&d_s, ns ? ns : 32));
+    if (hipMalloc((void**)&d_r, nrcv ? nrcv : 32) != hipSuccess) {
+        (void)hipFree(d_s);
+        return SHD_ENOMEM;
+    }
+    int rc = SHD_OK;
+    if (ns && hipMemcpyAsync(d_s, flat.data(), ns, hipMemcpyHostToDevice, e->stream) != hipSuccess) rc = SHD_ENODEV;
+    if (!rc && ncclAllToAllv(d_s, scount.data(), sdisp.data(), d_r, rcount.data(), rdisp.data(), ncclUint8, g->comm,
+                             e->stream) != ncclSuccess)
+        rc = SHD_ENODEV;
+    if (!rc) rc = x_ingest(e, xparams(g, 0, &e->d_ring[slot]), (const shd_event*)d_r, nrcv / sizeof(shd_event),
+                           (int)(e->round & 1));
+    if (!rc && hipStreamSynchronize(e->stream) != hipSuccess) rc = SHD_ENODEV;
+    (void)hipFree(d_s);
+    (void)hipFree(d_r);
+    return rc;
+}
+
+static int x_alloc(shd_xgroup* g) {
+    g->stride = (size_t)g->xcap + 1;
+    g->loc.resize(g->engs.size());
+    for (size_t k = 0; k < g->engs.size(); k++) {
+        shd_eng* e = g->engs[k];
+        shd_xgroup::Loc& L = g->loc[k];
+        SHD_HIP(hipSetDevice(e->device));
+        const size_t n = g->stride * (size_t)g->world;
+        int rc;
+        if ((rc = ealloc(e, &L.xsend, n)) || (rc = ealloc(e, &L.xrecv[0], n)) || (rc = ealloc(e, &L.xrecv[1], n)) ||
+            (rc = ealloc(e, &L.xcount, g->world)) || (rc = ealloc(e, &L.halt_hdr, g->world)))
+            return rc;
+        SHD_HIP(hipStreamSynchronize(e->stream));
+    }
+    return SHD_OK;
+}
+
+static uint32_t x_default_cap(const shd_eng* e, int world) {
+    // a round's sends to one peer are ~ nloc / world x (sends per host per
+    // window, well below 1 at W = the minimum path latency): two sends per
+    // host of headroom; bursts beyond the block spill to the host path, and
+    // spills in consecutive batches grow the block (x_grow)
+    return (uint32_t)std::max<int64_t>(256, 2 * (int64_t)e->nloc / world);
+}
+
+extern "C" int shd_xgroup_unique_id(uint8_t id[SHD_XID_BYTES]) {
+    if (!id) return SHD_EINVAL;
+    ncclUniqueId u;
+    SHD_NCCL(ncclGetUniqueId(&u));
+    memcpy(id, &u, SHD_XID_BYTES);
+    return SHD_OK;
+}
+
+static void x_free(shd_xgroup* g) {
+    if (!g) return;
+    if (g->comm) (void)ncclCommDestroy(g->comm);
+    for (auto& ev : g->eev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (g->xev) (void)hipEventDestroy(g->xev);
+    if (g->xs) (void)hipStreamDestroy(g->xs);
+    delete g;   // buffers belong to the engines' allocation lists
+}
+
+extern "C" int shd_xgroup_create_local(shd_eng* const* engines, int n, uint32_t block_events, shd_xgroup** out) {
+    if (!engines || n <= 0 || n > 64 || !out) return SHD_EINVAL;
+    shd_xgroup* g = new shd_xgroup();
+    g->world = n;
+    g->rank0 = 0;
+    for (int k = 0; k < n; k++) {
+        shd_eng* e = engines[k];
+        if (!e || e->device != engines[0]->device || e->P.H != engines[0]->P.H) { x_free(g); return SHD_EINVAL; }
+        const int64_t H = e->P.H;
+        if (e->h0 != (int32_t)((H * k) / n) || e->h0 + e->nloc != (int32_t)((H * (k + 1)) / n)) {
+            x_free(g);
+            return SHD_EINVAL;   // the group partition is (H*p)/N
+        }
+        g->engs.push_back(e);
+    }
+    g->window = kInf;
+    for (shd_eng* e : g->engs) g->window = std::min<uint64_t>(g->window, e->window);
+    g->end_time = engines[0]->P.end_time;
+    g->xcap = block_events ? block_events : x_default_cap(engines[0], n);
+    g->fixed_cap = block_events != 0;
+    if (hipSetDevice(engines[0]->device) != hipSuccess ||
+        hipStreamCreateWithFlags(&g->xs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g->xev, hipEventDisableTiming) != hipSuccess) {
+        x_free(g);
+        return SHD_ENODEV;
+    }
+    g->eev.assign(n, nullptr);
+    for (auto& ev : g->eev)
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) { x_free(g); return SHD_ENODEV; }
+    int rc = x_alloc(g);
+    if (rc) { x_free(g); return rc; }
+    *out = g;
+    return SHD_OK;
+}
+
+extern "C" int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
+                                      uint32_t block_events, shd_xgroup** out) {
+    if (!e || !id || world <= 0 || world > 64 || rank < 0 || rank >= world || !out) return SHD_EINVAL;
+    const int64_t H = e->P.H;
+    if (e->h0 != (int32_t)((H * rank) / world) || e->h0 + e->nloc != (int32_t)((H * (rank + 1)) / world))
+        return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(e->device));
+    shd_xgroup* g = new shd_xgroup();
+    g->rccl = true;
+    g->world = world;
+    g->rank0 = rank;
+    g->engs.push_back(e);
+    ncclUniqueId u;
+    memcpy(&u, id, SHD_XID_BYTES);
+    if (ncclCommInitRank(&g->comm, world, u, rank) != ncclSuccess) {
+        g->comm = nullptr;
+        x_free(g);
+        return SHD_ENODEV;
+    }
+    // the group agrees on W (min) and checks the model: H and end time equal everywhere
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d, 8 * (size_t)(3 * world + 3)) != hipSuccess) { x_free(g); return SHD_ENOMEM; }
+    const unsigned long long mine[3] = {(unsigned long long)e->window, (unsigned long long)H,
+                                        (unsigned long long)e->P.end_time};
+    std::vector<unsigned long long> all(3 * (size_t)world);
+    int rc = SHD_OK;
+    if (hipMemcpy(d + 3 * world, mine, 24, hipMemcpyHostToDevice) != hipSuccess ||
+        ncclAllGather(d + 3 * world, d, 3, ncclUint64, g->comm, e->stream) != ncclSuccess ||
+        hipMemcpyAsync(all.data(), d, 24 * (size_t)world, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+        hipStreamSynchronize(e->stream) != hipSuccess)
+        rc = SHD_ENODEV;
+    (void)hipFree(d);
+    if (rc) { x_free(g); return rc; }
+    g->window = kInf;
+    for (int r = 0; r < world; r++) {
+        if (all[3 * r + 1] != (unsigned long long)H || all[3 * r + 2] != e->P.end_time) { x_free(g); return SHD_EINVAL; }
+        g->window = std::min<uint64_t>(g->window, all[3 * r]);
+    }
+    g->end_time = e->P.end_time;
+    g->xcap = block_events ? block_events : x_default_cap(e, world);
+    g->fixed_cap = block_events != 0;
+    if ((rc = x_alloc(g))) { x_free(g); return rc; }
+    *out = g;
+    return SHD_OK;
+}
+
+extern "C" int shd_xgroup_next_time(shd_xgroup* g, uint64_t* t) {
+    if (!g || !t) return SHD_EINVAL;
+    *t = g->next;
+    return SHD_OK;
+}
+
+extern "C" void shd_xgroup_destroy(shd_xgroup* g) { x_free(g); }
+
+extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stats* st) {
+    if (!g) return SHD_EINVAL;
+    auto t0 = std::chrono::steady_clock::now();
+    const int nl = (int)g->engs.size();
+    int rc = SHD_OK;
+    shd_run_stats s{};
+    s.window_ns = g->window;
+    for (shd_eng* e : g->engs) {
+        SHD_HIP(hipSetDevice(e->device));
+        if (!e->booted && (rc = shd_eng_boot(e))) return rc;
+    }
+    if (!g->started) {
+        // the first headers: every engine's next event time after boot
+        for (int k = 0; k < nl; k++) {
+            shd_eng* e = g->engs[k];
+            SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
+            hipLaunchKernelGGL(k_xpack, dim3(1), dim3(64), 0, e->stream, xparams(g, k, e->d_sum), e->d_sum, 1);
+        }
+        if ((rc = x_exchange(g))) return rc;
+        g->started = true;
+    }
+    if ((rc = x_read_next(g))) return rc;
+    const uint64_t stop = std::min<uint64_t>(t_stop, g->end_time);
+    constexpr int B = shd_eng::kBatch;
+    std::vector<uint64_t> pend0(nl);
+    for (int k = 0; k < nl; k++) pend0[k] = g->engs[k]->pending_resolved;
+    double kms = 0;
+    while (g->next < stop && rc == SHD_OK) {
+        g->batches++;
+        for (int k = 0; k < nl; k++) {
+            shd_eng* e = g->engs[k];
+            // slot 0 keeps the previous batch's last round: a flag in its
+            // headers halts this batch's first round, and the recovery needs it
+            SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &e->d_ring[B], sizeof(DevSummary), hipMemcpyDeviceToDevice,
+                                   e->stream));
+            e->h_seed[1] = host_fresh_summary();
+            e->h_ctl->stop = stop;
+            e->h_ctl->round_base = e->round;
+            SHD_HIP(hipMemcpyAsync(&e->d_ring[1], &e->h_seed[1], sizeof(DevSummary), hipMemcpyHostToDevice,
+                                   e->stream));
+            SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
+            SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
+        }
+        for (int i = 0; i < B; i++) {
+            const int ri = (int)((g->xseq - 1) & 1);
+            for (int k = 0; k < nl; k++) {
+                shd_eng* e = g->engs[k];
+                const Params P = xparams(g, k, &e->d_ring[i + 1]);
+                const int grid = (e->nloc + P.hpw - 1) / P.hpw;
+                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, P,
+                                   (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
+                                   (const DevCtl*)e->d_ctl, i, g->window);
+            }
+            if ((rc = x_exchange(g))) return rc;
+            const int wi = (int)((g->xseq - 1) & 1);
+            for (int k = 0; k < nl; k++) {
+                shd_eng* e = g->engs[k];
+                const Params P = xparams(g, k, &e->d_ring[i + 1]);
+                const uint64_t nthr = (uint64_t)g->world * g->xcap;
+                hipLaunchKernelGGL(k_ingest_x, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, P,
+                                   (const shd_event*)g->loc[k].xrecv[wi], (const DevCtl*)e->d_ctl, i);
+            }
+        }
+        SHD_HIP(hipGetLastError());
+        for (int k = 0; k < nl; k++) {
+            shd_eng* e = g->engs[k];
+            SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost,
+                                   e->stream));
+        }
+        for (int k = 0; k < nl; k++) SHD_HIP(hipStreamSynchronize(g->engs[k]->stream));
+        int halted_at = -1;
+        bool done = false;
+        for (int i = 0; i < B; i++) {
+            const DevSummary& r0 = g->engs[0]->h_ring[i + 1];
+            if (r0.flags == 1u) { halted_at = i; break; }
+            if (r0.flags != 0u) break;   // skipped: cannot precede a halt
+            if (r0.ws >= stop) {
+                g->next = r0.ws;
+                done = true;
+                break;
+            }
+            s.n_rounds++;
+            uint64_t we = r0.ws + g->window;
+            if (we > stop || we < r0.ws) we = stop;
+            s.final_time = we;
+            for (int k = 0; k < nl; k++) {
+                shd_eng* e = g->engs[k];
+                const DevSummary& r = e->h_ring[i + 1];
+                s.n_events += r.n_events;
+                s.n_pkt_events += r.n_pkt_events;
+                const double ms = round_kernel_ms(e, r);
+                kms += ms;
+                e->last_kernel_ms = ms;
+                e->round++;
+                e->parity = (int)(e->round & 1);
+            }
+        }
+        if (done) break;
+        if (halted_at < 0) {
+            if ((rc = x_read_next(g))) break;
+            continue;
+        }
+        // the round before halted_at (ring slot halted_at) was flagged somewhere in the group
+        const int slot = halted_at;
+        std::vector<XHeader> hh(g->world);
+        SHD_HIP(hipMemcpy(hh.data(), g->loc[0].halt_hdr, sizeof(XHeader) * g->world, hipMemcpyDeviceToHost));
+        uint32_t fl = 0;
+        uint32_t errs = 0;
+        for (const XHeader& x : hh) {
+            fl |= x.flags;
+            errs |= x.error;
+        }
+        if (fl & XF_ERROR) {
+            s.error = errs;
+            rc = (errs & SHD_ERR_AMBIGUOUS) ? SHD_EAMBIG : SHD_EOVERFLOW;
+            break;
+        }
+        if (fl & XF_PENDING) {
+            std::vector<shd_pending> all;
+            for (int k = 0; k < nl; k++) g->engs[k]->round_pending = g->engs[k]->h_ring[slot].n_pending;
+            if ((rc = x_gather_pending(g, all))) break;
+            for (int k = 0; k < nl && !rc; k++) {
+                shd_eng* e = g->engs[k];
+                DevSummary* const keep = e->P.sum;
+                e->P.sum = &e->d_ring[slot];           // the flagged round's summary; remote -> e->P.remote
+                e->parity = (int)((e->round - 1) & 1);  // the flagged round's parity
+                rc = shd_eng_resolve(e, all.data(), all.size());
+                e->P.sum = keep;
+                e->parity = (int)(e->round & 1);
+            }
+            if (rc) break;
+            for (int k = 0; k < nl; k++) SHD_HIP(hipStreamSynchronize(g->engs[k]->stream));
+        }
+        if ((rc = x_exchange_remote(g, slot))) break;
+        if ((fl & XF_OVERFLOW) && !g->fixed_cap) {
+            // spills in two consecutive batches: the blocks are too small for
+            // this traffic, not just for a burst.  Every rank sees the same
+            // flags in the same batch, so all grow alike.
+            if (g->last_spill_batch != ~0ull && g->batches - g->last_spill_batch <= 1 && g->xcap < (1u << 22)) {
+                g->xcap *= 2;
+                if ((rc = x_alloc(g))) break;
+            }
+            g->last_spill_batch = g->batches;
+        }
+        // fresh headers: next event times after the recovery, no flags
+        for (int k = 0; k < nl; k++) {
+            shd_eng* e = g->engs[k];
+            SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
+            hipLaunchKernelGGL(k_xpack, dim3(1), dim3(64), 0, e->stream, xparams(g, k, &e->d_ring[slot]),
+                               (const DevSummary*)&e->d_ring[slot], 1);
+        }
+        if ((rc = x_exchange(g))) break;
+        for (int k = 0; k < nl; k++) {
+            DevSummary r;
+            shd_eng* e = g->engs[k];
+            SHD_HIP(hipMemcpyAsync(&r, &e->d_ring[slot], sizeof(r), hipMemcpyDeviceToHost, e->stream));
+            SHD_HIP(hipStreamSynchronize(e->stream));
+            if (r.error) {
+                s.error |= r.error;
+                rc = (r.error & SHD_ERR_AMBIGUOUS) ? SHD_EAMBIG : SHD_EOVERFLOW;
+            }
+        }
+        if (rc) break;
+        if ((rc = x_read_next(g))) break;
+    }
+    for (int k = 0; k < nl; k++) {
+        shd_eng* e = g->engs[k];
+        e->h_sum->next_time = g->next;
+        s.n_pending_resolved += e->pending_resolved - pend0[k];
+    }
+    s.device_ms_round_kernel = kms;
+    s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) *st = s;
+    return rc;
 }

@@ -15,6 +15,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SHDGPU_LIB") or os.path.join(HERE, "libshdgpu.so")   # override: profiling build
 
+SHD_XID_BYTES = 128
 SHD_MS = 1_000_000
 SHD_SEC = 1_000_000_000
 SHD_MTU = 1500
@@ -197,6 +198,13 @@ _SIGS = {
     "shd_eng_destroy": (None, [C.c_void_p]),
     "shd_version": (C.c_char_p, []),
     "shd_device_count": (C.c_int, [P(C.c_int)]),
+    "shd_xgroup_unique_id": (C.c_int, [P(C.c_uint8)]),
+    "shd_xgroup_create_rccl": (C.c_int, [C.c_void_p, P(C.c_uint8), C.c_int, C.c_int, C.c_uint32,
+                                         P(C.c_void_p)]),
+    "shd_xgroup_create_local": (C.c_int, [P(C.c_void_p), C.c_int, C.c_uint32, P(C.c_void_p)]),
+    "shd_xgroup_run_until": (C.c_int, [C.c_void_p, C.c_uint64, P(RunStats)]),
+    "shd_xgroup_next_time": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    "shd_xgroup_destroy": (None, [C.c_void_p]),
 }
 
 _lib = None

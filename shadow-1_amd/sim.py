@@ -190,6 +190,65 @@ class Engine:
             pass
 
 
+class XGroup:
+    """Engines stepping rounds together with one fixed-size all-to-all per
+    round (shd_xgroup, DESIGN.md "Multi-GPU").  `local(engines)`: all engines
+    in this process (device-to-device copies); `rccl(engine, uid, world,
+    rank)`: one engine per process over RCCL (uid from `unique_id()` on rank 0,
+    shared by every rank)."""
+
+    def __init__(self, ptr, engines):
+        self.ptr = ptr
+        self.engines = engines
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * S.SHD_XID_BYTES)()
+        S.check(S.lib().shd_xgroup_unique_id(buf), "shd_xgroup_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def local(cls, engines, block_events=0):
+        arr = (C.c_void_p * len(engines))(*[e.ptr.value for e in engines])
+        ptr = C.c_void_p()
+        S.check(S.lib().shd_xgroup_create_local(arr, len(engines), int(block_events), C.byref(ptr)),
+                "shd_xgroup_create_local")
+        return cls(ptr, list(engines))
+
+    @classmethod
+    def rccl(cls, engine, uid: bytes, world, rank, block_events=0):
+        buf = (C.c_uint8 * S.SHD_XID_BYTES).from_buffer_copy(uid)
+        ptr = C.c_void_p()
+        S.check(S.lib().shd_xgroup_create_rccl(engine.ptr, buf, int(world), int(rank), int(block_events),
+                                               C.byref(ptr)), "shd_xgroup_create_rccl")
+        return cls(ptr, [engine])
+
+    def run_until(self, t_stop) -> S.RunStats:
+        st = S.RunStats()
+        rc = S.lib().shd_xgroup_run_until(self.ptr, int(t_stop), C.byref(st))
+        S.check(rc, f"shd_xgroup_run_until (error bits {st.error:#x})")
+        return st
+
+    def run(self) -> S.RunStats:
+        return self.run_until(self.engines[0].model.params["end_time"])
+
+    def next_time(self) -> int:
+        t = C.c_uint64()
+        S.check(S.lib().shd_xgroup_next_time(self.ptr, C.byref(t)), "shd_xgroup_next_time")
+        return t.value
+
+    def close(self):
+        if self.ptr:
+            S.lib().shd_xgroup_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def sort_trace(tr: np.ndarray) -> np.ndarray:
     """Canonical order for multiset comparison of traces."""
     return np.sort(tr, order=["time", "host", "kind", "peer", "pkt", "seq"])

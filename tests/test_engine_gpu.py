@@ -124,3 +124,49 @@ def test_sharded_engines_match_oracle(parts):
     assert res.pkt_events == ost["n_pkt_events"]
     assert np.array_equal(tr, sort_trace(otr))
     assert np.array_equal(dg, odg)
+
+
+@pytest.mark.parametrize("parts,block", [(2, 0), (3, 0), (4, 6), (2, 1)])
+def test_engine_group_local_matches_oracle(parts, block):
+    """shd_xgroup (one fixed-size all-to-all per round, device-driven batches)
+    with the in-process transport: several engines on one GPU.  Small blocks
+    force spills, so the halt + host delivery path runs too; stopping and
+    resuming at arbitrary times must not change anything."""
+    from driver import partition
+    from sim import XGroup
+    g = W.geometric_graph(240, seed=6)
+    m = W.phold_model(W.hosts_on_vertices(240, 1), end_time=3 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    pb = partition(m.n_hosts, parts)
+    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
+    grp = XGroup.local(engines, block_events=block)
+    pkt = pend = 0
+    for t in (int(0.7 * S.SHD_SEC), int(1.0 * S.SHD_SEC) + 3, 2 * S.SHD_SEC, m.params["end_time"]):
+        st = grp.run_until(t)
+        pkt += st.n_pkt_events
+        pend += st.n_pending_resolved
+    assert pend > 0
+    tr = sort_trace(np.concatenate([e.trace() for e in engines]))
+    dg = np.concatenate([e.digest() for e in engines])
+    otr, odg, ost = O.engine_run(m, g)
+    assert pkt == ost["n_pkt_events"]
+    assert np.array_equal(tr, sort_trace(otr))
+    assert np.array_equal(dg, odg)
+    grp.close()
+
+
+def test_engine_group_rccl_single_rank():
+    """The RCCL transport end to end with one rank (the multi-rank case needs
+    one GPU per rank: RCCL refuses two ranks on one device)."""
+    from sim import XGroup
+    g = W.geometric_graph(200, seed=9)
+    m = W.phold_model(W.hosts_on_vertices(200, 1), end_time=2 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    eng = Engine(m, pc)
+    grp = XGroup.rccl(eng, XGroup.unique_id(), 1, 0)
+    st = grp.run()
+    otr, odg, ost = O.engine_run(m, g)
+    assert st.n_pkt_events == ost["n_pkt_events"]
+    assert np.array_equal(sort_trace(eng.trace()), sort_trace(otr))
+    assert np.array_equal(eng.digest(), odg)
+    grp.close()
