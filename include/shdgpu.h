@@ -219,8 +219,12 @@ typedef struct shd_model {
     uint32_t inbox_cap;             /* per-host per-round inbound capacity     */
     uint32_t codelq_cap;            /* per-host router queue capacity          */
     uint32_t txq_cap;               /* per-host interface send queue capacity  */
-    uint32_t _pad1;
+    uint32_t queue_flags;           /* SHD_QF_*: 0 = default (calendar + heap) */
 } shd_model;
+
+/* queue_flags: SHD_QF_NO_CALENDAR routes every inter-host event through the
+ * per-host inbox and heap (the calendar's fallback path), for testing */
+enum { SHD_QF_NO_CALENDAR = 1 };
 
 /* one event (32 B): key (time, dst, src, seq) = event_compare, event.c:110-153 */
 typedef struct shd_event {

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Per-block phase stamps of the round kernel (timing build).
+
+    make -C shadow-1_amd timing
+    SHDGPU_LIB=shadow-1_amd/libshdgpu_tim.so python scripts/round_timing.py
+
+Stamps (100 MHz wall clock, relative to the round's first kernel entry):
+0 kernel entry, 1 round body (after halt/ctl/prev loads), 2 after the idle
+check, 3 after the active hosts' processing, 4 after the block reduction,
+5 after the last-block ticket, 6 last block after the first-touch resolve.
+"""
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "shadow-1_amd")]
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vertices", type=int, default=10000)
+    ap.add_argument("--hosts", type=int, default=10000)
+    ap.add_argument("--load", type=int, default=16)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    import shdgpu as S
+    import workloads as W
+    from sim import Engine, PathCache
+    lib = S.lib()
+    f = lib.shd_debug_timing
+    f.restype = C.c_int
+    f.argtypes = [C.POINTER(C.c_uint64)]
+    g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0005)
+    hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
+    m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load, payload=1)
+    pc = PathCache(g, W.attached_vertices(hv), device=0)
+    pc.build()
+    eng = Engine(m, pc, 0, a.hosts, device=0)
+    eng.boot()
+    eng.run_until(2 * S.SHD_SEC)
+    st = eng.run_until(int(2.5 * S.SHD_SEC))
+    buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
+    f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
+    t = buf.reshape(64, 2048, 20).astype(np.int64)
+    grid = (a.hosts + 63) // 64
+    t = t[:, :grid, :]
+    print(f"kernel {st.device_ms_round_kernel / max(st.n_rounds, 1) * 1e3:.1f} us/round (in-kernel stamps), "
+          f"wall {st.wall_ms / max(st.n_rounds, 1) * 1e3:.1f} us/round, grid {grid}")
+    names = ["entry", "body", "idle-chk", "active", "reduce", "ticket", "resolve"]
+    rows = []
+    keep = []
+    for r in range(64):
+        x = t[r]
+        if (x[:, 0] == 0).any() or (x[:, 1:6] < x[:, :1]).any():
+            continue   # a forward-only round (stamp 0 only) or stale stamps
+        t0 = x[:, 0].min()
+        rel = (x[:, :11] - t0) / 100.0   # us
+        fresh = (x[:, 7:11] >= t0).all(axis=1, keepdims=True)   # stale stamps: no active host this round
+        rel[:, 7:11] = np.where(fresh, rel[:, 7:11], 0)
+        rows.append(rel)
+        keep.append(r)
+    rows = np.array(rows)   # rounds x blocks x 8
+    print(f"{len(rows)} rounds; us from the round's first kernel entry: mean over rounds of (mean, max over blocks)")
+    for k in range(6):
+        v = rows[:, :, k]
+        print(f"  {names[k]:9s} mean {v.mean():6.2f}  max {v.max(axis=1).mean():6.2f}")
+    last = rows[:, :, 6].max(axis=1)
+    print(f"  {names[6]:9s} (last block) {last.mean():6.2f}")
+    # inside the active section (first active lane's stamps; blocks with an active host)
+    act = rows[:, :, 9] > 0
+    for k0, k1, nm in ((2, 7, "load_ctx"), (7, 8, "bins+merge"), (8, 9, "event loop"), (9, 10, "cal clear+next"),
+                       (10, 3, "store ctx")):
+        d = (rows[:, :, k1] - rows[:, :, k0])
+        print(f"  {nm:15s} per block: mean {d[act].mean():7.2f} max {np.where(act, d, 0).max(axis=1).mean():7.2f} us")
+    raw = t[keep][:, :, 11:18].astype(np.float64)
+    ok = raw[:, :, 4] > 0
+    loopw = rows[:, :, 9] - rows[:, :, 8]   # us (wall) of the event loop
+    ghz = raw[:, :, 4][ok & act].sum() / (loopw[ok & act].sum() * 1e3) if (ok & act).any() else 0
+    print(f"  loop iterations/wave (max lane) mean {raw[:, :, 0][ok].mean():.1f} max {raw[:, :, 0].max():.0f}; "
+          f"clock64 rate {ghz:.2f} GHz")
+    tot = raw[:, :, 4][ok].mean()
+    for j, nm in ((1, "take_next"), (2, "begin_event"), (3, "run_work"), (5, "flush_wave"), (6, "inner loops")):
+        print(f"    {nm:12s} {raw[:, :, j][ok].mean():9.0f} cyc/wave ({100 * raw[:, :, j][ok].mean() / tot:4.1f}% of loop "
+              f"{tot:.0f}); per iteration {raw[:, :, j][ok].sum() / raw[:, :, 0][ok].sum():7.0f}")
+    d = rows[:, :, 3] - rows[:, :, 2]
+    print(f"  active-phase duration per block: mean {d.mean():.2f} max {d.max(axis=1).mean():.2f} us")
+    d = rows[:, :, 5] - rows[:, :, 3]
+    print(f"  reduce+ticket per block: mean {d.mean():.2f} max {d.max(axis=1).mean():.2f} us")
+    eng.close()
+    pc.close()
+
+
+if __name__ == "__main__":
+    main()

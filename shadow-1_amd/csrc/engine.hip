@@ -47,16 +47,67 @@ constexpr uint32_t F_REFILL_PENDING = 1u, F_NOTIFY_PENDING = 2u, F_LISTENING = 4
 constexpr double kRandMax = 2147483647.0;
 constexpr uint64_t kCodelTarget = 10ull * SHD_MS;      // router_queue_codel.c:42
 constexpr uint64_t kCodelInterval = 100ull * SHD_MS;   // router_queue_codel.c:48
+// calendar geometry: bins per host (a ring), event slots per bin, bitmap
+// words, and the append horizon in bins ahead of the round's first bin.  The
+// horizon stops short of the ring by 4 so that no append in round r can land
+// in a slot the owner reads or clears in round r or r+1.
+constexpr uint32_t kNB = 256, kBinCap = 4, kNBW = kNB / 32, kHorizon = kNB - 4;
+constexpr int kDueCap = 8;             // due-list slots per host (more due events take the heap)
+constexpr int kSendCap = 8;            // deferred sends per host between flushes (<= 16)
+constexpr int kBlock = 64;             // round-kernel workgroup: one wave, one host per lane
 
 struct CodelEnt {
     uint64_t ts;
     uint32_t src;
     uint32_t pkt;
 };
+// send-FIFO entry: the destination draw (rand_r value; the destination itself
+// is resolved when the send is flushed) and the packet id
 struct TxEnt {
-    uint32_t dst;
+    uint32_t r;
     uint32_t pkt;
 };
+
+// A send whose destination, path lookup and drop decision are deferred to the
+// host's next flush (flush_sends).  The host's own control flow never depends
+// on them: the RNG draws are made at send time, loopback is decided from the
+// host's own cumulative-weight interval, and the event ID a passing send
+// consumes is handled with provisional IDs fixed up at the flush.
+struct SendRec {
+    uint64_t now;      // send time
+    uint64_t q_seq;    // the executing event's seq (first-touch log key)
+    uint32_t q_src;    // the executing event's src
+    uint32_t pseq;     // provisional event ID - seq_base
+    uint32_t r;        // destination draw (rand_r value)
+    uint32_t chance;   // reliability draw (rand_r value)
+    uint32_t pkt;
+    uint32_t q_sub;    // send index within the executing event; bit 31: bootstrapping
+};
+static_assert(sizeof(SendRec) == 40, "send record layout");
+
+// Per-host state record in HBM (local host index).  The round kernel reads
+// and writes it whole, as 13 16-B accesses; it holds every field the host's
+// event handling mutates except the queues' contents.
+struct alignas(16) HostRec {
+    uint64_t ev_seq;                       // host_getNewEventID counter (host.c:397)
+    uint64_t cq_total, cq_iexp, cq_ndrop;  // CoDel: bytes queued, interval expiry, next drop
+    uint64_t rx_rem, tx_rem;               // token buckets: bytes remaining
+    uint64_t tt[3], ts[3];                 // timer slots (heartbeat, refill, notify): time, event ID
+    uint64_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;   // counters
+    uint32_t rng, pkt_seq;                 // rand_r state, packet counter
+    uint32_t rx_refill, tx_refill;         // token-bucket refill per 1 ms (bytes)
+    uint32_t flags, unread;
+    uint32_t cq_dc, cq_dcl, cq_head, cq_count;   // CoDel drop counts, FIFO head / length
+    uint32_t tq_head, tq_count, evq_n, pad[3];
+};
+static_assert(sizeof(HostRec) == 208, "host record: 13 x 16 B");
+
+// a block's share of the round summary (round_complete)
+struct BlockPart {
+    unsigned long long next, nev, npkt;
+    unsigned int err, pad;
+};
+constexpr uint32_t kTickGroup = 64;   // blocks per first-level completion ticket
 
 // a send whose (src,dst) pair was unranked at round start (include/shdgpu.h)
 using Pending = shd_pending;
@@ -111,9 +162,11 @@ constexpr uint32_t XF_PENDING = 1u, XF_OVERFLOW = 2u, XF_ERROR = 4u;
 // even-weight pick resolves in one 32-B load
 struct DestGuide {
     int32_t i;
-    int32_t pad;
+    int32_t att[3];  // attached-vertex index of hosts i .. i+2 (-1 past the end)
     double cum[3];   // dest_cum[i .. i+2], 2.0 past the end
+    double pad;
 };
+static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 
 struct Params {
     // hosts
@@ -123,48 +176,35 @@ struct Params {
     uint32_t evq_cap, inbox_cap, cq_cap, tq_cap;
     uint64_t end_time, bootstrap_end, heartbeat, app_start;
     uint32_t load, payload, trace, pkt_len;
-    // per-host state (local index)
-    uint32_t* rng;
-    uint64_t* ev_seq;
-    uint32_t* pkt_seq;
-    uint64_t* rx_rem;
-    uint64_t* tx_rem;
-    uint64_t* rx_refill;
-    uint64_t* tx_refill;
-    uint32_t* flags;
-    uint32_t* unread;
-    uint64_t* cq_total;
-    uint64_t* cq_iexp;
-    uint64_t* cq_ndrop;
-    uint32_t* cq_dc;
-    uint32_t* cq_dcl;
-    uint32_t* cq_head;
-    uint32_t* cq_count;
-    uint32_t* tq_head;
-    uint32_t* tq_count;
-    uint64_t* c_events;
-    uint64_t* c_pkt;
-    uint64_t* c_sent;
-    uint64_t* c_idrop;
-    uint64_t* c_cdrop;
-    uint64_t* c_recv;
-    // timer slots: the self events with at most one pending instance per host
-    // (heartbeat, token-bucket refill, epoll notification) as (time, seq)
-    uint64_t* tm_time[3];
-    uint64_t* tm_seq[3];
-    uint64_t* hnext;             // per-host earliest pending event (timers, heap)
+    // per-host state records (local index), and the earliest pending event
+    // of each host's timers and heap (read alone by the idle test)
+    HostRec* hs;
+    uint64_t* hnext;
     // queues: per-host 4-ary heap of the other events (packets, loopback, boot one-shots)
     shd_event* evq;              // slab of evq_stride entries per host, heap at +3
-    uint32_t* evq_n;
     uint32_t evq_stride;
     shd_event* inbox[2];
     uint32_t* inbox_n[2];
+    // round completion (round_complete): per-block and per-group summary
+    // shares, and the two-level tickets (reset by the blocks that win them)
+    BlockPart* part;
+    BlockPart* gpart;
+    uint32_t* tick;
+    // calendar (null = off): per host a ring of kNB time bins of width
+    // 2^bin_shift <= W ns with kBinCap event slots each.  Senders append with
+    // one atomic on the bin's count; the owner reads the <= 3 bins of its
+    // window in one pass.  Far-future events and full bins take the inbox.
+    shd_event* bins;             // [nloc][kNB][kBinCap]
+    uint32_t* bin_n;             // [nloc][kNB] appends (may exceed kBinCap: those went to the inbox)
+    uint32_t* bin_bits;          // [nloc][kNBW] non-empty bins
+    uint32_t bin_shift;
     CodelEnt* cq;
     TxEnt* tq;
     // global host tables (all H hosts)
     const int32_t* host_att;     // attached index of every host
     const double* dest_cum;
     const struct DestGuide* dest_guide;   // [H]: bucket k -> first i with dest_cum[i] >= k / H
+    double cum_last;             // dest_cum[H-1]: a draw above it has no destination
     // path cache
     int32_t T;
     int32_t complete, prefer_direct, directed;
@@ -208,6 +248,34 @@ enum {
     PR_TOTAL, PR_LOAD, PR_MERGE, PR_POP, PR_EXEC_PKT, PR_EXEC_NOTIFY, PR_EXEC_REFILL, PR_EXEC_OTHER, PR_PICK,
     PR_SEND, PR_STORE, PR_NEV, PR_N
 };
+#ifdef SHD_TIMING
+// -DSHD_TIMING (make timing -> libshdgpu_tim.so, scripts/round_timing.py):
+// wall-clock stamps per block at the round's phase boundaries, 64 round slots
+// keyed by the summary address x 2048 blocks x 8 stamps
+__device__ unsigned long long g_tim[64][2048][20];
+#define TIM(k)                                                                                         \
+    do {                                                                                               \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+        if (threadIdx.x == 0 && blockIdx.x < 2048)                                                     \
+            g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = wall_clock64();       \
+    } while (0)
+// inside a divergent region: the first active lane stamps
+#define TIMA(k)                                                                                        \
+    do {                                                                                               \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+        if ((int)threadIdx.x == __ffsll((unsigned long long)__ballot(1)) - 1 && blockIdx.x < 2048)     \
+            g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = wall_clock64();       \
+    } while (0)
+#define TIMV(k, v)                                                                                     \
+    do {                                                                                               \
+        if ((int)threadIdx.x == __ffsll((unsigned long long)__ballot(1)) - 1 && blockIdx.x < 2048)     \
+            g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = (v);                  \
+    } while (0)
+#else
+#define TIM(k)
+#define TIMA(k)
+#define TIMV(k, v)
+#endif
 #ifdef SHD_PROF
 __device__ unsigned long long g_prof[2 * PR_N + 2];
 // per-round wave timing (100 MHz wall clock), 128 round slots keyed by the
@@ -235,7 +303,6 @@ __device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
     r = (r << 10) ^ ((x >> 16) & 1023u);
     return (int32_t)r;
 }
-__device__ __forceinline__ double next_double_dev(uint32_t& x) { return (double)rand_r_dev(x) / kRandMax; }
 
 // --------------------------------------------------------------- per-host context
 struct HostCtx {
@@ -253,6 +320,15 @@ struct HostCtx {
     uint32_t tq_head, tq_count;
     uint32_t evq_n;
     shd_event top;              // heap root (valid when evq_n > 0)
+    shd_event* due;             // this lane's sorted calendar events of the window (LDS, stride 64)
+    uint32_t dh, nd;            // next / count of due events
+    shd_event dtop;             // due[dh] (valid when dh < nd)
+    SendRec* sq;                // this lane's deferred sends (LDS, stride 64)
+    uint32_t ns;                // deferred sends
+    uint64_t seq_base;          // ev_seq at the last flush: IDs >= it are provisional
+    double cum_lo, cum_hi;      // dest_cum[h-1] (-1 for h = 0), dest_cum[h]: loopback test
+    uint32_t w_msgs;            // the executing event's remaining work (run_work)
+    bool w_rx, w_tx, w_refill, w_sending;
     uint64_t tt0, tt1, tt2;     // timer times (kInf = empty): heartbeat, refill, notify
     uint64_t ts0, ts1, ts2;     // timer event IDs
     CodelEnt cq_hint;           // CoDel head entry held in registers (not yet stored)
@@ -265,6 +341,9 @@ struct HostCtx {
     uint32_t q_src;
     uint32_t q_sub;
     uint64_t min_emit;   // min time of events sent to other hosts
+    uint64_t ws;         // the round's window start (calendar append horizon)
+    uint32_t ws_mod;     // ws % 1 ms (refill alignment)
+    int np;              // the next round's inbox parity
     uint32_t err;
     uint32_t n_pend;
 #ifdef SHD_PROF
@@ -344,6 +423,10 @@ __device__ __forceinline__ bool bootstrapping(const Params& P, const HostCtx& c)
 // event_new_ (consumes the source's event ID, event.c:38) + scheduler_push
 // (discards time >= end, scheduler.c:346-349) for a self event
 __device__ void schedule_self(const Params& P, HostCtx& c, uint32_t kind, uint64_t delay, uint32_t pkt) {
+    // heap events carry exact IDs: the send loop flushes the deferred sends
+    // before a loopback send (timer slots may hold provisional IDs, fixed up
+    // by the flush)
+    if (kind != SHD_EV_HEARTBEAT && kind != SHD_EV_REFILL && kind != SHD_EV_NOTIFY && c.ns) c.err |= SHD_ERR_INTERNAL;
     shd_event e;
     e.time = c.now + delay;
     e.seq = c.ev_seq++;
@@ -370,16 +453,35 @@ __device__ void schedule_self(const Params& P, HostCtx& c, uint32_t kind, uint64
     }
 }
 
-// deliver an inter-host event: to the destination's inbox for the next round,
-// or to the remote outbox when the destination lives on another engine
-__device__ void emit_remote(const Params& P, HostCtx& c, const shd_event& e, int next_parity) {
-    if (e.time >= P.end_time) return;
-    if (e.time < c.min_emit) c.min_emit = e.time;
+// append an event of a later round to local host dl's calendar; false when it
+// is beyond the horizon of the round starting at `ws` or the bin is full (the
+// caller then takes the inbox).  The event is stored before the bin's bit is
+// set; readers filter slots by time, so a slot claimed but not yet written
+// (time still that of an older, processed event, or kInf) is never taken.
+__device__ __forceinline__ bool cal_push(const Params& P, int32_t dl, const shd_event& e, uint64_t ws) {
+    if (!P.bins) return false;
+    const uint64_t b = e.time >> P.bin_shift;
+    if (b - (ws >> P.bin_shift) > kHorizon) return false;
+    const uint32_t p = (uint32_t)b & (kNB - 1);
+    const size_t bi = (size_t)dl * kNB + p;
+    const uint32_t s = atomicAdd(&P.bin_n[bi], 1u);
+    if (s >= kBinCap) return false;
+    P.bins[bi * kBinCap + s] = e;
+    atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));
+    return true;
+}
+
+// deliver an inter-host event: to the destination's calendar (or inbox) for a
+// later round, or to the remote outbox when it lives on another engine
+// the calendar-less part of a delivery: the inbox of a local destination
+// (merged into its heap next round), else the peer's all-to-all block or the
+// remote outbox
+__device__ void emit_nocal(const Params& P, HostCtx& c, const shd_event& e) {
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl >= 0 && dl < P.nloc) {
-        uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
+        uint32_t slot = atomicAdd(&P.inbox_n[c.np][dl], 1u);
         if (slot >= P.inbox_cap) { c.err |= SHD_ERR_INBOX_OVERFLOW; return; }
-        P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
+        P.inbox[c.np][(size_t)dl * P.inbox_cap + slot] = e;
     } else {
         if (P.xsend) {   // exchange mode: straight into the peer's all-to-all block
             const int32_t peer = owner_of(P, e.dst);
@@ -402,7 +504,9 @@ __device__ void emit_remote(const Params& P, HostCtx& c, const shd_event& e, int
 __device__ void refill_if_needed(const Params& P, HostCtx& c) {
     const bool need = (c.tx_rem < c.tx_refill + SHD_MTU) || (c.rx_rem < c.rx_refill + SHD_MTU);
     if (need && !(c.flags & F_REFILL_PENDING)) {
-        const uint64_t until = SHD_MS - (c.now % SHD_MS);
+        // now % 1 ms from the round's ws % 1 ms and the 32-bit offset into the round
+        const uint32_t off = (uint32_t)(c.now - c.ws) + c.ws_mod;
+        const uint64_t until = SHD_MS - (off % (uint32_t)SHD_MS);
         schedule_self(P, c, SHD_EV_REFILL, until, 0);
         c.flags |= F_REFILL_PENDING;
     }
@@ -510,108 +614,290 @@ struct PathVal {
     bool log;            // the query must be logged for rank assignment
 };
 
-__device__ PathVal path_value(const Params& P, int32_t a, int32_t b) {
+// the raw candidates of a path value, loaded in one round trip (the mode
+// branches are uniform: kernel parameters); path_select applies the rank rule
+struct PathRaw {
+    shd_pv d, v1, v2;   // direct; row[a][b] (a == b: row[a][a]); row[b][a] (a == b: self[a])
+    int32_t rb, rs;     // rank[b], self_rank[a] (a == b)
+    uint32_t adj;
+};
+
+__device__ __forceinline__ void path_load(const Params& P, int32_t a, int32_t b, PathRaw& x) {
+    const size_t ab = (size_t)a * P.T + b, ba = (size_t)b * P.T + a;
+    x.adj = 0; x.rb = kNoRank; x.rs = kNoRank;
+    if (P.complete) { x.d = P.dir[ab]; return; }
+    if (P.prefer_direct) { x.adj = P.adj[ab]; x.d = P.dir[ab]; }
+    x.v1 = P.row[ab];
+    if (a == b) {
+        x.rs = P.self_rank[a];
+        x.v2 = P.self[a];
+    } else {
+        x.rb = P.rank[b];
+        x.v2 = P.row[ba];
+    }
+}
+
+__device__ __forceinline__ PathVal path_select(const Params& P, int32_t a, int32_t b, int32_t ra, const PathRaw& x) {
     PathVal v;
     v.resolved = true;
     v.log = false;
-    const size_t ab = (size_t)a * P.T + b, ba = (size_t)b * P.T + a;
-    if (P.complete || (P.prefer_direct && P.adj[ab])) {
-        const shd_pv d = P.dir[ab];
-        v.lat = d.lat; v.rel = d.rel;
+    if (P.complete || (P.prefer_direct && x.adj)) {
+        v.lat = x.d.lat; v.rel = x.d.rel;
         return v;
     }
-    // every candidate is loaded in one round trip; the rank rule picks after
-    const int32_t ra = P.rank[a];
     if (a == b) {
-        const int32_t rs = P.self_rank[a];
-        const shd_pv s = P.self[a], r = P.row[ab];
-        if (ra == kNoRank && rs == kNoRank) {
+        const shd_pv& sp = x.v2;   // self[a]
+        const shd_pv& r = x.v1;    // row[a][a]
+        if (ra == kNoRank && x.rs == kNoRank) {
             v.resolved = false; v.log = true;
-            v.lat = s.lat; v.rel = s.rel;
+            v.lat = sp.lat; v.rel = sp.rel;
             v.lat2 = r.lat; v.rel2 = r.rel;
-        } else if (rs < ra) {
-            v.lat = s.lat; v.rel = s.rel;
+        } else if (x.rs < ra) {
+            v.lat = sp.lat; v.rel = sp.rel;
         } else {
             v.lat = r.lat; v.rel = r.rel;
         }
         return v;
     }
-    const int32_t rb = P.rank[b];
-    const shd_pv vab = P.row[ab], vba = P.row[ba];
-    if (ra == kNoRank && rb == kNoRank) {
+    if (ra == kNoRank && x.rb == kNoRank) {
         v.resolved = false; v.log = true;
-        v.lat = vab.lat; v.rel = vab.rel;
-        v.lat2 = vba.lat; v.rel2 = vba.rel;
+        v.lat = x.v1.lat; v.rel = x.v1.rel;
+        v.lat2 = x.v2.lat; v.rel2 = x.v2.rel;
         return v;
     }
     if (P.directed && ra == kNoRank) v.log = true;   // row a still runs (directed rerun rule)
-    const shd_pv& w = ra < rb ? vab : vba;
+    const shd_pv& w = ra < x.rb ? x.v1 : x.v2;
     v.lat = w.lat; v.rel = w.rel;
     return v;
 }
 
-__device__ void log_pending(const Params& P, HostCtx& c, int32_t a, int32_t b, uint32_t delivered, uint32_t dst,
-                            uint32_t pkt, uint64_t seq) {
+__device__ PathVal path_value(const Params& P, int32_t a, int32_t b) {
+    PathRaw x;
+    const int32_t ra = P.complete ? kNoRank : P.rank[a];
+    path_load(P, a, b, x);
+    return path_select(P, a, b, ra, x);
+}
+
+__device__ void log_pending(const Params& P, HostCtx& c, const SendRec& q, int32_t a, int32_t b, uint32_t delivered,
+                            uint32_t dst, uint64_t seq) {
     unsigned long long i = atomicAdd(&P.sum->n_pending, 1ull);
     c.n_pend++;
     if (i >= P.pend_cap) { c.err |= SHD_ERR_PENDING_OVERFLOW; return; }
     Pending r;
-    r.qtime = c.now; r.qseq = c.q_seq; r.qhost = c.h; r.qsrc = c.q_src; r.qsub = c.q_sub++;
-    r.a = (uint32_t)a; r.b = (uint32_t)b; r.delivered = delivered; r.dst = dst; r.pkt = pkt; r.seq = seq;
+    r.qtime = q.now; r.qseq = q.q_seq; r.qhost = c.h; r.qsrc = q.q_src; r.qsub = q.q_sub & 0x7FFFFFFFu;
+    r.a = (uint32_t)a; r.b = (uint32_t)b; r.delivered = delivered; r.dst = dst; r.pkt = q.pkt; r.seq = seq;
     P.pend[i] = r;
 }
 
-// worker_sendPacket (worker.c:260-321)
-__device__ void worker_send_packet(const Params& P, HostCtx& c, uint32_t dst, uint32_t pkt, int next_parity) {
-    const int32_t a = c.att, b = P.host_att[dst];
-    const PathVal pv = path_value(P, a, b);
-    const double chance = next_double_dev(c.rng);
-    const bool boot = bootstrapping(P, c);
-    const bool pass = boot || chance <= pv.rel || P.payload == 0;
-    if (!pv.resolved) {
-        const bool pass2 = boot || chance <= pv.rel2 || P.payload == 0;
-        if (pass != pass2) c.err |= SHD_ERR_AMBIGUOUS;
-    }
-    if (pass) {
-        const uint64_t seq = c.ev_seq++;
-        trace(P, c, c.now, seq, c.h, dst, pkt, SHD_TR_SENT);
-        c.c_sent++;
-        if (pv.log) {
-            // 1 = delivery waits for the resolution, 2 = already delivered
-            log_pending(P, c, a, b, pv.resolved ? 2u : 1u, dst, pkt, seq);
-            if (!pv.resolved) return;
-        }
-        shd_event e;
-        e.time = c.now + (uint64_t)ceil(pv.lat * (double)SHD_MS);
-        e.seq = seq; e.src = c.h; e.dst = dst; e.pkt = pkt; e.kind = SHD_EV_PACKET;
-        emit_remote(P, c, e, next_parity);
-    } else {
-        trace(P, c, c.now, 0, c.h, dst, pkt, SHD_TR_INET_DROP);
-        c.c_idrop++;
-        if (pv.log) log_pending(P, c, a, b, 0u, dst, pkt, 0);
-    }
+// LDS of the round kernel (one wave per block; [slot][lane] layouts)
+__shared__ SendRec s_send[kSendCap * kBlock];    // deferred sends
+__shared__ shd_event s_res[kSendCap * kBlock];   // flush: resolved sends, then the events to deliver
+__shared__ uint16_t s_idx[kSendCap * kBlock];    // flush: record -> (lane << 4) | slot
+__shared__ int32_t s_att[kBlock];                // flush: each lane's attached vertex
+
+// loopback test of a destination draw (network_interface.c:548-555): the
+// first i with dest_cum[i] >= r is this host
+__device__ __forceinline__ bool is_self_draw(const HostCtx& c, uint32_t rv) {
+    const double r = (double)rv / kRandMax;
+    return c.cum_hi >= r && !(c.cum_lo >= r);
 }
 
-// _networkinterface_sendPackets (network_interface.c:519-579), FIFO qdisc
-__device__ void if_send_packets(const Params& P, HostCtx& c, int next_parity) {
+// _phold_chooseNode (test_phold.c:160-178): the first i with dest_cum[i] >= r.
+// guide[k] is a lower bound of it for any k <= r*H - 1; for even weights the
+// answer is one of the next three entries (their attached index inline), else
+// a binary search finishes the job.  Only called for draws r <= dest_cum[H-1].
+__device__ __forceinline__ uint32_t guide_index(const Params& P, double r) {
+    int32_t k = (int32_t)(r * (double)P.H) - 1;
+    return (uint32_t)(k < 0 ? 0 : (k > P.H - 1 ? P.H - 1 : k));
+}
+__device__ __forceinline__ void guide_pick(const Params& P, const DestGuide& g, double r, int32_t& dst, int32_t& att) {
+    // static indices only: a dynamically indexed guide would live in scratch
+    const bool f0 = g.cum[0] >= r, f1 = g.cum[1] >= r, f2 = g.cum[2] >= r;
+    if (f0 || f1 || f2) {
+        dst = g.i + (f0 ? 0 : f1 ? 1 : 2);
+        att = f0 ? g.att[0] : f1 ? g.att[1] : g.att[2];
+        return;
+    }
+    int32_t lo = g.i + 3, hi = P.H;
+    while (lo < hi) {
+        const int32_t mid = lo + ((hi - lo) >> 1);
+        if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
+    }
+    dst = lo;
+    att = P.host_att[lo];
+}
+
+// worker_sendPacket (worker.c:260-321), deferred: the reliability draw is
+// made now (it is drawn for every non-loopback send, worker.c:286); the
+// path lookup, the drop decision and the delivery happen at the next flush
+__device__ void worker_send_deferred(const Params& P, HostCtx& c, uint32_t rv, uint32_t pkt) {
+    const uint32_t chance = (uint32_t)rand_r_dev(c.rng);
+    SendRec q;
+    q.now = c.now; q.q_seq = c.q_seq; q.q_src = c.q_src;
+    q.pseq = (uint32_t)(c.ev_seq - c.seq_base);
+    q.r = rv; q.chance = chance; q.pkt = pkt;
+    q.q_sub = (c.q_sub++ & 0x7FFFFFFFu) | (bootstrapping(P, c) ? 0x80000000u : 0u);
+    c.sq[c.ns * kBlock] = q;
+    c.ns++;
+    c.ev_seq++;   // provisional: a dropped send gives its ID back at the flush
+}
+
+// Resolve every lane's deferred sends together.  Called by all lanes of the
+// wave (convergent; lanes with no host have ns = 0).  Record-parallel: each
+// lane picks the destination and looks up the path of one send (one memory
+// round trip each per 64 sends of the wave); then each host walks its own
+// sends in order (event IDs, counters, traces, first-touch logs, LDS only);
+// then record-parallel deliveries (one round trip for the calendar claims).
+__device__ void flush_wave(const Params& P, HostCtx& c) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t n = c.ns;
+    uint32_t pre = n;   // inclusive, then exclusive prefix of the lanes' counts
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(pre, off, 64);
+        if ((int)lane >= off) pre += o;
+    }
+    const uint32_t total = __shfl(pre, 63, 64);
+    pre -= n;
+    if (total == 0) return;
+    for (uint32_t i = 0; i < n; i++) s_idx[pre + i] = (uint16_t)((lane << 4) | i);
+    s_att[lane] = c.att;
+    __syncthreads();
+    uint32_t err = 0;
+    for (uint32_t base = 0; base < total; base += kBlock) {
+        const uint32_t r = base + lane;
+        if (r >= total) continue;
+        const uint32_t id = s_idx[r];
+        const uint32_t hl = id >> 4, i = id & 15u;
+        const SendRec q = s_send[i * kBlock + hl];
+        const int32_t a = s_att[hl];
+        const double rr = (double)q.r / kRandMax;
+        const DestGuide g = P.dest_guide[guide_index(P, rr)];
+        int32_t dst, b;
+        guide_pick(P, g, rr, dst, b);
+        PathRaw x;
+        const int32_t ra = P.complete ? kNoRank : P.rank[a];
+        path_load(P, a, b, x);
+        const PathVal pv = path_select(P, a, b, ra, x);
+        const double chance = (double)q.chance / kRandMax;
+        const bool boot = (q.q_sub >> 31) != 0;
+        const bool pass = boot || chance <= pv.rel || P.payload == 0;
+        if (!pv.resolved) {
+            const bool pass2 = boot || chance <= pv.rel2 || P.payload == 0;
+            if (pass != pass2) err |= SHD_ERR_AMBIGUOUS;
+        }
+        shd_event e;
+        e.time = q.now + (uint64_t)ceil(pv.lat * (double)SHD_MS);
+        e.seq = 0;
+        e.src = (uint32_t)b;   // the destination's attached index, for the first-touch log
+        e.dst = (uint32_t)dst;
+        e.pkt = 0;
+        e.kind = (pass ? 1u : 0u) | (pv.log ? 2u : 0u) | (pv.resolved ? 4u : 0u);
+        s_res[r] = e;
+    }
+    __syncthreads();
+    // per host, in send order (worker.c:286-320)
+    uint32_t failmask = 0, nfail = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        shd_event e = s_res[pre + i];
+        const SendRec q = s_send[i * kBlock + lane];
+        const bool pass = e.kind & 1u, log = (e.kind & 2u) != 0, resolved = (e.kind & 4u) != 0;
+        const int32_t b = (int32_t)e.src;
+        uint32_t emit = 0;
+        if (pass) {
+            const uint64_t seq = c.seq_base + q.pseq - nfail;
+            trace(P, c, q.now, seq, c.h, e.dst, q.pkt, SHD_TR_SENT);
+            c.c_sent++;
+            // 1 = delivery waits for the resolution, 2 = already delivered
+            if (log) log_pending(P, c, q, c.att, b, resolved ? 2u : 1u, e.dst, seq);
+            if (resolved && e.time < P.end_time) {   // scheduler_push drops time >= end
+                emit = SHD_EV_PACKET;
+                if (e.time < c.min_emit) c.min_emit = e.time;
+            }
+            e.seq = seq;
+        } else {
+            trace(P, c, q.now, 0, c.h, e.dst, q.pkt, SHD_TR_INET_DROP);
+            c.c_idrop++;
+            if (log) log_pending(P, c, q, c.att, b, 0u, e.dst, 0);
+            failmask |= 1u << i;
+            nfail++;
+        }
+        e.src = c.h;
+        e.pkt = q.pkt;
+        e.kind = emit;
+        s_res[pre + i] = e;
+    }
+    if (nfail) {
+        // timers scheduled since the last flush hold provisional IDs: an ID
+        // x loses the dropped sends issued before it
+        uint64_t f0 = 0, f1 = 0, f2 = 0;
+        const bool p0 = c.tt0 != kInf && c.ts0 >= c.seq_base, p1 = c.tt1 != kInf && c.ts1 >= c.seq_base,
+                   p2 = c.tt2 != kInf && c.ts2 >= c.seq_base;
+        if (p0 || p1 || p2) {
+            for (uint32_t i = 0; i < n; i++) {
+                if (!((failmask >> i) & 1u)) continue;
+                const uint64_t xi = c.seq_base + s_send[i * kBlock + lane].pseq;
+                f0 += xi < c.ts0; f1 += xi < c.ts1; f2 += xi < c.ts2;
+            }
+            if (p0) c.ts0 -= f0;
+            if (p1) c.ts1 -= f1;
+            if (p2) c.ts2 -= f2;
+        }
+        c.ev_seq -= nfail;
+    }
+    c.seq_base = c.ev_seq;
+    c.ns = 0;
+    __syncthreads();
+    // deliveries: calendar claims for 64 events at a time, then the stores
+    for (uint32_t base = 0; base < total; base += kBlock) {
+        const uint32_t r = base + lane;
+        if (r >= total) continue;
+        const shd_event e = s_res[r];
+        if (!e.kind) continue;
+        const int32_t dl = (int32_t)e.dst - P.h0;
+        const uint64_t bb = e.time >> P.bin_shift;
+        if (P.bins && dl >= 0 && dl < P.nloc && bb - (c.ws >> P.bin_shift) <= kHorizon) {
+            const size_t bi = (size_t)dl * kNB + ((uint32_t)bb & (kNB - 1));
+            const uint32_t slot = atomicAdd(&P.bin_n[bi], 1u);
+            if (slot < kBinCap) {
+                P.bins[bi * kBinCap + slot] = e;
+                const uint32_t p = (uint32_t)bb & (kNB - 1);
+                atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));
+                continue;
+            }
+        }
+        emit_nocal(P, c, e);
+    }
+    c.err |= err;
+    __syncthreads();   // s_res / s_idx are reused by the next flush
+}
+
+// _networkinterface_sendPackets (network_interface.c:519-579), FIFO qdisc.
+// Returns true when it stopped early for a flush of the deferred sends (the
+// buffer is full, or the next send is a loopback, whose trace and event take
+// the exact event ID); the caller flushes and calls it again.
+__device__ bool if_send_step(const Params& P, HostCtx& c) {
     const bool boot = bootstrapping(P, c);
     while (c.tx_rem >= SHD_MTU) {
         if (c.tq_count == 0) break;
         TxEnt p;
         if (c.tq_hv) {
             p = c.tq_hint;
-            c.tq_hv = false;
         } else {
             p = P.tq[(size_t)c.l * P.tq_cap + c.tq_head];
+            c.tq_hint = p;   // keep the peeked head: a flush may come first
+            c.tq_hv = true;
         }
+        const bool self = is_self_draw(c, p.r);
+        if (c.ns && (self || c.ns == (uint32_t)kSendCap)) return true;
+        c.tq_hv = false;
         c.tq_head = (c.tq_head + 1 == P.tq_cap) ? 0 : c.tq_head + 1;
         c.tq_count--;
-        if (p.dst == c.h) {
+        if (self) {
             trace(P, c, c.now, c.ev_seq, c.h, c.h, p.pkt, SHD_TR_LOCAL);
             schedule_self(P, c, SHD_EV_LOCAL, 1, p.pkt);
         } else {
             PROF_T0(ts)
-            worker_send_packet(P, c, p.dst, p.pkt, next_parity);
+            worker_send_deferred(P, c, p.r, p.pkt);
             PROF_ADD(c, PR_SEND, ts)
         }
         if (!boot) {
@@ -619,93 +905,69 @@ __device__ void if_send_packets(const Params& P, HostCtx& c, int next_parity) {
             refill_if_needed(P, c);
         }
     }
+    return false;
 }
 
-// _host_getRandomPort / _host_getRandomFreePort (host.c:1058-1110)
-__device__ __forceinline__ uint16_t random_port(HostCtx& c) {
-    const double f = next_double_dev(c.rng);
-    const double pick = round(f * (double)(65535 - SHD_MIN_RANDOM_PORT));
-    uint16_t p = (uint16_t)pick;
-    return (uint16_t)(p + (uint16_t)SHD_MIN_RANDOM_PORT);
-}
-__device__ void random_free_port(HostCtx& c) {
-    for (int i = 0; i < 10; i++)
-        if (random_port(c) != SHD_PHOLD_LISTEN_PORT) return;
-    (void)random_port(c);   // linear-search fallback: draws once, always finds a port
-}
+// _host_getRandomPort / _host_getRandomFreePort (host.c:1058-1110).
+// The draw lands in [MIN_RANDOM_PORT, 65535], never on the listener, so
+// exactly one rand_r step triple is consumed and its value is not needed.
+static_assert(SHD_PHOLD_LISTEN_PORT < SHD_MIN_RANDOM_PORT, "a random port never hits the listener");
+__device__ __forceinline__ void random_free_port(HostCtx& c) { (void)rand_r_dev(c.rng); }
 
-// _phold_sendNewMessage (test_phold.c:218-230) up to the socket send: pick
-// the destination, bind, queue the datagram; false when nothing was queued
+// _phold_sendNewMessage (test_phold.c:218-230) up to the socket send: draw
+// the destination (resolved at the flush; only whether one exists matters
+// here), bind, queue the datagram; false when nothing was queued
 __device__ bool enqueue_new_message(const Params& P, HostCtx& c) {
     PROF_T0(tp)
-    const double r = ((double)rand_r_dev(c.rng)) / kRandMax;
-    // first i with dest_cum[i] >= r.  guide[k] is a lower bound of it for any
-    // k <= r*H - 1 (DESIGN.md "Destination pick"); for even weights the answer
-    // is within the next few entries, else a binary search finishes the job.
-    int32_t k = (int32_t)(r * (double)P.H) - 1;
-    k = k < 0 ? 0 : (k > P.H - 1 ? P.H - 1 : k);
-    const DestGuide g = P.dest_guide[k];
-    int32_t lo = g.i;
-    {
-        const int32_t f = g.cum[0] >= r ? 0 : g.cum[1] >= r ? 1 : g.cum[2] >= r ? 2 : 3;
-        if (f < 3 || lo + 3 >= P.H) {
-            lo = f < 3 ? lo + f : P.H;
-        } else {
-            int32_t hi = P.H;
-            lo += 3;
-            while (lo < hi) {
-                const int32_t mid = lo + ((hi - lo) >> 1);
-                if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
-            }
-        }
-    }
+    const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
+    const double r = (double)rv / kRandMax;
     PROF_ADD(c, PR_PICK, tp)
-    if (lo >= P.H) return false;
-    const uint32_t dst = (uint32_t)lo;
+    if (!(P.cum_last >= r)) return false;   // no i with dest_cum[i] >= r
     random_free_port(c);
     const uint32_t pkt = c.pkt_seq++;
     if (c.tq_count >= P.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
     if (c.tq_count == 0) {
-        c.tq_hint = TxEnt{dst, pkt};
+        c.tq_hint = TxEnt{rv, pkt};
         c.tq_hv = true;
     } else {
         uint32_t tail = c.tq_head + c.tq_count;
         if (tail >= P.tq_cap) tail -= P.tq_cap;
-        P.tq[(size_t)c.l * P.tq_cap + tail] = TxEnt{dst, pkt};
+        P.tq[(size_t)c.l * P.tq_cap + tail] = TxEnt{rv, pkt};
     }
     c.tq_count++;
     return true;
 }
 
 // _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
-__device__ void refill_cb(const Params& P, HostCtx& c, int next_parity) {
+__device__ void refill_cb(const Params& P, HostCtx& c) {
     c.flags &= ~F_REFILL_PENDING;
     c.rx_rem += c.rx_refill;
     if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
     c.tx_rem += c.tx_refill;
     if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
     if_receive_packets(P, c);
-    if_send_packets(P, c, next_parity);
+    if (if_send_step(P, c)) c.err |= SHD_ERR_INTERNAL;   // boot: nothing queued, nothing deferred
     refill_if_needed(P, c);
 }
 
-// One event.  The kind-specific part only sets up work; the expensive shared
-// steps (CoDel dequeue + receive, message generation, the send loop with its
-// path lookups) run once below for every kind that needs them, so the lanes
-// of a wave that execute different kinds in the same iteration converge on
-// them instead of running them one kind after the other.  Per kind, the
-// steps and their order are the reference's:
+// One event, in two parts.  begin_event does the kind-specific part and
+// leaves the shared steps (CoDel dequeue + receive, message generation, the
+// send loop) as work in the context; run_work runs them, so the lanes of a
+// wave that execute different kinds in the same iteration converge on them.
+// run_work returns early when the deferred sends need a flush (the round loop
+// flushes and resumes it).  Per kind, the steps and their order are the
+// reference's:
 //   REFILL    refill_cb: top up, receive, send, schedule next refill
 //   PACKET    router_enqueue, receive if the queue was empty
 //   NOTIFY    one new message per unread datagram, each sent right away
 //   APP_START `load` new messages
-__device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int next_parity) {
+__device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
     c.c_events++;
     c.q_seq = e.seq;
     c.q_src = e.src;
     c.q_sub = 0;
-    uint32_t msgs = 0;
-    bool rx = false, tx = false, refill_chk = false;
+    c.w_msgs = 0;
+    c.w_rx = c.w_tx = c.w_refill = c.w_sending = false;
     switch (e.kind) {
     case SHD_EV_HEARTBEAT:
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
@@ -717,13 +979,13 @@ __device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int nex
         if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
         c.tx_rem += c.tx_refill;
         if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
-        rx = tx = refill_chk = true;
+        c.w_rx = c.w_tx = c.w_refill = true;
         break;
     case SHD_EV_REFILL_LO:
         break;
     case SHD_EV_APP_START:
         c.flags |= F_LISTENING;
-        msgs = P.load;
+        c.w_msgs = P.load;
         break;
     case SHD_EV_PACKET: {
         // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
@@ -742,7 +1004,7 @@ __device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int nex
         }
         c.cq_count++;
         c.cq_total += P.pkt_len;
-        rx = was_empty;
+        c.w_rx = was_empty;
         break;
     }
     case SHD_EV_LOCAL:
@@ -750,45 +1012,71 @@ __device__ void execute(const Params& P, HostCtx& c, const shd_event& e, int nex
         break;
     case SHD_EV_NOTIFY:
         c.flags &= ~F_NOTIFY_PENDING;
-        msgs = c.unread;
+        c.w_msgs = c.unread;
         c.unread = 0;
         break;
     default:
         c.err |= SHD_ERR_INTERNAL;
         break;
     }
-    if (rx) if_receive_packets(P, c);
-    while (msgs || tx) {
-        bool go = true;
-        if (msgs) {
-            go = enqueue_new_message(P, c);
-            msgs--;
-        } else {
-            tx = false;
-        }
-        if (go) if_send_packets(P, c, next_parity);
+    if (c.w_rx) {
+        if_receive_packets(P, c);
+        c.w_rx = false;
     }
-    if (refill_chk) refill_if_needed(P, c);
+}
+
+// the event's shared steps: while (msgs || tx) { a new message if any;
+// the send loop }; then the refill check.  False when it stopped for a flush.
+__device__ bool run_work(const Params& P, HostCtx& c) {
+    for (;;) {
+        if (c.w_sending) {
+            if (if_send_step(P, c)) return false;
+            c.w_sending = false;
+        }
+        if (c.w_msgs) {
+            const bool go = enqueue_new_message(P, c);
+            c.w_msgs--;
+            c.w_sending = go;
+            continue;
+        }
+        if (c.w_tx) {
+            c.w_tx = false;
+            c.w_sending = true;
+            continue;
+        }
+        break;
+    }
+    if (c.w_refill) {
+        refill_if_needed(P, c);
+        c.w_refill = false;
+    }
+    return true;
 }
 
 __device__ void load_ctx(const Params& P, HostCtx& c, int32_t l) {
     c.l = l;
     c.h = (uint32_t)(P.h0 + l);
-    c.rng = P.rng[l]; c.ev_seq = P.ev_seq[l]; c.pkt_seq = P.pkt_seq[l];
-    c.rx_rem = P.rx_rem[l]; c.tx_rem = P.tx_rem[l]; c.rx_refill = P.rx_refill[l]; c.tx_refill = P.tx_refill[l];
-    c.flags = P.flags[l]; c.unread = P.unread[l];
-    c.cq_total = P.cq_total[l]; c.cq_iexp = P.cq_iexp[l]; c.cq_ndrop = P.cq_ndrop[l];
-    c.cq_dc = P.cq_dc[l]; c.cq_dcl = P.cq_dcl[l]; c.cq_head = P.cq_head[l]; c.cq_count = P.cq_count[l];
-    c.tq_head = P.tq_head[l]; c.tq_count = P.tq_count[l];
-    c.evq_n = P.evq_n[l];
+    const HostRec r = P.hs[l];
+    c.rng = r.rng; c.ev_seq = r.ev_seq; c.pkt_seq = r.pkt_seq;
+    c.rx_rem = r.rx_rem; c.tx_rem = r.tx_rem; c.rx_refill = r.rx_refill; c.tx_refill = r.tx_refill;
+    c.flags = r.flags; c.unread = r.unread;
+    c.cq_total = r.cq_total; c.cq_iexp = r.cq_iexp; c.cq_ndrop = r.cq_ndrop;
+    c.cq_dc = r.cq_dc; c.cq_dcl = r.cq_dcl; c.cq_head = r.cq_head; c.cq_count = r.cq_count;
+    c.tq_head = r.tq_head; c.tq_count = r.tq_count;
+    c.evq_n = r.evq_n;
     c.top = P.evq[(size_t)l * P.evq_stride + 3];   // garbage when empty, never used then
-    c.tt0 = P.tm_time[0][l]; c.tt1 = P.tm_time[1][l]; c.tt2 = P.tm_time[2][l];
-    c.ts0 = P.tm_seq[0][l]; c.ts1 = P.tm_seq[1][l]; c.ts2 = P.tm_seq[2][l];
+    c.tt0 = r.tt[0]; c.tt1 = r.tt[1]; c.tt2 = r.tt[2];
+    c.ts0 = r.ts[0]; c.ts1 = r.ts[1]; c.ts2 = r.ts[2];
+    c.c_events = r.c_events; c.c_pkt = r.c_pkt; c.c_sent = r.c_sent;
+    c.c_idrop = r.c_idrop; c.c_cdrop = r.c_cdrop; c.c_recv = r.c_recv;
     c.cq_hv = false; c.tq_hv = false;
     c.att = P.host_att[c.h];
-    c.c_events = P.c_events[l]; c.c_pkt = P.c_pkt[l]; c.c_sent = P.c_sent[l];
-    c.c_idrop = P.c_idrop[l]; c.c_cdrop = P.c_cdrop[l]; c.c_recv = P.c_recv[l];
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
+    c.ws = 0; c.ws_mod = 0; c.due = nullptr; c.dh = 0; c.nd = 0;
+    c.sq = nullptr; c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
+    c.w_msgs = 0; c.w_rx = c.w_tx = c.w_refill = c.w_sending = false;
+    c.cum_hi = P.dest_cum[c.h];
+    c.cum_lo = c.h ? P.dest_cum[c.h - 1] : -1.0;
 }
 
 // earliest pending event of the host (timers and heap)
@@ -808,8 +1096,11 @@ __device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t 
     if (c.tt1 < bt || (c.tt1 == bt && c.tt1 != kInf && c.ts1 < bs)) { bt = c.tt1; bs = c.ts1; kind = SHD_EV_REFILL; slot = 1; }
     if (c.tt2 < bt || (c.tt2 == bt && c.tt2 != kInf && c.ts2 < bs)) { bt = c.tt2; bs = c.ts2; kind = SHD_EV_NOTIFY; slot = 2; }
     bool timer = bt != kInf;
-    if (c.evq_n) {
-        const shd_event& t = c.top;
+    // the queued candidate: heap root against the head of the due list
+    const bool hq = c.evq_n != 0, dq = c.dh < c.nd;
+    const bool use_due = dq && (!hq || ev_less(c.dtop, c.top));
+    if (hq || dq) {
+        const shd_event& t = use_due ? c.dtop : c.top;
         if (!timer || t.time < bt || (t.time == bt && (t.src < c.h || (t.src == c.h && t.seq < bs)))) timer = false;
     }
     if (timer) {
@@ -820,28 +1111,63 @@ __device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t 
         else c.tt2 = kInf;
         return true;
     }
-    if (!c.evq_n || c.top.time >= we) return false;
+    if (use_due) {   // due events are all < we
+        e = c.dtop;
+        if (++c.dh < c.nd) c.dtop = c.due[c.dh * kBlock];
+        return true;
+    }
+    if (!hq || c.top.time >= we) return false;
     e = c.top;
     heap_pop(P, c);
     return true;
 }
 
+// circular distance from bin position q to the first set bit of the bitmap
+// (kNB if none); static word indices only (no scratch)
+__device__ __forceinline__ uint32_t bits_first_from(const uint32_t (&w)[kNBW], uint32_t q) {
+    uint32_t best = kNB;
+#pragma unroll
+    for (int j = 0; j < (int)kNBW; j++) {
+        const uint32_t m = w[j];
+        const uint32_t base = 32u * j;
+        uint32_t hi, lo;   // bits at positions >= q, < q
+        if (base + 31 < q) { hi = 0; lo = m; }
+        else if (base >= q) { hi = m; lo = 0; }
+        else { const uint32_t k = q - base; hi = m & (~0u << k); lo = m & ((1u << k) - 1u); }
+        if (hi) { const uint32_t d = base + __builtin_ctz(hi) - q; best = d < best ? d : best; }
+        if (lo) { const uint32_t d = base + __builtin_ctz(lo) + kNB - q; best = d < best ? d : best; }
+    }
+    return best;
+}
+
+// lower bound of the earliest calendar event at or after `we`: the start of
+// the first non-empty bin from we's bin on (stale bits only lower it)
+__device__ __forceinline__ uint64_t cal_lower_bound(const Params& P, const uint32_t (&w)[kNBW], uint64_t we) {
+    const uint64_t bwe = we >> P.bin_shift;
+    const uint32_t d = bits_first_from(w, (uint32_t)bwe & (kNB - 1));
+    if (d >= kNB) return kInf;
+    const uint64_t t = (bwe + d) << P.bin_shift;
+    return t > we ? t : we;
+}
+
 __device__ void store_ctx(const Params& P, const HostCtx& c) {
     const int32_t l = c.l;
-    P.rng[l] = c.rng; P.ev_seq[l] = c.ev_seq; P.pkt_seq[l] = c.pkt_seq;
-    P.rx_rem[l] = c.rx_rem; P.tx_rem[l] = c.tx_rem;
-    P.flags[l] = c.flags; P.unread[l] = c.unread;
-    P.cq_total[l] = c.cq_total; P.cq_iexp[l] = c.cq_iexp; P.cq_ndrop[l] = c.cq_ndrop;
-    P.cq_dc[l] = c.cq_dc; P.cq_dcl[l] = c.cq_dcl; P.cq_head[l] = c.cq_head; P.cq_count[l] = c.cq_count;
-    P.tq_head[l] = c.tq_head; P.tq_count[l] = c.tq_count;
-    P.evq_n[l] = c.evq_n;
-    P.tm_time[0][l] = c.tt0; P.tm_time[1][l] = c.tt1; P.tm_time[2][l] = c.tt2;
-    P.tm_seq[0][l] = c.ts0; P.tm_seq[1][l] = c.ts1; P.tm_seq[2][l] = c.ts2;
+    HostRec r;
+    r.ev_seq = c.ev_seq; r.cq_total = c.cq_total; r.cq_iexp = c.cq_iexp; r.cq_ndrop = c.cq_ndrop;
+    r.rx_rem = c.rx_rem; r.tx_rem = c.tx_rem;
+    r.tt[0] = c.tt0; r.tt[1] = c.tt1; r.tt[2] = c.tt2;
+    r.ts[0] = c.ts0; r.ts[1] = c.ts1; r.ts[2] = c.ts2;
+    r.c_events = c.c_events; r.c_pkt = c.c_pkt; r.c_sent = c.c_sent;
+    r.c_idrop = c.c_idrop; r.c_cdrop = c.c_cdrop; r.c_recv = c.c_recv;
+    r.rng = c.rng; r.pkt_seq = c.pkt_seq; r.rx_refill = (uint32_t)c.rx_refill; r.tx_refill = (uint32_t)c.tx_refill;
+    r.flags = c.flags; r.unread = c.unread;
+    r.cq_dc = c.cq_dc; r.cq_dcl = c.cq_dcl; r.cq_head = c.cq_head; r.cq_count = c.cq_count;
+    r.tq_head = c.tq_head; r.tq_count = c.tq_count; r.evq_n = c.evq_n;
+    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    P.hs[l] = r;
     if (c.cq_hv) P.cq[(size_t)l * P.cq_cap + c.cq_head] = c.cq_hint;
     if (c.tq_hv) P.tq[(size_t)l * P.tq_cap + c.tq_head] = c.tq_hint;
     P.hnext[l] = host_next(c);
-    P.c_events[l] = c.c_events; P.c_pkt[l] = c.c_pkt; P.c_sent[l] = c.c_sent;
-    P.c_idrop[l] = c.c_idrop; P.c_cdrop[l] = c.c_cdrop; P.c_recv[l] = c.c_recv;
 }
 
 template <int BLOCK>
@@ -871,8 +1197,75 @@ __device__ void block_reduce_publish(const Params& P, uint64_t next, uint64_t ne
     }
 }
 
+// The round's summary without a same-address atomic per block: every block
+// writes its share; a two-level ticket (groups of kTickGroup blocks) elects
+// the last block of each group to fold the group, and the last of those to
+// fold the groups into P.sum.  True in that one block, which then sees every
+// block's stores (pending records, inbox and calendar appends).  One wave per
+// block (kBlock == 64).
+__device__ __forceinline__ void part_fold(BlockPart& a, const BlockPart& b) {
+    a.next = b.next < a.next ? b.next : a.next;
+    a.nev += b.nev;
+    a.npkt += b.npkt;
+    a.err |= b.err;
+}
+__device__ __forceinline__ void part_wave_reduce(BlockPart& q) {
+    for (int off = 32; off > 0; off >>= 1) {
+        BlockPart o;
+        o.next = __shfl_xor(q.next, off, 64);
+        o.nev = __shfl_xor(q.nev, off, 64);
+        o.npkt = __shfl_xor(q.npkt, off, 64);
+        o.err = __shfl_xor(q.err, off, 64);
+        part_fold(q, o);
+    }
+}
+__device__ bool round_complete(const Params& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
+    static_assert(kBlock == 64 && kTickGroup <= 64, "one wave per block; a group folds in one pass");
+    __shared__ int s_last;
+    BlockPart q{next, nev, npkt, err, 0};
+    part_wave_reduce(q);
+    const uint32_t nblk = gridDim.x, g = blockIdx.x / kTickGroup;
+    const uint32_t ngrp = (nblk + kTickGroup - 1) / kTickGroup;
+    if (threadIdx.x == 0) {
+        P.part[blockIdx.x] = q;
+        __threadfence();
+        const uint32_t gsize = nblk - g * kTickGroup < kTickGroup ? nblk - g * kTickGroup : kTickGroup;
+        s_last = atomicAdd(&P.tick[g], 1u) == gsize - 1;
+    }
+    __syncthreads();
+    if (!s_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    {
+        const uint32_t i = g * kTickGroup + threadIdx.x;
+        BlockPart x{kInf, 0, 0, 0, 0};
+        if (threadIdx.x < kTickGroup && i < nblk) x = P.part[i];
+        part_wave_reduce(x);
+        if (threadIdx.x == 0) {
+            P.gpart[g] = x;
+            P.tick[g] = 0;   // every block of the group has taken its ticket
+            __threadfence();
+            s_last = atomicAdd(&P.tick[ngrp], 1u) == ngrp - 1;
+        }
+    }
+    __syncthreads();
+    if (!s_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    BlockPart x{kInf, 0, 0, 0, 0};
+    for (uint32_t i = threadIdx.x; i < ngrp; i += 64) part_fold(x, P.gpart[i]);
+    part_wave_reduce(x);
+    if (threadIdx.x == 0) {
+        P.tick[ngrp] = 0;
+        if (x.next != kInf) atomicMin(&P.sum->next_time, x.next);
+        if (x.nev) atomicAdd(&P.sum->n_events, x.nev);
+        if (x.npkt) atomicAdd(&P.sum->n_pkt_events, x.npkt);
+        if (x.err) atomicOr(&P.sum->error, x.err);
+        __threadfence();
+    }
+    __syncthreads();
+    return true;
+}
+
 // ------------------------------------------------------------------ kernels
-constexpr int kBlock = 64;
 
 // host_boot for every local host at t = 0 (host.c:372-390)
 __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __restrict__ rng0,
@@ -884,55 +1277,120 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
     if (l < P.nloc) {
         const uint32_t h = (uint32_t)(P.h0 + l);
         // _networkinterface_setupTokenBuckets (network_interface.c:192-226)
-        P.rx_refill[l] = bw_down[h] * 1024 / 1000;
-        P.tx_refill[l] = bw_up[h] * 1024 / 1000;
-        P.rng[l] = rng0[h];
-        P.ev_seq[l] = 0; P.pkt_seq[l] = 0; P.rx_rem[l] = 0; P.tx_rem[l] = 0;
-        P.flags[l] = 0; P.unread[l] = 0;
-        P.cq_total[l] = 0; P.cq_iexp[l] = 0; P.cq_ndrop[l] = 0; P.cq_dc[l] = 0; P.cq_dcl[l] = 0;
-        P.cq_head[l] = 0; P.cq_count[l] = 0; P.tq_head[l] = 0; P.tq_count[l] = 0; P.evq_n[l] = 0;
-        for (int k = 0; k < 3; k++) { P.tm_time[k][l] = kInf; P.tm_seq[k][l] = 0; }
-        P.c_events[l] = 0; P.c_pkt[l] = 0; P.c_sent[l] = 0; P.c_idrop[l] = 0; P.c_cdrop[l] = 0; P.c_recv[l] = 0;
+        const uint64_t rxr = bw_down[h] * 1024 / 1000, txr = bw_up[h] * 1024 / 1000;
+        if ((rxr | txr) >> 32) err |= SHD_ERR_INTERNAL;   // > 4 GB per ms: outside the record's range
+        HostRec r;
+        r.ev_seq = 0; r.cq_total = 0; r.cq_iexp = 0; r.cq_ndrop = 0; r.rx_rem = 0; r.tx_rem = 0;
+        for (int k = 0; k < 3; k++) { r.tt[k] = kInf; r.ts[k] = 0; }
+        r.c_events = r.c_pkt = r.c_sent = r.c_idrop = r.c_cdrop = r.c_recv = 0;
+        r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
+        r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
+        r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        P.hs[l] = r;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
         HostCtx c;
         load_ctx(P, c, l);
         c.now = 0;
         c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);   // tracker_new, tracker.c:141,607-610
-        refill_cb(P, c, 0);                                      // ethernet startRefilling
+        refill_cb(P, c);                                         // ethernet startRefilling
         schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);        // loopback refill at +1 ms
         schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
         store_ctx(P, c);
         next = host_next(c);
-        err = c.err;
+        err |= c.err;
     }
     block_reduce_publish<kBlock>(P, next, 0, 0, err);
 }
 
-// one round [ws, we): merge inbox[parity], run events < we
-__device__ __forceinline__ void round_body(const Params& P, uint64_t we, int parity) {
+// bit p of a bitmap held in registers (static word indices only)
+__device__ __forceinline__ uint32_t bit_at(const uint32_t (&w)[kNBW], uint32_t p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < (int)kNBW; j++) v |= (p >> 5) == (uint32_t)j ? w[j] : 0u;
+    return (v >> (p & 31)) & 1u;
+}
+
+// one round [ws, we): merge inbox[parity] and the calendar bins of the
+// window, run events < we
+__device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_t we, int parity, uint64_t& next_out,
+                                           uint64_t& nev_out, uint64_t& npkt_out, uint32_t& err_out) {
+    __shared__ shd_event s_due[kDueCap * kBlock];   // [slot][lane]
     const int32_t l = (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
 #ifdef SHD_PROF
     const unsigned long long w0 = wall_clock64();
 #endif
+    TIM(1);
     uint64_t next = kInf, nev = 0, npkt = 0;
     uint32_t err = 0;
-    // hosts with nothing due this round touch 2-3 words, not their whole state
+    // the window's calendar bins: b0 .. b0 + nbin - 1 (nbin <= 3: bin width <= W)
+    const uint64_t b0 = ws >> P.bin_shift;
+    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
+    uint32_t w[kNBW];
+    // hosts with nothing due this round touch 3 words and their bitmap, not their whole state
     bool idle = false;
+    uint32_t wbits = 0;   // bit j: window bin j is non-empty
     if (l < P.nloc) {
         const uint32_t nin0 = P.inbox_n[parity][l];
         const uint64_t t0 = P.hnext[l];
-        if (nin0 == 0 && t0 >= we) { idle = true; next = t0; }
+        if (P.bins) {
+            const uint4* bp = (const uint4*)(P.bin_bits + (size_t)l * kNBW);
+            const uint4 x = bp[0], y = bp[1];
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++)
+                if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
+        } else {
+#pragma unroll
+            for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+        }
+        if (nbin > 3) err |= SHD_ERR_INTERNAL;   // window wider than W
+        if (nin0 == 0 && t0 >= we && wbits == 0) {
+            idle = true;
+            next = t0;
+            if (P.bins) {
+                const uint64_t cb = cal_lower_bound(P, w, we);
+                next = cb < next ? cb : next;
+            }
+        }
     }
-    if (l < P.nloc && !idle) {
+    TIM(2);
+    const bool active = l < P.nloc && !idle;
+#ifdef SHD_TIMING
+    uint64_t n_it = 0, k_tk = 0, k_be = 0, k_rw = 0, k_fl = 0, k_in = 0;
+    uint64_t k_l0 = 0;
+#define KT0(v) const uint64_t v = clock64();
+#define KTA(acc, v) acc += clock64() - v;
+#else
+#define KT0(v)
+#define KTA(acc, v)
+#endif
+    HostCtx c;   // idle lanes take part in the wave's flushes with no sends
+    c.ns = 0; c.att = 0; c.err = 0;
+    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
+    uint64_t ev0 = 0, pk0 = 0;
+    uint32_t bcnt[3] = {0, 0, 0};
+    if (active) {
         PROF_T0(t_all)
-        HostCtx c;
         load_ctx(P, c, l);
+        TIMA(7);
+        c.ws = ws;
+        c.ws_mod = (uint32_t)(ws % SHD_MS);
+        c.np = parity ^ 1;
+        c.due = s_due + threadIdx.x;
+        c.sq = s_send + threadIdx.x;
+        // calendar bin counts of the window (the slots are read below, per non-empty bin)
+        if (P.bins) {
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++)
+                if (j < nbin) bcnt[j] = P.bin_n[(size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1))];
+        }
 #ifdef SHD_PROF
         c.prof = ProfAcc{};
 #endif
         PROF_ADD(c, PR_LOAD, t_all)
-        const uint64_t ev0 = c.c_events, pk0 = c.c_pkt;
+        ev0 = c.c_events;
+        pk0 = c.c_pkt;
         // merge inbound events of the previous round
         PROF_T0(t_m)
         const uint32_t nin = P.inbox_n[parity][l];
@@ -942,28 +1400,132 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t we, int par
             for (uint32_t i = 0; i < n; i++) heap_push(P, c, in[i]);
             P.inbox_n[parity][l] = 0;
         }
-        PROF_ADD(c, PR_MERGE, t_m)
-        for (;;) {
-            PROF_T0(t_p)
-            shd_event e;
-            const bool more = take_next(P, c, we, e);
-            PROF_ADD(c, PR_POP, t_p)
-            if (!more) break;
-            c.now = e.time;
-            PROF_T0(t_x)
-            execute(P, c, e, parity ^ 1);
-#ifdef SHD_PROF
-            const int k = e.kind == SHD_EV_PACKET ? PR_EXEC_PKT : e.kind == SHD_EV_NOTIFY ? PR_EXEC_NOTIFY
-                        : e.kind == SHD_EV_REFILL ? PR_EXEC_REFILL : PR_EXEC_OTHER;
-            PROF_ADD(c, k, t_x)
-#endif
+        // the window's calendar events, sorted into the due list (slots are
+        // filtered by time: older processed events and slots claimed by this
+        // round's appends fall outside [ws, we))
+        if (P.bins) {
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                if (((wbits >> j) & 1u) == 0) continue;
+                const size_t bi = (size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+                shd_event bev[kBinCap];
+#pragma unroll
+                for (uint32_t s = 0; s < kBinCap; s++) bev[s] = P.bins[bi * kBinCap + s];
+                const uint32_t n = bcnt[j] < kBinCap ? bcnt[j] : kBinCap;
+#pragma unroll
+                for (uint32_t s = 0; s < kBinCap; s++) {
+                    const shd_event& x = bev[s];
+                    if (s < n && x.time >= ws && x.time < we) {
+                        if (c.nd == (uint32_t)kDueCap) {   // the due list is full: the heap takes it
+                            heap_push(P, c, x);
+                            continue;
+                        }
+                        uint32_t i = c.nd++;
+                        while (i > 0 && ev_less(x, c.due[(i - 1) * kBlock])) {
+                            c.due[i * kBlock] = c.due[(i - 1) * kBlock];
+                            i--;
+                        }
+                        c.due[i * kBlock] = x;
+                    }
+                }
+            }
+            if (c.nd) c.dtop = c.due[0];
         }
+        PROF_ADD(c, PR_MERGE, t_m)
+        TIMA(8);
+#ifdef SHD_TIMING
+        k_l0 = clock64();
+#endif
+    }
+    // the event loop.  An event's shared steps run in the same iteration as
+    // its start.  A lane whose deferred sends need a flush before it can go
+    // on (its send buffer is full, or a loopback send needs the exact event
+    // ID) leaves the inner loop with its event suspended; the wave's flush
+    // (all lanes, outside the inner loop) runs, and the suspended lanes
+    // resume.  Normally the outer loop runs once: one flush per round.
+    {
+        bool working = false, fin = !active;
+        do {
+            KT0(q4)
+            if (!fin) for (;;) {
+#ifdef SHD_TIMING
+                n_it++;
+#endif
+                if (!working) {
+                    PROF_T0(t_p)
+                    shd_event e;
+                    KT0(q0)
+                    const bool more = take_next(P, c, we, e);
+                    KTA(k_tk, q0)
+                    PROF_ADD(c, PR_POP, t_p)
+                    if (!more) {
+                        fin = true;
+                        break;
+                    }
+                    c.now = e.time;
+                    KT0(q1)
+                    begin_event(P, c, e);
+                    KTA(k_be, q1)
+                }
+                KT0(q2)
+                working = !run_work(P, c);
+                KTA(k_rw, q2)
+                if (working) break;
+            }
+            KTA(k_in, q4)
+            KT0(q3)
+            flush_wave(P, c);
+            KTA(k_fl, q3)
+        } while (__ballot(!fin) != 0);
+    }
+    TIM(9);
+    if (active) {
+#ifdef SHD_TIMING
+        {
+            uint64_t v[7] = {n_it, k_tk, k_be, k_rw, clock64() - k_l0, k_fl, k_in};
+#pragma unroll
+            for (int j = 0; j < 7; j++)
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(v[j], off, 64);
+                    v[j] = o > v[j] ? o : v[j];
+                }
+            TIMV(11, v[0]);
+            TIMV(12, v[1]);
+            TIMV(13, v[2]);
+            TIMV(14, v[3]);
+            TIMV(15, v[4]);
+            TIMV(16, v[5]);
+            TIMV(17, v[6]);
+        }
+#endif
         next = host_next(c);
         if (c.min_emit < next) next = c.min_emit;
+        if (P.bins) {
+            // bins wholly before we are consumed: reset them (no append of
+            // this round can target them: appends are >= we and within the horizon)
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                const uint64_t b = b0 + j;
+                if (j < nbin && ((b + 1) << P.bin_shift) <= we && (bcnt[j] || ((wbits >> j) & 1u))) {
+                    const uint32_t p = (uint32_t)b & (kNB - 1);
+                    P.bin_n[(size_t)l * kNB + p] = 0;
+                    if ((wbits >> j) & 1u) {
+                        const uint32_t m = 1u << (p & 31);
+                        atomicAnd(&P.bin_bits[(size_t)l * kNBW + (p >> 5)], ~m);
+#pragma unroll
+                        for (int k = 0; k < (int)kNBW; k++)
+                            if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
+                    }
+                }
+            }
+            const uint64_t cb = cal_lower_bound(P, w, we);
+            next = cb < next ? cb : next;
+        }
         nev = c.c_events - ev0;
         npkt = c.c_pkt - pk0;
-        err = c.err;
+        err |= c.err;
         PROF_T0(t_s)
+        TIMA(10);
         store_ctx(P, c);
         PROF_ADD(c, PR_STORE, t_s)
         PROF_ADD(c, PR_TOTAL, t_all)
@@ -996,11 +1558,15 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t we, int par
         }
     }
 #endif
-    block_reduce_publish<kBlock>(P, next, nev, npkt, err);
+    TIM(3);
+    next_out = next; nev_out = nev; npkt_out = npkt; err_out = err;
 }
 
-__global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t we, int parity) {
-    round_body(P, we, parity);
+__global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t ws, uint64_t we, int parity) {
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, ws, we, parity, next, nev, npkt, err);
+    (void)round_complete(P, next, nev, npkt, err);
 }
 
 // finalize resolved pending sends: value from the min-rank row, then deliver
@@ -1100,22 +1666,6 @@ __device__ void resolve_block(const Params& P, int next_parity) {
     }
 }
 
-// last-block ticket: true in the one block that finishes the round last; all
-// blocks' summary atomics and logged records are then visible to it
-__device__ __forceinline__ bool last_block(const Params& P) {
-    __shared__ int s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();   // release this block's stores (pending records, inbox)
-        const unsigned t = atomicAdd(&P.sum->done, 1u);
-        s_last = t == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!s_last) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    return true;
-}
-
 // device-driven round i of a batch (single engine): the window start is the
 // previous round's next event time (read on the device), so rounds run back
 // to back from one batch launch (or graph) with no host round trip; the last
@@ -1124,6 +1674,9 @@ __device__ __forceinline__ bool last_block(const Params& P) {
 __global__ __launch_bounds__(kBlock) void k_round_dev(Params P, const DevSummary* __restrict__ prev,
                                                        DevSummary* __restrict__ init,
                                                        const DevCtl* __restrict__ ctl, int i, uint64_t window) {
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
+#endif
     if (*P.halt) return;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     if (lead) {
@@ -1139,10 +1692,18 @@ __global__ __launch_bounds__(kBlock) void k_round_dev(Params P, const DevSummary
     }
     uint64_t we = ws + window;
     if (we > stop || we < ws) we = stop;
-    round_body(P, we, parity);
-    if (!last_block(P)) return;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, ws, we, parity, next, nev, npkt, err);
+    TIM(4);
+    if (!round_complete(P, next, nev, npkt, err)) {
+        TIM(5);
+        return;
+    }
+    TIM(5);
     if (threadIdx.x == 0) P.sum->ws = ws;
     resolve_block(P, parity ^ 1);
+    TIM(6);
     if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
 }
 
@@ -1251,8 +1812,10 @@ __global__ __launch_bounds__(kBlock) void k_round_x(Params P, const shd_event* _
     }
     uint64_t we = ws + window;
     if (we > stop || we < ws) we = stop;
-    round_body(P, we, parity);
-    if (!last_block(P)) return;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, ws, we, parity, next, nev, npkt, err);
+    if (!round_complete(P, next, nev, npkt, err)) return;
     if (threadIdx.x == 0) P.sum->ws = ws;
     xpack_block(P, P.sum, 0, P.sum->next_time);
     if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
@@ -1270,6 +1833,7 @@ __global__ void k_ingest_x(Params P, const shd_event* __restrict__ xrecv, const 
     const shd_event e = blk[1 + s];
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
+    if (cal_push(P, dl, e, P.sum->ws)) return;   // the horizon of the round that sent it
     const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
     if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
@@ -1279,17 +1843,18 @@ __global__ void k_digest(Params P, shd_host_digest* __restrict__ out) {
     const int32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= P.nloc) return;
     shd_host_digest d;
-    d.ev_seq = P.ev_seq[l]; d.rx_remaining = P.rx_rem[l]; d.tx_remaining = P.tx_rem[l];
-    d.codel_total = P.cq_total[l]; d.codel_interval_expire = P.cq_iexp[l]; d.codel_next_drop = P.cq_ndrop[l];
-    d.n_events = P.c_events[l]; d.n_pkt_events = P.c_pkt[l]; d.n_sent = P.c_sent[l];
-    d.n_inet_drop = P.c_idrop[l]; d.n_codel_drop = P.c_cdrop[l]; d.n_recv = P.c_recv[l];
-    d.rng = P.rng[l]; d.pkt_seq = P.pkt_seq[l];
-    const uint32_t f = P.flags[l];
+    const HostRec r = P.hs[l];
+    d.ev_seq = r.ev_seq; d.rx_remaining = r.rx_rem; d.tx_remaining = r.tx_rem;
+    d.codel_total = r.cq_total; d.codel_interval_expire = r.cq_iexp; d.codel_next_drop = r.cq_ndrop;
+    d.n_events = r.c_events; d.n_pkt_events = r.c_pkt; d.n_sent = r.c_sent;
+    d.n_inet_drop = r.c_idrop; d.n_codel_drop = r.c_cdrop; d.n_recv = r.c_recv;
+    d.rng = r.rng; d.pkt_seq = r.pkt_seq;
+    const uint32_t f = r.flags;
     d.codel_mode = (f & F_CODEL_DROP_MODE) ? 1u : 0u;
-    d.codel_count = P.cq_count[l]; d.codel_drop_count = P.cq_dc[l]; d.codel_drop_count_last = P.cq_dcl[l];
-    d.unread = P.unread[l];
+    d.codel_count = r.cq_count; d.codel_drop_count = r.cq_dc; d.codel_drop_count_last = r.cq_dcl;
+    d.unread = r.unread;
     d.flags = (f & F_REFILL_PENDING ? 1u : 0u) | (f & F_NOTIFY_PENDING ? 2u : 0u) | (f & F_LISTENING ? 4u : 0u) |
-              (P.tq_count[l] ? 8u : 0u);
+              (r.tq_count ? 8u : 0u);
     out[l] = d;
 }
 
@@ -1422,19 +1987,14 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.app_start = m->app_start; P.load = m->load; P.payload = m->payload; P.trace = m->trace;
     P.pkt_len = m->payload + SHD_HEADER_UDP;
     const size_t n = (size_t)e->nloc;
-    EALLOC(P.rng, n); EALLOC(P.ev_seq, n); EALLOC(P.pkt_seq, n); EALLOC(P.rx_rem, n); EALLOC(P.tx_rem, n);
-    EALLOC(P.rx_refill, n); EALLOC(P.tx_refill, n); EALLOC(P.flags, n); EALLOC(P.unread, n);
-    EALLOC(P.cq_total, n); EALLOC(P.cq_iexp, n); EALLOC(P.cq_ndrop, n); EALLOC(P.cq_dc, n); EALLOC(P.cq_dcl, n);
-    EALLOC(P.cq_head, n); EALLOC(P.cq_count, n); EALLOC(P.tq_head, n); EALLOC(P.tq_count, n);
-    EALLOC(P.c_events, n); EALLOC(P.c_pkt, n); EALLOC(P.c_sent, n); EALLOC(P.c_idrop, n); EALLOC(P.c_cdrop, n);
-    EALLOC(P.c_recv, n);
+    EALLOC(P.hs, n);
+    EALLOC(P.part, n);
+    EALLOC(P.gpart, n / kTickGroup + 2);
+    EALLOC(P.tick, n / kTickGroup + 3);
     {
         int rc;
         P.evq_stride = ((P.evq_cap + 3) & ~3u) + 4;   // heap root at +3: child groups 128-B aligned
-        if ((rc = ealloc(e, &P.evq, n * P.evq_stride, false)) || (rc = ealloc(e, &P.evq_n, n)) ||
-            (rc = ealloc(e, &P.tm_time[0], n)) || (rc = ealloc(e, &P.tm_time[1], n)) ||
-            (rc = ealloc(e, &P.tm_time[2], n)) || (rc = ealloc(e, &P.tm_seq[0], n)) ||
-            (rc = ealloc(e, &P.tm_seq[1], n)) || (rc = ealloc(e, &P.tm_seq[2], n)) || (rc = ealloc(e, &P.hnext, n)) ||
+        if ((rc = ealloc(e, &P.evq, n * P.evq_stride, false)) || (rc = ealloc(e, &P.hnext, n)) ||
             (rc = ealloc(e, &P.inbox[0], n * P.inbox_cap, false)) ||
             (rc = ealloc(e, &P.inbox[1], n * P.inbox_cap, false)) || (rc = ealloc(e, &P.inbox_n[0], n)) ||
             (rc = ealloc(e, &P.inbox_n[1], n)) || (rc = ealloc(e, &P.cq, n * P.cq_cap, false)) ||
@@ -1452,7 +2012,10 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         while (i < H && !(m->dest_cum[i] >= t)) i++;
         guide[k].i = i;
         guide[k].pad = 0;
-        for (int j = 0; j < 3; j++) guide[k].cum[j] = i + j < H ? m->dest_cum[i + j] : 2.0;
+        for (int j = 0; j < 3; j++) {
+            guide[k].cum[j] = i + j < H ? m->dest_cum[i + j] : 2.0;
+            guide[k].att[j] = i + j < H ? host_att[i + j] : -1;
+        }
     }
     for (int32_t i = 1; i < H; i++)
         if (!(m->dest_cum[i] >= m->dest_cum[i - 1])) { shd_eng_destroy(e); return SHD_EINVAL; }
@@ -1513,6 +2076,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.host_att = e->d_host_att;
     P.dest_cum = e->d_cum;
     P.dest_guide = e->d_guide;
+    P.cum_last = m->dest_cum[H - 1];
     P.T = pc->T;
     P.complete = pc->complete; P.prefer_direct = pc->prefer_direct; P.directed = pc->directed;
     P.row = pc->d_row; P.dir = pc->d_dir; P.self = pc->d_self;
@@ -1544,6 +2108,16 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         if (!(ml > 0.0) || bits == kDistInf) { shd_eng_destroy(e); return SHD_EINVAL; }
         e->window = (uint64_t)ceil(ml * (double)SHD_MS);
         if (e->window == 0) e->window = 1;
+    }
+    // calendar: bin width = the largest power of two <= W
+    if (!(m->queue_flags & SHD_QF_NO_CALENDAR)) {
+        P.bin_shift = 63u - (uint32_t)__builtin_clzll(e->window);
+        int rc;
+        if ((rc = ealloc(e, &P.bins, n * kNB * kBinCap, false)) || (rc = ealloc(e, &P.bin_n, n * kNB)) ||
+            (rc = ealloc(e, &P.bin_bits, n * kNBW))) {
+            shd_eng_destroy(e);
+            return rc;
+        }
     }
     *out = e;
     return SHD_OK;
@@ -1587,6 +2161,12 @@ extern "C" int shd_eng_boot(shd_eng* e) {
     memset(e->h_sum, 0, sizeof(DevSummary));
     int rc = reset_summary(e);
     if (rc) return rc;
+    if (e->P.bins) {   // empty calendar; every slot's time = kInf (never in a window)
+        const size_t n = (size_t)e->nloc;
+        SHD_HIP(hipMemsetAsync(e->P.bins, 0xFF, sizeof(shd_event) * n * kNB * kBinCap, e->stream));
+        SHD_HIP(hipMemsetAsync(e->P.bin_n, 0, 4 * n * kNB, e->stream));
+        SHD_HIP(hipMemsetAsync(e->P.bin_bits, 0, 4 * n * kNBW, e->stream));
+    }
     const int grid = (e->nloc + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(k_boot, dim3(grid), dim3(kBlock), 0, e->stream, e->P, e->d_rng0, e->d_bwd, e->d_bwu);
     SHD_HIP(hipGetLastError());
@@ -1613,14 +2193,14 @@ static void sort_pending(std::vector<shd_pending>& recs) {
 }
 
 extern "C" int shd_eng_round_kernel(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out) {
-    if (!e || !e->booted || we <= ws) return SHD_EINVAL;
+    if (!e || !e->booted || we <= ws || we - ws > e->window) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(e->device));
     int rc = reset_summary(e);
     if (rc) return rc;
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     e->P.sum = e->d_sum;
     SHD_HIP(hipEventRecord(e->ev0, e->stream));
-    hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, e->P, we, e->parity);
+    hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, e->P, ws, we, e->parity);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(e->ev1, e->stream));
     if ((rc = read_summary(e))) return rc;
@@ -1843,6 +2423,13 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     return rc;
 }
 
+#ifdef SHD_TIMING
+extern "C" int shd_debug_timing(uint64_t* out) {   // 64 x 2048 x 20
+    SHD_HIP(hipDeviceSynchronize());
+    SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tim), sizeof(g_tim)));
+    return SHD_OK;
+}
+#endif
 #ifdef SHD_PROF
 // profiling build only: read (and clear) the per-phase clock totals
 extern "C" int shd_debug_waves(uint64_t* out) {   // 128 x 8, then reset

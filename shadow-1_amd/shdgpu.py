@@ -20,6 +20,7 @@ SHD_MS = 1_000_000
 SHD_SEC = 1_000_000_000
 SHD_MTU = 1500
 SHD_HEADER_UDP = 42
+SHD_QF_NO_CALENDAR = 1      # queue_flags: every inter-host event through inbox + heap
 
 EV_HEARTBEAT, EV_REFILL, EV_REFILL_LO, EV_APP_START, EV_PACKET, EV_LOCAL, EV_NOTIFY = range(1, 8)
 TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL = range(1, 8)
@@ -89,7 +90,7 @@ class Model(C.Structure):
         ("heartbeat_interval", C.c_uint64), ("app_start", C.c_uint64),
         ("load", C.c_uint32), ("payload", C.c_uint32), ("trace", C.c_uint32),
         ("evq_cap", C.c_uint32), ("inbox_cap", C.c_uint32), ("codelq_cap", C.c_uint32),
-        ("txq_cap", C.c_uint32), ("_pad1", C.c_uint32),
+        ("txq_cap", C.c_uint32), ("queue_flags", C.c_uint32),
     ]
 
 
@@ -286,7 +287,7 @@ class ModelArrays:
     def __init__(self, host_vertex, host_rng, bw_down, bw_up, dest_cum, *, end_time,
                  app_start=1 * SHD_SEC, load=16, payload=1, heartbeat_interval=SHD_SEC,
                  bootstrap_end=0, trace=False, evq_cap=0, inbox_cap=0, codelq_cap=0,
-                 txq_cap=0):
+                 txq_cap=0, queue_flags=0):
         self.host_vertex = np.ascontiguousarray(host_vertex, dtype=np.int32)
         self.host_rng = np.ascontiguousarray(host_rng, dtype=np.uint32)
         self.bw_down = np.ascontiguousarray(bw_down, dtype=np.uint64)
@@ -302,7 +303,7 @@ class ModelArrays:
             as_ptr(self.bw_down, C.c_uint64), as_ptr(self.bw_up, C.c_uint64),
             as_ptr(self.dest_cum, C.c_double), int(end_time), int(bootstrap_end),
             int(heartbeat_interval), int(app_start), int(load), int(payload), int(bool(trace)),
-            int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), 0)
+            int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), int(queue_flags))
 
     @property
     def n_hosts(self):

@@ -37,9 +37,12 @@ def assert_same(gpu, ora):
     assert np.array_equal(gdg, odg)
 
 
-def test_geometric_one_host_per_vertex():
+@pytest.mark.parametrize("queue_flags", [0, S.SHD_QF_NO_CALENDAR])
+def test_geometric_one_host_per_vertex(queue_flags):
+    # queue_flags=NO_CALENDAR: every inter-host event takes the inbox + heap path
     g = W.geometric_graph(300, seed=2)
-    m = W.phold_model(W.hosts_on_vertices(300, 1), end_time=3 * S.SHD_SEC, trace=True)
+    m = W.phold_model(W.hosts_on_vertices(300, 1), end_time=3 * S.SHD_SEC, trace=True,
+                      queue_flags=queue_flags)
     gpu, ora, eng, _ = run_both(g, m)
     assert_same(gpu, ora)
     assert gpu[2].n_rounds > 100
