@@ -86,21 +86,25 @@ struct SendRec {
 static_assert(sizeof(SendRec) == 40, "send record layout");
 
 // Per-host state record in HBM (local host index).  The round kernel reads
-// and writes it whole, as 13 16-B accesses; it holds every field the host's
-// event handling mutates except the queues' contents.
+// and writes it whole, as 10 16-B accesses; it holds every field the host's
+// event handling mutates except the queues' contents and the counters.
 struct alignas(16) HostRec {
     uint64_t ev_seq;                       // host_getNewEventID counter (host.c:397)
     uint64_t cq_total, cq_iexp, cq_ndrop;  // CoDel: bytes queued, interval expiry, next drop
     uint64_t rx_rem, tx_rem;               // token buckets: bytes remaining
     uint64_t tt[3], ts[3];                 // timer slots (heartbeat, refill, notify): time, event ID
-    uint64_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;   // counters
     uint32_t rng, pkt_seq;                 // rand_r state, packet counter
     uint32_t rx_refill, tx_refill;         // token-bucket refill per 1 ms (bytes)
     uint32_t flags, unread;
     uint32_t cq_dc, cq_dcl, cq_head, cq_count;   // CoDel drop counts, FIFO head / length
     uint32_t tq_head, tq_count, evq_n, pad[3];
 };
-static_assert(sizeof(HostRec) == 208, "host record: 13 x 16 B");
+static_assert(sizeof(HostRec) == 160, "host record: 10 x 16 B");
+
+// per-host counters; a round adds its deltas with fire-and-forget atomics
+struct HostCnt {
+    unsigned long long events, pkt, sent, idrop, cdrop, recv;
+};
 
 // a block's share of the round summary (round_complete)
 struct BlockPart {
@@ -179,6 +183,7 @@ struct Params {
     // per-host state records (local index), and the earliest pending event
     // of each host's timers and heap (read alone by the idle test)
     HostRec* hs;
+    HostCnt* hc;
     uint64_t* hnext;
     // queues: per-host 4-ary heap of the other events (packets, loopback, boot one-shots)
     shd_event* evq;              // slab of evq_stride entries per host, heap at +3
@@ -204,7 +209,11 @@ struct Params {
     const int32_t* host_att;     // attached index of every host
     const double* dest_cum;
     const struct DestGuide* dest_guide;   // [H]: bucket k -> first i with dest_cum[i] >= k / H
-    double cum_last;             // dest_cum[H-1]: a draw above it has no destination
+    // destination draws as rand_r values x (r = x / RAND_MAX): there is a
+    // destination iff x <= dst_thr; host h's own draws (loopback) are
+    // self_thr[h].x <= x <= self_thr[h].y (precomputed, exact)
+    int32_t dst_thr;
+    const int2* self_thr;
     // path cache
     int32_t T;
     int32_t complete, prefer_direct, directed;
@@ -312,30 +321,26 @@ struct HostCtx {
     uint32_t rng;
     uint64_t ev_seq;
     uint32_t pkt_seq;
-    uint64_t rx_rem, tx_rem, rx_refill, tx_refill;
+    uint64_t rx_rem, tx_rem;
+    uint32_t rx_refill, tx_refill;
     uint32_t flags;
     uint32_t unread;
     uint64_t cq_total, cq_iexp, cq_ndrop;
     uint32_t cq_dc, cq_dcl, cq_head, cq_count;
     uint32_t tq_head, tq_count;
     uint32_t evq_n;
-    shd_event top;              // heap root (valid when evq_n > 0)
-    shd_event* due;             // this lane's sorted calendar events of the window (LDS, stride 64)
-    uint32_t dh, nd;            // next / count of due events
-    shd_event dtop;             // due[dh] (valid when dh < nd)
-    SendRec* sq;                // this lane's deferred sends (LDS, stride 64)
-    uint32_t ns;                // deferred sends
+    uint64_t top_time;          // heap root's time (the root itself: s_top; valid when evq_n > 0)
+    uint32_t dh, nd;            // next / count of the window's calendar events (s_due)
+    uint32_t ns;                // deferred sends (s_send)
     uint64_t seq_base;          // ev_seq at the last flush: IDs >= it are provisional
-    double cum_lo, cum_hi;      // dest_cum[h-1] (-1 for h = 0), dest_cum[h]: loopback test
-    uint32_t w_msgs;            // the executing event's remaining work (run_work)
-    bool w_rx, w_tx, w_refill, w_sending;
+    int32_t self_lo, self_hi;   // loopback draws (Params::self_thr)
+    uint32_t w_msgs;            // the executing event's remaining work (run_work): messages, W_* steps
+    uint32_t w_fl;
     uint64_t tt0, tt1, tt2;     // timer times (kInf = empty): heartbeat, refill, notify
     uint64_t ts0, ts1, ts2;     // timer event IDs
-    CodelEnt cq_hint;           // CoDel head entry held in registers (not yet stored)
-    TxEnt tq_hint;              // send FIFO head entry held in registers
-    bool cq_hv, tq_hv;
+    bool cq_hv, tq_hv;          // FIFO head entries held in LDS (s_cqh, s_tqh), not yet stored
     int32_t att;                // this host's attached-vertex index
-    uint64_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;
+    uint32_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;   // this round's counter deltas
     // current executing event key (for first-touch logging)
     uint64_t q_seq;
     uint32_t q_src;
@@ -351,6 +356,14 @@ struct HostCtx {
 #endif
 };
 
+constexpr uint32_t W_RX = 1u, W_TX = 2u, W_REFILL = 4u, W_SENDING = 8u;   // HostCtx::w_fl
+
+// per-lane LDS of the round kernel (one wave per block; [slot][lane] layouts)
+__shared__ shd_event s_top[kBlock];              // heap root
+__shared__ shd_event s_due[kDueCap * kBlock];    // the window's calendar events, sorted
+__shared__ CodelEnt s_cqh[kBlock];               // CoDel FIFO head
+__shared__ TxEnt s_tqh[kBlock];                  // send FIFO head
+
 __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) {
     if (a.time != b.time) return a.time < b.time;
     if (a.src != b.src) return a.src < b.src;
@@ -359,7 +372,7 @@ __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) 
 
 // 4-ary min-heap; the slab's entry 3 is the root, so the four children of
 // node i (4i+1 .. 4i+4) fill one aligned 128-B line.  The root is cached in
-// c.top: peeking never touches memory.
+// LDS (s_top) and its time in a register: peeking never touches HBM.
 __device__ __forceinline__ shd_event* heap_base(const Params& P, const HostCtx& c) {
     return P.evq + (size_t)c.l * P.evq_stride + 3;
 }
@@ -368,8 +381,16 @@ __device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
     shd_event* hp = heap_base(P, c);
     if (c.evq_n >= P.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
     uint32_t i = c.evq_n++;
-    if (i == 0) { hp[0] = e; c.top = e; return; }
-    if (ev_less(e, c.top)) c.top = e;   // it will end at the root
+    if (i == 0) {
+        hp[0] = e;
+        s_top[threadIdx.x] = e;
+        c.top_time = e.time;
+        return;
+    }
+    if (e.time <= c.top_time && ev_less(e, s_top[threadIdx.x])) {   // it will end at the root
+        s_top[threadIdx.x] = e;
+        c.top_time = e.time;
+    }
     while (i > 0) {
         const uint32_t p = (i - 1) >> 2;
         const shd_event pe = hp[p];
@@ -380,7 +401,7 @@ __device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
     hp[i] = e;
 }
 
-// remove the root (c.top); the new root is re-cached
+// remove the root; the new root is re-cached
 __device__ void heap_pop(const Params& P, HostCtx& c) {
     shd_event* hp = heap_base(P, c);
     const uint32_t n = --c.evq_n;
@@ -401,11 +422,11 @@ __device__ void heap_pop(const Params& P, HostCtx& c) {
             if (c1 + k < n && ev_less(ch[k], me)) { me = ch[k]; m = c1 + k; }
         if (!ev_less(me, last)) break;
         hp[i] = me;
-        if (i == 0) c.top = me;
+        if (i == 0) { s_top[threadIdx.x] = me; c.top_time = me.time; }
         i = m;
     }
     hp[i] = last;
-    if (i == 0) c.top = last;
+    if (i == 0) { s_top[threadIdx.x] = last; c.top_time = last.time; }
 }
 
 __device__ __forceinline__ void trace(const Params& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
@@ -539,7 +560,7 @@ __device__ bool codel_helper(const Params& P, HostCtx& c, bool& okToDrop, CodelE
     okToDrop = false;
     if (c.cq_count == 0) { c.cq_iexp = 0; return false; }
     if (c.cq_hv) {
-        out = c.cq_hint;
+        out = s_cqh[threadIdx.x];
         c.cq_hv = false;
     } else {
         out = P.cq[(size_t)c.l * P.cq_cap + c.cq_head];
@@ -696,10 +717,11 @@ __shared__ uint16_t s_idx[kSendCap * kBlock];    // flush: record -> (lane << 4)
 __shared__ int32_t s_att[kBlock];                // flush: each lane's attached vertex
 
 // loopback test of a destination draw (network_interface.c:548-555): the
-// first i with dest_cum[i] >= r is this host
+// first i with dest_cum[i] >= r = x / RAND_MAX is this host, i.e.
+// dest_cum[h-1] < r <= dest_cum[h]; r is monotone in x, so that is an
+// interval of x, precomputed on the host with the same division
 __device__ __forceinline__ bool is_self_draw(const HostCtx& c, uint32_t rv) {
-    const double r = (double)rv / kRandMax;
-    return c.cum_hi >= r && !(c.cum_lo >= r);
+    return (int32_t)rv >= c.self_lo && (int32_t)rv <= c.self_hi;
 }
 
 // _phold_chooseNode (test_phold.c:160-178): the first i with dest_cum[i] >= r.
@@ -737,7 +759,7 @@ __device__ void worker_send_deferred(const Params& P, HostCtx& c, uint32_t rv, u
     q.pseq = (uint32_t)(c.ev_seq - c.seq_base);
     q.r = rv; q.chance = chance; q.pkt = pkt;
     q.q_sub = (c.q_sub++ & 0x7FFFFFFFu) | (bootstrapping(P, c) ? 0x80000000u : 0u);
-    c.sq[c.ns * kBlock] = q;
+    s_send[c.ns * kBlock + threadIdx.x] = q;
     c.ns++;
     c.ev_seq++;   // provisional: a dropped send gives its ID back at the flush
 }
@@ -881,10 +903,10 @@ __device__ bool if_send_step(const Params& P, HostCtx& c) {
         if (c.tq_count == 0) break;
         TxEnt p;
         if (c.tq_hv) {
-            p = c.tq_hint;
+            p = s_tqh[threadIdx.x];
         } else {
             p = P.tq[(size_t)c.l * P.tq_cap + c.tq_head];
-            c.tq_hint = p;   // keep the peeked head: a flush may come first
+            s_tqh[threadIdx.x] = p;   // keep the peeked head: a flush may come first
             c.tq_hv = true;
         }
         const bool self = is_self_draw(c, p.r);
@@ -920,14 +942,13 @@ __device__ __forceinline__ void random_free_port(HostCtx& c) { (void)rand_r_dev(
 __device__ bool enqueue_new_message(const Params& P, HostCtx& c) {
     PROF_T0(tp)
     const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
-    const double r = (double)rv / kRandMax;
     PROF_ADD(c, PR_PICK, tp)
-    if (!(P.cum_last >= r)) return false;   // no i with dest_cum[i] >= r
+    if ((int32_t)rv > P.dst_thr) return false;   // no i with dest_cum[i] >= r
     random_free_port(c);
     const uint32_t pkt = c.pkt_seq++;
     if (c.tq_count >= P.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
     if (c.tq_count == 0) {
-        c.tq_hint = TxEnt{rv, pkt};
+        s_tqh[threadIdx.x] = TxEnt{rv, pkt};
         c.tq_hv = true;
     } else {
         uint32_t tail = c.tq_head + c.tq_count;
@@ -967,7 +988,7 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
     c.q_src = e.src;
     c.q_sub = 0;
     c.w_msgs = 0;
-    c.w_rx = c.w_tx = c.w_refill = c.w_sending = false;
+    c.w_fl = 0;
     switch (e.kind) {
     case SHD_EV_HEARTBEAT:
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
@@ -979,7 +1000,7 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
         c.tx_rem += c.tx_refill;
         if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
-        c.w_rx = c.w_tx = c.w_refill = true;
+        c.w_fl = W_RX | W_TX | W_REFILL;
         break;
     case SHD_EV_REFILL_LO:
         break;
@@ -994,8 +1015,8 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         const bool was_empty = c.cq_count == 0;
         if (c.cq_count >= P.cq_cap) { c.err |= SHD_ERR_CODELQ_OVERFLOW; break; }
         const CodelEnt ent{c.now, e.src, e.pkt};
-        if (was_empty) {   // the head stays in registers; stored only if still queued at round end
-            c.cq_hint = ent;
+        if (was_empty) {   // the head stays in LDS; stored only if still queued at round end
+            s_cqh[threadIdx.x] = ent;
             c.cq_hv = true;
         } else {
             uint32_t tail = c.cq_head + c.cq_count;
@@ -1004,7 +1025,7 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         }
         c.cq_count++;
         c.cq_total += P.pkt_len;
-        c.w_rx = was_empty;
+        c.w_fl = was_empty ? W_RX : 0u;
         break;
     }
     case SHD_EV_LOCAL:
@@ -1019,9 +1040,9 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         c.err |= SHD_ERR_INTERNAL;
         break;
     }
-    if (c.w_rx) {
+    if (c.w_fl & W_RX) {
         if_receive_packets(P, c);
-        c.w_rx = false;
+        c.w_fl &= ~W_RX;
     }
 }
 
@@ -1029,26 +1050,25 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
 // the send loop }; then the refill check.  False when it stopped for a flush.
 __device__ bool run_work(const Params& P, HostCtx& c) {
     for (;;) {
-        if (c.w_sending) {
+        if (c.w_fl & W_SENDING) {
             if (if_send_step(P, c)) return false;
-            c.w_sending = false;
+            c.w_fl &= ~W_SENDING;
         }
         if (c.w_msgs) {
             const bool go = enqueue_new_message(P, c);
             c.w_msgs--;
-            c.w_sending = go;
+            if (go) c.w_fl |= W_SENDING;
             continue;
         }
-        if (c.w_tx) {
-            c.w_tx = false;
-            c.w_sending = true;
+        if (c.w_fl & W_TX) {
+            c.w_fl = (c.w_fl & ~W_TX) | W_SENDING;
             continue;
         }
         break;
     }
-    if (c.w_refill) {
+    if (c.w_fl & W_REFILL) {
         refill_if_needed(P, c);
-        c.w_refill = false;
+        c.w_fl &= ~W_REFILL;
     }
     return true;
 }
@@ -1064,31 +1084,38 @@ __device__ void load_ctx(const Params& P, HostCtx& c, int32_t l) {
     c.cq_dc = r.cq_dc; c.cq_dcl = r.cq_dcl; c.cq_head = r.cq_head; c.cq_count = r.cq_count;
     c.tq_head = r.tq_head; c.tq_count = r.tq_count;
     c.evq_n = r.evq_n;
-    c.top = P.evq[(size_t)l * P.evq_stride + 3];   // garbage when empty, never used then
+    if (r.evq_n) {
+        const shd_event t = P.evq[(size_t)l * P.evq_stride + 3];
+        s_top[threadIdx.x] = t;
+        c.top_time = t.time;
+    } else {
+        c.top_time = kInf;
+    }
     c.tt0 = r.tt[0]; c.tt1 = r.tt[1]; c.tt2 = r.tt[2];
     c.ts0 = r.ts[0]; c.ts1 = r.ts[1]; c.ts2 = r.ts[2];
-    c.c_events = r.c_events; c.c_pkt = r.c_pkt; c.c_sent = r.c_sent;
-    c.c_idrop = r.c_idrop; c.c_cdrop = r.c_cdrop; c.c_recv = r.c_recv;
+    c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.cq_hv = false; c.tq_hv = false;
     c.att = P.host_att[c.h];
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
-    c.ws = 0; c.ws_mod = 0; c.due = nullptr; c.dh = 0; c.nd = 0;
-    c.sq = nullptr; c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
-    c.w_msgs = 0; c.w_rx = c.w_tx = c.w_refill = c.w_sending = false;
-    c.cum_hi = P.dest_cum[c.h];
-    c.cum_lo = c.h ? P.dest_cum[c.h - 1] : -1.0;
+    c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0;
+    c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
+    c.w_msgs = 0; c.w_fl = 0;
+    const int2 st = P.self_thr[c.h];
+    c.self_lo = st.x;
+    c.self_hi = st.y;
 }
 
 // earliest pending event of the host (timers and heap)
 __device__ __forceinline__ uint64_t host_next(const HostCtx& c) {
-    uint64_t t = c.evq_n ? c.top.time : kInf;
+    uint64_t t = c.evq_n ? c.top_time : kInf;
     t = c.tt0 < t ? c.tt0 : t;
     t = c.tt1 < t ? c.tt1 : t;
     return c.tt2 < t ? c.tt2 : t;
 }
 
 // the host's next event in (time, src, seq) order if it is before `we`:
-// the earliest timer (src = the host) against the heap root
+// the earliest timer (src = the host) against the heap root and the head
+// of the window's calendar events
 __device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t we, shd_event& e) {
     uint64_t bt = c.tt0, bs = c.ts0;
     uint32_t kind = SHD_EV_HEARTBEAT;
@@ -1097,11 +1124,24 @@ __device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t 
     if (c.tt2 < bt || (c.tt2 == bt && c.tt2 != kInf && c.ts2 < bs)) { bt = c.tt2; bs = c.ts2; kind = SHD_EV_NOTIFY; slot = 2; }
     bool timer = bt != kInf;
     // the queued candidate: heap root against the head of the due list
-    const bool hq = c.evq_n != 0, dq = c.dh < c.nd;
-    const bool use_due = dq && (!hq || ev_less(c.dtop, c.top));
+    const bool hq = c.evq_n != 0 && c.top_time < we, dq = c.dh < c.nd;   // due events are all < we
+    bool use_due = false;
     if (hq || dq) {
-        const shd_event& t = use_due ? c.dtop : c.top;
-        if (!timer || t.time < bt || (t.time == bt && (t.src < c.h || (t.src == c.h && t.seq < bs)))) timer = false;
+        shd_event t;
+        if (hq && dq) {
+            const shd_event d = s_due[c.dh * kBlock + threadIdx.x], h = s_top[threadIdx.x];
+            use_due = ev_less(d, h);
+            t = use_due ? d : h;
+        } else if (dq) {
+            t = s_due[c.dh * kBlock + threadIdx.x];
+            use_due = true;
+        } else {
+            t = s_top[threadIdx.x];
+        }
+        if (!timer || t.time < bt || (t.time == bt && (t.src < c.h || (t.src == c.h && t.seq < bs)))) {
+            timer = false;
+            e = t;
+        }
     }
     if (timer) {
         if (bt >= we) return false;
@@ -1111,13 +1151,11 @@ __device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t 
         else c.tt2 = kInf;
         return true;
     }
-    if (use_due) {   // due events are all < we
-        e = c.dtop;
-        if (++c.dh < c.nd) c.dtop = c.due[c.dh * kBlock];
+    if (use_due) {
+        c.dh++;
         return true;
     }
-    if (!hq || c.top.time >= we) return false;
-    e = c.top;
+    if (!hq) return false;
     heap_pop(P, c);
     return true;
 }
@@ -1157,16 +1195,21 @@ __device__ void store_ctx(const Params& P, const HostCtx& c) {
     r.rx_rem = c.rx_rem; r.tx_rem = c.tx_rem;
     r.tt[0] = c.tt0; r.tt[1] = c.tt1; r.tt[2] = c.tt2;
     r.ts[0] = c.ts0; r.ts[1] = c.ts1; r.ts[2] = c.ts2;
-    r.c_events = c.c_events; r.c_pkt = c.c_pkt; r.c_sent = c.c_sent;
-    r.c_idrop = c.c_idrop; r.c_cdrop = c.c_cdrop; r.c_recv = c.c_recv;
-    r.rng = c.rng; r.pkt_seq = c.pkt_seq; r.rx_refill = (uint32_t)c.rx_refill; r.tx_refill = (uint32_t)c.tx_refill;
+    r.rng = c.rng; r.pkt_seq = c.pkt_seq; r.rx_refill = c.rx_refill; r.tx_refill = c.tx_refill;
     r.flags = c.flags; r.unread = c.unread;
     r.cq_dc = c.cq_dc; r.cq_dcl = c.cq_dcl; r.cq_head = c.cq_head; r.cq_count = c.cq_count;
     r.tq_head = c.tq_head; r.tq_count = c.tq_count; r.evq_n = c.evq_n;
     r.pad[0] = r.pad[1] = r.pad[2] = 0;
     P.hs[l] = r;
-    if (c.cq_hv) P.cq[(size_t)l * P.cq_cap + c.cq_head] = c.cq_hint;
-    if (c.tq_hv) P.tq[(size_t)l * P.tq_cap + c.tq_head] = c.tq_hint;
+    if (c.cq_hv) P.cq[(size_t)l * P.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
+    if (c.tq_hv) P.tq[(size_t)l * P.tq_cap + c.tq_head] = s_tqh[threadIdx.x];
+    HostCnt* hc = P.hc + l;   // counter deltas: fire-and-forget atomics
+    if (c.c_events) atomicAdd(&hc->events, (unsigned long long)c.c_events);
+    if (c.c_pkt) atomicAdd(&hc->pkt, (unsigned long long)c.c_pkt);
+    if (c.c_sent) atomicAdd(&hc->sent, (unsigned long long)c.c_sent);
+    if (c.c_idrop) atomicAdd(&hc->idrop, (unsigned long long)c.c_idrop);
+    if (c.c_cdrop) atomicAdd(&hc->cdrop, (unsigned long long)c.c_cdrop);
+    if (c.c_recv) atomicAdd(&hc->recv, (unsigned long long)c.c_recv);
     P.hnext[l] = host_next(c);
 }
 
@@ -1282,7 +1325,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
         HostRec r;
         r.ev_seq = 0; r.cq_total = 0; r.cq_iexp = 0; r.cq_ndrop = 0; r.rx_rem = 0; r.tx_rem = 0;
         for (int k = 0; k < 3; k++) { r.tt[k] = kInf; r.ts[k] = 0; }
-        r.c_events = r.c_pkt = r.c_sent = r.c_idrop = r.c_cdrop = r.c_recv = 0;
+        P.hc[l] = HostCnt{0, 0, 0, 0, 0, 0};
         r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
         r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
         r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.pad[0] = r.pad[1] = r.pad[2] = 0;
@@ -1303,6 +1346,18 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
     block_reduce_publish<kBlock>(P, next, 0, 0, err);
 }
 
+// a calendar slot's event, if it is one of the window's: onto the due list
+// (unsorted; sorted once all bins are read), or the heap when the list is full
+__device__ __forceinline__ void due_add(const Params& P, HostCtx& c, const shd_event& x, uint64_t ws, uint64_t we) {
+    if (x.time < ws || x.time >= we) return;
+    if (c.nd == (uint32_t)kDueCap) {
+        heap_push(P, c, x);
+        return;
+    }
+    s_due[c.nd * kBlock + threadIdx.x] = x;
+    c.nd++;
+}
+
 // bit p of a bitmap held in registers (static word indices only)
 __device__ __forceinline__ uint32_t bit_at(const uint32_t (&w)[kNBW], uint32_t p) {
     uint32_t v = 0;
@@ -1315,7 +1370,6 @@ __device__ __forceinline__ uint32_t bit_at(const uint32_t (&w)[kNBW], uint32_t p
 // window, run events < we
 __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_t we, int parity, uint64_t& next_out,
                                            uint64_t& nev_out, uint64_t& npkt_out, uint32_t& err_out) {
-    __shared__ shd_event s_due[kDueCap * kBlock];   // [slot][lane]
     const int32_t l = (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
 #ifdef SHD_PROF
     const unsigned long long w0 = wall_clock64();
@@ -1351,6 +1405,12 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
             if (P.bins) {
                 const uint64_t cb = cal_lower_bound(P, w, we);
                 next = cb < next ? cb : next;
+                // the counts of the window's wholly consumed bins (appends
+                // that overflowed into the inbox leave a count without a bit)
+#pragma unroll
+                for (uint32_t j = 0; j < 2; j++)
+                    if (j < nbin && ((b0 + j + 1) << P.bin_shift) <= we)
+                        P.bin_n[(size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1))] = 0;
             }
         }
     }
@@ -1361,6 +1421,9 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
     uint64_t k_l0 = 0;
 #define KT0(v) const uint64_t v = clock64();
 #define KTA(acc, v) acc += clock64() - v;
+#elif defined(SHD_MARK)   // asm listing markers (static code-size census)
+#define KT0(v) asm volatile("; MARK " #v " begin" ::: "memory");
+#define KTA(acc, v) asm volatile("; MARK " #v " end" ::: "memory");
 #else
 #define KT0(v)
 #define KTA(acc, v)
@@ -1368,8 +1431,6 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
     c.ns = 0; c.att = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
-    uint64_t ev0 = 0, pk0 = 0;
-    uint32_t bcnt[3] = {0, 0, 0};
     if (active) {
         PROF_T0(t_all)
         load_ctx(P, c, l);
@@ -1377,20 +1438,10 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
         c.ws = ws;
         c.ws_mod = (uint32_t)(ws % SHD_MS);
         c.np = parity ^ 1;
-        c.due = s_due + threadIdx.x;
-        c.sq = s_send + threadIdx.x;
-        // calendar bin counts of the window (the slots are read below, per non-empty bin)
-        if (P.bins) {
-#pragma unroll
-            for (uint32_t j = 0; j < 3; j++)
-                if (j < nbin) bcnt[j] = P.bin_n[(size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1))];
-        }
 #ifdef SHD_PROF
         c.prof = ProfAcc{};
 #endif
         PROF_ADD(c, PR_LOAD, t_all)
-        ev0 = c.c_events;
-        pk0 = c.c_pkt;
         // merge inbound events of the previous round
         PROF_T0(t_m)
         const uint32_t nin = P.inbox_n[parity][l];
@@ -1400,36 +1451,34 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
             for (uint32_t i = 0; i < n; i++) heap_push(P, c, in[i]);
             P.inbox_n[parity][l] = 0;
         }
-        // the window's calendar events, sorted into the due list (slots are
-        // filtered by time: older processed events and slots claimed by this
-        // round's appends fall outside [ws, we))
+        // the window's calendar events, sorted into the due list.  The slots
+        // of a non-empty bin are filtered by time alone: a slot never written
+        // in the bin's current use holds kInf or an older use's event (before
+        // ws), a slot being written by this round's appends holds a time >= we
+        // (or still the old one), so the bin's count is not needed here
         if (P.bins) {
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++) {
                 if (((wbits >> j) & 1u) == 0) continue;
                 const size_t bi = (size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
-                shd_event bev[kBinCap];
-#pragma unroll
-                for (uint32_t s = 0; s < kBinCap; s++) bev[s] = P.bins[bi * kBinCap + s];
-                const uint32_t n = bcnt[j] < kBinCap ? bcnt[j] : kBinCap;
-#pragma unroll
-                for (uint32_t s = 0; s < kBinCap; s++) {
-                    const shd_event& x = bev[s];
-                    if (s < n && x.time >= ws && x.time < we) {
-                        if (c.nd == (uint32_t)kDueCap) {   // the due list is full: the heap takes it
-                            heap_push(P, c, x);
-                            continue;
-                        }
-                        uint32_t i = c.nd++;
-                        while (i > 0 && ev_less(x, c.due[(i - 1) * kBlock])) {
-                            c.due[i * kBlock] = c.due[(i - 1) * kBlock];
-                            i--;
-                        }
-                        c.due[i * kBlock] = x;
-                    }
-                }
+                static_assert(kBinCap == 4, "the slots are read as four named events");
+                const shd_event* bp = P.bins + bi * kBinCap;
+                const shd_event x0 = bp[0], x1 = bp[1], x2 = bp[2], x3 = bp[3];
+                due_add(P, c, x0, ws, we);
+                due_add(P, c, x1, ws, we);
+                due_add(P, c, x2, ws, we);
+                due_add(P, c, x3, ws, we);
             }
-            if (c.nd) c.dtop = c.due[0];
+            // insertion sort of the due list (LDS only)
+            for (uint32_t i = 1; i < c.nd; i++) {
+                const shd_event x = s_due[i * kBlock + threadIdx.x];
+                uint32_t k = i;
+                while (k > 0 && ev_less(x, s_due[(k - 1) * kBlock + threadIdx.x])) {
+                    s_due[k * kBlock + threadIdx.x] = s_due[(k - 1) * kBlock + threadIdx.x];
+                    k--;
+                }
+                s_due[k * kBlock + threadIdx.x] = x;
+            }
         }
         PROF_ADD(c, PR_MERGE, t_m)
         TIMA(8);
@@ -1444,39 +1493,47 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
     // (all lanes, outside the inner loop) runs, and the suspended lanes
     // resume.  Normally the outer loop runs once: one flush per round.
     {
-        bool working = false, fin = !active;
-        do {
+        // per-lane state: 0 needs its next event, 1 is running one, 2 waits
+        // for a flush, 3 is done.  Both loops exit on wave-uniform tests only
+        // (no divergent breaks: the exec-mask bookkeeping stays small).
+        uint32_t st = active ? 0u : 3u;
+        for (;;) {
             KT0(q4)
-            if (!fin) for (;;) {
+            for (;;) {
 #ifdef SHD_TIMING
                 n_it++;
 #endif
-                if (!working) {
+                if (st == 0u) {
                     PROF_T0(t_p)
                     shd_event e;
                     KT0(q0)
                     const bool more = take_next(P, c, we, e);
                     KTA(k_tk, q0)
                     PROF_ADD(c, PR_POP, t_p)
-                    if (!more) {
-                        fin = true;
-                        break;
+                    if (more) {
+                        c.now = e.time;
+                        KT0(q1)
+                        begin_event(P, c, e);
+                        KTA(k_be, q1)
+                        st = 1u;
+                    } else {
+                        st = 3u;
                     }
-                    c.now = e.time;
-                    KT0(q1)
-                    begin_event(P, c, e);
-                    KTA(k_be, q1)
                 }
-                KT0(q2)
-                working = !run_work(P, c);
-                KTA(k_rw, q2)
-                if (working) break;
+                if (st == 1u) {
+                    KT0(q2)
+                    st = run_work(P, c) ? 0u : 2u;
+                    KTA(k_rw, q2)
+                }
+                if (__ballot(st <= 1u) == 0) break;
             }
             KTA(k_in, q4)
             KT0(q3)
             flush_wave(P, c);
             KTA(k_fl, q3)
-        } while (__ballot(!fin) != 0);
+            if (__ballot(st == 2u) == 0) break;
+            if (st == 2u) st = 1u;
+        }
     }
     TIM(9);
     if (active) {
@@ -1502,11 +1559,12 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
         if (c.min_emit < next) next = c.min_emit;
         if (P.bins) {
             // bins wholly before we are consumed: reset them (no append of
-            // this round can target them: appends are >= we and within the horizon)
+            // this round can target them: appends are >= we and within the
+            // horizon).  Idle hosts reset their counts too (cal_reset_counts).
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++) {
                 const uint64_t b = b0 + j;
-                if (j < nbin && ((b + 1) << P.bin_shift) <= we && (bcnt[j] || ((wbits >> j) & 1u))) {
+                if (j < nbin && ((b + 1) << P.bin_shift) <= we) {
                     const uint32_t p = (uint32_t)b & (kNB - 1);
                     P.bin_n[(size_t)l * kNB + p] = 0;
                     if ((wbits >> j) & 1u) {
@@ -1521,8 +1579,8 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
             const uint64_t cb = cal_lower_bound(P, w, we);
             next = cb < next ? cb : next;
         }
-        nev = c.c_events - ev0;
-        npkt = c.c_pkt - pk0;
+        nev = c.c_events;
+        npkt = c.c_pkt;
         err |= c.err;
         PROF_T0(t_s)
         TIMA(10);
@@ -1671,21 +1729,26 @@ __device__ void resolve_block(const Params& P, int next_parity) {
 // to back from one batch launch (or graph) with no host round trip; the last
 // block resolves the round's first-touch log.  A round past `stop` only
 // forwards the time.  `init` is the next round's summary, initialised here.
-__global__ __launch_bounds__(kBlock) void k_round_dev(Params P, const DevSummary* __restrict__ prev,
+// The hot kernels take Params through a pointer to a device copy (one per
+// summary-ring slot): fields are scalar-loaded where used instead of all held
+// in SGPRs, which otherwise spill to VGPR lanes around every branch.
+__global__ __launch_bounds__(kBlock) void k_round_dev(const Params* __restrict__ Pp, const DevSummary* __restrict__ prev,
                                                        DevSummary* __restrict__ init,
                                                        const DevCtl* __restrict__ ctl, int i, uint64_t window) {
+    const Params& P = *Pp;
 #ifdef SHD_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
-    if (*P.halt) return;
+    // the round's inputs, loaded together (one round trip)
+    const uint32_t halt = *P.halt;
+    const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws = prev->next_time;
+    if (halt) return;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     if (lead) {
         atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
         *init = fresh_summary();
     }
-    const uint64_t stop = ctl->stop;
-    const int parity = (int)((ctl->round_base + (uint64_t)i) & 1);
-    const uint64_t ws = prev->next_time;
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
     if (ws >= stop) {
         if (lead) atomicMin(&P.sum->next_time, (unsigned long long)ws);
         return;
@@ -1768,9 +1831,10 @@ __global__ void k_xpack(Params P, const DevSummary* __restrict__ sum, int clean)
 // headers of the last exchange; any flagged header (a first-touch log, a
 // spill or an error anywhere in the group) halts the batch on every engine
 // alike.  The last block writes this engine's headers for the next exchange.
-__global__ __launch_bounds__(kBlock) void k_round_x(Params P, const shd_event* __restrict__ xrecv,
+__global__ __launch_bounds__(kBlock) void k_round_x(const Params* __restrict__ Pp, const shd_event* __restrict__ xrecv,
                                                     XHeader* __restrict__ halt_hdr, DevSummary* __restrict__ init,
                                                     const DevCtl* __restrict__ ctl, int i, uint64_t window) {
+    const Params& P = *Pp;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     if (*P.halt) {
         if (lead) P.sum->flags = 2u;
@@ -1846,8 +1910,9 @@ __global__ void k_digest(Params P, shd_host_digest* __restrict__ out) {
     const HostRec r = P.hs[l];
     d.ev_seq = r.ev_seq; d.rx_remaining = r.rx_rem; d.tx_remaining = r.tx_rem;
     d.codel_total = r.cq_total; d.codel_interval_expire = r.cq_iexp; d.codel_next_drop = r.cq_ndrop;
-    d.n_events = r.c_events; d.n_pkt_events = r.c_pkt; d.n_sent = r.c_sent;
-    d.n_inet_drop = r.c_idrop; d.n_codel_drop = r.c_cdrop; d.n_recv = r.c_recv;
+    const HostCnt k = P.hc[l];
+    d.n_events = k.events; d.n_pkt_events = k.pkt; d.n_sent = k.sent;
+    d.n_inet_drop = k.idrop; d.n_codel_drop = k.cdrop; d.n_recv = k.recv;
     d.rng = r.rng; d.pkt_seq = r.pkt_seq;
     const uint32_t f = r.flags;
     d.codel_mode = (f & F_CODEL_DROP_MODE) ? 1u : 0u;
@@ -1898,6 +1963,7 @@ struct shd_eng {
     int32_t* d_host_att = nullptr;
     double* d_cum = nullptr;
     DestGuide* d_guide = nullptr;
+    int2* d_self_thr = nullptr;
     int32_t* d_rank = nullptr;
     int32_t* d_self_rank = nullptr;
     DevSummary* d_sum = nullptr;
@@ -1924,9 +1990,24 @@ struct shd_eng {
     DevCtl* h_ctl = nullptr;
     DevSummary* h_seed = nullptr;           // pinned: ring slots 0 and 1 at a batch start
     hipGraphExec_t batch_graph = nullptr;   // captured batch of kBatch device-driven rounds
+    Params* d_pr = nullptr;                 // device copies of P, one per summary-ring slot (sum = &d_ring[i])
     double wall_khz = 100000.0;             // device wall clock (wall_clock64) rate
     uint64_t trace_cap = 0;
 };
+
+// the largest rand_r value x with (double)x / RAND_MAX <= c (-1 if none):
+// the quotient is correctly rounded on host and device alike and monotone in
+// x, so the device compares integers instead of dividing
+static int32_t draw_threshold(double c) {
+    int64_t lo = -1, hi = 2147483647;   // invariant: ok(lo) (or lo == -1), !ok(hi + 1)
+    auto ok = [c](int64_t x) { return (double)x / 2147483647.0 <= c; };
+    if (ok(hi)) return (int32_t)hi;
+    while (hi - lo > 1) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (ok(mid)) lo = mid; else hi = mid;
+    }
+    return (int32_t)lo;
+}
 
 template <typename T>
 static int ealloc(shd_eng* e, T** p, size_t n, bool zero = true) {
@@ -1988,6 +2069,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.pkt_len = m->payload + SHD_HEADER_UDP;
     const size_t n = (size_t)e->nloc;
     EALLOC(P.hs, n);
+    EALLOC(P.hc, n);
     EALLOC(P.part, n);
     EALLOC(P.gpart, n / kTickGroup + 2);
     EALLOC(P.tick, n / kTickGroup + 3);
@@ -2005,6 +2087,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     }
     EALLOC(e->d_rng0, H); EALLOC(e->d_bwd, H); EALLOC(e->d_bwu, H); EALLOC(e->d_host_att, H); EALLOC(e->d_cum, H);
     EALLOC(e->d_guide, H);
+    EALLOC(e->d_self_thr, H);
     // destination guide table: guide[k] = first i with cum[i] >= k / H (H if none)
     std::vector<DestGuide> guide(H);
     for (int32_t k = 0, i = 0; k < H; k++) {
@@ -2076,7 +2159,22 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.host_att = e->d_host_att;
     P.dest_cum = e->d_cum;
     P.dest_guide = e->d_guide;
-    P.cum_last = m->dest_cum[H - 1];
+    // draw thresholds: x / RAND_MAX <= c  <=>  x <= draw_threshold(c)
+    {
+        std::vector<int2> thr(H);
+        for (int32_t h = 0; h < H; h++) {
+            thr[h].x = h ? draw_threshold(m->dest_cum[h - 1]) + 1 : 0;
+            thr[h].y = draw_threshold(m->dest_cum[h]);
+        }
+        P.dst_thr = draw_threshold(m->dest_cum[H - 1]);
+        if (hipMemcpyAsync(e->d_self_thr, thr.data(), sizeof(int2) * (size_t)H, hipMemcpyHostToDevice, e->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess) {
+            shd_eng_destroy(e);
+            return SHD_ENODEV;
+        }
+        P.self_thr = e->d_self_thr;
+    }
     P.T = pc->T;
     P.complete = pc->complete; P.prefer_direct = pc->prefer_direct; P.directed = pc->directed;
     P.row = pc->d_row; P.dir = pc->d_dir; P.self = pc->d_self;
@@ -2109,7 +2207,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         e->window = (uint64_t)ceil(ml * (double)SHD_MS);
         if (e->window == 0) e->window = 1;
     }
-    // calendar: bin width = the largest power of two <= W
+    // calendar: bin width = the largest power of two <= W (Params complete below)
     if (!(m->queue_flags & SHD_QF_NO_CALENDAR)) {
         P.bin_shift = 63u - (uint32_t)__builtin_clzll(e->window);
         int rc;
@@ -2117,6 +2215,18 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             (rc = ealloc(e, &P.bin_bits, n * kNBW))) {
             shd_eng_destroy(e);
             return rc;
+        }
+    }
+    {   // the per-slot device copies of P
+        int rc;
+        if ((rc = ealloc(e, &e->d_pr, shd_eng::kRing, false))) { shd_eng_destroy(e); return rc; }
+        std::vector<Params> pr(shd_eng::kRing, P);
+        for (int i = 0; i < shd_eng::kRing; i++) pr[i].sum = &e->d_ring[i];
+        if (hipMemcpyAsync(e->d_pr, pr.data(), sizeof(Params) * pr.size(), hipMemcpyHostToDevice, e->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess) {
+            shd_eng_destroy(e);
+            return SHD_ENODEV;
         }
     }
     *out = e;
@@ -2314,9 +2424,8 @@ static int enqueue_batch(shd_eng* e) {
     constexpr int B = shd_eng::kBatch;
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     for (int i = 0; i < B; i++) {
-        Params P = e->P;
-        P.sum = &e->d_ring[i + 1];
-        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, P, (const DevSummary*)&e->d_ring[i],
+        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, (const Params*)(e->d_pr + i + 1),
+                           (const DevSummary*)&e->d_ring[i],
                            &e->d_ring[i + 2], (const DevCtl*)e->d_ctl, i, e->window);
     }
     SHD_HIP(hipGetLastError());
@@ -2583,6 +2692,7 @@ struct shd_xgroup {
         shd_event* xrecv[2] = {nullptr, nullptr};
         uint32_t* xcount = nullptr;
         XHeader* halt_hdr = nullptr;
+        Params* d_xpr = nullptr;   // device copies of the exchange-mode P, one per summary-ring slot
     };
     std::vector<Loc> loc;
     uint64_t xseq = 0;                 // exchanges done: the latest headers are in xrecv[(xseq - 1) & 1]
@@ -2817,8 +2927,12 @@ static int x_alloc(shd_xgroup* g) {
         const size_t n = g->stride * (size_t)g->world;
         int rc;
         if ((rc = ealloc(e, &L.xsend, n)) || (rc = ealloc(e, &L.xrecv[0], n)) || (rc = ealloc(e, &L.xrecv[1], n)) ||
-            (rc = ealloc(e, &L.xcount, g->world)) || (rc = ealloc(e, &L.halt_hdr, g->world)))
+            (rc = ealloc(e, &L.xcount, g->world)) || (rc = ealloc(e, &L.halt_hdr, g->world)) ||
+            (rc = ealloc(e, &L.d_xpr, shd_eng::kRing, false)))
             return rc;
+        std::vector<Params> pr(shd_eng::kRing);
+        for (int i = 0; i < shd_eng::kRing; i++) pr[i] = xparams(g, (int)k, &e->d_ring[i]);
+        SHD_HIP(hipMemcpyAsync(L.d_xpr, pr.data(), sizeof(Params) * pr.size(), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipStreamSynchronize(e->stream));
     }
     return SHD_OK;
@@ -2986,9 +3100,9 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             const int ri = (int)((g->xseq - 1) & 1);
             for (int k = 0; k < nl; k++) {
                 shd_eng* e = g->engs[k];
-                const Params P = xparams(g, k, &e->d_ring[i + 1]);
-                const int grid = (e->nloc + P.hpw - 1) / P.hpw;
-                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, P,
+                const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
+                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream,
+                                   (const Params*)(g->loc[k].d_xpr + i + 1),
                                    (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
                                    (const DevCtl*)e->d_ctl, i, g->window);
             }
