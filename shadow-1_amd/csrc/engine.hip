@@ -172,7 +172,8 @@ struct DestGuide {
 };
 static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 
-struct Params {
+template <template <class> class Ptr>
+struct ParamsT {
     // hosts
     int32_t H;                  // total hosts of the model
     int32_t h0, nloc;           // this engine's hosts [h0, h0+nloc)
@@ -182,67 +183,82 @@ struct Params {
     uint32_t load, payload, trace, pkt_len;
     // per-host state records (local index), and the earliest pending event
     // of each host's timers and heap (read alone by the idle test)
-    HostRec* hs;
-    HostCnt* hc;
-    uint64_t* hnext;
+    Ptr<HostRec> hs;
+    Ptr<HostCnt> hc;
+    Ptr<uint64_t> hnext;
     // queues: per-host 4-ary heap of the other events (packets, loopback, boot one-shots)
-    shd_event* evq;              // slab of evq_stride entries per host, heap at +3
+    Ptr<shd_event> evq;              // slab of evq_stride entries per host, heap at +3
     uint32_t evq_stride;
-    shd_event* inbox[2];
-    uint32_t* inbox_n[2];
+    Ptr<shd_event> inbox[2];
+    Ptr<uint32_t> inbox_n[2];
     // round completion (round_complete): per-block and per-group summary
     // shares, and the two-level tickets (reset by the blocks that win them)
-    BlockPart* part;
-    BlockPart* gpart;
-    uint32_t* tick;
+    Ptr<BlockPart> part;
+    Ptr<BlockPart> gpart;
+    Ptr<uint32_t> tick;
     // calendar (null = off): per host a ring of kNB time bins of width
     // 2^bin_shift <= W ns with kBinCap event slots each.  Senders append with
     // one atomic on the bin's count; the owner reads the <= 3 bins of its
     // window in one pass.  Far-future events and full bins take the inbox.
-    shd_event* bins;             // [nloc][kNB][kBinCap]
-    uint32_t* bin_n;             // [nloc][kNB] appends (may exceed kBinCap: those went to the inbox)
-    uint32_t* bin_bits;          // [nloc][kNBW] non-empty bins
+    Ptr<shd_event> bins;             // [nloc][kNB][kBinCap]
+    Ptr<uint32_t> bin_n;             // [nloc][kNB] appends (may exceed kBinCap: those went to the inbox)
+    Ptr<uint32_t> bin_bits;          // [nloc][kNBW] non-empty bins
     uint32_t bin_shift;
-    CodelEnt* cq;
-    TxEnt* tq;
+    Ptr<CodelEnt> cq;
+    Ptr<TxEnt> tq;
     // global host tables (all H hosts)
-    const int32_t* host_att;     // attached index of every host
-    const double* dest_cum;
-    const struct DestGuide* dest_guide;   // [H]: bucket k -> first i with dest_cum[i] >= k / H
+    Ptr<const int32_t> host_att;     // attached index of every host
+    Ptr<const double> dest_cum;
+    Ptr<const DestGuide> dest_guide;   // [H]: bucket k -> first i with dest_cum[i] >= k / H
     // destination draws as rand_r values x (r = x / RAND_MAX): there is a
     // destination iff x <= dst_thr; host h's own draws (loopback) are
     // self_thr[h].x <= x <= self_thr[h].y (precomputed, exact)
     int32_t dst_thr;
-    const int2* self_thr;
+    Ptr<const int2> self_thr;
     // path cache
     int32_t T;
     int32_t complete, prefer_direct, directed;
-    const shd_pv* row;           // [T][T] (lat, rel)
-    const shd_pv* dir;           // [T][T] direct-edge values
-    const shd_pv* self;          // [T] self-path values
-    const uint8_t* adj;
-    const int32_t* rank;
-    const int32_t* self_rank;
+    Ptr<const shd_pv> row;           // [T][T] (lat, rel)
+    Ptr<const shd_pv> dir;           // [T][T] direct-edge values
+    Ptr<const shd_pv> self;          // [T] self-path values
+    Ptr<const uint8_t> adj;
+    Ptr<const int32_t> rank;
+    Ptr<const int32_t> self_rank;
     // outputs
-    Pending* pend;
+    Ptr<Pending> pend;
     uint32_t pend_cap;
-    shd_event* remote;
+    Ptr<shd_event> remote;
     uint32_t remote_cap;
-    shd_trace_rec* trace_buf;
+    Ptr<shd_trace_rec> trace_buf;
     uint64_t trace_cap;
     unsigned long long* trace_n;   // cumulative trace records
-    DevSummary* sum;               // this round's summary
-    int32_t* next_rank;            // row-rank counter (device is the source of truth)
-    uint32_t* halt;                // set when a round needs host-side resolution
+    Ptr<DevSummary> sum;               // this round's summary
+    Ptr<int32_t> next_rank;            // row-rank counter (device is the source of truth)
+    Ptr<uint32_t> halt;                // set when a round needs host-side resolution
     // exchange mode (null xsend: remote events go to `remote`)
-    shd_event* xsend;              // [xworld][xcap + 1]
-    uint32_t* xcount;              // [xworld] events queued per peer this round
+    Ptr<shd_event> xsend;              // [xworld][xcap + 1]
+    Ptr<uint32_t> xcount;              // [xworld] events queued per peer this round
     uint32_t xcap;
     int32_t xworld;                // engines of the group; host partition (H*p)/xworld
 };
+// The host fills Params (plain pointers); device code reads the same bytes
+// as DParams, whose pointers carry the global address space, so that loads
+// and stores through a Params read via a pointer stay global_* instructions
+// (generic pointers would make every access a flat_* one).
+template <class T> using HostPtr = T*;
+#ifdef __HIP_DEVICE_COMPILE__
+template <class T> using GlobalPtr = T __attribute__((address_space(1)))*;
+#else   // the host pass only type-checks device code: no address spaces there
+template <class T> using GlobalPtr = T*;
+#endif
+using Params = ParamsT<HostPtr>;
+using DParams = ParamsT<GlobalPtr>;
+static_assert(sizeof(Params) == sizeof(DParams), "one layout");
+static inline const DParams& dp(const Params& P) { return *reinterpret_cast<const DParams*>(&P); }
+
 
 // engine of the group that owns host h: the partition is b[p] = (H*p)/N
-__device__ __forceinline__ int32_t owner_of(const Params& P, uint32_t h) {
+__device__ __forceinline__ int32_t owner_of(const DParams& P, uint32_t h) {
     const uint64_t H = (uint64_t)P.H, N = (uint64_t)P.xworld;
     int64_t p = (int64_t)(((uint64_t)h * N) / H);
     while (p + 1 < (int64_t)N && (H * (uint64_t)(p + 1)) / N <= h) p++;
@@ -373,11 +389,11 @@ __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) 
 // 4-ary min-heap; the slab's entry 3 is the root, so the four children of
 // node i (4i+1 .. 4i+4) fill one aligned 128-B line.  The root is cached in
 // LDS (s_top) and its time in a register: peeking never touches HBM.
-__device__ __forceinline__ shd_event* heap_base(const Params& P, const HostCtx& c) {
+__device__ __forceinline__ shd_event* heap_base(const DParams& P, const HostCtx& c) {
     return P.evq + (size_t)c.l * P.evq_stride + 3;
 }
 
-__device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
+__device__ void heap_push(const DParams& P, HostCtx& c, const shd_event& e) {
     shd_event* hp = heap_base(P, c);
     if (c.evq_n >= P.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
     uint32_t i = c.evq_n++;
@@ -402,7 +418,7 @@ __device__ void heap_push(const Params& P, HostCtx& c, const shd_event& e) {
 }
 
 // remove the root; the new root is re-cached
-__device__ void heap_pop(const Params& P, HostCtx& c) {
+__device__ void heap_pop(const DParams& P, HostCtx& c) {
     shd_event* hp = heap_base(P, c);
     const uint32_t n = --c.evq_n;
     if (n == 0) return;
@@ -429,7 +445,7 @@ __device__ void heap_pop(const Params& P, HostCtx& c) {
     if (i == 0) { s_top[threadIdx.x] = last; c.top_time = last.time; }
 }
 
-__device__ __forceinline__ void trace(const Params& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
+__device__ __forceinline__ void trace(const DParams& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
                                       uint32_t peer, uint32_t pkt, uint32_t kind) {
     if (!P.trace) return;
     unsigned long long i = atomicAdd(P.trace_n, 1ull);
@@ -439,11 +455,11 @@ __device__ __forceinline__ void trace(const Params& P, HostCtx& c, uint64_t t, u
     P.trace_buf[i] = r;
 }
 
-__device__ __forceinline__ bool bootstrapping(const Params& P, const HostCtx& c) { return c.now < P.bootstrap_end; }
+__device__ __forceinline__ bool bootstrapping(const DParams& P, const HostCtx& c) { return c.now < P.bootstrap_end; }
 
 // event_new_ (consumes the source's event ID, event.c:38) + scheduler_push
 // (discards time >= end, scheduler.c:346-349) for a self event
-__device__ void schedule_self(const Params& P, HostCtx& c, uint32_t kind, uint64_t delay, uint32_t pkt) {
+__device__ void schedule_self(const DParams& P, HostCtx& c, uint32_t kind, uint64_t delay, uint32_t pkt) {
     // heap events carry exact IDs: the send loop flushes the deferred sends
     // before a loopback send (timer slots may hold provisional IDs, fixed up
     // by the flush)
@@ -479,7 +495,7 @@ __device__ void schedule_self(const Params& P, HostCtx& c, uint32_t kind, uint64
 // caller then takes the inbox).  The event is stored before the bin's bit is
 // set; readers filter slots by time, so a slot claimed but not yet written
 // (time still that of an older, processed event, or kInf) is never taken.
-__device__ __forceinline__ bool cal_push(const Params& P, int32_t dl, const shd_event& e, uint64_t ws) {
+__device__ __forceinline__ bool cal_push(const DParams& P, int32_t dl, const shd_event& e, uint64_t ws) {
     if (!P.bins) return false;
     const uint64_t b = e.time >> P.bin_shift;
     if (b - (ws >> P.bin_shift) > kHorizon) return false;
@@ -497,7 +513,7 @@ __device__ __forceinline__ bool cal_push(const Params& P, int32_t dl, const shd_
 // the calendar-less part of a delivery: the inbox of a local destination
 // (merged into its heap next round), else the peer's all-to-all block or the
 // remote outbox
-__device__ void emit_nocal(const Params& P, HostCtx& c, const shd_event& e) {
+__device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl >= 0 && dl < P.nloc) {
         uint32_t slot = atomicAdd(&P.inbox_n[c.np][dl], 1u);
@@ -522,7 +538,7 @@ __device__ void emit_nocal(const Params& P, HostCtx& c, const shd_event& e) {
 
 // _networkinterface_scheduleNextRefillIfNeeded (network_interface.c:130-161),
 // timeStartedRefillingBuckets = 0
-__device__ void refill_if_needed(const Params& P, HostCtx& c) {
+__device__ void refill_if_needed(const DParams& P, HostCtx& c) {
     const bool need = (c.tx_rem < c.tx_refill + SHD_MTU) || (c.rx_rem < c.rx_refill + SHD_MTU);
     if (need && !(c.flags & F_REFILL_PENDING)) {
         // now % 1 ms from the round's ws % 1 ms and the 32-bit offset into the round
@@ -535,7 +551,7 @@ __device__ void refill_if_needed(const Params& P, HostCtx& c) {
 __device__ __forceinline__ void consume(uint64_t& rem, uint64_t n) { rem = (n >= rem) ? 0 : rem - n; }
 
 // _networkinterface_receivePacket (network_interface.c:375-419)
-__device__ void if_receive_packet(const Params& P, HostCtx& c, uint32_t src, uint32_t pkt) {
+__device__ void if_receive_packet(const DParams& P, HostCtx& c, uint32_t src, uint32_t pkt) {
     if (c.flags & F_LISTENING) {
         trace(P, c, c.now, 0, c.h, src, pkt, SHD_TR_RECV);
         c.c_recv++;
@@ -556,7 +572,7 @@ __device__ __forceinline__ uint64_t codel_control_law(uint32_t count, uint64_t t
     return (uint64_t)round(result);
 }
 
-__device__ bool codel_helper(const Params& P, HostCtx& c, bool& okToDrop, CodelEnt& out) {
+__device__ bool codel_helper(const DParams& P, HostCtx& c, bool& okToDrop, CodelEnt& out) {
     okToDrop = false;
     if (c.cq_count == 0) { c.cq_iexp = 0; return false; }
     if (c.cq_hv) {
@@ -578,12 +594,12 @@ __device__ bool codel_helper(const Params& P, HostCtx& c, bool& okToDrop, CodelE
     return true;
 }
 
-__device__ __forceinline__ void codel_drop(const Params& P, HostCtx& c, const CodelEnt& e) {
+__device__ __forceinline__ void codel_drop(const DParams& P, HostCtx& c, const CodelEnt& e) {
     trace(P, c, c.now, 0, c.h, e.src, e.pkt, SHD_TR_CODEL_DROP);
     c.c_cdrop++;
 }
 
-__device__ bool codel_dequeue(const Params& P, HostCtx& c, CodelEnt& out) {
+__device__ bool codel_dequeue(const DParams& P, HostCtx& c, CodelEnt& out) {
     bool okToDrop = false;
     CodelEnt pkt;
     bool have = codel_helper(P, c, okToDrop, pkt);
@@ -614,7 +630,7 @@ __device__ bool codel_dequeue(const Params& P, HostCtx& c, CodelEnt& out) {
 }
 
 // networkinterface_receivePackets (network_interface.c:421-455)
-__device__ void if_receive_packets(const Params& P, HostCtx& c) {
+__device__ void if_receive_packets(const DParams& P, HostCtx& c) {
     const bool boot = bootstrapping(P, c);
     while (boot || c.rx_rem >= SHD_MTU) {
         CodelEnt p;
@@ -643,7 +659,7 @@ struct PathRaw {
     uint32_t adj;
 };
 
-__device__ __forceinline__ void path_load(const Params& P, int32_t a, int32_t b, PathRaw& x) {
+__device__ __forceinline__ void path_load(const DParams& P, int32_t a, int32_t b, PathRaw& x) {
     const size_t ab = (size_t)a * P.T + b, ba = (size_t)b * P.T + a;
     x.adj = 0; x.rb = kNoRank; x.rs = kNoRank;
     if (P.complete) { x.d = P.dir[ab]; return; }
@@ -658,7 +674,7 @@ __device__ __forceinline__ void path_load(const Params& P, int32_t a, int32_t b,
     }
 }
 
-__device__ __forceinline__ PathVal path_select(const Params& P, int32_t a, int32_t b, int32_t ra, const PathRaw& x) {
+__device__ __forceinline__ PathVal path_select(const DParams& P, int32_t a, int32_t b, int32_t ra, const PathRaw& x) {
     PathVal v;
     v.resolved = true;
     v.log = false;
@@ -692,14 +708,14 @@ __device__ __forceinline__ PathVal path_select(const Params& P, int32_t a, int32
     return v;
 }
 
-__device__ PathVal path_value(const Params& P, int32_t a, int32_t b) {
+__device__ PathVal path_value(const DParams& P, int32_t a, int32_t b) {
     PathRaw x;
     const int32_t ra = P.complete ? kNoRank : P.rank[a];
     path_load(P, a, b, x);
     return path_select(P, a, b, ra, x);
 }
 
-__device__ void log_pending(const Params& P, HostCtx& c, const SendRec& q, int32_t a, int32_t b, uint32_t delivered,
+__device__ void log_pending(const DParams& P, HostCtx& c, const SendRec& q, int32_t a, int32_t b, uint32_t delivered,
                             uint32_t dst, uint64_t seq) {
     unsigned long long i = atomicAdd(&P.sum->n_pending, 1ull);
     c.n_pend++;
@@ -728,11 +744,11 @@ __device__ __forceinline__ bool is_self_draw(const HostCtx& c, uint32_t rv) {
 // guide[k] is a lower bound of it for any k <= r*H - 1; for even weights the
 // answer is one of the next three entries (their attached index inline), else
 // a binary search finishes the job.  Only called for draws r <= dest_cum[H-1].
-__device__ __forceinline__ uint32_t guide_index(const Params& P, double r) {
+__device__ __forceinline__ uint32_t guide_index(const DParams& P, double r) {
     int32_t k = (int32_t)(r * (double)P.H) - 1;
     return (uint32_t)(k < 0 ? 0 : (k > P.H - 1 ? P.H - 1 : k));
 }
-__device__ __forceinline__ void guide_pick(const Params& P, const DestGuide& g, double r, int32_t& dst, int32_t& att) {
+__device__ __forceinline__ void guide_pick(const DParams& P, const DestGuide& g, double r, int32_t& dst, int32_t& att) {
     // static indices only: a dynamically indexed guide would live in scratch
     const bool f0 = g.cum[0] >= r, f1 = g.cum[1] >= r, f2 = g.cum[2] >= r;
     if (f0 || f1 || f2) {
@@ -752,7 +768,7 @@ __device__ __forceinline__ void guide_pick(const Params& P, const DestGuide& g, 
 // worker_sendPacket (worker.c:260-321), deferred: the reliability draw is
 // made now (it is drawn for every non-loopback send, worker.c:286); the
 // path lookup, the drop decision and the delivery happen at the next flush
-__device__ void worker_send_deferred(const Params& P, HostCtx& c, uint32_t rv, uint32_t pkt) {
+__device__ void worker_send_deferred(const DParams& P, HostCtx& c, uint32_t rv, uint32_t pkt) {
     const uint32_t chance = (uint32_t)rand_r_dev(c.rng);
     SendRec q;
     q.now = c.now; q.q_seq = c.q_seq; q.q_src = c.q_src;
@@ -770,7 +786,7 @@ __device__ void worker_send_deferred(const Params& P, HostCtx& c, uint32_t rv, u
 // round trip each per 64 sends of the wave); then each host walks its own
 // sends in order (event IDs, counters, traces, first-touch logs, LDS only);
 // then record-parallel deliveries (one round trip for the calendar claims).
-__device__ void flush_wave(const Params& P, HostCtx& c) {
+__device__ void flush_wave(const DParams& P, HostCtx& c) {
     const uint32_t lane = threadIdx.x;
     const uint32_t n = c.ns;
     uint32_t pre = n;   // inclusive, then exclusive prefix of the lanes' counts
@@ -897,7 +913,7 @@ __device__ void flush_wave(const Params& P, HostCtx& c) {
 // Returns true when it stopped early for a flush of the deferred sends (the
 // buffer is full, or the next send is a loopback, whose trace and event take
 // the exact event ID); the caller flushes and calls it again.
-__device__ bool if_send_step(const Params& P, HostCtx& c) {
+__device__ bool if_send_step(const DParams& P, HostCtx& c) {
     const bool boot = bootstrapping(P, c);
     while (c.tx_rem >= SHD_MTU) {
         if (c.tq_count == 0) break;
@@ -939,7 +955,7 @@ __device__ __forceinline__ void random_free_port(HostCtx& c) { (void)rand_r_dev(
 // _phold_sendNewMessage (test_phold.c:218-230) up to the socket send: draw
 // the destination (resolved at the flush; only whether one exists matters
 // here), bind, queue the datagram; false when nothing was queued
-__device__ bool enqueue_new_message(const Params& P, HostCtx& c) {
+__device__ bool enqueue_new_message(const DParams& P, HostCtx& c) {
     PROF_T0(tp)
     const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
     PROF_ADD(c, PR_PICK, tp)
@@ -960,7 +976,7 @@ __device__ bool enqueue_new_message(const Params& P, HostCtx& c) {
 }
 
 // _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
-__device__ void refill_cb(const Params& P, HostCtx& c) {
+__device__ void refill_cb(const DParams& P, HostCtx& c) {
     c.flags &= ~F_REFILL_PENDING;
     c.rx_rem += c.rx_refill;
     if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
@@ -982,7 +998,7 @@ __device__ void refill_cb(const Params& P, HostCtx& c) {
 //   PACKET    router_enqueue, receive if the queue was empty
 //   NOTIFY    one new message per unread datagram, each sent right away
 //   APP_START `load` new messages
-__device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
+__device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     c.c_events++;
     c.q_seq = e.seq;
     c.q_src = e.src;
@@ -1000,7 +1016,17 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
         c.tx_rem += c.tx_refill;
         if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
-        c.w_fl = W_RX | W_TX | W_REFILL;
+        if (c.cq_count == 0 && c.tq_count == 0) {
+            // both queues empty: the receive loop's one dequeue attempt only
+            // resets CoDel's interval and drop mode; the send loop does nothing
+            if (bootstrapping(P, c) || c.rx_rem >= SHD_MTU) {
+                c.cq_iexp = 0;
+                c.flags &= ~F_CODEL_DROP_MODE;
+            }
+            refill_if_needed(P, c);
+        } else {
+            c.w_fl = W_RX | W_TX | W_REFILL;
+        }
         break;
     case SHD_EV_REFILL_LO:
         break;
@@ -1012,6 +1038,18 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
         c.c_pkt++;
         trace(P, c, c.now, e.seq, c.h, e.src, e.pkt, SHD_TR_ARRIVE);
+        if (c.cq_count == 0 && c.rx_rem >= SHD_MTU && !bootstrapping(P, c)) {
+            // an empty router queue and room in the receive bucket: the packet
+            // is enqueued and dequeued at once (sojourn 0: CoDel's interval
+            // and drop mode reset; the second dequeue attempt finds nothing)
+            c.cq_head = (c.cq_head + 1 == P.cq_cap) ? 0 : c.cq_head + 1;
+            c.cq_iexp = 0;
+            c.flags &= ~F_CODEL_DROP_MODE;
+            if_receive_packet(P, c, e.src, e.pkt);
+            consume(c.rx_rem, P.pkt_len);
+            refill_if_needed(P, c);
+            break;
+        }
         const bool was_empty = c.cq_count == 0;
         if (c.cq_count >= P.cq_cap) { c.err |= SHD_ERR_CODELQ_OVERFLOW; break; }
         const CodelEnt ent{c.now, e.src, e.pkt};
@@ -1044,11 +1082,33 @@ __device__ void begin_event(const Params& P, HostCtx& c, const shd_event& e) {
         if_receive_packets(P, c);
         c.w_fl &= ~W_RX;
     }
+    // new messages while the send queue is empty and the bucket has room go
+    // straight to the wire (enqueue, then the send loop pops it at once);
+    // anything else -- a loopback, a full send buffer, a backlog, the
+    // bootstrap period -- is left to run_work's general loop, in order
+    const bool boot = bootstrapping(P, c);
+    while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap && !boot) {
+        const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
+        c.w_msgs--;
+        if ((int32_t)rv > P.dst_thr) continue;   // no destination: nothing queued
+        random_free_port(c);
+        const uint32_t pkt = c.pkt_seq++;
+        if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
+            s_tqh[threadIdx.x] = TxEnt{rv, pkt};
+            c.tq_hv = true;
+            c.tq_count = 1;
+            c.w_fl |= W_SENDING;
+            break;
+        }
+        worker_send_deferred(P, c, rv, pkt);
+        consume(c.tx_rem, P.pkt_len);
+        refill_if_needed(P, c);
+    }
 }
 
 // the event's shared steps: while (msgs || tx) { a new message if any;
 // the send loop }; then the refill check.  False when it stopped for a flush.
-__device__ bool run_work(const Params& P, HostCtx& c) {
+__device__ bool run_work(const DParams& P, HostCtx& c) {
     for (;;) {
         if (c.w_fl & W_SENDING) {
             if (if_send_step(P, c)) return false;
@@ -1073,7 +1133,7 @@ __device__ bool run_work(const Params& P, HostCtx& c) {
     return true;
 }
 
-__device__ void load_ctx(const Params& P, HostCtx& c, int32_t l) {
+__device__ void load_ctx(const DParams& P, HostCtx& c, int32_t l) {
     c.l = l;
     c.h = (uint32_t)(P.h0 + l);
     const HostRec r = P.hs[l];
@@ -1116,7 +1176,7 @@ __device__ __forceinline__ uint64_t host_next(const HostCtx& c) {
 // the host's next event in (time, src, seq) order if it is before `we`:
 // the earliest timer (src = the host) against the heap root and the head
 // of the window's calendar events
-__device__ __forceinline__ bool take_next(const Params& P, HostCtx& c, uint64_t we, shd_event& e) {
+__device__ __forceinline__ bool take_next(const DParams& P, HostCtx& c, uint64_t we, shd_event& e) {
     uint64_t bt = c.tt0, bs = c.ts0;
     uint32_t kind = SHD_EV_HEARTBEAT;
     int slot = 0;
@@ -1180,7 +1240,7 @@ __device__ __forceinline__ uint32_t bits_first_from(const uint32_t (&w)[kNBW], u
 
 // lower bound of the earliest calendar event at or after `we`: the start of
 // the first non-empty bin from we's bin on (stale bits only lower it)
-__device__ __forceinline__ uint64_t cal_lower_bound(const Params& P, const uint32_t (&w)[kNBW], uint64_t we) {
+__device__ __forceinline__ uint64_t cal_lower_bound(const DParams& P, const uint32_t (&w)[kNBW], uint64_t we) {
     const uint64_t bwe = we >> P.bin_shift;
     const uint32_t d = bits_first_from(w, (uint32_t)bwe & (kNB - 1));
     if (d >= kNB) return kInf;
@@ -1188,7 +1248,7 @@ __device__ __forceinline__ uint64_t cal_lower_bound(const Params& P, const uint3
     return t > we ? t : we;
 }
 
-__device__ void store_ctx(const Params& P, const HostCtx& c) {
+__device__ void store_ctx(const DParams& P, const HostCtx& c) {
     const int32_t l = c.l;
     HostRec r;
     r.ev_seq = c.ev_seq; r.cq_total = c.cq_total; r.cq_iexp = c.cq_iexp; r.cq_ndrop = c.cq_ndrop;
@@ -1214,7 +1274,7 @@ __device__ void store_ctx(const Params& P, const HostCtx& c) {
 }
 
 template <int BLOCK>
-__device__ void block_reduce_publish(const Params& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
+__device__ void block_reduce_publish(const DParams& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
     __shared__ unsigned long long s_next[BLOCK / 64], s_ev[BLOCK / 64], s_pkt[BLOCK / 64];
     __shared__ unsigned int s_err[BLOCK / 64];
     // wave reductions (64 lanes)
@@ -1262,7 +1322,7 @@ __device__ __forceinline__ void part_wave_reduce(BlockPart& q) {
         part_fold(q, o);
     }
 }
-__device__ bool round_complete(const Params& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
+__device__ bool round_complete(const DParams& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
     static_assert(kBlock == 64 && kTickGroup <= 64, "one wave per block; a group folds in one pass");
     __shared__ int s_last;
     BlockPart q{next, nev, npkt, err, 0};
@@ -1311,7 +1371,7 @@ __device__ bool round_complete(const Params& P, uint64_t next, uint64_t nev, uin
 // ------------------------------------------------------------------ kernels
 
 // host_boot for every local host at t = 0 (host.c:372-390)
-__global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __restrict__ rng0,
+__global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __restrict__ rng0,
                                                   const uint64_t* __restrict__ bw_down,
                                                   const uint64_t* __restrict__ bw_up) {
     const int32_t l = blockIdx.x * kBlock + threadIdx.x;
@@ -1348,7 +1408,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(Params P, const uint32_t* __res
 
 // a calendar slot's event, if it is one of the window's: onto the due list
 // (unsorted; sorted once all bins are read), or the heap when the list is full
-__device__ __forceinline__ void due_add(const Params& P, HostCtx& c, const shd_event& x, uint64_t ws, uint64_t we) {
+__device__ __forceinline__ void due_add(const DParams& P, HostCtx& c, const shd_event& x, uint64_t ws, uint64_t we) {
     if (x.time < ws || x.time >= we) return;
     if (c.nd == (uint32_t)kDueCap) {
         heap_push(P, c, x);
@@ -1368,7 +1428,7 @@ __device__ __forceinline__ uint32_t bit_at(const uint32_t (&w)[kNBW], uint32_t p
 
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
 // window, run events < we
-__device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_t we, int parity, uint64_t& next_out,
+__device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64_t we, int parity, uint64_t& next_out,
                                            uint64_t& nev_out, uint64_t& npkt_out, uint32_t& err_out) {
     const int32_t l = (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
 #ifdef SHD_PROF
@@ -1620,7 +1680,7 @@ __device__ __forceinline__ void round_body(const Params& P, uint64_t ws, uint64_
     next_out = next; nev_out = nev; npkt_out = npkt; err_out = err;
 }
 
-__global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t ws, uint64_t we, int parity) {
+__global__ __launch_bounds__(kBlock) void k_round(DParams P, uint64_t ws, uint64_t we, int parity) {
     uint64_t next, nev, npkt;
     uint32_t err;
     round_body(P, ws, we, parity, next, nev, npkt, err);
@@ -1628,7 +1688,7 @@ __global__ __launch_bounds__(kBlock) void k_round(Params P, uint64_t ws, uint64_
 }
 
 // finalize resolved pending sends: value from the min-rank row, then deliver
-__device__ void finalize_one(const Params& P, const Pending& r, int next_parity, uint64_t& next, uint32_t& err) {
+__device__ void finalize_one(const DParams& P, const Pending& r, int next_parity, uint64_t& next, uint32_t& err) {
     if (r.delivered != 1u) return;
     const PathVal pv = path_value(P, (int32_t)r.a, (int32_t)r.b);
     if (!pv.resolved) err |= SHD_ERR_AMBIGUOUS;
@@ -1649,7 +1709,7 @@ __device__ void finalize_one(const Params& P, const Pending& r, int next_parity,
     }
 }
 
-__global__ void k_finalize(Params P, const Pending* __restrict__ pend, uint32_t n, int next_parity) {
+__global__ void k_finalize(DParams P, const Pending* __restrict__ pend, uint32_t n, int next_parity) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t next = kInf;
     uint32_t err = 0;
@@ -1672,7 +1732,7 @@ __device__ __forceinline__ bool pend_less(const Pending& x, const Pending& y) {
     return x.qsub < y.qsub;
 }
 
-__device__ void resolve_block(const Params& P, int next_parity) {
+__device__ void resolve_block(const DParams& P, int next_parity) {
     __shared__ Pending recs[kResolveMax];
     __shared__ int16_t order[kResolveMax];
     const unsigned long long n = P.sum->n_pending;
@@ -1732,10 +1792,10 @@ __device__ void resolve_block(const Params& P, int next_parity) {
 // The hot kernels take Params through a pointer to a device copy (one per
 // summary-ring slot): fields are scalar-loaded where used instead of all held
 // in SGPRs, which otherwise spill to VGPR lanes around every branch.
-__global__ __launch_bounds__(kBlock) void k_round_dev(const Params* __restrict__ Pp, const DevSummary* __restrict__ prev,
+__global__ __launch_bounds__(kBlock) void k_round_dev(const DParams* __restrict__ Pp, const DevSummary* __restrict__ prev,
                                                        DevSummary* __restrict__ init,
                                                        const DevCtl* __restrict__ ctl, int i, uint64_t window) {
-    const Params& P = *Pp;
+    const DParams& P = *Pp;
 #ifdef SHD_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
@@ -1771,7 +1831,7 @@ __global__ __launch_bounds__(kBlock) void k_round_dev(const Params* __restrict__
 }
 
 // ingest events from other engines into inbox[parity]
-__global__ void k_ingest(Params P, const shd_event* __restrict__ ev, uint64_t n, int parity) {
+__global__ void k_ingest(DParams P, const shd_event* __restrict__ ev, uint64_t n, int parity) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const shd_event e = ev[i];
@@ -1801,7 +1861,7 @@ __global__ void k_xcopy_local(XPtrs X, uint64_t stride) {
 // headers of this engine's blocks, one lane per peer: the engine's next event
 // time and the round's flags; `clean` after a host recovery (the recovered
 // round's flags are not repeated).  Resets the per-peer counters.
-__device__ void xpack_block(const Params& P, const DevSummary* sum, int clean, uint64_t next_time) {
+__device__ void xpack_block(const DParams& P, const DevSummary* sum, int clean, uint64_t next_time) {
     const int32_t p = threadIdx.x;
     if (p >= P.xworld) return;
     const uint32_t cnt = P.xcount[p];
@@ -1822,7 +1882,7 @@ __device__ void xpack_block(const Params& P, const DevSummary* sum, int clean, u
     P.xcount[p] = 0;
 }
 
-__global__ void k_xpack(Params P, const DevSummary* __restrict__ sum, int clean) {
+__global__ void k_xpack(DParams P, const DevSummary* __restrict__ sum, int clean) {
     if (*P.halt) return;
     xpack_block(P, sum, clean, sum->next_time);
 }
@@ -1831,10 +1891,10 @@ __global__ void k_xpack(Params P, const DevSummary* __restrict__ sum, int clean)
 // headers of the last exchange; any flagged header (a first-touch log, a
 // spill or an error anywhere in the group) halts the batch on every engine
 // alike.  The last block writes this engine's headers for the next exchange.
-__global__ __launch_bounds__(kBlock) void k_round_x(const Params* __restrict__ Pp, const shd_event* __restrict__ xrecv,
+__global__ __launch_bounds__(kBlock) void k_round_x(const DParams* __restrict__ Pp, const shd_event* __restrict__ xrecv,
                                                     XHeader* __restrict__ halt_hdr, DevSummary* __restrict__ init,
                                                     const DevCtl* __restrict__ ctl, int i, uint64_t window) {
-    const Params& P = *Pp;
+    const DParams& P = *Pp;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     if (*P.halt) {
         if (lead) P.sum->flags = 2u;
@@ -1886,7 +1946,7 @@ __global__ __launch_bounds__(kBlock) void k_round_x(const Params* __restrict__ P
 }
 
 // events received in the exchange -> inbox[parity] of the next round
-__global__ void k_ingest_x(Params P, const shd_event* __restrict__ xrecv, const DevCtl* __restrict__ ctl, int ri) {
+__global__ void k_ingest_x(DParams P, const shd_event* __restrict__ xrecv, const DevCtl* __restrict__ ctl, int ri) {
     if (*P.halt) return;
     const int parity = (int)((ctl->round_base + (uint64_t)ri + 1) & 1);   // the next round's inbox
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1903,7 +1963,7 @@ __global__ void k_ingest_x(Params P, const shd_event* __restrict__ xrecv, const 
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
 }
 
-__global__ void k_digest(Params P, shd_host_digest* __restrict__ out) {
+__global__ void k_digest(DParams P, shd_host_digest* __restrict__ out) {
     const int32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= P.nloc) return;
     shd_host_digest d;
@@ -2278,7 +2338,7 @@ extern "C" int shd_eng_boot(shd_eng* e) {
         SHD_HIP(hipMemsetAsync(e->P.bin_bits, 0, 4 * n * kNBW, e->stream));
     }
     const int grid = (e->nloc + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_boot, dim3(grid), dim3(kBlock), 0, e->stream, e->P, e->d_rng0, e->d_bwd, e->d_bwu);
+    hipLaunchKernelGGL(k_boot, dim3(grid), dim3(kBlock), 0, e->stream, dp(e->P), e->d_rng0, e->d_bwd, e->d_bwu);
     SHD_HIP(hipGetLastError());
     if ((rc = read_summary(e))) return rc;
     e->parity = 0;
@@ -2310,7 +2370,7 @@ extern "C" int shd_eng_round_kernel(shd_eng* e, uint64_t ws, uint64_t we, shd_ro
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     e->P.sum = e->d_sum;
     SHD_HIP(hipEventRecord(e->ev0, e->stream));
-    hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, e->P, ws, we, e->parity);
+    hipLaunchKernelGGL(k_round, dim3(grid), dim3(kBlock), 0, e->stream, dp(e->P), ws, we, e->parity);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipEventRecord(e->ev1, e->stream));
     if ((rc = read_summary(e))) return rc;
@@ -2376,7 +2436,7 @@ extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_al
     SHD_HIP(hipMemcpyAsync(e->d_next_rank, &e->next_rank, 4, hipMemcpyHostToDevice, e->stream));
     const uint32_t n = (uint32_t)e->round_pending;
     if (n) {
-        hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, e->P,
+        hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, dp(e->P),
                            (const Pending*)e->P.pend, n, e->parity ^ 1);
         SHD_HIP(hipGetLastError());
     }
@@ -2424,7 +2484,7 @@ static int enqueue_batch(shd_eng* e) {
     constexpr int B = shd_eng::kBatch;
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     for (int i = 0; i < B; i++) {
-        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, (const Params*)(e->d_pr + i + 1),
+        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, (const DParams*)(e->d_pr + i + 1),
                            (const DevSummary*)&e->d_ring[i],
                            &e->d_ring[i + 2], (const DevCtl*)e->d_ctl, i, e->window);
     }
@@ -2586,7 +2646,7 @@ extern "C" int shd_eng_ingest(shd_eng* e, const void* ev, uint64_t n) {
     if (!e || (n && !ev)) return SHD_EINVAL;
     if (!n) return SHD_OK;
     SHD_HIP(hipSetDevice(e->device));
-    hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, e->P,
+    hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, dp(e->P),
                        (const shd_event*)ev, n, e->parity);
     SHD_HIP(hipGetLastError());
     SHD_HIP(hipStreamSynchronize(e->stream));
@@ -2626,7 +2686,7 @@ extern "C" int shd_eng_digest(shd_eng* e, shd_host_digest* out) {
     SHD_HIP(hipSetDevice(e->device));
     shd_host_digest* d = nullptr;
     SHD_HIP(hipMalloc((void**)&d, sizeof(shd_host_digest) * (size_t)e->nloc));
-    hipLaunchKernelGGL(k_digest, dim3((e->nloc + 255) / 256), dim3(256), 0, e->stream, e->P, d);
+    hipLaunchKernelGGL(k_digest, dim3((e->nloc + 255) / 256), dim3(256), 0, e->stream, dp(e->P), d);
     hipError_t err = hipMemcpyAsync(out, d, sizeof(shd_host_digest) * (size_t)e->nloc, hipMemcpyDeviceToHost, e->stream);
     hipError_t err2 = hipStreamSynchronize(e->stream);
     (void)hipFree(d);
@@ -2822,7 +2882,7 @@ static int x_gather_pending(shd_xgroup* g, std::vector<shd_pending>& all) {
 
 static int x_ingest(shd_eng* e, const Params& P, const shd_event* d_ev, uint64_t n, int parity) {
     if (!n) return SHD_OK;
-    hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, P, d_ev, n, parity);
+    hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, dp(P), d_ev, n, parity);
     SHD_HIP(hipGetLastError());
     return SHD_OK;
 }
@@ -3069,7 +3129,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
-            hipLaunchKernelGGL(k_xpack, dim3(1), dim3(64), 0, e->stream, xparams(g, k, e->d_sum), e->d_sum, 1);
+            hipLaunchKernelGGL(k_xpack, dim3(1), dim3(64), 0, e->stream, dp(xparams(g, k, e->d_sum)), e->d_sum, 1);
         }
         if ((rc = x_exchange(g))) return rc;
         g->started = true;
@@ -3102,7 +3162,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
                 shd_eng* e = g->engs[k];
                 const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
                 hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream,
-                                   (const Params*)(g->loc[k].d_xpr + i + 1),
+                                   (const DParams*)(g->loc[k].d_xpr + i + 1),
                                    (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
                                    (const DevCtl*)e->d_ctl, i, g->window);
             }
@@ -3112,7 +3172,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
                 shd_eng* e = g->engs[k];
                 const Params P = xparams(g, k, &e->d_ring[i + 1]);
                 const uint64_t nthr = (uint64_t)g->world * g->xcap;
-                hipLaunchKernelGGL(k_ingest_x, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, P,
+                hipLaunchKernelGGL(k_ingest_x, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, dp(P),
                                    (const shd_event*)g->loc[k].xrecv[wi], (const DevCtl*)e->d_ctl, i);
             }
         }
@@ -3201,7 +3261,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
-            hipLaunchKernelGGL(k_xpack, dim3(1), dim3(64), 0, e->stream, xparams(g, k, &e->d_ring[slot]),
+            hipLaunchKernelGGL(k_xpack, dim3(1), dim3(64), 0, e->stream, dp(xparams(g, k, &e->d_ring[slot])),
                                (const DevSummary*)&e->d_ring[slot], 1);
         }
         if ((rc = x_exchange(g))) break;
