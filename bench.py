@@ -144,26 +144,32 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1 and not use_group:
-        pkt, evs, rounds, kms = st.pkt_events, st.events, st.rounds, st.kernel_ms
+        pkt, evs, rounds, kms, ems = st.pkt_events, st.events, st.rounds, st.kernel_ms, st.kernel_ms
     else:
-        pkt, evs, rounds, kms = st.n_pkt_events, st.n_events, st.n_rounds, st.device_ms_round_kernel
-    tot = torch.tensor([float(pkt), float(evs), float(kms)], dtype=torch.float64, device="cuda")
+        pkt, evs, rounds = st.n_pkt_events, st.n_events, st.n_rounds
+        kms, ems = st.device_ms_round_kernel, st.device_ms_launches
+    tot = torch.tensor([float(pkt), float(evs), float(kms), float(ems)], dtype=torch.float64, device="cuda")
     mx = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tot)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    pkt_all, ev_all, kms_all = tot.tolist()
+    pkt_all, ev_all, kms_all, ems_all = tot.tolist()
     elapsed = mx.item()
     value = pkt_all / elapsed
 
-    # roofline of the round kernel (per launch = per rank-round)
+    # roofline of the round kernel (per launch = per rank-round).  The launch
+    # duration is the HIP-event time of the round launches on the engine's
+    # stream over the timed region (batches of 64 graph-launched rounds; it
+    # includes the gaps between launches); the device-clock time inside the
+    # kernel (first block start to last block end) is reported beside it.
     launches = rounds * max(world, 1)
     alg_bytes = BYTES_PER_EVENT * ev_all + BYTES_PER_PKT_EVENT * pkt_all
-    avg_launch_ms = kms_all / max(launches, 1)
+    avg_launch_ms = (ems_all if ems_all > 0 else kms_all) / max(launches, 1)
     achieved = (alg_bytes / max(launches, 1)) / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
-                "kernel": "k_round", "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(),
+                "kernel": "k_round_dev", "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+                "avg_in_kernel_us": round(kms_all / max(launches, 1) * 1e3, 3),
                 "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1)}
 
     cpu_baseline = None
@@ -207,6 +213,22 @@ def main():
     pc.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic():
+    """HBM bytes per round-kernel launch from the committed rocprofv3 PMC
+    passes (profiles/r01/k_round_pmc_bytes.json: FETCH_SIZE x 2 + WRITE_SIZE,
+    the gfx950 correction), used only when that profile was taken of the
+    kernel source being run; else None."""
+    import hashlib
+    try:
+        prof = json.load(open(os.path.join(REPO, "profiles", "r01", "k_round_pmc_bytes.json")))
+        src = open(os.path.join(REPO, "shadow-1_amd", "csrc", "engine.hip"), "rb").read()
+    except (OSError, ValueError):
+        return None
+    if prof.get("engine_source_sha1") != hashlib.sha1(src).hexdigest():
+        return None
+    return prof.get("hbm_bytes_per_dispatch")
 
 
 def cpu_leg(args, S, W):

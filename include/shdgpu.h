@@ -316,8 +316,11 @@ typedef struct shd_run_stats {
     uint64_t n_pending_resolved;
     uint64_t window_ns;             /* the serial-equivalent window W          */
     uint64_t final_time;
-    double device_ms_round_kernel;  /* HIP-event time inside the round kernel  */
+    double device_ms_round_kernel;  /* round-kernel time, device wall clock (first block start
+                                       to last block end, summed over rounds) */
     double wall_ms;
+    double device_ms_launches;      /* HIP-event time of the round launches on the engine's
+                                       stream (batches; includes the gaps between launches) */
     uint32_t error;
     uint32_t _pad;
 } shd_run_stats;

@@ -2534,11 +2534,17 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         SHD_HIP(hipMemcpyAsync(e->d_ring, e->h_seed, 2 * sizeof(DevSummary), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
+        SHD_HIP(hipEventRecord(e->bev[0], e->stream));
         if ((rc = launch_batch(e))) break;
+        SHD_HIP(hipEventRecord(e->bev[1], e->stream));
         uint32_t halt = 0;
         SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost, e->stream));
         SHD_HIP(hipMemcpyAsync(&halt, e->d_halt, 4, hipMemcpyDeviceToHost, e->stream));
         SHD_HIP(hipStreamSynchronize(e->stream));
+        {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, e->bev[0], e->bev[1]) == hipSuccess) s.device_ms_launches += ms;
+        }
         for (int i = 0; i < B; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
@@ -3156,6 +3162,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         }
+        SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
         for (int i = 0; i < B; i++) {
             const int ri = (int)((g->xseq - 1) & 1);
             for (int k = 0; k < nl; k++) {
@@ -3177,12 +3184,18 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             }
         }
         SHD_HIP(hipGetLastError());
+        SHD_HIP(hipEventRecord(g->engs[0]->bev[1], g->engs[0]->stream));
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
             SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost,
                                    e->stream));
         }
         for (int k = 0; k < nl; k++) SHD_HIP(hipStreamSynchronize(g->engs[k]->stream));
+        {
+            float ms = 0;   // the batch on engine 0's stream: rounds + exchanges
+            if (hipEventElapsedTime(&ms, g->engs[0]->bev[0], g->engs[0]->bev[1]) == hipSuccess)
+                s.device_ms_launches += ms;
+        }
         int halted_at = -1;
         bool done = false;
         for (int i = 0; i < B; i++) {
