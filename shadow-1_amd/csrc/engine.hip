@@ -386,6 +386,40 @@ __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) 
     return a.seq < b.seq;
 }
 
+// An event held as two 16-B vectors.  Choosing between events held as
+// structs lets the compiler select between their addresses, which puts
+// them in scratch; selects between vector values stay in registers.
+// a = {time lo, time hi, seq lo, seq hi}, b = {src, dst, pkt, kind}.
+struct EvV {
+    uint4 a, b;
+};
+static_assert(sizeof(shd_event) == 32, "EvV mirrors shd_event");
+template <class T>
+__device__ __forceinline__ EvV ev_ld(T* p) {
+    const uint4* q = (const uint4*)p;
+    return EvV{q[0], q[1]};
+}
+template <class T>
+__device__ __forceinline__ void ev_st(T* p, const EvV& x) {
+    uint4* q = (uint4*)p;
+    q[0] = x.a;
+    q[1] = x.b;
+}
+__device__ __forceinline__ uint64_t evv_time(const EvV& x) { return ((uint64_t)x.a.y << 32) | x.a.x; }
+__device__ __forceinline__ uint64_t evv_seq(const EvV& x) { return ((uint64_t)x.a.w << 32) | x.a.z; }
+__device__ __forceinline__ bool evv_less(const EvV& x, const EvV& y) {
+    const uint64_t tx = evv_time(x), ty = evv_time(y);
+    if (tx != ty) return tx < ty;
+    if (x.b.x != y.b.x) return x.b.x < y.b.x;
+    return evv_seq(x) < evv_seq(y);
+}
+__device__ __forceinline__ EvV evv_sel(bool c, const EvV& x, const EvV& y) {
+    EvV r;
+    r.a.x = c ? x.a.x : y.a.x; r.a.y = c ? x.a.y : y.a.y; r.a.z = c ? x.a.z : y.a.z; r.a.w = c ? x.a.w : y.a.w;
+    r.b.x = c ? x.b.x : y.b.x; r.b.y = c ? x.b.y : y.b.y; r.b.z = c ? x.b.z : y.b.z; r.b.w = c ? x.b.w : y.b.w;
+    return r;
+}
+
 // 4-ary min-heap; the slab's entry 3 is the root, so the four children of
 // node i (4i+1 .. 4i+4) fill one aligned 128-B line.  The root is cached in
 // LDS (s_top) and its time in a register: peeking never touches HBM.
@@ -417,32 +451,34 @@ __device__ void heap_push(const DParams& P, HostCtx& c, const shd_event& e) {
     hp[i] = e;
 }
 
-// remove the root; the new root is re-cached
+// remove the root; the new root is re-cached.  The four children are read
+// whole (an index past the end rereads the last entry and never wins)
 __device__ void heap_pop(const DParams& P, HostCtx& c) {
     shd_event* hp = heap_base(P, c);
     const uint32_t n = --c.evq_n;
     if (n == 0) return;
-    const shd_event last = hp[n];
+    const EvV last = ev_ld(hp + n);
     uint32_t i = 0;
     for (;;) {
         const uint32_t c1 = 4 * i + 1;
         if (c1 >= n) break;
-        shd_event ch[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (c1 + k < n) ch[k] = hp[c1 + k];
         uint32_t m = c1;
-        shd_event me = ch[0];
+        EvV me = ev_ld(hp + c1);
 #pragma unroll
-        for (int k = 1; k < 4; k++)
-            if (c1 + k < n && ev_less(ch[k], me)) { me = ch[k]; m = c1 + k; }
-        if (!ev_less(me, last)) break;
-        hp[i] = me;
-        if (i == 0) { s_top[threadIdx.x] = me; c.top_time = me.time; }
+        for (int k = 1; k < 4; k++) {
+            const uint32_t ck = c1 + k < n ? c1 + k : n - 1;
+            const EvV x = ev_ld(hp + ck);
+            const bool lt = c1 + k < n && evv_less(x, me);
+            me = evv_sel(lt, x, me);
+            m = lt ? ck : m;
+        }
+        if (!evv_less(me, last)) break;
+        ev_st(hp + i, me);
+        if (i == 0) { ev_st(s_top + threadIdx.x, me); c.top_time = evv_time(me); }
         i = m;
     }
-    hp[i] = last;
-    if (i == 0) { s_top[threadIdx.x] = last; c.top_time = last.time; }
+    ev_st(hp + i, last);
+    if (i == 0) { ev_st(s_top + threadIdx.x, last); c.top_time = evv_time(last); }
 }
 
 __device__ __forceinline__ void trace(const DParams& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
@@ -748,15 +784,21 @@ __device__ __forceinline__ uint32_t guide_index(const DParams& P, double r) {
     int32_t k = (int32_t)(r * (double)P.H) - 1;
     return (uint32_t)(k < 0 ? 0 : (k > P.H - 1 ? P.H - 1 : k));
 }
-__device__ __forceinline__ void guide_pick(const DParams& P, const DestGuide& g, double r, int32_t& dst, int32_t& att) {
-    // static indices only: a dynamically indexed guide would live in scratch
-    const bool f0 = g.cum[0] >= r, f1 = g.cum[1] >= r, f2 = g.cum[2] >= r;
+__device__ __forceinline__ double u2d(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// the guide entry is passed as its three 16-B vectors (a struct chosen from
+// by index would be put in scratch): g0 = {i, att[0..2]}, g1 = {cum[0], cum[1]},
+// g2 = {cum[2], pad}
+__device__ __forceinline__ void guide_pick(const DParams& P, uint4 g0, uint4 g1, uint4 g2, double r, int32_t& dst,
+                                           int32_t& att) {
+    const bool f0 = u2d(g1.x, g1.y) >= r, f1 = u2d(g1.z, g1.w) >= r, f2 = u2d(g2.x, g2.y) >= r;
     if (f0 || f1 || f2) {
-        dst = g.i + (f0 ? 0 : f1 ? 1 : 2);
-        att = f0 ? g.att[0] : f1 ? g.att[1] : g.att[2];
+        dst = (int32_t)g0.x + (f0 ? 0 : f1 ? 1 : 2);
+        att = (int32_t)(f0 ? g0.y : f1 ? g0.z : g0.w);
         return;
     }
-    int32_t lo = g.i + 3, hi = P.H;
+    int32_t lo = (int32_t)g0.x + 3, hi = P.H;
     while (lo < hi) {
         const int32_t mid = lo + ((hi - lo) >> 1);
         if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
@@ -809,9 +851,10 @@ __device__ void flush_wave(const DParams& P, HostCtx& c) {
         const SendRec q = s_send[i * kBlock + hl];
         const int32_t a = s_att[hl];
         const double rr = (double)q.r / kRandMax;
-        const DestGuide g = P.dest_guide[guide_index(P, rr)];
+        const uint4* gq = (const uint4*)(P.dest_guide + guide_index(P, rr));
+        const uint4 g0 = gq[0], g1 = gq[1], g2 = gq[2];
         int32_t dst, b;
-        guide_pick(P, g, rr, dst, b);
+        guide_pick(P, g0, g1, g2, rr, dst, b);
         PathRaw x;
         const int32_t ra = P.complete ? kNoRank : P.rank[a];
         path_load(P, a, b, x);
@@ -1133,10 +1176,12 @@ __device__ bool run_work(const DParams& P, HostCtx& c) {
     return true;
 }
 
-__device__ void load_ctx(const DParams& P, HostCtx& c, int32_t l) {
+// the host's state from its record (loaded by the caller, with the idle
+// test: one memory round trip for both) and the heap root
+__device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l, const HostRec& r, int32_t att,
+                                         int2 st) {
     c.l = l;
     c.h = (uint32_t)(P.h0 + l);
-    const HostRec r = P.hs[l];
     c.rng = r.rng; c.ev_seq = r.ev_seq; c.pkt_seq = r.pkt_seq;
     c.rx_rem = r.rx_rem; c.tx_rem = r.tx_rem; c.rx_refill = r.rx_refill; c.tx_refill = r.tx_refill;
     c.flags = r.flags; c.unread = r.unread;
@@ -1155,12 +1200,11 @@ __device__ void load_ctx(const DParams& P, HostCtx& c, int32_t l) {
     c.ts0 = r.ts[0]; c.ts1 = r.ts[1]; c.ts2 = r.ts[2];
     c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.cq_hv = false; c.tq_hv = false;
-    c.att = P.host_att[c.h];
+    c.att = att;
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
     c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0;
     c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
     c.w_msgs = 0; c.w_fl = 0;
-    const int2 st = P.self_thr[c.h];
     c.self_lo = st.x;
     c.self_hi = st.y;
 }
@@ -1392,7 +1436,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         P.hs[l] = r;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
         HostCtx c;
-        load_ctx(P, c, l);
+        load_ctx(P, c, l, r, P.host_att[h], P.self_thr[h]);
         c.now = 0;
         c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);   // tracker_new, tracker.c:141,607-610
@@ -1407,15 +1451,31 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
 }
 
 // a calendar slot's event, if it is one of the window's: onto the due list
-// (unsorted; sorted once all bins are read), or the heap when the list is full
-__device__ __forceinline__ void due_add(const DParams& P, HostCtx& c, const shd_event& x, uint64_t ws, uint64_t we) {
-    if (x.time < ws || x.time >= we) return;
-    if (c.nd == (uint32_t)kDueCap) {
-        heap_push(P, c, x);
-        return;
+// (unsorted; sorted once all bins are read).  `nw` counts the window's
+// events; those past kDueCap go to the heap afterwards (due_overflow)
+__device__ __forceinline__ void due_add(const EvV& x, uint32_t& nw, uint64_t ws, uint64_t we) {
+    const uint64_t t = evv_time(x);
+    if (t < ws || t >= we) return;
+    if (nw < (uint32_t)kDueCap) ev_st(s_due + nw * kBlock + threadIdx.x, x);
+    nw++;
+}
+
+// rare: more than kDueCap window events.  The bins are read again in the
+// same order (the window's events in them cannot change during the round)
+// and the events past the first kDueCap go to the heap
+__device__ __forceinline__ void due_overflow(const DParams& P, HostCtx& c, uint64_t b0, uint32_t wbits, uint64_t ws,
+                                          uint64_t we) {
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < 3; j++) {
+        if (((wbits >> j) & 1u) == 0) continue;
+        const size_t bi = (size_t)c.l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+        for (uint32_t s = 0; s < kBinCap; s++) {
+            const shd_event& x = P.bins[bi * kBinCap + s];
+            if (x.time < ws || x.time >= we) continue;
+            if (k >= (uint32_t)kDueCap) heap_push(P, c, x);
+            k++;
+        }
     }
-    s_due[c.nd * kBlock + threadIdx.x] = x;
-    c.nd++;
 }
 
 // bit p of a bitmap held in registers (static word indices only)
@@ -1444,9 +1504,17 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
     // hosts with nothing due this round touch 3 words and their bitmap, not their whole state
     bool idle = false;
     uint32_t wbits = 0;   // bit j: window bin j is non-empty
+    // the host record is loaded with the idle test (one round trip for both)
+    HostRec rec;
+    int32_t rec_att = 0;
+    int2 rec_st = make_int2(0, 0);
+    uint32_t nin0 = 0;
     if (l < P.nloc) {
-        const uint32_t nin0 = P.inbox_n[parity][l];
+        nin0 = P.inbox_n[parity][l];
         const uint64_t t0 = P.hnext[l];
+        rec = P.hs[l];
+        rec_att = P.host_att[P.h0 + l];
+        rec_st = P.self_thr[P.h0 + l];
         if (P.bins) {
             const uint4* bp = (const uint4*)(P.bin_bits + (size_t)l * kNBW);
             const uint4 x = bp[0], y = bp[1];
@@ -1493,7 +1561,7 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
     if (active) {
         PROF_T0(t_all)
-        load_ctx(P, c, l);
+        load_ctx(P, c, l, rec, rec_att, rec_st);
         TIMA(7);
         c.ws = ws;
         c.ws_mod = (uint32_t)(ws % SHD_MS);
@@ -1504,7 +1572,7 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
         PROF_ADD(c, PR_LOAD, t_all)
         // merge inbound events of the previous round
         PROF_T0(t_m)
-        const uint32_t nin = P.inbox_n[parity][l];
+        const uint32_t nin = nin0;
         if (nin) {
             const shd_event* in = P.inbox[parity] + (size_t)l * P.inbox_cap;
             const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
@@ -1517,27 +1585,31 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
         // ws), a slot being written by this round's appends holds a time >= we
         // (or still the old one), so the bin's count is not needed here
         if (P.bins) {
+            uint32_t nw = 0;
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++) {
                 if (((wbits >> j) & 1u) == 0) continue;
                 const size_t bi = (size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
                 static_assert(kBinCap == 4, "the slots are read as four named events");
-                const shd_event* bp = P.bins + bi * kBinCap;
-                const shd_event x0 = bp[0], x1 = bp[1], x2 = bp[2], x3 = bp[3];
-                due_add(P, c, x0, ws, we);
-                due_add(P, c, x1, ws, we);
-                due_add(P, c, x2, ws, we);
-                due_add(P, c, x3, ws, we);
+                const auto bp = P.bins + bi * kBinCap;
+                const EvV x0 = ev_ld(bp), x1 = ev_ld(bp + 1), x2 = ev_ld(bp + 2), x3 = ev_ld(bp + 3);
+                due_add(x0, nw, ws, we);
+                due_add(x1, nw, ws, we);
+                due_add(x2, nw, ws, we);
+                due_add(x3, nw, ws, we);
             }
+            c.nd = nw < (uint32_t)kDueCap ? nw : (uint32_t)kDueCap;
+            if (nw > (uint32_t)kDueCap) due_overflow(P, c, b0, wbits, ws, we);
             // insertion sort of the due list (LDS only)
             for (uint32_t i = 1; i < c.nd; i++) {
-                const shd_event x = s_due[i * kBlock + threadIdx.x];
+                const EvV x = ev_ld(s_due + i * kBlock + threadIdx.x);
                 uint32_t k = i;
-                while (k > 0 && ev_less(x, s_due[(k - 1) * kBlock + threadIdx.x])) {
-                    s_due[k * kBlock + threadIdx.x] = s_due[(k - 1) * kBlock + threadIdx.x];
-                    k--;
+                for (; k > 0; k--) {
+                    const EvV y = ev_ld(s_due + (k - 1) * kBlock + threadIdx.x);
+                    if (!evv_less(x, y)) break;
+                    ev_st(s_due + k * kBlock + threadIdx.x, y);
                 }
-                s_due[k * kBlock + threadIdx.x] = x;
+                ev_st(s_due + k * kBlock + threadIdx.x, x);
             }
         }
         PROF_ADD(c, PR_MERGE, t_m)
