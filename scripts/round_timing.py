@@ -43,11 +43,18 @@ def main():
     eng = Engine(m, pc, 0, a.hosts, device=0)
     eng.boot()
     eng.run_until(2 * S.SHD_SEC)
+    kc = np.zeros(40, dtype=np.uint64)
+    fk = lib.shd_debug_kind_costs
+    fk.restype = C.c_int
+    fk.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    fk(kc.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
     st = eng.run_until(int(2.5 * S.SHD_SEC))
+    fk(kc.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
     buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
     f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
     t = buf.reshape(64, 2048, 20).astype(np.int64)
-    grid = (a.hosts + 63) // 64
+    hpw = int(os.environ.get("SHD_HPW", "64"))
+    grid = (a.hosts + hpw - 1) // hpw
     t = t[:, :grid, :]
     print(f"kernel {st.device_ms_round_kernel / max(st.n_rounds, 1) * 1e3:.1f} us/round (in-kernel stamps), "
           f"wall {st.wall_ms / max(st.n_rounds, 1) * 1e3:.1f} us/round, grid {grid}")
@@ -87,6 +94,19 @@ def main():
     for j, nm in ((1, "take_next"), (2, "begin_event"), (3, "run_work"), (5, "flush_wave"), (6, "inner loops")):
         print(f"    {nm:12s} {raw[:, :, j][ok].mean():9.0f} cyc/wave ({100 * raw[:, :, j][ok].mean() / tot:4.1f}% of loop "
               f"{tot:.0f}); per iteration {raw[:, :, j][ok].sum() / raw[:, :, 0][ok].sum():7.0f}")
+    kd = t[keep][:, :, 18:20].astype(np.float64)
+    it = raw[:, :, 0][ok].sum()
+    print(f"  divergence: {kd[:, :, 0][ok].sum() / it:.2f} distinct event kinds and "
+          f"{kd[:, :, 1][ok].sum() / it:.1f} lanes starting an event per iteration")
+    kc = kc.reshape(10, 4).astype(np.float64)
+    kn = {1: "HEARTBEAT", 2: "REFILL", 3: "REFILL_LO", 4: "APP_START", 5: "PACKET fast", 6: "LOCAL", 7: "NOTIFY",
+          8: "PACKET general"}
+    print("  single-class iterations: class, iterations, cycles per iteration (take_next / begin_event / rest)")
+    for k in range(1, 9):
+        if kc[k, 0]:
+            n = kc[k, 0]
+            print(f"    {kn[k]:15s} {n:10.0f} {kc[k, 1] / n:7.0f} ({kc[k, 2] / n:5.0f} / {kc[k, 3] / n:5.0f} / "
+                  f"{(kc[k, 1] - kc[k, 2] - kc[k, 3]) / n:5.0f})")
     d = rows[:, :, 3] - rows[:, :, 2]
     print(f"  active-phase duration per block: mean {d.mean():.2f} max {d.max(axis=1).mean():.2f} us")
     d = rows[:, :, 5] - rows[:, :, 3]

@@ -278,6 +278,11 @@ enum {
 // wall-clock stamps per block at the round's phase boundaries, 64 round slots
 // keyed by the summary address x 2048 blocks x 8 stamps
 __device__ unsigned long long g_tim[64][2048][20];
+// per event class, over iterations in which every lane that starts an event
+// starts one of that class: {iterations, cycles, of which take_next, of which
+// begin_event}.  Class = kind (1..7), 8 = a packet on the general path
+__device__ unsigned long long g_kc[10][4];
+__shared__ unsigned long long s_kc[10][4];
 #define TIM(k)                                                                                         \
     do {                                                                                               \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
@@ -1486,15 +1491,59 @@ __device__ __forceinline__ uint32_t bit_at(const uint32_t (&w)[kNBW], uint32_t p
     return (v >> (p & 31)) & 1u;
 }
 
+// the lane's host (P.nloc: none)
+__device__ __forceinline__ int32_t lane_host(const DParams& P) {
+    return (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
+}
+
+// what a round reads of a host before it knows the window: both inbox
+// counts, the earliest timer/heap time, the calendar bitmap, the host record,
+// its attached vertex and loopback thresholds.  None of it depends on the
+// window start, so the round kernels issue these loads together with the
+// loads of the window start and control words (one memory round trip).
+struct HostIn {
+    uint32_t nin[2];
+    uint64_t t0;
+    uint32_t w[kNBW];
+    HostRec rec;
+    int32_t att;
+    int2 st;
+};
+__device__ __forceinline__ void host_in_load(const DParams& P, int32_t l, HostIn& in) {
+    if (l < P.nloc) {
+        in.nin[0] = P.inbox_n[0][l];
+        in.nin[1] = P.inbox_n[1][l];
+        in.t0 = P.hnext[l];
+        in.rec = P.hs[l];
+        in.att = P.host_att[P.h0 + l];
+        in.st = P.self_thr[P.h0 + l];
+        if (P.bins) {
+            const uint4* bp = (const uint4*)(P.bin_bits + (size_t)l * kNBW);
+            const uint4 x = bp[0], y = bp[1];
+            in.w[0] = x.x; in.w[1] = x.y; in.w[2] = x.z; in.w[3] = x.w;
+            in.w[4] = y.x; in.w[5] = y.y; in.w[6] = y.z; in.w[7] = y.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < (int)kNBW; j++) in.w[j] = 0;
+        }
+    }
+}
+
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
 // window, run events < we
-__device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64_t we, int parity, uint64_t& next_out,
-                                           uint64_t& nev_out, uint64_t& npkt_out, uint32_t& err_out) {
-    const int32_t l = (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
+__device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, uint64_t ws, uint64_t we, int parity,
+                                           uint64_t& next_out, uint64_t& nev_out, uint64_t& npkt_out,
+                                           uint32_t& err_out) {
+    const int32_t l = lane_host(P);
 #ifdef SHD_PROF
     const unsigned long long w0 = wall_clock64();
 #endif
     TIM(1);
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 10; i++)
+            for (int j = 0; j < 4; j++) s_kc[i][j] = 0;
+#endif
     uint64_t next = kInf, nev = 0, npkt = 0;
     uint32_t err = 0;
     // the window's calendar bins: b0 .. b0 + nbin - 1 (nbin <= 3: bin width <= W)
@@ -1504,21 +1553,16 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
     // hosts with nothing due this round touch 3 words and their bitmap, not their whole state
     bool idle = false;
     uint32_t wbits = 0;   // bit j: window bin j is non-empty
-    // the host record is loaded with the idle test (one round trip for both)
-    HostRec rec;
-    int32_t rec_att = 0;
-    int2 rec_st = make_int2(0, 0);
+    const HostRec& rec = in.rec;
+    const int32_t rec_att = in.att;
+    const int2 rec_st = in.st;
     uint32_t nin0 = 0;
     if (l < P.nloc) {
-        nin0 = P.inbox_n[parity][l];
-        const uint64_t t0 = P.hnext[l];
-        rec = P.hs[l];
-        rec_att = P.host_att[P.h0 + l];
-        rec_st = P.self_thr[P.h0 + l];
+        nin0 = parity ? in.nin[1] : in.nin[0];
+        const uint64_t t0 = in.t0;
+#pragma unroll
+        for (int j = 0; j < (int)kNBW; j++) w[j] = in.w[j];
         if (P.bins) {
-            const uint4* bp = (const uint4*)(P.bin_bits + (size_t)l * kNBW);
-            const uint4 x = bp[0], y = bp[1];
-            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++)
                 if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
@@ -1546,7 +1590,7 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
     const bool active = l < P.nloc && !idle;
 #ifdef SHD_TIMING
     uint64_t n_it = 0, k_tk = 0, k_be = 0, k_rw = 0, k_fl = 0, k_in = 0;
-    uint64_t k_l0 = 0;
+    uint64_t k_l0 = 0, n_kinds = 0, n_lanes = 0;
 #define KT0(v) const uint64_t v = clock64();
 #define KTA(acc, v) acc += clock64() - v;
 #elif defined(SHD_MARK)   // asm listing markers (static code-size census)
@@ -1574,9 +1618,9 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
         PROF_T0(t_m)
         const uint32_t nin = nin0;
         if (nin) {
-            const shd_event* in = P.inbox[parity] + (size_t)l * P.inbox_cap;
+            const shd_event* ib = P.inbox[parity] + (size_t)l * P.inbox_cap;
             const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
-            for (uint32_t i = 0; i < n; i++) heap_push(P, c, in[i]);
+            for (uint32_t i = 0; i < n; i++) heap_push(P, c, ib[i]);
             P.inbox_n[parity][l] = 0;
         }
         // the window's calendar events, sorted into the due list.  The slots
@@ -1634,6 +1678,9 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
             for (;;) {
 #ifdef SHD_TIMING
                 n_it++;
+                const uint64_t i_t0 = clock64();
+                uint64_t i_tk = 0, i_be = 0;
+                uint32_t i_cls = 0;
 #endif
                 if (st == 0u) {
                     PROF_T0(t_p)
@@ -1641,12 +1688,30 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
                     KT0(q0)
                     const bool more = take_next(P, c, we, e);
                     KTA(k_tk, q0)
+#ifdef SHD_TIMING
+                    i_tk = clock64();
+                    if (more) {
+                        i_cls = e.kind & 7;
+                        if (e.kind == SHD_EV_PACKET && !(c.cq_count == 0 && c.rx_rem >= SHD_MTU && !bootstrapping(P, c)))
+                            i_cls = 8;
+                    }
+#endif
                     PROF_ADD(c, PR_POP, t_p)
+#ifdef SHD_TIMING
+                    {   // divergence census: distinct event kinds started in this iteration
+                        const uint32_t ks = more ? 1u << (e.kind & 31) : 0u;
+                        for (uint32_t b = 1; b < 8; b++) n_kinds += __ballot((ks >> b) & 1u) != 0;
+                        n_lanes += __popcll(__ballot(ks != 0));
+                    }
+#endif
                     if (more) {
                         c.now = e.time;
                         KT0(q1)
                         begin_event(P, c, e);
                         KTA(k_be, q1)
+#ifdef SHD_TIMING
+                        i_be = clock64();
+#endif
                         st = 1u;
                     } else {
                         st = 3u;
@@ -1657,6 +1722,23 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
                     st = run_work(P, c) ? 0u : 2u;
                     KTA(k_rw, q2)
                 }
+#ifdef SHD_TIMING
+                {
+                    const uint64_t i_t1 = clock64();
+                    const uint64_t m = __ballot(i_cls != 0);
+                    if (m) {
+                        const int f = __ffsll((unsigned long long)m) - 1;
+                        const uint32_t u = __shfl(i_cls, f, 64);
+                        const uint64_t tk = __shfl(i_tk, f, 64), be = __shfl(i_be, f, 64);
+                        if (__ballot(i_cls != 0 && i_cls != u) == 0 && threadIdx.x == 0) {
+                            s_kc[u][0] += 1;
+                            s_kc[u][1] += i_t1 - i_t0;
+                            s_kc[u][2] += tk - i_t0;
+                            s_kc[u][3] += be - tk;
+                        }
+                    }
+                }
+#endif
                 if (__ballot(st <= 1u) == 0) break;
             }
             KTA(k_in, q4)
@@ -1685,6 +1767,8 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
             TIMV(15, v[4]);
             TIMV(16, v[5]);
             TIMV(17, v[6]);
+            TIMV(18, n_kinds);
+            TIMV(19, n_lanes);
         }
 #endif
         next = host_next(c);
@@ -1748,6 +1832,12 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
         }
     }
 #endif
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 10; i++)
+            if (s_kc[i][0])
+                for (int j = 0; j < 4; j++) atomicAdd(&g_kc[i][j], s_kc[i][j]);
+#endif
     TIM(3);
     next_out = next; nev_out = nev; npkt_out = npkt; err_out = err;
 }
@@ -1755,7 +1845,9 @@ __device__ __forceinline__ void round_body(const DParams& P, uint64_t ws, uint64
 __global__ __launch_bounds__(kBlock) void k_round(DParams P, uint64_t ws, uint64_t we, int parity) {
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body(P, ws, we, parity, next, nev, npkt, err);
+    HostIn in;
+    host_in_load(P, lane_host(P), in);
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
     (void)round_complete(P, next, nev, npkt, err);
 }
 
@@ -1871,7 +1963,9 @@ __global__ __launch_bounds__(kBlock) void k_round_dev(const DParams* __restrict_
 #ifdef SHD_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
-    // the round's inputs, loaded together (one round trip)
+    // the round's inputs and the hosts' state, loaded together (one round trip)
+    HostIn in;
+    host_in_load(P, lane_host(P), in);
     const uint32_t halt = *P.halt;
     const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws = prev->next_time;
     if (halt) return;
@@ -1889,7 +1983,7 @@ __global__ __launch_bounds__(kBlock) void k_round_dev(const DParams* __restrict_
     if (we > stop || we < ws) we = stop;
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body(P, ws, we, parity, next, nev, npkt, err);
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
     TIM(4);
     if (!round_complete(P, next, nev, npkt, err)) {
         TIM(5);
@@ -1968,6 +2062,8 @@ __global__ __launch_bounds__(kBlock) void k_round_x(const DParams* __restrict__ 
                                                     const DevCtl* __restrict__ ctl, int i, uint64_t window) {
     const DParams& P = *Pp;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    HostIn in;
+    host_in_load(P, lane_host(P), in);
     if (*P.halt) {
         if (lead) P.sum->flags = 2u;
         return;
@@ -2010,7 +2106,7 @@ __global__ __launch_bounds__(kBlock) void k_round_x(const DParams* __restrict__ 
     if (we > stop || we < ws) we = stop;
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body(P, ws, we, parity, next, nev, npkt, err);
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
     if (!round_complete(P, next, nev, npkt, err)) return;
     if (threadIdx.x == 0) P.sum->ws = ws;
     xpack_block(P, P.sum, 0, P.sum->next_time);
@@ -2674,6 +2770,15 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
 extern "C" int shd_debug_timing(uint64_t* out) {   // 64 x 2048 x 20
     SHD_HIP(hipDeviceSynchronize());
     SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tim), sizeof(g_tim)));
+    return SHD_OK;
+}
+extern "C" int shd_debug_kind_costs(uint64_t* out, int reset) {   // 10 x 4
+    SHD_HIP(hipDeviceSynchronize());
+    SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kc), sizeof(g_kc)));
+    if (reset) {
+        static const unsigned long long z[10][4] = {};
+        SHD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_kc), z, sizeof(g_kc)));
+    }
     return SHD_OK;
 }
 #endif
