@@ -335,7 +335,23 @@ __device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
 }
 
 // --------------------------------------------------------------- per-host context
+// Params fields the event code reads on every event, held in registers.
+// Read through the Params pointer, they are invariant loads, which the
+// compiler re-issues (a scalar load and its wait) at each use rather than
+// keep; launder() makes each a VGPR value it must keep.
+struct HotK {
+    uint64_t end_time, boot_end;
+    uint32_t pkt_len, cq_cap, tq_cap, evq_cap, trace;
+    int32_t dst_thr;
+};
+template <class T>
+__device__ __forceinline__ T launder(T x) {
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 struct HostCtx {
+    HotK k;
     int32_t l;       // local index
     uint32_t h;      // global host id
     uint64_t now;
@@ -434,7 +450,7 @@ __device__ __forceinline__ shd_event* heap_base(const DParams& P, const HostCtx&
 
 __device__ void heap_push(const DParams& P, HostCtx& c, const shd_event& e) {
     shd_event* hp = heap_base(P, c);
-    if (c.evq_n >= P.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
+    if (c.evq_n >= c.k.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
     uint32_t i = c.evq_n++;
     if (i == 0) {
         hp[0] = e;
@@ -488,7 +504,7 @@ __device__ void heap_pop(const DParams& P, HostCtx& c) {
 
 __device__ __forceinline__ void trace(const DParams& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
                                       uint32_t peer, uint32_t pkt, uint32_t kind) {
-    if (!P.trace) return;
+    if (!c.k.trace) return;
     unsigned long long i = atomicAdd(P.trace_n, 1ull);
     if (i >= P.trace_cap) { c.err |= SHD_ERR_TRACE_OVERFLOW; return; }
     shd_trace_rec r;
@@ -496,7 +512,18 @@ __device__ __forceinline__ void trace(const DParams& P, HostCtx& c, uint64_t t, 
     P.trace_buf[i] = r;
 }
 
-__device__ __forceinline__ bool bootstrapping(const DParams& P, const HostCtx& c) { return c.now < P.bootstrap_end; }
+__device__ __forceinline__ bool bootstrapping(const DParams& P, const HostCtx& c) { return c.now < c.k.boot_end; }
+
+__device__ __forceinline__ void hot_load(const DParams& P, HostCtx& c) {
+    c.k.end_time = launder(P.end_time);
+    c.k.boot_end = launder(P.bootstrap_end);
+    c.k.pkt_len = launder(P.pkt_len);
+    c.k.cq_cap = launder(P.cq_cap);
+    c.k.tq_cap = launder(P.tq_cap);
+    c.k.evq_cap = launder(P.evq_cap);
+    c.k.trace = launder(P.trace);
+    c.k.dst_thr = launder(P.dst_thr);
+}
 
 // event_new_ (consumes the source's event ID, event.c:38) + scheduler_push
 // (discards time >= end, scheduler.c:346-349) for a self event
@@ -512,7 +539,7 @@ __device__ void schedule_self(const DParams& P, HostCtx& c, uint32_t kind, uint6
     e.dst = c.h;
     e.pkt = pkt;
     e.kind = kind;
-    if (e.time >= P.end_time) return;
+    if (e.time >= c.k.end_time) return;
     switch (kind) {   // at most one pending instance each (flags / self-rescheduling)
     case SHD_EV_HEARTBEAT:
         if (c.tt0 != kInf) c.err |= SHD_ERR_INTERNAL;
@@ -620,11 +647,11 @@ __device__ bool codel_helper(const DParams& P, HostCtx& c, bool& okToDrop, Codel
         out = s_cqh[threadIdx.x];
         c.cq_hv = false;
     } else {
-        out = P.cq[(size_t)c.l * P.cq_cap + c.cq_head];
+        out = P.cq[(size_t)c.l * c.k.cq_cap + c.cq_head];
     }
-    c.cq_head = (c.cq_head + 1 == P.cq_cap) ? 0 : c.cq_head + 1;
+    c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
     c.cq_count--;
-    c.cq_total -= P.pkt_len;
+    c.cq_total -= c.k.pkt_len;
     const uint64_t sojourn = c.now - out.ts;
     if (sojourn < kCodelTarget || c.cq_total < SHD_MTU) {
         c.cq_iexp = 0;
@@ -678,7 +705,7 @@ __device__ void if_receive_packets(const DParams& P, HostCtx& c) {
         if (!codel_dequeue(P, c, p)) break;
         if_receive_packet(P, c, p.src, p.pkt);
         if (!boot) {
-            consume(c.rx_rem, P.pkt_len);
+            consume(c.rx_rem, c.k.pkt_len);
             refill_if_needed(P, c);
         }
     }
@@ -895,7 +922,7 @@ __device__ void flush_wave(const DParams& P, HostCtx& c) {
             c.c_sent++;
             // 1 = delivery waits for the resolution, 2 = already delivered
             if (log) log_pending(P, c, q, c.att, b, resolved ? 2u : 1u, e.dst, seq);
-            if (resolved && e.time < P.end_time) {   // scheduler_push drops time >= end
+            if (resolved && e.time < c.k.end_time) {   // scheduler_push drops time >= end
                 emit = SHD_EV_PACKET;
                 if (e.time < c.min_emit) c.min_emit = e.time;
             }
@@ -969,14 +996,14 @@ __device__ bool if_send_step(const DParams& P, HostCtx& c) {
         if (c.tq_hv) {
             p = s_tqh[threadIdx.x];
         } else {
-            p = P.tq[(size_t)c.l * P.tq_cap + c.tq_head];
+            p = P.tq[(size_t)c.l * c.k.tq_cap + c.tq_head];
             s_tqh[threadIdx.x] = p;   // keep the peeked head: a flush may come first
             c.tq_hv = true;
         }
         const bool self = is_self_draw(c, p.r);
         if (c.ns && (self || c.ns == (uint32_t)kSendCap)) return true;
         c.tq_hv = false;
-        c.tq_head = (c.tq_head + 1 == P.tq_cap) ? 0 : c.tq_head + 1;
+        c.tq_head = (c.tq_head + 1 == c.k.tq_cap) ? 0 : c.tq_head + 1;
         c.tq_count--;
         if (self) {
             trace(P, c, c.now, c.ev_seq, c.h, c.h, p.pkt, SHD_TR_LOCAL);
@@ -987,7 +1014,7 @@ __device__ bool if_send_step(const DParams& P, HostCtx& c) {
             PROF_ADD(c, PR_SEND, ts)
         }
         if (!boot) {
-            consume(c.tx_rem, P.pkt_len);
+            consume(c.tx_rem, c.k.pkt_len);
             refill_if_needed(P, c);
         }
     }
@@ -1007,17 +1034,17 @@ __device__ bool enqueue_new_message(const DParams& P, HostCtx& c) {
     PROF_T0(tp)
     const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
     PROF_ADD(c, PR_PICK, tp)
-    if ((int32_t)rv > P.dst_thr) return false;   // no i with dest_cum[i] >= r
+    if ((int32_t)rv > c.k.dst_thr) return false;   // no i with dest_cum[i] >= r
     random_free_port(c);
     const uint32_t pkt = c.pkt_seq++;
-    if (c.tq_count >= P.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
+    if (c.tq_count >= c.k.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
     if (c.tq_count == 0) {
         s_tqh[threadIdx.x] = TxEnt{rv, pkt};
         c.tq_hv = true;
     } else {
         uint32_t tail = c.tq_head + c.tq_count;
-        if (tail >= P.tq_cap) tail -= P.tq_cap;
-        P.tq[(size_t)c.l * P.tq_cap + tail] = TxEnt{rv, pkt};
+        if (tail >= c.k.tq_cap) tail -= c.k.tq_cap;
+        P.tq[(size_t)c.l * c.k.tq_cap + tail] = TxEnt{rv, pkt};
     }
     c.tq_count++;
     return true;
@@ -1090,27 +1117,27 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
             // an empty router queue and room in the receive bucket: the packet
             // is enqueued and dequeued at once (sojourn 0: CoDel's interval
             // and drop mode reset; the second dequeue attempt finds nothing)
-            c.cq_head = (c.cq_head + 1 == P.cq_cap) ? 0 : c.cq_head + 1;
+            c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
             c.cq_iexp = 0;
             c.flags &= ~F_CODEL_DROP_MODE;
             if_receive_packet(P, c, e.src, e.pkt);
-            consume(c.rx_rem, P.pkt_len);
+            consume(c.rx_rem, c.k.pkt_len);
             refill_if_needed(P, c);
             break;
         }
         const bool was_empty = c.cq_count == 0;
-        if (c.cq_count >= P.cq_cap) { c.err |= SHD_ERR_CODELQ_OVERFLOW; break; }
+        if (c.cq_count >= c.k.cq_cap) { c.err |= SHD_ERR_CODELQ_OVERFLOW; break; }
         const CodelEnt ent{c.now, e.src, e.pkt};
         if (was_empty) {   // the head stays in LDS; stored only if still queued at round end
             s_cqh[threadIdx.x] = ent;
             c.cq_hv = true;
         } else {
             uint32_t tail = c.cq_head + c.cq_count;
-            if (tail >= P.cq_cap) tail -= P.cq_cap;
-            P.cq[(size_t)c.l * P.cq_cap + tail] = ent;
+            if (tail >= c.k.cq_cap) tail -= c.k.cq_cap;
+            P.cq[(size_t)c.l * c.k.cq_cap + tail] = ent;
         }
         c.cq_count++;
-        c.cq_total += P.pkt_len;
+        c.cq_total += c.k.pkt_len;
         c.w_fl = was_empty ? W_RX : 0u;
         break;
     }
@@ -1138,7 +1165,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap && !boot) {
         const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
         c.w_msgs--;
-        if ((int32_t)rv > P.dst_thr) continue;   // no destination: nothing queued
+        if ((int32_t)rv > c.k.dst_thr) continue;   // no destination: nothing queued
         random_free_port(c);
         const uint32_t pkt = c.pkt_seq++;
         if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
@@ -1149,7 +1176,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
             break;
         }
         worker_send_deferred(P, c, rv, pkt);
-        consume(c.tx_rem, P.pkt_len);
+        consume(c.tx_rem, c.k.pkt_len);
         refill_if_needed(P, c);
     }
 }
@@ -1310,8 +1337,8 @@ __device__ void store_ctx(const DParams& P, const HostCtx& c) {
     r.tq_head = c.tq_head; r.tq_count = c.tq_count; r.evq_n = c.evq_n;
     r.pad[0] = r.pad[1] = r.pad[2] = 0;
     P.hs[l] = r;
-    if (c.cq_hv) P.cq[(size_t)l * P.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
-    if (c.tq_hv) P.tq[(size_t)l * P.tq_cap + c.tq_head] = s_tqh[threadIdx.x];
+    if (c.cq_hv) P.cq[(size_t)l * c.k.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
+    if (c.tq_hv) P.tq[(size_t)l * c.k.tq_cap + c.tq_head] = s_tqh[threadIdx.x];
     HostCnt* hc = P.hc + l;   // counter deltas: fire-and-forget atomics
     if (c.c_events) atomicAdd(&hc->events, (unsigned long long)c.c_events);
     if (c.c_pkt) atomicAdd(&hc->pkt, (unsigned long long)c.c_pkt);
@@ -1441,6 +1468,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         P.hs[l] = r;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
         HostCtx c;
+        hot_load(P, c);
         load_ctx(P, c, l, r, P.host_att[h], P.self_thr[h]);
         c.now = 0;
         c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
@@ -1500,7 +1528,39 @@ __device__ __forceinline__ int32_t lane_host(const DParams& P) {
 // counts, the earliest timer/heap time, the calendar bitmap, the host record,
 // its attached vertex and loopback thresholds.  None of it depends on the
 // window start, so the round kernels issue these loads together with the
-// loads of the window start and control words (one memory round trip).
+// loads of the window start and control words (one memory round trip).  The
+// pointers come by value in the kernel arguments (RoundArgs), not through the
+// Params pointer: one scalar load level instead of two before the first
+// vector load.
+template <template <class> class Ptr>
+struct RoundArgsT {
+    Ptr<const HostRec> hs;
+    Ptr<const uint64_t> hnext;
+    Ptr<const uint32_t> nin0, nin1;
+    Ptr<const uint32_t> bits;   // null: no calendar
+    Ptr<const int32_t> att;     // host_att + h0
+    Ptr<const int2> st;         // self_thr + h0
+    Ptr<const uint32_t> halt;
+    int32_t nloc, hpw;
+};
+using DRoundArgs = RoundArgsT<GlobalPtr>;
+static DRoundArgs round_args(const Params& P) {
+    const DParams& d = dp(P);
+    DRoundArgs a;
+    a.hs = d.hs; a.hnext = d.hnext; a.nin0 = d.inbox_n[0]; a.nin1 = d.inbox_n[1];
+    a.bits = d.bins ? d.bin_bits : nullptr;
+    a.att = d.host_att + P.h0; a.st = d.self_thr + P.h0;
+    a.halt = d.halt; a.nloc = P.nloc; a.hpw = P.hpw;
+    return a;
+}
+__device__ __forceinline__ DRoundArgs round_args_dev(const DParams& P) {
+    DRoundArgs a;
+    a.hs = P.hs; a.hnext = P.hnext; a.nin0 = P.inbox_n[0]; a.nin1 = P.inbox_n[1];
+    a.bits = P.bins ? P.bin_bits : nullptr;
+    a.att = P.host_att + P.h0; a.st = P.self_thr + P.h0;
+    a.halt = P.halt; a.nloc = P.nloc; a.hpw = P.hpw;
+    return a;
+}
 struct HostIn {
     uint32_t nin[2];
     uint64_t t0;
@@ -1509,23 +1569,25 @@ struct HostIn {
     int32_t att;
     int2 st;
 };
-__device__ __forceinline__ void host_in_load(const DParams& P, int32_t l, HostIn& in) {
-    if (l < P.nloc) {
-        in.nin[0] = P.inbox_n[0][l];
-        in.nin[1] = P.inbox_n[1][l];
-        in.t0 = P.hnext[l];
-        in.rec = P.hs[l];
-        in.att = P.host_att[P.h0 + l];
-        in.st = P.self_thr[P.h0 + l];
-        if (P.bins) {
-            const uint4* bp = (const uint4*)(P.bin_bits + (size_t)l * kNBW);
-            const uint4 x = bp[0], y = bp[1];
-            in.w[0] = x.x; in.w[1] = x.y; in.w[2] = x.z; in.w[3] = x.w;
-            in.w[4] = y.x; in.w[5] = y.y; in.w[6] = y.z; in.w[7] = y.w;
-        } else {
+// every lane loads (lanes past the last host read the last host's entries
+// and ignore them): no branch, so no wait at a join before other loads issue
+__device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
+    const int32_t l0 = (int32_t)threadIdx.x < a.hpw ? (int32_t)blockIdx.x * a.hpw + (int32_t)threadIdx.x : a.nloc;
+    const int32_t l = l0 < a.nloc ? l0 : a.nloc - 1;
+    in.nin[0] = a.nin0[l];
+    in.nin[1] = a.nin1[l];
+    in.t0 = a.hnext[l];
+    in.rec = a.hs[l];
+    in.att = a.att[l];
+    in.st = a.st[l];
+    if (a.bits) {
+        const uint4* bp = (const uint4*)(a.bits + (size_t)l * kNBW);
+        const uint4 x = bp[0], y = bp[1];
+        in.w[0] = x.x; in.w[1] = x.y; in.w[2] = x.z; in.w[3] = x.w;
+        in.w[4] = y.x; in.w[5] = y.y; in.w[6] = y.z; in.w[7] = y.w;
+    } else {
 #pragma unroll
-            for (int j = 0; j < (int)kNBW; j++) in.w[j] = 0;
-        }
+        for (int j = 0; j < (int)kNBW; j++) in.w[j] = 0;
     }
 }
 
@@ -1601,6 +1663,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #define KTA(acc, v)
 #endif
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
+    hot_load(P, c);
     c.ns = 0; c.att = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
     if (active) {
@@ -1846,7 +1909,7 @@ __global__ __launch_bounds__(kBlock) void k_round(DParams P, uint64_t ws, uint64
     uint64_t next, nev, npkt;
     uint32_t err;
     HostIn in;
-    host_in_load(P, lane_host(P), in);
+    host_in_load(round_args_dev(P), in);
     round_body(P, in, ws, we, parity, next, nev, npkt, err);
     (void)round_complete(P, next, nev, npkt, err);
 }
@@ -1956,29 +2019,34 @@ __device__ void resolve_block(const DParams& P, int next_parity) {
 // The hot kernels take Params through a pointer to a device copy (one per
 // summary-ring slot): fields are scalar-loaded where used instead of all held
 // in SGPRs, which otherwise spill to VGPR lanes around every branch.
-__global__ __launch_bounds__(kBlock) void k_round_dev(const DParams* __restrict__ Pp, const DevSummary* __restrict__ prev,
-                                                       DevSummary* __restrict__ init,
-                                                       const DevCtl* __restrict__ ctl, int i, uint64_t window) {
+__global__ __launch_bounds__(kBlock) void k_round_dev(DRoundArgs a, const DevSummary* __restrict__ prev,
+                                                       const DevCtl* __restrict__ ctl, const DParams* __restrict__ Pp,
+                                                       DevSummary* __restrict__ init, int i, uint64_t window) {
     const DParams& P = *Pp;
 #ifdef SHD_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
     // the round's inputs and the hosts' state, loaded together (one round trip)
     HostIn in;
-    host_in_load(P, lane_host(P), in);
-    const uint32_t halt = *P.halt;
+    host_in_load(a, in);
+    const uint32_t halt = *a.halt;
     const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws = prev->next_time;
-    if (halt) return;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    // one test of all three loads, so that they issue together (no wait
+    // between the halt flag and the window start)
+    if ((halt != 0) | (ws >= stop)) {
+        if (halt == 0 && lead) {   // only forwards the time
+            atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+            *init = fresh_summary();
+            atomicMin(&P.sum->next_time, (unsigned long long)ws);
+        }
+        return;
+    }
     if (lead) {
         atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
         *init = fresh_summary();
     }
     const int parity = (int)((rbase + (uint64_t)i) & 1);
-    if (ws >= stop) {
-        if (lead) atomicMin(&P.sum->next_time, (unsigned long long)ws);
-        return;
-    }
     uint64_t we = ws + window;
     if (we > stop || we < ws) we = stop;
     uint64_t next, nev, npkt;
@@ -2057,14 +2125,15 @@ __global__ void k_xpack(DParams P, const DevSummary* __restrict__ sum, int clean
 // headers of the last exchange; any flagged header (a first-touch log, a
 // spill or an error anywhere in the group) halts the batch on every engine
 // alike.  The last block writes this engine's headers for the next exchange.
-__global__ __launch_bounds__(kBlock) void k_round_x(const DParams* __restrict__ Pp, const shd_event* __restrict__ xrecv,
+__global__ __launch_bounds__(kBlock) void k_round_x(DRoundArgs a, const DParams* __restrict__ Pp,
+                                                    const shd_event* __restrict__ xrecv,
                                                     XHeader* __restrict__ halt_hdr, DevSummary* __restrict__ init,
                                                     const DevCtl* __restrict__ ctl, int i, uint64_t window) {
     const DParams& P = *Pp;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     HostIn in;
-    host_in_load(P, lane_host(P), in);
-    if (*P.halt) {
+    host_in_load(a, in);
+    if (*a.halt) {
         if (lead) P.sum->flags = 2u;
         return;
     }
@@ -2652,9 +2721,9 @@ static int enqueue_batch(shd_eng* e) {
     constexpr int B = shd_eng::kBatch;
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     for (int i = 0; i < B; i++) {
-        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, (const DParams*)(e->d_pr + i + 1),
-                           (const DevSummary*)&e->d_ring[i],
-                           &e->d_ring[i + 2], (const DevCtl*)e->d_ctl, i, e->window);
+        hipLaunchKernelGGL(k_round_dev, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
+                           (const DevSummary*)&e->d_ring[i], (const DevCtl*)e->d_ctl,
+                           (const DParams*)(e->d_pr + i + 1), &e->d_ring[i + 2], i, e->window);
     }
     SHD_HIP(hipGetLastError());
     return SHD_OK;
@@ -3345,7 +3414,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             for (int k = 0; k < nl; k++) {
                 shd_eng* e = g->engs[k];
                 const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
-                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream,
+                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
                                    (const DParams*)(g->loc[k].d_xpr + i + 1),
                                    (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
                                    (const DevCtl*)e->d_ctl, i, g->window);
