@@ -346,7 +346,9 @@ struct HotK {
 };
 template <class T>
 __device__ __forceinline__ T launder(T x) {
+#ifndef SHD_NO_LAUNDER
     asm volatile("" : "+v"(x));
+#endif
     return x;
 }
 
