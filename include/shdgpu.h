@@ -322,7 +322,8 @@ typedef struct shd_run_stats {
     double device_ms_launches;      /* HIP-event time of the round launches on the engine's
                                        stream (batches; includes the gaps between launches) */
     uint32_t error;
-    uint32_t _pad;
+    uint32_t n_batches_ticketless;  /* device batches run without the completion ticket
+                                       (no first touch logged in the batch before) */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

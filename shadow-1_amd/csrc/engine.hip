@@ -2066,6 +2066,114 @@ __global__ __launch_bounds__(kBlock) void k_round_dev(DRoundArgs a, const DevSum
     if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
 }
 
+// Ticketless rounds.  Every block writes its share of the round's summary
+// (TlPart) and ends; there is no completion ticket.  The next round's blocks
+// each fold all the shares of this one (one load per lane, issued with the
+// host-state loads) to get their window start, and its block 0 publishes the
+// fold as this round's summary; k_fold_tl publishes the batch's last round.
+// Without a ticket no block sees the whole round's first-touch log, so a
+// round that logged is resolved by the host: the next round halts the batch.
+// The host runs these batches once a batch has logged nothing.
+struct TlPart {
+    unsigned long long next, t_end;
+    unsigned int nev, npkt, err, pad;
+};
+__device__ __forceinline__ void tl_fold(TlPart& a, const TlPart& b) {
+    a.next = b.next < a.next ? b.next : a.next;
+    a.t_end = b.t_end > a.t_end ? b.t_end : a.t_end;
+    a.nev += b.nev;
+    a.npkt += b.npkt;
+    a.err |= b.err;
+}
+// the wave's fold of the shares [0, n) (one wave per block)
+__device__ __forceinline__ TlPart tl_gather(const TlPart* __restrict__ parts, uint32_t n) {
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    for (uint32_t j = threadIdx.x; j < n; j += 64) tl_fold(f, parts[j]);
+    for (int off = 32; off > 0; off >>= 1) {
+        TlPart o;
+        o.next = __shfl_xor(f.next, off, 64);
+        o.t_end = __shfl_xor(f.t_end, off, 64);
+        o.nev = __shfl_xor(f.nev, off, 64);
+        o.npkt = __shfl_xor(f.npkt, off, 64);
+        o.err = __shfl_xor(f.err, off, 64);
+        tl_fold(f, o);
+    }
+    return f;
+}
+// publish a round's fold into its summary; a round that logged first touches
+// halts the batch (the host resolves its log)
+__device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint32_t* halt) {
+    if (f.next != kInf) atomicMin(&s->next_time, f.next);
+    if (f.nev) atomicAdd(&s->n_events, (unsigned long long)f.nev);
+    if (f.npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f.npkt);
+    if (f.err) atomicOr(&s->error, f.err);
+    atomicMax(&s->t_last, f.t_end);
+    if (s->n_pending) *halt = 1u;
+}
+
+// round i of a ticketless batch: shares of round i go to parts[i & 1]
+__global__ __launch_bounds__(kBlock) void k_round_tl(DRoundArgs a, DevSummary* __restrict__ prev,
+                                                      const DevCtl* __restrict__ ctl,
+                                                      const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
+                                                      TlPart* __restrict__ parts, int i, uint64_t window) {
+    const DParams& P = *Pp;
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
+#endif
+    const uint32_t nblk = gridDim.x;
+    HostIn in;
+    host_in_load(a, in);
+    // round 0 of the batch starts at the seeded time; later rounds fold the
+    // previous round's shares (its first-touch log count halts)
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    if (i > 0) f = tl_gather(parts + (size_t)((i - 1) & 1) * nblk, nblk);
+    const uint32_t halt = *a.halt;
+    const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws0 = prev->next_time, npend = prev->n_pending;
+    const uint64_t ws = f.next < ws0 ? f.next : ws0;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (lead && i > 0) tl_publish(prev, f, (uint32_t*)a.halt);
+    TlPart* mine = parts + (size_t)(i & 1) * nblk + blockIdx.x;
+    if ((halt != 0) | (i > 0 && npend != 0) | (ws >= stop)) {
+        if (halt == 0 && !(i > 0 && npend != 0)) {   // only forwards the time
+            if (lead) {
+                atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+                *init = fresh_summary();
+                P.sum->ws = ws;
+            }
+            if (threadIdx.x == 0) *mine = TlPart{ws, (unsigned long long)wall_clock64(), 0, 0, 0, 0};
+        }
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+        *init = fresh_summary();
+        P.sum->ws = ws;
+    }
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    TIM(4);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0) *mine = TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, 0};
+    TIM(5);
+}
+
+// after a ticketless batch: publish its last round (shares in parts[(n-1) & 1])
+__global__ __launch_bounds__(64) void k_fold_tl(const TlPart* __restrict__ parts, uint32_t nblk, int last,
+                                                DevSummary* __restrict__ s, uint32_t* __restrict__ halt) {
+    const TlPart f = tl_gather(parts + (size_t)(last & 1) * nblk, nblk);
+    if (threadIdx.x == 0 && *halt == 0u) tl_publish(s, f, halt);
+}
+
 // ingest events from other engines into inbox[parity]
 __global__ void k_ingest(DParams P, const shd_event* __restrict__ ev, uint64_t n, int parity) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2289,6 +2397,9 @@ struct shd_eng {
     DevCtl* h_ctl = nullptr;
     DevSummary* h_seed = nullptr;           // pinned: ring slots 0 and 1 at a batch start
     hipGraphExec_t batch_graph = nullptr;   // captured batch of kBatch device-driven rounds
+    hipGraphExec_t batch_graph_tl = nullptr;   // the same, ticketless (k_round_tl)
+    TlPart* d_tpart = nullptr;              // [2][grid] ticketless round shares
+    bool tl_ready = false;                  // the last batch logged no first touch: run ticketless
     Params* d_pr = nullptr;                 // device copies of P, one per summary-ring slot (sum = &d_ring[i])
     double wall_khz = 100000.0;             // device wall clock (wall_clock64) rate
     uint64_t trace_cap = 0;
@@ -2370,6 +2481,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     EALLOC(P.hs, n);
     EALLOC(P.hc, n);
     EALLOC(P.part, n);
+    EALLOC(e->d_tpart, 2 * n);
     EALLOC(P.gpart, n / kTickGroup + 2);
     EALLOC(P.tick, n / kTickGroup + 3);
     {
@@ -2731,21 +2843,36 @@ static int enqueue_batch(shd_eng* e) {
     return SHD_OK;
 }
 
-static int launch_batch(shd_eng* e) {
+static int enqueue_batch_tl(shd_eng* e) {
+    constexpr int B = shd_eng::kBatch;
+    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
+    for (int i = 0; i < B; i++) {
+        hipLaunchKernelGGL(k_round_tl, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P), &e->d_ring[i],
+                           (const DevCtl*)e->d_ctl, (const DParams*)(e->d_pr + i + 1), &e->d_ring[i + 2],
+                           e->d_tpart, i, e->window);
+    }
+    hipLaunchKernelGGL(k_fold_tl, dim3(1), dim3(64), 0, e->stream, (const TlPart*)e->d_tpart, (uint32_t)grid, B - 1,
+                       &e->d_ring[B], e->d_halt);
+    SHD_HIP(hipGetLastError());
+    return SHD_OK;
+}
+
+static int launch_batch(shd_eng* e, bool tl) {
     static const bool no_graph = getenv("SHD_NO_GRAPH") != nullptr;
-    if (no_graph) return enqueue_batch(e);
-    if (!e->batch_graph) {
+    if (no_graph) return tl ? enqueue_batch_tl(e) : enqueue_batch(e);
+    hipGraphExec_t& ge = tl ? e->batch_graph_tl : e->batch_graph;
+    if (!ge) {
         hipGraph_t gr = nullptr;
         SHD_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
-        const int rc = enqueue_batch(e);
+        const int rc = tl ? enqueue_batch_tl(e) : enqueue_batch(e);
         const hipError_t ec = hipStreamEndCapture(e->stream, &gr);
         if (rc) return rc;
         SHD_HIP(ec);
-        const hipError_t ei = hipGraphInstantiate(&e->batch_graph, gr, nullptr, nullptr, 0);
+        const hipError_t ei = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
         (void)hipGraphDestroy(gr);
         SHD_HIP(ei);
     }
-    SHD_HIP(hipGraphLaunch(e->batch_graph, e->stream));
+    SHD_HIP(hipGraphLaunch(ge, e->stream));
     return SHD_OK;
 }
 
@@ -2774,7 +2901,10 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         SHD_HIP(hipEventRecord(e->bev[0], e->stream));
-        if ((rc = launch_batch(e))) break;
+        static const bool no_tl = getenv("SHD_NO_TL") != nullptr;
+        const bool tl = e->tl_ready && !no_tl;
+        if ((rc = launch_batch(e, tl))) break;
+        if (tl) s.n_batches_ticketless++;
         SHD_HIP(hipEventRecord(e->bev[1], e->stream));
         uint32_t halt = 0;
         SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost, e->stream));
@@ -2784,6 +2914,8 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             float ms = 0;
             if (hipEventElapsedTime(&ms, e->bev[0], e->bev[1]) == hipSuccess) s.device_ms_launches += ms;
         }
+        // ticketless batches only while no round logs a first touch
+        bool logged = false;
         for (int i = 0; i < B; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
@@ -2791,7 +2923,8 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             const double ms = round_kernel_ms(e, r);
             e->kernel_ms_total += ms;
             e->last_kernel_ms = ms;
-            const bool halted_here = halt && r.n_pending > (unsigned long long)kResolveMax;
+            if (r.n_pending) logged = true;
+            const bool halted_here = halt && r.n_pending > (tl ? 0ull : (unsigned long long)kResolveMax);
             s.n_rounds++;
             s.n_events += r.n_events;
             s.n_pkt_events += r.n_pkt_events;
@@ -2828,6 +2961,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             }
             next = r.next_time;
         }
+        e->tl_ready = !logged && !halt;
     }
     e->h_sum->next_time = next;
     s.n_pending_resolved = e->pending_resolved - pend0;
@@ -2970,6 +3104,7 @@ extern "C" void shd_eng_destroy(shd_eng* e) {
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
     if (e->h_seed) (void)hipHostFree(e->h_seed);
     if (e->batch_graph) (void)hipGraphExecDestroy(e->batch_graph);
+    if (e->batch_graph_tl) (void)hipGraphExecDestroy(e->batch_graph_tl);
     for (auto& ev : e->bev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->ev0) (void)hipEventDestroy(e->ev0);

@@ -46,6 +46,7 @@ def test_geometric_one_host_per_vertex(queue_flags):
     gpu, ora, eng, _ = run_both(g, m)
     assert_same(gpu, ora)
     assert gpu[2].n_rounds > 100
+    assert gpu[2].n_batches_ticketless > 0                         # ticketless batches exercised
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_LOCAL) > 0     # self-sends exercised
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_INET_DROP) > 0  # reliability drops
 
