@@ -370,6 +370,7 @@ struct HostCtx {
     uint32_t evq_n;
     uint64_t top_time;          // heap root's time (the root itself: s_top; valid when evq_n > 0)
     uint32_t dh, nd;            // next / count of the window's calendar events (s_due)
+    uint64_t dt;                // time of the due list's head (kInf: none left)
     uint32_t ns;                // deferred sends (s_send)
     uint64_t seq_base;          // ev_seq at the last flush: IDs >= it are provisional
     int32_t self_lo, self_hi;   // loopback draws (Params::self_thr)
@@ -1236,7 +1237,7 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.cq_hv = false; c.tq_hv = false;
     c.att = att;
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
-    c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0;
+    c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0; c.dt = kInf;
     c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
     c.w_msgs = 0; c.w_fl = 0;
     c.self_lo = st.x;
@@ -1251,10 +1252,18 @@ __device__ __forceinline__ uint64_t host_next(const HostCtx& c) {
     return c.tt2 < t ? c.tt2 : t;
 }
 
+// the due list's next head time, after a take
+__device__ __forceinline__ void due_advance(HostCtx& c) {
+    c.dh++;
+    const uint32_t k = c.dh < c.nd ? c.dh : 0u;
+    const uint64_t t = s_due[k * kBlock + threadIdx.x].time;
+    c.dt = c.dh < c.nd ? t : kInf;
+}
+
 // the host's next event in (time, src, seq) order if it is before `we`:
 // the earliest timer (src = the host) against the heap root and the head
-// of the window's calendar events
-__device__ __forceinline__ bool take_next(const DParams& P, HostCtx& c, uint64_t we, shd_event& e) {
+// of the window's calendar events (general case: equal times)
+__device__ __forceinline__ bool take_next_full(const DParams& P, HostCtx& c, uint64_t we, shd_event& e) {
     uint64_t bt = c.tt0, bs = c.ts0;
     uint32_t kind = SHD_EV_HEARTBEAT;
     int slot = 0;
@@ -1290,11 +1299,41 @@ __device__ __forceinline__ bool take_next(const DParams& P, HostCtx& c, uint64_t
         return true;
     }
     if (use_due) {
-        c.dh++;
+        due_advance(c);
         return true;
     }
     if (!hq) return false;
     heap_pop(P, c);
+    return true;
+}
+
+// Common case: the earliest of the five candidate times (three timers, the
+// due head, the heap root) is unique, so it alone decides (a tie needs the
+// (src, seq) order: take_next_full).  Times only, all in registers.
+__device__ __forceinline__ bool take_next(const DParams& P, HostCtx& c, uint64_t we, shd_event& e) {
+    const uint64_t ht = c.evq_n ? c.top_time : kInf;
+    const uint64_t m01 = c.tt0 < c.tt1 ? c.tt0 : c.tt1;
+    const uint64_t bt = m01 < c.tt2 ? m01 : c.tt2;
+    const uint64_t qt = c.dt < ht ? c.dt : ht;
+    const uint64_t t = bt < qt ? bt : qt;
+    if (t >= we) return false;
+    const uint32_t neq = (uint32_t)(c.tt0 == t) + (uint32_t)(c.tt1 == t) + (uint32_t)(c.tt2 == t) +
+                         (uint32_t)(c.dt == t) + (uint32_t)(ht == t);
+    if (neq != 1u) return take_next_full(P, c, we, e);
+    if (c.dt == t) {
+        e = s_due[c.dh * kBlock + threadIdx.x];
+        due_advance(c);
+        return true;
+    }
+    if (ht == t) {
+        e = s_top[threadIdx.x];
+        heap_pop(P, c);
+        return true;
+    }
+    e.time = t; e.src = c.h; e.dst = c.h; e.pkt = 0;
+    if (c.tt0 == t) { e.seq = c.ts0; e.kind = SHD_EV_HEARTBEAT; c.tt0 = kInf; }
+    else if (c.tt1 == t) { e.seq = c.ts1; e.kind = SHD_EV_REFILL; c.tt1 = kInf; }
+    else { e.seq = c.ts2; e.kind = SHD_EV_NOTIFY; c.tt2 = kInf; }
     return true;
 }
 
@@ -1720,6 +1759,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                 }
                 ev_st(s_due + k * kBlock + threadIdx.x, x);
             }
+            c.dt = c.nd ? s_due[threadIdx.x].time : kInf;
         }
         PROF_ADD(c, PR_MERGE, t_m)
         TIMA(8);
