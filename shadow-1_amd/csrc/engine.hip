@@ -1165,22 +1165,24 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     // anything else -- a loopback, a full send buffer, a backlog, the
     // bootstrap period -- is left to run_work's general loop, in order
     const bool boot = bootstrapping(P, c);
+    // (one exit: a loopback ends the loop through tq_count)
     while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap && !boot) {
         const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
         c.w_msgs--;
-        if ((int32_t)rv > c.k.dst_thr) continue;   // no destination: nothing queued
-        random_free_port(c);
-        const uint32_t pkt = c.pkt_seq++;
-        if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
-            s_tqh[threadIdx.x] = TxEnt{rv, pkt};
-            c.tq_hv = true;
-            c.tq_count = 1;
-            c.w_fl |= W_SENDING;
-            break;
+        if ((int32_t)rv <= c.k.dst_thr) {   // else no destination: nothing queued
+            random_free_port(c);
+            const uint32_t pkt = c.pkt_seq++;
+            if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
+                s_tqh[threadIdx.x] = TxEnt{rv, pkt};
+                c.tq_hv = true;
+                c.tq_count = 1;
+                c.w_fl |= W_SENDING;
+            } else {
+                worker_send_deferred(P, c, rv, pkt);
+                consume(c.tx_rem, c.k.pkt_len);
+                refill_if_needed(P, c);
+            }
         }
-        worker_send_deferred(P, c, rv, pkt);
-        consume(c.tx_rem, c.k.pkt_len);
-        refill_if_needed(P, c);
     }
 }
 
