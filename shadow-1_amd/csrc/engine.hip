@@ -1083,6 +1083,34 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     c.q_sub = 0;
     c.w_msgs = 0;
     c.w_fl = 0;
+#ifndef SHD_NO_EVFAST
+    // The steady-state arrival, straight-line: a packet that meets an empty
+    // router queue with room in the receive bucket at a listening host (no
+    // tracing, past the bootstrap period) is enqueued, dequeued at once
+    // (sojourn 0: CoDel's interval and drop mode reset) and received; the
+    // epoll notification is scheduled at +1 ns unless one is pending (its ID
+    // is consumed even when it falls past the end).  The same steps as the
+    // general path below, in the same order.
+    if (e.kind == SHD_EV_PACKET && c.cq_count == 0 && c.rx_rem >= SHD_MTU && (c.flags & F_LISTENING) &&
+        !c.k.trace && !bootstrapping(P, c)) {
+        c.c_pkt++;
+        c.c_recv++;
+        c.unread++;
+        c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
+        c.cq_iexp = 0;
+        const bool nt = !(c.flags & F_NOTIFY_PENDING);
+        if (nt && c.tt2 != kInf) c.err |= SHD_ERR_INTERNAL;
+        const uint64_t id = c.ev_seq, tn = c.now + 1;
+        c.ev_seq += nt ? 1u : 0u;
+        const bool set = nt && tn < c.k.end_time;
+        c.tt2 = set ? tn : c.tt2;
+        c.ts2 = set ? id : c.ts2;
+        c.flags = (c.flags & ~F_CODEL_DROP_MODE) | F_NOTIFY_PENDING;
+        consume(c.rx_rem, c.k.pkt_len);
+        refill_if_needed(P, c);
+        return;
+    }
+#endif
     switch (e.kind) {
     case SHD_EV_HEARTBEAT:
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
