@@ -283,16 +283,21 @@ __device__ unsigned long long g_tim[64][2048][20];
 // begin_event}.  Class = kind (1..7), 8 = a packet on the general path
 __device__ unsigned long long g_kc[10][4];
 __shared__ unsigned long long s_kc[10][4];
+#ifdef SHD_TIMING_NOWAIT   // stamps when the wave gets there, without draining its memory ops
+#define TIM_WAIT()
+#else
+#define TIM_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
+#endif
 #define TIM(k)                                                                                         \
     do {                                                                                               \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+        TIM_WAIT();                                                                                    \
         if (threadIdx.x == 0 && blockIdx.x < 2048)                                                     \
             g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = wall_clock64();       \
     } while (0)
 // inside a divergent region: the first active lane stamps
 #define TIMA(k)                                                                                        \
     do {                                                                                               \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                    \
+        TIM_WAIT();                                                                                    \
         if ((int)threadIdx.x == __ffsll((unsigned long long)__ballot(1)) - 1 && blockIdx.x < 2048)     \
             g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = wall_clock64();       \
     } while (0)
@@ -451,7 +456,11 @@ __device__ __forceinline__ shd_event* heap_base(const DParams& P, const HostCtx&
     return P.evq + (size_t)c.l * P.evq_stride + 3;
 }
 
-__device__ void heap_push(const DParams& P, HostCtx& c, const shd_event& e) {
+// (e by value: an event passed by reference into global memory is loaded
+// once, and its time is consumed here, not left pending into the event loop)
+__device__ void heap_push(const DParams& P, HostCtx& c, const shd_event e_in) {
+    shd_event e = e_in;
+    e.time = launder(e.time);
     shd_event* hp = heap_base(P, c);
     if (c.evq_n >= c.k.evq_cap) { c.err |= SHD_ERR_EVQ_OVERFLOW; return; }
     uint32_t i = c.evq_n++;
@@ -1245,33 +1254,37 @@ __device__ bool run_work(const DParams& P, HostCtx& c) {
 // test: one memory round trip for both) and the heap root
 __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l, const HostRec& r, int32_t att,
                                          int2 st) {
+    // every field taken from the record is consumed here (launder): a load
+    // still pending at the event loop would make each iteration, and the
+    // code after the loop, wait for all the wave's outstanding stores (one
+    // vmcnt counter, in order)
     c.l = l;
     c.h = (uint32_t)(P.h0 + l);
-    c.rng = r.rng; c.ev_seq = r.ev_seq; c.pkt_seq = r.pkt_seq;
-    c.rx_rem = r.rx_rem; c.tx_rem = r.tx_rem; c.rx_refill = r.rx_refill; c.tx_refill = r.tx_refill;
-    c.flags = r.flags; c.unread = r.unread;
-    c.cq_total = r.cq_total; c.cq_iexp = r.cq_iexp; c.cq_ndrop = r.cq_ndrop;
-    c.cq_dc = r.cq_dc; c.cq_dcl = r.cq_dcl; c.cq_head = r.cq_head; c.cq_count = r.cq_count;
-    c.tq_head = r.tq_head; c.tq_count = r.tq_count;
-    c.evq_n = r.evq_n;
+    c.rng = launder(r.rng); c.ev_seq = launder(r.ev_seq); c.pkt_seq = launder(r.pkt_seq);
+    c.rx_rem = launder(r.rx_rem); c.tx_rem = launder(r.tx_rem); c.rx_refill = launder(r.rx_refill); c.tx_refill = launder(r.tx_refill);
+    c.flags = launder(r.flags); c.unread = launder(r.unread);
+    c.cq_total = launder(r.cq_total); c.cq_iexp = launder(r.cq_iexp); c.cq_ndrop = launder(r.cq_ndrop);
+    c.cq_dc = launder(r.cq_dc); c.cq_dcl = launder(r.cq_dcl); c.cq_head = launder(r.cq_head); c.cq_count = launder(r.cq_count);
+    c.tq_head = launder(r.tq_head); c.tq_count = launder(r.tq_count);
+    c.evq_n = launder(r.evq_n);
     if (r.evq_n) {
         const shd_event t = P.evq[(size_t)l * P.evq_stride + 3];
         s_top[threadIdx.x] = t;
-        c.top_time = t.time;
+        c.top_time = launder(t.time);
     } else {
         c.top_time = kInf;
     }
-    c.tt0 = r.tt[0]; c.tt1 = r.tt[1]; c.tt2 = r.tt[2];
-    c.ts0 = r.ts[0]; c.ts1 = r.ts[1]; c.ts2 = r.ts[2];
+    c.tt0 = launder(r.tt[0]); c.tt1 = launder(r.tt[1]); c.tt2 = launder(r.tt[2]);
+    c.ts0 = launder(r.ts[0]); c.ts1 = launder(r.ts[1]); c.ts2 = launder(r.ts[2]);
     c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.cq_hv = false; c.tq_hv = false;
-    c.att = att;
+    c.att = launder(att);
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
     c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0; c.dt = kInf;
     c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
     c.w_msgs = 0; c.w_fl = 0;
-    c.self_lo = st.x;
-    c.self_hi = st.y;
+    c.self_lo = launder(st.x);
+    c.self_hi = launder(st.y);
 }
 
 // earliest pending event of the host (timers and heap)
