@@ -48,8 +48,18 @@ def main():
     fk.restype = C.c_int
     fk.argtypes = [C.POINTER(C.c_uint64), C.c_int]
     fk(kc.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
+    cn = np.zeros(8, dtype=np.uint64)
+    fc = lib.shd_debug_counts
+    fc.restype = C.c_int
+    fc.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    fc(cn.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
     st = eng.run_until(int(2.5 * S.SHD_SEC))
     fk(kc.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
+    fc(cn.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
+    nr = max(st.n_rounds, 1)
+    names = ["cq HBM loads", "tq HBM loads", "heap pushes", "heap pops", "inbox merged", "events", "flushes (waves)",
+             "suspended lanes"]
+    print("per round: " + ", ".join(f"{names[i]} {cn[i] / nr:.1f}" for i in range(8)))
     buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
     f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
     t = buf.reshape(64, 2048, 20).astype(np.int64)

@@ -282,6 +282,10 @@ __device__ unsigned long long g_tim[64][2048][20];
 // starts one of that class: {iterations, cycles, of which take_next, of which
 // begin_event}.  Class = kind (1..7), 8 = a packet on the general path
 __device__ unsigned long long g_kc[10][4];
+// event-path counters (timing build): cq / tq entries loaded from HBM, heap
+// pushes / pops, inbox events merged, events, flushes, suspended lanes
+__device__ unsigned long long g_cnt[8];
+#define TCNT(i) atomicAdd(&g_cnt[i], 1ull)
 __shared__ unsigned long long s_kc[10][4];
 #ifdef SHD_TIMING_NOWAIT   // stamps when the wave gets there, without draining its memory ops
 #define TIM_WAIT()
@@ -310,6 +314,7 @@ __shared__ unsigned long long s_kc[10][4];
 #define TIM(k)
 #define TIMA(k)
 #define TIMV(k, v)
+#define TCNT(i)
 #endif
 #ifdef SHD_PROF
 __device__ unsigned long long g_prof[2 * PR_N + 2];
@@ -459,6 +464,7 @@ __device__ __forceinline__ shd_event* heap_base(const DParams& P, const HostCtx&
 // (e by value: an event passed by reference into global memory is loaded
 // once, and its time is consumed here, not left pending into the event loop)
 __device__ void heap_push(const DParams& P, HostCtx& c, const shd_event e_in) {
+    TCNT(2);
     shd_event e = e_in;
     e.time = launder(e.time);
     shd_event* hp = heap_base(P, c);
@@ -487,6 +493,7 @@ __device__ void heap_push(const DParams& P, HostCtx& c, const shd_event e_in) {
 // remove the root; the new root is re-cached.  The four children are read
 // whole (an index past the end rereads the last entry and never wins)
 __device__ void heap_pop(const DParams& P, HostCtx& c) {
+    TCNT(3);
     shd_event* hp = heap_base(P, c);
     const uint32_t n = --c.evq_n;
     if (n == 0) return;
@@ -660,6 +667,7 @@ __device__ bool codel_helper(const DParams& P, HostCtx& c, bool& okToDrop, Codel
         c.cq_hv = false;
     } else {
         out = P.cq[(size_t)c.l * c.k.cq_cap + c.cq_head];
+        TCNT(0);
     }
     c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
     c.cq_count--;
@@ -1009,6 +1017,7 @@ __device__ bool if_send_step(const DParams& P, HostCtx& c) {
             p = s_tqh[threadIdx.x];
         } else {
             p = P.tq[(size_t)c.l * c.k.tq_cap + c.tq_head];
+            TCNT(1);
             s_tqh[threadIdx.x] = p;   // keep the peeked head: a flush may come first
             c.tq_hv = true;
         }
@@ -1086,6 +1095,7 @@ __device__ void refill_cb(const DParams& P, HostCtx& c) {
 //   NOTIFY    one new message per unread datagram, each sent right away
 //   APP_START `load` new messages
 __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
+    TCNT(5);
     c.c_events++;
     c.q_seq = e.seq;
     c.q_src = e.src;
@@ -1117,6 +1127,32 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         c.flags = (c.flags & ~F_CODEL_DROP_MODE) | F_NOTIFY_PENDING;
         consume(c.rx_rem, c.k.pkt_len);
         refill_if_needed(P, c);
+        return;
+    }
+    // The steady-state notification, straight-line: one unread datagram, an
+    // empty send queue with room in the send bucket and in the deferred-send
+    // buffer, past the bootstrap period: one new message, sent at once
+    // unless it draws this host (then the general send loop takes it).  The
+    // same draws and steps, in the same order, as the general path below.
+    if (e.kind == SHD_EV_NOTIFY && c.unread == 1u && c.tq_count == 0 && c.tx_rem >= SHD_MTU &&
+        c.ns < (uint32_t)kSendCap && !c.k.trace && !bootstrapping(P, c)) {
+        c.flags &= ~F_NOTIFY_PENDING;
+        c.unread = 0;
+        const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
+        if ((int32_t)rv <= c.k.dst_thr) {   // else no destination: nothing queued
+            random_free_port(c);
+            const uint32_t pkt = c.pkt_seq++;
+            if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
+                s_tqh[threadIdx.x] = TxEnt{rv, pkt};
+                c.tq_hv = true;
+                c.tq_count = 1;
+                c.w_fl = W_SENDING;
+            } else {
+                worker_send_deferred(P, c, rv, pkt);
+                consume(c.tx_rem, c.k.pkt_len);
+                refill_if_needed(P, c);
+            }
+        }
         return;
     }
 #endif
@@ -1737,8 +1773,13 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #ifdef SHD_TIMING
     uint64_t n_it = 0, k_tk = 0, k_be = 0, k_rw = 0, k_fl = 0, k_in = 0;
     uint64_t k_l0 = 0, n_kinds = 0, n_lanes = 0;
+#ifdef SHD_TIMING_LIGHT   // phase stamps only: no clock reads inside the event loop
+#define KT0(v)
+#define KTA(acc, v)
+#else
 #define KT0(v) const uint64_t v = clock64();
 #define KTA(acc, v) acc += clock64() - v;
+#endif
 #elif defined(SHD_MARK)   // asm listing markers (static code-size census)
 #define KT0(v) asm volatile("; MARK " #v " begin" ::: "memory");
 #define KTA(acc, v) asm volatile("; MARK " #v " end" ::: "memory");
@@ -1767,7 +1808,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
         if (nin) {
             const shd_event* ib = P.inbox[parity] + (size_t)l * P.inbox_cap;
             const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
-            for (uint32_t i = 0; i < n; i++) heap_push(P, c, ib[i]);
+            for (uint32_t i = 0; i < n; i++) { TCNT(4); heap_push(P, c, ib[i]); }
             P.inbox_n[parity][l] = 0;
         }
         // the window's calendar events, sorted into the due list.  The slots
@@ -1826,6 +1867,8 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             for (;;) {
 #ifdef SHD_TIMING
                 n_it++;
+#endif
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
                 const uint64_t i_t0 = clock64();
                 uint64_t i_tk = 0, i_be = 0;
                 uint32_t i_cls = 0;
@@ -1836,7 +1879,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                     KT0(q0)
                     const bool more = take_next(P, c, we, e);
                     KTA(k_tk, q0)
-#ifdef SHD_TIMING
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
                     i_tk = clock64();
                     if (more) {
                         i_cls = e.kind & 7;
@@ -1845,7 +1888,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                     }
 #endif
                     PROF_ADD(c, PR_POP, t_p)
-#ifdef SHD_TIMING
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
                     {   // divergence census: distinct event kinds started in this iteration
                         const uint32_t ks = more ? 1u << (e.kind & 31) : 0u;
                         for (uint32_t b = 1; b < 8; b++) n_kinds += __ballot((ks >> b) & 1u) != 0;
@@ -1857,10 +1900,10 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                         KT0(q1)
                         begin_event(P, c, e);
                         KTA(k_be, q1)
-#ifdef SHD_TIMING
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
                         i_be = clock64();
 #endif
-                        st = 1u;
+                        st = (c.w_fl | c.w_msgs) ? 1u : 0u;   // the shared steps, if any are left
                     } else {
                         st = 3u;
                     }
@@ -1870,7 +1913,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                     st = run_work(P, c) ? 0u : 2u;
                     KTA(k_rw, q2)
                 }
-#ifdef SHD_TIMING
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
                 {
                     const uint64_t i_t1 = clock64();
                     const uint64_t m = __ballot(i_cls != 0);
@@ -1891,6 +1934,8 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             }
             KTA(k_in, q4)
             KT0(q3)
+            if (threadIdx.x == 0) TCNT(6);
+            if (st == 2u) TCNT(7);
             flush_wave(P, c);
             KTA(k_fl, q3)
             if (__ballot(st == 2u) == 0) break;
@@ -3058,6 +3103,15 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
 extern "C" int shd_debug_timing(uint64_t* out) {   // 64 x 2048 x 20
     SHD_HIP(hipDeviceSynchronize());
     SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tim), sizeof(g_tim)));
+    return SHD_OK;
+}
+extern "C" int shd_debug_counts(uint64_t* out, int reset) {   // 8
+    SHD_HIP(hipDeviceSynchronize());
+    SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cnt), sizeof(g_cnt)));
+    if (reset) {
+        static const unsigned long long z[8] = {};
+        SHD_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_cnt), z, sizeof(g_cnt)));
+    }
     return SHD_OK;
 }
 extern "C" int shd_debug_kind_costs(uint64_t* out, int reset) {   // 10 x 4
