@@ -1155,6 +1155,22 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         }
         return;
     }
+    // the periodic refill with both queues empty: top up; the receive loop's
+    // one dequeue attempt only resets CoDel's interval and drop mode, the
+    // send loop does nothing (as the general REFILL case below)
+    if (e.kind == SHD_EV_REFILL && c.cq_count == 0 && c.tq_count == 0) {
+        c.flags &= ~F_REFILL_PENDING;
+        c.rx_rem += c.rx_refill;
+        if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
+        c.tx_rem += c.tx_refill;
+        if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
+        if (bootstrapping(P, c) || c.rx_rem >= SHD_MTU) {
+            c.cq_iexp = 0;
+            c.flags &= ~F_CODEL_DROP_MODE;
+        }
+        refill_if_needed(P, c);
+        return;
+    }
 #endif
     switch (e.kind) {
     case SHD_EV_HEARTBEAT:
