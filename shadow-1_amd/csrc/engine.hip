@@ -172,6 +172,8 @@ struct DestGuide {
 };
 static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 
+constexpr int kDestExc = 16;   // closed-form destination exceptions (ParamsT::exc_x)
+
 template <template <class> class Ptr>
 struct ParamsT {
     // hosts
@@ -215,6 +217,12 @@ struct ParamsT {
     // self_thr[h].x <= x <= self_thr[h].y (precomputed, exact)
     int32_t dst_thr;
     Ptr<const int2> self_thr;
+    // closed-form destinations (dest_closed): even weights, host h attached
+    // at index h.  The draw x picks host max(ceil(x*H/RAND_MAX) - 1, 0),
+    // except at the listed draws (where the f64 cumulative sums round across
+    // a threshold); verified on the host at every step of both functions
+    int32_t dest_closed, n_exc;
+    int32_t exc_x[kDestExc], exc_d[kDestExc];
     // path cache
     int32_t T;
     int32_t complete, prefer_direct, directed;
@@ -902,11 +910,20 @@ __device__ void flush_wave(const DParams& P, HostCtx& c) {
         const uint32_t hl = id >> 4, i = id & 15u;
         const SendRec q = s_send[i * kBlock + hl];
         const int32_t a = s_att[hl];
-        const double rr = (double)q.r / kRandMax;
-        const uint4* gq = (const uint4*)(P.dest_guide + guide_index(P, rr));
-        const uint4 g0 = gq[0], g1 = gq[1], g2 = gq[2];
         int32_t dst, b;
-        guide_pick(P, g0, g1, g2, rr, dst, b);
+        if (P.dest_closed) {   // no table: one memory round trip fewer
+            const uint64_t nx = (uint64_t)q.r * (uint64_t)(uint32_t)P.H;
+            const uint64_t cx = (nx + 2147483646ull) / 2147483647ull;
+            int32_t d = cx ? (int32_t)cx - 1 : 0;
+            for (int j = 0; j < P.n_exc; j++) d = (int32_t)q.r == P.exc_x[j] ? P.exc_d[j] : d;
+            dst = d;
+            b = d;
+        } else {
+            const double rr = (double)q.r / kRandMax;
+            const uint4* gq = (const uint4*)(P.dest_guide + guide_index(P, rr));
+            const uint4 g0 = gq[0], g1 = gq[1], g2 = gq[2];
+            guide_pick(P, g0, g1, g2, rr, dst, b);
+        }
         PathRaw x;
         const int32_t ra = P.complete ? kNoRank : P.rank[a];
         path_load(P, a, b, x);
@@ -2722,6 +2739,49 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             thr[h].y = draw_threshold(m->dest_cum[h]);
         }
         P.dst_thr = draw_threshold(m->dest_cum[H - 1]);
+        // closed-form destinations: host h at attached index h, thresholds
+        // thr[i] = floor((i+1) R / H) but for a few i (the exceptions).  Both
+        // pick functions are step functions of x changing only at thr[i]+1
+        // and f(i)+1, so checking every such x (and 0) checks them all.
+        {
+            constexpr uint64_t R = 2147483647ull;
+            bool ok = getenv("SHD_NO_DEST_CLOSED") == nullptr;
+            for (int32_t h = 0; h < H && ok; h++) ok = host_att[h] == h;
+            std::vector<int32_t> ty(H);
+            for (int32_t i = 0; i < H; i++) ty[i] = thr[i].y;
+            auto f = [&](int32_t i) { return (int64_t)(((uint64_t)(i + 1) * R) / (uint64_t)H); };
+            auto pick_true = [&](int64_t x) {   // first i with thr[i] >= x
+                return (int32_t)(std::lower_bound(ty.begin(), ty.end(), (int32_t)x) - ty.begin());
+            };
+            auto pick_closed = [&](int64_t x) {
+                const uint64_t c = ((uint64_t)x * (uint64_t)H + (R - 1)) / R;
+                return c ? (int32_t)c - 1 : 0;
+            };
+            std::vector<std::pair<int32_t, int32_t>> exc;
+            for (int32_t i = 0; i < H && ok; i++) {
+                if (f(i) == ty[i]) continue;
+                const int64_t lo = std::min<int64_t>(f(i), ty[i]) + 1, hi = std::max<int64_t>(f(i), ty[i]);
+                for (int64_t x = lo; x <= hi && ok; x++) {
+                    if (x > P.dst_thr) break;
+                    const int32_t t = pick_true(x);
+                    if (t != pick_closed(x)) {
+                        if (exc.size() == (size_t)kDestExc) ok = false;
+                        else exc.push_back({(int32_t)x, t});
+                    }
+                }
+            }
+            auto pick_exc = [&](int64_t x) {
+                int32_t d = pick_closed(x);
+                for (auto& p : exc) if (p.first == x) d = p.second;
+                return d;
+            };
+            for (int32_t i = 0; i < H && ok; i++)
+                for (int64_t x : {(int64_t)0, (int64_t)ty[i] + 1, f(i) + 1})
+                    if (x <= P.dst_thr && pick_exc(x) != pick_true(x)) ok = false;
+            P.dest_closed = ok ? 1 : 0;
+            P.n_exc = ok ? (int32_t)exc.size() : 0;
+            for (size_t j = 0; j < exc.size() && ok; j++) { P.exc_x[j] = exc[j].first; P.exc_d[j] = exc[j].second; }
+        }
         if (hipMemcpyAsync(e->d_self_thr, thr.data(), sizeof(int2) * (size_t)H, hipMemcpyHostToDevice, e->stream) !=
                 hipSuccess ||
             hipStreamSynchronize(e->stream) != hipSuccess) {

@@ -37,8 +37,12 @@ def assert_same(gpu, ora):
     assert np.array_equal(gdg, odg)
 
 
-@pytest.mark.parametrize("queue_flags", [0, S.SHD_QF_NO_CALENDAR])
-def test_geometric_one_host_per_vertex(queue_flags):
+@pytest.mark.parametrize("queue_flags,closed", [(0, True), (S.SHD_QF_NO_CALENDAR, True), (0, False)])
+def test_geometric_one_host_per_vertex(queue_flags, closed, monkeypatch):
+    # one host per vertex, even weights: destinations in closed form (the
+    # table-free pick), or through the guide table (SHD_NO_DEST_CLOSED)
+    if not closed:
+        monkeypatch.setenv("SHD_NO_DEST_CLOSED", "1")
     # queue_flags=NO_CALENDAR: every inter-host event takes the inbox + heap path
     g = W.geometric_graph(300, seed=2)
     m = W.phold_model(W.hosts_on_vertices(300, 1), end_time=3 * S.SHD_SEC, trace=True,
