@@ -43,6 +43,7 @@ def main():
     eng = Engine(m, pc, 0, a.hosts, device=0)
     eng.boot()
     eng.run_until(2 * S.SHD_SEC)
+    eng.run_until(int(2.2 * S.SHD_SEC))   # ticketless batches from here on
     kc = np.zeros(40, dtype=np.uint64)
     fk = lib.shd_debug_kind_costs
     fk.restype = C.c_int
@@ -66,6 +67,7 @@ def main():
     hpw = int(os.environ.get("SHD_HPW", "64"))
     grid = (a.hosts + hpw - 1) // hpw
     t = t[:, :grid, :]
+    print(f"ticketless batches {st.n_batches_ticketless}")
     print(f"kernel {st.device_ms_round_kernel / max(st.n_rounds, 1) * 1e3:.1f} us/round (in-kernel stamps), "
           f"wall {st.wall_ms / max(st.n_rounds, 1) * 1e3:.1f} us/round, grid {grid}")
     names = ["entry", "body", "idle-chk", "active", "reduce", "ticket", "resolve"]
@@ -94,6 +96,13 @@ def main():
                        (10, 3, "store ctx")):
         d = (rows[:, :, k1] - rows[:, :, k0])
         print(f"  {nm:15s} per block: mean {d[act].mean():7.2f} max {np.where(act, d, 0).max(axis=1).mean():7.2f} us")
+    if os.environ.get("SHD_TIMING_LIGHT"):
+        fl = (t[keep][:, :, 11] - t[keep][:, :, 0].min(axis=1, keepdims=True)) / 100.0
+        ok = (t[keep][:, :, 11] >= t[keep][:, :, 0].min(axis=1, keepdims=True)) & (rows[:, :, 9] > 0)
+        d = rows[:, :, 9] - fl
+        print(f"  flush (light stamps) per block: mean {d[ok].mean():.2f} max {np.where(ok, d, 0).max(axis=1).mean():.2f} us; "
+              f"flush start mean {fl[ok].mean():.2f}")
+        return
     raw = t[keep][:, :, 11:18].astype(np.float64)
     ok = raw[:, :, 4] > 0
     loopw = rows[:, :, 9] - rows[:, :, 8]   # us (wall) of the event loop

@@ -1969,6 +1969,9 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             KT0(q3)
             if (threadIdx.x == 0) TCNT(6);
             if (st == 2u) TCNT(7);
+#ifdef SHD_TIMING_LIGHT
+            TIM(11);   // the (last) flush starts
+#endif
             flush_wave(P, c);
             KTA(k_fl, q3)
             if (__ballot(st == 2u) == 0) break;
@@ -1977,7 +1980,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     }
     TIM(9);
     if (active) {
-#ifdef SHD_TIMING
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
         {
             uint64_t v[7] = {n_it, k_tk, k_be, k_rw, clock64() - k_l0, k_fl, k_in};
 #pragma unroll
