@@ -166,9 +166,12 @@ def main():
     alg_bytes = BYTES_PER_EVENT * ev_all + BYTES_PER_PKT_EVENT * pkt_all
     avg_launch_ms = (ems_all if ems_all > 0 else kms_all) / max(launches, 1)
     achieved = (alg_bytes / max(launches, 1)) / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    # the dominant kernel: ticketless device rounds on one engine (k_round_tl,
+    # once no first touch is logged), the engine group's k_round_x across GPUs
+    kname = "k_round_x" if use_group else ("k_round" if world > 1 else "k_round_tl")
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(),
-                "kernel": "k_round_dev", "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname),
+                "kernel": kname, "avg_launch_us": round(avg_launch_ms * 1e3, 3),
                 "avg_in_kernel_us": round(kms_all / max(launches, 1) * 1e3, 3),
                 "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1)}
 
@@ -215,7 +218,7 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic():
+def pmc_traffic(kernel):
     """HBM bytes per round-kernel launch from the committed rocprofv3 PMC
     passes (profiles/r01/k_round_pmc_bytes.json: FETCH_SIZE x 2 + WRITE_SIZE,
     the gfx950 correction), used only when that profile was taken of the
@@ -226,7 +229,7 @@ def pmc_traffic():
         src = open(os.path.join(REPO, "shadow-1_amd", "csrc", "engine.hip"), "rb").read()
     except (OSError, ValueError):
         return None
-    if prof.get("engine_source_sha1") != hashlib.sha1(src).hexdigest():
+    if prof.get("engine_source_sha1") != hashlib.sha1(src).hexdigest() or prof.get("kernel") != kernel:
         return None
     return prof.get("hbm_bytes_per_dispatch")
 

@@ -1,0 +1,66 @@
+#!/usr/bin/env python3
+"""HBM bytes per dispatch of the round kernel from the rocprofv3 FETCH_SIZE
+and WRITE_SIZE passes of scripts/profile_round.sh, written as
+profiles/r01/k_round_pmc_bytes.json (read by bench.py's roofline `traffic`
+when the profiled engine source matches the one being run).
+
+    python scripts/pmc_bytes.py gpurun_out/prof_fetch gpurun_out/prof_write [--kernel k_round_tl]
+
+FETCH_SIZE is doubled: gfx950 reports half of the bytes of 16-B-per-lane
+reads (MI355X_MICROARCH.md, HBM / rocprofv3 section); WRITE_SIZE as read.
+Both counters are in KB.
+"""
+import argparse
+import csv
+import glob
+import hashlib
+import json
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(d, counter, kernel):
+    vals = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                    vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--kernel", default="k_round_tl")
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r01", "k_round_pmc_bytes.json"))
+    a = ap.parse_args()
+    fe = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
+    wr = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
+    if not fe or not wr:
+        raise SystemExit(f"no {a.kernel} dispatches with FETCH_SIZE / WRITE_SIZE")
+    f_kb = sum(fe) / len(fe)
+    w_kb = sum(wr) / len(wr)
+    src = open(os.path.join(REPO, "shadow-1_amd", "csrc", "engine.hip"), "rb").read()
+    out = {
+        "kernel": a.kernel,
+        "FETCH_SIZE_KB_avg_per_dispatch": round(f_kb, 3),
+        "FETCH_SIZE_dispatches": len(fe),
+        "WRITE_SIZE_KB_avg_per_dispatch": round(w_kb, 3),
+        "WRITE_SIZE_dispatches": len(wr),
+        "hbm_bytes_per_dispatch": int(round((2 * f_kb + w_kb) * 1024)),
+        "correction": "FETCH_SIZE doubled (gfx950 reports 1/2 of 16-B/lane reads, MI355X_MICROARCH.md "
+                      "HBM/rocprofv3 section); WRITE_SIZE as read",
+        "command": "rocprofv3 --pmc FETCH_SIZE (resp. WRITE_SIZE) -- python3 bench.py --steps 2 --warmup 2 "
+                   "--no-cpu-baseline, separate passes; averaged over every " + a.kernel + " dispatch of the run",
+        "engine_source_sha1": hashlib.sha1(src).hexdigest(),
+    }
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
