@@ -888,7 +888,16 @@ __device__ void worker_send_deferred(const DParams& P, HostCtx& c, uint32_t rv, 
 // round trip each per 64 sends of the wave); then each host walks its own
 // sends in order (event IDs, counters, traces, first-touch logs, LDS only);
 // then record-parallel deliveries (one round trip for the calendar claims).
-__device__ void flush_wave(const DParams& P, HostCtx& c) {
+// a delivery of the round's last flush whose calendar claim is in flight:
+// its store waits until the round's closing work is issued (flush_finish)
+struct PendDel {
+    uint64_t bi;     // bin index
+    uint32_t slot;   // claimed slot (kind 1)
+    uint32_t kind;   // 0 none, 1 calendar claim issued, 2 inbox / remote
+};
+
+__device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool defer, PendDel& pd) {
+    pd.kind = 0;
     const uint32_t lane = threadIdx.x;
     const uint32_t n = c.ns;
     uint32_t pre = n;   // inclusive, then exclusive prefix of the lanes' counts
@@ -997,7 +1006,26 @@ __device__ void flush_wave(const DParams& P, HostCtx& c) {
     c.seq_base = c.ev_seq;
     c.ns = 0;
     __syncthreads();
-    // deliveries: calendar claims for 64 events at a time, then the stores
+    // deliveries: calendar claims for 64 events at a time, then the stores.
+    // The round's last flush (one batch) only issues the claims; the stores
+    // follow the round's closing work, which hides the claims' round trip.
+    if (defer && total <= (uint32_t)kBlock) {
+        if (lane < total) {
+            const shd_event e = s_res[lane];
+            if (e.kind) {
+                const int32_t dl = (int32_t)e.dst - P.h0;
+                const uint64_t bb = e.time >> P.bin_shift;
+                pd.kind = 2;
+                if (P.bins && dl >= 0 && dl < P.nloc && bb - (c.ws >> P.bin_shift) <= kHorizon) {
+                    pd.bi = (size_t)dl * kNB + ((uint32_t)bb & (kNB - 1));
+                    pd.slot = atomicAdd(&P.bin_n[pd.bi], 1u);
+                    pd.kind = 1;
+                }
+            }
+        }
+        c.err |= err;
+        return;   // s_res[lane] stays for flush_finish
+    }
     for (uint32_t base = 0; base < total; base += kBlock) {
         const uint32_t r = base + lane;
         if (r >= total) continue;
@@ -1019,6 +1047,20 @@ __device__ void flush_wave(const DParams& P, HostCtx& c) {
     }
     c.err |= err;
     __syncthreads();   // s_res / s_idx are reused by the next flush
+}
+
+// the stores of the round's last flush (after its claims returned)
+__device__ __forceinline__ void flush_finish(const DParams& P, HostCtx& c, const PendDel& pd) {
+    if (pd.kind == 0) return;
+    const shd_event e = s_res[threadIdx.x];
+    if (pd.kind == 1 && pd.slot < kBinCap) {
+        P.bins[pd.bi * kBinCap + pd.slot] = e;
+        const uint32_t p = (uint32_t)(pd.bi & (kNB - 1));
+        const int32_t dl = (int32_t)e.dst - P.h0;
+        atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));
+        return;
+    }
+    emit_nocal(P, c, e);
 }
 
 // _networkinterface_sendPackets (network_interface.c:519-579), FIFO qdisc.
@@ -1822,6 +1864,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #endif
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
     hot_load(P, c);
+    PendDel pd;
     c.ns = 0; c.att = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
     if (active) {
@@ -1895,6 +1938,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
         // for a flush, 3 is done.  Both loops exit on wave-uniform tests only
         // (no divergent breaks: the exec-mask bookkeeping stays small).
         uint32_t st = active ? 0u : 3u;
+        pd.kind = 0;
         for (;;) {
             KT0(q4)
             for (;;) {
@@ -1972,9 +2016,10 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #ifdef SHD_TIMING_LIGHT
             TIM(11);   // the (last) flush starts
 #endif
-            flush_wave(P, c);
+            const bool last = __ballot(st == 2u) == 0;   // no lane waits to resume: the round's last flush
+            flush_wave(P, c, last, pd);
             KTA(k_fl, q3)
-            if (__ballot(st == 2u) == 0) break;
+            if (last) break;
             if (st == 2u) st = 1u;
         }
     }
@@ -2067,6 +2112,8 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             if (s_kc[i][0])
                 for (int j = 0; j < 4; j++) atomicAdd(&g_kc[i][j], s_kc[i][j]);
 #endif
+    flush_finish(P, c, pd);
+    err |= c.err;
     TIM(3);
     next_out = next; nev_out = nev; npkt_out = npkt; err_out = err;
 }
