@@ -1719,6 +1719,19 @@ __device__ __forceinline__ int32_t lane_host(const DParams& P) {
     return (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
 }
 
+// One scalar load per 64-B line of the Params copy, issued at kernel entry
+// with the other first loads; consumed (params_warm_done) where the kernel
+// waits for its window start anyway.  The round's later scalar loads of
+// Params fields then hit the scalar cache instead of each paying an L2 trip.
+__device__ __forceinline__ uint32_t params_warm(const DParams* Pp) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(Pp);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < (int)((sizeof(DParams) + 63) / 64); k++) acc ^= w[k * 16];
+    return acc;
+}
+__device__ __forceinline__ void params_warm_done(uint32_t acc) { asm volatile("" ::"s"(acc)); }
+
 // what a round reads of a host before it knows the window: both inbox
 // counts, the earliest timer/heap time, the calendar bitmap, the host record,
 // its attached vertex and loopback thresholds.  None of it depends on the
@@ -2311,6 +2324,18 @@ __device__ __forceinline__ TlPart tl_gather(const TlPart* __restrict__ parts, ui
     }
     return f;
 }
+__device__ __forceinline__ uint64_t tl_gather_next(const TlPart* __restrict__ parts, uint32_t n) {
+    uint64_t m = kInf;
+    for (uint32_t j = threadIdx.x; j < n; j += 64) {
+        const uint64_t v = parts[j].next;
+        m = v < m ? v : m;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(m, off, 64);
+        m = o < m ? o : m;
+    }
+    return m;
+}
 // publish a round's fold into its summary; a round that logged first touches
 // halts the batch (the host resolves its log)
 __device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint32_t* halt) {
@@ -2323,24 +2348,36 @@ __device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint3
 }
 
 // round i of a ticketless batch: shares of round i go to parts[i & 1]
-__global__ __launch_bounds__(kBlock) void k_round_tl(DRoundArgs a, DevSummary* __restrict__ prev,
-                                                      const DevCtl* __restrict__ ctl,
+// (argument order: what the first memory round trip needs comes first, so
+// that one scalar load batch brings all of it)
+__global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, DevSummary* __restrict__ prev,
+                                                      const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
                                                       const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
-                                                      TlPart* __restrict__ parts, int i, uint64_t window) {
+                                                      DRoundArgs a) {
     const DParams& P = *Pp;
 #ifdef SHD_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
-    const uint32_t nblk = gridDim.x;
+    const uint32_t nblk = (uint32_t)((a.nloc + a.hpw - 1) / a.hpw);   // == gridDim.x, without the dispatch-packet load
+    // all scalar arguments in the first load batch (the compiler otherwise
+    // fetches these after the host-state loads are issued, one level later)
+    asm volatile("" ::"s"(i), "s"(prev), "s"(ctl), "s"(parts));
+    const uint32_t warm = params_warm(Pp);
     HostIn in;
     host_in_load(a, in);
     // round 0 of the batch starts at the seeded time; later rounds fold the
     // previous round's shares (its first-touch log count halts)
-    TlPart f{kInf, 0, 0, 0, 0, 0};
-    if (i > 0) f = tl_gather(parts + (size_t)((i - 1) & 1) * nblk, nblk);
     const uint32_t halt = *a.halt;
     const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws0 = prev->next_time, npend = prev->n_pending;
+    // every block needs the shares' min next time; block 0 folds the rest
+    // of them too, for the summary
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    if (i > 0) {
+        if (blockIdx.x == 0) f = tl_gather(parts + (size_t)((i - 1) & 1) * nblk, nblk);
+        else f.next = tl_gather_next(parts + (size_t)((i - 1) & 1) * nblk, nblk);
+    }
     const uint64_t ws = f.next < ws0 ? f.next : ws0;
+    params_warm_done(warm);
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     if (lead && i > 0) tl_publish(prev, f, (uint32_t*)a.halt);
     TlPart* mine = parts + (size_t)(i & 1) * nblk + blockIdx.x;
@@ -3101,9 +3138,9 @@ static int enqueue_batch_tl(shd_eng* e) {
     constexpr int B = shd_eng::kBatch;
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     for (int i = 0; i < B; i++) {
-        hipLaunchKernelGGL(k_round_tl, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P), &e->d_ring[i],
-                           (const DevCtl*)e->d_ctl, (const DParams*)(e->d_pr + i + 1), &e->d_ring[i + 2],
-                           e->d_tpart, i, e->window);
+        hipLaunchKernelGGL(k_round_tl, dim3(grid), dim3(kBlock), 0, e->stream, e->window, i, &e->d_ring[i],
+                           (const DevCtl*)e->d_ctl, e->d_tpart, (const DParams*)(e->d_pr + i + 1), &e->d_ring[i + 2],
+                           round_args(e->P));
     }
     hipLaunchKernelGGL(k_fold_tl, dim3(1), dim3(64), 0, e->stream, (const TlPart*)e->d_tpart, (uint32_t)grid, B - 1,
                        &e->d_ring[B], e->d_halt);
