@@ -102,6 +102,16 @@ def main():
         d = rows[:, :, 9] - fl
         print(f"  flush (light stamps) per block: mean {d[ok].mean():.2f} max {np.where(ok, d, 0).max(axis=1).mean():.2f} us; "
               f"flush start mean {fl[ok].mean():.2f}")
+        t0 = t[keep][:, :, 0].min(axis=1, keepdims=True)
+        prev = fl
+        for k, nm in ((12, "prefix + index"), (13, "resolve (path loads)"), (14, "per-host walk")):
+            x = (t[keep][:, :, k] - t0) / 100.0
+            okk = ok & (t[keep][:, :, k] >= t0)
+            dd = x - prev
+            print(f"    {nm:22s} mean {dd[okk].mean():.2f} max {np.where(okk, dd, 0).max(axis=1).mean():.2f} us")
+            prev = x
+        dd = rows[:, :, 9] - prev
+        print(f"    {'claims issue':22s} mean {dd[ok].mean():.2f} us")
         return
     raw = t[keep][:, :, 11:18].astype(np.float64)
     ok = raw[:, :, 4] > 0

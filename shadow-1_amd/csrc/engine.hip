@@ -770,6 +770,33 @@ __device__ __forceinline__ void path_load(const DParams& P, int32_t a, int32_t b
     }
 }
 
+// the same candidates for the flush, every load unconditional (indices of
+// tables the mode does not use point at entry 0): no branch between loads,
+// so all of them are in flight together (one memory round trip).  The
+// direct-edge table and the rank arrays are always allocated; row falls
+// back to dir when there are no rows (complete graphs, which never use it)
+__device__ __forceinline__ void path_load_flat(const DParams& P, int32_t a, int32_t b, PathRaw& x) {
+    const size_t ab = (size_t)a * P.T + b, ba = (size_t)b * P.T + a;
+    const bool use_dir = P.complete || P.prefer_direct, use_rows = !P.complete;
+    const size_t i_d = use_dir ? ab : 0, i_ab = use_rows ? ab : 0, i_ba = use_rows ? ba : 0;
+    const shd_pv* rowp = P.row ? (const shd_pv*)P.row : (const shd_pv*)P.dir;
+    shd_pv d = P.dir[i_d];
+    uint32_t adj = P.adj[i_d];
+    shd_pv v1 = rowp[i_ab], v2 = rowp[i_ba], vs = P.self[a];
+    int32_t rb = P.rank[b], rs = P.self_rank[a];
+    // consumed here, all together: left to the compiler, each load would be
+    // sunk into the branch of path_select that uses it, one round trip each
+    d.lat = launder(d.lat); d.rel = launder(d.rel); adj = launder(adj);
+    v1.lat = launder(v1.lat); v1.rel = launder(v1.rel); v2.lat = launder(v2.lat); v2.rel = launder(v2.rel);
+    vs.lat = launder(vs.lat); vs.rel = launder(vs.rel); rb = launder(rb); rs = launder(rs);
+    x.d = d;
+    x.adj = P.prefer_direct ? adj : 0u;
+    x.v1 = v1;
+    x.v2 = a == b ? vs : v2;
+    x.rb = a == b ? kNoRank : rb;
+    x.rs = a == b ? rs : kNoRank;
+}
+
 __device__ __forceinline__ PathVal path_select(const DParams& P, int32_t a, int32_t b, int32_t ra, const PathRaw& x) {
     PathVal v;
     v.resolved = true;
@@ -911,6 +938,9 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     for (uint32_t i = 0; i < n; i++) s_idx[pre + i] = (uint16_t)((lane << 4) | i);
     s_att[lane] = c.att;
     __syncthreads();
+#ifdef SHD_TIMING_LIGHT
+    TIM(12);
+#endif
     uint32_t err = 0;
     for (uint32_t base = 0; base < total; base += kBlock) {
         const uint32_t r = base + lane;
@@ -924,7 +954,9 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             const uint64_t nx = (uint64_t)q.r * (uint64_t)(uint32_t)P.H;
             const uint64_t cx = (nx + 2147483646ull) / 2147483647ull;
             int32_t d = cx ? (int32_t)cx - 1 : 0;
-            for (int j = 0; j < P.n_exc; j++) d = (int32_t)q.r == P.exc_x[j] ? P.exc_d[j] : d;
+#pragma unroll
+            for (int j = 0; j < kDestExc; j++)   // unrolled: the list is read in one scalar batch
+                d = (j < P.n_exc && (int32_t)q.r == P.exc_x[j]) ? P.exc_d[j] : d;
             dst = d;
             b = d;
         } else {
@@ -934,8 +966,10 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             guide_pick(P, g0, g1, g2, rr, dst, b);
         }
         PathRaw x;
-        const int32_t ra = P.complete ? kNoRank : P.rank[a];
-        path_load(P, a, b, x);
+        int32_t ra_l = P.rank[a];
+        path_load_flat(P, a, b, x);
+        ra_l = launder(ra_l);
+        const int32_t ra = P.complete ? kNoRank : ra_l;
         const PathVal pv = path_select(P, a, b, ra, x);
         const double chance = (double)q.chance / kRandMax;
         const bool boot = (q.q_sub >> 31) != 0;
@@ -954,6 +988,9 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         s_res[r] = e;
     }
     __syncthreads();
+#ifdef SHD_TIMING_LIGHT
+    TIM(13);
+#endif
     // per host, in send order (worker.c:286-320)
     uint32_t failmask = 0, nfail = 0;
     for (uint32_t i = 0; i < n; i++) {
@@ -1006,6 +1043,9 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     c.seq_base = c.ev_seq;
     c.ns = 0;
     __syncthreads();
+#ifdef SHD_TIMING_LIGHT
+    TIM(14);
+#endif
     // deliveries: calendar claims for 64 events at a time, then the stores.
     // The round's last flush (one batch) only issues the claims; the stores
     // follow the round's closing work, which hides the claims' round trip.
