@@ -935,6 +935,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     const uint32_t total = __shfl(pre, 63, 64);
     pre -= n;
     if (total == 0) return;
+    const bool one = defer && total <= (uint32_t)kBlock;   // the round's last flush, one batch
     for (uint32_t i = 0; i < n; i++) s_idx[pre + i] = (uint16_t)((lane << 4) | i);
     s_att[lane] = c.att;
     __syncthreads();
@@ -986,6 +987,19 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         e.pkt = 0;
         e.kind = (pass ? 1u : 0u) | (pv.log ? 2u : 0u) | (pv.resolved ? 4u : 0u);
         s_res[r] = e;
+        // the round's last flush (one batch: record r is lane r's): the
+        // calendar claim goes out now, under the per-host walk and the
+        // round's closing work; the store follows in flush_finish
+        if (one && pass && pv.resolved && e.time < c.k.end_time) {
+            const int32_t dl = (int32_t)dst - P.h0;
+            const uint64_t bb = e.time >> P.bin_shift;
+            pd.kind = 2;
+            if (P.bins && dl >= 0 && dl < P.nloc && bb - (c.ws >> P.bin_shift) <= kHorizon) {
+                pd.bi = (size_t)dl * kNB + ((uint32_t)bb & (kNB - 1));
+                pd.slot = atomicAdd(&P.bin_n[pd.bi], 1u);
+                pd.kind = 1;
+            }
+        }
     }
     __syncthreads();
 #ifdef SHD_TIMING_LIGHT
@@ -1049,20 +1063,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     // deliveries: calendar claims for 64 events at a time, then the stores.
     // The round's last flush (one batch) only issues the claims; the stores
     // follow the round's closing work, which hides the claims' round trip.
-    if (defer && total <= (uint32_t)kBlock) {
-        if (lane < total) {
-            const shd_event e = s_res[lane];
-            if (e.kind) {
-                const int32_t dl = (int32_t)e.dst - P.h0;
-                const uint64_t bb = e.time >> P.bin_shift;
-                pd.kind = 2;
-                if (P.bins && dl >= 0 && dl < P.nloc && bb - (c.ws >> P.bin_shift) <= kHorizon) {
-                    pd.bi = (size_t)dl * kNB + ((uint32_t)bb & (kNB - 1));
-                    pd.slot = atomicAdd(&P.bin_n[pd.bi], 1u);
-                    pd.kind = 1;
-                }
-            }
-        }
+    if (one) {   // claims already issued in the resolve loop
         c.err |= err;
         return;   // s_res[lane] stays for flush_finish
     }
