@@ -2399,6 +2399,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
 #ifdef SHD_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
+    const unsigned long long t_entry = wall_clock64();   // the round's start on the device clock (t_first)
     const uint32_t nblk = (uint32_t)((a.nloc + a.hpw - 1) / a.hpw);   // == gridDim.x, without the dispatch-packet load
     // all scalar arguments in the first load batch (the compiler otherwise
     // fetches these after the host-state loads are issued, one level later)
@@ -2425,7 +2426,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
     if ((halt != 0) | (i > 0 && npend != 0) | (ws >= stop)) {
         if (halt == 0 && !(i > 0 && npend != 0)) {   // only forwards the time
             if (lead) {
-                atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+                atomicMin(&P.sum->t_first, t_entry);
                 *init = fresh_summary();
                 P.sum->ws = ws;
             }
@@ -2434,7 +2435,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
         return;
     }
     if (lead) {
-        atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+        atomicMin(&P.sum->t_first, t_entry);
         *init = fresh_summary();
         P.sum->ws = ws;
     }
