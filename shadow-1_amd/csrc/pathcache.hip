@@ -90,23 +90,46 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     if (tid == 0) { dist[src] = 0; upd[src] = 0; }
     __syncthreads();
 
-    // ---- frontier Bellman-Ford: vertices improved in iteration `it` relax in it+1
+    // ---- frontier Bellman-Ford: vertices improved in iteration `it` relax in it+1.
+    // Wave-cooperative: a wave ballots a 64-vertex chunk for frontier vertices
+    // (their arc ranges loaded by their own lanes in one batch), then each
+    // half-wave relaxes one frontier vertex's out-arcs, 32 arcs per load round,
+    // instead of one lane walking ~20 arcs with a dependent L2 load per arc.
+    // Any relaxation order reaches the same fixpoint: d[x] = min over paths of
+    // the left-folded sum (fl(a + w) is monotone in a).
+    const int lane = tid & 63, wv = tid >> 6, hl = lane & 31;
+    const bool upper = lane >= 32;
     int it = 0;
     for (;;) {
         if (tid == 0) flags[(it + 1) % 3] = 0;
         const uint16_t stamp = (uint16_t)it;
-        for (int32_t v = tid; v < V; v += BLOCK) {
-            if (upd[v] != stamp) continue;
-            const double dv = u2d(dist[v]);
-            const int32_t k1 = arc_off[v + 1];
-            for (int32_t k = arc_off[v]; k < k1; k++) {
-                const int32_t x = arc_dst[k];
-                const uint64_t nb = d2u(dv + arc_w[k]);
-                if (nb < dist[x]) {
-                    const uint64_t old = atomicMin((unsigned long long*)&dist[x], (unsigned long long)nb);
-                    if (nb < old) {
-                        upd[x] = (uint16_t)(it + 1);
-                        flags[it % 3] = 1;
+        for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
+            const int32_t v = c0 + lane;
+            const bool fr = v < V && upd[v] == stamp;
+            uint64_t mask = __ballot(fr);
+            if (!mask) continue;
+            int32_t beg = 0, end = 0;
+            uint64_t dvb = 0;
+            if (fr) { beg = arc_off[v]; end = arc_off[v + 1]; dvb = dist[v]; }
+            while (mask) {
+                const int l0 = __ffsll((unsigned long long)mask) - 1;
+                mask &= mask - 1;
+                const int l1 = mask ? __ffsll((unsigned long long)mask) - 1 : l0;
+                if (mask) mask &= mask - 1;
+                const int src_lane = upper ? l1 : l0;
+                // every lane takes part in every shuffle (an inactive source lane reads as 0)
+                const int32_t b = __shfl(beg, src_lane), e_all = __shfl(end, src_lane);
+                const int32_t e = (upper && l1 == l0) ? b : e_all;
+                const double dv = u2d((uint64_t)__shfl((long long)dvb, src_lane));
+                for (int32_t k = b + hl; k < e; k += 32) {
+                    const int32_t x = arc_dst[k];
+                    const uint64_t nb = d2u(dv + arc_w[k]);
+                    if (nb < dist[x]) {
+                        const uint64_t old = atomicMin((unsigned long long*)&dist[x], (unsigned long long)nb);
+                        if (nb < old) {
+                            upd[x] = (uint16_t)(it + 1);
+                            flags[it % 3] = 1;
+                        }
                     }
                 }
             }
@@ -117,8 +140,15 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         if (!more || it >= 0xFFFE) break;
     }
 
+#if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 1   // phase ablation (scripts/apsp_phases.sh)
+    __syncthreads();
+    return;
+#endif
     // ---- parent per vertex: smallest d[u] among exact predecessors; equal d[u]
     // (a tie Dijkstra breaks by heap order, unpinned) -> lowest edge id
+    // Lane per vertex (a half-wave-per-vertex version with shuffle reductions
+    // measured slower: 20 ms against 12.5 ms for the 10k-row table, since each
+    // wave then waits on two dependent L2 round trips per vertex pair)
     int64_t my_ties = 0;
     for (int32_t v = tid; v < V; v += BLOCK) {
         if (v == src) continue;
@@ -147,14 +177,25 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     if (tid == 0) atomicMax((unsigned long long*)&stats[2], (unsigned long long)it);
     __syncthreads();
 
-    // ---- properties per target: forward fold along the parent chain
+#if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 2
+    return;
+#endif
+    // ---- properties per target (topology.c:1407-1523).
+    // lat: the forward fold w1 + w2 + ... along the parent chain is the very
+    // relaxation that set dist[t] (the parent satisfies d[u] + w == d[t] with
+    // final values), so lat == dist[t] bit for bit.
+    // rel: ((1 * r(src)) * r(dst)) * r(e1) * r(e2) ...; for a target without a
+    // vertex factor that is the prefix P[t] = P[u] * r(e) over the tree,
+    // P[src] = 1 * r(src), computed level by level in LDS.  Targets with a
+    // vertex loss factor walk their chain (the factor enters second).
     double rsrc = 1.0;
     const bool has_rsrc = vrel(vloss, src, &rsrc);
     int32_t my_maxhops = 0;
     int64_t my_unroutable = 0, my_mismatch = 0;
+    // (1) special targets in full, lat half of the others
     for (int32_t j = tid; j < T; j += BLOCK) {
         const int32_t t = attached[j];
-        double lat, rel;
+        double lat, rel, rt;
         if (t == src) {
             // igraph 0.7.1 returns the path [src]: the self-loop edge alone, no
             // destination factor (topology.c:1456-1508)
@@ -169,12 +210,10 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             }
         } else if (dist[t] == kDistInf) {
             lat = -1.0; rel = -1.0; my_unroutable++;
-        } else {
+        } else if (vrel(vloss, t, &rt)) {
             rel = 1.0;
             if (has_rsrc) rel *= rsrc;
-            double rt;
-            if (vrel(vloss, t, &rt)) rel *= rt;
-            // hop count
+            rel *= rt;
             int32_t k = 0;
             for (int32_t v = t; v != src; v = rin_src[parent[v]]) k++;
             if (k > my_maxhops) my_maxhops = k;
@@ -197,8 +236,55 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             }
             if (d2u(lat) != dist[t]) my_mismatch++;
             if (lat == 0) lat = 1;   // topology.c:1848-1852
+        } else {
+            lat = u2d(dist[t]);
+            if (lat == 0) lat = 1;
+            out[(size_t)row * T + j].lat = lat;
+            continue;
         }
         out[(size_t)row * T + j] = shd_pv{lat, rel};
+    }
+    __syncthreads();
+    // (2) tree arrays: parent[v] <- parent vertex, dist[v] <- edge factor r(e)
+    constexpr uint16_t kTodo = 0xFFFF, kNever = 0xFFFE;
+    for (int32_t v = tid; v < V; v += BLOCK) {
+        if (v == src) {
+            dist[v] = d2u(has_rsrc ? 1.0 * rsrc : 1.0);
+            upd[v] = 0;
+        } else if (dist[v] != kDistInf && parent[v] >= 0) {
+            const int32_t a = parent[v];
+            parent[v] = rin_src[a];
+            dist[v] = d2u((double)1.0f - eloss[rin_eid[a]]);
+            upd[v] = kTodo;
+        } else {
+            upd[v] = kNever;
+        }
+    }
+    __syncthreads();
+    // (3) level passes: a vertex whose parent finished in an earlier level
+    // finishes now (reads of this level's writes see kTodo or lvl: no race)
+    for (int lvl = 1; lvl < (int)kNever; lvl++) {
+        if (tid == 0) flags[lvl % 3] = 0;
+        __syncthreads();
+        for (int32_t v = tid; v < V; v += BLOCK) {
+            if (upd[v] != kTodo) continue;
+            const int32_t u = parent[v];
+            if (upd[u] >= (uint16_t)lvl) continue;
+            dist[v] = d2u(u2d(dist[u]) * u2d(dist[v]));
+            upd[v] = (uint16_t)lvl;
+            flags[lvl % 3] = 1;
+        }
+        __syncthreads();
+        if (!flags[lvl % 3]) break;
+    }
+    // (4) rel half of the prefix targets
+    for (int32_t j = tid; j < T; j += BLOCK) {
+        const int32_t t = attached[j];
+        if (t == src || upd[t] >= kNever) continue;
+        double rt;
+        if (vrel(vloss, t, &rt)) continue;
+        out[(size_t)row * T + j].rel = u2d(dist[t]);
+        if ((int32_t)upd[t] > my_maxhops) my_maxhops = upd[t];
     }
     if (my_maxhops) atomicMax((unsigned long long*)&stats[1], (unsigned long long)my_maxhops);
     if (my_unroutable) atomicAdd((unsigned long long*)&stats[3], (unsigned long long)my_unroutable);

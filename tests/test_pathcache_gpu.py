@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+import shdgpu as S
 import workloads as W
 from pc_helpers import PathCache, same_bits
 
@@ -61,9 +62,16 @@ def test_bundled_forced_rows_bit_exact():
     assert int(np.sum(np.triu(lat < dl, 1))) == 737
 
 
-@pytest.mark.parametrize("V,seed", [(2000, 11), (3000, 5)])
-def test_geometric_rows_bit_exact(V, seed):
-    g = W.geometric_graph(V, seed=seed, vertex_loss=True)
+@pytest.mark.parametrize("V,seed,vloss", [(2000, 11, "all"), (3000, 5, "all"), (3000, 5, "none"),
+                                           (2500, 3, "mixed"), (10000, 1, "none")])
+def test_geometric_rows_bit_exact(V, seed, vloss):
+    # "none": every target takes the tree-prefix reliability; "all": every
+    # target has a vertex factor and walks its chain; "mixed": both in one row
+    g = W.geometric_graph(V, seed=seed, vertex_loss=vloss != "none")
+    if vloss == "mixed":
+        vl = g.vertex_loss.copy()
+        vl[::2] = np.nan          # attribute absent on even vertices
+        g = S.GraphArrays(V, g.src, g.dst, g.latency, g.loss, vl)
     att = np.arange(V, dtype=np.int32)
     pc = PathCache(g, att)
     info = pc.info()
