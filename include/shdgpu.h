@@ -324,6 +324,10 @@ typedef struct shd_run_stats {
     uint32_t error;
     uint32_t n_batches_ticketless;  /* device batches run without the completion ticket
                                        (no first touch logged in the batch before) */
+    uint32_t n_rounds_protected;    /* rounds run one at a time behind a state copy (they
+                                       could log many first touches) */
+    uint32_t n_rounds_rerun;        /* protected rounds rolled back and rerun after an
+                                       ambiguous first-touch drop decision */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

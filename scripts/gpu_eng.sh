@@ -1,0 +1,8 @@
+#!/bin/bash
+# engine parity tests (GPU), then the default bench
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1 || { tail -40 gpurun_out/t.log; exit 1; }
+tail -3 gpurun_out/t.log
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 2; }
+cat gpurun_out/bench.json

@@ -222,6 +222,7 @@ struct ParamsT {
     // except at the listed draws (where the f64 cumulative sums round across
     // a threshold); verified on the host at every step of both functions
     int32_t dest_closed, n_exc;
+    int32_t force_ambig;        // test hook (SHD_FORCE_AMBIG): every undecided first-touch send is ambiguous
     int32_t exc_x[kDestExc], exc_d[kDestExc];
     // path cache
     int32_t T;
@@ -977,7 +978,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         const bool pass = boot || chance <= pv.rel || P.payload == 0;
         if (!pv.resolved) {
             const bool pass2 = boot || chance <= pv.rel2 || P.payload == 0;
-            if (pass != pass2) err |= SHD_ERR_AMBIGUOUS;
+            if (pass != pass2 || P.force_ambig) err |= SHD_ERR_AMBIGUOUS;
         }
         shd_event e;
         e.time = q.now + (uint64_t)ceil(pv.lat * (double)SHD_MS);
@@ -2653,6 +2654,14 @@ struct shd_eng {
     int parity = 0;
     bool booted = false;
     std::vector<void*> allocs;
+    std::vector<size_t> alloc_bytes;
+    // protected rounds (DESIGN.md "First-touch rule"): device state copied
+    // before a round that may log many first touches, restored when one of its
+    // drop decisions turns out ambiguous, then the round reruns with the ranks
+    std::vector<void*> snap;
+    bool snap_failed = false;
+    bool logged_any = false;                // a round has logged a first touch
+    uint64_t last_logged = 0;               // first touches logged by the last round
     // inputs kept on device
     uint32_t* d_rng0 = nullptr;
     uint64_t* d_bwd = nullptr;
@@ -2714,6 +2723,7 @@ static int ealloc(shd_eng* e, T** p, size_t n, bool zero = true) {
     void* q = nullptr;
     SHD_HIP(hipMalloc(&q, sizeof(T) * (n ? n : 1)));
     e->allocs.push_back(q);
+    e->alloc_bytes.push_back(sizeof(T) * (n ? n : 1));
     if (zero) SHD_HIP(hipMemsetAsync(q, 0, sizeof(T) * (n ? n : 1), e->stream));
     *p = (T*)q;
     return SHD_OK;
@@ -2767,6 +2777,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
     P.app_start = m->app_start; P.load = m->load; P.payload = m->payload; P.trace = m->trace;
     P.pkt_len = m->payload + SHD_HEADER_UDP;
+    P.force_ambig = getenv("SHD_FORCE_AMBIG") != nullptr;
     const size_t n = (size_t)e->nloc;
     EALLOC(P.hs, n);
     EALLOC(P.hc, n);
@@ -3090,11 +3101,9 @@ extern "C" int shd_eng_pending_copy(shd_eng* e, shd_pending* out, uint64_t cap, 
     return SHD_OK;
 }
 
-extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_all) {
-    if (!e || (n_all && !all)) return SHD_EINVAL;
-    if (!n_all) return SHD_OK;
-    SHD_HIP(hipSetDevice(e->device));
-    // the device is the source of truth for ranks (k_resolve_dev assigns them too)
+// row ranks for a round's first-touch log, in serial order (the device holds
+// the ranks; they are read, extended and written back)
+static int assign_ranks(shd_eng* e, const shd_pending* all, uint64_t n_all) {
     SHD_HIP(hipMemcpyAsync(e->h_rank.data(), e->d_rank, 4 * (size_t)e->pc->T, hipMemcpyDeviceToHost, e->stream));
     SHD_HIP(hipMemcpyAsync(e->h_self_rank.data(), e->d_self_rank, 4 * (size_t)e->pc->T, hipMemcpyDeviceToHost,
                            e->stream));
@@ -3118,6 +3127,16 @@ extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_al
     SHD_HIP(hipMemcpyAsync(e->d_rank, e->h_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
     SHD_HIP(hipMemcpyAsync(e->d_self_rank, e->h_self_rank.data(), 4 * (size_t)T, hipMemcpyHostToDevice, e->stream));
     SHD_HIP(hipMemcpyAsync(e->d_next_rank, &e->next_rank, 4, hipMemcpyHostToDevice, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_all) {
+    if (!e || (n_all && !all)) return SHD_EINVAL;
+    if (!n_all) return SHD_OK;
+    SHD_HIP(hipSetDevice(e->device));
+    int rc = assign_ranks(e, all, n_all);
+    if (rc) return rc;
     const uint32_t n = (uint32_t)e->round_pending;
     if (n) {
         hipLaunchKernelGGL(k_finalize, dim3((n + 255) / 256), dim3(256), 0, e->stream, dp(e->P),
@@ -3209,6 +3228,86 @@ static int launch_batch(shd_eng* e, bool tl) {
     return SHD_OK;
 }
 
+// ---- protected rounds.  A first-touch send whose drop decision differs
+// under the two candidate rows cannot be decided before the round's log is
+// ranked (probability ~3.5e-7 per logged send on the bench graph: it fired
+// at 1M hosts, 16M sends logged at the application start).  Rounds that may
+// log many first touches -- every round until one has logged, and the round
+// after one that logged kProtectMin or more -- run one at a time behind a
+// copy of the engine's device state; an ambiguous round is rolled back,
+// ranked from its own log (the log does not depend on the decisions: queries
+// come from the RNG stream, and the drop decision only moves event IDs), and
+// rerun, now with no undecided send.
+static constexpr uint64_t kProtectMin = 64;
+
+static bool protect_all() { return getenv("SHD_PROTECT_ALL") != nullptr; }
+static bool protect_off() { return getenv("SHD_NO_PROTECT") != nullptr; }
+
+static int snapshot_state(shd_eng* e, bool restore) {
+    if (!restore && e->snap.size() != e->allocs.size()) {
+        for (size_t i = e->snap.size(); i < e->allocs.size(); i++) {
+            void* q = nullptr;
+            if (hipMalloc(&q, e->alloc_bytes[i]) != hipSuccess) {
+                (void)hipGetLastError();
+                for (void* p : e->snap) (void)hipFree(p);
+                e->snap.clear();
+                e->snap_failed = true;
+                fprintf(stderr, "libshdgpu: no memory for the protected-round state copy; "
+                                "rounds run unprotected (an ambiguous first touch fails the run)\n");
+                return SHD_ENOMEM;
+            }
+            e->snap.push_back(q);
+        }
+    }
+    for (size_t i = 0; i < e->allocs.size(); i++) {
+        void* dst = restore ? e->allocs[i] : e->snap[i];
+        const void* src = restore ? e->snap[i] : e->allocs[i];
+        SHD_HIP(hipMemcpyAsync(dst, src, e->alloc_bytes[i], hipMemcpyDeviceToDevice, e->stream));
+    }
+    return SHD_OK;
+}
+
+static bool want_protect(const shd_eng* e) {
+    if (protect_off() || e->snap_failed) return false;
+    return protect_all() || !e->logged_any || e->last_logged >= kProtectMin;
+}
+
+// one protected round [ws, we) (host-driven, k_round); returns its summary
+static int protected_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out, uint32_t* reruns) {
+    int rc = snapshot_state(e, false);
+    if (rc == SHD_ENOMEM) return shd_eng_run_round(e, ws, we, out);
+    if (rc) return rc;
+    const int parity0 = e->parity;
+    const uint64_t round0 = e->round;
+    const DevSummary sum0 = *e->h_sum;
+    if ((rc = shd_eng_round_kernel(e, ws, we, nullptr))) return rc;
+    if ((e->h_sum->error & SHD_ERR_AMBIGUOUS) && !(e->h_sum->error & ~(uint32_t)SHD_ERR_AMBIGUOUS) &&
+        e->round_pending && e->round_pending <= e->P.pend_cap) {
+        std::vector<shd_pending> recs(e->round_pending);
+        uint64_t n = 0;
+        if ((rc = shd_eng_pending_copy(e, recs.data(), recs.size(), &n))) return rc;
+        // roll back, keep nothing of the round but the ranks of its log
+        if ((rc = snapshot_state(e, true))) return rc;
+        e->parity = parity0;
+        e->round = round0;
+        *e->h_sum = sum0;
+        if ((rc = assign_ranks(e, recs.data(), n))) return rc;
+        (*reruns)++;
+        if ((rc = shd_eng_round_kernel(e, ws, we, nullptr))) return rc;
+        if (e->round_pending) {   // every pair of the log is ranked now
+            e->h_sum->error |= SHD_ERR_INTERNAL;
+            return shd_eng_end_round(e, out);
+        }
+    }
+    if (e->round_pending) {
+        std::vector<shd_pending> recs(e->round_pending);
+        uint64_t n = 0;
+        if ((rc = shd_eng_pending_copy(e, recs.data(), recs.size(), &n))) return rc;
+        if ((rc = shd_eng_resolve(e, recs.data(), n))) return rc;
+    }
+    return shd_eng_end_round(e, out);
+}
+
 extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;
     auto t0 = std::chrono::steady_clock::now();
@@ -3224,6 +3323,25 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     constexpr int B = shd_eng::kBatch, R = shd_eng::kRing;
     static_assert(R >= B + 2, "summary ring");
     while (next < stop && rc == SHD_OK) {
+        if (want_protect(e)) {
+            uint64_t we = next + e->window;
+            if (we > stop || we < next) we = stop;
+            shd_round_summary r{};
+            const uint64_t pend_before = e->pending_resolved;
+            rc = protected_round(e, next, we, &r, &s.n_rounds_rerun);
+            s.n_rounds_protected++;
+            if (rc && rc != SHD_EAMBIG && rc != SHD_EOVERFLOW) break;
+            s.n_rounds++;
+            s.n_events += r.n_events;
+            s.n_pkt_events += r.n_pkt_events;
+            s.final_time = we;
+            if (r.error) { s.error = r.error; break; }
+            e->last_logged = e->pending_resolved - pend_before;
+            if (e->last_logged) e->logged_any = true;
+            e->tl_ready = e->last_logged == 0;
+            next = r.next_time;
+            continue;
+        }
         // slot 0 carries the window start; rounds use slots 1..B
         e->h_seed[0] = host_fresh_summary();
         e->h_seed[0].next_time = next;
@@ -3282,11 +3400,15 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
                     break;
                 }
                 e->parity = saved_parity;
+                e->last_logged = r.n_pending;
+                e->logged_any = true;
                 next = e->h_sum->next_time;
                 if (e->h_sum->error) { s.error = e->h_sum->error; rc = SHD_EOVERFLOW; }
                 break;
             }
             if (r.n_pending) e->pending_resolved += r.n_pending;
+            e->last_logged = r.n_pending;
+            if (r.n_pending) e->logged_any = true;
             if (r.error) {
                 s.error = r.error;
                 rc = (r.error & SHD_ERR_AMBIGUOUS) ? SHD_EAMBIG : SHD_EOVERFLOW;

@@ -55,6 +55,34 @@ def test_geometric_one_host_per_vertex(queue_flags, closed, monkeypatch):
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_INET_DROP) > 0  # reliability drops
 
 
+@pytest.mark.parametrize("hpv", [1, 3])
+def test_ambiguous_first_touch_rounds_roll_back(hpv, monkeypatch):
+    # SHD_FORCE_AMBIG: every undecided first-touch send counts as ambiguous, so
+    # every round that logs one is rolled back to its state copy, ranked from
+    # its own log and rerun (SHD_PROTECT_ALL: every round behind a copy); the
+    # run must still be the serial oracle's, bit for bit
+    monkeypatch.setenv("SHD_FORCE_AMBIG", "1")
+    monkeypatch.setenv("SHD_PROTECT_ALL", "1")
+    g = W.geometric_graph(200, seed=4)
+    m = W.phold_model(W.hosts_on_vertices(200, hpv), end_time=3 * S.SHD_SEC, trace=True)
+    gpu, ora, eng, _ = run_both(g, m)
+    assert_same(gpu, ora)
+    st = gpu[2]
+    assert st.n_rounds_rerun > 0 and st.n_rounds_protected == st.n_rounds
+
+
+def test_default_protection_covers_the_application_start():
+    # without the hook: the rounds up to the first logging one, and those after
+    # a round that logged >= 64 first touches, run behind a state copy
+    g = W.geometric_graph(300, seed=2)
+    m = W.phold_model(W.hosts_on_vertices(300, 1), end_time=3 * S.SHD_SEC, trace=True)
+    gpu, ora, eng, _ = run_both(g, m)
+    assert_same(gpu, ora)
+    st = gpu[2]
+    assert 0 < st.n_rounds_protected < st.n_rounds and st.n_rounds_rerun == 0
+    assert st.n_batches_ticketless > 0
+
+
 def test_bundled_complete_graph_many_hosts_per_vertex():
     g = W.bundled_graph()
     rng = np.random.default_rng(0)
