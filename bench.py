@@ -128,7 +128,7 @@ def main():
 
     # warmup
     tw = time.perf_counter()
-    run(args.warmup * step)
+    wst = run(args.warmup * step)
     torch.cuda.synchronize()
     log(rank, f"warmup {time.perf_counter() - tw:.1f}s")
 
@@ -156,6 +156,10 @@ def main():
     pkt_all, ev_all, kms_all, ems_all = tot.tolist()
     elapsed = mx.item()
     value = pkt_all / elapsed
+    # rounds run behind a state copy (they could log many first touches) and
+    # those rolled back on an ambiguous drop decision, warm-up + timed region
+    protected = {k: int(getattr(wst, k, 0)) + int(getattr(st, k, 0))
+                 for k in ("n_rounds_protected", "n_rounds_rerun")}
 
     # roofline of the round kernel (per launch = per rank-round).  The launch
     # duration is the HIP-event time of the round launches on the engine's
@@ -203,6 +207,7 @@ def main():
                                     "torch.distributed" if world > 1 else "none (single engine)")},
             "all_events_per_s": round(ev_all / elapsed, 1),
             "rounds": int(rounds),
+            "first_touch": protected,
             "apsp": {"rows": int(info.rows_computed), "vertices": V, "build_ms": round(min(builds), 3),
                      "sssp_kernel_ms": round(info.build_ms_sssp, 3), "iterations": int(info.sssp_iterations_max),
                      "max_hops": int(info.max_hops), "ties": int(info.n_ties)},

@@ -148,7 +148,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     // (a tie Dijkstra breaks by heap order, unpinned) -> lowest edge id
     // Lane per vertex (a half-wave-per-vertex version with shuffle reductions
     // measured slower: 20 ms against 12.5 ms for the 10k-row table, since each
-    // wave then waits on two dependent L2 round trips per vertex pair)
+    // wave then waits on two dependent L2 round trips per vertex pair).  Arcs
+    // in order, so the (d[u], eid) rule sees them as before.
     int64_t my_ties = 0;
     for (int32_t v = tid; v < V; v += BLOCK) {
         if (v == src) continue;
@@ -158,15 +159,29 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         int32_t best = -1;
         uint64_t bestd = kDistInf;
         int nbest = 0;
-        for (int32_t k = rin_off[v]; k < rin_off[v + 1]; k++) {
-            const int32_t u = rin_src[k];
-            const uint64_t dub = dist[u];
-            if (dub == kDistInf) continue;
-            if (u2d(dub) + rin_w[k] == dv) {
-                if (best < 0 || dub < bestd) { best = k; bestd = dub; nbest = 1; }
-                else if (dub == bestd) {
-                    nbest++;
-                    if (rin_eid[k] < rin_eid[best]) best = k;
+        // arcs in groups of 8: the group's (u, w) loads are issued together
+        const int32_t kb = rin_off[v], ke = rin_off[v + 1];
+        for (int32_t k0 = kb; k0 < ke; k0 += 8) {
+            int32_t uu[8];
+            double ww[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int32_t k = min(k0 + j, ke - 1);
+                uu[j] = rin_src[k];
+                ww[j] = rin_w[k];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int32_t k = k0 + j;
+                if (k >= ke) break;
+                const uint64_t dub = dist[uu[j]];
+                if (dub == kDistInf) continue;
+                if (u2d(dub) + ww[j] == dv) {
+                    if (best < 0 || dub < bestd) { best = k; bestd = dub; nbest = 1; }
+                    else if (dub == bestd) {
+                        nbest++;
+                        if (rin_eid[k] < rin_eid[best]) best = k;
+                    }
                 }
             }
         }
