@@ -6,3 +6,5 @@ timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 tail -3 gpurun_out/t.log
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 2; }
 cat gpurun_out/bench.json
+timeout -k 10 300 python -u bench.py --group --steps 3 --no-cpu-baseline > gpurun_out/bench_group.json 2> gpurun_out/bench_group.err || { tail -20 gpurun_out/bench_group.err; exit 3; }
+cat gpurun_out/bench_group.json

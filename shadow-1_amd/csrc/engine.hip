@@ -3617,7 +3617,18 @@ struct shd_xgroup {
     bool fixed_cap = false;            // block size given by the caller
     uint64_t last_spill_batch = ~0ull; // batch index of the last spill halt
     uint64_t batches = 0;
+    int last_nb = shd_eng::kBatch;     // rounds in the last batch (its last summary is d_ring[last_nb])
+    // protected rounds (as for one engine): group-wide, so every rank decides alike
+    bool logged_any = false;
+    uint64_t last_logged = 0;          // first touches gathered from the whole group at the last log
 };
+
+static bool x_want_protect(const shd_xgroup* g) {
+    if (protect_off()) return false;
+    for (const shd_eng* e : g->engs)
+        if (e->snap_failed) return false;
+    return protect_all() || !g->logged_any || g->last_logged >= kProtectMin;
+}
 
 static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
     Params P = g->engs[k]->P;
@@ -3673,8 +3684,15 @@ static int x_read_next(shd_xgroup* g) {
     int rc = x_headers(g, h);
     if (rc) return rc;
     uint64_t t = kInf;
-    for (const XHeader& x : h) t = std::min<uint64_t>(t, x.next_time);
-    g->next = t;
+    uint32_t fl = 0;
+    for (const XHeader& x : h) {
+        t = std::min<uint64_t>(t, x.next_time);
+        fl |= x.flags;
+    }
+    // a flagged last round (first-touch log, spill, error) is recovered at the
+    // next batch's first round; its headers' times leave out what the
+    // recovery delivers, so the loop must run on whatever they say
+    g->next = fl ? 0 : t;
     return SHD_OK;
 }
 
@@ -3995,11 +4013,27 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
     double kms = 0;
     while (g->next < stop && rc == SHD_OK) {
         g->batches++;
+        // a protected batch is one round behind a copy of every engine's device
+        // state (the exchange buffers are engine allocations too)
+        const bool prot = x_want_protect(g);
+        const int nb = prot ? 1 : B;
+        const uint64_t xseq0 = g->xseq, next0 = g->next;
+        const int last_nb0 = g->last_nb;
+        std::vector<uint64_t> round0(nl);
+        if (prot) {
+            for (int k = 0; k < nl && !rc; k++) {
+                round0[k] = g->engs[k]->round;
+                SHD_HIP(hipSetDevice(g->engs[k]->device));
+                rc = snapshot_state(g->engs[k], false);
+            }
+            if (rc) break;
+            s.n_rounds_protected++;
+        }
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
             // slot 0 keeps the previous batch's last round: a flag in its
             // headers halts this batch's first round, and the recovery needs it
-            SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &e->d_ring[B], sizeof(DevSummary), hipMemcpyDeviceToDevice,
+            SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &e->d_ring[g->last_nb], sizeof(DevSummary), hipMemcpyDeviceToDevice,
                                    e->stream));
             e->h_seed[1] = host_fresh_summary();
             e->h_ctl->stop = stop;
@@ -4010,7 +4044,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         }
         SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
-        for (int i = 0; i < B; i++) {
+        for (int i = 0; i < nb; i++) {
             const int ri = (int)((g->xseq - 1) & 1);
             for (int k = 0; k < nl; k++) {
                 shd_eng* e = g->engs[k];
@@ -4043,9 +4077,39 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             if (hipEventElapsedTime(&ms, g->engs[0]->bev[0], g->engs[0]->bev[1]) == hipSuccess)
                 s.device_ms_launches += ms;
         }
+        g->last_nb = nb;
+        if (prot && g->engs[0]->h_ring[1].flags == 0u && g->engs[0]->h_ring[1].ws < stop) {
+            // the round ran; its flags came back with its own exchange
+            std::vector<XHeader> hh;
+            if ((rc = x_headers(g, hh))) break;
+            uint32_t fl = 0, errs = 0;
+            for (const XHeader& x : hh) {
+                fl |= x.flags;
+                errs |= x.error;
+            }
+            if ((fl & XF_ERROR) && errs == (uint32_t)SHD_ERR_AMBIGUOUS) {
+                std::vector<shd_pending> all;
+                for (int k = 0; k < nl; k++) g->engs[k]->round_pending = g->engs[k]->h_ring[1].n_pending;
+                if ((rc = x_gather_pending(g, all))) break;
+                for (int k = 0; k < nl && !rc; k++) {
+                    shd_eng* e = g->engs[k];
+                    SHD_HIP(hipSetDevice(e->device));
+                    if ((rc = snapshot_state(e, true))) break;
+                    e->round = round0[k];
+                    e->parity = (int)(e->round & 1);
+                    rc = assign_ranks(e, all.data(), all.size());
+                }
+                if (rc) break;
+                g->xseq = xseq0;
+                g->next = next0;
+                g->last_nb = last_nb0;
+                s.n_rounds_rerun++;
+                continue;   // the same round again, protected again, every pair of its log ranked
+            }
+        }
         int halted_at = -1;
         bool done = false;
-        for (int i = 0; i < B; i++) {
+        for (int i = 0; i < nb; i++) {
             const DevSummary& r0 = g->engs[0]->h_ring[i + 1];
             if (r0.flags == 1u) { halted_at = i; break; }
             if (r0.flags != 0u) break;   // skipped: cannot precede a halt
@@ -4072,9 +4136,11 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         }
         if (done) break;
         if (halted_at < 0) {
+            g->last_logged = 0;
             if ((rc = x_read_next(g))) break;
             continue;
         }
+        g->last_logged = 0;
         // the round before halted_at (ring slot halted_at) was flagged somewhere in the group
         const int slot = halted_at;
         std::vector<XHeader> hh(g->world);
@@ -4094,6 +4160,8 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             std::vector<shd_pending> all;
             for (int k = 0; k < nl; k++) g->engs[k]->round_pending = g->engs[k]->h_ring[slot].n_pending;
             if ((rc = x_gather_pending(g, all))) break;
+            g->last_logged = all.size();
+            if (!all.empty()) g->logged_any = true;
             for (int k = 0; k < nl && !rc; k++) {
                 shd_eng* e = g->engs[k];
                 DevSummary* const keep = e->P.sum;

@@ -191,6 +191,39 @@ def test_engine_group_local_matches_oracle(parts, block):
     grp.close()
 
 
+@pytest.mark.parametrize("parts", [2, 3])
+def test_engine_group_ambiguous_rounds_roll_back(parts, monkeypatch):
+    """Protected rounds in the engine group: with every undecided first-touch
+    send forced ambiguous and every round protected, each logging round is
+    rolled back on every engine (exchange buffers included), ranked from the
+    logs of all engines and rerun; the result is still the oracle's."""
+    from driver import partition
+    from sim import XGroup
+    monkeypatch.setenv("SHD_FORCE_AMBIG", "1")
+    monkeypatch.setenv("SHD_PROTECT_ALL", "1")
+    g = W.geometric_graph(200, seed=5)
+    m = W.phold_model(W.hosts_on_vertices(200, 2), end_time=3 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    pb = partition(m.n_hosts, parts)
+    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
+    grp = XGroup.local(engines)
+    pkt = rerun = prot = rounds = 0
+    for t in (int(1.0 * S.SHD_SEC) + 3, m.params["end_time"]):
+        st = grp.run_until(t)
+        pkt += st.n_pkt_events
+        rerun += st.n_rounds_rerun
+        prot += st.n_rounds_protected
+        rounds += st.n_rounds
+    assert rerun > 0 and prot >= rounds
+    tr = sort_trace(np.concatenate([e.trace() for e in engines]))
+    dg = np.concatenate([e.digest() for e in engines])
+    otr, odg, ost = O.engine_run(m, g)
+    assert pkt == ost["n_pkt_events"]
+    assert np.array_equal(tr, sort_trace(otr))
+    assert np.array_equal(dg, odg)
+    grp.close()
+
+
 def test_engine_group_rccl_single_rank():
     """The RCCL transport end to end with one rank (the multi-rank case needs
     one GPU per rank: RCCL refuses two ranks on one device)."""
