@@ -64,6 +64,12 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+# RCCL writes its version banner to stdout when a communicator is created:
+# everything but the JSON line goes to stderr
+_STDOUT_FD = os.dup(1)
+os.dup2(2, 1)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,6 +220,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
         }
+        sys.stdout.flush()
+        os.dup2(_STDOUT_FD, 1)   # the JSON line is the only thing on stdout
         print(json.dumps(out), flush=True)
     if use_group:
         grp.close()

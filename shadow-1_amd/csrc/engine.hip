@@ -3618,6 +3618,10 @@ struct shd_xgroup {
     uint64_t last_spill_batch = ~0ull; // batch index of the last spill halt
     uint64_t batches = 0;
     int last_nb = shd_eng::kBatch;     // rounds in the last batch (its last summary is d_ring[last_nb])
+    // full batches captured as HIP graphs (RCCL transport, one engine per
+    // process), one per exchange parity at the batch start
+    hipGraphExec_t graph[2] = {nullptr, nullptr};
+    bool graph_failed = false;
     // protected rounds (as for one engine): group-wide, so every rank decides alike
     bool logged_any = false;
     uint64_t last_logged = 0;          // first touches gathered from the whole group at the last log
@@ -3885,8 +3889,17 @@ extern "C" int shd_xgroup_unique_id(uint8_t id[SHD_XID_BYTES]) {
     return SHD_OK;
 }
 
+static void x_drop_graphs(shd_xgroup* g) {
+    for (auto& ge : g->graph)
+        if (ge) {
+            (void)hipGraphExecDestroy(ge);
+            ge = nullptr;
+        }
+}
+
 static void x_free(shd_xgroup* g) {
     if (!g) return;
+    x_drop_graphs(g);
     if (g->comm) (void)ncclCommDestroy(g->comm);
     for (auto& ev : g->eev)
         if (ev) (void)hipEventDestroy(ev);
@@ -3984,6 +3997,67 @@ extern "C" int shd_xgroup_next_time(shd_xgroup* g, uint64_t* t) {
 
 extern "C" void shd_xgroup_destroy(shd_xgroup* g) { x_free(g); }
 
+// nb rounds of the engine group: per round, every engine's k_round_x, the
+// all-to-all, every engine's k_ingest_x
+static int x_enqueue_rounds(shd_xgroup* g, int nb) {
+    const int nl = (int)g->engs.size();
+    int rc = SHD_OK;
+    for (int i = 0; i < nb; i++) {
+        const int ri = (int)((g->xseq - 1) & 1);
+        for (int k = 0; k < nl; k++) {
+            shd_eng* e = g->engs[k];
+            const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
+            hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
+                               (const DParams*)(g->loc[k].d_xpr + i + 1),
+                               (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
+                               (const DevCtl*)e->d_ctl, i, g->window);
+        }
+        if ((rc = x_exchange(g))) return rc;
+        const int wi = (int)((g->xseq - 1) & 1);
+        for (int k = 0; k < nl; k++) {
+            shd_eng* e = g->engs[k];
+            const Params P = xparams(g, k, &e->d_ring[i + 1]);
+            const uint64_t nthr = (uint64_t)g->world * g->xcap;
+            hipLaunchKernelGGL(k_ingest_x, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, dp(P),
+                               (const shd_event*)g->loc[k].xrecv[wi], (const DevCtl*)e->d_ctl, i);
+        }
+    }
+    return SHD_OK;
+}
+
+// a full batch replays a captured graph when the transport allows it (RCCL,
+// one engine per process); a capture that fails is not tried again
+static int x_launch_rounds(shd_xgroup* g, int nb) {
+    static const bool no_graph = getenv("SHD_NO_GRAPH") != nullptr;
+    if (nb != shd_eng::kBatch || !g->rccl || g->engs.size() != 1 || g->graph_failed || no_graph)
+        return x_enqueue_rounds(g, nb);
+    shd_eng* e = g->engs[0];
+    const int par = (int)(g->xseq & 1);
+    hipGraphExec_t& ge = g->graph[par];
+    if (!ge) {
+        const uint64_t xseq0 = g->xseq;
+        hipGraph_t gr = nullptr;
+        SHD_HIP(hipStreamBeginCapture(e->stream, hipStreamCaptureModeThreadLocal));
+        const int rc = x_enqueue_rounds(g, nb);
+        const hipError_t ec = hipStreamEndCapture(e->stream, &gr);
+        g->xseq = xseq0;
+        hipError_t ei = hipErrorUnknown;
+        if (rc == SHD_OK && ec == hipSuccess && gr) ei = hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0);
+        if (gr) (void)hipGraphDestroy(gr);
+        if (ei != hipSuccess) {
+            ge = nullptr;
+            (void)hipGetLastError();
+            g->graph_failed = true;
+            fprintf(stderr, "libshdgpu: engine-group batch capture failed (rc %d, %s); launching directly\n", rc,
+                    hipGetErrorString(ec != hipSuccess ? ec : ei));
+            return x_enqueue_rounds(g, nb);
+        }
+    }
+    SHD_HIP(hipGraphLaunch(ge, e->stream));
+    g->xseq += (uint64_t)nb;   // one exchange per round, as the direct launch counts them
+    return SHD_OK;
+}
+
 extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stats* st) {
     if (!g) return SHD_EINVAL;
     auto t0 = std::chrono::steady_clock::now();
@@ -4044,26 +4118,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         }
         SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
-        for (int i = 0; i < nb; i++) {
-            const int ri = (int)((g->xseq - 1) & 1);
-            for (int k = 0; k < nl; k++) {
-                shd_eng* e = g->engs[k];
-                const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
-                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
-                                   (const DParams*)(g->loc[k].d_xpr + i + 1),
-                                   (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
-                                   (const DevCtl*)e->d_ctl, i, g->window);
-            }
-            if ((rc = x_exchange(g))) return rc;
-            const int wi = (int)((g->xseq - 1) & 1);
-            for (int k = 0; k < nl; k++) {
-                shd_eng* e = g->engs[k];
-                const Params P = xparams(g, k, &e->d_ring[i + 1]);
-                const uint64_t nthr = (uint64_t)g->world * g->xcap;
-                hipLaunchKernelGGL(k_ingest_x, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, dp(P),
-                                   (const shd_event*)g->loc[k].xrecv[wi], (const DevCtl*)e->d_ctl, i);
-            }
-        }
+        if ((rc = x_launch_rounds(g, nb))) break;
         SHD_HIP(hipGetLastError());
         SHD_HIP(hipEventRecord(g->engs[0]->bev[1], g->engs[0]->stream));
         for (int k = 0; k < nl; k++) {
@@ -4181,6 +4236,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             // flags in the same batch, so all grow alike.
             if (g->last_spill_batch != ~0ull && g->batches - g->last_spill_batch <= 1 && g->xcap < (1u << 22)) {
                 g->xcap *= 2;
+                x_drop_graphs(g);   // the graphs point at the old blocks
                 if ((rc = x_alloc(g))) break;
             }
             g->last_spill_batch = g->batches;
