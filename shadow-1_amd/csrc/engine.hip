@@ -2583,6 +2583,88 @@ __global__ __launch_bounds__(kBlock) void k_round_x(DRoundArgs a, const DParams*
     if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
 }
 
+// The same round without the completion ticket: every block writes its share
+// of the summary and ends; k_xfold (one wave, launched next on the stream)
+// folds the shares and packs this engine's headers for the exchange.
+__global__ __launch_bounds__(kBlock) void k_round_xtl(DRoundArgs a, const DParams* __restrict__ Pp,
+                                                      const shd_event* __restrict__ xrecv,
+                                                      XHeader* __restrict__ halt_hdr, DevSummary* __restrict__ init,
+                                                      const DevCtl* __restrict__ ctl, int i, uint64_t window,
+                                                      TlPart* __restrict__ parts) {
+    const DParams& P = *Pp;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    const unsigned long long t_entry = wall_clock64();
+    HostIn in;
+    host_in_load(a, in);
+    if (*a.halt) {
+        if (lead) P.sum->flags = 2u;
+        return;
+    }
+    const uint64_t stop = ctl->stop;
+    const int parity = (int)((ctl->round_base + (uint64_t)i) & 1);
+    const size_t stride = (size_t)P.xcap + 1;
+    uint64_t ws = kInf;
+    uint32_t fl = 0;
+    for (int32_t p = 0; p < P.xworld; p++) {
+        const XHeader h = *(const XHeader*)(xrecv + (size_t)p * stride);
+        ws = h.next_time < ws ? h.next_time : ws;
+        fl |= h.flags;
+    }
+    if (fl) {
+        if (blockIdx.x == 0) {
+            if ((int32_t)threadIdx.x < P.xworld) halt_hdr[threadIdx.x] = *(const XHeader*)(xrecv + threadIdx.x * stride);
+            if (threadIdx.x == 0) {
+                *P.halt = 1u;
+                P.sum->flags = 1u;
+            }
+        }
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, t_entry);
+        *init = fresh_summary();
+        P.sum->ws = ws;
+    }
+    if (ws >= stop) return;   // only forwards the time (k_xfold packs it)
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0)
+        parts[(size_t)(i & 1) * gridDim.x + blockIdx.x] =
+            TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, 0};
+}
+
+__global__ __launch_bounds__(64) void k_xfold(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
+                                              const DevCtl* __restrict__ ctl) {
+    if (*P.halt) return;
+    const uint64_t ws = P.sum->ws;
+    if (ws >= ctl->stop) {
+        if (threadIdx.x == 0) atomicMin(&P.sum->next_time, (unsigned long long)ws);
+        xpack_block(P, P.sum, 1, ws);
+        return;
+    }
+    const TlPart f = tl_gather(parts + (size_t)(i & 1) * nblk, nblk);
+    if (threadIdx.x == 0) {
+        DevSummary* s = P.sum;
+        if (f.next != kInf) atomicMin(&s->next_time, f.next);
+        if (f.nev) atomicAdd(&s->n_events, (unsigned long long)f.nev);
+        if (f.npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f.npkt);
+        if (f.err) atomicOr(&s->error, f.err);
+        atomicMax(&s->t_last, f.t_end);
+    }
+    __syncthreads();
+    xpack_block(P, P.sum, 0, P.sum->next_time);
+}
+
 // events received in the exchange -> inbox[parity] of the next round
 __global__ void k_ingest_x(DParams P, const shd_event* __restrict__ xrecv, const DevCtl* __restrict__ ctl, int ri) {
     if (*P.halt) return;
@@ -3606,6 +3688,7 @@ struct shd_xgroup {
         uint32_t* xcount = nullptr;
         XHeader* halt_hdr = nullptr;
         Params* d_xpr = nullptr;   // device copies of the exchange-mode P, one per summary-ring slot
+        TlPart* parts = nullptr;   // [2][grid] ticketless round shares (k_round_xtl -> k_xfold)
     };
     std::vector<Loc> loc;
     uint64_t xseq = 0;                 // exchanges done: the latest headers are in xrecv[(xseq - 1) & 1]
@@ -3863,7 +3946,8 @@ static int x_alloc(shd_xgroup* g) {
         int rc;
         if ((rc = ealloc(e, &L.xsend, n)) || (rc = ealloc(e, &L.xrecv[0], n)) || (rc = ealloc(e, &L.xrecv[1], n)) ||
             (rc = ealloc(e, &L.xcount, g->world)) || (rc = ealloc(e, &L.halt_hdr, g->world)) ||
-            (rc = ealloc(e, &L.d_xpr, shd_eng::kRing, false)))
+            (rc = ealloc(e, &L.d_xpr, shd_eng::kRing, false)) ||
+            (rc = ealloc(e, &L.parts, 2 * (size_t)((e->nloc + e->P.hpw - 1) / e->P.hpw))))
             return rc;
         std::vector<Params> pr(shd_eng::kRing);
         for (int i = 0; i < shd_eng::kRing; i++) pr[i] = xparams(g, (int)k, &e->d_ring[i]);
@@ -4004,13 +4088,23 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
     int rc = SHD_OK;
     for (int i = 0; i < nb; i++) {
         const int ri = (int)((g->xseq - 1) & 1);
+        static const bool ticket = getenv("SHD_X_TICKET") != nullptr;   // A/B: the ticketed round
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
             const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
-            hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
-                               (const DParams*)(g->loc[k].d_xpr + i + 1),
-                               (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
-                               (const DevCtl*)e->d_ctl, i, g->window);
+            if (ticket) {
+                hipLaunchKernelGGL(k_round_x, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
+                                   (const DParams*)(g->loc[k].d_xpr + i + 1),
+                                   (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
+                                   (const DevCtl*)e->d_ctl, i, g->window);
+            } else {
+                hipLaunchKernelGGL(k_round_xtl, dim3(grid), dim3(kBlock), 0, e->stream, round_args(e->P),
+                                   (const DParams*)(g->loc[k].d_xpr + i + 1),
+                                   (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
+                                   (const DevCtl*)e->d_ctl, i, g->window, g->loc[k].parts);
+                hipLaunchKernelGGL(k_xfold, dim3(1), dim3(64), 0, e->stream, dp(xparams(g, k, &e->d_ring[i + 1])),
+                                   (const TlPart*)g->loc[k].parts, (uint32_t)grid, i, (const DevCtl*)e->d_ctl);
+            }
         }
         if ((rc = x_exchange(g))) return rc;
         const int wi = (int)((g->xseq - 1) & 1);
