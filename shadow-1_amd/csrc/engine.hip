@@ -2645,24 +2645,64 @@ __global__ __launch_bounds__(kBlock) void k_round_xtl(DRoundArgs a, const DParam
 
 __global__ __launch_bounds__(64) void k_xfold(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
                                               const DevCtl* __restrict__ ctl) {
-    if (*P.halt) return;
-    const uint64_t ws = P.sum->ws;
-    if (ws >= ctl->stop) {
-        if (threadIdx.x == 0) atomicMin(&P.sum->next_time, (unsigned long long)ws);
-        xpack_block(P, P.sum, 1, ws);
-        return;
+    // one load batch: halt, the summary fields the round accumulated (log
+    // count, spills, errors), the window start, the stop time and the shares;
+    // the summary is this kernel's alone to complete (fresh from the previous
+    // round but for those fields), so it is written with plain stores and the
+    // headers are packed from registers
+    DevSummary* sum = P.sum;
+    const uint32_t halt = *P.halt;
+    const uint64_t ws = sum->ws, stop = ctl->stop, npend = sum->n_pending, nrem = sum->n_remote;
+    const uint64_t next0 = sum->next_time;
+    const uint32_t err0 = sum->error;
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    const bool fwd = ws >= stop;
+    const TlPart* pp = parts + (size_t)(i & 1) * nblk;
+    for (uint32_t j = threadIdx.x; j < nblk; j += 64) {
+        const TlPart x = pp[j];
+        if (!fwd) tl_fold(f, x);
     }
-    const TlPart f = tl_gather(parts + (size_t)(i & 1) * nblk, nblk);
+    if (halt) return;
+    for (int off = 32; off > 0; off >>= 1) {
+        TlPart o;
+        o.next = __shfl_xor(f.next, off, 64);
+        o.t_end = __shfl_xor(f.t_end, off, 64);
+        o.nev = __shfl_xor(f.nev, off, 64);
+        o.npkt = __shfl_xor(f.npkt, off, 64);
+        o.err = __shfl_xor(f.err, off, 64);
+        tl_fold(f, o);
+    }
+    uint64_t next = fwd ? ws : f.next;
+    next = next0 < next ? next0 : next;
+    const uint32_t err = err0 | f.err;
     if (threadIdx.x == 0) {
-        DevSummary* s = P.sum;
-        if (f.next != kInf) atomicMin(&s->next_time, f.next);
-        if (f.nev) atomicAdd(&s->n_events, (unsigned long long)f.nev);
-        if (f.npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f.npkt);
-        if (f.err) atomicOr(&s->error, f.err);
-        atomicMax(&s->t_last, f.t_end);
+        sum->next_time = next;
+        if (!fwd) {
+            sum->n_events = f.nev;
+            sum->n_pkt_events = f.npkt;
+            sum->error = err;
+            sum->t_last = f.t_end;
+        }
     }
-    __syncthreads();
-    xpack_block(P, P.sum, 0, P.sum->next_time);
+    // this engine's headers (xpack_block with the values in registers)
+    const int32_t p = threadIdx.x;
+    if (p >= P.xworld) return;
+    const uint32_t cnt = P.xcount[p];
+    XHeader h;
+    h.next_time = next;
+    h.count = cnt < P.xcap ? cnt : P.xcap;
+    uint32_t fl = 0;
+    if (!fwd) {
+        if (npend) fl |= XF_PENDING;
+        if (nrem) fl |= XF_OVERFLOW;
+        if (err) fl |= XF_ERROR;
+    }
+    h.flags = fl;
+    h.n_pending = fwd ? 0 : npend;
+    h.error = fwd ? err0 : err;
+    h.pad = 0;
+    *(XHeader*)(P.xsend + (size_t)p * (P.xcap + 1)) = h;
+    P.xcount[p] = 0;
 }
 
 // events received in the exchange -> inbox[parity] of the next round
