@@ -224,7 +224,10 @@ typedef struct shd_model {
 
 /* queue_flags: SHD_QF_NO_CALENDAR routes every inter-host event through the
  * per-host inbox and heap (the calendar's fallback path), for testing */
-enum { SHD_QF_NO_CALENDAR = 1 };
+enum { SHD_QF_NO_CALENDAR = 1,
+       /* count packets per cached path entry on the device (incrementPathPacketCounter,
+        * topology.c:2053-2063 / worker.c:296; read with shd_eng_path_counts) */
+       SHD_QF_COUNT_PATHS = 2 };
 
 /* one event (32 B): key (time, dst, src, seq) = event_compare, event.c:110-153 */
 typedef struct shd_event {
@@ -343,6 +346,13 @@ int shd_eng_run_round(shd_eng* e, uint64_t window_start, uint64_t window_end,
                       shd_round_summary* out);
 /* whole single-engine run to end_time (rounds of W) */
 int shd_eng_run(shd_eng* e, shd_run_stats* out);
+/* per-path packet counters (model queue_flags & SHD_QF_COUNT_PATHS): out[a*T + b] =
+ * packets this engine sent over the cached entry stored as (a, b), a and b attached
+ * indices; a direct entry (complete graphs, prefer-direct adjacent pairs) and a
+ * vertex's own entry are keyed (min, max).  *n = T*T; SHD_ERANGE if cap < T*T.
+ * Replaces the Path.packetCount logged by _topology_logAllCachedPaths
+ * (topology.c:1929-1965); engines of a group each count their own sends. */
+int shd_eng_path_counts(shd_eng* e, uint64_t* out, uint64_t cap, uint64_t* n);
 /* rounds while the next event time is below t_stop (rounds never cross t_stop);
  * stats cover this call only */
 int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* out);

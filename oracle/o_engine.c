@@ -338,6 +338,12 @@ static void boot(ctx_t* c, uint32_t h) {
 
 static uint64_t g_mark = UINT64_MAX;
 void o_engine_set_mark(uint64_t t) { g_mark = t; }
+/* per-path packet counts at the end of a run (topology.c:2053-2063, logged by
+ * _topology_logAllCachedPaths at teardown, 1929-1965): counts[s*V + d] = the
+ * packet count of the cached entry stored as (s, d), 0 where none is stored */
+static uint64_t* g_counts = NULL;
+static int32_t g_counts_v = 0;
+void o_engine_set_counts_out(uint64_t* counts, int32_t n_vertices) { g_counts = counts; g_counts_v = n_vertices; }
 
 int o_engine_run(const shd_model* m, const shd_graph* gin, int32_t force_rows, o_run* out) {
     struct timespec t0, t1;
@@ -402,6 +408,9 @@ int o_engine_run(const shd_model* m, const shd_graph* gin, int32_t force_rows, o
     out->rows_run = o_topo_rows_run(c.topo);
     out->self_run = o_topo_self_run(c.topo);
     free(c.hosts); free(c.q.a); free(att); free(attached);
+    if (g_counts)
+        for (int32_t a = 0; a < g_counts_v; a++)
+            for (int32_t b = 0; b < g_counts_v; b++) g_counts[(size_t)a * g_counts_v + b] = o_topo_stored_count(c.topo, a, b);
     o_topo_free(c.topo); o_graph_free(g);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     out->wall_ms = (t1.tv_sec - t0.tv_sec) * 1e3 + (t1.tv_nsec - t0.tv_nsec) * 1e-6;

@@ -377,6 +377,10 @@ uint64_t o_topo_packet_count(o_topo* t, int32_t s, int32_t d) {
     if (!p && !t->g->directed) p = from_cache(t, d, s);
     return p ? p->count : 0;
 }
+uint64_t o_topo_stored_count(o_topo* t, int32_t s, int32_t d) {
+    slot_t* p = from_cache(t, s, d);
+    return p ? p->count : 0;
+}
 double o_topo_min_latency(o_topo* t) { return t->min_latency; }
 int32_t o_topo_rows_run(o_topo* t) { return t->rows_run; }
 int32_t o_topo_self_run(o_topo* t) { return t->self_run; }

@@ -83,6 +83,10 @@ void o_topo_free(o_topo* t);
 int o_topo_get(o_topo* t, int32_t s, int32_t d, double* lat, double* rel);
 void o_topo_count_packet(o_topo* t, int32_t s, int32_t d);
 uint64_t o_topo_packet_count(o_topo* t, int32_t s, int32_t d);
+/* the count of the entry stored as (s, d) only (no orientation fallback) */
+uint64_t o_topo_stored_count(o_topo* t, int32_t s, int32_t d);
+/* o_engine_run fills counts[s*V + d] = o_topo_stored_count at the end of the run */
+void o_engine_set_counts_out(uint64_t* counts, int32_t n_vertices);
 double o_topo_min_latency(o_topo* t);
 int32_t o_topo_rows_run(o_topo* t);
 int32_t o_topo_self_run(o_topo* t);

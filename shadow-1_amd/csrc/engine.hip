@@ -223,6 +223,7 @@ struct ParamsT {
     // a threshold); verified on the host at every step of both functions
     int32_t dest_closed, n_exc;
     int32_t force_ambig;        // test hook (SHD_FORCE_AMBIG): every undecided first-touch send is ambiguous
+    Ptr<uint32_t> pcount;       // per-path packet counters [T][T] (SHD_QF_COUNT_PATHS), else null
     int32_t exc_x[kDestExc], exc_d[kDestExc];
     // path cache
     int32_t T;
@@ -832,6 +833,15 @@ __device__ __forceinline__ PathVal path_select(const DParams& P, int32_t a, int3
     return v;
 }
 
+// the cached entry a served send counted against (topology.c:2053-2063): the
+// row of the lower rank (the entry stored first, write-once per pair), the
+// pair's direct entry (one per unordered pair), or the vertex's own entry
+__device__ __forceinline__ size_t path_key(const DParams& P, int32_t a, int32_t b, int32_t ra, int32_t rb, uint32_t adj) {
+    const int32_t lo = a < b ? a : b, hi = a < b ? b : a;
+    if (P.complete || (P.prefer_direct && adj) || a == b) return (size_t)lo * P.T + hi;
+    return ra < rb ? (size_t)a * P.T + b : (size_t)b * P.T + a;
+}
+
 __device__ PathVal path_value(const DParams& P, int32_t a, int32_t b) {
     PathRaw x;
     const int32_t ra = P.complete ? kNoRank : P.rank[a];
@@ -980,6 +990,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             const bool pass2 = boot || chance <= pv.rel2 || P.payload == 0;
             if (pass != pass2 || P.force_ambig) err |= SHD_ERR_AMBIGUOUS;
         }
+        if (P.pcount && pass && pv.resolved) atomicAdd(&P.pcount[path_key(P, a, b, ra, x.rb, x.adj)], 1u);
         shd_event e;
         e.time = q.now + (uint64_t)ceil(pv.lat * (double)SHD_MS);
         e.seq = 0;
@@ -2187,6 +2198,12 @@ __device__ void finalize_one(const DParams& P, const Pending& r, int next_parity
     if (r.delivered != 1u) return;
     const PathVal pv = path_value(P, (int32_t)r.a, (int32_t)r.b);
     if (!pv.resolved) err |= SHD_ERR_AMBIGUOUS;
+    if (P.pcount) {   // counted once the pair has its rank (incrementPathPacketCounter, worker.c:296)
+        const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
+        const int32_t ra = P.complete ? kNoRank : P.rank[a], rb = a == b ? kNoRank : P.rank[b];
+        const uint32_t adj = P.prefer_direct ? P.adj[(size_t)a * P.T + b] : 0u;
+        atomicAdd(&P.pcount[path_key(P, a, b, ra, rb, adj)], 1u);
+    }
     shd_event e;
     e.time = r.qtime + (uint64_t)ceil(pv.lat * (double)SHD_MS);
     e.seq = r.seq; e.src = r.qhost; e.dst = r.dst; e.pkt = r.pkt; e.kind = SHD_EV_PACKET;
@@ -3057,6 +3074,10 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.row = pc->d_row; P.dir = pc->d_dir; P.self = pc->d_self;
     P.adj = pc->d_adj;
     P.rank = e->d_rank; P.self_rank = e->d_self_rank;
+    if (m->queue_flags & SHD_QF_COUNT_PATHS) {
+        int rc;
+        if ((rc = ealloc(e, &P.pcount, (size_t)pc->T * pc->T))) { shd_eng_destroy(e); return rc; }
+    }
     P.sum = e->d_sum;
     // the serial-equivalent window W: min over every latency a send can be
     // served (rows, direct values, self values) -> ceil(lat * 1e6) ns
@@ -3665,6 +3686,20 @@ extern "C" int shd_eng_digest(shd_eng* e, shd_host_digest* out) {
     hipError_t err2 = hipStreamSynchronize(e->stream);
     (void)hipFree(d);
     if (err != hipSuccess || err2 != hipSuccess) return SHD_ENODEV;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_path_counts(shd_eng* e, uint64_t* out, uint64_t cap, uint64_t* n) {
+    if (!e || !n || (cap && !out)) return SHD_EINVAL;
+    if (!e->P.pcount) return SHD_EINVAL;   // SHD_QF_COUNT_PATHS was not set
+    const uint64_t cnt = (uint64_t)e->pc->T * e->pc->T;
+    *n = cnt;
+    if (cap < cnt) return SHD_ERANGE;
+    SHD_HIP(hipSetDevice(e->device));
+    std::vector<uint32_t> h(cnt);
+    SHD_HIP(hipMemcpyAsync(h.data(), (const uint32_t*)e->P.pcount, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
+    for (uint64_t i = 0; i < cnt; i++) out[i] = h[i];
     return SHD_OK;
 }
 

@@ -21,6 +21,7 @@ SHD_SEC = 1_000_000_000
 SHD_MTU = 1500
 SHD_HEADER_UDP = 42
 SHD_QF_NO_CALENDAR = 1      # queue_flags: every inter-host event through inbox + heap
+SHD_QF_COUNT_PATHS = 2      # queue_flags: per-path packet counters on the device
 
 EV_HEARTBEAT, EV_REFILL, EV_REFILL_LO, EV_APP_START, EV_PACKET, EV_LOCAL, EV_NOTIFY = range(1, 8)
 TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL = range(1, 8)
@@ -196,6 +197,7 @@ _SIGS = {
     "shd_eng_trace_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "shd_eng_trace_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_digest": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "shd_eng_path_counts": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint64, P(C.c_uint64)]),
     "shd_eng_stream": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
     "shd_eng_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "shd_eng_destroy": (None, [C.c_void_p]),

@@ -170,6 +170,18 @@ class Engine:
         S.check(S.lib().shd_eng_remote_buffer(self.ptr, C.byref(p), C.byref(n)), "remote_buffer")
         return p.value, n.value
 
+    def path_counts(self) -> np.ndarray:
+        """[T, T] uint64 packet counts per cached path entry (SHD_QF_COUNT_PATHS)."""
+        n = C.c_uint64()
+        rc = S.lib().shd_eng_path_counts(self.ptr, None, 0, C.byref(n))
+        if rc not in (0, -34):
+            S.check(rc, "shd_eng_path_counts")
+        out = np.zeros(n.value, dtype=np.uint64)
+        S.check(S.lib().shd_eng_path_counts(self.ptr, out.ctypes.data_as(C.POINTER(C.c_uint64)), n.value,
+                                            C.byref(n)), "shd_eng_path_counts")
+        T = int(round(np.sqrt(n.value)))
+        return out.reshape(T, T)
+
     def ingest(self, dev_ptr, n):
         S.check(S.lib().shd_eng_ingest(self.ptr, C.c_void_p(dev_ptr), int(n)), "ingest")
 

@@ -75,6 +75,7 @@ def lib():
         l.o_run_free.argtypes = [P(ORun)]
         l.o_event_compare.argtypes = [P(S.Event), P(S.Event)]
         l.o_engine_set_mark.argtypes = [C.c_uint64]
+        l.o_engine_set_counts_out.argtypes = [C.c_void_p, C.c_int32]
         _lib = l
     return _lib
 
@@ -137,9 +138,17 @@ class OTopo:
         return lib().o_topo_rows_run(self.ptr)
 
 
-def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None):
-    """Serial reference loop; returns (trace ndarray, digest ndarray, ORun stats dict)."""
+def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None, path_counts=None):
+    """Serial reference loop; returns (trace ndarray, digest ndarray, ORun stats dict).
+    path_counts: a uint64 [V, V] array filled with the packet count of every
+    cached path entry, by the orientation it is stored under."""
     lib().o_engine_set_mark((1 << 64) - 1 if mark is None else int(mark))
+    if path_counts is not None:
+        assert path_counts.dtype == np.uint64 and path_counts.shape == (g.n_vertices, g.n_vertices)
+        assert path_counts.flags.c_contiguous
+        lib().o_engine_set_counts_out(path_counts.ctypes.data, g.n_vertices)
+    else:
+        lib().o_engine_set_counts_out(None, 0)
     r = ORun()
     rc = lib().o_engine_run(C.byref(model.struct), C.byref(g.struct), int(force_rows), C.byref(r))
     assert rc == 0

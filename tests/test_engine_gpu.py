@@ -83,6 +83,37 @@ def test_default_protection_covers_the_application_start():
     assert st.n_batches_ticketless > 0
 
 
+@pytest.mark.parametrize("kind", ["rows", "rows_shared_vertices", "complete"])
+def test_per_path_packet_counters_match_oracle(kind):
+    # incrementPathPacketCounter (topology.c:2053-2063, worker.c:296): every
+    # passing send counts against the cached entry it was served from; the
+    # counts of each unordered pair (both orientations summed: a direct entry
+    # is keyed (min, max) here, by its first query in the reference) and of
+    # each vertex's own entry must match the serial oracle
+    if kind == "complete":
+        g = W.bundled_graph()
+        hv = np.random.default_rng(1).integers(0, g.n_vertices, 400).astype(np.int32)
+        hv = np.sort(hv)
+    else:
+        g = W.geometric_graph(250, seed=8)
+        hv = W.hosts_on_vertices(250, 2 if kind == "rows_shared_vertices" else 1)
+    m = W.phold_model(hv, end_time=3 * S.SHD_SEC, queue_flags=S.SHD_QF_COUNT_PATHS)
+    att = W.attached_vertices(m.host_vertex)
+    pc = PathCache(g, att)
+    eng = Engine(m, pc)
+    st = eng.run()
+    cnt = eng.path_counts()
+    V = g.n_vertices
+    ocnt = np.zeros((V, V), dtype=np.uint64)
+    _, _, ost = O.engine_run(m, g, path_counts=ocnt)
+    assert st.n_pkt_events == ost["n_pkt_events"]
+    o = ocnt[np.ix_(att, att)]                       # attached indices
+    sym = lambda c: np.triu(c + c.T, 1) + np.diag(np.diag(c))   # noqa: E731
+    assert int(o.sum()) > 1000
+    assert int(cnt.sum()) == int(o.sum())
+    assert np.array_equal(sym(cnt), sym(o))
+
+
 def test_bundled_complete_graph_many_hosts_per_vertex():
     g = W.bundled_graph()
     rng = np.random.default_rng(0)
