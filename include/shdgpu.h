@@ -100,6 +100,42 @@ typedef struct shd_graphml {
 } shd_graphml;
 int shd_graphml_load_file(const char* path, shd_graphml** out);
 int shd_graphml_load_string(const char* xml, size_t len, shd_graphml** out);
+
+/* ------------------------------------------------------------ config front-end */
+/*
+ * shadow.config.xml -> the registered host list (core/support/configuration.c,
+ * core/master.c:304-320,397): hosts in document order, `quantity` copies named
+ * "<id><i>" (i from 1) when quantity > 1, their hints and bandwidth overrides;
+ * the topology as a path or inline graphml (CDATA).  Units as in the file:
+ * seconds, KiB/s.
+ */
+typedef struct shd_config_host {
+    char* name;
+    char* ip_hint;          /* NULL when absent, as are the other hints */
+    char* citycode_hint;
+    char* countrycode_hint;
+    char* geocode_hint;
+    char* type_hint;
+    uint64_t bw_down_kibps; /* 0 = take the attached vertex's bandwidth (host.c:183-189) */
+    uint64_t bw_up_kibps;
+    uint64_t heartbeat_s;   /* 0 = the option default */
+} shd_config_host;
+typedef struct shd_config {
+    int32_t n_hosts;
+    shd_config_host* hosts;
+    uint64_t stop_time_s;       /* <shadow stoptime> (or legacy <kill time>) */
+    uint64_t bootstrap_time_s;  /* <shadow bootstraptime> */
+    char* topology_path;        /* <topology path>, NULL if inline */
+    char* topology_text;        /* inline graphml, NULL if by path */
+} shd_config;
+int shd_config_load_file(const char* path, shd_config** out);
+int shd_config_load_buffer(const char* xml, size_t len, shd_config** out);
+void shd_config_free(shd_config* c);
+/* dns_register in registration order (dns.c:102-134, host.c:166-167): each
+ * host's ethernet IPv4 (host byte order) -- the hint when it is unrestricted and
+ * not taken (127.0.0.1 stays local), else the next address after 11.0.0.0 that
+ * is neither reserved nor taken.  ip_out has n_hosts entries. */
+int shd_dns_assign(const shd_config* c, uint32_t* ip_out);
 void shd_graphml_free(shd_graphml* gm);
 
 /* ------------------------------------------------------------ path cache */

@@ -60,6 +60,17 @@ class GraphProps(C.Structure):
         "max_out_degree")]
 
 
+class ConfigHost(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("ip_hint", C.c_char_p), ("citycode_hint", C.c_char_p),
+                ("countrycode_hint", C.c_char_p), ("geocode_hint", C.c_char_p), ("type_hint", C.c_char_p),
+                ("bw_down_kibps", C.c_uint64), ("bw_up_kibps", C.c_uint64), ("heartbeat_s", C.c_uint64)]
+
+
+class Config(C.Structure):
+    _fields_ = [("n_hosts", C.c_int32), ("hosts", C.POINTER(ConfigHost)), ("stop_time_s", C.c_uint64),
+                ("bootstrap_time_s", C.c_uint64), ("topology_path", C.c_char_p), ("topology_text", C.c_char_p)]
+
+
 class GraphML(C.Structure):
     _fields_ = [
         ("g", Graph), ("bw_down", P(C.c_double)), ("bw_up", P(C.c_double)),
@@ -157,6 +168,10 @@ _SIGS = {
     "shd_graph_check": (C.c_int, [P(Graph), P(GraphProps)]),
     "shd_graphml_load_file": (C.c_int, [C.c_char_p, P(P(GraphML))]),
     "shd_graphml_load_string": (C.c_int, [C.c_char_p, C.c_size_t, P(P(GraphML))]),
+    "shd_config_load_file": (C.c_int, [C.c_char_p, P(P(Config))]),
+    "shd_config_load_buffer": (C.c_int, [C.c_char_p, C.c_size_t, P(P(Config))]),
+    "shd_config_free": (None, [P(Config)]),
+    "shd_dns_assign": (C.c_int, [P(Config), P(C.c_uint32)]),
     "shd_graphml_free": (None, [P(GraphML)]),
     "shd_pc_create": (C.c_int, [P(Graph), P(C.c_int32), C.c_int32, C.c_uint32, C.c_int,
                                 P(C.c_void_p)]),
@@ -271,6 +286,31 @@ class GraphArrays:
     @property
     def n_edges(self):
         return len(self.src)
+
+
+def load_config(xml: bytes):
+    """shadow.config.xml -> (hosts: list of dicts in registration order,
+    ips: host-order uint32 array from shd_dns_assign, stop_time_s, topology text or path)."""
+    ptr = P(Config)()
+    check(lib().shd_config_load_buffer(xml, len(xml), C.byref(ptr)), "shd_config_load_buffer")
+    try:
+        c = ptr.contents
+        dec = lambda b: None if b is None else b.decode()  # noqa: E731
+        hosts = [dict(name=dec(h.name), ip_hint=dec(h.ip_hint), citycode_hint=dec(h.citycode_hint),
+                      countrycode_hint=dec(h.countrycode_hint), geocode_hint=dec(h.geocode_hint),
+                      type_hint=dec(h.type_hint), bw_down_kibps=h.bw_down_kibps, bw_up_kibps=h.bw_up_kibps,
+                      heartbeat_s=h.heartbeat_s) for h in (c.hosts[i] for i in range(c.n_hosts))]
+        ips = np.zeros(max(c.n_hosts, 1), dtype=np.uint32)
+        check(lib().shd_dns_assign(ptr, ips.ctypes.data_as(P(C.c_uint32))), "shd_dns_assign")
+        topo = dec(c.topology_text) if c.topology_text else dec(c.topology_path)
+        return hosts, ips[:c.n_hosts], c.stop_time_s, topo
+    finally:
+        lib().shd_config_free(ptr)
+
+
+def ip_str(ip: int) -> str:
+    ip = int(ip)
+    return "%d.%d.%d.%d" % (ip >> 24, (ip >> 16) & 255, (ip >> 8) & 255, ip & 255)
 
 
 def graph_from_graphml(gm_ptr) -> GraphArrays:
