@@ -62,9 +62,10 @@ def test_c3_full_size_deterministic(c3):
     assert int(d1["n_events"].sum()) == st1.n_events
 
 
-@pytest.mark.parametrize("hosts,parts", [(V, 2), (2 * V, 2), (V, 4)])
+@pytest.mark.parametrize("hosts,parts", [(V, 2), (2 * V, 2), (V, 4), (4 * V, 4), (8 * V, 8)])
 def test_bench_workload_sharded_group_equals_single_engine(hosts, parts):
-    """(2 V, 2) is bench.py --gpus 2's workload, sharded as its ranks shard it."""
+    """(N V, N) is bench.py --gpus N's workload (weak scaling: N x 10 k hosts on the
+    same graph), sharded as its N ranks shard it."""
     from driver import partition
     from sim import XGroup
     g, m = bench_workload(hosts)
