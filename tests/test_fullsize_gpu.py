@@ -83,3 +83,29 @@ def test_bench_workload_sharded_group_equals_single_engine(hosts, parts):
     for e in engines:
         e.close()
     pc.close()
+
+
+def test_c5_million_hosts_group_equals_single_engine():
+    """BASELINE C5's scale on one GPU: 1 M hosts, 100 per vertex of the 10 k-vertex
+    graph (the scripts/c5_single.sh workload).  The application start logs
+    ~16 M first touches, so the protected rounds run here; two engines of a
+    group must end where one engine ends."""
+    from driver import partition
+    from sim import XGroup
+    g = W.geometric_graph(V, seed=1, loss_max=0.0005)
+    m = W.phold_model(W.hosts_on_vertices(V, 100), end_time=int(1.5 * S.SHD_SEC), seed=1, load=16,
+                      payload=1)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    st, d1 = single(m, pc)
+    assert st.error == 0 and st.n_rounds_protected > 0 and st.n_pkt_events > 10_000_000
+    pb = partition(m.n_hosts, 2)
+    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(2)]
+    grp = XGroup.local(engines)
+    gst = grp.run()
+    assert gst.error == 0
+    assert gst.n_pkt_events == st.n_pkt_events and gst.n_events == st.n_events
+    assert np.array_equal(np.concatenate([e.digest() for e in engines]), d1)
+    grp.close()
+    for e in engines:
+        e.close()
+    pc.close()
