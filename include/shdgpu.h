@@ -263,7 +263,10 @@ typedef struct shd_model {
 enum { SHD_QF_NO_CALENDAR = 1,
        /* count packets per cached path entry on the device (incrementPathPacketCounter,
         * topology.c:2053-2063 / worker.c:296; read with shd_eng_path_counts) */
-       SHD_QF_COUNT_PATHS = 2 };
+       SHD_QF_COUNT_PATHS = 2,
+       /* keep every host's tracker node counters at each heartbeat (tracker_heartbeat,
+        * tracker.c:566-611; read with shd_eng_heartbeats) */
+       SHD_QF_HEARTBEATS = 4 };
 
 /* one event (32 B): key (time, dst, src, seq) = event_compare, event.c:110-153 */
 typedef struct shd_event {
@@ -425,6 +428,15 @@ int shd_eng_trace_count(shd_eng* e, uint64_t* n);
 int shd_eng_trace_copy(shd_eng* e, shd_trace_rec* out, uint64_t cap, uint64_t* n);
 int shd_eng_digest(shd_eng* e, shd_host_digest* out);   /* [host_end-host_begin] */
 int shd_eng_stream(shd_eng* e, void** hip_stream);
+/* tracker node counters (model queue_flags & SHD_QF_HEARTBEATS): out[(l*K + k)*2 + j]
+ * = local host l's cumulative interface packet count, j = 0 in
+ * (_networkinterface_receivePacket, network_interface.c:415) / 1 out
+ * (_networkinterface_sendPackets, network_interface.c:571), taken at its heartbeat
+ * at (k+1)*heartbeat_interval; K = (end_time-1)/heartbeat_interval.  Each counted
+ * packet is a data packet of payload + 42 header bytes, so the per-interval
+ * differences give the [shadow-heartbeat] [node] line (tracker.c:419-465).
+ * *n = nloc*K*2; SHD_ERANGE if cap < *n. */
+int shd_eng_heartbeats(shd_eng* e, uint32_t* out, uint64_t cap, uint64_t* n);
 /* HIP-event device time of the last round kernel launch (ms) */
 int shd_eng_last_kernel_ms(shd_eng* e, double* ms);
 void shd_eng_destroy(shd_eng* e);

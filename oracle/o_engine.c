@@ -78,6 +78,10 @@ typedef struct {
     o_codel codel;
     txent* txq; uint32_t txq_head, txq_count, txq_cap;
     uint64_t n_events, n_pkt_events, n_sent, n_inet_drop, n_codel_drop, n_recv;
+    /* tracker node counters (tracker.c:216-275): packets through the interface,
+     * in (_networkinterface_receivePacket) and out (_networkinterface_sendPackets);
+     * cumulative here, differenced per heartbeat by the reader */
+    uint32_t if_in, if_out;
 } ohost;
 
 typedef struct {
@@ -134,6 +138,7 @@ static inline void consume(uint64_t* rem, uint64_t n) { *rem = (n >= *rem) ? 0 :
  * datagram to the bound UDP socket (PHOLD listener on 8998) or drop it */
 static void if_receive_packet(ctx_t* c, uint32_t h, uint32_t src, uint32_t pkt) {
     ohost* H = &c->hosts[h];
+    H->if_in++;                        /* tracker_addInputBytes, n_i.c:415 */
     if (H->listening) {
         trace(c, c->now, 0, h, src, pkt, SHD_TR_RECV);
         H->n_recv++;
@@ -202,6 +207,7 @@ static void if_send_packets(ctx_t* c, uint32_t h) {
         txent p = H->txq[H->txq_head];
         H->txq_head = (H->txq_head + 1) % H->txq_cap;
         H->txq_count--;
+        H->if_out++;                   /* tracker_addOutputBytes, n_i.c:571 */
         if (p.dst == h) {
             /* packet to our own address: +1 ns local task, no router / RNG */
             trace(c, c->now, H->ev_seq, h, h, p.pkt, SHD_TR_LOCAL);
@@ -278,12 +284,25 @@ static void refill_cb(ctx_t* c, uint32_t h) {
     refill_if_needed(c, h);
 }
 
+/* heartbeat snapshots (tracker_heartbeat, tracker.c:566-611): at the k-th
+ * heartbeat (time k*interval, k >= 1) host h stores its cumulative interface
+ * counters at g_hb[(h*g_hb_k + k-1)*2 + {0: in, 1: out}] */
+static uint32_t* g_hb = NULL;
+static uint32_t g_hb_k = 0;
+void o_engine_set_heartbeats_out(uint32_t* hb, uint32_t k_max) { g_hb = hb; g_hb_k = k_max; }
 static void execute(ctx_t* c, const shd_event* e) {
     uint32_t h = e->dst;
     ohost* H = &c->hosts[h];
     H->n_events++;
     switch (e->kind) {
     case SHD_EV_HEARTBEAT:
+        if (g_hb) {
+            uint64_t k = c->now / c->m->heartbeat_interval;
+            if (k >= 1 && k <= g_hb_k) {
+                g_hb[((uint64_t)h * g_hb_k + k - 1) * 2] = H->if_in;
+                g_hb[((uint64_t)h * g_hb_k + k - 1) * 2 + 1] = H->if_out;
+            }
+        }
         schedule_task(c, h, SHD_EV_HEARTBEAT, c->m->heartbeat_interval, 0);
         break;
     case SHD_EV_REFILL:

@@ -97,7 +97,9 @@ struct alignas(16) HostRec {
     uint32_t rx_refill, tx_refill;         // token-bucket refill per 1 ms (bytes)
     uint32_t flags, unread;
     uint32_t cq_dc, cq_dcl, cq_head, cq_count;   // CoDel drop counts, FIFO head / length
-    uint32_t tq_head, tq_count, evq_n, pad[3];
+    uint32_t tq_head, tq_count, evq_n;
+    uint32_t if_in, if_out;                // tracker node counters: interface packets in / out (cumulative)
+    uint32_t pad;
 };
 static_assert(sizeof(HostRec) == 160, "host record: 10 x 16 B");
 
@@ -224,6 +226,8 @@ struct ParamsT {
     int32_t dest_closed, n_exc;
     int32_t force_ambig;        // test hook (SHD_FORCE_AMBIG): every undecided first-touch send is ambiguous
     Ptr<uint32_t> pcount;       // per-path packet counters [T][T] (SHD_QF_COUNT_PATHS), else null
+    Ptr<uint2> hb;              // heartbeat snapshots [nloc][hb_k] (SHD_QF_HEARTBEATS), else null
+    uint32_t hb_k;
     int32_t exc_x[kDestExc], exc_d[kDestExc];
     // path cache
     int32_t T;
@@ -401,6 +405,7 @@ struct HostCtx {
     bool cq_hv, tq_hv;          // FIFO head entries held in LDS (s_cqh, s_tqh), not yet stored
     int32_t att;                // this host's attached-vertex index
     uint32_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;   // this round's counter deltas
+    uint32_t if_in, if_out;     // HostRec::if_in / if_out
     // current executing event key (for first-touch logging)
     uint64_t q_seq;
     uint32_t q_src;
@@ -649,6 +654,7 @@ __device__ __forceinline__ void consume(uint64_t& rem, uint64_t n) { rem = (n >=
 
 // _networkinterface_receivePacket (network_interface.c:375-419)
 __device__ void if_receive_packet(const DParams& P, HostCtx& c, uint32_t src, uint32_t pkt) {
+    c.if_in++;   // tracker_addInputBytes (network_interface.c:415)
     if (c.flags & F_LISTENING) {
         trace(P, c, c.now, 0, c.h, src, pkt, SHD_TR_RECV);
         c.c_recv++;
@@ -918,6 +924,7 @@ __device__ void worker_send_deferred(const DParams& P, HostCtx& c, uint32_t rv, 
     s_send[c.ns * kBlock + threadIdx.x] = q;
     c.ns++;
     c.ev_seq++;   // provisional: a dropped send gives its ID back at the flush
+    c.if_out++;   // tracker_addOutputBytes (network_interface.c:571)
 }
 
 // Resolve every lane's deferred sends together.  Called by all lanes of the
@@ -1140,6 +1147,7 @@ __device__ bool if_send_step(const DParams& P, HostCtx& c) {
         c.tq_count--;
         if (self) {
             trace(P, c, c.now, c.ev_seq, c.h, c.h, p.pkt, SHD_TR_LOCAL);
+            c.if_out++;
             schedule_self(P, c, SHD_EV_LOCAL, 1, p.pkt);
         } else {
             PROF_T0(ts)
@@ -1226,6 +1234,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         !c.k.trace && !bootstrapping(P, c)) {
         c.c_pkt++;
         c.c_recv++;
+        c.if_in++;
         c.unread++;
         c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
         c.cq_iexp = 0;
@@ -1286,6 +1295,12 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
 #endif
     switch (e.kind) {
     case SHD_EV_HEARTBEAT:
+        // tracker_heartbeat (tracker.c:566-611): the node counters at the k-th
+        // heartbeat, cumulative (the reader takes the per-interval differences)
+        if (P.hb) {
+            const uint64_t k = c.now / P.heartbeat;
+            if (k >= 1 && k <= P.hb_k) P.hb[(size_t)c.l * P.hb_k + (k - 1)] = make_uint2(c.if_in, c.if_out);
+        }
         schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
         break;
     case SHD_EV_REFILL:
@@ -1430,6 +1445,7 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.cq_total = launder(r.cq_total); c.cq_iexp = launder(r.cq_iexp); c.cq_ndrop = launder(r.cq_ndrop);
     c.cq_dc = launder(r.cq_dc); c.cq_dcl = launder(r.cq_dcl); c.cq_head = launder(r.cq_head); c.cq_count = launder(r.cq_count);
     c.tq_head = launder(r.tq_head); c.tq_count = launder(r.tq_count);
+    c.if_in = launder(r.if_in); c.if_out = launder(r.if_out);
     c.evq_n = launder(r.evq_n);
     if (r.evq_n) {
         const shd_event t = P.evq[(size_t)l * P.evq_stride + 3];
@@ -1583,7 +1599,7 @@ __device__ void store_ctx(const DParams& P, const HostCtx& c) {
     r.flags = c.flags; r.unread = c.unread;
     r.cq_dc = c.cq_dc; r.cq_dcl = c.cq_dcl; r.cq_head = c.cq_head; r.cq_count = c.cq_count;
     r.tq_head = c.tq_head; r.tq_count = c.tq_count; r.evq_n = c.evq_n;
-    r.pad[0] = r.pad[1] = r.pad[2] = 0;
+    r.if_in = c.if_in; r.if_out = c.if_out; r.pad = 0;
     P.hs[l] = r;
     if (c.cq_hv) P.cq[(size_t)l * c.k.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
     if (c.tq_hv) P.tq[(size_t)l * c.k.tq_cap + c.tq_head] = s_tqh[threadIdx.x];
@@ -1712,7 +1728,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         P.hc[l] = HostCnt{0, 0, 0, 0, 0, 0};
         r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
         r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
-        r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.pad[0] = r.pad[1] = r.pad[2] = 0;
+        r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.if_in = 0; r.if_out = 0; r.pad = 0;
         P.hs[l] = r;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
         HostCtx c;
@@ -2792,6 +2808,7 @@ struct shd_eng {
     uint64_t window = 0;
     int parity = 0;
     bool booted = false;
+    bool heartbeats = false;    // SHD_QF_HEARTBEATS: snapshots in P.hb
     std::vector<void*> allocs;
     std::vector<size_t> alloc_bytes;
     // protected rounds (DESIGN.md "First-touch rule"): device state copied
@@ -3077,6 +3094,15 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     if (m->queue_flags & SHD_QF_COUNT_PATHS) {
         int rc;
         if ((rc = ealloc(e, &P.pcount, (size_t)pc->T * pc->T))) { shd_eng_destroy(e); return rc; }
+    }
+    if ((m->queue_flags & SHD_QF_HEARTBEATS) && m->end_time > 0) {
+        // heartbeats at k * interval < end_time, k >= 1
+        const uint64_t k = (m->end_time - 1) / m->heartbeat_interval;
+        if (k > (1u << 20)) { shd_eng_destroy(e); return SHD_ERANGE; }
+        P.hb_k = (uint32_t)k;
+        e->heartbeats = true;
+        int rc;
+        if (k && (rc = ealloc(e, &P.hb, (size_t)n * k))) { shd_eng_destroy(e); return rc; }
     }
     P.sum = e->d_sum;
     // the serial-equivalent window W: min over every latency a send can be
@@ -3700,6 +3726,19 @@ extern "C" int shd_eng_path_counts(shd_eng* e, uint64_t* out, uint64_t cap, uint
     SHD_HIP(hipMemcpyAsync(h.data(), (const uint32_t*)e->P.pcount, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
     SHD_HIP(hipStreamSynchronize(e->stream));
     for (uint64_t i = 0; i < cnt; i++) out[i] = h[i];
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_heartbeats(shd_eng* e, uint32_t* out, uint64_t cap, uint64_t* n) {
+    if (!e || !n || (cap && !out)) return SHD_EINVAL;
+    if (!e->heartbeats) return SHD_EINVAL;   // not requested at creation
+    const uint64_t cnt = (uint64_t)e->nloc * e->P.hb_k * 2;
+    *n = cnt;
+    if (cap < cnt) return SHD_ERANGE;
+    if (!cnt) return SHD_OK;
+    SHD_HIP(hipSetDevice(e->device));
+    SHD_HIP(hipMemcpyAsync(out, (const uint2*)e->P.hb, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
+    SHD_HIP(hipStreamSynchronize(e->stream));
     return SHD_OK;
 }
 

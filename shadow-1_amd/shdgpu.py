@@ -22,6 +22,7 @@ SHD_MTU = 1500
 SHD_HEADER_UDP = 42
 SHD_QF_NO_CALENDAR = 1      # queue_flags: every inter-host event through inbox + heap
 SHD_QF_COUNT_PATHS = 2      # queue_flags: per-path packet counters on the device
+SHD_QF_HEARTBEATS = 4       # queue_flags: tracker node counters at every heartbeat
 
 EV_HEARTBEAT, EV_REFILL, EV_REFILL_LO, EV_APP_START, EV_PACKET, EV_LOCAL, EV_NOTIFY = range(1, 8)
 TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL = range(1, 8)
@@ -213,6 +214,7 @@ _SIGS = {
     "shd_eng_trace_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_digest": (C.c_int, [C.c_void_p, C.c_void_p]),
     "shd_eng_path_counts": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint64, P(C.c_uint64)]),
+    "shd_eng_heartbeats": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint64, P(C.c_uint64)]),
     "shd_eng_stream": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
     "shd_eng_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "shd_eng_destroy": (None, [C.c_void_p]),
@@ -352,3 +354,49 @@ class ModelArrays:
     @property
     def n_hosts(self):
         return len(self.host_vertex)
+
+
+# ---- tracker heartbeat lines (host/tracker.c) ----
+SHD_HEADER_UDP = 42          # definitions.h:176-183
+
+TRACKER_COUNTER_HEADER = (   # _tracker_getCounterHeaderString, tracker.c:391-397
+    "packets-total,bytes-total,packets-control,bytes-control-header,"
+    "packets-control-retrans,bytes-control-header-retrans,"
+    "packets-data,bytes-data-header,bytes-data-payload,"
+    "packets-data-retrans,bytes-data-header-retrans,bytes-data-payload-retrans")
+
+NODE_HEADER_LINE = (         # _tracker_logNode's header, tracker.c:429-441
+    "[shadow-heartbeat] [node-header] interval-seconds,recv-bytes,send-bytes,cpu-percent,"
+    "delayed-count,avgdelay-milliseconds;inbound-localhost-counters;outbound-localhost-counters;"
+    "inbound-remote-counters;outbound-remote-counters where counters are: " + TRACKER_COUNTER_HEADER)
+
+
+def _counter_string(packets: int, payload: int) -> str:
+    """_tracker_getCounterString (tracker.c:399-417) for `packets` first-sent UDP
+    datagrams (_tracker_updateCounters, tracker.c:183-214: payload > 0 is 'data',
+    payload 0 is 'control'); PHOLD-UDP has no retransmissions."""
+    h, p = packets * SHD_HEADER_UDP, packets * payload
+    if payload > 0:
+        f = (packets, h + p, 0, 0, 0, 0, packets, h, p, 0, 0, 0)
+    else:
+        f = (packets, h, packets, h, 0, 0, 0, 0, 0, 0, 0, 0)
+    return ",".join(str(x) for x in f)
+
+
+def tracker_node_lines(snapshots, interval_ns: int, payload: int) -> list:
+    """The [shadow-heartbeat] [node] lines of one host (tracker.c:419-465) from its
+    cumulative interface counters at each heartbeat (shd_eng_heartbeats: [K, 2]
+    uint32 in/out).  Every counter is cleared at each heartbeat (tracker.c:584-593),
+    so a line holds the differences to the previous heartbeat.  The loopback
+    shortcut keeps the host's own address (network_interface.c:548-555), so all
+    packets count as remote; the CPU model is off (cpu-percent 0, no delays)."""
+    lines, prev = [NODE_HEADER_LINE], (0, 0)
+    secs = int(interval_ns // SHD_SEC)
+    zero = _counter_string(0, payload)
+    for cin, cout in np.asarray(snapshots, dtype=np.int64).tolist():
+        din, dout = cin - prev[0], cout - prev[1]
+        prev = (cin, cout)
+        rb, sb = din * (SHD_HEADER_UDP + payload), dout * (SHD_HEADER_UDP + payload)
+        lines.append("[shadow-heartbeat] [node] %u,%d,%d,%f,%d,%f;%s;%s;%s;%s" % (
+            secs, rb, sb, 0.0, 0, 0.0, zero, zero, _counter_string(din, payload), _counter_string(dout, payload)))
+    return lines

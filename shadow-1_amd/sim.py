@@ -170,6 +170,19 @@ class Engine:
         S.check(S.lib().shd_eng_remote_buffer(self.ptr, C.byref(p), C.byref(n)), "remote_buffer")
         return p.value, n.value
 
+    def heartbeats(self) -> np.ndarray:
+        """[nloc, K, 2] uint32 cumulative interface packets (in, out) of each local host
+        at its k-th heartbeat (SHD_QF_HEARTBEATS); S.tracker_node_lines formats them."""
+        n = C.c_uint64()
+        rc = S.lib().shd_eng_heartbeats(self.ptr, None, 0, C.byref(n))
+        if rc not in (0, -34):
+            S.check(rc, "shd_eng_heartbeats")
+        out = np.zeros(n.value, dtype=np.uint32)
+        if n.value:
+            S.check(S.lib().shd_eng_heartbeats(self.ptr, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value,
+                                               C.byref(n)), "shd_eng_heartbeats")
+        return out.reshape(self.h1 - self.h0, -1, 2)
+
     def path_counts(self) -> np.ndarray:
         """[T, T] uint64 packet counts per cached path entry (SHD_QF_COUNT_PATHS)."""
         n = C.c_uint64()

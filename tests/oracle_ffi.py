@@ -76,6 +76,7 @@ def lib():
         l.o_event_compare.argtypes = [P(S.Event), P(S.Event)]
         l.o_engine_set_mark.argtypes = [C.c_uint64]
         l.o_engine_set_counts_out.argtypes = [C.c_void_p, C.c_int32]
+        l.o_engine_set_heartbeats_out.argtypes = [C.c_void_p, C.c_uint32]
         _lib = l
     return _lib
 
@@ -138,10 +139,18 @@ class OTopo:
         return lib().o_topo_rows_run(self.ptr)
 
 
-def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None, path_counts=None):
+def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None, path_counts=None,
+               heartbeats=None):
     """Serial reference loop; returns (trace ndarray, digest ndarray, ORun stats dict).
     path_counts: a uint64 [V, V] array filled with the packet count of every
-    cached path entry, by the orientation it is stored under."""
+    cached path entry, by the orientation it is stored under.
+    heartbeats: a uint32 [H, K, 2] array filled with each host's cumulative
+    interface (in, out) packet counts at its k-th heartbeat (tracker.c:566-611)."""
+    if heartbeats is not None:
+        assert heartbeats.dtype == np.uint32 and heartbeats.ndim == 3 and heartbeats.flags.c_contiguous
+        lib().o_engine_set_heartbeats_out(heartbeats.ctypes.data, heartbeats.shape[1])
+    else:
+        lib().o_engine_set_heartbeats_out(None, 0)
     lib().o_engine_set_mark((1 << 64) - 1 if mark is None else int(mark))
     if path_counts is not None:
         assert path_counts.dtype == np.uint64 and path_counts.shape == (g.n_vertices, g.n_vertices)

@@ -270,3 +270,36 @@ def test_engine_group_rccl_single_rank():
     assert np.array_equal(sort_trace(eng.trace()), sort_trace(otr))
     assert np.array_equal(eng.digest(), odg)
     grp.close()
+
+
+@pytest.mark.parametrize("kind", ["plain", "codel", "sharded"])
+def test_heartbeat_node_counters_match_oracle(kind):
+    """tracker_heartbeat (tracker.c:566-611): every host's interface counters at
+    each heartbeat (in: network_interface.c:415, out: 571), trace off so the
+    straight-line event paths run; the [node] lines follow from them."""
+    from driver import partition
+    from sim import XGroup
+    end = int(4.5 * S.SHD_SEC)
+    g = W.geometric_graph(200, seed=3)
+    kw = dict(load=24, payload=1000, bw_down=600, bw_up=100000, codelq_cap=256) if kind == "codel" else {}
+    m = W.phold_model(W.hosts_on_vertices(200, 1), end_time=end, queue_flags=S.SHD_QF_HEARTBEATS, **kw)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    if kind == "sharded":
+        pb = partition(m.n_hosts, 3)
+        engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(3)]
+        grp = XGroup.local(engines)
+        grp.run()
+        hb = np.concatenate([e.heartbeats() for e in engines])
+        grp.close()
+    else:
+        eng = Engine(m, pc)
+        eng.run()
+        hb = eng.heartbeats()
+    K = (end - 1) // S.SHD_SEC
+    ohb = np.zeros((m.n_hosts, K, 2), dtype=np.uint32)
+    O.engine_run(m, g, heartbeats=ohb)
+    assert hb.shape == ohb.shape == (m.n_hosts, 4, 2)
+    assert int(ohb[:, -1].sum()) > 1000
+    assert np.array_equal(hb, ohb)
+    lines = S.tracker_node_lines(hb[7], S.SHD_SEC, int(m.params["payload"]))
+    assert lines == S.tracker_node_lines(ohb[7], S.SHD_SEC, int(m.params["payload"]))

@@ -132,3 +132,40 @@ def test_serial_trace_is_time_ordered():
     tr, dg, st = O.engine_run(m, g)
     assert np.all(np.diff(tr["time"].astype(np.int64)) >= 0)
     assert st["rows_run"] == 0
+
+
+def test_oracle_heartbeat_counters_follow_the_trace():
+    """tracker node counters at each heartbeat (tracker.c:566-611): away from the
+    heartbeat instants themselves, the cumulative in / out counts equal the
+    interface receptions (RECV, IF_DROP) and departures (SENT, INET_DROP, LOCAL)
+    traced before them; the [node] lines carry the per-interval differences."""
+    end = int(3.5 * S.SHD_SEC)
+    g = W.geometric_graph(120, seed=5)
+    m = W.phold_model(W.hosts_on_vertices(120, 1), end_time=end, trace=True,
+                      queue_flags=S.SHD_QF_HEARTBEATS)
+    hb = np.zeros((m.n_hosts, 3, 2), dtype=np.uint32)
+    tr, _, _ = O.engine_run(m, g, heartbeats=hb)
+    inn = np.isin(tr["kind"], [S.TR_RECV, S.TR_IF_DROP])
+    out = np.isin(tr["kind"], [S.TR_SENT, S.TR_INET_DROP, S.TR_LOCAL])
+    checked = 0
+    for h in range(m.n_hosts):
+        mine = tr["host"] == h
+        for k in range(1, 4):
+            T = k * S.SHD_SEC
+            if np.any(mine & (tr["time"] == T)):
+                continue          # the order against the heartbeat needs the event key
+            assert hb[h, k - 1, 0] == np.count_nonzero(mine & inn & (tr["time"] < T))
+            assert hb[h, k - 1, 1] == np.count_nonzero(mine & out & (tr["time"] < T))
+            checked += 1
+    assert checked > 200 and int(hb[:, -1].sum()) > 1000
+    lines = S.tracker_node_lines(hb[3], S.SHD_SEC, 1)
+    assert lines[0].startswith("[shadow-heartbeat] [node-header] interval-seconds,")
+    assert len(lines) == 4
+    d = np.diff(np.vstack([[0, 0], hb[3].astype(np.int64)]), axis=0)
+    for line, (din, dout) in zip(lines[1:], d):
+        head, loc_in, loc_out, rem_in, rem_out = line.split("] [node] ")[1].split(";")
+        f = head.split(",")
+        assert f[0] == "1" and int(f[1]) == din * 43 and int(f[2]) == dout * 43
+        assert loc_in == loc_out == ",".join(["0"] * 12)
+        assert rem_in.split(",")[:2] == [str(din), str(din * 43)]
+        assert rem_out.split(",")[6:9] == [str(dout), str(dout * 42), str(dout)]
