@@ -42,14 +42,17 @@ def parse():
     ap.add_argument("--payload", type=int, default=1)
     ap.add_argument("--step-ms", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--edge-loss-max", type=float, default=0.0005,
-                    help="edge loss ~ U[0, x]; paths are ~20 hops, so the default keeps the per-path "
-                         "loss near U[0,1%%] and the PHOLD population alive for the whole run")
+    ap.add_argument("--edge-loss-max", type=float, default=0.0,
+                    help="edge loss ~ U[0, x] of the headline run.  PHOLD never regenerates a lost "
+                         "message, so any loss makes the population (and the rate) decay with "
+                         "simulated time; the default 0 keeps it stationary, so the value does not "
+                         "depend on --steps / --warmup")
+    ap.add_argument("--lossy-edge-loss-max", type=float, default=0.0005,
+                    help="edge loss ~ U[0, x] of the lossy C3 run reported beside the headline "
+                         "(its packet events per step show the decay); 0 skips it")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-seconds", type=float, default=1.0,
-                    help="steady-state simulated seconds the oracle is timed over")
-    ap.add_argument("--cpu-sample-hosts", type=int, default=2000,
-                    help="hosts (= vertices) of the CPU sample instance of the same workload")
+    ap.add_argument("--cpu-sample-steps", type=int, default=0,
+                    help="timed steps the CPU baseline runs (0 = all of them: the same window as value)")
     ap.add_argument("--exchange", choices=["rccl", "torch"], default="rccl",
                     help="N > 1: rccl = shd_xgroup (device-driven rounds, one fixed-size RCCL all-to-all "
                          "per round); torch = driver.DistCluster (host-driven, torch.distributed)")
@@ -194,9 +197,13 @@ def main():
                 "avg_in_kernel_us": round(kms_all / max(launches, 1) * 1e3, 3),
                 "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1)}
 
+    lossy = None
+    if world == 1 and args.lossy_edge_loss_max > 0 and not use_group:
+        lossy = lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, torch)
+
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline = cpu_leg(args, S, W)
+        cpu_baseline = cpu_leg(args, S, W, g, host_vertex, step, value)
 
     if rank == 0:
         out = {
@@ -212,7 +219,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (random geometric topology + PHOLD-UDP traffic, seed %d)" % args.seed,
-            "config": {"workload": "C3 PHOLD-UDP (N x %d hosts, %d-vertex geometric topology)"
+            "config": {"workload": "C3 PHOLD-UDP, stationary population (N x %d hosts, %d-vertex geometric topology)"
                                    % (args.hosts_per_gpu, V),
                        "edge_loss": "U[0,%g]" % args.edge_loss_max,
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
@@ -232,6 +239,7 @@ def main():
                      "max_hops": int(info.max_hops), "ties": int(info.n_ties)},
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
+            "lossy_c3": lossy,
         }
         sys.stdout.flush()
         os.dup2(_STDOUT_FD, 1)   # the JSON line is the only thing on stdout
@@ -242,6 +250,34 @@ def main():
     pc.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, torch):
+    """The same C3 workload with edge loss U[0, --lossy-edge-loss-max], timed
+    step by step: PHOLD never regenerates a lost message, so the population
+    and the rate decay with simulated time (reported per step, never `value`)."""
+    g = W.geometric_graph(args.vertices, seed=args.seed, loss_max=args.lossy_edge_loss_max)
+    model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load,
+                          payload=args.payload)
+    pc = PathCache(g, W.attached_vertices(host_vertex), device=dev)
+    eng = Engine(model, pc, device=dev)
+    eng.boot()
+    eng.run_until(args.warmup * step)
+    per_step, tot_pkt, tot_s = [], 0, 0.0
+    for k in range(args.steps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st = eng.run_until((args.warmup + k + 1) * step)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        per_step.append(int(st.n_pkt_events))
+        tot_pkt += st.n_pkt_events
+        tot_s += dt
+    eng.close()
+    pc.close()
+    return {"edge_loss": "U[0,%g]" % args.lossy_edge_loss_max, "value": round(tot_pkt / tot_s, 1),
+            "unit": "packet events/s", "packet_events_per_step": per_step,
+            "note": "lost messages are never regenerated: the rate depends on the simulated window"}
 
 
 def pmc_traffic(kernel):
@@ -260,12 +296,30 @@ def pmc_traffic(kernel):
     return prof.get("hbm_bytes_per_dispatch")
 
 
-def cpu_leg(args, S, W):
-    """The oracle's serial loop (the reference's --workers 0 semantics) timed
-    on this host, one core, on a bounded sample of the same workload family:
-    a --cpu-sample-hosts instance (hosts = vertices, same load and message
-    size), timed over --cpu-sample-seconds of steady state after the warm-up
-    (which includes the reference's lazy Dijkstra rows)."""
+def cpu_threads():
+    """Host cores to use: the box's CPU share (OMP_NUM_THREADS is set to it on
+    the GPU box), else the affinity mask."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, n or min(len(os.sched_getaffinity(0)), 16))
+
+
+def cpu_leg(args, S, W, g, host_vertex, step, value):
+    """The reference's scheduler semantics on the host cores, on the SAME
+    workload and simulated window as `value` (oracle.h o_baseline): one
+    warm-up to t = warmup steps (Dijkstra rows on all cores, then the serial
+    loop: boot, application start, lazy path cache), then the timed window
+    [warmup, warmup + steps) run twice from that state --
+      * serially on 1 core (--workers 0: one global queue, slave.c:415-428);
+      * in parallel rounds on `cores` threads, host-steal style
+        (scheduler_policy_host_steal.c:227-431; per-host queues, hosts pulled
+        in chunks, windows W <= every path latency so nothing is clamped and
+        the result is the serial one; first touches resolved at each round's
+        end in serial order) --
+    and both end states compared bit for bit.  --cpu-sample-steps bounds the
+    window (default: all timed steps)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     try:
         import oracle_ffi as O
@@ -273,35 +327,33 @@ def cpu_leg(args, S, W):
     except Exception as ex:   # the checker is absent: report it, never substitute
         return {"value": None, "unit": "packet events/s", "cores": 1, "kind": "port",
                 "sample": f"oracle unavailable: {ex}"}
-    step = args.step_ms * S.SHD_MS
-    n = min(args.cpu_sample_hosts, args.vertices)
-    g = W.geometric_graph(n, seed=args.seed, loss_max=args.edge_loss_max)
-    hv = W.hosts_on_vertices(n, 1)
-    mark = args.warmup * step
-    end = mark + int(args.cpu_sample_seconds * S.SHD_SEC)
-    m = W.phold_model(hv, end_time=end, seed=args.seed, load=args.load, payload=args.payload)
-    _, _, st = O.engine_run(m, g, mark=mark)
-    dt = (st["wall_ms"] - st["mark_wall_ms"]) * 1e-3
-    pkt = st["n_pkt_events"] - st["mark_pkt_events"]
-    # APSP CPU rate on the full-size topology: restated igraph Dijkstra rows, 1 core
-    gfull = W.geometric_graph(args.vertices, seed=args.seed, loss_max=args.edge_loss_max)
-    og = O.OGraph(gfull)
-    att = np.arange(args.vertices, dtype=np.int32)
-    t0 = time.perf_counter()
-    nrows = 16
-    for s in att[:nrows]:
-        og.row(int(s), att, count_ties=False)
-    ms_row = (time.perf_counter() - t0) * 1e3 / nrows
-    return {"value": round(pkt / dt, 1) if dt > 0 else None, "unit": "packet events/s", "cores": 1,
-            "kind": "port",
-            "sample": "oracle serial loop (reference --workers 0 semantics) on a %d-host instance of the "
-                      "same PHOLD-UDP workload (load %d), steady state over simulated [%.1f s, %.1f s): "
-                      "%d packet events in %.2f s (all events %d)"
-                      % (n, args.load, mark / 1e9, end / 1e9, pkt, dt, st["n_events"] - st["mark_events"]),
-            "warmup_wall_s": round(st["mark_wall_ms"] * 1e-3, 2),
-            "apsp_ms_per_row": round(ms_row, 3),
-            "apsp_rows": int(args.vertices),
-            "apsp_all_rows_s_extrapolated": round(ms_row * args.vertices / 1e3, 2)}
+    n_steps = args.steps if args.cpu_sample_steps <= 0 else min(args.steps, args.cpu_sample_steps)
+    t_mark = args.warmup * step
+    t_end = t_mark + n_steps * step
+    m = W.phold_model(host_vertex, end_time=(args.warmup + args.steps) * step, seed=args.seed, load=args.load,
+                      payload=args.payload)
+    thr = cpu_threads()
+    b = O.baseline(m, g, t_mark, t_end, thr)
+    ser = b["serial_pkt_events"] / (b["serial_ms"] * 1e-3) if b["serial_ms"] > 0 else None
+    par = b["parallel_pkt_events"] / (b["parallel_ms"] * 1e-3) if b["parallel_ms"] > 0 else None
+    win = "simulated [%g s, %g s)" % (t_mark / 1e9, t_end / 1e9)
+    return {"value": round(ser, 1) if ser else None, "unit": "packet events/s", "cores": 1, "kind": "port",
+            "sample": "oracle serial loop (reference --workers 0 semantics) on the bench's own workload "
+                      "(%d hosts, %d-vertex graph, load %d) over %s: %d packet events in %.2f s"
+                      % (len(host_vertex), args.vertices, args.load, win, b["serial_pkt_events"],
+                         b["serial_ms"] * 1e-3),
+            "parallel": {"value": round(par, 1) if par else None, "cores": int(b["threads"]),
+                         "kind": "port",
+                         "sample": "same state, same window, parallel rounds (host-steal equivalent, W = %d ns, "
+                                   "%d rounds, %d first-touch sends resolved at round ends): %d packet events "
+                                   "in %.2f s" % (b["window_ns"], b["parallel_rounds"], b["parallel_first_touch"],
+                                                   b["parallel_pkt_events"], b["parallel_ms"] * 1e-3),
+                         "same_end_state_as_serial": bool(b["same_end_state"]),
+                         "ambiguous_first_touches": int(b["ambiguous"])},
+            "gpu_over_cpu_1core": round(value / ser, 1) if ser else None,
+            "gpu_over_cpu_parallel": round(value / par, 1) if par else None,
+            "warmup_s": round((b["rows_ms"] + b["warmup_ms"]) * 1e-3, 2),
+            "apsp_rows_all_cores_s": round(b["rows_ms"] * 1e-3, 2)}
 
 
 if __name__ == "__main__":

@@ -119,6 +119,10 @@ typedef struct shd_config_host {
     uint64_t bw_down_kibps; /* 0 = take the attached vertex's bandwidth (host.c:183-189) */
     uint64_t bw_up_kibps;
     uint64_t heartbeat_s;   /* 0 = the option default */
+    int32_t n_processes;    /* <process> / <application> children, document order */
+    int32_t _pad;
+    uint64_t* process_start_s;   /* [n_processes] starttime (or legacy time), seconds
+                                  * (configuration.c:576-579; master.c:299 scales by 1 s) */
 } shd_config_host;
 typedef struct shd_config {
     int32_t n_hosts;
@@ -203,6 +207,9 @@ int shd_pc_packet_count(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex, uint
 /* master_updateMinTimeJump / _master_getMinTimeJump (master.c:133-159):
  * (u64)floor(min stored latency ms) * 1e6 ns, 10 ms default if 0, >= runahead */
 int shd_pc_min_time_jump(shd_pc* pc, uint64_t runahead_ns, uint64_t* jump_ns);
+/* the topology's minimumPathLatency (ms) over the entries stored so far
+ * (topology.c:1374-1378); 0 before any (the value worker_updateMinTimeJump gets) */
+int shd_pc_min_stored_latency(shd_pc* pc, double* ms);
 void shd_pc_destroy(shd_pc* pc);
 
 /* ------------------------------------------------------------ RNG / seeds */
@@ -221,6 +228,12 @@ int shd_topology_attach(const shd_graphml* gm, uint32_t* host_rng_state, const c
                         const char* citycode_hint, const char* countrycode_hint,
                         const char* geocode_hint, const char* type_hint,
                         int32_t* vertex_out, uint64_t* bw_down_out, uint64_t* bw_up_out);
+/* the same with the caller's RNG: next_double(rng) is the host's
+ * random_nextDouble (random.c:39-43), drawn once when the pick is random */
+int shd_topology_attach_cb(const shd_graphml* gm, double (*next_double)(void*), void* rng,
+                           const char* ip_hint, const char* citycode_hint, const char* countrycode_hint,
+                           const char* geocode_hint, const char* type_hint,
+                           int32_t* vertex_out, uint64_t* bw_down_out, uint64_t* bw_up_out);
 
 /* ------------------------------------------------------------ engine */
 /*
@@ -256,6 +269,16 @@ typedef struct shd_model {
     uint32_t codelq_cap;            /* per-host router queue capacity          */
     uint32_t txq_cap;               /* per-host interface send queue capacity  */
     uint32_t queue_flags;           /* SHD_QF_*: 0 = default (calendar + heap) */
+    /* Per-host variants (NULL / 0 = the scalar above for every host).  Each PHOLD
+     * process reads its own weights file (test_phold.c:341-356, per-process
+     * arguments), so hosts of different classes draw destinations from
+     * different cumulative weights: dest_cum is then [n_classes][H] and
+     * host_class[h] picks the row (the Tor-scale model: relays and clients). */
+    const uint8_t* host_class;      /* [H] or NULL (every host class 0)        */
+    int32_t n_classes;              /* rows of dest_cum (0 = 1)                */
+    int32_t _pad1;
+    /* <host heartbeatfrequency> per host (ns), tracker interval (host.c:240) */
+    const uint64_t* host_heartbeat; /* [H] or NULL                             */
 } shd_model;
 
 /* queue_flags: SHD_QF_NO_CALENDAR routes every inter-host event through the
@@ -266,7 +289,11 @@ enum { SHD_QF_NO_CALENDAR = 1,
        SHD_QF_COUNT_PATHS = 2,
        /* keep every host's tracker node counters at each heartbeat (tracker_heartbeat,
         * tracker.c:566-611; read with shd_eng_heartbeats) */
-       SHD_QF_HEARTBEATS = 4 };
+       SHD_QF_HEARTBEATS = 4,
+       /* boot schedules no application start: the caller pushes each host's
+        * process start events (<process starttime>, process_schedule,
+        * process.c:1344) with shd_eng_push_events */
+       SHD_QF_NO_APP_START = 8 };
 
 /* one event (32 B): key (time, dst, src, seq) = event_compare, event.c:110-153 */
 typedef struct shd_event {
@@ -379,6 +406,15 @@ int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin, int32_t h
 int shd_eng_window(shd_eng* e, uint64_t* window_ns);
 /* host_boot for every local host (host.c:372-390) at t=0 */
 int shd_eng_boot(shd_eng* e);
+/* Events from the caller (event_new_ + scheduler_push, event.c:28-43,
+ * scheduler.c:342-357): after shd_eng_boot and before the rounds reach their
+ * times.  Only self events of kind SHD_EV_APP_START (src == dst, a host of this
+ * engine) are accepted; each consumes its host's next event ID on the device
+ * (the `seq` field is ignored), in array order per host -- the order
+ * process_schedule runs a host's processes at boot (host.c:372-390) -- and is
+ * dropped when its time is >= end_time.  SHD_EINVAL for anything else, or
+ * for a time before the engine's current simulated time. */
+int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n);
 /* one round [window_start, window_end) on this engine; remote-bound events are
  * kept in the outbox until shd_eng_take_remote */
 int shd_eng_run_round(shd_eng* e, uint64_t window_start, uint64_t window_end,
@@ -457,6 +493,25 @@ void shd_eng_destroy(shd_eng* e);
 typedef struct shd_xgroup shd_xgroup;
 /* RCCL unique id: rank 0 makes it, every rank passes the same bytes */
 int shd_xgroup_unique_id(uint8_t id[SHD_XID_BYTES]);
+/* Communicators of a group, one per process:
+ *   rccl  one process per GPU, RCCL over xGMI (id from shd_xgroup_unique_id);
+ *   host  processes of one machine meeting in a POSIX shared-memory segment
+ *         named `name` (unique per group), device buffers staged through host
+ *         memory: several ranks may share one GPU, which RCCL refuses.
+ * A communicator serves the sharded path-cache build and an engine group. */
+typedef struct shd_comm shd_comm;
+int shd_comm_create_rccl(const uint8_t id[SHD_XID_BYTES], int world, int rank, int device, shd_comm** out);
+int shd_comm_create_host(const char* name, int world, int rank, int device, shd_comm** out);
+int shd_comm_rank(const shd_comm* c, int* rank, int* world);
+void shd_comm_destroy(shd_comm* c);
+/* The path cache's source rows sharded over the communicator's ranks: rank r
+ * computes rows [r*R, (r+1)*R) with R = ceil(T / world), then every rank
+ * all-gathers the row blocks into its full table (north_star: APSP sharded by
+ * source rows).  Same tables as shd_pc_build; build_ms_* time this rank's
+ * kernels, shd_pc_info.build_ms_device the whole call (exchange included). */
+int shd_pc_build_sharded(shd_pc* pc, shd_comm* comm);
+/* an engine group over a communicator (not owned: destroy it after the group) */
+int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out);
 /* block_events: events per peer block per round (0 = default) */
 int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
                            uint32_t block_events, shd_xgroup** out);

@@ -260,6 +260,11 @@ struct o_topo {
     double min_latency;
     int32_t rows_run, self_run;
     int32_t force_rows;
+    /* optional precomputed source rows by vertex (o_topo_set_row_cache): the
+     * values _topology_computeSourcePaths would compute (order-independent),
+     * NaN latency where computePathProperties fails; [V] pointers or NULL */
+    double** row_lat;
+    double** row_rel;
 };
 
 static uint64_t hkey(int32_t s, int32_t d) { return ((uint64_t)(uint32_t)s << 32) | (uint32_t)d; }
@@ -330,7 +335,13 @@ static int compute_source_paths(o_topo* t, int32_t s, int32_t d) {
     double* lat = malloc(sizeof(double) * t->nt);
     double* rel = malloc(sizeof(double) * t->nt);
     int32_t* ok = malloc(sizeof(int32_t) * t->nt);
-    o_sssp_row(t->g, s, t->targets, t->nt, lat, rel, ok, NULL, NULL);
+    if (t->row_lat && t->row_lat[s]) {
+        for (int32_t j = 0; j < t->nt; j++) {
+            lat[j] = t->row_lat[s][j]; rel[j] = t->row_rel[s][j]; ok[j] = !isnan(lat[j]);
+        }
+    } else {
+        o_sssp_row(t->g, s, t->targets, t->nt, lat, rel, ok, NULL, NULL);
+    }
     t->rows_run++;
     int all = 1;
     for (int32_t j = 0; j < t->nt; j++) {
@@ -384,3 +395,29 @@ uint64_t o_topo_stored_count(o_topo* t, int32_t s, int32_t d) {
 double o_topo_min_latency(o_topo* t) { return t->min_latency; }
 int32_t o_topo_rows_run(o_topo* t) { return t->rows_run; }
 int32_t o_topo_self_run(o_topo* t) { return t->self_run; }
+
+/* ---------------- support for the parallel baseline (o_baseline.c) ---------------- */
+void o_topo_set_row_cache(o_topo* t, double** row_lat, double** row_rel) { t->row_lat = row_lat; t->row_rel = row_rel; }
+int32_t o_topo_n_targets(const o_topo* t) { return t->nt; }
+const int32_t* o_topo_targets(const o_topo* t) { return t->targets; }
+int o_topo_is_complete(const o_topo* t) { return t->props.is_complete; }
+
+/* read-only lookup (no row runs, no stores; safe for concurrent readers): 1
+ * and the stored value when the pair has an entry in either orientation */
+int o_topo_peek(const o_topo* t, int32_t s, int32_t d, double* lat, double* rel) {
+    slot_t* p = tab_find((o_topo*)t, s, d);
+    if (!p && !t->g->directed) p = tab_find((o_topo*)t, d, s);
+    if (!p) return 0;
+    *lat = p->lat; *rel = p->rel;
+    return 1;
+}
+
+o_topo* o_topo_clone(const o_topo* t) {
+    o_topo* c = malloc(sizeof(*c));
+    *c = *t;
+    c->targets = malloc(sizeof(int32_t) * (t->nt + 1));
+    memcpy(c->targets, t->targets, sizeof(int32_t) * t->nt);
+    c->tab = malloc(sizeof(slot_t) * t->cap);
+    memcpy(c->tab, t->tab, sizeof(slot_t) * t->cap);
+    return c;
+}

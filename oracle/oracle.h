@@ -78,6 +78,14 @@ typedef struct o_topo o_topo;
 o_topo* o_topo_new(const o_graph* g, const int32_t* attached, int32_t n_attached,
                    int32_t force_rows);
 void o_topo_free(o_topo* t);
+/* precomputed rows by vertex ([V] pointers, NaN latency = no path) */
+void o_topo_set_row_cache(o_topo* t, double** row_lat, double** row_rel);
+int32_t o_topo_n_targets(const o_topo* t);
+const int32_t* o_topo_targets(const o_topo* t);
+int o_topo_is_complete(const o_topo* t);
+/* read-only: 1 and the value when the pair has an entry in either orientation */
+int o_topo_peek(const o_topo* t, int32_t s, int32_t d, double* lat, double* rel);
+o_topo* o_topo_clone(const o_topo* t);
 /* _topology_getPathEntry (topology.c:1969-2051) -> path latency/reliability;
  * returns 0 and -1/-1 when the reference returns NULL */
 int o_topo_get(o_topo* t, int32_t s, int32_t d, double* lat, double* rel);
@@ -122,12 +130,50 @@ typedef struct o_run {
     uint64_t mark_events, mark_pkt_events;
     double mark_wall_ms;
 } o_run;
+/* events pushed by the caller after boot (shd_eng_push_events semantics) */
+void o_engine_set_pushes(const shd_event* ev, uint64_t n);
 /* steady-state timing: record counters/wall time when sim time reaches t */
 void o_engine_set_mark(uint64_t t);
 /* serial mode (--workers 0): one global queue ordered by event_compare,
  * one round to end_time (slave.c:415-428) */
 int o_engine_run(const shd_model* m, const shd_graph* g, int32_t force_rows, o_run* out);
 void o_run_free(o_run* r);
+
+/* ---- engine state: the serial loop in steps, parallel rounds, clones ---- */
+typedef struct o_state o_state;
+typedef struct o_par_stats {
+    uint64_t rounds, n_events, n_pkt_events, first_touch_sends, ambiguous, window_ns;
+    double wall_ms;
+    int32_t threads, _pad;
+} o_par_stats;
+o_state* o_state_new(const shd_model* m, const shd_graph* g, int32_t force_rows);
+/* precompute every attached vertex's source row on `threads` cores */
+void o_state_rows(o_state* s, int threads);
+/* the serial loop (one global queue) while the next event is before t_until */
+void o_state_run_serial(o_state* s, uint64_t t_until);
+/* the same window in parallel rounds of W (W <= every path latency, so the
+ * result is the serial run's): hosts in chunks over `threads` cores, each host
+ * its own queue (scheduler_policy_host_steal.c:227-431 without the clamp);
+ * first touches of a round resolved at its end in serial order.  -1 for
+ * directed graphs or a traced model. */
+int o_state_run_parallel(o_state* s, uint64_t t_until, int threads, o_par_stats* st);
+o_state* o_state_clone(const o_state* s);
+void o_state_digest(const o_state* s, shd_host_digest* out);   /* [H] */
+const o_run* o_state_stats(const o_state* s);
+void o_state_free(o_state* s);
+
+/* the bench's CPU baseline (bench.py cpu_baseline): warm up to t_mark, then
+ * time [t_mark, t_end) serially on one core and in parallel rounds on
+ * `threads` cores from the same state; same_end_state = 1 when both end
+ * states are equal bit for bit */
+typedef struct o_baseline_out {
+    double rows_ms, warmup_ms, serial_ms, parallel_ms;
+    uint64_t serial_events, serial_pkt_events, parallel_events, parallel_pkt_events;
+    uint64_t parallel_rounds, parallel_first_touch, ambiguous, window_ns;
+    int32_t threads, same_end_state;
+} o_baseline_out;
+int o_baseline(const shd_model* m, const shd_graph* g, uint64_t t_mark, uint64_t t_end, int threads,
+               o_baseline_out* out);
 
 /* ---- reference priority order (event.c:110-153) as a checker ---- */
 int o_event_compare(const shd_event* a, const shd_event* b);

@@ -212,13 +212,16 @@ struct ParamsT {
     Ptr<TxEnt> tq;
     // global host tables (all H hosts)
     Ptr<const int32_t> host_att;     // attached index of every host
+    // destination weights per class (each PHOLD process reads its own weights
+    // file): row c of dest_cum / dest_guide is class c's, [n_cls][H]
     Ptr<const double> dest_cum;
-    Ptr<const DestGuide> dest_guide;   // [H]: bucket k -> first i with dest_cum[i] >= k / H
-    // destination draws as rand_r values x (r = x / RAND_MAX): there is a
-    // destination iff x <= dst_thr; host h's own draws (loopback) are
-    // self_thr[h].x <= x <= self_thr[h].y (precomputed, exact)
-    int32_t dst_thr;
-    Ptr<const int2> self_thr;
+    Ptr<const DestGuide> dest_guide;   // [n_cls][H]: bucket k -> first i with dest_cum[i] >= k / H
+    // destination draws as rand_r values x (r = x / RAND_MAX), per host h:
+    // there is a destination iff x <= self_thr[h].z; its own draws (loopback)
+    // are self_thr[h].x <= x <= self_thr[h].y (precomputed, exact); .w = class
+    Ptr<const int4> self_thr;
+    Ptr<const uint64_t> host_hb;     // per-host heartbeat interval [H] (null: `heartbeat`)
+    int32_t no_app_start;            // SHD_QF_NO_APP_START: boot schedules no application start
     // closed-form destinations (dest_closed): even weights, host h attached
     // at index h.  The draw x picks host max(ceil(x*H/RAND_MAX) - 1, 0),
     // except at the listed draws (where the f64 cumulative sums round across
@@ -366,7 +369,6 @@ __device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
 struct HotK {
     uint64_t end_time, boot_end;
     uint32_t pkt_len, cq_cap, tq_cap, evq_cap, trace;
-    int32_t dst_thr;
 };
 template <class T>
 __device__ __forceinline__ T launder(T x) {
@@ -398,6 +400,8 @@ struct HostCtx {
     uint32_t ns;                // deferred sends (s_send)
     uint64_t seq_base;          // ev_seq at the last flush: IDs >= it are provisional
     int32_t self_lo, self_hi;   // loopback draws (Params::self_thr)
+    int32_t dst_thr;            // draws with a destination: x <= dst_thr (this host's weights)
+    uint32_t cls;               // destination-weight class
     uint32_t w_msgs;            // the executing event's remaining work (run_work): messages, W_* steps
     uint32_t w_fl;
     uint64_t tt0, tt1, tt2;     // timer times (kInf = empty): heartbeat, refill, notify
@@ -548,6 +552,12 @@ __device__ __forceinline__ void trace(const DParams& P, HostCtx& c, uint64_t t, 
 
 __device__ __forceinline__ bool bootstrapping(const DParams& P, const HostCtx& c) { return c.now < c.k.boot_end; }
 
+// the tracker interval of host h (<host heartbeatfrequency>, host.c:240; the
+// option default otherwise)
+__device__ __forceinline__ uint64_t hb_interval(const DParams& P, uint32_t h) {
+    return P.host_hb ? P.host_hb[h] : P.heartbeat;
+}
+
 __device__ __forceinline__ void hot_load(const DParams& P, HostCtx& c) {
     c.k.end_time = launder(P.end_time);
     c.k.boot_end = launder(P.bootstrap_end);
@@ -556,7 +566,6 @@ __device__ __forceinline__ void hot_load(const DParams& P, HostCtx& c) {
     c.k.tq_cap = launder(P.tq_cap);
     c.k.evq_cap = launder(P.evq_cap);
     c.k.trace = launder(P.trace);
-    c.k.dst_thr = launder(P.dst_thr);
 }
 
 // event_new_ (consumes the source's event ID, event.c:38) + scheduler_push
@@ -871,6 +880,7 @@ __shared__ SendRec s_send[kSendCap * kBlock];    // deferred sends
 __shared__ shd_event s_res[kSendCap * kBlock];   // flush: resolved sends, then the events to deliver
 __shared__ uint16_t s_idx[kSendCap * kBlock];    // flush: record -> (lane << 4) | slot
 __shared__ int32_t s_att[kBlock];                // flush: each lane's attached vertex
+__shared__ uint32_t s_cls[kBlock];               // flush: each lane's destination-weight class
 
 // loopback test of a destination draw (network_interface.c:548-555): the
 // first i with dest_cum[i] >= r = x / RAND_MAX is this host, i.e.
@@ -894,8 +904,9 @@ __device__ __forceinline__ double u2d(uint32_t lo, uint32_t hi) {
 // the guide entry is passed as its three 16-B vectors (a struct chosen from
 // by index would be put in scratch): g0 = {i, att[0..2]}, g1 = {cum[0], cum[1]},
 // g2 = {cum[2], pad}
-__device__ __forceinline__ void guide_pick(const DParams& P, uint4 g0, uint4 g1, uint4 g2, double r, int32_t& dst,
-                                           int32_t& att) {
+template <class CumPtr>
+__device__ __forceinline__ void guide_pick(const DParams& P, CumPtr cum, uint4 g0, uint4 g1, uint4 g2, double r,
+                                           int32_t& dst, int32_t& att) {
     const bool f0 = u2d(g1.x, g1.y) >= r, f1 = u2d(g1.z, g1.w) >= r, f2 = u2d(g2.x, g2.y) >= r;
     if (f0 || f1 || f2) {
         dst = (int32_t)g0.x + (f0 ? 0 : f1 ? 1 : 2);
@@ -905,7 +916,7 @@ __device__ __forceinline__ void guide_pick(const DParams& P, uint4 g0, uint4 g1,
     int32_t lo = (int32_t)g0.x + 3, hi = P.H;
     while (lo < hi) {
         const int32_t mid = lo + ((hi - lo) >> 1);
-        if (P.dest_cum[mid] >= r) hi = mid; else lo = mid + 1;
+        if (cum[mid] >= r) hi = mid; else lo = mid + 1;
     }
     dst = lo;
     att = P.host_att[lo];
@@ -956,6 +967,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     const bool one = defer && total <= (uint32_t)kBlock;   // the round's last flush, one batch
     for (uint32_t i = 0; i < n; i++) s_idx[pre + i] = (uint16_t)((lane << 4) | i);
     s_att[lane] = c.att;
+    s_cls[lane] = c.cls;
     __syncthreads();
 #ifdef SHD_TIMING_LIGHT
     TIM(12);
@@ -980,9 +992,10 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             b = d;
         } else {
             const double rr = (double)q.r / kRandMax;
-            const uint4* gq = (const uint4*)(P.dest_guide + guide_index(P, rr));
+            const size_t row = (size_t)s_cls[hl] * (size_t)P.H;
+            const uint4* gq = (const uint4*)(P.dest_guide + row + guide_index(P, rr));
             const uint4 g0 = gq[0], g1 = gq[1], g2 = gq[2];
-            guide_pick(P, g0, g1, g2, rr, dst, b);
+            guide_pick(P, P.dest_cum + row, g0, g1, g2, rr, dst, b);
         }
         PathRaw x;
         int32_t ra_l = P.rank[a];
@@ -1175,7 +1188,7 @@ __device__ bool enqueue_new_message(const DParams& P, HostCtx& c) {
     PROF_T0(tp)
     const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
     PROF_ADD(c, PR_PICK, tp)
-    if ((int32_t)rv > c.k.dst_thr) return false;   // no i with dest_cum[i] >= r
+    if ((int32_t)rv > c.dst_thr) return false;   // no i with dest_cum[i] >= r
     random_free_port(c);
     const uint32_t pkt = c.pkt_seq++;
     if (c.tq_count >= c.k.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
@@ -1260,7 +1273,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         c.flags &= ~F_NOTIFY_PENDING;
         c.unread = 0;
         const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
-        if ((int32_t)rv <= c.k.dst_thr) {   // else no destination: nothing queued
+        if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
             random_free_port(c);
             const uint32_t pkt = c.pkt_seq++;
             if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
@@ -1298,10 +1311,10 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         // tracker_heartbeat (tracker.c:566-611): the node counters at the k-th
         // heartbeat, cumulative (the reader takes the per-interval differences)
         if (P.hb) {
-            const uint64_t k = c.now / P.heartbeat;
+            const uint64_t k = c.now / hb_interval(P, c.h);
             if (k >= 1 && k <= P.hb_k) P.hb[(size_t)c.l * P.hb_k + (k - 1)] = make_uint2(c.if_in, c.if_out);
         }
-        schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);
+        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, c.h), 0);
         break;
     case SHD_EV_REFILL:
         // _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
@@ -1385,7 +1398,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap && !boot) {
         const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
         c.w_msgs--;
-        if ((int32_t)rv <= c.k.dst_thr) {   // else no destination: nothing queued
+        if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
             random_free_port(c);
             const uint32_t pkt = c.pkt_seq++;
             if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
@@ -1432,7 +1445,7 @@ __device__ bool run_work(const DParams& P, HostCtx& c) {
 // the host's state from its record (loaded by the caller, with the idle
 // test: one memory round trip for both) and the heap root
 __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l, const HostRec& r, int32_t att,
-                                         int2 st) {
+                                         int4 st) {
     // every field taken from the record is consumed here (launder): a load
     // still pending at the event loop would make each iteration, and the
     // code after the loop, wait for all the wave's outstanding stores (one
@@ -1465,6 +1478,8 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.w_msgs = 0; c.w_fl = 0;
     c.self_lo = launder(st.x);
     c.self_hi = launder(st.y);
+    c.dst_thr = launder(st.z);
+    c.cls = launder((uint32_t)st.w);
 }
 
 // earliest pending event of the host (timers and heap)
@@ -1736,10 +1751,10 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         load_ctx(P, c, l, r, P.host_att[h], P.self_thr[h]);
         c.now = 0;
         c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
-        schedule_self(P, c, SHD_EV_HEARTBEAT, P.heartbeat, 0);   // tracker_new, tracker.c:141,607-610
-        refill_cb(P, c);                                         // ethernet startRefilling
-        schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);        // loopback refill at +1 ms
-        schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
+        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, h), 0);   // tracker_new, tracker.c:141,607-610
+        refill_cb(P, c);                                               // ethernet startRefilling
+        schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);              // loopback refill at +1 ms
+        if (!P.no_app_start) schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
         store_ctx(P, c);
         next = host_next(c);
         err |= c.err;
@@ -1816,7 +1831,7 @@ struct RoundArgsT {
     Ptr<const uint32_t> nin0, nin1;
     Ptr<const uint32_t> bits;   // null: no calendar
     Ptr<const int32_t> att;     // host_att + h0
-    Ptr<const int2> st;         // self_thr + h0
+    Ptr<const int4> st;         // self_thr + h0
     Ptr<const uint32_t> halt;
     int32_t nloc, hpw;
 };
@@ -1844,7 +1859,7 @@ struct HostIn {
     uint32_t w[kNBW];
     HostRec rec;
     int32_t att;
-    int2 st;
+    int4 st;
 };
 // every lane loads (lanes past the last host read the last host's entries
 // and ignore them): no branch, so no wait at a join before other loads issue
@@ -1894,7 +1909,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     uint32_t wbits = 0;   // bit j: window bin j is non-empty
     const HostRec& rec = in.rec;
     const int32_t rec_att = in.att;
-    const int2 rec_st = in.st;
+    const int4 rec_st = in.st;
     uint32_t nin0 = 0;
     if (l < P.nloc) {
         nin0 = parity ? in.nin[1] : in.nin[0];
@@ -1947,7 +1962,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
     hot_load(P, c);
     PendDel pd;
-    c.ns = 0; c.att = 0; c.err = 0;
+    c.ns = 0; c.att = 0; c.cls = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
     if (active) {
         PROF_T0(t_all)
@@ -2510,6 +2525,33 @@ __global__ void k_ingest(DParams P, const shd_event* __restrict__ ev, uint64_t n
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
 }
 
+// caller-pushed self events (shd_eng_push_events): one thread per host with
+// pushed events, in array order.  event_new_ consumes the host's next event ID
+// (event.c:38); scheduler_push drops a time >= end (scheduler.c:346-349); the
+// rest go to the inbox the next round merges into the host's heap
+__global__ void k_push(DParams P, const shd_event* __restrict__ ev, const uint32_t* __restrict__ grp_off,
+                       uint32_t ngrp, int parity) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ngrp) return;
+    const uint32_t b = grp_off[g], en = grp_off[g + 1];
+    const int32_t dl = (int32_t)ev[b].dst - P.h0;
+    uint64_t seq = P.hs[dl].ev_seq;
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    for (uint32_t i = b; i < en; i++) {
+        shd_event e = ev[i];
+        e.seq = seq++;
+        if (e.time >= P.end_time) continue;
+        const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+        if (slot >= P.inbox_cap) { err |= SHD_ERR_INBOX_OVERFLOW; continue; }
+        P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+        next = e.time < next ? e.time : next;
+    }
+    P.hs[dl].ev_seq = seq;
+    if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+    if (err) atomicOr(&P.sum->error, err);
+}
+
 // ---- exchange mode kernels (shd_xgroup) ----
 // local transport: block d of sender s -> block s of receiver d, header plus
 // the counted events only; grid (slots, receiver, sender)
@@ -2825,7 +2867,10 @@ struct shd_eng {
     int32_t* d_host_att = nullptr;
     double* d_cum = nullptr;
     DestGuide* d_guide = nullptr;
-    int2* d_self_thr = nullptr;
+    int4* d_self_thr = nullptr;
+    uint64_t* d_host_hb = nullptr;
+    int32_t n_cls = 1;
+    uint64_t t_done = 0;                    // end of the last executed round's window (push_events floor)
     int32_t* d_rank = nullptr;
     int32_t* d_self_rank = nullptr;
     DevSummary* d_sum = nullptr;
@@ -2898,6 +2943,19 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     if (!m->host_vertex || !m->host_rng || !m->bw_down_kibps || !m->bw_up_kibps || !m->dest_cum) return SHD_EINVAL;
     if (m->heartbeat_interval == 0) return SHD_EINVAL;
     const int32_t H = m->n_hosts;
+    // destination-weight classes: dest_cum is [n_cls][H], host_class picks the row
+    const int32_t n_cls = m->n_classes > 1 ? m->n_classes : 1;
+    if (n_cls > 1 && !m->host_class) return SHD_EINVAL;
+    if (n_cls > 256) return SHD_EINVAL;
+    if (m->host_class)
+        for (int32_t h = 0; h < H; h++)
+            if ((int32_t)m->host_class[h] >= n_cls) return SHD_EINVAL;
+    uint64_t hb_min = m->heartbeat_interval;
+    if (m->host_heartbeat)
+        for (int32_t h = 0; h < H; h++) {
+            if (m->host_heartbeat[h] == 0) return SHD_EINVAL;
+            hb_min = std::min<uint64_t>(hb_min, m->host_heartbeat[h]);
+        }
     // every host must sit on an attached vertex of the path cache
     std::vector<int32_t> host_att(H);
     std::vector<int32_t> hosts_on(pc->T, 0);
@@ -2953,23 +3011,30 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             return rc;
         }
     }
-    EALLOC(e->d_rng0, H); EALLOC(e->d_bwd, H); EALLOC(e->d_bwu, H); EALLOC(e->d_host_att, H); EALLOC(e->d_cum, H);
-    EALLOC(e->d_guide, H);
+    e->n_cls = n_cls;
+    const size_t HC = (size_t)H * (size_t)n_cls;
+    EALLOC(e->d_rng0, H); EALLOC(e->d_bwd, H); EALLOC(e->d_bwu, H); EALLOC(e->d_host_att, H); EALLOC(e->d_cum, HC);
+    EALLOC(e->d_guide, HC);
     EALLOC(e->d_self_thr, H);
-    // destination guide table: guide[k] = first i with cum[i] >= k / H (H if none)
-    std::vector<DestGuide> guide(H);
-    for (int32_t k = 0, i = 0; k < H; k++) {
-        const double t = (double)k / (double)H;
-        while (i < H && !(m->dest_cum[i] >= t)) i++;
-        guide[k].i = i;
-        guide[k].pad = 0;
-        for (int j = 0; j < 3; j++) {
-            guide[k].cum[j] = i + j < H ? m->dest_cum[i + j] : 2.0;
-            guide[k].att[j] = i + j < H ? host_att[i + j] : -1;
+    if (m->host_heartbeat) EALLOC(e->d_host_hb, H);
+    // destination guide table per class: guide[k] = first i with cum[i] >= k / H (H if none)
+    std::vector<DestGuide> guide(HC);
+    for (int32_t cl = 0; cl < n_cls; cl++) {
+        const double* cum = m->dest_cum + (size_t)cl * H;
+        DestGuide* gd = guide.data() + (size_t)cl * H;
+        for (int32_t k = 0, i = 0; k < H; k++) {
+            const double t = (double)k / (double)H;
+            while (i < H && !(cum[i] >= t)) i++;
+            gd[k].i = i;
+            gd[k].pad = 0;
+            for (int j = 0; j < 3; j++) {
+                gd[k].cum[j] = i + j < H ? cum[i + j] : 2.0;
+                gd[k].att[j] = i + j < H ? host_att[i + j] : -1;
+            }
         }
+        for (int32_t i = 1; i < H; i++)
+            if (!(cum[i] >= cum[i - 1])) { shd_eng_destroy(e); return SHD_EINVAL; }
     }
-    for (int32_t i = 1; i < H; i++)
-        if (!(m->dest_cum[i] >= m->dest_cum[i - 1])) { shd_eng_destroy(e); return SHD_EINVAL; }
     EALLOC(e->d_rank, pc->T); EALLOC(e->d_self_rank, pc->T);
     EALLOC(e->d_sum, 1);
     if (hipHostMalloc((void**)&e->h_sum, sizeof(DevSummary)) != hipSuccess) { shd_eng_destroy(e); return SHD_ENOMEM; }
@@ -3010,9 +3075,10 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         hipMemcpyAsync(e->d_bwd, m->bw_down_kibps, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(e->d_bwu, m->bw_up_kibps, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(e->d_host_att, host_att.data(), 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(e->d_cum, m->dest_cum, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
-        hipMemcpyAsync(e->d_guide, guide.data(), sizeof(DestGuide) * (size_t)H, hipMemcpyHostToDevice, s) !=
-            hipSuccess) {
+        hipMemcpyAsync(e->d_cum, m->dest_cum, 8 * HC, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(e->d_guide, guide.data(), sizeof(DestGuide) * HC, hipMemcpyHostToDevice, s) != hipSuccess ||
+        (m->host_heartbeat &&
+         hipMemcpyAsync(e->d_host_hb, m->host_heartbeat, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess)) {
         shd_eng_destroy(e);
         return SHD_ENODEV;
     }
@@ -3027,21 +3093,30 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.host_att = e->d_host_att;
     P.dest_cum = e->d_cum;
     P.dest_guide = e->d_guide;
+    P.host_hb = e->d_host_hb;
+    P.no_app_start = (m->queue_flags & SHD_QF_NO_APP_START) ? 1 : 0;
     // draw thresholds: x / RAND_MAX <= c  <=>  x <= draw_threshold(c)
     {
-        std::vector<int2> thr(H);
+        // per host, from its own class's cumulative weights
+        std::vector<int4> thr(H);
+        std::vector<int32_t> cls_dst_thr(n_cls);
+        for (int32_t cl = 0; cl < n_cls; cl++) cls_dst_thr[cl] = draw_threshold(m->dest_cum[(size_t)cl * H + H - 1]);
         for (int32_t h = 0; h < H; h++) {
-            thr[h].x = h ? draw_threshold(m->dest_cum[h - 1]) + 1 : 0;
-            thr[h].y = draw_threshold(m->dest_cum[h]);
+            const int32_t cl = m->host_class ? (int32_t)m->host_class[h] : 0;
+            const double* cum = m->dest_cum + (size_t)cl * H;
+            thr[h].x = h ? draw_threshold(cum[h - 1]) + 1 : 0;
+            thr[h].y = draw_threshold(cum[h]);
+            thr[h].z = cls_dst_thr[cl];
+            thr[h].w = cl;
         }
-        P.dst_thr = draw_threshold(m->dest_cum[H - 1]);
+        const int32_t dst_thr0 = cls_dst_thr[0];
         // closed-form destinations: host h at attached index h, thresholds
         // thr[i] = floor((i+1) R / H) but for a few i (the exceptions).  Both
         // pick functions are step functions of x changing only at thr[i]+1
         // and f(i)+1, so checking every such x (and 0) checks them all.
         {
             constexpr uint64_t R = 2147483647ull;
-            bool ok = getenv("SHD_NO_DEST_CLOSED") == nullptr;
+            bool ok = getenv("SHD_NO_DEST_CLOSED") == nullptr && n_cls == 1;
             for (int32_t h = 0; h < H && ok; h++) ok = host_att[h] == h;
             std::vector<int32_t> ty(H);
             for (int32_t i = 0; i < H; i++) ty[i] = thr[i].y;
@@ -3058,7 +3133,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
                 if (f(i) == ty[i]) continue;
                 const int64_t lo = std::min<int64_t>(f(i), ty[i]) + 1, hi = std::max<int64_t>(f(i), ty[i]);
                 for (int64_t x = lo; x <= hi && ok; x++) {
-                    if (x > P.dst_thr) break;
+                    if (x > dst_thr0) break;
                     const int32_t t = pick_true(x);
                     if (t != pick_closed(x)) {
                         if (exc.size() == (size_t)kDestExc) ok = false;
@@ -3073,12 +3148,12 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             };
             for (int32_t i = 0; i < H && ok; i++)
                 for (int64_t x : {(int64_t)0, (int64_t)ty[i] + 1, f(i) + 1})
-                    if (x <= P.dst_thr && pick_exc(x) != pick_true(x)) ok = false;
+                    if (x <= dst_thr0 && pick_exc(x) != pick_true(x)) ok = false;
             P.dest_closed = ok ? 1 : 0;
             P.n_exc = ok ? (int32_t)exc.size() : 0;
             for (size_t j = 0; j < exc.size() && ok; j++) { P.exc_x[j] = exc[j].first; P.exc_d[j] = exc[j].second; }
         }
-        if (hipMemcpyAsync(e->d_self_thr, thr.data(), sizeof(int2) * (size_t)H, hipMemcpyHostToDevice, e->stream) !=
+        if (hipMemcpyAsync(e->d_self_thr, thr.data(), sizeof(int4) * (size_t)H, hipMemcpyHostToDevice, e->stream) !=
                 hipSuccess ||
             hipStreamSynchronize(e->stream) != hipSuccess) {
             shd_eng_destroy(e);
@@ -3097,7 +3172,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     }
     if ((m->queue_flags & SHD_QF_HEARTBEATS) && m->end_time > 0) {
         // heartbeats at k * interval < end_time, k >= 1
-        const uint64_t k = (m->end_time - 1) / m->heartbeat_interval;
+        const uint64_t k = (m->end_time - 1) / hb_min;
         if (k > (1u << 20)) { shd_eng_destroy(e); return SHD_ERANGE; }
         P.hb_k = (uint32_t)k;
         e->heartbeats = true;
@@ -3211,6 +3286,59 @@ extern "C" int shd_eng_boot(shd_eng* e) {
     return SHD_OK;
 }
 
+extern "C" int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n) {
+    if (!e || (n && !ev)) return SHD_EINVAL;
+    if (!e->booted) return SHD_EINVAL;
+    if (!n) return SHD_OK;
+    if (n > (1u << 30)) return SHD_ERANGE;
+    for (uint64_t i = 0; i < n; i++) {
+        const shd_event& x = ev[i];
+        if (x.kind != SHD_EV_APP_START || x.src != x.dst || (int64_t)x.dst < e->h0 ||
+            (int64_t)x.dst >= (int64_t)e->h0 + e->nloc || x.time < e->t_done)
+            return SHD_EINVAL;
+    }
+    // stable grouping by host: a host's events keep their array order (its IDs)
+    std::vector<uint32_t> idx(n);
+    for (uint64_t i = 0; i < n; i++) idx[i] = (uint32_t)i;
+    std::stable_sort(idx.begin(), idx.end(), [ev](uint32_t a, uint32_t b) { return ev[a].dst < ev[b].dst; });
+    std::vector<shd_event> sorted(n);
+    std::vector<uint32_t> off;
+    for (uint64_t i = 0; i < n; i++) {
+        sorted[i] = ev[idx[i]];
+        sorted[i].pkt = 0;
+        if (i == 0 || sorted[i].dst != sorted[i - 1].dst) off.push_back((uint32_t)i);
+    }
+    off.push_back((uint32_t)n);
+    const uint32_t ngrp = (uint32_t)off.size() - 1;
+    SHD_HIP(hipSetDevice(e->device));
+    shd_event* d_ev = nullptr;
+    uint32_t* d_off = nullptr;
+    SHD_HIP(hipMalloc((void**)&d_ev, sizeof(shd_event) * n));
+    if (hipMalloc((void**)&d_off, 4 * off.size()) != hipSuccess) { (void)hipFree(d_ev); return SHD_ENOMEM; }
+    int rc = SHD_OK;
+    e->P.sum = e->d_sum;
+    if (hipMemcpyAsync(d_ev, sorted.data(), sizeof(shd_event) * n, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+        hipMemcpyAsync(d_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice, e->stream) != hipSuccess)
+        rc = SHD_ENODEV;
+    if (!rc) {
+        // the summary's next time is the loop's window start: seed it with the
+        // host view, the kernel lowers it to the earliest pushed time
+        e->h_sum->error = 0;
+        if (hipMemcpyAsync(e->d_sum, e->h_sum, sizeof(DevSummary), hipMemcpyHostToDevice, e->stream) != hipSuccess)
+            rc = SHD_ENODEV;
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(k_push, dim3((ngrp + 255) / 256), dim3(256), 0, e->stream, dp(e->P), (const shd_event*)d_ev,
+                           (const uint32_t*)d_off, ngrp, (int)(e->round & 1));
+        if (hipGetLastError() != hipSuccess) rc = SHD_ENODEV;
+    }
+    if (!rc) rc = read_summary(e);
+    (void)hipFree(d_ev);
+    (void)hipFree(d_off);
+    if (!rc && e->h_sum->error) rc = SHD_EOVERFLOW;
+    return rc;
+}
+
 // first-touch resolution in serial order: sort the logged queries
 // by the executing event's key, assign row ranks, finalize delivered sends
 // first-touch resolution in serial order (DESIGN.md "First-touch rule"): sort
@@ -3322,6 +3450,7 @@ extern "C" int shd_eng_end_round(shd_eng* e, shd_round_summary* out) {
     if (rc) return rc;
     e->parity ^= 1;
     e->round++;
+    e->t_done = std::max<uint64_t>(e->t_done, e->round_we);
     if (out) {
         out->window_start = e->round_ws; out->window_end = e->round_we;
         out->next_time = e->h_sum->next_time;
@@ -3588,6 +3717,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         e->tl_ready = !logged && !halt;
     }
     e->h_sum->next_time = next;
+    e->t_done = std::max<uint64_t>(e->t_done, s.final_time);
     s.n_pending_resolved = e->pending_resolved - pend0;
     s.device_ms_round_kernel = e->kernel_ms_total;
     s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -3785,11 +3915,9 @@ extern "C" void shd_eng_destroy(shd_eng* e) {
         }                                                                                            \
     } while (0)
 
-static_assert(sizeof(ncclUniqueId) == SHD_XID_BYTES, "RCCL unique id size");
-
 struct shd_xgroup {
-    bool rccl = false;
-    ncclComm_t comm = nullptr;
+    shd_comm* comm = nullptr;          // null: the local transport (engines of one process)
+    bool own_comm = false;             // created by shd_xgroup_create_rccl
     int world = 1;                     // engines in the group
     int rank0 = 0;                     // group rank of local engine 0
     std::vector<shd_eng*> engs;        // this process's engines, rank order
@@ -3846,9 +3974,10 @@ static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
 static int x_exchange(shd_xgroup* g) {
     const size_t bytes = g->stride * sizeof(shd_event);
     const int wi = (int)(g->xseq & 1);
-    if (g->rccl) {
+    if (g->comm) {
         shd_eng* e = g->engs[0];
-        SHD_NCCL(ncclAllToAll(g->loc[0].xsend, g->loc[0].xrecv[wi], bytes, ncclUint8, g->comm, e->stream));
+        const int rc = shd_comm_alltoall_dev(g->comm, g->loc[0].xsend, g->loc[0].xrecv[wi], bytes, e->stream);
+        if (rc) return rc;
     } else {
         const int n = g->world;
         for (int k = 0; k < n; k++) {
@@ -3907,48 +4036,23 @@ static int x_gather_pending(shd_xgroup* g, std::vector<shd_pending>& all) {
         mine.resize(at + n);
         if (n) SHD_HIP(hipMemcpy(mine.data() + at, e->P.pend, sizeof(shd_pending) * n, hipMemcpyDeviceToHost));
     }
-    if (!g->rccl) {
+    if (!g->comm) {
         all.swap(mine);
         return SHD_OK;
     }
-    shd_eng* e = g->engs[0];
-    unsigned long long* d_cnt = nullptr;
-    SHD_HIP(hipMalloc((void**)&d_cnt, 8 * (size_t)(g->world + 1)));
+    // every rank's count, then every rank's records (padded to the largest)
+    const int W = g->world;
     const unsigned long long my = mine.size();
-    std::vector<unsigned long long> cnt(g->world);
-    SHD_HIP(hipMemcpyAsync(d_cnt + g->world, &my, 8, hipMemcpyHostToDevice, e->stream));
-    ncclResult_t nr = ncclAllGather(d_cnt + g->world, d_cnt, 1, ncclUint64, g->comm, e->stream);
-    if (nr == ncclSuccess) {
-        (void)hipMemcpyAsync(cnt.data(), d_cnt, 8 * (size_t)g->world, hipMemcpyDeviceToHost, e->stream);
-        (void)hipStreamSynchronize(e->stream);
-    }
-    (void)hipFree(d_cnt);
-    if (nr != ncclSuccess) return SHD_ENODEV;
+    std::vector<unsigned long long> cnt(W);
+    int rc = shd_comm_allgather_host(g->comm, &my, 8, cnt.data());
+    if (rc) return rc;
     const unsigned long long mx = *std::max_element(cnt.begin(), cnt.end());
-    if (mx == 0) {
-        all.clear();
-        return SHD_OK;
-    }
-    const size_t blk = mx * sizeof(shd_pending);
-    char* d_buf = nullptr;
-    SHD_HIP(hipMalloc((void**)&d_buf, blk * (size_t)(g->world + 1)));
-    (void)hipMemsetAsync(d_buf + blk * g->world, 0, blk, e->stream);
-    if (!mine.empty())
-        (void)hipMemcpyAsync(d_buf + blk * g->world, mine.data(), sizeof(shd_pending) * mine.size(),
-                             hipMemcpyHostToDevice, e->stream);
-    std::vector<char> h(blk * (size_t)g->world);
-    nr = ncclAllGather(d_buf + blk * g->world, d_buf, blk, ncclUint8, g->comm, e->stream);
-    if (nr == ncclSuccess) {
-        (void)hipMemcpyAsync(h.data(), d_buf, h.size(), hipMemcpyDeviceToHost, e->stream);
-        (void)hipStreamSynchronize(e->stream);
-    }
-    (void)hipFree(d_buf);
-    if (nr != ncclSuccess) return SHD_ENODEV;
     all.clear();
-    for (int r = 0; r < g->world; r++) {
-        const shd_pending* p = (const shd_pending*)(h.data() + blk * r);
-        all.insert(all.end(), p, p + cnt[r]);
-    }
+    if (mx == 0) return SHD_OK;
+    std::vector<shd_pending> pad(mx), got((size_t)mx * W);
+    std::copy(mine.begin(), mine.end(), pad.begin());
+    if ((rc = shd_comm_allgather_host(g->comm, pad.data(), sizeof(shd_pending) * mx, got.data()))) return rc;
+    for (int r = 0; r < W; r++) all.insert(all.end(), got.begin() + (size_t)r * mx, got.begin() + (size_t)r * mx + cnt[r]);
     return SHD_OK;
 }
 
@@ -3983,7 +4087,7 @@ static int x_exchange_remote(shd_xgroup* g, int slot) {
         const unsigned long long z = 0;   // the spill is consumed
         SHD_HIP(hipMemcpy(&e->d_ring[slot].n_remote, &z, 8, hipMemcpyHostToDevice));
     }
-    if (!g->rccl) {
+    if (!g->comm) {
         for (int d = 0; d < nl; d++) {
             std::vector<shd_event> in;
             for (int s = 0; s < nl; s++) in.insert(in.end(), out[s][d].begin(), out[s][d].end());
@@ -4001,51 +4105,40 @@ static int x_exchange_remote(shd_xgroup* g, int slot) {
         }
         return SHD_OK;
     }
-    // RCCL: counts matrix, then one all-to-allv of the bucketed events
+    // a communicator (one engine per process): every rank's per-peer counts,
+    // then every rank's bucketed events (an all-to-all-v through an
+    // all-gather: spills are rare and small)
     shd_eng* e = g->engs[0];
-    const int W = g->world;
-    std::vector<unsigned long long> sc(W), all((size_t)W * W);
+    const int W = g->world, me = g->rank0;
+    std::vector<unsigned long long> sc(W), allc((size_t)W * W);
     for (int p = 0; p < W; p++) sc[p] = out[0][p].size();
-    unsigned long long* d_c = nullptr;
-    SHD_HIP(hipMalloc((void**)&d_c, 8 * (size_t)W * (W + 1)));
-    (void)hipMemcpyAsync(d_c + (size_t)W * W, sc.data(), 8 * (size_t)W, hipMemcpyHostToDevice, e->stream);
-    ncclResult_t nr = ncclAllGather(d_c + (size_t)W * W, d_c, W, ncclUint64, g->comm, e->stream);
-    if (nr == ncclSuccess) {
-        (void)hipMemcpyAsync(all.data(), d_c, 8 * (size_t)W * W, hipMemcpyDeviceToHost, e->stream);
-        (void)hipStreamSynchronize(e->stream);
+    int rc = shd_comm_allgather_host(g->comm, sc.data(), 8 * (size_t)W, allc.data());
+    if (rc) return rc;
+    unsigned long long mx = 0;
+    for (int r = 0; r < W; r++) {
+        unsigned long long t = 0;
+        for (int p = 0; p < W; p++) t += allc[(size_t)r * W + p];
+        mx = std::max(mx, t);
     }
-    (void)hipFree(d_c);
-    if (nr != ncclSuccess) return SHD_ENODEV;
-    const int me = g->rank0;
-    std::vector<size_t> scount(W), sdisp(W), rcount(W), rdisp(W);
-    size_t ns = 0, nrcv = 0;
-    for (int p = 0; p < W; p++) {
-        scount[p] = sc[p] * sizeof(shd_event);
-        sdisp[p] = ns;
-        ns += scount[p];
-        rcount[p] = all[(size_t)p * W + me] * sizeof(shd_event);
-        rdisp[p] = nrcv;
-        nrcv += rcount[p];
+    if (mx == 0) return SHD_OK;
+    std::vector<shd_event> flat(mx), got((size_t)mx * W);
+    size_t k = 0;
+    for (int p = 0; p < W; p++)
+        for (const shd_event& x : out[0][p]) flat[k++] = x;
+    if ((rc = shd_comm_allgather_host(g->comm, flat.data(), sizeof(shd_event) * mx, got.data()))) return rc;
+    std::vector<shd_event> in;
+    for (int r = 0; r < W; r++) {
+        size_t off = (size_t)r * mx;
+        for (int p = 0; p < me; p++) off += allc[(size_t)r * W + p];
+        in.insert(in.end(), got.begin() + off, got.begin() + off + allc[(size_t)r * W + me]);
     }
-    std::vector<shd_event> flat;
-    flat.reserve(ns / sizeof(shd_event));
-    for (int p = 0; p < W; p++) flat.insert(flat.end(), out[0][p].begin(), out[0][p].end());
-    char *d_s = nullptr, *d_r = nullptr;
-    SHD_HIP(hipMalloc((void**)&d_s, ns ? ns : 32));
-    if (hipMalloc((void**)&d_r, nrcv ? nrcv : 32) != hipSuccess) {
-        (void)hipFree(d_s);
-        return SHD_ENOMEM;
-    }
-    int rc = SHD_OK;
-    if (ns && hipMemcpyAsync(d_s, flat.data(), ns, hipMemcpyHostToDevice, e->stream) != hipSuccess) rc = SHD_ENODEV;
-    if (!rc && ncclAllToAllv(d_s, scount.data(), sdisp.data(), d_r, rcount.data(), rdisp.data(), ncclUint8, g->comm,
-                             e->stream) != ncclSuccess)
-        rc = SHD_ENODEV;
-    if (!rc) rc = x_ingest(e, xparams(g, 0, &e->d_ring[slot]), (const shd_event*)d_r, nrcv / sizeof(shd_event),
-                           (int)(e->round & 1));
+    if (in.empty()) return SHD_OK;
+    shd_event* d_ev = nullptr;
+    SHD_HIP(hipMalloc((void**)&d_ev, sizeof(shd_event) * in.size()));
+    if (hipMemcpy(d_ev, in.data(), sizeof(shd_event) * in.size(), hipMemcpyHostToDevice) != hipSuccess) rc = SHD_ENODEV;
+    if (!rc) rc = x_ingest(e, xparams(g, 0, &e->d_ring[slot]), d_ev, in.size(), (int)(e->round & 1));
     if (!rc && hipStreamSynchronize(e->stream) != hipSuccess) rc = SHD_ENODEV;
-    (void)hipFree(d_s);
-    (void)hipFree(d_r);
+    (void)hipFree(d_ev);
     return rc;
 }
 
@@ -4098,7 +4191,7 @@ static void x_drop_graphs(shd_xgroup* g) {
 static void x_free(shd_xgroup* g) {
     if (!g) return;
     x_drop_graphs(g);
-    if (g->comm) (void)ncclCommDestroy(g->comm);
+    if (g->comm && g->own_comm) shd_comm_destroy(g->comm);
     for (auto& ev : g->eev)
         if (ev) (void)hipEventDestroy(ev);
     if (g->xev) (void)hipEventDestroy(g->xev);
@@ -4141,38 +4234,23 @@ extern "C" int shd_xgroup_create_local(shd_eng* const* engines, int n, uint32_t 
     return SHD_OK;
 }
 
-extern "C" int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
-                                      uint32_t block_events, shd_xgroup** out) {
-    if (!e || !id || world <= 0 || world > 64 || rank < 0 || rank >= world || !out) return SHD_EINVAL;
+extern "C" int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out) {
+    if (!e || !comm || !out) return SHD_EINVAL;
+    const int world = comm->world, rank = comm->rank;
     const int64_t H = e->P.H;
     if (e->h0 != (int32_t)((H * rank) / world) || e->h0 + e->nloc != (int32_t)((H * (rank + 1)) / world))
         return SHD_EINVAL;
     SHD_HIP(hipSetDevice(e->device));
     shd_xgroup* g = new shd_xgroup();
-    g->rccl = true;
+    g->comm = comm;
     g->world = world;
     g->rank0 = rank;
     g->engs.push_back(e);
-    ncclUniqueId u;
-    memcpy(&u, id, SHD_XID_BYTES);
-    if (ncclCommInitRank(&g->comm, world, u, rank) != ncclSuccess) {
-        g->comm = nullptr;
-        x_free(g);
-        return SHD_ENODEV;
-    }
     // the group agrees on W (min) and checks the model: H and end time equal everywhere
-    unsigned long long* d = nullptr;
-    if (hipMalloc((void**)&d, 8 * (size_t)(3 * world + 3)) != hipSuccess) { x_free(g); return SHD_ENOMEM; }
     const unsigned long long mine[3] = {(unsigned long long)e->window, (unsigned long long)H,
                                         (unsigned long long)e->P.end_time};
     std::vector<unsigned long long> all(3 * (size_t)world);
-    int rc = SHD_OK;
-    if (hipMemcpy(d + 3 * world, mine, 24, hipMemcpyHostToDevice) != hipSuccess ||
-        ncclAllGather(d + 3 * world, d, 3, ncclUint64, g->comm, e->stream) != ncclSuccess ||
-        hipMemcpyAsync(all.data(), d, 24 * (size_t)world, hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
-        hipStreamSynchronize(e->stream) != hipSuccess)
-        rc = SHD_ENODEV;
-    (void)hipFree(d);
+    int rc = shd_comm_allgather_host(comm, mine, 24, all.data());
     if (rc) { x_free(g); return rc; }
     g->window = kInf;
     for (int r = 0; r < world; r++) {
@@ -4184,6 +4262,20 @@ extern "C" int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES
     g->fixed_cap = block_events != 0;
     if ((rc = x_alloc(g))) { x_free(g); return rc; }
     *out = g;
+    return SHD_OK;
+}
+
+extern "C" int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
+                                      uint32_t block_events, shd_xgroup** out) {
+    if (!e || !id || world <= 0 || world > 64 || rank < 0 || rank >= world || !out) return SHD_EINVAL;
+    const int64_t H = e->P.H;
+    if (e->h0 != (int32_t)((H * rank) / world) || e->h0 + e->nloc != (int32_t)((H * (rank + 1)) / world))
+        return SHD_EINVAL;
+    shd_comm* c = nullptr;
+    int rc = shd_comm_create_rccl(id, world, rank, e->device, &c);
+    if (rc) return rc;
+    if ((rc = shd_xgroup_create(e, c, block_events, out))) { shd_comm_destroy(c); return rc; }
+    (*out)->own_comm = true;
     return SHD_OK;
 }
 
@@ -4237,7 +4329,8 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
 // one engine per process); a capture that fails is not tried again
 static int x_launch_rounds(shd_xgroup* g, int nb) {
     static const bool no_graph = getenv("SHD_NO_GRAPH") != nullptr;
-    if (nb != shd_eng::kBatch || !g->rccl || g->engs.size() != 1 || g->graph_failed || no_graph)
+    if (nb != shd_eng::kBatch || !g->comm || g->comm->kind != SHD_COMM_RCCL || g->engs.size() != 1 ||
+        g->graph_failed || no_graph)
         return x_enqueue_rounds(g, nb);
     shd_eng* e = g->engs[0];
     const int par = (int)(g->xseq & 1);
@@ -4473,6 +4566,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
     for (int k = 0; k < nl; k++) {
         shd_eng* e = g->engs[k];
         e->h_sum->next_time = g->next;
+        e->t_done = std::max<uint64_t>(e->t_done, s.final_time);
         s.n_pending_resolved += e->pending_resolved - pend0[k];
     }
     s.device_ms_round_kernel = kms;

@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 #include <unordered_map>
 
@@ -315,13 +316,13 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
-    int64_t* __restrict__ stats) {
+    int64_t* __restrict__ stats, int32_t row0, int32_t row1) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint64_t* dist = (uint64_t*)smem;
     int32_t* parent = (int32_t*)(smem + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(smem + (size_t)12 * V);
     int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
-    for (int32_t row = blockIdx.x; row < T; row += gridDim.x)
+    for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
                             rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
@@ -335,13 +336,13 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
-    int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block) {
+    int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block, int32_t row0, int32_t row1) {
     __shared__ int flags[4];
     char* base = scratch + per_block * blockIdx.x;
     uint64_t* dist = (uint64_t*)base;
     int32_t* parent = (int32_t*)(base + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(base + (size_t)12 * V);
-    for (int32_t row = blockIdx.x; row < T; row += gridDim.x)
+    for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
                             rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
@@ -532,11 +533,25 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
 static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
 static constexpr size_t kLdsMax = 160 * 1024;
 
-extern "C" int shd_pc_build(shd_pc* pc) {
+// the build; with a communicator this rank computes its block of source
+// rows and the blocks are all-gathered (shd_pc_build_sharded)
+static int pc_build(shd_pc* pc, shd_comm* comm) {
     if (!pc) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(pc->device));
     const int32_t V = pc->V, T = pc->T;
     hipStream_t s = pc->stream;
+    const int W = comm ? comm->world : 1, me = comm ? comm->rank : 0;
+    const int32_t R = (int32_t)((T + W - 1) / W);              // rows per rank
+    const int32_t row0 = std::min<int32_t>(T, me * R), row1 = std::min<int32_t>(T, row0 + R);
+    if (pc->rows_mode && (size_t)R * W > (size_t)T && pc->rows_alloc < (size_t)R * W) {
+        // the all-gather takes equal blocks: pad the table to W * R rows
+        shd_pv* nr = nullptr;
+        SHD_HIP(hipMalloc((void**)&nr, sizeof(shd_pv) * (size_t)R * W * T));
+        (void)hipFree(pc->d_row);
+        pc->d_row = nr;
+        pc->rows_alloc = (size_t)R * W;
+    }
+    const auto t_call = std::chrono::steady_clock::now();
     int64_t init_stats[8] = {0, 0, 0, 0, 0, (int64_t)kDistInf, 0, 0};
     SHD_HIP(hipMemcpyAsync(pc->d_stats, init_stats, sizeof(init_stats), hipMemcpyHostToDevice, s));
     hipEvent_t ev[4];
@@ -562,25 +577,25 @@ extern "C" int shd_pc_build(shd_pc* pc) {
         if (lds <= kLdsMax) {
             if (V <= 2048) {
                 int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, kLdsMax / lds));
-                int grid = std::min(T, ncu * per_cu);
+                int grid = std::max(1, std::min(row1 - row0, ncu * per_cu));
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<256>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
-                                   pc->d_row, pc->d_stats);
+                                   pc->d_row, pc->d_stats, row0, row1);
             } else {
-                int grid = std::min(T, ncu);
+                int grid = std::max(1, std::min(row1 - row0, ncu));
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<1024>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_sssp_rows_lds<1024>, dim3(grid), dim3(1024), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
-                                   pc->d_row, pc->d_stats);
+                                   pc->d_row, pc->d_stats, row0, row1);
             }
         } else {
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
-            int grid = std::min(T, ncu * 4);
+            int grid = std::max(1, std::min(row1 - row0, ncu * 4));
             if (!pc->d_scratch || pc->scratch_bytes < per_block * grid) {
                 if (pc->d_scratch) (void)hipFree(pc->d_scratch);
                 pc->scratch_bytes = per_block * grid;
@@ -589,11 +604,17 @@ extern "C" int shd_pc_build(shd_pc* pc) {
             hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
                                pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
-                               pc->d_stats, (char*)pc->d_scratch, per_block);
+                               pc->d_stats, (char*)pc->d_scratch, per_block, row0, row1);
         }
         SHD_HIP(hipGetLastError());
     }
     SHD_HIP(hipEventRecord(ev[2], s));
+    if (comm && pc->rows_mode && W > 1) {
+        // the row blocks, all-gathered in place (block r starts at row r * R)
+        const size_t blk = sizeof(shd_pv) * (size_t)R * T;
+        const int rc = shd_comm_allgather_dev(comm, (const char*)pc->d_row + blk * me, pc->d_row, blk, s);
+        if (rc) { for (auto& e : ev) (void)hipEventDestroy(e); return rc; }
+    }
     {
         const size_t TT = (size_t)T * T;
         int blocks = (int)std::min<size_t>((TT + 255) / 256, 4096);
@@ -610,6 +631,20 @@ extern "C" int shd_pc_build(shd_pc* pc) {
     for (auto& e : ev) (void)hipEventDestroy(e);
     int64_t st[8];
     SHD_HIP(hipMemcpy(st, pc->d_stats, sizeof(st), hipMemcpyDeviceToHost));
+    if (comm && W > 1) {   // this rank's row statistics -> the group's
+        std::vector<int64_t> all((size_t)8 * W);
+        const int rc = shd_comm_allgather_host(comm, st, sizeof(st), all.data());
+        if (rc) return rc;
+        for (int r = 0; r < W; r++) {
+            if (r == me) continue;
+            const int64_t* o = &all[(size_t)8 * r];
+            st[0] += o[0];
+            st[1] = std::max(st[1], o[1]);
+            st[2] = std::max(st[2], o[2]);
+            st[3] += o[3];
+            st[4] += o[4];
+        }
+    }
     pc->info.rows_computed = pc->rows_mode ? T : 0;
     pc->info.n_ties = st[0];
     pc->info.max_hops = (int32_t)st[1];
@@ -622,13 +657,22 @@ extern "C" int shd_pc_build(shd_pc* pc) {
     pc->info.build_ms_direct = ms_dir;
     pc->info.build_ms_sssp = ms_rows;
     pc->info.build_ms_props = 0.0;   // fused into the SSSP kernel
-    pc->info.build_ms_device = ms_all;
+    pc->info.build_ms_device = comm ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                                                 t_call).count()
+                                    : ms_all;
     if (st[4] != 0) {
         fprintf(stderr, "libshdgpu: %lld latency folds differ from converged distances\n", (long long)st[4]);
         return SHD_ERANGE;
     }
     pc->built = true;
     return SHD_OK;
+}
+
+extern "C" int shd_pc_build(shd_pc* pc) { return pc_build(pc, nullptr); }
+
+extern "C" int shd_pc_build_sharded(shd_pc* pc, shd_comm* comm) {
+    if (!pc || !comm) return SHD_EINVAL;
+    return pc_build(pc, comm);
 }
 
 extern "C" int shd_pc_get_info(const shd_pc* pc, shd_pc_info* out) {
@@ -803,6 +847,12 @@ extern "C" int shd_pc_min_time_jump(shd_pc* pc, uint64_t runahead_ns, uint64_t* 
     if (j == 0) j = 10 * SHD_MS;
     if (runahead_ns > j) j = runahead_ns;
     *jump_ns = j;
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_min_stored_latency(shd_pc* pc, double* ms) {
+    if (!pc || !ms) return SHD_EINVAL;
+    *ms = pc->min_stored_latency;
     return SHD_OK;
 }
 

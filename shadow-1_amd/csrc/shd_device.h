@@ -54,6 +54,7 @@ struct shd_pc {
     // device tables [T][T] and [T] of (latency, reliability) pairs: one 16-B
     // load per lookup in the event loop
     shd_pv* d_row = nullptr;
+    size_t rows_alloc = 0;              // rows allocated in d_row beyond T (sharded builds pad to world blocks)
     shd_pv* d_dir = nullptr;
     shd_pv* d_self = nullptr;
     uint8_t* d_adj = nullptr;           // [T][T] 1 = adjacent (direct path exists)
@@ -73,3 +74,25 @@ struct shd_pc {
 
 // resolved value for a (src attached idx, dst attached idx) pair given ranks
 // (device + host): see DESIGN.md "First-touch rule".
+
+// ---- group communicators (comm.hip): RCCL or the host-memory transport ----
+#include <rccl/rccl.h>
+enum { SHD_COMM_RCCL = 1, SHD_COMM_HOST = 2 };
+struct shd_comm {
+    int kind = 0;
+    int world = 1, rank = 0, device = 0;
+    ncclComm_t nccl = nullptr;
+    shd_xhost* hx = nullptr;
+    hipStream_t s = nullptr;            // the communicator's own stream
+    void* h_stage = nullptr;            // pinned staging (host transport)
+    size_t h_stage_bytes = 0;
+};
+// device buffers, enqueued on `s` (RCCL) or staged through host memory
+// (host transport: synchronizes `s`); recv holds world blocks
+__attribute__((visibility("hidden"))) int shd_comm_alltoall_dev(shd_comm* c, const void* d_send, void* d_recv,
+                                                                size_t bytes_per_peer, hipStream_t s);
+__attribute__((visibility("hidden"))) int shd_comm_allgather_dev(shd_comm* c, const void* d_send, void* d_recv,
+                                                                 size_t bytes, hipStream_t s);
+// host buffers, blocking: out[r * bytes ...] = rank r's `bytes`
+__attribute__((visibility("hidden"))) int shd_comm_allgather_host(shd_comm* c, const void* mine, size_t bytes,
+                                                                  void* out);

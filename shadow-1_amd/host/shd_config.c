@@ -18,6 +18,7 @@
  * belong to is outside this path. */
 #include <ctype.h>
 #include <stdint.h>
+#include <arpa/inet.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -60,7 +61,7 @@ void shd_config_free(shd_config* c) {
     for (int32_t i = 0; i < c->n_hosts; i++) {
         shd_config_host* h = &c->hosts[i];
         free(h->name); free(h->ip_hint); free(h->citycode_hint); free(h->countrycode_hint);
-        free(h->geocode_hint); free(h->type_hint);
+        free(h->geocode_hint); free(h->type_hint); free(h->process_start_s);
     }
     free(c->hosts);
     free(c->topology_path);
@@ -124,6 +125,22 @@ static int parse_doc(xmlDocPtr doc, shd_config** out) {
             char* bd = attr_ci(n, "bandwidthdown");
             char* bu = attr_ci(n, "bandwidthup");
             char* hb = attr_ci(n, "heartbeatfrequency");
+            /* the host's processes in document order: their start times */
+            int32_t np = 0;
+            uint64_t* starts = NULL;
+            for (xmlNodePtr k = n->children; k && rc == SHD_OK; k = k->next) {
+                if (k->type != XML_ELEMENT_NODE) continue;
+                if (strcasecmp((const char*)k->name, "process") && strcasecmp((const char*)k->name, "application"))
+                    continue;
+                char* st = attr_ci(k, "starttime");
+                if (!st) st = attr_ci(k, "time");   /* deprecated alias, configuration.c:576-577 */
+                if (!st) { rc = SHD_EINVAL; break; }  /* starttime is required (configuration.c:596-598) */
+                uint64_t* ns = (uint64_t*)realloc(starts, sizeof(uint64_t) * (size_t)(np + 1));
+                if (!ns) { free(st); rc = SHD_ENOMEM; break; }
+                starts = ns;
+                starts[np++] = to_u64(st);
+                free(st);
+            }
             for (uint64_t i = 0; i < quantity && rc == SHD_OK; i++) {
                 shd_config_host h;
                 memset(&h, 0, sizeof(h));
@@ -140,8 +157,15 @@ static int parse_doc(xmlDocPtr doc, shd_config** out) {
                 h.bw_down_kibps = to_u64(bd);
                 h.bw_up_kibps = to_u64(bu);
                 h.heartbeat_s = to_u64(hb);
+                h.n_processes = np;
+                if (np) {
+                    h.process_start_s = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)np);
+                    if (!h.process_start_s) { free(h.name); rc = SHD_ENOMEM; break; }
+                    memcpy(h.process_start_s, starts, sizeof(uint64_t) * (size_t)np);
+                }
                 rc = add_host(c, &cap, &h);
             }
+            free(starts);
             free(id); free(iph); free(cch); free(coh); free(geh); free(tyh); free(bd); free(bu); free(hb);
         }
     }
@@ -172,16 +196,15 @@ int shd_config_load_file(const char* path, shd_config** out) {
 }
 
 /* ---------------------------------------------------------------- DNS */
-/* dotted quad -> host-order u32 (address_stringToIP through inet_addr); 0 with
- * *ok = 0 when malformed */
+/* dotted quad -> host-order u32 as address_stringToIP does it (inet_pton,
+ * address.c:145-152, then ntohl): no whitespace, signs or leading-zero
+ * octets; 0 with *ok = 0 when malformed */
 static uint32_t ip_parse(const char* s, int* ok) {
-    unsigned a, b, c, d;
-    char tail;
+    struct in_addr a;
     *ok = 0;
-    if (!s || sscanf(s, "%u.%u.%u.%u%c", &a, &b, &c, &d, &tail) != 4) return 0;
-    if (a > 255 || b > 255 || c > 255 || d > 255) return 0;
+    if (!s || inet_pton(AF_INET, s, &a) != 1) return 0;
     *ok = 1;
-    return (a << 24) | (b << 16) | (c << 8) | d;
+    return ntohl(a.s_addr);
 }
 
 /* _dns_isRestricted (dns.c:74-95), on host-order addresses */

@@ -268,10 +268,20 @@ static int ip_usable(const char* s, uint32_t* ip) {
 }
 static int str_eq(const char* a, const char* b) { return a && b && strcasecmp(a, b) == 0; }
 
+static double draw_state(void* st) { return shd_next_double((uint32_t*)st); }
+
 int shd_topology_attach(const shd_graphml* gm, uint32_t* rng, const char* ip_hint,
                         const char* city, const char* country, const char* geo, const char* type,
                         int32_t* vertex_out, uint64_t* bw_down_out, uint64_t* bw_up_out) {
-    if (!gm || !rng || !vertex_out) return SHD_EINVAL;
+    if (!rng) return SHD_EINVAL;
+    return shd_topology_attach_cb(gm, draw_state, rng, ip_hint, city, country, geo, type, vertex_out,
+                                  bw_down_out, bw_up_out);
+}
+
+int shd_topology_attach_cb(const shd_graphml* gm, double (*next_double)(void*), void* rng, const char* ip_hint,
+                           const char* city, const char* country, const char* geo, const char* type,
+                           int32_t* vertex_out, uint64_t* bw_down_out, uint64_t* bw_up_out) {
+    if (!gm || !next_double || !vertex_out) return SHD_EINVAL;
     int32_t V = gm->g.n_vertices;
     enum { CITY_TYPE, CITY, COUNTRY_TYPE, COUNTRY, GEO_TYPE, GEO, TYPE, ALL, NQ };
     int32_t* q[NQ]; int32_t qn[NQ]; int32_t nip[NQ];
@@ -321,7 +331,7 @@ int shd_topology_attach(const shd_graphml* gm, uint32_t* rng, const char* ip_hin
             if (match > best || best == 0) { best = match; vertex = v; }
         }
     } else {
-        double r = shd_next_double(rng);
+        double r = next_double(rng);
         int32_t range = n - 1;
         int32_t chosen = (int32_t)round((double)(range * r));
         vertex = q[pick][chosen];

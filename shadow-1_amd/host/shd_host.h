@@ -5,6 +5,7 @@
 #ifndef SHD_HOST_H
 #define SHD_HOST_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/shdgpu.h"
@@ -39,6 +40,18 @@ typedef struct shd_csr {
 __attribute__((visibility("hidden"))) int shd_csr_build(const shd_graph* g, shd_csr* out);
 __attribute__((visibility("hidden"))) void shd_csr_free(shd_csr* c);
 __attribute__((visibility("hidden"))) int32_t shd_csr_get_eid(const shd_csr* c, int32_t a, int32_t b);
+
+/* host-memory transport of an engine group (shd_xhost.c): processes of one
+ * machine meeting in a POSIX shared-memory segment */
+typedef struct shd_xhost shd_xhost;
+__attribute__((visibility("hidden"))) int shd_xhost_open(const char* name, int world, int rank, size_t slot_bytes,
+                                                         shd_xhost** out);
+__attribute__((visibility("hidden"))) int shd_xhost_barrier(shd_xhost* x);
+__attribute__((visibility("hidden"))) int shd_xhost_allgather(shd_xhost* x, const void* mine, size_t bytes,
+                                                              void* out);
+__attribute__((visibility("hidden"))) int shd_xhost_alltoall(shd_xhost* x, const void* send, size_t bytes,
+                                                             void* recv);
+__attribute__((visibility("hidden"))) void shd_xhost_close(shd_xhost* x);
 
 #ifdef __cplusplus
 }

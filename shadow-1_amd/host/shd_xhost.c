@@ -1,0 +1,148 @@
+/*
+ * shd_xhost.c -- the host-memory transport of the engine group (shd_comm of
+ * kind "host"): ranks are processes on one machine (any GPUs, or one GPU
+ * shared), meeting in a POSIX shared-memory segment.  It carries the same
+ * collectives the RCCL transport does (all-to-all of the per-round blocks,
+ * all-gather of first-touch logs and row shards, the spill exchange), staged
+ * through host memory: the per-round exchange of slave.c:437-462's rounds
+ * without a GPU interconnect, so the group protocol can run with several
+ * processes where RCCL cannot (RCCL refuses two ranks on one device).
+ *
+ * Segment: a header (barrier count and generation), then `world` scratch
+ * slots of `slot` bytes.  A collective writes the caller's part into its
+ * slot, meets at the barrier, reads what it needs, meets again; larger
+ * payloads go in pieces of the slot size.  The segment is created zero-filled
+ * by whichever rank opens it first; rank 0 unlinks it at close.  The name
+ * must be unique per group (a stale segment's barrier state would be reused):
+ * callers derive it from a random token, as RCCL's unique id.
+ */
+#include <errno.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "shd_host.h"
+
+struct shd_xhost_hdr {
+    uint32_t count;       /* arrivals at the current barrier */
+    uint32_t gen;         /* barrier generation */
+    uint32_t world;
+    uint32_t pad;
+};
+
+struct shd_xhost {
+    char name[128];
+    int world, rank, fd;
+    size_t slot;          /* scratch bytes per rank */
+    size_t map_bytes;
+    char* base;           /* mapping: header, then world slots */
+    double timeout_s;
+};
+
+static char* slot_ptr(shd_xhost* x, int r) { return x->base + 64 + (size_t)r * x->slot; }
+
+int shd_xhost_open(const char* name, int world, int rank, size_t slot_bytes, shd_xhost** out) {
+    if (!name || !*name || strlen(name) > 100 || world <= 0 || world > 64 || rank < 0 || rank >= world ||
+        !slot_bytes || !out)
+        return SHD_EINVAL;
+    shd_xhost* x = calloc(1, sizeof(*x));
+    if (!x) return SHD_ENOMEM;
+    snprintf(x->name, sizeof(x->name), "/%s", name[0] == '/' ? name + 1 : name);
+    x->world = world;
+    x->rank = rank;
+    x->slot = (slot_bytes + 63) & ~(size_t)63;
+    x->map_bytes = 64 + (size_t)world * x->slot;
+    const char* to = getenv("SHD_XHOST_TIMEOUT");
+    x->timeout_s = to ? atof(to) : 300.0;
+    x->fd = shm_open(x->name, O_RDWR | O_CREAT, 0600);
+    if (x->fd < 0) { free(x); return SHD_ENODEV; }
+    /* every rank grows it to the same size (a no-op after the first) */
+    struct stat st;
+    if (fstat(x->fd, &st) != 0 || ((size_t)st.st_size < x->map_bytes && ftruncate(x->fd, (off_t)x->map_bytes) != 0)) {
+        close(x->fd);
+        free(x);
+        return SHD_ENOMEM;
+    }
+    x->base = mmap(NULL, x->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, x->fd, 0);
+    if (x->base == MAP_FAILED) { close(x->fd); free(x); return SHD_ENOMEM; }
+    *out = x;
+    return shd_xhost_barrier(x);
+}
+
+static double mono_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+/* a generation barrier; SHD_ENODEV if the others do not arrive in time */
+int shd_xhost_barrier(shd_xhost* x) {
+    struct shd_xhost_hdr* h = (struct shd_xhost_hdr*)x->base;
+    const uint32_t g = __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE);
+    if (__atomic_add_fetch(&h->count, 1, __ATOMIC_ACQ_REL) == (uint32_t)x->world) {
+        __atomic_store_n(&h->count, 0, __ATOMIC_RELAXED);
+        __atomic_store_n(&h->gen, g + 1, __ATOMIC_RELEASE);
+        return SHD_OK;
+    }
+    const double t0 = mono_s();
+    unsigned spins = 0;
+    while (__atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) == g) {
+        if (++spins > 1000) sched_yield();
+        if ((spins & 0xFFF) == 0 && mono_s() - t0 > x->timeout_s) {
+            fprintf(stderr, "libshdgpu: host transport %s: rank %d waited %.0f s at a barrier\n", x->name, x->rank,
+                    x->timeout_s);
+            return SHD_ENODEV;
+        }
+    }
+    return SHD_OK;
+}
+
+/* out[r] = the `bytes` each rank r passed (out: world * bytes) */
+int shd_xhost_allgather(shd_xhost* x, const void* mine, size_t bytes, void* out) {
+    const size_t piece = x->slot;
+    for (size_t off = 0; off < bytes || (bytes == 0 && off == 0); off += piece) {
+        const size_t n = bytes - off < piece ? bytes - off : piece;
+        if (n) memcpy(slot_ptr(x, x->rank), (const char*)mine + off, n);
+        int rc = shd_xhost_barrier(x);
+        if (rc) return rc;
+        for (int r = 0; r < x->world && n; r++) memcpy((char*)out + (size_t)r * bytes + off, slot_ptr(x, r), n);
+        if ((rc = shd_xhost_barrier(x))) return rc;
+        if (bytes == 0) break;
+    }
+    return SHD_OK;
+}
+
+/* send: world blocks of `bytes` (block p for rank p); recv: world blocks
+ * (block p from rank p) */
+int shd_xhost_alltoall(shd_xhost* x, const void* send, size_t bytes, void* recv) {
+    const int W = x->world;
+    const size_t piece = x->slot / (size_t)W;
+    if (!piece) return SHD_ERANGE;
+    for (size_t off = 0; off < bytes; off += piece) {
+        const size_t n = bytes - off < piece ? bytes - off : piece;
+        char* mine = slot_ptr(x, x->rank);
+        for (int p = 0; p < W; p++) memcpy(mine + (size_t)p * piece, (const char*)send + (size_t)p * bytes + off, n);
+        int rc = shd_xhost_barrier(x);
+        if (rc) return rc;
+        for (int p = 0; p < W; p++)
+            memcpy((char*)recv + (size_t)p * bytes + off, slot_ptr(x, p) + (size_t)x->rank * piece, n);
+        if ((rc = shd_xhost_barrier(x))) return rc;
+    }
+    return SHD_OK;
+}
+
+void shd_xhost_close(shd_xhost* x) {
+    if (!x) return;
+    (void)shd_xhost_barrier(x);   /* nobody is inside a collective any more */
+    munmap(x->base, x->map_bytes);
+    close(x->fd);
+    if (x->rank == 0) shm_unlink(x->name);
+    free(x);
+}

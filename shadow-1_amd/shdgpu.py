@@ -23,6 +23,7 @@ SHD_HEADER_UDP = 42
 SHD_QF_NO_CALENDAR = 1      # queue_flags: every inter-host event through inbox + heap
 SHD_QF_COUNT_PATHS = 2      # queue_flags: per-path packet counters on the device
 SHD_QF_HEARTBEATS = 4       # queue_flags: tracker node counters at every heartbeat
+SHD_QF_NO_APP_START = 8     # queue_flags: the caller pushes the application starts (shd_eng_push_events)
 
 EV_HEARTBEAT, EV_REFILL, EV_REFILL_LO, EV_APP_START, EV_PACKET, EV_LOCAL, EV_NOTIFY = range(1, 8)
 TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL = range(1, 8)
@@ -64,7 +65,8 @@ class GraphProps(C.Structure):
 class ConfigHost(C.Structure):
     _fields_ = [("name", C.c_char_p), ("ip_hint", C.c_char_p), ("citycode_hint", C.c_char_p),
                 ("countrycode_hint", C.c_char_p), ("geocode_hint", C.c_char_p), ("type_hint", C.c_char_p),
-                ("bw_down_kibps", C.c_uint64), ("bw_up_kibps", C.c_uint64), ("heartbeat_s", C.c_uint64)]
+                ("bw_down_kibps", C.c_uint64), ("bw_up_kibps", C.c_uint64), ("heartbeat_s", C.c_uint64),
+                ("n_processes", C.c_int32), ("_pad", C.c_int32), ("process_start_s", C.POINTER(C.c_uint64))]
 
 
 class Config(C.Structure):
@@ -104,6 +106,8 @@ class Model(C.Structure):
         ("load", C.c_uint32), ("payload", C.c_uint32), ("trace", C.c_uint32),
         ("evq_cap", C.c_uint32), ("inbox_cap", C.c_uint32), ("codelq_cap", C.c_uint32),
         ("txq_cap", C.c_uint32), ("queue_flags", C.c_uint32),
+        ("host_class", P(C.c_uint8)), ("n_classes", C.c_int32), ("_pad1", C.c_int32),
+        ("host_heartbeat", P(C.c_uint64)),
     ]
 
 
@@ -188,6 +192,7 @@ _SIGS = {
     "shd_pc_count_packet": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "shd_pc_packet_count": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint64)]),
     "shd_pc_min_time_jump": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "shd_pc_min_stored_latency": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "shd_pc_destroy": (None, [C.c_void_p]),
     "shd_rand_r": (C.c_int32, [P(C.c_uint32)]),
     "shd_next_double": (C.c_double, [P(C.c_uint32)]),
@@ -196,10 +201,14 @@ _SIGS = {
     "shd_topology_attach": (C.c_int, [P(GraphML), P(C.c_uint32), C.c_char_p, C.c_char_p,
                                       C.c_char_p, C.c_char_p, C.c_char_p, P(C.c_int32),
                                       P(C.c_uint64), P(C.c_uint64)]),
+    "shd_topology_attach_cb": (C.c_int, [P(GraphML), C.c_void_p, C.c_void_p, C.c_char_p, C.c_char_p,
+                                         C.c_char_p, C.c_char_p, C.c_char_p, P(C.c_int32),
+                                         P(C.c_uint64), P(C.c_uint64)]),
     "shd_eng_create": (C.c_int, [P(Model), C.c_void_p, C.c_int32, C.c_int32, C.c_int,
                                  P(C.c_void_p)]),
     "shd_eng_window": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "shd_eng_boot": (C.c_int, [C.c_void_p]),
+    "shd_eng_push_events": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "shd_eng_run_round": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(RoundSummary)]),
     "shd_eng_run": (C.c_int, [C.c_void_p, P(RunStats)]),
     "shd_eng_run_until": (C.c_int, [C.c_void_p, C.c_uint64, P(RunStats)]),
@@ -225,6 +234,12 @@ _SIGS = {
                                          P(C.c_void_p)]),
     "shd_xgroup_create_local": (C.c_int, [P(C.c_void_p), C.c_int, C.c_uint32, P(C.c_void_p)]),
     "shd_xgroup_run_until": (C.c_int, [C.c_void_p, C.c_uint64, P(RunStats)]),
+    "shd_xgroup_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, P(C.c_void_p)]),
+    "shd_comm_create_rccl": (C.c_int, [P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(C.c_void_p)]),
+    "shd_comm_create_host": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, P(C.c_void_p)]),
+    "shd_comm_rank": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),
+    "shd_comm_destroy": (None, [C.c_void_p]),
+    "shd_pc_build_sharded": (C.c_int, [C.c_void_p, C.c_void_p]),
     "shd_xgroup_next_time": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "shd_xgroup_destroy": (None, [C.c_void_p]),
 }
@@ -301,7 +316,9 @@ def load_config(xml: bytes):
         hosts = [dict(name=dec(h.name), ip_hint=dec(h.ip_hint), citycode_hint=dec(h.citycode_hint),
                       countrycode_hint=dec(h.countrycode_hint), geocode_hint=dec(h.geocode_hint),
                       type_hint=dec(h.type_hint), bw_down_kibps=h.bw_down_kibps, bw_up_kibps=h.bw_up_kibps,
-                      heartbeat_s=h.heartbeat_s) for h in (c.hosts[i] for i in range(c.n_hosts))]
+                      heartbeat_s=h.heartbeat_s,
+                      process_start_s=[h.process_start_s[k] for k in range(h.n_processes)])
+                 for h in (c.hosts[i] for i in range(c.n_hosts))]
         ips = np.zeros(max(c.n_hosts, 1), dtype=np.uint32)
         check(lib().shd_dns_assign(ptr, ips.ctypes.data_as(P(C.c_uint32))), "shd_dns_assign")
         topo = dec(c.topology_text) if c.topology_text else dec(c.topology_path)
@@ -333,23 +350,35 @@ class ModelArrays:
     def __init__(self, host_vertex, host_rng, bw_down, bw_up, dest_cum, *, end_time,
                  app_start=1 * SHD_SEC, load=16, payload=1, heartbeat_interval=SHD_SEC,
                  bootstrap_end=0, trace=False, evq_cap=0, inbox_cap=0, codelq_cap=0,
-                 txq_cap=0, queue_flags=0):
+                 txq_cap=0, queue_flags=0, host_class=None, host_heartbeat=None):
+        """dest_cum: [H] (one weights row for every host) or [n_classes, H] with
+        host_class [H] picking each host's row; host_heartbeat: [H] ns or None."""
         self.host_vertex = np.ascontiguousarray(host_vertex, dtype=np.int32)
         self.host_rng = np.ascontiguousarray(host_rng, dtype=np.uint32)
         self.bw_down = np.ascontiguousarray(bw_down, dtype=np.uint64)
         self.bw_up = np.ascontiguousarray(bw_up, dtype=np.uint64)
         self.dest_cum = np.ascontiguousarray(dest_cum, dtype=np.float64)
         H = len(self.host_vertex)
-        assert all(len(a) == H for a in (self.host_rng, self.bw_down, self.bw_up, self.dest_cum))
+        n_classes = 1 if self.dest_cum.ndim == 1 else self.dest_cum.shape[0]
+        assert all(len(a) == H for a in (self.host_rng, self.bw_down, self.bw_up))
+        assert self.dest_cum.shape[-1] == H
+        self.host_class = None if host_class is None else np.ascontiguousarray(host_class, dtype=np.uint8)
+        assert n_classes == 1 or (self.host_class is not None and len(self.host_class) == H)
+        self.n_classes = n_classes
+        self.host_heartbeat = None if host_heartbeat is None else \
+            np.ascontiguousarray(host_heartbeat, dtype=np.uint64)
         self.params = dict(end_time=int(end_time), app_start=int(app_start), load=int(load),
                            payload=int(payload), heartbeat_interval=int(heartbeat_interval),
-                           bootstrap_end=int(bootstrap_end), trace=int(bool(trace)))
+                           bootstrap_end=int(bootstrap_end), trace=int(bool(trace)),
+                           queue_flags=int(queue_flags))
         self.struct = Model(
             H, 0, as_ptr(self.host_vertex, C.c_int32), as_ptr(self.host_rng, C.c_uint32),
             as_ptr(self.bw_down, C.c_uint64), as_ptr(self.bw_up, C.c_uint64),
             as_ptr(self.dest_cum, C.c_double), int(end_time), int(bootstrap_end),
             int(heartbeat_interval), int(app_start), int(load), int(payload), int(bool(trace)),
-            int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), int(queue_flags))
+            int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), int(queue_flags),
+            None if self.host_class is None else as_ptr(self.host_class, C.c_uint8), int(n_classes), 0,
+            None if self.host_heartbeat is None else as_ptr(self.host_heartbeat, C.c_uint64))
 
     @property
     def n_hosts(self):
@@ -390,11 +419,17 @@ def tracker_node_lines(snapshots, interval_ns: int, payload: int) -> list:
     so a line holds the differences to the previous heartbeat.  The loopback
     shortcut keeps the host's own address (network_interface.c:548-555), so all
     packets count as remote; the CPU model is off (cpu-percent 0, no delays)."""
-    lines, prev = [NODE_HEADER_LINE], (0, 0)
     secs = int(interval_ns // SHD_SEC)
     zero = _counter_string(0, payload)
+    # tracker_new runs the first heartbeat inline at boot (tracker.c:141): the
+    # header, then an all-zero line, before the K periodic ones
+    lines = [NODE_HEADER_LINE, "[shadow-heartbeat] [node] %u,%d,%d,%f,%d,%f;%s;%s;%s;%s" % (
+        secs, 0, 0, 0.0, 0, 0.0, zero, zero, zero, zero)]
+    prev = (0, 0)
     for cin, cout in np.asarray(snapshots, dtype=np.int64).tolist():
-        din, dout = cin - prev[0], cout - prev[1]
+        # the device counters are cumulative uint32 (wrap after 2^32 packets);
+        # the reference's are per-interval gsize, cleared at every heartbeat
+        din, dout = (cin - prev[0]) & 0xFFFFFFFF, (cout - prev[1]) & 0xFFFFFFFF
         prev = (cin, cout)
         rb, sb = din * (SHD_HEADER_UDP + payload), dout * (SHD_HEADER_UDP + payload)
         lines.append("[shadow-heartbeat] [node] %u,%d,%d,%f,%d,%f;%s;%s;%s;%s" % (

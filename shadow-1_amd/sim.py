@@ -28,6 +28,10 @@ class PathCache:
     def build(self):
         S.check(S.lib().shd_pc_build(self.ptr), "shd_pc_build")
 
+    def build_sharded(self, comm: "Comm"):
+        """Source rows sharded over the communicator's ranks, then all-gathered."""
+        S.check(S.lib().shd_pc_build_sharded(self.ptr, comm.ptr), "shd_pc_build_sharded")
+
     def info(self) -> S.PcInfo:
         i = S.PcInfo()
         S.check(S.lib().shd_pc_get_info(self.ptr, C.byref(i)), "shd_pc_get_info")
@@ -92,6 +96,12 @@ class Engine:
 
     def boot(self):
         S.check(S.lib().shd_eng_boot(self.ptr), "shd_eng_boot")
+
+    def push_events(self, events: np.ndarray):
+        """shd_eng_push_events: caller-scheduled application starts (after boot)."""
+        ev = np.ascontiguousarray(events, dtype=S.EVENT_DTYPE)
+        S.check(S.lib().shd_eng_push_events(self.ptr, ev.ctypes.data if len(ev) else None, len(ev)),
+                "shd_eng_push_events")
 
     def run(self) -> S.RunStats:
         st = S.RunStats()
@@ -181,7 +191,8 @@ class Engine:
         if n.value:
             S.check(S.lib().shd_eng_heartbeats(self.ptr, out.ctypes.data_as(C.POINTER(C.c_uint32)), n.value,
                                                C.byref(n)), "shd_eng_heartbeats")
-        return out.reshape(self.h1 - self.h0, -1, 2)
+        nloc = self.h1 - self.h0
+        return out.reshape(nloc, (n.value // (2 * nloc)) if nloc else 0, 2)
 
     def path_counts(self) -> np.ndarray:
         """[T, T] uint64 packet counts per cached path entry (SHD_QF_COUNT_PATHS)."""
@@ -207,6 +218,40 @@ class Engine:
         if self.ptr:
             S.lib().shd_eng_destroy(self.ptr)
             self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Comm:
+    """A group communicator (shd_comm): `rccl(uid, world, rank, device)` or
+    `host(name, world, rank, device)` (processes of one machine, shared memory)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    @classmethod
+    def rccl(cls, uid: bytes, world, rank, device=0):
+        buf = (C.c_uint8 * S.SHD_XID_BYTES).from_buffer_copy(uid)
+        ptr = C.c_void_p()
+        S.check(S.lib().shd_comm_create_rccl(buf, int(world), int(rank), int(device), C.byref(ptr)),
+                "shd_comm_create_rccl")
+        return cls(ptr)
+
+    @classmethod
+    def host(cls, name: str, world, rank, device=0):
+        ptr = C.c_void_p()
+        S.check(S.lib().shd_comm_create_host(name.encode(), int(world), int(rank), int(device), C.byref(ptr)),
+                "shd_comm_create_host")
+        return cls(ptr)
+
+    def close(self):
+        if self.ptr:
+            S.lib().shd_comm_destroy(self.ptr)
+            self.ptr = None
 
     def __del__(self):
         try:
@@ -246,6 +291,14 @@ class XGroup:
         ptr = C.c_void_p()
         S.check(S.lib().shd_xgroup_create_rccl(engine.ptr, buf, int(world), int(rank), int(block_events),
                                                C.byref(ptr)), "shd_xgroup_create_rccl")
+        return cls(ptr, [engine])
+
+    @classmethod
+    def over(cls, engine, comm: Comm, block_events=0):
+        """One engine of this process in a group over a communicator."""
+        ptr = C.c_void_p()
+        S.check(S.lib().shd_xgroup_create(engine.ptr, comm.ptr, int(block_events), C.byref(ptr)),
+                "shd_xgroup_create")
         return cls(ptr, [engine])
 
     def run_until(self, t_stop) -> S.RunStats:

@@ -156,17 +156,80 @@ def uniform_cum(n_hosts: int) -> np.ndarray:
     return cum
 
 
+def phold_cum(weights) -> np.ndarray:
+    """_phold_chooseNode's cumulative weights (test_phold.c:160-178) from a
+    weights file's values (test_phold.c:341-356): totalWeight is the sequential
+    sum of the weights, and cumulative += weights[i] / totalWeight, in order."""
+    w = np.ascontiguousarray(weights, dtype=np.float64)
+    total = np.add.accumulate(w)[-1] if len(w) else 0.0       # sequential left fold
+    return np.add.accumulate(w / total)                       # per-element division, then the fold
+
+
 def phold_model(host_vertex, *, end_time, seed=1, bw_down=10240, bw_up=10240, load=16,
                 payload=1, app_start=S.SHD_SEC, heartbeat=S.SHD_SEC, bootstrap_end=0,
-                trace=False, **caps) -> S.ModelArrays:
+                trace=False, dest_cum=None, host_class=None, host_rng=None, **caps) -> S.ModelArrays:
+    """PHOLD-UDP hosts; dest_cum None = uniform weights over all hosts, else
+    [H] or [n_classes, H] (then host_class [H]); host_rng None = the seed
+    chain after the attach draw (one random pick per host)."""
     H = len(host_vertex)
-    seeds = after_attach_draw(seed_chain(H, seed))
+    seeds = after_attach_draw(seed_chain(H, seed)) if host_rng is None else host_rng
     bd = np.broadcast_to(np.asarray(bw_down, dtype=np.uint64), (H,)).copy()
     bu = np.broadcast_to(np.asarray(bw_up, dtype=np.uint64), (H,)).copy()
-    return S.ModelArrays(host_vertex, seeds, bd, bu, uniform_cum(H), end_time=end_time,
+    cum = uniform_cum(H) if dest_cum is None else dest_cum
+    return S.ModelArrays(host_vertex, seeds, bd, bu, cum, end_time=end_time,
                          app_start=app_start, load=load, payload=payload,
                          heartbeat_interval=heartbeat, bootstrap_end=bootstrap_end, trace=trace,
-                         **caps)
+                         host_class=host_class, **caps)
+
+
+def attach_random(gm_ptr, seeds: np.ndarray):
+    """topology_attach for hosts with no hints (topology.c:2326-2334): one
+    host-RNG draw picks the vertex.  Returns (vertex [H], rng after [H],
+    bw_down [H], bw_up [H]) with the vertex bandwidths (host.c:183-189)."""
+    lib = S.lib()
+    H = len(seeds)
+    vert = np.empty(H, np.int32)
+    rng = np.ascontiguousarray(seeds, dtype=np.uint32).copy()
+    bd = np.empty(H, np.uint64)
+    bu = np.empty(H, np.uint64)
+    st = S.C.c_uint32()
+    v = S.C.c_int32()
+    d = S.C.c_uint64()
+    u = S.C.c_uint64()
+    for h in range(H):
+        st.value = int(rng[h])
+        S.check(lib.shd_topology_attach(gm_ptr, S.C.byref(st), None, None, None, None, None,
+                                        S.C.byref(v), S.C.byref(d), S.C.byref(u)), "shd_topology_attach")
+        vert[h], rng[h], bd[h], bu[h] = v.value, st.value, d.value, u.value
+    return vert, rng, bd, bu
+
+
+def tor_model(n_relays: int, n_clients: int, *, end_time, seed=1, load=4, payload=1,
+              app_start=S.SHD_SEC, client_share=0.5, sigma=1.0, trace=False, **caps):
+    """BASELINE C4, synthetic Tor-scale traffic on the bundled topology (the
+    ccs-2018 traffic model is a placeholder in the reference,
+    docs/2018-ccs-tmodel.md:1).  Hosts 0..R-1 are relays, R..R+C-1 clients,
+    each a PHOLD-UDP process with its own weights file (test_phold.c:341-356):
+      - a client sends to relays only, by relay weight (log-normal, seeded);
+      - a relay forwards to relays by the same weights and to clients
+        (uniformly) with total share `client_share`.
+    Hosts attach at random with their RNG (topology.c:2326-2334) and take the
+    vertex bandwidths.  Returns (graph, model, graphml pointer to free)."""
+    xml = bundled_graphml_bytes()
+    g, gm = load_graphml_bytes(xml)
+    H = n_relays + n_clients
+    seeds = seed_chain(H, seed)
+    vert, rng, bd, bu = attach_random(gm, seeds)
+    S.lib().shd_graphml_free(gm)
+    wr = np.random.default_rng(seed + 7).lognormal(0.0, sigma, n_relays)
+    w_client_row = np.concatenate([wr, np.zeros(n_clients)])
+    cw = float(np.add.accumulate(wr)[-1]) * client_share / (1.0 - client_share) / max(n_clients, 1)
+    w_relay_row = np.concatenate([wr, np.full(n_clients, cw)])
+    cum = np.stack([phold_cum(w_relay_row), phold_cum(w_client_row)])
+    cls = np.concatenate([np.zeros(n_relays, np.uint8), np.ones(n_clients, np.uint8)])
+    m = phold_model(vert, end_time=end_time, seed=seed, bw_down=bd, bw_up=bu, load=load, payload=payload,
+                    app_start=app_start, trace=trace, dest_cum=cum, host_class=cls, host_rng=rng, **caps)
+    return g, m
 
 
 def hosts_on_vertices(n_vertices: int, hosts_per_vertex: int) -> np.ndarray:
@@ -176,3 +239,52 @@ def hosts_on_vertices(n_vertices: int, hosts_per_vertex: int) -> np.ndarray:
 
 def attached_vertices(host_vertex) -> np.ndarray:
     return np.unique(np.asarray(host_vertex, dtype=np.int32))
+
+
+def config_model(xml: bytes, *, load=16, payload=1, seed=1, trace=False, topology_bytes=None, **caps):
+    """A shadow.config.xml through the reference's set-up path, with PHOLD-UDP
+    in place of the configured plugins (the tgen binary of the bundled example
+    is not in the reference tree):
+      configuration_new -> hosts in document order, `quantity` names, hints,
+        bandwidth overrides, <process starttime> (shd_config_load_buffer);
+      dns_register (shd_dns_assign); seed chain (master.c:95,417 -> slave.c:301);
+      topology_new on the inline or referenced graphml;
+      topology_attach per host (hints, one RNG draw) with the vertex bandwidth
+        unless the host sets its own (host.c:176-192);
+      process_schedule per process at boot (host.c:372-390): pushed starts.
+    Returns (graph, model, pushed start events, host names, ips)."""
+    hosts, ips, stop_s, topo = S.load_config(xml)
+    if topology_bytes is not None:
+        gxml = topology_bytes
+    elif topo and topo.lstrip().startswith("<"):
+        gxml = topo.encode()
+    else:
+        raise ValueError("config_model: the topology is a path; pass its bytes as topology_bytes")
+    lib = S.lib()
+    gm = S.P(S.GraphML)()
+    S.check(lib.shd_graphml_load_string(gxml, len(gxml), S.C.byref(gm)), "shd_graphml_load_string")
+    g = S.graph_from_graphml(gm)
+    H = len(hosts)
+    seeds = seed_chain(H, seed)
+    vert = np.empty(H, np.int32)
+    rng = seeds.copy()
+    bd = np.empty(H, np.uint64)
+    bu = np.empty(H, np.uint64)
+    st, v, d, u = S.C.c_uint32(), S.C.c_int32(), S.C.c_uint64(), S.C.c_uint64()
+    enc = lambda x: None if x is None else x.encode()  # noqa: E731
+    for i, h in enumerate(hosts):
+        st.value = int(rng[i])
+        S.check(lib.shd_topology_attach(gm, S.C.byref(st), enc(h["ip_hint"]), enc(h["citycode_hint"]),
+                                        enc(h["countrycode_hint"]), enc(h["geocode_hint"]), enc(h["type_hint"]),
+                                        S.C.byref(v), S.C.byref(d), S.C.byref(u)), "shd_topology_attach")
+        vert[i], rng[i] = v.value, st.value
+        bd[i] = h["bw_down_kibps"] or d.value
+        bu[i] = h["bw_up_kibps"] or u.value
+    lib.shd_graphml_free(gm)
+    hb = np.array([(h["heartbeat_s"] or 1) * S.SHD_SEC for h in hosts], dtype=np.uint64)
+    pushes = np.array([(t * S.SHD_SEC, 0, i, i, 0, S.EV_APP_START)
+                       for i, h in enumerate(hosts) for t in h["process_start_s"]], dtype=S.EVENT_DTYPE)
+    m = S.ModelArrays(vert, rng, bd, bu, uniform_cum(H), end_time=stop_s * S.SHD_SEC, load=load,
+                      payload=payload, trace=trace, host_heartbeat=hb,
+                      queue_flags=S.SHD_QF_NO_APP_START | caps.pop("queue_flags", 0), **caps)
+    return g, m, pushes, [h["name"] for h in hosts], ips

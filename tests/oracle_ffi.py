@@ -35,6 +35,14 @@ class OCodel(C.Structure):
                 ("drop_count", C.c_uint32), ("drop_count_last", C.c_uint32)]
 
 
+class OBaseline(C.Structure):
+    _fields_ = [(n, C.c_double) for n in ("rows_ms", "warmup_ms", "serial_ms", "parallel_ms")] + \
+               [(n, C.c_uint64) for n in ("serial_events", "serial_pkt_events", "parallel_events",
+                                          "parallel_pkt_events", "parallel_rounds", "parallel_first_touch",
+                                          "ambiguous", "window_ns")] + \
+               [("threads", C.c_int32), ("same_end_state", C.c_int32)]
+
+
 _lib = None
 
 
@@ -77,6 +85,8 @@ def lib():
         l.o_engine_set_mark.argtypes = [C.c_uint64]
         l.o_engine_set_counts_out.argtypes = [C.c_void_p, C.c_int32]
         l.o_engine_set_heartbeats_out.argtypes = [C.c_void_p, C.c_uint32]
+        l.o_engine_set_pushes.argtypes = [C.c_void_p, C.c_uint64]
+        l.o_baseline.argtypes = [P(S.Model), P(S.Graph), C.c_uint64, C.c_uint64, C.c_int, P(OBaseline)]
         _lib = l
     return _lib
 
@@ -140,7 +150,7 @@ class OTopo:
 
 
 def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None, path_counts=None,
-               heartbeats=None):
+               heartbeats=None, pushes=None):
     """Serial reference loop; returns (trace ndarray, digest ndarray, ORun stats dict).
     path_counts: a uint64 [V, V] array filled with the packet count of every
     cached path entry, by the orientation it is stored under.
@@ -151,6 +161,9 @@ def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=No
         lib().o_engine_set_heartbeats_out(heartbeats.ctypes.data, heartbeats.shape[1])
     else:
         lib().o_engine_set_heartbeats_out(None, 0)
+    push = None if pushes is None else np.ascontiguousarray(pushes, dtype=S.EVENT_DTYPE)
+    lib().o_engine_set_pushes(None if push is None or not len(push) else push.ctypes.data,
+                              0 if push is None else len(push))
     lib().o_engine_set_mark((1 << 64) - 1 if mark is None else int(mark))
     if path_counts is not None:
         assert path_counts.dtype == np.uint64 and path_counts.shape == (g.n_vertices, g.n_vertices)
@@ -172,6 +185,7 @@ def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=No
                  self_run=r.self_run, wall_ms=r.wall_ms, mark_events=r.mark_events,
                  mark_pkt_events=r.mark_pkt_events, mark_wall_ms=r.mark_wall_ms)
     lib().o_run_free(C.byref(r))
+    reset_outputs()
     return tr, dg, stats
 
 
@@ -179,3 +193,26 @@ def rand_r(state: int):
     s = C.c_uint32(state)
     v = lib().o_rand_r(C.byref(s))
     return v, s.value
+
+
+def reset_outputs():
+    """Clear the oracle's optional output / input hooks (heartbeat snapshots,
+    path counts, pushed events, the mark): they point at caller arrays."""
+    lib().o_engine_set_heartbeats_out(None, 0)
+    lib().o_engine_set_counts_out(None, 0)
+    lib().o_engine_set_pushes(None, 0)
+    lib().o_engine_set_mark((1 << 64) - 1)
+
+
+def baseline(model: S.ModelArrays, g: S.GraphArrays, t_mark: int, t_end: int, threads: int) -> dict:
+    """The bench's CPU baseline (oracle.h o_baseline): warm up to t_mark, then
+    the window [t_mark, t_end) serially on one core and in parallel rounds on
+    `threads` cores from the same state; returns the timings, the counts and
+    whether both end states are equal."""
+    reset_outputs()
+    o = OBaseline()
+    rc = lib().o_baseline(C.byref(model.struct), C.byref(g.struct), int(t_mark), int(t_end), int(threads),
+                          C.byref(o))
+    out = {f: getattr(o, f) for f, _ in OBaseline._fields_}
+    out["rc"] = rc
+    return out

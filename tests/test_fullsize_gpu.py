@@ -1,111 +1,170 @@
-"""Event-loop parity at BASELINE's full sizes (C3: 10 k hosts on the 10 k-vertex
-geometric graph; the N = 2 bench workload: 20 k hosts on the same graph).
+"""Event-loop parity at BASELINE's full sizes against oracle fixtures.
 
-The serial oracle needs about a minute for the 10 k Dijkstra rows alone, so at
-these sizes parity is checked through properties that do not depend on size:
-the run is the same, bit for bit, whether the hosts run on one engine or are
-sharded over an engine group exactly as bench.py --gpus N shards them
-(contiguous registration-order blocks, one all-to-all per round), and the same
-from one run to the next (the reference's determinism tests,
-src/test/determinism).  The small-size tests in test_engine_gpu.py tie both
-sides to the oracle.
+tests/golden/make_fullsize.py ran the serial oracle (the reference's
+--workers 0 loop restated) on each configuration of tests/fullsize_configs.py
+and committed what the HIP engine must reproduce bit for bit:
+
+* C1  the bundled example config (2 hosts, 1-vertex topology) through the
+      config front-end: the full trace and both host digests;
+* C3  the bench's headline (10 k hosts on the 10 k-vertex graph, lossless) and
+      its lossy run (edge loss U[0, 0.0005]), 3 simulated seconds: every host's
+      digest and trace multiset hash, on one engine and on groups of 2 and 4
+      engines sharded as bench.py --gpus N shards them;
+* C5  1 M hosts with CoDel queues building (1500-B payloads, rx 1024 KiB/s):
+      digest hashes per 1024-host block and the counter sums, on one engine and
+      on a 2-engine group.
+
+Beyond the fixtures, the bench workloads at N = 1..8 (N x 10 k hosts) sharded
+over N engines must equal one engine running all the hosts (the reference's
+determinism tests compare runs the same way, src/test/determinism).
 """
+import os
+
 import numpy as np
 import pytest
 
+import fixture_hash as FH
 import shdgpu as S
 import workloads as W
-from sim import Engine, PathCache
+from fullsize_configs import CONFIGS, V, build, c3_hosts
+from sim import Engine, PathCache, XGroup, sort_trace
 
 pytestmark = pytest.mark.gpu
 
-V = 10000
-END = 3 * S.SHD_SEC          # boot, application start at 1 s, two seconds of traffic
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def bench_workload(hosts):
-    """The host placement and PHOLD model bench.py builds (seed 1, load 16,
-    1-byte payloads, edge loss U[0, 0.0005])."""
-    g = W.geometric_graph(V, seed=1, loss_max=0.0005)
-    hpv = max(1, hosts // V)
-    hv = (np.arange(hosts, dtype=np.int64) * V // hosts).astype(np.int32) if hosts != V * hpv else \
-        W.hosts_on_vertices(V, hpv)
-    m = W.phold_model(hv, end_time=END, seed=1, load=16, payload=1)
-    return g, m
+def fixture(key):
+    return np.load(os.path.join(GOLDEN, CONFIGS[key]["file"]))
 
 
-def single(m, pc):
-    e = Engine(m, pc)
-    st = e.run()
-    dg = e.digest()
-    e.close()
-    return st, dg
+def run_engines(m, pc, parts, pushes=None):
+    """One engine (parts = 1) or a local group of `parts` engines; returns
+    (stats, engines, group or None)."""
+    from driver import partition
+    if parts == 1:
+        e = Engine(m, pc)
+        if pushes is not None:
+            e.boot()
+            e.push_events(pushes)
+        return e.run(), [e], None
+    pb = partition(m.n_hosts, parts)
+    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
+    if pushes is not None:
+        for e in engines:
+            e.boot()
+            mine = pushes[(pushes["dst"] >= e.h0) & (pushes["dst"] < e.h1)]
+            e.push_events(mine)
+    grp = XGroup.local(engines)
+    return grp.run(), engines, grp
 
 
-@pytest.fixture(scope="module")
-def c3():
-    g, m = bench_workload(V)
+def close_all(engines, grp):
+    if grp is not None:
+        grp.close()
+    for e in engines:
+        e.close()
+
+
+@pytest.mark.parametrize("parts", [1, 2])
+def test_c1_example_config_matches_oracle_fixture(parts):
+    fx = fixture("c1")
+    g, m, pushes = build("c1")
     pc = PathCache(g, W.attached_vertices(m.host_vertex))
-    yield g, m, pc
+    st, engines, grp = run_engines(m, pc, parts, pushes)
+    assert st.error == 0
+    tr = sort_trace(np.concatenate([e.trace() for e in engines]))
+    dg = np.concatenate([e.digest() for e in engines])
+    assert (st.n_events, st.n_pkt_events) == tuple(int(x) for x in fx["totals"][:2])
+    assert np.array_equal(tr, sort_trace(fx["trace"]))
+    assert np.array_equal(dg, fx["digest"])
+    close_all(engines, grp)
     pc.close()
 
 
-def test_c3_full_size_deterministic(c3):
-    _, m, pc = c3
-    st1, d1 = single(m, pc)
-    st2, d2 = single(m, pc)
-    assert st1.n_pkt_events > 1_000_000 and st1.error == 0
-    assert (st1.n_events, st1.n_pkt_events, st1.n_rounds) == (st2.n_events, st2.n_pkt_events, st2.n_rounds)
-    assert np.array_equal(d1, d2)
-    # per-host counters add up to the run's totals
-    assert int(d1["n_pkt_events"].sum()) == st1.n_pkt_events
-    assert int(d1["n_events"].sum()) == st1.n_events
+@pytest.fixture(scope="module", params=["c3", "c3_lossy"])
+def c3(request):
+    g, m, _ = build(request.param)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    yield request.param, m, pc
+    pc.close()
 
 
-@pytest.mark.parametrize("hosts,parts", [(V, 2), (2 * V, 2), (V, 4), (4 * V, 4), (8 * V, 8)])
+@pytest.mark.parametrize("parts", [1, 2, 4])
+def test_c3_full_size_matches_oracle_fixture(c3, parts):
+    key, m, pc = c3
+    fx = fixture(key)
+    st, engines, grp = run_engines(m, pc, parts)
+    assert st.error == 0
+    tr = np.concatenate([e.trace() for e in engines])
+    dg = np.concatenate([e.digest() for e in engines])
+    n_ev, n_pkt, n_tr = (int(x) for x in fx["totals"])
+    assert (st.n_events, st.n_pkt_events, len(tr)) == (n_ev, n_pkt, n_tr)
+    assert n_pkt > 1_000_000
+    assert np.array_equal(dg, fx["digest"])
+    th = FH.trace_host_hashes(tr, m.n_hosts)
+    bad = np.nonzero(th != fx["trace_hash"])[0]
+    assert len(bad) == 0, f"{len(bad)} hosts' traces differ, first {bad[:8]}"
+    close_all(engines, grp)
+
+
+@pytest.mark.parametrize("parts", [1, 2])
+def test_c5_codel_million_hosts_matches_oracle_fixture(parts):
+    cfg = CONFIGS["c5"]
+    fx = fixture("c5")
+    g, m, _ = build("c5")
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    st, engines, grp = run_engines(m, pc, parts)
+    assert st.error == 0
+    dg = np.concatenate([e.digest() for e in engines])
+    close_all(engines, grp)
+    pc.close()
+    n_ev, n_pkt, _ = (int(x) for x in fx["totals"])
+    assert (st.n_events, st.n_pkt_events) == (n_ev, n_pkt)
+    sums = [int(dg[f].sum()) for f in ("n_events", "n_pkt_events", "n_sent", "n_inet_drop", "n_codel_drop",
+                                       "n_recv")]
+    assert sums == [int(x) for x in fx["sums"]]
+    assert sums[4] > 10_000                    # CoDel dropped: the queues built
+    bh = FH.digest_block_hashes(dg, cfg["block"])
+    bad = np.nonzero(bh != fx["block_hash"])[0]
+    assert len(bad) == 0, f"{len(bad)} host blocks differ, first {bad[:8]}"
+
+
+def test_bench_headline_run_to_run_deterministic():
+    g = W.geometric_graph(V, seed=1, loss_max=0.0)
+    m = W.phold_model(c3_hosts(V), end_time=3 * S.SHD_SEC, seed=1, load=16, payload=1)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    outs = []
+    for _ in range(2):
+        e = Engine(m, pc)
+        st = e.run()
+        outs.append(((st.n_events, st.n_pkt_events, st.n_rounds), e.digest()))
+        e.close()
+    assert outs[0][0] == outs[1][0] and np.array_equal(outs[0][1], outs[1][1])
+    d1 = outs[0][1]
+    assert int(d1["n_pkt_events"].sum()) == outs[0][0][1]
+    pc.close()
+
+
+@pytest.mark.parametrize("hosts,parts", [(2 * V, 2), (4 * V, 4), (8 * V, 8)])
 def test_bench_workload_sharded_group_equals_single_engine(hosts, parts):
     """(N V, N) is bench.py --gpus N's workload (weak scaling: N x 10 k hosts on the
     same graph), sharded as its N ranks shard it."""
     from driver import partition
-    from sim import XGroup
-    g, m = bench_workload(hosts)
+    g = W.geometric_graph(V, seed=1, loss_max=0.0)
+    m = W.phold_model(c3_hosts(hosts), end_time=3 * S.SHD_SEC, seed=1, load=16, payload=1)
     pc = PathCache(g, W.attached_vertices(m.host_vertex))
-    st, d1 = single(m, pc)
+    e = Engine(m, pc)
+    st = e.run()
+    d1 = e.digest()
+    e.close()
     pb = partition(m.n_hosts, parts)
     engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
     grp = XGroup.local(engines)
     gst = grp.run()
-    dg = np.concatenate([e.digest() for e in engines])
+    dg = np.concatenate([x.digest() for x in engines])
     assert gst.error == 0
     assert gst.n_pkt_events == st.n_pkt_events and gst.n_events == st.n_events
     assert np.array_equal(dg, d1)
-    grp.close()
-    for e in engines:
-        e.close()
-    pc.close()
-
-
-def test_c5_million_hosts_group_equals_single_engine():
-    """BASELINE C5's scale on one GPU: 1 M hosts, 100 per vertex of the 10 k-vertex
-    graph (the scripts/c5_single.sh workload).  The application start logs
-    ~16 M first touches, so the protected rounds run here; two engines of a
-    group must end where one engine ends."""
-    from driver import partition
-    from sim import XGroup
-    g = W.geometric_graph(V, seed=1, loss_max=0.0005)
-    m = W.phold_model(W.hosts_on_vertices(V, 100), end_time=int(1.5 * S.SHD_SEC), seed=1, load=16,
-                      payload=1)
-    pc = PathCache(g, W.attached_vertices(m.host_vertex))
-    st, d1 = single(m, pc)
-    assert st.error == 0 and st.n_rounds_protected > 0 and st.n_pkt_events > 10_000_000
-    pb = partition(m.n_hosts, 2)
-    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(2)]
-    grp = XGroup.local(engines)
-    gst = grp.run()
-    assert gst.error == 0
-    assert gst.n_pkt_events == st.n_pkt_events and gst.n_events == st.n_events
-    assert np.array_equal(np.concatenate([e.digest() for e in engines]), d1)
-    grp.close()
-    for e in engines:
-        e.close()
+    close_all(engines, grp)
     pc.close()

@@ -160,12 +160,37 @@ def test_oracle_heartbeat_counters_follow_the_trace():
     assert checked > 200 and int(hb[:, -1].sum()) > 1000
     lines = S.tracker_node_lines(hb[3], S.SHD_SEC, 1)
     assert lines[0].startswith("[shadow-heartbeat] [node-header] interval-seconds,")
-    assert len(lines) == 4
+    # the boot heartbeat (tracker_new -> tracker_heartbeat inline, tracker.c:141)
+    # logs an all-zero line, then one line per periodic heartbeat: K + 1 lines
+    assert len(lines) == 1 + 1 + 3
+    assert lines[1] == lines[1].split("] [node] ")[0] + "] [node] 1,0,0,0.000000,0,0.000000;" + ";".join(
+        [",".join(["0"] * 12)] * 4)
     d = np.diff(np.vstack([[0, 0], hb[3].astype(np.int64)]), axis=0)
-    for line, (din, dout) in zip(lines[1:], d):
+    for line, (din, dout) in zip(lines[2:], d):
         head, loc_in, loc_out, rem_in, rem_out = line.split("] [node] ")[1].split(";")
         f = head.split(",")
         assert f[0] == "1" and int(f[1]) == din * 43 and int(f[2]) == dout * 43
         assert loc_in == loc_out == ",".join(["0"] * 12)
         assert rem_in.split(",")[:2] == [str(din), str(din * 43)]
         assert rem_out.split(",")[6:9] == [str(dout), str(dout * 42), str(dout)]
+
+
+@pytest.mark.parametrize("kind", ["rows", "rows_lossy", "complete"])
+def test_parallel_rounds_equal_the_serial_loop(kind):
+    """The CPU baseline's parallel variant (host-partitioned rounds of W <=
+    every path latency, per-host queues, first touches resolved at the round's
+    end in serial order) ends in the serial loop's state, bit for bit, from a
+    state warmed up serially; several first-touch rounds fall in the window."""
+    if kind == "complete":
+        g = W.bundled_graph()
+        hv = np.sort(np.random.default_rng(3).integers(0, g.n_vertices, 600)).astype(np.int32)
+    else:
+        g = W.geometric_graph(400, seed=9, loss_max=0.01 if kind == "rows_lossy" else 0.0)
+        hv = W.hosts_on_vertices(400, 1)
+    m = W.phold_model(hv, end_time=4 * S.SHD_SEC, load=8)
+    out = O.baseline(m, g, int(1.3 * S.SHD_SEC), 4 * S.SHD_SEC, 4)
+    assert out["rc"] == 0 and out["same_end_state"] == 1, out
+    assert out["serial_pkt_events"] == out["parallel_pkt_events"] > 10000
+    assert out["ambiguous"] == 0
+    if kind != "complete":
+        assert out["parallel_first_touch"] > 0

@@ -1,0 +1,91 @@
+"""The engine group across PROCESSES: `world` child processes, one engine
+each, over the host-memory communicator (shd_comm_create_host; RCCL refuses
+two ranks on one GPU, so this is how the multi-process group protocol runs on
+a one-GPU box).  Every rank builds its share of the path cache's source rows
+and all-gathers them (shd_pc_build_sharded, APSP sharded by source rows); the
+group then runs the round protocol of shd_xgroup -- per-round all-to-all of
+blocks with headers, halts, first-touch logs gathered from every rank, spills
+delivered with the all-to-all-v, protected rounds -- with stops and resumes.
+The union of the ranks' traces and host states must be the serial oracle's,
+bit for bit, and every rank's table the single-process build's.
+"""
+import os
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+import shdgpu as S
+import workloads as W
+from sim import PathCache, sort_trace
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def run_ranks(world, tmp_path, extra=(), env_extra=None, timeout=240):
+    name = "shdtest_" + uuid.uuid4().hex[:16]
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "xgroup_worker.py"), "--rank", str(r),
+                               "--world", str(world), "--name", name, "--out", str(tmp_path)] + list(extra),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env)
+             for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append(out.decode(errors="replace"))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{outs[r][-3000:]}"
+    return [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(world)]
+
+
+def check_against_oracle(res, V, hpv, end_s, loss, load):
+    g = W.geometric_graph(V, seed=6, loss_max=loss)
+    m = W.phold_model(W.hosts_on_vertices(V, hpv), end_time=int(end_s * S.SHD_SEC), trace=True, load=load)
+    otr, odg, ost = O.engine_run(m, g)
+    tr = sort_trace(np.concatenate([r["trace"] for r in res]))
+    dg = np.concatenate([r["digest"] for r in res])
+    pkt = sum(int(r["stats"][0]) for r in res)
+    assert pkt == ost["n_pkt_events"] > 0
+    assert np.array_equal(tr, sort_trace(otr))
+    assert np.array_equal(dg, odg)
+    # the sharded tables are the one-process build's, on every rank
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    lat, rel = pc.rows()
+    info = pc.info()
+    for r in res:
+        assert np.array_equal(r["lat"].view(np.uint64), lat.view(np.uint64))
+        assert np.array_equal(r["rel"].view(np.uint64), rel.view(np.uint64))
+        assert tuple(r["ties"].tolist()) == (info.n_ties, info.max_hops, info.sssp_iterations_max)
+    pc.close()
+    return res
+
+
+@pytest.mark.parametrize("world,block", [(2, 0), (3, 0), (2, 4)])
+def test_multiprocess_group_matches_oracle(world, block, tmp_path):
+    """block 4: tiny per-peer blocks force spills (halts + the all-to-all-v)."""
+    res = run_ranks(world, tmp_path, extra=["--block", str(block)])
+    check_against_oracle(res, 240, 1, 3.0, 0.01, 16)
+    assert sum(int(r["stats"][2]) for r in res) > 0          # first-touch logs resolved across ranks
+    rounds = {int(r["stats"][3]) for r in res}
+    assert len(rounds) == 1                                    # every rank ran the same rounds
+
+
+def test_multiprocess_group_rolls_back_ambiguous_rounds(tmp_path):
+    """Every undecided first-touch send forced ambiguous and every round
+    protected: each logging round is rolled back on every process from its
+    state copy, ranked from the logs all-gathered from every rank, rerun."""
+    res = run_ranks(2, tmp_path, extra=["--vertices", "160", "--hpv", "2"],
+                    env_extra={"SHD_FORCE_AMBIG": "1", "SHD_PROTECT_ALL": "1"})
+    check_against_oracle(res, 160, 2, 3.0, 0.01, 16)
+    assert all(int(r["stats"][5]) > 0 for r in res)            # reruns happened on every rank
