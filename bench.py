@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--vertices", type=int, default=10000)
     ap.add_argument("--hosts-per-gpu", type=int, default=10000)
-    ap.add_argument("--load", type=int, default=16)
+    ap.add_argument("--load", type=int, default=None,
+                    help="PHOLD messages per host at the application start (default 16; 4 for c4)")
     ap.add_argument("--payload", type=int, default=1)
     ap.add_argument("--step-ms", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1)
@@ -50,6 +51,11 @@ def parse():
     ap.add_argument("--lossy-edge-loss-max", type=float, default=0.0005,
                     help="edge loss ~ U[0, x] of the lossy C3 run reported beside the headline "
                          "(its packet events per step show the decay); 0 skips it")
+    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
+                    help="c3: PHOLD-UDP on the geometric topology (the headline, weak scaling); c4: the "
+                         "Tor-scale relay/client model on the bundled topology (hosts fixed, strong scaling)")
+    ap.add_argument("--relays", type=int, default=6500)
+    ap.add_argument("--clients", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=0,
                     help="timed steps the CPU baseline runs (0 = all of them: the same window as value)")
@@ -75,6 +81,8 @@ os.dup2(2, 1)
 
 def main():
     args = parse()
+    if args.load is None:
+        args.load = 4 if args.workload == "c4" else 16
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -95,29 +103,58 @@ def main():
     from driver import DistCluster, partition
 
     t_setup = time.perf_counter()
-    V = args.vertices
-    H = args.hosts_per_gpu * max(world, 1)
-    g = W.geometric_graph(V, seed=args.seed, loss_max=args.edge_loss_max)
-    hpv = max(1, H // V)
-    host_vertex = (np.arange(H, dtype=np.int64) * V // H).astype(np.int32) if H != V * hpv else \
-        W.hosts_on_vertices(V, hpv)
     step = args.step_ms * S.SHD_MS
     end_time = (args.warmup + args.steps) * step
-    model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load,
-                          payload=args.payload)
+    if args.workload == "c4":
+        # BASELINE C4: Tor-scale relays + clients on the bundled topology,
+        # the hosts split over the ranks (strong scaling: the total is fixed)
+        g, model = W.tor_model(args.relays, args.clients, end_time=end_time, seed=args.seed, load=args.load,
+                               payload=args.payload)
+        host_vertex = model.host_vertex
+        V, H = g.n_vertices, model.n_hosts
+    else:
+        V = args.vertices
+        H = args.hosts_per_gpu * max(world, 1)
+        g = W.geometric_graph(V, seed=args.seed, loss_max=args.edge_loss_max)
+        hpv = max(1, H // V)
+        host_vertex = (np.arange(H, dtype=np.int64) * V // H).astype(np.int32) if H != V * hpv else \
+            W.hosts_on_vertices(V, hpv)
+        model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load,
+                              payload=args.payload)
     att = W.attached_vertices(host_vertex)
+    use_group = args.group or (world > 1 and args.exchange == "rccl")
+    comm = None
+    if use_group:
+        # one communicator per process: the sharded path-cache build and the
+        # engine group's per-round exchange both run over it
+        from sim import Comm, XGroup
+        uid = torch.zeros(S.SHD_XID_BYTES, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(XGroup.unique_id()), dtype=torch.uint8))
+        if world > 1:
+            dist.broadcast(uid, 0)
+        comm = Comm.rccl(bytes(uid.cpu().numpy().tobytes()), max(world, 1), rank, dev)
     # host buffers handed over at the boundary (graph CSR, model tables): their
     # upload is timed apart and reported as the PCIe-inclusive rate, never `value`
     torch.cuda.synchronize()
     t_up = time.perf_counter()
-    pc = PathCache(g, att, device=dev)
+    pc = PathCache(g, att, device=dev, build=False)
     torch.cuda.synchronize()
     upload_s = time.perf_counter() - t_up
-    builds = []
+    # APSP (BASELINE metric 2): every rank builds every row (replicated), and
+    # with a communicator each rank builds its block of rows and all-gathers
+    # them (sharded by source rows); both timed, the engine runs on the last
+    builds, sharded = [], []
     for _ in range(2):
         pc.build()
         builds.append(pc.info().build_ms_device)
     info = pc.info()
+    if comm is not None and world > 1:
+        for _ in range(2):
+            if world > 1:
+                dist.barrier()
+            pc.build_sharded(comm)
+            sharded.append(pc.info().build_ms_device)
     pb = partition(H, max(world, 1))
     t_up = time.perf_counter()
     eng = Engine(model, pc, pb[rank], pb[rank + 1], device=dev)
@@ -126,15 +163,8 @@ def main():
     log(rank, f"setup {time.perf_counter() - t_setup:.1f}s  V={V} E={g.n_edges} H={H} W={eng.window}ns "
               f"apsp={min(builds):.1f}ms iters={info.sssp_iterations_max} hops={info.max_hops}")
 
-    use_group = args.group or (world > 1 and args.exchange == "rccl")
     if use_group:
-        from sim import XGroup
-        uid = torch.zeros(S.SHD_XID_BYTES, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(XGroup.unique_id()), dtype=torch.uint8))
-        if world > 1:
-            dist.broadcast(uid, 0)
-        grp = XGroup.rccl(eng, bytes(uid.cpu().numpy().tobytes()), max(world, 1), rank)
+        grp = XGroup.over(eng, comm)
         run = lambda t: grp.run_until(t)  # noqa: E731
     elif world > 1:
         cl = DistCluster(eng, pb, rank, world, dist, torch)
@@ -198,12 +228,12 @@ def main():
                 "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1)}
 
     lossy = None
-    if world == 1 and args.lossy_edge_loss_max > 0 and not use_group:
+    if world == 1 and args.lossy_edge_loss_max > 0 and not use_group and args.workload == "c3":
         lossy = lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, torch)
 
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline = cpu_leg(args, S, W, g, host_vertex, step, value)
+        cpu_baseline = cpu_leg(args, S, W, g, model, step, value)
 
     if rank == 0:
         out = {
@@ -215,13 +245,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "c4" else "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (random geometric topology + PHOLD-UDP traffic, seed %d)" % args.seed,
-            "config": {"workload": "C3 PHOLD-UDP, stationary population (N x %d hosts, %d-vertex geometric topology)"
-                                   % (args.hosts_per_gpu, V),
-                       "edge_loss": "U[0,%g]" % args.edge_loss_max,
+            "data": ("synthetic (bundled topology, Tor-scale relay/client PHOLD-UDP traffic, seed %d)"
+                     if args.workload == "c4" else
+                     "synthetic (random geometric topology + PHOLD-UDP traffic, seed %d)") % args.seed,
+            "config": {"workload": ("C4 Tor-scale (%d relays + %d clients, bundled %d-vertex topology; edge loss "
+                                    "0.005: the population decays, the rate depends on the window)"
+                                    % (args.relays, args.clients, V)) if args.workload == "c4" else
+                                   ("C3 PHOLD-UDP, stationary population (N x %d hosts, %d-vertex geometric topology)"
+                                    % (args.hosts_per_gpu, V)),
+                       "edge_loss": "bundled (0.005)" if args.workload == "c4" else "U[0,%g]" % args.edge_loss_max,
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
                        "payload_bytes": args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
                        "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1),
@@ -236,7 +271,11 @@ def main():
             "first_touch": protected,
             "apsp": {"rows": int(info.rows_computed), "vertices": V, "build_ms": round(min(builds), 3),
                      "sssp_kernel_ms": round(info.build_ms_sssp, 3), "iterations": int(info.sssp_iterations_max),
-                     "max_hops": int(info.max_hops), "ties": int(info.n_ties)},
+                     "max_hops": int(info.max_hops), "ties": int(info.n_ties),
+                     "replicated_build_ms": round(min(builds), 3),
+                     "sharded_build_ms": round(min(sharded), 3) if sharded else None,
+                     "sharded_note": "rows [r*T/N, (r+1)*T/N) per rank + RCCL all-gather (wall time of the call)"
+                                     if sharded else "N = 1: no sharding"},
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
             "lossy_c3": lossy,
@@ -248,6 +287,8 @@ def main():
         grp.close()
     eng.close()
     pc.close()
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 
@@ -306,7 +347,7 @@ def cpu_threads():
     return max(1, n or min(len(os.sched_getaffinity(0)), 16))
 
 
-def cpu_leg(args, S, W, g, host_vertex, step, value):
+def cpu_leg(args, S, W, g, model, step, value):
     """The reference's scheduler semantics on the host cores, on the SAME
     workload and simulated window as `value` (oracle.h o_baseline): one
     warm-up to t = warmup steps (Dijkstra rows on all cores, then the serial
@@ -330,8 +371,8 @@ def cpu_leg(args, S, W, g, host_vertex, step, value):
     n_steps = args.steps if args.cpu_sample_steps <= 0 else min(args.steps, args.cpu_sample_steps)
     t_mark = args.warmup * step
     t_end = t_mark + n_steps * step
-    m = W.phold_model(host_vertex, end_time=(args.warmup + args.steps) * step, seed=args.seed, load=args.load,
-                      payload=args.payload)
+    m = model
+    host_vertex = model.host_vertex
     thr = cpu_threads()
     b = O.baseline(m, g, t_mark, t_end, thr)
     ser = b["serial_pkt_events"] / (b["serial_ms"] * 1e-3) if b["serial_ms"] > 0 else None
@@ -340,7 +381,7 @@ def cpu_leg(args, S, W, g, host_vertex, step, value):
     return {"value": round(ser, 1) if ser else None, "unit": "packet events/s", "cores": 1, "kind": "port",
             "sample": "oracle serial loop (reference --workers 0 semantics) on the bench's own workload "
                       "(%d hosts, %d-vertex graph, load %d) over %s: %d packet events in %.2f s"
-                      % (len(host_vertex), args.vertices, args.load, win, b["serial_pkt_events"],
+                      % (len(host_vertex), g.n_vertices, args.load, win, b["serial_pkt_events"],
                          b["serial_ms"] * 1e-3),
             "parallel": {"value": round(par, 1) if par else None, "cores": int(b["threads"]),
                          "kind": "port",

@@ -3567,6 +3567,9 @@ static int snapshot_state(shd_eng* e, bool restore) {
 
 static bool want_protect(const shd_eng* e) {
     if (protect_off() || e->snap_failed) return false;
+    // complete graphs serve the direct value, which does not depend on which
+    // endpoint came first: nothing is ever logged, nothing can be ambiguous
+    if (e->P.complete && !protect_all()) return false;
     return protect_all() || !e->logged_any || e->last_logged >= kProtectMin;
 }
 
@@ -3663,8 +3666,12 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             float ms = 0;
             if (hipEventElapsedTime(&ms, e->bev[0], e->bev[1]) == hipSuccess) s.device_ms_launches += ms;
         }
-        // ticketless batches only while no round logs a first touch
-        bool logged = false;
+        // ticketless batches unless first touches come thick: a ticketless
+        // round that logs halts its batch for the host's resolution, a
+        // ticketed one resolves a small log on the device.  After a batch
+        // with at most one logging round the next batch is ticketless (the
+        // late, rare logs cost one halt each); after more, it is ticketed.
+        uint32_t n_logs = 0;
         for (int i = 0; i < B; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
@@ -3672,7 +3679,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             const double ms = round_kernel_ms(e, r);
             e->kernel_ms_total += ms;
             e->last_kernel_ms = ms;
-            if (r.n_pending) logged = true;
+            if (r.n_pending) n_logs++;
             const bool halted_here = halt && r.n_pending > (tl ? 0ull : (unsigned long long)kResolveMax);
             s.n_rounds++;
             s.n_events += r.n_events;
@@ -3714,10 +3721,12 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             }
             next = r.next_time;
         }
-        e->tl_ready = !logged && !halt;
+        static const bool tl_strict = getenv("SHD_TL_STRICT") != nullptr;   // A/B: ticketless only after a quiet batch
+        e->tl_ready = tl_strict ? (n_logs == 0 && !halt) : n_logs <= 1;
     }
     e->h_sum->next_time = next;
-    e->t_done = std::max<uint64_t>(e->t_done, s.final_time);
+    // every event before `stop` has run: the engine's clock stands at stop
+    if (rc == SHD_OK) e->t_done = std::max<uint64_t>(e->t_done, std::min<uint64_t>(stop, next));
     s.n_pending_resolved = e->pending_resolved - pend0;
     s.device_ms_round_kernel = e->kernel_ms_total;
     s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -3954,6 +3963,7 @@ struct shd_xgroup {
 
 static bool x_want_protect(const shd_xgroup* g) {
     if (protect_off()) return false;
+    if (g->engs[0]->P.complete && !protect_all()) return false;   // nothing is ever logged (want_protect)
     for (const shd_eng* e : g->engs)
         if (e->snap_failed) return false;
     return protect_all() || !g->logged_any || g->last_logged >= kProtectMin;
@@ -4566,7 +4576,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
     for (int k = 0; k < nl; k++) {
         shd_eng* e = g->engs[k];
         e->h_sum->next_time = g->next;
-        e->t_done = std::max<uint64_t>(e->t_done, s.final_time);
+        if (rc == SHD_OK) e->t_done = std::max<uint64_t>(e->t_done, std::min<uint64_t>(stop, g->next));
         s.n_pending_resolved += e->pending_resolved - pend0[k];
     }
     s.device_ms_round_kernel = kms;

@@ -227,6 +227,16 @@ def tor_model(n_relays: int, n_clients: int, *, end_time, seed=1, load=4, payloa
     w_relay_row = np.concatenate([wr, np.full(n_clients, cw)])
     cum = np.stack([phold_cum(w_relay_row), phold_cum(w_client_row)])
     cls = np.concatenate([np.zeros(n_relays, np.uint8), np.ones(n_clients, np.uint8)])
+    # the popular relays take far more than a uniform share of the traffic:
+    # per-host queue capacities sized for the heaviest relay, not the mean
+    # (an overflow is reported as SHD_EOVERFLOW, never silent)
+    p_client = wr.max() / float(np.add.accumulate(wr)[-1])
+    p_relay = wr.max() / float(np.add.accumulate(w_relay_row)[-1])
+    burst = load * (n_clients * p_client + n_relays * p_relay)   # the start's sends to the heaviest relay
+    pow2 = lambda x: 1 << int(math.ceil(math.log2(max(x, 1))))  # noqa: E731
+    caps.setdefault("inbox_cap", max(1024, pow2(2 * burst)))
+    caps.setdefault("evq_cap", max(2048, pow2(4 * burst)))
+    caps.setdefault("codelq_cap", max(1024, pow2(2 * burst)))
     m = phold_model(vert, end_time=end_time, seed=seed, bw_down=bd, bw_up=bu, load=load, payload=payload,
                     app_start=app_start, trace=trace, dest_cum=cum, host_class=cls, host_rng=rng, **caps)
     return g, m

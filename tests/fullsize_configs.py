@@ -42,5 +42,5 @@ def build(key, trace=None):
         return g, m, None
     # c5: CoDel queues building at 1 M hosts
     m = W.phold_model(W.hosts_on_vertices(V, 100), end_time=cfg["end"], seed=1, load=32, payload=1500,
-                      bw_down=1024, bw_up=10240, codelq_cap=256, trace=bool(trace))
+                      bw_down=512, bw_up=10240, codelq_cap=256, trace=bool(trace))
     return g, m, None

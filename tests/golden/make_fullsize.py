@@ -16,7 +16,7 @@ bench runs them, and commits what the HIP engine must reproduce bit for bit:
   c3_lossy_full.npz   the same with edge loss U[0, 0.0005] (bench's lossy run).
   c5_codel_full.npz   C5 at full size with CoDel queues building: 1 M hosts,
                       100 per vertex of the 10 k-vertex graph, edge loss
-                      U[0, 0.01], 1500-B payloads, rx 1024 KiB/s, load 32,
+                      U[0, 0.01], 1500-B payloads, rx 512 KiB/s, load 32,
                       to 1.25 s (the application starts at 1 s): digest hashes
                       per 1024-host block, the CoDel drop total, totals.
 

@@ -10,7 +10,7 @@ and committed what the HIP engine must reproduce bit for bit:
       its lossy run (edge loss U[0, 0.0005]), 3 simulated seconds: every host's
       digest and trace multiset hash, on one engine and on groups of 2 and 4
       engines sharded as bench.py --gpus N shards them;
-* C5  1 M hosts with CoDel queues building (1500-B payloads, rx 1024 KiB/s):
+* C5  1 M hosts with CoDel queues building (1500-B payloads, rx 512 KiB/s):
       digest hashes per 1024-host block and the counter sums, on one engine and
       on a 2-engine group.
 
@@ -124,7 +124,7 @@ def test_c5_codel_million_hosts_matches_oracle_fixture(parts):
     sums = [int(dg[f].sum()) for f in ("n_events", "n_pkt_events", "n_sent", "n_inet_drop", "n_codel_drop",
                                        "n_recv")]
     assert sums == [int(x) for x in fx["sums"]]
-    assert sums[4] > 10_000                    # CoDel dropped: the queues built
+    assert sums[4] > 100_000                   # CoDel dropped: the queues built
     bh = FH.digest_block_hashes(dg, cfg["block"])
     bad = np.nonzero(bh != fx["block_hash"])[0]
     assert len(bad) == 0, f"{len(bad)} host blocks differ, first {bad[:8]}"

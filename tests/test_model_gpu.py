@@ -57,7 +57,9 @@ def test_three_weight_classes_on_geometric_graph(parts):
             w[V // 2:] = 0.0
         rows.append(W.phold_cum(w))
     cls = (np.arange(V) % 3).astype(np.uint8)
-    m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, dest_cum=np.stack(rows), host_class=cls)
+    # skewed weights: the heaviest hosts receive many times the mean (capacities sized for them)
+    m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, dest_cum=np.stack(rows), host_class=cls,
+                      inbox_cap=1024, evq_cap=4096, codelq_cap=1024)
     pc = PathCache(g, W.attached_vertices(hv))
     if parts == 1:
         eng = Engine(m, pc)
