@@ -323,12 +323,12 @@ def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, t
 
 def pmc_traffic(kernel):
     """HBM bytes per round-kernel launch from the committed rocprofv3 PMC
-    passes (profiles/r01/k_round_pmc_bytes.json: FETCH_SIZE x 2 + WRITE_SIZE,
+    passes (profiles/r02/k_round_pmc_bytes.json: FETCH_SIZE x 2 + WRITE_SIZE,
     the gfx950 correction), used only when that profile was taken of the
     kernel source being run; else None."""
     import hashlib
     try:
-        prof = json.load(open(os.path.join(REPO, "profiles", "r01", "k_round_pmc_bytes.json")))
+        prof = json.load(open(os.path.join(REPO, "profiles", "r02", "k_round_pmc_bytes.json")))
         src = open(os.path.join(REPO, "shadow-1_amd", "csrc", "engine.hip"), "rb").read()
     except (OSError, ValueError):
         return None

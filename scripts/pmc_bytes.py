@@ -35,7 +35,7 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--kernel", default="k_round_tl")
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r01", "k_round_pmc_bytes.json"))
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r02", "k_round_pmc_bytes.json"))
     a = ap.parse_args()
     fe = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
     wr = per_dispatch(a.write_dir, "WRITE_SIZE", a.kernel)
@@ -53,7 +53,7 @@ def main():
         "hbm_bytes_per_dispatch": int(round((2 * f_kb + w_kb) * 1024)),
         "correction": "FETCH_SIZE doubled (gfx950 reports 1/2 of 16-B/lane reads, MI355X_MICROARCH.md "
                       "HBM/rocprofv3 section); WRITE_SIZE as read",
-        "command": "rocprofv3 --pmc FETCH_SIZE (resp. WRITE_SIZE) -- python3 bench.py --steps 2 --warmup 2 "
+        "command": "rocprofv3 --pmc FETCH_SIZE (resp. WRITE_SIZE) -- python3 bench.py --steps 2 --warmup 2 --lossy-edge-loss-max 0 "
                    "--no-cpu-baseline, separate passes; averaged over every " + a.kernel + " dispatch of the run",
         "engine_source_sha1": hashlib.sha1(src).hexdigest(),
     }

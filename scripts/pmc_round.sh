@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-ARGS="--steps 1 --warmup 2 --no-cpu-baseline"
+ARGS="--steps 1 --warmup 2 --no-cpu-baseline --lossy-edge-loss-max 0"
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM" \
            "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES SQ_INSTS_LDS" ; do

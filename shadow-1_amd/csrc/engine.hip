@@ -3170,9 +3170,9 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         int rc;
         if ((rc = ealloc(e, &P.pcount, (size_t)pc->T * pc->T))) { shd_eng_destroy(e); return rc; }
     }
-    if ((m->queue_flags & SHD_QF_HEARTBEATS) && m->end_time > 0) {
-        // heartbeats at k * interval < end_time, k >= 1
-        const uint64_t k = (m->end_time - 1) / hb_min;
+    if (m->queue_flags & SHD_QF_HEARTBEATS) {
+        // heartbeats at k * interval < end_time, k >= 1 (none when end_time is 0)
+        const uint64_t k = m->end_time > 0 ? (m->end_time - 1) / hb_min : 0;
         if (k > (1u << 20)) { shd_eng_destroy(e); return SHD_ERANGE; }
         P.hb_k = (uint32_t)k;
         e->heartbeats = true;
