@@ -174,7 +174,9 @@ struct DestGuide {
 };
 static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 
-constexpr int kDestExc = 16;   // closed-form destination exceptions (ParamsT::exc_x)
+constexpr int kDestExc = 16;
+// ParamsT::feat: the model's optional features (all off on the bench's models)
+constexpr uint32_t F_TRACE = 1u, F_HB = 2u, F_PCOUNT = 4u, F_HOSTHB = 8u, F_AMBIG = 16u;   // closed-form destination exceptions (ParamsT::exc_x)
 
 template <template <class> class Ptr>
 struct ParamsT {
@@ -184,7 +186,7 @@ struct ParamsT {
     int32_t hpw;                // hosts per wave in the round kernel (lanes >= hpw idle)
     uint32_t evq_cap, inbox_cap, cq_cap, tq_cap;
     uint64_t end_time, bootstrap_end, heartbeat, app_start;
-    uint32_t load, payload, trace, pkt_len;
+    uint32_t load, payload, feat, pkt_len;   // feat: F_* optional features of the model
     // per-host state records (local index), and the earliest pending event
     // of each host's timers and heap (read alone by the idle test)
     Ptr<HostRec> hs;
@@ -368,13 +370,21 @@ __device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
 // keep; launder() makes each a VGPR value it must keep.
 struct HotK {
     uint64_t end_time, boot_end;
-    uint32_t pkt_len, cq_cap, tq_cap, evq_cap, trace;
+    uint32_t pkt_len, cq_cap, tq_cap, evq_cap;
+    uint32_t feat;   // F_* (wave-uniform, held in an SGPR)
 };
 template <class T>
 __device__ __forceinline__ T launder(T x) {
 #ifndef SHD_NO_LAUNDER
     asm volatile("" : "+v"(x));
 #endif
+    return x;
+}
+// the same for a wave-uniform value, kept in an SGPR: branches on it are
+// scalar branches, so a feature that is off costs a compare and a jump, and
+// the loads behind it are skipped rather than issued under an empty exec mask
+__device__ __forceinline__ uint32_t launder_s(uint32_t x) {
+    asm volatile("" : "+s"(x));
     return x;
 }
 
@@ -542,7 +552,7 @@ __device__ void heap_pop(const DParams& P, HostCtx& c) {
 
 __device__ __forceinline__ void trace(const DParams& P, HostCtx& c, uint64_t t, uint64_t seq, uint32_t host,
                                       uint32_t peer, uint32_t pkt, uint32_t kind) {
-    if (!c.k.trace) return;
+    if (!(c.k.feat & F_TRACE)) return;
     unsigned long long i = atomicAdd(P.trace_n, 1ull);
     if (i >= P.trace_cap) { c.err |= SHD_ERR_TRACE_OVERFLOW; return; }
     shd_trace_rec r;
@@ -554,8 +564,8 @@ __device__ __forceinline__ bool bootstrapping(const DParams& P, const HostCtx& c
 
 // the tracker interval of host h (<host heartbeatfrequency>, host.c:240; the
 // option default otherwise)
-__device__ __forceinline__ uint64_t hb_interval(const DParams& P, uint32_t h) {
-    return P.host_hb ? P.host_hb[h] : P.heartbeat;
+__device__ __forceinline__ uint64_t hb_interval(const DParams& P, uint32_t feat, uint32_t h) {
+    return (feat & F_HOSTHB) ? P.host_hb[h] : P.heartbeat;
 }
 
 __device__ __forceinline__ void hot_load(const DParams& P, HostCtx& c) {
@@ -565,7 +575,7 @@ __device__ __forceinline__ void hot_load(const DParams& P, HostCtx& c) {
     c.k.cq_cap = launder(P.cq_cap);
     c.k.tq_cap = launder(P.tq_cap);
     c.k.evq_cap = launder(P.evq_cap);
-    c.k.trace = launder(P.trace);
+    c.k.feat = launder_s(P.feat);
 }
 
 // event_new_ (consumes the source's event ID, event.c:38) + scheduler_push
@@ -1008,9 +1018,9 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         const bool pass = boot || chance <= pv.rel || P.payload == 0;
         if (!pv.resolved) {
             const bool pass2 = boot || chance <= pv.rel2 || P.payload == 0;
-            if (pass != pass2 || P.force_ambig) err |= SHD_ERR_AMBIGUOUS;
+            if (pass != pass2 || (c.k.feat & F_AMBIG)) err |= SHD_ERR_AMBIGUOUS;
         }
-        if (P.pcount && pass && pv.resolved) atomicAdd(&P.pcount[path_key(P, a, b, ra, x.rb, x.adj)], 1u);
+        if ((c.k.feat & F_PCOUNT) && pass && pv.resolved) atomicAdd(&P.pcount[path_key(P, a, b, ra, x.rb, x.adj)], 1u);
         shd_event e;
         e.time = q.now + (uint64_t)ceil(pv.lat * (double)SHD_MS);
         e.seq = 0;
@@ -1227,6 +1237,35 @@ __device__ void refill_cb(const DParams& P, HostCtx& c) {
 //   PACKET    router_enqueue, receive if the queue was empty
 //   NOTIFY    one new message per unread datagram, each sent right away
 //   APP_START `load` new messages
+// The steady-state notification, straight-line: one unread datagram, an
+// empty send queue with room in the send bucket and in the deferred-send
+// buffer, past the bootstrap period: one new message, sent at once unless it
+// draws this host (then the general send loop takes it).  The same draws and
+// steps, in the same order, as the general NOTIFY path of begin_event.
+__device__ __forceinline__ bool notify_fast_ok(const DParams& P, const HostCtx& c) {
+    return c.unread == 1u && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap &&
+           !(c.k.feat & F_TRACE) && !bootstrapping(P, c);
+}
+__device__ __forceinline__ void notify_fast(const DParams& P, HostCtx& c) {
+    c.flags &= ~F_NOTIFY_PENDING;
+    c.unread = 0;
+    const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
+    if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
+        random_free_port(c);
+        const uint32_t pkt = c.pkt_seq++;
+        if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
+            s_tqh[threadIdx.x] = TxEnt{rv, pkt};
+            c.tq_hv = true;
+            c.tq_count = 1;
+            c.w_fl = W_SENDING;
+        } else {
+            worker_send_deferred(P, c, rv, pkt);
+            consume(c.tx_rem, c.k.pkt_len);
+            refill_if_needed(P, c);
+        }
+    }
+}
+
 __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     TCNT(5);
     c.c_events++;
@@ -1244,7 +1283,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     // is consumed even when it falls past the end).  The same steps as the
     // general path below, in the same order.
     if (e.kind == SHD_EV_PACKET && c.cq_count == 0 && c.rx_rem >= SHD_MTU && (c.flags & F_LISTENING) &&
-        !c.k.trace && !bootstrapping(P, c)) {
+        !(c.k.feat & F_TRACE) && !bootstrapping(P, c)) {
         c.c_pkt++;
         c.c_recv++;
         c.if_in++;
@@ -1263,30 +1302,8 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         refill_if_needed(P, c);
         return;
     }
-    // The steady-state notification, straight-line: one unread datagram, an
-    // empty send queue with room in the send bucket and in the deferred-send
-    // buffer, past the bootstrap period: one new message, sent at once
-    // unless it draws this host (then the general send loop takes it).  The
-    // same draws and steps, in the same order, as the general path below.
-    if (e.kind == SHD_EV_NOTIFY && c.unread == 1u && c.tq_count == 0 && c.tx_rem >= SHD_MTU &&
-        c.ns < (uint32_t)kSendCap && !c.k.trace && !bootstrapping(P, c)) {
-        c.flags &= ~F_NOTIFY_PENDING;
-        c.unread = 0;
-        const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
-        if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
-            random_free_port(c);
-            const uint32_t pkt = c.pkt_seq++;
-            if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
-                s_tqh[threadIdx.x] = TxEnt{rv, pkt};
-                c.tq_hv = true;
-                c.tq_count = 1;
-                c.w_fl = W_SENDING;
-            } else {
-                worker_send_deferred(P, c, rv, pkt);
-                consume(c.tx_rem, c.k.pkt_len);
-                refill_if_needed(P, c);
-            }
-        }
+    if (e.kind == SHD_EV_NOTIFY && notify_fast_ok(P, c)) {
+        notify_fast(P, c);
         return;
     }
     // the periodic refill with both queues empty: top up; the receive loop's
@@ -1310,11 +1327,11 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     case SHD_EV_HEARTBEAT:
         // tracker_heartbeat (tracker.c:566-611): the node counters at the k-th
         // heartbeat, cumulative (the reader takes the per-interval differences)
-        if (P.hb) {
-            const uint64_t k = c.now / hb_interval(P, c.h);
+        if (c.k.feat & F_HB) {
+            const uint64_t k = c.now / hb_interval(P, c.k.feat, c.h);
             if (k >= 1 && k <= P.hb_k) P.hb[(size_t)c.l * P.hb_k + (k - 1)] = make_uint2(c.if_in, c.if_out);
         }
-        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, c.h), 0);
+        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, c.k.feat, c.h), 0);
         break;
     case SHD_EV_REFILL:
         // _networkinterface_refillTokenBucketsCB (network_interface.c:163-183)
@@ -1751,7 +1768,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         load_ctx(P, c, l, r, P.host_att[h], P.self_thr[h]);
         c.now = 0;
         c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
-        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, h), 0);   // tracker_new, tracker.c:141,607-610
+        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, c.k.feat, h), 0);   // tracker_new, tracker.c:141,607-610
         refill_cb(P, c);                                               // ethernet startRefilling
         schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);              // loopback refill at +1 ms
         if (!P.no_app_start) schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
@@ -2078,6 +2095,28 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                         i_be = clock64();
 #endif
                         st = (c.w_fl | c.w_msgs) ? 1u : 0u;   // the shared steps, if any are left
+#ifndef SHD_NO_FUSE
+                        // An arrival schedules its notification at +1 ns, and
+                        // that is almost always the host's next event: when the
+                        // notification timer is strictly the earliest candidate
+                        // (so take_next would return it next) and in the window,
+                        // it runs now, in the same iteration (the wave's lanes
+                        // then run arrival + notification together instead of
+                        // spreading them over two iterations)
+                        if (st == 0u && c.tt2 < we) {
+                            const uint64_t t = c.tt2, ht = c.evq_n ? c.top_time : kInf;
+                            if (t < c.tt0 && t < c.tt1 && t < c.dt && t < ht && notify_fast_ok(P, c)) {
+                                TCNT(5);
+                                c.tt2 = kInf;
+                                c.now = t;
+                                c.c_events++;
+                                c.q_seq = c.ts2; c.q_src = c.h; c.q_sub = 0;
+                                c.w_msgs = 0; c.w_fl = 0;
+                                notify_fast(P, c);
+                                st = c.w_fl ? 1u : 0u;
+                            }
+                        }
+#endif
                     } else {
                         st = 3u;
                     }
@@ -2989,7 +3028,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.cq_cap = m->codelq_cap ? m->codelq_cap : 64;
     P.tq_cap = m->txq_cap ? m->txq_cap : 64;
     P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
-    P.app_start = m->app_start; P.load = m->load; P.payload = m->payload; P.trace = m->trace;
+    P.app_start = m->app_start; P.load = m->load; P.payload = m->payload;
     P.pkt_len = m->payload + SHD_HEADER_UDP;
     P.force_ambig = getenv("SHD_FORCE_AMBIG") != nullptr;
     const size_t n = (size_t)e->nloc;
@@ -3179,6 +3218,8 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         int rc;
         if (k && (rc = ealloc(e, &P.hb, (size_t)n * k))) { shd_eng_destroy(e); return rc; }
     }
+    P.feat = (m->trace ? F_TRACE : 0u) | (P.hb ? F_HB : 0u) | (P.pcount ? F_PCOUNT : 0u) |
+             (P.host_hb ? F_HOSTHB : 0u) | (P.force_ambig ? F_AMBIG : 0u);
     P.sum = e->d_sum;
     // the serial-equivalent window W: min over every latency a send can be
     // served (rows, direct values, self values) -> ceil(lat * 1e6) ns
