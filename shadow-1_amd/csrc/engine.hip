@@ -1266,6 +1266,22 @@ __device__ __forceinline__ void notify_fast(const DParams& P, HostCtx& c) {
     }
 }
 
+// the periodic refill with both queues empty: top up; the receive loop's
+// one dequeue attempt only resets CoDel's interval and drop mode, the send
+// loop does nothing (as the general REFILL case of begin_event)
+__device__ __forceinline__ void refill_fast(const DParams& P, HostCtx& c) {
+    c.flags &= ~F_REFILL_PENDING;
+    c.rx_rem += c.rx_refill;
+    if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
+    c.tx_rem += c.tx_refill;
+    if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
+    if (bootstrapping(P, c) || c.rx_rem >= SHD_MTU) {
+        c.cq_iexp = 0;
+        c.flags &= ~F_CODEL_DROP_MODE;
+    }
+    refill_if_needed(P, c);
+}
+
 __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     TCNT(5);
     c.c_events++;
@@ -1306,20 +1322,8 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         notify_fast(P, c);
         return;
     }
-    // the periodic refill with both queues empty: top up; the receive loop's
-    // one dequeue attempt only resets CoDel's interval and drop mode, the
-    // send loop does nothing (as the general REFILL case below)
     if (e.kind == SHD_EV_REFILL && c.cq_count == 0 && c.tq_count == 0) {
-        c.flags &= ~F_REFILL_PENDING;
-        c.rx_rem += c.rx_refill;
-        if (c.rx_rem > c.rx_refill + SHD_MTU) c.rx_rem = c.rx_refill + SHD_MTU;
-        c.tx_rem += c.tx_refill;
-        if (c.tx_rem > c.tx_refill + SHD_MTU) c.tx_rem = c.tx_refill + SHD_MTU;
-        if (bootstrapping(P, c) || c.rx_rem >= SHD_MTU) {
-            c.cq_iexp = 0;
-            c.flags &= ~F_CODEL_DROP_MODE;
-        }
-        refill_if_needed(P, c);
+        refill_fast(P, c);
         return;
     }
 #endif
@@ -2114,6 +2118,20 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
                                 c.w_msgs = 0; c.w_fl = 0;
                                 notify_fast(P, c);
                                 st = c.w_fl ? 1u : 0u;
+                            }
+                        }
+                        // the same for the periodic refill (at the next 1 ms
+                        // boundary) with both queues empty
+                        if (st == 0u && c.tt1 < we) {
+                            const uint64_t t = c.tt1, ht = c.evq_n ? c.top_time : kInf;
+                            if (t < c.tt0 && t < c.tt2 && t < c.dt && t < ht && c.cq_count == 0 && c.tq_count == 0) {
+                                TCNT(5);
+                                c.tt1 = kInf;
+                                c.now = t;
+                                c.c_events++;
+                                c.q_seq = c.ts1; c.q_src = c.h; c.q_sub = 0;
+                                c.w_msgs = 0; c.w_fl = 0;
+                                refill_fast(P, c);
                             }
                         }
 #endif
