@@ -304,7 +304,11 @@ __device__ unsigned long long g_kc[10][4];
 // event-path counters (timing build): cq / tq entries loaded from HBM, heap
 // pushes / pops, inbox events merged, events, flushes, suspended lanes
 __device__ unsigned long long g_cnt[8];
+#ifdef SHD_TIMING_LIGHT   // phase stamps only: no per-event counters either
+#define TCNT(i)
+#else
 #define TCNT(i) atomicAdd(&g_cnt[i], 1ull)
+#endif
 __shared__ unsigned long long s_kc[10][4];
 #ifdef SHD_TIMING_NOWAIT   // stamps when the wave gets there, without draining its memory ops
 #define TIM_WAIT()
