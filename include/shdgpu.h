@@ -512,6 +512,15 @@ void shd_comm_destroy(shd_comm* c);
 int shd_pc_build_sharded(shd_pc* pc, shd_comm* comm);
 /* an engine group over a communicator (not owned: destroy it after the group) */
 int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out);
+/* the same group with the peer-to-peer transport: every engine's receive
+ * blocks in uncached device memory exported by IPC handle and mapped by every
+ * rank; a round's blocks are stored straight into the peers' receive blocks
+ * (xGMI between GPUs), header last under a tag that is never reused, and each
+ * receiver's next kernel waits for every peer's tag (bounded: 30 s, then
+ * SHD_ENODEV).  No collective launch per round; the communicator carries the
+ * handle exchange and the host-side recovery.  The ranks' processes must be
+ * able to map each other's memory (one node); all ranks fail alike if not. */
+int shd_xgroup_create_p2p(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out);
 /* block_events: events per peer block per round (0 = default) */
 int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
                            uint32_t block_events, shd_xgroup** out);

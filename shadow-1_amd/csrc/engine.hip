@@ -148,6 +148,7 @@ __device__ __forceinline__ DevSummary fresh_summary() {
 struct DevCtl {
     unsigned long long stop;
     unsigned long long round_base;
+    unsigned long long xtag;   // peer-to-peer exchanges: the tag of the batch's first round (round i: + i)
 };
 
 // Exchange mode (shd_xgroup): the per-peer blocks of the fixed-size
@@ -2859,6 +2860,87 @@ __global__ void k_ingest_x(DParams P, const shd_event* __restrict__ xrecv, const
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
 }
 
+// ---- peer-to-peer exchange (shd_xgroup_create_p2p) ----
+// Every engine's receive blocks ([2][world][stride] events) live in uncached
+// device memory exported by IPC handle and mapped by every peer; a sender
+// writes its block for peer p straight into p's receive blocks (over xGMI
+// between GPUs), header last, tagged with the exchange's number; the
+// receiver's next kernel waits for every peer's tag, then ingests.  Tags are
+// never reused (a rerun round takes new ones), so a stale block cannot match.
+constexpr unsigned long long kXWaitTicks = 3000000000ull;   // 30 s at the 100 MHz wall clock
+
+__device__ __forceinline__ uint32_t x_tag(const DevCtl* ctl, uint32_t add, int use_ctl) {
+    return use_ctl ? (uint32_t)ctl->xtag + add : add;
+}
+
+// block p: this engine's block for peer p -> p's receive block `me` of parity wi
+__global__ __launch_bounds__(256) void k_xput(const shd_event* __restrict__ xsend, shd_event* const* __restrict__ peers,
+                                               uint32_t stride, uint32_t xcap, int world, int me, int wi,
+                                               const DevCtl* __restrict__ ctl, uint32_t tag_add, int use_ctl) {
+    const int p = blockIdx.x;
+    const shd_event* src = xsend + (size_t)p * stride;
+    shd_event* dst = peers[p] + ((size_t)wi * world + me) * stride;
+    XHeader h = *(const XHeader*)src;
+    const uint32_t n = h.count < xcap ? h.count : xcap;
+    for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) dst[1 + s] = src[1 + s];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        h.pad = x_tag(ctl, tag_add, use_ctl);
+        uint32_t* hw = (uint32_t*)dst;
+        const uint32_t* hv = (const uint32_t*)&h;
+        for (int k = 0; k < 7; k++) hw[k] = hv[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the events and the header body first
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(hw + 7, hv[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// wait for every peer's block of this exchange (bounded: a peer that never
+// comes sets *xerr, and later waits of the batch return at once), then, for a
+// round's exchange, the received events -> the next round's calendar / inbox
+__global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event* __restrict__ xrecv,
+                                                       const DevCtl* __restrict__ ctl, uint32_t tag_add,
+                                                       int use_ctl, int ri, int ingest, uint32_t* __restrict__ xerr) {
+    __shared__ uint32_t s_bad;
+    const uint32_t tag = x_tag(ctl, tag_add, use_ctl);
+    const size_t stride = (size_t)P.xcap + 1;
+    if (threadIdx.x == 0) s_bad = __hip_atomic_load(xerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_bad) return;
+    if ((int32_t)threadIdx.x < P.xworld) {
+        const uint32_t* tw = (const uint32_t*)(xrecv + threadIdx.x * stride) + 7;
+        const unsigned long long t0 = wall_clock64();
+        while (__hip_atomic_load(tw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > kXWaitTicks) {
+                atomicOr(&s_bad, 1u);
+                __hip_atomic_fetch_or(xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (threadIdx.x == 0) *P.halt = 1u;
+        return;
+    }
+    if (!ingest || *P.halt) return;
+    const int parity = (int)((ctl->round_base + (uint64_t)ri + 1) & 1);   // the next round's inbox
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t p = t / P.xcap, s = t % P.xcap;
+    if (p >= (uint64_t)P.xworld) return;
+    const shd_event* blk = xrecv + p * stride;
+    if (s >= ((const XHeader*)blk)->count) return;
+    const shd_event e = blk[1 + s];
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
+    if (cal_push(P, dl, e, P.sum->ws)) return;
+    const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+    if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
+    P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+}
+
 __global__ void k_digest(DParams P, shd_host_digest* __restrict__ out) {
     const int32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= P.nloc) return;
@@ -4022,6 +4104,13 @@ struct shd_xgroup {
     // protected rounds (as for one engine): group-wide, so every rank decides alike
     bool logged_any = false;
     uint64_t last_logged = 0;          // first touches gathered from the whole group at the last log
+    // peer-to-peer transport (shd_xgroup_create_p2p; one engine per process)
+    bool p2p = false;
+    shd_event* p2p_base = nullptr;     // own receive blocks [2][world][stride], uncached, IPC-exported
+    std::vector<shd_event*> p2p_peer;  // every rank's receive blocks as mapped here (own: p2p_base)
+    shd_event** d_peers = nullptr;     // the same on the device
+    uint32_t* d_xerr = nullptr;        // set by a wait that timed out
+    uint64_t xepoch = 0;               // exchange tags issued (never rolled back)
 };
 
 static bool x_want_protect(const shd_xgroup* g) {
@@ -4044,10 +4133,40 @@ static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
 
 // the fixed-size all-to-all: block d of every sender's xsend -> block s of
 // receiver d's xrecv[xseq & 1]
+// a peer-to-peer exchange: every engine's blocks put into the peers' receive
+// blocks of parity wi under tag (ctl->xtag + tag_add, or tag_add), then the
+// wait for every peer's (and, for a round, the ingest of what came)
+static void x_p2p_launch(shd_xgroup* g, int wi, uint32_t tag_add, int use_ctl, const Params& P, int ri, int ingest) {
+    shd_eng* e = g->engs[0];
+    hipLaunchKernelGGL(k_xput, dim3(g->world), dim3(256), 0, e->stream, (const shd_event*)g->loc[0].xsend,
+                       (shd_event* const*)g->d_peers, (uint32_t)g->stride, g->xcap, g->world, g->rank0, wi,
+                       (const DevCtl*)e->d_ctl, tag_add, use_ctl);
+    const uint64_t nthr = ingest ? (uint64_t)g->world * g->xcap : 1;
+    hipLaunchKernelGGL(k_xwait_ingest, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, dp(P),
+                       (const shd_event*)g->loc[0].xrecv[wi], (const DevCtl*)e->d_ctl, tag_add, use_ctl, ri, ingest,
+                       g->d_xerr);
+}
+
+static int x_p2p_check(shd_xgroup* g) {
+    if (!g->p2p) return SHD_OK;
+    uint32_t bad = 0;
+    SHD_HIP(hipMemcpy(&bad, g->d_xerr, 4, hipMemcpyDeviceToHost));
+    if (bad) {
+        fprintf(stderr, "libshdgpu: peer-to-peer exchange: a peer's block did not come within %llu s\n",
+                kXWaitTicks / 100000000ull);
+        return SHD_ENODEV;
+    }
+    return SHD_OK;
+}
+
 static int x_exchange(shd_xgroup* g) {
     const size_t bytes = g->stride * sizeof(shd_event);
     const int wi = (int)(g->xseq & 1);
-    if (g->comm) {
+    if (g->p2p) {
+        const uint32_t tag = (uint32_t)(++g->xepoch);
+        x_p2p_launch(g, wi, tag, 0, xparams(g, 0, g->engs[0]->d_sum), 0, 0);
+        SHD_HIP(hipGetLastError());
+    } else if (g->comm) {
         shd_eng* e = g->engs[0];
         const int rc = shd_comm_alltoall_dev(g->comm, g->loc[0].xsend, g->loc[0].xrecv[wi], bytes, e->stream);
         if (rc) return rc;
@@ -4079,7 +4198,7 @@ static int x_headers(shd_xgroup* g, std::vector<XHeader>& h) {
     SHD_HIP(hipMemcpy2DAsync(h.data(), sizeof(XHeader), src, g->stride * sizeof(shd_event), sizeof(XHeader),
                              g->world, hipMemcpyDeviceToHost, e->stream));
     SHD_HIP(hipStreamSynchronize(e->stream));
-    return SHD_OK;
+    return x_p2p_check(g);
 }
 
 static int x_read_next(shd_xgroup* g) {
@@ -4215,6 +4334,74 @@ static int x_exchange_remote(shd_xgroup* g, int slot) {
     return rc;
 }
 
+static void x_p2p_unmap(shd_xgroup* g) {
+    for (size_t p = 0; p < g->p2p_peer.size(); p++)
+        if (g->p2p_peer[p] && g->p2p_peer[p] != g->p2p_base) (void)hipIpcCloseMemHandle(g->p2p_peer[p]);
+    g->p2p_peer.clear();
+    if (g->p2p_base) (void)hipFree(g->p2p_base);
+    g->p2p_base = nullptr;
+}
+
+// the peer-to-peer receive blocks: allocated uncached (a peer's stores land
+// in memory, no L2 of this GPU holds a stale copy), exported by IPC handle,
+// every rank's handle all-gathered and mapped.  The handle exchange is also
+// the barrier that makes the old blocks (a regrowth) free to release: every
+// rank is between batches, all puts into them done
+static int x_p2p_map(shd_xgroup* g) {
+    shd_eng* e = g->engs[0];
+    const int W = g->world;
+    x_p2p_unmap(g);
+    // every step is collective: a rank that fails still takes part in both
+    // all-gathers, so that every rank learns it and all fail alike
+    struct Share {
+        hipIpcMemHandle_t h;
+        uint32_t ok;
+        uint32_t pad[15];
+    };
+    Share mine{};
+    const size_t bytes = 2 * (size_t)W * g->stride * sizeof(shd_event);
+    if (hipExtMallocWithFlags((void**)&g->p2p_base, bytes, hipDeviceMallocUncached) == hipSuccess &&
+        hipMemset(g->p2p_base, 0, bytes) == hipSuccess &&   // tag 0: no exchange yet (tags start at 1)
+        hipDeviceSynchronize() == hipSuccess && hipIpcGetMemHandle(&mine.h, g->p2p_base) == hipSuccess)
+        mine.ok = 1;
+    (void)hipGetLastError();
+    std::vector<Share> all(W);
+    int rc = shd_comm_allgather_host(g->comm, &mine, sizeof(Share), all.data());
+    if (rc) return rc;
+    uint32_t ok = 1;
+    for (const Share& x : all) ok &= x.ok;
+    g->p2p_peer.assign(W, nullptr);
+    for (int p = 0; p < W && ok; p++) {
+        if (p == g->rank0) {
+            g->p2p_peer[p] = g->p2p_base;
+            continue;
+        }
+        void* q = nullptr;
+        if (hipIpcOpenMemHandle(&q, all[p].h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+            (void)hipGetLastError();
+            ok = 0;
+            break;
+        }
+        g->p2p_peer[p] = (shd_event*)q;
+    }
+    if (ok && !g->d_peers && ealloc(e, &g->d_peers, (size_t)64)) ok = 0;
+    if (ok && !g->d_xerr && ealloc(e, &g->d_xerr, 1)) ok = 0;
+    if (ok && hipMemcpy(g->d_peers, g->p2p_peer.data(), sizeof(shd_event*) * W, hipMemcpyHostToDevice) != hipSuccess)
+        ok = 0;
+    // the second all-gather: every rank mapped every block (and a barrier: no
+    // rank puts into the new blocks before every rank has them)
+    std::vector<uint32_t> oks(W);
+    if ((rc = shd_comm_allgather_host(g->comm, &ok, 4, oks.data()))) return rc;
+    for (uint32_t x : oks) ok &= x;
+    if (!ok) {
+        x_p2p_unmap(g);
+        return SHD_ENODEV;
+    }
+    g->loc[0].xrecv[0] = g->p2p_base;
+    g->loc[0].xrecv[1] = g->p2p_base + (size_t)W * g->stride;
+    return SHD_OK;
+}
+
 static int x_alloc(shd_xgroup* g) {
     g->stride = (size_t)g->xcap + 1;
     g->loc.resize(g->engs.size());
@@ -4224,8 +4411,13 @@ static int x_alloc(shd_xgroup* g) {
         SHD_HIP(hipSetDevice(e->device));
         const size_t n = g->stride * (size_t)g->world;
         int rc;
-        if ((rc = ealloc(e, &L.xsend, n)) || (rc = ealloc(e, &L.xrecv[0], n)) || (rc = ealloc(e, &L.xrecv[1], n)) ||
-            (rc = ealloc(e, &L.xcount, g->world)) || (rc = ealloc(e, &L.halt_hdr, g->world)) ||
+        if (g->p2p) {
+            if ((rc = ealloc(e, &L.xsend, n)) || (rc = x_p2p_map(g))) return rc;
+        } else if ((rc = ealloc(e, &L.xsend, n)) || (rc = ealloc(e, &L.xrecv[0], n)) ||
+                   (rc = ealloc(e, &L.xrecv[1], n))) {
+            return rc;
+        }
+        if ((rc = ealloc(e, &L.xcount, g->world)) || (rc = ealloc(e, &L.halt_hdr, g->world)) ||
             (rc = ealloc(e, &L.d_xpr, shd_eng::kRing, false)) ||
             (rc = ealloc(e, &L.parts, 2 * (size_t)((e->nloc + e->P.hpw - 1) / e->P.hpw))))
             return rc;
@@ -4264,6 +4456,7 @@ static void x_drop_graphs(shd_xgroup* g) {
 static void x_free(shd_xgroup* g) {
     if (!g) return;
     x_drop_graphs(g);
+    x_p2p_unmap(g);
     if (g->comm && g->own_comm) shd_comm_destroy(g->comm);
     for (auto& ev : g->eev)
         if (ev) (void)hipEventDestroy(ev);
@@ -4307,7 +4500,7 @@ extern "C" int shd_xgroup_create_local(shd_eng* const* engines, int n, uint32_t 
     return SHD_OK;
 }
 
-extern "C" int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out) {
+static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p, shd_xgroup** out) {
     if (!e || !comm || !out) return SHD_EINVAL;
     const int world = comm->world, rank = comm->rank;
     const int64_t H = e->P.H;
@@ -4318,6 +4511,7 @@ extern "C" int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_even
     g->comm = comm;
     g->world = world;
     g->rank0 = rank;
+    g->p2p = p2p;
     g->engs.push_back(e);
     // the group agrees on W (min) and checks the model: H and end time equal everywhere
     const unsigned long long mine[3] = {(unsigned long long)e->window, (unsigned long long)H,
@@ -4336,6 +4530,15 @@ extern "C" int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_even
     if ((rc = x_alloc(g))) { x_free(g); return rc; }
     *out = g;
     return SHD_OK;
+}
+
+extern "C" int shd_xgroup_create(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out) {
+    return x_create(e, comm, block_events, false, out);
+}
+
+extern "C" int shd_xgroup_create_p2p(shd_eng* e, shd_comm* comm, uint32_t block_events, shd_xgroup** out) {
+    if (comm && comm->world > 64) return SHD_EINVAL;   // d_peers holds 64 pointers
+    return x_create(e, comm, block_events, true, out);
 }
 
 extern "C" int shd_xgroup_create_rccl(shd_eng* e, const uint8_t id[SHD_XID_BYTES], int world, int rank,
@@ -4385,6 +4588,13 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
                                    (const TlPart*)g->loc[k].parts, (uint32_t)grid, i, (const DevCtl*)e->d_ctl);
             }
         }
+        if (g->p2p) {   // put, wait and ingest; the tag is ctl->xtag + i
+            const int wi = (int)(g->xseq & 1);
+            shd_eng* e = g->engs[0];
+            x_p2p_launch(g, wi, (uint32_t)i, 1, xparams(g, 0, &e->d_ring[i + 1]), i, 1);
+            g->xseq++;
+            continue;
+        }
         if ((rc = x_exchange(g))) return rc;
         const int wi = (int)((g->xseq - 1) & 1);
         for (int k = 0; k < nl; k++) {
@@ -4402,7 +4612,7 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
 // one engine per process); a capture that fails is not tried again
 static int x_launch_rounds(shd_xgroup* g, int nb) {
     static const bool no_graph = getenv("SHD_NO_GRAPH") != nullptr;
-    if (nb != shd_eng::kBatch || !g->comm || g->comm->kind != SHD_COMM_RCCL || g->engs.size() != 1 ||
+    if (nb != shd_eng::kBatch || !g->comm || (g->comm->kind != SHD_COMM_RCCL && !g->p2p) || g->engs.size() != 1 ||
         g->graph_failed || no_graph)
         return x_enqueue_rounds(g, nb);
     shd_eng* e = g->engs[0];
@@ -4486,6 +4696,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             e->h_seed[1] = host_fresh_summary();
             e->h_ctl->stop = stop;
             e->h_ctl->round_base = e->round;
+            e->h_ctl->xtag = g->xepoch + 1;   // peer-to-peer: round i's exchange is tagged xtag + i
             SHD_HIP(hipMemcpyAsync(&e->d_ring[1], &e->h_seed[1], sizeof(DevSummary), hipMemcpyHostToDevice,
                                    e->stream));
             SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
@@ -4493,6 +4704,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         }
         SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
         if ((rc = x_launch_rounds(g, nb))) break;
+        g->xepoch += (uint64_t)nb;
         SHD_HIP(hipGetLastError());
         SHD_HIP(hipEventRecord(g->engs[0]->bev[1], g->engs[0]->stream));
         for (int k = 0; k < nl; k++) {
@@ -4501,6 +4713,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
                                    e->stream));
         }
         for (int k = 0; k < nl; k++) SHD_HIP(hipStreamSynchronize(g->engs[k]->stream));
+        if ((rc = x_p2p_check(g))) break;
         {
             float ms = 0;   // the batch on engine 0's stream: rounds + exchanges
             if (hipEventElapsedTime(&ms, g->engs[0]->bev[0], g->engs[0]->bev[1]) == hipSuccess)

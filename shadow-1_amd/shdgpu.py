@@ -235,6 +235,7 @@ _SIGS = {
     "shd_xgroup_create_local": (C.c_int, [P(C.c_void_p), C.c_int, C.c_uint32, P(C.c_void_p)]),
     "shd_xgroup_run_until": (C.c_int, [C.c_void_p, C.c_uint64, P(RunStats)]),
     "shd_xgroup_create": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, P(C.c_void_p)]),
+    "shd_xgroup_create_p2p": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, P(C.c_void_p)]),
     "shd_comm_create_rccl": (C.c_int, [P(C.c_uint8), C.c_int, C.c_int, C.c_int, P(C.c_void_p)]),
     "shd_comm_create_host": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, P(C.c_void_p)]),
     "shd_comm_rank": (C.c_int, [C.c_void_p, P(C.c_int), P(C.c_int)]),

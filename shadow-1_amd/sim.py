@@ -294,12 +294,16 @@ class XGroup:
         return cls(ptr, [engine])
 
     @classmethod
-    def over(cls, engine, comm: Comm, block_events=0):
-        """One engine of this process in a group over a communicator."""
+    def over(cls, engine, comm: Comm, block_events=0, p2p=False):
+        """One engine of this process in a group over a communicator; p2p: the
+        peer-to-peer transport (receive blocks mapped by IPC handle, stored
+        into directly), else the communicator's all-to-all."""
         ptr = C.c_void_p()
-        S.check(S.lib().shd_xgroup_create(engine.ptr, comm.ptr, int(block_events), C.byref(ptr)),
-                "shd_xgroup_create")
-        return cls(ptr, [engine])
+        fn = "shd_xgroup_create_p2p" if p2p else "shd_xgroup_create"
+        S.check(getattr(S.lib(), fn)(engine.ptr, comm.ptr, int(block_events), C.byref(ptr)), fn)
+        g = cls(ptr, [engine])
+        g.p2p = p2p
+        return g
 
     def run_until(self, t_stop) -> S.RunStats:
         st = S.RunStats()

@@ -71,21 +71,28 @@ def check_against_oracle(res, V, hpv, end_s, loss, load):
     return res
 
 
+@pytest.mark.parametrize("p2p", [False, True], ids=["alltoall", "p2p"])
 @pytest.mark.parametrize("world,block", [(2, 0), (3, 0), (2, 4)])
-def test_multiprocess_group_matches_oracle(world, block, tmp_path):
-    """block 4: tiny per-peer blocks force spills (halts + the all-to-all-v)."""
-    res = run_ranks(world, tmp_path, extra=["--block", str(block)])
+def test_multiprocess_group_matches_oracle(world, block, p2p, tmp_path):
+    """block 4: tiny per-peer blocks force spills (halts + the all-to-all-v,
+    and regrown blocks: the peer-to-peer receive blocks are remapped).  p2p:
+    each rank's receive blocks mapped by every rank and stored into directly,
+    with tagged headers and in-kernel waits (on this box the ranks share one
+    GPU: the protocol, not xGMI)."""
+    res = run_ranks(world, tmp_path, extra=["--block", str(block)] + (["--p2p"] if p2p else []))
     check_against_oracle(res, 240, 1, 3.0, 0.01, 16)
     assert sum(int(r["stats"][2]) for r in res) > 0          # first-touch logs resolved across ranks
     rounds = {int(r["stats"][3]) for r in res}
     assert len(rounds) == 1                                    # every rank ran the same rounds
 
 
-def test_multiprocess_group_rolls_back_ambiguous_rounds(tmp_path):
+@pytest.mark.parametrize("p2p", [False, True], ids=["alltoall", "p2p"])
+def test_multiprocess_group_rolls_back_ambiguous_rounds(p2p, tmp_path):
     """Every undecided first-touch send forced ambiguous and every round
     protected: each logging round is rolled back on every process from its
-    state copy, ranked from the logs all-gathered from every rank, rerun."""
-    res = run_ranks(2, tmp_path, extra=["--vertices", "160", "--hpv", "2"],
+    state copy, ranked from the logs all-gathered from every rank, rerun
+    (p2p: the rerun's exchanges take new tags)."""
+    res = run_ranks(2, tmp_path, extra=["--vertices", "160", "--hpv", "2"] + (["--p2p"] if p2p else []),
                     env_extra={"SHD_FORCE_AMBIG": "1", "SHD_PROTECT_ALL": "1"})
     check_against_oracle(res, 160, 2, 3.0, 0.01, 16)
     assert all(int(r["stats"][5]) > 0 for r in res)            # reruns happened on every rank

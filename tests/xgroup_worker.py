@@ -5,7 +5,8 @@
 Each rank builds the same model, creates a host-memory communicator
 (shd_comm_create_host), builds the path cache with its source rows sharded
 over the ranks and all-gathered (shd_pc_build_sharded), runs its engine in a
-group over that communicator (shd_xgroup_create) with stops and resumes, and
+group over that communicator (shd_xgroup_create, or shd_xgroup_create_p2p:
+receive blocks mapped by IPC handle) with stops and resumes, and
 writes its trace, host digests and the full row table to <out>/rank<r>.npz.
 """
 import argparse
@@ -38,6 +39,7 @@ def main():
     ap.add_argument("--loss", type=float, default=0.01)
     ap.add_argument("--load", type=int, default=16)
     ap.add_argument("--block", type=int, default=0)
+    ap.add_argument("--p2p", action="store_true", help="the peer-to-peer transport (shd_xgroup_create_p2p)")
     a = ap.parse_args()
     import shdgpu as S
     import workloads as W
@@ -52,7 +54,7 @@ def main():
     info = pc.info()
     pb = partition(m.n_hosts, a.world)
     eng = Engine(m, pc, pb[a.rank], pb[a.rank + 1])
-    grp = XGroup.over(eng, comm, block_events=a.block)
+    grp = XGroup.over(eng, comm, block_events=a.block, p2p=a.p2p)
     pkt = ev = pend = rounds = prot = rerun = 0
     for t in (int(0.7 * S.SHD_SEC), S.SHD_SEC + 3, 2 * S.SHD_SEC, end):
         st = grp.run_until(min(t, end))
