@@ -59,9 +59,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=0,
                     help="timed steps the CPU baseline runs (0 = all of them: the same window as value)")
-    ap.add_argument("--exchange", choices=["rccl", "torch"], default="rccl",
-                    help="N > 1: rccl = shd_xgroup (device-driven rounds, one fixed-size RCCL all-to-all "
-                         "per round); torch = driver.DistCluster (host-driven, torch.distributed)")
+    ap.add_argument("--exchange", choices=["p2p", "rccl", "torch"], default="p2p",
+                    help="N > 1: p2p = shd_xgroup with the peer-to-peer transport (each rank's receive blocks "
+                         "IPC-mapped by every rank and stored into over xGMI, tagged headers, in-kernel waits; "
+                         "falls back to rccl if the mapping fails); rccl = shd_xgroup with one fixed-size RCCL "
+                         "all-to-all per round; torch = driver.DistCluster (host-driven, torch.distributed)")
     ap.add_argument("--group", action="store_true",
                     help="run the shd_xgroup path even at N = 1 (a one-rank RCCL group)")
     ap.add_argument("--quiet", action="store_true")
@@ -122,7 +124,7 @@ def main():
         model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load,
                               payload=args.payload)
     att = W.attached_vertices(host_vertex)
-    use_group = args.group or (world > 1 and args.exchange == "rccl")
+    use_group = args.group or (world > 1 and args.exchange in ("p2p", "rccl"))
     comm = None
     if use_group:
         # one communicator per process: the sharded path-cache build and the
@@ -163,8 +165,18 @@ def main():
     log(rank, f"setup {time.perf_counter() - t_setup:.1f}s  V={V} E={g.n_edges} H={H} W={eng.window}ns "
               f"apsp={min(builds):.1f}ms iters={info.sssp_iterations_max} hops={info.max_hops}")
 
+    exchange = "none (single engine)"
     if use_group:
-        grp = XGroup.over(eng, comm)
+        exchange = "shd_xgroup/RCCL all-to-all"
+        grp = None
+        if args.exchange == "p2p":
+            try:   # every rank fails alike (the mapping is checked collectively)
+                grp = XGroup.over(eng, comm, p2p=True)
+                exchange = "shd_xgroup/peer-to-peer (IPC-mapped receive blocks, xGMI stores)"
+            except S.ShdError as ex:
+                log(rank, f"peer-to-peer transport unavailable ({ex}); RCCL all-to-all instead")
+        if grp is None:
+            grp = XGroup.over(eng, comm)
         run = lambda t: grp.run_until(t)  # noqa: E731
     elif world > 1:
         cl = DistCluster(eng, pb, rank, world, dist, torch)
@@ -220,7 +232,7 @@ def main():
     achieved = (alg_bytes / max(launches, 1)) / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     # the dominant kernel: ticketless device rounds on one engine (k_round_tl,
     # once no first touch is logged), the engine group's k_round_x across GPUs
-    kname = "k_round_x" if use_group else ("k_round" if world > 1 else "k_round_tl")
+    kname = "k_round_xtl" if use_group else ("k_round" if world > 1 else "k_round_tl")
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname),
                 "kernel": kname, "avg_launch_us": round(avg_launch_ms * 1e3, 3),
@@ -260,7 +272,7 @@ def main():
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
                        "payload_bytes": args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
                        "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1),
-                       "exchange": ("shd_xgroup/RCCL all-to-all" if use_group else
+                       "exchange": (exchange if use_group else
                                     "torch.distributed" if world > 1 else "none (single engine)")},
             "all_events_per_s": round(ev_all / elapsed, 1),
             # the same events over the timed region plus the one-time host->device

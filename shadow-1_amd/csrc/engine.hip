@@ -2896,12 +2896,102 @@ __global__ __launch_bounds__(256) void k_xput(const shd_event* __restrict__ xsen
     }
 }
 
+// k_xfold and k_xput in one launch (peer-to-peer rounds): block p folds the
+// round's shares (every block alike), packs this engine's header for peer p
+// (block 0 also completes the summary), then puts the block into p's receive
+// blocks.  A halted round re-sends the last header under the new tag, as the
+// all-to-all re-sends the unchanged send blocks.
+__device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
+                                          const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers, int me,
+                                          int wi, uint32_t tag_add, int use_ctl, int p) {
+    __shared__ TlPart s_f[4];
+    DevSummary* sum = P.sum;
+    const uint32_t halt = *P.halt;
+    const uint64_t ws = sum->ws, stop = ctl->stop, npend = sum->n_pending, nrem = sum->n_remote;
+    const uint64_t next0 = sum->next_time;
+    const uint32_t err0 = sum->error;
+    const size_t stride = (size_t)P.xcap + 1;
+    shd_event* src = P.xsend + (size_t)p * stride;
+    if (!halt) {
+        const bool fwd = ws >= stop;
+        TlPart f{kInf, 0, 0, 0, 0, 0};
+        const TlPart* pp = parts + (size_t)(i & 1) * nblk;
+        for (uint32_t j = threadIdx.x; j < nblk; j += blockDim.x)
+            if (!fwd) tl_fold(f, pp[j]);
+        for (int off = 32; off > 0; off >>= 1) {
+            TlPart o;
+            o.next = __shfl_xor(f.next, off, 64);
+            o.t_end = __shfl_xor(f.t_end, off, 64);
+            o.nev = __shfl_xor(f.nev, off, 64);
+            o.npkt = __shfl_xor(f.npkt, off, 64);
+            o.err = __shfl_xor(f.err, off, 64);
+            tl_fold(f, o);
+        }
+        if ((threadIdx.x & 63) == 0) s_f[threadIdx.x >> 6] = f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (uint32_t w = 1; w < blockDim.x / 64; w++) tl_fold(f, s_f[w]);
+            uint64_t next = fwd ? ws : f.next;
+            next = next0 < next ? next0 : next;
+            const uint32_t err = err0 | f.err;
+            if (p == 0) {
+                sum->next_time = next;
+                if (!fwd) {
+                    sum->n_events = f.nev;
+                    sum->n_pkt_events = f.npkt;
+                    atomicOr(&sum->error, err);   // the ingest of the same launch may add bits
+                    sum->t_last = f.t_end;
+                }
+            }
+            const uint32_t cnt = P.xcount[p];
+            XHeader h;
+            h.next_time = next;
+            h.count = cnt < P.xcap ? cnt : P.xcap;
+            uint32_t fl = 0;
+            if (!fwd) {
+                if (npend) fl |= XF_PENDING;
+                if (nrem) fl |= XF_OVERFLOW;
+                if (err) fl |= XF_ERROR;
+            }
+            h.flags = fl;
+            h.n_pending = fwd ? 0 : npend;
+            h.error = fwd ? err0 : err;
+            h.pad = 0;
+            *(XHeader*)src = h;
+            P.xcount[p] = 0;
+        }
+    }
+    __syncthreads();
+    // the put (as k_xput)
+    shd_event* dst = peers[p] + ((size_t)wi * P.xworld + me) * stride;
+    XHeader h = *(const XHeader*)src;
+    const uint32_t n = h.count < P.xcap ? h.count : P.xcap;
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) dst[1 + k] = src[1 + k];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        h.pad = x_tag(ctl, tag_add, use_ctl);
+        uint32_t* hw = (uint32_t*)dst;
+        const uint32_t* hv = (const uint32_t*)&h;
+        for (int k = 0; k < 7; k++) hw[k] = hv[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(hw + 7, hv[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_xfold_put(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
+                                                    const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
+                                                    int me, int wi, uint32_t tag_add, int use_ctl) {
+    xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, use_ctl, (int)blockIdx.x);
+}
+
 // wait for every peer's block of this exchange (bounded: a peer that never
 // comes sets *xerr, and later waits of the batch return at once), then, for a
 // round's exchange, the received events -> the next round's calendar / inbox
-__global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event* __restrict__ xrecv,
-                                                       const DevCtl* __restrict__ ctl, uint32_t tag_add,
-                                                       int use_ctl, int ri, int ingest, uint32_t* __restrict__ xerr) {
+__device__ __forceinline__ void xwait_ingest(const DParams& P, const shd_event* __restrict__ xrecv,
+                                             const DevCtl* __restrict__ ctl, uint32_t tag_add, int use_ctl, int ri,
+                                             int ingest, uint32_t* __restrict__ xerr, uint32_t blk) {
     __shared__ uint32_t s_bad;
     const uint32_t tag = x_tag(ctl, tag_add, use_ctl);
     const size_t stride = (size_t)P.xcap + 1;
@@ -2911,7 +3001,9 @@ __global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event
     if ((int32_t)threadIdx.x < P.xworld) {
         const uint32_t* tw = (const uint32_t*)(xrecv + threadIdx.x * stride) + 7;
         const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(tw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
+        // relaxed polls (an acquire per poll would invalidate this CU's caches
+        // each time), one acquire once the tag is there
+        while (__hip_atomic_load(tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != tag) {
             __builtin_amdgcn_s_sleep(1);
             if (wall_clock64() - t0 > kXWaitTicks) {
                 atomicOr(&s_bad, 1u);
@@ -2920,6 +3012,7 @@ __global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event
             }
         }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     __syncthreads();
     if (s_bad) {
         if (threadIdx.x == 0) *P.halt = 1u;
@@ -2927,18 +3020,37 @@ __global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event
     }
     if (!ingest || *P.halt) return;
     const int parity = (int)((ctl->round_base + (uint64_t)ri + 1) & 1);   // the next round's inbox
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = (uint64_t)blk * blockDim.x + threadIdx.x;
     const uint64_t p = t / P.xcap, s = t % P.xcap;
     if (p >= (uint64_t)P.xworld) return;
-    const shd_event* blk = xrecv + p * stride;
-    if (s >= ((const XHeader*)blk)->count) return;
-    const shd_event e = blk[1 + s];
+    const shd_event* b = xrecv + p * stride;
+    if (s >= ((const XHeader*)b)->count) return;
+    const shd_event e = b[1 + s];
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
     if (cal_push(P, dl, e, P.sum->ws)) return;
     const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
     if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+}
+
+__global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event* __restrict__ xrecv,
+                                                       const DevCtl* __restrict__ ctl, uint32_t tag_add,
+                                                       int use_ctl, int ri, int ingest, uint32_t* __restrict__ xerr) {
+    xwait_ingest(P, xrecv, ctl, tag_add, use_ctl, ri, ingest, xerr, blockIdx.x);
+}
+
+// a round's whole exchange in one launch: blocks [0, world) fold and put
+// (k_xfold_put), the rest wait for every peer's block and ingest.  The put
+// blocks never wait, so the launch completes whatever the placement
+__global__ __launch_bounds__(256) void k_xchg(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
+                                               const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
+                                               int me, int wi, uint32_t tag_add, const shd_event* __restrict__ xrecv,
+                                               uint32_t* __restrict__ xerr) {
+    if ((int)blockIdx.x < P.xworld)
+        xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, 1, (int)blockIdx.x);
+    else
+        xwait_ingest(P, xrecv, ctl, tag_add, 1, i, 1, xerr, blockIdx.x - (uint32_t)P.xworld);
 }
 
 __global__ void k_digest(DParams P, shd_host_digest* __restrict__ out) {
@@ -4584,14 +4696,37 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
                                    (const DParams*)(g->loc[k].d_xpr + i + 1),
                                    (const shd_event*)g->loc[k].xrecv[ri], g->loc[k].halt_hdr, &e->d_ring[i + 2],
                                    (const DevCtl*)e->d_ctl, i, g->window, g->loc[k].parts);
+                if (g->p2p) continue;   // k_xfold_put below
                 hipLaunchKernelGGL(k_xfold, dim3(1), dim3(64), 0, e->stream, dp(xparams(g, k, &e->d_ring[i + 1])),
                                    (const TlPart*)g->loc[k].parts, (uint32_t)grid, i, (const DevCtl*)e->d_ctl);
             }
         }
-        if (g->p2p) {   // put, wait and ingest; the tag is ctl->xtag + i
+        if (g->p2p) {   // fold + put, then wait and ingest; the tag is ctl->xtag + i
             const int wi = (int)(g->xseq & 1);
             shd_eng* e = g->engs[0];
-            x_p2p_launch(g, wi, (uint32_t)i, 1, xparams(g, 0, &e->d_ring[i + 1]), i, 1);
+            const Params P = xparams(g, 0, &e->d_ring[i + 1]);
+            const uint32_t nblk = (uint32_t)((e->nloc + e->P.hpw - 1) / e->P.hpw);
+            static const bool split = getenv("SHD_X_SPLIT_PUT") != nullptr;   // A/B: k_xfold, then k_xput
+            static const bool two = getenv("SHD_X_TWO_LAUNCH") != nullptr;    // A/B: k_xfold_put, k_xwait_ingest
+            if (!split && !two) {
+                const uint64_t nthr = (uint64_t)g->world * g->xcap;
+                hipLaunchKernelGGL(k_xchg, dim3((unsigned)(g->world + (nthr + 255) / 256)), dim3(256), 0, e->stream,
+                                   dp(P), (const TlPart*)g->loc[0].parts, nblk, i, (const DevCtl*)e->d_ctl,
+                                   (shd_event* const*)g->d_peers, g->rank0, wi, (uint32_t)i,
+                                   (const shd_event*)g->loc[0].xrecv[wi], g->d_xerr);
+            } else if (split) {
+                hipLaunchKernelGGL(k_xfold, dim3(1), dim3(64), 0, e->stream, dp(P), (const TlPart*)g->loc[0].parts,
+                                   nblk, i, (const DevCtl*)e->d_ctl);
+                x_p2p_launch(g, wi, (uint32_t)i, 1, P, i, 1);
+            } else {
+                hipLaunchKernelGGL(k_xfold_put, dim3(g->world), dim3(256), 0, e->stream, dp(P),
+                                   (const TlPart*)g->loc[0].parts, nblk, i, (const DevCtl*)e->d_ctl,
+                                   (shd_event* const*)g->d_peers, g->rank0, wi, (uint32_t)i, 1);
+                const uint64_t nthr = (uint64_t)g->world * g->xcap;
+                hipLaunchKernelGGL(k_xwait_ingest, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream,
+                                   dp(P), (const shd_event*)g->loc[0].xrecv[wi], (const DevCtl*)e->d_ctl, (uint32_t)i,
+                                   1, i, 1, g->d_xerr);
+            }
             g->xseq++;
             continue;
         }
