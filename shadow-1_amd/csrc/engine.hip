@@ -2874,26 +2874,41 @@ __device__ __forceinline__ uint32_t x_tag(const DevCtl* ctl, uint32_t add, int u
 }
 
 // block p: this engine's block for peer p -> p's receive block `me` of parity wi
+// The block's events and header go out as write-through system-scope stores
+// (the receive blocks are uncached: no L2 on either side keeps them); every
+// storing wave drains them (vmcnt(0)) before the barrier, then one lane
+// stores the header body, drains it, and stores the tag.  fence: a release
+// fence (an L2 write-back) before the tag as well (A/B, SHD_X_FENCE)
+__device__ __forceinline__ void x_put(const shd_event* __restrict__ src, shd_event* __restrict__ dst, uint32_t n,
+                                      XHeader h, uint32_t tag, int fence) {
+    const unsigned long long* s8 = (const unsigned long long*)(src + 1);
+    unsigned long long* d8 = (unsigned long long*)(dst + 1);
+    for (uint32_t k = threadIdx.x; k < 4 * n; k += blockDim.x)
+        __hip_atomic_store(d8 + k, s8[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        h.pad = tag;
+        unsigned long long* hw = (unsigned long long*)dst;
+        const unsigned long long* hv = (const unsigned long long*)&h;
+        for (int k = 0; k < 3; k++) __hip_atomic_store(hw + k, hv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store((uint32_t*)dst + 6, h.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((uint32_t*)dst + 7, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_xput(const shd_event* __restrict__ xsend, shd_event* const* __restrict__ peers,
                                                uint32_t stride, uint32_t xcap, int world, int me, int wi,
-                                               const DevCtl* __restrict__ ctl, uint32_t tag_add, int use_ctl) {
+                                               const DevCtl* __restrict__ ctl, uint32_t tag_add, int use_ctl,
+                                               int fence) {
     const int p = blockIdx.x;
     const shd_event* src = xsend + (size_t)p * stride;
     shd_event* dst = peers[p] + ((size_t)wi * world + me) * stride;
     XHeader h = *(const XHeader*)src;
     const uint32_t n = h.count < xcap ? h.count : xcap;
-    for (uint32_t s = threadIdx.x; s < n; s += blockDim.x) dst[1 + s] = src[1 + s];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        h.pad = x_tag(ctl, tag_add, use_ctl);
-        uint32_t* hw = (uint32_t*)dst;
-        const uint32_t* hv = (const uint32_t*)&h;
-        for (int k = 0; k < 7; k++) hw[k] = hv[k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: the events and the header body first
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(hw + 7, hv[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    x_put(src, dst, n, h, x_tag(ctl, tag_add, use_ctl), fence);
 }
 
 // k_xfold and k_xput in one launch (peer-to-peer rounds): block p folds the
@@ -2903,7 +2918,7 @@ __global__ __launch_bounds__(256) void k_xput(const shd_event* __restrict__ xsen
 // all-to-all re-sends the unchanged send blocks.
 __device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
                                           const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers, int me,
-                                          int wi, uint32_t tag_add, int use_ctl, int p) {
+                                          int wi, uint32_t tag_add, int use_ctl, int p, int fence) {
     __shared__ TlPart s_f[4];
     DevSummary* sum = P.sum;
     const uint32_t halt = *P.halt;
@@ -2966,24 +2981,13 @@ __device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __rest
     shd_event* dst = peers[p] + ((size_t)wi * P.xworld + me) * stride;
     XHeader h = *(const XHeader*)src;
     const uint32_t n = h.count < P.xcap ? h.count : P.xcap;
-    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) dst[1 + k] = src[1 + k];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        h.pad = x_tag(ctl, tag_add, use_ctl);
-        uint32_t* hw = (uint32_t*)dst;
-        const uint32_t* hv = (const uint32_t*)&h;
-        for (int k = 0; k < 7; k++) hw[k] = hv[k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(hw + 7, hv[7], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    x_put(src, dst, n, h, x_tag(ctl, tag_add, use_ctl), fence);
 }
 
 __global__ __launch_bounds__(256) void k_xfold_put(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
                                                     const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
-                                                    int me, int wi, uint32_t tag_add, int use_ctl) {
-    xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, use_ctl, (int)blockIdx.x);
+                                                    int me, int wi, uint32_t tag_add, int use_ctl, int fence) {
+    xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, use_ctl, (int)blockIdx.x, fence);
 }
 
 // wait for every peer's block of this exchange (bounded: a peer that never
@@ -3046,9 +3050,9 @@ __global__ __launch_bounds__(256) void k_xwait_ingest(DParams P, const shd_event
 __global__ __launch_bounds__(256) void k_xchg(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
                                                const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
                                                int me, int wi, uint32_t tag_add, const shd_event* __restrict__ xrecv,
-                                               uint32_t* __restrict__ xerr) {
+                                               uint32_t* __restrict__ xerr, int fence) {
     if ((int)blockIdx.x < P.xworld)
-        xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, 1, (int)blockIdx.x);
+        xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, 1, (int)blockIdx.x, fence);
     else
         xwait_ingest(P, xrecv, ctl, tag_add, 1, i, 1, xerr, blockIdx.x - (uint32_t)P.xworld);
 }
@@ -4248,11 +4252,16 @@ static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
 // a peer-to-peer exchange: every engine's blocks put into the peers' receive
 // blocks of parity wi under tag (ctl->xtag + tag_add, or tag_add), then the
 // wait for every peer's (and, for a round, the ingest of what came)
+static int x_fence() {
+    static const int f = getenv("SHD_X_FENCE") != nullptr;
+    return f;
+}
+
 static void x_p2p_launch(shd_xgroup* g, int wi, uint32_t tag_add, int use_ctl, const Params& P, int ri, int ingest) {
     shd_eng* e = g->engs[0];
     hipLaunchKernelGGL(k_xput, dim3(g->world), dim3(256), 0, e->stream, (const shd_event*)g->loc[0].xsend,
                        (shd_event* const*)g->d_peers, (uint32_t)g->stride, g->xcap, g->world, g->rank0, wi,
-                       (const DevCtl*)e->d_ctl, tag_add, use_ctl);
+                       (const DevCtl*)e->d_ctl, tag_add, use_ctl, x_fence());
     const uint64_t nthr = ingest ? (uint64_t)g->world * g->xcap : 1;
     hipLaunchKernelGGL(k_xwait_ingest, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream, dp(P),
                        (const shd_event*)g->loc[0].xrecv[wi], (const DevCtl*)e->d_ctl, tag_add, use_ctl, ri, ingest,
@@ -4713,7 +4722,7 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
                 hipLaunchKernelGGL(k_xchg, dim3((unsigned)(g->world + (nthr + 255) / 256)), dim3(256), 0, e->stream,
                                    dp(P), (const TlPart*)g->loc[0].parts, nblk, i, (const DevCtl*)e->d_ctl,
                                    (shd_event* const*)g->d_peers, g->rank0, wi, (uint32_t)i,
-                                   (const shd_event*)g->loc[0].xrecv[wi], g->d_xerr);
+                                   (const shd_event*)g->loc[0].xrecv[wi], g->d_xerr, x_fence());
             } else if (split) {
                 hipLaunchKernelGGL(k_xfold, dim3(1), dim3(64), 0, e->stream, dp(P), (const TlPart*)g->loc[0].parts,
                                    nblk, i, (const DevCtl*)e->d_ctl);
@@ -4721,7 +4730,7 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
             } else {
                 hipLaunchKernelGGL(k_xfold_put, dim3(g->world), dim3(256), 0, e->stream, dp(P),
                                    (const TlPart*)g->loc[0].parts, nblk, i, (const DevCtl*)e->d_ctl,
-                                   (shd_event* const*)g->d_peers, g->rank0, wi, (uint32_t)i, 1);
+                                   (shd_event* const*)g->d_peers, g->rank0, wi, (uint32_t)i, 1, x_fence());
                 const uint64_t nthr = (uint64_t)g->world * g->xcap;
                 hipLaunchKernelGGL(k_xwait_ingest, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, e->stream,
                                    dp(P), (const shd_event*)g->loc[0].xrecv[wi], (const DevCtl*)e->d_ctl, (uint32_t)i,
