@@ -1860,6 +1860,8 @@ struct RoundArgsT {
     Ptr<const int4> st;         // self_thr + h0
     Ptr<const uint32_t> halt;
     int32_t nloc, hpw;
+    uint32_t nblk;   // grid size (blocks of hpw hosts)
+    uint32_t pad;
 };
 using DRoundArgs = RoundArgsT<GlobalPtr>;
 static DRoundArgs round_args(const Params& P) {
@@ -1869,6 +1871,7 @@ static DRoundArgs round_args(const Params& P) {
     a.bits = d.bins ? d.bin_bits : nullptr;
     a.att = d.host_att + P.h0; a.st = d.self_thr + P.h0;
     a.halt = d.halt; a.nloc = P.nloc; a.hpw = P.hpw;
+    a.nblk = (uint32_t)((P.nloc + P.hpw - 1) / P.hpw); a.pad = 0;
     return a;
 }
 __device__ __forceinline__ DRoundArgs round_args_dev(const DParams& P) {
@@ -1877,6 +1880,7 @@ __device__ __forceinline__ DRoundArgs round_args_dev(const DParams& P) {
     a.bits = P.bins ? P.bin_bits : nullptr;
     a.att = P.host_att + P.h0; a.st = P.self_thr + P.h0;
     a.halt = P.halt; a.nloc = P.nloc; a.hpw = P.hpw;
+    a.nblk = (uint32_t)((P.nloc + P.hpw - 1) / P.hpw); a.pad = 0;
     return a;
 }
 struct HostIn {
@@ -2488,6 +2492,38 @@ __device__ __forceinline__ uint64_t tl_gather_next(const TlPart* __restrict__ pa
     }
     return m;
 }
+// The shares in two phases, so that their loads go out first and the
+// host-state loads behind them (the window start waits only for these):
+// tl_issue loads shares [base, base + 256) as four independent loads per lane
+// (indices past the end read the last share and are not folded), tl_fold4
+// folds them in
+__device__ __forceinline__ void tl_issue(const TlPart* __restrict__ parts, uint32_t n, uint32_t base, TlPart (&v)[4]) {
+    const uint32_t last = n - 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t j = base + 64u * k + threadIdx.x;
+        v[k] = parts[j < n ? j : last];
+    }
+}
+__device__ __forceinline__ void tl_fold4(TlPart& f, const TlPart (&v)[4], uint32_t n, uint32_t base) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (base + 64u * k + threadIdx.x < n) tl_fold(f, v[k]);
+}
+__device__ __forceinline__ void tl_reduce(TlPart& f, bool full) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(f.next, off, 64);
+        f.next = o < f.next ? o : f.next;
+        if (full) {
+            const uint64_t te = __shfl_xor(f.t_end, off, 64);
+            f.t_end = te > f.t_end ? te : f.t_end;
+            f.nev += __shfl_xor(f.nev, off, 64);
+            f.npkt += __shfl_xor(f.npkt, off, 64);
+            f.err |= __shfl_xor(f.err, off, 64);
+        }
+    }
+}
+
 // publish a round's fold into its summary; a round that logged first touches
 // halts the batch (the host resolves its log)
 __device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint32_t* halt) {
@@ -2511,23 +2547,36 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
     if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
 #endif
     const unsigned long long t_entry = wall_clock64();   // the round's start on the device clock (t_first)
-    const uint32_t nblk = (uint32_t)((a.nloc + a.hpw - 1) / a.hpw);   // == gridDim.x, without the dispatch-packet load
+    const uint32_t nblk = a.nblk;   // == gridDim.x, without the dispatch-packet load
     // all scalar arguments in the first load batch (the compiler otherwise
-    // fetches these after the host-state loads are issued, one level later)
-    asm volatile("" ::"s"(i), "s"(prev), "s"(ctl), "s"(parts));
+    // fetches some after the first vector loads are issued, one level later)
+    asm volatile("" ::"s"(i), "s"(prev), "s"(ctl), "s"(parts), "s"(nblk), "s"(a.nloc), "s"(a.hpw), "s"(window));
+    // the window start's inputs go out first: halt, the control words, the
+    // previous round's summary and its shares (round 0 of the batch starts at
+    // the seeded time; later rounds fold the previous round's shares, whose
+    // first-touch log count halts).  The host-state loads follow; the window
+    // start then waits for its own loads only (vmcnt counts in issue order)
+    uint32_t halt = *a.halt;
+    uint64_t stop = ctl->stop, rbase = ctl->round_base, ws0 = prev->next_time, npend = prev->n_pending;
+    const TlPart* pp = parts + (size_t)((i - 1) & 1) * nblk;
+    TlPart pv[4];
+    if (i > 0) tl_issue(pp, nblk, 0, pv);
     const uint32_t warm = params_warm(Pp);
     HostIn in;
     host_in_load(a, in);
-    // round 0 of the batch starts at the seeded time; later rounds fold the
-    // previous round's shares (its first-touch log count halts)
-    const uint32_t halt = *a.halt;
-    const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws0 = prev->next_time, npend = prev->n_pending;
+    // consumed only here, once every load is out (the compiler would
+    // otherwise move their scalar copies, and the waits, above the rest)
+    asm volatile("" : "+v"(halt), "+v"(stop), "+v"(rbase), "+v"(ws0), "+v"(npend));
     // every block needs the shares' min next time; block 0 folds the rest
     // of them too, for the summary
     TlPart f{kInf, 0, 0, 0, 0, 0};
     if (i > 0) {
-        if (blockIdx.x == 0) f = tl_gather(parts + (size_t)((i - 1) & 1) * nblk, nblk);
-        else f.next = tl_gather_next(parts + (size_t)((i - 1) & 1) * nblk, nblk);
+        tl_fold4(f, pv, nblk, 0);
+        for (uint32_t base = 256; base < nblk; base += 256) {   // grids above 256 blocks
+            tl_issue(pp, nblk, base, pv);
+            tl_fold4(f, pv, nblk, base);
+        }
+        tl_reduce(f, blockIdx.x == 0);
     }
     const uint64_t ws = f.next < ws0 ? f.next : ws0;
     params_warm_done(warm);
