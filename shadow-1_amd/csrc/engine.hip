@@ -2780,22 +2780,28 @@ __global__ __launch_bounds__(kBlock) void k_round_xtl(DRoundArgs a, const DParam
     const DParams& P = *Pp;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
     const unsigned long long t_entry = wall_clock64();
+    const int32_t xworld = P.xworld;
+    const size_t stride = (size_t)P.xcap + 1;
+    // as k_round_tl: the window start's loads first (halt, control words,
+    // every peer's header: lane p loads header p), the host state behind them
+    uint32_t halt = *a.halt;
+    uint64_t stop = ctl->stop, rbase = ctl->round_base;
+    const XHeader hx = *(const XHeader*)(xrecv + (size_t)((int32_t)threadIdx.x < xworld ? threadIdx.x : 0) * stride);
+    uint64_t ws = (int32_t)threadIdx.x < xworld ? hx.next_time : kInf;
+    uint32_t fl = (int32_t)threadIdx.x < xworld ? hx.flags : 0u;
     HostIn in;
     host_in_load(a, in);
-    if (*a.halt) {
+    asm volatile("" : "+v"(halt), "+v"(stop), "+v"(rbase), "+v"(ws), "+v"(fl));
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(ws, off, 64);
+        ws = o < ws ? o : ws;
+        fl |= __shfl_xor(fl, off, 64);
+    }
+    if (halt) {
         if (lead) P.sum->flags = 2u;
         return;
     }
-    const uint64_t stop = ctl->stop;
-    const int parity = (int)((ctl->round_base + (uint64_t)i) & 1);
-    const size_t stride = (size_t)P.xcap + 1;
-    uint64_t ws = kInf;
-    uint32_t fl = 0;
-    for (int32_t p = 0; p < P.xworld; p++) {
-        const XHeader h = *(const XHeader*)(xrecv + (size_t)p * stride);
-        ws = h.next_time < ws ? h.next_time : ws;
-        fl |= h.flags;
-    }
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
     if (fl) {
         if (blockIdx.x == 0) {
             if ((int32_t)threadIdx.x < P.xworld) halt_hdr[threadIdx.x] = *(const XHeader*)(xrecv + threadIdx.x * stride);
@@ -4673,6 +4679,7 @@ extern "C" int shd_xgroup_create_local(shd_eng* const* engines, int n, uint32_t 
 static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p, shd_xgroup** out) {
     if (!e || !comm || !out) return SHD_EINVAL;
     const int world = comm->world, rank = comm->rank;
+    if (world > 64) return SHD_EINVAL;   // the round kernel folds the peers' headers in one wave
     const int64_t H = e->P.H;
     if (e->h0 != (int32_t)((H * rank) / world) || e->h0 + e->nloc != (int32_t)((H * (rank + 1)) / world))
         return SHD_EINVAL;
