@@ -1896,12 +1896,11 @@ struct HostIn {
 __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
     const int32_t l0 = (int32_t)threadIdx.x < a.hpw ? (int32_t)blockIdx.x * a.hpw + (int32_t)threadIdx.x : a.nloc;
     const int32_t l = l0 < a.nloc ? l0 : a.nloc - 1;
+    // the idle test's words first: the idle test and the window's bin loads
+    // wait for them only, not for the 160-B record behind them
     in.nin[0] = a.nin0[l];
     in.nin[1] = a.nin1[l];
     in.t0 = a.hnext[l];
-    in.rec = a.hs[l];
-    in.att = a.att[l];
-    in.st = a.st[l];
     if (a.bits) {
         const uint4* bp = (const uint4*)(a.bits + (size_t)l * kNBW);
         const uint4 x = bp[0], y = bp[1];
@@ -1911,6 +1910,9 @@ __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
 #pragma unroll
         for (int j = 0; j < (int)kNBW; j++) in.w[j] = 0;
     }
+    in.rec = a.hs[l];
+    in.att = a.att[l];
+    in.st = a.st[l];
 }
 
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
@@ -1994,6 +1996,20 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     PendDel pd;
     c.ns = 0; c.att = 0; c.cls = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
+    // the window's non-empty bins, all slots loaded before the host record is
+    // consumed (one round trip, overlapping the record's)
+    EvV bx[3][kBinCap];
+    if (active && P.bins) {
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++) {
+            if (((wbits >> j) & 1u) == 0) continue;
+            const size_t bi = (size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+            static_assert(kBinCap == 4, "the slots are read as four named events");
+            const auto bp = P.bins + bi * kBinCap;
+#pragma unroll
+            for (uint32_t k = 0; k < kBinCap; k++) bx[j][k] = ev_ld(bp + k);
+        }
+    }
     if (active) {
         PROF_T0(t_all)
         load_ctx(P, c, l, rec, rec_att, rec_st);
@@ -2024,14 +2040,8 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++) {
                 if (((wbits >> j) & 1u) == 0) continue;
-                const size_t bi = (size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
-                static_assert(kBinCap == 4, "the slots are read as four named events");
-                const auto bp = P.bins + bi * kBinCap;
-                const EvV x0 = ev_ld(bp), x1 = ev_ld(bp + 1), x2 = ev_ld(bp + 2), x3 = ev_ld(bp + 3);
-                due_add(x0, nw, ws, we);
-                due_add(x1, nw, ws, we);
-                due_add(x2, nw, ws, we);
-                due_add(x3, nw, ws, we);
+#pragma unroll
+                for (uint32_t k = 0; k < kBinCap; k++) due_add(bx[j][k], nw, ws, we);
             }
             c.nd = nw < (uint32_t)kDueCap ? nw : (uint32_t)kDueCap;
             if (nw > (uint32_t)kDueCap) due_overflow(P, c, b0, wbits, ws, we);
