@@ -293,7 +293,11 @@ enum { SHD_QF_NO_CALENDAR = 1,
        /* boot schedules no application start: the caller pushes each host's
         * process start events (<process starttime>, process_schedule,
         * process.c:1344) with shd_eng_push_events */
-       SHD_QF_NO_APP_START = 8 };
+       SHD_QF_NO_APP_START = 8,
+       /* with `trace`: also the application's side of each datagram
+        * (SHD_TR_CREATED, SHD_TR_READ), for the [STATUS] packet lines
+        * (packet_addDeliveryStatus, packet.c:647-659; shdgpu.status_lines) */
+       SHD_QF_TRACE_STATUS = 16 };
 
 /* one event (32 B): key (time, dst, src, seq) = event_compare, event.c:110-153 */
 typedef struct shd_event {
@@ -332,7 +336,15 @@ enum {
     SHD_TR_CODEL_DROP = 4,  /* PDS_ROUTER_DROPPED in CoDel (router_queue_codel.c:135) */
     SHD_TR_RECV = 5,        /* PDS_RCV_INTERFACE_RECEIVED (network_interface.c:380)  */
     SHD_TR_IF_DROP = 6,     /* PDS_RCV_INTERFACE_DROPPED (no bound socket)           */
-    SHD_TR_LOCAL = 7        /* loopback shortcut delivery                            */
+    SHD_TR_LOCAL = 7,       /* loopback shortcut delivery                            */
+    /* SHD_QF_TRACE_STATUS only: */
+    SHD_TR_CREATED = 8,     /* the application's sendto: PDS_SND_CREATED (udp.c:116) and
+                               PDS_SND_SOCKET_BUFFERED (socket.c:405); seq = the source
+                               port drawn by the implicit bind (host.c:1058-1110), peer =
+                               ~0 (the destination is in the packet's SENT / INET_DROP /
+                               LOCAL record)                                             */
+    SHD_TR_READ = 9         /* the application's recvfrom of the socket's oldest datagram:
+                               PDS_RCV_SOCKET_DELIVERED (udp.c:158); peer = pkt = ~0     */
 };
 
 /* per-host end state, compared bit for bit against the oracle */

@@ -355,8 +355,10 @@ static void send_new_message(ctx_t* c, uint32_t h) {
     while (lo < hi) { int32_t mid = lo + (hi - lo) / 2; if (cum[mid] >= r) hi = mid; else lo = mid + 1; }
     if (lo >= c->m->n_hosts) return;      /* NULL node: nothing sent */
     uint32_t dst = (uint32_t)lo;
-    (void)random_free_port(H);
+    const uint16_t port = random_free_port(H);
     uint32_t pkt = H->pkt_seq++;
+    /* packet_new + PDS_SND_CREATED (udp.c:116), PDS_SND_SOCKET_BUFFERED (socket.c:405) */
+    if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, port, h, ~0u, pkt, SHD_TR_CREATED);
     if (H->txq_count == H->txq_cap) {
         uint32_t ncap = H->txq_cap * 2;
         txent* nq = malloc(sizeof(txent) * ncap);
@@ -431,7 +433,12 @@ static void execute(ctx_t* c, const shd_event* e) {
         H->notify_pending = 0;
         uint32_t n = H->unread;
         H->unread = 0;
-        for (uint32_t i = 0; i < n; i++) send_new_message(c, h);
+        /* _phold_wait_and_process_events (test_phold.c:287-315): each recvfrom
+         * (PDS_RCV_SOCKET_DELIVERED, udp.c:158) answered by one new message */
+        for (uint32_t i = 0; i < n; i++) {
+            if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, 0, h, ~0u, ~0u, SHD_TR_READ);
+            send_new_message(c, h);
+        }
         break;
     }
     default:

@@ -175,9 +175,9 @@ struct DestGuide {
 };
 static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 
-constexpr int kDestExc = 16;
+constexpr int kDestExc = 16;   // closed-form destination exceptions (ParamsT::exc_x)
 // ParamsT::feat: the model's optional features (all off on the bench's models)
-constexpr uint32_t F_TRACE = 1u, F_HB = 2u, F_PCOUNT = 4u, F_HOSTHB = 8u, F_AMBIG = 16u;   // closed-form destination exceptions (ParamsT::exc_x)
+constexpr uint32_t F_TRACE = 1u, F_HB = 2u, F_PCOUNT = 4u, F_HOSTHB = 8u, F_AMBIG = 16u, F_STATUS = 64u;
 
 template <template <class> class Ptr>
 struct ParamsT {
@@ -440,7 +440,7 @@ struct HostCtx {
 #endif
 };
 
-constexpr uint32_t W_RX = 1u, W_TX = 2u, W_REFILL = 4u, W_SENDING = 8u;   // HostCtx::w_fl
+constexpr uint32_t W_RX = 1u, W_TX = 2u, W_REFILL = 4u, W_SENDING = 8u, W_READ = 16u;   // HostCtx::w_fl (W_READ: the messages answer reads)
 
 // per-lane LDS of the round kernel (one wave per block; [slot][lane] layouts)
 __shared__ shd_event s_top[kBlock];              // heap root
@@ -1195,6 +1195,26 @@ __device__ bool if_send_step(const DParams& P, HostCtx& c) {
 // exactly one rand_r step triple is consumed and its value is not needed.
 static_assert(SHD_PHOLD_LISTEN_PORT < SHD_MIN_RANDOM_PORT, "a random port never hits the listener");
 __device__ __forceinline__ void random_free_port(HostCtx& c) { (void)rand_r_dev(c.rng); }
+// the same draw, with the port it makes (the status trace records it):
+// round(nextDouble * (65535 - MIN_RANDOM_PORT)) + MIN_RANDOM_PORT
+__device__ __forceinline__ uint32_t random_free_port_value(HostCtx& c) {
+    const int32_t v = rand_r_dev(c.rng);
+    const double pick = rint((double)v / 2147483647.0 * (double)(65535u - SHD_MIN_RANDOM_PORT));
+    return (uint32_t)(uint16_t)((uint16_t)pick + (uint16_t)SHD_MIN_RANDOM_PORT);
+}
+// the application's side of a datagram (SHD_QF_TRACE_STATUS): the bind's port
+// draw and the SND_CREATED record, or the plain draw
+__device__ __forceinline__ void bind_and_create(const DParams& P, HostCtx& c, uint32_t pkt) {
+    if (c.k.feat & F_STATUS) {
+        const uint32_t port = random_free_port_value(c);
+        trace(P, c, c.now, port, c.h, ~0u, pkt, SHD_TR_CREATED);
+    } else {
+        random_free_port(c);
+    }
+}
+__device__ __forceinline__ void app_read(const DParams& P, HostCtx& c) {
+    if ((c.k.feat & F_STATUS) && (c.w_fl & W_READ)) trace(P, c, c.now, 0, c.h, ~0u, ~0u, SHD_TR_READ);
+}
 
 // _phold_sendNewMessage (test_phold.c:218-230) up to the socket send: draw
 // the destination (resolved at the flush; only whether one exists matters
@@ -1204,7 +1224,7 @@ __device__ bool enqueue_new_message(const DParams& P, HostCtx& c) {
     const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
     PROF_ADD(c, PR_PICK, tp)
     if ((int32_t)rv > c.dst_thr) return false;   // no i with dest_cum[i] >= r
-    random_free_port(c);
+    bind_and_create(P, c, c.pkt_seq);
     const uint32_t pkt = c.pkt_seq++;
     if (c.tq_count >= c.k.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
     if (c.tq_count == 0) {
@@ -1405,6 +1425,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     case SHD_EV_NOTIFY:
         c.flags &= ~F_NOTIFY_PENDING;
         c.w_msgs = c.unread;
+        c.w_fl |= W_READ;
         c.unread = 0;
         break;
     default:
@@ -1422,10 +1443,11 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     const bool boot = bootstrapping(P, c);
     // (one exit: a loopback ends the loop through tq_count)
     while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap && !boot) {
+        app_read(P, c);
         const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
         c.w_msgs--;
         if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
-            random_free_port(c);
+            bind_and_create(P, c, c.pkt_seq);
             const uint32_t pkt = c.pkt_seq++;
             if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
                 s_tqh[threadIdx.x] = TxEnt{rv, pkt};
@@ -1450,6 +1472,7 @@ __device__ bool run_work(const DParams& P, HostCtx& c) {
             c.w_fl &= ~W_SENDING;
         }
         if (c.w_msgs) {
+            app_read(P, c);
             const bool go = enqueue_new_message(P, c);
             c.w_msgs--;
             if (go) c.w_fl |= W_SENDING;
@@ -2117,7 +2140,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
                         i_be = clock64();
 #endif
-                        st = (c.w_fl | c.w_msgs) ? 1u : 0u;   // the shared steps, if any are left
+                        st = ((c.w_fl & ~W_READ) | c.w_msgs) ? 1u : 0u;   // the shared steps, if any are left
 #ifndef SHD_NO_FUSE
                         // An arrival schedules its notification at +1 ns, and
                         // that is almost always the host's next event: when the
@@ -2489,18 +2512,6 @@ __device__ __forceinline__ TlPart tl_gather(const TlPart* __restrict__ parts, ui
         tl_fold(f, o);
     }
     return f;
-}
-__device__ __forceinline__ uint64_t tl_gather_next(const TlPart* __restrict__ parts, uint32_t n) {
-    uint64_t m = kInf;
-    for (uint32_t j = threadIdx.x; j < n; j += 64) {
-        const uint64_t v = parts[j].next;
-        m = v < m ? v : m;
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(m, off, 64);
-        m = o < m ? o : m;
-    }
-    return m;
 }
 // The shares in two phases, so that their loads go out first and the
 // host-state loads behind them (the window start waits only for these):
@@ -3504,7 +3515,8 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         if (k && (rc = ealloc(e, &P.hb, (size_t)n * k))) { shd_eng_destroy(e); return rc; }
     }
     P.feat = (m->trace ? F_TRACE : 0u) | (P.hb ? F_HB : 0u) | (P.pcount ? F_PCOUNT : 0u) |
-             (P.host_hb ? F_HOSTHB : 0u) | (P.force_ambig ? F_AMBIG : 0u);
+             (P.host_hb ? F_HOSTHB : 0u) | (P.force_ambig ? F_AMBIG : 0u) |
+             ((m->trace && (m->queue_flags & SHD_QF_TRACE_STATUS)) ? F_STATUS : 0u);
     P.sum = e->d_sum;
     // the serial-equivalent window W: min over every latency a send can be
     // served (rows, direct values, self values) -> ceil(lat * 1e6) ns

@@ -24,9 +24,12 @@ SHD_QF_NO_CALENDAR = 1      # queue_flags: every inter-host event through inbox 
 SHD_QF_COUNT_PATHS = 2      # queue_flags: per-path packet counters on the device
 SHD_QF_HEARTBEATS = 4       # queue_flags: tracker node counters at every heartbeat
 SHD_QF_NO_APP_START = 8     # queue_flags: the caller pushes the application starts (shd_eng_push_events)
+SHD_QF_TRACE_STATUS = 16    # queue_flags: with trace, the application's records too (status_lines)
+SHD_PHOLD_LISTEN_PORT = 8998   # PHOLD_LISTEN_PORT, test_phold.c:34
+SHD_MIN_RANDOM_PORT = 10000    # MIN_RANDOM_PORT, definitions.h:94
 
 EV_HEARTBEAT, EV_REFILL, EV_REFILL_LO, EV_APP_START, EV_PACKET, EV_LOCAL, EV_NOTIFY = range(1, 8)
-TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL = range(1, 8)
+TR_SENT, TR_INET_DROP, TR_ARRIVE, TR_CODEL_DROP, TR_RECV, TR_IF_DROP, TR_LOCAL, TR_CREATED, TR_READ = range(1, 10)
 
 ERRORS = {
     0: "ok", -22: "EINVAL", -12: "ENOMEM", -19: "ENODEV", -75: "EOVERFLOW",
@@ -436,3 +439,105 @@ def tracker_node_lines(snapshots, interval_ns: int, payload: int) -> list:
         lines.append("[shadow-heartbeat] [node] %u,%d,%d,%f,%d,%f;%s;%s;%s;%s" % (
             secs, rb, sb, 0.0, 0, 0.0, zero, zero, _counter_string(din, payload), _counter_string(dout, payload)))
     return lines
+
+
+# ---- [STATUS] packet lines (packet_addDeliveryStatus, packet.c:647-659) ----
+# Every status a packet passes through is logged as `[<STATUS>] <packet_toString>`
+# (packet.c:518-641), the string ending in the packet's whole status list so far.
+# The lines come from an engine (or oracle) trace recorded with
+# SHD_QF_TRACE_STATUS; each trace kind stands for the reference's calls:
+_STATUS_OF = {
+    TR_CREATED: ("SND_CREATED", "SND_SOCKET_BUFFERED"),          # udp.c:116, socket.c:405
+    TR_SENT: ("SND_INTERFACE_SENT", "INET_SENT"),                # network_interface.c:545, worker.c:306
+    TR_INET_DROP: ("SND_INTERFACE_SENT", "INET_DROPPED"),        # network_interface.c:545, worker.c:319
+    TR_LOCAL: ("SND_INTERFACE_SENT",),                           # network_interface.c:545 (own address)
+    TR_ARRIVE: ("ROUTER_ENQUEUED",),                             # router.c:113
+    TR_CODEL_DROP: ("ROUTER_DROPPED",),                          # router_queue_codel.c:139
+    # router.c:129 (not for the loopback shortcut), network_interface.c:382,
+    # socket.c:143, socket.c:330
+    TR_RECV: ("ROUTER_DEQUEUED", "RCV_INTERFACE_RECEIVED", "RCV_SOCKET_PROCESSED", "RCV_SOCKET_BUFFERED"),
+    TR_IF_DROP: ("ROUTER_DEQUEUED", "RCV_INTERFACE_RECEIVED", "RCV_INTERFACE_DROPPED"),   # n_i.c:382, 411
+    TR_READ: ("RCV_SOCKET_DELIVERED",),                          # udp.c:158
+}
+
+
+def ip_string(ip) -> str:
+    """A host address as address_ipToNewString prints it (dotted quad); `ip` is
+    a dotted string or a host-order integer."""
+    if isinstance(ip, str):
+        return ip
+    ip = int(ip)
+    return "%d.%d.%d.%d" % ((ip >> 24) & 255, (ip >> 16) & 255, (ip >> 8) & 255, ip & 255)
+
+
+def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT) -> list:
+    """[STATUS] lines of a run traced with SHD_QF_TRACE_STATUS: a list of
+    (time_ns, host index, line), line = "[<STATUS>] packetID=<hostID>:<pkt>
+    <srcIP>:<srcPort> -> <dstIP>:<dstPort> bytes=<n> status=<S1>,...,<Sk>"
+    (packet.c:522-547, 616-633, 657).  `ips[h]` is host h's address,
+    `host_ids[h]` its host_getID (default h + 1); the destination port is the
+    PHOLD listener (test_phold.c:223), the source port the implicit bind's
+    draw (the CREATED record).  Order: by (time, host), records of one host in
+    the engine's order, except that a datagram sent in the instant it was
+    created follows its creation at once, as in the reference's call chain
+    (sendto -> networkinterface_wantsSend -> _networkinterface_sendPackets)."""
+    tr = np.asarray(trace, dtype=TRACE_DTYPE)
+    if host_ids is None:
+        host_ids = [h + 1 for h in range(len(ips))]
+    order = np.lexsort((np.arange(len(tr)), tr["host"], tr["time"]))
+    tr = tr[order]
+    NONE = 0xFFFFFFFF
+    port, dst, created_at, local = {}, {}, {}, set()
+    for r in tr:
+        k, h, p = int(r["kind"]), int(r["host"]), int(r["pkt"])
+        if k == TR_CREATED:
+            port[(h, p)] = int(r["seq"])
+            created_at[(h, p)] = int(r["time"])
+        elif k in (TR_SENT, TR_INET_DROP, TR_LOCAL):
+            dst[(h, p)] = int(r["peer"])
+            if k == TR_LOCAL:
+                local.add((h, p))
+    sends = {}   # sender records that follow their creation
+    for i, r in enumerate(tr):
+        k, h, p = int(r["kind"]), int(r["host"]), int(r["pkt"])
+        if k in (TR_SENT, TR_INET_DROP, TR_LOCAL) and created_at.get((h, p)) == int(r["time"]):
+            sends[(h, p)] = i
+    hist = {}
+    inbox = {}   # per host: datagrams buffered in the socket, oldest first
+    out = []
+
+    def emit(t, at, key, statuses):
+        src, pkt = key
+        st = hist.setdefault(key, [])
+        d = dst.get(key, NONE)
+        head = "packetID=%u:%u %s:%u -> %s:%u bytes=%u" % (
+            host_ids[src], pkt, ip_string(ips[src]), port.get(key, 0),
+            ip_string(ips[d]) if d != NONE else "?", listen_port, payload)
+        for name in statuses:
+            st.append(name)
+            out.append((t, at, "[%s] %s status=%s" % (name, head, ",".join(st))))
+
+    for i, r in enumerate(tr):
+        k, h, p, t = int(r["kind"]), int(r["host"]), int(r["pkt"]), int(r["time"])
+        if k in (TR_SENT, TR_INET_DROP, TR_LOCAL) and sends.get((h, p)) == i:
+            continue   # emitted with its creation
+        if k == TR_CREATED:
+            emit(t, h, (h, p), _STATUS_OF[k])
+            j = sends.get((h, p))
+            if j is not None:
+                emit(t, h, (h, p), _STATUS_OF[int(tr[j]["kind"])])
+        elif k in (TR_SENT, TR_INET_DROP, TR_LOCAL):
+            emit(t, h, (h, p), _STATUS_OF[k])
+        elif k == TR_READ:
+            q = inbox.get(h)
+            if q:
+                emit(t, h, q.pop(0), _STATUS_OF[k])
+        else:   # the receiver's records name the packet by (source, pkt)
+            key = (int(r["peer"]), p)
+            names = _STATUS_OF[k]
+            if k in (TR_RECV, TR_IF_DROP) and key in local:
+                names = names[1:]   # the loopback shortcut skips the router
+            emit(t, h, key, names)
+            if k == TR_RECV:
+                inbox.setdefault(h, []).append(key)
+    return out

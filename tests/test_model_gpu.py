@@ -138,3 +138,27 @@ def test_push_events_rejects_what_it_cannot_take():
     eng.push_events(np.array([(S.SHD_SEC + 5, 0, 1, 1, 0, S.EV_APP_START)], dtype=S.EVENT_DTYPE))
     st = eng.run()
     assert st.n_pkt_events > 0
+
+
+@pytest.mark.parametrize("codel", [False, True], ids=["plain", "codel"])
+def test_status_trace_matches_oracle(codel):
+    """SHD_QF_TRACE_STATUS: the application's records (CREATED with the bind's
+    port draw, READ) on the device equal the oracle's, and so do the [STATUS]
+    lines made from them (packet.c:518-659).  codel: 1500-B payloads into a
+    512 KiB/s receive bucket, so packets queue and CoDel drops some."""
+    V = 120
+    g = W.geometric_graph(V, seed=9)
+    kw = dict(payload=1500, bw_down=512, codelq_cap=256, load=32) if codel else dict(load=4)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=3 * S.SHD_SEC, trace=True,
+                      queue_flags=S.SHD_QF_TRACE_STATUS, **kw)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    eng = Engine(m, pc)
+    st = eng.run()
+    otr = assert_same_run(eng, st.n_pkt_events, m, g)
+    kinds = np.bincount(otr["kind"], minlength=10)
+    assert kinds[S.TR_CREATED] > 0 and kinds[S.TR_READ] > 0
+    if codel:
+        assert kinds[S.TR_CODEL_DROP] > 0
+    ips = ["11.0.0.%d" % (h + 1) for h in range(V)]
+    payload = kw.get("payload", 1)
+    assert S.status_lines(eng.trace(), ips, payload=payload) == S.status_lines(otr, ips, payload=payload)

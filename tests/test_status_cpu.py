@@ -1,0 +1,77 @@
+"""The [STATUS] packet lines (packet_addDeliveryStatus / packet_toString,
+packet.c:518-659) from a status trace (SHD_QF_TRACE_STATUS), on a hand-built
+trace whose expected lines follow the reference's call chain, and on an
+oracle run (every datagram's statuses well formed)."""
+import numpy as np
+
+import oracle_ffi as O
+import shdgpu as S
+import workloads as W
+
+NONE = 0xFFFFFFFF
+
+
+def rec(t, seq, host, peer, pkt, kind):
+    return (t, seq, host, peer, pkt, kind)
+
+
+def test_status_lines_follow_the_reference_call_chain():
+    # host 0 creates packet 5 (port 12345) to host 1 and sends it at once; it
+    # arrives at t=2000, is dequeued, read at t=2001; host 1 answers with
+    # packet 0 to itself (loopback: no router), received at +1 ns
+    tr = np.array([
+        rec(1000, 12345, 0, NONE, 5, S.TR_CREATED),
+        rec(2000, 7, 1, 0, 5, S.TR_ARRIVE),
+        rec(2000, 0, 1, 0, 5, S.TR_RECV),
+        rec(2001, 0, 1, NONE, NONE, S.TR_READ),
+        rec(2001, 10001, 1, NONE, 0, S.TR_CREATED),
+        rec(2002, 0, 1, 1, 0, S.TR_RECV),
+        rec(1000, 3, 0, 1, 5, S.TR_SENT),          # out of order, as a flush writes it
+        rec(2001, 9, 1, 1, 0, S.TR_LOCAL),
+    ], dtype=S.TRACE_DTYPE)
+    lines = S.status_lines(tr, ["11.0.0.1", "11.0.0.2"], host_ids=[7, 8])
+    a = "packetID=7:5 11.0.0.1:12345 -> 11.0.0.2:8998 bytes=1 status="
+    b = "packetID=8:0 11.0.0.2:10001 -> 11.0.0.2:8998 bytes=1 status="
+    want = [
+        (1000, 0, "[SND_CREATED] " + a + "SND_CREATED"),
+        (1000, 0, "[SND_SOCKET_BUFFERED] " + a + "SND_CREATED,SND_SOCKET_BUFFERED"),
+        (1000, 0, "[SND_INTERFACE_SENT] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT"),
+        (1000, 0, "[INET_SENT] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,INET_SENT"),
+        (2000, 1, "[ROUTER_ENQUEUED] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,INET_SENT,"
+                                             "ROUTER_ENQUEUED"),
+    ]
+    assert lines[:5] == want
+    seq_a = [l for t, h, l in lines if "packetID=7:5" in l]
+    assert seq_a[-1].startswith("[RCV_SOCKET_DELIVERED] ")
+    assert seq_a[-1].endswith("ROUTER_ENQUEUED,ROUTER_DEQUEUED,RCV_INTERFACE_RECEIVED,RCV_SOCKET_PROCESSED,"
+                              "RCV_SOCKET_BUFFERED,RCV_SOCKET_DELIVERED")
+    assert [t for t, h, l in lines if "packetID=7:5" in l][-1] == 2001
+    seq_b = [l for t, h, l in lines if "packetID=8:0" in l]
+    assert seq_b[-1].endswith("status=SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,RCV_INTERFACE_RECEIVED,"
+                              "RCV_SOCKET_PROCESSED,RCV_SOCKET_BUFFERED")   # loopback: no router, not read yet
+    assert [x[0] for x in lines] == sorted(x[0] for x in lines)
+
+
+def test_oracle_status_trace_is_well_formed():
+    V = 40
+    g = W.geometric_graph(V, seed=3)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=2 * S.SHD_SEC, trace=True, load=3,
+                      queue_flags=S.SHD_QF_TRACE_STATUS)
+    otr, odg, ost = O.engine_run(m, g)
+    kinds = np.bincount(otr["kind"], minlength=10)
+    assert kinds[S.TR_CREATED] == kinds[S.TR_SENT] + kinds[S.TR_INET_DROP] + kinds[S.TR_LOCAL] > 0
+    assert kinds[S.TR_READ] > 0
+    assert np.all((otr["seq"][otr["kind"] == S.TR_CREATED] >= S.SHD_MIN_RANDOM_PORT))
+    lines = S.status_lines(otr, ["11.0.0.%d" % (h + 1) for h in range(V)])
+    by_pkt = {}
+    for t, h, l in lines:
+        by_pkt.setdefault(l.split()[1], []).append(l.split("status=")[1].split(","))
+    for key, sts in by_pkt.items():
+        last = sts[-1]
+        assert last[:2] == ["SND_CREATED", "SND_SOCKET_BUFFERED"], key
+        assert all(s == last[:len(s)] for s in sts)          # each line's list extends the previous
+    # without the flag the trace has no application records
+    m2 = W.phold_model(W.hosts_on_vertices(V, 1), end_time=2 * S.SHD_SEC, trace=True, load=3)
+    otr2, _, _ = O.engine_run(m2, g)
+    assert not np.any(otr2["kind"] >= S.TR_CREATED)
+    assert len(otr2) == len(otr) - kinds[S.TR_CREATED] - kinds[S.TR_READ]
