@@ -149,6 +149,7 @@ struct DevCtl {
     unsigned long long stop;
     unsigned long long round_base;
     unsigned long long xtag;   // peer-to-peer exchanges: the tag of the batch's first round (round i: + i)
+    unsigned long long xpar;   // peer-to-peer: the receive-block parity of the batch's first round (round i: + i)
 };
 
 // Exchange mode (shd_xgroup): the per-peer blocks of the fixed-size
@@ -260,6 +261,11 @@ struct ParamsT {
     Ptr<uint32_t> xcount;              // [xworld] events queued per peer this round
     uint32_t xcap;
     int32_t xworld;                // engines of the group; host partition (H*p)/xworld
+    // peer-to-peer transport: every rank's receive blocks ([2][xworld][xcap+1]
+    // events, mapped here); a round stores its sends to peer p straight into
+    // block (wi, xme) of xpeer[p] (null: the send blocks xsend)
+    shd_event* const* xpeer;
+    int32_t xme, xpad;
 };
 // The host fills Params (plain pointers); device code reads the same bytes
 // as DParams, whose pointers carry the global address space, so that loads
@@ -433,6 +439,8 @@ struct HostCtx {
     uint64_t ws;         // the round's window start (calendar append horizon)
     uint32_t ws_mod;     // ws % 1 ms (refill alignment)
     int np;              // the next round's inbox parity
+    uint32_t xwi;        // peer-to-peer: this round's receive-block parity
+    uint32_t xput;       // peer-to-peer: this lane stored into a peer's receive block
     uint32_t err;
     uint32_t n_pend;
 #ifdef SHD_PROF
@@ -634,6 +642,16 @@ __device__ __forceinline__ bool cal_push(const DParams& P, int32_t dl, const shd
     return true;
 }
 
+// a 16-B write-through (system-scope) store: the line leaves every cache on
+// the way (peer-to-peer receive blocks).  hipcc does not count it: its
+// writers drain with an explicit s_waitcnt vmcnt(0); the s_nop keeps the
+// data registers intact until the store has read them
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_sys(void* p, uint4 v) {
+    const u32x4 x = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
+}
+
 // deliver an inter-host event: to the destination's calendar (or inbox) for a
 // later round, or to the remote outbox when it lives on another engine
 // the calendar-less part of a delivery: the inbox of a local destination
@@ -650,7 +668,15 @@ __device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
             const int32_t peer = owner_of(P, e.dst);
             const uint32_t s = atomicAdd(&P.xcount[peer], 1u);
             if (s < P.xcap) {
-                P.xsend[(size_t)peer * (P.xcap + 1) + 1 + s] = e;
+                if (P.xpeer) {   // peer-to-peer: into the peer's receive block, write-through
+                    shd_event* d = P.xpeer[peer] + ((size_t)c.xwi * P.xworld + P.xme) * (P.xcap + 1) + 1 + s;
+                    const EvV x = ev_ld(&e);
+                    st16_sys(d, x.a);
+                    st16_sys((char*)d + 16, x.b);
+                    c.xput = 1;
+                } else {
+                    P.xsend[(size_t)peer * (P.xcap + 1) + 1 + s] = e;
+                }
                 return;
             }
             // block full: spill to the remote buffer (the header says so, the
@@ -1942,7 +1968,7 @@ __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
 // window, run events < we
 __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, uint64_t ws, uint64_t we, int parity,
                                            uint64_t& next_out, uint64_t& nev_out, uint64_t& npkt_out,
-                                           uint32_t& err_out) {
+                                           uint32_t& err_out, uint32_t xwi = 0) {
     const int32_t l = lane_host(P);
 #ifdef SHD_PROF
     const unsigned long long w0 = wall_clock64();
@@ -2018,7 +2044,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     hot_load(P, c);
     PendDel pd;
     c.ns = 0; c.att = 0; c.cls = 0; c.err = 0;
-    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1;
+    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0;
     // the window's non-empty bins, all slots loaded before the host record is
     // consumed (one round trip, overlapping the record's)
     EvV bx[3][kBinCap];
@@ -2310,6 +2336,9 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #endif
     flush_finish(P, c, pd);
     err |= c.err;
+    // peer-to-peer: a wave that stored into a peer's receive block drains
+    // those stores before the round ends (k_xchg tags the blocks next)
+    if (P.xpeer && __ballot(c.xput != 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     TIM(3);
     next_out = next; nev_out = nev; npkt_out = npkt; err_out = err;
 }
@@ -2843,7 +2872,7 @@ __global__ __launch_bounds__(kBlock) void k_round_xtl(DRoundArgs a, const DParam
     if (we > stop || we < ws) we = stop;
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    round_body(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((ctl->xpar + (uint64_t)i) & 1));
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(next, off, 64);
         next = o < next ? o : next;
@@ -2957,21 +2986,20 @@ __device__ __forceinline__ uint32_t x_tag(const DevCtl* ctl, uint32_t add, int u
 // fence (an L2 write-back) before the tag as well (A/B, SHD_X_FENCE)
 __device__ __forceinline__ void x_put(const shd_event* __restrict__ src, shd_event* __restrict__ dst, uint32_t n,
                                       XHeader h, uint32_t tag, int fence) {
-    const unsigned long long* s8 = (const unsigned long long*)(src + 1);
-    unsigned long long* d8 = (unsigned long long*)(dst + 1);
-    for (uint32_t k = threadIdx.x; k < 4 * n; k += blockDim.x)
-        __hip_atomic_store(d8 + k, s8[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint4* s16 = (const uint4*)(src + 1);
+    for (uint32_t k = threadIdx.x; k < 2 * n; k += blockDim.x) st16_sys((uint4*)(dst + 1) + k, s16[k]);
+    // the header's first 16 B ride with the events; its second 16 B (which
+    // holds the tag) go alone, after every storing wave drained (one 16-B
+    // store is not torn: a reader that sees the tag sees all of the header)
+    const uint4 g0 = make_uint4((uint32_t)h.next_time, (uint32_t)(h.next_time >> 32), h.count, h.flags);
+    const uint4 g1 = make_uint4((uint32_t)h.n_pending, (uint32_t)(h.n_pending >> 32), h.error, tag);
+    if (threadIdx.x == 0) st16_sys(dst, g0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
     __syncthreads();
     if (threadIdx.x == 0) {
-        h.pad = tag;
-        unsigned long long* hw = (unsigned long long*)dst;
-        const unsigned long long* hv = (const unsigned long long*)&h;
-        for (int k = 0; k < 3; k++) __hip_atomic_store(hw + k, hv[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store((uint32_t*)dst + 6, h.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        st16_sys((uint4*)dst + 1, g1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store((uint32_t*)dst + 7, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -3053,10 +3081,11 @@ __device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __rest
         }
     }
     __syncthreads();
-    // the put (as k_xput)
+    // the put (as k_xput); the round stored its events into the peer's block
+    // already (P.xpeer): then only the header goes
     shd_event* dst = peers[p] + ((size_t)wi * P.xworld + me) * stride;
     XHeader h = *(const XHeader*)src;
-    const uint32_t n = h.count < P.xcap ? h.count : P.xcap;
+    const uint32_t n = P.xpeer ? 0u : (h.count < P.xcap ? h.count : P.xcap);
     x_put(src, dst, n, h, x_tag(ctl, tag_add, use_ctl), fence);
 }
 
@@ -4306,6 +4335,13 @@ struct shd_xgroup {
     uint64_t xepoch = 0;               // exchange tags issued (never rolled back)
 };
 
+// peer-to-peer: the round stores its sends straight into the peers' receive
+// blocks (A/B: SHD_X_STAGED copies them from the send blocks in k_xchg)
+static bool x_direct() {
+    static const bool staged = getenv("SHD_X_STAGED") != nullptr;
+    return !staged;
+}
+
 static bool x_want_protect(const shd_xgroup* g) {
     if (protect_off()) return false;
     if (g->engs[0]->P.complete && !protect_all()) return false;   // nothing is ever logged (want_protect)
@@ -4320,6 +4356,8 @@ static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
     P.xcount = g->loc[k].xcount;
     P.xcap = g->xcap;
     P.xworld = g->world;
+    P.xpeer = (g->p2p && x_direct()) ? (shd_event* const*)g->d_peers : nullptr;
+    P.xme = g->rank0;
     P.sum = sum;
     return P;
 }
@@ -4769,7 +4807,8 @@ static int x_enqueue_rounds(shd_xgroup* g, int nb) {
     int rc = SHD_OK;
     for (int i = 0; i < nb; i++) {
         const int ri = (int)((g->xseq - 1) & 1);
-        static const bool ticket = getenv("SHD_X_TICKET") != nullptr;   // A/B: the ticketed round
+        static const bool ticket_env = getenv("SHD_X_TICKET") != nullptr;   // A/B: the ticketed round
+        const bool ticket = ticket_env && !g->p2p;   // (the peer-to-peer exchange folds the ticketless shares)
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
             const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
@@ -4919,6 +4958,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             e->h_ctl->stop = stop;
             e->h_ctl->round_base = e->round;
             e->h_ctl->xtag = g->xepoch + 1;   // peer-to-peer: round i's exchange is tagged xtag + i
+            e->h_ctl->xpar = g->xseq & 1;     // peer-to-peer: round i's receive blocks have parity xpar + i
             SHD_HIP(hipMemcpyAsync(&e->d_ring[1], &e->h_seed[1], sizeof(DevSummary), hipMemcpyHostToDevice,
                                    e->stream));
             SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
