@@ -4607,6 +4607,9 @@ static int x_p2p_map(shd_xgroup* g) {
     uint32_t ok = 1;
     for (const Share& x : all) ok &= x.ok;
     g->p2p_peer.assign(W, nullptr);
+    // test hook: this rank fails to map its peers (every rank must then fail alike)
+    if (const char* f = getenv("SHD_P2P_FAIL_RANK"))
+        if (atoi(f) == g->rank0) ok = 0;
     for (int p = 0; p < W && ok; p++) {
         if (p == g->rank0) {
             g->p2p_peer[p] = g->p2p_base;

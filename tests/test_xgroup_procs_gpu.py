@@ -96,3 +96,13 @@ def test_multiprocess_group_rolls_back_ambiguous_rounds(p2p, tmp_path):
                     env_extra={"SHD_FORCE_AMBIG": "1", "SHD_PROTECT_ALL": "1"})
     check_against_oracle(res, 160, 2, 3.0, 0.01, 16)
     assert all(int(r["stats"][5]) > 0 for r in res)            # reruns happened on every rank
+
+
+def test_p2p_mapping_failure_on_one_rank_fails_every_rank_alike(tmp_path):
+    """A rank that cannot map its peers' receive blocks (test hook) takes part
+    in both all-gathers of the mapping: every rank gets SHD_ENODEV from
+    shd_xgroup_create_p2p, none waits forever, and all fall back to the
+    all-to-all transport (as bench.py does) and still match the oracle."""
+    res = run_ranks(2, tmp_path, extra=["--p2p"], env_extra={"SHD_P2P_FAIL_RANK": "1"})
+    check_against_oracle(res, 240, 1, 3.0, 0.01, 16)
+    assert all(int(r["stats"][6]) == 1 for r in res)

@@ -54,7 +54,14 @@ def main():
     info = pc.info()
     pb = partition(m.n_hosts, a.world)
     eng = Engine(m, pc, pb[a.rank], pb[a.rank + 1])
-    grp = XGroup.over(eng, comm, block_events=a.block, p2p=a.p2p)
+    fallback = 0
+    try:
+        grp = XGroup.over(eng, comm, block_events=a.block, p2p=a.p2p)
+    except S.ShdError:   # the peer-to-peer mapping failed on some rank: every rank falls back alike
+        if not a.p2p:
+            raise
+        fallback = 1
+        grp = XGroup.over(eng, comm, block_events=a.block)
     pkt = ev = pend = rounds = prot = rerun = 0
     for t in (int(0.7 * S.SHD_SEC), S.SHD_SEC + 3, 2 * S.SHD_SEC, end):
         st = grp.run_until(min(t, end))
@@ -65,7 +72,7 @@ def main():
         prot += st.n_rounds_protected
         rerun += st.n_rounds_rerun
     np.savez(os.path.join(a.out, f"rank{a.rank}.npz"), trace=eng.trace(), digest=eng.digest(), lat=lat, rel=rel,
-             stats=np.array([pkt, ev, pend, rounds, prot, rerun], dtype=np.uint64),
+             stats=np.array([pkt, ev, pend, rounds, prot, rerun, fallback], dtype=np.uint64),
              ties=np.array([info.n_ties, info.max_hops, info.sssp_iterations_max], dtype=np.int64))
     grp.close()
     eng.close()
