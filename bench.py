@@ -27,8 +27,11 @@ sys.path[:0] = [os.path.join(REPO, "shadow-1_amd")]
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8 TB/s HBM3E (spec)
-BYTES_PER_EVENT = 64             # event record stored once + loaded once
-BYTES_PER_PKT_EVENT = 16 + 32    # path entry (lat+rel f64) + router-queue entry in/out
+# algorithmic bytes = 80 per packet event (event read 32 +
+# new event written 32 + path entry 16) + 136 per active host-round (host
+# state read + written once per round in which the host executes anything)
+BYTES_PER_PKT_EVENT = 80
+BYTES_PER_HOST_ROUND = 136
 
 
 def parse():
@@ -205,15 +208,18 @@ def main():
     elapsed = t1 - t0
     if world > 1 and not use_group:
         pkt, evs, rounds, kms, ems = st.pkt_events, st.events, st.rounds, st.kernel_ms, st.kernel_ms
+        hr = getattr(st, "host_rounds", 0)
     else:
         pkt, evs, rounds = st.n_pkt_events, st.n_events, st.n_rounds
         kms, ems = st.device_ms_round_kernel, st.device_ms_launches
-    tot = torch.tensor([float(pkt), float(evs), float(kms), float(ems)], dtype=torch.float64, device="cuda")
+        hr = st.n_host_rounds
+    tot = torch.tensor([float(pkt), float(evs), float(kms), float(ems), float(hr)], dtype=torch.float64,
+                       device="cuda")
     mx = torch.tensor([elapsed, upload_s], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tot)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    pkt_all, ev_all, kms_all, ems_all = tot.tolist()
+    pkt_all, ev_all, kms_all, ems_all, hr_all = tot.tolist()
     elapsed, upload_max = mx.tolist()
     value = pkt_all / elapsed
     # rounds run behind a state copy (they could log many first touches) and
@@ -227,7 +233,7 @@ def main():
     # includes the gaps between launches); the device-clock time inside the
     # kernel (first block start to last block end) is reported beside it.
     launches = rounds * max(world, 1)
-    alg_bytes = BYTES_PER_EVENT * ev_all + BYTES_PER_PKT_EVENT * pkt_all
+    alg_bytes = BYTES_PER_PKT_EVENT * pkt_all + BYTES_PER_HOST_ROUND * hr_all
     avg_launch_ms = (ems_all if ems_all > 0 else kms_all) / max(launches, 1)
     achieved = (alg_bytes / max(launches, 1)) / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     # the dominant kernel: ticketless device rounds on one engine (k_round_tl,
@@ -237,7 +243,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname),
                 "kernel": kname, "avg_launch_us": round(avg_launch_ms * 1e3, 3),
                 "avg_in_kernel_us": round(kms_all / max(launches, 1) * 1e3, 3),
-                "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1)}
+                "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1),
+                "alg_bytes": "SURVEY.md 8(d): 80 B x packet events + 136 B x active host-rounds",
+                "packet_events_per_launch": round(pkt_all / max(launches, 1), 1),
+                "active_hosts_per_launch": round(hr_all / max(launches, 1), 1)}
 
     lossy = None
     if world == 1 and args.lossy_edge_loss_max > 0 and not use_group and args.workload == "c3":

@@ -409,6 +409,8 @@ typedef struct shd_run_stats {
                                        could log many first touches) */
     uint32_t n_rounds_rerun;        /* protected rounds rolled back and rerun after an
                                        ambiguous first-touch drop decision */
+    uint64_t n_host_rounds;         /* (host, round) pairs in which the host executed at least
+                                       one event: the host-state reads of SURVEY.md 8(d) */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

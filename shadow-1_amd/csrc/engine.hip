@@ -111,7 +111,7 @@ struct HostCnt {
 // a block's share of the round summary (round_complete)
 struct BlockPart {
     unsigned long long next, nev, npkt;
-    unsigned int err, pad;
+    unsigned int err, nact;   // nact: hosts with at least one event
 };
 constexpr uint32_t kTickGroup = 64;   // blocks per first-level completion ticket
 
@@ -132,7 +132,7 @@ struct DevSummary {
     unsigned long long t_first;    // device wall clock: first block start, last block end
     unsigned long long t_last;
     unsigned int done;             // blocks finished (last-block ticket)
-    unsigned int pad;
+    unsigned int n_active;         // hosts that executed at least one event (ticketless rounds)
 };
 
 __device__ __forceinline__ DevSummary fresh_summary() {
@@ -1741,6 +1741,7 @@ __device__ __forceinline__ void part_fold(BlockPart& a, const BlockPart& b) {
     a.nev += b.nev;
     a.npkt += b.npkt;
     a.err |= b.err;
+    a.nact += b.nact;
 }
 __device__ __forceinline__ void part_wave_reduce(BlockPart& q) {
     for (int off = 32; off > 0; off >>= 1) {
@@ -1749,13 +1750,14 @@ __device__ __forceinline__ void part_wave_reduce(BlockPart& q) {
         o.nev = __shfl_xor(q.nev, off, 64);
         o.npkt = __shfl_xor(q.npkt, off, 64);
         o.err = __shfl_xor(q.err, off, 64);
+        o.nact = __shfl_xor(q.nact, off, 64);
         part_fold(q, o);
     }
 }
 __device__ bool round_complete(const DParams& P, uint64_t next, uint64_t nev, uint64_t npkt, uint32_t err) {
     static_assert(kBlock == 64 && kTickGroup <= 64, "one wave per block; a group folds in one pass");
     __shared__ int s_last;
-    BlockPart q{next, nev, npkt, err, 0};
+    BlockPart q{next, nev, npkt, err, nev != 0 ? 1u : 0u};   // summed over the lanes below
     part_wave_reduce(q);
     const uint32_t nblk = gridDim.x, g = blockIdx.x / kTickGroup;
     const uint32_t ngrp = (nblk + kTickGroup - 1) / kTickGroup;
@@ -1792,6 +1794,7 @@ __device__ bool round_complete(const DParams& P, uint64_t next, uint64_t nev, ui
         if (x.nev) atomicAdd(&P.sum->n_events, x.nev);
         if (x.npkt) atomicAdd(&P.sum->n_pkt_events, x.npkt);
         if (x.err) atomicOr(&P.sum->error, x.err);
+        if (x.nact) atomicAdd(&P.sum->n_active, x.nact);
         __threadfence();
     }
     __syncthreads();
@@ -2518,7 +2521,7 @@ __global__ __launch_bounds__(kBlock) void k_round_dev(DRoundArgs a, const DevSum
 // The host runs these batches once a batch has logged nothing.
 struct TlPart {
     unsigned long long next, t_end;
-    unsigned int nev, npkt, err, pad;
+    unsigned int nev, npkt, err, nact;   // nact: hosts with at least one event
 };
 __device__ __forceinline__ void tl_fold(TlPart& a, const TlPart& b) {
     a.next = b.next < a.next ? b.next : a.next;
@@ -2526,6 +2529,7 @@ __device__ __forceinline__ void tl_fold(TlPart& a, const TlPart& b) {
     a.nev += b.nev;
     a.npkt += b.npkt;
     a.err |= b.err;
+    a.nact += b.nact;
 }
 // the wave's fold of the shares [0, n) (one wave per block)
 __device__ __forceinline__ TlPart tl_gather(const TlPart* __restrict__ parts, uint32_t n) {
@@ -2538,6 +2542,7 @@ __device__ __forceinline__ TlPart tl_gather(const TlPart* __restrict__ parts, ui
         o.nev = __shfl_xor(f.nev, off, 64);
         o.npkt = __shfl_xor(f.npkt, off, 64);
         o.err = __shfl_xor(f.err, off, 64);
+        o.nact = __shfl_xor(f.nact, off, 64);
         tl_fold(f, o);
     }
     return f;
@@ -2570,6 +2575,7 @@ __device__ __forceinline__ void tl_reduce(TlPart& f, bool full) {
             f.nev += __shfl_xor(f.nev, off, 64);
             f.npkt += __shfl_xor(f.npkt, off, 64);
             f.err |= __shfl_xor(f.err, off, 64);
+            f.nact += __shfl_xor(f.nact, off, 64);
         }
     }
 }
@@ -2581,6 +2587,7 @@ __device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint3
     if (f.nev) atomicAdd(&s->n_events, (unsigned long long)f.nev);
     if (f.npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f.npkt);
     if (f.err) atomicOr(&s->error, f.err);
+    if (f.nact) atomicAdd(&s->n_active, f.nact);
     atomicMax(&s->t_last, f.t_end);
     if (s->n_pending) *halt = 1u;
 }
@@ -2656,6 +2663,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
     uint32_t err;
     round_body(P, in, ws, we, parity, next, nev, npkt, err);
     TIM(4);
+    const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));   // hosts that executed an event
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(next, off, 64);
         next = o < next ? o : next;
@@ -2663,7 +2671,8 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
         npkt += __shfl_xor(npkt, off, 64);
         err |= __shfl_xor(err, off, 64);
     }
-    if (threadIdx.x == 0) *mine = TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, 0};
+    if (threadIdx.x == 0)
+        *mine = TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, nact};
     TIM(5);
 }
 
@@ -2873,6 +2882,7 @@ __global__ __launch_bounds__(kBlock) void k_round_xtl(DRoundArgs a, const DParam
     uint64_t next, nev, npkt;
     uint32_t err;
     round_body(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((ctl->xpar + (uint64_t)i) & 1));
+    const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));   // hosts that executed an event
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t o = __shfl_xor(next, off, 64);
         next = o < next ? o : next;
@@ -2882,7 +2892,7 @@ __global__ __launch_bounds__(kBlock) void k_round_xtl(DRoundArgs a, const DParam
     }
     if (threadIdx.x == 0)
         parts[(size_t)(i & 1) * gridDim.x + blockIdx.x] =
-            TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, 0};
+            TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, nact};
 }
 
 __global__ __launch_bounds__(64) void k_xfold(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
@@ -2912,6 +2922,7 @@ __global__ __launch_bounds__(64) void k_xfold(DParams P, const TlPart* __restric
         o.nev = __shfl_xor(f.nev, off, 64);
         o.npkt = __shfl_xor(f.npkt, off, 64);
         o.err = __shfl_xor(f.err, off, 64);
+        o.nact = __shfl_xor(f.nact, off, 64);
         tl_fold(f, o);
     }
     uint64_t next = fwd ? ws : f.next;
@@ -2922,6 +2933,7 @@ __global__ __launch_bounds__(64) void k_xfold(DParams P, const TlPart* __restric
         if (!fwd) {
             sum->n_events = f.nev;
             sum->n_pkt_events = f.npkt;
+            sum->n_active = f.nact;
             sum->error = err;
             sum->t_last = f.t_end;
         }
@@ -3044,6 +3056,7 @@ __device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __rest
             o.nev = __shfl_xor(f.nev, off, 64);
             o.npkt = __shfl_xor(f.npkt, off, 64);
             o.err = __shfl_xor(f.err, off, 64);
+            o.nact = __shfl_xor(f.nact, off, 64);
             tl_fold(f, o);
         }
         if ((threadIdx.x & 63) == 0) s_f[threadIdx.x >> 6] = f;
@@ -3058,6 +3071,7 @@ __device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __rest
                 if (!fwd) {
                     sum->n_events = f.nev;
                     sum->n_pkt_events = f.npkt;
+                    sum->n_active = f.nact;
                     atomicOr(&sum->error, err);   // the ingest of the same launch may add bits
                     sum->t_last = f.t_end;
                 }
@@ -3246,7 +3260,7 @@ struct shd_eng {
     std::vector<int32_t> h_rank, h_self_rank;
     int32_t next_rank = 0;
     uint64_t pending_resolved = 0;
-    uint64_t round_ws = 0, round_we = 0, round_pending = 0, round_events = 0, round_pkt = 0;
+    uint64_t round_ws = 0, round_we = 0, round_pending = 0, round_events = 0, round_pkt = 0, round_active = 0;
     uint64_t round = 0;                     // rounds executed (parity = round & 1)
     // device-driven pipeline
     static constexpr int kBatch = 64;
@@ -3742,6 +3756,7 @@ extern "C" int shd_eng_round_kernel(shd_eng* e, uint64_t ws, uint64_t we, shd_ro
     e->round_pending = e->h_sum->n_pending;
     e->round_events = e->h_sum->n_events;
     e->round_pkt = e->h_sum->n_pkt_events;
+    e->round_active = e->h_sum->n_active;
     if (out) {
         out->window_start = ws; out->window_end = we;
         out->next_time = e->h_sum->next_time;
@@ -4002,6 +4017,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             s.n_rounds++;
             s.n_events += r.n_events;
             s.n_pkt_events += r.n_pkt_events;
+            s.n_host_rounds += e->round_active;   // the kept run of the round
             s.final_time = we;
             if (r.error) { s.error = r.error; break; }
             e->last_logged = e->pending_resolved - pend_before;
@@ -4051,6 +4067,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             s.n_rounds++;
             s.n_events += r.n_events;
             s.n_pkt_events += r.n_pkt_events;
+            s.n_host_rounds += r.n_active;
             uint64_t we = ws + e->window;
             if (we > stop || we < ws) we = stop;
             s.final_time = we;
@@ -5034,6 +5051,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
                 const DevSummary& r = e->h_ring[i + 1];
                 s.n_events += r.n_events;
                 s.n_pkt_events += r.n_pkt_events;
+                s.n_host_rounds += r.n_active;
                 const double ms = round_kernel_ms(e, r);
                 kms += ms;
                 e->last_kernel_ms = ms;

@@ -138,11 +138,15 @@ def test_bench_headline_run_to_run_deterministic():
     for _ in range(2):
         e = Engine(m, pc)
         st = e.run()
-        outs.append(((st.n_events, st.n_pkt_events, st.n_rounds), e.digest()))
+        outs.append(((st.n_events, st.n_pkt_events, st.n_rounds, st.n_host_rounds), e.digest()))
         e.close()
     assert outs[0][0] == outs[1][0] and np.array_equal(outs[0][1], outs[1][1])
     d1 = outs[0][1]
     assert int(d1["n_pkt_events"].sum()) == outs[0][0][1]
+    # active host-rounds (bench.py's roofline bytes): at most one per host per
+    # round, at most one per event
+    n_ev, _, n_rounds, n_hr = outs[0][0]
+    assert 0 < n_hr <= min(n_ev, n_rounds * m.n_hosts)
     pc.close()
 
 
@@ -165,6 +169,7 @@ def test_bench_workload_sharded_group_equals_single_engine(hosts, parts):
     dg = np.concatenate([x.digest() for x in engines])
     assert gst.error == 0
     assert gst.n_pkt_events == st.n_pkt_events and gst.n_events == st.n_events
+    assert gst.n_host_rounds == st.n_host_rounds   # the same rounds, the same active hosts
     assert np.array_equal(dg, d1)
     close_all(engines, grp)
     pc.close()
