@@ -289,6 +289,8 @@ def main():
             "pcie_inclusive": {"value": round(pkt_all / (elapsed + upload_max), 1),
                                "upload_ms": round(upload_max * 1e3, 3)},
             "rounds": int(rounds),
+            "timed_batches": None if (world > 1 and not use_group) else int(getattr(st, "n_batches", 0)),
+            "timed_batches_ticketless": None if (world > 1 and not use_group) else int(st.n_batches_ticketless),
             "first_touch": protected,
             "apsp": {"rows": int(info.rows_computed), "vertices": V, "build_ms": round(min(builds), 3),
                      "sssp_kernel_ms": round(info.build_ms_sssp, 3), "iterations": int(info.sssp_iterations_max),
@@ -355,7 +357,7 @@ def pmc_traffic(kernel):
         return None
     if prof.get("engine_source_sha1") != hashlib.sha1(src).hexdigest() or prof.get("kernel") != kernel:
         return None
-    return prof.get("hbm_bytes_per_dispatch")
+    return prof.get("hbm_bytes_per_round_timed", prof.get("hbm_bytes_per_dispatch"))
 
 
 def cpu_threads():

@@ -411,6 +411,8 @@ typedef struct shd_run_stats {
                                        ambiguous first-touch drop decision */
     uint64_t n_host_rounds;         /* (host, round) pairs in which the host executed at least
                                        one event: the host-state reads of SURVEY.md 8(d) */
+    uint64_t n_batches;             /* device batches launched (shd_eng: 64 round launches
+                                       each; shd_xgroup: up to 64 rounds each) */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

@@ -21,13 +21,29 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_dispatch(d, counter, kernel):
+    """the counter's value per dispatch of `kernel`, in dispatch order"""
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                    vals.append(float(row["Counter_Value"]))
-    return vals
+                    key = int(row.get("Dispatch_Id") or row.get("Correlation_Id") or len(vals))
+                    vals.append((key, float(row["Counter_Value"])))
+    return [v for _, v in sorted(vals)]
+
+
+def timed(vals, bench_json):
+    """the timed region's dispatches: the last 64 x (ticketless batches) of
+    the run (bench.py --pmc-run writes the counts of its timed region); None
+    unless every timed batch was ticketless"""
+    try:
+        b = json.load(open(bench_json))
+    except (OSError, ValueError):
+        return None
+    n = int(b.get("timed_batches_ticketless") or 0) * 64
+    if not n or int(b.get("timed_batches") or -1) * 64 != n or n > len(vals):
+        return None
+    return vals[-n:], int(b["rounds"])
 
 
 def main():
@@ -35,6 +51,8 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--kernel", default="k_round_tl")
+    ap.add_argument("--fetch-bench", help="the FETCH_SIZE pass's bench.py JSON line (its timed-region counts)")
+    ap.add_argument("--write-bench", help="the WRITE_SIZE pass's bench.py JSON line")
     ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r02", "k_round_pmc_bytes.json"))
     a = ap.parse_args()
     fe = per_dispatch(a.fetch_dir, "FETCH_SIZE", a.kernel)
@@ -57,6 +75,18 @@ def main():
                    "--no-cpu-baseline, separate passes; averaged over every " + a.kernel + " dispatch of the run",
         "engine_source_sha1": hashlib.sha1(src).hexdigest(),
     }
+    tf = timed(fe, a.fetch_bench) if a.fetch_bench else None
+    tw = timed(wr, a.write_bench) if a.write_bench else None
+    if tf and tw and tf[1] == tw[1]:
+        # the timed region alone (warm-up rounds log first touches: halted
+        # batches leave cheap forward-only launches that dilute the average):
+        # the bytes of every launch of the timed batches over its rounds, as
+        # bench.py's roofline counts launches
+        out["timed_rounds"] = tf[1]
+        out["timed_dispatches"] = len(tf[0])
+        out["FETCH_SIZE_KB_timed_per_round"] = round(sum(tf[0]) / tf[1], 3)
+        out["WRITE_SIZE_KB_timed_per_round"] = round(sum(tw[0]) / tw[1], 3)
+        out["hbm_bytes_per_round_timed"] = int(round((2 * sum(tf[0]) + sum(tw[0])) / tf[1] * 1024))
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))

@@ -17,10 +17,11 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
     python3 bench.py $ARGS > $O/bench_under_rocprof.json 2> $O/trace.err || { tail $O/trace.err; exit 2; }
 cp "$(find $O/trace -name '*kernel_stats.csv' | head -1)" $O/bench_kernel_stats.csv && rm -rf $O/trace || exit 2
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o run -- \
-    python3 bench.py $ARGS > /dev/null 2> $O/fetch.err || { tail $O/fetch.err; exit 3; }
+    python3 bench.py $ARGS > $O/fetch_bench.json 2> $O/fetch.err || { tail $O/fetch.err; exit 3; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- \
-    python3 bench.py $ARGS > /dev/null 2> $O/write.err || { tail $O/write.err; exit 4; }
-python3 scripts/pmc_bytes.py $O/fetch $O/write --out $O/k_round_pmc_bytes.json > /dev/null && rm -rf $O/fetch $O/write || exit 5
+    python3 bench.py $ARGS > $O/write_bench.json 2> $O/write.err || { tail $O/write.err; exit 4; }
+python3 scripts/pmc_bytes.py $O/fetch $O/write --fetch-bench $O/fetch_bench.json --write-bench $O/write_bench.json \
+    --out $O/k_round_pmc_bytes.json > /dev/null && rm -rf $O/fetch $O/write || exit 5
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM" \
            "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM SQ_BUSY_CYCLES SQ_INSTS_LDS" ; do

@@ -1962,9 +1962,11 @@ __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
 #pragma unroll
         for (int j = 0; j < (int)kNBW; j++) in.w[j] = 0;
     }
+#ifdef SHD_REC_EARLY   // A/B: every lane's record in the first round trip
     in.rec = a.hs[l];
     in.att = a.att[l];
     in.st = a.st[l];
+#endif
 }
 
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
@@ -1991,9 +1993,15 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     // hosts with nothing due this round touch 3 words and their bitmap, not their whole state
     bool idle = false;
     uint32_t wbits = 0;   // bit j: window bin j is non-empty
+#ifdef SHD_REC_EARLY
     const HostRec& rec = in.rec;
     const int32_t rec_att = in.att;
     const int4 rec_st = in.st;
+#else
+    HostRec rec;
+    int32_t rec_att;
+    int4 rec_st;
+#endif
     uint32_t nin0 = 0;
     if (l < P.nloc) {
         nin0 = parity ? in.nin[1] : in.nin[0];
@@ -2013,14 +2021,10 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             idle = true;
             next = t0;
             if (P.bins) {
+                // the window's bins hold nothing: their counts are zero (a
+                // count is nonzero only behind a set bit, cal_push), no reset
                 const uint64_t cb = cal_lower_bound(P, w, we);
                 next = cb < next ? cb : next;
-                // the counts of the window's wholly consumed bins (appends
-                // that overflowed into the inbox leave a count without a bit)
-#pragma unroll
-                for (uint32_t j = 0; j < 2; j++)
-                    if (j < nbin && ((b0 + j + 1) << P.bin_shift) <= we)
-                        P.bin_n[(size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1))] = 0;
             }
         }
     }
@@ -2062,6 +2066,15 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             for (uint32_t k = 0; k < kBinCap; k++) bx[j][k] = ev_ld(bp + k);
         }
     }
+#ifndef SHD_REC_EARLY
+    // the host record behind the bins, in the same round trip, for the
+    // hosts with something due only (idle hosts' records are never read)
+    if (active) {
+        rec = P.hs[l];
+        rec_att = P.host_att[P.h0 + l];
+        rec_st = P.self_thr[P.h0 + l];
+    }
+#endif
     if (active) {
         PROF_T0(t_all)
         load_ctx(P, c, l, rec, rec_att, rec_st);
@@ -2275,20 +2288,22 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
         if (P.bins) {
             // bins wholly before we are consumed: reset them (no append of
             // this round can target them: appends are >= we and within the
-            // horizon).  Idle hosts reset their counts too (cal_reset_counts).
+            // horizon).  Only a bin with its bit set has a nonzero count: an
+            // append that claims a slot sets the bit once its event is stored,
+            // and one past the capacity follows the claims below it (cal_push,
+            // flush), so the empty bins' counts are left alone -- a store per
+            // host and bin, most of the round's write traffic otherwise.
 #pragma unroll
             for (uint32_t j = 0; j < 3; j++) {
                 const uint64_t b = b0 + j;
-                if (j < nbin && ((b + 1) << P.bin_shift) <= we) {
+                if (j < nbin && ((b + 1) << P.bin_shift) <= we && ((wbits >> j) & 1u)) {
                     const uint32_t p = (uint32_t)b & (kNB - 1);
                     P.bin_n[(size_t)l * kNB + p] = 0;
-                    if ((wbits >> j) & 1u) {
-                        const uint32_t m = 1u << (p & 31);
-                        atomicAnd(&P.bin_bits[(size_t)l * kNBW + (p >> 5)], ~m);
+                    const uint32_t m = 1u << (p & 31);
+                    atomicAnd(&P.bin_bits[(size_t)l * kNBW + (p >> 5)], ~m);
 #pragma unroll
-                        for (int k = 0; k < (int)kNBW; k++)
-                            if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
-                    }
+                    for (int k = 0; k < (int)kNBW; k++)
+                        if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
                 }
             }
             const uint64_t cb = cal_lower_bound(P, w, we);
@@ -4039,6 +4054,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         static const bool no_tl = getenv("SHD_NO_TL") != nullptr;
         const bool tl = e->tl_ready && !no_tl;
         if ((rc = launch_batch(e, tl))) break;
+        s.n_batches++;
         if (tl) s.n_batches_ticketless++;
         SHD_HIP(hipEventRecord(e->bev[1], e->stream));
         uint32_t halt = 0;
@@ -4986,6 +5002,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         }
         SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
         if ((rc = x_launch_rounds(g, nb))) break;
+        s.n_batches++;
         g->xepoch += (uint64_t)nb;
         SHD_HIP(hipGetLastError());
         SHD_HIP(hipEventRecord(g->engs[0]->bev[1], g->engs[0]->stream));
