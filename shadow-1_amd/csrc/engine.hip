@@ -3150,23 +3150,45 @@ __device__ __forceinline__ void xwait_ingest(const DParams& P, const shd_event* 
             }
         }
     }
+#ifdef SHD_X_ACQUIRE   // A/B: an acquire fence (this CU's L1 invalidated) after the polls
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
+    // no acquire fence: the receive blocks are uncached device memory (no L2
+    // line of them on any XCD) and this CU holds no L1 line of them (the
+    // kernel started with an invalidated L1, and the polls bypass it), so
+    // the loads behind the barrier read what the peers' drained
+    // write-through stores left in memory
     __syncthreads();
     if (s_bad) {
         if (threadIdx.x == 0) *P.halt = 1u;
         return;
     }
-    if (!ingest || *P.halt) return;
-    const int parity = (int)((ctl->round_base + (uint64_t)ri + 1) & 1);   // the next round's inbox
+    if (!ingest) return;
     const uint64_t t = (uint64_t)blk * blockDim.x + threadIdx.x;
     const uint64_t p = t / P.xcap, s = t % P.xcap;
     if (p >= (uint64_t)P.xworld) return;
+    // halt, the round base, the block's count and the slot's event in one
+    // round trip (the slot is inside the block whatever the count); each is
+    // consumed only once all are out, or the compiler would issue them one
+    // behind the other's branch
     const shd_event* b = xrecv + p * stride;
-    if (s >= ((const XHeader*)b)->count) return;
-    const shd_event e = b[1 + s];
+    uint32_t halt = *P.halt;
+    uint64_t rbase = ctl->round_base, ws = P.sum->ws;
+    uint32_t cnt = ((const XHeader*)b)->count;
+    uint4 e0 = ((const uint4*)(b + 1 + s))[0], e1 = ((const uint4*)(b + 1 + s))[1];
+    asm volatile("" : "+v"(halt), "+v"(rbase), "+v"(ws), "+v"(cnt), "+v"(e0.x), "+v"(e0.y), "+v"(e0.z), "+v"(e0.w), "+v"(e1.x),
+                 "+v"(e1.y), "+v"(e1.z), "+v"(e1.w));
+    if (halt || s >= cnt) return;
+    const int parity = (int)((rbase + (uint64_t)ri + 1) & 1);   // the next round's inbox
+    shd_event e;
+    {
+        const uint4 ev[2] = {e0, e1};
+        static_assert(sizeof(ev) == sizeof(e), "two 16-B halves");
+        __builtin_memcpy(&e, ev, sizeof(e));
+    }
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
-    if (cal_push(P, dl, e, P.sum->ws)) return;
+    if (cal_push(P, dl, e, ws)) return;
     const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
     if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
     P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
