@@ -175,7 +175,9 @@ def main():
         if args.exchange == "p2p":
             try:   # every rank fails alike (the mapping is checked collectively)
                 grp = XGroup.over(eng, comm, p2p=True)
-                exchange = "shd_xgroup/peer-to-peer (IPC-mapped receive blocks, xGMI stores)"
+                exchange = ("shd_xgroup/peer-to-peer (IPC-mapped receive blocks, xGMI stores, "
+                            + ("a separate exchange launch per round)" if os.environ.get("SHD_X_UNFUSED") else
+                               "each round's launch completes the previous round's exchange)"))
             except S.ShdError as ex:
                 log(rank, f"peer-to-peer transport unavailable ({ex}); RCCL all-to-all instead")
         if grp is None:
@@ -238,7 +240,9 @@ def main():
     achieved = (alg_bytes / max(launches, 1)) / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     # the dominant kernel: ticketless device rounds on one engine (k_round_tl,
     # once no first touch is logged), the engine group's k_round_x across GPUs
-    kname = "k_round_xtl" if use_group else ("k_round" if world > 1 else "k_round_tl")
+    # (peer-to-peer rounds after a batch's first are k_round_px, which also completes the exchange)
+    fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and not os.environ.get("SHD_X_UNFUSED")
+    kname = ("k_round_px" if fused else "k_round_xtl") if use_group else ("k_round" if world > 1 else "k_round_tl")
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname),
                 "kernel": kname, "avg_launch_us": round(avg_launch_ms * 1e3, 3),

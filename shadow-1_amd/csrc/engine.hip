@@ -154,16 +154,23 @@ struct DevCtl {
 
 // Exchange mode (shd_xgroup): the per-peer blocks of the fixed-size
 // all-to-all buffers start with one header slot, then `xcap` events.
+// Granule 0 (the first 16 B) holds what a round needs to start -- the next
+// time, the flags and, peer-to-peer, the exchange's tag -- so that one 16-B
+// store publishes it and one 16-B load reads it; granule 1 what a flagged
+// round's recovery needs.
 struct XHeader {
     unsigned long long next_time;  // sender's earliest pending event (its hosts + its sends in flight)
-    uint32_t count;                // events in this block (<= xcap)
     uint32_t flags;                // XF_* of the sender's round
+    uint32_t tag;                  // peer-to-peer: the exchange's number (0 on the other transports)
     unsigned long long n_pending;  // sender's first-touch log of the round
     uint32_t error;
-    uint32_t pad;
+    uint32_t count;                // events in this block (<= xcap)
 };
 static_assert(sizeof(XHeader) == sizeof(shd_event), "header fills one event slot");
 constexpr uint32_t XF_PENDING = 1u, XF_OVERFLOW = 2u, XF_ERROR = 4u;
+// fused peer-to-peer rounds: event slots per (sender, destination block) region
+// and round; one lane of the receiving block reads one slot
+constexpr uint32_t kXSlots = 64;
 
 // destination-pick guide: for bucket k, i = the first index with
 // dest_cum[i] >= k / H, and the next three cumulative weights inline, so an
@@ -266,6 +273,13 @@ struct ParamsT {
     // block (wi, xme) of xpeer[p] (null: the send blocks xsend)
     shd_event* const* xpeer;
     int32_t xme, xpad;
+    // fused peer-to-peer rounds: a send for host d of peer p goes to p's
+    // region [wi][xme][(d - h0(p)) / hpw] (xpeer[p] + xroff, kXSlots events
+    // per region; slot from xcnt[wi][p][block]); null xcnt: the blocks above
+    Ptr<uint32_t> xcnt;                // [2][xworld][xnbx]
+    uint32_t xnbx;                     // region blocks per rank: ceil(ceil(H / xworld) / hpw)
+    uint32_t xrcap;                    // region slots used: min(kXSlots, xcap) (small blocks force spills)
+    uint64_t xroff;                    // events from a rank's receive base to its regions
 };
 // The host fills Params (plain pointers); device code reads the same bytes
 // as DParams, whose pointers carry the global address space, so that loads
@@ -664,7 +678,23 @@ __device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
         if (slot >= P.inbox_cap) { c.err |= SHD_ERR_INBOX_OVERFLOW; return; }
         P.inbox[c.np][(size_t)dl * P.inbox_cap + slot] = e;
     } else {
-        if (P.xsend) {   // exchange mode: straight into the peer's all-to-all block
+        if (P.xcnt) {   // fused peer-to-peer rounds: into the region of the destination's block
+            const int32_t peer = owner_of(P, e.dst);
+            const uint32_t hp0 = (uint32_t)(((uint64_t)P.H * (uint64_t)peer) / (uint64_t)P.xworld);
+            const uint32_t blk = (e.dst - hp0) / (uint32_t)P.hpw;
+            const size_t r = ((size_t)c.xwi * P.xworld + peer) * P.xnbx + blk;
+            const uint32_t s = blk < P.xnbx ? atomicAdd(&P.xcnt[r], 1u) : kXSlots;
+            if (s < P.xrcap) {
+                shd_event* d = P.xpeer[peer] + P.xroff +
+                               (((size_t)c.xwi * P.xworld + P.xme) * P.xnbx + blk) * kXSlots + s;
+                const EvV x = ev_ld(&e);
+                st16_sys(d, x.a);
+                st16_sys((char*)d + 16, x.b);
+                c.xput = 1;
+                return;
+            }
+            // region full: spill (as a full block below)
+        } else if (P.xsend) {   // exchange mode: straight into the peer's all-to-all block
             const int32_t peer = owner_of(P, e.dst);
             const uint32_t s = atomicAdd(&P.xcount[peer], 1u);
             if (s < P.xcap) {
@@ -2772,7 +2802,7 @@ __device__ void xpack_block(const DParams& P, const DevSummary* sum, int clean, 
     h.flags = fl;
     h.n_pending = clean ? 0 : sum->n_pending;
     h.error = sum->error;
-    h.pad = 0;
+    h.tag = 0;
     *(XHeader*)(P.xsend + (size_t)p * (P.xcap + 1)) = h;
     P.xcount[p] = 0;
 }
@@ -2969,7 +2999,7 @@ __global__ __launch_bounds__(64) void k_xfold(DParams P, const TlPart* __restric
     h.flags = fl;
     h.n_pending = fwd ? 0 : npend;
     h.error = fwd ? err0 : err;
-    h.pad = 0;
+    h.tag = 0;
     *(XHeader*)(P.xsend + (size_t)p * (P.xcap + 1)) = h;
     P.xcount[p] = 0;
 }
@@ -3015,17 +3045,17 @@ __device__ __forceinline__ void x_put(const shd_event* __restrict__ src, shd_eve
                                       XHeader h, uint32_t tag, int fence) {
     const uint4* s16 = (const uint4*)(src + 1);
     for (uint32_t k = threadIdx.x; k < 2 * n; k += blockDim.x) st16_sys((uint4*)(dst + 1) + k, s16[k]);
-    // the header's first 16 B ride with the events; its second 16 B (which
-    // holds the tag) go alone, after every storing wave drained (one 16-B
+    // the header's second 16 B ride with the events; its first 16 B (which
+    // hold the tag) go alone, after every storing wave drained (one 16-B
     // store is not torn: a reader that sees the tag sees all of the header)
-    const uint4 g0 = make_uint4((uint32_t)h.next_time, (uint32_t)(h.next_time >> 32), h.count, h.flags);
-    const uint4 g1 = make_uint4((uint32_t)h.n_pending, (uint32_t)(h.n_pending >> 32), h.error, tag);
-    if (threadIdx.x == 0) st16_sys(dst, g0);
+    const uint4 g0 = make_uint4((uint32_t)h.next_time, (uint32_t)(h.next_time >> 32), h.flags, tag);
+    const uint4 g1 = make_uint4((uint32_t)h.n_pending, (uint32_t)(h.n_pending >> 32), h.error, h.count);
+    if (threadIdx.x == 0) st16_sys((uint4*)dst + 1, g1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave, before the barrier
     __syncthreads();
     if (threadIdx.x == 0) {
         if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        st16_sys((uint4*)dst + 1, g1);
+        st16_sys(dst, g0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 }
@@ -3104,7 +3134,7 @@ __device__ __forceinline__ void xfold_put(const DParams& P, const TlPart* __rest
             h.flags = fl;
             h.n_pending = fwd ? 0 : npend;
             h.error = fwd ? err0 : err;
-            h.pad = 0;
+            h.tag = 0;
             *(XHeader*)src = h;
             P.xcount[p] = 0;
         }
@@ -3137,7 +3167,7 @@ __device__ __forceinline__ void xwait_ingest(const DParams& P, const shd_event* 
     __syncthreads();
     if (s_bad) return;
     if ((int32_t)threadIdx.x < P.xworld) {
-        const uint32_t* tw = (const uint32_t*)(xrecv + threadIdx.x * stride) + 7;
+        const uint32_t* tw = (const uint32_t*)(xrecv + threadIdx.x * stride) + 3;   // XHeader::tag
         const unsigned long long t0 = wall_clock64();
         // relaxed polls (an acquire per poll would invalidate this CU's caches
         // each time), one acquire once the tag is there
@@ -3211,6 +3241,345 @@ __global__ __launch_bounds__(256) void k_xchg(DParams P, const TlPart* __restric
         xfold_put(P, parts, nblk, i, ctl, peers, me, wi, tag_add, 1, (int)blockIdx.x, fence);
     else
         xwait_ingest(P, xrecv, ctl, tag_add, 1, i, 1, xerr, blockIdx.x - (uint32_t)P.xworld);
+}
+
+// ---- fused peer-to-peer rounds (the default peer-to-peer schedule) ----
+// Round i's launch (k_round_px) also completes exchange i - 1, so a round is
+// one launch: blocks [0, world) fold round i - 1's shares and put this
+// engine's header for peer p (granule 0 -- next time, flags, tag -- in one
+// 16-B store; a flagged header's granule 1 first, drained); every block then
+// waits for every peer's header of exchange i - 1 (lane p polls peer p's
+// granule 0), takes the window start as their min, and ingests what the
+// peers stored for its own hosts during round i - 1: region [wi][p][block]
+// of kXSlots events, lane k reading slot k of every peer's region.  An event
+// goes to its host's calendar (or inbox), and the lane that owns the host
+// learns it through LDS, so the host state loaded at entry stays valid
+// without a second round trip.  A batch: k_round_xtl (round 0: the exchange
+// before it is done), k_round_px (rounds 1 ..), k_xchg_px (the last round's
+// exchange).  Region slots hold an event iff its time is nonzero; the
+// receiver zeroes a slot's time once it took the event (the sender stores
+// into that region again two exchanges later, after it saw this engine's
+// next header, which follows the end of this launch).
+static_assert(kXSlots == (uint32_t)kBlock, "one region slot per lane");
+
+__device__ __forceinline__ uint4 ld16_sys(const void* p) {
+    u32x4 x;
+    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(x) : "v"(p) : "memory");
+    return make_uint4(x[0], x[1], x[2], x[3]);
+}
+
+// the events of the regions [p][blk] (p != xme) of one parity -> calendar /
+// inbox[parity] of the block's hosts; s_n / s_w (or null): what each lane's
+// host received, for the lane (inbox count, calendar bins).  Returns error bits.
+__device__ uint32_t xrgn_ingest(const DParams& P, shd_event* __restrict__ rgn, uint32_t blk, uint64_t ws_send,
+                                int parity, uint32_t* s_n, uint32_t (*s_w)[kBlock]) {
+    uint32_t err = 0;
+    const int32_t W = P.xworld;
+    for (int32_t p0 = 0; p0 < W; p0 += 8) {
+        uint4 ea[8], eb[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {   // every slot's load out before any is consumed
+            const int32_t p = p0 + k;
+            ea[k] = make_uint4(0, 0, 0, 0);
+            eb[k] = ea[k];
+            if (p < W && p != P.xme) {
+                const uint4* q = (const uint4*)(rgn + ((size_t)p * P.xnbx + blk) * kXSlots + threadIdx.x);
+                ea[k] = q[0];
+                eb[k] = q[1];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if ((ea[k].x | ea[k].y) == 0) continue;   // time 0: an empty slot
+            shd_event e;
+            {
+                const uint4 ev[2] = {ea[k], eb[k]};
+                __builtin_memcpy(&e, ev, sizeof(e));
+            }
+            *(uint64_t*)(rgn + ((size_t)(p0 + k) * P.xnbx + blk) * kXSlots + threadIdx.x) = 0;   // taken
+            const int32_t dl = (int32_t)e.dst - P.h0;
+            const int32_t j = dl - (int32_t)blk * P.hpw;
+            if (dl < 0 || dl >= P.nloc || j < 0 || j >= P.hpw) {
+                err |= SHD_ERR_REMOTE_OVERFLOW;
+                continue;
+            }
+            if (P.bins) {   // cal_push, the bin noted for the owner lane
+                const uint64_t bb = e.time >> P.bin_shift;
+                if (bb - (ws_send >> P.bin_shift) <= kHorizon) {
+                    const uint32_t pb = (uint32_t)bb & (kNB - 1);
+                    const size_t bi = (size_t)dl * kNB + pb;
+                    const uint32_t s = atomicAdd(&P.bin_n[bi], 1u);
+                    if (s < kBinCap) {
+                        P.bins[bi * kBinCap + s] = e;
+                        atomicOr(&P.bin_bits[(size_t)dl * kNBW + (pb >> 5)], 1u << (pb & 31));
+                        if (s_w) atomicOr(&s_w[pb >> 5][j], 1u << (pb & 31));
+                        continue;
+                    }
+                }
+            }
+            const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+            if (slot >= P.inbox_cap) {
+                err |= SHD_ERR_INBOX_OVERFLOW;
+                continue;
+            }
+            P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+            if (s_n) atomicAdd(&s_n[j], 1u);
+        }
+    }
+    return err;
+}
+
+// block p (< world) of an exchange: fold the round's shares (loaded into pv
+// by the caller; more past 256 blocks), complete its summary (block 0), pack
+// this engine's header for peer p and put it into p's header block (wi, me).
+// A halted round re-sends the last header under the new tag.
+__device__ __forceinline__ void px_fold_put(const DParams& P, DevSummary* sum, const TlPart (&pv)[4],
+                                            const TlPart* __restrict__ pp, uint32_t nblk, uint64_t pws,
+                                            uint64_t npend, uint64_t nrem, uint64_t pnext, uint32_t perr,
+                                            uint64_t stop, uint32_t halt, shd_event* const* __restrict__ peers,
+                                            int world, int me, int wi, uint32_t tag) {
+    const int p = (int)blockIdx.x;
+    const size_t stride = (size_t)P.xcap + 1;
+    shd_event* src = P.xsend + (size_t)p * stride;
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    tl_fold4(f, pv, nblk, 0);
+    for (uint32_t base = 256; base < nblk; base += 256) {
+        TlPart v[4];
+        tl_issue(pp, nblk, base, v);
+        tl_fold4(f, v, nblk, base);
+    }
+    tl_reduce(f, true);
+    XHeader h;
+    if (!halt) {
+        const bool fwd = pws >= stop;
+        uint64_t next = fwd ? pws : f.next;
+        next = pnext < next ? pnext : next;
+        const uint32_t err = perr | f.err;
+        h.next_time = next;
+        uint32_t fl = 0;
+        if (!fwd) {
+            if (npend) fl |= XF_PENDING;
+            if (nrem) fl |= XF_OVERFLOW;
+            if (err) fl |= XF_ERROR;
+        }
+        h.flags = fl;
+        h.tag = 0;
+        h.n_pending = fwd ? 0 : npend;
+        h.error = fwd ? perr : err;
+        h.count = 0;
+        if (threadIdx.x == 0) {
+            if (p == 0) {
+                sum->next_time = next;
+                if (!fwd) {
+                    sum->n_events = f.nev;
+                    sum->n_pkt_events = f.npkt;
+                    sum->n_active = f.nact;
+                    atomicOr(&sum->error, err);
+                    sum->t_last = f.t_end;
+                }
+            }
+            *(XHeader*)src = h;   // the last header (a halted round re-sends it)
+        }
+    } else {
+        h = *(const XHeader*)src;
+    }
+    if (threadIdx.x == 0) {
+        shd_event* dst = peers[p] + ((size_t)wi * world + me) * stride;
+        const uint4 g0 = make_uint4((uint32_t)h.next_time, (uint32_t)(h.next_time >> 32), h.flags, tag);
+        const uint4 g1 = make_uint4((uint32_t)h.n_pending, (uint32_t)(h.n_pending >> 32), h.error, h.count);
+        st16_sys((uint4*)dst + 1, g1);
+        if (h.flags) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a flagged header's body before its tag
+        st16_sys(dst, g0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+// wait for every peer's header of an exchange (lane p polls peer p's granule
+// 0, bounded: a peer that never comes sets *xerr, and later waits return at
+// once); the min next time and the flags over the group.  Wave-uniform.
+__device__ __forceinline__ bool px_wait(const shd_event* __restrict__ xhdr, size_t stride, int world, uint32_t tag,
+                                        uint32_t bad, uint32_t* __restrict__ xerr, uint64_t& ws, uint32_t& fl) {
+    ws = kInf;
+    fl = 0;
+    if (!bad && (int)threadIdx.x < world) {
+        const void* hp = xhdr + (size_t)threadIdx.x * stride;
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+            const uint4 hx = ld16_sys(hp);
+            if (hx.w == tag) {
+                ws = ((uint64_t)hx.y << 32) | hx.x;
+                fl = hx.z;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > kXWaitTicks) {
+                bad = 1;
+                __hip_atomic_fetch_or(xerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(ws, off, 64);
+        ws = o < ws ? o : ws;
+        fl |= __shfl_xor(fl, off, 64);
+    }
+    return __ballot(bad != 0) != 0;
+}
+
+// zero this block's stripe of the region counters of parity wi (their sends
+// were made in the previous round of that parity; the next use is two rounds on)
+__device__ __forceinline__ void px_reset_counts(const DParams& P, int wi, uint32_t blk, uint32_t nblk) {
+    const size_t n = (size_t)P.xworld * P.xnbx;
+    uint32_t* c = P.xcnt + (size_t)wi * n;
+    for (size_t j = (size_t)blk * kBlock + threadIdx.x; j < n; j += (size_t)nblk * kBlock) c[j] = 0;
+}
+
+__global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, DevSummary* __restrict__ prev,
+                                                      const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
+                                                      const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
+                                                      DRoundArgs a, const shd_event* __restrict__ xhdr,
+                                                      shd_event* __restrict__ rgn, shd_event* const* __restrict__ peers,
+                                                      XHeader* __restrict__ halt_hdr, uint32_t* __restrict__ xerr,
+                                                      int world, int me, int wprev) {
+    __shared__ uint32_t s_xn[kBlock];
+    __shared__ uint32_t s_xw[kNBW][kBlock];
+    const DParams& P = *Pp;
+    const unsigned long long t_entry = wall_clock64();
+    const uint32_t nblk = a.nblk;
+    const bool putter = (int)blockIdx.x < world;
+    asm volatile("" ::"s"(i), "s"(prev), "s"(ctl), "s"(parts), "s"(nblk), "s"(a.nloc), "s"(a.hpw), "s"(window));
+    // the loads of the exchange go out first (halt, control words, round
+    // i - 1's summary, its shares for the put blocks), the host state behind
+    uint32_t halt = *a.halt, bad = *xerr;
+    uint64_t stop = ctl->stop, rbase = ctl->round_base, xtag = ctl->xtag, xpar = ctl->xpar, pws = prev->ws;
+    uint64_t npend = 0, nrem = 0, pnext = 0;
+    uint32_t perr = 0;
+    const TlPart* pp = parts + (size_t)((i - 1) & 1) * nblk;
+    TlPart pv[4];
+    if (putter) {
+        tl_issue(pp, nblk, 0, pv);
+        npend = prev->n_pending;
+        nrem = prev->n_remote;
+        pnext = prev->next_time;
+        perr = prev->error;
+    }
+    const uint32_t warm = params_warm(Pp);
+    HostIn in;
+    host_in_load(a, in);
+    s_xn[threadIdx.x] = 0;
+#pragma unroll
+    for (int k = 0; k < (int)kNBW; k++) s_xw[k][threadIdx.x] = 0;
+    asm volatile("" : "+v"(halt), "+v"(bad), "+v"(stop), "+v"(rbase), "+v"(xtag), "+v"(xpar), "+v"(pws));
+    const uint32_t tag = (uint32_t)(xtag + (uint64_t)(i - 1));
+    const size_t stride = (size_t)P.xcap + 1;
+    if (putter)
+        px_fold_put(P, prev, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wprev, tag);
+    if (blockIdx.x >= nblk) return;   // a put block past the engine's hosts (grid = max(nblk, world))
+    uint64_t ws;
+    uint32_t fl;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (px_wait(xhdr, stride, world, tag, bad, xerr, ws, fl)) {
+        if (threadIdx.x == 0) *P.halt = 1u;
+        if (lead) P.sum->flags = 2u;
+        return;
+    }
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
+    __syncthreads();   // s_xn / s_xw zeroed
+    uint32_t ierr = 0;
+    if (!halt) ierr = xrgn_ingest(P, rgn, blockIdx.x, pws, parity, s_xn, s_xw);
+    px_reset_counts(P, wprev, blockIdx.x, nblk);
+    __syncthreads();
+    if (halt) {
+        if (lead) P.sum->flags = 2u;
+        return;
+    }
+    if (fl) {   // flagged somewhere in the group: every engine halts here alike
+        if (blockIdx.x == 0) {
+            if ((int)threadIdx.x < world) {
+                const void* hp = xhdr + (size_t)threadIdx.x * stride;
+                const uint4 g0 = ld16_sys(hp), g1 = ld16_sys((const uint4*)hp + 1);
+                XHeader h;
+                h.next_time = ((uint64_t)g0.y << 32) | g0.x;
+                h.flags = g0.z;
+                h.tag = g0.w;
+                h.n_pending = ((uint64_t)g1.y << 32) | g1.x;
+                h.error = g1.z;
+                h.count = g1.w;
+                halt_hdr[threadIdx.x] = h;
+            }
+            if (threadIdx.x == 0) {
+                *P.halt = 1u;
+                P.sum->flags = 1u;
+            }
+        }
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, t_entry);
+        *init = fresh_summary();
+        P.sum->ws = ws;
+    }
+    if (ws >= stop) return;   // only forwards the time (the next exchange packs it)
+    params_warm_done(warm);
+    {   // what this lane's host received in the exchange
+        const uint32_t n = s_xn[threadIdx.x];
+        if (parity) in.nin[1] += n;
+        else in.nin[0] += n;
+#pragma unroll
+        for (int k = 0; k < (int)kNBW; k++) in.w[k] |= s_xw[k][threadIdx.x];
+    }
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((xpar + (uint64_t)i) & 1));
+    err |= ierr;
+    const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0)
+        parts[(size_t)(i & 1) * nblk + blockIdx.x] =
+            TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, nact};
+}
+
+// the exchange of a batch's last round i (P.sum: its summary): blocks
+// [0, world) fold and put, blocks [world, world + nblk) wait and ingest their
+// block's regions into the next round's calendar / inbox
+__global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
+                                                     const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
+                                                     int world, int me, int wi, const shd_event* __restrict__ xhdr,
+                                                     shd_event* __restrict__ rgn, uint32_t* __restrict__ xerr) {
+    DevSummary* sum = P.sum;
+    uint32_t halt = *P.halt, bad = *xerr;
+    uint64_t stop = ctl->stop, rbase = ctl->round_base, xtag = ctl->xtag, pws = sum->ws;
+    const uint32_t tag = (uint32_t)(xtag + (uint64_t)i);
+    const TlPart* pp = parts + (size_t)(i & 1) * nblk;
+    if ((int)blockIdx.x < world) {
+        TlPart pv[4];
+        tl_issue(pp, nblk, 0, pv);
+        const uint64_t npend = sum->n_pending, nrem = sum->n_remote, pnext = sum->next_time;
+        const uint32_t perr = sum->error;
+        px_fold_put(P, sum, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wi, tag);
+        return;
+    }
+    const uint32_t blk = blockIdx.x - (uint32_t)world;
+    uint64_t ws;
+    uint32_t fl;
+    if (px_wait(xhdr, (size_t)P.xcap + 1, world, tag, bad, xerr, ws, fl)) {
+        if (threadIdx.x == 0) *P.halt = 1u;
+        return;
+    }
+    if (!halt) {
+        const uint32_t err = xrgn_ingest(P, rgn, blk, pws, (int)((rbase + (uint64_t)i + 1) & 1), nullptr, nullptr);
+        if (err) atomicOr(&sum->error, err);
+    }
+    px_reset_counts(P, wi, blk, nblk);
 }
 
 __global__ void k_digest(DParams P, shd_host_digest* __restrict__ out) {
@@ -4362,6 +4731,7 @@ struct shd_xgroup {
         XHeader* halt_hdr = nullptr;
         Params* d_xpr = nullptr;   // device copies of the exchange-mode P, one per summary-ring slot
         TlPart* parts = nullptr;   // [2][grid] ticketless round shares (k_round_xtl -> k_xfold)
+        uint32_t* xcnt = nullptr;  // fused peer-to-peer rounds: region slot counters [2][world][xnbx]
     };
     std::vector<Loc> loc;
     uint64_t xseq = 0;                 // exchanges done: the latest headers are in xrecv[(xseq - 1) & 1]
@@ -4388,6 +4758,8 @@ struct shd_xgroup {
     shd_event** d_peers = nullptr;     // the same on the device
     uint32_t* d_xerr = nullptr;        // set by a wait that timed out
     uint64_t xepoch = 0;               // exchange tags issued (never rolled back)
+    bool fused = false;                // peer-to-peer rounds fused with their exchange (k_round_px)
+    uint32_t xnbx = 0;                 // fused: region blocks per rank
 };
 
 // peer-to-peer: the round stores its sends straight into the peers' receive
@@ -4395,6 +4767,18 @@ struct shd_xgroup {
 static bool x_direct() {
     static const bool staged = getenv("SHD_X_STAGED") != nullptr;
     return !staged;
+}
+
+// peer-to-peer rounds complete the previous round's exchange in their own
+// launch (k_round_px); SHD_X_UNFUSED=1 keeps the separate k_xchg launch (A/B)
+static bool x_fuse_env() {
+    static const bool unfused = getenv("SHD_X_UNFUSED") != nullptr;
+    return !unfused;
+}
+
+// the fused schedule's regions: own base of parity w
+static shd_event* x_rgn(const shd_xgroup* g, int w) {
+    return g->p2p_base + 2 * (size_t)g->world * g->stride + (size_t)w * g->world * g->xnbx * kXSlots;
 }
 
 static bool x_want_protect(const shd_xgroup* g) {
@@ -4414,6 +4798,12 @@ static Params xparams(const shd_xgroup* g, int k, DevSummary* sum) {
     P.xpeer = (g->p2p && x_direct()) ? (shd_event* const*)g->d_peers : nullptr;
     P.xme = g->rank0;
     P.sum = sum;
+    if (g->fused) {
+        P.xcnt = g->loc[k].xcnt;
+        P.xnbx = g->xnbx;
+        P.xrcap = std::min<uint32_t>(kXSlots, g->xcap);
+        P.xroff = 2 * (uint64_t)g->world * g->stride;
+    }
     return P;
 }
 
@@ -4650,7 +5040,8 @@ static int x_p2p_map(shd_xgroup* g) {
         uint32_t pad[15];
     };
     Share mine{};
-    const size_t bytes = 2 * (size_t)W * g->stride * sizeof(shd_event);
+    const size_t bytes = (2 * (size_t)W * g->stride + (g->fused ? 2 * (size_t)W * g->xnbx * kXSlots : 0)) *
+                         sizeof(shd_event);
     if (hipExtMallocWithFlags((void**)&g->p2p_base, bytes, hipDeviceMallocUncached) == hipSuccess &&
         hipMemset(g->p2p_base, 0, bytes) == hipSuccess &&   // tag 0: no exchange yet (tags start at 1)
         hipDeviceSynchronize() == hipSuccess && hipIpcGetMemHandle(&mine.h, g->p2p_base) == hipSuccess)
@@ -4699,6 +5090,11 @@ static int x_p2p_map(shd_xgroup* g) {
 static int x_alloc(shd_xgroup* g) {
     g->stride = (size_t)g->xcap + 1;
     g->loc.resize(g->engs.size());
+    if (g->fused) {
+        const shd_eng* e = g->engs[0];
+        const int64_t per = (e->P.H + g->world - 1) / g->world;
+        g->xnbx = (uint32_t)((per + e->P.hpw - 1) / e->P.hpw);
+    }
     for (size_t k = 0; k < g->engs.size(); k++) {
         shd_eng* e = g->engs[k];
         shd_xgroup::Loc& L = g->loc[k];
@@ -4715,6 +5111,7 @@ static int x_alloc(shd_xgroup* g) {
             (rc = ealloc(e, &L.d_xpr, shd_eng::kRing, false)) ||
             (rc = ealloc(e, &L.parts, 2 * (size_t)((e->nloc + e->P.hpw - 1) / e->P.hpw))))
             return rc;
+        if (g->fused && (rc = ealloc(e, &L.xcnt, 2 * (size_t)g->world * g->xnbx))) return rc;
         std::vector<Params> pr(shd_eng::kRing);
         for (int i = 0; i < shd_eng::kRing; i++) pr[i] = xparams(g, (int)k, &e->d_ring[i]);
         SHD_HIP(hipMemcpyAsync(L.d_xpr, pr.data(), sizeof(Params) * pr.size(), hipMemcpyHostToDevice, e->stream));
@@ -4809,16 +5206,22 @@ static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p,
     g->p2p = p2p;
     g->engs.push_back(e);
     // the group agrees on W (min) and checks the model: H and end time equal everywhere
-    const unsigned long long mine[3] = {(unsigned long long)e->window, (unsigned long long)H,
-                                        (unsigned long long)e->P.end_time};
-    std::vector<unsigned long long> all(3 * (size_t)world);
-    int rc = shd_comm_allgather_host(comm, mine, 24, all.data());
+    // (and the hosts per wave: the fused schedule's regions are per block of hpw hosts)
+    const unsigned long long mine[4] = {(unsigned long long)e->window, (unsigned long long)H,
+                                        (unsigned long long)e->P.end_time, (unsigned long long)e->P.hpw};
+    std::vector<unsigned long long> all(4 * (size_t)world);
+    int rc = shd_comm_allgather_host(comm, mine, 32, all.data());
     if (rc) { x_free(g); return rc; }
     g->window = kInf;
     for (int r = 0; r < world; r++) {
-        if (all[3 * r + 1] != (unsigned long long)H || all[3 * r + 2] != e->P.end_time) { x_free(g); return SHD_EINVAL; }
-        g->window = std::min<uint64_t>(g->window, all[3 * r]);
+        if (all[4 * r + 1] != (unsigned long long)H || all[4 * r + 2] != e->P.end_time ||
+            all[4 * r + 3] != (unsigned long long)e->P.hpw) {
+            x_free(g);
+            return SHD_EINVAL;
+        }
+        g->window = std::min<uint64_t>(g->window, all[4 * r]);
     }
+    g->fused = p2p && x_direct() && x_fuse_env();
     g->end_time = e->P.end_time;
     g->xcap = block_events ? block_events : x_default_cap(e, world);
     g->fixed_cap = block_events != 0;
@@ -4860,7 +5263,36 @@ extern "C" void shd_xgroup_destroy(shd_xgroup* g) { x_free(g); }
 
 // nb rounds of the engine group: per round, every engine's k_round_x, the
 // all-to-all, every engine's k_ingest_x
+static int x_enqueue_fused(shd_xgroup* g, int nb) {
+    shd_eng* e = g->engs[0];
+    shd_xgroup::Loc& L = g->loc[0];
+    const uint32_t nblk = (uint32_t)((e->nloc + e->P.hpw - 1) / e->P.hpw);
+    for (int i = 0; i < nb; i++) {
+        const int wp = (int)((g->xseq - 1) & 1);   // exchange i - 1 (for round 0: the one before the batch)
+        if (i == 0) {
+            hipLaunchKernelGGL(k_round_xtl, dim3(nblk), dim3(kBlock), 0, e->stream, round_args(e->P),
+                               (const DParams*)(L.d_xpr + 1), (const shd_event*)L.xrecv[wp], L.halt_hdr,
+                               &e->d_ring[2], (const DevCtl*)e->d_ctl, 0, g->window, L.parts);
+        } else {
+            // every peer's header needs its put block, also when the engine has fewer blocks of hosts
+            const uint32_t grid = std::max<uint32_t>(nblk, (uint32_t)g->world);
+            hipLaunchKernelGGL(k_round_px, dim3(grid), dim3(kBlock), 0, e->stream, g->window, i, &e->d_ring[i],
+                               (const DevCtl*)e->d_ctl, L.parts, (const DParams*)(L.d_xpr + i + 1), &e->d_ring[i + 2],
+                               round_args(e->P), (const shd_event*)L.xrecv[wp], x_rgn(g, wp),
+                               (shd_event* const*)g->d_peers, L.halt_hdr, g->d_xerr, g->world, g->rank0, wp);
+        }
+        g->xseq++;   // exchange i: completed by round i + 1's launch, or k_xchg_px below
+    }
+    const int wl = (int)((g->xseq - 1) & 1);
+    const Params P = xparams(g, 0, &e->d_ring[nb]);
+    hipLaunchKernelGGL(k_xchg_px, dim3((unsigned)g->world + nblk), dim3(kBlock), 0, e->stream, dp(P),
+                       (const TlPart*)L.parts, nblk, nb - 1, (const DevCtl*)e->d_ctl, (shd_event* const*)g->d_peers,
+                       g->world, g->rank0, wl, (const shd_event*)L.xrecv[wl], x_rgn(g, wl), g->d_xerr);
+    return SHD_OK;
+}
+
 static int x_enqueue_rounds(shd_xgroup* g, int nb) {
+    if (g->fused) return x_enqueue_fused(g, nb);
     const int nl = (int)g->engs.size();
     int rc = SHD_OK;
     for (int i = 0; i < nb; i++) {
