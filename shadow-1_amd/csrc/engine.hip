@@ -171,6 +171,7 @@ constexpr uint32_t XF_PENDING = 1u, XF_OVERFLOW = 2u, XF_ERROR = 4u;
 // fused peer-to-peer rounds: event slots per (sender, destination block) region
 // and round; one lane of the receiving block reads one slot
 constexpr uint32_t kXSlots = 64;
+constexpr int kXReplMax = 8;   // fused peer-to-peer rounds: copies of a header's granule 0 (x_nrep)
 
 // destination-pick guide: for bucket k, i = the first index with
 // dest_cum[i] >= k / H, and the next three cumulative weights inline, so an
@@ -467,6 +468,11 @@ constexpr uint32_t W_RX = 1u, W_TX = 2u, W_REFILL = 4u, W_SENDING = 8u, W_READ =
 // per-lane LDS of the round kernel (one wave per block; [slot][lane] layouts)
 __shared__ shd_event s_top[kBlock];              // heap root
 __shared__ shd_event s_due[kDueCap * kBlock];    // the window's calendar events, sorted
+// fused peer-to-peer rounds: events received for the window itself, per host
+// (they join the due list after the calendar's; round_body<true>)
+constexpr int kRxCap = 4;
+__shared__ shd_event s_rx[kRxCap * kBlock];
+__shared__ uint32_t s_rxn[kBlock];
 __shared__ CodelEnt s_cqh[kBlock];               // CoDel FIFO head
 __shared__ TxEnt s_tqh[kBlock];                  // send FIFO head
 
@@ -1884,7 +1890,7 @@ __device__ __forceinline__ void due_add(const EvV& x, uint32_t& nw, uint64_t ws,
 // same order (the window's events in them cannot change during the round)
 // and the events past the first kDueCap go to the heap
 __device__ __forceinline__ void due_overflow(const DParams& P, HostCtx& c, uint64_t b0, uint32_t wbits, uint64_t ws,
-                                          uint64_t we) {
+                                          uint64_t we, uint32_t nrx = 0) {
     uint32_t k = 0;
     for (uint32_t j = 0; j < 3; j++) {
         if (((wbits >> j) & 1u) == 0) continue;
@@ -1895,6 +1901,12 @@ __device__ __forceinline__ void due_overflow(const DParams& P, HostCtx& c, uint6
             if (k >= (uint32_t)kDueCap) heap_push(P, c, x);
             k++;
         }
+    }
+    for (uint32_t r = 0; r < nrx; r++) {   // then the received ones, in the order due_add took them
+        const shd_event& x = s_rx[r * kBlock + threadIdx.x];
+        if (x.time < ws || x.time >= we) continue;
+        if (k >= (uint32_t)kDueCap) heap_push(P, c, x);
+        k++;
     }
 }
 
@@ -2001,6 +2013,7 @@ __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
 
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
 // window, run events < we
+template <bool RX = false>   // RX: the fused peer-to-peer round's received window events (s_rx)
 __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, uint64_t ws, uint64_t we, int parity,
                                            uint64_t& next_out, uint64_t& nev_out, uint64_t& npkt_out,
                                            uint32_t& err_out, uint32_t xwi = 0) {
@@ -2047,7 +2060,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
             for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
         }
         if (nbin > 3) err |= SHD_ERR_INTERNAL;   // window wider than W
-        if (nin0 == 0 && t0 >= we && wbits == 0) {
+        if (nin0 == 0 && t0 >= we && wbits == 0 && (!RX || s_rxn[threadIdx.x] == 0)) {
             idle = true;
             next = t0;
             if (P.bins) {
@@ -2138,8 +2151,14 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #pragma unroll
                 for (uint32_t k = 0; k < kBinCap; k++) due_add(bx[j][k], nw, ws, we);
             }
+            uint32_t nrx = 0;
+            if (RX) {
+                nrx = s_rxn[threadIdx.x];
+                nrx = nrx < (uint32_t)kRxCap ? nrx : (uint32_t)kRxCap;
+                for (uint32_t r = 0; r < nrx; r++) due_add(ev_ld(s_rx + r * kBlock + threadIdx.x), nw, ws, we);
+            }
             c.nd = nw < (uint32_t)kDueCap ? nw : (uint32_t)kDueCap;
-            if (nw > (uint32_t)kDueCap) due_overflow(P, c, b0, wbits, ws, we);
+            if (nw > (uint32_t)kDueCap) due_overflow(P, c, b0, wbits, ws, we, nrx);
             // insertion sort of the due list (LDS only)
             for (uint32_t i = 1; i < c.nd; i++) {
                 const EvV x = ev_ld(s_due + i * kBlock + threadIdx.x);
@@ -3271,11 +3290,11 @@ __device__ __forceinline__ uint4 ld16_sys(const void* p) {
 // the events of the regions [p][blk] (p != xme) of one parity -> calendar /
 // inbox[parity] of the block's hosts; s_n / s_w (or null): what each lane's
 // host received, for the lane (inbox count, calendar bins).  Returns error bits.
-__device__ uint32_t xrgn_ingest(const DParams& P, shd_event* __restrict__ rgn, uint32_t blk, uint64_t ws_send,
-                                int parity, uint32_t* s_n, uint32_t (*s_w)[kBlock]) {
+__device__ uint32_t xrgn_ingest_from(const DParams& P, shd_event* __restrict__ rgn, uint32_t blk, uint64_t ws_send,
+                                     int parity, uint32_t* s_n, uint32_t (*s_w)[kBlock], int32_t first) {
     uint32_t err = 0;
     const int32_t W = P.xworld;
-    for (int32_t p0 = 0; p0 < W; p0 += 8) {
+    for (int32_t p0 = first; p0 < W; p0 += 8) {
         uint4 ea[8], eb[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {   // every slot's load out before any is consumed
@@ -3328,6 +3347,109 @@ __device__ uint32_t xrgn_ingest(const DParams& P, shd_event* __restrict__ rgn, u
     }
     return err;
 }
+__device__ __forceinline__ uint32_t xrgn_ingest(const DParams& P, shd_event* __restrict__ rgn, uint32_t blk,
+                                                uint64_t ws_send, int parity, uint32_t* s_n, uint32_t (*s_w)[kBlock]) {
+    return xrgn_ingest_from(P, rgn, blk, ws_send, parity, s_n, s_w, 0);
+}
+
+// the fused round's ingest (its window [ws, we) known, the round to run):
+// peers [0, 8) of the regions only (the rest through xrgn_ingest).  An event
+// of the window joins its host's due list (s_rx); a later one within the
+// horizon claims its calendar slot now and is stored after the round
+// (xrgn_store: the claims' round trip overlaps the round's), parked in
+// s_def[k], its bin noted in s_w for the owner lane's next time; the rest
+// (a full s_rx, beyond the horizon) go to the calendar / inbox at once,
+// noted in s_n / s_w.  dm bit k: slot k's claim is in sl[k].
+__device__ __forceinline__ uint32_t xrgn_take(const DParams& P, shd_event* __restrict__ rgn, uint32_t blk,
+                                              uint64_t ws, uint64_t we, int parity, uint32_t* s_n,
+                                              uint32_t (*s_w)[kBlock], shd_event* s_def, uint32_t (&sl)[8],
+                                              uint32_t& dm) {
+    uint32_t err = 0;
+    const int32_t W = P.xworld;
+    uint4 ea[8], eb[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        ea[k] = make_uint4(0, 0, 0, 0);
+        eb[k] = ea[k];
+        if (k < W && k != P.xme) {
+            const uint4* q = (const uint4*)(rgn + ((size_t)k * P.xnbx + blk) * kXSlots + threadIdx.x);
+            ea[k] = q[0];
+            eb[k] = q[1];
+        }
+    }
+    dm = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if ((ea[k].x | ea[k].y) == 0) continue;
+        shd_event e;
+        {
+            const uint4 ev[2] = {ea[k], eb[k]};
+            __builtin_memcpy(&e, ev, sizeof(e));
+        }
+        *(uint64_t*)(rgn + ((size_t)k * P.xnbx + blk) * kXSlots + threadIdx.x) = 0;   // taken
+        const int32_t dl = (int32_t)e.dst - P.h0;
+        const int32_t j = dl - (int32_t)blk * P.hpw;
+        if (dl < 0 || dl >= P.nloc || j < 0 || j >= P.hpw) {
+            err |= SHD_ERR_REMOTE_OVERFLOW;
+            continue;
+        }
+        const uint64_t bb = e.time >> P.bin_shift;
+        if (e.time < ws) {   // cannot be: the sender's next time counts it
+            err |= SHD_ERR_INTERNAL;
+            continue;
+        }
+        if (e.time < we) {   // the window's
+            const uint32_t r = atomicAdd(&s_rxn[j], 1u);
+            if (r < (uint32_t)kRxCap) {
+                s_rx[r * kBlock + j] = e;
+                continue;
+            }
+        } else if (bb - (ws >> P.bin_shift) <= kHorizon) {
+            const uint32_t pb = (uint32_t)bb & (kNB - 1);
+            sl[k] = atomicAdd(&P.bin_n[(size_t)dl * kNB + pb], 1u);   // consumed after the round
+            s_def[k * kBlock + threadIdx.x] = e;
+            dm |= 1u << k;
+            atomicOr(&s_w[pb >> 5][j], 1u << (pb & 31));
+            continue;
+        }
+        // at once: the inbox of this round (merged at its start)
+        const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+        if (slot >= P.inbox_cap) {
+            err |= SHD_ERR_INBOX_OVERFLOW;
+            continue;
+        }
+        P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+        atomicAdd(&s_n[j], 1u);
+    }
+    return err;
+}
+
+// after the round: the parked events into the slots claimed for them (a full
+// bin: the next round's inbox)
+__device__ __forceinline__ uint32_t xrgn_store(const DParams& P, const shd_event* s_def, const uint32_t (&sl)[8],
+                                               uint32_t dm, int next_parity) {
+    uint32_t err = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        if (!((dm >> k) & 1u)) continue;
+        const shd_event e = s_def[k * kBlock + threadIdx.x];
+        const int32_t dl = (int32_t)e.dst - P.h0;
+        const uint32_t pb = (uint32_t)(e.time >> P.bin_shift) & (kNB - 1);
+        const size_t bi = (size_t)dl * kNB + pb;
+        if (sl[k] < kBinCap) {
+            P.bins[bi * kBinCap + sl[k]] = e;
+            atomicOr(&P.bin_bits[(size_t)dl * kNBW + (pb >> 5)], 1u << (pb & 31));
+            continue;
+        }
+        const uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
+        if (slot >= P.inbox_cap) {
+            err |= SHD_ERR_INBOX_OVERFLOW;
+            continue;
+        }
+        P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
+    }
+    return err;
+}
 
 // block p (< world) of an exchange: fold the round's shares (loaded into pv
 // by the caller; more past 256 blocks), complete its summary (block 0), pack
@@ -3337,7 +3459,7 @@ __device__ __forceinline__ void px_fold_put(const DParams& P, DevSummary* sum, c
                                             const TlPart* __restrict__ pp, uint32_t nblk, uint64_t pws,
                                             uint64_t npend, uint64_t nrem, uint64_t pnext, uint32_t perr,
                                             uint64_t stop, uint32_t halt, shd_event* const* __restrict__ peers,
-                                            int world, int me, int wi, uint32_t tag) {
+                                            int world, int me, int wi, uint32_t tag, uint64_t xhoff, int nrep) {
     const int p = (int)blockIdx.x;
     const size_t stride = (size_t)P.xcap + 1;
     shd_event* src = P.xsend + (size_t)p * stride;
@@ -3383,12 +3505,18 @@ __device__ __forceinline__ void px_fold_put(const DParams& P, DevSummary* sum, c
     } else {
         h = *(const XHeader*)src;
     }
-    if (threadIdx.x == 0) {
+    // granule 0 also into the nrep - 1 replicas (the pollers of the peer's
+    // blocks spread over them: fewer reads of one address per round trip)
+    if ((int)threadIdx.x < nrep) {
         shd_event* dst = peers[p] + ((size_t)wi * world + me) * stride;
         const uint4 g0 = make_uint4((uint32_t)h.next_time, (uint32_t)(h.next_time >> 32), h.flags, tag);
-        const uint4 g1 = make_uint4((uint32_t)h.n_pending, (uint32_t)(h.n_pending >> 32), h.error, h.count);
-        st16_sys((uint4*)dst + 1, g1);
+        if (threadIdx.x == 0) {
+            const uint4 g1 = make_uint4((uint32_t)h.n_pending, (uint32_t)(h.n_pending >> 32), h.error, h.count);
+            st16_sys((uint4*)dst + 1, g1);
+        }
         if (h.flags) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // a flagged header's body before its tag
+        if (threadIdx.x > 0)
+            dst = peers[p] + xhoff + ((size_t)wi * (kXReplMax - 1) + (threadIdx.x - 1)) * world + me;
         st16_sys(dst, g0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -3398,11 +3526,15 @@ __device__ __forceinline__ void px_fold_put(const DParams& P, DevSummary* sum, c
 // 0, bounded: a peer that never comes sets *xerr, and later waits return at
 // once); the min next time and the flags over the group.  Wave-uniform.
 __device__ __forceinline__ bool px_wait(const shd_event* __restrict__ xhdr, size_t stride, int world, uint32_t tag,
-                                        uint32_t bad, uint32_t* __restrict__ xerr, uint64_t& ws, uint32_t& fl) {
+                                        uint32_t bad, uint32_t* __restrict__ xerr, uint64_t& ws, uint32_t& fl,
+                                        const shd_event* __restrict__ xrep, int nrep, uint32_t blk) {
     ws = kInf;
     fl = 0;
     if (!bad && (int)threadIdx.x < world) {
-        const void* hp = xhdr + (size_t)threadIdx.x * stride;
+        // replica blk % nrep of granule 0 (replica 0: the header block itself)
+        const uint32_t r = blk % (uint32_t)nrep;
+        const void* hp = r == 0 ? (const void*)(xhdr + (size_t)threadIdx.x * stride)
+                                : (const void*)(xrep + (size_t)(r - 1) * world + threadIdx.x);
         const unsigned long long t0 = wall_clock64();
         for (;;) {
             const uint4 hx = ld16_sys(hp);
@@ -3441,9 +3573,11 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
                                                       DRoundArgs a, const shd_event* __restrict__ xhdr,
                                                       shd_event* __restrict__ rgn, shd_event* const* __restrict__ peers,
                                                       XHeader* __restrict__ halt_hdr, uint32_t* __restrict__ xerr,
-                                                      int world, int me, int wprev) {
+                                                      int world, int me, int wprev, const shd_event* __restrict__ xrep,
+                                                      uint64_t xhoff, int nrep) {
     __shared__ uint32_t s_xn[kBlock];
     __shared__ uint32_t s_xw[kNBW][kBlock];
+    __shared__ shd_event s_def[8 * kBlock];
     const DParams& P = *Pp;
     const unsigned long long t_entry = wall_clock64();
     const uint32_t nblk = a.nblk;
@@ -3468,26 +3602,41 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
     HostIn in;
     host_in_load(a, in);
     s_xn[threadIdx.x] = 0;
+    s_rxn[threadIdx.x] = 0;
 #pragma unroll
     for (int k = 0; k < (int)kNBW; k++) s_xw[k][threadIdx.x] = 0;
     asm volatile("" : "+v"(halt), "+v"(bad), "+v"(stop), "+v"(rbase), "+v"(xtag), "+v"(xpar), "+v"(pws));
     const uint32_t tag = (uint32_t)(xtag + (uint64_t)(i - 1));
     const size_t stride = (size_t)P.xcap + 1;
     if (putter)
-        px_fold_put(P, prev, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wprev, tag);
+        px_fold_put(P, prev, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wprev, tag,
+                    xhoff, nrep);
     if (blockIdx.x >= nblk) return;   // a put block past the engine's hosts (grid = max(nblk, world))
     uint64_t ws;
     uint32_t fl;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-    if (px_wait(xhdr, stride, world, tag, bad, xerr, ws, fl)) {
+    if (px_wait(xhdr, stride, world, tag, bad, xerr, ws, fl, xrep, nrep, blockIdx.x)) {
         if (threadIdx.x == 0) *P.halt = 1u;
         if (lead) P.sum->flags = 2u;
         return;
     }
     const int parity = (int)((rbase + (uint64_t)i) & 1);
-    __syncthreads();   // s_xn / s_xw zeroed
+    __syncthreads();   // s_xn / s_xw / s_rxn zeroed
     uint32_t ierr = 0;
-    if (!halt) ierr = xrgn_ingest(P, rgn, blockIdx.x, pws, parity, s_xn, s_xw);
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    // a round that runs takes the window's events onto the due lists and
+    // defers the calendar stores of the rest; otherwise all go in at once
+    const bool runs = !halt && !fl && ws < stop && P.bins;
+    uint32_t sl[8], dm = 0;
+    if (runs) {
+        ierr = xrgn_take(P, rgn, blockIdx.x, ws, we, parity, s_xn, s_xw, s_def, sl, dm);
+        if (world > 8) {   // peers past the first eight
+            ierr |= xrgn_ingest_from(P, rgn, blockIdx.x, pws, parity, s_xn, s_xw, 8);
+        }
+    } else if (!halt) {
+        ierr = xrgn_ingest(P, rgn, blockIdx.x, pws, parity, s_xn, s_xw);
+    }
     px_reset_counts(P, wprev, blockIdx.x, nblk);
     __syncthreads();
     if (halt) {
@@ -3522,6 +3671,7 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
     }
     if (ws >= stop) return;   // only forwards the time (the next exchange packs it)
     params_warm_done(warm);
+    // (the window end: computed above)
     {   // what this lane's host received in the exchange
         const uint32_t n = s_xn[threadIdx.x];
         if (parity) in.nin[1] += n;
@@ -3529,11 +3679,10 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
 #pragma unroll
         for (int k = 0; k < (int)kNBW; k++) in.w[k] |= s_xw[k][threadIdx.x];
     }
-    uint64_t we = ws + window;
-    if (we > stop || we < ws) we = stop;
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((xpar + (uint64_t)i) & 1));
+    round_body<true>(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((xpar + (uint64_t)i) & 1));
+    if (dm) ierr |= xrgn_store(P, s_def, sl, dm, parity ^ 1);
     err |= ierr;
     const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));
     for (int off = 32; off > 0; off >>= 1) {
@@ -3554,7 +3703,8 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
 __global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
                                                      const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
                                                      int world, int me, int wi, const shd_event* __restrict__ xhdr,
-                                                     shd_event* __restrict__ rgn, uint32_t* __restrict__ xerr) {
+                                                     shd_event* __restrict__ rgn, uint32_t* __restrict__ xerr,
+                                                     const shd_event* __restrict__ xrep, uint64_t xhoff, int nrep) {
     DevSummary* sum = P.sum;
     uint32_t halt = *P.halt, bad = *xerr;
     uint64_t stop = ctl->stop, rbase = ctl->round_base, xtag = ctl->xtag, pws = sum->ws;
@@ -3565,13 +3715,14 @@ __global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __r
         tl_issue(pp, nblk, 0, pv);
         const uint64_t npend = sum->n_pending, nrem = sum->n_remote, pnext = sum->next_time;
         const uint32_t perr = sum->error;
-        px_fold_put(P, sum, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wi, tag);
+        px_fold_put(P, sum, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wi, tag, xhoff,
+                    nrep);
         return;
     }
     const uint32_t blk = blockIdx.x - (uint32_t)world;
     uint64_t ws;
     uint32_t fl;
-    if (px_wait(xhdr, (size_t)P.xcap + 1, world, tag, bad, xerr, ws, fl)) {
+    if (px_wait(xhdr, (size_t)P.xcap + 1, world, tag, bad, xerr, ws, fl, xrep, nrep, blk)) {
         if (threadIdx.x == 0) *P.halt = 1u;
         return;
     }
@@ -4781,6 +4932,23 @@ static shd_event* x_rgn(const shd_xgroup* g, int w) {
     return g->p2p_base + 2 * (size_t)g->world * g->stride + (size_t)w * g->world * g->xnbx * kXSlots;
 }
 
+// header granule replicas (fused schedule): [2][kXReplMax - 1][world] 32-B
+// slots after the regions; SHD_X_REPL (1 .. 8, default 8) copies in use
+static int x_nrep() {
+    static const int n = [] {
+        const char* v = getenv("SHD_X_REPL");
+        const int k = v ? atoi(v) : kXReplMax;
+        return k < 1 ? 1 : (k > kXReplMax ? kXReplMax : k);
+    }();
+    return n;
+}
+static uint64_t x_hoff(const shd_xgroup* g) {
+    return 2 * (uint64_t)g->world * g->stride + 2 * (uint64_t)g->world * g->xnbx * kXSlots;
+}
+static const shd_event* x_rep(const shd_xgroup* g, int w) {
+    return g->p2p_base + x_hoff(g) + (size_t)w * (kXReplMax - 1) * g->world;
+}
+
 static bool x_want_protect(const shd_xgroup* g) {
     if (protect_off()) return false;
     if (g->engs[0]->P.complete && !protect_all()) return false;   // nothing is ever logged (want_protect)
@@ -5040,7 +5208,8 @@ static int x_p2p_map(shd_xgroup* g) {
         uint32_t pad[15];
     };
     Share mine{};
-    const size_t bytes = (2 * (size_t)W * g->stride + (g->fused ? 2 * (size_t)W * g->xnbx * kXSlots : 0)) *
+    const size_t bytes = (2 * (size_t)W * g->stride +
+                          (g->fused ? 2 * (size_t)W * g->xnbx * kXSlots + 2 * (size_t)(kXReplMax - 1) * W : 0)) *
                          sizeof(shd_event);
     if (hipExtMallocWithFlags((void**)&g->p2p_base, bytes, hipDeviceMallocUncached) == hipSuccess &&
         hipMemset(g->p2p_base, 0, bytes) == hipSuccess &&   // tag 0: no exchange yet (tags start at 1)
@@ -5279,7 +5448,8 @@ static int x_enqueue_fused(shd_xgroup* g, int nb) {
             hipLaunchKernelGGL(k_round_px, dim3(grid), dim3(kBlock), 0, e->stream, g->window, i, &e->d_ring[i],
                                (const DevCtl*)e->d_ctl, L.parts, (const DParams*)(L.d_xpr + i + 1), &e->d_ring[i + 2],
                                round_args(e->P), (const shd_event*)L.xrecv[wp], x_rgn(g, wp),
-                               (shd_event* const*)g->d_peers, L.halt_hdr, g->d_xerr, g->world, g->rank0, wp);
+                               (shd_event* const*)g->d_peers, L.halt_hdr, g->d_xerr, g->world, g->rank0, wp,
+                               x_rep(g, wp), x_hoff(g), x_nrep());
         }
         g->xseq++;   // exchange i: completed by round i + 1's launch, or k_xchg_px below
     }
@@ -5287,7 +5457,8 @@ static int x_enqueue_fused(shd_xgroup* g, int nb) {
     const Params P = xparams(g, 0, &e->d_ring[nb]);
     hipLaunchKernelGGL(k_xchg_px, dim3((unsigned)g->world + nblk), dim3(kBlock), 0, e->stream, dp(P),
                        (const TlPart*)L.parts, nblk, nb - 1, (const DevCtl*)e->d_ctl, (shd_event* const*)g->d_peers,
-                       g->world, g->rank0, wl, (const shd_event*)L.xrecv[wl], x_rgn(g, wl), g->d_xerr);
+                       g->world, g->rank0, wl, (const shd_event*)L.xrecv[wl], x_rgn(g, wl), g->d_xerr, x_rep(g, wl),
+                       x_hoff(g), x_nrep());
     return SHD_OK;
 }
 
