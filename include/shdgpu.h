@@ -266,8 +266,9 @@ typedef struct shd_model {
     uint32_t trace;                 /* record delivered-packet trace           */
     uint32_t evq_cap;               /* per-host event heap capacity (0=default) */
     uint32_t inbox_cap;             /* per-host per-round inbound capacity     */
-    uint32_t codelq_cap;            /* per-host router queue capacity          */
-    uint32_t txq_cap;               /* per-host interface send queue capacity  */
+    uint32_t codelq_cap;            /* per-host router queue capacity (<= 65535, and
+                                       x (payload + 42) below 2^32; 0 = 64)    */
+    uint32_t txq_cap;               /* per-host interface send queue capacity (<= 65535; 0 = 64) */
     uint32_t queue_flags;           /* SHD_QF_*: 0 = default (calendar + heap) */
     /* Per-host variants (NULL / 0 = the scalar above for every host).  Each PHOLD
      * process reads its own weights file (test_phold.c:341-356, per-process

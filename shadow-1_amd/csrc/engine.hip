@@ -85,23 +85,32 @@ struct SendRec {
 };
 static_assert(sizeof(SendRec) == 40, "send record layout");
 
-// Per-host state record in HBM (local host index).  The round kernel reads
-// and writes it whole, as 10 16-B accesses; it holds every field the host's
-// event handling mutates except the queues' contents and the counters.
-struct alignas(16) HostRec {
+// Per-host state record in HBM (local host index), one 128-B line: the round
+// kernel reads and writes it whole, as 8 16-B accesses; it holds every field
+// the host's event handling mutates except the queues' contents and the
+// counters.  Narrowed where the range allows (HostCtx holds the full widths):
+// a live timer's event ID as its distance back from ev_seq (a timer is armed
+// at most a heartbeat interval's events ago; an empty slot's ID is never
+// read), the token buckets and CoDel's byte count in 32 bits (checked at
+// create: refill + MTU and capacity x packet length below 2^32), the FIFO
+// heads and lengths in 16 bits (capacities <= 65535).
+struct alignas(128) HostRec {
     uint64_t ev_seq;                       // host_getNewEventID counter (host.c:397)
-    uint64_t cq_total, cq_iexp, cq_ndrop;  // CoDel: bytes queued, interval expiry, next drop
-    uint64_t rx_rem, tx_rem;               // token buckets: bytes remaining
-    uint64_t tt[3], ts[3];                 // timer slots (heartbeat, refill, notify): time, event ID
+    uint64_t cq_iexp, cq_ndrop;            // CoDel: interval expiry, next drop
+    uint64_t tt[3];                        // timer slots (heartbeat, refill, notify): time (kInf: empty)
+    uint32_t ts_back[3];                   // ... their event IDs: ev_seq - ID (0 for an empty slot)
+    uint32_t rx_rem, tx_rem;               // token buckets: bytes remaining
+    uint32_t cq_total;                     // CoDel: bytes queued
     uint32_t rng, pkt_seq;                 // rand_r state, packet counter
     uint32_t rx_refill, tx_refill;         // token-bucket refill per 1 ms (bytes)
     uint32_t flags, unread;
-    uint32_t cq_dc, cq_dcl, cq_head, cq_count;   // CoDel drop counts, FIFO head / length
-    uint32_t tq_head, tq_count, evq_n;
+    uint32_t cq_dc, cq_dcl;                // CoDel drop counts
+    uint16_t cq_head, cq_count, tq_head, tq_count;   // FIFO heads / lengths
+    uint32_t evq_n;
     uint32_t if_in, if_out;                // tracker node counters: interface packets in / out (cumulative)
     uint32_t pad;
 };
-static_assert(sizeof(HostRec) == 160, "host record: 10 x 16 B");
+static_assert(sizeof(HostRec) == 128, "host record: one 128-B line, 8 x 16 B");
 
 // per-host counters; a round adds its deltas with fire-and-forget atomics
 struct HostCnt {
@@ -1579,7 +1588,8 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
         c.top_time = kInf;
     }
     c.tt0 = launder(r.tt[0]); c.tt1 = launder(r.tt[1]); c.tt2 = launder(r.tt[2]);
-    c.ts0 = launder(r.ts[0]); c.ts1 = launder(r.ts[1]); c.ts2 = launder(r.ts[2]);
+    c.ts0 = c.ev_seq - launder(r.ts_back[0]); c.ts1 = c.ev_seq - launder(r.ts_back[1]);
+    c.ts2 = c.ev_seq - launder(r.ts_back[2]);
     c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.cq_hv = false; c.tq_hv = false;
     c.att = launder(att);
@@ -1717,14 +1727,17 @@ __device__ __forceinline__ uint64_t cal_lower_bound(const DParams& P, const uint
 __device__ void store_ctx(const DParams& P, const HostCtx& c) {
     const int32_t l = c.l;
     HostRec r;
-    r.ev_seq = c.ev_seq; r.cq_total = c.cq_total; r.cq_iexp = c.cq_iexp; r.cq_ndrop = c.cq_ndrop;
-    r.rx_rem = c.rx_rem; r.tx_rem = c.tx_rem;
+    r.ev_seq = c.ev_seq; r.cq_total = (uint32_t)c.cq_total; r.cq_iexp = c.cq_iexp; r.cq_ndrop = c.cq_ndrop;
+    r.rx_rem = (uint32_t)c.rx_rem; r.tx_rem = (uint32_t)c.tx_rem;
     r.tt[0] = c.tt0; r.tt[1] = c.tt1; r.tt[2] = c.tt2;
-    r.ts[0] = c.ts0; r.ts[1] = c.ts1; r.ts[2] = c.ts2;
+    r.ts_back[0] = c.tt0 != kInf ? (uint32_t)(c.ev_seq - c.ts0) : 0u;
+    r.ts_back[1] = c.tt1 != kInf ? (uint32_t)(c.ev_seq - c.ts1) : 0u;
+    r.ts_back[2] = c.tt2 != kInf ? (uint32_t)(c.ev_seq - c.ts2) : 0u;
     r.rng = c.rng; r.pkt_seq = c.pkt_seq; r.rx_refill = c.rx_refill; r.tx_refill = c.tx_refill;
     r.flags = c.flags; r.unread = c.unread;
-    r.cq_dc = c.cq_dc; r.cq_dcl = c.cq_dcl; r.cq_head = c.cq_head; r.cq_count = c.cq_count;
-    r.tq_head = c.tq_head; r.tq_count = c.tq_count; r.evq_n = c.evq_n;
+    r.cq_dc = c.cq_dc; r.cq_dcl = c.cq_dcl;
+    r.cq_head = (uint16_t)c.cq_head; r.cq_count = (uint16_t)c.cq_count;
+    r.tq_head = (uint16_t)c.tq_head; r.tq_count = (uint16_t)c.tq_count; r.evq_n = c.evq_n;
     r.if_in = c.if_in; r.if_out = c.if_out; r.pad = 0;
     P.hs[l] = r;
     if (c.cq_hv) P.cq[(size_t)l * c.k.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
@@ -1850,10 +1863,11 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         const uint32_t h = (uint32_t)(P.h0 + l);
         // _networkinterface_setupTokenBuckets (network_interface.c:192-226)
         const uint64_t rxr = bw_down[h] * 1024 / 1000, txr = bw_up[h] * 1024 / 1000;
-        if ((rxr | txr) >> 32) err |= SHD_ERR_INTERNAL;   // > 4 GB per ms: outside the record's range
+        // bucket capacity refill + MTU within the record's 32 bits
+        if (((rxr + SHD_MTU) | (txr + SHD_MTU)) >> 32) err |= SHD_ERR_INTERNAL;
         HostRec r;
         r.ev_seq = 0; r.cq_total = 0; r.cq_iexp = 0; r.cq_ndrop = 0; r.rx_rem = 0; r.tx_rem = 0;
-        for (int k = 0; k < 3; k++) { r.tt[k] = kInf; r.ts[k] = 0; }
+        for (int k = 0; k < 3; k++) { r.tt[k] = kInf; r.ts_back[k] = 0; }
         P.hc[l] = HostCnt{0, 0, 0, 0, 0, 0};
         r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
         r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
@@ -3923,6 +3937,12 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.inbox_cap = m->inbox_cap ? m->inbox_cap : std::max<uint32_t>(64, 4 * m->load + 32);
     P.cq_cap = m->codelq_cap ? m->codelq_cap : 64;
     P.tq_cap = m->txq_cap ? m->txq_cap : 64;
+    // the host record keeps FIFO positions in 16 bits and CoDel's queued bytes in 32
+    if (P.cq_cap > 65535 || P.tq_cap > 65535 ||
+        (uint64_t)P.cq_cap * ((uint64_t)m->payload + SHD_HEADER_UDP) >> 32) {
+        shd_eng_destroy(e);
+        return SHD_EINVAL;
+    }
     P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
     P.app_start = m->app_start; P.load = m->load; P.payload = m->payload;
     P.pkt_len = m->payload + SHD_HEADER_UDP;
