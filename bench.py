@@ -193,7 +193,29 @@ def main():
 
     # warmup
     tw = time.perf_counter()
-    wst = run(args.warmup * step)
+    failed = None
+    try:
+        wst = run(args.warmup * step)
+    except S.ShdError as ex:
+        if not (use_group and getattr(grp, "p2p", False)):
+            raise
+        failed = ex
+    if use_group and getattr(grp, "p2p", False):
+        # a peer-to-peer exchange that never completes (its waits end after
+        # 30 s with ENODEV) fails the warm-up on every rank; then all of them
+        # rebuild the engine and run over the RCCL all-to-all instead
+        bad = torch.tensor([1.0 if failed is not None else 0.0], device="cuda")
+        if world > 1:
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item() > 0:
+            log(rank, f"peer-to-peer warm-up failed ({failed or 'on another rank'}); RCCL all-to-all instead")
+            grp.close()
+            eng.close()
+            eng = Engine(model, pc, pb[rank], pb[rank + 1], device=dev)
+            grp = XGroup.over(eng, comm)
+            exchange = "shd_xgroup/RCCL all-to-all (peer-to-peer warm-up failed)"
+            run = lambda t: grp.run_until(t)  # noqa: E731
+            wst = run(args.warmup * step)
     torch.cuda.synchronize()
     log(rank, f"warmup {time.perf_counter() - tw:.1f}s")
 
