@@ -72,7 +72,8 @@ constexpr int kChunk = 32;   // edges folded per pass of the forward chain walk
 template <int BLOCK>
 __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
-                             const double* __restrict__ arc_w, const int32_t* __restrict__ rin_off,
+                             const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src,
+                             const int32_t* __restrict__ arc_rin, const int32_t* __restrict__ rin_off,
                              const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
                              const double* __restrict__ rin_w, const double* __restrict__ w_e,
                              const double* __restrict__ eloss, const double* __restrict__ vloss,
@@ -145,39 +146,57 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     __syncthreads();
     return;
 #endif
-    // ---- parent per vertex: smallest d[u] among exact predecessors; equal d[u]
-    // (a tie Dijkstra breaks by heap order, unpinned) -> lowest edge id
-    // Lane per vertex (a half-wave-per-vertex version with shuffle reductions
-    // measured slower: 20 ms against 12.5 ms for the 10k-row table, since each
-    // wave then waits on two dependent L2 round trips per vertex pair).  Arcs
-    // in order, so the (d[u], eid) rule sees them as before.
+    // ---- parent per vertex: smallest d[u] among exact predecessors (d[u] + w
+    // == d[v]; every such u is final: a later decrease of d[u] would undercut
+    // d[v]), equal d[u] (a tie Dijkstra breaks by heap order, unpinned) ->
+    // lowest edge id.  One streaming pass over the forward arcs in CSR order
+    // (coalesced: lane per arc, four arcs per lane in flight) counts each
+    // vertex's exact predecessors and records one; the few vertices with more
+    // than one (ties, equal-cost paths) take the exact rule over their in-arcs.
+    // (Round 1 scanned every vertex's in-arcs, lane per vertex: uncoalesced,
+    // 9.7 of the 29 ms of the 10 k-row table.)
     int64_t my_ties = 0;
-    for (int32_t v = tid; v < V; v += BLOCK) {
-        if (v == src) continue;
-        const uint64_t dvb = dist[v];
-        if (dvb == kDistInf) continue;
-        const double dv = u2d(dvb);
-        int32_t best = -1;
-        uint64_t bestd = kDistInf;
-        int nbest = 0;
-        // arcs in groups of 8: the group's (u, w) loads are issued together
-        const int32_t kb = rin_off[v], ke = rin_off[v + 1];
-        for (int32_t k0 = kb; k0 < ke; k0 += 8) {
-            int32_t uu[8];
-            double ww[8];
+    {
+        uint32_t* cnt2 = (uint32_t*)upd;   // two 16-bit counts per word (the BF stamps are done with)
+        for (int32_t w = tid; w < (V + 1) / 2; w += BLOCK) cnt2[w] = 0;
+        __syncthreads();
+        const int32_t na = arc_off[V];
+        for (int32_t k0 = tid; k0 < na; k0 += 4 * BLOCK) {
+            int32_t uu[4], xx[4];
+            double ww[4];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int32_t k = min(k0 + j, ke - 1);
-                uu[j] = rin_src[k];
-                ww[j] = rin_w[k];
+            for (int j = 0; j < 4; j++) {   // the four arcs' loads go out together
+                const int32_t k = min(k0 + j * BLOCK, na - 1);
+                uu[j] = arc_src[k];
+                xx[j] = arc_dst[k];
+                ww[j] = arc_w[k];
             }
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int32_t k = k0 + j;
-                if (k >= ke) break;
+            for (int j = 0; j < 4; j++) {
+                const int32_t k = k0 + j * BLOCK;
+                if (k >= na) break;
+                const int32_t x = xx[j];
+                if (x == src) continue;
                 const uint64_t dub = dist[uu[j]];
                 if (dub == kDistInf) continue;
-                if (u2d(dub) + ww[j] == dv) {
+                if (u2d(dub) + ww[j] == u2d(dist[x])) {
+                    atomicAdd(&cnt2[x >> 1], 1u << ((x & 1) * 16));
+                    parent[x] = arc_rin[k];
+                }
+            }
+        }
+        __syncthreads();
+        for (int32_t v = tid; v < V; v += BLOCK) {
+            if (upd[v] <= 1) continue;
+            const double dv = u2d(dist[v]);
+            int32_t best = -1;
+            uint64_t bestd = kDistInf;
+            int nbest = 0;
+            const int32_t kb = rin_off[v], ke = rin_off[v + 1];
+            for (int32_t k = kb; k < ke; k++) {
+                const uint64_t dub = dist[rin_src[k]];
+                if (dub == kDistInf) continue;
+                if (u2d(dub) + rin_w[k] == dv) {
                     if (best < 0 || dub < bestd) { best = k; bestd = dub; nbest = 1; }
                     else if (dub == bestd) {
                         nbest++;
@@ -185,9 +204,9 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                     }
                 }
             }
+            parent[v] = best;
+            if (nbest > 1) my_ties++;
         }
-        parent[v] = best;
-        if (nbest > 1) my_ties++;
     }
     if (my_ties) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)my_ties);
     if (tid == 0) atomicMax((unsigned long long*)&stats[2], (unsigned long long)it);
@@ -311,7 +330,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     int32_t V, int32_t T, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
-    const double* __restrict__ arc_w, const int32_t* __restrict__ rin_off,
+    const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src, const int32_t* __restrict__ arc_rin,
+    const int32_t* __restrict__ rin_off,
     const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
     const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
@@ -323,7 +343,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     uint16_t* upd = (uint16_t*)(smem + (size_t)12 * V);
     int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
     for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
-        sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
+        sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
+                            rin_eid,
                             rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
 }
@@ -331,7 +352,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     int32_t V, int32_t T, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
-    const double* __restrict__ arc_w, const int32_t* __restrict__ rin_off,
+    const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src, const int32_t* __restrict__ arc_rin,
+    const int32_t* __restrict__ rin_off,
     const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
     const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
@@ -343,7 +365,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     int32_t* parent = (int32_t*)(base + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(base + (size_t)12 * V);
     for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
-        sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, rin_off, rin_src, rin_eid,
+        sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
+                            rin_eid,
                             rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
 }
@@ -436,7 +459,8 @@ static int dalloc_copy(T** d, const T* h, size_t n) {
 }
 
 static void pc_free_device(shd_pc* pc) {
-    void* ptrs[] = {pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
+    void* ptrs[] = {pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off,
+                    pc->d_rin_src, pc->d_rin_eid,
                     pc->d_rin_w, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
                     pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                     pc->d_dir, pc->d_self, pc->d_adj,
@@ -495,10 +519,25 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
     }
     const shd_csr& c = pc->csr;
     const int32_t na = c.arc_off[V];
+    // per forward arc: its tail vertex and the index of the same arc among its
+    // head's in-arcs (the parent pass streams the forward arcs, the tree walks
+    // use the in-arc indices)
+    std::vector<int32_t> arc_src((size_t)na + 1), arc_rin((size_t)na + 1);
+    for (int32_t u = 0; u < V; u++)
+        for (int32_t k = c.arc_off[u]; k < c.arc_off[u + 1]; k++) {
+            arc_src[k] = u;
+            const int32_t x = c.arc_dst[k];
+            int32_t a = -1;
+            for (int32_t j = c.rin_off[x]; j < c.rin_off[x + 1]; j++)
+                if (c.rin_src[j] == u && c.rin_eid[j] == c.arc_eid[k]) { a = j; break; }
+            if (a < 0) { shd_pc_destroy(pc); return SHD_EINVAL; }   // the two CSRs disagree
+            arc_rin[k] = a;
+        }
     if ((rc = dalloc_copy(&pc->d_arc_off, c.arc_off, V + 1)) || (rc = dalloc_copy(&pc->d_arc_dst, c.arc_dst, na)) ||
         (rc = dalloc_copy(&pc->d_arc_w, c.arc_w, na)) || (rc = dalloc_copy(&pc->d_rin_off, c.rin_off, V + 1)) ||
         (rc = dalloc_copy(&pc->d_rin_src, c.rin_src, na)) || (rc = dalloc_copy(&pc->d_rin_eid, c.rin_eid, na)) ||
         (rc = dalloc_copy(&pc->d_rin_w, c.rin_w, na)) || (rc = dalloc_copy(&pc->d_inc_off, c.inc_off, V + 1)) ||
+        (rc = dalloc_copy(&pc->d_arc_src, arc_src.data(), na)) || (rc = dalloc_copy(&pc->d_arc_rin, arc_rin.data(), na)) ||
         (rc = dalloc_copy(&pc->d_inc_eid, c.inc_eid, c.inc_off[V])) ||
         (rc = dalloc_copy(&pc->d_nbr_off, c.nbr_off, V + 1)) || (rc = dalloc_copy(&pc->d_nbr_v, c.nbr_v, c.nbr_off[V])) ||
         (rc = dalloc_copy(&pc->d_nbr_eid, c.nbr_eid, c.nbr_off[V])) || (rc = dalloc_copy(&pc->d_w, pc->h_w, E)) ||
@@ -581,7 +620,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<256>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
-                                   pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
+                                   pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1);
             } else {
@@ -589,7 +628,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<1024>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_sssp_rows_lds<1024>, dim3(grid), dim3(1024), lds, s, V, T, pc->d_arc_off,
-                                   pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
+                                   pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1);
             }
@@ -602,7 +641,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                 SHD_HIP(hipMalloc(&pc->d_scratch, pc->scratch_bytes));
             }
             hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
-                               pc->d_arc_dst, pc->d_arc_w, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
+                               pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
                                pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                                pc->d_stats, (char*)pc->d_scratch, per_block, row0, row1);
         }

@@ -47,6 +47,8 @@ struct shd_pc {
     double* d_arc_w = nullptr;
     int32_t *d_rin_off = nullptr, *d_rin_src = nullptr, *d_rin_eid = nullptr;
     double* d_rin_w = nullptr;
+    int32_t* d_arc_src = nullptr;   // forward arc -> tail vertex
+    int32_t* d_arc_rin = nullptr;   // forward arc -> its index among the head's in-arcs
     int32_t *d_inc_off = nullptr, *d_inc_eid = nullptr;
     int32_t *d_nbr_off = nullptr, *d_nbr_v = nullptr, *d_nbr_eid = nullptr;
     double *d_w = nullptr, *d_eloss = nullptr, *d_vloss = nullptr;
