@@ -75,7 +75,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src,
                              const int32_t* __restrict__ arc_rin, const int32_t* __restrict__ rin_off,
                              const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
-                             const double* __restrict__ rin_w, const double* __restrict__ w_e,
+                             const double* __restrict__ rin_w, const double* __restrict__ rin_r,
+                             const double* __restrict__ w_e,
                              const double* __restrict__ eloss, const double* __restrict__ vloss,
                              const int32_t* __restrict__ attached, const int32_t* __restrict__ self_eid,
                              shd_pv* __restrict__ out,
@@ -274,51 +275,94 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         } else {
             lat = u2d(dist[t]);
             if (lat == 0) lat = 1;
-            out[(size_t)row * T + j].lat = lat;
+            // the whole pair (rel filled in by (4)): a wave's stores then cover
+            // whole lines, where 8-B stores at a 16-B stride leave every line
+            // (and ECC word) half written, for a read-modify-write in memory
+            out[(size_t)row * T + j] = shd_pv{lat, 0.0};
             continue;
         }
         out[(size_t)row * T + j] = shd_pv{lat, rel};
     }
     __syncthreads();
+#if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 4   // phase ablation: targets' first pass only
+    return;
+#endif
     // (2) tree arrays: parent[v] <- parent vertex, dist[v] <- edge factor r(e)
+    // (rin_r: the in-arc's 1 - loss, precomputed), four vertices per thread
+    // with their loads out together
     constexpr uint16_t kTodo = 0xFFFF, kNever = 0xFFFE;
-    for (int32_t v = tid; v < V; v += BLOCK) {
-        if (v == src) {
-            dist[v] = d2u(has_rsrc ? 1.0 * rsrc : 1.0);
-            upd[v] = 0;
-        } else if (dist[v] != kDistInf && parent[v] >= 0) {
-            const int32_t a = parent[v];
-            parent[v] = rin_src[a];
-            dist[v] = d2u((double)1.0f - eloss[rin_eid[a]]);
-            upd[v] = kTodo;
-        } else {
-            upd[v] = kNever;
+    for (int32_t v0 = tid; v0 < V; v0 += 4 * BLOCK) {
+        int32_t pa[4], pu[4];
+        double pr[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int32_t v = v0 + j * BLOCK;
+            pa[j] = (v < V && v != src && dist[v] != kDistInf) ? parent[v] : -1;
+            pu[j] = pa[j] >= 0 ? rin_src[pa[j]] : -1;
+            pr[j] = pa[j] >= 0 ? rin_r[pa[j]] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int32_t v = v0 + j * BLOCK;
+            if (v >= V) break;
+            if (v == src) {
+                dist[v] = d2u(has_rsrc ? 1.0 * rsrc : 1.0);
+                upd[v] = 0;
+            } else if (pa[j] >= 0) {
+                parent[v] = pu[j];
+                dist[v] = d2u(pr[j]);
+                upd[v] = kTodo;
+            } else {
+                upd[v] = kNever;
+            }
         }
     }
     __syncthreads();
-    // (3) level passes: a vertex whose parent finished in an earlier level
-    // finishes now (reads of this level's writes see kTodo or lvl: no race)
-    for (int lvl = 1; lvl < (int)kNever; lvl++) {
-        if (tid == 0) flags[lvl % 3] = 0;
-        __syncthreads();
-        for (int32_t v = tid; v < V; v += BLOCK) {
-            if (upd[v] != kTodo) continue;
-            const int32_t u = parent[v];
-            if (upd[u] >= (uint16_t)lvl) continue;
-            dist[v] = d2u(u2d(dist[u]) * u2d(dist[v]));
-            upd[v] = (uint16_t)lvl;
-            flags[lvl % 3] = 1;
+#if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 3   // phase ablation: no level passes
+    return;
+#endif
+    // (3) the tree prefix, without a barrier per level: every thread sweeps
+    // its own vertices until each is done; a vertex finishes once its parent
+    // has (P[v] = P[u] * r(e), the order of the reference's forward fold),
+    // taking the parent's depth + 1 (the level the per-level passes of round 1
+    // gave it).  Its product is written before its depth (a workgroup release
+    // between them), and readers read the depth first, through volatile LDS
+    // accesses, so a done parent's product is its final one.  A chain of L
+    // hops needs at most L sweeps of its vertices' threads; threads never
+    // wait on each other, so some vertex finishes in every round of sweeps.
+    {
+        volatile uint16_t* vupd = upd;
+        volatile uint64_t* vdist = dist;
+        bool left = true;
+        for (int32_t sweep = 0; left; sweep++) {
+            left = false;
+            for (int32_t v = tid; v < V; v += BLOCK) {
+                if (vupd[v] != kTodo) continue;
+                const int32_t u = parent[v];
+                const uint16_t du = vupd[u];
+                if (du >= kNever) {   // the parent is not done yet
+                    left = true;
+                    continue;
+                }
+                vdist[v] = d2u(u2d(vdist[u]) * u2d(vdist[v]));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                vupd[v] = (uint16_t)(du + 1);
+            }
+            if (sweep > V) {   // cannot be: a parent chain longer than the graph
+                atomicAdd((unsigned long long*)&stats[4], 1ull);
+                break;
+            }
         }
-        __syncthreads();
-        if (!flags[lvl % 3]) break;
     }
+    __syncthreads();
     // (4) rel half of the prefix targets
     for (int32_t j = tid; j < T; j += BLOCK) {
         const int32_t t = attached[j];
         if (t == src || upd[t] >= kNever) continue;
         double rt;
         if (vrel(vloss, t, &rt)) continue;
-        out[(size_t)row * T + j].rel = u2d(dist[t]);
+        shd_pv* o = &out[(size_t)row * T + j];
+        *o = shd_pv{o->lat, u2d(dist[t])};   // the pair whole again (see (1))
         if ((int32_t)upd[t] > my_maxhops) my_maxhops = upd[t];
     }
     if (my_maxhops) atomicMax((unsigned long long*)&stats[1], (unsigned long long)my_maxhops);
@@ -333,7 +377,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src, const int32_t* __restrict__ arc_rin,
     const int32_t* __restrict__ rin_off,
     const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
-    const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
+    const double* __restrict__ rin_w, const double* __restrict__ rin_r, const double* __restrict__ w_e,
+    const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, int32_t row0, int32_t row1) {
@@ -345,7 +390,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
-                            rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
+                            rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
 }
 
@@ -355,7 +400,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src, const int32_t* __restrict__ arc_rin,
     const int32_t* __restrict__ rin_off,
     const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
-    const double* __restrict__ rin_w, const double* __restrict__ w_e, const double* __restrict__ eloss,
+    const double* __restrict__ rin_w, const double* __restrict__ rin_r, const double* __restrict__ w_e,
+    const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block, int32_t row0, int32_t row1) {
@@ -367,7 +413,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
-                            rin_w, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
+                            rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags);
 }
 
@@ -461,7 +507,7 @@ static int dalloc_copy(T** d, const T* h, size_t n) {
 static void pc_free_device(shd_pc* pc) {
     void* ptrs[] = {pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off,
                     pc->d_rin_src, pc->d_rin_eid,
-                    pc->d_rin_w, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
+                    pc->d_rin_w, pc->d_rin_r, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
                     pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                     pc->d_dir, pc->d_self, pc->d_adj,
                     pc->d_scratch, pc->d_stats};
@@ -533,11 +579,15 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
             if (a < 0) { shd_pc_destroy(pc); return SHD_EINVAL; }   // the two CSRs disagree
             arc_rin[k] = a;
         }
+    // per in-arc: the edge's reliability factor 1 - loss ((double)1.0f - loss, topology.c:437)
+    std::vector<double> rin_r((size_t)na + 1);
+    for (int32_t a = 0; a < na; a++) rin_r[a] = (double)1.0f - g->edge_loss[c.rin_eid[a]];
     if ((rc = dalloc_copy(&pc->d_arc_off, c.arc_off, V + 1)) || (rc = dalloc_copy(&pc->d_arc_dst, c.arc_dst, na)) ||
         (rc = dalloc_copy(&pc->d_arc_w, c.arc_w, na)) || (rc = dalloc_copy(&pc->d_rin_off, c.rin_off, V + 1)) ||
         (rc = dalloc_copy(&pc->d_rin_src, c.rin_src, na)) || (rc = dalloc_copy(&pc->d_rin_eid, c.rin_eid, na)) ||
         (rc = dalloc_copy(&pc->d_rin_w, c.rin_w, na)) || (rc = dalloc_copy(&pc->d_inc_off, c.inc_off, V + 1)) ||
         (rc = dalloc_copy(&pc->d_arc_src, arc_src.data(), na)) || (rc = dalloc_copy(&pc->d_arc_rin, arc_rin.data(), na)) ||
+        (rc = dalloc_copy(&pc->d_rin_r, rin_r.data(), na)) ||
         (rc = dalloc_copy(&pc->d_inc_eid, c.inc_eid, c.inc_off[V])) ||
         (rc = dalloc_copy(&pc->d_nbr_off, c.nbr_off, V + 1)) || (rc = dalloc_copy(&pc->d_nbr_v, c.nbr_v, c.nbr_off[V])) ||
         (rc = dalloc_copy(&pc->d_nbr_eid, c.nbr_eid, c.nbr_off[V])) || (rc = dalloc_copy(&pc->d_w, pc->h_w, E)) ||
@@ -621,7 +671,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
-                                   pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
+                                   pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
+                                   pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1);
             } else {
                 int grid = std::max(1, std::min(row1 - row0, ncu));
@@ -629,7 +680,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
                 hipLaunchKernelGGL(k_sssp_rows_lds<1024>, dim3(grid), dim3(1024), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
-                                   pc->d_rin_w, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
+                                   pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
+                                   pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1);
             }
         } else {
@@ -642,7 +694,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
             }
             hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
-                               pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
+                               pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                                pc->d_stats, (char*)pc->d_scratch, per_block, row0, row1);
         }
         SHD_HIP(hipGetLastError());

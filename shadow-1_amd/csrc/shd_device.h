@@ -49,6 +49,7 @@ struct shd_pc {
     double* d_rin_w = nullptr;
     int32_t* d_arc_src = nullptr;   // forward arc -> tail vertex
     int32_t* d_arc_rin = nullptr;   // forward arc -> its index among the head's in-arcs
+    double* d_rin_r = nullptr;      // in-arc -> its edge's 1 - loss
     int32_t *d_inc_off = nullptr, *d_inc_eid = nullptr;
     int32_t *d_nbr_off = nullptr, *d_nbr_v = nullptr, *d_nbr_eid = nullptr;
     double *d_w = nullptr, *d_eloss = nullptr, *d_vloss = nullptr;
