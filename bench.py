@@ -54,9 +54,12 @@ def parse():
     ap.add_argument("--lossy-edge-loss-max", type=float, default=0.0005,
                     help="edge loss ~ U[0, x] of the lossy C3 run reported beside the headline "
                          "(its packet events per step show the decay); 0 skips it")
-    ap.add_argument("--workload", choices=["c3", "c4"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
                     help="c3: PHOLD-UDP on the geometric topology (the headline, weak scaling); c4: the "
-                         "Tor-scale relay/client model on the bundled topology (hosts fixed, strong scaling)")
+                         "Tor-scale relay/client model on the bundled topology (hosts fixed, strong scaling); "
+                         "c5: 1 M hosts (100 per vertex of the geometric topology), 1500-B messages, 512 KiB/s "
+                         "downlinks so CoDel queues build, edge loss U[0, 0.01] (hosts fixed, strong scaling; "
+                         "lost messages are not regenerated, so the rate depends on the window)")
     ap.add_argument("--relays", type=int, default=6500)
     ap.add_argument("--clients", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -87,7 +90,7 @@ os.dup2(2, 1)
 def main():
     args = parse()
     if args.load is None:
-        args.load = 4 if args.workload == "c4" else 16
+        args.load = {"c4": 4, "c5": 32}.get(args.workload, 16)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -117,6 +120,15 @@ def main():
                                payload=args.payload)
         host_vertex = model.host_vertex
         V, H = g.n_vertices, model.n_hosts
+    elif args.workload == "c5":
+        # BASELINE C5 exactly as tests/fullsize_configs.py builds its fixture, the
+        # 1 M hosts split over the ranks (the total is fixed)
+        V, hpv = args.vertices, 100
+        g = W.geometric_graph(V, seed=args.seed, loss_max=0.01)
+        host_vertex = W.hosts_on_vertices(V, hpv)
+        H = len(host_vertex)
+        model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load, payload=1500,
+                              bw_down=512, bw_up=10240, codelq_cap=256)
     else:
         V = args.vertices
         H = args.hosts_per_gpu * max(world, 1)
@@ -292,7 +304,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "strong" if args.workload == "c4" else "weak",
+            "scaling": "strong" if args.workload in ("c4", "c5") else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (bundled topology, Tor-scale relay/client PHOLD-UDP traffic, seed %d)"
@@ -301,11 +313,15 @@ def main():
             "config": {"workload": ("C4 Tor-scale (%d relays + %d clients, bundled %d-vertex topology; edge loss "
                                     "0.005: the population decays, the rate depends on the window)"
                                     % (args.relays, args.clients, V)) if args.workload == "c4" else
+                                   ("C5 1 M hosts (100 per vertex, %d-vertex geometric topology), 1500-B messages, "
+                                    "512 KiB/s downlinks (CoDel queues build), edge loss U[0,0.01]: the population "
+                                    "decays, the rate depends on the window" % V) if args.workload == "c5" else
                                    ("C3 PHOLD-UDP, stationary population (N x %d hosts, %d-vertex geometric topology)"
                                     % (args.hosts_per_gpu, V)),
-                       "edge_loss": "bundled (0.005)" if args.workload == "c4" else "U[0,%g]" % args.edge_loss_max,
+                       "edge_loss": ("bundled (0.005)" if args.workload == "c4" else
+                                     "U[0,0.01]" if args.workload == "c5" else "U[0,%g]" % args.edge_loss_max),
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
-                       "payload_bytes": args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
+                       "payload_bytes": 1500 if args.workload == "c5" else args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
                        "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1),
                        "exchange": (exchange if use_group else
                                     "torch.distributed" if world > 1 else "none (single engine)")},
