@@ -53,7 +53,9 @@ constexpr uint64_t kCodelInterval = 100ull * SHD_MS;   // router_queue_codel.c:4
 // in a slot the owner reads or clears in round r or r+1.
 constexpr uint32_t kNB = 256, kBinCap = 4, kNBW = kNB / 32, kHorizon = kNB - 4;
 constexpr int kDueCap = 8;             // due-list slots per host (more due events take the heap)
-constexpr int kSendCap = 8;            // deferred sends per host between flushes (<= 16)
+constexpr int kSendCap = 6;            // deferred sends per host between flushes (<= 16; with the
+                                       // due list and the flush's arrays, 49 KB of LDS per block:
+                                       // three blocks per CU once hosts fill the machine)
 constexpr int kBlock = 64;             // round-kernel workgroup: one wave, one host per lane
 
 struct CodelEnt {
@@ -3294,6 +3296,7 @@ __global__ __launch_bounds__(256) void k_xchg(DParams P, const TlPart* __restric
 // into that region again two exchanges later, after it saw this engine's
 // next header, which follows the end of this launch).
 static_assert(kXSlots == (uint32_t)kBlock, "one region slot per lane");
+constexpr int kXDefCap = 4;   // received events per lane whose calendar store waits for the round's end
 
 __device__ __forceinline__ uint4 ld16_sys(const void* p) {
     u32x4 x;
@@ -3371,7 +3374,8 @@ __device__ __forceinline__ uint32_t xrgn_ingest(const DParams& P, shd_event* __r
 // of the window joins its host's due list (s_rx); a later one within the
 // horizon claims its calendar slot now and is stored after the round
 // (xrgn_store: the claims' round trip overlaps the round's), parked in
-// s_def[k], its bin noted in s_w for the owner lane's next time; the rest
+// s_def (at most kXDefCap per lane, in arrival order), its bin noted in s_w
+// for the owner lane's next time; the rest
 // (a full s_rx, beyond the horizon) go to the calendar / inbox at once,
 // noted in s_n / s_w.  dm bit k: slot k's claim is in sl[k].
 __device__ __forceinline__ uint32_t xrgn_take(const DParams& P, shd_event* __restrict__ rgn, uint32_t blk,
@@ -3418,10 +3422,10 @@ __device__ __forceinline__ uint32_t xrgn_take(const DParams& P, shd_event* __res
                 s_rx[r * kBlock + j] = e;
                 continue;
             }
-        } else if (bb - (ws >> P.bin_shift) <= kHorizon) {
+        } else if (bb - (ws >> P.bin_shift) <= kHorizon && __popc(dm) < kXDefCap) {
             const uint32_t pb = (uint32_t)bb & (kNB - 1);
             sl[k] = atomicAdd(&P.bin_n[(size_t)dl * kNB + pb], 1u);   // consumed after the round
-            s_def[k * kBlock + threadIdx.x] = e;
+            s_def[__popc(dm) * kBlock + threadIdx.x] = e;                // parked in arrival order
             dm |= 1u << k;
             atomicOr(&s_w[pb >> 5][j], 1u << (pb & 31));
             continue;
@@ -3446,7 +3450,7 @@ __device__ __forceinline__ uint32_t xrgn_store(const DParams& P, const shd_event
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         if (!((dm >> k) & 1u)) continue;
-        const shd_event e = s_def[k * kBlock + threadIdx.x];
+        const shd_event e = s_def[__popc(dm & ((1u << k) - 1u)) * kBlock + threadIdx.x];
         const int32_t dl = (int32_t)e.dst - P.h0;
         const uint32_t pb = (uint32_t)(e.time >> P.bin_shift) & (kNB - 1);
         const size_t bi = (size_t)dl * kNB + pb;
@@ -3591,7 +3595,7 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
                                                       uint64_t xhoff, int nrep) {
     __shared__ uint32_t s_xn[kBlock];
     __shared__ uint32_t s_xw[kNBW][kBlock];
-    __shared__ shd_event s_def[8 * kBlock];
+    __shared__ shd_event s_def[kXDefCap * kBlock];
     const DParams& P = *Pp;
     const unsigned long long t_entry = wall_clock64();
     const uint32_t nblk = a.nblk;
