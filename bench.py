@@ -70,6 +70,10 @@ def parse():
                          "IPC-mapped by every rank and stored into over xGMI, tagged headers, in-kernel waits; "
                          "falls back to rccl if the mapping fails); rccl = shd_xgroup with one fixed-size RCCL "
                          "all-to-all per round; torch = driver.DistCluster (host-driven, torch.distributed)")
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="the engine group's communicator: rccl (one process per GPU), or host (processes of one "
+                         "machine over shared memory, torch.distributed over gloo, every rank on GPU 0): a "
+                         "rehearsal of the N > 1 path on a one-GPU machine, not a measurement")
     ap.add_argument("--group", action="store_true",
                     help="run the shd_xgroup path even at N = 1 (a one-rank RCCL group)")
     ap.add_argument("--quiet", action="store_true")
@@ -97,13 +101,15 @@ def main():
     n_gpus = args.gpus
     import torch
     dist = None
+    rehearsal = args.comm == "host" and world > 1
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(0 if rehearsal else local_rank)
+        dist.init_process_group("gloo" if rehearsal else "nccl")
     else:
         torch.cuda.set_device(0)
-    dev = local_rank if world > 1 else 0
+    dev = local_rank if world > 1 and not rehearsal else 0
+    tdev = "cpu" if rehearsal else "cuda"   # the torch.distributed tensors' device
 
     import shdgpu as S
     import workloads as W
@@ -145,12 +151,16 @@ def main():
         # one communicator per process: the sharded path-cache build and the
         # engine group's per-round exchange both run over it
         from sim import Comm, XGroup
-        uid = torch.zeros(S.SHD_XID_BYTES, dtype=torch.uint8, device="cuda")
+        uid = torch.zeros(S.SHD_XID_BYTES, dtype=torch.uint8, device=tdev)
         if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(XGroup.unique_id()), dtype=torch.uint8))
+            uid.copy_(torch.frombuffer(bytearray(XGroup.unique_id() if not rehearsal else os.urandom(S.SHD_XID_BYTES)),
+                                       dtype=torch.uint8))
         if world > 1:
             dist.broadcast(uid, 0)
-        comm = Comm.rccl(bytes(uid.cpu().numpy().tobytes()), max(world, 1), rank, dev)
+        if rehearsal:   # the shared-memory segment's name from the broadcast token
+            comm = Comm.host("shdbench_" + bytes(uid.cpu().numpy().tobytes())[:8].hex(), world, rank, dev)
+        else:
+            comm = Comm.rccl(bytes(uid.cpu().numpy().tobytes()), max(world, 1), rank, dev)
     # host buffers handed over at the boundary (graph CSR, model tables): their
     # upload is timed apart and reported as the PCIe-inclusive rate, never `value`
     torch.cuda.synchronize()
@@ -216,7 +226,7 @@ def main():
         # a peer-to-peer exchange that never completes (its waits end after
         # 30 s with ENODEV) fails the warm-up on every rank; then all of them
         # rebuild the engine and run over the RCCL all-to-all instead
-        bad = torch.tensor([1.0 if failed is not None else 0.0], device="cuda")
+        bad = torch.tensor([1.0 if failed is not None else 0.0], device=tdev)
         if world > 1:
             dist.all_reduce(bad, op=dist.ReduceOp.MAX)
         if bad.item() > 0:
@@ -250,8 +260,8 @@ def main():
         kms, ems = st.device_ms_round_kernel, st.device_ms_launches
         hr = st.n_host_rounds
     tot = torch.tensor([float(pkt), float(evs), float(kms), float(ems), float(hr)], dtype=torch.float64,
-                       device="cuda")
-    mx = torch.tensor([elapsed, upload_s], dtype=torch.float64, device="cuda")
+                       device=tdev)
+    mx = torch.tensor([elapsed, upload_s], dtype=torch.float64, device=tdev)
     if world > 1:
         dist.all_reduce(tot)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -322,7 +332,10 @@ def main():
                                      "U[0,0.01]" if args.workload == "c5" else "U[0,%g]" % args.edge_loss_max),
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
                        "payload_bytes": 1500 if args.workload == "c5" else args.payload, "sim_seconds_per_step": args.step_ms / 1000.0,
-                       "window_ns": int(eng.window), "parallelism": "hosts sharded over %d GPU" % max(world, 1),
+                       "window_ns": int(eng.window),
+                       "parallelism": ("REHEARSAL (not a measurement): hosts sharded over %d processes sharing "
+                                       "GPU 0, host-memory communicator" % world) if rehearsal else
+                                      "hosts sharded over %d GPU" % max(world, 1),
                        "exchange": (exchange if use_group else
                                     "torch.distributed" if world > 1 else "none (single engine)")},
             "all_events_per_s": round(ev_all / elapsed, 1),
