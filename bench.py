@@ -197,8 +197,12 @@ def main():
         if args.exchange == "p2p":
             try:   # every rank fails alike (the mapping is checked collectively)
                 grp = XGroup.over(eng, comm, p2p=True)
+                # (ranks sharing a GPU are fused only while all their blocks fit its CUs one each)
+                two_launch = os.environ.get("SHD_X_UNFUSED") or (
+                    rehearsal and world * -(-(pb[rank + 1] - pb[rank]) // 64) >
+                    torch.cuda.get_device_properties(dev).multi_processor_count)
                 exchange = ("shd_xgroup/peer-to-peer (IPC-mapped receive blocks, xGMI stores, "
-                            + ("a separate exchange launch per round)" if os.environ.get("SHD_X_UNFUSED") else
+                            + ("a separate exchange launch per round)" if two_launch else
                                "each round's launch completes the previous round's exchange)"))
             except S.ShdError as ex:
                 log(rank, f"peer-to-peer transport unavailable ({ex}); RCCL all-to-all instead")
@@ -285,7 +289,7 @@ def main():
     # the dominant kernel: ticketless device rounds on one engine (k_round_tl,
     # once no first touch is logged), the engine group's k_round_x across GPUs
     # (peer-to-peer rounds after a batch's first are k_round_px, which also completes the exchange)
-    fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and not os.environ.get("SHD_X_UNFUSED")
+    fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and "completes the previous" in exchange
     kname = ("k_round_px" if fused else "k_round_xtl") if use_group else ("k_round" if world > 1 else "k_round_tl")
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname),

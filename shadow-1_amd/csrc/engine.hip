@@ -5399,22 +5399,44 @@ static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p,
     g->p2p = p2p;
     g->engs.push_back(e);
     // the group agrees on W (min) and checks the model: H and end time equal everywhere
-    // (and the hosts per wave: the fused schedule's regions are per block of hpw hosts)
-    const unsigned long long mine[4] = {(unsigned long long)e->window, (unsigned long long)H,
-                                        (unsigned long long)e->P.end_time, (unsigned long long)e->P.hpw};
-    std::vector<unsigned long long> all(4 * (size_t)world);
-    int rc = shd_comm_allgather_host(comm, mine, 32, all.data());
+    // (and the hosts per wave: the fused schedule's regions are per block of hpw hosts;
+    // the device and round-kernel grid: see below)
+    hipDeviceProp_t prop{};
+    int ncu = 256;
+    unsigned long long dev_id = (unsigned long long)e->device;
+    if (hipGetDeviceProperties(&prop, e->device) == hipSuccess) {
+        ncu = prop.multiProcessorCount;
+        dev_id = ((unsigned long long)prop.pciDomainID << 32) | ((unsigned long long)prop.pciBusID << 8) |
+                 (unsigned long long)prop.pciDeviceID;
+    }
+    const unsigned long long nblk = (unsigned long long)((e->nloc + e->P.hpw - 1) / e->P.hpw);
+    const unsigned long long mine[6] = {(unsigned long long)e->window, (unsigned long long)H,
+                                        (unsigned long long)e->P.end_time, (unsigned long long)e->P.hpw,
+                                        dev_id, nblk};
+    std::vector<unsigned long long> all(6 * (size_t)world);
+    int rc = shd_comm_allgather_host(comm, mine, sizeof(mine), all.data());
     if (rc) { x_free(g); return rc; }
     g->window = kInf;
+    unsigned long long shared_blocks = 0;
+    int sharers = 0;
     for (int r = 0; r < world; r++) {
-        if (all[4 * r + 1] != (unsigned long long)H || all[4 * r + 2] != e->P.end_time ||
-            all[4 * r + 3] != (unsigned long long)e->P.hpw) {
+        if (all[6 * r + 1] != (unsigned long long)H || all[6 * r + 2] != e->P.end_time ||
+            all[6 * r + 3] != (unsigned long long)e->P.hpw) {
             x_free(g);
             return SHD_EINVAL;
         }
-        g->window = std::min<uint64_t>(g->window, all[4 * r]);
+        g->window = std::min<uint64_t>(g->window, all[6 * r]);
+        if (all[6 * r + 4] == dev_id) {
+            sharers++;
+            shared_blocks += all[6 * r + 5];
+        }
     }
-    g->fused = p2p && x_direct() && x_fuse_env();
+    // Every block of a fused round waits for the peers' headers, so the peers'
+    // launches must run beside it.  With one rank per GPU they do; ranks that
+    // share a GPU (tests, rehearsals) are fused only while all their blocks fit
+    // the GPU's compute units one each (three ranks of 157 blocks on one GPU
+    // waited out their 30 s: the device did not run the three launches at once)
+    g->fused = p2p && x_direct() && x_fuse_env() && (sharers <= 1 || shared_blocks <= (unsigned long long)ncu);
     g->end_time = e->P.end_time;
     g->xcap = block_events ? block_events : x_default_cap(e, world);
     g->fixed_cap = block_events != 0;
