@@ -52,10 +52,10 @@ constexpr uint64_t kCodelInterval = 100ull * SHD_MS;   // router_queue_codel.c:4
 // horizon stops short of the ring by 4 so that no append in round r can land
 // in a slot the owner reads or clears in round r or r+1.
 constexpr uint32_t kNB = 256, kBinCap = 4, kNBW = kNB / 32, kHorizon = kNB - 4;
-constexpr int kDueCap = 8;             // due-list slots per host (more due events take the heap)
-constexpr int kSendCap = 6;            // deferred sends per host between flushes (<= 16; with the
-                                       // due list and the flush's arrays, 49 KB of LDS per block:
-                                       // three blocks per CU once hosts fill the machine)
+constexpr int kDueCap = 6;             // due-list slots per host (more due events take the heap)
+constexpr int kSendCap = 5;            // deferred sends per host between flushes (<= 16; with the
+                                       // due list and the flush's arrays, 40 KB of LDS per block:
+                                       // four blocks per CU once hosts fill the machine)
 constexpr int kBlock = 64;             // round-kernel workgroup: one wave, one host per lane
 
 struct CodelEnt {
