@@ -1,5 +1,7 @@
 #!/bin/bash
-# A/B of the per-host LDS capacities (default 6/5 against 8/8, libshdgpu_var.so): one-rank fused group and the headline
+# A/B of the per-host LDS capacities (default 6/5 against 8/8, libshdgpu_var.so): one-rank fused group and the headline.
+# (Built while engine.hip read kDueCap / kSendCap from SHD_DUE_CAP / SHD_SEND_CAP: make variant VARIANT_FLAGS="-DSHD_DUE_CAP=8 -DSHD_SEND_CAP=8";
+# the product keeps plain constants.)
 set -o pipefail
 mkdir -p gpurun_out/ab
 G="--group --exchange p2p --steps 4 --warmup 2 --no-cpu-baseline --lossy-edge-loss-max 0"
