@@ -4935,6 +4935,10 @@ struct shd_xgroup {
     uint64_t xepoch = 0;               // exchange tags issued (never rolled back)
     bool fused = false;                // peer-to-peer rounds fused with their exchange (k_round_px)
     uint32_t xnbx = 0;                 // fused: region blocks per rank
+    // one engine per process: the last exchange's headers and the wait-error word,
+    // copied back with the batch's summaries (one stream synchronisation per batch)
+    XHeader* h_hdr = nullptr;          // pinned, [64]
+    uint32_t* h_xerr = nullptr;        // pinned
 };
 
 // peer-to-peer: the round stores its sends straight into the peers' receive
@@ -5074,13 +5078,19 @@ static int x_headers(shd_xgroup* g, std::vector<XHeader>& h) {
     return x_p2p_check(g);
 }
 
+static void x_next_from(shd_xgroup* g, const XHeader* h, int n);
 static int x_read_next(shd_xgroup* g) {
     std::vector<XHeader> h;
     int rc = x_headers(g, h);
     if (rc) return rc;
+    x_next_from(g, h.data(), (int)h.size());
+    return SHD_OK;
+}
+static void x_next_from(shd_xgroup* g, const XHeader* h, int n) {
     uint64_t t = kInf;
     uint32_t fl = 0;
-    for (const XHeader& x : h) {
+    for (int i = 0; i < n; i++) {
+        const XHeader& x = h[i];
         t = std::min<uint64_t>(t, x.next_time);
         fl |= x.flags;
     }
@@ -5088,7 +5098,6 @@ static int x_read_next(shd_xgroup* g) {
     // next batch's first round; its headers' times leave out what the
     // recovery delivers, so the loop must run on whatever they say
     g->next = fl ? 0 : t;
-    return SHD_OK;
 }
 
 // every engine's first-touch records of the flagged round, in any order
@@ -5339,6 +5348,8 @@ static void x_drop_graphs(shd_xgroup* g) {
 
 static void x_free(shd_xgroup* g) {
     if (!g) return;
+    if (g->h_hdr) (void)hipHostFree(g->h_hdr);
+    if (g->h_xerr) (void)hipHostFree(g->h_xerr);
     x_drop_graphs(g);
     x_p2p_unmap(g);
     if (g->comm && g->own_comm) shd_comm_destroy(g->comm);
@@ -5441,6 +5452,13 @@ static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p,
     g->xcap = block_events ? block_events : x_default_cap(e, world);
     g->fixed_cap = block_events != 0;
     if ((rc = x_alloc(g))) { x_free(g); return rc; }
+    if (hipHostMalloc((void**)&g->h_hdr, sizeof(XHeader) * 64, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&g->h_xerr, sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        x_free(g);
+        return SHD_ENOMEM;
+    }
+    *g->h_xerr = 0;
     *out = g;
     return SHD_OK;
 }
@@ -5682,8 +5700,24 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost,
                                    e->stream));
         }
+        // one engine per process: the last exchange's headers and the wait-error word
+        // come back with the summaries (no synchronous copy of its own for each)
+        const bool prefetched = g->h_hdr && nl == 1;
+        if (prefetched) {
+            shd_eng* e = g->engs[0];
+            SHD_HIP(hipMemcpy2DAsync(g->h_hdr, sizeof(XHeader), g->loc[0].xrecv[(g->xseq - 1) & 1],
+                                     g->stride * sizeof(shd_event), sizeof(XHeader), g->world,
+                                     hipMemcpyDeviceToHost, e->stream));
+            if (g->p2p) SHD_HIP(hipMemcpyAsync(g->h_xerr, g->d_xerr, 4, hipMemcpyDeviceToHost, e->stream));
+        }
         for (int k = 0; k < nl; k++) SHD_HIP(hipStreamSynchronize(g->engs[k]->stream));
-        if ((rc = x_p2p_check(g))) break;
+        if (prefetched && g->p2p ? *g->h_xerr != 0 : false) {
+            fprintf(stderr, "libshdgpu: peer-to-peer exchange: a peer's block did not come within %llu s\n",
+                    kXWaitTicks / 100000000ull);
+            rc = SHD_ENODEV;
+            break;
+        }
+        if (!prefetched && (rc = x_p2p_check(g))) break;
         {
             float ms = 0;   // the batch on engine 0's stream: rounds + exchanges
             if (hipEventElapsedTime(&ms, g->engs[0]->bev[0], g->engs[0]->bev[1]) == hipSuccess)
@@ -5750,7 +5784,8 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         if (done) break;
         if (halted_at < 0) {
             g->last_logged = 0;
-            if ((rc = x_read_next(g))) break;
+            if (prefetched) x_next_from(g, g->h_hdr, g->world);
+            else if ((rc = x_read_next(g))) break;
             continue;
         }
         g->last_logged = 0;
