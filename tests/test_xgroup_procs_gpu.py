@@ -98,6 +98,25 @@ def test_multiprocess_p2p_fused_rounds(world, hpv, tmp_path):
 
 
 @pytest.mark.parametrize("p2p", [False, True], ids=["alltoall", "p2p"])
+def test_multiprocess_group_tor_model(p2p, tmp_path):
+    """BASELINE C4's relay/client model over 3 processes: per-class destination
+    weights (each PHOLD process's weights file), hosts attached at random on
+    the bundled (complete) topology, the relays -- most of the traffic -- all
+    on rank 0, so the exchange is lopsided.  Bit-exact vs the serial oracle."""
+    R, C, load = 40, 200, 4
+    res = run_ranks(3, tmp_path, extra=["--tor", f"{R},{C}", "--load", str(load), "--end-s", "2.5"] +
+                    (["--p2p"] if p2p else []))
+    g, m = W.tor_model(R, C, end_time=int(2.5 * S.SHD_SEC), trace=True, load=load)
+    otr, odg, ost = O.engine_run(m, g)
+    tr = sort_trace(np.concatenate([r["trace"] for r in res]))
+    dg = np.concatenate([r["digest"] for r in res])
+    assert sum(int(r["stats"][0]) for r in res) == ost["n_pkt_events"] > 0
+    assert np.array_equal(tr, sort_trace(otr))
+    assert np.array_equal(dg, odg)
+    assert len({int(r["stats"][3]) for r in res}) == 1
+
+
+@pytest.mark.parametrize("p2p", [False, True], ids=["alltoall", "p2p"])
 def test_multiprocess_group_rolls_back_ambiguous_rounds(p2p, tmp_path):
     """Every undecided first-touch send forced ambiguous and every round
     protected: each logging round is rolled back on every process from its

@@ -19,9 +19,11 @@ sys.path[:0] = [os.path.join(os.path.dirname(HERE), "shadow-1_amd"), HERE]
 import numpy as np  # noqa: E402
 
 
-def model(V, hpv, end, loss, load):
+def model(V, hpv, end, loss, load, tor=None):
     import shdgpu as S
     import workloads as W
+    if tor:   # the Tor-scale relay/client model (per-class destination weights) on the bundled topology
+        return W.tor_model(tor[0], tor[1], end_time=end, trace=True, load=load)
     g = W.geometric_graph(V, seed=6, loss_max=loss)
     m = W.phold_model(W.hosts_on_vertices(V, hpv), end_time=end, trace=True, load=load)
     return g, m
@@ -40,18 +42,21 @@ def main():
     ap.add_argument("--load", type=int, default=16)
     ap.add_argument("--block", type=int, default=0)
     ap.add_argument("--p2p", action="store_true", help="the peer-to-peer transport (shd_xgroup_create_p2p)")
+    ap.add_argument("--tor", default="", help="R,C: the Tor-scale model with R relays and C clients")
     a = ap.parse_args()
     import shdgpu as S
     import workloads as W
     from driver import partition
     from sim import Comm, Engine, PathCache, XGroup
     end = int(a.end_s * S.SHD_SEC)
-    g, m = model(a.vertices, a.hpv, end, a.loss, a.load)
+    tor = tuple(int(x) for x in a.tor.split(",")) if a.tor else None
+    g, m = model(a.vertices, a.hpv, end, a.loss, a.load, tor)
     comm = Comm.host(a.name, a.world, a.rank, device=0)
     pc = PathCache(g, W.attached_vertices(m.host_vertex), build=False)
     pc.build_sharded(comm)
-    lat, rel = pc.rows()
     info = pc.info()
+    # (a complete graph keeps only the direct table: no rows to compare)
+    lat, rel = pc.rows() if not info.is_complete else (np.zeros(0), np.zeros(0))
     pb = partition(m.n_hosts, a.world)
     eng = Engine(m, pc, pb[a.rank], pb[a.rank + 1])
     fallback = 0
