@@ -481,7 +481,7 @@ __shared__ shd_event s_top[kBlock];              // heap root
 __shared__ shd_event s_due[kDueCap * kBlock];    // the window's calendar events, sorted
 // fused peer-to-peer rounds: events received for the window itself, per host
 // (they join the due list after the calendar's; round_body<true>)
-constexpr int kRxCap = 4;
+constexpr int kRxCap = 2;
 __shared__ shd_event s_rx[kRxCap * kBlock];
 __shared__ uint32_t s_rxn[kBlock];
 __shared__ CodelEnt s_cqh[kBlock];               // CoDel FIFO head
@@ -3296,7 +3296,7 @@ __global__ __launch_bounds__(256) void k_xchg(DParams P, const TlPart* __restric
 // into that region again two exchanges later, after it saw this engine's
 // next header, which follows the end of this launch).
 static_assert(kXSlots == (uint32_t)kBlock, "one region slot per lane");
-constexpr int kXDefCap = 4;   // received events per lane whose calendar store waits for the round's end
+constexpr int kXDefCap = 2;   // received events per lane whose calendar store waits for the round's end
 
 __device__ __forceinline__ uint4 ld16_sys(const void* p) {
     u32x4 x;
