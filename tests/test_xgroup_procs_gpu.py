@@ -86,12 +86,14 @@ def test_multiprocess_group_matches_oracle(world, block, p2p, tmp_path):
     assert len(rounds) == 1                                    # every rank ran the same rounds
 
 
-@pytest.mark.parametrize("world,hpv", [(4, 1), (3, 3)])
+@pytest.mark.parametrize("world,hpv", [(4, 1), (3, 3), (9, 1)])
 def test_multiprocess_p2p_fused_rounds(world, hpv, tmp_path):
     """The fused peer-to-peer schedule with more ranks than round-kernel blocks
     (4 ranks of 60 hosts: one block each, the launch padded to a put block per
-    peer) and with several blocks per rank (3 x 240 hosts: 4 blocks, events
-    sorted into per-destination-block regions of every peer)."""
+    peer), with several blocks per rank (3 x 240 hosts: 4 blocks, events
+    sorted into per-destination-block regions of every peer), and with more
+    than eight peers (9 ranks: the regions of peers past the eighth are taken
+    by the round's second ingest pass)."""
     res = run_ranks(world, tmp_path, extra=["--p2p", "--hpv", str(hpv)])
     check_against_oracle(res, 240, hpv, 3.0, 0.01, 16)
     assert len({int(r["stats"][3]) for r in res}) == 1
