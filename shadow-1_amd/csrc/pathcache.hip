@@ -619,6 +619,10 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
     return SHD_OK;
 }
 
+#ifndef SHD_ROW_BLOCK
+#define SHD_ROW_BLOCK 1024
+#endif
+constexpr int kRowBlock = SHD_ROW_BLOCK;   // workgroup of the LDS row kernel past 2 k vertices
 static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
 static constexpr size_t kLdsMax = 160 * 1024;
 
@@ -676,9 +680,9 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_row, pc->d_stats, row0, row1);
             } else {
                 int grid = std::max(1, std::min(row1 - row0, ncu));
-                SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<1024>,
+                SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<kRowBlock>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-                hipLaunchKernelGGL(k_sssp_rows_lds<1024>, dim3(grid), dim3(1024), lds, s, V, T, pc->d_arc_off,
+                hipLaunchKernelGGL(k_sssp_rows_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds, s, V, T, pc->d_arc_off,
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
