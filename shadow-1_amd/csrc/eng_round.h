@@ -1,0 +1,951 @@
+// eng_round.h -- the round kernels of one engine: boot, the round body (idle
+// test, calendar merge, event loop, flush, close), round completion, the
+// ticketed (k_round_dev) and ticketless (k_round_tl) batches, first-touch
+// finalization, pushed events, digests.
+// Part of libshdgpu's engine translation unit (csrc/engine.hip includes it
+// inside its anonymous namespace); not a standalone header.
+#pragma once
+
+// ------------------------------------------------------------------ kernels
+
+// host_boot for every local host at t = 0 (host.c:372-390)
+__global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __restrict__ rng0,
+                                                  const uint64_t* __restrict__ bw_down,
+                                                  const uint64_t* __restrict__ bw_up) {
+    const int32_t l = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    if (l < P.nloc) {
+        const uint32_t h = (uint32_t)(P.h0 + l);
+        // _networkinterface_setupTokenBuckets (network_interface.c:192-226)
+        const uint64_t rxr = bw_down[h] * 1024 / 1000, txr = bw_up[h] * 1024 / 1000;
+        // bucket capacity refill + MTU within the record's 32 bits
+        if (((rxr + SHD_MTU) | (txr + SHD_MTU)) >> 32) err |= SHD_ERR_INTERNAL;
+        HostRec r;
+        r.ev_seq = 0; r.cq_total = 0; r.cq_iexp = 0; r.cq_ndrop = 0; r.rx_rem = 0; r.tx_rem = 0;
+        for (int k = 0; k < 3; k++) { r.tt[k] = kInf; r.ts_back[k] = 0; }
+        P.hc[l] = HostCnt{0, 0, 0, 0, 0, 0};
+        r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
+        r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
+        r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.if_in = 0; r.if_out = 0; r.pad = 0;
+        P.hs[l] = r;
+        P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
+        HostCtx c;
+        hot_load(P, c);
+        load_ctx(P, c, l, r, P.host_att[h], P.self_thr[h]);
+        c.now = 0;
+        c.q_seq = 0; c.q_src = c.h; c.q_sub = 0;
+        schedule_self(P, c, SHD_EV_HEARTBEAT, hb_interval(P, c.k.feat, h), 0);   // tracker_new, tracker.c:141,607-610
+        refill_cb(P, c);                                               // ethernet startRefilling
+        schedule_self(P, c, SHD_EV_REFILL_LO, SHD_MS, 0);              // loopback refill at +1 ms
+        if (!P.no_app_start) schedule_self(P, c, SHD_EV_APP_START, P.app_start, 0);   // process_schedule
+        store_ctx(P, c);
+        next = host_next(c);
+        err |= c.err;
+    }
+    block_reduce_publish<kBlock>(P, next, 0, 0, err);
+}
+
+// a calendar slot's event, if it is one of the window's: onto the due list
+// (unsorted; sorted once all bins are read).  `nw` counts the window's
+// events; those past kDueCap go to the heap afterwards (due_overflow)
+__device__ __forceinline__ void due_add(const EvV& x, uint32_t& nw, uint64_t ws, uint64_t we) {
+    const uint64_t t = evv_time(x);
+    if (t < ws || t >= we) return;
+    if (nw < (uint32_t)kDueCap) ev_st(s_due + nw * kBlock + threadIdx.x, x);
+    nw++;
+}
+
+// rare: more than kDueCap window events.  The bins are read again in the
+// same order (the window's events in them cannot change during the round)
+// and the events past the first kDueCap go to the heap
+__device__ __forceinline__ void due_overflow(const DParams& P, HostCtx& c, uint64_t b0, uint32_t wbits, uint64_t ws,
+                                          uint64_t we, uint32_t nrx = 0) {
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < 3; j++) {
+        if (((wbits >> j) & 1u) == 0) continue;
+        const size_t bi = (size_t)c.l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+        for (uint32_t s = 0; s < kBinCap; s++) {
+            const shd_event& x = P.bins[bi * kBinCap + s];
+            if (x.time < ws || x.time >= we) continue;
+            if (k >= (uint32_t)kDueCap) heap_push(P, c, x);
+            k++;
+        }
+    }
+    for (uint32_t r = 0; r < nrx; r++) {   // then the received ones, in the order due_add took them
+        const shd_event& x = s_rx[r * kBlock + threadIdx.x];
+        if (x.time < ws || x.time >= we) continue;
+        if (k >= (uint32_t)kDueCap) heap_push(P, c, x);
+        k++;
+    }
+}
+
+// bit p of a bitmap held in registers (static word indices only)
+__device__ __forceinline__ uint32_t bit_at(const uint32_t (&w)[kNBW], uint32_t p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < (int)kNBW; j++) v |= (p >> 5) == (uint32_t)j ? w[j] : 0u;
+    return (v >> (p & 31)) & 1u;
+}
+
+// the lane's host (P.nloc: none)
+__device__ __forceinline__ int32_t lane_host(const DParams& P) {
+    return (int32_t)threadIdx.x < P.hpw ? (int32_t)blockIdx.x * P.hpw + (int32_t)threadIdx.x : P.nloc;
+}
+
+// One scalar load per 64-B line of the Params copy, issued at kernel entry
+// with the other first loads; consumed (params_warm_done) where the kernel
+// waits for its window start anyway.  The round's later scalar loads of
+// Params fields then hit the scalar cache instead of each paying an L2 trip.
+__device__ __forceinline__ uint32_t params_warm(const DParams* Pp) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(Pp);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < (int)((sizeof(DParams) + 63) / 64); k++) acc ^= w[k * 16];
+    return acc;
+}
+__device__ __forceinline__ void params_warm_done(uint32_t acc) { asm volatile("" ::"s"(acc)); }
+
+// what a round reads of a host before it knows the window: both inbox
+// counts, the earliest timer/heap time, the calendar bitmap, the host record,
+// its attached vertex and loopback thresholds.  None of it depends on the
+// window start, so the round kernels issue these loads together with the
+// loads of the window start and control words (one memory round trip).  The
+// pointers come by value in the kernel arguments (RoundArgs), not through the
+// Params pointer: one scalar load level instead of two before the first
+// vector load.
+template <template <class> class Ptr>
+struct RoundArgsT {
+    Ptr<const HostRec> hs;
+    Ptr<const uint64_t> hnext;
+    Ptr<const uint32_t> nin0, nin1;
+    Ptr<const uint32_t> bits;   // null: no calendar
+    Ptr<const int32_t> att;     // host_att + h0
+    Ptr<const int4> st;         // self_thr + h0
+    Ptr<const uint32_t> halt;
+    int32_t nloc, hpw;
+    uint32_t nblk;   // grid size (blocks of hpw hosts)
+    uint32_t pad;
+};
+using DRoundArgs = RoundArgsT<GlobalPtr>;
+static DRoundArgs round_args(const Params& P) {
+    const DParams& d = dp(P);
+    DRoundArgs a;
+    a.hs = d.hs; a.hnext = d.hnext; a.nin0 = d.inbox_n[0]; a.nin1 = d.inbox_n[1];
+    a.bits = d.bins ? d.bin_bits : nullptr;
+    a.att = d.host_att + P.h0; a.st = d.self_thr + P.h0;
+    a.halt = d.halt; a.nloc = P.nloc; a.hpw = P.hpw;
+    a.nblk = (uint32_t)((P.nloc + P.hpw - 1) / P.hpw); a.pad = 0;
+    return a;
+}
+__device__ __forceinline__ DRoundArgs round_args_dev(const DParams& P) {
+    DRoundArgs a;
+    a.hs = P.hs; a.hnext = P.hnext; a.nin0 = P.inbox_n[0]; a.nin1 = P.inbox_n[1];
+    a.bits = P.bins ? P.bin_bits : nullptr;
+    a.att = P.host_att + P.h0; a.st = P.self_thr + P.h0;
+    a.halt = P.halt; a.nloc = P.nloc; a.hpw = P.hpw;
+    a.nblk = (uint32_t)((P.nloc + P.hpw - 1) / P.hpw); a.pad = 0;
+    return a;
+}
+struct HostIn {
+    uint32_t nin[2];
+    uint64_t t0;
+    uint32_t w[kNBW];
+    HostRec rec;
+    int32_t att;
+    int4 st;
+};
+// every lane loads (lanes past the last host read the last host's entries
+// and ignore them): no branch, so no wait at a join before other loads issue
+__device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
+    const int32_t l0 = (int32_t)threadIdx.x < a.hpw ? (int32_t)blockIdx.x * a.hpw + (int32_t)threadIdx.x : a.nloc;
+    const int32_t l = l0 < a.nloc ? l0 : a.nloc - 1;
+    // the idle test's words first: the idle test and the window's bin loads
+    // wait for them only, not for the 160-B record behind them
+    in.nin[0] = a.nin0[l];
+    in.nin[1] = a.nin1[l];
+    in.t0 = a.hnext[l];
+    if (a.bits) {
+        const uint4* bp = (const uint4*)(a.bits + (size_t)l * kNBW);
+        const uint4 x = bp[0], y = bp[1];
+        in.w[0] = x.x; in.w[1] = x.y; in.w[2] = x.z; in.w[3] = x.w;
+        in.w[4] = y.x; in.w[5] = y.y; in.w[6] = y.z; in.w[7] = y.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < (int)kNBW; j++) in.w[j] = 0;
+    }
+}
+
+// one round [ws, we): merge inbox[parity] and the calendar bins of the
+// window, run events < we
+template <bool RX = false>   // RX: the fused peer-to-peer round's received window events (s_rx)
+__device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, uint64_t ws, uint64_t we, int parity,
+                                           uint64_t& next_out, uint64_t& nev_out, uint64_t& npkt_out,
+                                           uint32_t& err_out, uint32_t xwi = 0) {
+    const int32_t l = lane_host(P);
+#ifdef SHD_PROF
+    const unsigned long long w0 = wall_clock64();
+#endif
+    TIM(1);
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 10; i++)
+            for (int j = 0; j < 4; j++) s_kc[i][j] = 0;
+#endif
+    uint64_t next = kInf, nev = 0, npkt = 0;
+    uint32_t err = 0;
+    // the window's calendar bins: b0 .. b0 + nbin - 1 (nbin <= 3: bin width <= W)
+    const uint64_t b0 = ws >> P.bin_shift;
+    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
+    uint32_t w[kNBW];
+    // hosts with nothing due this round touch 3 words and their bitmap, not their whole state
+    bool idle = false;
+    uint32_t wbits = 0;   // bit j: window bin j is non-empty
+    HostRec rec;
+    int32_t rec_att;
+    int4 rec_st;
+    uint32_t nin0 = 0;
+    if (l < P.nloc) {
+        nin0 = parity ? in.nin[1] : in.nin[0];
+        const uint64_t t0 = in.t0;
+#pragma unroll
+        for (int j = 0; j < (int)kNBW; j++) w[j] = in.w[j];
+        if (P.bins) {
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++)
+                if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
+        } else {
+#pragma unroll
+            for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+        }
+        if (nbin > 3) err |= SHD_ERR_INTERNAL;   // window wider than W
+        if (nin0 == 0 && t0 >= we && wbits == 0 && (!RX || s_rxn[threadIdx.x] == 0)) {
+            idle = true;
+            next = t0;
+            if (P.bins) {
+                // the window's bins hold nothing: their counts are zero (a
+                // count is nonzero only behind a set bit, cal_push), no reset
+                const uint64_t cb = cal_lower_bound(P, w, we);
+                next = cb < next ? cb : next;
+            }
+        }
+    }
+    TIM(2);
+    const bool active = l < P.nloc && !idle;
+#ifdef SHD_TIMING
+    uint64_t n_it = 0, k_tk = 0, k_be = 0, k_rw = 0, k_fl = 0, k_in = 0;
+    uint64_t k_l0 = 0, n_kinds = 0, n_lanes = 0;
+#ifdef SHD_TIMING_LIGHT   // phase stamps only: no clock reads inside the event loop
+#define KT0(v)
+#define KTA(acc, v)
+#else
+#define KT0(v) const uint64_t v = clock64();
+#define KTA(acc, v) acc += clock64() - v;
+#endif
+#else
+#define KT0(v)
+#define KTA(acc, v)
+#endif
+    HostCtx c;   // idle lanes take part in the wave's flushes with no sends
+    hot_load(P, c);
+    PendDel pd;
+    c.ns = 0; c.att = 0; c.cls = 0; c.err = 0;
+    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0;
+    // the window's non-empty bins, all slots loaded before the host record is
+    // consumed (one round trip, overlapping the record's)
+    EvV bx[3][kBinCap];
+    if (active && P.bins) {
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++) {
+            if (((wbits >> j) & 1u) == 0) continue;
+            const size_t bi = (size_t)l * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+            static_assert(kBinCap == 4, "the slots are read as four named events");
+            const auto bp = P.bins + bi * kBinCap;
+#pragma unroll
+            for (uint32_t k = 0; k < kBinCap; k++) bx[j][k] = ev_ld(bp + k);
+        }
+    }
+    // the host record behind the bins, in the same round trip, for the
+    // hosts with something due only (idle hosts' records are never read)
+    if (active) {
+        rec = P.hs[l];
+        rec_att = P.host_att[P.h0 + l];
+        rec_st = P.self_thr[P.h0 + l];
+    }
+    if (active) {
+        PROF_T0(t_all)
+        load_ctx(P, c, l, rec, rec_att, rec_st);
+        TIMA(7);
+        c.ws = ws;
+        c.ws_mod = (uint32_t)(ws % SHD_MS);
+        c.np = parity ^ 1;
+#ifdef SHD_PROF
+        c.prof = ProfAcc{};
+#endif
+        PROF_ADD(c, PR_LOAD, t_all)
+        // merge inbound events of the previous round
+        PROF_T0(t_m)
+        const uint32_t nin = nin0;
+        if (nin) {
+            const shd_event* ib = P.inbox[parity] + (size_t)l * P.inbox_cap;
+            const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
+            for (uint32_t i = 0; i < n; i++) { TCNT(4); heap_push(P, c, ib[i]); }
+            P.inbox_n[parity][l] = 0;
+        }
+        // the window's calendar events, sorted into the due list.  The slots
+        // of a non-empty bin are filtered by time alone: a slot never written
+        // in the bin's current use holds kInf or an older use's event (before
+        // ws), a slot being written by this round's appends holds a time >= we
+        // (or still the old one), so the bin's count is not needed here
+        if (P.bins) {
+            uint32_t nw = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                if (((wbits >> j) & 1u) == 0) continue;
+#pragma unroll
+                for (uint32_t k = 0; k < kBinCap; k++) due_add(bx[j][k], nw, ws, we);
+            }
+            uint32_t nrx = 0;
+            if (RX) {
+                nrx = s_rxn[threadIdx.x];
+                nrx = nrx < (uint32_t)kRxCap ? nrx : (uint32_t)kRxCap;
+                for (uint32_t r = 0; r < nrx; r++) due_add(ev_ld(s_rx + r * kBlock + threadIdx.x), nw, ws, we);
+            }
+            c.nd = nw < (uint32_t)kDueCap ? nw : (uint32_t)kDueCap;
+            if (nw > (uint32_t)kDueCap) due_overflow(P, c, b0, wbits, ws, we, nrx);
+            // insertion sort of the due list (LDS only)
+            for (uint32_t i = 1; i < c.nd; i++) {
+                const EvV x = ev_ld(s_due + i * kBlock + threadIdx.x);
+                uint32_t k = i;
+                for (; k > 0; k--) {
+                    const EvV y = ev_ld(s_due + (k - 1) * kBlock + threadIdx.x);
+                    if (!evv_less(x, y)) break;
+                    ev_st(s_due + k * kBlock + threadIdx.x, y);
+                }
+                ev_st(s_due + k * kBlock + threadIdx.x, x);
+            }
+            c.dt = c.nd ? s_due[threadIdx.x].time : kInf;
+        }
+        PROF_ADD(c, PR_MERGE, t_m)
+        TIMA(8);
+#ifdef SHD_TIMING
+        k_l0 = clock64();
+#endif
+    }
+    // the event loop.  An event's shared steps run in the same iteration as
+    // its start.  A lane whose deferred sends need a flush before it can go
+    // on (its send buffer is full, or a loopback send needs the exact event
+    // ID) leaves the inner loop with its event suspended; the wave's flush
+    // (all lanes, outside the inner loop) runs, and the suspended lanes
+    // resume.  Normally the outer loop runs once: one flush per round.
+    {
+        // per-lane state: 0 needs its next event, 1 is running one, 2 waits
+        // for a flush, 3 is done.  Both loops exit on wave-uniform tests only
+        // (no divergent breaks: the exec-mask bookkeeping stays small).
+        uint32_t st = active ? 0u : 3u;
+        pd.kind = 0;
+        for (;;) {
+            KT0(q4)
+            for (;;) {
+#ifdef SHD_TIMING
+                n_it++;
+#endif
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
+                const uint64_t i_t0 = clock64();
+                uint64_t i_tk = 0, i_be = 0;
+                uint32_t i_cls = 0;
+#endif
+                if (st == 0u) {
+                    PROF_T0(t_p)
+                    shd_event e;
+                    KT0(q0)
+                    const bool more = take_next(P, c, we, e);
+                    KTA(k_tk, q0)
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
+                    i_tk = clock64();
+                    if (more) {
+                        i_cls = e.kind & 7;
+                        if (e.kind == SHD_EV_PACKET && !(c.cq_count == 0 && c.rx_rem >= SHD_MTU && !bootstrapping(P, c)))
+                            i_cls = 8;
+                    }
+#endif
+                    PROF_ADD(c, PR_POP, t_p)
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
+                    {   // divergence census: distinct event kinds started in this iteration
+                        const uint32_t ks = more ? 1u << (e.kind & 31) : 0u;
+                        for (uint32_t b = 1; b < 8; b++) n_kinds += __ballot((ks >> b) & 1u) != 0;
+                        n_lanes += __popcll(__ballot(ks != 0));
+                    }
+#endif
+                    if (more) {
+                        c.now = e.time;
+                        KT0(q1)
+                        begin_event(P, c, e);
+                        KTA(k_be, q1)
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
+                        i_be = clock64();
+#endif
+                        st = ((c.w_fl & ~W_READ) | c.w_msgs) ? 1u : 0u;   // the shared steps, if any are left
+#ifndef SHD_NO_FUSE
+                        // An arrival schedules its notification at +1 ns, and
+                        // that is almost always the host's next event: when the
+                        // notification timer is strictly the earliest candidate
+                        // (so take_next would return it next) and in the window,
+                        // it runs now, in the same iteration (the wave's lanes
+                        // then run arrival + notification together instead of
+                        // spreading them over two iterations)
+                        if (st == 0u && c.tt2 < we) {
+                            const uint64_t t = c.tt2, ht = c.evq_n ? c.top_time : kInf;
+                            if (t < c.tt0 && t < c.tt1 && t < c.dt && t < ht && notify_fast_ok(P, c)) {
+                                TCNT(5);
+                                c.tt2 = kInf;
+                                c.now = t;
+                                c.c_events++;
+                                c.q_seq = c.ts2; c.q_src = c.h; c.q_sub = 0;
+                                c.w_msgs = 0; c.w_fl = 0;
+                                notify_fast(P, c);
+                                st = c.w_fl ? 1u : 0u;
+                            }
+                        }
+                        // the same for the periodic refill (at the next 1 ms
+                        // boundary) with both queues empty
+                        if (st == 0u && c.tt1 < we) {
+                            const uint64_t t = c.tt1, ht = c.evq_n ? c.top_time : kInf;
+                            if (t < c.tt0 && t < c.tt2 && t < c.dt && t < ht && c.cq_count == 0 && c.tq_count == 0) {
+                                TCNT(5);
+                                c.tt1 = kInf;
+                                c.now = t;
+                                c.c_events++;
+                                c.q_seq = c.ts1; c.q_src = c.h; c.q_sub = 0;
+                                c.w_msgs = 0; c.w_fl = 0;
+                                refill_fast(P, c);
+                            }
+                        }
+#endif
+                    } else {
+                        st = 3u;
+                    }
+                }
+                if (st == 1u) {
+                    KT0(q2)
+                    st = run_work(P, c) ? 0u : 2u;
+                    KTA(k_rw, q2)
+                }
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
+                {
+                    const uint64_t i_t1 = clock64();
+                    const uint64_t m = __ballot(i_cls != 0);
+                    if (m) {
+                        const int f = __ffsll((unsigned long long)m) - 1;
+                        const uint32_t u = __shfl(i_cls, f, 64);
+                        const uint64_t tk = __shfl(i_tk, f, 64), be = __shfl(i_be, f, 64);
+                        if (__ballot(i_cls != 0 && i_cls != u) == 0 && threadIdx.x == 0) {
+                            s_kc[u][0] += 1;
+                            s_kc[u][1] += i_t1 - i_t0;
+                            s_kc[u][2] += tk - i_t0;
+                            s_kc[u][3] += be - tk;
+                        }
+                    }
+                }
+#endif
+                if (__ballot(st <= 1u) == 0) break;
+            }
+            KTA(k_in, q4)
+            KT0(q3)
+            if (threadIdx.x == 0) TCNT(6);
+            if (st == 2u) TCNT(7);
+#ifdef SHD_TIMING_LIGHT
+            TIM(11);   // the (last) flush starts
+#endif
+            const bool last = __ballot(st == 2u) == 0;   // no lane waits to resume: the round's last flush
+            flush_wave(P, c, last, pd);
+            KTA(k_fl, q3)
+            if (last) break;
+            if (st == 2u) st = 1u;
+        }
+    }
+    TIM(9);
+    if (active) {
+#if defined(SHD_TIMING) && !defined(SHD_TIMING_LIGHT)
+        {
+            uint64_t v[7] = {n_it, k_tk, k_be, k_rw, clock64() - k_l0, k_fl, k_in};
+#pragma unroll
+            for (int j = 0; j < 7; j++)
+                for (int off = 32; off > 0; off >>= 1) {
+                    const uint64_t o = __shfl_xor(v[j], off, 64);
+                    v[j] = o > v[j] ? o : v[j];
+                }
+            TIMV(11, v[0]);
+            TIMV(12, v[1]);
+            TIMV(13, v[2]);
+            TIMV(14, v[3]);
+            TIMV(15, v[4]);
+            TIMV(16, v[5]);
+            TIMV(17, v[6]);
+            TIMV(18, n_kinds);
+            TIMV(19, n_lanes);
+        }
+#endif
+        next = host_next(c);
+        if (c.min_emit < next) next = c.min_emit;
+        if (P.bins) {
+            // bins wholly before we are consumed: reset them (no append of
+            // this round can target them: appends are >= we and within the
+            // horizon).  Only a bin with its bit set has a nonzero count: an
+            // append that claims a slot sets the bit once its event is stored,
+            // and one past the capacity follows the claims below it (cal_push,
+            // flush), so the empty bins' counts are left alone -- a store per
+            // host and bin, most of the round's write traffic otherwise.
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                const uint64_t b = b0 + j;
+                if (j < nbin && ((b + 1) << P.bin_shift) <= we && ((wbits >> j) & 1u)) {
+                    const uint32_t p = (uint32_t)b & (kNB - 1);
+                    P.bin_n[(size_t)l * kNB + p] = 0;
+                    const uint32_t m = 1u << (p & 31);
+                    atomicAnd(&P.bin_bits[(size_t)l * kNBW + (p >> 5)], ~m);
+#pragma unroll
+                    for (int k = 0; k < (int)kNBW; k++)
+                        if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
+                }
+            }
+            const uint64_t cb = cal_lower_bound(P, w, we);
+            next = cb < next ? cb : next;
+        }
+        nev = c.c_events;
+        npkt = c.c_pkt;
+        err |= c.err;
+        PROF_T0(t_s)
+        TIMA(10);
+        store_ctx(P, c);
+        PROF_ADD(c, PR_STORE, t_s)
+        PROF_ADD(c, PR_TOTAL, t_all)
+#ifdef SHD_PROF
+        c.prof.v[PR_NEV] = nev;
+        for (int i = 0; i < PR_N; i++) {
+            atomicAdd(&g_prof[i], c.prof.v[i]);
+            atomicMax(&g_prof[PR_N + i], c.prof.v[i]);
+        }
+        atomicAdd(&g_prof[2 * PR_N], 1ull);
+#endif
+    }
+#ifdef SHD_PROF
+    {
+        uint64_t mx = nev;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        const unsigned long long w1 = wall_clock64();
+        if (threadIdx.x == 0) {
+            unsigned long long* g = g_wave[((uintptr_t)P.sum / sizeof(DevSummary)) & 127];
+            atomicMin(&g[0], w0);
+            atomicMax(&g[1], w1);
+            atomicMax(&g[2], w1 - w0);
+            atomicAdd(&g[3], w1 - w0);
+            atomicAdd(&g[4], 1ull);
+            atomicMax(&g[5], (unsigned long long)mx);
+            atomicAdd(&g[6], (unsigned long long)mx);
+        }
+    }
+#endif
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 10; i++)
+            if (s_kc[i][0])
+                for (int j = 0; j < 4; j++) atomicAdd(&g_kc[i][j], s_kc[i][j]);
+#endif
+    flush_finish(P, c, pd);
+    err |= c.err;
+    // peer-to-peer: a wave that stored into a peer's receive block drains
+    // those stores before the round ends (k_xchg tags the blocks next)
+    if (P.xpeer && __ballot(c.xput != 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    TIM(3);
+    next_out = next; nev_out = nev; npkt_out = npkt; err_out = err;
+}
+
+__global__ __launch_bounds__(kBlock) void k_round(DParams P, uint64_t ws, uint64_t we, int parity) {
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    HostIn in;
+    host_in_load(round_args_dev(P), in);
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    (void)round_complete(P, next, nev, npkt, err);
+}
+
+// finalize resolved pending sends: value from the min-rank row, then deliver
+__device__ void finalize_one(const DParams& P, const Pending& r, int next_parity, uint64_t& next, uint32_t& err) {
+    if (r.delivered != 1u) return;
+    const PathVal pv = path_value(P, (int32_t)r.a, (int32_t)r.b);
+    if (!pv.resolved) err |= SHD_ERR_AMBIGUOUS;
+    if (P.pcount) {   // counted once the pair has its rank (incrementPathPacketCounter, worker.c:296)
+        const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
+        const int32_t ra = P.complete ? kNoRank : P.rank[a], rb = a == b ? kNoRank : P.rank[b];
+        const uint32_t adj = P.prefer_direct ? P.adj[(size_t)a * P.T + b] : 0u;
+        atomicAdd(&P.pcount[path_key(P, a, b, ra, rb, adj)], 1u);
+    }
+    shd_event e;
+    e.time = r.qtime + (uint64_t)ceil(pv.lat * (double)SHD_MS);
+    e.seq = r.seq; e.src = r.qhost; e.dst = r.dst; e.pkt = r.pkt; e.kind = SHD_EV_PACKET;
+    if (e.time >= P.end_time) return;
+    if (e.time < next) next = e.time;
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl >= 0 && dl < P.nloc) {
+        uint32_t slot = atomicAdd(&P.inbox_n[next_parity][dl], 1u);
+        if (slot >= P.inbox_cap) err |= SHD_ERR_INBOX_OVERFLOW;
+        else P.inbox[next_parity][(size_t)dl * P.inbox_cap + slot] = e;
+    } else {
+        unsigned long long slot = atomicAdd(&P.sum->n_remote, 1ull);
+        if (slot >= P.remote_cap) err |= SHD_ERR_REMOTE_OVERFLOW;
+        else P.remote[slot] = e;
+    }
+}
+
+__global__ void k_finalize(DParams P, const Pending* __restrict__ pend, uint32_t n, int next_parity) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    if (i < n) finalize_one(P, pend[i], next_parity, next, err);
+    if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+    if (err) atomicOr(&P.sum->error, err);
+}
+
+// device-side first-touch resolution for rounds with few logged queries (the
+// common case after warm-up), run by the last block of the round: rank the
+// records by serial key (counting sort: keys are unique), one lane assigns
+// row ranks in that order, every lane finalizes its records.  Larger rounds
+// halt the batch for the host path (shd_eng_resolve).
+constexpr int kResolveMax = 256;
+__device__ __forceinline__ bool pend_less(const Pending& x, const Pending& y) {
+    if (x.qtime != y.qtime) return x.qtime < y.qtime;
+    if (x.qhost != y.qhost) return x.qhost < y.qhost;
+    if (x.qsrc != y.qsrc) return x.qsrc < y.qsrc;
+    if (x.qseq != y.qseq) return x.qseq < y.qseq;
+    return x.qsub < y.qsub;
+}
+
+__device__ void resolve_block(const DParams& P, int next_parity) {
+    __shared__ Pending recs[kResolveMax];
+    __shared__ int16_t order[kResolveMax];
+    const unsigned long long n = P.sum->n_pending;
+    if (n == 0) return;
+    if (n > (unsigned long long)kResolveMax) {
+        if (threadIdx.x == 0) *P.halt = 1u;
+        return;
+    }
+    const int cnt = (int)n;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) recs[i] = P.pend[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+        int pos = 0;
+        for (int j = 0; j < cnt; j++) pos += pend_less(recs[j], recs[i]) ? 1 : 0;
+        order[pos] = (int16_t)i;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t nr = *P.next_rank;
+        int32_t* rank = (int32_t*)P.rank;
+        int32_t* srank = (int32_t*)P.self_rank;
+        for (int k = 0; k < cnt; k++) {
+            const Pending& r = recs[order[k]];
+            const int32_t a = (int32_t)r.a, b = (int32_t)r.b;
+            if (a == b) {
+                if (rank[a] == kNoRank && srank[a] == kNoRank) srank[a] = nr++;
+            } else if (P.directed) {
+                if (rank[a] == kNoRank) rank[a] = nr++;
+            } else {
+                if (rank[a] == kNoRank && rank[b] == kNoRank) rank[a] = nr++;
+            }
+        }
+        *P.next_rank = nr;
+        __threadfence();
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // drop L1 lines of the rank arrays
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) finalize_one(P, recs[i], next_parity, next, err);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0) {
+        if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+        if (err) atomicOr(&P.sum->error, err);
+    }
+}
+
+// device-driven round i of a batch (single engine): the window start is the
+// previous round's next event time (read on the device), so rounds run back
+// to back from one batch launch (or graph) with no host round trip; the last
+// block resolves the round's first-touch log.  A round past `stop` only
+// forwards the time.  `init` is the next round's summary, initialised here.
+// The hot kernels take Params through a pointer to a device copy (one per
+// summary-ring slot): fields are scalar-loaded where used instead of all held
+// in SGPRs, which otherwise spill to VGPR lanes around every branch.
+__global__ __launch_bounds__(kBlock) void k_round_dev(DRoundArgs a, const DevSummary* __restrict__ prev,
+                                                       const DevCtl* __restrict__ ctl, const DParams* __restrict__ Pp,
+                                                       DevSummary* __restrict__ init, int i, uint64_t window) {
+    const DParams& P = *Pp;
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
+#endif
+    // the round's inputs and the hosts' state, loaded together (one round trip)
+    HostIn in;
+    host_in_load(a, in);
+    const uint32_t halt = *a.halt;
+    const uint64_t stop = ctl->stop, rbase = ctl->round_base, ws = prev->next_time;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    // one test of all three loads, so that they issue together (no wait
+    // between the halt flag and the window start)
+    if ((halt != 0) | (ws >= stop)) {
+        if (halt == 0 && lead) {   // only forwards the time
+            atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+            *init = fresh_summary();
+            atomicMin(&P.sum->next_time, (unsigned long long)ws);
+        }
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, (unsigned long long)wall_clock64());
+        *init = fresh_summary();
+    }
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    TIM(4);
+    if (!round_complete(P, next, nev, npkt, err)) {
+        TIM(5);
+        return;
+    }
+    TIM(5);
+    if (threadIdx.x == 0) P.sum->ws = ws;
+    resolve_block(P, parity ^ 1);
+    TIM(6);
+    if (threadIdx.x == 0) atomicMax(&P.sum->t_last, (unsigned long long)wall_clock64());
+}
+
+// Ticketless rounds.  Every block writes its share of the round's summary
+// (TlPart) and ends; there is no completion ticket.  The next round's blocks
+// each fold all the shares of this one (one load per lane, issued with the
+// host-state loads) to get their window start, and its block 0 publishes the
+// fold as this round's summary; k_fold_tl publishes the batch's last round.
+// Without a ticket no block sees the whole round's first-touch log, so a
+// round that logged is resolved by the host: the next round halts the batch.
+// The host runs these batches once a batch has logged nothing.
+struct TlPart {
+    unsigned long long next, t_end;
+    unsigned int nev, npkt, err, nact;   // nact: hosts with at least one event
+};
+__device__ __forceinline__ void tl_fold(TlPart& a, const TlPart& b) {
+    a.next = b.next < a.next ? b.next : a.next;
+    a.t_end = b.t_end > a.t_end ? b.t_end : a.t_end;
+    a.nev += b.nev;
+    a.npkt += b.npkt;
+    a.err |= b.err;
+    a.nact += b.nact;
+}
+// the wave's fold of the shares [0, n) (one wave per block)
+__device__ __forceinline__ TlPart tl_gather(const TlPart* __restrict__ parts, uint32_t n) {
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    for (uint32_t j = threadIdx.x; j < n; j += 64) tl_fold(f, parts[j]);
+    for (int off = 32; off > 0; off >>= 1) {
+        TlPart o;
+        o.next = __shfl_xor(f.next, off, 64);
+        o.t_end = __shfl_xor(f.t_end, off, 64);
+        o.nev = __shfl_xor(f.nev, off, 64);
+        o.npkt = __shfl_xor(f.npkt, off, 64);
+        o.err = __shfl_xor(f.err, off, 64);
+        o.nact = __shfl_xor(f.nact, off, 64);
+        tl_fold(f, o);
+    }
+    return f;
+}
+// The shares in two phases, so that their loads go out first and the
+// host-state loads behind them (the window start waits only for these):
+// tl_issue loads shares [base, base + 256) as four independent loads per lane
+// (indices past the end read the last share and are not folded), tl_fold4
+// folds them in
+__device__ __forceinline__ void tl_issue(const TlPart* __restrict__ parts, uint32_t n, uint32_t base, TlPart (&v)[4]) {
+    const uint32_t last = n - 1;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t j = base + 64u * k + threadIdx.x;
+        v[k] = parts[j < n ? j : last];
+    }
+}
+__device__ __forceinline__ void tl_fold4(TlPart& f, const TlPart (&v)[4], uint32_t n, uint32_t base) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (base + 64u * k + threadIdx.x < n) tl_fold(f, v[k]);
+}
+__device__ __forceinline__ void tl_reduce(TlPart& f, bool full) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(f.next, off, 64);
+        f.next = o < f.next ? o : f.next;
+        if (full) {
+            const uint64_t te = __shfl_xor(f.t_end, off, 64);
+            f.t_end = te > f.t_end ? te : f.t_end;
+            f.nev += __shfl_xor(f.nev, off, 64);
+            f.npkt += __shfl_xor(f.npkt, off, 64);
+            f.err |= __shfl_xor(f.err, off, 64);
+            f.nact += __shfl_xor(f.nact, off, 64);
+        }
+    }
+}
+
+// publish a round's fold into its summary; a round that logged first touches
+// halts the batch (the host resolves its log)
+__device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint32_t* halt) {
+    if (f.next != kInf) atomicMin(&s->next_time, f.next);
+    if (f.nev) atomicAdd(&s->n_events, (unsigned long long)f.nev);
+    if (f.npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f.npkt);
+    if (f.err) atomicOr(&s->error, f.err);
+    if (f.nact) atomicAdd(&s->n_active, f.nact);
+    atomicMax(&s->t_last, f.t_end);
+    if (s->n_pending) *halt = 1u;
+}
+
+// round i of a ticketless batch: shares of round i go to parts[i & 1]
+// (argument order: what the first memory round trip needs comes first, so
+// that one scalar load batch brings all of it)
+__global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, DevSummary* __restrict__ prev,
+                                                      const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
+                                                      const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
+                                                      DRoundArgs a) {
+    const DParams& P = *Pp;
+#ifdef SHD_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = wall_clock64();
+#endif
+    const unsigned long long t_entry = wall_clock64();   // the round's start on the device clock (t_first)
+    const uint32_t nblk = a.nblk;   // == gridDim.x, without the dispatch-packet load
+    // all scalar arguments in the first load batch (the compiler otherwise
+    // fetches some after the first vector loads are issued, one level later)
+    asm volatile("" ::"s"(i), "s"(prev), "s"(ctl), "s"(parts), "s"(nblk), "s"(a.nloc), "s"(a.hpw), "s"(window));
+    // the window start's inputs go out first: halt, the control words, the
+    // previous round's summary and its shares (round 0 of the batch starts at
+    // the seeded time; later rounds fold the previous round's shares, whose
+    // first-touch log count halts).  The host-state loads follow; the window
+    // start then waits for its own loads only (vmcnt counts in issue order)
+    uint32_t halt = *a.halt;
+    uint64_t stop = ctl->stop, rbase = ctl->round_base, ws0 = prev->next_time, npend = prev->n_pending;
+    const TlPart* pp = parts + (size_t)((i - 1) & 1) * nblk;
+    TlPart pv[4];
+    if (i > 0) tl_issue(pp, nblk, 0, pv);
+    const uint32_t warm = params_warm(Pp);
+    HostIn in;
+    host_in_load(a, in);
+    // consumed only here, once every load is out (the compiler would
+    // otherwise move their scalar copies, and the waits, above the rest)
+    asm volatile("" : "+v"(halt), "+v"(stop), "+v"(rbase), "+v"(ws0), "+v"(npend));
+    // every block needs the shares' min next time; block 0 folds the rest
+    // of them too, for the summary
+    TlPart f{kInf, 0, 0, 0, 0, 0};
+    if (i > 0) {
+        tl_fold4(f, pv, nblk, 0);
+        for (uint32_t base = 256; base < nblk; base += 256) {   // grids above 256 blocks
+            tl_issue(pp, nblk, base, pv);
+            tl_fold4(f, pv, nblk, base);
+        }
+        tl_reduce(f, blockIdx.x == 0);
+    }
+    const uint64_t ws = f.next < ws0 ? f.next : ws0;
+    params_warm_done(warm);
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    if (lead && i > 0) tl_publish(prev, f, (uint32_t*)a.halt);
+    TlPart* mine = parts + (size_t)(i & 1) * nblk + blockIdx.x;
+    if ((halt != 0) | (i > 0 && npend != 0) | (ws >= stop)) {
+        if (halt == 0 && !(i > 0 && npend != 0)) {   // only forwards the time
+            if (lead) {
+                atomicMin(&P.sum->t_first, t_entry);
+                *init = fresh_summary();
+                P.sum->ws = ws;
+            }
+            if (threadIdx.x == 0) *mine = TlPart{ws, (unsigned long long)wall_clock64(), 0, 0, 0, 0};
+        }
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, t_entry);
+        *init = fresh_summary();
+        P.sum->ws = ws;
+    }
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    uint64_t next, nev, npkt;
+    uint32_t err;
+    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    TIM(4);
+    const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));   // hosts that executed an event
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0)
+        *mine = TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, nact};
+    TIM(5);
+}
+
+// after a ticketless batch: publish its last round (shares in parts[(n-1) & 1])
+__global__ __launch_bounds__(64) void k_fold_tl(const TlPart* __restrict__ parts, uint32_t nblk, int last,
+                                                DevSummary* __restrict__ s, uint32_t* __restrict__ halt) {
+    const TlPart f = tl_gather(parts + (size_t)(last & 1) * nblk, nblk);
+    if (threadIdx.x == 0 && *halt == 0u) tl_publish(s, f, halt);
+}
+
+// ingest events from other engines into inbox[parity]
+__global__ void k_ingest(DParams P, const shd_event* __restrict__ ev, uint64_t n, int parity) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const shd_event e = ev[i];
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    if (dl < 0 || dl >= P.nloc) { atomicOr(&P.sum->error, SHD_ERR_REMOTE_OVERFLOW); return; }
+    uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+    if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
+    P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+}
+
+// caller-pushed self events (shd_eng_push_events): one thread per host with
+// pushed events, in array order.  event_new_ consumes the host's next event ID
+// (event.c:38); scheduler_push drops a time >= end (scheduler.c:346-349); the
+// rest go to the inbox the next round merges into the host's heap
+__global__ void k_push(DParams P, const shd_event* __restrict__ ev, const uint32_t* __restrict__ grp_off,
+                       uint32_t ngrp, int parity) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ngrp) return;
+    const uint32_t b = grp_off[g], en = grp_off[g + 1];
+    const int32_t dl = (int32_t)ev[b].dst - P.h0;
+    const uint64_t seq0 = P.hs[dl].ev_seq;
+    uint64_t seq = seq0;
+    uint64_t next = kInf;
+    uint32_t err = 0;
+    for (uint32_t i = b; i < en; i++) {
+        shd_event e = ev[i];
+        e.seq = seq++;
+        if (e.time >= P.end_time) continue;
+        const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+        if (slot >= P.inbox_cap) { err |= SHD_ERR_INBOX_OVERFLOW; continue; }
+        P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+        next = e.time < next ? e.time : next;
+    }
+    // the record keeps a live timer's ID as its distance back from ev_seq
+    // (store_ctx): the IDs consumed here move ev_seq, not the timers' IDs
+    HostRec& r = P.hs[dl];
+    for (int k = 0; k < 3; k++) {
+        if (r.tt[k] == kInf) continue;
+        const uint64_t back = (uint64_t)r.ts_back[k] + (seq - seq0);
+        if (back >> 32) err |= SHD_ERR_INTERNAL;
+        r.ts_back[k] = (uint32_t)back;
+    }
+    r.ev_seq = seq;
+    if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
+    if (err) atomicOr(&P.sum->error, err);
+}

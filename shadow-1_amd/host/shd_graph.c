@@ -257,12 +257,21 @@ int shd_graph_check(const shd_graph* g, shd_graph_props* out) {
 }
 
 /* ------------------------------------------------------------------ attach */
+/* address_stringToIP (address.c:145-152): inet_pton, the network-order s_addr,
+ * INADDR_NONE when the string does not parse (strictly dotted-quad decimal:
+ * no "10.1", no octal or hex parts) */
+static uint32_t string_to_ip(const char* s) {
+    struct in_addr a;
+    if (s && inet_pton(AF_INET, s, &a) == 1) return a.s_addr;
+    return INADDR_NONE;
+}
+/* a usable IP (topology.c:2123-2128, 2261-2267): the network-order value is
+ * compared with the HOST-order constants as the reference does, so on x86-64
+ * "127.0.0.1" is usable and "1.0.0.127" (s_addr == INADDR_LOOPBACK) is not */
 static int ip_usable(const char* s, uint32_t* ip) {
     if (!s) return 0;
-    struct in_addr a;
-    if (inet_aton(s, &a) == 0) return 0;
-    uint32_t v = a.s_addr;
-    if (v == INADDR_NONE || v == htonl(INADDR_ANY) || v == htonl(INADDR_LOOPBACK)) return 0;
+    const uint32_t v = string_to_ip(s);
+    if (v == INADDR_NONE || v == INADDR_ANY || v == INADDR_LOOPBACK) return 0;
     *ip = v;
     return 1;
 }
@@ -323,10 +332,8 @@ int shd_topology_attach_cb(const shd_graphml* gm, double (*next_double)(void*), 
         uint32_t best = 0;
         for (int32_t i = 0; i < n; i++) {
             int32_t v = q[pick][i];
-            uint32_t vip = 0;
-            const char* s = gm->vertex_ip ? gm->vertex_ip[v] : NULL;
-            struct in_addr a;
-            vip = (s && inet_aton(s, &a)) ? a.s_addr : INADDR_NONE;
+            /* every candidate's IP as parsed, usable or not (topology.c:2232-2236) */
+            const uint32_t vip = string_to_ip(gm->vertex_ip ? gm->vertex_ip[v] : NULL);
             uint32_t match = ~(vip ^ req_ip);
             if (match > best || best == 0) { best = match; vertex = v; }
         }

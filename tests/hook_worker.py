@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Scenarios that need a semantics-changing test hook -- TEST INFRASTRUCTURE.
+
+The hooks (SHD_FORCE_AMBIG: every undecided first-touch send counts as
+ambiguous; SHD_PROTECT_ALL: every round behind a state copy) exist only in the
+test build libshdgpu_th.so (-DSHD_TEST_HOOKS).  tests/test_engine_gpu.py runs
+each scenario here in a child process with SHDGPU_LIB pointing at that build,
+so the pytest process itself only ever loads the product library.  The child
+checks the run against the serial oracle bit for bit and prints one JSON line
+of run statistics; any mismatch is an assertion (non-zero exit).
+"""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(os.path.dirname(HERE), "shadow-1_amd"), HERE]
+
+import numpy as np  # noqa: E402
+
+
+def engine_rollback(hpv):
+    import oracle_ffi as O
+    import workloads as W
+    import shdgpu as S
+    from sim import Engine, PathCache, sort_trace
+    g = W.geometric_graph(200, seed=4)
+    m = W.phold_model(W.hosts_on_vertices(200, hpv), end_time=3 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    eng = Engine(m, pc)
+    st = eng.run()
+    otr, odg, ost = O.engine_run(m, g)
+    assert st.n_events == ost["n_events"] and st.n_pkt_events == ost["n_pkt_events"]
+    assert np.array_equal(sort_trace(eng.trace()), sort_trace(otr))
+    assert np.array_equal(eng.digest(), odg)
+    return dict(rerun=st.n_rounds_rerun, protected=st.n_rounds_protected, rounds=st.n_rounds)
+
+
+def group_rollback(parts):
+    import oracle_ffi as O
+    import workloads as W
+    import shdgpu as S
+    from driver import partition
+    from sim import Engine, PathCache, XGroup, sort_trace
+    g = W.geometric_graph(200, seed=5)
+    m = W.phold_model(W.hosts_on_vertices(200, 2), end_time=3 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    pb = partition(m.n_hosts, parts)
+    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
+    grp = XGroup.local(engines)
+    pkt = rerun = prot = rounds = 0
+    for t in (int(1.0 * S.SHD_SEC) + 3, m.params["end_time"]):
+        st = grp.run_until(t)
+        pkt += st.n_pkt_events
+        rerun += st.n_rounds_rerun
+        prot += st.n_rounds_protected
+        rounds += st.n_rounds
+    tr = sort_trace(np.concatenate([e.trace() for e in engines]))
+    dg = np.concatenate([e.digest() for e in engines])
+    otr, odg, ost = O.engine_run(m, g)
+    assert pkt == ost["n_pkt_events"]
+    assert np.array_equal(tr, sort_trace(otr))
+    assert np.array_equal(dg, odg)
+    grp.close()
+    return dict(rerun=rerun, protected=prot, rounds=rounds)
+
+
+SCENARIOS = {"engine_rollback": engine_rollback, "group_rollback": group_rollback}
+
+
+def main():
+    import shdgpu as S
+    assert os.path.basename(S.LIB_PATH) == "libshdgpu_th.so", S.LIB_PATH
+    name, arg = sys.argv[1], int(sys.argv[2])
+    print(json.dumps(SCENARIOS[name](arg)))
+
+
+if __name__ == "__main__":
+    main()

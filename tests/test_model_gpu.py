@@ -117,6 +117,33 @@ def test_pushed_application_starts_match_oracle():
     assert_same_run(eng, st.n_pkt_events, m, g, pushes=pushes)
 
 
+def test_pushed_starts_at_the_first_heartbeat_keep_timer_ids():
+    """Several processes per host starting exactly at the first heartbeat
+    (1 s): the pushes consume event IDs after the boot timers were armed, so
+    the heartbeat (ID 0) and the pending refill keep their IDs and run before
+    the starts in (time, src, seq) order (event.c:110-153).  A shift of the
+    timers' IDs by the pushed count would put the starts first and change the
+    heartbeat counters and every later ID (advisor finding, round 2)."""
+    V = 80
+    g = W.geometric_graph(V, seed=13)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=3 * S.SHD_SEC, trace=True, load=3,
+                      queue_flags=S.SHD_QF_NO_APP_START | S.SHD_QF_HEARTBEATS)
+    ev = []
+    for h in range(V):
+        for _ in range(4 + h % 3):   # 4..6 processes per host, all at 1 s
+            ev.append((S.SHD_SEC, 0, h, h, 0, S.EV_APP_START))
+    pushes = np.array(ev, dtype=S.EVENT_DTYPE)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    eng = Engine(m, pc)
+    eng.boot()
+    eng.push_events(pushes)
+    st = eng.run()
+    K = (3 * S.SHD_SEC - 1) // S.SHD_SEC
+    ohb = np.zeros((V, K, 2), dtype=np.uint32)
+    assert_same_run(eng, st.n_pkt_events, m, g, pushes=pushes, heartbeats=ohb)
+    assert np.array_equal(eng.heartbeats(), ohb)
+
+
 def test_push_events_rejects_what_it_cannot_take():
     V = 60
     g = W.geometric_graph(V, seed=7)

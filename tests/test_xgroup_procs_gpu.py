@@ -27,6 +27,10 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+# the test build with the semantics-changing hooks (-DSHD_TEST_HOOKS), for the ranks that need one
+TH_LIB = os.path.join(os.path.dirname(HERE), "shadow-1_amd", "libshdgpu_th.so")
+
+
 def run_ranks(world, tmp_path, extra=(), env_extra=None, timeout=240):
     name = "shdtest_" + uuid.uuid4().hex[:16]
     env = dict(os.environ)
@@ -125,7 +129,7 @@ def test_multiprocess_group_rolls_back_ambiguous_rounds(p2p, tmp_path):
     state copy, ranked from the logs all-gathered from every rank, rerun
     (p2p: the rerun's exchanges take new tags)."""
     res = run_ranks(2, tmp_path, extra=["--vertices", "160", "--hpv", "2"] + (["--p2p"] if p2p else []),
-                    env_extra={"SHD_FORCE_AMBIG": "1", "SHD_PROTECT_ALL": "1"})
+                    env_extra={"SHD_FORCE_AMBIG": "1", "SHD_PROTECT_ALL": "1", "SHDGPU_LIB": TH_LIB})
     check_against_oracle(res, 160, 2, 3.0, 0.01, 16)
     assert all(int(r["stats"][5]) > 0 for r in res)            # reruns happened on every rank
 
@@ -135,6 +139,6 @@ def test_p2p_mapping_failure_on_one_rank_fails_every_rank_alike(tmp_path):
     in both all-gathers of the mapping: every rank gets SHD_ENODEV from
     shd_xgroup_create_p2p, none waits forever, and all fall back to the
     all-to-all transport (as bench.py does) and still match the oracle."""
-    res = run_ranks(2, tmp_path, extra=["--p2p"], env_extra={"SHD_P2P_FAIL_RANK": "1"})
+    res = run_ranks(2, tmp_path, extra=["--p2p"], env_extra={"SHD_P2P_FAIL_RANK": "1", "SHDGPU_LIB": TH_LIB})
     check_against_oracle(res, 240, 1, 3.0, 0.01, 16)
     assert all(int(r["stats"][6]) == 1 for r in res)
