@@ -462,6 +462,28 @@ _STATUS_OF = {
 }
 
 
+# the delivery-status flags (packet.h:19-41), by the names packet_toString prints
+STATUS_FLAG = {
+    "SND_CREATED": 1 << 1, "SND_TCP_ENQUEUE_THROTTLED": 1 << 2, "SND_TCP_ENQUEUE_RETRANSMIT": 1 << 3,
+    "SND_TCP_DEQUEUE_RETRANSMIT": 1 << 4, "SND_TCP_RETRANSMITTED": 1 << 5, "SND_SOCKET_BUFFERED": 1 << 6,
+    "SND_INTERFACE_SENT": 1 << 7, "INET_SENT": 1 << 8, "INET_DROPPED": 1 << 9, "ROUTER_ENQUEUED": 1 << 10,
+    "ROUTER_DEQUEUED": 1 << 11, "ROUTER_DROPPED": 1 << 12, "RCV_INTERFACE_RECEIVED": 1 << 13,
+    "RCV_INTERFACE_DROPPED": 1 << 14, "RCV_SOCKET_PROCESSED": 1 << 15, "RCV_SOCKET_DROPPED": 1 << 16,
+    "RCV_TCP_ENQUEUE_UNORDERED": 1 << 17, "RCV_SOCKET_BUFFERED": 1 << 18, "RCV_SOCKET_DELIVERED": 1 << 19,
+}
+
+
+def status_line(name: str, host_id: int, pkt: int, src_ip, sport: int, dst_ip, dport: int, payload: int,
+                history) -> str:
+    """One [STATUS] line of a UDP datagram: `[<name>] ` + packet_toString
+    (packet.c:518-547 UDP header part, 616-633 the ordered status list), as
+    packet_addDeliveryStatus logs it (packet.c:647-659); `history` is the
+    datagram's status list including `name`."""
+    return "[%s] packetID=%u:%u %s:%u -> %s:%u bytes=%u status=%s" % (
+        name, host_id, pkt, ip_string(src_ip), sport, ip_string(dst_ip) if dst_ip is not None else "?", dport,
+        payload, ",".join(history))
+
+
 def ip_string(ip) -> str:
     """A host address as address_ipToNewString prints it (dotted quad); `ip` is
     a dotted string or a host-order integer."""
@@ -481,7 +503,10 @@ def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int =
     draw (the CREATED record).  Order: by (time, host), records of one host in
     the engine's order, except that a datagram sent in the instant it was
     created follows its creation at once, as in the reference's call chain
-    (sendto -> networkinterface_wantsSend -> _networkinterface_sendPackets)."""
+    (sendto -> networkinterface_wantsSend -> _networkinterface_sendPackets).
+    Each packet object's release logs a PDS_DESTROYED line (packet.c:198) where
+    its last reference goes during the run; the frees at the simulation's
+    teardown (datagrams still queued or unread at the end) are not included."""
     tr = np.asarray(trace, dtype=TRACE_DTYPE)
     if host_ids is None:
         host_ids = [h + 1 for h in range(len(ips))]
@@ -511,12 +536,32 @@ def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int =
         src, pkt = key
         st = hist.setdefault(key, [])
         d = dst.get(key, NONE)
-        head = "packetID=%u:%u %s:%u -> %s:%u bytes=%u" % (
-            host_ids[src], pkt, ip_string(ips[src]), port.get(key, 0),
-            ip_string(ips[d]) if d != NONE else "?", listen_port, payload)
         for name in statuses:
             st.append(name)
-            out.append((t, at, "[%s] %s status=%s" % (name, head, ",".join(st))))
+            out.append((t, at, status_line(name, host_ids[src], pkt, ips[src], port.get(key, 0),
+                                           ips[d] if d != NONE else None, listen_port, payload, st)))
+
+    arrived = {(int(r["peer"]), int(r["pkt"])) for r in tr if int(r["kind"]) == TR_ARRIVE}
+
+    def destroyed(t, at, key, copy_dropped=False):
+        # packet_unref's last reference (packet.c:194-201) logs PDS_DESTROYED with
+        # the object's list.  A sent datagram is two objects from INET_SENT on
+        # (worker.c:306-313 copies it for the receiver): the sender's original
+        # is released at once (network_interface.c:577), after the copy when
+        # scheduler_push dropped the copy's event past the end (scheduler.c:346-349)
+        d = dst.get(key, NONE)
+        st = hist[key] + ["PDS_DESTROYED"]
+        line = status_line("PDS_DESTROYED", host_ids[key[0]], key[1], ips[key[0]], port.get(key, 0),
+                           ips[d] if d != NONE else None, listen_port, payload, st)
+        for _ in range(2 if copy_dropped else 1):
+            out.append((t, at, line))
+
+    def send_side(t, h, key, k):
+        emit(t, h, key, _STATUS_OF[k])
+        if k == TR_SENT:
+            destroyed(t, h, key, copy_dropped=key not in arrived)
+        elif k == TR_INET_DROP:
+            destroyed(t, h, key)
 
     for i, r in enumerate(tr):
         k, h, p, t = int(r["kind"]), int(r["host"]), int(r["pkt"]), int(r["time"])
@@ -526,13 +571,15 @@ def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int =
             emit(t, h, (h, p), _STATUS_OF[k])
             j = sends.get((h, p))
             if j is not None:
-                emit(t, h, (h, p), _STATUS_OF[int(tr[j]["kind"])])
+                send_side(t, h, (h, p), int(tr[j]["kind"]))
         elif k in (TR_SENT, TR_INET_DROP, TR_LOCAL):
-            emit(t, h, (h, p), _STATUS_OF[k])
+            send_side(t, h, (h, p), k)
         elif k == TR_READ:
             q = inbox.get(h)
             if q:
-                emit(t, h, q.pop(0), _STATUS_OF[k])
+                key = q.pop(0)
+                emit(t, h, key, _STATUS_OF[k])
+                destroyed(t, h, key)   # the socket's reference, udp.c:169
         else:   # the receiver's records name the packet by (source, pkt)
             key = (int(r["peer"]), p)
             names = _STATUS_OF[k]
@@ -541,4 +588,8 @@ def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int =
             emit(t, h, key, names)
             if k == TR_RECV:
                 inbox.setdefault(h, []).append(key)
+            elif k in (TR_CODEL_DROP, TR_IF_DROP):
+                # the queue's reference (router_queue_codel.c), or the interface's
+                # (network_interface.c:446) / the local task's (:553): the last one
+                destroyed(t, h, key)
     return out

@@ -3,11 +3,13 @@ registration order, `quantity` naming (master.c:304-320), hints and overrides
 (configuration.c:404-480), DNS addresses (dns.c:40-134, 183-196; host.c:166-167),
 and the inline-graphml topology through the product loader.
 
-The expected addresses below are restated by hand from dns.c: the counter
-starts at 11.0.0.0 and is pre-incremented, reserved ranges and taken
-addresses are skipped, a hint is kept when it is unrestricted and not taken,
-and 127.0.0.1 stays local.  No reference run backs them (Shadow cannot be
-built here): parity unpinned beyond that restatement.
+The expected addresses below (the counter starts at 11.0.0.0 and is
+pre-incremented, reserved ranges and taken addresses are skipped, a hint is
+kept when it is unrestricted and not taken, and 127.0.0.1 stays local) are
+the reference's own: this CONFIG's hosts are case 0 of tests/golden/ref_net.json,
+which the reference's dns.c compiled unmodified produced
+(tests/golden/make_ref_net.py); test_ref_net_cpu.py checks them and two more
+cases against that fixture.
 """
 import os
 

@@ -1,7 +1,8 @@
 """The [STATUS] packet lines (packet_addDeliveryStatus / packet_toString,
 packet.c:518-659) from a status trace (SHD_QF_TRACE_STATUS), on a hand-built
 trace whose expected lines follow the reference's call chain, and on an
-oracle run (every datagram's statuses well formed)."""
+oracle run (every datagram's statuses well formed).  The line format and each
+fate's lines are pinned to the reference's packet.c in test_ref_net_cpu.py."""
 import numpy as np
 
 import oracle_ffi as O
@@ -37,14 +38,17 @@ def test_status_lines_follow_the_reference_call_chain():
         (1000, 0, "[SND_SOCKET_BUFFERED] " + a + "SND_CREATED,SND_SOCKET_BUFFERED"),
         (1000, 0, "[SND_INTERFACE_SENT] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT"),
         (1000, 0, "[INET_SENT] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,INET_SENT"),
+        # the sender releases its original at once; the copy travels on
+        (1000, 0, "[PDS_DESTROYED] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,INET_SENT,"
+                                           "PDS_DESTROYED"),
         (2000, 1, "[ROUTER_ENQUEUED] " + a + "SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,INET_SENT,"
                                              "ROUTER_ENQUEUED"),
     ]
-    assert lines[:5] == want
+    assert lines[:6] == want
     seq_a = [l for t, h, l in lines if "packetID=7:5" in l]
-    assert seq_a[-1].startswith("[RCV_SOCKET_DELIVERED] ")
+    assert seq_a[-2].startswith("[RCV_SOCKET_DELIVERED] ")
     assert seq_a[-1].endswith("ROUTER_ENQUEUED,ROUTER_DEQUEUED,RCV_INTERFACE_RECEIVED,RCV_SOCKET_PROCESSED,"
-                              "RCV_SOCKET_BUFFERED,RCV_SOCKET_DELIVERED")
+                              "RCV_SOCKET_BUFFERED,RCV_SOCKET_DELIVERED,PDS_DESTROYED")   # the read releases it
     assert [t for t, h, l in lines if "packetID=7:5" in l][-1] == 2001
     seq_b = [l for t, h, l in lines if "packetID=8:0" in l]
     assert seq_b[-1].endswith("status=SND_CREATED,SND_SOCKET_BUFFERED,SND_INTERFACE_SENT,RCV_INTERFACE_RECEIVED,"
@@ -67,9 +71,14 @@ def test_oracle_status_trace_is_well_formed():
     for t, h, l in lines:
         by_pkt.setdefault(l.split()[1], []).append(l.split("status=")[1].split(","))
     for key, sts in by_pkt.items():
-        last = sts[-1]
+        live = [x for x in sts if x[-1] != "PDS_DESTROYED"]
+        last = live[-1]
         assert last[:2] == ["SND_CREATED", "SND_SOCKET_BUFFERED"], key
-        assert all(s == last[:len(s)] for s in sts)          # each line's list extends the previous
+        assert all(x == last[:len(x)] for x in live)          # each line's list extends the previous
+        # a release closes one object's list: the list it ends is one of the packet's lists
+        for x in sts:
+            if x[-1] == "PDS_DESTROYED":
+                assert x[:-1] in live, key
     # without the flag the trace has no application records
     m2 = W.phold_model(W.hosts_on_vertices(V, 1), end_time=2 * S.SHD_SEC, trace=True, load=3)
     otr2, _, _ = O.engine_run(m2, g)
