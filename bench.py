@@ -80,6 +80,28 @@ def parse():
     return ap.parse_args()
 
 
+class Roctx:
+    """roctx ranges (libroctx64) around the timed region, so that a
+    `rocprofv3 --marker-trace --kernel-trace` run of this script can restrict
+    its kernel statistics to the timed region (scripts/rocprof_timed.py);
+    without the profiler they cost nothing.  Absent library: no markers."""
+    def __init__(self):
+        import ctypes
+        try:
+            self.lib = ctypes.CDLL("libroctx64.so")
+            self.lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+        except OSError:
+            self.lib = None
+
+    def push(self, name):
+        if self.lib is not None:
+            self.lib.roctxRangePushA(name.encode())
+
+    def pop(self):
+        if self.lib is not None:
+            self.lib.roctxRangePop()
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -250,11 +272,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    mark = Roctx()
     barrier()
+    mark.push("shd_timed_region")
     t0 = time.perf_counter()
     st = run(end_time)
     barrier()
     t1 = time.perf_counter()
+    mark.pop()
     elapsed = t1 - t0
     if world > 1 and not use_group:
         pkt, evs, rounds, kms, ems = st.pkt_events, st.events, st.rounds, st.kernel_ms, st.kernel_ms
@@ -277,11 +302,12 @@ def main():
     protected = {k: int(getattr(wst, k, 0)) + int(getattr(st, k, 0))
                  for k in ("n_rounds_protected", "n_rounds_rerun")}
 
-    # roofline of the round kernel (per launch = per rank-round).  The launch
-    # duration is the HIP-event time of the round launches on the engine's
-    # stream over the timed region (batches of 64 graph-launched rounds; it
-    # includes the gaps between launches); the device-clock time inside the
-    # kernel (first block start to last block end) is reported beside it.
+    # roofline of the round kernel, per round (per rank-round).  The round's
+    # duration is the HIP-event time of the batches on the engine's stream over
+    # the timed region divided by their rounds (a batch is one persistent
+    # launch of up to 128 rounds, k_round_ps, or 64 graph-launched round
+    # kernels; either way the gaps between launches are included); the
+    # device-clock time of the rounds themselves is reported beside it.
     launches = rounds * max(world, 1)
     alg_bytes = BYTES_PER_PKT_EVENT * pkt_all + BYTES_PER_HOST_ROUND * hr_all
     avg_launch_ms = (ems_all if ems_all > 0 else kms_all) / max(launches, 1)
@@ -290,10 +316,17 @@ def main():
     # once no first touch is logged), the engine group's k_round_x across GPUs
     # (peer-to-peer rounds after a batch's first are k_round_px, which also completes the exchange)
     fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and "completes the previous" in exchange
-    kname = ("k_round_px" if fused else "k_round_xtl") if use_group else ("k_round" if world > 1 else "k_round_tl")
+    n_ps = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_persistent", 0))
+    n_bat = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches", 0))
+    kname = ("k_round_px" if fused else "k_round_xtl") if use_group else \
+        ("k_round" if world > 1 else ("k_round_ps" if n_ps and 2 * n_ps >= n_bat else "k_round_tl"))
+    wkey = "%s-%dh" % (args.workload, H // max(world, 1))
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(kname),
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(wkey, kname),
+                "traffic_key": wkey + "/" + kname,
                 "kernel": kname, "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+                "avg_round_us": round(avg_launch_ms * 1e3, 3),
+                "rounds_per_launch": round(rounds / max(n_bat, 1), 1) if n_bat else None,
                 "avg_in_kernel_us": round(kms_all / max(launches, 1) * 1e3, 3),
                 "launches": int(launches), "bytes_per_launch": round(alg_bytes / max(launches, 1), 1),
                 "alg_bytes": "SURVEY.md 8(d): 80 B x packet events + 136 B x active host-rounds",
@@ -350,6 +383,7 @@ def main():
             "rounds": int(rounds),
             "timed_batches": None if (world > 1 and not use_group) else int(getattr(st, "n_batches", 0)),
             "timed_batches_ticketless": None if (world > 1 and not use_group) else int(st.n_batches_ticketless),
+            "timed_batches_persistent": None if (world > 1 and not use_group) else n_ps,
             "first_touch": protected,
             "apsp": {"rows": int(info.rows_computed), "vertices": V, "build_ms": round(min(builds), 3),
                      "sssp_kernel_ms": round(info.build_ms_sssp, 3), "iterations": int(info.sssp_iterations_max),
@@ -403,20 +437,31 @@ def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, t
             "note": "lost messages are never regenerated: the rate depends on the simulated window"}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per round-kernel launch from the committed rocprofv3 PMC
-    passes (profiles/r02/k_round_pmc_bytes.json: FETCH_SIZE x 2 + WRITE_SIZE,
-    the gfx950 correction), used only when that profile was taken of the
-    kernel source being run; else None."""
+def engine_source_sha1():
+    """SHA-1 over the engine's translation unit (engine.hip and its parts)"""
     import hashlib
+    h = hashlib.sha1()
+    d = os.path.join(REPO, "shadow-1_amd", "csrc")
+    for f in ("engine.hip", "eng_device.h", "eng_round.h", "eng_exchange.h", "eng_group.h", "shd_device.h"):
+        h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
+
+def pmc_traffic(workload, kernel):
+    """HBM bytes per round of the round kernel from the committed rocprofv3
+    PMC passes of THIS workload and kernel (profiles/r03/pmc_traffic.json,
+    scripts/pmc_traffic.py: FETCH_SIZE x the calibrated read correction +
+    WRITE_SIZE, over the timed region's dispatches), used only when they were
+    taken of the engine source being run; else None (no inherited numbers)."""
     try:
-        prof = json.load(open(os.path.join(REPO, "profiles", "r02", "k_round_pmc_bytes.json")))
-        src = open(os.path.join(REPO, "shadow-1_amd", "csrc", "engine.hip"), "rb").read()
+        prof = json.load(open(os.path.join(REPO, "profiles", "r03", "pmc_traffic.json")))
+        sha = engine_source_sha1()
     except (OSError, ValueError):
         return None
-    if prof.get("engine_source_sha1") != hashlib.sha1(src).hexdigest() or prof.get("kernel") != kernel:
+    if prof.get("engine_source_sha1") != sha:
         return None
-    return prof.get("hbm_bytes_per_round_timed", prof.get("hbm_bytes_per_dispatch"))
+    ent = prof.get("entries", {}).get(workload + "/" + kernel)
+    return None if ent is None else ent.get("hbm_bytes_per_round")
 
 
 def cpu_threads():

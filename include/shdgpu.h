@@ -413,7 +413,10 @@ typedef struct shd_run_stats {
     uint64_t n_host_rounds;         /* (host, round) pairs in which the host executed at least
                                        one event: the host-state reads of SURVEY.md 8(d) */
     uint64_t n_batches;             /* device batches launched (shd_eng: 64 round launches
-                                       each; shd_xgroup: up to 64 rounds each) */
+                                       each, or one persistent launch of 128 rounds;
+                                       shd_xgroup: up to 64 rounds each) */
+    uint64_t n_batches_persistent;  /* shd_eng batches run as one persistent launch
+                                       (k_round_ps: the round grid fits the GPU) */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

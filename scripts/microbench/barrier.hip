@@ -48,13 +48,15 @@ __global__ __launch_bounds__(64) void k_pers(uint4* __restrict__ shares, uint4* 
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (lane == 0) st16_sc1(&shares[b], make_uint4(b, r, acc, tag));
+        // parity slots: a block can run one round ahead of a slow poller, never two
+        uint4* sh = shares + (size_t)(r & 1) * kGrid;
+        if (lane == 0) st16_sc1(&sh[b], make_uint4(b, r, acc, tag));
         // poll every block's share of round r
         const unsigned long long t0 = wall_clock64();
         for (;;) {
             bool ok = true;
             for (unsigned j = lane; j < (unsigned)kGrid; j += 64) {
-                const uint4 s = ld16_sc1(&shares[j]);
+                const uint4 s = ld16_sc1(&sh[j]);
                 ok = ok && s.w == tag;
                 acc += s.z;
             }
@@ -87,6 +89,7 @@ static void run(hipStream_t s, uint4* shares, uint4* slots, unsigned long long* 
     unsigned hb = 0;
     CK(hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost));
     printf("%-52s %6.2f us per round%s\n", name, best, hb ? "  (FAILED: stale or timeout)" : "");
+    CK(hipMemset(bad, 0, 4));
 }
 
 int main() {
@@ -95,11 +98,11 @@ int main() {
     uint4 *shares, *slots;
     unsigned long long* stamps;
     unsigned* bad;
-    CK(hipMalloc(&shares, kGrid * 16));
+    CK(hipMalloc(&shares, 2 * kGrid * 16));
     CK(hipMalloc(&slots, 2 * kGrid * 64 * 16));
     CK(hipMalloc(&stamps, kRounds * 8));
     CK(hipMalloc(&bad, 4));
-    CK(hipMemset(shares, 0, kGrid * 16));
+    CK(hipMemset(shares, 0, 2 * kGrid * 16));
     CK(hipMemset(slots, 0, 2 * kGrid * 64 * 16));
     CK(hipMemset(bad, 0, 4));
     unsigned tag0 = 1;

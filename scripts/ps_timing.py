@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Per-block phase stamps of the persistent round kernel (k_round_ps), from
+the timing build:
+
+    make -C shadow-1_amd timing TIMING_FLAGS=-DSHD_TIMING_LIGHT
+    SHDGPU_LIB=shadow-1_amd/libshdgpu_tim.so python3 scripts/ps_timing.py
+
+Stamps (100 MHz wall clock; every stamp first drains the wave's memory ops):
+0 round start, 1 hand-off words read (idle test), 2 bins + inbox merged and
+sorted, 3 last flush starts, 4 event loop + flushes done, 5 close done
+(bin resets, last deliveries), 6 share published (drained), 7 every share of
+the round seen.  Printed relative to the round's earliest start: mean over
+rounds of the mean and the max over blocks; and the phase durations.
+"""
+import ctypes as C
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "shadow-1_amd")]
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--vertices", type=int, default=10000)
+    ap.add_argument("--hosts", type=int, default=10000)
+    ap.add_argument("--load", type=int, default=16)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    import shdgpu as S
+    import workloads as W
+    from sim import Engine, PathCache
+    lib = S.lib()
+    f = lib.shd_debug_timing
+    f.restype = C.c_int
+    f.argtypes = [C.POINTER(C.c_uint64)]
+    g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0)
+    hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
+    m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load, payload=1)
+    pc = PathCache(g, W.attached_vertices(hv), device=0)
+    pc.build()
+    eng = Engine(m, pc, 0, a.hosts, device=0)
+    eng.boot()
+    eng.run_until(2 * S.SHD_SEC)
+    st = eng.run_until(int(2.06 * S.SHD_SEC))   # under one persistent batch: its rounds leave their stamps
+    print(f"persistent batches {st.n_batches_persistent} of {st.n_batches}, rounds {st.n_rounds}, "
+          f"{st.device_ms_launches / max(st.n_rounds, 1) * 1e3:.2f} us/round (HIP events)")
+    buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
+    f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
+    t = buf.reshape(64, 2048, 20).astype(np.int64)
+    grid = (a.hosts + 63) // 64
+    t = t[:, :grid, :8]
+    rows = []
+    for r in range(64):
+        x = t[r]
+        t0 = x[:, 0].min()
+        if t0 == 0 or (x[:, 6:8] < t0).any():
+            continue
+        rel = (x - t0) / 100.0
+        rel[x < t0] = np.nan    # a phase no lane of the block reached this round (no active host)
+        rows.append(rel)
+    rows = np.array(rows)
+    names = ["start", "words read", "bins merged", "last flush", "loop done", "close done", "published", "all seen"]
+    print(f"{len(rows)} rounds; us from the round's earliest block start: mean over rounds of (mean, max over blocks)")
+    for k in range(8):
+        v = rows[:, :, k]
+        print(f"  {k} {names[k]:12s} mean {np.nanmean(v):6.2f}  max {np.nanmean(np.nanmax(v, axis=1)):6.2f}")
+    per = np.diff(np.nanmax(rows[:, :, 7], axis=1))
+    print(f"  round period (max 'all seen' to the next) {np.mean(per[per > 0]):.2f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -635,6 +635,22 @@ __device__ __forceinline__ bool cal_push(const DParams& P, int32_t dl, const shd
     return true;
 }
 
+// An event handed to another host's calendar or inbox: four agent-scope
+// 8-B stores (global_store_dwordx2 sc1: written through to memory, the line
+// dropped from the writer's L2), counted by the compiler like plain stores.
+// The persistent rounds (k_round_ps) read such events in a later round of
+// the same launch, on another CU and possibly another XCD, with sc1 loads
+// after every writer drained (MI355X_MICROARCH.md, inter-workgroup
+// visibility: sc1 stores + sc1 loads); the launch-per-round kernels read them
+// after a kernel boundary, for which a plain store would do as well.
+__device__ __forceinline__ void ev_st_sc1(shd_event* p, const shd_event& e) {
+    uint64_t* d = (uint64_t*)p;
+    __hip_atomic_store(d + 0, (uint64_t)e.time, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 1, (uint64_t)e.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 2, ((uint64_t)e.dst << 32) | e.src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(d + 3, ((uint64_t)e.kind << 32) | e.pkt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // a 16-B write-through (system-scope) store: the line leaves every cache on
 // the way (peer-to-peer receive blocks).  hipcc does not count it: its
 // writers drain with an explicit s_waitcnt vmcnt(0); the s_nop keeps the
@@ -655,7 +671,7 @@ __device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
     if (dl >= 0 && dl < P.nloc) {
         uint32_t slot = atomicAdd(&P.inbox_n[c.np][dl], 1u);
         if (slot >= P.inbox_cap) { c.err |= SHD_ERR_INBOX_OVERFLOW; return; }
-        P.inbox[c.np][(size_t)dl * P.inbox_cap + slot] = e;
+        ev_st_sc1(&P.inbox[c.np][(size_t)dl * P.inbox_cap + slot], e);
     } else {
         if (P.xcnt) {   // fused peer-to-peer rounds: into the region of the destination's block
             const int32_t peer = owner_of(P, e.dst);
@@ -1160,7 +1176,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             const size_t bi = (size_t)dl * kNB + ((uint32_t)bb & (kNB - 1));
             const uint32_t slot = atomicAdd(&P.bin_n[bi], 1u);
             if (slot < kBinCap) {
-                P.bins[bi * kBinCap + slot] = e;
+                ev_st_sc1(&P.bins[bi * kBinCap + slot], e);
                 const uint32_t p = (uint32_t)bb & (kNB - 1);
                 atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));
                 continue;
@@ -1177,7 +1193,7 @@ __device__ __forceinline__ void flush_finish(const DParams& P, HostCtx& c, const
     if (pd.kind == 0) return;
     const shd_event e = s_res[threadIdx.x];
     if (pd.kind == 1 && pd.slot < kBinCap) {
-        P.bins[pd.bi * kBinCap + pd.slot] = e;
+        ev_st_sc1(&P.bins[pd.bi * kBinCap + pd.slot], e);
         const uint32_t p = (uint32_t)(pd.bi & (kNB - 1));
         const int32_t dl = (int32_t)e.dst - P.h0;
         atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));

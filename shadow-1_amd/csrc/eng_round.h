@@ -901,6 +901,441 @@ __global__ __launch_bounds__(64) void k_fold_tl(const TlPart* __restrict__ parts
     if (threadIdx.x == 0 && *halt == 0u) tl_publish(s, f, halt);
 }
 
+// ------------------------------------------------------------- persistent rounds
+// k_round_ps: a batch of rounds in ONE launch, for a single engine whose round
+// grid fits the GPU one block per CU (10 k hosts: 157 blocks).  Every block
+// keeps its 64 hosts' state (HostCtx) in registers, and their heap roots and
+// FIFO heads in LDS, from the first round of the batch to the last; the
+// records, next times and counters are stored once, at the end.  Between
+// rounds there is no kernel boundary: each block publishes its share of the
+// round (next time, flags; counts) as two tagged 16-B write-through granules
+// into a parity slot, after its wave drained every hand-off store, and every
+// block polls all shares of the round before it starts the next one -- the
+// window start is their min (slave.c:437-462 / master.c:450-480's round step,
+// as k_round_tl's fold).  Hand-offs between blocks within the launch follow
+// the sc1-store / sc1-load form of MI355X_MICROARCH.md (inter-workgroup
+// visibility): calendar and inbox events are stored with ev_st_sc1, the
+// counts reset with agent-scope stores, claimed with atomics; the owner reads
+// its bitmap, inbox counts, bins and inbox events with sc1 buffer loads.
+// A round that logged a first touch, or an error, ends the launch after its
+// summary is published (the host resolves it, as for k_round_tl); so does a
+// window start at or past the stop time.
+struct PsShare {
+    uint4 a;   // next time lo, hi, flags (SHD_ERR_* | kPsPend), tag
+    uint4 b;   // events, packet events, active hosts, tag
+};
+static_assert(sizeof(PsShare) == 32, "two 16-B granules");
+constexpr uint32_t kPsPend = 0x40000000u;   // share flag: the block's hosts logged a first touch
+constexpr uint32_t kBufWord3 = 0x00020000u;  // raw buffer descriptor word 3 (gfx9)
+constexpr int kAuxSc1 = 16;                   // buffer op cache policy: sc1 (agent scope)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, uint64_t bytes) {
+    const uint32_t n = bytes > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)n, (int)kBufWord3);
+}
+__device__ __forceinline__ uint4 ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kAuxSc1);
+    return make_uint4(x[0], x[1], x[2], x[3]);
+}
+__device__ __forceinline__ uint32_t ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, kAuxSc1);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4 v) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, kAuxSc1);
+}
+__device__ __forceinline__ shd_event evv_event(const EvV& x) {
+    shd_event e;
+    e.time = evv_time(x); e.seq = evv_seq(x);
+    e.src = x.b.x; e.dst = x.b.y; e.pkt = x.b.z; e.kind = x.b.w;
+    return e;
+}
+
+// this block's windows onto the hand-off arrays (the block's hosts only);
+// nin / inbox: the round's parity (chosen per round by scalar selects: an
+// array indexed by the parity would be kept in scratch)
+struct PsRsrc {
+    __amdgpu_buffer_rsrc_t bits, bins, nin, inbox;
+};
+
+// the rare overflow of the due list, as due_overflow, reading the bins again
+// with sc1 loads (they may hold other blocks' appends of this launch)
+__device__ void ps_due_overflow(const DParams& P, HostCtx& c, const PsRsrc& R, uint32_t lb, uint64_t b0,
+                                uint32_t wbits, uint64_t ws, uint64_t we) {
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < 3; j++) {
+        if (((wbits >> j) & 1u) == 0) continue;
+        const uint32_t bi = lb * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+        for (uint32_t s = 0; s < kBinCap; s++) {
+            const uint32_t off = (bi * kBinCap + s) * 32u;
+            const EvV x{ld16_sc1(R.bins, off), ld16_sc1(R.bins, off + 16)};
+            const uint64_t t = evv_time(x);
+            if (t < ws || t >= we) continue;
+            if (k >= (uint32_t)kDueCap) heap_push(P, c, evv_event(x));
+            k++;
+        }
+    }
+}
+
+// per-round fields of a persistent host context
+__device__ __forceinline__ void ps_round_reset(HostCtx& c, uint64_t ws, int parity) {
+    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = 0; c.xput = 0;
+    c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
+    c.min_emit = kInf; c.err = 0; c.n_pend = 0;
+    c.dh = 0; c.nd = 0; c.dt = kInf; c.ns = 0; c.seq_base = c.ev_seq;
+    c.w_msgs = 0; c.w_fl = 0;
+}
+
+// One round [ws, we) of the lane's host (has: the lane has one; lb: its index
+// in the block) on the context it keeps in registers; as round_body
+__device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, const PsRsrc& R, uint64_t ws,
+                         uint64_t we, int parity, uint64_t& next_out) {
+    ps_round_reset(c, ws, parity);
+    // the round's hand-off words: this parity's inbox count, the calendar bitmap
+    uint32_t nin = 0;
+    uint32_t w[kNBW];
+#pragma unroll
+    for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+    if (has) {
+        nin = ld4_sc1(R.nin, lb * 4u);
+        if (P.bins) {
+            const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+        }
+    }
+    const uint64_t b0 = ws >> P.bin_shift;
+    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
+    uint32_t wbits = 0;
+    if (P.bins) {
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++)
+            if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
+    }
+    if (nbin > 3) c.err |= SHD_ERR_INTERNAL;
+    uint64_t next = kInf;
+    const uint64_t t0 = host_next(c);
+    bool active = false;
+    TIM(1);
+    if (has) {
+        if (nin == 0 && t0 >= we && wbits == 0) {
+            next = t0;
+            if (P.bins) {
+                const uint64_t cb = cal_lower_bound(P, w, we);
+                next = cb < next ? cb : next;
+            }
+        } else {
+            active = true;
+        }
+    }
+    // the window's bins, every slot of a non-empty one in one round trip
+    EvV bx[3][kBinCap];
+    if (active && P.bins) {
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++) {
+            if (((wbits >> j) & 1u) == 0) continue;
+            const uint32_t bi = lb * kNB + ((uint32_t)(b0 + j) & (kNB - 1));
+#pragma unroll
+            for (uint32_t k = 0; k < kBinCap; k++) {
+                const uint32_t off = (bi * kBinCap + k) * 32u;
+                bx[j][k] = EvV{ld16_sc1(R.bins, off), ld16_sc1(R.bins, off + 16)};
+            }
+        }
+    }
+    if (active) {
+        if (nin) {   // inbound events of the previous round -> heap
+            const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t off = (lb * P.inbox_cap + i) * 32u;
+                heap_push(P, c, evv_event(EvV{ld16_sc1(R.inbox, off), ld16_sc1(R.inbox, off + 16)}));
+            }
+            __hip_atomic_store(&P.inbox_n[parity][c.l], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (P.bins) {
+            uint32_t nw = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                if (((wbits >> j) & 1u) == 0) continue;
+#pragma unroll
+                for (uint32_t k = 0; k < kBinCap; k++) due_add(bx[j][k], nw, ws, we);
+            }
+            c.nd = nw < (uint32_t)kDueCap ? nw : (uint32_t)kDueCap;
+            if (nw > (uint32_t)kDueCap) ps_due_overflow(P, c, R, lb, b0, wbits, ws, we);
+            for (uint32_t i = 1; i < c.nd; i++) {   // insertion sort of the due list (LDS)
+                const EvV x = ev_ld(s_due + i * kBlock + threadIdx.x);
+                uint32_t k = i;
+                for (; k > 0; k--) {
+                    const EvV y = ev_ld(s_due + (k - 1) * kBlock + threadIdx.x);
+                    if (!evv_less(x, y)) break;
+                    ev_st(s_due + k * kBlock + threadIdx.x, y);
+                }
+                ev_st(s_due + k * kBlock + threadIdx.x, x);
+            }
+            c.dt = c.nd ? s_due[threadIdx.x].time : kInf;
+        }
+    }
+    TIM(2);
+    // the event loop (as round_body's): per-lane state 0 needs its next event,
+    // 1 runs one, 2 waits for a flush, 3 done; wave-uniform exits only
+    PendDel pd;
+    pd.kind = 0;
+    {
+        uint32_t st = active ? 0u : 3u;
+        for (;;) {
+            for (;;) {
+                if (st == 0u) {
+                    shd_event e;
+                    if (take_next(P, c, we, e)) {
+                        c.now = e.time;
+                        begin_event(P, c, e);
+                        st = ((c.w_fl & ~W_READ) | c.w_msgs) ? 1u : 0u;
+#ifndef SHD_NO_FUSE
+                        if (st == 0u && c.tt2 < we) {   // the notification, when it is next (round_body)
+                            const uint64_t t = c.tt2, ht = c.evq_n ? c.top_time : kInf;
+                            if (t < c.tt0 && t < c.tt1 && t < c.dt && t < ht && notify_fast_ok(P, c)) {
+                                c.tt2 = kInf; c.now = t; c.c_events++;
+                                c.q_seq = c.ts2; c.q_src = c.h; c.q_sub = 0;
+                                c.w_msgs = 0; c.w_fl = 0;
+                                notify_fast(P, c);
+                                st = c.w_fl ? 1u : 0u;
+                            }
+                        }
+                        if (st == 0u && c.tt1 < we) {   // the periodic refill, when it is next
+                            const uint64_t t = c.tt1, ht = c.evq_n ? c.top_time : kInf;
+                            if (t < c.tt0 && t < c.tt2 && t < c.dt && t < ht && c.cq_count == 0 && c.tq_count == 0) {
+                                c.tt1 = kInf; c.now = t; c.c_events++;
+                                c.q_seq = c.ts1; c.q_src = c.h; c.q_sub = 0;
+                                c.w_msgs = 0; c.w_fl = 0;
+                                refill_fast(P, c);
+                            }
+                        }
+#endif
+                    } else {
+                        st = 3u;
+                    }
+                }
+                if (st == 1u) st = run_work(P, c) ? 0u : 2u;
+                if (__ballot(st <= 1u) == 0) break;
+            }
+            const bool last = __ballot(st == 2u) == 0;
+#ifdef SHD_TIMING
+            if (last) TIM(3);   // the round's last flush starts
+#endif
+            flush_wave(P, c, last, pd);
+            if (last) break;
+            if (st == 2u) st = 1u;
+        }
+    }
+    TIM(4);
+    if (active) {
+        next = host_next(c);
+        if (c.min_emit < next) next = c.min_emit;
+        if (P.bins) {   // consumed bins: counts reset (write-through), bits cleared
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                const uint64_t b = b0 + j;
+                if (j < nbin && ((b + 1) << P.bin_shift) <= we && ((wbits >> j) & 1u)) {
+                    const uint32_t p = (uint32_t)b & (kNB - 1);
+                    __hip_atomic_store(&P.bin_n[(size_t)c.l * kNB + p], 0u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t m = 1u << (p & 31);
+                    atomicAnd(&P.bin_bits[(size_t)c.l * kNBW + (p >> 5)], ~m);
+#pragma unroll
+                    for (int k = 0; k < (int)kNBW; k++)
+                        if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
+                }
+            }
+            const uint64_t cb = cal_lower_bound(P, w, we);
+            next = cb < next ? cb : next;
+        }
+    }
+    flush_finish(P, c, pd);
+    TIM(5);
+    next_out = next;
+}
+
+// the share of round i: both granules tagged, stored write-through after the
+// wave's hand-off stores drained
+__device__ __forceinline__ void ps_publish(__amdgpu_buffer_rsrc_t rs, uint32_t slot, uint64_t next, uint32_t flags,
+                                           uint32_t nev, uint32_t npkt, uint32_t nact, uint32_t tag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
+    if (threadIdx.x == 0) {
+        st16_sc1(rs, slot * 32u, make_uint4((uint32_t)next, (uint32_t)(next >> 32), flags, tag));
+        st16_sc1(rs, slot * 32u + 16u, make_uint4(nev, npkt, nact, tag));
+    }
+}
+
+// every block's share of round i (slots [base, base + nblk)): poll until all
+// carry `tag`, folding them; block 0 also folds the counts.  False on timeout
+__device__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nblk, uint32_t tag, bool counts,
+                          uint64_t ticks, uint64_t& next, uint32_t& flags, uint32_t& nev, uint32_t& npkt,
+                          uint32_t& nact) {
+    next = kInf; flags = 0; nev = 0; npkt = 0; nact = 0;
+    const unsigned long long t0 = wall_clock64();
+    for (uint32_t c0 = 0; c0 < nblk; c0 += 256) {
+        uint32_t need = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (c0 + 64u * k + threadIdx.x < nblk) need |= 1u << k;
+        while (__ballot(need != 0)) {
+            uint4 a[4], b[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t off = (base + c0 + 64u * k + threadIdx.x) * 32u;
+                a[k] = make_uint4(0, 0, 0, 0);
+                b[k] = a[k];
+                if ((need >> k) & 1u) {
+                    a[k] = ld16_sc1(rs, off);
+                    if (counts) b[k] = ld16_sc1(rs, off + 16u);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (!((need >> k) & 1u) || a[k].w != tag || (counts && b[k].w != tag)) continue;
+                const uint64_t t = ((uint64_t)a[k].y << 32) | a[k].x;
+                next = t < next ? t : next;
+                flags |= a[k].z;
+                nev += b[k].x; npkt += b[k].y; nact += b[k].z;
+                need &= ~(1u << k);
+            }
+            if (__ballot(need != 0) == 0) break;
+            if (wall_clock64() - t0 > ticks) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        flags |= __shfl_xor(flags, off, 64);
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        nact += __shfl_xor(nact, off, 64);
+    }
+    return true;
+}
+
+// a summary slot set fresh, written through (other blocks' atomics go to it)
+__device__ __forceinline__ void ps_fresh(DevSummary* s) {
+    uint64_t* d = (uint64_t*)s;
+    static_assert(sizeof(DevSummary) % 8 == 0, "8-B words");
+    const DevSummary z = fresh_summary();
+    const uint64_t* q = (const uint64_t*)&z;
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(DevSummary) / 8); k++)
+        __hip_atomic_store(d + k, q[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, DevSummary* __restrict__ ring,
+                                                      const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
+                                                      const DParams* __restrict__ Pr, uint64_t ticks) {
+    const DParams& P0 = Pr[1];
+    const uint32_t nblk = (uint32_t)((P0.nloc + P0.hpw - 1) / P0.hpw);
+    const int32_t l = lane_host(P0);
+    const bool has = l < P0.nloc;
+    const uint32_t lb = threadIdx.x;
+    const uint32_t hb = blockIdx.x * (uint32_t)P0.hpw;   // the block's first host
+    PsRsrc R0, R1;   // parity 0 and 1
+    {
+        const uint32_t hpw = (uint32_t)P0.hpw;
+        R0.bits = buf_rsrc(P0.bin_bits ? P0.bin_bits + (size_t)hb * kNBW : nullptr, (uint64_t)hpw * kNBW * 4);
+        R0.bins = buf_rsrc(P0.bins ? P0.bins + (size_t)hb * kNB * kBinCap : nullptr,
+                           (uint64_t)hpw * kNB * kBinCap * sizeof(shd_event));
+        R1.bits = R0.bits;
+        R1.bins = R0.bins;
+        R0.nin = buf_rsrc(P0.inbox_n[0] + hb, (uint64_t)hpw * 4);
+        R1.nin = buf_rsrc(P0.inbox_n[1] + hb, (uint64_t)hpw * 4);
+        R0.inbox = buf_rsrc(P0.inbox[0] + (size_t)hb * P0.inbox_cap, (uint64_t)hpw * P0.inbox_cap * sizeof(shd_event));
+        R1.inbox = buf_rsrc(P0.inbox[1] + (size_t)hb * P0.inbox_cap, (uint64_t)hpw * P0.inbox_cap * sizeof(shd_event));
+    }
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
+    HostCtx c;
+    hot_load(P0, c);
+    if (has) {
+        load_ctx(P0, c, l, P0.hs[l], P0.host_att[P0.h0 + l], P0.self_thr[P0.h0 + l]);
+    } else {
+        c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf;
+        c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
+    }
+    uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t ws = ring[0].next_time;
+    const uint64_t stop = ctl->stop, rbase = ctl->round_base;
+    const uint32_t tag0 = (uint32_t)ctl->xtag;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    for (int i = 0; i < nb; i++) {
+        const DParams& P = Pr[i + 1];
+        const unsigned long long t_start = wall_clock64();
+#ifdef SHD_TIMING
+        if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = t_start;
+#endif
+        if (lead) ps_fresh(&ring[i + 2]);   // the next round's summary (this round's: ring[i + 1])
+        const int parity = (int)((rbase + (uint64_t)i) & 1);
+        uint64_t we = ws + window;
+        if (we > stop || we < ws) we = stop;
+        uint64_t next;
+        PsRsrc R = R0;
+        R.nin = parity ? R1.nin : R0.nin;
+        R.inbox = parity ? R1.inbox : R0.inbox;
+        ps_round(P, c, has, lb, R, ws, we, parity, next);
+        acc[0] += c.c_events; acc[1] += c.c_pkt; acc[2] += c.c_sent;
+        acc[3] += c.c_idrop; acc[4] += c.c_cdrop; acc[5] += c.c_recv;
+        uint32_t nev = c.c_events, npkt = c.c_pkt, err = c.err;
+        const uint32_t pend = c.n_pend ? kPsPend : 0u;
+        const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));
+        uint32_t fl = err | pend;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(next, off, 64);
+            next = o < next ? o : next;
+            nev += __shfl_xor(nev, off, 64);
+            npkt += __shfl_xor(npkt, off, 64);
+            fl |= __shfl_xor(fl, off, 64);
+        }
+        const uint32_t tag = tag0 + (uint32_t)i;
+        const uint32_t base = (uint32_t)(i & 1) * nblk;
+        ps_publish(rs, base + blockIdx.x, next, fl, nev, npkt, nact, tag);
+        TIM(6);
+        uint64_t f_next;
+        uint32_t f_fl, f_nev, f_npkt, f_nact;
+        const bool ok_v = ps_gather(rs, base, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
+        TIM(7);
+        // the folds are wave-uniform: said so to the compiler, so that the
+        // round loop and the parity branch stay scalar (with a vector exit
+        // condition the host context would be merged through divergent flow)
+        const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;
+        f_fl = __builtin_amdgcn_readfirstlane(f_fl);
+        f_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(f_next >> 32)) << 32) |
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)f_next);
+        if (!ok) {   // a block never came: the launch is not resident (or a block faulted)
+            if (threadIdx.x == 0) {
+                atomicOr(&ring[i + 1].error, SHD_ERR_INTERNAL);
+                *P.halt = 1u;
+            }
+            break;
+        }
+        if (lead) {   // round i's summary (its log count came by atomics during the round)
+            DevSummary* s = &ring[i + 1];
+            atomicMin(&s->next_time, f_next);
+            if (f_nev) atomicAdd(&s->n_events, (unsigned long long)f_nev);
+            if (f_npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f_npkt);
+            if (f_nact) atomicAdd(&s->n_active, f_nact);
+            if (f_fl & ~kPsPend) atomicOr(&s->error, f_fl & ~kPsPend);
+            atomicMin(&s->t_first, t_start);
+            atomicMax(&s->t_last, (unsigned long long)wall_clock64());
+            __hip_atomic_store(&s->ws, (unsigned long long)ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f_fl & kPsPend) *P.halt = 1u;
+        }
+        if (f_fl) break;            // a first touch to resolve, or an error: the host takes over
+        ws = f_next;
+        if (ws >= stop) break;      // the rest only forwards the time (ring[i + 1].next_time says so)
+    }
+    // the hosts' state, once for the whole batch
+    if (has) {
+        c.c_events = acc[0]; c.c_pkt = acc[1]; c.c_sent = acc[2];
+        c.c_idrop = acc[3]; c.c_cdrop = acc[4]; c.c_recv = acc[5];
+        store_ctx(P0, c);
+    }
+}
+
 // ingest events from other engines into inbox[parity]
 __global__ void k_ingest(DParams P, const shd_event* __restrict__ ev, uint64_t n, int parity) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

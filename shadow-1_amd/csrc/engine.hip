@@ -109,7 +109,9 @@ struct shd_eng {
     uint64_t round = 0;                     // rounds executed (parity = round & 1)
     // device-driven pipeline
     static constexpr int kBatch = 64;
+    static constexpr int kPsBatch = 128;      // rounds of a persistent launch (k_round_ps)
     static constexpr int kRing = 2 * kBatch + 2;
+    static_assert(kPsBatch + 2 <= kRing, "a persistent batch's summaries fit the ring");
     DevSummary* d_ring = nullptr;
     DevSummary* h_ring = nullptr;           // pinned
     uint32_t* d_halt = nullptr;
@@ -124,6 +126,11 @@ struct shd_eng {
     TlPart* d_tpart = nullptr;              // [2][grid] ticketless round shares
     bool tl_ready = false;                  // the last batch logged no first touch: run ticketless
     Params* d_pr = nullptr;                 // device copies of P, one per summary-ring slot (sum = &d_ring[i])
+    // persistent rounds (k_round_ps): one launch per batch when the round grid
+    // fits the GPU one block per CU and the engine holds every host
+    bool ps_ok = false;
+    PsShare* d_pshare = nullptr;            // [2][grid] tagged round shares
+    uint32_t ps_epoch = 1;                  // share tags issued (never 0, never reused)
     double wall_khz = 100000.0;             // device wall clock (wall_clock64) rate
     uint64_t trace_cap = 0;
 };
@@ -460,6 +467,20 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             return SHD_ENODEV;
         }
     }
+    {   // persistent rounds: every block resident (one per CU), one engine for all hosts
+        const int grid = (e->nloc + P.hpw - 1) / P.hpw;
+        int ncu = 0, per_cu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_round_ps), kBlock,
+                                                         0) != hipSuccess)
+            per_cu = 0;
+        (void)hipGetLastError();
+        e->ps_ok = e->h0 == 0 && e->nloc == H && ncu > 0 && per_cu >= 1 && grid <= ncu;
+        if (e->ps_ok) {
+            int rc;
+            if ((rc = ealloc(e, &e->d_pshare, 2 * (size_t)grid))) { shd_eng_destroy(e); return rc; }
+        }
+    }
     *out = e;
     return SHD_OK;
 }
@@ -759,6 +780,19 @@ static int launch_batch(shd_eng* e, bool tl) {
     return SHD_OK;
 }
 
+// a persistent batch: nb rounds in one launch (k_round_ps); the shares' tags
+// advance past the batch whatever it ran
+static int launch_batch_ps(shd_eng* e, int nb) {
+    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
+    const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
+    hipLaunchKernelGGL(k_round_ps, dim3(grid), dim3(kBlock), 0, e->stream, e->window, nb, e->d_ring,
+                       (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr, ticks);
+    SHD_HIP(hipGetLastError());
+    e->ps_epoch += (uint32_t)nb;
+    if (e->ps_epoch < (uint32_t)nb + 1u) e->ps_epoch = 1;   // (wrapped: restart past 0)
+    return SHD_OK;
+}
+
 // ---- protected rounds.  A first-touch send whose drop decision differs
 // under the two candidate rows cannot be decided before the round's log is
 // ranked (probability ~3.5e-7 per logged send on the bench graph: it fired
@@ -883,18 +917,27 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         e->h_seed[1] = host_fresh_summary();
         e->h_ctl->stop = stop;
         e->h_ctl->round_base = e->round;
+        e->h_ctl->xtag = e->ps_epoch;   // persistent rounds: round i's shares are tagged ps_epoch + i
         SHD_HIP(hipMemcpyAsync(e->d_ring, e->h_seed, 2 * sizeof(DevSummary), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipMemcpyAsync(e->d_ctl, e->h_ctl, sizeof(DevCtl), hipMemcpyHostToDevice, e->stream));
         SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         SHD_HIP(hipEventRecord(e->bev[0], e->stream));
         static const bool no_tl = getenv("SHD_NO_TL") != nullptr;
+        static const bool no_ps = getenv("SHD_NO_PS") != nullptr;   // perf knob: launch-per-round batches only
         const bool tl = e->tl_ready && !no_tl;
-        if ((rc = launch_batch(e, tl))) break;
+        const bool ps = tl && e->ps_ok && !no_ps;
+        const int nb = ps ? shd_eng::kPsBatch : B;
+        if (ps) {
+            if ((rc = launch_batch_ps(e, nb))) break;
+            s.n_batches_persistent++;
+        } else if ((rc = launch_batch(e, tl))) {
+            break;
+        }
         s.n_batches++;
         if (tl) s.n_batches_ticketless++;
         SHD_HIP(hipEventRecord(e->bev[1], e->stream));
         uint32_t halt = 0;
-        SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost, e->stream));
+        SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (nb + 1), hipMemcpyDeviceToHost, e->stream));
         SHD_HIP(hipMemcpyAsync(&halt, e->d_halt, 4, hipMemcpyDeviceToHost, e->stream));
         SHD_HIP(hipStreamSynchronize(e->stream));
         {
@@ -907,7 +950,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         // with at most one logging round the next batch is ticketless (the
         // late, rare logs cost one halt each); after more, it is ticketed.
         uint32_t n_logs = 0;
-        for (int i = 0; i < B; i++) {
+        for (int i = 0; i < nb; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
             if (ws >= stop) { next = ws; break; }   // the rest only forwarded the time

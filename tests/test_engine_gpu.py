@@ -51,6 +51,7 @@ def test_geometric_one_host_per_vertex(queue_flags, closed, monkeypatch):
     assert_same(gpu, ora)
     assert gpu[2].n_rounds > 100
     assert gpu[2].n_batches_ticketless > 0                         # ticketless batches exercised
+    assert gpu[2].n_batches_persistent > 0                         # ... as persistent launches (k_round_ps)
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_LOCAL) > 0     # self-sends exercised
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_INET_DROP) > 0  # reliability drops
 
