@@ -40,7 +40,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--vertices", type=int, default=10000)
-    ap.add_argument("--hosts-per-gpu", type=int, default=10000)
+    ap.add_argument("--hosts-per-gpu", type=int, default=None,
+                    help="c3: hosts per GPU (default 10000, weak scaling); c5: given, the C5 model with this many "
+                         "hosts per GPU (weak scaling: 125000 is the per-GPU shard of the north star's 1 M hosts "
+                         "over 8 GPUs), absent, 1 M hosts split over the GPUs (strong scaling)")
     ap.add_argument("--load", type=int, default=None,
                     help="PHOLD messages per host at the application start (default 16; 4 for c4)")
     ap.add_argument("--payload", type=int, default=1)
@@ -81,17 +84,21 @@ def parse():
 
 
 class Roctx:
-    """roctx ranges (libroctx64) around the timed region, so that a
+    """roctx ranges around the timed region, so that a
     `rocprofv3 --marker-trace --kernel-trace` run of this script can restrict
     its kernel statistics to the timed region (scripts/rocprof_timed.py);
     without the profiler they cost nothing.  Absent library: no markers."""
     def __init__(self):
         import ctypes
-        try:
-            self.lib = ctypes.CDLL("libroctx64.so")
-            self.lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
-        except OSError:
-            self.lib = None
+        self.lib = None
+        # rocprofv3 (rocprofiler-sdk) traces the markers of its own roctx library
+        for name in ("librocprofiler-sdk-roctx.so", "libroctx64.so"):
+            try:
+                self.lib = ctypes.CDLL(name)
+                self.lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                break
+            except OSError:
+                self.lib = None
 
     def push(self, name):
         if self.lib is not None:
@@ -150,16 +157,21 @@ def main():
         V, H = g.n_vertices, model.n_hosts
     elif args.workload == "c5":
         # BASELINE C5 exactly as tests/fullsize_configs.py builds its fixture, the
-        # 1 M hosts split over the ranks (the total is fixed)
+        # 1 M hosts split over the ranks (the total is fixed); or with
+        # --hosts-per-gpu, the same model at that many hosts per GPU
         V, hpv = args.vertices, 100
         g = W.geometric_graph(V, seed=args.seed, loss_max=0.01)
-        host_vertex = W.hosts_on_vertices(V, hpv)
-        H = len(host_vertex)
+        if args.hosts_per_gpu:
+            H = args.hosts_per_gpu * max(world, 1)
+            host_vertex = (np.arange(H, dtype=np.int64) * V // H).astype(np.int32)
+        else:
+            host_vertex = W.hosts_on_vertices(V, hpv)
+            H = len(host_vertex)
         model = W.phold_model(host_vertex, end_time=end_time, seed=args.seed, load=args.load, payload=1500,
                               bw_down=512, bw_up=10240, codelq_cap=256)
     else:
         V = args.vertices
-        H = args.hosts_per_gpu * max(world, 1)
+        H = (args.hosts_per_gpu or 10000) * max(world, 1)
         g = W.geometric_graph(V, seed=args.seed, loss_max=args.edge_loss_max)
         hpv = max(1, H // V)
         host_vertex = (np.arange(H, dtype=np.int64) * V // H).astype(np.int32) if H != V * hpv else \
@@ -351,7 +363,8 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "strong" if args.workload in ("c4", "c5") else "weak",
+            "scaling": "strong" if args.workload == "c4" or (args.workload == "c5" and not args.hosts_per_gpu)
+                       else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic (bundled topology, Tor-scale relay/client PHOLD-UDP traffic, seed %d)"
@@ -360,11 +373,13 @@ def main():
             "config": {"workload": ("C4 Tor-scale (%d relays + %d clients, bundled %d-vertex topology; edge loss "
                                     "0.005: the population decays, the rate depends on the window)"
                                     % (args.relays, args.clients, V)) if args.workload == "c4" else
-                                   ("C5 1 M hosts (100 per vertex, %d-vertex geometric topology), 1500-B messages, "
+                                   ("C5 model, %d hosts (%s, %d-vertex geometric topology), 1500-B messages, "
                                     "512 KiB/s downlinks (CoDel queues build), edge loss U[0,0.01]: the population "
-                                    "decays, the rate depends on the window" % V) if args.workload == "c5" else
+                                    "decays, the rate depends on the window"
+                                    % (H, "%d per GPU" % args.hosts_per_gpu if args.hosts_per_gpu else "100 per vertex",
+                                       V)) if args.workload == "c5" else
                                    ("C3 PHOLD-UDP, stationary population (N x %d hosts, %d-vertex geometric topology)"
-                                    % (args.hosts_per_gpu, V)),
+                                    % (args.hosts_per_gpu or 10000, V)),
                        "edge_loss": ("bundled (0.005)" if args.workload == "c4" else
                                      "U[0,0.01]" if args.workload == "c5" else "U[0,%g]" % args.edge_loss_max),
                        "hosts": H, "vertices": V, "edges": int(g.n_edges), "load": args.load,
@@ -437,16 +452,6 @@ def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, t
             "note": "lost messages are never regenerated: the rate depends on the simulated window"}
 
 
-def engine_source_sha1():
-    """SHA-1 over the engine's translation unit (engine.hip and its parts)"""
-    import hashlib
-    h = hashlib.sha1()
-    d = os.path.join(REPO, "shadow-1_amd", "csrc")
-    for f in ("engine.hip", "eng_device.h", "eng_round.h", "eng_exchange.h", "eng_group.h", "shd_device.h"):
-        h.update(open(os.path.join(d, f), "rb").read())
-    return h.hexdigest()
-
-
 def pmc_traffic(workload, kernel):
     """HBM bytes per round of the round kernel from the committed rocprofv3
     PMC passes of THIS workload and kernel (profiles/r03/pmc_traffic.json,
@@ -454,8 +459,9 @@ def pmc_traffic(workload, kernel):
     WRITE_SIZE, over the timed region's dispatches), used only when they were
     taken of the engine source being run; else None (no inherited numbers)."""
     try:
+        import shdgpu as S
         prof = json.load(open(os.path.join(REPO, "profiles", "r03", "pmc_traffic.json")))
-        sha = engine_source_sha1()
+        sha = S.engine_source_sha1()
     except (OSError, ValueError):
         return None
     if prof.get("engine_source_sha1") != sha:

@@ -635,20 +635,24 @@ __device__ __forceinline__ bool cal_push(const DParams& P, int32_t dl, const shd
     return true;
 }
 
-// An event handed to another host's calendar or inbox: four agent-scope
-// 8-B stores (global_store_dwordx2 sc1: written through to memory, the line
-// dropped from the writer's L2), counted by the compiler like plain stores.
-// The persistent rounds (k_round_ps) read such events in a later round of
-// the same launch, on another CU and possibly another XCD, with sc1 loads
-// after every writer drained (MI355X_MICROARCH.md, inter-workgroup
-// visibility: sc1 stores + sc1 loads); the launch-per-round kernels read them
-// after a kernel boundary, for which a plain store would do as well.
+// An event handed to another host's calendar or inbox: two 16-B agent-scope
+// write-through stores (global_store_dwordx4 sc1: written through to memory,
+// the line dropped from the writer's L2).  The persistent rounds (k_round_ps)
+// read such events in a later round of the same launch, on another CU and
+// possibly another XCD, with sc1 loads after every writer drained
+// (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores + sc1 loads);
+// the launch-per-round kernels read them after a kernel boundary.  hipcc does
+// not count an asm store: the writers drain with an explicit
+// s_waitcnt vmcnt(0) (vmcnt is in issue order, so the compiler's own waits
+// stay conservative); the s_nop keeps the data registers intact until the
+// store has read them.  (Four 8-B atomic stores would write 4x the bytes:
+// rocprofv3 WRITE_SIZE counts 32 B per 8-B sc1 store, profiles/r03.)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void ev_st_sc1(shd_event* p, const shd_event& e) {
-    uint64_t* d = (uint64_t*)p;
-    __hip_atomic_store(d + 0, (uint64_t)e.time, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d + 1, (uint64_t)e.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d + 2, ((uint64_t)e.dst << 32) | e.src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(d + 3, ((uint64_t)e.kind << 32) | e.pkt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32x4_t a = {(uint32_t)e.time, (uint32_t)(e.time >> 32), (uint32_t)e.seq, (uint32_t)(e.seq >> 32)};
+    const u32x4_t b = {e.src, e.dst, e.pkt, e.kind};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\tglobal_store_dwordx4 %0, %2, off offset:16 sc1\n\ts_nop 1"
+                 ::"v"(p), "v"(a), "v"(b) : "memory");
 }
 
 // a 16-B write-through (system-scope) store: the line leaves every cache on

@@ -1073,6 +1073,24 @@ __device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, co
                 ev_st(s_due + k * kBlock + threadIdx.x, x);
             }
             c.dt = c.nd ? s_due[threadIdx.x].time : kInf;
+            // the window's wholly consumed bins: counts reset (write-through) and
+            // bits cleared now, so that these stores land during the event loop
+            // rather than in front of the round's share (no append of this round
+            // can target them: appends are >= we and within the horizon)
+#pragma unroll
+            for (uint32_t j = 0; j < 3; j++) {
+                const uint64_t b = b0 + j;
+                if (j < nbin && ((b + 1) << P.bin_shift) <= we && ((wbits >> j) & 1u)) {
+                    const uint32_t p = (uint32_t)b & (kNB - 1);
+                    __hip_atomic_store(&P.bin_n[(size_t)c.l * kNB + p], 0u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t m = 1u << (p & 31);
+                    atomicAnd(&P.bin_bits[(size_t)c.l * kNBW + (p >> 5)], ~m);
+#pragma unroll
+                    for (int k = 0; k < (int)kNBW; k++)
+                        if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
+                }
+            }
         }
     }
     TIM(2);
@@ -1131,21 +1149,7 @@ __device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, co
     if (active) {
         next = host_next(c);
         if (c.min_emit < next) next = c.min_emit;
-        if (P.bins) {   // consumed bins: counts reset (write-through), bits cleared
-#pragma unroll
-            for (uint32_t j = 0; j < 3; j++) {
-                const uint64_t b = b0 + j;
-                if (j < nbin && ((b + 1) << P.bin_shift) <= we && ((wbits >> j) & 1u)) {
-                    const uint32_t p = (uint32_t)b & (kNB - 1);
-                    __hip_atomic_store(&P.bin_n[(size_t)c.l * kNB + p], 0u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t m = 1u << (p & 31);
-                    atomicAnd(&P.bin_bits[(size_t)c.l * kNBW + (p >> 5)], ~m);
-#pragma unroll
-                    for (int k = 0; k < (int)kNBW; k++)
-                        if ((p >> 5) == (uint32_t)k) w[k] &= ~m;
-                }
-            }
+        if (P.bins) {   // (the consumed bins were cleared in w above)
             const uint64_t cb = cal_lower_bound(P, w, we);
             next = cb < next ? cb : next;
         }
@@ -1201,7 +1205,6 @@ __device__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nbl
             }
             if (__ballot(need != 0) == 0) break;
             if (wall_clock64() - t0 > ticks) return false;
-            __builtin_amdgcn_s_sleep(1);
         }
     }
     for (int off = 32; off > 0; off >>= 1) {

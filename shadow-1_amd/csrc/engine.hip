@@ -475,7 +475,8 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
                                                          0) != hipSuccess)
             per_cu = 0;
         (void)hipGetLastError();
-        e->ps_ok = e->h0 == 0 && e->nloc == H && ncu > 0 && per_cu >= 1 && grid <= ncu;
+        // (blocks of one wave: up to two per CU, below what LDS and registers admit)
+        e->ps_ok = e->h0 == 0 && e->nloc == H && ncu > 0 && per_cu >= 2 && grid <= 2 * ncu;
         if (e->ps_ok) {
             int rc;
             if ((rc = ealloc(e, &e->d_pshare, 2 * (size_t)grid))) { shd_eng_destroy(e); return rc; }

@@ -252,6 +252,17 @@ _SIGS = {
 _lib = None
 
 
+def engine_source_sha1() -> str:
+    """SHA-1 over the engine's translation unit (csrc/engine.hip and its parts):
+    the key under which profiles (PMC traffic) of this source are recorded."""
+    import hashlib
+    h = hashlib.sha1()
+    d = os.path.join(HERE, "csrc")
+    for f in ("engine.hip", "eng_device.h", "eng_round.h", "eng_exchange.h", "eng_group.h", "shd_device.h"):
+        h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()
+
+
 def lib() -> C.CDLL:
     """Load libshdgpu.so (raises if it has not been built)."""
     global _lib
