@@ -428,12 +428,20 @@ int shd_eng_window(shd_eng* e, uint64_t* window_ns);
 int shd_eng_boot(shd_eng* e);
 /* Events from the caller (event_new_ + scheduler_push, event.c:28-43,
  * scheduler.c:342-357): after shd_eng_boot and before the rounds reach their
- * times.  Only self events of kind SHD_EV_APP_START (src == dst, a host of this
- * engine) are accepted; each consumes its host's next event ID on the device
- * (the `seq` field is ignored), in array order per host -- the order
- * process_schedule runs a host's processes at boot (host.c:372-390) -- and is
- * dropped when its time is >= end_time.  SHD_EINVAL for anything else, or
- * for a time before the engine's current simulated time. */
+ * times (time >= the end of the last round run).  Two kinds are accepted:
+ *  - SHD_EV_APP_START self events (src == dst, a host of this engine): each
+ *    consumes its host's next event ID on the device (the `seq` field is
+ *    ignored), in array order per host -- the order process_schedule runs a
+ *    host's processes at boot (host.c:372-390);
+ *  - SHD_EV_PACKET deliveries from a host outside this engine (src in
+ *    [0, n_hosts) but not in [host_begin, host_end); dst a host of this
+ *    engine): packet ingress from hosts the caller simulates itself
+ *    (worker_sendPacket's scheduler_push of the packet event for a host of
+ *    another worker, worker.c:541-571).  `seq` is the sender's event ID and
+ *    `pkt` its packet ID, both kept; the event merges into its host's queue
+ *    by (time, src, seq) like any other.
+ * Either is dropped when its time is >= end_time.  SHD_EINVAL for anything
+ * else, or for a time before the engine's current simulated time. */
 int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n);
 /* one round [window_start, window_end) on this engine; remote-bound events are
  * kept in the outbox until shd_eng_take_remote */
@@ -449,7 +457,9 @@ int shd_eng_run(shd_eng* e, shd_run_stats* out);
  * (topology.c:1929-1965); engines of a group each count their own sends. */
 int shd_eng_path_counts(shd_eng* e, uint64_t* out, uint64_t cap, uint64_t* n);
 /* rounds while the next event time is below t_stop (rounds never cross t_stop);
- * stats cover this call only */
+ * stats cover this call only.  A whole-model engine only (host_begin 0,
+ * host_end n_hosts; SHD_EINVAL otherwise): a partial engine runs rounds
+ * (shd_eng_run_round) or joins a group. */
 int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* out);
 /* A round split into its phases, for drivers that own several engines (one
  * per GPU, DESIGN.md "Multi-GPU").  shd_eng_run_round = round_kernel, then,
@@ -478,6 +488,13 @@ int shd_eng_end_round(shd_eng* e, shd_round_summary* out);
 /* events this engine produced for hosts of other engines (device to device
  * copy into dev_dst, capacity cap events) and ingest of received events */
 int shd_eng_remote_copy(shd_eng* e, void* dev_dst, uint64_t cap, uint64_t* n);
+/* packet egress: the events the last round (shd_eng_run_round) produced for
+ * hosts outside this engine -- the deliveries offloaded hosts send to hosts
+ * the caller simulates -- copied to a host array of capacity cap (SHD_ERANGE
+ * with *n = the count when cap is short).  The round's outbox holds them until
+ * the next round starts; the caller owes them to their destination hosts
+ * (worker_sendPacket, worker.c:541-571). */
+int shd_eng_take_remote(shd_eng* e, shd_event* out, uint64_t cap, uint64_t* n);
 int shd_eng_ingest(shd_eng* e, const void* dev_events, uint64_t n_events);
 int shd_eng_next_time(shd_eng* e, uint64_t* next_time);
 int shd_eng_trace_count(shd_eng* e, uint64_t* n);

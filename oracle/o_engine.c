@@ -116,6 +116,11 @@ typedef struct {
     uint64_t q_time, q_seq;
     uint32_t q_host, q_src, q_sub;
     uint64_t n_ambig, n_events, n_pkt;
+    /* one side of a co-simulation (o_state_new_part): only the hosts
+     * [h_lo, h_hi) live here; events for the others leave by `egress`
+     * (part = 0: every host is here) */
+    int32_t part, h_lo, h_hi;
+    evvec egress;
 } ctx_t;
 
 static void evvec_push(evvec* v, const shd_event* e) {
@@ -146,6 +151,10 @@ static void push_event(ctx_t* c, uint32_t src, uint32_t dst, uint64_t t, uint32_
     shd_event e;
     e.time = t; e.seq = c->hosts[src].ev_seq++; e.src = src; e.dst = dst; e.pkt = pkt; e.kind = kind;
     if (t >= c->m->end_time) return;
+    if (c->part && (dst < (uint32_t)c->h_lo || dst >= (uint32_t)c->h_hi)) {   /* the other side's host */
+        evvec_push(&c->egress, &e);
+        return;
+    }
     if (!c->hq) eh_push(&c->q, &e);
     else if (dst == src) eh_push(&c->hq[dst], &e);    /* the executing host's own queue */
     else evvec_push(&c->mbox, &e);                    /* delivered at the round's end */
@@ -488,10 +497,13 @@ static double now_ms(void) {
     return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
 }
 
-o_state* o_state_new(const shd_model* m, const shd_graph* gin, int32_t force_rows) {
+static o_state* state_new(const shd_model* m, const shd_graph* gin, int32_t force_rows, int32_t h_lo,
+                          int32_t h_hi) {
     o_state* S = calloc(1, sizeof(*S));
     ctx_t* c = &S->c;
     c->m = m; c->out = &S->run;
+    c->part = !(h_lo == 0 && h_hi == m->n_hosts);
+    c->h_lo = h_lo; c->h_hi = h_hi;   /* the hosts that boot here */
     S->g = o_graph_new(gin);
     c->g = S->g;
     /* attached vertices = verticesWithAttachedHosts */
@@ -518,16 +530,65 @@ o_state* o_state_new(const shd_model* m, const shd_graph* gin, int32_t force_row
         o_codel_init(&H->codel, 16);
         H->txq_cap = 16; H->txq = malloc(sizeof(txent) * 16);
     }
-    for (int32_t h = 0; h < m->n_hosts; h++) boot(c, (uint32_t)h);
+    for (int32_t h = h_lo; h < h_hi; h++) boot(c, (uint32_t)h);
     for (uint64_t i = 0; i < g_npush; i++) {
         const shd_event* p = &g_push[i];
         if (p->kind != SHD_EV_APP_START || p->src != p->dst || p->dst >= (uint32_t)m->n_hosts) {
             fprintf(stderr, "oracle: bad pushed event\n");
             abort();
         }
-        push_event(c, p->src, p->dst, p->time, p->kind, 0);
+        if (p->dst >= (uint32_t)h_lo && p->dst < (uint32_t)h_hi) push_event(c, p->src, p->dst, p->time, p->kind, 0);
     }
     return S;
+}
+o_state* o_state_new(const shd_model* m, const shd_graph* gin, int32_t force_rows) {
+    return state_new(m, gin, force_rows, 0, m->n_hosts);
+}
+
+/* ---- co-simulation: one side of packet ingress/egress at the boundary.
+ * Hosts [h_lo, h_hi) run here in the serial loop; the others are simulated
+ * elsewhere (the GPU engine, or another part).  worker_sendPacket's scheduler_push
+ * of a packet for a host of another worker (worker.c:541-571) becomes an
+ * egress event; the other side's packets for hosts here arrive by
+ * o_state_inject, between windows of W (every cross-host event of a window
+ * lands at or after its end, so the union is the serial run). ---- */
+o_state* o_state_new_part(const shd_model* m, const shd_graph* gin, int32_t h_lo, int32_t h_hi) {
+    if (h_lo < 0 || h_hi > m->n_hosts || h_lo >= h_hi) return NULL;
+    return state_new(m, gin, 0, h_lo, h_hi);
+}
+int o_state_inject(o_state* S, const shd_event* ev, uint64_t n) {
+    ctx_t* c = &S->c;
+    for (uint64_t i = 0; i < n; i++) {
+        const shd_event* e = &ev[i];
+        if (e->kind != SHD_EV_PACKET || e->dst < (uint32_t)c->h_lo || e->dst >= (uint32_t)c->h_hi ||
+            (e->src >= (uint32_t)c->h_lo && e->src < (uint32_t)c->h_hi))
+            return -1;
+        if (e->time >= c->m->end_time) continue;   /* scheduler_push drops it (scheduler.c:346-349) */
+        if (c->hq) eh_push(&c->hq[e->dst], e);
+        else eh_push(&c->q, e);
+    }
+    return 0;
+}
+/* the events for the other side's hosts since the last call: *n = the count;
+ * copied when out != NULL and cap covers it (then the list empties) */
+int o_state_take_egress(o_state* S, shd_event* out, uint64_t cap, uint64_t* n) {
+    evvec* v = &S->c.egress;
+    *n = v->n;
+    if (!out) return 0;
+    if (cap < v->n) return -1;
+    memcpy(out, v->a, sizeof(shd_event) * v->n);
+    v->n = 0;
+    return 0;
+}
+/* time of the next event here (UINT64_MAX when none) */
+uint64_t o_state_next_time(const o_state* S) { return S->c.q.n ? S->c.q.a[0].time : UINT64_MAX; }
+/* the trace so far: *n = its length; copied when out != NULL and cap covers it */
+int o_state_trace(const o_state* S, shd_trace_rec* out, uint64_t cap, uint64_t* n) {
+    *n = S->run.n_trace;
+    if (!out) return 0;
+    if (cap < S->run.n_trace) return -1;
+    memcpy(out, S->run.trace, sizeof(shd_trace_rec) * S->run.n_trace);
+    return 0;
 }
 
 /* every attached vertex's source row, `threads` rows at a time (the values
@@ -663,7 +724,7 @@ int o_state_run_parallel(o_state* S, uint64_t t_until, int threads, o_par_stats*
     const shd_model* m = base->m;
     const int32_t H = m->n_hosts;
     memset(st, 0, sizeof(*st));
-    if (S->g->directed || m->trace) return -1;   /* the bench graphs: undirected, no trace */
+    if (S->g->directed || m->trace || S->c.part) return -1;   /* the bench graphs: undirected, no trace, whole */
     o_state_rows(S, threads);
     /* per-host queues from the global one */
     eheap* hq = calloc(H, sizeof(eheap));
@@ -784,6 +845,8 @@ o_state* o_state_clone(const o_state* S) {
     for (int32_t h = 0; h < H; h++) ohost_clone(&C->c.hosts[h], &S->c.hosts[h]);
     C->c.q.a = malloc(sizeof(shd_event) * (S->c.q.cap ? S->c.q.cap : 1));
     memcpy(C->c.q.a, S->c.q.a, sizeof(shd_event) * S->c.q.n);
+    C->c.egress.a = malloc(sizeof(shd_event) * (S->c.egress.cap ? S->c.egress.cap : 1));
+    memcpy(C->c.egress.a, S->c.egress.a, sizeof(shd_event) * S->c.egress.n);
     C->shared = 1;
     return C;
 }
@@ -812,7 +875,7 @@ const o_run* o_state_stats(const o_state* S) { return &S->run; }
 void o_state_free(o_state* S) {
     if (!S) return;
     for (int32_t h = 0; h < S->c.m->n_hosts; h++) { o_codel_free(&S->c.hosts[h].codel); free(S->c.hosts[h].txq); }
-    free(S->c.hosts); free(S->c.q.a);
+    free(S->c.hosts); free(S->c.q.a); free(S->c.egress.a);
     o_topo_free(S->c.topo);
     if (!S->shared) {
         if (S->row_lat) {

@@ -160,6 +160,15 @@ int o_state_run_parallel(o_state* s, uint64_t t_until, int threads, o_par_stats*
 o_state* o_state_clone(const o_state* s);
 void o_state_digest(const o_state* s, shd_host_digest* out);   /* [H] */
 const o_run* o_state_stats(const o_state* s);
+/* co-simulation (packet ingress/egress at the boundary, shd_eng_push_events /
+ * shd_eng_take_remote): a state of the hosts [h_lo, h_hi) only; sends to
+ * other hosts leave by o_state_take_egress, the other side's packets for hosts
+ * here come in by o_state_inject; o_state_run_serial runs the windows */
+o_state* o_state_new_part(const shd_model* m, const shd_graph* g, int32_t h_lo, int32_t h_hi);
+int o_state_inject(o_state* s, const shd_event* ev, uint64_t n);
+int o_state_take_egress(o_state* s, shd_event* out, uint64_t cap, uint64_t* n);
+uint64_t o_state_next_time(const o_state* s);
+int o_state_trace(const o_state* s, shd_trace_rec* out, uint64_t cap, uint64_t* n);
 void o_state_free(o_state* s);
 
 /* the bench's CPU baseline (bench.py cpu_baseline): warm up to t_mark, then

@@ -1387,3 +1387,20 @@ __global__ void k_push(DParams P, const shd_event* __restrict__ ev, const uint32
     if (next != kInf) atomicMin(&P.sum->next_time, (unsigned long long)next);
     if (err) atomicOr(&P.sum->error, err);
 }
+
+// packets from hosts outside this engine (shd_eng_push_events: the delivery
+// events a CPU-side host's worker_sendPacket made, worker.c:260-321): the
+// sender's event ID and packet id come with them; scheduler_push drops a time
+// >= end (scheduler.c:346-349); the rest go to the inbox the next round
+// merges into the destination's heap.  One thread per event.
+__global__ void k_push_packets(DParams P, const shd_event* __restrict__ ev, uint32_t n, int parity) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const shd_event e = ev[i];
+    if (e.time >= P.end_time) return;
+    const int32_t dl = (int32_t)e.dst - P.h0;
+    const uint32_t slot = atomicAdd(&P.inbox_n[parity][dl], 1u);
+    if (slot >= P.inbox_cap) { atomicOr(&P.sum->error, SHD_ERR_INBOX_OVERFLOW); return; }
+    P.inbox[parity][(size_t)dl * P.inbox_cap + slot] = e;
+    atomicMin(&P.sum->next_time, (unsigned long long)e.time);
+}

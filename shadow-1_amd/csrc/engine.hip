@@ -545,24 +545,30 @@ extern "C" int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n) 
     if (!e->booted) return SHD_EINVAL;
     if (!n) return SHD_OK;
     if (n > (1u << 30)) return SHD_ERANGE;
+    // two kinds: application starts of this engine's hosts (each consumes its
+    // host's next event ID here), and packet deliveries from hosts outside this
+    // engine (their sender's ID and packet id come with them)
+    std::vector<shd_event> starts, pkts;
     for (uint64_t i = 0; i < n; i++) {
         const shd_event& x = ev[i];
-        if (x.kind != SHD_EV_APP_START || x.src != x.dst || (int64_t)x.dst < e->h0 ||
-            (int64_t)x.dst >= (int64_t)e->h0 + e->nloc || x.time < e->t_done)
+        const bool local_dst = (int64_t)x.dst >= e->h0 && (int64_t)x.dst < (int64_t)e->h0 + e->nloc;
+        const bool local_src = (int64_t)x.src >= e->h0 && (int64_t)x.src < (int64_t)e->h0 + e->nloc;
+        if (!local_dst || x.time < e->t_done) return SHD_EINVAL;
+        if (x.kind == SHD_EV_APP_START && x.src == x.dst) {
+            starts.push_back(x);
+            starts.back().pkt = 0;
+        } else if (x.kind == SHD_EV_PACKET && !local_src && (int64_t)x.src < (int64_t)e->H) {
+            pkts.push_back(x);
+        } else {
             return SHD_EINVAL;
+        }
     }
-    // stable grouping by host: a host's events keep their array order (its IDs)
-    std::vector<uint32_t> idx(n);
-    for (uint64_t i = 0; i < n; i++) idx[i] = (uint32_t)i;
-    std::stable_sort(idx.begin(), idx.end(), [ev](uint32_t a, uint32_t b) { return ev[a].dst < ev[b].dst; });
-    std::vector<shd_event> sorted(n);
+    // stable grouping of the starts by host: a host's starts keep their array order (its IDs)
+    std::stable_sort(starts.begin(), starts.end(), [](const shd_event& a, const shd_event& b) { return a.dst < b.dst; });
     std::vector<uint32_t> off;
-    for (uint64_t i = 0; i < n; i++) {
-        sorted[i] = ev[idx[i]];
-        sorted[i].pkt = 0;
-        if (i == 0 || sorted[i].dst != sorted[i - 1].dst) off.push_back((uint32_t)i);
-    }
-    off.push_back((uint32_t)n);
+    for (size_t i = 0; i < starts.size(); i++)
+        if (i == 0 || starts[i].dst != starts[i - 1].dst) off.push_back((uint32_t)i);
+    off.push_back((uint32_t)starts.size());
     const uint32_t ngrp = (uint32_t)off.size() - 1;
     SHD_HIP(hipSetDevice(e->device));
     shd_event* d_ev = nullptr;
@@ -571,19 +577,29 @@ extern "C" int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n) 
     if (hipMalloc((void**)&d_off, 4 * off.size()) != hipSuccess) { (void)hipFree(d_ev); return SHD_ENOMEM; }
     int rc = SHD_OK;
     e->P.sum = e->d_sum;
-    if (hipMemcpyAsync(d_ev, sorted.data(), sizeof(shd_event) * n, hipMemcpyHostToDevice, e->stream) != hipSuccess ||
+    if ((!starts.empty() && hipMemcpyAsync(d_ev, starts.data(), sizeof(shd_event) * starts.size(),
+                                           hipMemcpyHostToDevice, e->stream) != hipSuccess) ||
+        (!pkts.empty() && hipMemcpyAsync(d_ev + starts.size(), pkts.data(), sizeof(shd_event) * pkts.size(),
+                                         hipMemcpyHostToDevice, e->stream) != hipSuccess) ||
         hipMemcpyAsync(d_off, off.data(), 4 * off.size(), hipMemcpyHostToDevice, e->stream) != hipSuccess)
         rc = SHD_ENODEV;
     if (!rc) {
         // the summary's next time is the loop's window start: seed it with the
-        // host view, the kernel lowers it to the earliest pushed time
+        // host view, the kernels lower it to the earliest pushed time
         e->h_sum->error = 0;
         if (hipMemcpyAsync(e->d_sum, e->h_sum, sizeof(DevSummary), hipMemcpyHostToDevice, e->stream) != hipSuccess)
             rc = SHD_ENODEV;
     }
-    if (!rc) {
+    const int parity = (int)(e->round & 1);
+    if (!rc && ngrp) {
         hipLaunchKernelGGL(k_push, dim3((ngrp + 255) / 256), dim3(256), 0, e->stream, dp(e->P), (const shd_event*)d_ev,
-                           (const uint32_t*)d_off, ngrp, (int)(e->round & 1));
+                           (const uint32_t*)d_off, ngrp, parity);
+        if (hipGetLastError() != hipSuccess) rc = SHD_ENODEV;
+    }
+    if (!rc && !pkts.empty()) {
+        const uint32_t np = (uint32_t)pkts.size();
+        hipLaunchKernelGGL(k_push_packets, dim3((np + 255) / 256), dim3(256), 0, e->stream, dp(e->P),
+                           (const shd_event*)(d_ev + starts.size()), np, parity);
         if (hipGetLastError() != hipSuccess) rc = SHD_ENODEV;
     }
     if (!rc) rc = read_summary(e);
@@ -593,8 +609,23 @@ extern "C" int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n) 
     return rc;
 }
 
-// first-touch resolution in serial order: sort the logged queries
-// by the executing event's key, assign row ranks, finalize delivered sends
+// the outbox of the last round (events for hosts of other engines or of the
+// CPU side), copied to the caller's host array
+extern "C" int shd_eng_take_remote(shd_eng* e, shd_event* out, uint64_t cap, uint64_t* n) {
+    if (!e || !n) return SHD_EINVAL;
+    const uint64_t cnt = std::min<uint64_t>(e->h_sum->n_remote, e->P.remote_cap);
+    if (e->h_sum->n_remote > e->P.remote_cap) return SHD_EOVERFLOW;
+    if (cnt > cap) { *n = cnt; return SHD_ERANGE; }
+    SHD_HIP(hipSetDevice(e->device));
+    if (cnt) {
+        if (!out) return SHD_EINVAL;
+        SHD_HIP(hipMemcpyAsync(out, e->P.remote, sizeof(shd_event) * cnt, hipMemcpyDeviceToHost, e->stream));
+        SHD_HIP(hipStreamSynchronize(e->stream));
+    }
+    *n = cnt;
+    return SHD_OK;
+}
+
 // first-touch resolution in serial order (DESIGN.md "First-touch rule"): sort
 // the logged queries of ALL engines by the executing event's key, assign row
 // ranks (identically on every engine), then finalize this engine's sends
@@ -879,6 +910,9 @@ static int protected_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summa
 
 extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;
+    // a partial engine's sends to hosts outside it leave by rounds
+    // (shd_eng_run_round + shd_eng_take_remote) or a group, never a batch
+    if (e->h0 != 0 || e->nloc != e->H) return SHD_EINVAL;
     auto t0 = std::chrono::steady_clock::now();
     int rc = SHD_OK;
     if (!e->booted && (rc = shd_eng_boot(e))) return rc;

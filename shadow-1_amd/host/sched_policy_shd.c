@@ -20,8 +20,21 @@
  *     at or past the barrier wait.
  *
  * getNextTime is the minimum of the heap's head and the engine's next event.
- * The two kinds do not exchange packets (an offloaded host's traffic stays on
- * the device); that is the partition INTEGRATION.md describes.
+ *
+ * With a bridge (schedulerpolicygpurounds_new_bridged) the engine holds only
+ * some hosts of the model (a partial engine) and the two sides exchange
+ * packets, the way two of Shadow's workers do (worker_sendPacket's
+ * scheduler_push of a deliver-packet task for another worker's host,
+ * worker.c:541-571):
+ *   - ingress: a push whose event the bridge claims (a packet for an
+ *     offloaded host) becomes an shd_event; the policy keeps it until the
+ *     engine's next round (shd_eng_push_events) and drops the Shadow event;
+ *   - egress: after each engine round, the deliveries its hosts sent to
+ *     CPU-side hosts (shd_eng_take_remote) become Shadow events through the
+ *     bridge and join the heap; every one is due at or after the barrier.
+ * The engine then runs one device round per Shadow round, [its next event,
+ * barrier): the bridge needs Shadow's window (the runahead) to be at most the
+ * engine's W, so that nothing either side sends lands inside the round.
  *
  * Shadow's own functions (event.c, glib) are resolved when Shadow links this
  * file; with -DSHD_CHECK_AGAINST_REFERENCE and the reference header included
@@ -68,6 +81,21 @@ extern void g_queue_free(GQueue* queue);
 #define SHD_SP_GPU_ROUNDS 6   /* the SchedulerPolicyType value it would take */
 #define SHD_SIMTIME_MAX_ (UINT64_MAX - 1)
 
+/* packet ingress / egress between Shadow's CPU-side hosts and a partial
+ * engine's offloaded hosts (the integrator's conversions of Shadow's Event
+ * and Packet objects; INTEGRATION.md "Mixed CPU/GPU hosts") */
+typedef struct shd_policy_bridge {
+    /* a push of `event` (srcHost -> dstHost): return 1 and fill *out (kind
+     * SHD_EV_PACKET, time, model host IDs src/dst, seq = the event's ID, pkt =
+     * the packet's ID) when it is a packet for an offloaded host; 0 keeps the
+     * event on the CPU side */
+    int (*ingress)(void* user, Event* event, Host* srcHost, Host* dstHost, shd_event* out);
+    /* the Shadow deliver-packet event for a delivery from an offloaded host to a
+     * CPU-side host (NULL: dropped, and counted as an error) */
+    Event* (*egress)(void* user, const shd_event* delivery);
+    void* user;
+} shd_policy_bridge;
+
 typedef struct {
     Event** heap;              /* binary min-heap in event_compare order */
     size_t n, cap;
@@ -76,6 +104,12 @@ typedef struct {
     shd_xgroup* grp;           /* or the engine group this process drives */
     SimulationTime advanced;   /* the engine has run every round below this barrier */
     int error;                 /* the engine's last error status */
+    int bridged;               /* a partial engine exchanging packets through `bridge` */
+    shd_policy_bridge bridge;
+    shd_event* ingress;        /* packets for offloaded hosts, until the engine's next round */
+    size_t n_in, cap_in;
+    shd_event* egress;         /* a round's deliveries to CPU-side hosts */
+    size_t cap_out;
 } gpu_policy;
 
 static int ev_lt(Event* a, Event* b) { return event_compare(a, b, NULL) < 0; }
@@ -92,10 +126,31 @@ static GQueue* _gpurounds_getHosts(SchedulerPolicy* policy) {
     return d->hosts;
 }
 
+static void heap_push(gpu_policy* d, Event* event);
+
 static void _gpurounds_push(SchedulerPolicy* policy, Event* event, Host* srcHost, Host* dstHost,
                             SimulationTime barrier) {
     gpu_policy* d = policy->data;
-    (void)srcHost; (void)dstHost; (void)barrier;   /* global order: no clamp (global_single.c:40-55) */
+    (void)barrier;   /* global order: no clamp (global_single.c:40-55) */
+    if (d->bridged) {
+        shd_event x;
+        if (d->bridge.ingress(d->bridge.user, event, srcHost, dstHost, &x)) {
+            if (d->n_in == d->cap_in) {
+                size_t nc = d->cap_in ? 2 * d->cap_in : 1024;
+                shd_event* ni = realloc(d->ingress, sizeof(shd_event) * nc);
+                if (!ni) { d->error = SHD_ENOMEM; event_unref(event); return; }
+                d->ingress = ni;
+                d->cap_in = nc;
+            }
+            d->ingress[d->n_in++] = x;
+            event_unref(event);   /* the packet lives on the device now */
+            return;
+        }
+    }
+    heap_push(d, event);
+}
+
+static void heap_push(gpu_policy* d, Event* event) {
     if (d->n == d->cap) {
         size_t nc = d->cap ? 2 * d->cap : 1024;
         Event** nh = realloc(d->heap, sizeof(Event*) * nc);
@@ -130,9 +185,48 @@ static Event* heap_pop(gpu_policy* d) {
     return top;
 }
 
+/* the buffered ingress into the engine (one push per flush) */
+static void flush_ingress(gpu_policy* d) {
+    if (!d->n_in) return;
+    const int rc = shd_eng_push_events(d->eng, d->ingress, d->n_in);
+    if (rc != SHD_OK) d->error = rc;
+    d->n_in = 0;
+}
+
+/* bridged: the engine's one round of this Shadow round, then its egress */
+static void advance_bridged(gpu_policy* d, SimulationTime barrier) {
+    flush_ingress(d);
+    uint64_t g = UINT64_MAX, W = 0;
+    shd_eng_next_time(d->eng, &g);
+    shd_eng_window(d->eng, &W);
+    const SimulationTime ws = g > d->advanced ? g : d->advanced;
+    d->advanced = barrier;
+    if (ws >= barrier) return;                     /* nothing on the device before the barrier */
+    if (barrier - ws > W) { d->error = SHD_EINVAL; return; }   /* Shadow's window is wider than W */
+    shd_round_summary r;
+    int rc = shd_eng_run_round(d->eng, ws, barrier, &r);
+    if (rc != SHD_OK) { d->error = rc; return; }
+    uint64_t n = 0;
+    rc = shd_eng_take_remote(d->eng, d->egress, d->cap_out, &n);
+    if (rc == SHD_ERANGE) {
+        shd_event* no = realloc(d->egress, sizeof(shd_event) * n);
+        if (!no) { d->error = SHD_ENOMEM; return; }
+        d->egress = no;
+        d->cap_out = n;
+        rc = shd_eng_take_remote(d->eng, d->egress, d->cap_out, &n);
+    }
+    if (rc != SHD_OK) { d->error = rc; return; }
+    for (uint64_t i = 0; i < n; i++) {
+        Event* ev = d->bridge.egress(d->bridge.user, &d->egress[i]);
+        if (ev) heap_push(d, ev);
+        else d->error = SHD_EINVAL;
+    }
+}
+
 /* run the engine's rounds below the barrier once per barrier */
 static void advance(gpu_policy* d, SimulationTime barrier) {
     if (barrier <= d->advanced || (!d->eng && !d->grp)) return;
+    if (d->bridged) { advance_bridged(d, barrier); return; }
     shd_run_stats st;
     const int rc = d->grp ? shd_xgroup_run_until(d->grp, barrier, &st) : shd_eng_run_until(d->eng, barrier, &st);
     if (rc != SHD_OK) d->error = rc;
@@ -150,6 +244,7 @@ static SimulationTime _gpurounds_getNextTime(SchedulerPolicy* policy) {
     gpu_policy* d = policy->data;
     SimulationTime t = d->n ? event_getTime(d->heap[0]) : (SimulationTime)SHD_SIMTIME_MAX_;
     uint64_t g = UINT64_MAX;
+    if (d->bridged) flush_ingress(d);   /* the engine's next time covers what it was sent */
     if (d->grp) shd_xgroup_next_time(d->grp, &g);
     else if (d->eng) shd_eng_next_time(d->eng, &g);
     return g < t ? g : t;
@@ -159,6 +254,8 @@ static void _gpurounds_free(SchedulerPolicy* policy) {
     gpu_policy* d = policy->data;
     while (d->n) event_unref(heap_pop(d));
     free(d->heap);
+    free(d->ingress);
+    free(d->egress);
     if (d->hosts) g_queue_free(d->hosts);
     free(d);
     free(policy);
@@ -182,6 +279,18 @@ SchedulerPolicy* schedulerpolicygpurounds_new(shd_eng* eng, shd_xgroup* grp) {
     p->pop = _gpurounds_pop;
     p->getNextTime = _gpurounds_getNextTime;
     p->free = _gpurounds_free;
+    return p;
+}
+
+/* the policy over a partial engine whose hosts exchange packets with Shadow's
+ * CPU-side hosts through `bridge` (copied); NULL for an incomplete bridge */
+SchedulerPolicy* schedulerpolicygpurounds_new_bridged(shd_eng* eng, const shd_policy_bridge* bridge) {
+    if (!eng || !bridge || !bridge->ingress || !bridge->egress) return NULL;
+    SchedulerPolicy* p = schedulerpolicygpurounds_new(eng, NULL);
+    if (!p) return NULL;
+    gpu_policy* d = p->data;
+    d->bridged = 1;
+    d->bridge = *bridge;
     return p;
 }
 

@@ -221,6 +221,7 @@ _SIGS = {
     "shd_eng_resolve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "shd_eng_end_round": (C.c_int, [C.c_void_p, P(RoundSummary)]),
     "shd_eng_remote_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "shd_eng_take_remote": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_ingest": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "shd_eng_next_time": (C.c_int, [C.c_void_p, P(C.c_uint64)]),
     "shd_eng_trace_count": (C.c_int, [C.c_void_p, P(C.c_uint64)]),

@@ -98,7 +98,8 @@ class Engine:
         S.check(S.lib().shd_eng_boot(self.ptr), "shd_eng_boot")
 
     def push_events(self, events: np.ndarray):
-        """shd_eng_push_events: caller-scheduled application starts (after boot)."""
+        """shd_eng_push_events: caller-scheduled application starts, and packet
+        deliveries from hosts the caller simulates (ingress), after boot."""
         ev = np.ascontiguousarray(events, dtype=S.EVENT_DTYPE)
         S.check(S.lib().shd_eng_push_events(self.ptr, ev.ctypes.data if len(ev) else None, len(ev)),
                 "shd_eng_push_events")
@@ -154,6 +155,19 @@ class Engine:
         S.check(S.lib().shd_eng_remote_copy(self.ptr, C.c_void_p(dev_ptr), int(cap_events), C.byref(n)),
                 "shd_eng_remote_copy")
         return n.value
+
+    def take_remote(self) -> np.ndarray:
+        """shd_eng_take_remote: the last round's deliveries to hosts outside
+        this engine (egress), as an EVENT_DTYPE array."""
+        n = C.c_uint64()
+        rc = S.lib().shd_eng_take_remote(self.ptr, None, 0, C.byref(n))
+        if rc == -34:   # ERANGE: n holds the count
+            out = np.empty(n.value, dtype=S.EVENT_DTYPE)
+            rc = S.lib().shd_eng_take_remote(self.ptr, out.ctypes.data, n.value, C.byref(n))
+            S.check(rc, "shd_eng_take_remote")
+            return out[:n.value]
+        S.check(rc, "shd_eng_take_remote")
+        return np.empty(0, dtype=S.EVENT_DTYPE)
 
     def next_time(self) -> int:
         t = C.c_uint64()

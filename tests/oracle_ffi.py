@@ -87,6 +87,20 @@ def lib():
         l.o_engine_set_heartbeats_out.argtypes = [C.c_void_p, C.c_uint32]
         l.o_engine_set_pushes.argtypes = [C.c_void_p, C.c_uint64]
         l.o_baseline.argtypes = [P(S.Model), P(S.Graph), C.c_uint64, C.c_uint64, C.c_int, P(OBaseline)]
+        l.o_state_new.restype = C.c_void_p
+        l.o_state_new.argtypes = [P(S.Model), P(S.Graph), C.c_int32]
+        l.o_state_new_part.restype = C.c_void_p
+        l.o_state_new_part.argtypes = [P(S.Model), P(S.Graph), C.c_int32, C.c_int32]
+        l.o_state_run_serial.argtypes = [C.c_void_p, C.c_uint64]
+        l.o_state_inject.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        l.o_state_take_egress.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
+        l.o_state_next_time.restype = C.c_uint64
+        l.o_state_next_time.argtypes = [C.c_void_p]
+        l.o_state_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
+        l.o_state_digest.argtypes = [C.c_void_p, C.c_void_p]
+        l.o_state_stats.restype = P(ORun)
+        l.o_state_stats.argtypes = [C.c_void_p]
+        l.o_state_free.argtypes = [C.c_void_p]
         _lib = l
     return _lib
 
@@ -187,6 +201,67 @@ def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=No
     lib().o_run_free(C.byref(r))
     reset_outputs()
     return tr, dg, stats
+
+
+class OState:
+    """An oracle engine state (oracle.h o_state_*).  With `hosts=(lo, hi)` it is
+    one side of a co-simulation: only those hosts run here, their sends to the
+    others leave by take_egress(), the others' packets come in by inject()."""
+
+    def __init__(self, model: S.ModelArrays, g: S.GraphArrays, hosts=None, pushes=None):
+        self.model, self.g = model, g   # the state points into both
+        push = None if pushes is None else np.ascontiguousarray(pushes, dtype=S.EVENT_DTYPE)
+        lib().o_engine_set_pushes(None if push is None or not len(push) else push.ctypes.data,
+                                  0 if push is None else len(push))
+        if hosts is None:
+            self.ptr = lib().o_state_new(C.byref(model.struct), C.byref(g.struct), 0)
+        else:
+            self.ptr = lib().o_state_new_part(C.byref(model.struct), C.byref(g.struct), int(hosts[0]),
+                                              int(hosts[1]))
+        reset_outputs()
+        assert self.ptr, "o_state_new_part: bad host range"
+
+    def run_serial(self, t_until):
+        lib().o_state_run_serial(self.ptr, int(t_until))
+
+    def inject(self, events):
+        ev = np.ascontiguousarray(events, dtype=S.EVENT_DTYPE)
+        assert lib().o_state_inject(self.ptr, ev.ctypes.data if len(ev) else None, len(ev)) == 0
+
+    def take_egress(self) -> np.ndarray:
+        n = C.c_uint64()
+        lib().o_state_take_egress(self.ptr, None, 0, C.byref(n))
+        out = np.empty(n.value, dtype=S.EVENT_DTYPE)
+        assert lib().o_state_take_egress(self.ptr, out.ctypes.data if n.value else None, n.value,
+                                         C.byref(n)) == 0
+        return out
+
+    def next_time(self) -> int:
+        return lib().o_state_next_time(self.ptr)
+
+    def trace(self) -> np.ndarray:
+        n = C.c_uint64()
+        lib().o_state_trace(self.ptr, None, 0, C.byref(n))
+        out = np.empty(n.value, dtype=S.TRACE_DTYPE)
+        if n.value:
+            assert lib().o_state_trace(self.ptr, out.ctypes.data, n.value, C.byref(n)) == 0
+        return out
+
+    def digest(self) -> np.ndarray:
+        out = np.empty(self.model.n_hosts, dtype=S.DIGEST_DTYPE)
+        lib().o_state_digest(self.ptr, out.ctypes.data)
+        return out
+
+    def counts(self):
+        r = lib().o_state_stats(self.ptr).contents
+        return r.n_events, r.n_pkt_events
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            lib().o_state_free(self.ptr)
+            self.ptr = None
+
+    __del__ = close
 
 
 def rand_r(state: int):

@@ -43,7 +43,8 @@ def test_topology_adapter_exports_the_reference_api():
     defined = {s for s in nm(TOPO_LIB, "--defined-only") if s.startswith("topology_")}
     assert TOPOLOGY_API <= defined
     assert defined - TOPOLOGY_API == {"topology_shd_getPathPacketCount"}
-    assert {"schedulerpolicygpurounds_new", "schedulerpolicygpurounds_error"} <= nm(TOPO_LIB, "--defined-only")
+    assert {"schedulerpolicygpurounds_new", "schedulerpolicygpurounds_new_bridged",
+            "schedulerpolicygpurounds_error"} <= nm(TOPO_LIB, "--defined-only")
     undefined = nm(TOPO_LIB, "--undefined-only")
     assert SHADOW_PROVIDES <= undefined
 

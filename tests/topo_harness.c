@@ -44,15 +44,23 @@ int harness_min_jumps(double* out, int cap) {
 
 /* ---- Shadow's Event (event.c:18-43, event_compare 110-153) and glib's GQueue,
  * as much of them as sched_policy_shd.c calls ---- */
-struct _Event { uint64_t time; uint32_t dst, src; uint64_t seq; int refs; };
+struct _Event { uint64_t time; uint32_t dst, src; uint64_t seq; int refs; uint32_t pkt; };
 struct _Event* harness_event_new(uint64_t time, uint32_t src, uint32_t dst, uint64_t seq) {
     struct _Event* e = malloc(sizeof(*e));
-    e->time = time; e->src = src; e->dst = dst; e->seq = seq; e->refs = 1;
+    e->time = time; e->src = src; e->dst = dst; e->seq = seq; e->refs = 1; e->pkt = ~0u;
+    return e;
+}
+/* a deliver-packet task: the event's packet ID */
+struct _Event* harness_packet_event_new(uint64_t time, uint32_t src, uint32_t dst, uint64_t seq, uint32_t pkt) {
+    struct _Event* e = harness_event_new(time, src, dst, seq);
+    e->pkt = pkt;
     return e;
 }
 uint64_t event_getTime(struct _Event* e) { return e->time; }
 uint64_t harness_event_seq(struct _Event* e) { return e->seq; }
 uint32_t harness_event_dst(struct _Event* e) { return e->dst; }
+uint32_t harness_event_src(struct _Event* e) { return e->src; }
+uint32_t harness_event_pkt(struct _Event* e) { return e->pkt; }
 static int g_unrefs = 0;
 void event_unref(struct _Event* e) { if (--e->refs == 0) { free(e); g_unrefs++; } }
 int harness_unrefs(void) { return g_unrefs; }
