@@ -330,8 +330,10 @@ def main():
     fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and "completes the previous" in exchange
     n_ps = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_persistent", 0))
     n_bat = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches", 0))
+    n_sp = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_sparse", 0))
     kname = ("k_round_px" if fused else "k_round_xtl") if use_group else \
-        ("k_round" if world > 1 else ("k_round_ps" if n_ps and 2 * n_ps >= n_bat else "k_round_tl"))
+        ("k_round" if world > 1 else (("k_round_sp" if 2 * n_sp >= n_ps else "k_round_ps")
+                                       if n_ps and 2 * n_ps >= n_bat else "k_round_tl"))
     wkey = "%s-%dh" % (args.workload, H // max(world, 1))
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(wkey, kname),

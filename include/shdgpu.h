@@ -416,7 +416,9 @@ typedef struct shd_run_stats {
                                        each, or one persistent launch of 128 rounds;
                                        shd_xgroup: up to 64 rounds each) */
     uint64_t n_batches_persistent;  /* shd_eng batches run as one persistent launch
-                                       (k_round_ps: the round grid fits the GPU) */
+                                       (k_round_ps: the round grid fits the GPU;
+                                       k_round_sp: more hosts, blocks of many) */
+    uint64_t n_batches_sparse;      /* ... of them, sparse (k_round_sp)           */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

@@ -27,7 +27,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--vertices", type=int, default=10000)
     ap.add_argument("--hosts", type=int, default=10000)
-    ap.add_argument("--load", type=int, default=16)
+    ap.add_argument("--load", type=int, default=None)
+    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
+                    help="c4: bench.py's Tor-scale model (6.5 k relays + 50 k clients); c5: bench.py's C5 "
+                         "model at --hosts hosts (the per-GPU shard: 125000)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -43,9 +46,19 @@ def main():
     except AttributeError:   # plain build: kernel time only
         f = lambda b, k: None  # noqa: E731
     buf = (C.c_uint64 * n)()
-    g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0005)
-    hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
-    m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load, payload=1)
+    if a.workload == "c4":   # as bench.py --workload c4 (lossless edges: --lossy-edge-loss-max 0)
+        g, m = W.tor_model(6500, 50000, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 4, payload=1)
+        hv = m.host_vertex
+        a.hosts = m.n_hosts
+    elif a.workload == "c5":
+        g = W.geometric_graph(a.vertices, seed=1, loss_max=0.01)
+        hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
+        m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 32, payload=1500, bw_down=512,
+                          bw_up=10240, codelq_cap=256)
+    else:
+        g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0005)
+        hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
+        m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 16, payload=1)
     pc = PathCache(g, W.attached_vertices(hv), device=0)
     pc.build()
     eng = Engine(m, pc, 0, a.hosts, device=0)

@@ -6,7 +6,7 @@ the timing build:
     SHDGPU_LIB=shadow-1_amd/libshdgpu_tim.so python3 scripts/ps_timing.py
 
 Stamps (100 MHz wall clock; every stamp first drains the wave's memory ops):
-0 round start, 1 hand-off words read (idle test), 2 bins + inbox merged and
+0 round start, 1 hand-off words read (idle test; k_round_sp: the scan and compaction), 2 bins + inbox merged and
 sorted, 3 last flush starts, 4 event loop + flushes done, 5 close done
 (bin resets, last deliveries), 6 share published (drained), 7 every share of
 the round seen.  Printed relative to the round's earliest start: mean over
@@ -27,7 +27,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--vertices", type=int, default=10000)
     ap.add_argument("--hosts", type=int, default=10000)
-    ap.add_argument("--load", type=int, default=16)
+    ap.add_argument("--load", type=int, default=None)
+    ap.add_argument("--workload", choices=["c3", "c5"], default="c3",
+                    help="c5: bench.py's C5 model at --hosts hosts (the per-GPU shard: 125000; k_round_sp)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -38,32 +40,48 @@ def main():
     f = lib.shd_debug_timing
     f.restype = C.c_int
     f.argtypes = [C.POINTER(C.c_uint64)]
-    g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0)
     hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
-    m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load, payload=1)
+    if a.workload == "c5":
+        g = W.geometric_graph(a.vertices, seed=1, loss_max=0.01)
+        m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 32, payload=1500, bw_down=512,
+                          bw_up=10240, codelq_cap=256)
+    else:
+        g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0)
+        m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 16, payload=1)
     pc = PathCache(g, W.attached_vertices(hv), device=0)
     pc.build()
     eng = Engine(m, pc, 0, a.hosts, device=0)
     eng.boot()
     eng.run_until(2 * S.SHD_SEC)
-    st = eng.run_until(int(2.06 * S.SHD_SEC))   # under one persistent batch: its rounds leave their stamps
+    buf0 = np.zeros(64 * 2048 * 20, dtype=np.uint64)
+    f(buf0.ctypes.data_as(C.POINTER(C.c_uint64)))   # the stamps before the measured rounds
+    st = eng.run_until(2 * S.SHD_SEC + 60 * eng.window)   # under one persistent batch: its rounds leave their stamps
     print(f"persistent batches {st.n_batches_persistent} of {st.n_batches}, rounds {st.n_rounds}, "
           f"{st.device_ms_launches / max(st.n_rounds, 1) * 1e3:.2f} us/round (HIP events)")
     buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
     f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
     t = buf.reshape(64, 2048, 20).astype(np.int64)
-    grid = (a.hosts + 63) // 64
-    t = t[:, :grid, :8]
+    t_before = buf0.reshape(64, 2048, 20).astype(np.int64)
+    # the measured launch's blocks (k_round_ps: one per 64 hosts; k_round_sp: fewer) and its rounds' slots
+    fresh = t[:, :, 0] != t_before[:, :, 0]
+    grid = int(np.count_nonzero(fresh.any(axis=0)))
+    t = np.where(fresh[:, :, None], t, 0)[:, :grid, :8]
     rows = []
+    skipped = [0, 0]
     for r in range(64):
         x = t[r]
         t0 = x[:, 0].min()
         if t0 == 0 or (x[:, 6:8] < t0).any():
+            skipped[0 if t0 == 0 else 1] += 1
             continue
         rel = (x - t0) / 100.0
         rel[x < t0] = np.nan    # a phase no lane of the block reached this round (no active host)
         rows.append(rel)
     rows = np.array(rows)
+    if not len(rows):
+        print(f"no complete round among the 64 slots (no start stamp: {skipped[0]}, older stamps: {skipped[1]}; "
+              f"{grid} blocks)")
+        return
     names = ["start", "words read", "bins merged", "last flush", "loop done", "close done", "published", "all seen"]
     print(f"{len(rows)} rounds; us from the round's earliest block start: mean over rounds of (mean, max over blocks)")
     for k in range(8):

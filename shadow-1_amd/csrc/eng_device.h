@@ -17,9 +17,10 @@ constexpr uint64_t kCodelInterval = 100ull * SHD_MS;   // router_queue_codel.c:4
 // in a slot the owner reads or clears in round r or r+1.
 constexpr uint32_t kNB = 256, kBinCap = 4, kNBW = kNB / 32, kHorizon = kNB - 4;
 constexpr int kDueCap = 6;             // due-list slots per host (more due events take the heap)
-constexpr int kSendCap = 5;            // deferred sends per host between flushes (<= 16; with the
-                                       // due list and the flush's arrays, 40 KB of LDS per block:
-                                       // four blocks per CU once hosts fill the machine)
+constexpr int kPool = 288;             // deferred sends of the wave between flushes, in one pool
+                                       // shared by its hosts (a busy host may take most of it);
+                                       // with the due list and the flush's arrays, < 40 KB of LDS
+                                       // per block: four blocks per CU once hosts fill the machine
 constexpr int kBlock = 64;             // round-kernel workgroup: one wave, one host per lane
 
 struct CodelEnt {
@@ -48,8 +49,11 @@ struct SendRec {
     uint32_t chance;   // reliability draw (rand_r value)
     uint32_t pkt;
     uint32_t q_sub;    // send index within the executing event; bit 31: bootstrapping
+    uint16_t lane;     // the sending host's lane
+    uint16_t next;     // the host's next record in the pool (in send order)
+    uint32_t _pad;
 };
-static_assert(sizeof(SendRec) == 40, "send record layout");
+static_assert(sizeof(SendRec) == 48, "send record layout");
 
 // Per-host state record in HBM (local host index), one 128-B line: the round
 // kernel reads and writes it whole, as 8 16-B accesses; it holds every field
@@ -945,12 +949,29 @@ __device__ void log_pending(const DParams& P, HostCtx& c, const SendRec& q, int3
     P.pend[i] = r;
 }
 
-// LDS of the round kernel (one wave per block; [slot][lane] layouts)
-__shared__ SendRec s_send[kSendCap * kBlock];    // deferred sends
-__shared__ shd_event s_res[kSendCap * kBlock];   // flush: resolved sends, then the events to deliver
-__shared__ uint16_t s_idx[kSendCap * kBlock];    // flush: record -> (lane << 4) | slot
+// LDS of the round kernel (one wave per block).  The deferred sends of the
+// wave's hosts share one pool: a record is claimed with an LDS atomic and
+// linked into its host's list (head / tail per lane), so that one busy host
+// (a popular relay) can defer hundreds of sends between flushes while the
+// others defer a few.  A send may be deferred only while the pool has room
+// for one more record per lane (send_room): every code path defers at most
+// one send per lane between two such checks.
+__shared__ SendRec s_send[kPool];               // deferred sends
+__shared__ shd_event s_res[kPool];              // flush: resolved sends, then the events to deliver
+__shared__ uint32_t s_pool_n;                   // records claimed (may pass kPool: then unclaimed)
+__shared__ uint16_t s_shd[kBlock], s_stl[kBlock];   // each lane's first and last record
 __shared__ int32_t s_att[kBlock];                // flush: each lane's attached vertex
 __shared__ uint32_t s_cls[kBlock];               // flush: each lane's destination-weight class
+
+__device__ __forceinline__ bool send_room() {
+    const uint32_t n = __hip_atomic_load(&s_pool_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return n + (uint32_t)kBlock <= (uint32_t)kPool;
+}
+// no deferred sends (round start; every lane of the wave)
+__device__ __forceinline__ void send_pool_reset(HostCtx& c) {
+    c.ns = 0;
+    s_pool_n = 0;
+}
 
 // loopback test of a destination draw (network_interface.c:548-555): the
 // first i with dest_cum[i] >= r = x / RAND_MAX is this host, i.e.
@@ -1002,7 +1023,14 @@ __device__ void worker_send_deferred(const DParams& P, HostCtx& c, uint32_t rv, 
     q.pseq = (uint32_t)(c.ev_seq - c.seq_base);
     q.r = rv; q.chance = chance; q.pkt = pkt;
     q.q_sub = (c.q_sub++ & 0x7FFFFFFFu) | (bootstrapping(P, c) ? 0x80000000u : 0u);
-    s_send[c.ns * kBlock + threadIdx.x] = q;
+    q.lane = (uint16_t)threadIdx.x;
+    q.next = 0xFFFFu;
+    q._pad = 0;
+    const uint32_t k = atomicAdd(&s_pool_n, 1u);   // < kPool: the caller saw send_room()
+    s_send[k] = q;
+    if (c.ns) s_send[s_stl[threadIdx.x]].next = (uint16_t)k;
+    else s_shd[threadIdx.x] = (uint16_t)k;
+    s_stl[threadIdx.x] = (uint16_t)k;
     c.ns++;
     c.ev_seq++;   // provisional: a dropped send gives its ID back at the flush
     c.if_out++;   // tracker_addOutputBytes (network_interface.c:571)
@@ -1026,16 +1054,10 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     pd.kind = 0;
     const uint32_t lane = threadIdx.x;
     const uint32_t n = c.ns;
-    uint32_t pre = n;   // inclusive, then exclusive prefix of the lanes' counts
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(pre, off, 64);
-        if ((int)lane >= off) pre += o;
-    }
-    const uint32_t total = __shfl(pre, 63, 64);
-    pre -= n;
+    const uint32_t claimed = __hip_atomic_load(&s_pool_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const uint32_t total = __builtin_amdgcn_readfirstlane(claimed < (uint32_t)kPool ? claimed : (uint32_t)kPool);
     if (total == 0) return;
     const bool one = defer && total <= (uint32_t)kBlock;   // the round's last flush, one batch
-    for (uint32_t i = 0; i < n; i++) s_idx[pre + i] = (uint16_t)((lane << 4) | i);
     s_att[lane] = c.att;
     s_cls[lane] = c.cls;
     __syncthreads();
@@ -1046,9 +1068,8 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     for (uint32_t base = 0; base < total; base += kBlock) {
         const uint32_t r = base + lane;
         if (r >= total) continue;
-        const uint32_t id = s_idx[r];
-        const uint32_t hl = id >> 4, i = id & 15u;
-        const SendRec q = s_send[i * kBlock + hl];
+        const SendRec q = s_send[r];
+        const uint32_t hl = q.lane;
         const int32_t a = s_att[hl];
         int32_t dst, b;
         if (P.dest_closed) {   // no table: one memory round trip fewer
@@ -1107,11 +1128,17 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
 #ifdef SHD_TIMING_LIGHT
     TIM(13);
 #endif
-    // per host, in send order (worker.c:286-320)
-    uint32_t failmask = 0, nfail = 0;
+    // per host, in send order (worker.c:286-320).  Timers scheduled since the
+    // last flush hold provisional IDs: an ID x loses the dropped sends issued
+    // before it
+    uint32_t nfail = 0;
+    uint64_t f0 = 0, f1 = 0, f2 = 0;
+    const bool p0 = c.tt0 != kInf && c.ts0 >= c.seq_base, p1 = c.tt1 != kInf && c.ts1 >= c.seq_base,
+               p2 = c.tt2 != kInf && c.ts2 >= c.seq_base;
+    uint32_t k = n ? s_shd[lane] : 0u;
     for (uint32_t i = 0; i < n; i++) {
-        shd_event e = s_res[pre + i];
-        const SendRec q = s_send[i * kBlock + lane];
+        shd_event e = s_res[k];
+        const SendRec q = s_send[k];
         const bool pass = e.kind & 1u, log = (e.kind & 2u) != 0, resolved = (e.kind & 4u) != 0;
         const int32_t b = (int32_t)e.src;
         uint32_t emit = 0;
@@ -1130,35 +1157,26 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             trace(P, c, q.now, 0, c.h, e.dst, q.pkt, SHD_TR_INET_DROP);
             c.c_idrop++;
             if (log) log_pending(P, c, q, c.att, b, 0u, e.dst, 0);
-            failmask |= 1u << i;
+            const uint64_t xi = c.seq_base + q.pseq;
+            f0 += xi < c.ts0; f1 += xi < c.ts1; f2 += xi < c.ts2;
             nfail++;
         }
         e.src = c.h;
         e.pkt = q.pkt;
         e.kind = emit;
-        s_res[pre + i] = e;
+        s_res[k] = e;
+        k = q.next;
     }
     if (nfail) {
-        // timers scheduled since the last flush hold provisional IDs: an ID
-        // x loses the dropped sends issued before it
-        uint64_t f0 = 0, f1 = 0, f2 = 0;
-        const bool p0 = c.tt0 != kInf && c.ts0 >= c.seq_base, p1 = c.tt1 != kInf && c.ts1 >= c.seq_base,
-                   p2 = c.tt2 != kInf && c.ts2 >= c.seq_base;
-        if (p0 || p1 || p2) {
-            for (uint32_t i = 0; i < n; i++) {
-                if (!((failmask >> i) & 1u)) continue;
-                const uint64_t xi = c.seq_base + s_send[i * kBlock + lane].pseq;
-                f0 += xi < c.ts0; f1 += xi < c.ts1; f2 += xi < c.ts2;
-            }
-            if (p0) c.ts0 -= f0;
-            if (p1) c.ts1 -= f1;
-            if (p2) c.ts2 -= f2;
-        }
+        if (p0) c.ts0 -= f0;
+        if (p1) c.ts1 -= f1;
+        if (p2) c.ts2 -= f2;
         c.ev_seq -= nfail;
     }
     c.seq_base = c.ev_seq;
     c.ns = 0;
     __syncthreads();
+    if (lane == 0) s_pool_n = 0;   // (every lane read it above, before the barrier)
 #ifdef SHD_TIMING_LIGHT
     TIM(14);
 #endif
@@ -1189,7 +1207,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         emit_nocal(P, c, e);
     }
     c.err |= err;
-    __syncthreads();   // s_res / s_idx are reused by the next flush
+    __syncthreads();   // s_res is reused by the next flush
 }
 
 // the stores of the round's last flush (after its claims returned)
@@ -1224,7 +1242,7 @@ __device__ bool if_send_step(const DParams& P, HostCtx& c) {
             c.tq_hv = true;
         }
         const bool self = is_self_draw(c, p.r);
-        if (c.ns && (self || c.ns == (uint32_t)kSendCap)) return true;
+        if ((c.ns && self) || !send_room()) return true;
         c.tq_hv = false;
         c.tq_head = (c.tq_head + 1 == c.k.tq_cap) ? 0 : c.tq_head + 1;
         c.tq_count--;
@@ -1323,7 +1341,7 @@ __device__ void refill_cb(const DParams& P, HostCtx& c) {
 // draws this host (then the general send loop takes it).  The same draws and
 // steps, in the same order, as the general NOTIFY path of begin_event.
 __device__ __forceinline__ bool notify_fast_ok(const DParams& P, const HostCtx& c) {
-    return c.unread == 1u && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap &&
+    return c.unread == 1u && c.tq_count == 0 && c.tx_rem >= SHD_MTU && send_room() &&
            !(c.k.feat & F_TRACE) && !bootstrapping(P, c);
 }
 __device__ __forceinline__ void notify_fast(const DParams& P, HostCtx& c) {
@@ -1497,7 +1515,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     // bootstrap period -- is left to run_work's general loop, in order
     const bool boot = bootstrapping(P, c);
     // (one exit: a loopback ends the loop through tq_count)
-    while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && c.ns < (uint32_t)kSendCap && !boot) {
+    while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && send_room() && !boot) {
         app_read(P, c);
         const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
         c.w_msgs--;
@@ -1579,7 +1597,7 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.att = launder(att);
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
     c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0; c.dt = kInf;
-    c.ns = 0; c.seq_base = c.ev_seq; c.np = 0;
+    send_pool_reset(c); c.seq_base = c.ev_seq; c.np = 0;
     c.w_msgs = 0; c.w_fl = 0;
     c.self_lo = launder(st.x);
     c.self_hi = launder(st.y);

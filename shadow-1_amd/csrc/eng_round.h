@@ -249,7 +249,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
     hot_load(P, c);
     PendDel pd;
-    c.ns = 0; c.att = 0; c.cls = 0; c.err = 0;
+    send_pool_reset(c); c.att = 0; c.cls = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0;
     // the window's non-empty bins, all slots loaded before the host record is
     // consumed (one round trip, overlapping the record's)
@@ -272,8 +272,8 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
         rec_att = P.host_att[P.h0 + l];
         rec_st = P.self_thr[P.h0 + l];
     }
+    PROF_T0(t_all)
     if (active) {
-        PROF_T0(t_all)
         load_ctx(P, c, l, rec, rec_att, rec_st);
         TIMA(7);
         c.ws = ws;
@@ -984,51 +984,31 @@ __device__ __forceinline__ void ps_round_reset(HostCtx& c, uint64_t ws, int pari
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = 0; c.xput = 0;
     c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
-    c.dh = 0; c.nd = 0; c.dt = kInf; c.ns = 0; c.seq_base = c.ev_seq;
+    c.dh = 0; c.nd = 0; c.dt = kInf; send_pool_reset(c); c.seq_base = c.ev_seq;
     c.w_msgs = 0; c.w_fl = 0;
 }
 
-// One round [ws, we) of the lane's host (has: the lane has one; lb: its index
-// in the block) on the context it keeps in registers; as round_body
-__device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, const PsRsrc& R, uint64_t ws,
-                         uint64_t we, int parity, uint64_t& next_out) {
-    ps_round_reset(c, ws, parity);
-    // the round's hand-off words: this parity's inbox count, the calendar bitmap
-    uint32_t nin = 0;
-    uint32_t w[kNBW];
-#pragma unroll
-    for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
-    if (has) {
-        nin = ld4_sc1(R.nin, lb * 4u);
-        if (P.bins) {
-            const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
-            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-        }
-    }
+// The round of a lane's host once its hand-off words are read (nin: this
+// parity's inbox count; w: the calendar bitmap, wbits its window bins):
+// bins and inbox merged, the event loop, the close.  `active` lanes run; the
+// others take part in the wave's flushes only.  `next` holds an idle lane's
+// next time on entry and is set for an active one.  As round_body, with the
+// hand-off arrays read by sc1 loads (other blocks of the launch wrote them).
+// SP (k_round_sp): the context is loaded here, from the record the caller
+// issued the loads of, once the bins' loads are out too (one round trip)
+struct SpIn {
+    HostRec rec;
+    int32_t att;
+    int4 st;
+    int32_t l;
+};
+template <bool SP>
+__device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool active, uint32_t lb, const PsRsrc& R,
+                                              uint64_t ws, uint64_t we, int parity, uint32_t nin,
+                                              uint32_t (&w)[kNBW], uint32_t wbits, uint64_t& next,
+                                              const SpIn* sp = nullptr) {
     const uint64_t b0 = ws >> P.bin_shift;
     const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
-    uint32_t wbits = 0;
-    if (P.bins) {
-#pragma unroll
-        for (uint32_t j = 0; j < 3; j++)
-            if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
-    }
-    if (nbin > 3) c.err |= SHD_ERR_INTERNAL;
-    uint64_t next = kInf;
-    const uint64_t t0 = host_next(c);
-    bool active = false;
-    TIM(1);
-    if (has) {
-        if (nin == 0 && t0 >= we && wbits == 0) {
-            next = t0;
-            if (P.bins) {
-                const uint64_t cb = cal_lower_bound(P, w, we);
-                next = cb < next ? cb : next;
-            }
-        } else {
-            active = true;
-        }
-    }
     // the window's bins, every slot of a non-empty one in one round trip
     EvV bx[3][kBinCap];
     if (active && P.bins) {
@@ -1042,6 +1022,10 @@ __device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, co
                 bx[j][k] = EvV{ld16_sc1(R.bins, off), ld16_sc1(R.bins, off + 16)};
             }
         }
+    }
+    if (SP) {
+        if (active) load_ctx(P, c, sp->l, sp->rec, sp->att, sp->st);
+        ps_round_reset(c, ws, parity);
     }
     if (active) {
         if (nin) {   // inbound events of the previous round -> heap
@@ -1156,6 +1140,60 @@ __device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, co
     }
     flush_finish(P, c, pd);
     TIM(5);
+}
+
+// the window bins of a bitmap (bit j: bin b0 + j is non-empty); an idle
+// host's next time from its own next event and its bitmap
+__device__ __forceinline__ uint32_t ps_window_bits(const DParams& P, HostCtx& c, const uint32_t (&w)[kNBW],
+                                                   uint64_t ws, uint64_t we) {
+    const uint64_t b0 = ws >> P.bin_shift;
+    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
+    uint32_t wbits = 0;
+    if (P.bins) {
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++)
+            if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
+    }
+    if (nbin > 3) c.err |= SHD_ERR_INTERNAL;
+    return wbits;
+}
+__device__ __forceinline__ uint64_t ps_idle_next(const DParams& P, const uint32_t (&w)[kNBW], uint64_t t0,
+                                                 uint64_t we) {
+    uint64_t next = t0;
+    if (P.bins) {
+        const uint64_t cb = cal_lower_bound(P, w, we);
+        next = cb < next ? cb : next;
+    }
+    return next;
+}
+
+// One round [ws, we) of the lane's host (has: the lane has one; lb: its index
+// in the block) on the context it keeps in registers; as round_body
+__device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, const PsRsrc& R, uint64_t ws,
+                         uint64_t we, int parity, uint64_t& next_out) {
+    ps_round_reset(c, ws, parity);
+    // the round's hand-off words: this parity's inbox count, the calendar bitmap
+    uint32_t nin = 0;
+    uint32_t w[kNBW];
+#pragma unroll
+    for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+    if (has) {
+        nin = ld4_sc1(R.nin, lb * 4u);
+        if (P.bins) {
+            const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+        }
+    }
+    const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
+    uint64_t next = kInf;
+    const uint64_t t0 = host_next(c);
+    bool active = false;
+    TIM(1);
+    if (has) {
+        if (nin == 0 && t0 >= we && wbits == 0) next = ps_idle_next(P, w, t0, we);
+        else active = true;
+    }
+    ps_round_body<false>(P, c, active, lb, R, ws, we, parity, nin, w, wbits, next);
     next_out = next;
 }
 
@@ -1336,6 +1374,201 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         c.c_events = acc[0]; c.c_pkt = acc[1]; c.c_sent = acc[2];
         c.c_idrop = acc[3]; c.c_cdrop = acc[4]; c.c_recv = acc[5];
         store_ctx(P0, c);
+    }
+}
+
+// ------------------------------------------------------ sparse persistent rounds
+// k_round_sp: k_round_ps for engines whose hosts outnumber what one resident
+// wave per 64 hosts can hold (the per-GPU shard of the north-star model:
+// 125 k hosts = 1954 waves of ~256 VGPRs and 40 KB of LDS, against 1024 such
+// waves resident; k_round_tl then runs every round in two passes of blocks).
+// Here a block owns `sph` hosts (a multiple of 64; one block per CU) and, per
+// round, scans their hand-off words and own next times (hnext), compacts the
+// hosts with something due into a list in LDS, and runs them 64 at a time:
+// each pass loads its hosts' records (load_ctx), runs ps_round_body, and
+// stores them (store_ctx, with hnext).  In the models this is for, a few
+// percent of the hosts have an event in a given window, so a round is one
+// pass of a few active lanes per block instead of every host's lane.  The
+// hosts' records, heaps and queues are read and written by their own block
+// only (plain accesses, one CU); the hand-off arrays by sc1 loads, as in
+// k_round_ps, whose share protocol and ring summaries this kernel shares.
+constexpr uint32_t kSpMaxHosts = 4096;   // hosts per block at most (64 groups of 64)
+__shared__ uint16_t s_act[kSpMaxHosts];  // the round's active hosts (index in the block)
+__shared__ uint32_t s_aw[(kNBW + 1) * kBlock];   // the first pass's hand-off words: bitmap, inbox count
+
+__global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, DevSummary* __restrict__ ring,
+                                                      const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
+                                                      const DParams* __restrict__ Pr, uint64_t ticks, uint32_t sph) {
+    const DParams& P0 = Pr[1];
+    const uint32_t nblk = gridDim.x;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t hb = blockIdx.x * sph;   // the block's first host
+    const uint32_t nh = (uint32_t)P0.nloc - hb < sph ? (uint32_t)P0.nloc - hb : sph;
+    const uint32_t ngrp = (nh + 63u) >> 6;
+    PsRsrc R0, R1;   // parity 0 and 1, over the block's hosts
+    {
+        R0.bits = buf_rsrc(P0.bin_bits ? P0.bin_bits + (size_t)hb * kNBW : nullptr, (uint64_t)nh * kNBW * 4);
+        R0.bins = buf_rsrc(P0.bins ? P0.bins + (size_t)hb * kNB * kBinCap : nullptr,
+                           (uint64_t)nh * kNB * kBinCap * sizeof(shd_event));
+        R1.bits = R0.bits;
+        R1.bins = R0.bins;
+        R0.nin = buf_rsrc(P0.inbox_n[0] + hb, (uint64_t)nh * 4);
+        R1.nin = buf_rsrc(P0.inbox_n[1] + hb, (uint64_t)nh * 4);
+        R0.inbox = buf_rsrc(P0.inbox[0] + (size_t)hb * P0.inbox_cap, (uint64_t)nh * P0.inbox_cap * sizeof(shd_event));
+        R1.inbox = buf_rsrc(P0.inbox[1] + (size_t)hb * P0.inbox_cap, (uint64_t)nh * P0.inbox_cap * sizeof(shd_event));
+    }
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
+    HostCtx c;
+    hot_load(P0, c);
+    c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf;
+    c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
+    uint64_t ws = ring[0].next_time;
+    const uint64_t stop = ctl->stop, rbase = ctl->round_base;
+    const uint32_t tag0 = (uint32_t)ctl->xtag;
+    const bool lead = blockIdx.x == 0 && lane == 0;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    for (int i = 0; i < nb; i++) {
+        const DParams& P = Pr[i + 1];
+        const unsigned long long t_start = wall_clock64();
+#ifdef SHD_TIMING
+        if (lane == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = t_start;
+#endif
+        if (lead) ps_fresh(&ring[i + 2]);
+        const int parity = (int)((rbase + (uint64_t)i) & 1);
+        uint64_t we = ws + window;
+        if (we > stop || we < ws) we = stop;
+        PsRsrc R = R0;
+        R.nin = parity ? R1.nin : R0.nin;
+        R.inbox = parity ? R1.inbox : R0.inbox;
+        ps_round_reset(c, ws, parity);
+        // the scan: every host's words and own next time, four groups per round trip
+        uint64_t next = kInf;
+        uint32_t nact = 0;
+        for (uint32_t g0 = 0; g0 < ngrp; g0 += 4) {
+            uint32_t nin4[4], w4[4][kNBW];
+            uint64_t t4[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t lb = (g0 + q) * 64u + lane;
+                nin4[q] = 0; t4[q] = kInf;
+#pragma unroll
+                for (int j = 0; j < (int)kNBW; j++) w4[q][j] = 0;
+                if (g0 + q < ngrp && lb < nh) {
+                    nin4[q] = ld4_sc1(R.nin, lb * 4u);
+                    if (P.bins) {
+                        const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                        w4[q][0] = x.x; w4[q][1] = x.y; w4[q][2] = x.z; w4[q][3] = x.w;
+                        w4[q][4] = y.x; w4[q][5] = y.y; w4[q][6] = y.z; w4[q][7] = y.w;
+                    }
+                    t4[q] = P.hnext[hb + lb];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t lb = (g0 + q) * 64u + lane;
+                const bool has = g0 + q < ngrp && lb < nh;
+                const uint32_t wbits = ps_window_bits(P, c, w4[q], ws, we);
+                const bool act = has && !(nin4[q] == 0 && t4[q] >= we && wbits == 0);
+                if (has && !act) {
+                    const uint64_t t = ps_idle_next(P, w4[q], t4[q], we);
+                    next = t < next ? t : next;
+                }
+                const uint64_t m = __ballot(act);
+                if (act) {
+                    const uint32_t k = nact + (uint32_t)__popcll(m & lt_mask);
+                    s_act[k] = (uint16_t)lb;
+                    if (k < (uint32_t)kBlock) {
+#pragma unroll
+                        for (int j = 0; j < (int)kNBW; j++) s_aw[j * kBlock + k] = w4[q][j];
+                        s_aw[kNBW * kBlock + k] = nin4[q];
+                    }
+                }
+                nact += (uint32_t)__popcll(m);
+            }
+        }
+        __syncthreads();
+        TIM(1);
+        // the active hosts, 64 at a time
+        uint32_t nev = 0, npkt = 0, fl = 0, nhost = 0;
+        for (uint32_t base = 0; base < nact; base += kBlock) {
+            const uint32_t k = base + lane;
+            const bool act = k < nact;
+            const uint32_t lb = act ? (uint32_t)s_act[k] : 0u;
+            const int32_t l = (int32_t)(hb + lb);
+            uint32_t nin = 0, w[kNBW];
+#pragma unroll
+            for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+            if (act) {
+                if (base == 0) {
+#pragma unroll
+                    for (int j = 0; j < (int)kNBW; j++) w[j] = s_aw[j * kBlock + k];
+                    nin = s_aw[kNBW * kBlock + k];
+                } else {   // later passes (more than 64 active hosts): the words again
+                    nin = ld4_sc1(R.nin, lb * 4u);
+                    if (P.bins) {
+                        const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+                    }
+                }
+            }
+            SpIn in;   // the record's loads go out with the bins' (ps_round_body<true>)
+            in.l = l;
+            if (act) {
+                in.rec = P.hs[l];
+                in.att = P.host_att[P.h0 + l];
+                in.st = P.self_thr[P.h0 + l];
+            }
+            const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
+            uint64_t hn = kInf;
+            ps_round_body<true>(P, c, act, lb, R, ws, we, parity, nin, w, wbits, hn, &in);
+            if (act) store_ctx(P, c);
+            next = hn < next ? hn : next;
+            nev += c.c_events; npkt += c.c_pkt;
+            fl |= c.err | (c.n_pend ? kPsPend : 0u);
+            nhost += (uint32_t)__popcll(__ballot(act && c.c_events != 0));
+            __syncthreads();   // (the next pass reuses the lanes' LDS slots)
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(next, off, 64);
+            next = o < next ? o : next;
+            nev += __shfl_xor(nev, off, 64);
+            npkt += __shfl_xor(npkt, off, 64);
+            fl |= __shfl_xor(fl, off, 64);
+        }
+        const uint32_t tag = tag0 + (uint32_t)i;
+        const uint32_t sbase = (uint32_t)(i & 1) * nblk;
+        ps_publish(rs, sbase + blockIdx.x, next, fl, nev, npkt, nhost, tag);
+        TIM(6);
+        uint64_t f_next;
+        uint32_t f_fl, f_nev, f_npkt, f_nact;
+        const bool ok_v = ps_gather(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
+        TIM(7);
+        const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;
+        f_fl = __builtin_amdgcn_readfirstlane(f_fl);
+        f_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(f_next >> 32)) << 32) |
+                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)f_next);
+        if (!ok) {
+            if (lane == 0) {
+                atomicOr(&ring[i + 1].error, SHD_ERR_INTERNAL);
+                *P.halt = 1u;
+            }
+            break;
+        }
+        if (lead) {
+            DevSummary* sm = &ring[i + 1];
+            atomicMin(&sm->next_time, f_next);
+            if (f_nev) atomicAdd(&sm->n_events, (unsigned long long)f_nev);
+            if (f_npkt) atomicAdd(&sm->n_pkt_events, (unsigned long long)f_npkt);
+            if (f_nact) atomicAdd(&sm->n_active, f_nact);
+            if (f_fl & ~kPsPend) atomicOr(&sm->error, f_fl & ~kPsPend);
+            atomicMin(&sm->t_first, t_start);
+            atomicMax(&sm->t_last, (unsigned long long)wall_clock64());
+            __hip_atomic_store(&sm->ws, (unsigned long long)ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (f_fl & kPsPend) *P.halt = 1u;
+        }
+        if (f_fl) break;
+        ws = f_next;
+        if (ws >= stop) break;
     }
 }
 

@@ -129,6 +129,9 @@ struct shd_eng {
     // persistent rounds (k_round_ps): one launch per batch when the round grid
     // fits the GPU one block per CU and the engine holds every host
     bool ps_ok = false;
+    bool sp_ok = false;                     // the sparse persistent kernel (k_round_sp) instead
+    uint32_t sp_hosts = 0;                  // ... its hosts per block
+    uint32_t sp_grid = 0;
     PsShare* d_pshare = nullptr;            // [2][grid] tagged round shares
     uint32_t ps_epoch = 1;                  // share tags issued (never 0, never reused)
     double wall_khz = 100000.0;             // device wall clock (wall_clock64) rate
@@ -476,10 +479,34 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             per_cu = 0;
         (void)hipGetLastError();
         // (blocks of one wave: up to two per CU, below what LDS and registers admit)
-        e->ps_ok = e->h0 == 0 && e->nloc == H && ncu > 0 && per_cu >= 2 && grid <= 2 * ncu;
-        if (e->ps_ok) {
+        // SHD_SP_HOSTS=<n>: the sparse kernel with n hosts per block whatever the size
+        // (it selects between exact paths: a knob for tests and measurements)
+        const char* sp_env = getenv("SHD_SP_HOSTS");
+        const uint32_t sp_force = sp_env ? (uint32_t)strtoul(sp_env, nullptr, 10) : 0u;
+        e->ps_ok = e->h0 == 0 && e->nloc == H && ncu > 0 && per_cu >= 2 && grid <= 2 * ncu && !sp_force;
+        size_t nshare = e->ps_ok ? (size_t)grid : 0;
+        if (!e->ps_ok && e->h0 == 0 && e->nloc == H && ncu > 0) {
+            // too many hosts for a resident wave each: blocks of sph hosts, one per CU
+            int per_cu_sp = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_sp, reinterpret_cast<const void*>(&k_round_sp),
+                                                             kBlock, 0) != hipSuccess)
+                per_cu_sp = 0;
+            (void)hipGetLastError();
+            const uint64_t per = ((uint64_t)e->nloc + ncu - 1) / ncu;
+            const uint32_t sph = sp_force ? (sp_force + 63) / 64 * 64
+                                          : (uint32_t)std::max<uint64_t>(256, (per + 63) / 64 * 64);
+            const uint32_t g = (uint32_t)(((uint64_t)e->nloc + sph - 1) / sph);
+            const bool no_sp = getenv("SHD_NO_SP") != nullptr;   // perf knob: k_round_tl batches instead
+            if (!no_sp && per_cu_sp >= 1 && sph <= kSpMaxHosts && g <= (uint32_t)(ncu * per_cu_sp)) {
+                e->sp_ok = true;
+                e->sp_hosts = sph;
+                e->sp_grid = g;
+                nshare = g;
+            }
+        }
+        if (nshare) {
             int rc;
-            if ((rc = ealloc(e, &e->d_pshare, 2 * (size_t)grid))) { shd_eng_destroy(e); return rc; }
+            if ((rc = ealloc(e, &e->d_pshare, 2 * nshare))) { shd_eng_destroy(e); return rc; }
         }
     }
     *out = e;
@@ -815,10 +842,15 @@ static int launch_batch(shd_eng* e, bool tl) {
 // a persistent batch: nb rounds in one launch (k_round_ps); the shares' tags
 // advance past the batch whatever it ran
 static int launch_batch_ps(shd_eng* e, int nb) {
-    const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
-    hipLaunchKernelGGL(k_round_ps, dim3(grid), dim3(kBlock), 0, e->stream, e->window, nb, e->d_ring,
-                       (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr, ticks);
+    if (e->sp_ok) {
+        hipLaunchKernelGGL(k_round_sp, dim3(e->sp_grid), dim3(kBlock), 0, e->stream, e->window, nb, e->d_ring,
+                           (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr, ticks, e->sp_hosts);
+    } else {
+        const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
+        hipLaunchKernelGGL(k_round_ps, dim3(grid), dim3(kBlock), 0, e->stream, e->window, nb, e->d_ring,
+                           (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr, ticks);
+    }
     SHD_HIP(hipGetLastError());
     e->ps_epoch += (uint32_t)nb;
     if (e->ps_epoch < (uint32_t)nb + 1u) e->ps_epoch = 1;   // (wrapped: restart past 0)
@@ -960,11 +992,12 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         static const bool no_tl = getenv("SHD_NO_TL") != nullptr;
         static const bool no_ps = getenv("SHD_NO_PS") != nullptr;   // perf knob: launch-per-round batches only
         const bool tl = e->tl_ready && !no_tl;
-        const bool ps = tl && e->ps_ok && !no_ps;
+        const bool ps = tl && (e->ps_ok || e->sp_ok) && !no_ps;
         const int nb = ps ? shd_eng::kPsBatch : B;
         if (ps) {
             if ((rc = launch_batch_ps(e, nb))) break;
             s.n_batches_persistent++;
+            if (e->sp_ok) s.n_batches_sparse++;
         } else if ((rc = launch_batch(e, tl))) {
             break;
         }

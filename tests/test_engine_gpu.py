@@ -196,6 +196,32 @@ def test_run_to_run_determinism():
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("sph,kind", [(256, "geo"), (64, "geo"), (1024, "codel"), (192, "complete")])
+def test_sparse_persistent_rounds_match_oracle(sph, kind, monkeypatch):
+    """k_round_sp (the engines with more hosts than resident waves: the C5
+    shard) forced on small models with SHD_SP_HOSTS: blocks of `sph` hosts scan
+    their hosts, compact the active ones and run them 64 at a time (several
+    passes a round at 1024 hosts per block); the result is the serial run's."""
+    monkeypatch.setenv("SHD_SP_HOSTS", str(sph))
+    if kind == "complete":
+        g = W.bundled_graph()
+        hv = np.sort(np.random.default_rng(2).integers(0, g.n_vertices, 700)).astype(np.int32)
+        m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, load=8)
+    elif kind == "codel":
+        g = W.geometric_graph(300, seed=8)
+        m = W.phold_model(W.hosts_on_vertices(300, 4), end_time=3 * S.SHD_SEC, trace=True, load=24,
+                          payload=1000, bw_down=600, bw_up=100000, codelq_cap=256)
+    else:
+        g = W.geometric_graph(400, seed=2)
+        m = W.phold_model(W.hosts_on_vertices(400, 2), end_time=3 * S.SHD_SEC, trace=True)
+    gpu, ora, eng, _ = run_both(g, m)
+    assert_same(gpu, ora)
+    st = gpu[2]
+    assert st.n_batches_sparse > 0 and st.n_batches_sparse == st.n_batches_persistent
+    if kind == "codel":
+        assert np.count_nonzero(gpu[0]["kind"] == S.TR_CODEL_DROP) > 0
+
+
 @pytest.mark.parametrize("parts", [2, 3])
 def test_sharded_engines_match_oracle(parts):
     """Hosts partitioned over several engines (DESIGN.md "Multi-GPU"): the
