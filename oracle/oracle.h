@@ -17,10 +17,17 @@
  *    its TIE-BREAKING is restated from its published algorithm and is
  *    "parity unpinned" ("Oracle").
  *  - Event loop: restated from worker.c / event.c / scheduler.c /
- *    network_interface.c / router.c; the reference loop cannot be built here
- *    (process.c needs generated rpth.h, topology.c needs igraph).  Its pieces
- *    are pinned individually (RNG, CoDel, queue order) and the loop by
- *    self-consistency with the GPU engine.
+ *    network_interface.c / router.c / tracker.c.  Pinned as a whole to the
+ *    reference's OWN serial loop: worker.c, scheduler.c, host.c,
+ *    network_interface.c, router*.c, descriptor/*.c, tracker.c, packet.c ...
+ *    compiled unmodified into oracle/_ref/libshdref_loop.so, with test doubles
+ *    only for what the image cannot build (slave.c, the igraph topology --
+ *    served by this oracle's lazy path cache --, the rpth process layer, the
+ *    loggers; oracle/ref_harness/ref_loop.c).  Every [STATUS] and [node] line,
+ *    event-ID and packet counter and RNG state of eight models (lossy, CoDel,
+ *    loopback, per-host heartbeats, pushed multi-process starts, bootstrap,
+ *    the Tor-scale classes, C1) equals the reference's
+ *    (tests/golden/ref_loop.json, tests/test_ref_loop_cpu.py).
  */
 #ifndef SHD_ORACLE_H
 #define SHD_ORACLE_H

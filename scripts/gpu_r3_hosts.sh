@@ -2,7 +2,7 @@
 # round 3: per-GPU shard of the north star (C5 model, 125 k hosts) as one engine and as a
 # one-rank fused group; C4 (Tor-scale, 56.5 k hosts); C3 at 100 k hosts
 set -o pipefail
-O=gpurun_out/r03/hosts
+O=${HOSTS_OUT:-gpurun_out/r03/hosts}
 mkdir -p $O
 run() {  # name, args...
   local n=$1; shift

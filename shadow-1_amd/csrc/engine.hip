@@ -130,6 +130,8 @@ struct shd_eng {
     // fits the GPU one block per CU and the engine holds every host
     bool ps_ok = false;
     bool sp_ok = false;                     // the sparse persistent kernel (k_round_sp) instead
+    bool sp_dense = false;                  // the last batch had many active hosts: launch-per-round batches
+    bool sp_forced = false;                 // SHD_SP_HOSTS: the sparse kernel whatever the density
     uint32_t sp_hosts = 0;                  // ... its hosts per block
     uint32_t sp_grid = 0;
     PsShare* d_pshare = nullptr;            // [2][grid] tagged round shares
@@ -499,6 +501,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             const bool no_sp = getenv("SHD_NO_SP") != nullptr;   // perf knob: k_round_tl batches instead
             if (!no_sp && per_cu_sp >= 1 && sph <= kSpMaxHosts && g <= (uint32_t)(ncu * per_cu_sp)) {
                 e->sp_ok = true;
+                e->sp_forced = sp_force != 0;
                 e->sp_hosts = sph;
                 e->sp_grid = g;
                 nshare = g;
@@ -841,6 +844,9 @@ static int launch_batch(shd_eng* e, bool tl) {
 
 // a persistent batch: nb rounds in one launch (k_round_ps); the shares' tags
 // advance past the batch whatever it ran
+// active hosts per round above which launch-per-round batches beat k_round_sp
+static constexpr double kSpDenseFrac = 0.08;
+
 static int launch_batch_ps(shd_eng* e, int nb) {
     const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
     if (e->sp_ok) {
@@ -992,7 +998,12 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         static const bool no_tl = getenv("SHD_NO_TL") != nullptr;
         static const bool no_ps = getenv("SHD_NO_PS") != nullptr;   // perf knob: launch-per-round batches only
         const bool tl = e->tl_ready && !no_tl;
-        const bool ps = tl && (e->ps_ok || e->sp_ok) && !no_ps;
+        // the sparse kernel scans and compacts its blocks' active hosts every
+        // round: it wins while few hosts are active (C5 at 125 k hosts: 4 % of
+        // the hosts per round, 25.3 against 30.8 us per round), launch-per-round
+        // batches when many are (C4: 14 %, 146 against 211 us; C3 at 100 k: 37 %,
+        // 43 against 63 us).  Both are exact: the choice follows the last batch.
+        const bool ps = tl && (e->ps_ok || (e->sp_ok && !e->sp_dense)) && !no_ps;
         const int nb = ps ? shd_eng::kPsBatch : B;
         if (ps) {
             if ((rc = launch_batch_ps(e, nb))) break;
@@ -1018,6 +1029,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         // with at most one logging round the next batch is ticketless (the
         // late, rare logs cost one halt each); after more, it is ticketed.
         uint32_t n_logs = 0;
+        uint64_t b_rounds = 0, b_active = 0;
         for (int i = 0; i < nb; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
@@ -1031,6 +1043,8 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             s.n_events += r.n_events;
             s.n_pkt_events += r.n_pkt_events;
             s.n_host_rounds += r.n_active;
+            b_rounds++;
+            b_active += r.n_active;
             uint64_t we = ws + e->window;
             if (we > stop || we < ws) we = stop;
             s.final_time = we;
@@ -1069,6 +1083,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             next = r.next_time;
         }
         e->tl_ready = n_logs <= 1;
+        if (b_rounds && tl && !e->sp_forced) e->sp_dense = (double)b_active > kSpDenseFrac * (double)b_rounds * (double)e->nloc;
     }
     e->h_sum->next_time = next;
     // every event before `stop` has run: the engine's clock stands at stop
