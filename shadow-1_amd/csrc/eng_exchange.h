@@ -607,7 +607,8 @@ __device__ __forceinline__ uint32_t xrgn_store(const DParams& P, const shd_event
 __device__ __forceinline__ void px_fold_put(const DParams& P, DevSummary* sum, const TlPart (&pv)[4],
                                             const TlPart* __restrict__ pp, uint32_t nblk, uint64_t pws,
                                             uint64_t npend, uint64_t nrem, uint64_t pnext, uint32_t perr,
-                                            uint64_t stop, uint32_t halt, shd_event* const* __restrict__ peers,
+                                            uint64_t stop, uint32_t halt, uint32_t bad,
+                                            shd_event* const* __restrict__ peers,
                                             int world, int me, int wi, uint32_t tag, uint64_t xhoff, int nrep) {
     const int p = (int)blockIdx.x;
     const size_t stride = (size_t)P.xcap + 1;
@@ -653,6 +654,13 @@ __device__ __forceinline__ void px_fold_put(const DParams& P, DevSummary* sum, c
         }
     } else {
         h = *(const XHeader*)src;
+        // this engine's wait for a peer timed out: the re-sent header carries
+        // an error, so that every peer halts at the same exchange and fails
+        // alike (no rank runs on, or enters a recovery collective, alone)
+        if (bad) {
+            h.flags |= XF_ERROR;
+            h.error |= SHD_ERR_INTERNAL;
+        }
     }
     // granule 0 also into the nrep - 1 replicas (the pollers of the peer's
     // blocks spread over them: fewer reads of one address per round trip)
@@ -758,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
     const uint32_t tag = (uint32_t)(xtag + (uint64_t)(i - 1));
     const size_t stride = (size_t)P.xcap + 1;
     if (putter)
-        px_fold_put(P, prev, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wprev, tag,
+        px_fold_put(P, prev, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, bad, peers, world, me, wprev, tag,
                     xhoff, nrep);
     if (blockIdx.x >= nblk) return;   // a put block past the engine's hosts (grid = max(nblk, world))
     uint64_t ws;
@@ -864,7 +872,7 @@ __global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __r
         tl_issue(pp, nblk, 0, pv);
         const uint64_t npend = sum->n_pending, nrem = sum->n_remote, pnext = sum->next_time;
         const uint32_t perr = sum->error;
-        px_fold_put(P, sum, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, peers, world, me, wi, tag, xhoff,
+        px_fold_put(P, sum, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, bad, peers, world, me, wi, tag, xhoff,
                     nrep);
         return;
     }

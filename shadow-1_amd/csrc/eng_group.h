@@ -909,10 +909,20 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             // spills in two consecutive batches: the blocks are too small for
             // this traffic, not just for a burst.  Every rank sees the same
             // flags in the same batch, so all grow alike.
-            if (g->last_spill_batch != ~0ull && g->batches - g->last_spill_batch <= 1 && g->xcap < (1u << 22)) {
-                g->xcap *= 2;
-                x_drop_graphs(g);   // the graphs point at the old blocks
-                if ((rc = x_alloc(g))) break;
+            if (g->last_spill_batch != ~0ull && g->batches - g->last_spill_batch <= 1) {
+                if (g->fused && g->xcap >= kXSlots) {
+                    // fused rounds spill from a full region (kXSlots events per
+                    // peer and destination block, whatever xcap): a hot block
+                    // outruns its regions, so the two-launch schedule takes
+                    // over, whose per-peer blocks of xcap events do not spill
+                    g->fused = false;
+                    x_drop_graphs(g);
+                    if ((rc = x_alloc(g))) break;
+                } else if (g->xcap < (1u << 22)) {
+                    g->xcap *= 2;
+                    x_drop_graphs(g);   // the graphs point at the old blocks
+                    if ((rc = x_alloc(g))) break;
+                }
             }
             g->last_spill_batch = g->batches;
         }

@@ -34,7 +34,7 @@ struct shd_xhost_hdr {
     uint32_t count;       /* arrivals at the current barrier */
     uint32_t gen;         /* barrier generation */
     uint32_t world;
-    uint32_t pad;
+    uint32_t broken;      /* set by a rank whose barrier timed out: every barrier fails */
 };
 
 struct shd_xhost {
@@ -82,9 +82,12 @@ static double mono_s(void) {
     return t.tv_sec + t.tv_nsec * 1e-9;
 }
 
-/* a generation barrier; SHD_ENODEV if the others do not arrive in time */
+/* a generation barrier; SHD_ENODEV if the others do not arrive in time.  A
+ * timeout breaks the group for good (its arrival count can no longer be
+ * trusted): the ranks waiting, and every later barrier, fail at once. */
 int shd_xhost_barrier(shd_xhost* x) {
     struct shd_xhost_hdr* h = (struct shd_xhost_hdr*)x->base;
+    if (__atomic_load_n(&h->broken, __ATOMIC_ACQUIRE)) return SHD_ENODEV;
     const uint32_t g = __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE);
     if (__atomic_add_fetch(&h->count, 1, __ATOMIC_ACQ_REL) == (uint32_t)x->world) {
         __atomic_store_n(&h->count, 0, __ATOMIC_RELAXED);
@@ -95,9 +98,11 @@ int shd_xhost_barrier(shd_xhost* x) {
     unsigned spins = 0;
     while (__atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) == g) {
         if (++spins > 1000) sched_yield();
+        if (__atomic_load_n(&h->broken, __ATOMIC_ACQUIRE)) return SHD_ENODEV;
         if ((spins & 0xFFF) == 0 && mono_s() - t0 > x->timeout_s) {
             fprintf(stderr, "libshdgpu: host transport %s: rank %d waited %.0f s at a barrier\n", x->name, x->rank,
                     x->timeout_s);
+            __atomic_store_n(&h->broken, 1u, __ATOMIC_RELEASE);
             return SHD_ENODEV;
         }
     }
