@@ -64,6 +64,21 @@ __device__ __forceinline__ bool vrel(const double* vloss, int32_t v, double* r) 
     return true;
 }
 
+#ifdef SHD_SSSP_TIMING   // measurement build (scripts/sssp_timing.py): cycles per phase per block
+__device__ unsigned long long g_sssp_tim[1024][8];
+extern "C" int shd_debug_sssp_timing(unsigned long long* out) {
+    if (hipDeviceSynchronize() != hipSuccess) return SHD_ENODEV;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sssp_tim), sizeof(g_sssp_tim)) == hipSuccess ? SHD_OK : SHD_ENODEV;
+}
+#define SST_T0(v) const unsigned long long v = clock64();
+#define SST_ADD(k, v) if (threadIdx.x % 64 == 0 && blockIdx.x < 1024) atomicAdd(&g_sssp_tim[blockIdx.x][k], clock64() - v);
+#define SST_CNT(k, n) if (blockIdx.x < 1024) atomicAdd(&g_sssp_tim[blockIdx.x][k], (unsigned long long)(n));
+#else
+#define SST_T0(v)
+#define SST_ADD(k, v)
+#define SST_CNT(k, n)
+#endif
+
 // ------------------------------------------------------------------ SSSP rows
 // Per-row working set: dist u64[V], parent i32[V] (index into the rin_* arcs),
 // upd u16[V] (iteration at which the vertex last improved = frontier stamp).
@@ -103,14 +118,18 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     const int lane = tid & 63, wv = tid >> 6, hl = lane & 31;
     const bool upper = lane >= 32;
     int it = 0;
+    SST_T0(t_bf)
     for (;;) {
         if (tid == 0) flags[(it + 1) % 3] = 0;
         const uint16_t stamp = (uint16_t)it;
+        SST_T0(t_it)
         for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
             const int32_t v = c0 + lane;
             const bool fr = v < V && upd[v] == stamp;
             uint64_t mask = __ballot(fr);
             if (!mask) continue;
+            SST_T0(t_rx)
+            if (lane == 0) { SST_CNT(5, __popcll(mask)); }
             int32_t beg = 0, end = 0;
             uint64_t dvb = 0;
             if (fr) { beg = arc_off[v]; end = arc_off[v + 1]; dvb = dist[v]; }
@@ -136,12 +155,18 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                     }
                 }
             }
+            SST_ADD(2, t_rx)
         }
+        SST_ADD(1, t_it)
+        SST_T0(t_bar)
         __syncthreads();
+        SST_ADD(3, t_bar)
         const bool more = flags[it % 3] != 0;
         it++;
         if (!more || it >= 0xFFFE) break;
     }
+    SST_ADD(0, t_bf)
+    if (tid == 0) { SST_CNT(4, it); SST_CNT(7, 1); }
 
 #if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 1   // phase ablation (scripts/apsp_phases.sh)
     __syncthreads();
