@@ -277,9 +277,6 @@ def main():
                         % ("host-memory" if args.comm == "host" else "RCCL"))
             run = lambda t: grp.run_until(t)  # noqa: E731
             wst = run(args.warmup * step)
-    if use_group and "completes the previous" in exchange and int(getattr(wst, "n_batches_persistent", 0)):
-        exchange = ("shd_xgroup/peer-to-peer (IPC-mapped receive regions, xGMI stores; a batch of rounds is one "
-                    "persistent launch per rank, each round ending in one group-wide barrier of per-block shares)")
     torch.cuda.synchronize()
     log(rank, f"warmup {time.perf_counter() - tw:.1f}s")
 
@@ -331,13 +328,11 @@ def main():
     # the dominant kernel: ticketless device rounds on one engine (k_round_tl,
     # once no first touch is logged), the engine group's k_round_x across GPUs
     # (peer-to-peer rounds after a batch's first are k_round_px, which also completes the exchange)
-    fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and (
-        "completes the previous" in exchange or "persistent launch" in exchange)
+    fused = use_group and exchange.startswith("shd_xgroup/peer-to-peer") and "completes the previous" in exchange
     n_ps = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_persistent", 0))
     n_bat = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches", 0))
     n_sp = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_sparse", 0))
-    kname = ("k_round_pg" if fused and n_ps and 2 * n_ps >= n_bat else "k_round_px" if fused else "k_round_xtl") \
-        if use_group else \
+    kname = ("k_round_px" if fused else "k_round_xtl") if use_group else \
         ("k_round" if world > 1 else (("k_round_sp" if 2 * n_sp >= n_ps else "k_round_ps")
                                        if n_ps and 2 * n_ps >= n_bat else "k_round_tl"))
     wkey = "%s-%dh" % (args.workload, H // max(world, 1))

@@ -450,10 +450,6 @@ __shared__ shd_event s_due[kDueCap * kBlock];    // the window's calendar events
 constexpr int kRxCap = 2;
 __shared__ shd_event s_rx[kRxCap * kBlock];
 __shared__ uint32_t s_rxn[kBlock];
-// persistent group rounds (k_round_pg): what the peers' events put into each
-// lane's host's inbox (count) and calendar (bitmap bits) at the round's start
-__shared__ uint32_t s_gxn[kBlock];
-__shared__ uint32_t s_gxw[kNBW][kBlock];
 __shared__ CodelEnt s_cqh[kBlock];               // CoDel FIFO head
 __shared__ TxEnt s_tqh[kBlock];                  // send FIFO head
 
@@ -697,12 +693,10 @@ __device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
                 const EvV x = ev_ld(&e);
                 st16_sys(d, x.a);
                 st16_sys((char*)d + 16, x.b);
-                c.xput |= 1u;
+                c.xput = 1;
                 return;
             }
-            // region full: spill (as a full block below); persistent group
-            // rounds (k_round_pg) flag it in the block's share
-            c.xput |= 2u;
+            // region full: spill (as a full block below)
         } else if (P.xsend) {   // exchange mode: straight into the peer's all-to-all block
             const int32_t peer = owner_of(P, e.dst);
             const uint32_t s = atomicAdd(&P.xcount[peer], 1u);
@@ -712,7 +706,7 @@ __device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
                     const EvV x = ev_ld(&e);
                     st16_sys(d, x.a);
                     st16_sys((char*)d + 16, x.b);
-                    c.xput |= 1u;
+                    c.xput = 1;
                 } else {
                     P.xsend[(size_t)peer * (P.xcap + 1) + 1 + s] = e;
                 }

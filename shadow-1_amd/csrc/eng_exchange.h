@@ -480,7 +480,7 @@ __device__ uint32_t xrgn_ingest_from(const DParams& P, shd_event* __restrict__ r
                     const size_t bi = (size_t)dl * kNB + pb;
                     const uint32_t s = atomicAdd(&P.bin_n[bi], 1u);
                     if (s < kBinCap) {
-                        ev_st_sc1(&P.bins[bi * kBinCap + s], e);   // write-through: a persistent launch reads it with sc1 loads
+                        ev_st_sc1(&P.bins[bi * kBinCap + s], e);   // write-through: the hand-off reaches other XCDs without a kernel boundary
                         atomicOr(&P.bin_bits[(size_t)dl * kNBW + (pb >> 5)], 1u << (pb & 31));
                         if (s_w) atomicOr(&s_w[pb >> 5][j], 1u << (pb & 31));
                         continue;
@@ -725,8 +725,8 @@ __device__ __forceinline__ bool px_wait(const shd_event* __restrict__ xhdr, size
 __device__ __forceinline__ void px_reset_counts(const DParams& P, int wi, uint32_t blk, uint32_t nblk) {
     const size_t n = (size_t)P.xworld * P.xnbx;
     uint32_t* c = P.xcnt + (size_t)wi * n;
-    // agent-scope stores: the counters take other XCDs' atomics, and within a
-    // persistent launch (k_round_pg) no kernel boundary writes a plain store back
+    // agent-scope stores: the counters take other XCDs' atomics (a plain store
+    // could sit in this XCD's L2 until a kernel boundary writes it back)
     for (size_t j = (size_t)blk * kBlock + threadIdx.x; j < n; j += (size_t)nblk * kBlock)
         __hip_atomic_store(&c[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -935,300 +935,4 @@ __global__ void k_min_valid(const shd_pv* __restrict__ a, size_t n, unsigned lon
         __syncthreads();
     }
     if (threadIdx.x == 0) atomicMin(out, sm[0]);
-}
-
-// ---- persistent group rounds (k_round_pg) ----
-// One launch runs a batch of up to 128 rounds of one rank of a peer-to-peer
-// group, its hosts' state in registers across the batch (as k_round_ps for one
-// engine).  A round's sends for other ranks' hosts go into their regions, as
-// in the fused schedule; its end is ONE barrier over the whole group: every
-// block stores its share of the round (next time, flags; counts) into every
-// rank's share area (16-B system-scope write-through stores, after the wave
-// drained its region and hand-off stores), and every block polls the
-// world x blocks shares in its own rank's area.  Once all carry the round's
-// tag, every rank's region stores of the round have landed: the window start
-// is the min of the shares' next times, and each block takes what the peers
-// stored for its hosts (xrgn_take) at the start of the next round.  A flagged
-// share (first touch, error, a full region) ends the batch on every rank at
-// the same round; the last round's regions are ingested into the calendars
-// before the launch ends, and, for the host's next batch, every rank's next
-// time is put into the peers' header blocks as the last exchange's headers
-// (then waited for, so that no rank's host reads them early).
-constexpr uint32_t kPsSpill = 0x20000000u;   // share flag: a region of this block's sends was full
-constexpr uint64_t kAuxSys = 17;             // buffer op cache policy: sc0 sc1 (system scope)
-
-__device__ __forceinline__ uint4 ld16_sysb(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, (int)kAuxSys);
-    return make_uint4(x[0], x[1], x[2], x[3]);
-}
-
-// blocks of rank r (contiguous host ranges: owner_of's split)
-__device__ __forceinline__ uint32_t pg_nblk(const DParams& P, int r) {
-    const uint64_t a = ((uint64_t)P.H * (uint64_t)r) / (uint64_t)P.xworld;
-    const uint64_t b = ((uint64_t)P.H * (uint64_t)(r + 1)) / (uint64_t)P.xworld;
-    return (uint32_t)((b - a + (uint64_t)P.hpw - 1) / (uint64_t)P.hpw);
-}
-
-// this block's share of a round into every rank's area (lane p: rank p)
-__device__ __forceinline__ void pg_publish(shd_event* const* __restrict__ peers, uint64_t shoff, int world, int me,
-                                           uint32_t xnbx, uint32_t par, uint32_t blk, uint64_t next, uint32_t flags,
-                                           uint32_t nev, uint32_t npkt, uint32_t nact, uint32_t tag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's region and hand-off stores have landed
-    if ((int)threadIdx.x < world) {
-        shd_event* d = peers[threadIdx.x] + shoff + ((size_t)(par * (uint32_t)world + (uint32_t)me) * xnbx + blk);
-        st16_sys((uint4*)d + 1, make_uint4(nev, npkt, nact, tag));
-        st16_sys(d, make_uint4((uint32_t)next, (uint32_t)(next >> 32), flags, tag));
-    }
-}
-
-// every rank's shares of a round (area of parity par: [world][xnbx]), polled
-// until all carry `tag`: the min next time and the flags over the group, the
-// counts over this rank's blocks.  False on timeout.  Wave-uniform results.
-__device__ __forceinline__ bool pg_gather(__amdgpu_buffer_rsrc_t rs, const DParams& P, uint32_t par, int world, int me,
-                          uint32_t xnbx, uint32_t tag, uint64_t ticks, uint64_t& next, uint32_t& flags,
-                          uint32_t& nev, uint32_t& npkt, uint32_t& nact) {
-    next = kInf; flags = 0; nev = 0; npkt = 0; nact = 0;
-    const uint32_t total = (uint32_t)world * xnbx;
-    const uint32_t base = par * total;
-    const unsigned long long t0 = wall_clock64();
-    for (uint32_t c0 = 0; c0 < total; c0 += 256) {
-        uint32_t need = 0, mine = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t idx = c0 + 64u * k + threadIdx.x;
-            if (idx >= total) continue;
-            const uint32_t r = idx / xnbx, b = idx - r * xnbx;
-            if (b < pg_nblk(P, (int)r)) {
-                need |= 1u << k;
-                if ((int)r == me) mine |= 1u << k;
-            }
-        }
-        while (__ballot(need != 0)) {
-            uint4 a[4], bb[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t off = (base + c0 + 64u * k + threadIdx.x) * 32u;
-                a[k] = make_uint4(0, 0, 0, 0);
-                bb[k] = a[k];
-                if ((need >> k) & 1u) {
-                    a[k] = ld16_sysb(rs, off);
-                    bb[k] = ld16_sysb(rs, off + 16u);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (!((need >> k) & 1u) || a[k].w != tag || bb[k].w != tag) continue;
-                const uint64_t t = ((uint64_t)a[k].y << 32) | a[k].x;
-                next = t < next ? t : next;
-                flags |= a[k].z;
-                if ((mine >> k) & 1u) { nev += bb[k].x; npkt += bb[k].y; nact += bb[k].z; }
-                need &= ~(1u << k);
-            }
-            if (__ballot(need != 0) == 0) break;
-            if (wall_clock64() - t0 > ticks) return false;
-        }
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(next, off, 64);
-        next = o < next ? o : next;
-        flags |= __shfl_xor(flags, off, 64);
-        nev += __shfl_xor(nev, off, 64);
-        npkt += __shfl_xor(npkt, off, 64);
-        nact += __shfl_xor(nact, off, 64);
-    }
-    return true;
-}
-
-__global__ __launch_bounds__(kBlock) void k_round_pg(uint64_t window, int nb, DevSummary* __restrict__ ring,
-                                                      const DevCtl* __restrict__ ctl, const DParams* __restrict__ Pr,
-                                                      uint64_t ticks, shd_event* const* __restrict__ peers,
-                                                      shd_event* __restrict__ own, uint64_t shoff, uint64_t rgnoff,
-                                                      XHeader* __restrict__ halt_hdr, uint32_t* __restrict__ xerr,
-                                                      int world, int me) {
-    __shared__ shd_event s_def[kXDefCap * kBlock];
-    const DParams& P0 = Pr[1];
-    const uint32_t nblk = (uint32_t)((P0.nloc + P0.hpw - 1) / P0.hpw);
-    const uint32_t xnbx = P0.xnbx;
-    const size_t stride = (size_t)P0.xcap + 1;
-    const int32_t l = lane_host(P0);
-    const bool has = l < P0.nloc;
-    const uint32_t lb = threadIdx.x;
-    const uint32_t hb = blockIdx.x * (uint32_t)P0.hpw;
-    PsRsrc R0, R1;
-    {
-        const uint32_t hpw = (uint32_t)P0.hpw;
-        R0.bits = buf_rsrc(P0.bin_bits ? P0.bin_bits + (size_t)hb * kNBW : nullptr, (uint64_t)hpw * kNBW * 4);
-        R0.bins = buf_rsrc(P0.bins ? P0.bins + (size_t)hb * kNB * kBinCap : nullptr,
-                           (uint64_t)hpw * kNB * kBinCap * sizeof(shd_event));
-        R1.bits = R0.bits;
-        R1.bins = R0.bins;
-        R0.nin = buf_rsrc(P0.inbox_n[0] + hb, (uint64_t)hpw * 4);
-        R1.nin = buf_rsrc(P0.inbox_n[1] + hb, (uint64_t)hpw * 4);
-        R0.inbox = buf_rsrc(P0.inbox[0] + (size_t)hb * P0.inbox_cap, (uint64_t)hpw * P0.inbox_cap * sizeof(shd_event));
-        R1.inbox = buf_rsrc(P0.inbox[1] + (size_t)hb * P0.inbox_cap, (uint64_t)hpw * P0.inbox_cap * sizeof(shd_event));
-    }
-    const __amdgpu_buffer_rsrc_t rsh = buf_rsrc(own + shoff, (uint64_t)2 * (uint64_t)world * xnbx * sizeof(shd_event));
-    HostCtx c;
-    hot_load(P0, c);
-    if (has) {
-        load_ctx(P0, c, l, P0.hs[l], P0.host_att[P0.h0 + l], P0.self_thr[P0.h0 + l]);
-    } else {
-        c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf;
-        c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
-    }
-    uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-    uint64_t ws = ring[0].next_time, ws_prev = ws;
-    const uint64_t stop = ctl->stop, rbase = ctl->round_base, xpar = ctl->xpar;
-    const uint32_t tag0 = (uint32_t)ctl->xtag;
-    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-    int last = -1;          // the last round that ran (its exchange is ingested at the end)
-    uint64_t ws_last = ws;
-    bool flagged = false, failed = false;
-    for (int i = 0; i < nb; i++) {
-        const DParams& P = Pr[i + 1];
-        const unsigned long long t_start = wall_clock64();
-        if (lead) ps_fresh(&ring[i + 2]);
-        const int parity = (int)((rbase + (uint64_t)i) & 1);
-        const int wx = (int)((xpar + (uint64_t)i) & 1);   // this round's region parity
-        uint64_t we = ws + window;
-        if (we > stop || we < ws) we = stop;
-        PsRsrc R = R0;
-        R.nin = parity ? R1.nin : R0.nin;
-        R.inbox = parity ? R1.inbox : R0.inbox;
-        // what the peers stored for this block's hosts in round i - 1
-        s_gxn[lb] = 0;
-        s_rxn[lb] = 0;
-#pragma unroll
-        for (int k = 0; k < (int)kNBW; k++) s_gxw[k][lb] = 0;
-        __syncthreads();
-        uint32_t sl[8], dm = 0, ierr = 0;
-        if (i > 0) {
-            shd_event* rgn = own + rgnoff + (size_t)(wx ^ 1) * (size_t)world * xnbx * kXSlots;
-            ierr = xrgn_take(P, rgn, blockIdx.x, ws, we, parity, s_gxn, s_gxw, s_def, sl, dm);
-            if (world > 8) ierr |= xrgn_ingest_from(P, rgn, blockIdx.x, ws_prev, parity, s_gxn, s_gxw, 8);
-            px_reset_counts(P, wx ^ 1, blockIdx.x, nblk);   // round i - 1's sends are all in (its barrier)
-        }
-        // the take's inbox and calendar stores landed before the owner lanes read them back
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        uint64_t next;
-        ps_round<true>(P, c, has, lb, R, ws, we, parity, next, wx);
-        if (dm) ierr |= xrgn_store(P, s_def, sl, dm, parity ^ 1);
-        acc[0] += c.c_events; acc[1] += c.c_pkt; acc[2] += c.c_sent;
-        acc[3] += c.c_idrop; acc[4] += c.c_cdrop; acc[5] += c.c_recv;
-        uint32_t nev = c.c_events, npkt = c.c_pkt;
-        const uint32_t pend = c.n_pend ? kPsPend : 0u;
-        const uint32_t spill = (c.xput & 2u) ? kPsSpill : 0u;
-        const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));
-        uint32_t fl = c.err | ierr | pend | spill;
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t o = __shfl_xor(next, off, 64);
-            next = o < next ? o : next;
-            nev += __shfl_xor(nev, off, 64);
-            npkt += __shfl_xor(npkt, off, 64);
-            fl |= __shfl_xor(fl, off, 64);
-        }
-        const uint32_t tag = tag0 + (uint32_t)i;
-        pg_publish(peers, shoff, world, me, xnbx, (uint32_t)(i & 1), blockIdx.x, next, fl, nev, npkt, nact, tag);
-        uint64_t f_next;
-        uint32_t f_fl, f_nev, f_npkt, f_nact;
-        const bool ok_v = pg_gather(rsh, P, (uint32_t)(i & 1), world, me, xnbx, tag, ticks, f_next, f_fl, f_nev,
-                                    f_npkt, f_nact);
-        const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;
-        f_fl = __builtin_amdgcn_readfirstlane(f_fl);
-        f_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(f_next >> 32)) << 32) |
-                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)f_next);
-        if (!ok) {   // a block (of some rank) never came
-            if (threadIdx.x == 0) {
-                atomicOr(&ring[i + 1].error, SHD_ERR_INTERNAL);
-                atomicOr(xerr, 1u);
-                *P.halt = 1u;
-            }
-            failed = true;
-            break;
-        }
-        if (lead) {   // round i's summary (this rank's counts; the group's next time)
-            DevSummary* s = &ring[i + 1];
-            atomicMin(&s->next_time, f_next);
-            if (f_nev) atomicAdd(&s->n_events, (unsigned long long)f_nev);
-            if (f_npkt) atomicAdd(&s->n_pkt_events, (unsigned long long)f_npkt);
-            if (f_nact) atomicAdd(&s->n_active, f_nact);
-            const uint32_t e = f_fl & ~(kPsPend | kPsSpill);
-            if (e) atomicOr(&s->error, e);
-            atomicMin(&s->t_first, t_start);
-            atomicMax(&s->t_last, (unsigned long long)wall_clock64());
-            __hip_atomic_store(&s->ws, (unsigned long long)ws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        last = i;
-        ws_last = ws;
-        if (f_fl) { flagged = true; break; }
-        ws_prev = ws;
-        ws = f_next;
-        if (ws >= stop) break;
-    }
-    last = __builtin_amdgcn_readfirstlane(last);
-    if (last >= 0 && !failed) {
-        const DParams& P = P0;
-        const int wx = (int)((xpar + (uint64_t)last) & 1);
-        const int par_next = (int)((rbase + (uint64_t)last + 1) & 1);
-        // the last round's exchange: this block's regions into calendars / the next round's inbox
-        shd_event* rgn = own + rgnoff + (size_t)wx * (size_t)world * xnbx * kXSlots;
-        const uint32_t err = xrgn_ingest(P, rgn, blockIdx.x, ws_last, par_next, nullptr, nullptr);
-        if (err) atomicOr(&ring[last + 1].error, err);
-        px_reset_counts(P, wx, blockIdx.x, nblk);
-        if (flagged) {   // the next round halted: the host recovers the flagged one (ring[last + 1])
-            if (lead) ring[last + 2].flags = 1u;
-            if (blockIdx.x == 0) {
-                const uint32_t par = (uint32_t)(last & 1);
-                for (int r = 0; r < world; r++) {   // per rank: its blocks' flags as header flags
-                    uint32_t f = 0;
-                    for (uint32_t b = threadIdx.x; b < pg_nblk(P, r); b += kBlock)
-                        f |= ld16_sysb(rsh, ((par * (uint32_t)world + (uint32_t)r) * xnbx + b) * 32u).z;
-                    for (int off = 32; off > 0; off >>= 1) f |= __shfl_xor(f, off, 64);
-                    if (threadIdx.x == 0) {
-                        XHeader h{};
-                        h.next_time = kInf;
-                        const uint32_t e = f & ~(kPsPend | kPsSpill);
-                        h.flags = ((f & kPsPend) ? XF_PENDING : 0u) | ((f & kPsSpill) ? XF_OVERFLOW : 0u) |
-                                  (e ? XF_ERROR : 0u);
-                        h.error = e;
-                        halt_hdr[r] = h;
-                    }
-                }
-                if (threadIdx.x == 0) *P.halt = 1u;
-            }
-        } else {
-            if (ws >= stop && lead) {   // the next round only forwards the time
-                __hip_atomic_store(&ring[last + 2].ws, (unsigned long long)ws, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&ring[last + 2].next_time, (unsigned long long)ws, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            // the last exchange's headers, as the fused schedule leaves them: this
-            // rank's (= the group's) next time in every peer's header block of the
-            // batch's last parity; then every peer's, waited for
-            const int wl = (int)((xpar + (uint64_t)nb - 1) & 1);
-            const uint32_t htag = tag0 + (uint32_t)nb + 0x40000000u;
-            if (blockIdx.x == 0 && (int)threadIdx.x < world) {
-                shd_event* d = peers[threadIdx.x] + ((size_t)wl * world + me) * stride;
-                st16_sys((uint4*)d + 1, make_uint4(0, 0, 0, 0));
-                st16_sys(d, make_uint4((uint32_t)ws, (uint32_t)(ws >> 32), 0u, htag));
-            }
-            if (blockIdx.x == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                uint64_t t;
-                uint32_t fl2;
-                const shd_event* xhdr = own + (size_t)wl * world * stride;
-                if (px_wait(xhdr, stride, world, htag, 0u, xerr, t, fl2, xhdr, 1, 0)) {
-                    if (threadIdx.x == 0) *P.halt = 1u;
-                }
-            }
-        }
-    }
-    if (has) {
-        c.c_events = acc[0]; c.c_pkt = acc[1]; c.c_sent = acc[2];
-        c.c_idrop = acc[3]; c.c_cdrop = acc[4]; c.c_recv = acc[5];
-        store_ctx(P0, c);
-    }
 }

@@ -60,7 +60,6 @@ struct shd_xgroup {
     uint32_t* d_xerr = nullptr;        // set by a wait that timed out
     uint64_t xepoch = 0;               // exchange tags issued (never rolled back)
     bool fused = false;                // peer-to-peer rounds fused with their exchange (k_round_px)
-    bool pg = false;                   // fused batches as ONE persistent launch (k_round_pg)
     uint32_t xnbx = 0;                 // fused: region blocks per rank
     // one engine per process: the last exchange's headers and the wait-error word,
     // copied back with the batch's summaries (one stream synchronisation per batch)
@@ -88,8 +87,6 @@ static uint64_t x_hoff(const shd_xgroup* g) {
 static const shd_event* x_rep(const shd_xgroup* g, int w) {
     return g->p2p_base + x_hoff(g) + (size_t)w * (kXReplMax - 1) * g->world;
 }
-// persistent group rounds' shares (k_round_pg): [2][world][xnbx] 32-B slots after the replicas
-static uint64_t x_shoff(const shd_xgroup* g) { return x_hoff(g) + 2 * (uint64_t)(kXReplMax - 1) * g->world; }
 
 static bool x_want_protect(const shd_xgroup* g) {
     if (protect_off()) return false;
@@ -351,9 +348,7 @@ static int x_p2p_map(shd_xgroup* g) {
     };
     Share mine{};
     const size_t bytes = (2 * (size_t)W * g->stride +
-                          (g->fused ? 2 * (size_t)W * g->xnbx * kXSlots + 2 * (size_t)(kXReplMax - 1) * W +
-                                          2 * (size_t)W * g->xnbx
-                                    : 0)) *
+                          (g->fused ? 2 * (size_t)W * g->xnbx * kXSlots + 2 * (size_t)(kXReplMax - 1) * W : 0)) *
                          sizeof(shd_event);
     if (hipExtMallocWithFlags((void**)&g->p2p_base, bytes, hipDeviceMallocUncached) == hipSuccess &&
         hipMemset(g->p2p_base, 0, bytes) == hipSuccess &&   // tag 0: no exchange yet (tags start at 1)
@@ -560,20 +555,6 @@ static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p,
     // the GPU's compute units one each (three ranks of 157 blocks on one GPU
     // waited out their 30 s: the device did not run the three launches at once)
     g->fused = p2p && x_fuse_env() && (sharers <= 1 || shared_blocks <= (unsigned long long)ncu);
-    {   // persistent batches: every block of this rank resident at once (its own
-        // blocks wait for each other every round, as in k_round_ps)
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_round_pg), kBlock,
-                                                         0) != hipSuccess)
-            per_cu = 0;
-        (void)hipGetLastError();
-        // opt-in (SHD_X_PG=1) until it is bit-exact on every group test: the
-        // 3-process Tor-scale model still loses 25 of 22963 packet events with it
-        // (DESIGN.md section 8); the launch-per-round fused schedule is the default
-        static const bool want_pg = getenv("SHD_X_PG") != nullptr;
-        g->pg = g->fused && want_pg && per_cu >= 1 && nblk <= (unsigned long long)ncu * (unsigned long long)per_cu &&
-                nblk <= (unsigned long long)2 * ncu;
-    }
     g->end_time = e->P.end_time;
     g->xcap = block_events ? block_events : x_default_cap(e, world);
     g->fixed_cap = block_events != 0;
@@ -774,22 +755,12 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             if (rc) break;
             s.n_rounds_protected++;
         }
-        // a persistent batch (k_round_pg): unprotected rounds of a fused group,
-        // one engine per process; it starts from the group's next time
-        const bool pgb = g->pg && !prot && nl == 1;
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
-            if (pgb) {
-                e->h_seed[0] = host_fresh_summary();
-                e->h_seed[0].next_time = g->next;
-                SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &e->h_seed[0], sizeof(DevSummary), hipMemcpyHostToDevice,
-                                       e->stream));
-            } else {
-                // slot 0 keeps the previous batch's last round: a flag in its
-                // headers halts this batch's first round, and the recovery needs it
-                SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &e->d_ring[g->last_nb], sizeof(DevSummary),
-                                       hipMemcpyDeviceToDevice, e->stream));
-            }
+            // slot 0 keeps the previous batch's last round: a flag in its
+            // headers halts this batch's first round, and the recovery needs it
+            SHD_HIP(hipMemcpyAsync(&e->d_ring[0], &e->d_ring[g->last_nb], sizeof(DevSummary), hipMemcpyDeviceToDevice,
+                                   e->stream));
             e->h_seed[1] = host_fresh_summary();
             e->h_ctl->stop = stop;
             e->h_ctl->round_base = e->round;
@@ -801,28 +772,14 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         }
         SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
-        if (pgb) {
-            shd_eng* e = g->engs[0];
-            const uint32_t nblk = (uint32_t)((e->nloc + e->P.hpw - 1) / e->P.hpw);
-            const uint64_t ticks = (uint64_t)(30.0 * e->wall_khz * 1000.0);   // 30 s: a peer that never comes
-            hipLaunchKernelGGL(k_round_pg, dim3(nblk), dim3(kBlock), 0, e->stream, g->window, nb, e->d_ring,
-                               (const DevCtl*)e->d_ctl, (const DParams*)g->loc[0].d_xpr, ticks,
-                               (shd_event* const*)g->d_peers, g->p2p_base, x_shoff(g),
-                               (uint64_t)2 * (uint64_t)g->world * g->stride, g->loc[0].halt_hdr, g->d_xerr, g->world,
-                               g->rank0);
-            g->xseq += (uint64_t)nb;   // one region parity (and exchange number) per round
-            s.n_batches_persistent++;
-        } else if ((rc = x_launch_rounds(g, nb))) {
-            break;
-        }
+        if ((rc = x_launch_rounds(g, nb))) break;
         s.n_batches++;
         g->xepoch += (uint64_t)nb;
         SHD_HIP(hipGetLastError());
         SHD_HIP(hipEventRecord(g->engs[0]->bev[1], g->engs[0]->stream));
         for (int k = 0; k < nl; k++) {
             shd_eng* e = g->engs[k];
-            // (a persistent batch's last round can mark ring[B + 1]: the round after it halted)
-            SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 2), hipMemcpyDeviceToHost,
+            SHD_HIP(hipMemcpyAsync(e->h_ring, e->d_ring, sizeof(DevSummary) * (B + 1), hipMemcpyDeviceToHost,
                                    e->stream));
         }
         // one engine per process: the last exchange's headers and the wait-error word
@@ -880,10 +837,9 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
         }
         int halted_at = -1;
         bool done = false;
-        for (int i = 0; i < nb + (pgb ? 1 : 0); i++) {
+        for (int i = 0; i < nb; i++) {
             const DevSummary& r0 = g->engs[0]->h_ring[i + 1];
             if (r0.flags == 1u) { halted_at = i; break; }
-            if (i == nb) break;   // (persistent: only a halt mark past the batch's rounds)
             if (r0.flags != 0u) break;   // skipped: cannot precede a halt
             if (r0.ws >= stop) {
                 g->next = r0.ws;
@@ -963,7 +919,6 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
                     // xcap events do not spill
                     if (nb > 1) {
                         g->fused = false;
-                        g->pg = false;
                         x_drop_graphs(g);
                         if ((rc = x_alloc(g))) break;
                     }

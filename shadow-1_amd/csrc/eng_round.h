@@ -963,7 +963,7 @@ struct PsRsrc {
 // the rare overflow of the due list, as due_overflow, reading the bins again
 // with sc1 loads (they may hold other blocks' appends of this launch)
 __device__ void ps_due_overflow(const DParams& P, HostCtx& c, const PsRsrc& R, uint32_t lb, uint64_t b0,
-                                uint32_t wbits, uint64_t ws, uint64_t we, uint32_t nrx = 0) {
+                                uint32_t wbits, uint64_t ws, uint64_t we) {
     uint32_t k = 0;
     for (uint32_t j = 0; j < 3; j++) {
         if (((wbits >> j) & 1u) == 0) continue;
@@ -976,12 +976,6 @@ __device__ void ps_due_overflow(const DParams& P, HostCtx& c, const PsRsrc& R, u
             if (k >= (uint32_t)kDueCap) heap_push(P, c, evv_event(x));
             k++;
         }
-    }
-    for (uint32_t r = 0; r < nrx; r++) {   // then the received ones (k_round_pg), in due_add's order
-        const shd_event& x = s_rx[r * kBlock + threadIdx.x];
-        if (x.time < ws || x.time >= we) continue;
-        if (k >= (uint32_t)kDueCap) heap_push(P, c, x);
-        k++;
     }
 }
 
@@ -1008,7 +1002,7 @@ struct SpIn {
     int4 st;
     int32_t l;
 };
-template <bool SP, bool RX = false>
+template <bool SP>
 __device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool active, uint32_t lb, const PsRsrc& R,
                                               uint64_t ws, uint64_t we, int parity, uint32_t nin,
                                               uint32_t (&w)[kNBW], uint32_t wbits, uint64_t& next,
@@ -1050,14 +1044,8 @@ __device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool
 #pragma unroll
                 for (uint32_t k = 0; k < kBinCap; k++) due_add(bx[j][k], nw, ws, we);
             }
-            uint32_t nrx = 0;
-            if (RX) {   // the window's events the peers stored in this block's regions (k_round_pg)
-                nrx = s_rxn[threadIdx.x];
-                nrx = nrx < (uint32_t)kRxCap ? nrx : (uint32_t)kRxCap;
-                for (uint32_t r = 0; r < nrx; r++) due_add(ev_ld(s_rx + r * kBlock + threadIdx.x), nw, ws, we);
-            }
             c.nd = nw < (uint32_t)kDueCap ? nw : (uint32_t)kDueCap;
-            if (nw > (uint32_t)kDueCap) ps_due_overflow(P, c, R, lb, b0, wbits, ws, we, nrx);
+            if (nw > (uint32_t)kDueCap) ps_due_overflow(P, c, R, lb, b0, wbits, ws, we);
             for (uint32_t i = 1; i < c.nd; i++) {   // insertion sort of the due list (LDS)
                 const EvV x = ev_ld(s_due + i * kBlock + threadIdx.x);
                 uint32_t k = i;
@@ -1181,11 +1169,9 @@ __device__ __forceinline__ uint64_t ps_idle_next(const DParams& P, const uint32_
 
 // One round [ws, we) of the lane's host (has: the lane has one; lb: its index
 // in the block) on the context it keeps in registers; as round_body
-template <bool RX = false>
-__device__ __forceinline__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, const PsRsrc& R, uint64_t ws,
-                         uint64_t we, int parity, uint64_t& next_out, int xwi = 0) {
+__device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, const PsRsrc& R, uint64_t ws,
+                         uint64_t we, int parity, uint64_t& next_out) {
     ps_round_reset(c, ws, parity);
-    c.xwi = xwi;
     // the round's hand-off words: this parity's inbox count, the calendar bitmap
     uint32_t nin = 0;
     uint32_t w[kNBW];
@@ -1197,12 +1183,6 @@ __device__ __forceinline__ void ps_round(const DParams& P, HostCtx& c, bool has,
             const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
             w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
         }
-        if (RX) {   // the bins the peers' deferred events claimed for this host (k_round_pg;
-            // their inbox events are in the count read above: it is read after
-            // the regions were taken)
-#pragma unroll
-            for (int k = 0; k < (int)kNBW; k++) w[k] |= s_gxw[k][lb];
-        }
     }
     const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
     uint64_t next = kInf;
@@ -1210,10 +1190,10 @@ __device__ __forceinline__ void ps_round(const DParams& P, HostCtx& c, bool has,
     bool active = false;
     TIM(1);
     if (has) {
-        if (nin == 0 && t0 >= we && wbits == 0 && (!RX || s_rxn[lb] == 0)) next = ps_idle_next(P, w, t0, we);
+        if (nin == 0 && t0 >= we && wbits == 0) next = ps_idle_next(P, w, t0, we);
         else active = true;
     }
-    ps_round_body<false, RX>(P, c, active, lb, R, ws, we, parity, nin, w, wbits, next);
+    ps_round_body<false>(P, c, active, lb, R, ws, we, parity, nin, w, wbits, next);
     next_out = next;
 }
 
@@ -1337,7 +1317,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         PsRsrc R = R0;
         R.nin = parity ? R1.nin : R0.nin;
         R.inbox = parity ? R1.inbox : R0.inbox;
-        ps_round<false>(P, c, has, lb, R, ws, we, parity, next);
+        ps_round(P, c, has, lb, R, ws, we, parity, next);
         acc[0] += c.c_events; acc[1] += c.c_pkt; acc[2] += c.c_sent;
         acc[3] += c.c_idrop; acc[4] += c.c_cdrop; acc[5] += c.c_recv;
         uint32_t nev = c.c_events, npkt = c.c_pkt, err = c.err;
