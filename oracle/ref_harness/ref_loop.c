@@ -50,6 +50,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <errno.h>
+#include <fcntl.h>
 #include <sys/epoll.h>
 
 #include "main/core/logger/shadow_logger.h"
@@ -61,6 +63,7 @@
 #include "main/core/work/task.h"
 #include "main/core/worker.h"
 #include "main/host/descriptor/descriptor.h"
+#include "main/host/descriptor/socket.h"
 #include "main/host/host.h"
 #include "main/host/process.h"
 #include "main/routing/address.h"
@@ -92,6 +95,10 @@ typedef struct ref_loop_cfg {
     ref_path_fn path;
     void* path_ctx;
     const char* root_dir;         /* host data directories (host_setup mkdirs them) */
+    /* app 1 (TCP echo): proc_peer[k] = -1 for a server, else the server process
+     * the client k connects to; each client sends tcp_bytes, the server echoes */
+    const int32_t* proc_peer;
+    uint32_t tcp_bytes, _pad3;
 } ref_loop_cfg;
 
 typedef struct ref_loop_out {
@@ -234,7 +241,12 @@ struct _Process {
     gboolean running;
     gint epollfd;     /* the descriptor whose readiness continues the process */
     gint listenfd;
+    /* app 1 (TCP echo) */
+    gint index, step, fd, wait_fd;
+    guint32 done;
+    gchar* buf;
 };
+static Process** g_procs;
 
 Process* process_new(gpointer host, guint processID, SimulationTime startTime, SimulationTime stopTime,
                      const gchar* pluginName, const gchar* pluginPath, const gchar* pluginSymbol,
@@ -246,11 +258,20 @@ Process* process_new(gpointer host, guint processID, SimulationTime startTime, S
     p->refcount = 1;
     p->epollfd = -1;
     p->listenfd = -1;
+    p->fd = -1;
+    p->wait_fd = -1;
+    p->index = arguments ? atoi(arguments) : -1;
+    if (g_cfg->app == 1 && g_procs && p->index >= 0 && p->index < g_cfg->n_procs) g_procs[p->index] = p;
     return p;
 }
 void process_ref(Process* proc) { proc->refcount++; }
 void process_unref(Process* proc) {
-    if (--proc->refcount == 0) g_free(proc);
+    if (--proc->refcount == 0) {
+        if (g_procs && proc->index >= 0 && proc->index < g_cfg->n_procs && g_procs[proc->index] == proc)
+            g_procs[proc->index] = NULL;
+        g_free(proc->buf);
+        g_free(proc);
+    }
 }
 gboolean process_isRunning(Process* proc) { return proc->running; }
 gboolean process_wantsNotify(Process* proc, gint epollfd) {
@@ -335,6 +356,159 @@ static void phold_continue(Process* proc) {
     }
 }
 
+
+/* ---- app 1: src/test/tcp/test_tcp.c's echo test in its nonblocking-epoll
+ * mode (_run_server / _run_client, test_tcp.c:713-810), restated over the
+ * host_* calls the syscall handlers make.  The client fills its buffer with
+ * rand() (_fillcharbuf, test_tcp.c:103-108: process_emu_rand draws the host
+ * RNG, process.c:4772-4777), connects, sends tcp_bytes, reads them back and
+ * closes; the server binds port 0 (a random port, host.c:1165-1170), listens,
+ * accepts one peer, reads tcp_bytes, echoes them and closes both sockets.
+ * The port reaches the client as the test's message queue hands it over
+ * (test_tcp.c:268-273, 204-205).  A wait (_wait_epoll, test_tcp.c:132-174)
+ * watches the descriptor for EPOLLIN / EPOLLOUT on the process's epoll and
+ * removes the watch when the process continues. */
+enum { T_SRV_START, T_SRV_ACCEPT, T_SRV_RECV, T_SRV_SEND, T_CLI_START, T_CLI_CONNECT, T_CLI_SEND,
+       T_CLI_RECV, T_DONE };
+
+static void tcp_wait(Process* proc, gint fd, uint32_t events) {
+    Host* host = proc->host;
+    struct epoll_event ev;
+    memset(&ev, 0, sizeof(ev));
+    ev.events = events;
+    ev.data.fd = fd;
+    proc->wait_fd = fd;
+    (void)host_epollControl(host, proc->epollfd, EPOLL_CTL_ADD, fd, &ev);
+}
+
+static int tcp_server_port(int32_t spi, in_addr_t* ip, in_port_t* port) {
+    Process* s = (spi >= 0 && spi < g_cfg->n_procs) ? g_procs[spi] : NULL;
+    if (!s || s->listenfd < 0) return -1;
+    Descriptor* d = host_lookupDescriptor(s->host, s->listenfd);
+    if (!d) return -1;
+    in_addr_t bip = 0;
+    socket_getSocketName((Socket*)d, &bip, port);
+    *ip = host_getDefaultIP(s->host);
+    return 0;
+}
+
+static void tcp_run(Process* proc) {
+    Host* host = proc->host;
+    const uint32_t N = g_cfg->tcp_bytes;
+    for (;;) {
+        switch (proc->step) {
+        case T_SRV_START: {
+            proc->listenfd = host_createDescriptor(host, DT_TCPSOCKET);
+            Descriptor* d = host_lookupDescriptor(host, proc->listenfd);
+            descriptor_setFlags(d, descriptor_getFlags(d) | O_NONBLOCK);
+            struct sockaddr_in a;
+            memset(&a, 0, sizeof(a));
+            a.sin_family = AF_INET;
+            a.sin_addr.s_addr = htonl(INADDR_ANY);
+            a.sin_port = 0;
+            (void)host_bindToInterface(host, proc->listenfd, (struct sockaddr*)&a);
+            (void)host_listenForPeer(host, proc->listenfd, 100);
+            proc->step = T_SRV_ACCEPT;
+            break;
+        }
+        case T_SRV_ACCEPT: {
+            in_addr_t ip = 0;
+            in_port_t port = 0;
+            gint child = -1;
+            gint rc = host_acceptNewPeer(host, proc->listenfd, &ip, &port, &child);
+            if (rc == EWOULDBLOCK || rc == EAGAIN) { tcp_wait(proc, proc->listenfd, EPOLLIN); return; }
+            if (rc != 0) { proc->step = T_DONE; return; }
+            proc->fd = child;
+            proc->done = 0;
+            proc->step = T_SRV_RECV;
+            break;
+        }
+        case T_SRV_RECV:
+        case T_CLI_RECV: {
+            while (proc->done < N) {
+                in_addr_t ip = 0;
+                in_port_t port = 0;
+                gsize n = 0;
+                gint rc = host_receiveUserData(host, proc->fd, proc->buf + proc->done, N - proc->done, &ip, &port, &n);
+                if (rc == EWOULDBLOCK || rc == EAGAIN) { tcp_wait(proc, proc->fd, EPOLLIN); return; }
+                if (rc != 0 || n == 0) break;   /* error or EOF */
+                proc->done += (guint32)n;
+            }
+            if (proc->step == T_SRV_RECV) {
+                proc->done = 0;
+                proc->step = T_SRV_SEND;
+            } else {
+                (void)host_closeUser(host, proc->fd);
+                proc->step = T_DONE;
+            }
+            break;
+        }
+        case T_SRV_SEND:
+        case T_CLI_SEND: {
+            while (proc->done < N) {
+                gsize n = 0;
+                gint rc = host_sendUserData(host, proc->fd, proc->buf + proc->done, N - proc->done, 0, 0, &n);
+                if (rc == EWOULDBLOCK || rc == EAGAIN) { tcp_wait(proc, proc->fd, EPOLLOUT); return; }
+                if (rc != 0 || n == 0) break;
+                proc->done += (guint32)n;
+            }
+            if (proc->step == T_SRV_SEND) {
+                (void)host_closeUser(host, proc->fd);
+                (void)host_closeUser(host, proc->listenfd);
+                proc->step = T_DONE;
+            } else {
+                proc->done = 0;
+                proc->step = T_CLI_RECV;
+            }
+            break;
+        }
+        case T_CLI_START: {
+            for (uint32_t i = 0; i < N; i++)
+                proc->buf[i] = (gchar)('a' + random_rand(host_getRandom(host)) % 26);
+            proc->fd = host_createDescriptor(host, DT_TCPSOCKET);
+            Descriptor* d = host_lookupDescriptor(host, proc->fd);
+            descriptor_setFlags(d, descriptor_getFlags(d) | O_NONBLOCK);
+            proc->step = T_CLI_CONNECT;
+            break;
+        }
+        case T_CLI_CONNECT: {
+            struct sockaddr_in a;
+            memset(&a, 0, sizeof(a));
+            a.sin_family = AF_INET;
+            if (tcp_server_port(g_cfg->proc_peer[proc->index], &a.sin_addr.s_addr, &a.sin_port) != 0) {
+                proc->step = T_DONE;
+                return;
+            }
+            gint rc = host_connectToPeer(host, proc->fd, (struct sockaddr*)&a);
+            if (rc == EINPROGRESS || rc == EALREADY) { tcp_wait(proc, proc->fd, EPOLLOUT); return; }
+            if (rc != 0 && rc != EISCONN) { proc->step = T_DONE; return; }
+            proc->done = 0;
+            proc->step = T_CLI_SEND;
+            break;
+        }
+        default:
+            return;
+        }
+    }
+}
+
+static void tcp_start(Process* proc) {
+    proc->buf = g_malloc0(g_cfg->tcp_bytes ? g_cfg->tcp_bytes : 1);
+    proc->epollfd = host_createDescriptor(proc->host, DT_EPOLL);
+    proc->step = g_cfg->proc_peer[proc->index] < 0 ? T_SRV_START : T_CLI_START;
+    tcp_run(proc);
+}
+
+static void tcp_continue(Process* proc) {
+    Host* host = proc->host;
+    struct epoll_event evs[4];
+    gint nfds = 0;
+    if (host_epollGetEvents(host, proc->epollfd, evs, 4, &nfds) != 0 || nfds <= 0) return;
+    (void)host_epollControl(host, proc->epollfd, EPOLL_CTL_DEL, proc->wait_fd, NULL);
+    proc->wait_fd = -1;
+    tcp_run(proc);
+}
+
 static void process_start_task(Process* proc, gpointer nothing) {
     /* _process_start (process.c:1055-1195): the process runs its main until it
      * blocks */
@@ -342,6 +516,7 @@ static void process_start_task(Process* proc, gpointer nothing) {
     worker_setActiveProcess(proc);
     proc->running = TRUE;
     if (g_cfg->app == 0) phold_start(proc);
+    else if (g_cfg->app == 1) tcp_start(proc);
     worker_setActiveProcess(NULL);
 }
 static void process_stop_task(Process* proc, gpointer nothing) { process_stop(proc); }
@@ -369,6 +544,7 @@ void process_continue(Process* proc) {
     if (!process_isRunning(proc)) return;
     worker_setActiveProcess(proc);
     if (g_cfg->app == 0) phold_continue(proc);
+    else if (g_cfg->app == 1) tcp_continue(proc);
     worker_setActiveProcess(NULL);
 }
 
@@ -392,6 +568,10 @@ int ref_loop_run(const ref_loop_cfg* cfg, ref_loop_out* out) {
     Scheduler* sched = scheduler_new(SP_SERIAL_GLOBAL, 0, &g_slave, 1, cfg->end_time);
     g_sched = sched;
     g_hosts = calloc((size_t)H, sizeof(Host*));
+    if (cfg->app == 1) {
+        if (cfg->n_procs <= 0 || !cfg->proc_peer) return -3;
+        g_procs = calloc((size_t)cfg->n_procs, sizeof(Process*));
+    }
     for (int32_t i = 0; i < H; i++) {
         /* master.c:300-380 (host parameters), slave_addNewVirtualHost (host_new +
          * host_setup + scheduler_addHost) */
@@ -417,7 +597,14 @@ int ref_loop_run(const ref_loop_cfg* cfg, ref_loop_out* out) {
         p.qdisc = options_getQueuingDiscipline(g_options);
         Host* host = host_new(&p);
         host_setup(host, g_dns, (Topology*)&g_topology, 0, cfg->root_dir);
-        if (cfg->n_procs > 0) {
+        if (cfg->app == 1) {
+            for (int32_t k = 0; k < cfg->n_procs; k++)
+                if (cfg->proc_host[k] == i) {
+                    char arg[16];
+                    snprintf(arg, sizeof(arg), "%d", k);
+                    host_addApplication(host, cfg->proc_start[k], 0, "testtcp", "testtcp.so", NULL, NULL, NULL, arg);
+                }
+        } else if (cfg->n_procs > 0) {
             for (int32_t k = 0; k < cfg->n_procs; k++)
                 if (cfg->proc_host[k] == i)
                     host_addApplication(host, cfg->proc_start[k], 0, "phold", "phold.so", NULL, NULL, NULL, "");

@@ -34,7 +34,8 @@ class Cfg(C.Structure):
                 ("end_time", C.c_uint64), ("bootstrap_end", C.c_uint64),
                 ("heartbeat_interval", C.c_uint64), ("app_start", C.c_uint64),
                 ("load", C.c_uint32), ("payload", C.c_uint32),
-                ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p)]
+                ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p),
+                ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32)]
 
 
 class Out(C.Structure):
@@ -63,7 +64,7 @@ def _ptr(a, ct):
     return None if a is None else a.ctypes.data_as(P(ct))
 
 
-def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None):
+def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None):
     """run_inproc in a forked child: the reference keeps process-wide state
     (the worker's thread-private object, glib quarks), so one run per process."""
     import multiprocessing as mp
@@ -72,7 +73,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None):
 
     def child():
         try:
-            wr.send(("ok", run_inproc(model, g, host_start, procs)))
+            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp)))
         except BaseException as ex:   # noqa: BLE001 -- reported to the parent
             wr.send(("err", repr(ex)))
         wr.close()
@@ -90,12 +91,14 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None):
     return res
 
 
-def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None):
+def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None):
     """Run the model through the reference's loop; returns dict(lines=[(t, h, line)],
     ip=[str], next_event_id, next_packet_id, rng_probe (uint arrays)).
     host_start: [H] process start times (default: the model's app_start);
     procs: [(host, start)] processes in <process> order instead (the oracle's
-    and the engine's pushed SHD_EV_APP_START events, in push order)."""
+    and the engine's pushed SHD_EV_APP_START events, in push order);
+    tcp: dict(peers=[-1 | server process index per process], nbytes=N) runs
+    the TCP echo test (test_tcp.c) in those processes instead of PHOLD."""
     m = model.struct
     H = int(m.n_hosts)
     og = O.lib().o_graph_new(C.byref(g.struct))
@@ -105,7 +108,12 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     keep = []
     cfg = Cfg()
     cfg.n_hosts = H
-    cfg.app = 0
+    cfg.app = 0 if tcp is None else 1
+    if tcp is not None:
+        pp = np.ascontiguousarray(tcp["peers"], dtype=np.int32)
+        keep.append(pp)
+        cfg.proc_peer = _ptr(pp, C.c_int32)
+        cfg.tcp_bytes = int(tcp.get("nbytes", 20000))
     cfg.host_seed = m.host_rng
     cfg.host_vertex = m.host_vertex
     cfg.bw_down_kibps = m.bw_down_kibps
