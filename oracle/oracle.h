@@ -19,7 +19,7 @@
  *  - Event loop: restated from worker.c / event.c / scheduler.c /
  *    network_interface.c / router.c / tracker.c.  Pinned as a whole to the
  *    reference's OWN serial loop: worker.c, scheduler.c, host.c,
- *    network_interface.c, router*.c, descriptor/*.c, tracker.c, packet.c ...
+ *    network_interface.c, router*.c, descriptor/ (all), tracker.c, packet.c ...
  *    compiled unmodified into oracle/_ref/libshdref_loop.so, with test doubles
  *    only for what the image cannot build (slave.c, the igraph topology --
  *    served by this oracle's lazy path cache --, the rpth process layer, the
@@ -194,7 +194,30 @@ int o_baseline(const shd_model* m, const shd_graph* g, uint64_t t_mark, uint64_t
 /* ---- reference priority order (event.c:110-153) as a checker ---- */
 int o_event_compare(const shd_event* a, const shd_event* b);
 
+/* ---- the TCP path (o_tcp.c): the echo test of src/test/tcp/test_tcp.c on the
+ * serial loop, writing packet.c's [STATUS] lines ("<time>\t<host>\t<line>\n";
+ * host -1: a delivery's copy released after its task) ---- */
+typedef struct o_tcp_cfg {
+    int32_t n_hosts, n_procs;
+    const uint32_t* host_ip;          /* [H] host byte order (the DNS's) */
+    const uint32_t* host_seed;        /* [H] host RNG state after attach */
+    const int32_t* host_vertex;       /* [H] */
+    const uint64_t* bw_down_kibps, *bw_up_kibps;   /* [H] */
+    const int32_t* proc_host;         /* [P] */
+    const uint64_t* proc_start;       /* [P] */
+    const int32_t* proc_peer;         /* [P] -1 server, else the server process */
+    uint64_t end_time, heartbeat_interval;
+    uint32_t tcp_bytes, recv_buf, send_buf, tcp_window;
+} o_tcp_cfg;
+typedef struct o_tcp_out {
+    char* lines; size_t len; uint64_t n_lines;
+    uint64_t* next_event_id; uint64_t* next_packet_id; uint32_t* rng_probe;
+} o_tcp_out;
+int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out);
+void o_tcp_free(o_tcp_out* out);
+
 #ifdef __cplusplus
 }
+
 #endif
 #endif

@@ -291,3 +291,84 @@ def baseline(model: S.ModelArrays, g: S.GraphArrays, t_mark: int, t_end: int, th
     out = {f: getattr(o, f) for f, _ in OBaseline._fields_}
     out["rc"] = rc
     return out
+
+
+# ---- the TCP path (o_tcp.c) ----
+class TcpCfg(C.Structure):
+    _fields_ = [("n_hosts", C.c_int32), ("n_procs", C.c_int32),
+                ("host_ip", C.POINTER(C.c_uint32)), ("host_seed", C.POINTER(C.c_uint32)),
+                ("host_vertex", C.POINTER(C.c_int32)),
+                ("bw_down_kibps", C.POINTER(C.c_uint64)), ("bw_up_kibps", C.POINTER(C.c_uint64)),
+                ("proc_host", C.POINTER(C.c_int32)), ("proc_start", C.POINTER(C.c_uint64)),
+                ("proc_peer", C.POINTER(C.c_int32)),
+                ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
+                ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
+                ("tcp_window", C.c_uint32)]
+
+
+class TcpOut(C.Structure):
+    _fields_ = [("lines", C.c_char_p), ("len", C.c_size_t), ("n_lines", C.c_uint64),
+                ("next_event_id", C.POINTER(C.c_uint64)), ("next_packet_id", C.POINTER(C.c_uint64)),
+                ("rng_probe", C.POINTER(C.c_uint32))]
+
+
+def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf=131072, tcp_window=10):
+    """The oracle's TCP echo run (o_tcp.c) on the model's hosts: procs = [(host,
+    start)], peers = [-1 | server process]; ips: host-order uint32 per host.
+    Returns dict(lines=[(t, h, line)], next_event_id, next_packet_id, rng_probe)
+    with a delivery copy's release (host -1) put on its receiver, as the
+    reference-loop binding does."""
+    import numpy as np
+    m = model.struct
+    H = int(m.n_hosts)
+    og = lib().o_graph_new(C.byref(g.struct))
+    hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
+    att = np.ascontiguousarray(np.unique(hv).astype(np.int32))
+    topo = lib().o_topo_new(og, att.ctypes.data_as(C.POINTER(C.c_int32)), len(att), 0)
+    ipa = np.ascontiguousarray(ips, dtype=np.uint32)
+    ph = np.ascontiguousarray([p[0] for p in procs], dtype=np.int32)
+    ps = np.ascontiguousarray([p[1] for p in procs], dtype=np.uint64)
+    pp = np.ascontiguousarray(peers, dtype=np.int32)
+    cfg = TcpCfg()
+    cfg.n_hosts = H
+    cfg.n_procs = len(ph)
+    cfg.host_ip = ipa.ctypes.data_as(C.POINTER(C.c_uint32))
+    cfg.host_seed = m.host_rng
+    cfg.host_vertex = m.host_vertex
+    cfg.bw_down_kibps = m.bw_down_kibps
+    cfg.bw_up_kibps = m.bw_up_kibps
+    cfg.proc_host = ph.ctypes.data_as(C.POINTER(C.c_int32))
+    cfg.proc_start = ps.ctypes.data_as(C.POINTER(C.c_uint64))
+    cfg.proc_peer = pp.ctypes.data_as(C.POINTER(C.c_int32))
+    cfg.end_time = m.end_time
+    cfg.heartbeat_interval = m.heartbeat_interval
+    cfg.tcp_bytes = nbytes
+    cfg.recv_buf = recv_buf
+    cfg.send_buf = send_buf
+    cfg.tcp_window = tcp_window
+    out = TcpOut()
+    l = lib()
+    l.o_tcp_run.argtypes = [C.POINTER(TcpCfg), C.c_void_p, C.POINTER(TcpOut)]
+    l.o_tcp_free.argtypes = [C.POINTER(TcpOut)]
+    try:
+        rc = l.o_tcp_run(C.byref(cfg), topo, C.byref(out))
+        assert rc == 0, rc
+        text = C.string_at(out.lines, out.len).decode() if out.len else ""
+        ipstr = [".".join(str((int(x) >> s) & 255) for s in (24, 16, 8, 0)) for x in ipa]
+        by_ip = {ip: h for h, ip in enumerate(ipstr)}
+        lines = []
+        for ln in text.splitlines():
+            t, h, body = ln.split("\t", 2)
+            h = int(h)
+            if h < 0 and " -> " in body:
+                h = by_ip[body.split(" -> ")[1].split(":")[0]]
+            lines.append((int(t), h, body))
+        res = dict(lines=lines,
+                   next_event_id=np.ctypeslib.as_array(out.next_event_id, shape=(H,)).copy(),
+                   next_packet_id=np.ctypeslib.as_array(out.next_packet_id, shape=(H,)).copy(),
+                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy())
+        l.o_tcp_free(C.byref(out))
+    finally:
+        lib().o_topo_free(topo)
+        lib().o_graph_free(og)
+    return res
