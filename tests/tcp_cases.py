@@ -1,0 +1,79 @@
+"""TCP echo models (src/test/tcp/test_tcp.c in its nonblocking-epoll mode) run
+through the reference's own loop (oracle/_ref/libshdref_loop.so, app 1) and
+the oracle's restatement (oracle/o_tcp.c) -- TEST INFRASTRUCTURE.
+
+The first two cases are the reference's own TCP tests
+(src/test/tcp/tcp-nonblocking-epoll-{lossless,lossy}.test.shadow.config.xml):
+one vertex with a 50 ms self-loop, loss 0 / 0.25, 10240 KiB/s, the server at
+1 s, the client at 2 s, 20000 bytes each way, kill at 300 s.  The others widen
+them: a 2 MB transfer (slow start into congestion avoidance, buffer
+autotuning), 2 % loss on 500 kB (fast retransmit, SACK ranges), slow links
+(CoDel queues at the receiver), heavy loss (RTO backoff), ten pairs on a lossy
+geometric graph, and hosts running several servers and clients at once.
+"""
+import hashlib
+
+import numpy as np
+
+import shdgpu as S
+import workloads as W
+
+SEC = S.SHD_SEC
+
+
+def _one_vertex(lat, loss):
+    return S.GraphArrays(1, [0], [0], [lat], [loss])
+
+
+def _pair(lat, loss, nbytes, end_s, **bw):
+    g = _one_vertex(lat, loss)
+    return dict(graph=g, hv=[0, 0], procs=[(0, SEC), (1, 2 * SEC)], peers=[-1, 0], nbytes=nbytes, end=end_s, bw=bw)
+
+
+def _geo_pairs():
+    g = W.geometric_graph(30, seed=4, loss_max=0.05)
+    H = 20
+    procs = [(2 * i, SEC) for i in range(H // 2)] + [(2 * i + 1, 2 * SEC + i * 1000) for i in range(H // 2)]
+    peers = [-1] * (H // 2) + list(range(H // 2))
+    return dict(graph=g, hv=list(np.arange(H) % 30), procs=procs, peers=peers, nbytes=100000, end=60, bw={})
+
+
+def _shared_hosts():
+    g = W.geometric_graph(10, seed=2, loss_max=0.02)
+    procs = [(0, SEC), (1, SEC), (2, SEC), (0, 2 * SEC), (1, 2 * SEC), (2, 2 * SEC), (0, 2 * SEC + 5)]
+    return dict(graph=g, hv=[0, 3, 7], procs=procs, peers=[-1, -1, -1, 1, 2, 0, 2], nbytes=200000, end=60, bw={})
+
+
+CASES = {
+    "ref_epoll_lossless": lambda: _pair(50.0, 0.0, 20000, 300),
+    "ref_epoll_lossy": lambda: _pair(50.0, 0.25, 20000, 300),
+    "bulk_2mb": lambda: _pair(50.0, 0.0, 2000000, 60),
+    "lossy_2pct": lambda: _pair(50.0, 0.02, 500000, 60),
+    "slow_links": lambda: _pair(20.0, 0.0, 300000, 60, bw_down=256, bw_up=512),
+    "heavy_loss": lambda: _pair(30.0, 0.25, 200000, 200),
+    "geo_pairs": _geo_pairs,
+    "shared_hosts": _shared_hosts,
+}
+
+
+def build(name):
+    c = CASES[name]()
+    m = W.phold_model(np.asarray(c["hv"], dtype=np.int32), end_time=c["end"] * SEC, trace=True,
+                      queue_flags=S.SHD_QF_TRACE_STATUS, load=0, **c["bw"])
+    return c, m
+
+
+def status_lines(lines):
+    """The [STATUS] lines (the tracker's heartbeat lines are not part of the TCP restatement)."""
+    return [ln for ln in lines if not ln[2].startswith("[shadow-heartbeat]")]
+
+
+def digest(lines):
+    h = hashlib.sha256()
+    for t, host, body in lines:
+        h.update(f"{t}\t{host}\t{body}\n".encode())
+    return h.hexdigest()
+
+
+def ip_ints(ips):
+    return [int.from_bytes(bytes(int(x) for x in ip.split(".")), "big") for ip in ips]
