@@ -1,0 +1,76 @@
+/*
+ * shdtcp.h -- the TCP path on the GPU, C ABI.
+ *
+ * Runs the reference's TCP (host/descriptor/tcp.c, tcp_cong_reno.c,
+ * tcp_retransmit_tally.cc, the socket buffers of socket.c and the interface of
+ * network_interface.c) for client/server processes running the reference's own
+ * TCP test application (src/test/tcp/test_tcp.c, nonblocking-epoll: connect,
+ * send N bytes, read them echoed back, close) on every host of a model, in
+ * conservative rounds on one GPU: one lane per host, a round is every event
+ * before the window's end (the smallest path latency), deliveries cross hosts
+ * through a mailbox between rounds.  Results equal the reference's serial loop
+ * (tests/test_tcp_gpu.py against tests/golden/ref_tcp.json).
+ *
+ * The boundary is the same one shdgpu.h draws for the UDP path: plain
+ * pointers and sizes, no torch types.  Path latency and reliability per host
+ * pair come from the caller (Shadow's topology_getLatency /
+ * topology_getReliability, topology.c:2053-2092, or shd_pc_lookup), resolved
+ * in the order the serial loop touches them.
+ */
+#ifndef SHD_TCP_H
+#define SHD_TCP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct shd_tcp_model {
+    int32_t n_hosts, n_procs;
+    const uint32_t* host_ip;          /* [H] host byte order (dns.c's addresses)        */
+    const uint32_t* host_seed;        /* [H] host RNG state after attach                */
+    const uint64_t* bw_down_kibps;    /* [H]                                            */
+    const uint64_t* bw_up_kibps;      /* [H]                                            */
+    const double* path_lat_ms;        /* [H*H] src*H + dst; < 0: no route               */
+    const double* path_rel;           /* [H*H]                                          */
+    const int32_t* proc_host;         /* [P] the host of each process, <process> order  */
+    const uint64_t* proc_start;       /* [P] start time (ns)                            */
+    const int32_t* proc_peer;         /* [P] -1: server; else the server process index  */
+    uint64_t end_time;                /* ns; events at or past it are never run         */
+    uint64_t heartbeat_interval;      /* ns (tracker heartbeats consume event IDs)      */
+    uint32_t tcp_bytes;               /* bytes each client sends (test_tcp.c BUFFERSIZE) */
+    uint32_t recv_buf, send_buf;      /* initial socket buffers (CONFIG_*_BUFFER_SIZE)   */
+    uint32_t tcp_window;              /* --tcp-windows (options.c:79)                    */
+} shd_tcp_model;
+
+typedef struct shd_tcp_result {
+    char* lines;                      /* "<time>\t<host>\t[STATUS] ...\n", each host's lines in
+                                         its execution order, hosts in index order           */
+    size_t len;
+    uint64_t n_lines;
+    uint64_t* next_event_id;          /* [H] host event counter at the end                */
+    uint64_t* next_packet_id;         /* [H]                                              */
+    uint32_t* rng_probe;              /* [H] the next rand_r value of each host RNG       */
+    uint64_t rounds;                  /* conservative rounds run                          */
+    uint64_t events;                  /* events executed                                  */
+    double device_ms;                 /* GPU time of the rounds (HIP events)              */
+    uint32_t error;                   /* SHD_TCP_ERR_* bits; nonzero: results invalid     */
+} shd_tcp_result;
+
+enum {
+    SHD_TCP_ERR_EVQ = 1, SHD_TCP_ERR_POOL = 2, SHD_TCP_ERR_QUEUE = 4, SHD_TCP_ERR_SOCKETS = 8,
+    SHD_TCP_ERR_MAILBOX = 16, SHD_TCP_ERR_TRACE = 32, SHD_TCP_ERR_SACK = 64, SHD_TCP_ERR_INTERNAL = 128
+};
+
+/* Run the model to end_time on the current HIP device.  trace != 0 writes the
+ * [STATUS] lines (packet.c:647-659).  Returns 0 or a negative errno-style code;
+ * *out is allocated by the call and released by shd_tcp_result_free. */
+int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out);
+void shd_tcp_result_free(shd_tcp_result* r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

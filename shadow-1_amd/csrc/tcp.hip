@@ -1,0 +1,1978 @@
+// tcp.hip -- the TCP path on the GPU (include/shdtcp.h).
+//
+// The reference's TCP, run for the processes of the reference's own TCP test
+// (src/test/tcp/test_tcp.c, nonblocking-epoll) on every host of a model:
+//
+//   connection state machine   host/descriptor/tcp.c:607-698, 1777-2099
+//   segments, windows, flush   tcp.c:729-852, 1090-1278
+//   retransmission, RTO        tcp.c:854-1065, 1280-1333 (RFC 6298)
+//   SACK / lost ranges         tcp_retransmit_tally.cc
+//   Reno                       tcp_cong_reno.c
+//   buffer autotuning          tcp.c:363-591
+//   user send / receive        tcp.c:2126-2327, host.c:1466-1604
+//   connect / listen / accept  tcp.c:1462-1558, host.c:1111-1358
+//   close                      tcp.c:2363-2408
+//   socket buffers             socket.c:284-455
+//   interface, FIFO qdisc      network_interface.c:87-226, 375-605
+//   worker_sendPacket          worker.c:260-321
+//   router + CoDel             router.c:104-140, router_queue_codel.c
+//   epoll notification         epoll.c:252-395, 411-615, 638-683
+//   binary heaps               utility/priority_queue.c
+//
+// Execution: conservative rounds of width W = the smallest path latency
+// between hosts (ceil(ms * 1e6)); one lane per host runs every event of its
+// own heap before the round's end in event order (time, src, seq; event.c:
+// 110-153), exactly as the serial loop would, because nothing another host
+// does inside the round can reach it before the round ends.  A delivery to
+// another host goes into the round's mailbox with its packet copy and is
+// taken by the receiver's lane at the start of the next round.  Every piece
+// of state lives in HBM in fixed-capacity per-host / per-socket arrays; an
+// overflow sets an error bit instead of corrupting anything.
+//
+// The work is branchy per-host control flow with a few events per host and
+// round: latency-bound by design ("TCP"); it shares nothing with
+// the UDP engine's LDS-resident round kernels.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/shdtcp.h"
+
+namespace {
+
+constexpr uint64_t kMs = 1000000ull;
+constexpr uint64_t kSec = 1000000000ull;
+constexpr uint32_t kMTU = 1500, kHdr = 66, kMSS = kMTU - kHdr;
+constexpr int kSock = 8;            // sockets per host (a listener, its children, clients)
+constexpr int kProcs = 8;           // processes per host
+constexpr uint32_t kQ = 4096;       // per-socket packet queues
+constexpr uint32_t kQc = 256;       // control-packet queue
+constexpr uint32_t kTimers = 256;   // pending RTO timer expirations
+constexpr uint32_t kSacks = 512;    // the receiver's SACK list
+constexpr uint32_t kRanges = 64;    // tally ranges per set
+constexpr uint32_t kKids = 8;
+constexpr uint32_t kPool = 16384;   // packets per host
+constexpr uint32_t kPktSack = 64;   // SACK entries carried by one segment
+constexpr uint32_t kEv = 8192;      // events per host
+constexpr uint32_t kCq = 4096;      // CoDel queue per host
+constexpr uint32_t kTr = 1u << 16;  // trace records per host
+constexpr uint32_t kTrSack = 1u << 20;
+constexpr uint32_t kMail = 1u << 16;
+
+// ProtocolTCPFlags (protocol.h:23-31)
+enum : uint32_t { F_RST = 1 << 1, F_SYN = 1 << 2, F_ACK = 1 << 3, F_SACK = 1 << 4, F_FIN = 1 << 5, F_DUPACK = 1 << 6 };
+enum : uint8_t {
+    S_SND_CREATED, S_SND_TCP_ENQUEUE_THROTTLED, S_SND_TCP_ENQUEUE_RETRANSMIT, S_SND_TCP_DEQUEUE_RETRANSMIT,
+    S_SND_TCP_RETRANSMITTED, S_SND_SOCKET_BUFFERED, S_SND_INTERFACE_SENT, S_INET_SENT, S_INET_DROPPED,
+    S_ROUTER_ENQUEUED, S_ROUTER_DEQUEUED, S_ROUTER_DROPPED, S_RCV_INTERFACE_RECEIVED, S_RCV_INTERFACE_DROPPED,
+    S_RCV_SOCKET_PROCESSED, S_RCV_SOCKET_DROPPED, S_RCV_TCP_ENQUEUE_UNORDERED, S_RCV_SOCKET_BUFFERED,
+    S_RCV_SOCKET_DELIVERED, S_DESTROYED
+};
+const char* const kStatusName[] = {
+    "SND_CREATED", "SND_TCP_ENQUEUE_THROTTLED", "SND_TCP_ENQUEUE_RETRANSMIT", "SND_TCP_DEQUEUE_RETRANSMIT",
+    "SND_TCP_RETRANSMITTED", "SND_SOCKET_BUFFERED", "SND_INTERFACE_SENT", "INET_SENT", "INET_DROPPED",
+    "ROUTER_ENQUEUED", "ROUTER_DEQUEUED", "ROUTER_DROPPED", "RCV_INTERFACE_RECEIVED", "RCV_INTERFACE_DROPPED",
+    "RCV_SOCKET_PROCESSED", "RCV_SOCKET_DROPPED", "RCV_TCP_ENQUEUE_UNORDERED", "RCV_SOCKET_BUFFERED",
+    "RCV_SOCKET_DELIVERED", "PDS_DESTROYED"};
+enum : uint32_t { DS_ACTIVE = 1, DS_READABLE = 2, DS_WRITABLE = 4, DS_CLOSED = 8 };
+enum { TS_CLOSED, TS_LISTEN, TS_SYNSENT, TS_SYNRECEIVED, TS_ESTABLISHED, TS_FINWAIT1, TS_FINWAIT2, TS_CLOSING,
+       TS_TIMEWAIT, TS_CLOSEWAIT, TS_LASTACK };
+enum : uint32_t { TF_LOCAL_CLOSED_RD = 1, TF_LOCAL_CLOSED_WR = 2, TF_REMOTE_CLOSED = 4, TF_EOF_RD_SIGNALED = 8,
+                  TF_EOF_WR_SIGNALED = 16, TF_RESET_SIGNALED = 32, TF_WAS_ESTABLISHED = 64,
+                  TF_CONNECT_SIGNALED = 128, TF_SHOULD_SEND_WR_FIN = 256 };
+enum : uint32_t { TE_CONNECTION_RESET = 1, TE_SEND_EOF = 2, TE_RECEIVE_EOF = 4 };
+enum : uint32_t { PF_PROCESSED = 1, PF_DATA_RECEIVED = 2, PF_DATA_ACKED = 4, PF_DATA_LOST = 16, PF_RWND_UPDATED = 32 };
+enum { E_WOULDBLOCK = 11, E_INPROGRESS = 115, E_ALREADY = 114, E_ISCONN = 106, E_NOTCONN = 107, E_PIPE = 32,
+       E_CONNRESET = 104, E_CONNREFUSED = 111 };
+enum : uint32_t { K_HEARTBEAT, K_REFILL, K_REFILL_LO, K_PSTART, K_NOTIFY, K_DELIVER, K_DELACK, K_RTO, K_CLOSE,
+                  K_WINUPD };
+enum { T_SRV_START, T_SRV_ACCEPT, T_SRV_RECV, T_SRV_SEND, T_CLI_START, T_CLI_CONNECT, T_CLI_SEND, T_CLI_RECV,
+       T_DONE };
+
+struct DPkt {
+    uint32_t host_id; int32_t refs;
+    uint64_t pid;
+    uint32_t flags, sip, dip;
+    uint16_t sport, dport;
+    uint32_t seq, ack, win, len;
+    uint64_t tsval, tsecho;
+    double prio;
+    uint32_t nsack, nst;
+    uint8_t st[32];
+    int32_t sacks[kPktSack];
+};
+struct DEv { uint64_t time, seq; uint32_t src, kind; int32_t obj, pkt; };
+struct Mail { uint32_t dst, src; uint64_t time, seq; DPkt pkt; };
+struct TRec {
+    uint64_t time; int32_t host; uint32_t status;
+    uint32_t host_id, flags, sip, dip;
+    uint64_t pid;
+    uint16_t sport, dport; uint32_t seq, ack, win, len;
+    uint64_t tsval, tsecho;
+    uint32_t sack_off, nsack, nst;
+    uint8_t st[32];
+};
+template <uint32_t N> struct Ring {   // GQueue
+    uint32_t head, n;
+    int32_t a[N];
+};
+template <uint32_t N> struct IHeap { uint32_t n; int32_t a[N]; };   // priority_queue.c over indices
+template <uint32_t N> struct THeap { uint32_t n; uint64_t a[N]; };  // timer expirations
+struct Rng64 { int64_t a, b; };
+struct RVec { uint32_t n; Rng64 r[kRanges]; };
+struct Tally { int64_t last_ack; uint64_t ndup; RVec marked, sacked, retx, lost, tmp; };
+
+struct DSock {
+    int32_t used, host, proc;
+    uint32_t status;
+    int32_t bound; uint32_t bound_ip; uint16_t bound_port, peer_port;
+    uint32_t peer_ip;
+    int32_t assoc, assoc_general;
+    uint64_t in_len, in_size, in_pending, out_len, out_size, out_pending;
+    Ring<kQ> in, out;
+    Ring<kQc> outctl;
+    int32_t state, state_last;
+    uint32_t flags, error;
+    uint32_t r_start, r_next, r_window, r_end, r_last_window, r_last_ack, r_last_seq;
+    uint64_t r_last_ts; int32_t r_winupd;
+    uint32_t s_unacked, s_next, s_window, s_end, s_last_ack, s_last_window, s_highest, s_packets_sent,
+        s_quick_acks, s_delack_counter;
+    int32_t s_delack_sched;
+    uint32_t nsack; int32_t sacks[kSacks];
+    uint32_t nrtx; int32_t rtx[kQ]; uint64_t rtx_len; int32_t rto; THeap<kTimers> timers; uint64_t desired;
+    uint32_t backoff;
+    Tally tally;
+    int32_t at_did_init; uint64_t at_bytes, at_last_adjust, at_space;
+    uint32_t cwnd; int32_t reno_state; uint64_t reno_ndup; uint32_t reno_nacked, reno_ssthresh;
+    int32_t srtt, rttvar;
+    uint64_t retx_count; uint32_t info_rtt;
+    IHeap<kQ> throttled; uint64_t throttled_len;
+    IHeap<kQ> unordered; uint64_t unordered_len;
+    int32_t partial; uint32_t partial_off;
+    int32_t server; uint32_t nkids, npending; int32_t kids[kKids], pending[kKids];
+    uint32_t last_peer_ip, last_ip; uint16_t last_peer_port;
+    int32_t child, parent, child_state;
+};
+struct DProc {
+    int32_t host, index, peer, running, step, fd, listenfd, wait_fd;
+    uint32_t wait_events, done;
+    int32_t ep_ready, ep_scheduled, ep_notifying;
+    uint64_t start;
+};
+struct DHost {
+    uint32_t ip, rng, pkt_seq, err;
+    uint64_t ev_seq, events;
+    double prio;
+    uint64_t rx_rem, rx_cap, rx_refill, tx_rem, tx_cap, tx_refill;
+    uint64_t bw_down, bw_up;   // configured KiB/s (worker_getNodeBandwidth{Down,Up})
+    int32_t refill_pending, nsock, next_handle;
+    IHeap<2 * kSock> fifo;
+    // CoDel (router_queue_codel.c)
+    uint32_t cq_head, cq_n; uint64_t cq_total, cq_iexp, cq_next_drop; uint32_t cq_dc, cq_dc_last; int32_t cq_mode;
+    uint32_t nfree, ntr, ntrs, nev;
+};
+struct CqEnt { uint64_t ts; uint32_t len; int32_t pkt; };
+
+struct Glob {
+    int32_t H, P;
+    const double *lat, *rel;
+    uint64_t end_time, hb, window_end, now_dummy;
+    uint32_t tcp_bytes, trace, recv_buf, send_buf, tcp_window, _pad;
+    DHost* host;
+    DSock* sock;            // [H][kSock]
+    DProc* proc;            // [P]
+    int32_t* host_procs;    // [H][kProcs]
+    DPkt* pool;             // [H][kPool]
+    int32_t* freel;         // [H][kPool]
+    DEv* ev;                // [H][kEv]
+    CqEnt* cq;              // [H][kCq]
+    Mail* mail_in; uint32_t* n_in;
+    Mail* mail_out; uint32_t* n_out;
+    TRec* tr;               // [H][kTr]
+    int32_t* trs;           // [H][kTrSack]
+    uint64_t* next_time;    // [H]
+};
+
+// ------------------------------------------------------------ per-lane context
+struct L {
+    const Glob* g;
+    int32_t h;
+    DHost* H;
+    uint64_t now;
+    int32_t active;
+};
+__device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * kPool + i]; }
+__device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
+
+__device__ int32_t rand_r_dev(uint32_t* state) {   // glibc rand_r (random.c's source)
+    uint32_t next = *state;
+    int32_t result;
+    next *= 1103515245u; next += 12345u;
+    result = (int32_t)((next / 65536u) % 2048u);
+    next *= 1103515245u; next += 12345u;
+    result <<= 10; result ^= (int32_t)((next / 65536u) % 1024u);
+    next *= 1103515245u; next += 12345u;
+    result <<= 10; result ^= (int32_t)((next / 65536u) % 1024u);
+    *state = next;
+    return result;
+}
+__device__ double next_double(uint32_t* s) { return (double)(((double)rand_r_dev(s)) / ((double)2147483647)); }
+
+// ------------------------------------------------------------ heaps (priority_queue.c)
+template <uint32_t N, class Less> __device__ uint32_t ih_up(IHeap<N>& q, uint32_t i, Less lt) {
+    while (i > 0 && lt(q.a[i], q.a[(i - 1) / 2])) { int32_t t = q.a[i]; q.a[i] = q.a[(i - 1) / 2]; q.a[(i - 1) / 2] = t; i = (i - 1) / 2; }
+    return i;
+}
+template <uint32_t N, class Less> __device__ uint32_t ih_down(IHeap<N>& q, uint32_t i, Less lt) {
+    uint32_t ch;
+    while ((ch = 2 * i + 1) < q.n) {
+        if (ch + 1 < q.n && lt(q.a[ch + 1], q.a[ch])) ch = ch + 1;
+        if (lt(q.a[ch], q.a[i])) { int32_t t = q.a[i]; q.a[i] = q.a[ch]; q.a[ch] = t; i = ch; } else break;
+    }
+    return i;
+}
+template <uint32_t N> __device__ int ih_find(const IHeap<N>& q, int32_t x) {
+    for (uint32_t i = 0; i < q.n; i++) if (q.a[i] == x) return (int)i;
+    return -1;
+}
+template <uint32_t N, class Less> __device__ bool ih_push(IHeap<N>& q, int32_t x, Less lt, uint32_t& err) {
+    const int old = ih_find(q, x);
+    if (old >= 0) { ih_up(q, ih_down(q, (uint32_t)old, lt), lt); return false; }
+    if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return false; }
+    q.a[q.n++] = x;
+    ih_up(q, q.n - 1, lt);
+    return true;
+}
+template <uint32_t N, class Less> __device__ int32_t ih_pop(IHeap<N>& q, Less lt) {
+    if (!q.n) return -1;
+    const int32_t x = q.a[0];
+    q.a[0] = q.a[q.n - 1];
+    q.a[q.n - 1] = x;
+    q.n--;
+    ih_down(q, 0, lt);
+    return x;
+}
+struct SeqLess {   // packet_compareTCPSequence (packet.c:207-221)
+    const DPkt* pool;
+    __device__ bool operator()(int32_t a, int32_t b) const { return pool[a].seq < pool[b].seq; }
+};
+template <uint32_t N> __device__ void th_push(THeap<N>& q, uint64_t x, uint32_t& err) {
+    if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return; }
+    uint32_t i = q.n++;
+    q.a[i] = x;
+    while (i > 0 && q.a[i] < q.a[(i - 1) / 2]) { uint64_t t = q.a[i]; q.a[i] = q.a[(i - 1) / 2]; q.a[(i - 1) / 2] = t; i = (i - 1) / 2; }
+}
+template <uint32_t N> __device__ void th_pop(THeap<N>& q) {
+    if (!q.n) return;
+    uint64_t x = q.a[0];
+    q.a[0] = q.a[q.n - 1];
+    q.a[q.n - 1] = x;
+    q.n--;
+    uint32_t i = 0, ch;
+    while ((ch = 2 * i + 1) < q.n) {
+        if (ch + 1 < q.n && q.a[ch + 1] < q.a[ch]) ch = ch + 1;
+        if (q.a[ch] < q.a[i]) { uint64_t t = q.a[i]; q.a[i] = q.a[ch]; q.a[ch] = t; i = ch; } else break;
+    }
+}
+template <uint32_t N> __device__ void rg_push(Ring<N>& r, int32_t x, uint32_t& err) {
+    if (r.n >= N) { err |= SHD_TCP_ERR_QUEUE; return; }
+    r.a[(r.head + r.n) % N] = x;
+    r.n++;
+}
+template <uint32_t N> __device__ int32_t rg_peek(const Ring<N>& r) { return r.n ? r.a[r.head] : -1; }
+template <uint32_t N> __device__ int32_t rg_pop(Ring<N>& r) {
+    if (!r.n) return -1;
+    const int32_t x = r.a[r.head];
+    r.head = (r.head + 1) % N;
+    r.n--;
+    return x;
+}
+
+// ------------------------------------------------------------ event heap (event.c:110-153)
+__device__ __forceinline__ bool ev_less(const DEv& a, const DEv& b) {
+    if (a.time != b.time) return a.time < b.time;
+    if (a.src != b.src) return a.src < b.src;
+    return a.seq < b.seq;
+}
+__device__ void evq_push(const L& c, const DEv& e) {
+    DEv* q = c.g->ev + (size_t)c.h * kEv;
+    uint32_t& n = c.H->nev;
+    if (n >= kEv) { c.H->err |= SHD_TCP_ERR_EVQ; return; }
+    uint32_t i = n++;
+    while (i > 0) {
+        const uint32_t p = (i - 1) / 2;
+        if (!ev_less(e, q[p])) break;
+        q[i] = q[p];
+        i = p;
+    }
+    q[i] = e;
+}
+__device__ DEv evq_pop(const L& c) {
+    DEv* q = c.g->ev + (size_t)c.h * kEv;
+    uint32_t& n = c.H->nev;
+    const DEv top = q[0], last = q[--n];
+    uint32_t i = 0;
+    for (;;) {
+        const uint32_t l = 2 * i + 1, r = l + 1;
+        uint32_t m = i;
+        const DEv* best = &last;
+        if (l < n && ev_less(q[l], *best)) { m = l; best = &q[l]; }
+        if (r < n && ev_less(q[r], *best)) { m = r; best = &q[r]; }
+        if (m == i) break;
+        q[i] = q[m];
+        i = m;
+    }
+    if (n) q[i] = last;
+    return top;
+}
+// event_new_ consumes the source's ID; scheduler_push drops past the end (scheduler.c:342-357)
+__device__ bool sched_task(L& c, uint64_t delay, uint32_t kind, int32_t obj) {
+    DEv e;
+    e.time = c.now + delay; e.seq = c.H->ev_seq++; e.src = (uint32_t)c.h; e.kind = kind; e.obj = obj; e.pkt = -1;
+    if (e.time >= c.g->end_time) return false;
+    evq_push(c, e);
+    return true;
+}
+
+// ------------------------------------------------------------ packets and their lines
+__device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDeliveryStatus (packet.c:647-659)
+    DPkt* p = PK(c, pi);
+    if (p->nst < 32) p->st[p->nst++] = st;
+    if (!c.g->trace) return;
+    DHost* H = c.H;
+    if (H->ntr >= kTr) { H->err |= SHD_TCP_ERR_TRACE; return; }
+    TRec* r = &c.g->tr[(size_t)c.h * kTr + H->ntr++];
+    r->time = c.now; r->host = c.active; r->status = st;
+    r->host_id = p->host_id; r->pid = p->pid; r->flags = p->flags; r->sip = p->sip; r->dip = p->dip;
+    r->sport = p->sport; r->dport = p->dport; r->seq = p->seq; r->ack = p->ack; r->win = p->win; r->len = p->len;
+    r->tsval = p->tsval; r->tsecho = p->tsecho; r->nst = p->nst;
+    for (uint32_t i = 0; i < p->nst && i < 32; i++) r->st[i] = p->st[i];
+    r->sack_off = H->ntrs; r->nsack = p->nsack;
+    if (H->ntrs + p->nsack > kTrSack) { H->err |= SHD_TCP_ERR_TRACE; r->nsack = 0; return; }
+    for (uint32_t i = 0; i < p->nsack; i++) c.g->trs[(size_t)c.h * kTrSack + H->ntrs + i] = p->sacks[i];
+    H->ntrs += p->nsack;
+}
+__device__ int32_t pkt_alloc(L& c) {
+    DHost* H = c.H;
+    if (!H->nfree) { H->err |= SHD_TCP_ERR_POOL; return -1; }
+    return c.g->freel[(size_t)c.h * kPool + --H->nfree];
+}
+__device__ int32_t pkt_new(L& c, uint32_t len) {   // packet_new (packet.c:74-95)
+    const int32_t i = pkt_alloc(c);
+    if (i < 0) return -1;
+    DPkt* p = PK(c, i);
+    memset(p, 0, sizeof(DPkt) - sizeof(p->sacks));
+    p->refs = 1;
+    p->host_id = (uint32_t)c.h + 1;
+    p->pid = c.H->pkt_seq++;
+    p->len = len;
+    if (len > 0) p->prio = ++c.H->prio;   // host_getNextPacketPriority (host.c:1663-1666)
+    return i;
+}
+__device__ void pkt_ref(L& c, int32_t i) { PK(c, i)->refs++; }
+__device__ void pkt_unref(L& c, int32_t i) {   // packet.c:194-201
+    DPkt* p = PK(c, i);
+    if (--p->refs == 0) {
+        pkt_status(c, i, S_DESTROYED);
+        c.g->freel[(size_t)c.h * kPool + c.H->nfree++] = i;
+    }
+}
+
+// ------------------------------------------------------------ epoll (one watch per process)
+__device__ bool watch_ready(const L& c, const DProc* pr) {
+    if (pr->wait_fd < 0) return false;
+    const DSock* k = &c.g->sock[pr->wait_fd];
+    if ((k->status & DS_CLOSED) || !(k->status & DS_ACTIVE)) return false;
+    return ((k->status & DS_READABLE) && (pr->wait_events & 1)) || ((k->status & DS_WRITABLE) && (pr->wait_events & 4));
+}
+__device__ void ep_schedule(L& c, DProc* pr) {   // _epoll_scheduleNotification (epoll.c:345-366)
+    if (pr->ep_notifying) return;
+    if (!pr->ep_scheduled && pr->running)
+        if (sched_task(c, 1, K_NOTIFY, pr->index)) pr->ep_scheduled = 1;
+}
+__device__ void ep_status_changed(L& c, DProc* pr) {   // epoll_descriptorStatusChanged (epoll.c:585-615)
+    pr->ep_ready = watch_ready(c, pr);
+    if (pr->ep_ready) ep_schedule(c, pr);
+}
+__device__ void sock_status(L& c, DSock* k, uint32_t bits, bool set) {   // descriptor_adjustStatus
+    if (set) k->status |= bits; else k->status &= ~bits;
+    if (k->proc >= 0) {
+        DProc* pr = &c.g->proc[k->proc];
+        if (pr->wait_fd == sidx(c, k)) ep_status_changed(c, pr);
+    }
+}
+
+// ------------------------------------------------------------ socket buffers (socket.c)
+__device__ __forceinline__ uint64_t in_size(const DSock* k) { return k->in_pending ? k->in_pending : k->in_size; }
+__device__ __forceinline__ uint64_t out_size(const DSock* k) { return k->out_pending ? k->out_pending : k->out_size; }
+__device__ __forceinline__ uint64_t in_space(const DSock* k) { const uint64_t s = in_size(k); return s < k->in_len ? 0 : s - k->in_len; }
+__device__ __forceinline__ uint64_t out_space(const DSock* k) { const uint64_t s = out_size(k); return s < k->out_len ? 0 : s - k->out_len; }
+__device__ void set_in_size(DSock* k, uint64_t n) {
+    if (n >= k->in_len) { k->in_size = n; k->in_pending = 0; } else { k->in_size = k->in_len; k->in_pending = n; }
+}
+__device__ void set_out_size(DSock* k, uint64_t n) {
+    if (n >= k->out_len) { k->out_size = n; k->out_pending = 0; } else { k->out_size = k->out_len; k->out_pending = n; }
+}
+__device__ __forceinline__ uint64_t tcp_out_len(const DSock* k) { return k->throttled_len + k->rtx_len; }
+__device__ uint64_t space_out(const DSock* k) {
+    const int64_t s = (int64_t)out_space(k) - (int64_t)tcp_out_len(k);
+    return s > 0 ? (uint64_t)s : 0;
+}
+__device__ uint64_t space_in(const DSock* k) {
+    const int64_t s = (int64_t)in_space(k) - (int64_t)k->unordered_len;
+    return s > 0 ? (uint64_t)s : 0;
+}
+__device__ uint64_t space_out_incl_tcp(const DSock* k) {
+    const uint64_t sp = out_space(k), tl = tcp_out_len(k);
+    return tl < sp ? sp - tl : 0;
+}
+__device__ int32_t sock_peek_out(const L& c, const DSock* k) { return k->outctl.n ? rg_peek(k->outctl) : rg_peek(k->out); }
+struct SockLess {   // _networkinterface_compareSocket: never equal
+    const L* c;
+    __device__ bool operator()(int32_t a, int32_t b) const {
+        const DPkt* pa = PK(*c, sock_peek_out(*c, &c->g->sock[a]));
+        const DPkt* pb = PK(*c, sock_peek_out(*c, &c->g->sock[b]));
+        return !(pa->prio > pb->prio);
+    }
+};
+
+__device__ void if_send_packets(L& c);
+__device__ bool sock_add_input(L& c, DSock* k, int32_t pi) {   // socket.c:319-343
+    DPkt* p = PK(c, pi);
+    if (p->len > in_space(k)) return false;
+    rg_push(k->in, pi, c.H->err);
+    pkt_ref(c, pi);
+    k->in_len += p->len;
+    pkt_status(c, pi, S_RCV_SOCKET_BUFFERED);
+    if (k->in_len > 0) sock_status(c, k, DS_READABLE, true);
+    return true;
+}
+__device__ int32_t sock_remove_input(L& c, DSock* k) {   // socket.c:345-372
+    const int32_t pi = rg_pop(k->in);
+    if (pi >= 0) {
+        k->in_len -= PK(c, pi)->len;
+        if (k->in_pending > 0) set_in_size(k, k->in_pending);
+        if (k->in_len <= 0) sock_status(c, k, DS_READABLE, false);
+    }
+    return pi;
+}
+__device__ bool sock_add_output(L& c, DSock* k, int32_t pi) {   // socket.c:385-424
+    DPkt* p = PK(c, pi);
+    if (p->len > out_space(k)) return false;
+    if (p->prio == 0.0) rg_push(k->outctl, pi, c.H->err); else rg_push(k->out, pi, c.H->err);
+    k->out_len += p->len;
+    pkt_status(c, pi, S_SND_SOCKET_BUFFERED);
+    if (space_out_incl_tcp(k) <= 0) sock_status(c, k, DS_WRITABLE, false);
+    // networkinterface_wantsSend (network_interface.c:581-605): tracked once
+    if (ih_find(c.H->fifo, sidx(c, k)) < 0) ih_push(c.H->fifo, sidx(c, k), SockLess{&c}, c.H->err);
+    if_send_packets(c);
+    return true;
+}
+__device__ int32_t sock_remove_output(L& c, DSock* k) {   // socket.c:426-451
+    const int32_t pi = k->outctl.n ? rg_pop(k->outctl) : rg_pop(k->out);
+    if (pi >= 0) {
+        k->out_len -= PK(c, pi)->len;
+        if (k->out_pending > 0) set_out_size(k, k->out_pending);
+        if (space_out_incl_tcp(k) > 0) sock_status(c, k, DS_WRITABLE, true);
+    }
+    return pi;
+}
+
+// ------------------------------------------------------------ paths
+__device__ int32_t host_of_ip(const L& c, uint32_t ip) {
+    for (int32_t i = 0; i < c.g->H; i++) if (c.g->host[i].ip == ip) return i;
+    return -1;
+}
+__device__ void path(const L& c, int32_t a, int32_t b, double& lat, double& rel) {
+    lat = c.g->lat[(size_t)a * c.g->H + b];
+    rel = c.g->rel[(size_t)a * c.g->H + b];
+}
+
+// ------------------------------------------------------------ retransmit queue
+__device__ int rtx_find(const L& c, const DSock* k, uint32_t seq) {
+    for (uint32_t i = 0; i < k->nrtx; i++) if (PK(c, k->rtx[i])->seq == seq) return (int)i;
+    return -1;
+}
+__device__ void rtx_remove_at(DSock* k, uint32_t i) {
+    for (uint32_t j = i; j + 1 < k->nrtx; j++) k->rtx[j] = k->rtx[j + 1];
+    k->nrtx--;
+}
+__device__ void tcp_add_retransmit(L& c, DSock* k, int32_t pi) {   // tcp.c:854-873
+    DPkt* p = PK(c, pi);
+    if (rtx_find(c, k, p->seq) >= 0) return;
+    if (k->nrtx >= kQ) { c.H->err |= SHD_TCP_ERR_QUEUE; return; }
+    k->rtx[k->nrtx++] = pi;
+    pkt_ref(c, pi);
+    pkt_status(c, pi, S_SND_TCP_ENQUEUE_RETRANSMIT);
+    k->rtx_len += p->len;
+    if (space_out(k) == 0) sock_status(c, k, DS_WRITABLE, false);
+}
+__device__ void tcp_clear_retransmit(L& c, DSock* k, uint32_t seq) {   // tcp.c:876-897 (sequence order)
+    for (;;) {   // repeatedly take the lowest sequence below `seq`
+        int best = -1;
+        for (uint32_t i = 0; i < k->nrtx; i++) {
+            const uint32_t s = PK(c, k->rtx[i])->seq;
+            if (s < seq && (best < 0 || s < PK(c, k->rtx[best])->seq)) best = (int)i;
+        }
+        if (best < 0) break;
+        const int32_t pi = k->rtx[best];
+        k->rtx_len -= PK(c, pi)->len;
+        pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
+        rtx_remove_at(k, (uint32_t)best);
+        pkt_unref(c, pi);
+    }
+    if (space_out(k) > 0) sock_status(c, k, DS_WRITABLE, true);
+}
+__device__ void tcp_clear_retransmit_range(L& c, DSock* k, uint32_t begin, uint32_t end) {   // tcp.c:900-920
+    for (uint32_t sq = begin; sq < end; ++sq) {
+        const int at = rtx_find(c, k, sq);
+        if (at >= 0) {
+            const int32_t pi = k->rtx[at];
+            k->rtx_len -= PK(c, pi)->len;
+            pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
+            rtx_remove_at(k, (uint32_t)at);
+            pkt_unref(c, pi);
+        }
+    }
+    if (space_out(k) > 0) sock_status(c, k, DS_WRITABLE, true);
+}
+
+// ------------------------------------------------------------ the retransmit tally (tcp_retransmit_tally.cc)
+__device__ void rv_insert_at(RVec& v, uint32_t at, int64_t a, int64_t b, uint32_t& err) {
+    if (v.n >= kRanges) { err |= SHD_TCP_ERR_QUEUE; return; }
+    for (uint32_t j = v.n; j > at; j--) v.r[j] = v.r[j - 1];
+    v.r[at].a = a; v.r[at].b = b; v.n++;
+}
+__device__ void rv_push(RVec& v, int64_t a, int64_t b, uint32_t& err) { rv_insert_at(v, v.n, a, b, err); }
+__device__ __forceinline__ bool r_overlap(Rng64 x, Rng64 y) { return x.a < y.b && y.a < x.b; }
+__device__ __forceinline__ bool r_adj(Rng64 x, Rng64 y) { return x.b == y.a || y.b == x.a; }
+__device__ void ranges_insert(RVec& v, int64_t a, int64_t b, uint32_t& err) {   // cc:57-102
+    const Rng64 val = {a, b};
+    uint32_t first = v.n, it = 0;
+    for (; it < v.n && val.b >= v.r[it].a; ++it)
+        if (first == v.n && (r_overlap(v.r[it], val) || r_adj(v.r[it], val))) first = it;
+    const uint32_t second = it;
+    if (first == v.n) { rv_insert_at(v, second, a, b, err); return; }
+    Rng64& x = v.r[first];
+    if (val.a < x.a) x.a = val.a;
+    if (val.b > x.b) x.b = val.b;
+    for (uint32_t j = first + 1; j < second; j++) {
+        if (v.r[j].a < x.a) x.a = v.r[j].a;
+        if (v.r[j].b > x.b) x.b = v.r[j].b;
+    }
+    const uint32_t ne = second - (first + 1);
+    for (uint32_t j = second; j < v.n; j++) v.r[j - ne] = v.r[j];
+    v.n -= ne;
+}
+__device__ void ranges_subtract(const RVec& lhs, const RVec& rhs, RVec& out, uint32_t& err) {   // cc:104-175
+    out.n = 0;
+    if (rhs.n == 0) { for (uint32_t i = 0; i < lhs.n; i++) rv_push(out, lhs.r[i].a, lhs.r[i].b, err); return; }
+    if (lhs.n == 0) return;
+    uint32_t idx = 0, j = 0;
+    Rng64 cur = lhs.r[0];
+    while (idx < lhs.n && j < rhs.n) {
+        const Rng64 rj = rhs.r[j];
+        if (rj.b <= cur.a) {
+            ++j;
+        } else if (cur.b <= rj.a) {
+            rv_push(out, cur.a, cur.b, err);
+            ++idx;
+            if (idx < lhs.n) cur = lhs.r[idx];
+        } else {
+            Rng64 sub[2]; int ns = 0;
+            if (r_overlap(cur, rj)) {
+                if (cur.a < rj.a) { sub[ns].a = cur.a; sub[ns].b = rj.a; ns++; }
+                if (rj.b < cur.b) { sub[ns].a = rj.b; sub[ns].b = cur.b; ns++; }
+            } else {
+                sub[ns++] = cur;
+            }
+            if (ns == 2) rv_push(out, sub[0].a, sub[0].b, err);
+            if (ns >= 1) cur = sub[ns - 1];
+            else { ++idx; if (idx < lhs.n) cur = lhs.r[idx]; }
+        }
+    }
+    if (j == rhs.n) {
+        rv_push(out, cur.a, cur.b, err);
+        ++idx;
+        while (idx < lhs.n) { rv_push(out, lhs.r[idx].a, lhs.r[idx].b, err); idx++; }
+    }
+}
+__device__ void tally_compute_lost(Tally& t, uint32_t& err) {
+    ranges_subtract(t.marked, t.sacked, t.tmp, err);
+    ranges_subtract(t.tmp, t.retx, t.lost, err);
+}
+__device__ void tally_tidy(const Tally& t, RVec& v) {   // cc:316-335
+    if (v.n > 0 && t.last_ack >= v.r[0].a && t.last_ack < v.r[0].b - 1) {
+        v.r[0].a = t.last_ack;
+    } else if (v.n > 0 && t.last_ack >= v.r[0].b - 1) {
+        uint32_t k = 0;
+        for (uint32_t i = 0; i < v.n; i++) if (!(t.last_ack >= v.r[i].b)) v.r[k++] = v.r[i];
+        v.n = k;
+    }
+}
+__device__ uint32_t tally_update(Tally& t, uint32_t last_ack, bool is_dup, uint32_t& err) {   // cc:192-220
+    uint32_t ret = 0;
+    if (is_dup && (int64_t)last_ack == t.last_ack) {
+        ++t.ndup;
+    } else if ((int64_t)last_ack > t.last_ack) {
+        t.last_ack = last_ack;
+        t.ndup = 0;
+        tally_tidy(t, t.marked);
+        tally_tidy(t, t.sacked);
+        tally_tidy(t, t.retx);
+    }
+    bool contains = false;
+    for (uint32_t i = 0; i < t.retx.n; i++)
+        if (t.last_ack >= t.retx.r[i].a && t.last_ack < t.retx.r[i].b) contains = true;
+    if (t.ndup >= 3 && !contains) {
+        ranges_insert(t.marked, t.last_ack, t.last_ack + 1, err);
+        tally_compute_lost(t, err);
+        if (t.lost.n > 0) ret |= PF_DATA_LOST;
+    }
+    return ret;
+}
+__device__ void tally_mark_sacked(Tally& t, const int32_t* s, uint32_t n, uint32_t& err) {   // cc:224-245
+    int64_t first = -1;
+    for (uint32_t i = 0; i < n; i++) {
+        if (first == -1) first = s[i];
+        if (i + 1 == n || s[i + 1] != s[i] + 1) { ranges_insert(t.sacked, first, (int64_t)s[i] + 1, err); first = -1; }
+    }
+}
+
+// ------------------------------------------------------------ timers
+__device__ void tcp_schedule_rto(L& c, DSock* k, uint64_t now, uint64_t delay) {   // tcp.c:925-946
+    th_push(k->timers, now + delay, c.H->err);
+    sched_task(c, delay, K_RTO, sidx(c, k));
+}
+__device__ void tcp_schedule_rto_if_needed(L& c, DSock* k, uint64_t now) {   // tcp.c:948-960
+    if (k->timers.n && k->timers.a[0] <= k->desired) return;
+    tcp_schedule_rto(c, k, now, k->desired - now);
+}
+__device__ void tcp_set_rto_timer(L& c, DSock* k, uint64_t now) {   // tcp.c:962-971
+    k->desired = now + (uint64_t)k->rto * kMs;
+    tcp_schedule_rto_if_needed(c, k, now);
+}
+__device__ void tcp_set_rto(DSock* k, int v) {   // tcp.c:982-989
+    k->rto = v;
+    if (k->rto > 120000) k->rto = 120000;
+    if (k->rto < 200) k->rto = 200;
+}
+
+// ------------------------------------------------------------ Reno (tcp_cong_reno.c)
+__device__ void reno_new_ack(DSock* k, uint32_t n) {
+    if (k->reno_state == 0) {   // slow start (:65-89), into congestion avoidance with the leftover
+        k->reno_ndup = 0;
+        const uint32_t nc = k->cwnd + n;
+        if (nc < k->reno_ssthresh) { k->cwnd = nc; return; }
+        n = nc - k->reno_ssthresh;
+        k->cwnd = k->reno_ssthresh;
+        k->reno_nacked = 0;
+        k->reno_state = 2;
+    } else if (k->reno_state == 1) {   // fast recovery (:97-104)
+        k->reno_ndup = 0;
+        k->cwnd = k->reno_ssthresh;
+        k->reno_nacked = 0;
+        k->reno_state = 2;
+    }
+    k->reno_nacked += n;   // congestion avoidance (:108-118)
+    while (k->reno_nacked >= k->cwnd) { k->reno_nacked -= k->cwnd; k->cwnd += 1; }
+}
+__device__ void reno_dup_ack(DSock* k) {
+    if (k->reno_state == 1) { k->cwnd += 1; return; }
+    k->reno_ndup++;
+    if (k->reno_ndup == 3) { k->reno_ssthresh = (k->cwnd / 2) + 1; k->cwnd = k->reno_ssthresh + 3; k->reno_state = 1; }
+}
+__device__ void reno_timeout(DSock* k) {
+    k->reno_ndup = 0;
+    k->reno_ssthresh = (k->cwnd / 2) + 1;
+    k->cwnd = 10;
+    k->reno_state = 0;
+}
+
+// ------------------------------------------------------------ TCP
+__device__ int32_t sock_new(L& c) {   // host_createDescriptor + tcp_new (tcp.c:2452-2512)
+    DHost* H = c.H;
+    if (H->nsock >= kSock) { H->err |= SHD_TCP_ERR_SOCKETS; return -1; }
+    const int32_t si = c.h * kSock + H->nsock++;
+    DSock* k = &c.g->sock[si];
+    memset(k, 0, offsetof(DSock, in));
+    k->used = 1; k->host = c.h; k->proc = -1; k->parent = -1; k->partial = -1;
+    k->in.head = k->in.n = 0; k->out.head = k->out.n = 0; k->outctl.head = k->outctl.n = 0;
+    k->state = TS_CLOSED; k->state_last = 0; k->flags = 0; k->error = 0;
+    return si;
+}
+__device__ void sock_init_tcp(DSock* k, uint32_t recv_buf, uint32_t send_buf, uint32_t iw) {
+    k->in_size = recv_buf; k->out_size = send_buf;
+    k->r_winupd = 0; k->r_last_ts = 0; k->r_last_seq = 0; k->r_start = 1; k->r_next = 1; k->r_end = 1;
+    k->r_window = iw; k->r_last_window = iw; k->r_last_ack = 1;
+    k->s_unacked = 1; k->s_next = 1; k->s_end = 1; k->s_last_ack = 1; k->s_window = iw; k->s_last_window = iw;
+    k->s_highest = 0; k->s_packets_sent = 0; k->s_quick_acks = 0; k->s_delack_counter = 0; k->s_delack_sched = 0;
+    k->nsack = 0; k->nrtx = 0; k->rtx_len = 0; k->timers.n = 0; k->desired = 0; k->backoff = 0;
+    k->tally.last_ack = -1; k->tally.ndup = 0;
+    k->tally.marked.n = k->tally.sacked.n = k->tally.retx.n = k->tally.lost.n = k->tally.tmp.n = 0;
+    k->at_did_init = 0; k->at_bytes = 0; k->at_last_adjust = 0; k->at_space = 0;
+    k->cwnd = 1; k->reno_state = 0; k->reno_ndup = 0; k->reno_nacked = 0; k->reno_ssthresh = 0x7fffffffu;
+    k->srtt = 0; k->rttvar = 0; k->retx_count = 0; k->info_rtt = 0;
+    k->throttled.n = 0; k->throttled_len = 0; k->unordered.n = 0; k->unordered_len = 0;
+    k->partial = -1; k->partial_off = 0;
+    k->server = 0; k->nkids = 0; k->npending = 0; k->last_peer_ip = 0; k->last_ip = 0; k->last_peer_port = 0;
+    k->child = 0; k->parent = -1; k->child_state = 0;
+    tcp_set_rto(k, 1000);
+}
+__device__ uint32_t tcp_get_ip(const L& c, const DSock* k) {   // tcp.c:335-353
+    if (k->server) return k->bound ? k->bound_ip : k->last_ip;
+    if (k->child) { const DSock* pa = &c.g->sock[k->parent]; return pa->bound ? pa->bound_ip : pa->last_ip; }
+    return k->bound_ip;
+}
+__device__ uint32_t tcp_get_peer_ip(const DSock* k) {
+    uint32_t ip = k->peer_ip;
+    if (k->server && ip == 0) ip = k->last_peer_ip;
+    return ip;
+}
+__device__ uint32_t src_ip_for(const L& c, const DSock* k, uint32_t dst) {
+    uint32_t ip = tcp_get_ip(c, k);
+    if (ip == 0) ip = (dst == 0x7f000001u) ? 0x7f000001u : c.g->host[k->host].ip;
+    return ip;
+}
+__device__ void tcp_update_rcv_window(DSock* k) { k->r_window = (uint32_t)(in_space(k) / kMSS); }   // tcp.c:762-782
+__device__ void tcp_update_snd_window(DSock* k) {   // tcp.c:784-789
+    const int lw = (int)k->r_last_window;
+    k->s_window = (uint32_t)((int)k->cwnd < lw ? (int)k->cwnd : lw);
+}
+__device__ void tcp_set_state(L& c, DSock* k, int st);
+__device__ void tcp_tune_initial_buffers(L& c, DSock* k) {   // tcp.c:441-533
+    k->at_did_init = 1;
+    const uint32_t dip = tcp_get_peer_ip(k);
+    const uint32_t sip = src_ip_for(c, k, dip);
+    if (sip == dip) { set_in_size(k, 6291456); set_out_size(k, 4194304); k->info_rtt = 0xffffffffu; return; }
+    const int32_t a = host_of_ip(c, sip), b = host_of_ip(c, dip);
+    double l1, l2, r;
+    path(c, a, b, l1, r);   // _tcp_calculateRTT (tcp.c:363-405)
+    path(c, b, a, l2, r);
+    const uint32_t rtt = (uint32_t)ceil(l1) + (uint32_t)ceil(l2);
+    const DHost* A = &c.g->host[a];
+    const DHost* B = &c.g->host[b];
+    const uint32_t sbw = (uint32_t)A->bw_up < (uint32_t)B->bw_down ? (uint32_t)A->bw_up : (uint32_t)B->bw_down;
+    const uint32_t rbw = (uint32_t)A->bw_down < (uint32_t)B->bw_up ? (uint32_t)A->bw_down : (uint32_t)B->bw_up;
+    // float arithmetic as the reference writes it (tcp.c:504, 514)
+    uint64_t sendbuf = (uint64_t)(((float)(rtt * sbw) * 1024.0f * 1.25f) / 1000.0f);
+    uint64_t recvbuf = (uint64_t)(((float)(rtt * rbw) * 1024.0f * 1.25f) / 1000.0f);
+    sendbuf = sendbuf < 16384 ? 16384 : sendbuf > 4194304 ? 4194304 : sendbuf;
+    recvbuf = recvbuf < 87380 ? 87380 : recvbuf > 6291456 ? 6291456 : recvbuf;
+    set_in_size(k, recvbuf);
+    set_out_size(k, sendbuf);
+}
+__device__ uint64_t rtt_mem(const L& c, const DSock* k, bool rmem) {   // tcp.c:407-427
+    const DHost* H = &c.g->host[k->host];
+    const uint64_t refill = rmem ? H->rx_refill : H->tx_refill;
+    const uint64_t kib = (uint64_t)(uint32_t)((refill * 1000u) / 1024u);
+    const double rtt_s = ((double)k->srtt) / ((double)1000);
+    return (uint64_t)((double)(kib * 1024) * rtt_s);
+}
+__device__ __forceinline__ uint64_t clamp_u(uint64_t v, uint64_t lo, uint64_t hi) { return v < lo ? lo : v > hi ? hi : v; }
+__device__ void tcp_autotune_rcv(L& c, DSock* k, uint32_t copied) {   // tcp.c:535-564
+    k->at_bytes += copied;
+    uint64_t space = 2 * k->at_bytes;
+    if (k->at_space > space) space = k->at_space;
+    const uint64_t cur = in_size(k);
+    if (space > cur) {
+        k->at_space = space;
+        const uint64_t mx = clamp_u(rtt_mem(c, k, true), 6291456, 62914560);
+        const uint64_t nsz = space < mx ? space : mx;
+        if (nsz > cur) set_in_size(k, nsz);
+    }
+    if (k->at_last_adjust == 0) {
+        k->at_last_adjust = c.now;
+    } else if (k->srtt > 0) {
+        if (c.now - k->at_last_adjust > (uint64_t)k->srtt * kMs) { k->at_last_adjust = c.now; k->at_bytes = 0; }
+    }
+}
+__device__ void tcp_autotune_snd(L& c, DSock* k) {   // tcp.c:566-591
+    const uint64_t mx = clamp_u(rtt_mem(c, k, false), 4194304, 41943040);
+    uint64_t nsz = (uint64_t)2404 * 2 * (uint64_t)k->cwnd;
+    if (nsz > mx) nsz = mx;
+    if (nsz > out_size(k)) set_out_size(k, nsz);
+}
+__device__ void tcp_buffer_out(L& c, DSock* k, int32_t pi) {   // tcp.c:729-745
+    if (ih_find(k->throttled, pi) >= 0) return;
+    ih_push(k->throttled, pi, SeqLess{c.g->pool + (size_t)c.h * kPool}, c.H->err);
+    pkt_ref(c, pi);
+    k->throttled_len += PK(c, pi)->len;
+    if (space_out(k) == 0) sock_status(c, k, DS_WRITABLE, false);
+    pkt_status(c, pi, S_SND_TCP_ENQUEUE_THROTTLED);
+}
+__device__ void tcp_buffer_in(L& c, DSock* k, int32_t pi) {   // tcp.c:747-760
+    if (ih_find(k->unordered, pi) >= 0) return;
+    ih_push(k->unordered, pi, SeqLess{c.g->pool + (size_t)c.h * kPool}, c.H->err);
+    pkt_ref(c, pi);
+    k->unordered_len += PK(c, pi)->len;
+    pkt_status(c, pi, S_RCV_TCP_ENQUEUE_UNORDERED);
+}
+__device__ int32_t tcp_create_packet(L& c, DSock* k, uint32_t flags, uint32_t len) {   // tcp.c:791-835
+    const uint32_t dip = tcp_get_peer_ip(k);
+    const uint16_t sport = k->child ? c.g->sock[k->parent].bound_port : k->bound_port;
+    const uint16_t dport = k->server ? k->last_peer_port : k->peer_port;
+    const uint32_t sip = src_ip_for(c, k, dip);
+    tcp_update_rcv_window(k);
+    const bool fin_not_ack = (flags & F_FIN) && !(flags & F_ACK);
+    const uint32_t seq = (len > 0 || fin_not_ack) ? k->s_next : 0;
+    const int32_t pi = pkt_new(c, len);
+    if (pi < 0) return -1;
+    DPkt* p = PK(c, pi);
+    p->flags = flags; p->sip = sip; p->sport = sport; p->dip = dip; p->dport = dport; p->seq = seq;
+    pkt_status(c, pi, S_SND_CREATED);
+    if (seq > 0) k->s_next++;
+    return pi;
+}
+__device__ void tcp_retransmit_packet(L& c, DSock* k, uint32_t seq) {   // tcp.c:1027-1065
+    const int at = rtx_find(c, k, seq);
+    if (at < 0) return;
+    const int32_t pi = k->rtx[at];
+    rtx_remove_at(k, (uint32_t)at);
+    k->rtx_len -= PK(c, pi)->len;
+    pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
+    if (space_out(k) > 0) sock_status(c, k, DS_WRITABLE, true);
+    tcp_set_rto_timer(c, k, c.now);
+    tcp_buffer_out(c, k, pi);
+    pkt_status(c, pi, S_SND_TCP_RETRANSMITTED);
+    k->retx_count++;
+    pkt_unref(c, pi);
+}
+// tcp_networkInterfaceIsAboutToSendPacket (tcp.c:1090-1119)
+__device__ void tcp_about_to_send(L& c, DSock* k, int32_t pi) {
+    DPkt* p = PK(c, pi);
+    if (k->nsack > 0) {
+        if (k->nsack > kPktSack) c.H->err |= SHD_TCP_ERR_SACK;
+        p->flags |= F_SACK;
+        p->nsack = k->nsack < kPktSack ? k->nsack : kPktSack;
+        for (uint32_t i = 0; i < p->nsack; i++) p->sacks[i] = k->sacks[i];
+    }
+    p->ack = k->r_next;
+    p->win = k->r_window;
+    p->tsval = c.now;
+    p->tsecho = k->r_last_ts;
+    k->s_last_ack = k->r_next;
+    k->s_last_window = k->r_window;
+    if (p->flags & F_ACK) k->s_delack_counter = 0;
+    if (p->seq > 0 || (p->flags & F_SYN)) {
+        tcp_add_retransmit(c, k, pi);
+        if (!k->desired) tcp_set_rto_timer(c, k, c.now);
+    }
+}
+// _tcp_flush (tcp.c:1121-1278).  The FIN it may send flushes again; that
+// inner flush reaches its own FIN step in FINWAIT1 / LASTACK, where
+// _tcp_sendShutdownFin sends nothing, so the inner pass only clears the flag.
+__device__ void tcp_flush_body(L& c, DSock* k, bool outer);
+__device__ void tcp_send_shutdown_fin(L& c, DSock* k, bool from_flush) {   // tcp.c:1067-1088
+    bool send = false;
+    if (k->state == TS_ESTABLISHED || k->state == TS_SYNRECEIVED) { tcp_set_state(c, k, TS_FINWAIT1); send = true; }
+    else if (k->state == TS_CLOSEWAIT) { tcp_set_state(c, k, TS_LASTACK); send = true; }
+    if (send) {
+        const int32_t fin = tcp_create_packet(c, k, F_FIN, 0);
+        if (fin < 0) return;
+        tcp_buffer_out(c, k, fin);
+        tcp_flush_body(c, k, false);
+        pkt_unref(c, fin);
+    }
+}
+__device__ void tcp_flush_body(L& c, DSock* k, bool outer) {
+    tcp_update_rcv_window(k);
+    tcp_update_snd_window(k);
+    const uint32_t nl = k->tally.lost.n;
+    if (nl > 0) {
+        Rng64 lr[kRanges];
+        for (uint32_t i = 0; i < nl; i++) lr[i] = k->tally.lost.r[i];
+        for (uint32_t i = 0; i < nl; i++) {
+            for (uint32_t j = (uint32_t)lr[i].a; j < (uint32_t)lr[i].b; ++j) tcp_retransmit_packet(c, k, j);
+            ranges_insert(k->tally.retx, lr[i].a, lr[i].b, c.H->err);   // mark_retransmitted (cc:257-263)
+            tally_compute_lost(k->tally, c.H->err);
+        }
+    }
+    const SeqLess lt{c.g->pool + (size_t)c.h * kPool};
+    while (k->throttled.n) {
+        const int32_t pi = k->throttled.a[0];
+        DPkt* p = PK(c, pi);
+        const uint32_t len = p->len;
+        if (len > 0) {
+            const bool in_window = p->seq < (uint32_t)(k->s_unacked + k->s_window);
+            const bool in_buffer = len <= out_space(k);
+            if (!in_buffer || !in_window) break;
+        }
+        ih_pop(k->throttled, lt);
+        k->throttled_len -= len;
+        sock_add_output(c, k, pi);
+        k->s_packets_sent++;
+        if (p->seq > k->s_highest) k->s_highest = p->seq;
+    }
+    while (k->unordered.n) {
+        const int32_t pi = k->unordered.a[0];
+        DPkt* p = PK(c, pi);
+        if (p->seq == k->r_next && sock_add_input(c, k, pi)) {
+            k->r_last_seq = p->seq;
+            ih_pop(k->unordered, lt);
+            const uint32_t len = p->len;
+            pkt_unref(c, pi);
+            k->unordered_len -= len;
+            k->r_next++;
+            continue;
+        }
+        break;
+    }
+    if ((k->flags & TF_SHOULD_SEND_WR_FIN) && tcp_out_len(k) == 0) {
+        if (outer) tcp_send_shutdown_fin(c, k, true);
+        k->flags &= ~TF_SHOULD_SEND_WR_FIN;
+    }
+    if ((k->flags & TF_LOCAL_CLOSED_WR) || (k->error & TE_CONNECTION_RESET)) k->error |= TE_SEND_EOF;
+    if ((k->flags & TF_LOCAL_CLOSED_RD) || (k->flags & TF_REMOTE_CLOSED) || (k->error & TE_CONNECTION_RESET)) {
+        if (k->r_next >= k->r_end && !(k->flags & TF_EOF_RD_SIGNALED)) {
+            k->error |= TE_RECEIVE_EOF;
+            sock_status(c, k, DS_READABLE, true);
+        }
+    }
+    if ((k->error & TE_CONNECTION_RESET) && (k->flags & TF_RESET_SIGNALED)) sock_status(c, k, DS_WRITABLE, false);
+    else if ((k->error & TE_SEND_EOF) && (k->flags & TF_EOF_WR_SIGNALED)) sock_status(c, k, DS_WRITABLE, false);
+    else if (space_out(k) <= 0) sock_status(c, k, DS_WRITABLE, false);
+    else sock_status(c, k, DS_WRITABLE, true);
+}
+__device__ __forceinline__ void tcp_flush(L& c, DSock* k) { tcp_flush_body(c, k, true); }
+__device__ void tcp_send_control(L& c, DSock* k, uint32_t flags) {   // tcp.c:837-852
+    const int32_t ci = tcp_create_packet(c, k, flags, 0);
+    if (ci < 0) return;
+    PK(c, ci)->prio = 0.0;
+    tcp_buffer_out(c, k, ci);
+    tcp_flush(c, k);
+    pkt_unref(c, ci);
+}
+__device__ void tcp_set_state(L& c, DSock* k, int st) {   // tcp.c:607-693
+    k->state_last = k->state;
+    k->state = st;
+    if (st == TS_LISTEN) {
+        sock_status(c, k, DS_ACTIVE, true);
+    } else if (st == TS_ESTABLISHED) {
+        k->flags |= TF_WAS_ESTABLISHED;
+        sock_status(c, k, DS_ACTIVE | DS_WRITABLE, true);
+    } else if (st == TS_CLOSED) {
+        tcp_clear_retransmit(c, k, 0xffffffffu);
+        sock_status(c, k, DS_ACTIVE, false);
+        if (!k->server || k->nkids == 0) {
+            if (k->child && k->parent >= 0) {
+                DSock* pa = &c.g->sock[k->parent];
+                for (uint32_t i = 0; i < pa->nkids; i++)
+                    if (pa->kids[i] == sidx(c, k)) { pa->kids[i] = pa->kids[--pa->nkids]; break; }
+                if (pa->state == TS_CLOSED && pa->nkids == 0) { pa->assoc = 0; pa->assoc_general = 0; }
+            }
+            k->assoc = 0;   // host_closeDescriptor: _host_disassociateInterface
+            k->assoc_general = 0;
+        }
+    } else if (st == TS_TIMEWAIT) {
+        const uint64_t delay = (k->child && k->parent >= 0) ? kSec : 60 * kSec;   // CONFIG_TCPCLOSETIMER_DELAY
+        sched_task(c, delay, K_CLOSE, sidx(c, k));
+    }
+}
+__device__ void tcp_update_rtt(L& c, DSock* k, uint64_t ts) {   // tcp.c:991-1025
+    int rtt = (int)((c.now - ts) / kMs);
+    if (rtt <= 0) rtt = 1;
+    if (!k->srtt) {
+        k->srtt = rtt;
+        k->rttvar = rtt / 2;
+        if (!k->at_did_init) tcp_tune_initial_buffers(c, k);
+    } else {
+        k->rttvar = (3 * k->rttvar / 4) + (abs(k->srtt - rtt) / 4);
+        k->srtt = (7 * k->srtt / 8) + (rtt / 8);
+    }
+    tcp_set_rto(k, k->srtt + 4 * k->rttvar);
+}
+__device__ uint32_t tcp_data_processing(L& c, DSock* k, int32_t pi) {   // tcp.c:1597-1660
+    DPkt* p = PK(c, pi);
+    uint32_t fl = 0;
+    if (p->seq >= k->r_next + k->r_window) {
+        fl |= PF_PROCESSED;
+        pkt_status(c, pi, S_RCV_SOCKET_DROPPED);
+    } else if (p->seq >= k->r_next) {
+        fl |= PF_PROCESSED;
+        const bool is_next = p->seq == k->r_next;
+        const bool fits = p->len <= space_in(k);
+        if (!is_next && fits) {
+            if (k->nsack >= kSacks) c.H->err |= SHD_TCP_ERR_SACK;
+            else k->sacks[k->nsack++] = (int32_t)p->seq;
+        } else if (k->nsack > 0) {
+            uint32_t it = 0;
+            if (k->sacks[0] <= (int32_t)p->seq + 1) {
+                uint32_t nx = 1;
+                while (nx < k->nsack) {
+                    const int32_t cur = k->sacks[it], nxt = k->sacks[nx];
+                    if (cur + 1 < nxt && cur > (int32_t)p->seq) break;
+                    it = nx;
+                    nx = it + 1;
+                }
+                const int32_t cut = k->sacks[it];   // _tcp_removeSacks (tcp.c:1579-1595)
+                uint32_t w = 0;
+                for (uint32_t i = 0; i < k->nsack; i++) if (k->sacks[i] > cut) k->sacks[w++] = k->sacks[i];
+                k->nsack = w;
+            }
+        }
+        const bool waiting_read = (k->status & DS_READABLE) != 0;
+        if ((is_next && !waiting_read) || fits) {
+            tcp_buffer_in(c, k, pi);
+            fl |= PF_DATA_RECEIVED;
+        } else {
+            pkt_status(c, pi, S_RCV_SOCKET_DROPPED);
+        }
+    }
+    return fl;
+}
+__device__ uint32_t tcp_ack_processing(L& c, DSock* k, int32_t pi) {   // tcp.c:1662-1750
+    DPkt* p = PK(c, pi);
+    uint32_t fl = PF_PROCESSED;
+    const uint32_t prev_win = k->r_last_window;
+    const bool valid_ack = p->ack > k->s_unacked && p->ack <= k->s_next;
+    const bool valid_win = (p->ack == k->r_last_ack && p->win > prev_win) || (p->ack > k->r_last_ack && p->win != prev_win);
+    if (p->win != prev_win) fl |= PF_RWND_UPDATED;
+    const bool is_dup = (p->flags & F_DUPACK) != 0;
+    fl |= tally_update(k->tally, p->ack, is_dup, c.H->err);
+    if (is_dup) reno_dup_ack(k);
+    int n_acked = 0;
+    if (valid_ack) {
+        tcp_clear_retransmit_range(c, k, k->r_last_ack, p->ack);
+        k->r_last_ack = p->ack;
+        n_acked = (int)(p->ack - k->s_unacked);
+        k->s_unacked = p->ack;
+        if (n_acked > 0) {
+            fl |= PF_DATA_ACKED;
+            reno_new_ack(k, (uint32_t)n_acked);
+            tcp_autotune_snd(c, k);
+        }
+        if (k->backoff > 2) { k->srtt = 0; k->rttvar = 0; tcp_set_rto(k, 1000); }
+        k->backoff = 0;
+    }
+    if (valid_win) k->r_last_window = p->win;
+    if (k->rtx_len == 0) k->desired = 0;
+    else if (n_acked > 0) tcp_set_rto_timer(c, k, c.now);
+    return fl;
+}
+__device__ void tcp_process(L& c, DSock* k, int32_t pi) {   // tcp.c:1777-2099
+    DPkt* p = PK(c, pi);
+    if (k->server) {   // _tcp_getSourceTCP: a child keyed by the peer's ip:port
+        for (uint32_t i = 0; i < k->nkids; i++) {
+            DSock* ch = &c.g->sock[k->kids[i]];
+            if (ch->peer_ip == p->sip && ch->peer_port == p->sport) { k = ch; break; }
+        }
+    }
+    if (p->flags & F_RST) {
+        if (!(k->state & TS_LISTEN) && !(k->error & TE_CONNECTION_RESET)) {
+            k->error |= TE_CONNECTION_RESET;
+            k->flags |= TF_REMOTE_CLOSED;
+            tcp_set_state(c, k, TS_TIMEWAIT);
+            k->r_end = k->r_next;
+        }
+        return;
+    }
+    if (k->server) { k->last_peer_ip = p->sip; k->last_peer_port = p->sport; k->last_ip = p->dip; }
+    uint32_t fl = 0, resp = 0;
+    switch (k->state) {
+    case TS_LISTEN:
+        if (p->flags & F_SYN) {
+            fl |= PF_PROCESSED;
+            const int32_t ci = sock_new(c);   // a multiplexed child (tcp.c:1824-1853)
+            if (ci < 0) return;
+            DSock* ch = &c.g->sock[ci];
+            sock_init_tcp(ch, c.g->recv_buf, c.g->send_buf, c.g->tcp_window);
+            ch->child = 1;
+            ch->parent = sidx(c, k);
+            ch->child_state = 1;
+            ch->peer_ip = p->sip; ch->peer_port = p->sport;
+            ch->bound = 1; ch->bound_ip = k->bound_ip; ch->bound_port = k->bound_port;
+            if (k->nkids >= kKids) { c.H->err |= SHD_TCP_ERR_SOCKETS; return; }
+            k->kids[k->nkids++] = ci;
+            ch->r_start = p->seq;
+            ch->r_next = ch->r_start + 1;
+            tcp_set_state(c, ch, TS_SYNRECEIVED);
+            k = ch;
+            resp = F_SYN | F_ACK;
+        }
+        break;
+    case TS_SYNSENT:
+        if ((p->flags & F_SYN) && (p->flags & F_ACK)) {
+            fl |= PF_PROCESSED;
+            k->r_start = p->seq;
+            k->r_next = k->r_start + 1;
+            resp |= F_ACK;
+            tcp_set_state(c, k, TS_ESTABLISHED);
+            tcp_clear_retransmit(c, k, 1);
+        } else if (p->flags & F_SYN) {
+            fl |= PF_PROCESSED;
+            k->r_start = p->seq;
+            k->r_next = k->r_start + 1;
+            resp |= F_ACK;
+            tcp_set_state(c, k, TS_SYNRECEIVED);
+        }
+        break;
+    case TS_SYNRECEIVED:
+        if (p->flags & F_ACK) {
+            fl |= PF_PROCESSED;
+            tcp_set_state(c, k, TS_ESTABLISHED);
+            tcp_clear_retransmit(c, k, 1);
+            if (k->child) {
+                k->child_state = 2;
+                DSock* pa = &c.g->sock[k->parent];
+                if (pa->npending >= kKids) { c.H->err |= SHD_TCP_ERR_SOCKETS; return; }
+                pa->pending[pa->npending++] = sidx(c, k);
+                sock_status(c, pa, DS_READABLE, true);
+            }
+        }
+        break;
+    case TS_ESTABLISHED:
+        if (p->flags & F_FIN) {
+            fl |= PF_PROCESSED;
+            k->flags |= TF_REMOTE_CLOSED;
+            resp |= F_FIN | F_ACK;
+            tcp_set_state(c, k, TS_CLOSEWAIT);
+            k->r_end = p->seq;
+        }
+        break;
+    case TS_FINWAIT1:
+        if ((p->flags & F_FIN) && (p->flags & F_ACK)) {
+            fl |= PF_PROCESSED;
+            tcp_set_state(c, k, TS_FINWAIT2);
+        } else if (p->flags & F_FIN) {
+            fl |= PF_PROCESSED;
+            resp |= F_FIN | F_ACK;
+            k->flags |= TF_REMOTE_CLOSED;
+            tcp_set_state(c, k, TS_CLOSING);
+            k->r_end = p->seq;
+        }
+        break;
+    case TS_FINWAIT2:
+        if (p->flags & F_FIN) {
+            fl |= PF_PROCESSED;
+            resp |= F_FIN | F_ACK;
+            k->flags |= TF_REMOTE_CLOSED;
+            tcp_set_state(c, k, TS_TIMEWAIT);
+            k->r_end = p->seq;
+        }
+        break;
+    case TS_CLOSING:
+        if ((p->flags & F_FIN) && (p->flags & F_ACK)) { fl |= PF_PROCESSED; tcp_set_state(c, k, TS_TIMEWAIT); }
+        break;
+    case TS_TIMEWAIT:
+    case TS_CLOSEWAIT:
+        break;
+    case TS_LASTACK:
+        if ((p->flags & F_FIN) && (p->flags & F_ACK)) { fl |= PF_PROCESSED; tcp_set_state(c, k, TS_CLOSED); return; }
+        break;
+    default:
+        pkt_status(c, pi, S_RCV_SOCKET_DROPPED);
+        return;
+    }
+    if (k->state == TS_LISTEN) {
+        if (!(fl & PF_PROCESSED)) pkt_status(c, pi, S_RCV_SOCKET_DROPPED);
+        return;
+    }
+    if (p->len > 0 && !(k->error & TE_RECEIVE_EOF)) fl |= tcp_data_processing(c, k, pi);
+    if (p->flags & F_ACK) fl |= tcp_ack_processing(c, k, pi);
+    if (!(fl & PF_PROCESSED)) { pkt_status(c, pi, S_RCV_SOCKET_DROPPED); return; }
+    if (p->nsack) tally_mark_sacked(k->tally, p->sacks, p->nsack, c.H->err);
+    k->r_last_ts = p->tsval;
+    if (p->tsecho && k->backoff == 0) tcp_update_rtt(c, k, p->tsecho);
+    if (p->seq > k->r_next && p->seq < k->r_next + k->r_window) resp |= (F_ACK | F_DUPACK);
+    else if (fl & PF_DATA_RECEIVED) resp |= F_ACK;
+    if (resp != 0 && (!(k->error & TE_RECEIVE_EOF) || (resp & F_FIN))) {
+        if (resp != F_ACK) {
+            tcp_send_control(c, k, resp);
+        } else {
+            if (!k->s_delack_sched) {   // a delayed ACK task (tcp.c:2066-2089)
+                uint64_t delay;
+                if (k->s_quick_acks < 1000) { delay = kMs; k->s_quick_acks++; } else delay = 5 * kMs;
+                sched_task(c, delay, K_DELACK, sidx(c, k));
+                k->s_delack_sched = 1;
+            }
+            k->s_delack_counter++;
+        }
+    }
+    tcp_flush(c, k);
+    k->r_last_ts = 0;
+}
+
+// ------------------------------------------------------------ the interface (network_interface.c)
+__device__ void refill_if_needed(L& c) {   // :130-161, started at t = 0
+    DHost* H = c.H;
+    if (((H->tx_rem < H->tx_cap) || (H->rx_rem < H->rx_cap)) && !H->refill_pending) {
+        sched_task(c, kMs - (c.now % kMs), K_REFILL, -1);
+        H->refill_pending = 1;
+    }
+}
+__device__ __forceinline__ void consume(uint64_t& rem, uint64_t n) { rem = (n >= rem) ? 0 : rem - n; }
+__device__ DSock* lookup_socket(L& c, uint16_t port, uint32_t peer_ip, uint16_t peer_port) {   // :385-403
+    for (int32_t j = 0; j < c.H->nsock; j++) {
+        DSock* k = &c.g->sock[c.h * kSock + j];
+        if (k->assoc && k->assoc_general && k->bound_port == port) return k;
+    }
+    for (int32_t j = 0; j < c.H->nsock; j++) {
+        DSock* k = &c.g->sock[c.h * kSock + j];
+        if (k->assoc && !k->assoc_general && k->bound_port == port && k->peer_ip == peer_ip && k->peer_port == peer_port)
+            return k;
+    }
+    return nullptr;
+}
+// CoDel (router_queue_codel.c:148-267)
+constexpr uint64_t kCodelTarget = 10 * kMs, kCodelInterval = 100 * kMs;
+__device__ bool cq_helper(L& c, bool& ok, CqEnt& out) {
+    DHost* H = c.H;
+    ok = false;
+    if (H->cq_n == 0) { H->cq_iexp = 0; return false; }
+    out = c.g->cq[(size_t)c.h * kCq + H->cq_head];
+    H->cq_head = (H->cq_head + 1) % kCq;
+    H->cq_n--;
+    H->cq_total -= out.len;
+    const uint64_t sojourn = c.now - out.ts;
+    if (sojourn < kCodelTarget || H->cq_total < kMTU) {
+        H->cq_iexp = 0;
+    } else {
+        if (H->cq_iexp == 0) H->cq_iexp = c.now + kCodelInterval;
+        else if (c.now >= H->cq_iexp) ok = true;
+    }
+    return true;
+}
+__device__ uint64_t cq_law(uint32_t count, uint64_t ts) {
+    return (uint64_t)round(((double)(ts + kCodelInterval)) / sqrt((double)count));
+}
+__device__ void cq_drop(L& c, const CqEnt& e) {
+    pkt_status(c, e.pkt, S_ROUTER_DROPPED);
+    pkt_unref(c, e.pkt);
+}
+__device__ bool cq_dequeue(L& c, CqEnt& out) {
+    DHost* H = c.H;
+    bool ok = false;
+    CqEnt e;
+    bool have = cq_helper(c, ok, e);
+    if (!have) { H->cq_mode = 0; return false; }
+    if (H->cq_mode) {
+        if (!ok) H->cq_mode = 0;
+        while (c.now >= H->cq_next_drop && H->cq_mode) {
+            cq_drop(c, e);
+            H->cq_dc++;
+            have = cq_helper(c, ok, e);
+            if (ok) H->cq_next_drop = cq_law(H->cq_dc, H->cq_next_drop);
+            else H->cq_mode = 0;
+        }
+    } else if (ok) {
+        cq_drop(c, e);
+        have = cq_helper(c, ok, e);
+        H->cq_mode = 1;
+        const uint32_t delta = H->cq_dc - H->cq_dc_last;
+        H->cq_dc = 1;
+        const bool recent = c.now < H->cq_next_drop + 16 * kCodelInterval;
+        if (recent && delta > 1) H->cq_dc = delta;
+        H->cq_next_drop = cq_law(H->cq_dc, c.now);
+        H->cq_dc_last = H->cq_dc;
+    }
+    if (!have) return false;
+    out = e;
+    return true;
+}
+__device__ void if_receive_packets(L& c) {   // :421-455
+    DHost* H = c.H;
+    while (H->rx_rem >= kMTU) {
+        CqEnt e;
+        if (!cq_dequeue(c, e)) break;
+        pkt_status(c, e.pkt, S_ROUTER_DEQUEUED);
+        DPkt* p = PK(c, e.pkt);
+        const uint64_t len = (uint64_t)p->len + kHdr;
+        pkt_status(c, e.pkt, S_RCV_INTERFACE_RECEIVED);   // _networkinterface_receivePacket (:375-419)
+        DSock* k = lookup_socket(c, p->dport, p->sip, p->sport);
+        if (k) {
+            pkt_status(c, e.pkt, S_RCV_SOCKET_PROCESSED);   // socket_pushInPacket
+            tcp_process(c, k, e.pkt);
+        } else {
+            pkt_status(c, e.pkt, S_RCV_INTERFACE_DROPPED);
+        }
+        pkt_unref(c, e.pkt);
+        consume(H->rx_rem, len);
+        refill_if_needed(c);
+    }
+}
+__device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
+    DPkt* p = PK(c, pi);
+    const int32_t d = host_of_ip(c, p->dip);
+    double lat, rel;
+    path(c, c.h, d, lat, rel);
+    const double chance = next_double(&c.H->rng);
+    if (chance <= rel || p->len == 0) {
+        const uint64_t t = c.now + (uint64_t)ceil(lat * (double)kMs);
+        pkt_status(c, pi, S_INET_SENT);
+        const uint64_t seq = c.H->ev_seq++;   // event_new_ (the delivery's ID)
+        if (t >= c.g->end_time) return;
+        if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
+        const uint32_t slot = atomicAdd(c.g->n_out, 1u);
+        if (slot >= kMail) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+        Mail* m = &c.g->mail_out[slot];
+        m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
+        m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
+        m->pkt.refs = 1;
+        atomicMin((unsigned long long*)&c.g->next_time[c.g->H], (unsigned long long)t);
+    } else {
+        pkt_status(c, pi, S_INET_DROPPED);
+    }
+}
+__device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
+    DHost* H = c.H;
+    const SockLess lt{&c};
+    while (H->tx_rem >= kMTU) {
+        int32_t pi = -1;
+        while (pi < 0 && H->fifo.n) {   // _networkinterface_selectFirstInFirstOut (:492-517)
+            const int32_t si = ih_pop(H->fifo, lt);
+            DSock* k = &c.g->sock[si];
+            pi = sock_remove_output(c, k);
+            if (pi >= 0) tcp_about_to_send(c, k, pi);
+            if (sock_peek_out(c, k) >= 0) ih_push(H->fifo, si, lt, H->err);
+        }
+        if (pi < 0) break;
+        pkt_status(c, pi, S_SND_INTERFACE_SENT);
+        worker_send_packet(c, pi);
+        consume(H->tx_rem, (uint64_t)PK(c, pi)->len + kHdr);
+        refill_if_needed(c);
+        pkt_unref(c, pi);
+    }
+}
+__device__ void refill_cb(L& c) {   // :163-183
+    DHost* H = c.H;
+    H->refill_pending = 0;
+    H->rx_rem += H->rx_refill; if (H->rx_rem > H->rx_cap) H->rx_rem = H->rx_cap;
+    H->tx_rem += H->tx_refill; if (H->tx_rem > H->tx_cap) H->tx_rem = H->tx_cap;
+    if_receive_packets(c);
+    if_send_packets(c);
+    refill_if_needed(c);
+}
+
+// ------------------------------------------------------------ host calls (host.c)
+__device__ uint16_t random_port(L& c) {   // :1058-1070
+    const double f = next_double(&c.H->rng);
+    const double pick = round(f * (double)(65535 - 10000));
+    return (uint16_t)((uint16_t)pick + 10000);
+}
+__device__ bool port_free(L& c, uint16_t port) {
+    for (int32_t j = 0; j < c.H->nsock; j++) {
+        const DSock* k = &c.g->sock[c.h * kSock + j];
+        if (k->assoc && k->bound_port == port) return false;
+    }
+    return true;
+}
+__device__ uint16_t random_free_port(L& c) {   // :1072-1110
+    for (int i = 0; i < 10; i++) { const uint16_t p = random_port(c); if (port_free(c, p)) return p; }
+    const uint16_t start = random_port(c);
+    uint16_t next = start == 65535 ? 10000 : (uint16_t)(start + 1);
+    while (next != start) { if (port_free(c, next)) return next; next = next == 65535 ? 10000 : (uint16_t)(next + 1); }
+    return 0;
+}
+__device__ int tcp_connect_error(DSock* k) {   // tcp.c:1367-1390
+    if (k->error & TE_CONNECTION_RESET) {
+        k->flags |= TF_RESET_SIGNALED;
+        return (k->flags & TF_WAS_ESTABLISHED) ? E_CONNRESET : E_CONNREFUSED;
+    }
+    if (k->state == TS_SYNSENT || k->state == TS_SYNRECEIVED) return E_ALREADY;
+    if ((k->flags & TF_EOF_RD_SIGNALED) && (k->flags & TF_EOF_WR_SIGNALED)) return E_NOTCONN;
+    if (k->state != TS_CLOSED) return E_ISCONN;
+    return 0;
+}
+__device__ void tcp_eof_signalled(L& c, DSock* k, uint32_t f) {   // tcp.c:2113-2124
+    k->flags |= f;
+    if ((k->flags & TF_EOF_RD_SIGNALED) && (k->flags & TF_EOF_WR_SIGNALED)) {
+        sock_status(c, k, DS_CLOSED, true);
+        sock_status(c, k, DS_ACTIVE, false);
+    }
+}
+__device__ int host_send(L& c, DSock* k, uint64_t n, uint64_t& copied) {   // host.c:1466-1555, tcp.c:2126-2178
+    if (k->status & DS_CLOSED) return 9;
+    const int err = tcp_connect_error(k);
+    if (err != E_ISCONN) {
+        if (err == E_ALREADY) { sock_status(c, k, DS_WRITABLE, false); return E_WOULDBLOCK; }
+        return err;
+    }
+    if (k->error & TE_SEND_EOF) {
+        if (k->flags & TF_EOF_WR_SIGNALED) return E_NOTCONN;
+        tcp_eof_signalled(c, k, TF_EOF_WR_SIGNALED);
+        return E_PIPE;
+    }
+    const uint64_t acceptable = n < 65535 ? n : 65535;
+    const uint64_t space = space_out(k);
+    uint64_t remaining = acceptable < space ? acceptable : space, done = 0;
+    while (remaining > 0) {
+        const uint64_t cl = remaining < kMSS ? remaining : kMSS;
+        const int32_t pi = tcp_create_packet(c, k, F_ACK, (uint32_t)cl);
+        if (pi < 0) return E_WOULDBLOCK;
+        if (cl > 0) k->s_end++;
+        tcp_buffer_out(c, k, pi);
+        pkt_unref(c, pi);
+        remaining -= cl;
+        done += cl;
+    }
+    tcp_flush(c, k);
+    if (done == 0) return E_WOULDBLOCK;
+    copied = done;
+    return 0;
+}
+__device__ int host_receive(L& c, DSock* k, uint64_t n, uint64_t& copied) {   // host.c:1557-1604, tcp.c:2192-2327
+    tcp_flush(c, k);
+    uint64_t remaining = n, total = 0;
+    if (remaining > 0 && k->partial >= 0) {
+        const uint32_t pb = PK(c, k->partial)->len - k->partial_off;
+        const uint64_t cl = pb < remaining ? pb : remaining;
+        total += cl; remaining -= cl;
+        if (cl >= pb) {
+            pkt_status(c, k->partial, S_RCV_SOCKET_DELIVERED);
+            pkt_unref(c, k->partial);
+            k->partial = -1;
+            k->partial_off = 0;
+        } else {
+            k->partial_off += (uint32_t)cl;
+        }
+    }
+    while (remaining > 0) {
+        const int32_t pi = sock_remove_input(c, k);
+        if (pi < 0) break;
+        const uint32_t plen = PK(c, pi)->len;
+        const uint64_t cl = plen < remaining ? plen : remaining;
+        total += cl; remaining -= cl;
+        if (cl < plen) { k->partial = pi; k->partial_off = (uint32_t)cl; break; }
+        pkt_status(c, pi, S_RCV_SOCKET_DELIVERED);
+        pkt_unref(c, pi);
+    }
+    if (k->in_len > 0 || k->partial >= 0) {
+        sock_status(c, k, DS_READABLE, true);
+    } else if (k->unordered_len == 0 && (k->error & TE_RECEIVE_EOF)) {
+        if (total > 0) {
+            sock_status(c, k, DS_READABLE, true);
+        } else {
+            if (k->flags & TF_EOF_RD_SIGNALED) return E_NOTCONN;
+            tcp_eof_signalled(c, k, TF_EOF_RD_SIGNALED);
+            copied = 0;
+            return 0;
+        }
+    } else {
+        sock_status(c, k, DS_READABLE, false);
+    }
+    tcp_autotune_rcv(c, k, (uint32_t)total);
+    tcp_update_rcv_window(k);
+    if (k->r_window > k->s_last_window && !k->r_winupd) {
+        sched_task(c, 1, K_WINUPD, sidx(c, k));
+        k->r_winupd = 1;
+    }
+    if (total == 0) return E_WOULDBLOCK;
+    copied = total;
+    return 0;
+}
+__device__ void tcp_close(L& c, DSock* k) {   // descriptor_close + tcp_close (tcp.c:2363-2408)
+    sock_status(c, k, DS_CLOSED, true);
+    k->flags |= TF_LOCAL_CLOSED_WR | TF_LOCAL_CLOSED_RD;
+    sock_status(c, k, DS_ACTIVE, false);
+    switch (k->state) {
+    case TS_LISTEN:
+    case TS_SYNSENT: tcp_set_state(c, k, TS_CLOSED); return;
+    case TS_SYNRECEIVED:
+    case TS_ESTABLISHED:
+    case TS_CLOSEWAIT:
+        if (tcp_out_len(k) == 0) tcp_send_shutdown_fin(c, k, false);
+        else k->flags |= TF_SHOULD_SEND_WR_FIN;
+        return;
+    case TS_FINWAIT1: case TS_FINWAIT2: case TS_CLOSING: case TS_TIMEWAIT: case TS_LASTACK: return;
+    default: tcp_set_state(c, k, TS_CLOSED); return;
+    }
+}
+
+// ------------------------------------------------------------ the echo application (test_tcp.c:713-810)
+__device__ void app_wait(L& c, DProc* pr, int32_t fd, uint32_t events) {   // epoll_ctl ADD (epoll.c:411-433)
+    pr->wait_fd = fd;
+    pr->wait_events = events;
+    c.g->sock[fd].proc = pr->index;
+    ep_status_changed(c, pr);
+}
+__device__ void app_run(L& c, DProc* pr) {
+    const uint32_t N = c.g->tcp_bytes;
+    for (int guard = 0; guard < 64; guard++) {
+        switch (pr->step) {
+        case T_SRV_START: {
+            const int32_t li = sock_new(c);
+            if (li < 0) { pr->step = T_DONE; return; }
+            DSock* l = &c.g->sock[li];
+            sock_init_tcp(l, c.g->recv_buf, c.g->send_buf, c.g->tcp_window);
+            pr->listenfd = li;
+            l->bound = 1; l->bound_ip = 0; l->bound_port = random_free_port(c);   // bind INADDR_ANY:0
+            l->assoc = 1; l->assoc_general = 1;
+            l->server = 1;   // listen (tcp.c:1486-1494)
+            tcp_set_state(c, l, TS_LISTEN);
+            pr->step = T_SRV_ACCEPT;
+            break;
+        }
+        case T_SRV_ACCEPT: {   // tcp_acceptServerPeer (tcp.c:1496-1558)
+            DSock* l = &c.g->sock[pr->listenfd];
+            if (l->npending == 0) {
+                sock_status(c, l, DS_READABLE, false);
+                app_wait(c, pr, pr->listenfd, 1);
+                return;
+            }
+            const int32_t ci = l->pending[0];
+            for (uint32_t i = 1; i < l->npending; i++) l->pending[i - 1] = l->pending[i];
+            l->npending--;
+            DSock* ch = &c.g->sock[ci];
+            ch->child_state = 3;
+            sock_status(c, ch, DS_ACTIVE | DS_WRITABLE, true);
+            sock_status(c, l, DS_READABLE, l->npending > 0);
+            pr->fd = ci;
+            pr->done = 0;
+            pr->step = T_SRV_RECV;
+            break;
+        }
+        case T_SRV_RECV:
+        case T_CLI_RECV: {
+            while (pr->done < N) {
+                uint64_t n = 0;
+                const int rc = host_receive(c, &c.g->sock[pr->fd], N - pr->done, n);
+                if (rc == E_WOULDBLOCK) { app_wait(c, pr, pr->fd, 1); return; }
+                if (rc != 0 || n == 0) break;
+                pr->done += (uint32_t)n;
+            }
+            if (pr->step == T_SRV_RECV) { pr->done = 0; pr->step = T_SRV_SEND; }
+            else { tcp_close(c, &c.g->sock[pr->fd]); pr->step = T_DONE; }
+            break;
+        }
+        case T_SRV_SEND:
+        case T_CLI_SEND: {
+            while (pr->done < N) {
+                uint64_t n = 0;
+                const int rc = host_send(c, &c.g->sock[pr->fd], N - pr->done, n);
+                if (rc == E_WOULDBLOCK) { app_wait(c, pr, pr->fd, 4); return; }
+                if (rc != 0 || n == 0) break;
+                pr->done += (uint32_t)n;
+            }
+            if (pr->step == T_SRV_SEND) {
+                tcp_close(c, &c.g->sock[pr->fd]);
+                tcp_close(c, &c.g->sock[pr->listenfd]);
+                pr->step = T_DONE;
+            } else {
+                pr->done = 0;
+                pr->step = T_CLI_RECV;
+            }
+            break;
+        }
+        case T_CLI_START: {
+            for (uint32_t i = 0; i < N; i++) (void)rand_r_dev(&c.H->rng);   // _fillcharbuf: rand()
+            const int32_t si = sock_new(c);
+            if (si < 0) { pr->step = T_DONE; return; }
+            sock_init_tcp(&c.g->sock[si], c.g->recv_buf, c.g->send_buf, c.g->tcp_window);
+            pr->fd = si;
+            pr->step = T_CLI_CONNECT;
+            break;
+        }
+        case T_CLI_CONNECT: {   // host_connectToPeer (host.c:1191-1282), tcp_connectToPeer (tcp.c:1462-1484)
+            const DProc* sp = &c.g->proc[pr->peer];
+            if (sp->listenfd < 0) { pr->step = T_DONE; return; }
+            const int32_t sh = sp->host;
+            const uint32_t ip = c.g->host[sh].ip;
+            const uint16_t port = c.g->sock[sp->listenfd].bound_port;
+            DSock* k = &c.g->sock[pr->fd];
+            if (!k->bound) {   // implicit bind to the default interface, peer-specific
+                const uint16_t bp = random_free_port(c);
+                k->bound = 1; k->bound_ip = c.H->ip; k->bound_port = bp;
+                k->peer_ip = ip; k->peer_port = port;
+                k->assoc = 1; k->assoc_general = 0;
+            }
+            int rc = tcp_connect_error(k);
+            if (rc == E_ISCONN && !(k->flags & TF_CONNECT_SIGNALED)) {
+                k->flags |= TF_CONNECT_SIGNALED;
+                rc = 0;
+            } else if (rc == 0) {
+                tcp_send_control(c, k, F_SYN);
+                tcp_set_state(c, k, TS_SYNSENT);
+                rc = E_INPROGRESS;
+            }
+            if (rc == E_INPROGRESS || rc == E_ALREADY) { app_wait(c, pr, pr->fd, 4); return; }
+            if (rc != 0 && rc != E_ISCONN) { pr->step = T_DONE; return; }
+            pr->done = 0;
+            pr->step = T_CLI_SEND;
+            break;
+        }
+        default:
+            return;
+        }
+    }
+}
+
+// ------------------------------------------------------------ events
+__device__ void execute(L& c, const DEv& e) {
+    switch (e.kind) {
+    case K_HEARTBEAT: sched_task(c, c.g->hb, K_HEARTBEAT, -1); break;   // tracker.c:607-610
+    case K_REFILL: refill_cb(c); break;
+    case K_REFILL_LO: break;
+    case K_PSTART: {   // the process's start task (process.c:1334-1357)
+        DProc* pr = &c.g->proc[e.obj];
+        if (pr->running) break;
+        pr->running = 1;
+        pr->step = pr->peer < 0 ? T_SRV_START : T_CLI_START;
+        app_run(c, pr);
+        break;
+    }
+    case K_NOTIFY: {   // _epoll_tryNotify (epoll.c:638-683)
+        DProc* pr = &c.g->proc[e.obj];
+        pr->ep_scheduled = 0;
+        if (!pr->running || !pr->ep_ready) break;
+        pr->ep_notifying = 1;
+        if (watch_ready(c, pr)) {   // epoll_wait collects the event, then EPOLL_CTL_DEL
+            if (pr->wait_fd >= 0) c.g->sock[pr->wait_fd].proc = -1;
+            pr->wait_fd = -1;
+            pr->ep_ready = 0;
+            app_run(c, pr);
+        }
+        pr->ep_notifying = 0;
+        pr->ep_ready = watch_ready(c, pr);
+        if (pr->ep_ready) ep_schedule(c, pr);
+        break;
+    }
+    case K_DELIVER: {   // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
+        DHost* H = c.H;
+        const bool was_empty = H->cq_n == 0;
+        if (H->cq_n >= kCq) { H->err |= SHD_TCP_ERR_QUEUE; break; }
+        CqEnt* q = &c.g->cq[(size_t)c.h * kCq + (H->cq_head + H->cq_n) % kCq];
+        q->ts = c.now; q->len = PK(c, e.pkt)->len + kHdr; q->pkt = e.pkt;
+        H->cq_n++;
+        H->cq_total += q->len;
+        pkt_ref(c, e.pkt);
+        pkt_status(c, e.pkt, S_ROUTER_ENQUEUED);
+        if (was_empty) if_receive_packets(c);
+        c.active = -1;   // the task's reference goes after event_execute cleared the host
+        pkt_unref(c, e.pkt);
+        break;
+    }
+    case K_DELACK: {   // tcp.c:1767-1774
+        DSock* k = &c.g->sock[e.obj];
+        k->s_delack_sched = 0;
+        if (k->s_delack_counter > 0) { tcp_send_control(c, k, F_ACK); k->s_delack_counter = 0; }
+        break;
+    }
+    case K_RTO: {   // tcp.c:1280-1333
+        DSock* k = &c.g->sock[e.obj];
+        th_pop(k->timers);
+        if (k->state == TS_CLOSED) { k->desired = 0; tcp_clear_retransmit(c, k, 0xffffffffu); break; }
+        if (k->nrtx == 0) { k->desired = 0; break; }
+        if (k->desired == 0) break;
+        if (k->desired > c.now) { tcp_schedule_rto_if_needed(c, k, c.now); break; }
+        k->backoff++;
+        tcp_set_rto(k, k->rto * 2);
+        tcp_set_rto_timer(c, k, c.now);
+        reno_timeout(k);
+        k->tally.retx.n = 0;   // retransmit_tally_clear_retransmitted
+        uint32_t b = k->r_last_ack, en = k->s_highest + 1;   // retransmit_tally_mark_lost (cc:247-255)
+        if (b != en + 1) {
+            if (b == en) en += 1;
+            ranges_insert(k->tally.marked, b, en, c.H->err);
+            tally_compute_lost(k->tally, c.H->err);
+        }
+        tcp_flush(c, k);
+        break;
+    }
+    case K_CLOSE: tcp_set_state(c, &c.g->sock[e.obj], TS_CLOSED); break;   // tcp.c:695-698
+    case K_WINUPD: {   // tcp.c:2180-2190
+        DSock* k = &c.g->sock[e.obj];
+        tcp_send_control(c, k, F_ACK);
+        k->r_winupd = 0;
+        break;
+    }
+    default: c.H->err |= SHD_TCP_ERR_INTERNAL; break;
+    }
+}
+
+// host_boot at t = 0 (host.c:372-390): heartbeat, the ethernet refill inline,
+// the loopback refill at +1 ms, then each process's start task
+__global__ void k_tcp_boot(Glob g) {
+    const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (h >= g.H) return;
+    Glob gl = g;
+    L c{&gl, h, &gl.host[h], 0, h};
+    sched_task(c, gl.hb, K_HEARTBEAT, -1);
+    refill_cb(c);
+    sched_task(c, kMs, K_REFILL_LO, -1);
+    for (int j = 0; j < kProcs; j++) {
+        const int32_t pi = gl.host_procs[h * kProcs + j];
+        if (pi < 0) break;
+        const uint64_t st = gl.proc[pi].start;
+        sched_task(c, st > 0 ? st : 1, K_PSTART, pi);
+    }
+    const uint32_t n = c.H->nev;
+    gl.next_time[h] = n ? gl.ev[(size_t)h * kEv].time : ~0ull;
+}
+
+// one conservative round: the mailbox's deliveries for this host, then every
+// event before the window's end
+__global__ void k_tcp_round(Glob g, uint64_t wend) {
+    const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (h >= g.H) return;
+    Glob gl = g;
+    L c{&gl, h, &gl.host[h], 0, h};
+    const uint32_t nin = *gl.n_in;
+    for (uint32_t i = 0; i < nin && i < kMail; i++) {
+        const Mail* m = &gl.mail_in[i];
+        if ((int32_t)m->dst != h) continue;
+        const int32_t pi = pkt_alloc(c);
+        if (pi < 0) break;
+        *PK(c, pi) = m->pkt;
+        DEv e;
+        e.time = m->time; e.seq = m->seq; e.src = m->src; e.kind = K_DELIVER; e.obj = -1; e.pkt = pi;
+        evq_push(c, e);
+    }
+    uint64_t nev = 0;
+    while (c.H->nev && gl.ev[(size_t)h * kEv].time < wend && !c.H->err) {
+        const DEv e = evq_pop(c);
+        c.now = e.time;
+        c.active = h;
+        execute(c, e);
+        if (++nev > (1u << 24)) c.H->err |= SHD_TCP_ERR_INTERNAL;   // a runaway round: stop, report
+    }
+    c.H->events += nev;
+    // a host that stopped on an error leaves the run (the caller sees the bit)
+    gl.next_time[h] = (c.H->nev && !c.H->err) ? gl.ev[(size_t)h * kEv].time : ~0ull;
+}
+
+#define HCHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "shd_tcp: %s: %s\n", #x, hipGetErrorString(e_)); rc = -5; goto done; } } while (0)
+
+void ip_str(uint32_t ip, char* b) { snprintf(b, 20, "%u.%u.%u.%u", (ip >> 24) & 255, (ip >> 16) & 255, (ip >> 8) & 255, ip & 255); }
+
+// packet_toString (packet.c:518-641) from a device record
+void format_line(std::string& o, const TRec& r, const int32_t* sacks, int32_t host) {
+    char buf[512], s[20], d[20];
+    ip_str(r.sip, s);
+    ip_str(r.dip, d);
+    snprintf(buf, sizeof(buf), "%llu\t%d\t[%s] packetID=%u:%llu %s:%u -> %s:%u seq=%u ack=%u sack=",
+             (unsigned long long)r.time, host, kStatusName[r.status], r.host_id, (unsigned long long)r.pid, s, r.sport, d,
+             r.dport, r.seq, r.ack);
+    o += buf;
+    int32_t first = -1, last = -1;
+    for (uint32_t i = 0; i < r.nsack; i++) {
+        const int32_t sq = sacks[i];
+        if (first == -1) first = sq;
+        else if (last == -1 || sq == last + 1) last = sq;
+        else { snprintf(buf, sizeof(buf), "%d-%d ", first, last); o += buf; first = sq; last = -1; }
+    }
+    if (first != -1) {
+        snprintf(buf, sizeof(buf), "%d", first); o += buf;
+        if (last != -1) { snprintf(buf, sizeof(buf), "-%d", last); o += buf; }
+    } else {
+        o += "NA";
+    }
+    snprintf(buf, sizeof(buf), " window=%u bytes=%u header=", r.win, r.len);
+    o += buf;
+    if (r.flags & F_RST) o += "RST";
+    if (r.flags & F_SYN) o += "SYN";
+    if (r.flags & F_FIN) o += "FIN";
+    if (r.flags & F_ACK) o += "ACK";
+    if (r.flags & F_DUPACK) o += "DUPACK";
+    snprintf(buf, sizeof(buf), " tsval=%llu tsechoreply=%llu", (unsigned long long)r.tsval, (unsigned long long)r.tsecho);
+    o += buf;
+    if (r.nst) {
+        o += " status=";
+        for (uint32_t i = 0; i < r.nst && i < 32; i++) {
+            o += kStatusName[r.st[i]];
+            if (i + 1 < r.nst) o += ",";
+        }
+    }
+    o += "\n";
+}
+
+int32_t rand_r_host(uint32_t* state) {
+    uint32_t next = *state;
+    int32_t result;
+    next *= 1103515245u; next += 12345u;
+    result = (int32_t)((next / 65536u) % 2048u);
+    next *= 1103515245u; next += 12345u;
+    result <<= 10; result ^= (int32_t)((next / 65536u) % 1024u);
+    next *= 1103515245u; next += 12345u;
+    result <<= 10; result ^= (int32_t)((next / 65536u) % 1024u);
+    *state = next;
+    return result;
+}
+
+}  // namespace
+
+extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
+    if (!m || !out || m->n_hosts <= 0 || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
+        !m->bw_up_kibps || !m->path_lat_ms || !m->path_rel || (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
+        return -22;
+    const int32_t H = m->n_hosts, P = m->n_procs;
+    for (int32_t k = 0; k < P; k++) {
+        if (m->proc_host[k] < 0 || m->proc_host[k] >= H) return -22;
+        if (m->proc_peer[k] >= P || (m->proc_peer[k] >= 0 && m->proc_peer[m->proc_peer[k]] >= 0)) return -22;
+    }
+    // the window: the smallest latency between two different hosts, in ns (ceil, worker.c:293)
+    uint64_t W = ~0ull;
+    for (int32_t a = 0; a < H; a++)
+        for (int32_t b = 0; b < H; b++) {
+            if (a == b) continue;
+            const double l = m->path_lat_ms[(size_t)a * H + b];
+            if (l < 0) continue;
+            const uint64_t w = (uint64_t)ceil(l * (double)kMs);
+            if (w < W) W = w;
+        }
+    if (W == 0) return -22;
+    if (W == ~0ull) W = m->end_time ? m->end_time : 1;
+
+    int rc = 0;
+    Glob g;
+    memset(&g, 0, sizeof(g));
+    std::vector<DHost> hh(H);
+    std::vector<DProc> pp(P > 0 ? P : 1);
+    std::vector<int32_t> hp((size_t)H * kProcs, -1);
+    std::vector<int32_t> fl(kPool);
+    shd_tcp_result* res = (shd_tcp_result*)calloc(1, sizeof(shd_tcp_result));
+    double* d_lat = nullptr; double* d_rel = nullptr;
+    uint32_t* d_nmail = nullptr;
+    Mail* d_mail = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    uint64_t rounds = 0;
+    std::vector<uint64_t> nt(H + 1);
+    std::vector<DHost> hout(H);
+    for (int32_t i = 0; i < H; i++) {
+        DHost& x = hh[i];
+        memset(&x, 0, sizeof(x));
+        x.ip = m->host_ip[i];
+        x.rng = m->host_seed[i];
+        x.bw_down = m->bw_down_kibps[i];
+        x.bw_up = m->bw_up_kibps[i];
+        x.tx_refill = m->bw_up_kibps[i] * 1024 / 1000;   // _networkinterface_setupTokenBuckets (:192-226)
+        x.rx_refill = m->bw_down_kibps[i] * 1024 / 1000;
+        x.tx_cap = x.tx_refill + kMTU;
+        x.rx_cap = x.rx_refill + kMTU;
+        x.nfree = kPool;
+        x.next_handle = 3;
+    }
+    for (int32_t k = 0; k < P; k++) {
+        DProc& pr = pp[k];
+        memset(&pr, 0, sizeof(pr));
+        pr.host = m->proc_host[k]; pr.index = k; pr.peer = m->proc_peer[k]; pr.start = m->proc_start[k];
+        pr.fd = pr.listenfd = pr.wait_fd = -1;
+        int32_t* slot = &hp[(size_t)pr.host * kProcs];
+        int j = 0;
+        while (j < kProcs && slot[j] >= 0) j++;
+        if (j == kProcs) { free(res); return -22; }
+        slot[j] = k;
+    }
+    for (uint32_t i = 0; i < kPool; i++) fl[i] = (int32_t)(kPool - 1 - i);   // pops 0, 1, 2, ...
+
+    g.H = H; g.P = P;
+    g.end_time = m->end_time; g.hb = m->heartbeat_interval ? m->heartbeat_interval : kSec;
+    g.tcp_bytes = m->tcp_bytes; g.trace = trace ? 1 : 0;
+    g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
+    HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)H * H));
+    HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)H * H));
+    HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)H * H, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(d_rel, m->path_rel, sizeof(double) * (size_t)H * H, hipMemcpyHostToDevice));
+    g.lat = d_lat; g.rel = d_rel;
+    HCHECK(hipMalloc(&g.host, sizeof(DHost) * H));
+    HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * H, hipMemcpyHostToDevice));
+    HCHECK(hipMalloc(&g.sock, sizeof(DSock) * (size_t)H * kSock));
+    HCHECK(hipMemset(g.sock, 0, sizeof(DSock) * (size_t)H * kSock));
+    HCHECK(hipMalloc(&g.proc, sizeof(DProc) * pp.size()));
+    HCHECK(hipMemcpy(g.proc, pp.data(), sizeof(DProc) * pp.size(), hipMemcpyHostToDevice));
+    HCHECK(hipMalloc(&g.host_procs, sizeof(int32_t) * hp.size()));
+    HCHECK(hipMemcpy(g.host_procs, hp.data(), sizeof(int32_t) * hp.size(), hipMemcpyHostToDevice));
+    HCHECK(hipMalloc(&g.pool, sizeof(DPkt) * (size_t)H * kPool));
+    HCHECK(hipMalloc(&g.freel, sizeof(int32_t) * (size_t)H * kPool));
+    for (int32_t i = 0; i < H; i++)
+        HCHECK(hipMemcpy(g.freel + (size_t)i * kPool, fl.data(), sizeof(int32_t) * kPool, hipMemcpyHostToDevice));
+    HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
+    HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
+    HCHECK(hipMalloc(&d_mail, sizeof(Mail) * 2 * (size_t)kMail));
+    HCHECK(hipMalloc(&d_nmail, sizeof(uint32_t) * 2));
+    HCHECK(hipMemset(d_nmail, 0, sizeof(uint32_t) * 2));
+    if (trace) {
+        HCHECK(hipMalloc(&g.tr, sizeof(TRec) * (size_t)H * kTr));
+        HCHECK(hipMalloc(&g.trs, sizeof(int32_t) * (size_t)H * kTrSack));
+    }
+    HCHECK(hipMalloc(&g.next_time, sizeof(uint64_t) * (H + 1)));
+    HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (H + 1)));
+    HCHECK(hipEventCreate(&e0));
+    HCHECK(hipEventCreate(&e1));
+    {
+        const int threads = 64, blocks = (H + threads - 1) / threads;
+        HCHECK(hipEventRecord(e0, 0));
+        k_tcp_boot<<<blocks, threads>>>(g);
+        HCHECK(hipGetLastError());
+        int cur = 0;   // mailbox A is read by the next round, B written
+        for (;;) {
+            HCHECK(hipMemcpy(nt.data(), g.next_time, sizeof(uint64_t) * (H + 1), hipMemcpyDeviceToHost));
+            uint64_t T = ~0ull;
+            for (int32_t i = 0; i <= H; i++) T = nt[i] < T ? nt[i] : T;
+            if (T == ~0ull || T >= m->end_time) break;
+            g.mail_in = d_mail + (size_t)cur * kMail; g.n_in = d_nmail + cur;
+            g.mail_out = d_mail + (size_t)(1 - cur) * kMail; g.n_out = d_nmail + (1 - cur);
+            HCHECK(hipMemset(g.n_out, 0, sizeof(uint32_t)));
+            HCHECK(hipMemset(g.next_time + H, 0xff, sizeof(uint64_t)));
+            k_tcp_round<<<blocks, threads>>>(g, T + W);
+            HCHECK(hipGetLastError());
+            if (++rounds > (1ull << 26)) { res->error |= SHD_TCP_ERR_INTERNAL; break; }
+            cur = 1 - cur;
+            uint32_t nout = 0;
+            HCHECK(hipMemcpy(&nout, d_nmail + cur, sizeof(uint32_t), hipMemcpyDeviceToHost));
+            if (nout > kMail) { res->error |= SHD_TCP_ERR_MAILBOX; break; }
+        }
+        HCHECK(hipEventRecord(e1, 0));
+        HCHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HCHECK(hipEventElapsedTime(&ms, e0, e1));
+        res->device_ms = ms;
+    }
+    HCHECK(hipMemcpy(hout.data(), g.host, sizeof(DHost) * H, hipMemcpyDeviceToHost));
+    res->next_event_id = (uint64_t*)calloc(H, sizeof(uint64_t));
+    res->next_packet_id = (uint64_t*)calloc(H, sizeof(uint64_t));
+    res->rng_probe = (uint32_t*)calloc(H, sizeof(uint32_t));
+    res->rounds = rounds;
+    for (int32_t i = 0; i < H; i++) {
+        res->next_event_id[i] = hout[i].ev_seq;
+        res->next_packet_id[i] = hout[i].pkt_seq;
+        uint32_t st = hout[i].rng;
+        res->rng_probe[i] = (uint32_t)rand_r_host(&st);
+        res->events += hout[i].events;
+        res->error |= hout[i].err;
+    }
+    if (trace) {
+        std::string text;
+        std::vector<TRec> recs;
+        std::vector<int32_t> sk;
+        for (int32_t i = 0; i < H; i++) {
+            recs.resize(hout[i].ntr);
+            sk.resize(hout[i].ntrs + 1);
+            if (hout[i].ntr)
+                HCHECK(hipMemcpy(recs.data(), g.tr + (size_t)i * kTr, sizeof(TRec) * hout[i].ntr, hipMemcpyDeviceToHost));
+            if (hout[i].ntrs)
+                HCHECK(hipMemcpy(sk.data(), g.trs + (size_t)i * kTrSack, sizeof(int32_t) * hout[i].ntrs, hipMemcpyDeviceToHost));
+            for (const TRec& r : recs) format_line(text, r, sk.data() + r.sack_off, i);
+            res->n_lines += hout[i].ntr;
+        }
+        res->lines = (char*)malloc(text.size() + 1);
+        memcpy(res->lines, text.data(), text.size());
+        res->lines[text.size()] = 0;
+        res->len = text.size();
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_mail); (void)hipFree(d_nmail);
+    (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
+    (void)hipFree(g.pool); (void)hipFree(g.freel); (void)hipFree(g.ev); (void)hipFree(g.cq);
+    (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);
+    if (rc) { shd_tcp_result_free(res); return rc; }
+    *out = res;
+    return 0;
+}
+
+extern "C" void shd_tcp_result_free(shd_tcp_result* r) {
+    if (!r) return;
+    free(r->lines);
+    free(r->next_event_id);
+    free(r->next_packet_id);
+    free(r->rng_probe);
+    free(r);
+}

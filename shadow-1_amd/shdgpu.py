@@ -174,7 +174,29 @@ class RunStats(C.Structure):
 
 
 # exported symbols (checked by tests/test_abi.py against include/shdgpu.h)
+class TcpModel(C.Structure):
+    """shd_tcp_model (include/shdtcp.h)"""
+    _fields_ = [("n_hosts", C.c_int32), ("n_procs", C.c_int32),
+                ("host_ip", P(C.c_uint32)), ("host_seed", P(C.c_uint32)),
+                ("bw_down_kibps", P(C.c_uint64)), ("bw_up_kibps", P(C.c_uint64)),
+                ("path_lat_ms", P(C.c_double)), ("path_rel", P(C.c_double)),
+                ("proc_host", P(C.c_int32)), ("proc_start", P(C.c_uint64)), ("proc_peer", P(C.c_int32)),
+                ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
+                ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
+                ("tcp_window", C.c_uint32)]
+
+
+class TcpResult(C.Structure):
+    """shd_tcp_result (include/shdtcp.h)"""
+    _fields_ = [("lines", C.c_void_p), ("len", C.c_size_t), ("n_lines", C.c_uint64),
+                ("next_event_id", P(C.c_uint64)), ("next_packet_id", P(C.c_uint64)),
+                ("rng_probe", P(C.c_uint32)), ("rounds", C.c_uint64), ("events", C.c_uint64),
+                ("device_ms", C.c_double), ("error", C.c_uint32)]
+
+
 _SIGS = {
+    "shd_tcp_run": (C.c_int, [P(TcpModel), C.c_int32, P(P(TcpResult))]),
+    "shd_tcp_result_free": (None, [P(TcpResult)]),
     "shd_graph_check": (C.c_int, [P(Graph), P(GraphProps)]),
     "shd_graphml_load_file": (C.c_int, [C.c_char_p, P(P(GraphML))]),
     "shd_graphml_load_string": (C.c_int, [C.c_char_p, C.c_size_t, P(P(GraphML))]),

@@ -3,7 +3,8 @@ INFRASTRUCTURE.  Runs each case of tests/tcp_cases.py through
 oracle/_ref/libshdref_loop.so (the reference's tcp.c, tcp_cong_reno.c,
 tcp_retransmit_tally.cc, socket.c, network_interface.c, worker.c ... compiled
 unmodified; oracle/Makefile `ref`) and stores what a run must reproduce:
-the host IPs, the number and SHA-256 of the [STATUS] lines, and every host's
+the host IPs, the number and SHA-256 of the [STATUS] lines (in the serial
+order, and grouped by host in each host's order), and every host's
 next event ID, next packet ID and RNG draw at the end.
 
     python tests/golden/make_ref_tcp.py        # -> tests/golden/ref_tcp.json
@@ -26,6 +27,7 @@ def main():
         r = R.run(m, c["graph"], procs=c["procs"], tcp=dict(peers=c["peers"], nbytes=c["nbytes"]))
         st = TC.status_lines(r["lines"])
         out[name] = dict(ips=r["ip"], n_status=len(st), status_sha256=TC.digest(st),
+                         status_by_host_sha256=TC.digest(TC.by_host(st)),
                          next_event_id=[int(x) for x in r["next_event_id"]],
                          next_packet_id=[int(x) for x in r["next_packet_id"]],
                          rng_probe=[int(x) for x in r["rng_probe"]])

@@ -77,3 +77,9 @@ def digest(lines):
 
 def ip_ints(ips):
     return [int.from_bytes(bytes(int(x) for x in ip.split(".")), "big") for ip in ips]
+
+
+def by_host(lines):
+    """Each host's lines in its own order (the GPU runs hosts in parallel; a
+    host's own sequence is the serial loop's)."""
+    return sorted(lines, key=lambda x: x[1])   # stable: keeps each host's order

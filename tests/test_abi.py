@@ -10,8 +10,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared():
-    h = open(os.path.join(REPO, "include", "shdgpu.h")).read()
-    return set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(shd_[a-z_0-9]+)\(", h, re.M))
+    out = set()
+    for name in ("shdgpu.h", "shdtcp.h"):   # the library's C ABI (include/*.h)
+        h = open(os.path.join(REPO, "include", name)).read()
+        out |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(shd_[a-z_0-9]+)\(", h, re.M))
+    return out
 
 
 def exported():

@@ -1,0 +1,38 @@
+"""The TCP path on the GPU (csrc/tcp.hip through include/shdtcp.h) against the
+reference's own TCP loop: every case of tests/tcp_cases.py, each host's
+[STATUS] lines in its own order equal to the reference's
+(tests/golden/ref_tcp.json: count and SHA-256 grouped by host), every host's
+event-ID counter, packet counter and RNG state equal at the end.  The oracle's
+lines (oracle/o_tcp.c, pinned to the same fixtures on the CPU) locate the first
+difference when there is one."""
+import json
+import os
+
+import pytest
+
+import oracle_ffi as O
+import tcp as TCPGPU
+import tcp_cases as TC
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
+
+
+@pytest.mark.parametrize("name", list(TC.CASES))
+def test_tcp_gpu_equals_reference(name):
+    f = FIX[name]
+    c, m = TC.build(name)
+    ips = TC.ip_ints(f["ips"])
+    r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"])
+    got = r["lines"]
+    if TC.digest(got) != f["status_by_host_sha256"]:
+        want = TC.by_host(O.tcp_run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"])["lines"])
+        for i, (x, y) in enumerate(zip(got, want)):
+            assert x == y, (i, x, y)
+        assert len(got) == len(want), (len(got), len(want))
+    assert len(got) == f["n_status"]
+    assert r["next_event_id"].tolist() == f["next_event_id"]
+    assert r["next_packet_id"].tolist() == f["next_packet_id"]
+    assert r["rng_probe"].tolist() == f["rng_probe"]
+    assert r["rounds"] > 0 and r["events"] > 0

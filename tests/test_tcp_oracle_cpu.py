@@ -35,6 +35,7 @@ def test_tcp_oracle_equals_reference_fixture(name):
     o = _oracle(name)
     assert len(o["lines"]) == f["n_status"]
     assert TC.digest(o["lines"]) == f["status_sha256"]
+    assert TC.digest(TC.by_host(o["lines"])) == f["status_by_host_sha256"]
     assert o["next_event_id"].tolist() == f["next_event_id"]
     assert o["next_packet_id"].tolist() == f["next_packet_id"]
     assert o["rng_probe"].tolist() == f["rng_probe"]
