@@ -57,12 +57,15 @@ def parse():
     ap.add_argument("--lossy-edge-loss-max", type=float, default=0.0005,
                     help="edge loss ~ U[0, x] of the lossy C3 run reported beside the headline "
                          "(its packet events per step show the decay); 0 skips it")
-    ap.add_argument("--workload", choices=["c3", "c4", "c5"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c4", "c5", "tcp"], default="c3",
                     help="c3: PHOLD-UDP on the geometric topology (the headline, weak scaling); c4: the "
                          "Tor-scale relay/client model on the bundled topology (hosts fixed, strong scaling); "
                          "c5: 1 M hosts (100 per vertex of the geometric topology), 1500-B messages, 512 KiB/s "
                          "downlinks so CoDel queues build, edge loss U[0, 0.01] (hosts fixed, strong scaling; "
-                         "lost messages are not regenerated, so the rate depends on the window)")
+                         "lost messages are not regenerated, so the rate depends on the window); tcp: the "
+                         "TCP path (include/shdtcp.h) on workloads.tcp_echo_model, one run per step")
+    ap.add_argument("--tcp-bytes", type=int, default=500000, help="tcp: bytes each client echoes")
+    ap.add_argument("--tcp-end-s", type=int, default=20, help="tcp: simulated seconds")
     ap.add_argument("--relays", type=int, default=6500)
     ap.add_argument("--clients", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -122,6 +125,8 @@ os.dup2(2, 1)
 
 def main():
     args = parse()
+    if args.workload == "tcp":
+        return tcp_main(args)
     if args.load is None:
         args.load = {"c4": 4, "c5": 32}.get(args.workload, 16)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -425,6 +430,80 @@ def main():
         comm.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def tcp_main(args):
+    """The TCP path measured like the headline: a step is one
+    whole shd_tcp_run of workloads.tcp_echo_model (hosts resident in HBM from
+    the call's upload on; the value is device time of the rounds, HIP events on
+    the run's stream).  Replicas only: the TCP path runs on one GPU."""
+    import torch
+    import shdgpu as S
+    import workloads as W
+    import tcp as T
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--workload tcp runs on one GPU (replicas only)")
+    torch.cuda.set_device(0)
+    H = args.hosts_per_gpu or 4096
+    V = min(args.vertices, 1000)
+    g, m, ips, procs, peers, nb = W.tcp_echo_model(H, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,
+                                                  loss_max=args.edge_loss_max)
+    for _ in range(args.warmup):
+        T.run(m, g, ips, procs, peers, nbytes=nb, trace=False)
+    mark = Roctx()
+    runs = []
+    torch.cuda.synchronize()
+    mark.push("shd_timed_region")
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runs.append(T.run(m, g, ips, procs, peers, nbytes=nb, trace=False))
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    mark.pop()
+    r = runs[-1]
+    assert all(x["events"] == r["events"] and x["rounds"] == r["rounds"] for x in runs), "runs differ"
+    dev_s = sum(x["device_ms"] for x in runs) / 1e3
+    events = r["events"] * len(runs)
+    deliv = r["deliveries"] * len(runs)
+    # algorithmic bytes per executed event: its 32-B record pushed and popped
+    # once (64 B); per delivery the mailbox record written and read once
+    mail_b = 712   # sizeof(Mail) in csrc/tcp.hip (static_assert there)
+    alg = 64 * r["events"] + 2 * mail_b * r["deliveries"]
+    per_round_us = r["device_ms"] * 1e3 / max(r["rounds"], 1)
+    achieved = alg / (r["device_ms"] / 1e3) / 1e9
+    cpu = None
+    if not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
+        import oracle_ffi as O
+        tc = time.perf_counter()
+        o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb, lines=False)
+        cs = time.perf_counter() - tc
+        same = (o["events"] == r["events"] and o["next_event_id"].tolist() == r["next_event_id"].tolist()
+                and o["rng_probe"].tolist() == r["rng_probe"].tolist())
+        cpu = {"value": round(o["events"] / cs, 1), "unit": "TCP events/s", "cores": 1, "kind": "port",
+               "sample": "oracle/o_tcp.c serial loop (pinned to the reference's tcp.c loop) on the same model, "
+                         "[STATUS] lines off: %d events in %.2f s" % (o["events"], cs),
+               "same_end_state_as_gpu": bool(same)}
+    out = {
+        "metric": "simulated TCP events/sec", "value": round(events / dev_s, 1), "unit": "events/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dev_s * 1e3 / len(runs), 3), "higher_is_better": True, "scaling": "replicas only",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (random geometric topology + TCP echo pairs, seed %d)"
+        % args.seed,
+        "config": {"workload": "TCP echo (src/test/tcp/test_tcp.c, nonblocking-epoll), %d hosts / %d pairs, "
+                               "%d-vertex geometric topology, %d B each way, %d s simulated"
+                               % (H, H // 2, V, nb, args.tcp_end_s),
+                   "hosts": H, "vertices": V, "parallelism": "one lane per host, 1 GPU"},
+        "packet_deliveries_per_s": round(deliv / dev_s, 1), "wall_s": round(wall, 3),
+        "rounds": r["rounds"], "events_per_run": r["events"], "deliveries_per_run": r["deliveries"],
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(achieved / 8000.0, 6), "traffic": None, "kernel": "k_tcp_round",
+                     "avg_round_us": round(per_round_us, 3),
+                     "alg_bytes": "64 B x events + 2 x %d B x deliveries" % mail_b},
+        "cpu_baseline": cpu,
+    }
+    os.dup2(_STDOUT_FD, 1)
+    print(json.dumps(out), flush=True)
 
 
 def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, torch):

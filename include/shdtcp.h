@@ -57,6 +57,8 @@ typedef struct shd_tcp_result {
     uint64_t events;                  /* events executed                                  */
     double device_ms;                 /* GPU time of the rounds (HIP events)              */
     uint32_t error;                   /* SHD_TCP_ERR_* bits; nonzero: results invalid     */
+    uint64_t deliveries;              /* packets handed to a receiving host (worker.c:260-321's
+                                         delivery events executed)                           */
 } shd_tcp_result;
 
 enum {

@@ -89,7 +89,7 @@ typedef struct opkt {
     int32_t* sacks; uint32_t nsack;
     uint32_t len;
     double prio;
-    uint8_t st[64]; uint32_t nst;
+    uint8_t st[128]; uint32_t nst;
     int32_t owner;               /* host whose active events print its lines (-2: none) */
 } opkt;
 
@@ -472,6 +472,7 @@ static void pkt_string(const opkt* p, obuf* b) {
  * the simulated time, on the active host */
 static void pkt_status(opkt* p, int st) {
     if (p->nst < sizeof(p->st)) p->st[p->nst++] = (uint8_t)st;
+    if (G->cfg->no_lines) return;
     obuf* b = &G->out;
     ob_printf(b, "%llu\t%d\t[%s] ", (unsigned long long)G->now, G->active, k_status_name[st]);
     pkt_string(p, b);
@@ -1731,6 +1732,7 @@ int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out) {
     if (!cfg || !out || cfg->n_hosts <= 0) return -1;
     T t;
     memset(&t, 0, sizeof(t));
+    out->events = 0;
     G = &t;
     t.cfg = cfg;
     t.topo = topo;
@@ -1772,6 +1774,7 @@ int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out) {
         tev e = q_pop(&t);
         t.now = e.time;
         execute(&e);
+        out->events++;
     }
     out->lines = t.out.s;
     out->len = t.out.len;

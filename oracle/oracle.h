@@ -208,10 +208,12 @@ typedef struct o_tcp_cfg {
     const int32_t* proc_peer;         /* [P] -1 server, else the server process */
     uint64_t end_time, heartbeat_interval;
     uint32_t tcp_bytes, recv_buf, send_buf, tcp_window;
+    uint32_t no_lines, _pad;          /* 1: keep the statuses, write no lines (bench.py's CPU baseline) */
 } o_tcp_cfg;
 typedef struct o_tcp_out {
     char* lines; size_t len; uint64_t n_lines;
     uint64_t* next_event_id; uint64_t* next_packet_id; uint32_t* rng_probe;
+    uint64_t events;                  /* events executed */
 } o_tcp_out;
 int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out);
 void o_tcp_free(o_tcp_out* out);

@@ -39,6 +39,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -58,7 +59,8 @@ constexpr uint32_t kSacks = 512;    // the receiver's SACK list
 constexpr uint32_t kRanges = 64;    // tally ranges per set
 constexpr uint32_t kKids = 8;
 constexpr uint32_t kPool = 16384;   // packets per host
-constexpr uint32_t kPktSack = 64;   // SACK entries carried by one segment
+constexpr uint32_t kPktSack = 128;  // SACK entries carried by one segment (the receive window's holes)
+constexpr uint32_t kSt = 96;        // delivery statuses a packet's line lists (each loss retransmission adds 6)
 constexpr uint32_t kEv = 8192;      // events per host
 constexpr uint32_t kCq = 4096;      // CoDel queue per host
 constexpr uint32_t kTr = 1u << 16;  // trace records per host
@@ -104,11 +106,12 @@ struct DPkt {
     uint64_t tsval, tsecho;
     double prio;
     uint32_t nsack, nst;
-    uint8_t st[32];
+    uint8_t st[kSt];
     int32_t sacks[kPktSack];
 };
 struct DEv { uint64_t time, seq; uint32_t src, kind; int32_t obj, pkt; };
 struct Mail { uint32_t dst, src; uint64_t time, seq; DPkt pkt; };
+static_assert(sizeof(DEv) == 32 && sizeof(Mail) == 712, "bench.py's algorithmic bytes of the TCP rounds");
 struct TRec {
     uint64_t time; int32_t host; uint32_t status;
     uint32_t host_id, flags, sip, dip;
@@ -116,7 +119,7 @@ struct TRec {
     uint16_t sport, dport; uint32_t seq, ack, win, len;
     uint64_t tsval, tsecho;
     uint32_t sack_off, nsack, nst;
-    uint8_t st[32];
+    uint8_t st[kSt];
 };
 template <uint32_t N> struct Ring {   // GQueue
     uint32_t head, n;
@@ -167,7 +170,7 @@ struct DProc {
 };
 struct DHost {
     uint32_t ip, rng, pkt_seq, err;
-    uint64_t ev_seq, events;
+    uint64_t ev_seq, events, deliveries;
     double prio;
     uint64_t rx_rem, rx_cap, rx_refill, tx_rem, tx_cap, tx_refill;
     uint64_t bw_down, bw_up;   // configured KiB/s (worker_getNodeBandwidth{Down,Up})
@@ -179,10 +182,17 @@ struct DHost {
 };
 struct CqEnt { uint64_t ts; uint32_t len; int32_t pkt; };
 
+// the round driver's device-side state (the host only reads it between batches)
+struct TCtl {
+    uint64_t wend;       // the running round's window end
+    uint64_t rounds;     // rounds started; round k reads mailbox k & 1 and writes the other
+    uint32_t halted, _pad;
+};
+
 struct Glob {
     int32_t H, P;
     const double *lat, *rel;
-    uint64_t end_time, hb, window_end, now_dummy;
+    uint64_t end_time, hb, W, now_dummy;
     uint32_t tcp_bytes, trace, recv_buf, send_buf, tcp_window, _pad;
     DHost* host;
     DSock* sock;            // [H][kSock]
@@ -192,8 +202,14 @@ struct Glob {
     int32_t* freel;         // [H][kPool]
     DEv* ev;                // [H][kEv]
     CqEnt* cq;              // [H][kCq]
-    Mail* mail_in; uint32_t* n_in;
-    Mail* mail_out; uint32_t* n_out;
+    Mail* mail;             // [2][kMail] the two mailboxes (a round's input, its output)
+    uint32_t* nmail;        // [2] their fill counts
+    int32_t* mhead;         // [2][H] each destination's list of mails (-1: none)
+    int32_t* mnext;         // [2][kMail] the next mail of the same destination
+    TCtl* ctl;
+    const uint64_t* ip_key; // [H] (ip << 32 | host) ascending: host_of_ip's table
+    Mail* mail_in; int32_t* mhead_in; int32_t* mnext_in;     // a lane's view of the round
+    Mail* mail_out; uint32_t* n_out; int32_t* mhead_out; int32_t* mnext_out;
     TRec* tr;               // [H][kTr]
     int32_t* trs;           // [H][kTrSack]
     uint64_t* next_time;    // [H]
@@ -343,16 +359,17 @@ __device__ bool sched_task(L& c, uint64_t delay, uint32_t kind, int32_t obj) {
 // ------------------------------------------------------------ packets and their lines
 __device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDeliveryStatus (packet.c:647-659)
     DPkt* p = PK(c, pi);
-    if (p->nst < 32) p->st[p->nst++] = st;
-    if (!c.g->trace) return;
     DHost* H = c.H;
+    if (p->nst < kSt) p->st[p->nst++] = st;
+    else if (c.g->trace) H->err |= SHD_TCP_ERR_TRACE;   // a line would lose statuses: fail, never truncate
+    if (!c.g->trace) return;
     if (H->ntr >= kTr) { H->err |= SHD_TCP_ERR_TRACE; return; }
     TRec* r = &c.g->tr[(size_t)c.h * kTr + H->ntr++];
     r->time = c.now; r->host = c.active; r->status = st;
     r->host_id = p->host_id; r->pid = p->pid; r->flags = p->flags; r->sip = p->sip; r->dip = p->dip;
     r->sport = p->sport; r->dport = p->dport; r->seq = p->seq; r->ack = p->ack; r->win = p->win; r->len = p->len;
     r->tsval = p->tsval; r->tsecho = p->tsecho; r->nst = p->nst;
-    for (uint32_t i = 0; i < p->nst && i < 32; i++) r->st[i] = p->st[i];
+    for (uint32_t i = 0; i < p->nst; i++) r->st[i] = p->st[i];
     r->sack_off = H->ntrs; r->nsack = p->nsack;
     if (H->ntrs + p->nsack > kTrSack) { H->err |= SHD_TCP_ERR_TRACE; r->nsack = 0; return; }
     for (uint32_t i = 0; i < p->nsack; i++) c.g->trs[(size_t)c.h * kTrSack + H->ntrs + i] = p->sacks[i];
@@ -485,9 +502,17 @@ __device__ int32_t sock_remove_output(L& c, DSock* k) {   // socket.c:426-451
 }
 
 // ------------------------------------------------------------ paths
+// the first host holding ip (dns.c: one address per host), by binary search
+// over the sorted (ip, host) keys
 __device__ int32_t host_of_ip(const L& c, uint32_t ip) {
-    for (int32_t i = 0; i < c.g->H; i++) if (c.g->host[i].ip == ip) return i;
-    return -1;
+    const uint64_t* k = c.g->ip_key;
+    uint32_t lo = 0, hi = (uint32_t)c.g->H;
+    const uint64_t x = (uint64_t)ip << 32;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (k[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    return (lo < (uint32_t)c.g->H && (uint32_t)(k[lo] >> 32) == ip) ? (int32_t)(uint32_t)k[lo] : -1;
 }
 __device__ void path(const L& c, int32_t a, int32_t b, double& lat, double& rel) {
     lat = c.g->lat[(size_t)a * c.g->H + b];
@@ -1315,6 +1340,7 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
         m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
+        c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
         atomicMin((unsigned long long*)&c.g->next_time[c.g->H], (unsigned long long)t);
     } else {
         pkt_status(c, pi, S_INET_DROPPED);
@@ -1686,6 +1712,12 @@ __device__ void execute(L& c, const DEv& e) {
     }
 }
 
+// every host's packet free list: pops 0, 1, 2, ...
+__global__ void k_tcp_free_init(int32_t* freel, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) freel[i] = (int32_t)(kPool - 1 - (uint32_t)(i % kPool));
+}
+
 // host_boot at t = 0 (host.c:372-390): heartbeat, the ethernet refill inline,
 // the loopback refill at +1 ms, then each process's start task
 __global__ void k_tcp_boot(Glob g) {
@@ -1706,23 +1738,64 @@ __global__ void k_tcp_boot(Glob g) {
     gl.next_time[h] = n ? gl.ev[(size_t)h * kEv].time : ~0ull;
 }
 
+// the next round's window (worker.c:293's conservative width W past the
+// earliest pending event of any host or mailbox); ends the run at end_time.
+// One block; launched before every round, so a batch of rounds runs without
+// the host.
+__global__ void k_tcp_window(Glob g) {
+    __shared__ uint64_t red[16];
+    TCtl* ctl = g.ctl;
+    if (ctl->halted) return;
+    uint64_t t = ~0ull;
+    for (int32_t i = (int32_t)threadIdx.x; i <= g.H; i += (int32_t)blockDim.x) {
+        const uint64_t x = g.next_time[i];
+        t = x < t ? x : t;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(t, o);
+        t = y < t ? y : t;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < blockDim.x / 64; w++) t = red[w] < t ? red[w] : t;
+        if (t == ~0ull || t >= g.end_time) {
+            ctl->halted = 1;
+        } else {
+            const uint64_t k = ctl->rounds;
+            ctl->wend = t + g.W;
+            ctl->rounds = k + 1;
+            g.nmail[(k + 1) & 1] = 0;     // round k's output mailbox starts empty
+            g.next_time[g.H] = ~0ull;     // ... and so does its earliest delivery
+        }
+    }
+}
+
 // one conservative round: the mailbox's deliveries for this host, then every
 // event before the window's end
-__global__ void k_tcp_round(Glob g, uint64_t wend) {
+__global__ void k_tcp_round(Glob g) {
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (h >= g.H) return;
+    if (h >= g.H || g.ctl->halted) return;
+    const uint64_t k = g.ctl->rounds - 1, wend = g.ctl->wend;
+    const uint32_t in = (uint32_t)(k & 1), out = in ^ 1u;
     Glob gl = g;
+    gl.mail_in = g.mail + (size_t)in * kMail; gl.mhead_in = g.mhead + (size_t)in * g.H;
+    gl.mnext_in = g.mnext + (size_t)in * kMail;
+    gl.mail_out = g.mail + (size_t)out * kMail; gl.n_out = g.nmail + out;
+    gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * kMail;
     L c{&gl, h, &gl.host[h], 0, h};
-    const uint32_t nin = *gl.n_in;
-    for (uint32_t i = 0; i < nin && i < kMail; i++) {
-        const Mail* m = &gl.mail_in[i];
-        if ((int32_t)m->dst != h) continue;
+    // this host's deliveries (any order: the heap's key (time, src, seq) is unique)
+    int32_t s = gl.mhead_in[h];
+    gl.mhead_in[h] = -1;   // the list is empty again when this mailbox is next written
+    for (; s >= 0; s = gl.mnext_in[s]) {
+        const Mail* m = &gl.mail_in[s];
         const int32_t pi = pkt_alloc(c);
         if (pi < 0) break;
         *PK(c, pi) = m->pkt;
         DEv e;
         e.time = m->time; e.seq = m->seq; e.src = m->src; e.kind = K_DELIVER; e.obj = -1; e.pkt = pi;
         evq_push(c, e);
+        c.H->deliveries++;
     }
     uint64_t nev = 0;
     while (c.H->nev && gl.ev[(size_t)h * kEv].time < wend && !c.H->err) {
@@ -1774,7 +1847,7 @@ void format_line(std::string& o, const TRec& r, const int32_t* sacks, int32_t ho
     o += buf;
     if (r.nst) {
         o += " status=";
-        for (uint32_t i = 0; i < r.nst && i < 32; i++) {
+        for (uint32_t i = 0; i < r.nst && i < kSt; i++) {
             o += kStatusName[r.st[i]];
             if (i + 1 < r.nst) o += ",";
         }
@@ -1825,12 +1898,15 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     std::vector<DHost> hh(H);
     std::vector<DProc> pp(P > 0 ? P : 1);
     std::vector<int32_t> hp((size_t)H * kProcs, -1);
-    std::vector<int32_t> fl(kPool);
     shd_tcp_result* res = (shd_tcp_result*)calloc(1, sizeof(shd_tcp_result));
     double* d_lat = nullptr; double* d_rel = nullptr;
-    uint32_t* d_nmail = nullptr;
-    Mail* d_mail = nullptr;
+    uint64_t* d_ipk = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipStream_t st = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    TCtl hctl;
+    std::vector<uint64_t> ipk(H);
     uint64_t rounds = 0;
     std::vector<uint64_t> nt(H + 1);
     std::vector<DHost> hout(H);
@@ -1859,9 +1935,10 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         if (j == kProcs) { free(res); return -22; }
         slot[j] = k;
     }
-    for (uint32_t i = 0; i < kPool; i++) fl[i] = (int32_t)(kPool - 1 - i);   // pops 0, 1, 2, ...
 
-    g.H = H; g.P = P;
+    for (int32_t i = 0; i < H; i++) ipk[i] = ((uint64_t)m->host_ip[i] << 32) | (uint32_t)i;
+    std::sort(ipk.begin(), ipk.end());
+    g.H = H; g.P = P; g.W = W;
     g.end_time = m->end_time; g.hb = m->heartbeat_interval ? m->heartbeat_interval : kSec;
     g.tcp_bytes = m->tcp_bytes; g.trace = trace ? 1 : 0;
     g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
@@ -1880,13 +1957,21 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMemcpy(g.host_procs, hp.data(), sizeof(int32_t) * hp.size(), hipMemcpyHostToDevice));
     HCHECK(hipMalloc(&g.pool, sizeof(DPkt) * (size_t)H * kPool));
     HCHECK(hipMalloc(&g.freel, sizeof(int32_t) * (size_t)H * kPool));
-    for (int32_t i = 0; i < H; i++)
-        HCHECK(hipMemcpy(g.freel + (size_t)i * kPool, fl.data(), sizeof(int32_t) * kPool, hipMemcpyHostToDevice));
+    k_tcp_free_init<<<(unsigned)(((size_t)H * kPool + 255) / 256), 256>>>(g.freel, (size_t)H * kPool);
+    HCHECK(hipGetLastError());
     HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
-    HCHECK(hipMalloc(&d_mail, sizeof(Mail) * 2 * (size_t)kMail));
-    HCHECK(hipMalloc(&d_nmail, sizeof(uint32_t) * 2));
-    HCHECK(hipMemset(d_nmail, 0, sizeof(uint32_t) * 2));
+    HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)kMail));
+    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2));
+    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2));
+    HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
+    HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
+    HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)kMail));
+    HCHECK(hipMalloc(&g.ctl, sizeof(TCtl)));
+    HCHECK(hipMemset(g.ctl, 0, sizeof(TCtl)));
+    HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * (size_t)H));
+    HCHECK(hipMemcpy(d_ipk, ipk.data(), sizeof(uint64_t) * (size_t)H, hipMemcpyHostToDevice));
+    g.ip_key = d_ipk;
     if (trace) {
         HCHECK(hipMalloc(&g.tr, sizeof(TRec) * (size_t)H * kTr));
         HCHECK(hipMalloc(&g.trs, sizeof(int32_t) * (size_t)H * kTrSack));
@@ -1895,30 +1980,37 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (H + 1)));
     HCHECK(hipEventCreate(&e0));
     HCHECK(hipEventCreate(&e1));
+    HCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     {
-        const int threads = 64, blocks = (H + threads - 1) / threads;
-        HCHECK(hipEventRecord(e0, 0));
-        k_tcp_boot<<<blocks, threads>>>(g);
-        HCHECK(hipGetLastError());
-        int cur = 0;   // mailbox A is read by the next round, B written
-        for (;;) {
-            HCHECK(hipMemcpy(nt.data(), g.next_time, sizeof(uint64_t) * (H + 1), hipMemcpyDeviceToHost));
-            uint64_t T = ~0ull;
-            for (int32_t i = 0; i <= H; i++) T = nt[i] < T ? nt[i] : T;
-            if (T == ~0ull || T >= m->end_time) break;
-            g.mail_in = d_mail + (size_t)cur * kMail; g.n_in = d_nmail + cur;
-            g.mail_out = d_mail + (size_t)(1 - cur) * kMail; g.n_out = d_nmail + (1 - cur);
-            HCHECK(hipMemset(g.n_out, 0, sizeof(uint32_t)));
-            HCHECK(hipMemset(g.next_time + H, 0xff, sizeof(uint64_t)));
-            k_tcp_round<<<blocks, threads>>>(g, T + W);
-            HCHECK(hipGetLastError());
-            if (++rounds > (1ull << 26)) { res->error |= SHD_TCP_ERR_INTERNAL; break; }
-            cur = 1 - cur;
-            uint32_t nout = 0;
-            HCHECK(hipMemcpy(&nout, d_nmail + cur, sizeof(uint32_t), hipMemcpyDeviceToHost));
-            if (nout > kMail) { res->error |= SHD_TCP_ERR_MAILBOX; break; }
+        // rounds run in batches of kBatch (window kernel, round kernel) pairs
+        // captured once as a graph: no host round trip inside a batch; a
+        // halted run turns the batch's remaining kernels into no-ops
+        // hosts per wave: each lane walks its own host's branchy chain, so
+        // fewer lanes per wave means less divergence and more waves for the
+        // SIMDs to interleave (A/B knob SHD_TCP_LANES while measuring)
+        const char* lv = getenv("SHD_TCP_LANES");
+        const int threads = lv ? atoi(lv) : 64, blocks = (H + threads - 1) / threads;
+        if (threads < 1 || threads > 64) { rc = -22; goto done; }
+        constexpr int kBatch = 64;
+        HCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < kBatch; i++) {
+            k_tcp_window<<<1, 1024, 0, st>>>(g);
+            k_tcp_round<<<blocks, threads, 0, st>>>(g);
         }
-        HCHECK(hipEventRecord(e1, 0));
+        HCHECK(hipStreamEndCapture(st, &graph));
+        HCHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
+        HCHECK(hipEventRecord(e0, st));
+        k_tcp_boot<<<blocks, threads, 0, st>>>(g);
+        HCHECK(hipGetLastError());
+        for (;;) {
+            HCHECK(hipGraphLaunch(gexec, st));
+            HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
+            HCHECK(hipStreamSynchronize(st));
+            if (hctl.halted) break;
+            if (hctl.rounds > (1ull << 26)) { res->error |= SHD_TCP_ERR_INTERNAL; break; }
+        }
+        rounds = hctl.rounds;
+        HCHECK(hipEventRecord(e1, st));
         HCHECK(hipEventSynchronize(e1));
         float ms = 0;
         HCHECK(hipEventElapsedTime(&ms, e0, e1));
@@ -1935,6 +2027,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         uint32_t st = hout[i].rng;
         res->rng_probe[i] = (uint32_t)rand_r_host(&st);
         res->events += hout[i].events;
+        res->deliveries += hout[i].deliveries;
         res->error |= hout[i].err;
     }
     if (trace) {
@@ -1959,7 +2052,11 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
 done:
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
-    (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_mail); (void)hipFree(d_nmail);
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (st) (void)hipStreamDestroy(st);
+    (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_ipk);
+    (void)hipFree(g.mail); (void)hipFree(g.nmail); (void)hipFree(g.mhead); (void)hipFree(g.mnext); (void)hipFree(g.ctl);
     (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
     (void)hipFree(g.pool); (void)hipFree(g.freel); (void)hipFree(g.ev); (void)hipFree(g.cq);
     (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);

@@ -191,7 +191,7 @@ class TcpResult(C.Structure):
     _fields_ = [("lines", C.c_void_p), ("len", C.c_size_t), ("n_lines", C.c_uint64),
                 ("next_event_id", P(C.c_uint64)), ("next_packet_id", P(C.c_uint64)),
                 ("rng_probe", P(C.c_uint32)), ("rounds", C.c_uint64), ("events", C.c_uint64),
-                ("device_ms", C.c_double), ("error", C.c_uint32)]
+                ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64)]
 
 
 _SIGS = {

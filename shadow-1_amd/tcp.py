@@ -91,7 +91,8 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
                    next_event_id=np.ctypeslib.as_array(r.next_event_id, shape=(H,)).copy(),
                    next_packet_id=np.ctypeslib.as_array(r.next_packet_id, shape=(H,)).copy(),
                    rng_probe=np.ctypeslib.as_array(r.rng_probe, shape=(H,)).copy(),
-                   rounds=int(r.rounds), events=int(r.events), device_ms=float(r.device_ms))
+                   rounds=int(r.rounds), events=int(r.events), deliveries=int(r.deliveries),
+                   device_ms=float(r.device_ms))
     finally:
         S.lib().shd_tcp_result_free(res)
     return out

@@ -298,3 +298,28 @@ def config_model(xml: bytes, *, load=16, payload=1, seed=1, trace=False, topolog
                       payload=payload, trace=trace, host_heartbeat=hb,
                       queue_flags=S.SHD_QF_NO_APP_START | caps.pop("queue_flags", 0), **caps)
     return g, m, pushes, [h["name"] for h in hosts], ips
+
+
+def tcp_echo_model(n_hosts: int, n_vertices: int, *, seed: int = 1, end_s: int = 20, nbytes: int = 100000,
+                   loss_max: float = 0.0, bw_down=10240, bw_up=10240):
+    """The TCP path's scaled model (include/shdtcp.h): the reference's TCP echo
+    test (src/test/tcp/test_tcp.c, nonblocking-epoll) run by n_hosts / 2
+    client/server pairs on a random geometric topology.  Host h sits on vertex
+    h * V // H; even hosts run a server from 1 s; the client on host 2i + 1
+    starts at 2 s + i us and connects to the server of pair (i + n/2) mod n,
+    so connections cross the graph.  Addresses are 11.0.0.1 upwards (no .0 /
+    .255 octet, as dns.c hands them out).  Returns (graph, model, ips, procs,
+    peers, nbytes)."""
+    H = int(n_hosts) & ~1
+    n = H // 2
+    g = geometric_graph(n_vertices, seed=seed, loss_max=loss_max)
+    hv = (np.arange(H, dtype=np.int64) * n_vertices // H).astype(np.int32)
+    m = phold_model(hv, end_time=end_s * S.SHD_SEC, seed=seed, load=0, bw_down=bw_down, bw_up=bw_up)
+    ips, ip = [], (11 << 24) + 1
+    while len(ips) < H:
+        if (ip & 255) not in (0, 255):
+            ips.append(ip)
+        ip += 1
+    procs = [(2 * i, S.SHD_SEC) for i in range(n)] + [(2 * i + 1, 2 * S.SHD_SEC + i * 1000) for i in range(n)]
+    peers = [-1] * n + [(i + n // 2) % n for i in range(n)]
+    return g, m, ips, procs, peers, nbytes

@@ -303,16 +303,17 @@ class TcpCfg(C.Structure):
                 ("proc_peer", C.POINTER(C.c_int32)),
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
-                ("tcp_window", C.c_uint32)]
+                ("tcp_window", C.c_uint32), ("no_lines", C.c_uint32), ("_pad", C.c_uint32)]
 
 
 class TcpOut(C.Structure):
     _fields_ = [("lines", C.c_char_p), ("len", C.c_size_t), ("n_lines", C.c_uint64),
                 ("next_event_id", C.POINTER(C.c_uint64)), ("next_packet_id", C.POINTER(C.c_uint64)),
-                ("rng_probe", C.POINTER(C.c_uint32))]
+                ("rng_probe", C.POINTER(C.c_uint32)), ("events", C.c_uint64)]
 
 
-def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf=131072, tcp_window=10):
+def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf=131072, tcp_window=10,
+            lines=True):
     """The oracle's TCP echo run (o_tcp.c) on the model's hosts: procs = [(host,
     start)], peers = [-1 | server process]; ips: host-order uint32 per host.
     Returns dict(lines=[(t, h, line)], next_event_id, next_packet_id, rng_probe)
@@ -346,6 +347,7 @@ def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf
     cfg.recv_buf = recv_buf
     cfg.send_buf = send_buf
     cfg.tcp_window = tcp_window
+    cfg.no_lines = 0 if lines else 1
     out = TcpOut()
     l = lib()
     l.o_tcp_run.argtypes = [C.POINTER(TcpCfg), C.c_void_p, C.POINTER(TcpOut)]
@@ -366,7 +368,8 @@ def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf
         res = dict(lines=lines,
                    next_event_id=np.ctypeslib.as_array(out.next_event_id, shape=(H,)).copy(),
                    next_packet_id=np.ctypeslib.as_array(out.next_packet_id, shape=(H,)).copy(),
-                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy())
+                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy(),
+                   events=int(out.events))
         l.o_tcp_free(C.byref(out))
     finally:
         lib().o_topo_free(topo)

@@ -17,8 +17,8 @@ def declared():
     return out
 
 
-def exported():
-    out = subprocess.run(["nm", "-D", "--defined-only", S.LIB_PATH], capture_output=True, text=True,
+def exported(path=None):
+    out = subprocess.run(["nm", "-D", "--defined-only", path or S.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
     return {l.split()[-1] for l in out.splitlines() if l.split()[-1].startswith("shd_")}
 
@@ -32,6 +32,13 @@ def test_every_declared_symbol_is_exported_and_bound():
     assert d, "no declarations parsed"
     assert d == e, (d - e, e - d)
     assert d == set(S.exported_symbols())
+
+
+def test_test_hook_build_exports_the_same_abi():
+    # tests/hook_worker.py and xgroup_worker.py load the test build in place of
+    # the product library: it must bind every symbol shdgpu.lib() binds
+    th = os.path.join(os.path.dirname(S.LIB_PATH), "libshdgpu_th.so")
+    assert exported(th) == exported()
 
 
 def test_code_object_targets_gfx950():

@@ -36,3 +36,20 @@ def test_tcp_gpu_equals_reference(name):
     assert r["next_packet_id"].tolist() == f["next_packet_id"]
     assert r["rng_probe"].tolist() == f["rng_probe"]
     assert r["rounds"] > 0 and r["events"] > 0
+
+
+@pytest.mark.parametrize("hosts,loss", [(64, 0.0), (96, 0.02)])
+def test_tcp_gpu_scaled_model_equals_oracle(hosts, loss):
+    """bench.py --workload tcp's model (workloads.tcp_echo_model) at a size the
+    oracle runs in a second: every host's [STATUS] lines and end state equal
+    the oracle's (oracle/o_tcp.c, pinned above to the reference's tcp.c loop)."""
+    import workloads as W
+    g, m, ips, procs, peers, nb = W.tcp_echo_model(hosts, 40, end_s=12, nbytes=60000, loss_max=loss)
+    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb)
+    o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb)
+    want = TC.by_host(o["lines"])
+    assert len(r["lines"]) == len(want) and r["lines"] == want
+    assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
+    assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
+    assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
+    assert r["events"] == o["events"] and r["deliveries"] > 0
