@@ -7,6 +7,8 @@ O=gpurun_out/r03t
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_tcp_gpu.py -x -v --timeout 120 --timeout-method thread > $O/tcp_tests.log 2>&1 || { tail -30 $O/tcp_tests.log; exit 1; }
 tail -2 $O/tcp_tests.log
+timeout -k 10 300 python3 bench.py --workload tcp --hosts-per-gpu 512 --steps 1 --warmup 0 --no-cpu-baseline > $O/tcp_bench512.json 2> $O/tcp_bench512.err || { tail $O/tcp_bench512.err; exit 2; }
+cat $O/tcp_bench512.json
 timeout -k 10 600 python3 bench.py --workload tcp --steps 2 --warmup 1 > $O/tcp_bench.json 2> $O/tcp_bench.err || { tail $O/tcp_bench.err; exit 2; }
 cat $O/tcp_bench.json
 for L in 1 4 16; do

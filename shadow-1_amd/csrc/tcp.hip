@@ -893,7 +893,9 @@ __device__ void tcp_about_to_send(L& c, DSock* k, int32_t pi) {
 // _tcp_flush (tcp.c:1121-1278).  The FIN it may send flushes again; that
 // inner flush reaches its own FIN step in FINWAIT1 / LASTACK, where
 // _tcp_sendShutdownFin sends nothing, so the inner pass only clears the flag.
-__device__ void tcp_flush_body(L& c, DSock* k, bool outer);
+// Outer and inner flush are separate instantiations: the call graph has no
+// cycle, so the compiler sizes every lane's stack exactly (no dynamic stack).
+template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k);
 __device__ void tcp_send_shutdown_fin(L& c, DSock* k, bool from_flush) {   // tcp.c:1067-1088
     bool send = false;
     if (k->state == TS_ESTABLISHED || k->state == TS_SYNRECEIVED) { tcp_set_state(c, k, TS_FINWAIT1); send = true; }
@@ -902,11 +904,11 @@ __device__ void tcp_send_shutdown_fin(L& c, DSock* k, bool from_flush) {   // tc
         const int32_t fin = tcp_create_packet(c, k, F_FIN, 0);
         if (fin < 0) return;
         tcp_buffer_out(c, k, fin);
-        tcp_flush_body(c, k, false);
+        tcp_flush_body<false>(c, k);
         pkt_unref(c, fin);
     }
 }
-__device__ void tcp_flush_body(L& c, DSock* k, bool outer) {
+template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
     tcp_update_rcv_window(k);
     tcp_update_snd_window(k);
     const uint32_t nl = k->tally.lost.n;
@@ -950,7 +952,7 @@ __device__ void tcp_flush_body(L& c, DSock* k, bool outer) {
         break;
     }
     if ((k->flags & TF_SHOULD_SEND_WR_FIN) && tcp_out_len(k) == 0) {
-        if (outer) tcp_send_shutdown_fin(c, k, true);
+        if (kOuter) tcp_send_shutdown_fin(c, k, true);
         k->flags &= ~TF_SHOULD_SEND_WR_FIN;
     }
     if ((k->flags & TF_LOCAL_CLOSED_WR) || (k->error & TE_CONNECTION_RESET)) k->error |= TE_SEND_EOF;
@@ -965,7 +967,7 @@ __device__ void tcp_flush_body(L& c, DSock* k, bool outer) {
     else if (space_out(k) <= 0) sock_status(c, k, DS_WRITABLE, false);
     else sock_status(c, k, DS_WRITABLE, true);
 }
-__device__ __forceinline__ void tcp_flush(L& c, DSock* k) { tcp_flush_body(c, k, true); }
+__device__ __forceinline__ void tcp_flush(L& c, DSock* k) { tcp_flush_body<true>(c, k); }
 __device__ void tcp_send_control(L& c, DSock* k, uint32_t flags) {   // tcp.c:837-852
     const int32_t ci = tcp_create_packet(c, k, flags, 0);
     if (ci < 0) return;

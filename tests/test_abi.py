@@ -59,3 +59,15 @@ def test_no_oracle_on_product_path():
             if f.endswith((".py", ".c", ".h", ".hip", ".cpp")):
                 src = open(os.path.join(root, f), errors="ignore").read()
                 assert "oracle_ffi" not in src and "liboracle" not in src, f
+
+
+def test_no_kernel_uses_a_dynamic_stack():
+    # a recursive or indirect device call makes the compiler under-size a
+    # lane's scratch (the runtime then allocates the static estimate only);
+    # every kernel's AMDGPU metadata must say its stack size is exact
+    import re
+    blob = open(S.LIB_PATH, "rb").read()
+    key = b".uses_dynamic_stack"
+    vals = [blob[m.end():m.end() + 1] for m in re.finditer(re.escape(key), blob)]
+    assert vals, "no kernel metadata found"
+    assert set(vals) == {b"\xc2"}, "a kernel uses a dynamic stack (msgpack true)"
