@@ -1776,15 +1776,22 @@ __global__ void k_tcp_window(Glob g) {
 // one conservative round: the mailbox's deliveries for this host, then every
 // event before the window's end
 __global__ void k_tcp_round(Glob g) {
+    // the round's view of the globals is uniform: one copy in LDS that every
+    // lane's c.g reads by broadcast (a per-lane copy would live in scratch)
+    __shared__ Glob gl;
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (h >= g.H || g.ctl->halted) return;
+    if (g.ctl->halted) return;   // uniform: read before any lane diverges
     const uint64_t k = g.ctl->rounds - 1, wend = g.ctl->wend;
     const uint32_t in = (uint32_t)(k & 1), out = in ^ 1u;
-    Glob gl = g;
-    gl.mail_in = g.mail + (size_t)in * kMail; gl.mhead_in = g.mhead + (size_t)in * g.H;
-    gl.mnext_in = g.mnext + (size_t)in * kMail;
-    gl.mail_out = g.mail + (size_t)out * kMail; gl.n_out = g.nmail + out;
-    gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * kMail;
+    if (threadIdx.x == 0) {
+        gl = g;
+        gl.mail_in = g.mail + (size_t)in * kMail; gl.mhead_in = g.mhead + (size_t)in * g.H;
+        gl.mnext_in = g.mnext + (size_t)in * kMail;
+        gl.mail_out = g.mail + (size_t)out * kMail; gl.n_out = g.nmail + out;
+        gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * kMail;
+    }
+    __syncthreads();
+    if (h >= g.H) return;
     L c{&gl, h, &gl.host[h], 0, h};
     // this host's deliveries (any order: the heap's key (time, src, seq) is unique)
     int32_t s = gl.mhead_in[h];
