@@ -444,10 +444,11 @@ def tcp_main(args):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload tcp runs on one GPU (replicas only)")
     torch.cuda.set_device(0)
-    H = args.hosts_per_gpu or 4096
+    H = args.hosts_per_gpu or 16384
     V = min(args.vertices, 1000)
-    g, m, ips, procs, peers, nb = W.tcp_echo_model(H, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,
-                                                  loss_max=args.edge_loss_max)
+    mk = lambda n: W.tcp_echo_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,  # noqa: E731
+                                    loss_max=args.edge_loss_max)
+    g, m, ips, procs, peers, nb = mk(H)
     for _ in range(args.warmup):
         T.run(m, g, ips, procs, peers, nbytes=nb, trace=False)
     mark = Roctx()
@@ -473,16 +474,24 @@ def tcp_main(args):
     achieved = alg / (r["device_ms"] / 1e3) / 1e9
     cpu = None
     if not args.no_cpu_baseline:
+        # bounded sample: the same model at min(H, 4096) hosts (the same
+        # per-pair work); the GPU runs that sample too, and the end states of
+        # every host must agree
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
         import oracle_ffi as O
+        hs = min(H, 4096)
+        gs, ms, ipss, pss, prs, _ = mk(hs) if hs != H else (g, m, ips, procs, peers, nb)
+        rs = T.run(ms, gs, ipss, pss, prs, nbytes=nb, trace=False) if hs != H else r
         tc = time.perf_counter()
-        o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb, lines=False)
+        o = O.tcp_run(ms, gs, ipss, pss, prs, nbytes=nb, lines=False)
         cs = time.perf_counter() - tc
-        same = (o["events"] == r["events"] and o["next_event_id"].tolist() == r["next_event_id"].tolist()
-                and o["rng_probe"].tolist() == r["rng_probe"].tolist())
+        same = (o["events"] == rs["events"] and o["next_event_id"].tolist() == rs["next_event_id"].tolist()
+                and o["next_packet_id"].tolist() == rs["next_packet_id"].tolist()
+                and o["rng_probe"].tolist() == rs["rng_probe"].tolist())
         cpu = {"value": round(o["events"] / cs, 1), "unit": "TCP events/s", "cores": 1, "kind": "port",
-               "sample": "oracle/o_tcp.c serial loop (pinned to the reference's tcp.c loop) on the same model, "
-                         "[STATUS] lines off: %d events in %.2f s" % (o["events"], cs),
+               "sample": "oracle/o_tcp.c serial loop (pinned to the reference's tcp.c loop), [STATUS] lines off, "
+                         "on the same model at %d hosts: %d events in %.2f s" % (hs, o["events"], cs),
+               "gpu_sample_value": round(rs["events"] / (rs["device_ms"] / 1e3), 1),
                "same_end_state_as_gpu": bool(same)}
     out = {
         "metric": "simulated TCP events/sec", "value": round(events / dev_s, 1), "unit": "events/s",

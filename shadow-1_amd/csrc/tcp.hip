@@ -58,7 +58,7 @@ constexpr uint32_t kTimers = 256;   // pending RTO timer expirations
 constexpr uint32_t kSacks = 512;    // the receiver's SACK list
 constexpr uint32_t kRanges = 64;    // tally ranges per set
 constexpr uint32_t kKids = 8;
-constexpr uint32_t kPool = 16384;   // packets per host
+constexpr uint32_t kPool = 8192;    // packets per host (buffered, in flight, queued for retransmission)
 constexpr uint32_t kPktSack = 128;  // SACK entries carried by one segment (the receive window's holes)
 constexpr uint32_t kSt = 96;        // delivery statuses a packet's line lists (each loss retransmission adds 6)
 constexpr uint32_t kEv = 8192;      // events per host
@@ -1722,7 +1722,7 @@ __global__ void k_tcp_free_init(int32_t* freel, size_t n) {
 
 // host_boot at t = 0 (host.c:372-390): heartbeat, the ethernet refill inline,
 // the loopback refill at +1 ms, then each process's start task
-__global__ void k_tcp_boot(Glob g) {
+__global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (h >= g.H) return;
     Glob gl = g;
@@ -1775,7 +1775,7 @@ __global__ void k_tcp_window(Glob g) {
 
 // one conservative round: the mailbox's deliveries for this host, then every
 // event before the window's end
-__global__ void k_tcp_round(Glob g) {
+__global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
     // the round's view of the globals is uniform: one copy in LDS that every
     // lane's c.g reads by broadcast (a per-lane copy would live in scratch)
     __shared__ Glob gl;
