@@ -66,6 +66,8 @@ def parse():
                          "TCP path (include/shdtcp.h) on workloads.tcp_echo_model, one run per step")
     ap.add_argument("--tcp-bytes", type=int, default=500000, help="tcp: bytes each client echoes")
     ap.add_argument("--tcp-end-s", type=int, default=20, help="tcp: simulated seconds")
+    ap.add_argument("--tcp-pool", type=int, default=2048,
+                    help="tcp: packet pool per host (shd_tcp_model.packets_per_host; overflow fails the run)")
     ap.add_argument("--relays", type=int, default=6500)
     ap.add_argument("--clients", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -444,20 +446,21 @@ def tcp_main(args):
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--workload tcp runs on one GPU (replicas only)")
     torch.cuda.set_device(0)
-    H = args.hosts_per_gpu or 16384
+    H = args.hosts_per_gpu or 65536
+    pool = args.tcp_pool
     V = min(args.vertices, 1000)
     mk = lambda n: W.tcp_echo_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,  # noqa: E731
                                     loss_max=args.edge_loss_max)
     g, m, ips, procs, peers, nb = mk(H)
     for _ in range(args.warmup):
-        T.run(m, g, ips, procs, peers, nbytes=nb, trace=False)
+        T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool)
     mark = Roctx()
     runs = []
     torch.cuda.synchronize()
     mark.push("shd_timed_region")
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        runs.append(T.run(m, g, ips, procs, peers, nbytes=nb, trace=False))
+        runs.append(T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool))
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     mark.pop()
@@ -481,7 +484,7 @@ def tcp_main(args):
         import oracle_ffi as O
         hs = min(H, 4096)
         gs, ms, ipss, pss, prs, _ = mk(hs) if hs != H else (g, m, ips, procs, peers, nb)
-        rs = T.run(ms, gs, ipss, pss, prs, nbytes=nb, trace=False) if hs != H else r
+        rs = T.run(ms, gs, ipss, pss, prs, nbytes=nb, trace=False, packets_per_host=pool) if hs != H else r
         tc = time.perf_counter()
         o = O.tcp_run(ms, gs, ipss, pss, prs, nbytes=nb, lines=False)
         cs = time.perf_counter() - tc
@@ -502,7 +505,8 @@ def tcp_main(args):
         "config": {"workload": "TCP echo (src/test/tcp/test_tcp.c, nonblocking-epoll), %d hosts / %d pairs, "
                                "%d-vertex geometric topology, %d B each way, %d s simulated"
                                % (H, H // 2, V, nb, args.tcp_end_s),
-                   "hosts": H, "vertices": V, "parallelism": "one lane per host, 1 GPU"},
+                   "hosts": H, "vertices": V, "packets_per_host": pool,
+                   "parallelism": "one lane per host, 1 GPU"},
         "packet_deliveries_per_s": round(deliv / dev_s, 1), "wall_s": round(wall, 3),
         "rounds": r["rounds"], "events_per_run": r["events"], "deliveries_per_run": r["deliveries"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": 8000.0, "unit": "GB/s",

@@ -33,8 +33,11 @@ typedef struct shd_tcp_model {
     const uint32_t* host_seed;        /* [H] host RNG state after attach                */
     const uint64_t* bw_down_kibps;    /* [H]                                            */
     const uint64_t* bw_up_kibps;      /* [H]                                            */
-    const double* path_lat_ms;        /* [H*H] src*H + dst; < 0: no route               */
-    const double* path_rel;           /* [H*H]                                          */
+    int32_t n_vertices;               /* V: the attached vertices the tables index      */
+    const int32_t* host_vertex;       /* [H] each host's vertex index in [0, V)         */
+    const double* path_lat_ms;        /* [V*V] src_vertex*V + dst_vertex; < 0: no route
+                                         (pairs no host pair uses may be left < 0)       */
+    const double* path_rel;           /* [V*V]                                          */
     const int32_t* proc_host;         /* [P] the host of each process, <process> order  */
     const uint64_t* proc_start;       /* [P] start time (ns)                            */
     const int32_t* proc_peer;         /* [P] -1: server; else the server process index  */
@@ -43,6 +46,8 @@ typedef struct shd_tcp_model {
     uint32_t tcp_bytes;               /* bytes each client sends (test_tcp.c BUFFERSIZE) */
     uint32_t recv_buf, send_buf;      /* initial socket buffers (CONFIG_*_BUFFER_SIZE)   */
     uint32_t tcp_window;              /* --tcp-windows (options.c:79)                    */
+    uint32_t packets_per_host;        /* packet pool per host (0: 8192); more live packets
+                                         set SHD_TCP_ERR_POOL                             */
 } shd_tcp_model;
 
 typedef struct shd_tcp_result {

@@ -58,7 +58,7 @@ constexpr uint32_t kTimers = 256;   // pending RTO timer expirations
 constexpr uint32_t kSacks = 512;    // the receiver's SACK list
 constexpr uint32_t kRanges = 64;    // tally ranges per set
 constexpr uint32_t kKids = 8;
-constexpr uint32_t kPool = 8192;    // packets per host (buffered, in flight, queued for retransmission)
+constexpr uint32_t kPoolDefault = 8192;   // packets per host (buffered, in flight, queued for retransmission)
 constexpr uint32_t kPktSack = 128;  // SACK entries carried by one segment (the receive window's holes)
 constexpr uint32_t kSt = 96;        // delivery statuses a packet's line lists (each loss retransmission adds 6)
 constexpr uint32_t kEv = 8192;      // events per host
@@ -198,8 +198,10 @@ struct Glob {
     DSock* sock;            // [H][kSock]
     DProc* proc;            // [P]
     int32_t* host_procs;    // [H][kProcs]
-    DPkt* pool;             // [H][kPool]
-    int32_t* freel;         // [H][kPool]
+    DPkt* pool;             // [H][pool_cap]
+    int32_t* freel;         // [H][pool_cap]
+    const int32_t* hv;      // [H] host -> vertex (the path tables' index)
+    int32_t V; uint32_t pool_cap;
     DEv* ev;                // [H][kEv]
     CqEnt* cq;              // [H][kCq]
     Mail* mail;             // [2][kMail] the two mailboxes (a round's input, its output)
@@ -223,7 +225,7 @@ struct L {
     uint64_t now;
     int32_t active;
 };
-__device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * kPool + i]; }
+__device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * c.g->pool_cap + i]; }
 __device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
 
 __device__ int32_t rand_r_dev(uint32_t* state) {   // glibc rand_r (random.c's source)
@@ -378,7 +380,7 @@ __device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDelive
 __device__ int32_t pkt_alloc(L& c) {
     DHost* H = c.H;
     if (!H->nfree) { H->err |= SHD_TCP_ERR_POOL; return -1; }
-    return c.g->freel[(size_t)c.h * kPool + --H->nfree];
+    return c.g->freel[(size_t)c.h * c.g->pool_cap + --H->nfree];
 }
 __device__ int32_t pkt_new(L& c, uint32_t len) {   // packet_new (packet.c:74-95)
     const int32_t i = pkt_alloc(c);
@@ -397,7 +399,7 @@ __device__ void pkt_unref(L& c, int32_t i) {   // packet.c:194-201
     DPkt* p = PK(c, i);
     if (--p->refs == 0) {
         pkt_status(c, i, S_DESTROYED);
-        c.g->freel[(size_t)c.h * kPool + c.H->nfree++] = i;
+        c.g->freel[(size_t)c.h * c.g->pool_cap + c.H->nfree++] = i;
     }
 }
 
@@ -515,8 +517,9 @@ __device__ int32_t host_of_ip(const L& c, uint32_t ip) {
     return (lo < (uint32_t)c.g->H && (uint32_t)(k[lo] >> 32) == ip) ? (int32_t)(uint32_t)k[lo] : -1;
 }
 __device__ void path(const L& c, int32_t a, int32_t b, double& lat, double& rel) {
-    lat = c.g->lat[(size_t)a * c.g->H + b];
-    rel = c.g->rel[(size_t)a * c.g->H + b];
+    const size_t i = (size_t)c.g->hv[a] * (size_t)c.g->V + (size_t)c.g->hv[b];
+    lat = c.g->lat[i];
+    rel = c.g->rel[i];
 }
 
 // ------------------------------------------------------------ retransmit queue
@@ -826,7 +829,7 @@ __device__ void tcp_autotune_snd(L& c, DSock* k) {   // tcp.c:566-591
 }
 __device__ void tcp_buffer_out(L& c, DSock* k, int32_t pi) {   // tcp.c:729-745
     if (ih_find(k->throttled, pi) >= 0) return;
-    ih_push(k->throttled, pi, SeqLess{c.g->pool + (size_t)c.h * kPool}, c.H->err);
+    ih_push(k->throttled, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err);
     pkt_ref(c, pi);
     k->throttled_len += PK(c, pi)->len;
     if (space_out(k) == 0) sock_status(c, k, DS_WRITABLE, false);
@@ -834,7 +837,7 @@ __device__ void tcp_buffer_out(L& c, DSock* k, int32_t pi) {   // tcp.c:729-745
 }
 __device__ void tcp_buffer_in(L& c, DSock* k, int32_t pi) {   // tcp.c:747-760
     if (ih_find(k->unordered, pi) >= 0) return;
-    ih_push(k->unordered, pi, SeqLess{c.g->pool + (size_t)c.h * kPool}, c.H->err);
+    ih_push(k->unordered, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err);
     pkt_ref(c, pi);
     k->unordered_len += PK(c, pi)->len;
     pkt_status(c, pi, S_RCV_TCP_ENQUEUE_UNORDERED);
@@ -921,7 +924,7 @@ template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
             tally_compute_lost(k->tally, c.H->err);
         }
     }
-    const SeqLess lt{c.g->pool + (size_t)c.h * kPool};
+    const SeqLess lt{c.g->pool + (size_t)c.h * c.g->pool_cap};
     while (k->throttled.n) {
         const int32_t pi = k->throttled.a[0];
         DPkt* p = PK(c, pi);
@@ -1715,9 +1718,9 @@ __device__ void execute(L& c, const DEv& e) {
 }
 
 // every host's packet free list: pops 0, 1, 2, ...
-__global__ void k_tcp_free_init(int32_t* freel, size_t n) {
+__global__ void k_tcp_free_init(int32_t* freel, size_t n, uint32_t cap) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) freel[i] = (int32_t)(kPool - 1 - (uint32_t)(i % kPool));
+    if (i < n) freel[i] = (int32_t)(cap - 1 - (uint32_t)(i % cap));
 }
 
 // host_boot at t = 0 (host.c:372-390): heartbeat, the ethernet refill inline,
@@ -1881,23 +1884,36 @@ int32_t rand_r_host(uint32_t* state) {
 
 extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
     if (!m || !out || m->n_hosts <= 0 || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
-        !m->bw_up_kibps || !m->path_lat_ms || !m->path_rel || (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
+        !m->bw_up_kibps || !m->path_lat_ms || !m->path_rel || !m->host_vertex || m->n_vertices <= 0 ||
+        (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
         return -22;
     const int32_t H = m->n_hosts, P = m->n_procs;
     for (int32_t k = 0; k < P; k++) {
         if (m->proc_host[k] < 0 || m->proc_host[k] >= H) return -22;
         if (m->proc_peer[k] >= P || (m->proc_peer[k] >= 0 && m->proc_peer[m->proc_peer[k]] >= 0)) return -22;
     }
-    // the window: the smallest latency between two different hosts, in ns (ceil, worker.c:293)
+    const int32_t V = m->n_vertices;
+    const uint32_t pool_cap = m->packets_per_host ? m->packets_per_host : kPoolDefault;
+    if (pool_cap > (1u << 24)) return -22;
+    // the window: the smallest latency between two different hosts, in ns
+    // (ceil, worker.c:293), over the vertex pairs some pair of distinct hosts
+    // realizes (a vertex with itself only when two hosts share it)
+    std::vector<int32_t> per_vertex(V, 0);
+    for (int32_t a = 0; a < H; a++) {
+        if (m->host_vertex[a] < 0 || m->host_vertex[a] >= V) return -22;
+        per_vertex[m->host_vertex[a]]++;
+    }
     uint64_t W = ~0ull;
-    for (int32_t a = 0; a < H; a++)
-        for (int32_t b = 0; b < H; b++) {
-            if (a == b) continue;
-            const double l = m->path_lat_ms[(size_t)a * H + b];
+    for (int32_t u = 0; u < V; u++) {
+        if (!per_vertex[u]) continue;
+        for (int32_t v = 0; v < V; v++) {
+            if (!per_vertex[v] || (u == v && per_vertex[u] < 2)) continue;
+            const double l = m->path_lat_ms[(size_t)u * V + v];
             if (l < 0) continue;
             const uint64_t w = (uint64_t)ceil(l * (double)kMs);
             if (w < W) W = w;
         }
+    }
     if (W == 0) return -22;
     if (W == ~0ull) W = m->end_time ? m->end_time : 1;
 
@@ -1909,6 +1925,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     std::vector<int32_t> hp((size_t)H * kProcs, -1);
     shd_tcp_result* res = (shd_tcp_result*)calloc(1, sizeof(shd_tcp_result));
     double* d_lat = nullptr; double* d_rel = nullptr;
+    int32_t* d_hv = nullptr;
     uint64_t* d_ipk = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipStream_t st = nullptr;
@@ -1930,7 +1947,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         x.rx_refill = m->bw_down_kibps[i] * 1024 / 1000;
         x.tx_cap = x.tx_refill + kMTU;
         x.rx_cap = x.rx_refill + kMTU;
-        x.nfree = kPool;
+        x.nfree = pool_cap;
         x.next_handle = 3;
     }
     for (int32_t k = 0; k < P; k++) {
@@ -1951,11 +1968,13 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     g.end_time = m->end_time; g.hb = m->heartbeat_interval ? m->heartbeat_interval : kSec;
     g.tcp_bytes = m->tcp_bytes; g.trace = trace ? 1 : 0;
     g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
-    HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)H * H));
-    HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)H * H));
-    HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)H * H, hipMemcpyHostToDevice));
-    HCHECK(hipMemcpy(d_rel, m->path_rel, sizeof(double) * (size_t)H * H, hipMemcpyHostToDevice));
-    g.lat = d_lat; g.rel = d_rel;
+    HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)V * V));
+    HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)V * V));
+    HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(d_rel, m->path_rel, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
+    HCHECK(hipMalloc(&d_hv, sizeof(int32_t) * (size_t)H));
+    HCHECK(hipMemcpy(d_hv, m->host_vertex, sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
+    g.lat = d_lat; g.rel = d_rel; g.hv = d_hv; g.V = V; g.pool_cap = pool_cap;
     HCHECK(hipMalloc(&g.host, sizeof(DHost) * H));
     HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * H, hipMemcpyHostToDevice));
     HCHECK(hipMalloc(&g.sock, sizeof(DSock) * (size_t)H * kSock));
@@ -1964,9 +1983,9 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMemcpy(g.proc, pp.data(), sizeof(DProc) * pp.size(), hipMemcpyHostToDevice));
     HCHECK(hipMalloc(&g.host_procs, sizeof(int32_t) * hp.size()));
     HCHECK(hipMemcpy(g.host_procs, hp.data(), sizeof(int32_t) * hp.size(), hipMemcpyHostToDevice));
-    HCHECK(hipMalloc(&g.pool, sizeof(DPkt) * (size_t)H * kPool));
-    HCHECK(hipMalloc(&g.freel, sizeof(int32_t) * (size_t)H * kPool));
-    k_tcp_free_init<<<(unsigned)(((size_t)H * kPool + 255) / 256), 256>>>(g.freel, (size_t)H * kPool);
+    HCHECK(hipMalloc(&g.pool, sizeof(DPkt) * (size_t)H * pool_cap));
+    HCHECK(hipMalloc(&g.freel, sizeof(int32_t) * (size_t)H * pool_cap));
+    k_tcp_free_init<<<(unsigned)(((size_t)H * pool_cap + 255) / 256), 256>>>(g.freel, (size_t)H * pool_cap, pool_cap);
     HCHECK(hipGetLastError());
     HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
@@ -2064,7 +2083,7 @@ done:
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
     if (st) (void)hipStreamDestroy(st);
-    (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_ipk);
+    (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_ipk); (void)hipFree(d_hv);
     (void)hipFree(g.mail); (void)hipFree(g.nmail); (void)hipFree(g.mhead); (void)hipFree(g.mnext); (void)hipFree(g.ctl);
     (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
     (void)hipFree(g.pool); (void)hipFree(g.freel); (void)hipFree(g.ev); (void)hipFree(g.cq);

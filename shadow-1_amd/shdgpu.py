@@ -179,11 +179,12 @@ class TcpModel(C.Structure):
     _fields_ = [("n_hosts", C.c_int32), ("n_procs", C.c_int32),
                 ("host_ip", P(C.c_uint32)), ("host_seed", P(C.c_uint32)),
                 ("bw_down_kibps", P(C.c_uint64)), ("bw_up_kibps", P(C.c_uint64)),
+                ("n_vertices", C.c_int32), ("host_vertex", P(C.c_int32)),
                 ("path_lat_ms", P(C.c_double)), ("path_rel", P(C.c_double)),
                 ("proc_host", P(C.c_int32)), ("proc_start", P(C.c_uint64)), ("proc_peer", P(C.c_int32)),
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
-                ("tcp_window", C.c_uint32)]
+                ("tcp_window", C.c_uint32), ("packets_per_host", C.c_uint32)]
 
 
 class TcpResult(C.Structure):

@@ -23,37 +23,40 @@ TCP_WINDOW = 10     # --tcp-windows default (options.c:79)
 
 
 def path_table(model: S.ModelArrays, g: S.GraphArrays, procs, peers):
-    """[H, H] latency (ms) and reliability per host pair from the path cache,
-    pairs resolved in first-touch order (clients by start time); pairs that
-    never talk stay -1."""
+    """Latency (ms) and reliability per pair of attached vertices ([V, V],
+    V = the distinct vertices the hosts sit on) from the path cache, pairs
+    resolved in first-touch order (clients by start time); pairs no
+    connection uses stay -1.  Returns (lat, rel, host -> vertex index)."""
     m = model.struct
     H = int(m.n_hosts)
     hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
-    pc = sim.PathCache(g, np.unique(hv))
-    lat = np.full((H, H), -1.0)
-    rel = np.full((H, H), -1.0)
+    att, hvi = np.unique(hv, return_inverse=True)
+    V = len(att)
+    pc = sim.PathCache(g, att)
+    lat = np.full((V, V), -1.0)
+    rel = np.full((V, V), -1.0)
     order = sorted((p[1], k) for k, p in enumerate(procs) if peers[k] >= 0)
     try:
         for _, k in order:
-            a, b = procs[k][0], procs[peers[k]][0]
+            a, b = hvi[procs[k][0]], hvi[procs[peers[k]][0]]
             for s, d in ((a, b), (b, a)):
                 if lat[s, d] < 0:
-                    lat[s, d], rel[s, d] = pc.lookup(hv[s], hv[d])
+                    lat[s, d], rel[s, d] = pc.lookup(att[s], att[d])
     finally:
         pc.close()
-    return lat, rel
+    return lat, rel, hvi.astype(np.int32)
 
 
 def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000, trace=True,
-        recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW):
+        recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0):
     """Run the TCP echo model on the GPU: procs = [(host, start ns)], peers =
     [-1 | server process]; ips: host-order uint32 per host.  Returns
     dict(lines=[(t, h, line)] in each host's order, next_event_id,
     next_packet_id, rng_probe, rounds, events, device_ms)."""
     m = model.struct
     H = int(m.n_hosts)
-    lat, rel = path_table(model, g, procs, peers)
-    keep = dict(ip=np.ascontiguousarray(ips, dtype=np.uint32),
+    lat, rel, hvi = path_table(model, g, procs, peers)
+    keep = dict(ip=np.ascontiguousarray(ips, dtype=np.uint32), hv=np.ascontiguousarray(hvi),
                 lat=np.ascontiguousarray(lat), rel=np.ascontiguousarray(rel),
                 ph=np.ascontiguousarray([p[0] for p in procs], dtype=np.int32),
                 ps=np.ascontiguousarray([p[1] for p in procs], dtype=np.uint64),
@@ -65,6 +68,8 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
     tm.host_seed = m.host_rng
     tm.bw_down_kibps = m.bw_down_kibps
     tm.bw_up_kibps = m.bw_up_kibps
+    tm.n_vertices = lat.shape[0]
+    tm.host_vertex = S.as_ptr(keep["hv"], C.c_int32)
     tm.path_lat_ms = S.as_ptr(keep["lat"], C.c_double)
     tm.path_rel = S.as_ptr(keep["rel"], C.c_double)
     tm.proc_host = S.as_ptr(keep["ph"], C.c_int32)
@@ -76,6 +81,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
     tm.recv_buf = recv_buf
     tm.send_buf = send_buf
     tm.tcp_window = tcp_window
+    tm.packets_per_host = packets_per_host
     res = C.POINTER(S.TcpResult)()
     S.check(S.lib().shd_tcp_run(C.byref(tm), 1 if trace else 0, C.byref(res)), "shd_tcp_run")
     try:

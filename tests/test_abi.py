@@ -71,3 +71,18 @@ def test_no_kernel_uses_a_dynamic_stack():
     vals = [blob[m.end():m.end() + 1] for m in re.finditer(re.escape(key), blob)]
     assert vals, "no kernel metadata found"
     assert set(vals) == {b"\xc2"}, "a kernel uses a dynamic stack (msgpack true)"
+
+
+def test_tcp_struct_layout_matches_the_header(tmp_path):
+    # the ctypes mirrors of shd_tcp_model / shd_tcp_result against gcc's layout
+    import ctypes as C
+    src = tmp_path / "l.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s/include/shdtcp.h"\n'
+                   'int main(void){printf("%%zu %%zu %%zu %%zu %%zu\\n", sizeof(shd_tcp_model),'
+                   ' offsetof(shd_tcp_model, host_vertex), offsetof(shd_tcp_model, packets_per_host),'
+                   ' sizeof(shd_tcp_result), offsetof(shd_tcp_result, deliveries));return 0;}\n' % REPO)
+    exe = tmp_path / "l"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [C.sizeof(S.TcpModel), S.TcpModel.host_vertex.offset, S.TcpModel.packets_per_host.offset,
+                   C.sizeof(S.TcpResult), S.TcpResult.deliveries.offset]
