@@ -65,7 +65,7 @@ constexpr uint32_t kEv = 8192;      // events per host
 constexpr uint32_t kCq = 4096;      // CoDel queue per host
 constexpr uint32_t kTr = 1u << 16;  // trace records per host
 constexpr uint32_t kTrSack = 1u << 20;
-constexpr uint32_t kMail = 1u << 16;
+constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 16 per host)
 
 // ProtocolTCPFlags (protocol.h:23-31)
 enum : uint32_t { F_RST = 1 << 1, F_SYN = 1 << 2, F_ACK = 1 << 3, F_SACK = 1 << 4, F_FIN = 1 << 5, F_DUPACK = 1 << 6 };
@@ -204,10 +204,11 @@ struct Glob {
     int32_t V; uint32_t pool_cap;
     DEv* ev;                // [H][kEv]
     CqEnt* cq;              // [H][kCq]
-    Mail* mail;             // [2][kMail] the two mailboxes (a round's input, its output)
+    Mail* mail;             // [2][mail_cap] the two mailboxes (a round's input, its output)
     uint32_t* nmail;        // [2] their fill counts
     int32_t* mhead;         // [2][H] each destination's list of mails (-1: none)
-    int32_t* mnext;         // [2][kMail] the next mail of the same destination
+    int32_t* mnext;         // [2][mail_cap] the next mail of the same destination
+    uint32_t mail_cap, _pad2;
     TCtl* ctl;
     const uint64_t* ip_key; // [H] (ip << 32 | host) ascending: host_of_ip's table
     Mail* mail_in; int32_t* mhead_in; int32_t* mnext_in;     // a lane's view of the round
@@ -1340,7 +1341,7 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
         if (t >= c.g->end_time) return;
         if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
         const uint32_t slot = atomicAdd(c.g->n_out, 1u);
-        if (slot >= kMail) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+        if (slot >= c.g->mail_cap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
         Mail* m = &c.g->mail_out[slot];
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
         m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
@@ -1788,10 +1789,10 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
     const uint32_t in = (uint32_t)(k & 1), out = in ^ 1u;
     if (threadIdx.x == 0) {
         gl = g;
-        gl.mail_in = g.mail + (size_t)in * kMail; gl.mhead_in = g.mhead + (size_t)in * g.H;
-        gl.mnext_in = g.mnext + (size_t)in * kMail;
-        gl.mail_out = g.mail + (size_t)out * kMail; gl.n_out = g.nmail + out;
-        gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * kMail;
+        gl.mail_in = g.mail + (size_t)in * g.mail_cap; gl.mhead_in = g.mhead + (size_t)in * g.H;
+        gl.mnext_in = g.mnext + (size_t)in * g.mail_cap;
+        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + out;
+        gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * g.mail_cap;
     }
     __syncthreads();
     if (h >= g.H) return;
@@ -1883,7 +1884,7 @@ int32_t rand_r_host(uint32_t* state) {
 }  // namespace
 
 extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
-    if (!m || !out || m->n_hosts <= 0 || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
+    if (!m || !out || m->n_hosts <= 0 || m->n_hosts > (1 << 26) || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
         !m->bw_up_kibps || !m->path_lat_ms || !m->path_rel || !m->host_vertex || m->n_vertices <= 0 ||
         (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
         return -22;
@@ -1989,12 +1990,13 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipGetLastError());
     HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
-    HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)kMail));
+    g.mail_cap = (uint32_t)H * 16u > kMailMin ? (uint32_t)H * 16u : kMailMin;
+    HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
     HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2));
     HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2));
     HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
-    HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)kMail));
+    HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
     HCHECK(hipMalloc(&g.ctl, sizeof(TCtl)));
     HCHECK(hipMemset(g.ctl, 0, sizeof(TCtl)));
     HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * (size_t)H));
