@@ -82,6 +82,7 @@ const char* const kStatusName[] = {
     "ROUTER_ENQUEUED", "ROUTER_DEQUEUED", "ROUTER_DROPPED", "RCV_INTERFACE_RECEIVED", "RCV_INTERFACE_DROPPED",
     "RCV_SOCKET_PROCESSED", "RCV_SOCKET_DROPPED", "RCV_TCP_ENQUEUE_UNORDERED", "RCV_SOCKET_BUFFERED",
     "RCV_SOCKET_DELIVERED", "PDS_DESTROYED"};
+enum : uint32_t { Q_THROTTLED = 1, Q_UNORDERED = 2 };
 enum : uint32_t { DS_ACTIVE = 1, DS_READABLE = 2, DS_WRITABLE = 4, DS_CLOSED = 8 };
 enum { TS_CLOSED, TS_LISTEN, TS_SYNSENT, TS_SYNRECEIVED, TS_ESTABLISHED, TS_FINWAIT1, TS_FINWAIT2, TS_CLOSING,
        TS_TIMEWAIT, TS_CLOSEWAIT, TS_LASTACK };
@@ -106,12 +107,14 @@ struct DPkt {
     uint64_t tsval, tsecho;
     double prio;
     uint32_t nsack, nst;
+    uint32_t inq, _pad;     // Q_THROTTLED / Q_UNORDERED: in its socket's heap (the reference's
+                            // priority_queue membership lookup, O(1) instead of a scan)
     uint8_t st[kSt];
     int32_t sacks[kPktSack];
 };
 struct DEv { uint64_t time, seq; uint32_t src, kind; int32_t obj, pkt; };
 struct Mail { uint32_t dst, src; uint64_t time, seq; DPkt pkt; };
-static_assert(sizeof(DEv) == 32 && sizeof(Mail) == 712, "bench.py's algorithmic bytes of the TCP rounds");
+static_assert(sizeof(DEv) == 32 && sizeof(Mail) == 720, "bench.py's algorithmic bytes of the TCP rounds");
 struct TRec {
     uint64_t time; int32_t host; uint32_t status;
     uint32_t host_id, flags, sip, dip;
@@ -263,6 +266,13 @@ template <uint32_t N> __device__ int ih_find(const IHeap<N>& q, int32_t x) {
 template <uint32_t N, class Less> __device__ bool ih_push(IHeap<N>& q, int32_t x, Less lt, uint32_t& err) {
     const int old = ih_find(q, x);
     if (old >= 0) { ih_up(q, ih_down(q, (uint32_t)old, lt), lt); return false; }
+    if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return false; }
+    q.a[q.n++] = x;
+    ih_up(q, q.n - 1, lt);
+    return true;
+}
+// push of an element known to be absent (its membership is tracked outside)
+template <uint32_t N, class Less> __device__ bool ih_push_new(IHeap<N>& q, int32_t x, Less lt, uint32_t& err) {
     if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return false; }
     q.a[q.n++] = x;
     ih_up(q, q.n - 1, lt);
@@ -829,16 +839,20 @@ __device__ void tcp_autotune_snd(L& c, DSock* k) {   // tcp.c:566-591
     if (nsz > out_size(k)) set_out_size(k, nsz);
 }
 __device__ void tcp_buffer_out(L& c, DSock* k, int32_t pi) {   // tcp.c:729-745
-    if (ih_find(k->throttled, pi) >= 0) return;
-    ih_push(k->throttled, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err);
+    DPkt* p = PK(c, pi);
+    if (p->inq & Q_THROTTLED) return;   // already queued (priority_queue_push's lookup)
+    if (!ih_push_new(k->throttled, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err)) return;
+    p->inq |= Q_THROTTLED;
     pkt_ref(c, pi);
     k->throttled_len += PK(c, pi)->len;
     if (space_out(k) == 0) sock_status(c, k, DS_WRITABLE, false);
     pkt_status(c, pi, S_SND_TCP_ENQUEUE_THROTTLED);
 }
 __device__ void tcp_buffer_in(L& c, DSock* k, int32_t pi) {   // tcp.c:747-760
-    if (ih_find(k->unordered, pi) >= 0) return;
-    ih_push(k->unordered, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err);
+    DPkt* p = PK(c, pi);
+    if (p->inq & Q_UNORDERED) return;
+    if (!ih_push_new(k->unordered, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err)) return;
+    p->inq |= Q_UNORDERED;
     pkt_ref(c, pi);
     k->unordered_len += PK(c, pi)->len;
     pkt_status(c, pi, S_RCV_TCP_ENQUEUE_UNORDERED);
@@ -936,6 +950,7 @@ template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
             if (!in_buffer || !in_window) break;
         }
         ih_pop(k->throttled, lt);
+        p->inq &= ~Q_THROTTLED;
         k->throttled_len -= len;
         sock_add_output(c, k, pi);
         k->s_packets_sent++;
@@ -947,6 +962,7 @@ template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
         if (p->seq == k->r_next && sock_add_input(c, k, pi)) {
             k->r_last_seq = p->seq;
             ih_pop(k->unordered, lt);
+            p->inq &= ~Q_UNORDERED;
             const uint32_t len = p->len;
             pkt_unref(c, pi);
             k->unordered_len -= len;
@@ -1346,6 +1362,7 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
         m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
+        m->pkt.inq = 0;   // the copy is in no queue of the receiver
         c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
         atomicMin((unsigned long long*)&c.g->next_time[c.g->H], (unsigned long long)t);
     } else {
