@@ -151,7 +151,9 @@ struct DSock {
         s_quick_acks, s_delack_counter;
     int32_t s_delack_sched;
     uint32_t nsack; int32_t sacks[kSacks];
-    uint32_t nrtx; int32_t rtx[kQ]; uint64_t rtx_len; int32_t rto; THeap<kTimers> timers; uint64_t desired;
+    // the retransmit queue (tcp.c's GHashTable by sequence) as a sequence-sorted
+    // window [rh, rh + nrtx) of rtx (packets) and rtxs (their sequences)
+    uint32_t nrtx, rh; int32_t rtx[kQ]; uint32_t rtxs[kQ]; uint64_t rtx_len; int32_t rto; THeap<kTimers> timers; uint64_t desired;
     uint32_t backoff;
     Tally tally;
     int32_t at_did_init; uint64_t at_bytes, at_last_adjust, at_space;
@@ -534,50 +536,80 @@ __device__ void path(const L& c, int32_t a, int32_t b, double& lat, double& rel)
 }
 
 // ------------------------------------------------------------ retransmit queue
-__device__ int rtx_find(const L& c, const DSock* k, uint32_t seq) {
-    for (uint32_t i = 0; i < k->nrtx; i++) if (PK(c, k->rtx[i])->seq == seq) return (int)i;
-    return -1;
+// logical index i of the window is physical rh + i; sequences are unique
+__device__ uint32_t rtx_lower(const DSock* k, uint32_t seq) {   // first i with seq_i >= seq
+    uint32_t lo = 0, hi = k->nrtx;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (k->rtxs[k->rh + mid] < seq) lo = mid + 1; else hi = mid;
+    }
+    return lo;
 }
-__device__ void rtx_remove_at(DSock* k, uint32_t i) {
-    for (uint32_t j = i; j + 1 < k->nrtx; j++) k->rtx[j] = k->rtx[j + 1];
-    k->nrtx--;
+__device__ int rtx_find(const L& c, const DSock* k, uint32_t seq) {
+    const uint32_t i = rtx_lower(k, seq);
+    return (i < k->nrtx && k->rtxs[k->rh + i] == seq) ? (int)i : -1;
+}
+__device__ __forceinline__ int32_t rtx_at(const DSock* k, uint32_t i) { return k->rtx[k->rh + i]; }
+__device__ void rtx_remove_at(DSock* k, uint32_t i) {   // shifts the shorter side
+    if (i < k->nrtx - 1 - i) {
+        for (uint32_t j = i; j > 0; j--) {
+            k->rtx[k->rh + j] = k->rtx[k->rh + j - 1];
+            k->rtxs[k->rh + j] = k->rtxs[k->rh + j - 1];
+        }
+        k->rh++;
+    } else {
+        for (uint32_t j = i; j + 1 < k->nrtx; j++) {
+            k->rtx[k->rh + j] = k->rtx[k->rh + j + 1];
+            k->rtxs[k->rh + j] = k->rtxs[k->rh + j + 1];
+        }
+    }
+    if (--k->nrtx == 0) k->rh = 0;
+}
+__device__ bool rtx_insert(DSock* k, int32_t pi, uint32_t seq, uint32_t& err) {
+    if (k->nrtx >= kQ) { err |= SHD_TCP_ERR_QUEUE; return false; }
+    if (k->rh + k->nrtx == kQ) {   // the window reached the end: move it to the front
+        for (uint32_t j = 0; j < k->nrtx; j++) { k->rtx[j] = k->rtx[k->rh + j]; k->rtxs[j] = k->rtxs[k->rh + j]; }
+        k->rh = 0;
+    }
+    uint32_t i = k->nrtx;
+    while (i > 0 && k->rtxs[k->rh + i - 1] > seq) {   // from the end: sends append in order
+        k->rtx[k->rh + i] = k->rtx[k->rh + i - 1];
+        k->rtxs[k->rh + i] = k->rtxs[k->rh + i - 1];
+        i--;
+    }
+    k->rtx[k->rh + i] = pi;
+    k->rtxs[k->rh + i] = seq;
+    k->nrtx++;
+    return true;
 }
 __device__ void tcp_add_retransmit(L& c, DSock* k, int32_t pi) {   // tcp.c:854-873
     DPkt* p = PK(c, pi);
     if (rtx_find(c, k, p->seq) >= 0) return;
-    if (k->nrtx >= kQ) { c.H->err |= SHD_TCP_ERR_QUEUE; return; }
-    k->rtx[k->nrtx++] = pi;
+    if (!rtx_insert(k, pi, p->seq, c.H->err)) return;
     pkt_ref(c, pi);
     pkt_status(c, pi, S_SND_TCP_ENQUEUE_RETRANSMIT);
     k->rtx_len += p->len;
     if (space_out(k) == 0) sock_status(c, k, DS_WRITABLE, false);
 }
 __device__ void tcp_clear_retransmit(L& c, DSock* k, uint32_t seq) {   // tcp.c:876-897 (sequence order)
-    for (;;) {   // repeatedly take the lowest sequence below `seq`
-        int best = -1;
-        for (uint32_t i = 0; i < k->nrtx; i++) {
-            const uint32_t s = PK(c, k->rtx[i])->seq;
-            if (s < seq && (best < 0 || s < PK(c, k->rtx[best])->seq)) best = (int)i;
-        }
-        if (best < 0) break;
-        const int32_t pi = k->rtx[best];
+    while (k->nrtx && k->rtxs[k->rh] < seq) {   // the lowest sequence below `seq` first
+        const int32_t pi = rtx_at(k, 0);
         k->rtx_len -= PK(c, pi)->len;
         pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
-        rtx_remove_at(k, (uint32_t)best);
+        rtx_remove_at(k, 0);
         pkt_unref(c, pi);
     }
     if (space_out(k) > 0) sock_status(c, k, DS_WRITABLE, true);
 }
 __device__ void tcp_clear_retransmit_range(L& c, DSock* k, uint32_t begin, uint32_t end) {   // tcp.c:900-920
-    for (uint32_t sq = begin; sq < end; ++sq) {
-        const int at = rtx_find(c, k, sq);
-        if (at >= 0) {
-            const int32_t pi = k->rtx[at];
-            k->rtx_len -= PK(c, pi)->len;
-            pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
-            rtx_remove_at(k, (uint32_t)at);
-            pkt_unref(c, pi);
-        }
+    // the sequences in [begin, end) present, ascending (a run of the window)
+    const uint32_t at = rtx_lower(k, begin);
+    while (at < k->nrtx && k->rtxs[k->rh + at] < end) {
+        const int32_t pi = rtx_at(k, at);
+        k->rtx_len -= PK(c, pi)->len;
+        pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
+        rtx_remove_at(k, at);
+        pkt_unref(c, pi);
     }
     if (space_out(k) > 0) sock_status(c, k, DS_WRITABLE, true);
 }
@@ -752,7 +784,7 @@ __device__ void sock_init_tcp(DSock* k, uint32_t recv_buf, uint32_t send_buf, ui
     k->r_window = iw; k->r_last_window = iw; k->r_last_ack = 1;
     k->s_unacked = 1; k->s_next = 1; k->s_end = 1; k->s_last_ack = 1; k->s_window = iw; k->s_last_window = iw;
     k->s_highest = 0; k->s_packets_sent = 0; k->s_quick_acks = 0; k->s_delack_counter = 0; k->s_delack_sched = 0;
-    k->nsack = 0; k->nrtx = 0; k->rtx_len = 0; k->timers.n = 0; k->desired = 0; k->backoff = 0;
+    k->nsack = 0; k->nrtx = 0; k->rh = 0; k->rtx_len = 0; k->timers.n = 0; k->desired = 0; k->backoff = 0;
     k->tally.last_ack = -1; k->tally.ndup = 0;
     k->tally.marked.n = k->tally.sacked.n = k->tally.retx.n = k->tally.lost.n = k->tally.tmp.n = 0;
     k->at_did_init = 0; k->at_bytes = 0; k->at_last_adjust = 0; k->at_space = 0;
@@ -876,7 +908,7 @@ __device__ int32_t tcp_create_packet(L& c, DSock* k, uint32_t flags, uint32_t le
 __device__ void tcp_retransmit_packet(L& c, DSock* k, uint32_t seq) {   // tcp.c:1027-1065
     const int at = rtx_find(c, k, seq);
     if (at < 0) return;
-    const int32_t pi = k->rtx[at];
+    const int32_t pi = rtx_at(k, (uint32_t)at);
     rtx_remove_at(k, (uint32_t)at);
     k->rtx_len -= PK(c, pi)->len;
     pkt_status(c, pi, S_SND_TCP_DEQUEUE_RETRANSMIT);
