@@ -2064,12 +2064,9 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         // rounds run in batches of kBatch (window kernel, round kernel) pairs
         // captured once as a graph: no host round trip inside a batch; a
         // halted run turns the batch's remaining kernels into no-ops
-        // hosts per wave: each lane walks its own host's branchy chain, so
-        // fewer lanes per wave means less divergence and more waves for the
-        // SIMDs to interleave (A/B knob SHD_TCP_LANES while measuring)
-        const char* lv = getenv("SHD_TCP_LANES");
-        const int threads = lv ? atoi(lv) : 64, blocks = (H + threads - 1) / threads;
-        if (threads < 1 || threads > 64) { rc = -22; goto done; }
+        // one host per lane, 64 per wave (16 per wave measured +4 % at 16 k
+        // hosts, DESIGN.md §6: not kept)
+        const int threads = 64, blocks = (H + threads - 1) / threads;
         constexpr int kBatch = 64;
         HCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
         for (int i = 0; i < kBatch; i++) {
