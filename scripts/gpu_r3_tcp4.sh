@@ -3,7 +3,7 @@
 # parity tests, the 65 k-host bench line (CPU baseline on its 4096-host
 # sample), and rocprof kernel statistics (csv)
 set -o pipefail
-O=gpurun_out/r03y
+O=gpurun_out/r03x
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_tcp_gpu.py -x -v --timeout 120 --timeout-method thread > $O/tcp_tests.log 2>&1 || { tail -30 $O/tcp_tests.log; exit 1; }
 tail -2 $O/tcp_tests.log

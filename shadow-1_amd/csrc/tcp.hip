@@ -65,9 +65,7 @@ constexpr uint32_t kEv = 8192;      // events per host
 constexpr uint32_t kCq = 4096;      // CoDel queue per host
 constexpr uint32_t kTr = 1u << 16;  // trace records per host
 constexpr uint32_t kTrSack = 1u << 20;
-constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 32 per host)
-constexpr uint32_t kMailSub = 64;   // a mailbox in 64 parts with a fill counter each (host h uses
-                                    // part h % 64): slot claims spread over 64 addresses
+constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 16 per host)
 
 // ProtocolTCPFlags (protocol.h:23-31)
 enum : uint32_t { F_RST = 1 << 1, F_SYN = 1 << 2, F_ACK = 1 << 3, F_SACK = 1 << 4, F_FIN = 1 << 5, F_DUPACK = 1 << 6 };
@@ -212,7 +210,7 @@ struct Glob {
     DEv* ev;                // [H][kEv]
     CqEnt* cq;              // [H][kCq]
     Mail* mail;             // [2][mail_cap] the two mailboxes (a round's input, its output)
-    uint32_t* nmail;        // [2][kMailSub] their parts' fill counts
+    uint32_t* nmail;        // [2] their fill counts
     int32_t* mhead;         // [2][H] each destination's list of mails (-1: none)
     int32_t* mnext;         // [2][mail_cap] the next mail of the same destination
     uint32_t mail_cap, _pad2;
@@ -232,7 +230,6 @@ struct L {
     DHost* H;
     uint64_t now;
     int32_t active;
-    uint64_t mail_min;      // the earliest delivery this lane put into the round's mailbox
 };
 __device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * c.g->pool_cap + i]; }
 __device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
@@ -1391,17 +1388,15 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
         const uint64_t seq = c.H->ev_seq++;   // event_new_ (the delivery's ID)
         if (t >= c.g->end_time) return;
         if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
-        const uint32_t part = (uint32_t)c.h % kMailSub, per = c.g->mail_cap / kMailSub;
-        const uint32_t k = atomicAdd(c.g->n_out + part, 1u);
-        if (k >= per) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
-        const uint32_t slot = part * per + k;
+        const uint32_t slot = atomicAdd(c.g->n_out, 1u);
+        if (slot >= c.g->mail_cap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
         Mail* m = &c.g->mail_out[slot];
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
         m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
         m->pkt.inq = 0;   // the copy is in no queue of the receiver
         c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
-        if (t < c.mail_min) c.mail_min = t;   // folded into next_time[h] at the round's end
+        atomicMin((unsigned long long*)&c.g->next_time[c.g->H], (unsigned long long)t);
     } else {
         pkt_status(c, pi, S_INET_DROPPED);
     }
@@ -1784,7 +1779,7 @@ __global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (h >= g.H) return;
     Glob gl = g;
-    L c{&gl, h, &gl.host[h], 0, h, ~0ull};
+    L c{&gl, h, &gl.host[h], 0, h};
     sched_task(c, gl.hb, K_HEARTBEAT, -1);
     refill_cb(c);
     sched_task(c, kMs, K_REFILL_LO, -1);
@@ -1806,10 +1801,6 @@ __global__ void k_tcp_window(Glob g) {
     __shared__ uint64_t red[16];
     TCtl* ctl = g.ctl;
     if (ctl->halted) return;
-    {   // the next round's output mailbox starts empty (read before thread 0 moves rounds on)
-        const uint64_t k = ctl->rounds;
-        if (threadIdx.x < kMailSub) g.nmail[((k + 1) & 1) * kMailSub + threadIdx.x] = 0;
-    }
     uint64_t t = ~0ull;
     for (int32_t i = (int32_t)threadIdx.x; i <= g.H; i += (int32_t)blockDim.x) {
         const uint64_t x = g.next_time[i];
@@ -1829,7 +1820,8 @@ __global__ void k_tcp_window(Glob g) {
             const uint64_t k = ctl->rounds;
             ctl->wend = t + g.W;
             ctl->rounds = k + 1;
-            g.next_time[g.H] = ~0ull;     // (unused slot: deliveries fold into their sender's)
+            g.nmail[(k + 1) & 1] = 0;     // round k's output mailbox starts empty
+            g.next_time[g.H] = ~0ull;     // ... and so does its earliest delivery
         }
     }
 }
@@ -1848,12 +1840,12 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
         gl = g;
         gl.mail_in = g.mail + (size_t)in * g.mail_cap; gl.mhead_in = g.mhead + (size_t)in * g.H;
         gl.mnext_in = g.mnext + (size_t)in * g.mail_cap;
-        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + (size_t)out * kMailSub;
+        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + out;
         gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * g.mail_cap;
     }
     __syncthreads();
     if (h >= g.H) return;
-    L c{&gl, h, &gl.host[h], 0, h, ~0ull};
+    L c{&gl, h, &gl.host[h], 0, h};
     // this host's deliveries (any order: the heap's key (time, src, seq) is unique)
     int32_t s = gl.mhead_in[h];
     gl.mhead_in[h] = -1;   // the list is empty again when this mailbox is next written
@@ -1876,10 +1868,8 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
         if (++nev > (1u << 24)) c.H->err |= SHD_TCP_ERR_INTERNAL;   // a runaway round: stop, report
     }
     c.H->events += nev;
-    // a host that stopped on an error leaves the run (the caller sees the bit);
-    // the deliveries it sent this round count toward the next window either way
-    const uint64_t own = (c.H->nev && !c.H->err) ? gl.ev[(size_t)h * kEv].time : ~0ull;
-    gl.next_time[h] = own < c.mail_min ? own : c.mail_min;
+    // a host that stopped on an error leaves the run (the caller sees the bit)
+    gl.next_time[h] = (c.H->nev && !c.H->err) ? gl.ev[(size_t)h * kEv].time : ~0ull;
 }
 
 #define HCHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "shd_tcp: %s: %s\n", #x, hipGetErrorString(e_)); rc = -5; goto done; } } while (0)
@@ -1943,7 +1933,7 @@ int32_t rand_r_host(uint32_t* state) {
 }  // namespace
 
 extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
-    if (!m || !out || m->n_hosts <= 0 || m->n_hosts > (1 << 25) || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
+    if (!m || !out || m->n_hosts <= 0 || m->n_hosts > (1 << 26) || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
         !m->bw_up_kibps || !m->path_lat_ms || !m->path_rel || !m->host_vertex || m->n_vertices <= 0 ||
         (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
         return -22;
@@ -2049,10 +2039,10 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipGetLastError());
     HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
-    g.mail_cap = (uint32_t)H * 32u > kMailMin ? (uint32_t)H * 32u : kMailMin;
+    g.mail_cap = (uint32_t)H * 16u > kMailMin ? (uint32_t)H * 16u : kMailMin;
     HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
-    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2 * kMailSub));
-    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * kMailSub));
+    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2));
+    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2));
     HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
