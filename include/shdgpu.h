@@ -512,6 +512,42 @@ int shd_eng_stream(shd_eng* e, void** hip_stream);
  * differences give the [shadow-heartbeat] [node] line (tracker.c:419-465).
  * *n = nloc*K*2; SHD_ERANGE if cap < *n. */
 int shd_eng_heartbeats(shd_eng* e, uint32_t* out, uint64_t cap, uint64_t* n);
+
+/* ---- the reference's log lines, made by the library ----
+ * A set of lines: line i is text[off[i] .. off[i+1]) (no newline; text is
+ * NUL-terminated after the last line), logged at simulated time time[i] (ns)
+ * by host index host[i].  Released with shd_lines_free. */
+typedef struct shd_lines {
+    uint64_t n;
+    uint64_t* time;
+    uint32_t* host;
+    uint64_t* off;                  /* [n + 1] */
+    char* text;
+} shd_lines;
+/* The [STATUS] lines of packet_addDeliveryStatus (packet.c:647-659) from a
+ * trace recorded with SHD_QF_TRACE_STATUS: every status each UDP datagram
+ * passes through, "[<STATUS>] packetID=<hostID>:<pkt> <srcIP>:<srcPort> ->
+ * <dstIP>:<dstPort> bytes=<payload> status=<S1>,...,<Sk>" (packet_toString,
+ * packet.c:518-547, 616-633), and PDS_DESTROYED where a packet object's last
+ * reference goes (packet.c:194-201; not the frees at teardown).  ips[h]: host
+ * h's address (host order), host_ids[h] its host_getID (NULL: h + 1),
+ * listen_port the destination port.  Ordered by (time, host), each host's
+ * lines in the reference's call-chain order. */
+int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, const uint32_t* host_ids,
+                     uint32_t n_hosts, uint32_t payload, uint32_t listen_port, shd_lines** out);
+/* The [shadow-heartbeat] lines of _tracker_logNode (tracker.c:419-465) of one
+ * host: the header and the all-zero boot line at t = 0 (tracker_new's inline
+ * heartbeat, tracker.c:141), then one line per snapshot k at (k+1)*interval
+ * from the cumulative interface counters snapshots[2k] (in), [2k+1] (out). */
+int shd_node_lines(const uint32_t* snapshots, uint64_t k, uint64_t interval_ns, uint32_t payload, uint32_t host,
+                   shd_lines** out);
+/* The same from an engine: the [STATUS] lines of its whole trace (the model's
+ * payload; ips / host_ids over all H hosts), and local host l's [node] lines
+ * (its own heartbeat interval; heartbeats before end_time). */
+int shd_eng_status_lines(shd_eng* e, const uint32_t* ips, const uint32_t* host_ids, uint32_t listen_port,
+                         shd_lines** out);
+int shd_eng_node_lines(shd_eng* e, uint32_t local_host, shd_lines** out);
+void shd_lines_free(shd_lines* l);
 /* HIP-event device time of the last round kernel launch (ms) */
 int shd_eng_last_kernel_ms(shd_eng* e, double* ms);
 void shd_eng_destroy(shd_eng* e);

@@ -50,6 +50,17 @@ typedef struct shd_tcp_model {
                                          set SHD_TCP_ERR_POOL                             */
 } shd_tcp_model;
 
+/* the first path query a host made of a vertex pair (topology_isRoutable /
+ * getLatency / getReliability): the executing event's key (event_compare:
+ * time, host, src, seq) and the query's index within that event; the caller
+ * ranks the run's first touches in this order (shadow-1_amd/tcp.py) */
+typedef struct shd_tcp_query {
+    uint64_t time, seq;
+    uint32_t host, src, index;
+    int32_t v_src, v_dst;             /* vertex indices (path table) of the query       */
+    uint32_t _pad;
+} shd_tcp_query;
+
 typedef struct shd_tcp_result {
     char* lines;                      /* "<time>\t<host>\t[STATUS] ...\n", each host's lines in
                                          its execution order, hosts in index order           */
@@ -64,16 +75,23 @@ typedef struct shd_tcp_result {
     uint32_t error;                   /* SHD_TCP_ERR_* bits; nonzero: results invalid     */
     uint64_t deliveries;              /* packets handed to a receiving host (worker.c:260-321's
                                          delivery events executed)                           */
+    shd_tcp_query* queries;           /* each host's first query of each vertex pair      */
+    uint64_t n_queries;
 } shd_tcp_result;
 
 enum {
     SHD_TCP_ERR_EVQ = 1, SHD_TCP_ERR_POOL = 2, SHD_TCP_ERR_QUEUE = 4, SHD_TCP_ERR_SOCKETS = 8,
-    SHD_TCP_ERR_MAILBOX = 16, SHD_TCP_ERR_TRACE = 32, SHD_TCP_ERR_SACK = 64, SHD_TCP_ERR_INTERNAL = 128
+    SHD_TCP_ERR_MAILBOX = 16, SHD_TCP_ERR_TRACE = 32, SHD_TCP_ERR_SACK = 64, SHD_TCP_ERR_INTERNAL = 128,
+    SHD_TCP_ERR_QLOG = 256
 };
 
 /* Run the model to end_time on the current HIP device.  trace != 0 writes the
- * [STATUS] lines (packet.c:647-659).  Returns 0 or a negative errno-style code;
- * *out is allocated by the call and released by shd_tcp_result_free. */
+ * [STATUS] lines (packet.c:647-659).  Returns 0 or a negative errno-style code:
+ * -22 an invalid model, -113 a client whose server has no route in either
+ * direction (the reference's connect fails with ECONNREFUSED there,
+ * host.c:1224-1234; the device application has no such branch), -12 no device
+ * memory for the trace buffers, -5 a HIP error.  *out is allocated by the call
+ * and released by shd_tcp_result_free. */
 int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out);
 void shd_tcp_result_free(shd_tcp_result* r);
 

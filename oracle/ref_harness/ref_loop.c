@@ -99,6 +99,10 @@ typedef struct ref_loop_cfg {
      * the client k connects to; each client sends tcp_bytes, the server echoes */
     const int32_t* proc_peer;
     uint32_t tcp_bytes, _pad3;
+    /* 1: the default log level's work only -- debug records filtered (the
+     * [STATUS] lines are not even formatted) and no line kept: for timing the
+     * reference's loop (scripts/r04/ref_loop_timing.py) */
+    int32_t quiet, _pad4;
 } ref_loop_cfg;
 
 typedef struct ref_loop_out {
@@ -194,7 +198,9 @@ struct _ShadowLogger { int dummy; };
 static struct _ShadowLogger g_slogger;
 ShadowLogger* shadow_logger_getDefault() { return &g_slogger; }
 /* debug filter level: packet_addDeliveryStatus logs every status (packet.c:652) */
-gboolean shadow_logger_shouldFilter(ShadowLogger* logger, LogLevel level) { return FALSE; }
+gboolean shadow_logger_shouldFilter(ShadowLogger* logger, LogLevel level) {
+    return g_cfg && g_cfg->quiet && level > LOGLEVEL_MESSAGE;
+}
 void shadow_logger_flushRecords(ShadowLogger* logger, pthread_t callerThread) {}
 void shadow_logger_register(ShadowLogger* logger, pthread_t callerThread) {}
 Logger* logger_getDefault(void) { return NULL; }
@@ -213,7 +219,8 @@ static void out_append(const char* s, size_t n) {
 
 void logger_log(Logger* logger, LogLevel level, const gchar* fileName, const gchar* functionName,
                 const gint lineNumber, const gchar* format, ...) {
-    if (!g_out || level != LOGLEVEL_MESSAGE || !g_sched || !scheduler_isRunning(g_sched) || !worker_isAlive())
+    if (!g_out || level != LOGLEVEL_MESSAGE || !g_sched || !scheduler_isRunning(g_sched) || !worker_isAlive() ||
+        g_cfg->quiet)
         return;
     /* a packet whose last reference goes with its deliver task is released
      * after event_execute cleared the active host (event.c:86, worker.c:187):

@@ -74,6 +74,7 @@ struct shd_eng {
     int parity = 0;
     bool booted = false;
     bool heartbeats = false;    // SHD_QF_HEARTBEATS: snapshots in P.hb
+    std::vector<uint64_t> host_hb;   // <host heartbeatfrequency> per host (empty: P.heartbeat)
     std::vector<void*> allocs;
     std::vector<size_t> alloc_bytes;
     // protected rounds (DESIGN.md "First-touch rule"): device state copied
@@ -229,6 +230,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         shd_eng_destroy(e);
         return SHD_EINVAL;
     }
+    if (m->host_heartbeat) e->host_hb.assign(m->host_heartbeat, m->host_heartbeat + H);
     P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
     P.app_start = m->app_start; P.load = m->load; P.payload = m->payload;
     P.pkt_len = m->payload + SHD_HEADER_UDP;
@@ -1240,6 +1242,34 @@ extern "C" int shd_eng_heartbeats(shd_eng* e, uint32_t* out, uint64_t cap, uint6
     SHD_HIP(hipMemcpyAsync(out, (const uint2*)e->P.hb, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
     SHD_HIP(hipStreamSynchronize(e->stream));
     return SHD_OK;
+}
+
+extern "C" int shd_eng_status_lines(shd_eng* e, const uint32_t* ips, const uint32_t* host_ids, uint32_t listen_port,
+                                    shd_lines** out) {
+    if (!e || !ips || !out) return SHD_EINVAL;
+    uint64_t n = 0, got = 0;
+    int rc = shd_eng_trace_count(e, &n);
+    if (rc) return rc;
+    std::vector<shd_trace_rec> tr(n ? n : 1);
+    if (n && (rc = shd_eng_trace_copy(e, tr.data(), n, &got))) return rc;
+    return shd_status_lines(tr.data(), got, ips, host_ids, (uint32_t)e->H, e->P.payload, listen_port, out);
+}
+
+extern "C" int shd_eng_node_lines(shd_eng* e, uint32_t local_host, shd_lines** out) {
+    if (!e || !out || local_host >= (uint32_t)e->nloc || !e->heartbeats) return SHD_EINVAL;
+    const uint32_t h = (uint32_t)e->h0 + local_host;
+    const uint64_t iv = e->host_hb.empty() ? e->P.heartbeat : e->host_hb[h];
+    // this host's heartbeats at k * iv < end_time, k >= 1 (P.hb holds hb_k per host)
+    uint64_t k = e->P.end_time > 0 && iv ? (e->P.end_time - 1) / iv : 0;
+    if (k > e->P.hb_k) k = e->P.hb_k;
+    std::vector<uint32_t> snap(2 * (k ? k : 1));
+    if (k) {
+        SHD_HIP(hipSetDevice(e->device));
+        SHD_HIP(hipMemcpyAsync(snap.data(), (const uint2*)e->P.hb + (size_t)local_host * e->P.hb_k, 8 * k,
+                               hipMemcpyDeviceToHost, e->stream));
+        SHD_HIP(hipStreamSynchronize(e->stream));
+    }
+    return shd_node_lines(snap.data(), k, iv, e->P.payload, h, out);
 }
 
 extern "C" int shd_eng_stream(shd_eng* e, void** s) {

@@ -66,6 +66,7 @@ constexpr uint32_t kCq = 4096;      // CoDel queue per host
 constexpr uint32_t kTr = 1u << 16;  // trace records per host
 constexpr uint32_t kTrSack = 1u << 20;
 constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 16 per host)
+constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
 
 // ProtocolTCPFlags (protocol.h:23-31)
 enum : uint32_t { F_RST = 1 << 1, F_SYN = 1 << 2, F_ACK = 1 << 3, F_SACK = 1 << 4, F_FIN = 1 << 5, F_DUPACK = 1 << 6 };
@@ -184,6 +185,10 @@ struct DHost {
     // CoDel (router_queue_codel.c)
     uint32_t cq_head, cq_n; uint64_t cq_total, cq_iexp, cq_next_drop; uint32_t cq_dc, cq_dc_last; int32_t cq_mode;
     uint32_t nfree, ntr, ntrs, nev;
+    // the vertex pairs this host has queried (unordered, (min << 32) | max):
+    // its first query of each goes to the run's first-query log (touch_log)
+    uint32_t npq, _pq_pad;
+    uint64_t pq[kPq];
 };
 struct CqEnt { uint64_t ts; uint32_t len; int32_t pkt; };
 
@@ -221,6 +226,9 @@ struct Glob {
     TRec* tr;               // [H][kTr]
     int32_t* trs;           // [H][kTrSack]
     uint64_t* next_time;    // [H]
+    shd_tcp_query* qlog;    // [qlog_cap] each host's first query of each vertex pair (touch_log)
+    uint32_t* nqlog;
+    uint32_t qlog_cap, _pad3;
 };
 
 // ------------------------------------------------------------ per-lane context
@@ -230,6 +238,10 @@ struct L {
     DHost* H;
     uint64_t now;
     int32_t active;
+    // the executing event's key (event_compare: time, this host, src, seq) and
+    // the index of the next path query within it (first-query log)
+    uint32_t ksrc, kq;
+    uint64_t kseq;
 };
 __device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * c.g->pool_cap + i]; }
 __device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
@@ -529,10 +541,49 @@ __device__ int32_t host_of_ip(const L& c, uint32_t ip) {
     }
     return (lo < (uint32_t)c.g->H && (uint32_t)(k[lo] >> 32) == ip) ? (int32_t)(uint32_t)k[lo] : -1;
 }
-__device__ void path(const L& c, int32_t a, int32_t b, double& lat, double& rel) {
+// A path query of the executing event (topology_isRoutable / getLatency /
+// getReliability, topology.c:2053-2092).  Which endpoint's Dijkstra row serves
+// a pair depends on the serial order of every pair's FIRST query
+// (_topology_getPathEntry, topology.c:1969-2051): the host's
+// first query of each vertex pair is logged with the event's key, so the
+// caller can rank the run's first touches in serial order afterwards and
+// check the tables it passed against them (shadow-1_amd/tcp.py)
+__device__ void touch_log(L& c, int32_t va, int32_t vb) {
+    const uint32_t q = c.kq++;
+    const uint64_t key = va < vb ? ((uint64_t)(uint32_t)va << 32) | (uint32_t)vb
+                                 : ((uint64_t)(uint32_t)vb << 32) | (uint32_t)va;
+    DHost* H = c.H;
+    const uint32_t n = H->npq < kPq ? H->npq : kPq;
+    for (uint32_t i = 0; i < n; i++)
+        if (H->pq[i] == key) return;
+    if (H->npq < kPq) H->pq[H->npq] = key;
+    H->npq++;   // past kPq every unremembered pair's query is logged (a superset: harmless)
+    const uint32_t slot = atomicAdd(c.g->nqlog, 1u);
+    if (slot >= c.g->qlog_cap) { H->err |= SHD_TCP_ERR_QLOG; return; }
+    shd_tcp_query r;
+    r.time = c.now; r.seq = c.kseq; r.host = (uint32_t)c.h; r.src = c.ksrc; r.index = q;
+    r.v_src = va; r.v_dst = vb; r._pad = 0;
+    c.g->qlog[slot] = r;
+}
+
+// the path entry of hosts a -> b; an unknown host or a pair with no route
+// (latency < 0: shd_tcp_run refuses models whose connections have one, so
+// this is an internal error) fails the run instead of scheduling a delivery
+// at a negative delay
+__device__ void path(L& c, int32_t a, int32_t b, double& lat, double& rel) {
+    if (a < 0 || b < 0) {
+        c.H->err |= SHD_TCP_ERR_INTERNAL;
+        lat = 1.0; rel = 0.0;
+        return;
+    }
+    touch_log(c, c.g->hv[a], c.g->hv[b]);
     const size_t i = (size_t)c.g->hv[a] * (size_t)c.g->V + (size_t)c.g->hv[b];
     lat = c.g->lat[i];
     rel = c.g->rel[i];
+    if (!(lat >= 0.0)) {
+        c.H->err |= SHD_TCP_ERR_INTERNAL;
+        lat = 1.0; rel = 0.0;
+    }
 }
 
 // ------------------------------------------------------------ retransmit queue
@@ -1656,6 +1707,7 @@ __device__ void app_run(L& c, DProc* pr) {
             const int32_t sh = sp->host;
             const uint32_t ip = c.g->host[sh].ip;
             const uint16_t port = c.g->sock[sp->listenfd].bound_port;
+            if (ip != c.H->ip) touch_log(c, c.g->hv[c.h], c.g->hv[sh]);   // topology_isRoutable (host.c:1224-1234)
             DSock* k = &c.g->sock[pr->fd];
             if (!k->bound) {   // implicit bind to the default interface, peer-specific
                 const uint16_t bp = random_free_port(c);
@@ -1779,7 +1831,7 @@ __global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (h >= g.H) return;
     Glob gl = g;
-    L c{&gl, h, &gl.host[h], 0, h};
+    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0};
     sched_task(c, gl.hb, K_HEARTBEAT, -1);
     refill_cb(c);
     sched_task(c, kMs, K_REFILL_LO, -1);
@@ -1845,7 +1897,7 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
     }
     __syncthreads();
     if (h >= g.H) return;
-    L c{&gl, h, &gl.host[h], 0, h};
+    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0};
     // this host's deliveries (any order: the heap's key (time, src, seq) is unique)
     int32_t s = gl.mhead_in[h];
     gl.mhead_in[h] = -1;   // the list is empty again when this mailbox is next written
@@ -1864,6 +1916,7 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
         const DEv e = evq_pop(c);
         c.now = e.time;
         c.active = h;
+        c.ksrc = e.src; c.kseq = e.seq; c.kq = 0;
         execute(c, e);
         if (++nev > (1u << 24)) c.H->err |= SHD_TCP_ERR_INTERNAL;   // a runaway round: stop, report
     }
@@ -1943,16 +1996,23 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         if (m->proc_peer[k] >= P || (m->proc_peer[k] >= 0 && m->proc_peer[m->proc_peer[k]] >= 0)) return -22;
     }
     const int32_t V = m->n_vertices;
+    for (int32_t a = 0; a < H; a++)
+        if (m->host_vertex[a] < 0 || m->host_vertex[a] >= V) return -22;
+    // a client whose server is unreachable: the reference's connect fails with
+    // ECONNREFUSED (host.c:1224-1234, topology_isRoutable); the device
+    // application has no such branch, so the model is refused here
+    for (int32_t k = 0; k < P; k++) {
+        if (m->proc_peer[k] < 0) continue;
+        const size_t u = (size_t)m->host_vertex[m->proc_host[k]], v = (size_t)m->host_vertex[m->proc_host[m->proc_peer[k]]];
+        if (!(m->path_lat_ms[u * V + v] >= 0.0) || !(m->path_lat_ms[v * V + u] >= 0.0)) return -113;   // EHOSTUNREACH
+    }
     const uint32_t pool_cap = m->packets_per_host ? m->packets_per_host : kPoolDefault;
     if (pool_cap > (1u << 24)) return -22;
     // the window: the smallest latency between two different hosts, in ns
     // (ceil, worker.c:293), over the vertex pairs some pair of distinct hosts
     // realizes (a vertex with itself only when two hosts share it)
     std::vector<int32_t> per_vertex(V, 0);
-    for (int32_t a = 0; a < H; a++) {
-        if (m->host_vertex[a] < 0 || m->host_vertex[a] >= V) return -22;
-        per_vertex[m->host_vertex[a]]++;
-    }
+    for (int32_t a = 0; a < H; a++) per_vertex[m->host_vertex[a]]++;
     uint64_t W = ~0ull;
     for (int32_t u = 0; u < V; u++) {
         if (!per_vertex[u]) continue;
@@ -2052,14 +2112,30 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMemcpy(d_ipk, ipk.data(), sizeof(uint64_t) * (size_t)H, hipMemcpyHostToDevice));
     g.ip_key = d_ipk;
     if (trace) {
-        HCHECK(hipMalloc(&g.tr, sizeof(TRec) * (size_t)H * kTr));
-        HCHECK(hipMalloc(&g.trs, sizeof(int32_t) * (size_t)H * kTrSack));
+        // kTr records and kTrSack SACK words per host (about 16 MB): a traced
+        // run of many hosts may not fit; say so instead of a bare -ENOMEM
+        const size_t need = (sizeof(TRec) * (size_t)kTr + sizeof(int32_t) * (size_t)kTrSack) * (size_t)H;
+        if (hipMalloc(&g.tr, sizeof(TRec) * (size_t)H * kTr) != hipSuccess ||
+            hipMalloc(&g.trs, sizeof(int32_t) * (size_t)H * kTrSack) != hipSuccess) {
+            (void)hipGetLastError();
+            fprintf(stderr, "shd_tcp_run: no device memory for the status trace of %d hosts (%.1f GB); "
+                            "run without trace\n", H, need / 1e9);
+            rc = -12;
+            goto done;
+        }
     }
     HCHECK(hipMalloc(&g.next_time, sizeof(uint64_t) * (H + 1)));
     HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (H + 1)));
+    g.qlog_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);
+    HCHECK(hipMalloc(&g.qlog, sizeof(shd_tcp_query) * (size_t)g.qlog_cap));
+    HCHECK(hipMalloc(&g.nqlog, sizeof(uint32_t)));
+    HCHECK(hipMemset(g.nqlog, 0, sizeof(uint32_t)));
     HCHECK(hipEventCreate(&e0));
     HCHECK(hipEventCreate(&e1));
     HCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    // the initialisation above (k_tcp_free_init, the memsets) ran on the null
+    // stream, which a non-blocking stream does not wait for: finish it first
+    HCHECK(hipDeviceSynchronize());
     {
         // rounds run in batches of kBatch (window kernel, round kernel) pairs
         // captured once as a graph: no host round trip inside a batch; a
@@ -2093,6 +2169,14 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         res->device_ms = ms;
     }
     HCHECK(hipMemcpy(hout.data(), g.host, sizeof(DHost) * H, hipMemcpyDeviceToHost));
+    {   // the first-query log
+        uint32_t nq = 0;
+        HCHECK(hipMemcpy(&nq, g.nqlog, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (nq > g.qlog_cap) nq = g.qlog_cap;   // (the run's error bits say so)
+        res->queries = (shd_tcp_query*)malloc(sizeof(shd_tcp_query) * (nq ? nq : 1));
+        res->n_queries = nq;
+        if (nq) HCHECK(hipMemcpy(res->queries, g.qlog, sizeof(shd_tcp_query) * nq, hipMemcpyDeviceToHost));
+    }
     res->next_event_id = (uint64_t*)calloc(H, sizeof(uint64_t));
     res->next_packet_id = (uint64_t*)calloc(H, sizeof(uint64_t));
     res->rng_probe = (uint32_t*)calloc(H, sizeof(uint32_t));
@@ -2136,6 +2220,7 @@ done:
     (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
     (void)hipFree(g.pool); (void)hipFree(g.freel); (void)hipFree(g.ev); (void)hipFree(g.cq);
     (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);
+    (void)hipFree(g.qlog); (void)hipFree(g.nqlog);
     if (rc) { shd_tcp_result_free(res); return rc; }
     *out = res;
     return 0;
@@ -2147,5 +2232,6 @@ extern "C" void shd_tcp_result_free(shd_tcp_result* r) {
     free(r->next_event_id);
     free(r->next_packet_id);
     free(r->rng_probe);
+    free(r->queries);
     free(r);
 }

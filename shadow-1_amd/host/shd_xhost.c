@@ -11,10 +11,13 @@
  * Segment: a header (barrier count and generation), then `world` scratch
  * slots of `slot` bytes.  A collective writes the caller's part into its
  * slot, meets at the barrier, reads what it needs, meets again; larger
- * payloads go in pieces of the slot size.  The segment is created zero-filled
- * by whichever rank opens it first; rank 0 unlinks it at close.  The name
- * must be unique per group (a stale segment's barrier state would be reused):
- * callers derive it from a random token, as RCCL's unique id.
+ * payloads go in pieces of the slot size.  Rank 0 creates the segment
+ * (exclusively: a segment of that name left by an earlier group -- one whose
+ * rank 0 died before unlinking it, or whose barrier broke -- is marked
+ * superseded, unlinked and created afresh) and unlinks it at close; the other
+ * ranks wait for rank 0's `ready` word, and drop a segment that is broken or
+ * superseded and open the name again.  Callers still derive the name from a
+ * random token, as RCCL's unique id.
  */
 #include <errno.h>
 #include <fcntl.h>
@@ -35,7 +38,10 @@ struct shd_xhost_hdr {
     uint32_t gen;         /* barrier generation */
     uint32_t world;
     uint32_t broken;      /* set by a rank whose barrier timed out: every barrier fails */
+    uint32_t ready;       /* kReady once rank 0 has initialised the segment */
+    uint32_t superseded;  /* set by a rank 0 that replaced this (stale) segment */
 };
+enum { kReady = 0x58484F53u };
 
 struct shd_xhost {
     char name[128];
@@ -47,6 +53,84 @@ struct shd_xhost {
 };
 
 static char* slot_ptr(shd_xhost* x, int r) { return x->base + 64 + (size_t)r * x->slot; }
+
+static double mono_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+/* rank 0: a fresh zero-filled segment under the name, replacing a stale one */
+static int xhost_create(shd_xhost* x) {
+    for (int tries = 0; tries < 4; tries++) {
+        x->fd = shm_open(x->name, O_RDWR | O_CREAT | O_EXCL, 0600);
+        if (x->fd >= 0) break;
+        if (errno != EEXIST) return SHD_ENODEV;
+        const int old = shm_open(x->name, O_RDWR, 0600);
+        if (old >= 0) {
+            struct stat so;
+            if (fstat(old, &so) == 0 && (size_t)so.st_size >= sizeof(struct shd_xhost_hdr)) {
+                void* m = mmap(NULL, sizeof(struct shd_xhost_hdr), PROT_READ | PROT_WRITE, MAP_SHARED, old, 0);
+                if (m != MAP_FAILED) {
+                    __atomic_store_n(&((struct shd_xhost_hdr*)m)->superseded, 1u, __ATOMIC_RELEASE);
+                    munmap(m, sizeof(struct shd_xhost_hdr));
+                }
+            }
+            close(old);
+        }
+        fprintf(stderr, "libshdgpu: host transport %s: replacing a stale segment of that name\n", x->name);
+        shm_unlink(x->name);
+    }
+    if (x->fd < 0) return SHD_ENODEV;
+    if (ftruncate(x->fd, (off_t)x->map_bytes) != 0) { close(x->fd); shm_unlink(x->name); return SHD_ENOMEM; }
+    x->base = mmap(NULL, x->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, x->fd, 0);
+    if (x->base == MAP_FAILED) { close(x->fd); shm_unlink(x->name); return SHD_ENOMEM; }
+    struct shd_xhost_hdr* h = (struct shd_xhost_hdr*)x->base;
+    h->world = (uint32_t)x->world;
+    __atomic_store_n(&h->ready, (uint32_t)kReady, __ATOMIC_RELEASE);
+    return SHD_OK;
+}
+
+/* the other ranks: rank 0's segment once it is ready (a broken or superseded
+ * one is dropped and the name opened again), within the barrier timeout */
+static int xhost_join(shd_xhost* x) {
+    const double t0 = mono_s();
+    for (;;) {
+        if (mono_s() - t0 > x->timeout_s) {
+            fprintf(stderr, "libshdgpu: host transport %s: rank %d found no ready segment in %.0f s\n", x->name,
+                    x->rank, x->timeout_s);
+            return SHD_ENODEV;
+        }
+        x->fd = shm_open(x->name, O_RDWR, 0600);
+        if (x->fd < 0) {
+            if (errno != ENOENT) return SHD_ENODEV;
+            usleep(200);
+            continue;
+        }
+        struct stat st;
+        if (fstat(x->fd, &st) != 0 || (size_t)st.st_size < x->map_bytes) {   /* not sized yet (or stale) */
+            close(x->fd);
+            usleep(200);
+            continue;
+        }
+        x->base = mmap(NULL, x->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, x->fd, 0);
+        if (x->base == MAP_FAILED) { close(x->fd); return SHD_ENOMEM; }
+        struct shd_xhost_hdr* h = (struct shd_xhost_hdr*)x->base;
+        for (;;) {
+            const int bad = __atomic_load_n(&h->superseded, __ATOMIC_ACQUIRE) ||
+                            __atomic_load_n(&h->broken, __ATOMIC_ACQUIRE);
+            if (!bad && __atomic_load_n(&h->ready, __ATOMIC_ACQUIRE) == (uint32_t)kReady) {
+                if (h->world != (uint32_t)x->world) { munmap(x->base, x->map_bytes); close(x->fd); return SHD_EINVAL; }
+                return SHD_OK;
+            }
+            if (bad || mono_s() - t0 > x->timeout_s) break;
+            usleep(100);
+        }
+        munmap(x->base, x->map_bytes);
+        close(x->fd);
+        usleep(200);
+    }
+}
 
 int shd_xhost_open(const char* name, int world, int rank, size_t slot_bytes, shd_xhost** out) {
     if (!name || !*name || strlen(name) > 100 || world <= 0 || world > 64 || rank < 0 || rank >= world ||
@@ -61,25 +145,10 @@ int shd_xhost_open(const char* name, int world, int rank, size_t slot_bytes, shd
     x->map_bytes = 64 + (size_t)world * x->slot;
     const char* to = getenv("SHD_XHOST_TIMEOUT");
     x->timeout_s = to ? atof(to) : 300.0;
-    x->fd = shm_open(x->name, O_RDWR | O_CREAT, 0600);
-    if (x->fd < 0) { free(x); return SHD_ENODEV; }
-    /* every rank grows it to the same size (a no-op after the first) */
-    struct stat st;
-    if (fstat(x->fd, &st) != 0 || ((size_t)st.st_size < x->map_bytes && ftruncate(x->fd, (off_t)x->map_bytes) != 0)) {
-        close(x->fd);
-        free(x);
-        return SHD_ENOMEM;
-    }
-    x->base = mmap(NULL, x->map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, x->fd, 0);
-    if (x->base == MAP_FAILED) { close(x->fd); free(x); return SHD_ENOMEM; }
+    const int rc = rank == 0 ? xhost_create(x) : xhost_join(x);
+    if (rc) { free(x); return rc; }
     *out = x;
     return shd_xhost_barrier(x);
-}
-
-static double mono_s(void) {
-    struct timespec t;
-    clock_gettime(CLOCK_MONOTONIC, &t);
-    return t.tv_sec + t.tv_nsec * 1e-9;
 }
 
 /* a generation barrier; SHD_ENODEV if the others do not arrive in time.  A
@@ -87,7 +156,8 @@ static double mono_s(void) {
  * trusted): the ranks waiting, and every later barrier, fail at once. */
 int shd_xhost_barrier(shd_xhost* x) {
     struct shd_xhost_hdr* h = (struct shd_xhost_hdr*)x->base;
-    if (__atomic_load_n(&h->broken, __ATOMIC_ACQUIRE)) return SHD_ENODEV;
+    if (__atomic_load_n(&h->broken, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->superseded, __ATOMIC_ACQUIRE))
+        return SHD_ENODEV;
     const uint32_t g = __atomic_load_n(&h->gen, __ATOMIC_ACQUIRE);
     if (__atomic_add_fetch(&h->count, 1, __ATOMIC_ACQ_REL) == (uint32_t)x->world) {
         __atomic_store_n(&h->count, 0, __ATOMIC_RELAXED);
@@ -98,7 +168,8 @@ int shd_xhost_barrier(shd_xhost* x) {
     unsigned spins = 0;
     while (__atomic_load_n(&h->gen, __ATOMIC_ACQUIRE) == g) {
         if (++spins > 1000) sched_yield();
-        if (__atomic_load_n(&h->broken, __ATOMIC_ACQUIRE)) return SHD_ENODEV;
+        if (__atomic_load_n(&h->broken, __ATOMIC_ACQUIRE) || __atomic_load_n(&h->superseded, __ATOMIC_ACQUIRE))
+            return SHD_ENODEV;
         if ((spins & 0xFFF) == 0 && mono_s() - t0 > x->timeout_s) {
             fprintf(stderr, "libshdgpu: host transport %s: rank %d waited %.0f s at a barrier\n", x->name, x->rank,
                     x->timeout_s);

@@ -192,7 +192,19 @@ class TcpResult(C.Structure):
     _fields_ = [("lines", C.c_void_p), ("len", C.c_size_t), ("n_lines", C.c_uint64),
                 ("next_event_id", P(C.c_uint64)), ("next_packet_id", P(C.c_uint64)),
                 ("rng_probe", P(C.c_uint32)), ("rounds", C.c_uint64), ("events", C.c_uint64),
-                ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64)]
+                ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64),
+                ("queries", C.c_void_p), ("n_queries", C.c_uint64)]
+
+
+TCP_QUERY_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("src", "<u4"), ("index", "<u4"),
+                            ("v_src", "<i4"), ("v_dst", "<i4"), ("_pad", "<u4")])   # shd_tcp_query
+
+
+class Lines(C.Structure):
+    """shd_lines (include/shdgpu.h): line i is text[off[i]:off[i+1]], logged at
+    time[i] by host[i]"""
+    _fields_ = [("n", C.c_uint64), ("time", C.POINTER(C.c_uint64)), ("host", C.POINTER(C.c_uint32)),
+                ("off", C.POINTER(C.c_uint64)), ("text", C.c_void_p)]
 
 
 _SIGS = {
@@ -254,6 +266,12 @@ _SIGS = {
     "shd_eng_path_counts": (C.c_int, [C.c_void_p, P(C.c_uint64), C.c_uint64, P(C.c_uint64)]),
     "shd_eng_heartbeats": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint64, P(C.c_uint64)]),
     "shd_eng_stream": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
+    "shd_status_lines": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint32), P(C.c_uint32), C.c_uint32, C.c_uint32,
+                                   C.c_uint32, P(P(Lines))]),
+    "shd_node_lines": (C.c_int, [P(C.c_uint32), C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P(P(Lines))]),
+    "shd_eng_status_lines": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32, P(P(Lines))]),
+    "shd_eng_node_lines": (C.c_int, [C.c_void_p, C.c_uint32, P(P(Lines))]),
+    "shd_lines_free": (None, [P(Lines)]),
     "shd_eng_last_kernel_ms": (C.c_int, [C.c_void_p, P(C.c_double)]),
     "shd_eng_destroy": (None, [C.c_void_p]),
     "shd_version": (C.c_char_p, []),
@@ -453,7 +471,45 @@ def _counter_string(packets: int, payload: int) -> str:
     return ",".join(str(x) for x in f)
 
 
+def take_lines(ptr) -> list:
+    """[(time_ns, host, line)] of a shd_lines* made by the library, which is freed"""
+    try:
+        L = ptr.contents
+        n = int(L.n)
+        if n == 0:
+            return []
+        off = np.ctypeslib.as_array(L.off, shape=(n + 1,)).copy()
+        t = np.ctypeslib.as_array(L.time, shape=(n,)).tolist()
+        h = np.ctypeslib.as_array(L.host, shape=(n,)).tolist()
+        text = C.string_at(L.text, int(off[-1])).decode()
+        return [(t[i], h[i], text[off[i]:off[i + 1]]) for i in range(n)]
+    finally:
+        lib().shd_lines_free(ptr)
+
+
+def _ips_u32(ips) -> np.ndarray:
+    out = np.empty(len(ips), dtype=np.uint32)
+    for i, ip in enumerate(ips):
+        if isinstance(ip, str):
+            a = [int(x) for x in ip.split(".")]
+            out[i] = (a[0] << 24) | (a[1] << 16) | (a[2] << 8) | a[3]
+        else:
+            out[i] = int(ip)
+    return out
+
+
 def tracker_node_lines(snapshots, interval_ns: int, payload: int) -> list:
+    """The [shadow-heartbeat] [node] lines of one host (tracker.c:419-465), made
+    by the library's writer (shd_node_lines) from the host's cumulative
+    interface counters at each heartbeat ([K, 2] uint32 in/out)."""
+    snap = np.ascontiguousarray(np.asarray(snapshots, dtype=np.uint32).reshape(-1, 2))
+    out = C.POINTER(Lines)()
+    check(lib().shd_node_lines(snap.ctypes.data_as(C.POINTER(C.c_uint32)), len(snap), int(interval_ns),
+                               int(payload), 0, C.byref(out)), "shd_node_lines")
+    return [x[2] for x in take_lines(out)]
+
+
+def tracker_node_lines_py(snapshots, interval_ns: int, payload: int) -> list:
     """The [shadow-heartbeat] [node] lines of one host (tracker.c:419-465) from its
     cumulative interface counters at each heartbeat (shd_eng_heartbeats: [K, 2]
     uint32 in/out).  Every counter is cleared at each heartbeat (tracker.c:584-593),
@@ -530,6 +586,22 @@ def ip_string(ip) -> str:
 
 
 def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT) -> list:
+    """[STATUS] lines of a run traced with SHD_QF_TRACE_STATUS, made by the
+    library's writer (shd_status_lines, include/shdgpu.h): a list of
+    (time_ns, host index, line).  status_lines_py is the same algorithm in
+    Python (tests/test_status_cpu.py checks the two against each other)."""
+    tr = np.ascontiguousarray(np.asarray(trace, dtype=TRACE_DTYPE))
+    ip = _ips_u32(ips)
+    ids = None if host_ids is None else np.ascontiguousarray(np.asarray(host_ids, dtype=np.uint32))
+    out = C.POINTER(Lines)()
+    check(lib().shd_status_lines(tr.ctypes.data if len(tr) else None, len(tr),
+                                 ip.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                 None if ids is None else ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                 len(ip), int(payload), int(listen_port), C.byref(out)), "shd_status_lines")
+    return take_lines(out)
+
+
+def status_lines_py(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT) -> list:
     """[STATUS] lines of a run traced with SHD_QF_TRACE_STATUS: a list of
     (time_ns, host index, line), line = "[<STATUS>] packetID=<hostID>:<pkt>
     <srcIP>:<srcPort> -> <dstIP>:<dstPort> bytes=<n> status=<S1>,...,<Sk>"

@@ -208,6 +208,24 @@ class Engine:
         nloc = self.h1 - self.h0
         return out.reshape(nloc, (n.value // (2 * nloc)) if nloc else 0, 2)
 
+    def status_lines(self, ips, host_ids=None, listen_port=S.SHD_PHOLD_LISTEN_PORT) -> list:
+        """[(time_ns, host, line)]: the [STATUS] lines of the engine's trace, made
+        by the library (shd_eng_status_lines, packet.c:647-659)"""
+        ip = S._ips_u32(ips)
+        ids = None if host_ids is None else np.ascontiguousarray(np.asarray(host_ids, dtype=np.uint32))
+        out = C.POINTER(S.Lines)()
+        S.check(S.lib().shd_eng_status_lines(self.ptr, ip.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                             None if ids is None else ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                             int(listen_port), C.byref(out)), "shd_eng_status_lines")
+        return S.take_lines(out)
+
+    def node_lines(self, local_host: int) -> list:
+        """[(time_ns, host, line)]: local host l's [shadow-heartbeat] lines, made by
+        the library from its heartbeat counters (shd_eng_node_lines, tracker.c:419-465)"""
+        out = C.POINTER(S.Lines)()
+        S.check(S.lib().shd_eng_node_lines(self.ptr, int(local_host), C.byref(out)), "shd_eng_node_lines")
+        return S.take_lines(out)
+
     def path_counts(self) -> np.ndarray:
         """[T, T] uint64 packet counts per cached path entry (SHD_QF_COUNT_PATHS)."""
         n = C.c_uint64()

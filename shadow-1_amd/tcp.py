@@ -3,10 +3,22 @@
 Mirrors what a Shadow build would do around shd_tcp_run: the hosts' addresses
 and RNG states come from the config front-end (dns.c's addresses, the seed
 chain after attach), and the path latency / reliability of every host pair is
-read from the product's lazy path cache (shd_pc_lookup, topology.c:2053-2092)
-in the order the serial loop first touches the pairs: a client's connect
-(host_connectToPeer's topology_isRoutable, host.c:1224-1234) touches
-(client, server) before anything travels back.
+read from the product's lazy path cache (shd_pc_lookup, topology.c:2053-2092).
+
+Which endpoint's Dijkstra row serves a pair depends on the serial order of
+every pair's FIRST query (_topology_getPathEntry, topology.c:1969-2051):
+the tables passed to shd_tcp_run are resolved in a first-touch order, and the
+run logs each host's first query of each vertex pair with its event key
+(shd_tcp_result.queries).  The driver ranks the logged queries in serial
+order (time, host, src, seq, index within the event), replays them through a
+fresh lazy cache and compares the values every logged pair gets with the ones
+the run used: equal, the run's order of first touches IS the serial one (the
+run is a deterministic function of the values, so the serial loop with these
+values makes the same queries in the same order); otherwise the run is
+repeated with the new tables, until they agree (first_touch_runs in the
+result).  The first guess is a client's connect touching (client, server)
+first (topology_isRoutable, host.c:1224-1234), clients by start time: right
+for the echo application, so one run.
 """
 from __future__ import annotations
 
@@ -22,40 +34,85 @@ SEND_BUF = 131072   # CONFIG_SEND_BUFFER_SIZE (definitions.h:153)
 TCP_WINDOW = 10     # --tcp-windows default (options.c:79)
 
 
-def path_table(model: S.ModelArrays, g: S.GraphArrays, procs, peers):
+def resolve(g: S.GraphArrays, att, first_queries, pairs, V):
+    """[V, V] latency / reliability tables from a fresh lazy path cache whose
+    first touches are `first_queries` [(s, d)] in that order (vertex indices);
+    then both orientations of every pair in `pairs` (cache hits: their rows
+    have run).  Pairs not listed stay -1."""
+    lat = np.full((V, V), -1.0)
+    rel = np.full((V, V), -1.0)
+    pc = sim.PathCache(g, att)
+    try:
+        for s, d in first_queries:
+            pc.lookup(att[s], att[d])
+        for s, d in pairs:
+            for x, y in ((s, d), (d, s)):
+                lat[x, y], rel[x, y] = pc.lookup(att[x], att[y])
+    finally:
+        pc.close()
+    return lat, rel
+
+
+def path_table(model: S.ModelArrays, g: S.GraphArrays, procs, peers, reverse=False):
     """Latency (ms) and reliability per pair of attached vertices ([V, V],
     V = the distinct vertices the hosts sit on) from the path cache, pairs
-    resolved in first-touch order (clients by start time); pairs no
-    connection uses stay -1.  Returns (lat, rel, host -> vertex index)."""
+    resolved in the first guess of the first-touch order (clients by start
+    time, each touching (client, server) first); pairs no connection uses stay
+    -1; reverse: the clients in reverse order (a wrong guess, for tests).
+    Returns (lat, rel, host -> vertex index, attached vertices)."""
     m = model.struct
     H = int(m.n_hosts)
     hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
     att, hvi = np.unique(hv, return_inverse=True)
-    V = len(att)
-    pc = sim.PathCache(g, att)
-    lat = np.full((V, V), -1.0)
-    rel = np.full((V, V), -1.0)
-    order = sorted((p[1], k) for k, p in enumerate(procs) if peers[k] >= 0)
-    try:
-        for _, k in order:
-            a, b = hvi[procs[k][0]], hvi[procs[peers[k]][0]]
-            for s, d in ((a, b), (b, a)):
-                if lat[s, d] < 0:
-                    lat[s, d], rel[s, d] = pc.lookup(att[s], att[d])
-    finally:
-        pc.close()
-    return lat, rel, hvi.astype(np.int32)
+    order = sorted(((p[1], k) for k, p in enumerate(procs) if peers[k] >= 0), reverse=reverse)
+    q = [(hvi[procs[k][0]], hvi[procs[peers[k]][0]]) for _, k in order]
+    lat, rel = resolve(g, att, q, q, len(att))
+    return lat, rel, hvi.astype(np.int32), att
+
+
+def serial_first_queries(queries: np.ndarray):
+    """The logged first queries in serial order (event_compare's key, then the
+    query's index within the event): [(s, d)] vertex pairs, and the distinct
+    unordered pairs"""
+    q = queries[np.lexsort((queries["index"], queries["seq"], queries["src"], queries["host"], queries["time"]))]
+    order = [(int(a), int(b)) for a, b in zip(q["v_src"], q["v_dst"])]
+    pairs = sorted({(min(a, b), max(a, b)) for a, b in order})
+    return order, pairs
 
 
 def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000, trace=True,
-        recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0):
+        recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0, guess_reversed=False):
     """Run the TCP echo model on the GPU: procs = [(host, start ns)], peers =
     [-1 | server process]; ips: host-order uint32 per host.  Returns
     dict(lines=[(t, h, line)] in each host's order, next_event_id,
-    next_packet_id, rng_probe, rounds, events, device_ms)."""
+    next_packet_id, rng_probe, rounds, events, device_ms, first_touch_runs).
+    guess_reversed: start from a wrong first-touch guess (tests)."""
+    lat, rel, hvi, att = path_table(model, g, procs, peers, reverse=guess_reversed)
+    V = lat.shape[0]
+    for runs in range(1, 9):
+        out = _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
+                        packets_per_host)
+        order, pairs = serial_first_queries(out.pop("queries"))
+        lat2, rel2 = resolve(g, att, order, pairs, V)
+        ij = tuple(np.array([(a, b) for a, b in pairs] + [(b, a) for a, b in pairs], dtype=np.int64).T) \
+            if pairs else (np.zeros(0, np.int64), np.zeros(0, np.int64))
+        same = np.array_equal(lat[ij].view(np.uint64), lat2[ij].view(np.uint64)) and \
+            np.array_equal(rel[ij].view(np.uint64), rel2[ij].view(np.uint64))
+        if same:
+            out["first_touch_runs"] = runs
+            out["first_touch_pairs"] = len(pairs)
+            return out
+        # the serial order of this run's first touches: run again on it
+        lat, rel = lat.copy(), rel.copy()
+        lat[ij], rel[ij] = lat2[ij], rel2[ij]
+    raise S.ShdError("shd_tcp_run: the first-touch order did not settle in 8 runs")
+
+
+def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
+              packets_per_host):
+    """one shd_tcp_run on the given path tables"""
     m = model.struct
     H = int(m.n_hosts)
-    lat, rel, hvi = path_table(model, g, procs, peers)
     keep = dict(ip=np.ascontiguousarray(ips, dtype=np.uint32), hv=np.ascontiguousarray(hvi),
                 lat=np.ascontiguousarray(lat), rel=np.ascontiguousarray(rel),
                 ph=np.ascontiguousarray([p[0] for p in procs], dtype=np.int32),
@@ -98,7 +155,10 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
                    next_packet_id=np.ctypeslib.as_array(r.next_packet_id, shape=(H,)).copy(),
                    rng_probe=np.ctypeslib.as_array(r.rng_probe, shape=(H,)).copy(),
                    rounds=int(r.rounds), events=int(r.events), deliveries=int(r.deliveries),
-                   device_ms=float(r.device_ms))
+                   device_ms=float(r.device_ms),
+                   queries=np.frombuffer(C.string_at(r.queries, int(r.n_queries) * S.TCP_QUERY_DTYPE.itemsize),
+                                         dtype=S.TCP_QUERY_DTYPE).copy() if r.n_queries else
+                   np.zeros(0, dtype=S.TCP_QUERY_DTYPE))
     finally:
         S.lib().shd_tcp_result_free(res)
     return out

@@ -35,7 +35,8 @@ class Cfg(C.Structure):
                 ("heartbeat_interval", C.c_uint64), ("app_start", C.c_uint64),
                 ("load", C.c_uint32), ("payload", C.c_uint32),
                 ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p),
-                ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32)]
+                ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32),
+                ("quiet", C.c_int32), ("_pad4", C.c_int32)]
 
 
 class Out(C.Structure):
@@ -64,7 +65,7 @@ def _ptr(a, ct):
     return None if a is None else a.ctypes.data_as(P(ct))
 
 
-def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None):
+def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False):
     """run_inproc in a forked child: the reference keeps process-wide state
     (the worker's thread-private object, glib quarks), so one run per process."""
     import multiprocessing as mp
@@ -73,7 +74,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp
 
     def child():
         try:
-            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp)))
+            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp, quiet)))
         except BaseException as ex:   # noqa: BLE001 -- reported to the parent
             wr.send(("err", repr(ex)))
         wr.close()
@@ -91,7 +92,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp
     return res
 
 
-def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None):
+def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False):
     """Run the model through the reference's loop; returns dict(lines=[(t, h, line)],
     ip=[str], next_event_id, next_packet_id, rng_probe (uint arrays)).
     host_start: [H] process start times (default: the model's app_start);
@@ -108,6 +109,7 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     keep = []
     cfg = Cfg()
     cfg.n_hosts = H
+    cfg.quiet = 1 if quiet else 0
     cfg.app = 0 if tcp is None else 1
     if tcp is not None:
         pp = np.ascontiguousarray(tcp["peers"], dtype=np.int32)
@@ -145,7 +147,10 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     cfg.root_dir = tmp.encode()
     out = Out()
     try:
+        import time
+        t0 = time.perf_counter()
         rc = lib().ref_loop_run(C.byref(cfg), C.byref(out))
+        run_s = time.perf_counter() - t0
         assert rc == 0, rc
         text = C.string_at(out.lines, out.len).decode() if out.len else ""
         ips = [".".join(str((x >> s) & 255) for s in (24, 16, 8, 0))
@@ -163,7 +168,7 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
         res = dict(lines=lines, ip=ips,
                    next_event_id=np.ctypeslib.as_array(out.next_event_id, shape=(H,)).copy(),
                    next_packet_id=np.ctypeslib.as_array(out.next_packet_id, shape=(H,)).copy(),
-                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy())
+                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy(), run_s=run_s)
         lib().ref_loop_free(C.byref(out))
     finally:
         O.lib().o_topo_free(topo)

@@ -9,7 +9,8 @@ one vertex with a 50 ms self-loop, loss 0 / 0.25, 10240 KiB/s, the server at
 them: a 2 MB transfer (slow start into congestion avoidance, buffer
 autotuning), 2 % loss on 500 kB (fast retransmit, SACK ranges), slow links
 (CoDel queues at the receiver), heavy loss (RTO backoff), ten pairs on a lossy
-geometric graph, and hosts running several servers and clients at once.
+geometric graph, hosts running several servers and clients at once, and a
+pair whose first touch comes from the server's side.
 """
 import hashlib
 
@@ -44,6 +45,19 @@ def _shared_hosts():
     return dict(graph=g, hv=[0, 3, 7], procs=procs, peers=[-1, -1, -1, 1, 2, 0, 2], nbytes=200000, end=60, bw={})
 
 
+def _server_first():
+    """the server side touches first: host 1 runs two servers and, at 2 s, a
+    client of host 0's server, so vertex 17's row runs first; at 3 s host 2
+    connects to one of host 1's servers and at 4 s host 0 to the other -- (0, 17)
+    is then served by the row of 17, the server's vertex, not the connecting
+    client's (a 40-vertex geometric graph: multi-hop paths whose two
+    orientations differ in the last bits).  (test_tcp.c's server serves one
+    peer and closes its listener: one server per client.)"""
+    g = W.geometric_graph(40, seed=6, loss_max=0.01)
+    procs = [(0, SEC), (1, SEC), (1, SEC), (1, 2 * SEC), (2, 3 * SEC), (0, 4 * SEC)]
+    return dict(graph=g, hv=[0, 17, 33], procs=procs, peers=[-1, -1, -1, 0, 1, 2], nbytes=50000, end=30, bw={})
+
+
 CASES = {
     "ref_epoll_lossless": lambda: _pair(50.0, 0.0, 20000, 300),
     "ref_epoll_lossy": lambda: _pair(50.0, 0.25, 20000, 300),
@@ -53,6 +67,7 @@ CASES = {
     "heavy_loss": lambda: _pair(30.0, 0.25, 200000, 200),
     "geo_pairs": _geo_pairs,
     "shared_hosts": _shared_hosts,
+    "server_first": _server_first,
 }
 
 

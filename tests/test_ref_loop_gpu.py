@@ -5,9 +5,10 @@ scheduler.c, host.c, network_interface.c, router*.c, descriptor/*.c,
 tracker.c, packet.c compiled unmodified from /root/reference
 (tests/golden/make_ref_loop.py) -- logged and ended in for the models of
 tests/ref_loop_cases.py.  The engine runs the same models through
-libshdgpu.so; its trace makes the [STATUS] lines (shdgpu.status_lines), its
-tracker counters the [node] lines, and both, with every host's event-ID and
-packet counters and RNG state, must be the reference's.
+libshdgpu.so; the library's writers make the [STATUS] lines from its trace
+(shd_eng_status_lines) and the [node] lines from its tracker counters
+(shd_eng_node_lines), and both, with every host's event-ID and packet counters
+and RNG state, must be the reference's.
 """
 import json
 import os
@@ -39,10 +40,14 @@ def test_engine_equals_reference_loop(name):
         eng.boot()
         eng.push_events(case["pushes"])
     eng.run()
-    st = sorted(S.status_lines(eng.trace(), fx["ips"], payload=int(m.struct.payload)),
-                key=lambda x: (x[0], x[1]))
+    # the library's own writers (shd_eng_status_lines / shd_eng_node_lines: what a
+    # Shadow build linking the C-ABI logs), from the device trace and counters
+    st = sorted(eng.status_lines(fx["ips"]), key=lambda x: (x[0], x[1]))
     assert len(st) == fx["n_status"]
     assert RC.digest_lines(st) == fx["status_sha256"]
+    hbl = sorted((x for h in range(m.n_hosts) for x in eng.node_lines(h)), key=lambda x: (x[0], x[1]))
+    assert len(hbl) == fx["n_heartbeat"]
+    assert RC.digest_lines(hbl) == fx["heartbeat_sha256"]
     hb = eng.heartbeats()
     assert RC.digest_lines(RC.heartbeat_lines(m, hb, hb.shape[1])) == fx["heartbeat_sha256"]
     dg = eng.digest()

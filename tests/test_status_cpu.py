@@ -84,3 +84,28 @@ def test_oracle_status_trace_is_well_formed():
     otr2, _, _ = O.engine_run(m2, g)
     assert not np.any(otr2["kind"] >= S.TR_CREATED)
     assert len(otr2) == len(otr) - kinds[S.TR_CREATED] - kinds[S.TR_READ]
+
+
+def test_c_writer_equals_the_python_restatement():
+    """libshdgpu's writers (shd_status_lines, shd_node_lines: the C-ABI a Shadow
+    build links) against the Python restatement of the same algorithm, line for
+    line and in the same order: an oracle status trace with CoDel drops,
+    interface drops past the end and loopback sends, and heartbeat snapshots
+    with a 32-bit wrap.  (test_ref_loop_cpu.py pins the writer to the
+    reference's own lines.)"""
+    V = 30
+    g = W.geometric_graph(V, seed=5)
+    for kw in ({}, {"payload": 1500, "bw_down": 512, "load": 6}):
+        m = W.phold_model(W.hosts_on_vertices(V, 2), end_time=2 * S.SHD_SEC, trace=True,
+                          queue_flags=S.SHD_QF_TRACE_STATUS, **({"load": 3} | kw))
+        otr, _, _ = O.engine_run(m, g)
+        ips = ["10.%d.%d.%d" % (h >> 16, (h >> 8) & 255, h & 255) for h in range(2 * V)]
+        ids = [3 * h + 2 for h in range(2 * V)]
+        for pl in (1, 1500):
+            c = S.status_lines(otr, ips, host_ids=ids, payload=pl)
+            assert c == S.status_lines_py(otr, ips, host_ids=ids, payload=pl)
+            assert len(c) > len(otr)
+    snaps = np.array([[5, 7], [9, 9], [0xFFFFFFF0, 20], [3, 25]], dtype=np.uint32)
+    for pl in (0, 1, 1500):
+        assert S.tracker_node_lines(snaps, S.SHD_SEC, pl) == S.tracker_node_lines_py(snaps, S.SHD_SEC, pl)
+        assert S.tracker_node_lines(snaps[:0], 2 * S.SHD_SEC, pl) == S.tracker_node_lines_py(snaps[:0], 2 * S.SHD_SEC, pl)

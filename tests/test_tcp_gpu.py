@@ -8,6 +8,7 @@ difference when there is one."""
 import json
 import os
 
+import numpy as np
 import pytest
 
 import oracle_ffi as O
@@ -53,3 +54,28 @@ def test_tcp_gpu_scaled_model_equals_oracle(hosts, loss):
     assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
     assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
     assert r["events"] == o["events"] and r["deliveries"] > 0
+
+
+@pytest.mark.parametrize("name", ["geo_pairs", "shared_hosts", "server_first"])
+def test_tcp_gpu_first_touch_order_settles(name):
+    """The path tables start from a wrong first-touch order (the clients
+    reversed): the run's first-query log ranks the touches in serial order and
+    the driver reruns until the tables agree (shadow-1_amd/tcp.py) -- the end
+    result is the reference's, whatever the first guess."""
+    f = FIX[name]
+    c, m = TC.build(name)
+    ips = TC.ip_ints(f["ips"])
+    r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], guess_reversed=True)
+    assert TC.digest(r["lines"]) == f["status_by_host_sha256"]
+    assert r["next_event_id"].tolist() == f["next_event_id"]
+    assert r["rng_probe"].tolist() == f["rng_probe"]
+    assert r["first_touch_pairs"] > 0
+    # where the reversed guess serves some pair from the other endpoint's row
+    # (and the two orientations differ in their bits), a second run settles it
+    lat_r, rel_r, _, _ = TCPGPU.path_table(m, c["graph"], c["procs"], c["peers"], reverse=True)
+    lat_c, rel_c, _, _ = TCPGPU.path_table(m, c["graph"], c["procs"], c["peers"])
+    wrong = not (np.array_equal(lat_r.view(np.uint64), lat_c.view(np.uint64)) and
+                 np.array_equal(rel_r.view(np.uint64), rel_c.view(np.uint64)))
+    assert r["first_touch_runs"] == (2 if wrong else 1)
+    if name == "server_first":
+        assert wrong   # the case is built so that the order matters
