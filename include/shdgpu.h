@@ -280,7 +280,20 @@ typedef struct shd_model {
     int32_t _pad1;
     /* <host heartbeatfrequency> per host (ns), tracker interval (host.c:240) */
     const uint64_t* host_heartbeat; /* [H] or NULL                             */
+    /* The application every host runs (the device application hook):
+     *   SHD_APP_PHOLD     test_phold.c (load, dest_cum, host_class above);
+     *   SHD_APP_UDP_ECHO  a UDP request/response echo: app_peer[h] = -1 makes h a
+     *                     server on PHOLD's port answering every datagram it reads
+     *                     with `payload` bytes to the sender's address and port;
+     *                     app_peer[h] = s makes h a client of server host s that
+     *                     keeps `load` requests in flight on one socket (the
+     *                     first sendto binds it: one random port). */
+    uint32_t app;                   /* SHD_APP_*                               */
+    int32_t _pad2;
+    const int32_t* app_peer;        /* [H] (SHD_APP_UDP_ECHO) or NULL          */
 } shd_model;
+
+enum { SHD_APP_PHOLD = 0, SHD_APP_UDP_ECHO = 1 };
 
 /* queue_flags: SHD_QF_NO_CALENDAR routes every inter-host event through the
  * per-host inbox and heap (the calendar's fallback path), for testing */
@@ -531,10 +544,13 @@ typedef struct shd_lines {
  * packet.c:518-547, 616-633), and PDS_DESTROYED where a packet object's last
  * reference goes (packet.c:194-201; not the frees at teardown).  ips[h]: host
  * h's address (host order), host_ids[h] its host_getID (NULL: h + 1),
- * listen_port the destination port.  Ordered by (time, host), each host's
- * lines in the reference's call-chain order. */
+ * listen_port the destination port; app_peer: NULL (PHOLD) or the model's
+ * SHD_APP_UDP_ECHO roles -- a datagram to a client goes to the port its socket
+ * was bound to (its own datagrams' source port).  Ordered by (time, host),
+ * each host's lines in the reference's call-chain order. */
 int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, const uint32_t* host_ids,
-                     uint32_t n_hosts, uint32_t payload, uint32_t listen_port, shd_lines** out);
+                     uint32_t n_hosts, uint32_t payload, uint32_t listen_port, const int32_t* app_peer,
+                     shd_lines** out);
 /* The [shadow-heartbeat] lines of _tracker_logNode (tracker.c:419-465) of one
  * host: the header and the all-zero boot line at t = 0 (tracker_new's inline
  * heartbeat, tracker.c:141), then one line per snapshot k at (k+1)*interval

@@ -83,6 +83,10 @@ typedef struct {
      * in (_networkinterface_receivePacket) and out (_networkinterface_sendPackets);
      * cumulative here, differenced per heartbeat by the reader */
     uint32_t if_in, if_out;
+    /* SHD_APP_UDP_ECHO: the sources of the datagrams the socket holds, in
+     * arrival order (recvfrom's address); a client's implicitly bound port */
+    uint32_t* rxq; uint32_t rxq_head, rxq_count, rxq_cap;
+    int bound; uint16_t port;
 } ohost;
 
 /* a send whose pair had no cache entry at round start (parallel mode): its
@@ -188,6 +192,16 @@ static void if_receive_packet(ctx_t* c, uint32_t h, uint32_t src, uint32_t pkt) 
         trace(c, c->now, 0, h, src, pkt, SHD_TR_RECV);
         H->n_recv++;
         H->unread++;
+        if (c->m->app == SHD_APP_UDP_ECHO) {   /* the socket keeps the datagram's source */
+            if (H->rxq_count == H->rxq_cap) {
+                uint32_t ncap = H->rxq_cap ? 2 * H->rxq_cap : 16;
+                uint32_t* nq = malloc(sizeof(uint32_t) * ncap);
+                for (uint32_t i = 0; i < H->rxq_count; i++) nq[i] = H->rxq[(H->rxq_head + i) % H->rxq_cap];
+                free(H->rxq); H->rxq = nq; H->rxq_cap = ncap; H->rxq_head = 0;
+            }
+            H->rxq[(H->rxq_head + H->rxq_count) % H->rxq_cap] = src;
+            H->rxq_count++;
+        }
         /* socket readable -> epoll schedules one notification at +1 ns */
         if (!H->notify_pending) {
             schedule_task(c, h, SHD_EV_NOTIFY, 1, 0);
@@ -379,6 +393,30 @@ static void send_new_message(ctx_t* c, uint32_t h) {
     if_send_packets(c, h);
 }
 
+/* SHD_APP_UDP_ECHO (ref_loop.c app 2): one datagram of `payload` bytes to
+ * dst from the host's one socket -- a server's bound listener (PHOLD's port,
+ * no draw), a client's socket, bound by its first sendto (one random port,
+ * host.c:1514-1525); then as send_new_message */
+static void echo_send(ctx_t* c, uint32_t h, uint32_t dst) {
+    ohost* H = &c->hosts[h];
+    uint16_t port = SHD_PHOLD_LISTEN_PORT;
+    if (c->m->app_peer[h] >= 0) {
+        if (!H->bound) { H->port = random_free_port(H); H->bound = 1; }
+        port = H->port;
+    }
+    uint32_t pkt = H->pkt_seq++;
+    if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, port, h, ~0u, pkt, SHD_TR_CREATED);
+    if (H->txq_count == H->txq_cap) {
+        uint32_t ncap = H->txq_cap * 2;
+        txent* nq = malloc(sizeof(txent) * ncap);
+        for (uint32_t i = 0; i < H->txq_count; i++) nq[i] = H->txq[(H->txq_head + i) % H->txq_cap];
+        free(H->txq); H->txq = nq; H->txq_cap = ncap; H->txq_head = 0;
+    }
+    H->txq[(H->txq_head + H->txq_count) % H->txq_cap] = (txent){dst, pkt};
+    H->txq_count++;
+    if_send_packets(c, h);
+}
+
 /* _networkinterface_refillTokenBucketsCB (network_interface.c:163-183) */
 static void refill_cb(ctx_t* c, uint32_t h) {
     ohost* H = &c->hosts[h];
@@ -424,6 +462,11 @@ static void execute(ctx_t* c, const shd_event* e) {
         break;
     case SHD_EV_APP_START:
         H->listening = 1;
+        if (c->m->app == SHD_APP_UDP_ECHO) {   /* a client sends `load` requests; a server waits */
+            if (c->m->app_peer[h] >= 0)
+                for (uint32_t i = 0; i < c->m->load; i++) echo_send(c, h, (uint32_t)c->m->app_peer[h]);
+            break;
+        }
         for (uint32_t i = 0; i < c->m->load; i++) send_new_message(c, h);
         break;
     case SHD_EV_PACKET: {
@@ -446,7 +489,14 @@ static void execute(ctx_t* c, const shd_event* e) {
          * (PDS_RCV_SOCKET_DELIVERED, udp.c:158) answered by one new message */
         for (uint32_t i = 0; i < n; i++) {
             if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, 0, h, ~0u, ~0u, SHD_TR_READ);
-            send_new_message(c, h);
+            if (c->m->app == SHD_APP_UDP_ECHO) {   /* the reply to the sender, or the next request */
+                const uint32_t src = H->rxq[H->rxq_head];
+                H->rxq_head = (H->rxq_head + 1) % H->rxq_cap;
+                H->rxq_count--;
+                echo_send(c, h, c->m->app_peer[h] < 0 ? src : (uint32_t)c->m->app_peer[h]);
+            } else {
+                send_new_message(c, h);
+            }
         }
         break;
     }

@@ -78,7 +78,7 @@ typedef int (*ref_path_fn)(void* ctx, int32_t src_vertex, int32_t dst_vertex, do
 
 typedef struct ref_loop_cfg {
     int32_t n_hosts;
-    int32_t app;                  /* 0 = PHOLD-UDP (test_phold.c) */
+    int32_t app;                  /* 0 = PHOLD-UDP (test_phold.c), 1 = TCP echo, 2 = UDP echo */
     const uint32_t* host_seed;    /* [H] host RNG state after attach (the model's host_rng) */
     const int32_t* host_vertex;   /* [H] */
     const uint64_t* bw_down_kibps, *bw_up_kibps;   /* [H] */
@@ -363,6 +363,71 @@ static void phold_continue(Process* proc) {
     }
 }
 
+/* ---- app 2: a UDP request/response echo over the same host_* calls (the
+ * device application hook's second application, shdgpu.h SHD_APP_UDP_ECHO).
+ * A server (peer -1) binds PHOLD_LISTEN_PORT and answers every datagram it
+ * reads with one of `payload` bytes to the sender's address and port, from
+ * its bound socket; a client opens one socket, sends `load` requests to its
+ * server's listener (the first sendto binds the socket implicitly: one
+ * random port, host.c:1514-1525) and answers every reply it reads with a new
+ * request on the same socket -- a closed loop of `load` requests in flight.
+ * cfg->proc_peer is indexed by host here: the server host of each client. */
+static const gchar g_echo_buf[65536];
+
+static void echo_send(Process* proc, in_addr_t ip, in_port_t port) {
+    gsize bytes = 0;
+    (void)host_sendUserData(proc->host, proc->listenfd, (gpointer)g_echo_buf, g_cfg->payload ? g_cfg->payload : 1,
+                            ip, (in_addr_t)port, &bytes);
+}
+
+static void echo_start(Process* proc) {
+    Host* host = proc->host;
+    const int32_t h = host_index_of(host_getID(host));
+    const int32_t peer = g_cfg->proc_peer[h];
+    proc->listenfd = host_createDescriptor(host, DT_UDPSOCKET);
+    Descriptor* desc = host_lookupDescriptor(host, proc->listenfd);
+    descriptor_setFlags(desc, descriptor_getFlags(desc) | O_NONBLOCK);
+    if (peer < 0) {
+        struct sockaddr_in bindAddr;
+        memset(&bindAddr, 0, sizeof(bindAddr));
+        bindAddr.sin_family = AF_INET;
+        bindAddr.sin_addr.s_addr = htonl(INADDR_ANY);
+        bindAddr.sin_port = htons(PHOLD_LISTEN_PORT);
+        (void)host_bindToInterface(host, proc->listenfd, (struct sockaddr*)&bindAddr);
+    }
+    proc->epollfd = host_createDescriptor(host, DT_EPOLL);
+    struct epoll_event ev;
+    memset(&ev, 0, sizeof(ev));
+    ev.events = EPOLLIN;
+    ev.data.fd = proc->listenfd;
+    (void)host_epollControl(host, proc->epollfd, EPOLL_CTL_ADD, proc->listenfd, &ev);
+    if (peer >= 0)
+        for (uint32_t i = 0; i < g_cfg->load; i++)
+            echo_send(proc, host_getDefaultIP(g_hosts[peer]), htons(PHOLD_LISTEN_PORT));
+}
+
+/* every readable datagram answered (as phold_continue's loop) */
+static void echo_continue(Process* proc) {
+    Host* host = proc->host;
+    const int32_t peer = g_cfg->proc_peer[host_index_of(host_getID(host))];
+    for (;;) {
+        struct epoll_event evs[10];
+        gint nfds = 0;
+        if (host_epollGetEvents(host, proc->epollfd, evs, 10, &nfds) != 0 || nfds <= 0) break;
+        for (gint i = 0; i < nfds; i++) {
+            for (;;) {
+                gchar buffer[65536];
+                in_addr_t ip = 0;
+                in_port_t port = 0;
+                gsize nBytes = 0;
+                gint rc = host_receiveUserData(host, proc->listenfd, buffer, sizeof(buffer), &ip, &port, &nBytes);
+                if (rc != 0 || nBytes == 0) break;
+                if (peer < 0) echo_send(proc, ip, port);
+                else echo_send(proc, host_getDefaultIP(g_hosts[peer]), htons(PHOLD_LISTEN_PORT));
+            }
+        }
+    }
+}
 
 /* ---- app 1: src/test/tcp/test_tcp.c's echo test in its nonblocking-epoll
  * mode (_run_server / _run_client, test_tcp.c:713-810), restated over the
@@ -524,6 +589,7 @@ static void process_start_task(Process* proc, gpointer nothing) {
     proc->running = TRUE;
     if (g_cfg->app == 0) phold_start(proc);
     else if (g_cfg->app == 1) tcp_start(proc);
+    else if (g_cfg->app == 2) echo_start(proc);
     worker_setActiveProcess(NULL);
 }
 static void process_stop_task(Process* proc, gpointer nothing) { process_stop(proc); }
@@ -552,6 +618,7 @@ void process_continue(Process* proc) {
     worker_setActiveProcess(proc);
     if (g_cfg->app == 0) phold_continue(proc);
     else if (g_cfg->app == 1) tcp_continue(proc);
+    else if (g_cfg->app == 2) echo_continue(proc);
     worker_setActiveProcess(NULL);
 }
 

@@ -7,7 +7,12 @@
 #pragma once
 
 constexpr uint64_t kInf = 0xFFFFFFFFFFFFFFFFull;
-constexpr uint32_t F_REFILL_PENDING = 1u, F_NOTIFY_PENDING = 2u, F_LISTENING = 4u, F_CODEL_DROP_MODE = 8u;
+constexpr uint32_t F_REFILL_PENDING = 1u, F_NOTIFY_PENDING = 2u, F_LISTENING = 4u, F_CODEL_DROP_MODE = 8u,
+                   F_BOUND = 16u;   // a UDP echo client's socket is bound (its first sendto drew the port)
+// a send's destination draw (TxEnt::r, SendRec::r): a rand_r value (PHOLD's
+// destination pick, resolved at the flush), or a host named by the
+// application (the UDP echo's server or the sender being answered)
+constexpr uint32_t kDstHost = 0x80000000u;
 constexpr double kRandMax = 2147483647.0;
 constexpr uint64_t kCodelTarget = 10ull * SHD_MS;      // router_queue_codel.c:42
 constexpr uint64_t kCodelInterval = 100ull * SHD_MS;   // router_queue_codel.c:48
@@ -78,7 +83,8 @@ struct alignas(128) HostRec {
     uint16_t cq_head, cq_count, tq_head, tq_count;   // FIFO heads / lengths
     uint32_t evq_n;
     uint32_t if_in, if_out;                // tracker node counters: interface packets in / out (cumulative)
-    uint32_t pad;
+    uint16_t rq_head;                      // UDP echo: the head of the socket's source ring (its length is unread)
+    uint16_t port;                         // UDP echo client: its socket's port (F_BOUND)
 };
 static_assert(sizeof(HostRec) == 128, "host record: one 128-B line, 8 x 16 B");
 
@@ -165,7 +171,8 @@ static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 
 constexpr int kDestExc = 16;   // closed-form destination exceptions (ParamsT::exc_x)
 // ParamsT::feat: the model's optional features (all off on the bench's models)
-constexpr uint32_t F_TRACE = 1u, F_HB = 2u, F_PCOUNT = 4u, F_HOSTHB = 8u, F_AMBIG = 16u, F_STATUS = 64u;
+constexpr uint32_t F_TRACE = 1u, F_HB = 2u, F_PCOUNT = 4u, F_HOSTHB = 8u, F_AMBIG = 16u, F_STATUS = 64u,
+                   F_ECHO = 128u;   // the application is SHD_APP_UDP_ECHO
 
 template <template <class> class Ptr>
 struct ParamsT {
@@ -212,6 +219,12 @@ struct ParamsT {
     // are self_thr[h].x <= x <= self_thr[h].y (precomputed, exact); .w = class
     Ptr<const int4> self_thr;
     Ptr<const uint64_t> host_hb;     // per-host heartbeat interval [H] (null: `heartbeat`)
+    // the application (shd_model::app): SHD_APP_PHOLD, or SHD_APP_UDP_ECHO with
+    // app_peer[h] = -1 (server) | the server host, and per host a ring of the
+    // sources of the datagrams its socket holds ([nloc][rq_cap], recvfrom's address)
+    uint32_t app, rq_cap;
+    Ptr<const int32_t> app_peer;
+    Ptr<uint32_t> rq;
     int32_t no_app_start;            // SHD_QF_NO_APP_START: boot schedules no application start
     // closed-form destinations (dest_closed): even weights, host h attached
     // at index h.  The draw x picks host max(ceil(x*H/RAND_MAX) - 1, 0),
@@ -423,6 +436,8 @@ struct HostCtx {
     int32_t att;                // this host's attached-vertex index
     uint32_t c_events, c_pkt, c_sent, c_idrop, c_cdrop, c_recv;   // this round's counter deltas
     uint32_t if_in, if_out;     // HostRec::if_in / if_out
+    int32_t peer;               // UDP echo: -1 a server, else the client's server host (PHOLD: -1)
+    uint32_t rq_head, port;     // HostRec::rq_head / port
     // current executing event key (for first-touch logging)
     uint64_t q_seq;
     uint32_t q_src;
@@ -435,6 +450,10 @@ struct HostCtx {
     uint32_t xput;       // peer-to-peer: this lane stored into a peer's receive block
     uint32_t err;
     uint32_t n_pend;
+    // k_round_ps: the first calendar bin the receivers did NOT load ahead for
+    // the next round (0 elsewhere): an append to an earlier bin, and every
+    // inbox append, is noted for the share (note_dirty)
+    uint64_t pf_lim;
 #ifdef SHD_PROF
     ProfAcc prof;
 #endif
@@ -452,6 +471,20 @@ __shared__ shd_event s_rx[kRxCap * kBlock];
 __shared__ uint32_t s_rxn[kBlock];
 __shared__ CodelEnt s_cqh[kBlock];               // CoDel FIFO head
 __shared__ TxEnt s_tqh[kBlock];                  // send FIFO head
+
+// k_round_ps's cross-barrier prefetch (eng_round.h): the blocks load the next
+// window's calendar bins before the round's barrier, so an append that lands
+// in a bin a receiver may already have read (before HostCtx::pf_lim), or in an
+// inbox, is noted here and published with the round's share; the receiving
+// host then reads its hand-off words after the barrier, as without prefetch
+constexpr uint32_t kDirtyMax = 3;                 // destinations one share names
+constexpr uint32_t kDirtyNone = 0xFFFFFFFFu, kDirtyAll = 0xFFFFFFFEu;
+__shared__ uint32_t s_dn;                          // appends noted this round
+__shared__ uint32_t s_dl[kDirtyMax];              // ... their local destinations (the first kDirtyMax)
+__device__ __forceinline__ void note_dirty(int32_t dl) {
+    const uint32_t k = atomicAdd(&s_dn, 1u);
+    if (k < kDirtyMax) s_dl[k] = (uint32_t)dl;
+}
 
 __device__ __forceinline__ bool ev_less(const shd_event& a, const shd_event& b) {
     if (a.time != b.time) return a.time < b.time;
@@ -677,6 +710,7 @@ __device__ __forceinline__ void st16_sys(void* p, uint4 v) {
 __device__ void emit_nocal(const DParams& P, HostCtx& c, const shd_event& e) {
     const int32_t dl = (int32_t)e.dst - P.h0;
     if (dl >= 0 && dl < P.nloc) {
+        if (c.pf_lim) note_dirty(dl);
         uint32_t slot = atomicAdd(&P.inbox_n[c.np][dl], 1u);
         if (slot >= P.inbox_cap) { c.err |= SHD_ERR_INBOX_OVERFLOW; return; }
         ev_st_sc1(&P.inbox[c.np][(size_t)dl * P.inbox_cap + slot], e);
@@ -735,6 +769,16 @@ __device__ void refill_if_needed(const DParams& P, HostCtx& c) {
 }
 __device__ __forceinline__ void consume(uint64_t& rem, uint64_t n) { rem = (n >= rem) ? 0 : rem - n; }
 
+// UDP echo: the socket keeps each datagram's source (recvfrom's address), in
+// arrival order, in a ring of rq_cap behind rq_head; its length is `unread`
+// (called after unread counted the datagram)
+__device__ __forceinline__ void rq_push(const DParams& P, HostCtx& c, uint32_t src) {
+    if (c.unread > P.rq_cap) { c.err |= SHD_ERR_INTERNAL; return; }
+    uint32_t t = c.rq_head + c.unread - 1;
+    if (t >= P.rq_cap) t -= P.rq_cap;
+    P.rq[(size_t)c.l * P.rq_cap + t] = src;
+}
+
 // _networkinterface_receivePacket (network_interface.c:375-419)
 __device__ void if_receive_packet(const DParams& P, HostCtx& c, uint32_t src, uint32_t pkt) {
     c.if_in++;   // tracker_addInputBytes (network_interface.c:415)
@@ -742,6 +786,7 @@ __device__ void if_receive_packet(const DParams& P, HostCtx& c, uint32_t src, ui
         trace(P, c, c.now, 0, c.h, src, pkt, SHD_TR_RECV);
         c.c_recv++;
         c.unread++;
+        if (c.k.feat & F_ECHO) rq_push(P, c, src);
         if (!(c.flags & F_NOTIFY_PENDING)) {   // epoll.c:345-365, +1 ns
             schedule_self(P, c, SHD_EV_NOTIFY, 1, 0);
             c.flags |= F_NOTIFY_PENDING;
@@ -1047,7 +1092,8 @@ __device__ void worker_send_deferred(const DParams& P, HostCtx& c, uint32_t rv, 
 struct PendDel {
     uint64_t bi;     // bin index
     uint32_t slot;   // claimed slot (kind 1)
-    uint32_t kind;   // 0 none, 1 calendar claim issued, 2 inbox / remote
+    uint16_t kind;   // 0 none, 1 calendar claim issued, 2 inbox / remote
+    uint16_t near;   // kind 1: the bin is before HostCtx::pf_lim (note_dirty)
 };
 
 __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool defer, PendDel& pd) {
@@ -1072,7 +1118,10 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         const uint32_t hl = q.lane;
         const int32_t a = s_att[hl];
         int32_t dst, b;
-        if (P.dest_closed) {   // no table: one memory round trip fewer
+        if (q.r & kDstHost) {   // a destination the application named (UDP echo)
+            dst = (int32_t)(q.r & ~kDstHost);
+            b = P.host_att[dst];
+        } else if (P.dest_closed) {   // no table: one memory round trip fewer
             const uint64_t nx = (uint64_t)q.r * (uint64_t)(uint32_t)P.H;
             const uint64_t cx = (nx + 2147483646ull) / 2147483647ull;
             int32_t d = cx ? (int32_t)cx - 1 : 0;
@@ -1121,6 +1170,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
                 pd.bi = (size_t)dl * kNB + ((uint32_t)bb & (kNB - 1));
                 pd.slot = atomicAdd(&P.bin_n[pd.bi], 1u);
                 pd.kind = 1;
+                pd.near = bb < c.pf_lim ? 1u : 0u;
             }
         }
     }
@@ -1201,6 +1251,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
                 ev_st_sc1(&P.bins[bi * kBinCap + slot], e);
                 const uint32_t p = (uint32_t)bb & (kNB - 1);
                 atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));
+                if (bb < c.pf_lim) note_dirty(dl);
                 continue;
             }
         }
@@ -1219,6 +1270,7 @@ __device__ __forceinline__ void flush_finish(const DParams& P, HostCtx& c, const
         const uint32_t p = (uint32_t)(pd.bi & (kNB - 1));
         const int32_t dl = (int32_t)e.dst - P.h0;
         atomicOr(&P.bin_bits[(size_t)dl * kNBW + (p >> 5)], 1u << (p & 31));
+        if (pd.near) note_dirty(dl);
         return;
     }
     emit_nocal(P, c, e);
@@ -1289,16 +1341,54 @@ __device__ __forceinline__ void app_read(const DParams& P, HostCtx& c) {
     if ((c.k.feat & F_STATUS) && (c.w_fl & W_READ)) trace(P, c, c.now, 0, c.h, ~0u, ~0u, SHD_TR_READ);
 }
 
+// The device application hook: the draws and records of one new datagram
+// before it is queued on the interface; rv: its destination draw (kDstHost |
+// host: a named destination), false when nothing is sent.  `reading`: the
+// message answers a datagram the application just read (NOTIFY's messages).
+//   PHOLD (_phold_sendNewMessage, test_phold.c:218-230): the destination draw,
+//     resolved at the flush (no destination: nothing sent), the implicit
+//     bind's port draw, SND_CREATED;
+//   UDP echo (oracle/ref_harness/ref_loop.c app 2): the datagram read leaves
+//     the socket (its source: the ring); a server answers that source from
+//     its bound listener, a client asks its server again from its one socket,
+//     bound by its first sendto (one port draw, host.c:1514-1525).
+__device__ __forceinline__ bool app_message(const DParams& P, HostCtx& c, bool reading, uint32_t& rv,
+                                            uint32_t& pkt) {
+    if (!(c.k.feat & F_ECHO)) {
+        rv = (uint32_t)rand_r_dev(c.rng);
+        if ((int32_t)rv > c.dst_thr) return false;   // no i with dest_cum[i] >= r
+        bind_and_create(P, c, c.pkt_seq);
+        pkt = c.pkt_seq++;
+        return true;
+    }
+    uint32_t dst = (uint32_t)c.peer, sport = SHD_PHOLD_LISTEN_PORT;
+    if (reading) {
+        const uint32_t src = P.rq[(size_t)c.l * P.rq_cap + c.rq_head];
+        c.rq_head = c.rq_head + 1 == P.rq_cap ? 0u : c.rq_head + 1;
+        if (c.peer < 0) dst = src;
+    }
+    if (c.peer >= 0) {
+        if (!(c.flags & F_BOUND)) {
+            c.port = random_free_port_value(c);
+            c.flags |= F_BOUND;
+        }
+        sport = c.port;
+    }
+    if (c.k.feat & F_STATUS) trace(P, c, c.now, sport, c.h, ~0u, c.pkt_seq, SHD_TR_CREATED);
+    rv = dst | kDstHost;
+    pkt = c.pkt_seq++;
+    return true;
+}
+
 // _phold_sendNewMessage (test_phold.c:218-230) up to the socket send: draw
 // the destination (resolved at the flush; only whether one exists matters
 // here), bind, queue the datagram; false when nothing was queued
 __device__ bool enqueue_new_message(const DParams& P, HostCtx& c) {
     PROF_T0(tp)
-    const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
+    uint32_t rv, pkt;
+    const bool go = app_message(P, c, (c.w_fl & W_READ) != 0, rv, pkt);
     PROF_ADD(c, PR_PICK, tp)
-    if ((int32_t)rv > c.dst_thr) return false;   // no i with dest_cum[i] >= r
-    bind_and_create(P, c, c.pkt_seq);
-    const uint32_t pkt = c.pkt_seq++;
+    if (!go) return false;
     if (c.tq_count >= c.k.tq_cap) { c.err |= SHD_ERR_TXQ_OVERFLOW; return false; }
     if (c.tq_count == 0) {
         s_tqh[threadIdx.x] = TxEnt{rv, pkt};
@@ -1347,10 +1437,8 @@ __device__ __forceinline__ bool notify_fast_ok(const DParams& P, const HostCtx& 
 __device__ __forceinline__ void notify_fast(const DParams& P, HostCtx& c) {
     c.flags &= ~F_NOTIFY_PENDING;
     c.unread = 0;
-    const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
-    if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
-        random_free_port(c);
-        const uint32_t pkt = c.pkt_seq++;
+    uint32_t rv, pkt;
+    if (app_message(P, c, true, rv, pkt)) {   // else no destination: nothing queued
         if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
             s_tqh[threadIdx.x] = TxEnt{rv, pkt};
             c.tq_hv = true;
@@ -1402,6 +1490,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         c.c_recv++;
         c.if_in++;
         c.unread++;
+        if (c.k.feat & F_ECHO) rq_push(P, c, e.src);
         c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
         c.cq_iexp = 0;
         const bool nt = !(c.flags & F_NOTIFY_PENDING);
@@ -1458,7 +1547,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         break;
     case SHD_EV_APP_START:
         c.flags |= F_LISTENING;
-        c.w_msgs = P.load;
+        c.w_msgs = ((c.k.feat & F_ECHO) && c.peer < 0) ? 0u : P.load;   // a UDP echo server waits
         break;
     case SHD_EV_PACKET: {
         // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
@@ -1517,11 +1606,10 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
     // (one exit: a loopback ends the loop through tq_count)
     while (c.w_msgs && c.tq_count == 0 && c.tx_rem >= SHD_MTU && send_room() && !boot) {
         app_read(P, c);
-        const uint32_t rv = (uint32_t)rand_r_dev(c.rng);
+        uint32_t rv, pkt;
+        const bool go = app_message(P, c, (c.w_fl & W_READ) != 0, rv, pkt);
         c.w_msgs--;
-        if ((int32_t)rv <= c.dst_thr) {   // else no destination: nothing queued
-            bind_and_create(P, c, c.pkt_seq);
-            const uint32_t pkt = c.pkt_seq++;
+        if (go) {   // else no destination: nothing queued
             if (is_self_draw(c, rv)) {   // loopback: queued; run_work sends it (after a flush)
                 s_tqh[threadIdx.x] = TxEnt{rv, pkt};
                 c.tq_hv = true;
@@ -1581,6 +1669,8 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.cq_dc = launder(r.cq_dc); c.cq_dcl = launder(r.cq_dcl); c.cq_head = launder(r.cq_head); c.cq_count = launder(r.cq_count);
     c.tq_head = launder(r.tq_head); c.tq_count = launder(r.tq_count);
     c.if_in = launder(r.if_in); c.if_out = launder(r.if_out);
+    c.rq_head = launder((uint32_t)r.rq_head); c.port = launder((uint32_t)r.port);
+    c.peer = (c.k.feat & F_ECHO) ? launder(P.app_peer[P.h0 + l]) : -1;
     c.evq_n = launder(r.evq_n);
     if (r.evq_n) {
         const shd_event t = P.evq[(size_t)l * P.evq_stride + 3];
@@ -1595,7 +1685,7 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.cq_hv = false; c.tq_hv = false;
     c.att = launder(att);
-    c.min_emit = kInf; c.err = 0; c.n_pend = 0;
+    c.min_emit = kInf; c.err = 0; c.n_pend = 0; c.pf_lim = 0;
     c.ws = 0; c.ws_mod = 0; c.dh = 0; c.nd = 0; c.dt = kInf;
     send_pool_reset(c); c.seq_base = c.ev_seq; c.np = 0;
     c.w_msgs = 0; c.w_fl = 0;
@@ -1726,7 +1816,7 @@ __device__ __forceinline__ uint64_t cal_lower_bound(const DParams& P, const uint
     return t > we ? t : we;
 }
 
-__device__ void store_ctx(const DParams& P, HostCtx& c) {
+__device__ __forceinline__ void store_ctx(const DParams& P, HostCtx& c) {
     const int32_t l = c.l;
     HostRec r;
     r.ev_seq = c.ev_seq; r.cq_total = (uint32_t)c.cq_total; r.cq_iexp = c.cq_iexp; r.cq_ndrop = c.cq_ndrop;
@@ -1746,7 +1836,8 @@ __device__ void store_ctx(const DParams& P, HostCtx& c) {
     r.cq_dc = c.cq_dc; r.cq_dcl = c.cq_dcl;
     r.cq_head = (uint16_t)c.cq_head; r.cq_count = (uint16_t)c.cq_count;
     r.tq_head = (uint16_t)c.tq_head; r.tq_count = (uint16_t)c.tq_count; r.evq_n = c.evq_n;
-    r.if_in = c.if_in; r.if_out = c.if_out; r.pad = 0;
+    r.if_in = c.if_in; r.if_out = c.if_out;
+    r.rq_head = (uint16_t)c.rq_head; r.port = (uint16_t)c.port;
     P.hs[l] = r;
     if (c.cq_hv) P.cq[(size_t)l * c.k.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
     if (c.tq_hv) P.tq[(size_t)l * c.k.tq_cap + c.tq_head] = s_tqh[threadIdx.x];

@@ -27,7 +27,7 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         P.hc[l] = HostCnt{0, 0, 0, 0, 0, 0};
         r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
         r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
-        r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.if_in = 0; r.if_out = 0; r.pad = 0;
+        r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.if_in = 0; r.if_out = 0; r.rq_head = 0; r.port = 0;
         P.hs[l] = r;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;
         HostCtx c;
@@ -250,7 +250,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
     hot_load(P, c);
     PendDel pd;
     send_pool_reset(c); c.att = 0; c.cls = 0; c.err = 0;
-    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0;
+    c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0; c.pf_lim = 0;
     // the window's non-empty bins, all slots loaded before the host record is
     // consumed (one round trip, overlapping the record's)
     EvV bx[3][kBinCap];
@@ -923,8 +923,9 @@ __global__ __launch_bounds__(64) void k_fold_tl(const TlPart* __restrict__ parts
 struct PsShare {
     uint4 a;   // next time lo, hi, flags (SHD_ERR_* | kPsPend), tag
     uint4 b;   // events, packet events, active hosts, tag
+    uint4 c;   // k_round_ps: the noted destinations (note_dirty: local host, kDirtyNone, kDirtyAll) x 3, tag
 };
-static_assert(sizeof(PsShare) == 32, "two 16-B granules");
+static_assert(sizeof(PsShare) == 48, "three 16-B granules");
 constexpr uint32_t kPsPend = 0x40000000u;   // share flag: the block's hosts logged a first touch
 constexpr uint32_t kBufWord3 = 0x00020000u;  // raw buffer descriptor word 3 (gfx9)
 constexpr int kAuxSc1 = 16;                   // buffer op cache policy: sc1 (agent scope)
@@ -962,7 +963,7 @@ struct PsRsrc {
 
 // the rare overflow of the due list, as due_overflow, reading the bins again
 // with sc1 loads (they may hold other blocks' appends of this launch)
-__device__ void ps_due_overflow(const DParams& P, HostCtx& c, const PsRsrc& R, uint32_t lb, uint64_t b0,
+__device__ __forceinline__ void ps_due_overflow(const DParams& P, HostCtx& c, const PsRsrc& R, uint32_t lb, uint64_t b0,
                                 uint32_t wbits, uint64_t ws, uint64_t we) {
     uint32_t k = 0;
     for (uint32_t j = 0; j < 3; j++) {
@@ -979,21 +980,27 @@ __device__ void ps_due_overflow(const DParams& P, HostCtx& c, const PsRsrc& R, u
     }
 }
 
-// per-round fields of a persistent host context
-__device__ __forceinline__ void ps_round_reset(HostCtx& c, uint64_t ws, int parity) {
+// per-round fields of a persistent host context.  pf (k_round_ps with a
+// calendar): the receivers load the next window's first kPfBins bins before
+// the round's barrier, so appends to earlier bins are noted (HostCtx::pf_lim)
+constexpr uint32_t kPfBins = 3;
+__device__ __forceinline__ void ps_round_reset(const DParams& P, HostCtx& c, uint64_t ws, uint64_t we, int parity,
+                                               bool pf) {
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = 0; c.xput = 0;
     c.c_events = c.c_pkt = c.c_sent = c.c_idrop = c.c_cdrop = c.c_recv = 0;
     c.min_emit = kInf; c.err = 0; c.n_pend = 0;
     c.dh = 0; c.nd = 0; c.dt = kInf; send_pool_reset(c); c.seq_base = c.ev_seq;
     c.w_msgs = 0; c.w_fl = 0;
+    c.pf_lim = pf ? (we >> P.bin_shift) + kPfBins : 0;
+    if (pf && threadIdx.x == 0) s_dn = 0;
 }
 
 // The round of a lane's host once its hand-off words are read (nin: this
-// parity's inbox count; w: the calendar bitmap, wbits its window bins):
-// bins and inbox merged, the event loop, the close.  `active` lanes run; the
-// others take part in the wave's flushes only.  `next` holds an idle lane's
-// next time on entry and is set for an active one.  As round_body, with the
-// hand-off arrays read by sc1 loads (other blocks of the launch wrote them).
+// parity's inbox count; w: the calendar bitmap, wbits its window bins), up to
+// its event loop: bins and inbox merged into the due list and the heap, the
+// window's wholly consumed bins reset.  `active` lanes run; the others take
+// part in the wave's flushes only.  As round_body, with the hand-off arrays
+// read by sc1 loads (other blocks of the launch wrote them).
 // SP (k_round_sp): the context is loaded here, from the record the caller
 // issued the loads of, once the bins' loads are out too (one round trip)
 struct SpIn {
@@ -1003,10 +1010,9 @@ struct SpIn {
     int32_t l;
 };
 template <bool SP>
-__device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool active, uint32_t lb, const PsRsrc& R,
-                                              uint64_t ws, uint64_t we, int parity, uint32_t nin,
-                                              uint32_t (&w)[kNBW], uint32_t wbits, uint64_t& next,
-                                              const SpIn* sp = nullptr) {
+__device__ __forceinline__ void ps_prologue(const DParams& P, HostCtx& c, bool active, uint32_t lb, const PsRsrc& R,
+                                            uint64_t ws, uint64_t we, int parity, uint32_t nin, uint32_t (&w)[kNBW],
+                                            uint32_t wbits, const SpIn* sp = nullptr) {
     const uint64_t b0 = ws >> P.bin_shift;
     const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
     // the window's bins, every slot of a non-empty one in one round trip
@@ -1025,7 +1031,7 @@ __device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool
     }
     if (SP) {
         if (active) load_ctx(P, c, sp->l, sp->rec, sp->att, sp->st);
-        ps_round_reset(c, ws, parity);
+        ps_round_reset(P, c, ws, we, parity, false);
     }
     if (active) {
         if (nin) {   // inbound events of the previous round -> heap
@@ -1078,8 +1084,125 @@ __device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool
         }
     }
     TIM(2);
-    // the event loop (as round_body's): per-lane state 0 needs its next event,
-    // 1 runs one, 2 waits for a flush, 3 done; wave-uniform exits only
+}
+
+// k_round_ps, a round whose window the previous round loaded ahead (every
+// host of the wave unnoted): the due list is in s_due already -- pnd sorted
+// events of the bins from the previous window's end on, of which those before
+// `we` are this round's -- and the bitmap of the previous round's close (pw)
+// names the window's non-empty bins.  The bins wholly consumed are reset as
+// in ps_prologue; their bits go to cm, cleared from the bitmap loaded at this
+// round's start once it has landed (ps_loop_close).
+__device__ __forceinline__ void ps_prologue_pf(const DParams& P, HostCtx& c, bool active, uint64_t ws, uint64_t we,
+                                               uint32_t pnd, uint32_t wbits, uint32_t (&cm)[kNBW]) {
+    const uint64_t b0 = ws >> P.bin_shift;
+    const uint32_t nbin = (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u;
+    if (active) {
+        uint32_t nd = 0;
+        for (; nd < pnd; nd++)
+            if (s_due[nd * kBlock + threadIdx.x].time >= we) break;
+        c.nd = nd;
+        c.dt = nd ? s_due[threadIdx.x].time : kInf;
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++) {
+            const uint64_t b = b0 + j;
+            if (j < nbin && ((b + 1) << P.bin_shift) <= we && ((wbits >> j) & 1u)) {
+                const uint32_t p = (uint32_t)b & (kNB - 1);
+                __hip_atomic_store(&P.bin_n[(size_t)c.l * kNB + p], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t m = 1u << (p & 31);
+                atomicAnd(&P.bin_bits[(size_t)c.l * kNBW + (p >> 5)], ~m);
+#pragma unroll
+                for (int k = 0; k < (int)kNBW; k++)
+                    if ((p >> 5) == (uint32_t)k) cm[k] |= m;
+            }
+        }
+    }
+    TIM(2);
+}
+
+// the next window's first kPfBins bins (from bin b on), loaded before the
+// round's barrier: the slots of each non-empty one (bit set in w) in registers
+struct PfBins {
+    EvV x[kPfBins][kBinCap];
+    uint32_t m;   // bit j: bin b + j was loaded
+};
+__device__ __forceinline__ void pf_issue(const PsRsrc& R, uint32_t lb, uint64_t b, const uint32_t (&w)[kNBW],
+                                         bool has, PfBins& pb) {
+    pb.m = 0;
+    if (!has) return;
+#pragma unroll
+    for (uint32_t j = 0; j < kPfBins; j++) {
+        const uint32_t p = (uint32_t)(b + j) & (kNB - 1);
+        if (!bit_at(w, p)) continue;
+        pb.m |= 1u << j;
+        const uint32_t bi = lb * kNB + p;
+#pragma unroll
+        for (uint32_t k = 0; k < kBinCap; k++) {
+            const uint32_t off = (bi * kBinCap + k) * 32u;
+            pb.x[j][k] = EvV{ld16_sc1(R.bins, off), ld16_sc1(R.bins, off + 16)};
+        }
+    }
+}
+// the loaded bins' events in [lo, hi) into s_due, sorted (the round's due
+// list is spent); their count, or kDueCap + 1 when they do not fit (the next
+// round then reads its window as without prefetch)
+__device__ __forceinline__ uint32_t pf_stage(const PfBins& pb, uint64_t lo, uint64_t hi) {
+    uint32_t nw = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kPfBins; j++) {
+        if (((pb.m >> j) & 1u) == 0) continue;
+#pragma unroll
+        for (uint32_t k = 0; k < kBinCap; k++) due_add(pb.x[j][k], nw, lo, hi);
+    }
+    if (nw > (uint32_t)kDueCap) return (uint32_t)kDueCap + 1u;
+    for (uint32_t i = 1; i < nw; i++) {
+        const EvV x = ev_ld(s_due + i * kBlock + threadIdx.x);
+        uint32_t k = i;
+        for (; k > 0; k--) {
+            const EvV y = ev_ld(s_due + (k - 1) * kBlock + threadIdx.x);
+            if (!evv_less(x, y)) break;
+            ev_st(s_due + k * kBlock + threadIdx.x, y);
+        }
+        ev_st(s_due + k * kBlock + threadIdx.x, x);
+    }
+    return nw;
+}
+
+// the window bins of a bitmap (bit j: bin b0 + j is non-empty); an idle
+// host's next time from its own next event and its bitmap
+__device__ __forceinline__ uint32_t ps_window_bits(const DParams& P, HostCtx& c, const uint32_t (&w)[kNBW],
+                                                   uint64_t ws, uint64_t we) {
+    const uint64_t b0 = ws >> P.bin_shift;
+    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
+    uint32_t wbits = 0;
+    if (P.bins) {
+#pragma unroll
+        for (uint32_t j = 0; j < 3; j++)
+            if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
+    }
+    if (nbin > 3) c.err |= SHD_ERR_INTERNAL;
+    return wbits;
+}
+__device__ __forceinline__ uint64_t ps_idle_next(const DParams& P, const uint32_t (&w)[kNBW], uint64_t t0,
+                                                 uint64_t we) {
+    uint64_t next = t0;
+    if (P.bins) {
+        const uint64_t cb = cal_lower_bound(P, w, we);
+        next = cb < next ? cb : next;
+    }
+    return next;
+}
+
+// The round's event loop (as round_body's: per-lane state 0 needs its next
+// event, 1 runs one, 2 waits for a flush, 3 done; wave-uniform exits only)
+// and its close: the lane's next time (an idle lane's from its timers and
+// bitmap), the last flush's stores.  cm: bits to clear from w first (bins the
+// prologue reset, when w was loaded in parallel).  PF: the next window's bins
+// are loaded between the loop and the close, into *pb.
+template <bool PF>
+__device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool active, bool has, const PsRsrc& R,
+                                              uint32_t lb, uint64_t we, uint32_t (&w)[kNBW],
+                                              const uint32_t (&cm)[kNBW], uint64_t& next, PfBins* pb) {
     PendDel pd;
     pd.kind = 0;
     {
@@ -1130,90 +1253,71 @@ __device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool
         }
     }
     TIM(4);
+#pragma unroll
+    for (int k = 0; k < (int)kNBW; k++) w[k] &= ~cm[k];
+    if (PF) pf_issue(R, lb, we >> P.bin_shift, w, has, *pb);
     if (active) {
         next = host_next(c);
         if (c.min_emit < next) next = c.min_emit;
-        if (P.bins) {   // (the consumed bins were cleared in w above)
+        if (P.bins) {   // (the consumed bins were cleared in w)
             const uint64_t cb = cal_lower_bound(P, w, we);
             next = cb < next ? cb : next;
         }
+    } else if (has) {
+        next = ps_idle_next(P, w, host_next(c), we);
     }
     flush_finish(P, c, pd);
     TIM(5);
 }
 
-// the window bins of a bitmap (bit j: bin b0 + j is non-empty); an idle
-// host's next time from its own next event and its bitmap
-__device__ __forceinline__ uint32_t ps_window_bits(const DParams& P, HostCtx& c, const uint32_t (&w)[kNBW],
-                                                   uint64_t ws, uint64_t we) {
-    const uint64_t b0 = ws >> P.bin_shift;
-    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - b0) + 1u : 0u;
-    uint32_t wbits = 0;
-    if (P.bins) {
+// k_round_sp's round of an active host (ps_prologue + ps_loop_close)
+template <bool SP>
+__device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool active, uint32_t lb, const PsRsrc& R,
+                                              uint64_t ws, uint64_t we, int parity, uint32_t nin,
+                                              uint32_t (&w)[kNBW], uint32_t wbits, uint64_t& next,
+                                              const SpIn* sp = nullptr) {
+    ps_prologue<SP>(P, c, active, lb, R, ws, we, parity, nin, w, wbits, sp);
+    uint32_t cm[kNBW];
 #pragma unroll
-        for (uint32_t j = 0; j < 3; j++)
-            if (j < nbin) wbits |= bit_at(w, (uint32_t)(b0 + j) & (kNB - 1)) << j;
-    }
-    if (nbin > 3) c.err |= SHD_ERR_INTERNAL;
-    return wbits;
-}
-__device__ __forceinline__ uint64_t ps_idle_next(const DParams& P, const uint32_t (&w)[kNBW], uint64_t t0,
-                                                 uint64_t we) {
-    uint64_t next = t0;
-    if (P.bins) {
-        const uint64_t cb = cal_lower_bound(P, w, we);
-        next = cb < next ? cb : next;
-    }
-    return next;
+    for (int k = 0; k < (int)kNBW; k++) cm[k] = 0;
+    ps_loop_close<false>(P, c, active, active, R, lb, we, w, cm, next, nullptr);
 }
 
-// One round [ws, we) of the lane's host (has: the lane has one; lb: its index
-// in the block) on the context it keeps in registers; as round_body
-__device__ void ps_round(const DParams& P, HostCtx& c, bool has, uint32_t lb, const PsRsrc& R, uint64_t ws,
-                         uint64_t we, int parity, uint64_t& next_out) {
-    ps_round_reset(c, ws, parity);
-    // the round's hand-off words: this parity's inbox count, the calendar bitmap
-    uint32_t nin = 0;
-    uint32_t w[kNBW];
-#pragma unroll
-    for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
-    if (has) {
-        nin = ld4_sc1(R.nin, lb * 4u);
-        if (P.bins) {
-            const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
-            w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-        }
-    }
-    const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
-    uint64_t next = kInf;
-    const uint64_t t0 = host_next(c);
-    bool active = false;
-    TIM(1);
-    if (has) {
-        if (nin == 0 && t0 >= we && wbits == 0) next = ps_idle_next(P, w, t0, we);
-        else active = true;
-    }
-    ps_round_body<false>(P, c, active, lb, R, ws, we, parity, nin, w, wbits, next);
-    next_out = next;
-}
-
-// the share of round i: both granules tagged, stored write-through after the
-// wave's hand-off stores drained
+// the share of round i: its three granules tagged, stored write-through after
+// the wave's hand-off stores drained; d: the noted destinations
 __device__ __forceinline__ void ps_publish(__amdgpu_buffer_rsrc_t rs, uint32_t slot, uint64_t next, uint32_t flags,
-                                           uint32_t nev, uint32_t npkt, uint32_t nact, uint32_t tag) {
+                                           uint32_t nev, uint32_t npkt, uint32_t nact, uint32_t tag, uint4 d) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
     if (threadIdx.x == 0) {
-        st16_sc1(rs, slot * 32u, make_uint4((uint32_t)next, (uint32_t)(next >> 32), flags, tag));
-        st16_sc1(rs, slot * 32u + 16u, make_uint4(nev, npkt, nact, tag));
+        st16_sc1(rs, slot * 48u, make_uint4((uint32_t)next, (uint32_t)(next >> 32), flags, tag));
+        st16_sc1(rs, slot * 48u + 16u, make_uint4(nev, npkt, nact, tag));
+        st16_sc1(rs, slot * 48u + 32u, make_uint4(d.x, d.y, d.z, tag));
     }
+}
+// the block's noted destinations for its share (after its last flush)
+__device__ __forceinline__ uint4 ps_noted(bool pf) {
+    uint4 d = make_uint4(kDirtyNone, kDirtyNone, kDirtyNone, 0);
+    if (!pf) return d;
+    const uint32_t n = s_dn;
+    if (n > kDirtyMax) return make_uint4(kDirtyAll, kDirtyAll, kDirtyAll, 0);
+    if (n > 0) d.x = s_dl[0];
+    if (n > 1) d.y = s_dl[1];
+    if (n > 2) d.z = s_dl[2];
+    return d;
 }
 
 // every block's share of round i (slots [base, base + nblk)): poll until all
-// carry `tag`, folding them; block 0 also folds the counts.  False on timeout
-__device__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nblk, uint32_t tag, bool counts,
+// carry `tag`, folding them; block 0 also folds the counts.  DIRTY: the noted
+// destinations too -- bit k of `dmask`: host hb + k of this block was named,
+// `dall`: some block noted more than it could name.  False on timeout
+template <bool DIRTY>
+__device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nblk, uint32_t tag, bool counts,
                           uint64_t ticks, uint64_t& next, uint32_t& flags, uint32_t& nev, uint32_t& npkt,
-                          uint32_t& nact) {
+                          uint32_t& nact, uint32_t hb = 0, uint32_t hpw = 0, uint64_t* dmask = nullptr,
+                          bool* dall = nullptr) {
     next = kInf; flags = 0; nev = 0; npkt = 0; nact = 0;
+    uint64_t dm = 0;
+    uint32_t da = 0;
     const unsigned long long t0 = wall_clock64();
     for (uint32_t c0 = 0; c0 < nblk; c0 += 256) {
         uint32_t need = 0;
@@ -1221,24 +1325,35 @@ __device__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nbl
         for (int k = 0; k < 4; k++)
             if (c0 + 64u * k + threadIdx.x < nblk) need |= 1u << k;
         while (__ballot(need != 0)) {
-            uint4 a[4], b[4];
+            uint4 a[4], b[4], d[4];
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint32_t off = (base + c0 + 64u * k + threadIdx.x) * 32u;
+                const uint32_t off = (base + c0 + 64u * k + threadIdx.x) * 48u;
                 a[k] = make_uint4(0, 0, 0, 0);
                 b[k] = a[k];
+                d[k] = a[k];
                 if ((need >> k) & 1u) {
                     a[k] = ld16_sc1(rs, off);
                     if (counts) b[k] = ld16_sc1(rs, off + 16u);
+                    if (DIRTY) d[k] = ld16_sc1(rs, off + 32u);
                 }
             }
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                if (!((need >> k) & 1u) || a[k].w != tag || (counts && b[k].w != tag)) continue;
+                if (!((need >> k) & 1u) || a[k].w != tag || (counts && b[k].w != tag) || (DIRTY && d[k].w != tag))
+                    continue;
                 const uint64_t t = ((uint64_t)a[k].y << 32) | a[k].x;
                 next = t < next ? t : next;
                 flags |= a[k].z;
                 nev += b[k].x; npkt += b[k].y; nact += b[k].z;
+                if (DIRTY) {
+                    const uint32_t v[3] = {d[k].x, d[k].y, d[k].z};
+#pragma unroll
+                    for (int q = 0; q < 3; q++) {
+                        if (v[q] == kDirtyAll) da = 1;
+                        else if (v[q] - hb < hpw) dm |= 1ull << (v[q] - hb);
+                    }
+                }
                 need &= ~(1u << k);
             }
             if (__ballot(need != 0) == 0) break;
@@ -1252,6 +1367,14 @@ __device__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nbl
         nev += __shfl_xor(nev, off, 64);
         npkt += __shfl_xor(npkt, off, 64);
         nact += __shfl_xor(nact, off, 64);
+        if (DIRTY) {
+            dm |= __shfl_xor(dm, off, 64);
+            da |= __shfl_xor(da, off, 64);
+        }
+    }
+    if (DIRTY) {
+        *dmask = dm;
+        *dall = da != 0;
     }
     return true;
 }
@@ -1266,6 +1389,30 @@ __device__ __forceinline__ void ps_fresh(DevSummary* s) {
     for (int k = 0; k < (int)(sizeof(DevSummary) / 8); k++)
         __hip_atomic_store(d + k, q[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Cross-barrier prefetch (round 4).  A round's critical path starts with two
+// dependent memory round trips per host -- the hand-off words (inbox count,
+// calendar bitmap), then the window's bins -- behind the barrier.  But the
+// next window's events are, but for a few, in the calendar before the round
+// ends: a delivery made in round i lands at or after we_i + W, so only the
+// sends with a latency below ~3 W can reach the bins [b(we_i), b(we_i) + 3)
+// after the receiver has read them.  So each block loads those bins of its
+// hosts between its last flush and its close (the loads overlap the flush's
+// claims and the close's stores, and land before the share's drain), stages
+// their events in the due list after publishing, and the next round starts
+// its event loop right after the barrier.  Every append to a bin before
+// pf_lim, and every inbox append, is noted by its sender (note_dirty) and
+// named in the sender's share; a wave with a named host (or whose window
+// reaches past the loaded bins, or whose prefetch overflowed the due list)
+// reads its hand-off words after the barrier as before.  The bitmap each round
+// uses for its close and for the next prefetch is loaded at its start and
+// consumed after its loop; it holds every append of the rounds before (an
+// append of this round is covered by its sender's own next time, min_emit).
+#ifndef SHD_NO_PF
+constexpr bool kPsPf = true;
+#else
+constexpr bool kPsPf = false;
+#endif
 
 __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, DevSummary* __restrict__ ring,
                                                       const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
@@ -1295,14 +1442,24 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
     if (has) {
         load_ctx(P0, c, l, P0.hs[l], P0.host_att[P0.h0 + l], P0.self_thr[P0.h0 + l]);
     } else {
-        c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf;
-        c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
+        c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
+        c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false; c.pf_lim = 0;
     }
     uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
     uint64_t ws = ring[0].next_time;
     const uint64_t stop = ctl->stop, rbase = ctl->round_base;
     const uint32_t tag0 = (uint32_t)ctl->xtag;
     const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    // the prefetch carried from a round to the next (wave-uniform but pnd,
+    // dirty): valid, its first bin, the due events staged (kDueCap + 1:
+    // overflow), the bitmap of that round's close, named by a share
+    const bool pfm = kPsPf && P0.bins != nullptr;
+    bool pf = false;
+    uint64_t pf_b0 = 0;
+    uint32_t pnd = 0, dirty = 0;
+    uint32_t pw[kNBW];
+#pragma unroll
+    for (int k = 0; k < (int)kNBW; k++) pw[k] = 0;
     for (int i = 0; i < nb; i++) {
         const DParams& P = Pr[i + 1];
         const unsigned long long t_start = wall_clock64();
@@ -1313,11 +1470,45 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         const int parity = (int)((rbase + (uint64_t)i) & 1);
         uint64_t we = ws + window;
         if (we > stop || we < ws) we = stop;
-        uint64_t next;
         PsRsrc R = R0;
         R.nin = parity ? R1.nin : R0.nin;
         R.inbox = parity ? R1.inbox : R0.inbox;
-        ps_round(P, c, has, lb, R, ws, we, parity, next);
+        const bool fast = pf && ((we - 1) >> P.bin_shift) <= pf_b0 + (kPfBins - 1) &&
+                          __ballot(has && (dirty != 0 || pnd > (uint32_t)kDueCap)) == 0;
+        ps_round_reset(P, c, ws, we, parity, pfm);
+        uint32_t w[kNBW], cm[kNBW];
+#pragma unroll
+        for (int k = 0; k < (int)kNBW; k++) { w[k] = 0; cm[k] = 0; }
+        bool active = false;
+        if (fast) {
+            // the bitmap for the close and the next prefetch goes out now and is
+            // consumed after the loop; the window's events are staged already
+            if (has) {
+                const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+            }
+            const uint32_t wbits = ps_window_bits(P, c, pw, ws, we);
+            TIM(1);
+            active = has && !(host_next(c) >= we && wbits == 0);   // (no inbox: it would have been named)
+            ps_prologue_pf(P, c, active, ws, we, pnd, wbits, cm);
+        } else {
+            // the round's hand-off words: this parity's inbox count, the calendar bitmap
+            uint32_t nin = 0;
+            if (has) {
+                nin = ld4_sc1(R.nin, lb * 4u);
+                if (P.bins) {
+                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+                }
+            }
+            const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
+            TIM(1);
+            active = has && !(nin == 0 && host_next(c) >= we && wbits == 0);
+            ps_prologue<false>(P, c, active, lb, R, ws, we, parity, nin, w, wbits);
+        }
+        uint64_t next = kInf;
+        PfBins pb;
+        ps_loop_close<kPsPf>(P, c, active, has, R, lb, we, w, cm, next, &pb);
         acc[0] += c.c_events; acc[1] += c.c_pkt; acc[2] += c.c_sent;
         acc[3] += c.c_idrop; acc[4] += c.c_cdrop; acc[5] += c.c_recv;
         uint32_t nev = c.c_events, npkt = c.c_pkt, err = c.err;
@@ -1333,11 +1524,20 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         }
         const uint32_t tag = tag0 + (uint32_t)i;
         const uint32_t base = (uint32_t)(i & 1) * nblk;
-        ps_publish(rs, base + blockIdx.x, next, fl, nev, npkt, nact, tag);
+        ps_publish(rs, base + blockIdx.x, next, fl, nev, npkt, nact, tag, ps_noted(pfm));
         TIM(6);
-        uint64_t f_next;
+        if (pfm) {   // the next window's events, staged while the other blocks finish
+            const uint64_t b1 = we >> P.bin_shift;
+            pnd = pf_stage(pb, we, (b1 + kPfBins) << P.bin_shift);
+            pf_b0 = b1;
+#pragma unroll
+            for (int k = 0; k < (int)kNBW; k++) pw[k] = w[k];
+        }
+        uint64_t f_next, dm = 0;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
-        const bool ok_v = ps_gather(rs, base, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
+        bool dall = false;
+        const bool ok_v = ps_gather<kPsPf>(rs, base, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt,
+                                           f_nact, hb, (uint32_t)P.hpw, &dm, &dall);
         TIM(7);
         // the folds are wave-uniform: said so to the compiler, so that the
         // round loop and the parity branch stay scalar (with a vector exit
@@ -1368,6 +1568,8 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         if (f_fl) break;            // a first touch to resolve, or an error: the host takes over
         ws = f_next;
         if (ws >= stop) break;      // the rest only forwards the time (ring[i + 1].next_time says so)
+        pf = pfm;
+        dirty = (dall || ((dm >> lb) & 1ull)) ? 1u : 0u;
     }
     // the hosts' state, once for the whole batch
     if (has) {
@@ -1393,6 +1595,13 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
 // only (plain accesses, one CU); the hand-off arrays by sc1 loads, as in
 // k_round_ps, whose share protocol and ring summaries this kernel shares.
 constexpr uint32_t kSpMaxHosts = 4096;   // hosts per block at most (64 groups of 64)
+// groups of 64 hosts whose hand-off words one scan batch loads together (one
+// memory round trip each batch; 8: the 125 k-host shard's ~490 hosts per block
+// in one)
+#ifndef SHD_SP_SCAN
+#define SHD_SP_SCAN 8
+#endif
+constexpr int kSpScan = SHD_SP_SCAN;
 __shared__ uint16_t s_act[kSpMaxHosts];  // the round's active hosts (index in the block)
 __shared__ uint32_t s_aw[(kNBW + 1) * kBlock];   // the first pass's hand-off words: bitmap, inbox count
 
@@ -1420,7 +1629,7 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
     HostCtx c;
     hot_load(P0, c);
-    c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf;
+    c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
     c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
     uint64_t ws = ring[0].next_time;
     const uint64_t stop = ctl->stop, rbase = ctl->round_base;
@@ -1440,15 +1649,15 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         PsRsrc R = R0;
         R.nin = parity ? R1.nin : R0.nin;
         R.inbox = parity ? R1.inbox : R0.inbox;
-        ps_round_reset(c, ws, parity);
+        ps_round_reset(P, c, ws, we, parity, false);
         // the scan: every host's words and own next time, four groups per round trip
         uint64_t next = kInf;
         uint32_t nact = 0;
-        for (uint32_t g0 = 0; g0 < ngrp; g0 += 4) {
-            uint32_t nin4[4], w4[4][kNBW];
-            uint64_t t4[4];
+        for (uint32_t g0 = 0; g0 < ngrp; g0 += kSpScan) {
+            uint32_t nin4[kSpScan], w4[kSpScan][kNBW];
+            uint64_t t4[kSpScan];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < kSpScan; q++) {
                 const uint32_t lb = (g0 + q) * 64u + lane;
                 nin4[q] = 0; t4[q] = kInf;
 #pragma unroll
@@ -1464,7 +1673,7 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < kSpScan; q++) {
                 const uint32_t lb = (g0 + q) * 64u + lane;
                 const bool has = g0 + q < ngrp && lb < nh;
                 const uint32_t wbits = ps_window_bits(P, c, w4[q], ws, we);
@@ -1537,11 +1746,11 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         }
         const uint32_t tag = tag0 + (uint32_t)i;
         const uint32_t sbase = (uint32_t)(i & 1) * nblk;
-        ps_publish(rs, sbase + blockIdx.x, next, fl, nev, npkt, nhost, tag);
+        ps_publish(rs, sbase + blockIdx.x, next, fl, nev, npkt, nhost, tag, ps_noted(false));
         TIM(6);
         uint64_t f_next;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
-        const bool ok_v = ps_gather(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
+        const bool ok_v = ps_gather<false>(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
         TIM(7);
         const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;
         f_fl = __builtin_amdgcn_readfirstlane(f_fl);

@@ -75,6 +75,7 @@ struct shd_eng {
     bool booted = false;
     bool heartbeats = false;    // SHD_QF_HEARTBEATS: snapshots in P.hb
     std::vector<uint64_t> host_hb;   // <host heartbeatfrequency> per host (empty: P.heartbeat)
+    std::vector<int32_t> app_peer;   // SHD_APP_UDP_ECHO roles (empty: PHOLD)
     std::vector<void*> allocs;
     std::vector<size_t> alloc_bytes;
     // protected rounds (DESIGN.md "First-touch rule"): device state copied
@@ -93,6 +94,7 @@ struct shd_eng {
     DestGuide* d_guide = nullptr;
     int4* d_self_thr = nullptr;
     uint64_t* d_host_hb = nullptr;
+    int32_t* d_app_peer = nullptr;
     int32_t n_cls = 1;
     uint64_t t_done = 0;                    // end of the last executed round's window (push_events floor)
     int32_t* d_rank = nullptr;
@@ -231,6 +233,26 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         return SHD_EINVAL;
     }
     if (m->host_heartbeat) e->host_hb.assign(m->host_heartbeat, m->host_heartbeat + H);
+    if (m->app == SHD_APP_UDP_ECHO) {
+        // the UDP echo's roles: every client's server is a server host; a
+        // socket holds at most the requests in flight to it (its clients' loads)
+        if (!m->app_peer) { shd_eng_destroy(e); return SHD_EINVAL; }
+        std::vector<uint64_t> held(H, m->load);
+        for (int32_t h = 0; h < H; h++) {
+            const int32_t s = m->app_peer[h];
+            if (s < -1 || s >= H || s == h || (s >= 0 && m->app_peer[s] != -1)) { shd_eng_destroy(e); return SHD_EINVAL; }
+            if (s >= 0) held[s] += m->load;
+        }
+        uint64_t cap = 16;
+        for (int32_t h = 0; h < H; h++) cap = std::max<uint64_t>(cap, held[h]);
+        if (cap > 65535) { shd_eng_destroy(e); return SHD_ERANGE; }   // (a 16-bit ring head in the record)
+        P.rq_cap = (uint32_t)cap;
+        e->app_peer.assign(m->app_peer, m->app_peer + H);
+    } else if (m->app != SHD_APP_PHOLD) {
+        shd_eng_destroy(e);
+        return SHD_EINVAL;
+    }
+    P.app = m->app;
     P.end_time = m->end_time; P.bootstrap_end = m->bootstrap_end; P.heartbeat = m->heartbeat_interval;
     P.app_start = m->app_start; P.load = m->load; P.payload = m->payload;
     P.pkt_len = m->payload + SHD_HEADER_UDP;
@@ -260,6 +282,10 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     EALLOC(e->d_guide, HC);
     EALLOC(e->d_self_thr, H);
     if (m->host_heartbeat) EALLOC(e->d_host_hb, H);
+    if (P.app == SHD_APP_UDP_ECHO) {
+        EALLOC(e->d_app_peer, H);
+        EALLOC(P.rq, n * P.rq_cap);
+    }
     // destination guide table per class: guide[k] = first i with cum[i] >= k / H (H if none)
     std::vector<DestGuide> guide(HC);
     for (int32_t cl = 0; cl < n_cls; cl++) {
@@ -321,7 +347,9 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         hipMemcpyAsync(e->d_cum, m->dest_cum, 8 * HC, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemcpyAsync(e->d_guide, guide.data(), sizeof(DestGuide) * HC, hipMemcpyHostToDevice, s) != hipSuccess ||
         (m->host_heartbeat &&
-         hipMemcpyAsync(e->d_host_hb, m->host_heartbeat, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess)) {
+         hipMemcpyAsync(e->d_host_hb, m->host_heartbeat, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess) ||
+        (e->d_app_peer &&
+         hipMemcpyAsync(e->d_app_peer, m->app_peer, 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess)) {
         shd_eng_destroy(e);
         return SHD_ENODEV;
     }
@@ -337,6 +365,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.dest_cum = e->d_cum;
     P.dest_guide = e->d_guide;
     P.host_hb = e->d_host_hb;
+    P.app_peer = e->d_app_peer;
     P.no_app_start = (m->queue_flags & SHD_QF_NO_APP_START) ? 1 : 0;
     // draw thresholds: x / RAND_MAX <= c  <=>  x <= draw_threshold(c)
     {
@@ -424,7 +453,8 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     }
     P.feat = (m->trace ? F_TRACE : 0u) | (P.hb ? F_HB : 0u) | (P.pcount ? F_PCOUNT : 0u) |
              (P.host_hb ? F_HOSTHB : 0u) | (P.force_ambig ? F_AMBIG : 0u) |
-             ((m->trace && (m->queue_flags & SHD_QF_TRACE_STATUS)) ? F_STATUS : 0u);
+             ((m->trace && (m->queue_flags & SHD_QF_TRACE_STATUS)) ? F_STATUS : 0u) |
+             (P.app == SHD_APP_UDP_ECHO ? F_ECHO : 0u);
     P.sum = e->d_sum;
     // the serial-equivalent window W: min over every latency a send can be
     // served (rows, direct values, self values) -> ceil(lat * 1e6) ns
@@ -1252,7 +1282,8 @@ extern "C" int shd_eng_status_lines(shd_eng* e, const uint32_t* ips, const uint3
     if (rc) return rc;
     std::vector<shd_trace_rec> tr(n ? n : 1);
     if (n && (rc = shd_eng_trace_copy(e, tr.data(), n, &got))) return rc;
-    return shd_status_lines(tr.data(), got, ips, host_ids, (uint32_t)e->H, e->P.payload, listen_port, out);
+    return shd_status_lines(tr.data(), got, ips, host_ids, (uint32_t)e->H, e->P.payload, listen_port,
+                            e->app_peer.empty() ? nullptr : e->app_peer.data(), out);
 }
 
 extern "C" int shd_eng_node_lines(shd_eng* e, uint32_t local_host, shd_lines** out) {

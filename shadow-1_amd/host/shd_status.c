@@ -211,6 +211,7 @@ typedef struct {
     const uint32_t* ips;
     const uint32_t* ids;
     uint32_t nh, payload, lport;
+    const uint32_t* dport;   /* [nh] the port a datagram to host h is addressed to */
     char* line;
 } wctx;
 
@@ -221,9 +222,10 @@ static void put_line(wctx* w, uint64_t t, uint32_t at, const dgram* d, int name)
     o += sprintf(o, "[%s] packetID=%u:%u ", kStName[name], w->ids ? w->ids[src] : src + 1, pkt);
     o += ip_str(o, w->ips[src]);
     o += sprintf(o, ":%u -> ", d->port);
-    if (d->dst != 0xFFFFFFFFu && d->dst < w->nh) o += ip_str(o, w->ips[d->dst]);
+    const int known = d->dst != 0xFFFFFFFFu && d->dst < w->nh;
+    if (known) o += ip_str(o, w->ips[d->dst]);
     else *o++ = '?';
-    o += sprintf(o, ":%u bytes=%u status=", w->lport, w->payload);
+    o += sprintf(o, ":%u bytes=%u status=", known ? w->dport[d->dst] : w->lport, w->payload);
     for (int k = 0; k < d->nh; k++) {
         if (k) *o++ = ',';
         const char* s = kStName[d->hist[k]];
@@ -258,7 +260,8 @@ static void send_side(wctx* w, uint64_t t, uint32_t h, dgram* d, uint32_t kind) 
 }
 
 int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, const uint32_t* host_ids,
-                     uint32_t n_hosts, uint32_t payload, uint32_t listen_port, shd_lines** out) {
+                     uint32_t n_hosts, uint32_t payload, uint32_t listen_port, const int32_t* app_peer,
+                     shd_lines** out) {
     if (!out || (n && !tr) || !ips || !n_hosts) return SHD_EINVAL;
     for (uint64_t i = 0; i < n; i++)
         if (tr[i].host >= n_hosts || tr[i].kind < SHD_TR_SENT || tr[i].kind > SHD_TR_READ) return SHD_EINVAL;
@@ -273,7 +276,12 @@ int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, c
     m.mask = cap - 1;
     fifo* inbox = calloc(n_hosts, sizeof(fifo));
     char* line = malloc(512 + HIST_MAX * 32);
-    if (!s || !m.t || !inbox || !line) { rc = SHD_ENOMEM; goto out; }
+    uint32_t* dport = malloc(n_hosts * sizeof(uint32_t));   /* the port datagrams to host h go to */
+    if (!s || !m.t || !inbox || !line || !dport) { rc = SHD_ENOMEM; goto out; }
+    for (uint32_t h = 0; h < n_hosts; h++) dport[h] = listen_port;
+    if (app_peer)   /* UDP echo: a client's socket port, from its own datagrams' source port */
+        for (uint64_t i = 0; i < n; i++)
+            if (tr[i].kind == SHD_TR_CREATED && app_peer[tr[i].host] >= 0) dport[tr[i].host] = (uint32_t)(tr[i].seq & 0xFFFF);
     for (uint64_t i = 0; i < cap; i++) m.t[i].key = ~0ull;
     for (uint64_t i = 0; i < n; i++) { s[i].r = &tr[i]; s[i].i = i; }
     qsort(s, n, sizeof(srec), srec_cmp);   /* by (time, host), records of one host in trace order */
@@ -301,7 +309,7 @@ int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, c
             if (d->created_at == r->time) d->send_i = (int64_t)i;
         }
     }
-    wctx w = {&b, &m, ips, host_ids, n_hosts, payload, listen_port, line};
+    wctx w = {&b, &m, ips, host_ids, n_hosts, payload, listen_port, dport, line};
     for (uint64_t i = 0; i < n && !b.oom; i++) {
         const shd_trace_rec* r = s[i].r;
         const uint32_t k = r->kind, h = r->host;
@@ -343,6 +351,7 @@ out:
         for (uint32_t h = 0; h < n_hosts; h++) free(inbox[h].q);
     free(inbox);
     free(line);
+    free(dport);
     free(m.t);
     free(s);
     if (rc) { shd_lines_free(b.l); return rc; }

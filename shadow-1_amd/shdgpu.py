@@ -111,7 +111,11 @@ class Model(C.Structure):
         ("txq_cap", C.c_uint32), ("queue_flags", C.c_uint32),
         ("host_class", P(C.c_uint8)), ("n_classes", C.c_int32), ("_pad1", C.c_int32),
         ("host_heartbeat", P(C.c_uint64)),
+        ("app", C.c_uint32), ("_pad2", C.c_int32), ("app_peer", P(C.c_int32)),
     ]
+
+
+SHD_APP_PHOLD, SHD_APP_UDP_ECHO = 0, 1
 
 
 class Event(C.Structure):
@@ -267,7 +271,7 @@ _SIGS = {
     "shd_eng_heartbeats": (C.c_int, [C.c_void_p, P(C.c_uint32), C.c_uint64, P(C.c_uint64)]),
     "shd_eng_stream": (C.c_int, [C.c_void_p, P(C.c_void_p)]),
     "shd_status_lines": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint32), P(C.c_uint32), C.c_uint32, C.c_uint32,
-                                   C.c_uint32, P(P(Lines))]),
+                                   C.c_uint32, P(C.c_int32), P(P(Lines))]),
     "shd_node_lines": (C.c_int, [P(C.c_uint32), C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, P(P(Lines))]),
     "shd_eng_status_lines": (C.c_int, [C.c_void_p, P(C.c_uint32), P(C.c_uint32), C.c_uint32, P(P(Lines))]),
     "shd_eng_node_lines": (C.c_int, [C.c_void_p, C.c_uint32, P(P(Lines))]),
@@ -409,9 +413,11 @@ class ModelArrays:
     def __init__(self, host_vertex, host_rng, bw_down, bw_up, dest_cum, *, end_time,
                  app_start=1 * SHD_SEC, load=16, payload=1, heartbeat_interval=SHD_SEC,
                  bootstrap_end=0, trace=False, evq_cap=0, inbox_cap=0, codelq_cap=0,
-                 txq_cap=0, queue_flags=0, host_class=None, host_heartbeat=None):
+                 txq_cap=0, queue_flags=0, host_class=None, host_heartbeat=None, app_peer=None):
         """dest_cum: [H] (one weights row for every host) or [n_classes, H] with
-        host_class [H] picking each host's row; host_heartbeat: [H] ns or None."""
+        host_class [H] picking each host's row; host_heartbeat: [H] ns or None;
+        app_peer: None (every host runs PHOLD) or [H] -1 | server host (every
+        host runs the UDP request/response echo, SHD_APP_UDP_ECHO)."""
         self.host_vertex = np.ascontiguousarray(host_vertex, dtype=np.int32)
         self.host_rng = np.ascontiguousarray(host_rng, dtype=np.uint32)
         self.bw_down = np.ascontiguousarray(bw_down, dtype=np.uint64)
@@ -426,6 +432,9 @@ class ModelArrays:
         self.n_classes = n_classes
         self.host_heartbeat = None if host_heartbeat is None else \
             np.ascontiguousarray(host_heartbeat, dtype=np.uint64)
+        self.app_peer = None if app_peer is None else np.ascontiguousarray(app_peer, dtype=np.int32)
+        assert self.app_peer is None or len(self.app_peer) == H
+        self.app = SHD_APP_PHOLD if self.app_peer is None else SHD_APP_UDP_ECHO
         self.params = dict(end_time=int(end_time), app_start=int(app_start), load=int(load),
                            payload=int(payload), heartbeat_interval=int(heartbeat_interval),
                            bootstrap_end=int(bootstrap_end), trace=int(bool(trace)),
@@ -437,7 +446,8 @@ class ModelArrays:
             int(heartbeat_interval), int(app_start), int(load), int(payload), int(bool(trace)),
             int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), int(queue_flags),
             None if self.host_class is None else as_ptr(self.host_class, C.c_uint8), int(n_classes), 0,
-            None if self.host_heartbeat is None else as_ptr(self.host_heartbeat, C.c_uint64))
+            None if self.host_heartbeat is None else as_ptr(self.host_heartbeat, C.c_uint64),
+            self.app, 0, None if self.app_peer is None else as_ptr(self.app_peer, C.c_int32))
 
     @property
     def n_hosts(self):
@@ -585,11 +595,13 @@ def ip_string(ip) -> str:
     return "%d.%d.%d.%d" % ((ip >> 24) & 255, (ip >> 16) & 255, (ip >> 8) & 255, ip & 255)
 
 
-def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT) -> list:
+def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT,
+                 app_peer=None) -> list:
     """[STATUS] lines of a run traced with SHD_QF_TRACE_STATUS, made by the
     library's writer (shd_status_lines, include/shdgpu.h): a list of
-    (time_ns, host index, line).  status_lines_py is the same algorithm in
-    Python (tests/test_status_cpu.py checks the two against each other)."""
+    (time_ns, host index, line).  app_peer: the UDP echo model's roles (None:
+    PHOLD).  status_lines_py is the same algorithm in Python
+    (tests/test_status_cpu.py checks the two against each other)."""
     tr = np.ascontiguousarray(np.asarray(trace, dtype=TRACE_DTYPE))
     ip = _ips_u32(ips)
     ids = None if host_ids is None else np.ascontiguousarray(np.asarray(host_ids, dtype=np.uint32))
@@ -597,11 +609,15 @@ def status_lines(trace, ips, host_ids=None, payload: int = 1, listen_port: int =
     check(lib().shd_status_lines(tr.ctypes.data if len(tr) else None, len(tr),
                                  ip.ctypes.data_as(C.POINTER(C.c_uint32)),
                                  None if ids is None else ids.ctypes.data_as(C.POINTER(C.c_uint32)),
-                                 len(ip), int(payload), int(listen_port), C.byref(out)), "shd_status_lines")
+                                 len(ip), int(payload), int(listen_port),
+                                 None if app_peer is None else
+                                 np.ascontiguousarray(app_peer, dtype=np.int32).ctypes.data_as(C.POINTER(C.c_int32)),
+                                 C.byref(out)), "shd_status_lines")
     return take_lines(out)
 
 
-def status_lines_py(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT) -> list:
+def status_lines_py(trace, ips, host_ids=None, payload: int = 1, listen_port: int = SHD_PHOLD_LISTEN_PORT,
+                    app_peer=None) -> list:
     """[STATUS] lines of a run traced with SHD_QF_TRACE_STATUS: a list of
     (time_ns, host index, line), line = "[<STATUS>] packetID=<hostID>:<pkt>
     <srcIP>:<srcPort> -> <dstIP>:<dstPort> bytes=<n> status=<S1>,...,<Sk>"
@@ -621,6 +637,11 @@ def status_lines_py(trace, ips, host_ids=None, payload: int = 1, listen_port: in
     order = np.lexsort((np.arange(len(tr)), tr["host"], tr["time"]))
     tr = tr[order]
     NONE = 0xFFFFFFFF
+    dport = [listen_port] * len(ips)   # a UDP echo client's socket port: its own datagrams' source port
+    if app_peer is not None:
+        for r in tr:
+            if int(r["kind"]) == TR_CREATED and app_peer[int(r["host"])] >= 0:
+                dport[int(r["host"])] = int(r["seq"]) & 0xFFFF
     port, dst, created_at, local = {}, {}, {}, set()
     for r in tr:
         k, h, p = int(r["kind"]), int(r["host"]), int(r["pkt"])
@@ -647,7 +668,8 @@ def status_lines_py(trace, ips, host_ids=None, payload: int = 1, listen_port: in
         for name in statuses:
             st.append(name)
             out.append((t, at, status_line(name, host_ids[src], pkt, ips[src], port.get(key, 0),
-                                           ips[d] if d != NONE else None, listen_port, payload, st)))
+                                           ips[d] if d != NONE else None, dport[d] if d != NONE else listen_port,
+                                           payload, st)))
 
     arrived = {(int(r["peer"]), int(r["pkt"])) for r in tr if int(r["kind"]) == TR_ARRIVE}
 
@@ -660,7 +682,7 @@ def status_lines_py(trace, ips, host_ids=None, payload: int = 1, listen_port: in
         d = dst.get(key, NONE)
         st = hist[key] + ["PDS_DESTROYED"]
         line = status_line("PDS_DESTROYED", host_ids[key[0]], key[1], ips[key[0]], port.get(key, 0),
-                           ips[d] if d != NONE else None, listen_port, payload, st)
+                           ips[d] if d != NONE else None, dport[d] if d != NONE else listen_port, payload, st)
         for _ in range(2 if copy_dropped else 1):
             out.append((t, at, line))
 

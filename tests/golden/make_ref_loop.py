@@ -48,7 +48,7 @@ def main(names):
     for name in names or list(RC.CASES):
         case = RC.CASES[name]()
         t0 = time.time()
-        r = R.run(case["model"], case["graph"], procs=RC.procs_of(case))
+        r = R.run(case["model"], case["graph"], procs=RC.procs_of(case), echo=case["model"].app_peer)
         st, hb = RC.split_lines(r["lines"])
         data[name] = dict(ips=r["ip"], n_status=len(st), status_sha256=RC.digest_lines(st),
                           n_heartbeat=len(hb), heartbeat_sha256=RC.digest_lines(hb),

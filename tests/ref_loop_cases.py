@@ -103,6 +103,32 @@ def _c1():
     return dict(model=m, graph=g, pushes=pushes)
 
 
+def _udp_echo():
+    """The second device application (SHD_APP_UDP_ECHO, ref_loop.c app 2): 20
+    servers and 40 clients, two or three clients per server, 4 requests in
+    flight each, edge loss U[0, 0.02] (lost requests and replies shrink the
+    loops)."""
+    V = 60
+    g = W.geometric_graph(V, seed=17, loss_max=0.02)
+    peer = np.array([-1] * 20 + [(h * 7) % 20 for h in range(20, V)], dtype=np.int32)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=3 * S.SHD_SEC, trace=True, load=4, queue_flags=TS,
+                      app_peer=peer)
+    return dict(model=m, graph=g)
+
+
+def _udp_echo_codel():
+    """UDP echo with 1500-B datagrams into 512 KiB/s receive buckets at the
+    servers: 8 servers, 32 clients with 8 requests in flight each -- CoDel
+    queues build and drop at the servers."""
+    V = 40
+    g = W.geometric_graph(V, seed=29)
+    peer = np.array([-1] * 8 + [h % 8 for h in range(8, V)], dtype=np.int32)
+    bw = np.where(peer < 0, 512, 10240).astype(np.uint64)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=3 * S.SHD_SEC, trace=True, load=8, payload=1500,
+                      bw_down=bw, codelq_cap=512, queue_flags=TS, app_peer=peer)
+    return dict(model=m, graph=g)
+
+
 CASES = {
     "phold_v100": _phold_v100,
     "codel": _codel,
@@ -112,6 +138,8 @@ CASES = {
     "tor": _tor,
     "bootstrap": _bootstrap,
     "c1": _c1,
+    "udp_echo": _udp_echo,
+    "udp_echo_codel": _udp_echo_codel,
 }
 
 

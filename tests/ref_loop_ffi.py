@@ -65,7 +65,7 @@ def _ptr(a, ct):
     return None if a is None else a.ctypes.data_as(P(ct))
 
 
-def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False):
+def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False, echo=None):
     """run_inproc in a forked child: the reference keeps process-wide state
     (the worker's thread-private object, glib quarks), so one run per process."""
     import multiprocessing as mp
@@ -74,7 +74,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp
 
     def child():
         try:
-            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp, quiet)))
+            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp, quiet, echo)))
         except BaseException as ex:   # noqa: BLE001 -- reported to the parent
             wr.send(("err", repr(ex)))
         wr.close()
@@ -92,14 +92,16 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp
     return res
 
 
-def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False):
+def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False,
+               echo=None):
     """Run the model through the reference's loop; returns dict(lines=[(t, h, line)],
     ip=[str], next_event_id, next_packet_id, rng_probe (uint arrays)).
     host_start: [H] process start times (default: the model's app_start);
     procs: [(host, start)] processes in <process> order instead (the oracle's
     and the engine's pushed SHD_EV_APP_START events, in push order);
     tcp: dict(peers=[-1 | server process index per process], nbytes=N) runs
-    the TCP echo test (test_tcp.c) in those processes instead of PHOLD."""
+    the TCP echo test (test_tcp.c) in those processes instead of PHOLD;
+    echo: [H] -1 | server host runs the UDP request/response echo instead."""
     m = model.struct
     H = int(m.n_hosts)
     og = O.lib().o_graph_new(C.byref(g.struct))
@@ -111,6 +113,11 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     cfg.n_hosts = H
     cfg.quiet = 1 if quiet else 0
     cfg.app = 0 if tcp is None else 1
+    if echo is not None:   # the UDP echo application: echo[h] = -1 (server) or h's server host
+        cfg.app = 2
+        ep = np.ascontiguousarray(echo, dtype=np.int32)
+        keep.append(ep)
+        cfg.proc_peer = _ptr(ep, C.c_int32)
     if tcp is not None:
         pp = np.ascontiguousarray(tcp["peers"], dtype=np.int32)
         keep.append(pp)

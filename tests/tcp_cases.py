@@ -53,7 +53,7 @@ def _server_first():
     client's (a 40-vertex geometric graph: multi-hop paths whose two
     orientations differ in the last bits).  (test_tcp.c's server serves one
     peer and closes its listener: one server per client.)"""
-    g = W.geometric_graph(40, seed=6, loss_max=0.01)
+    g = W.geometric_graph(40, seed=24, loss_max=0.01)
     procs = [(0, SEC), (1, SEC), (1, SEC), (1, 2 * SEC), (2, 3 * SEC), (0, 4 * SEC)]
     return dict(graph=g, hv=[0, 17, 33], procs=procs, peers=[-1, -1, -1, 0, 1, 2], nbytes=50000, end=30, bw={})
 

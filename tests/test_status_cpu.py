@@ -105,6 +105,15 @@ def test_c_writer_equals_the_python_restatement():
             c = S.status_lines(otr, ips, host_ids=ids, payload=pl)
             assert c == S.status_lines_py(otr, ips, host_ids=ids, payload=pl)
             assert len(c) > len(otr)
+    # the UDP echo application: replies go to each client's bound port
+    peer = np.array([-1] * 6 + [h % 6 for h in range(6, V)], dtype=np.int32)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=2 * S.SHD_SEC, trace=True, load=3,
+                      queue_flags=S.SHD_QF_TRACE_STATUS, app_peer=peer)
+    otr, _, _ = O.engine_run(m, g)
+    ips = ["11.0.%d.%d" % (h >> 8, h & 255) for h in range(V)]
+    c = S.status_lines(otr, ips, payload=1, app_peer=peer)
+    assert c == S.status_lines_py(otr, ips, payload=1, app_peer=peer)
+    assert any(":8998 -> " in x[2] for x in c) and any(" -> 11.0.0.%d:8998 " % (k + 1) in x[2] for k in range(6) for x in c[:50])
     snaps = np.array([[5, 7], [9, 9], [0xFFFFFFF0, 20], [3, 25]], dtype=np.uint32)
     for pl in (0, 1, 1500):
         assert S.tracker_node_lines(snaps, S.SHD_SEC, pl) == S.tracker_node_lines_py(snaps, S.SHD_SEC, pl)
