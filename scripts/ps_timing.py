@@ -65,7 +65,8 @@ def main():
     # the measured launch's blocks (k_round_ps: one per 64 hosts; k_round_sp: fewer) and its rounds' slots
     fresh = t[:, :, 0] != t_before[:, :, 0]
     grid = int(np.count_nonzero(fresh.any(axis=0)))
-    t = np.where(fresh[:, :, None], t, 0)[:, :grid, :8]
+    t_all = np.where(fresh[:, :, None], t, 0)[:, :grid, :]
+    t = t_all[:, :, :8]
     rows = []
     skipped = [0, 0]
     for r in range(64):
@@ -87,6 +88,17 @@ def main():
     for k in range(8):
         v = rows[:, :, k]
         print(f"  {k} {names[k]:12s} mean {np.nanmean(v):6.2f}  max {np.nanmean(np.nanmax(v, axis=1)):6.2f}")
+    # the last flush's resolve loop (stamps 12, 13), in blocks that flushed
+    fl = []
+    for r in range(64):
+        x = t_all[r]
+        t0 = x[:, 0].min()
+        ok = (x[:, 12] >= t0) & (x[:, 13] >= x[:, 12]) & (t0 > 0)
+        if ok.any():
+            fl.append(((x[ok, 12] - t0) / 100.0, (x[ok, 13] - x[ok, 12]) / 100.0))
+    if fl:
+        print(f"  last flush resolve: starts mean {np.mean([a.mean() for a, _ in fl]):.2f} us, lasts mean "
+              f"{np.mean([b.mean() for _, b in fl]):.2f} / max {np.mean([b.max() for _, b in fl]):.2f} us")
     per = np.diff(np.nanmax(rows[:, :, 7], axis=1))
     print(f"  round period (max 'all seen' to the next) {np.mean(per[per > 0]):.2f} us")
 

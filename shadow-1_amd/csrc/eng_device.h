@@ -1096,6 +1096,19 @@ struct PendDel {
     uint16_t near;   // kind 1: the bin is before HostCtx::pf_lim (note_dirty)
 };
 
+// the destination of a draw with closed-form destinations (dest_closed):
+// _phold_chooseNode's first i with dest_cum[i] >= x / RAND_MAX, from the
+// even cumulative weights' formula and the host-made exception list
+__device__ __forceinline__ int32_t closed_dest(const DParams& P, uint32_t r) {
+    const uint64_t nx = (uint64_t)r * (uint64_t)(uint32_t)P.H;
+    const uint64_t cx = (nx + 2147483646ull) / 2147483647ull;
+    int32_t d = cx ? (int32_t)cx - 1 : 0;
+#pragma unroll
+    for (int j = 0; j < kDestExc; j++)   // unrolled: the list is read in one scalar batch
+        d = (j < P.n_exc && (int32_t)r == P.exc_x[j]) ? P.exc_d[j] : d;
+    return d;
+}
+
 __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool defer, PendDel& pd) {
     pd.kind = 0;
     const uint32_t lane = threadIdx.x;
@@ -1122,14 +1135,8 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             dst = (int32_t)(q.r & ~kDstHost);
             b = P.host_att[dst];
         } else if (P.dest_closed) {   // no table: one memory round trip fewer
-            const uint64_t nx = (uint64_t)q.r * (uint64_t)(uint32_t)P.H;
-            const uint64_t cx = (nx + 2147483646ull) / 2147483647ull;
-            int32_t d = cx ? (int32_t)cx - 1 : 0;
-#pragma unroll
-            for (int j = 0; j < kDestExc; j++)   // unrolled: the list is read in one scalar batch
-                d = (j < P.n_exc && (int32_t)q.r == P.exc_x[j]) ? P.exc_d[j] : d;
-            dst = d;
-            b = d;
+            dst = closed_dest(P, q.r);
+            b = dst;
         } else {
             const double rr = (double)q.r / kRandMax;
             const size_t row = (size_t)s_cls[hl] * (size_t)P.H;
