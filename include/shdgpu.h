@@ -500,6 +500,32 @@ int shd_eng_pending_copy(shd_eng* e, shd_pending* out, uint64_t cap, uint64_t* n
  * finalized (delivery time from the min-rank row) */
 int shd_eng_resolve(shd_eng* e, const shd_pending* all, uint64_t n_all);
 int shd_eng_end_round(shd_eng* e, shd_round_summary* out);
+/* One lazy path cache across a co-simulation (INTEGRATION.md "Mixed CPU/GPU
+ * hosts"): shd_eng_round_begin = shd_eng_round_kernel behind a device state
+ * copy while first touches may still come.  When its summary carries
+ * SHD_ERR_AMBIGUOUS (a first-touch drop decision that depends on which row
+ * ranks first), shd_eng_round_retry rolls the engine back to the copy, ranks
+ * `all` (this round's pending records and the other side's first touches of
+ * the window) in serial event order and runs the window again (then
+ * end_round; nothing is left to resolve).  SHD_EAMBIG from the retry when the
+ * round ran without a copy (out of device memory for it). */
+int shd_eng_round_begin(shd_eng* e, uint64_t window_start, uint64_t window_end, shd_round_summary* out);
+int shd_eng_round_retry(shd_eng* e, const shd_pending* all, uint64_t n_all, shd_round_summary* out);
+/* The CPU side of that protocol on a path cache its lookups go through (the
+ * topology adapter's, topology_shd.c): shd_pc_defer_touches takes the engine's
+ * first touches of the window (shd_pending, attached indices, any order;
+ * SHD_EINVAL while the last window's are not all applied); shd_pc_query_key
+ * names the executing event (event_compare's key: time, host = its
+ * destination, src, seq) before its lookups, which count from 0 within it;
+ * shd_pc_lookup then applies every deferred touch before the query's key
+ * first, and logs the query when it ranks a row or a self path;
+ * shd_pc_take_touches applies the rest and returns the logged queries in
+ * event order (*n = the count; copied when out != NULL and cap covers it,
+ * SHD_ERANGE otherwise; then the log empties).  The pc and the engine must
+ * start with the same ranks (both fresh). */
+int shd_pc_defer_touches(shd_pc* pc, const shd_pending* recs, uint64_t n);
+int shd_pc_query_key(shd_pc* pc, uint64_t time, uint32_t host, uint32_t src, uint64_t seq);
+int shd_pc_take_touches(shd_pc* pc, shd_pending* out, uint64_t cap, uint64_t* n);
 /* events this engine produced for hosts of other engines (device to device
  * copy into dev_dst, capacity cap events) and ingest of received events */
 int shd_eng_remote_copy(shd_eng* e, void* dev_dst, uint64_t cap, uint64_t* n);

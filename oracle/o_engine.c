@@ -125,6 +125,13 @@ typedef struct {
      * (part = 0: every host is here) */
     int32_t part, h_lo, h_hi;
     evvec egress;
+    /* one lazy cache across the sides (o_state_defer_touches): the other
+     * side's first touches of the window, sorted, the next to apply; this
+     * side's own; the attached vertices by index */
+    shd_pending* ftd; uint64_t nftd, iftd;
+    shd_pending* ftown; uint64_t nftown, capftown;
+    int32_t ft_on;
+    const int32_t* attached;
 } ctx_t;
 
 static void evvec_push(evvec* v, const shd_event* e) {
@@ -289,12 +296,46 @@ static void worker_send_packet_par(ctx_t* c, uint32_t h, uint32_t dst, uint32_t 
     }
 }
 
+/* event_compare's order of two queries' executing events (time, host, src,
+ * seq), then their position in the event */
+static int pend_key_less(const shd_pending* x, const shd_pending* y) {
+    if (x->qtime != y->qtime) return x->qtime < y->qtime;
+    if (x->qhost != y->qhost) return x->qhost < y->qhost;
+    if (x->qsrc != y->qsrc) return x->qsrc < y->qsrc;
+    if (x->qseq != y->qseq) return x->qseq < y->qseq;
+    return x->qsub < y->qsub;
+}
+static int pend_key_cmp(const void* a, const void* b) {
+    const shd_pending* x = a; const shd_pending* y = b;
+    return pend_key_less(x, y) ? -1 : pend_key_less(y, x) ? 1 : 0;
+}
+/* the one-cache protocol at a query of this side (serial mode): the other
+ * side's first touches before it in event order go to the cache first; a
+ * query that runs a row or a self path is logged as this side's first touch */
+static void first_touch_sync(ctx_t* c, int32_t sv, int32_t dv) {
+    shd_pending k;
+    memset(&k, 0, sizeof(k));
+    k.qtime = c->q_time; k.qseq = c->q_seq; k.qhost = c->q_host; k.qsrc = c->q_src; k.qsub = c->q_sub++;
+    while (c->iftd < c->nftd && pend_key_less(&c->ftd[c->iftd], &k)) {
+        const shd_pending* r = &c->ftd[c->iftd++];
+        o_topo_touch(c->topo, c->attached[r->a], c->attached[r->b]);
+    }
+    if (!o_topo_would_run(c->topo, sv, dv)) return;
+    if (c->nftown == c->capftown) {
+        c->capftown = c->capftown ? 2 * c->capftown : 64;
+        c->ftown = realloc(c->ftown, c->capftown * sizeof(shd_pending));
+    }
+    k.a = (uint32_t)c->att_index[sv]; k.b = (uint32_t)c->att_index[dv];
+    c->ftown[c->nftown++] = k;
+}
+
 /* worker_sendPacket (worker.c:260-321) */
 static void worker_send_packet(ctx_t* c, uint32_t h, uint32_t dst, uint32_t pkt) {
     if (c->hq) { worker_send_packet_par(c, h, dst, pkt); return; }
     ohost* H = &c->hosts[h];
     int32_t sv = c->m->host_vertex[h], dv = c->m->host_vertex[dst];
     double lat, rel;
+    if (c->ft_on) first_touch_sync(c, sv, dv);
     o_topo_get(c->topo, sv, dv, &lat, &rel);          /* topology_getReliability */
     double reliability = rel;
     double chance = o_next_double(&H->rng);
@@ -567,6 +608,7 @@ static o_state* state_new(const shd_model* m, const shd_graph* gin, int32_t forc
     }
     free(att);
     c->att_index = S->att_index;
+    c->attached = S->attached;
     c->topo = o_topo_new(S->g, S->attached, S->na, force_rows);
     c->hosts = calloc(m->n_hosts, sizeof(ohost));
     for (int32_t h = 0; h < m->n_hosts; h++) {
@@ -630,6 +672,32 @@ int o_state_take_egress(o_state* S, shd_event* out, uint64_t cap, uint64_t* n) {
     v->n = 0;
     return 0;
 }
+int o_state_defer_touches(o_state* S, const shd_pending* recs, uint64_t n) {
+    ctx_t* c = &S->c;
+    if (c->hq || c->iftd < c->nftd) return -1;   /* serial mode; the last window's all applied */
+    for (uint64_t i = 0; i < n; i++)
+        if (recs[i].a >= (uint32_t)S->na || recs[i].b >= (uint32_t)S->na) return -1;
+    c->ft_on = 1;
+    c->ftd = realloc(c->ftd, (n + 1) * sizeof(shd_pending));
+    if (n) memcpy(c->ftd, recs, n * sizeof(shd_pending));
+    qsort(c->ftd, n, sizeof(shd_pending), pend_key_cmp);
+    c->nftd = n; c->iftd = 0;
+    return 0;
+}
+int o_state_take_touches(o_state* S, shd_pending* out, uint64_t cap, uint64_t* n) {
+    ctx_t* c = &S->c;
+    while (c->iftd < c->nftd) {
+        const shd_pending* r = &c->ftd[c->iftd++];
+        o_topo_touch(c->topo, c->attached[r->a], c->attached[r->b]);
+    }
+    *n = c->nftown;
+    if (!out) return 0;
+    if (cap < c->nftown) return -1;
+    if (c->nftown) memcpy(out, c->ftown, c->nftown * sizeof(shd_pending));
+    c->nftown = 0;
+    return 0;
+}
+
 /* time of the next event here (UINT64_MAX when none) */
 uint64_t o_state_next_time(const o_state* S) { return S->c.q.n ? S->c.q.a[0].time : UINT64_MAX; }
 /* the trace so far: *n = its length; copied when out != NULL and cap covers it */
@@ -897,6 +965,8 @@ o_state* o_state_clone(const o_state* S) {
     memcpy(C->c.q.a, S->c.q.a, sizeof(shd_event) * S->c.q.n);
     C->c.egress.a = malloc(sizeof(shd_event) * (S->c.egress.cap ? S->c.egress.cap : 1));
     memcpy(C->c.egress.a, S->c.egress.a, sizeof(shd_event) * S->c.egress.n);
+    C->c.ftd = NULL; C->c.nftd = C->c.iftd = 0;   /* the one-cache protocol starts afresh */
+    C->c.ftown = NULL; C->c.nftown = C->c.capftown = 0; C->c.ft_on = 0;
     C->shared = 1;
     return C;
 }
@@ -925,7 +995,7 @@ const o_run* o_state_stats(const o_state* S) { return &S->run; }
 void o_state_free(o_state* S) {
     if (!S) return;
     for (int32_t h = 0; h < S->c.m->n_hosts; h++) { o_codel_free(&S->c.hosts[h].codel); free(S->c.hosts[h].txq); }
-    free(S->c.hosts); free(S->c.q.a); free(S->c.egress.a);
+    free(S->c.hosts); free(S->c.q.a); free(S->c.egress.a); free(S->c.ftd); free(S->c.ftown);
     o_topo_free(S->c.topo);
     if (!S->shared) {
         if (S->row_lat) {

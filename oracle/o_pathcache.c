@@ -412,6 +412,14 @@ int o_topo_peek(const o_topo* t, int32_t s, int32_t d, double* lat, double* rel)
     return 1;
 }
 
+int o_topo_would_run(const o_topo* t, int32_t s, int32_t d) {
+    if (tab_find((o_topo*)t, s, d)) return 0;
+    if (!t->g->directed && tab_find((o_topo*)t, d, s)) return 0;
+    if (t->props.is_complete || (t->g->prefer_direct && o_get_eid(t->g, s, d) >= 0)) return 0;
+    return 1;
+}
+void o_topo_touch(o_topo* t, int32_t s, int32_t d) { (void)get_path_entry(t, s, d); }
+
 o_topo* o_topo_clone(const o_topo* t) {
     o_topo* c = malloc(sizeof(*c));
     *c = *t;

@@ -93,6 +93,11 @@ int o_topo_is_complete(const o_topo* t);
 /* read-only: 1 and the value when the pair has an entry in either orientation */
 int o_topo_peek(const o_topo* t, int32_t s, int32_t d, double* lat, double* rel);
 o_topo* o_topo_clone(const o_topo* t);
+/* 1 when _topology_getPathEntry(s, d) would run a source row or a self path
+ * now (no entry to serve it, not a direct-path pair): a first touch */
+int o_topo_would_run(const o_topo* t, int32_t s, int32_t d);
+/* _topology_getPathEntry(s, d) for its effect on the cache only */
+void o_topo_touch(o_topo* t, int32_t s, int32_t d);
 /* _topology_getPathEntry (topology.c:1969-2051) -> path latency/reliability;
  * returns 0 and -1/-1 when the reference returns NULL */
 int o_topo_get(o_topo* t, int32_t s, int32_t d, double* lat, double* rel);
@@ -175,6 +180,16 @@ o_state* o_state_new_part(const shd_model* m, const shd_graph* g, int32_t h_lo, 
 int o_state_inject(o_state* s, const shd_event* ev, uint64_t n);
 int o_state_take_egress(o_state* s, shd_event* out, uint64_t cap, uint64_t* n);
 uint64_t o_state_next_time(const o_state* s);
+/* one lazy path cache across the sides (round 4): before a window, the other
+ * side's first touches of that window (shd_pending records, attached indices,
+ * any order) -- each is applied to this side's cache just before the first
+ * query of this side that comes after it in event order; after the window,
+ * o_state_take_touches applies the rest and returns this side's own first
+ * touches of the window (o_topo_would_run at the query) as shd_pending
+ * records, in event order: *n = the count, copied when out != NULL and cap
+ * covers it (then the list empties) */
+int o_state_defer_touches(o_state* s, const shd_pending* recs, uint64_t n);
+int o_state_take_touches(o_state* s, shd_pending* out, uint64_t cap, uint64_t* n);
 int o_state_trace(const o_state* s, shd_trace_rec* out, uint64_t cap, uint64_t* n);
 void o_state_free(o_state* s);
 

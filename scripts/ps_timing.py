@@ -99,6 +99,26 @@ def main():
     if fl:
         print(f"  last flush resolve: starts mean {np.mean([a.mean() for a, _ in fl]):.2f} us, lasts mean "
               f"{np.mean([b.mean() for _, b in fl]):.2f} / max {np.mean([b.max() for _, b in fl]):.2f} us")
+    # the event loop: iterations (16), flushes (17), active lanes (18) per block and round, and
+    # how the loop's length (stamp 2 -> 4) follows them
+    it, nfl, nact, dur, seg = [], [], [], [], []
+    for r in range(64):
+        x = t_all[r]
+        t0 = x[:, 0].min()
+        ok = (t0 > 0) & (x[:, 4] >= x[:, 2]) & (x[:, 2] >= t0) & (x[:, 16] < 10000)
+        it += list(x[ok, 16]); nfl += list(x[ok, 17]); nact += list(x[ok, 18])
+        seg += [list(v) for v in x[ok][:, [8, 9, 10, 11, 15, 19]] / 100.0]
+        dur += list((x[ok, 4] - x[ok, 2]) / 100.0)
+    if it:
+        it, nfl, nact, dur, seg = map(np.array, (it, nfl, nact, dur, seg))
+        print(f"  loop: iterations mean {it.mean():.2f} max {it.max()}; flushes mean {nfl.mean():.2f}; "
+              f"active lanes mean {nact.mean():.1f}; loop us mean {dur.mean():.2f}")
+        for k in sorted(set(it.tolist()))[:12]:
+            sel = it == k
+            print(f"    {k:3d} iterations: {sel.sum():5d} block-rounds, loop {dur[sel].mean():.2f} us "
+                  f"(take+begin {seg[sel, 0].mean():.2f} = take_next {seg[sel, 3].mean():.2f} + begin_event "
+                  f"{seg[sel, 4].mean():.2f} + notify {seg[sel, 5].mean():.2f} + rest; run_work "
+                  f"{seg[sel, 1].mean():.2f}, early flushes {seg[sel, 2].mean():.2f}), flushes {nfl[sel].mean():.2f}")
     per = np.diff(np.nanmax(rows[:, :, 7], axis=1))
     print(f"  round period (max 'all seen' to the next) {np.mean(per[per > 0]):.2f} us")
 

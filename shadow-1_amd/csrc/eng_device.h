@@ -983,9 +983,13 @@ __device__ PathVal path_value(const DParams& P, int32_t a, int32_t b) {
     return path_select(P, a, b, ra, x);
 }
 
+// the persistent kernels' summary of the running round (they read one copy
+// of the parameters for the whole batch, whose `sum` is the batch's first)
+__shared__ DevSummary* s_rsum;
+
 __device__ void log_pending(const DParams& P, HostCtx& c, const SendRec& q, int32_t a, int32_t b, uint32_t delivered,
-                            uint32_t dst, uint64_t seq) {
-    unsigned long long i = atomicAdd(&P.sum->n_pending, 1ull);
+                            uint32_t dst, uint64_t seq, DevSummary* sum) {
+    unsigned long long i = atomicAdd(&sum->n_pending, 1ull);
     c.n_pend++;
     if (i >= P.pend_cap) { c.err |= SHD_ERR_PENDING_OVERFLOW; return; }
     Pending r;
@@ -1109,6 +1113,7 @@ __device__ __forceinline__ int32_t closed_dest(const DParams& P, uint32_t r) {
     return d;
 }
 
+template <bool PS = false>
 __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool defer, PendDel& pd) {
     pd.kind = 0;
     const uint32_t lane = threadIdx.x;
@@ -1204,7 +1209,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
             trace(P, c, q.now, seq, c.h, e.dst, q.pkt, SHD_TR_SENT);
             c.c_sent++;
             // 1 = delivery waits for the resolution, 2 = already delivered
-            if (log) log_pending(P, c, q, c.att, b, resolved ? 2u : 1u, e.dst, seq);
+            if (log) log_pending(P, c, q, c.att, b, resolved ? 2u : 1u, e.dst, seq, PS ? s_rsum : P.sum);
             if (resolved && e.time < c.k.end_time) {   // scheduler_push drops time >= end
                 emit = SHD_EV_PACKET;
                 if (e.time < c.min_emit) c.min_emit = e.time;
@@ -1213,7 +1218,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
         } else {
             trace(P, c, q.now, 0, c.h, e.dst, q.pkt, SHD_TR_INET_DROP);
             c.c_idrop++;
-            if (log) log_pending(P, c, q, c.att, b, 0u, e.dst, 0);
+            if (log) log_pending(P, c, q, c.att, b, 0u, e.dst, 0, PS ? s_rsum : P.sum);
             const uint64_t xi = c.seq_base + q.pseq;
             f0 += xi < c.ts0; f1 += xi < c.ts1; f2 += xi < c.ts2;
             nfail++;

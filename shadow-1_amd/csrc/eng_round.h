@@ -1205,17 +1205,39 @@ __device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool
                                               const uint32_t (&cm)[kNBW], uint64_t& next, PfBins* pb) {
     PendDel pd;
     pd.kind = 0;
+#ifdef SHD_TIMING_LIGHT
+    uint32_t n_it = 0, n_fl = 0;
+    unsigned long long t_take = 0, t_work = 0, t_fl = 0, ta = 0, t_q[3] = {0, 0, 0};
+#endif
     {
         uint32_t st = active ? 0u : 3u;
         for (;;) {
             for (;;) {
+#ifdef SHD_TIMING_LIGHT
+                n_it++;
+                ta = wall_clock64();
+#endif
                 if (st == 0u) {
                     shd_event e;
-                    if (take_next(P, c, we, e)) {
+#ifdef SHD_TIMING_LIGHT
+                    const unsigned long long q0 = wall_clock64();
+#endif
+                    const bool got = take_next(P, c, we, e);
+#ifdef SHD_TIMING_LIGHT
+                    const unsigned long long q1 = wall_clock64();
+                    t_q[0] += q1 - q0;
+#endif
+                    if (got) {
                         c.now = e.time;
                         begin_event(P, c, e);
+#ifdef SHD_TIMING_LIGHT
+                        t_q[1] += wall_clock64() - q1;
+#endif
                         st = ((c.w_fl & ~W_READ) | c.w_msgs) ? 1u : 0u;
 #ifndef SHD_NO_FUSE
+#ifdef SHD_TIMING_LIGHT
+                        const unsigned long long q2 = wall_clock64();
+#endif
                         if (st == 0u && c.tt2 < we) {   // the notification, when it is next (round_body)
                             const uint64_t t = c.tt2, ht = c.evq_n ? c.top_time : kInf;
                             if (t < c.tt0 && t < c.tt1 && t < c.dt && t < ht && notify_fast_ok(P, c)) {
@@ -1226,6 +1248,9 @@ __device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool
                                 st = c.w_fl ? 1u : 0u;
                             }
                         }
+#ifdef SHD_TIMING_LIGHT
+                        t_q[2] += wall_clock64() - q2;
+#endif
                         if (st == 0u && c.tt1 < we) {   // the periodic refill, when it is next
                             const uint64_t t = c.tt1, ht = c.evq_n ? c.top_time : kInf;
                             if (t < c.tt0 && t < c.tt2 && t < c.dt && t < ht && c.cq_count == 0 && c.tq_count == 0) {
@@ -1240,19 +1265,47 @@ __device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool
                         st = 3u;
                     }
                 }
+#ifdef SHD_TIMING_LIGHT
+                {
+                    const unsigned long long tb = wall_clock64();
+                    t_take += tb - ta;
+                    ta = tb;
+                }
+#endif
                 if (st == 1u) st = run_work(P, c) ? 0u : 2u;
+#ifdef SHD_TIMING_LIGHT
+                t_work += wall_clock64() - ta;
+#endif
                 if (__ballot(st <= 1u) == 0) break;
             }
             const bool last = __ballot(st == 2u) == 0;
 #ifdef SHD_TIMING
             if (last) TIM(3);   // the round's last flush starts
 #endif
-            flush_wave(P, c, last, pd);
+#ifdef SHD_TIMING_LIGHT
+            n_fl++;
+            ta = wall_clock64();
+#endif
+            flush_wave<true>(P, c, last, pd);
+#ifdef SHD_TIMING_LIGHT
+            if (!last) t_fl += wall_clock64() - ta;
+#endif
             if (last) break;
             if (st == 2u) st = 1u;
         }
     }
     TIM(4);
+#ifdef SHD_TIMING_LIGHT
+    TIMV(16, (uint64_t)n_it);   // loop iterations of the wave
+    TIMV(17, (uint64_t)n_fl);   // flushes
+    TIMV(18, (uint64_t)__popcll(__ballot(active)));
+    TIMV(8, t_take);    // in take_next + begin_event (+ the fused notification / refill)
+    TIMV(9, t_work);    // in run_work
+    TIMV(10, t_fl);     // in the flushes before the last
+    TIMV(11, t_q[0]);   // of 8: take_next
+    TIMV(15, t_q[1]);   //       begin_event
+    TIMV(19, t_q[2]);   //       the fused notification (the rest: the fused refill, the loop's own)
+#endif
 #pragma unroll
     for (int k = 0; k < (int)kNBW; k++) w[k] &= ~cm[k];
     if (PF) pf_issue(R, lb, we >> P.bin_shift, w, has, *pb);
@@ -1408,6 +1461,22 @@ __device__ __forceinline__ void ps_fresh(DevSummary* s) {
 // uses for its close and for the next prefetch is loaded at its start and
 // consumed after its loop; it holds every append of the rounds before (an
 // append of this round is covered by its sender's own next time, min_emit).
+// The persistent kernels' parameters: one copy for the whole batch (P0 =
+// Pr[1]), whose fields stay in the scalar cache across rounds -- the copies
+// Pr[i + 1] differ in `sum` only, and a copy per round made every round's
+// first read of each field a scalar-cache miss; the round's summary is
+// s_rsum.  (Timing builds keep the copy per round: the stamps' slot follows
+// P.sum.  SHD_PS_PR: the same, for an A/B.)
+#if defined(SHD_TIMING) || defined(SHD_PS_PR)
+#define PS_PARAMS(i)                                    \
+    const DParams& P = Pr[(i) + 1];                     \
+    if (threadIdx.x == 0) s_rsum = &ring[(i) + 1]
+#else
+#define PS_PARAMS(i)                                    \
+    const DParams& P = P0;                              \
+    if (threadIdx.x == 0) s_rsum = &ring[(i) + 1]
+#endif
+
 #ifndef SHD_NO_PF
 constexpr bool kPsPf = true;
 #else
@@ -1461,7 +1530,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
 #pragma unroll
     for (int k = 0; k < (int)kNBW; k++) pw[k] = 0;
     for (int i = 0; i < nb; i++) {
-        const DParams& P = Pr[i + 1];
+        PS_PARAMS(i);
         const unsigned long long t_start = wall_clock64();
 #ifdef SHD_TIMING
         if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = t_start;
@@ -1637,7 +1706,7 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
     const bool lead = blockIdx.x == 0 && lane == 0;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     for (int i = 0; i < nb; i++) {
-        const DParams& P = Pr[i + 1];
+        PS_PARAMS(i);
         const unsigned long long t_start = wall_clock64();
 #ifdef SHD_TIMING
         if (lane == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = t_start;

@@ -83,6 +83,11 @@ struct shd_eng {
     // drop decisions turns out ambiguous, then the round reruns with the ranks
     std::vector<void*> snap;
     bool snap_failed = false;
+    // shd_eng_round_begin's state copy, for shd_eng_round_retry
+    bool rb_snap = false;
+    int rb_parity = 0;
+    uint64_t rb_round = 0, rb_ws = 0, rb_we = 0;
+    DevSummary rb_sum{};
     bool logged_any = false;                // a round has logged a first touch
     uint64_t last_logged = 0;               // first touches logged by the last round
     // inputs kept on device
@@ -805,6 +810,9 @@ extern "C" int shd_eng_end_round(shd_eng* e, shd_round_summary* out) {
         out->n_events = e->round_events; out->n_pkt_events = e->round_pkt;
         out->n_pending = e->round_pending; out->n_remote = e->h_sum->n_remote; out->error = e->h_sum->error;
     }
+    // finalized: a later shd_eng_resolve without a round (first touches of
+    // another side only) assigns ranks and finalizes nothing
+    e->round_pending = 0;
     if (e->h_sum->error & SHD_ERR_AMBIGUOUS) return SHD_EAMBIG;
     if (e->h_sum->error) return SHD_EOVERFLOW;
     return SHD_OK;
@@ -976,6 +984,57 @@ static int protected_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summa
         if ((rc = shd_eng_resolve(e, recs.data(), n))) return rc;
     }
     return shd_eng_end_round(e, out);
+}
+
+// A round whose first touches are ranked with another side's (one lazy path
+// cache across a co-simulation, INTEGRATION.md "Mixed CPU/GPU hosts"): the
+// kernel behind a state copy when first touches may still come (want_protect);
+// shd_eng_round_retry rolls back to it, ranks `all` in serial order and runs
+// the window again (an ambiguous first-touch drop decision: the other side's
+// first touches of the window may rank rows before the engine's)
+extern "C" int shd_eng_round_begin(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out) {
+    if (!e || !e->booted || we <= ws || we - ws > e->window) return SHD_EINVAL;
+    SHD_HIP(hipSetDevice(e->device));
+    e->rb_snap = false;
+    if (want_protect(e)) {
+        const int rc = snapshot_state(e, false);
+        if (rc == SHD_OK) {
+            e->rb_snap = true;
+            e->rb_parity = e->parity;
+            e->rb_round = e->round;
+            e->rb_sum = *e->h_sum;
+            e->rb_ws = ws;
+            e->rb_we = we;
+        } else if (rc != SHD_ENOMEM) {
+            return rc;
+        }
+    }
+    const int rc = shd_eng_round_kernel(e, ws, we, out);
+    if (rc) return rc;
+    e->last_logged = e->round_pending;
+    if (e->round_pending) e->logged_any = true;
+    return SHD_OK;
+}
+
+extern "C" int shd_eng_round_retry(shd_eng* e, const shd_pending* all, uint64_t n_all, shd_round_summary* out) {
+    if (!e || (n_all && !all)) return SHD_EINVAL;
+    if (!e->rb_snap) return SHD_EAMBIG;   // not protected: the ambiguity stands
+    SHD_HIP(hipSetDevice(e->device));
+    e->rb_snap = false;
+    int rc = snapshot_state(e, true);
+    if (rc) return rc;
+    e->parity = e->rb_parity;
+    e->round = e->rb_round;
+    *e->h_sum = e->rb_sum;
+    if ((rc = assign_ranks(e, all, n_all))) return rc;
+    if ((rc = shd_eng_round_kernel(e, e->rb_ws, e->rb_we, out))) return rc;
+    // every first touch of the window is ranked now: the engine's (its queries
+    // after an ambiguous one share their source with it) and the other side's
+    if (e->round_pending) {
+        e->h_sum->error |= SHD_ERR_INTERNAL;
+        if (out) out->error = e->h_sum->error;
+    }
+    return SHD_OK;
 }
 
 extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {

@@ -881,10 +881,99 @@ static int run_row_for_min(shd_pc* pc, int32_t a) {
     return SHD_OK;
 }
 
+// One lazy cache across a co-simulation, this cache being the CPU side's
+// (INTEGRATION.md "Mixed CPU/GPU hosts"): the other side's first touches of
+// the window, in event order, applied just before this side's first later
+// query; this side's own first touches (lookups that rank a row), logged
+struct PcTouches {
+    std::vector<shd_pending> defer;
+    size_t next = 0;
+    std::vector<shd_pending> own;
+    shd_pending key{};
+    bool on = false;
+};
+static bool pend_key_less(const shd_pending& x, const shd_pending& y) {
+    if (x.qtime != y.qtime) return x.qtime < y.qtime;
+    if (x.qhost != y.qhost) return x.qhost < y.qhost;
+    if (x.qsrc != y.qsrc) return x.qsrc < y.qsrc;
+    if (x.qseq != y.qseq) return x.qseq < y.qseq;
+    return x.qsub < y.qsub;
+}
+static int pc_lookup_at(shd_pc* pc, int32_t a, int32_t b, double* lat, double* rel);
+
+// the deferred touches before `k` (or all: k null) to the cache
+static int pc_apply_deferred(shd_pc* pc, const shd_pending* k) {
+    PcTouches* t = (PcTouches*)pc->touches;
+    while (t->next < t->defer.size() && (!k || pend_key_less(t->defer[t->next], *k))) {
+        const shd_pending& r = t->defer[t->next++];
+        double l, q;
+        const int rc = pc_lookup_at(pc, (int32_t)r.a, (int32_t)r.b, &l, &q);
+        if (rc) return rc;
+    }
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_defer_touches(shd_pc* pc, const shd_pending* recs, uint64_t n) {
+    if (!pc || (n && !recs)) return SHD_EINVAL;
+    if (!pc->touches) pc->touches = new PcTouches();
+    PcTouches* t = (PcTouches*)pc->touches;
+    if (t->next < t->defer.size()) return SHD_EINVAL;   // the last window's not all applied
+    for (uint64_t i = 0; i < n; i++)
+        if (recs[i].a >= (uint32_t)pc->T || recs[i].b >= (uint32_t)pc->T) return SHD_EINVAL;
+    t->defer.assign(recs, recs + n);
+    std::sort(t->defer.begin(), t->defer.end(), pend_key_less);
+    t->next = 0;
+    t->on = true;
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_query_key(shd_pc* pc, uint64_t time, uint32_t host, uint32_t src, uint64_t seq) {
+    if (!pc) return SHD_EINVAL;
+    if (!pc->touches) pc->touches = new PcTouches();
+    PcTouches* t = (PcTouches*)pc->touches;
+    t->key = shd_pending{};
+    t->key.qtime = time; t->key.qhost = host; t->key.qsrc = src; t->key.qseq = seq; t->key.qsub = 0;
+    return SHD_OK;
+}
+
+extern "C" int shd_pc_take_touches(shd_pc* pc, shd_pending* out, uint64_t cap, uint64_t* n) {
+    if (!pc || !n) return SHD_EINVAL;
+    PcTouches* t = (PcTouches*)pc->touches;
+    if (!t) { *n = 0; return SHD_OK; }
+    if (pc->built) {
+        const int rc = pc_apply_deferred(pc, nullptr);
+        if (rc) return rc;
+    }
+    *n = t->own.size();
+    if (!out) return SHD_OK;
+    if (cap < t->own.size()) return SHD_ERANGE;
+    if (!t->own.empty()) memcpy(out, t->own.data(), sizeof(shd_pending) * t->own.size());
+    t->own.clear();
+    return SHD_OK;
+}
+
 extern "C" int shd_pc_lookup(shd_pc* pc, int32_t sv, int32_t dv, double* lat, double* rel) {
     if (!pc || !pc->built || !lat || !rel || sv < 0 || dv < 0 || sv >= pc->V || dv >= pc->V) return SHD_EINVAL;
     const int32_t a = pc->h_att_index[sv], b = pc->h_att_index[dv];
     if (a < 0 || b < 0) { *lat = -1; *rel = -1; return SHD_EINVAL; }
+    PcTouches* t = (PcTouches*)pc->touches;
+    if (!t || !t->on) return pc_lookup_at(pc, a, b, lat, rel);
+    shd_pending k = t->key;
+    k.qsub = t->key.qsub++;
+    int rc = pc_apply_deferred(pc, &k);
+    if (rc) return rc;
+    const int32_t nr0 = pc->next_rank;
+    if ((rc = pc_lookup_at(pc, a, b, lat, rel))) return rc;
+    if (pc->next_rank != nr0) {   // this lookup ranked a row (or a self path): a first touch
+        k.a = (uint32_t)a;
+        k.b = (uint32_t)b;
+        t->own.push_back(k);
+    }
+    return SHD_OK;
+}
+
+// shd_pc_lookup by attached indices (the rank rule, then the value)
+static int pc_lookup_at(shd_pc* pc, int32_t a, int32_t b, double* lat, double* rel) {
     SHD_HIP(hipSetDevice(pc->device));
     const int32_t T = pc->T;
     uint8_t adj = 0;
@@ -985,5 +1074,6 @@ extern "C" void shd_pc_destroy(shd_pc* pc) {
     free(pc->h_attached); free(pc->h_att_index); free(pc->h_w); free(pc->h_eloss); free(pc->h_vloss);
     free(pc->h_self_eid); free(pc->h_rank); free(pc->h_self_rank); free(pc->h_direct_stored);
     delete (std::unordered_map<uint64_t, uint64_t>*)pc->counts;
+    delete (PcTouches*)pc->touches;
     delete pc;
 }

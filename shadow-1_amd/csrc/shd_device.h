@@ -73,6 +73,7 @@ struct shd_pc {
     int32_t next_rank = 0;
     double min_stored_latency = 0.0;
     void* counts = nullptr;             // std::unordered_map<uint64_t,uint64_t>*
+    void* touches = nullptr;            // PcTouches* (shd_pc_defer_touches), or null
 };
 
 // resolved value for a (src attached idx, dst attached idx) pair given ranks

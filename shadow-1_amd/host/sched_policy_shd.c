@@ -45,6 +45,7 @@
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "../../include/shdgpu.h"
 
@@ -94,6 +95,17 @@ typedef struct shd_policy_bridge {
      * CPU-side host (NULL: dropped, and counted as an error) */
     Event* (*egress)(void* user, const shd_event* delivery);
     void* user;
+    /* optional (both or neither): one lazy path cache across the sides
+     * (topology.c:1969-2051 is one global cache).  touches_in hands the CPU
+     * side the engine's first touches of the round before the round's CPU
+     * events pop (the CPU side's cache applies each just before its first
+     * later query, in event_compare order); touches_out, after them, returns
+     * the CPU side's own first touches of the round (its queries that ran a
+     * source row or a self path), which the engine's resolution ranks with its
+     * own.  NULL: the two sides' first touches of a round are not ordered with
+     * each other, exact on complete and prefer-direct graphs only. */
+    void (*touches_in)(void* user, const shd_pending* engine_touches, uint64_t n);
+    uint64_t (*touches_out)(void* user, const shd_pending** cpu_touches);
 } shd_policy_bridge;
 
 typedef struct {
@@ -110,6 +122,11 @@ typedef struct {
     size_t n_in, cap_in;
     shd_event* egress;         /* a round's deliveries to CPU-side hosts */
     size_t cap_out;
+    int open;                  /* touches bridge: 1 a round ran whose resolution waits for the CPU side's
+                                  first touches, 2 a window with no device round (ranks only) */
+    int open_ambiguous;        /* its kernel flagged an ambiguous first-touch drop decision */
+    shd_pending* touch;        /* its first touches: the engine's, then the CPU side's */
+    size_t n_touch, cap_touch;
 } gpu_policy;
 
 static int ev_lt(Event* a, Event* b) { return event_compare(a, b, NULL) < 0; }
@@ -193,19 +210,86 @@ static void flush_ingress(gpu_policy* d) {
     d->n_in = 0;
 }
 
-/* bridged: the engine's one round of this Shadow round, then its egress */
+static int touch_room(gpu_policy* d, size_t n) {
+    if (d->n_touch + n <= d->cap_touch) return 1;
+    size_t nc = d->cap_touch ? d->cap_touch : 256;
+    while (nc < d->n_touch + n) nc *= 2;
+    shd_pending* nt = realloc(d->touch, sizeof(shd_pending) * nc);
+    if (!nt) { d->error = SHD_ENOMEM; return 0; }
+    d->touch = nt;
+    d->cap_touch = nc;
+    return 1;
+}
+
+static void take_egress(gpu_policy* d);
+
+/* touches bridge: the open round's resolution, over both sides' first touches
+ * (after the round's CPU events), then its end and egress */
+static void finish_open(gpu_policy* d) {
+    if (!d->open) return;
+    const int open = d->open;
+    d->open = 0;
+    const shd_pending* cp = NULL;
+    const uint64_t nc = d->bridge.touches_out(d->bridge.user, &cp);
+    if (nc && (!cp || !touch_room(d, nc))) { if (!cp) d->error = SHD_EINVAL; return; }
+    if (nc) memcpy(d->touch + d->n_touch, cp, sizeof(shd_pending) * nc);
+    d->n_touch += nc;
+    const int ran = open == 1;   /* 2: no device round this window, ranks only */
+    shd_round_summary r;
+    int rc;
+    if (ran && d->open_ambiguous)   /* the drop decision waited for the ranking: the window again */
+        rc = shd_eng_round_retry(d->eng, d->touch, d->n_touch, &r);
+    else
+        rc = shd_eng_resolve(d->eng, d->touch, d->n_touch);
+    d->n_touch = 0;
+    if (rc != SHD_OK) { d->error = rc; return; }
+    if (!ran) return;
+    if ((rc = shd_eng_end_round(d->eng, &r)) != SHD_OK) { d->error = rc; return; }
+    take_egress(d);
+}
+
+/* bridged: the engine's one round of this Shadow round, then its egress
+ * (touches bridge: the round's kernel and its first touches to the CPU side;
+ * the rest in finish_open) */
 static void advance_bridged(gpu_policy* d, SimulationTime barrier) {
+    finish_open(d);
     flush_ingress(d);
     uint64_t g = UINT64_MAX, W = 0;
     shd_eng_next_time(d->eng, &g);
     shd_eng_window(d->eng, &W);
     const SimulationTime ws = g > d->advanced ? g : d->advanced;
     d->advanced = barrier;
-    if (ws >= barrier) return;                     /* nothing on the device before the barrier */
+    if (ws >= barrier) {                           /* nothing on the device before the barrier */
+        if (d->bridge.touches_in) {   /* the CPU side's first touches still go to the engine's ranks */
+            d->bridge.touches_in(d->bridge.user, NULL, 0);
+            d->open = 2;
+        }
+        return;
+    }
     if (barrier - ws > W) { d->error = SHD_EINVAL; return; }   /* Shadow's window is wider than W */
     shd_round_summary r;
-    int rc = shd_eng_run_round(d->eng, ws, barrier, &r);
+    int rc;
+    if (d->bridge.touches_in) {
+        if ((rc = shd_eng_round_begin(d->eng, ws, barrier, &r)) != SHD_OK) { d->error = rc; return; }
+        d->open_ambiguous = (r.error & SHD_ERR_AMBIGUOUS) != 0;
+        uint64_t n = 0;
+        rc = shd_eng_pending_copy(d->eng, NULL, 0, &n);
+        if (rc != SHD_OK && rc != SHD_ERANGE) { d->error = rc; return; }
+        if (!touch_room(d, n)) return;
+        if (n && (rc = shd_eng_pending_copy(d->eng, d->touch, d->cap_touch, &n)) != SHD_OK) { d->error = rc; return; }
+        d->n_touch = n;
+        d->bridge.touches_in(d->bridge.user, d->touch, n);
+        d->open = 1;
+        return;
+    }
+    rc = shd_eng_run_round(d->eng, ws, barrier, &r);
     if (rc != SHD_OK) { d->error = rc; return; }
+    take_egress(d);
+}
+
+/* the round's deliveries to CPU-side hosts, as Shadow events in the heap */
+static void take_egress(gpu_policy* d) {
+    int rc;
     uint64_t n = 0;
     rc = shd_eng_take_remote(d->eng, d->egress, d->cap_out, &n);
     if (rc == SHD_ERANGE) {
@@ -242,9 +326,12 @@ static Event* _gpurounds_pop(SchedulerPolicy* policy, SimulationTime barrier) {
 
 static SimulationTime _gpurounds_getNextTime(SchedulerPolicy* policy) {
     gpu_policy* d = policy->data;
+    if (d->bridged) {
+        finish_open(d);     /* the round's CPU events have run: its egress joins the heap */
+        flush_ingress(d);   /* the engine's next time covers what it was sent */
+    }
     SimulationTime t = d->n ? event_getTime(d->heap[0]) : (SimulationTime)SHD_SIMTIME_MAX_;
     uint64_t g = UINT64_MAX;
-    if (d->bridged) flush_ingress(d);   /* the engine's next time covers what it was sent */
     if (d->grp) shd_xgroup_next_time(d->grp, &g);
     else if (d->eng) shd_eng_next_time(d->eng, &g);
     return g < t ? g : t;
@@ -256,6 +343,7 @@ static void _gpurounds_free(SchedulerPolicy* policy) {
     free(d->heap);
     free(d->ingress);
     free(d->egress);
+    free(d->touch);
     if (d->hosts) g_queue_free(d->hosts);
     free(d);
     free(policy);
@@ -285,7 +373,8 @@ SchedulerPolicy* schedulerpolicygpurounds_new(shd_eng* eng, shd_xgroup* grp) {
 /* the policy over a partial engine whose hosts exchange packets with Shadow's
  * CPU-side hosts through `bridge` (copied); NULL for an incomplete bridge */
 SchedulerPolicy* schedulerpolicygpurounds_new_bridged(shd_eng* eng, const shd_policy_bridge* bridge) {
-    if (!eng || !bridge || !bridge->ingress || !bridge->egress) return NULL;
+    if (!eng || !bridge || !bridge->ingress || !bridge->egress || !bridge->touches_in != !bridge->touches_out)
+        return NULL;
     SchedulerPolicy* p = schedulerpolicygpurounds_new(eng, NULL);
     if (!p) return NULL;
     gpu_policy* d = p->data;

@@ -25,6 +25,7 @@ SHD_QF_COUNT_PATHS = 2      # queue_flags: per-path packet counters on the devic
 SHD_QF_HEARTBEATS = 4       # queue_flags: tracker node counters at every heartbeat
 SHD_QF_NO_APP_START = 8     # queue_flags: the caller pushes the application starts (shd_eng_push_events)
 SHD_QF_TRACE_STATUS = 16    # queue_flags: with trace, the application's records too (status_lines)
+ERR_AMBIGUOUS = 16          # shd_round_summary.error: an ambiguous first-touch drop decision (SHD_ERR_AMBIGUOUS)
 SHD_PHOLD_LISTEN_PORT = 8998   # PHOLD_LISTEN_PORT, test_phold.c:34
 SHD_MIN_RANDOM_PORT = 10000    # MIN_RANDOM_PORT, definitions.h:94
 
@@ -259,6 +260,11 @@ _SIGS = {
     "shd_eng_round_kernel": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, P(RoundSummary)]),
     "shd_eng_pending_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_resolve": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "shd_eng_round_begin": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p]),
+    "shd_pc_defer_touches": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "shd_pc_query_key": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64]),
+    "shd_pc_take_touches": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
+    "shd_eng_round_retry": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     "shd_eng_end_round": (C.c_int, [C.c_void_p, P(RoundSummary)]),
     "shd_eng_remote_copy": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),
     "shd_eng_take_remote": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]),

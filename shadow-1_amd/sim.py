@@ -128,6 +128,20 @@ class Engine:
         S.check(S.lib().shd_eng_round_kernel(self.ptr, int(ws), int(we), C.byref(r)), "round_kernel")
         return r
 
+    def round_begin(self, ws, we) -> S.RoundSummary:
+        """round_kernel behind a state copy (shd_eng_round_begin)"""
+        r = S.RoundSummary()
+        S.check(S.lib().shd_eng_round_begin(self.ptr, int(ws), int(we), C.byref(r)), "shd_eng_round_begin")
+        return r
+
+    def round_retry(self, recs: np.ndarray) -> S.RoundSummary:
+        """roll back to round_begin's copy, rank `recs`, run the window again"""
+        recs = np.ascontiguousarray(recs, dtype=S.PENDING_DTYPE)
+        r = S.RoundSummary()
+        S.check(S.lib().shd_eng_round_retry(self.ptr, recs.ctypes.data if len(recs) else None, len(recs),
+                                            C.byref(r)), "shd_eng_round_retry")
+        return r
+
     def pending_records(self) -> np.ndarray:
         n = C.c_uint64()
         cap = 4096

@@ -67,6 +67,8 @@ def lib():
         l.o_topo_new.argtypes = [C.c_void_p, P(C.c_int32), C.c_int32, C.c_int32]
         l.o_topo_free.argtypes = [C.c_void_p]
         l.o_topo_get.argtypes = [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double), P(C.c_double)]
+        l.o_topo_would_run.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
+        l.o_topo_touch.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         l.o_topo_count_packet.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         l.o_topo_packet_count.restype = C.c_uint64
         l.o_topo_packet_count.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
@@ -94,6 +96,8 @@ def lib():
         l.o_state_run_serial.argtypes = [C.c_void_p, C.c_uint64]
         l.o_state_inject.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         l.o_state_take_egress.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
+        l.o_state_defer_touches.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
+        l.o_state_take_touches.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
         l.o_state_next_time.restype = C.c_uint64
         l.o_state_next_time.argtypes = [C.c_void_p]
         l.o_state_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, P(C.c_uint64)]
@@ -161,6 +165,12 @@ class OTopo:
 
     def rows_run(self):
         return lib().o_topo_rows_run(self.ptr)
+
+    def would_run(self, s, d) -> bool:
+        return bool(lib().o_topo_would_run(self.ptr, int(s), int(d)))
+
+    def touch(self, s, d):
+        lib().o_topo_touch(self.ptr, int(s), int(d))
 
 
 def engine_run(model: S.ModelArrays, g: S.GraphArrays, force_rows=False, mark=None, path_counts=None,
@@ -234,6 +244,22 @@ class OState:
         out = np.empty(n.value, dtype=S.EVENT_DTYPE)
         assert lib().o_state_take_egress(self.ptr, out.ctypes.data if n.value else None, n.value,
                                          C.byref(n)) == 0
+        return out
+
+    def defer_touches(self, recs):
+        """the other side's first touches of the coming window (one lazy cache
+        across the sides, oracle.h o_state_defer_touches)"""
+        r = np.ascontiguousarray(recs, dtype=S.PENDING_DTYPE)
+        assert lib().o_state_defer_touches(self.ptr, r.ctypes.data if len(r) else None, len(r)) == 0
+
+    def take_touches(self) -> np.ndarray:
+        """this side's first touches of the window just run (the other side's
+        deferred ones applied first)"""
+        n = C.c_uint64()
+        lib().o_state_take_touches(self.ptr, None, 0, C.byref(n))
+        out = np.empty(n.value, dtype=S.PENDING_DTYPE)
+        assert lib().o_state_take_touches(self.ptr, out.ctypes.data if n.value else None, n.value,
+                                          C.byref(n)) == 0
         return out
 
     def next_time(self) -> int:

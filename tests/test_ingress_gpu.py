@@ -13,9 +13,20 @@ the whole serial run).
   loop: CPU-side sends pushed through the policy reach the engine, the
   engine's sends come back as Shadow events popped in their round.
 The union of both sides' traces and end states must equal the whole model's
-serial oracle run bit for bit.  The bundled topology is complete, so a path's
-value does not depend on which side touched it first (on other graphs the two
-sides' first touches within a window are not interleaved: DESIGN.md).
+serial oracle run bit for bit.
+
+One lazy path cache across the sides (topology.c:1969-2051 is one global
+cache): on a graph that is not complete, a pair's value depends on which
+endpoint's row ran first, so the two sides' first touches of a window are put
+in one serial order.  The engine runs its window first (its first touches are
+pending, their deliveries wait); the CPU side gets them (o_state_defer_touches)
+and applies each to its cache just before its first later query, in event
+order; its own first touches come back (o_state_take_touches), and the
+engine's resolution ranks both (shd_eng_resolve over the union).  The grid
+graph below has integer latencies, so distant vertices are joined by many
+shortest paths and each endpoint's Dijkstra takes its own, with its own
+reliability: the orientations of a pair differ, and without the protocol the
+co-simulation diverges from the serial run (checked).
 """
 import ctypes as C
 
@@ -32,28 +43,44 @@ U64_MAX = (1 << 64) - 1
 EINVAL = -22
 
 
-def model(n_hosts=300, seed=3, **kw):
-    g = W.bundled_graph()
+def grid_graph(side=6, seed=5, loss_max=0.05):
+    """side x side grid, every edge (and self loop) 1 ms: equal-latency paths
+    everywhere, edge loss U[0, loss_max]"""
+    rng = np.random.default_rng(seed)
+    src, dst = [], []
+    for y in range(side):
+        for x in range(side):
+            v = y * side + x
+            if x + 1 < side:
+                src.append(v); dst.append(v + 1)
+            if y + 1 < side:
+                src.append(v); dst.append(v + side)
+    V = side * side
+    src += list(range(V))
+    dst += list(range(V))
+    perm = rng.permutation(len(src))
+    src, dst = np.array(src)[perm], np.array(dst)[perm]
+    return S.GraphArrays(V, src, dst, np.ones(len(src)), rng.random(len(src)) * loss_max)
+
+
+def model(n_hosts=300, seed=3, graph="bundled", **kw):
+    g = W.bundled_graph() if graph == "bundled" else grid_graph()
     hv = np.sort(np.random.default_rng(seed).integers(0, g.n_vertices, n_hosts)).astype(np.int32)
     kw.setdefault("load", 8)
     m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, **kw)
     return g, m
 
 
-def check_union(m, g, cut, gtr, gdg, ctr, cdg):
+def union_equal(m, g, cut, gtr, gdg, ctr, cdg):
     otr, odg, _ = O.engine_run(m, g)
     tr = sort_trace(np.concatenate([ctr, gtr]))
-    assert len(tr) == len(otr)
-    assert np.array_equal(tr, sort_trace(otr))
-    assert np.array_equal(cdg[:cut], odg[:cut])
-    assert np.array_equal(gdg, odg[cut:])
+    return (len(tr) == len(otr) and np.array_equal(tr, sort_trace(otr)) and np.array_equal(cdg[:cut], odg[:cut])
+            and np.array_equal(gdg, odg[cut:]))
 
 
-@pytest.mark.parametrize("cut,kw", [(120, {}), (1, {}), (299, {}),
-                                    (70, dict(load=24, payload=1000, bw_down=200, bw_up=100000,
-                                              codelq_cap=256, queue_flags=S.SHD_QF_TRACE_STATUS))])
-def test_engine_exchanges_packets_with_cpu_side_hosts(cut, kw):
-    g, m = model(**kw)
+def cosim(m, g, cut, one_cache=True):
+    """the engine over hosts [cut, H), the oracle over [0, cut), window by
+    window; one_cache: the first touches of both sides in one serial order"""
     H = m.n_hosts
     pc = PathCache(g, W.attached_vertices(m.host_vertex))
     eng = Engine(m, pc, cut, H)
@@ -61,14 +88,30 @@ def test_engine_exchanges_packets_with_cpu_side_hosts(cut, kw):
     cpu = O.OState(m, g, hosts=(0, cut))
     Wn = eng.window
     end = m.params["end_time"]
-    n_in = n_out = rounds = 0
+    n = dict(ingress=0, egress=0, rounds=0, engine_touches=0, cpu_touches=0, retries=0)
     while True:
         ws = min(cpu.next_time(), eng.next_time())
         if ws >= end:
             break
         we = ws + Wn
-        cpu.run_serial(we)
-        eng.run_round(ws, we)
+        if one_cache:
+            r = eng.round_begin(ws, we)                # the engine's window first: its first touches pend
+            pe = eng.pending_records()
+            cpu.defer_touches(pe)                      # applied at their place in the CPU side's order
+            cpu.run_serial(we)
+            pcpu = cpu.take_touches()
+            both = np.concatenate([pe, pcpu])
+            if r.error & S.ERR_AMBIGUOUS:              # a drop decision the ranking decides: run it again
+                assert eng.round_retry(both).error == 0
+                n["retries"] += 1
+            else:
+                eng.resolve(both)                      # one ranking of both sides' first touches
+            eng.end_round()
+            n["engine_touches"] += len(pe)
+            n["cpu_touches"] += len(pcpu)
+        else:
+            cpu.run_serial(we)
+            eng.run_round(ws, we)
         out = eng.take_remote()                    # engine -> CPU side (egress)
         inc = cpu.take_egress()                    # CPU side -> engine (ingress)
         assert np.all(out["time"] >= we) and np.all(out["dst"] < cut) and np.all(out["src"] >= cut)
@@ -76,15 +119,37 @@ def test_engine_exchanges_packets_with_cpu_side_hosts(cut, kw):
         if len(inc):
             eng.push_events(inc)
         cpu.inject(out)
-        n_in += len(inc)
-        n_out += len(out)
-        rounds += 1
-    assert n_in > 50 and n_out > 50 and rounds > 100
-    check_union(m, g, cut, eng.trace(), eng.digest(), cpu.trace(), cpu.digest())
-    if kw:
-        assert np.count_nonzero(eng.trace()["kind"] == S.TR_CODEL_DROP) > 0
+        n["ingress"] += len(inc)
+        n["egress"] += len(out)
+        n["rounds"] += 1
+    res = (eng.trace(), eng.digest(), cpu.trace(), cpu.digest())
     cpu.close()
     eng.close()
+    pc.close()
+    return res, n
+
+
+@pytest.mark.parametrize("graph,cut,kw", [("bundled", 120, {}), ("bundled", 1, {}), ("bundled", 299, {}),
+                                          ("bundled", 70, dict(load=24, payload=1000, bw_down=200, bw_up=100000,
+                                                               codelq_cap=256, queue_flags=S.SHD_QF_TRACE_STATUS)),
+                                          ("grid", 120, {}), ("grid", 1, {}), ("grid", 299, {})])
+def test_engine_exchanges_packets_with_cpu_side_hosts(graph, cut, kw):
+    g, m = model(graph=graph, **kw)
+    (gtr, gdg, ctr, cdg), n = cosim(m, g, cut)
+    assert n["ingress"] > 50 and n["egress"] > 50 and n["rounds"] > 100
+    if graph == "grid":   # both sides touch first, on a graph where it matters
+        assert n["engine_touches"] > 0 and n["cpu_touches"] > 0
+    assert union_equal(m, g, cut, gtr, gdg, ctr, cdg)
+    if kw:
+        assert np.count_nonzero(gtr["kind"] == S.TR_CODEL_DROP) > 0
+
+
+def test_grid_orientations_matter_without_one_cache():
+    """the grid model is one where the first-touch order decides values: the
+    two sides' first touches left unordered, the union is not the serial run"""
+    g, m = model(graph="grid")
+    (gtr, gdg, ctr, cdg), _ = cosim(m, g, 120, one_cache=False)
+    assert not union_equal(m, g, 120, gtr, gdg, ctr, cdg)
 
 
 def test_push_events_validates_packet_ingress():
@@ -117,13 +182,17 @@ def test_push_events_validates_packet_ingress():
 # ---- through the scheduler policy (sched_policy_shd.c) ----
 ING = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.POINTER(S.Event))
 EGR = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.POINTER(S.Event))
+TIN = C.CFUNCTYPE(None, C.c_void_p, C.c_void_p, C.c_uint64)
+TOUT = C.CFUNCTYPE(C.c_uint64, C.c_void_p, C.POINTER(C.c_void_p))
 
 
 class Bridge(C.Structure):
-    _fields_ = [("ingress", ING), ("egress", EGR), ("user", C.c_void_p)]
+    _fields_ = [("ingress", ING), ("egress", EGR), ("user", C.c_void_p), ("touches_in", TIN),
+                ("touches_out", TOUT)]
 
 
-def test_bridged_policy_exchanges_packets_in_shadows_round_loop():
+@pytest.mark.parametrize("graph,one_cache", [("bundled", False), ("grid", True)])
+def test_bridged_policy_exchanges_packets_in_shadows_round_loop(graph, one_cache):
     import test_boundary_gpu as B
     h, t = B.libs()
     for f, res, args in (("harness_packet_event_new", C.c_void_p,
@@ -137,7 +206,7 @@ def test_bridged_policy_exchanges_packets_in_shadows_round_loop():
     t.schedulerpolicygpurounds_new_bridged.restype = C.c_void_p
     t.schedulerpolicygpurounds_new_bridged.argtypes = [C.c_void_p, C.POINTER(Bridge)]
 
-    g, m = model(seed=9)
+    g, m = model(seed=9, graph=graph)
     H, cut = m.n_hosts, 140
     pc = PathCache(g, W.attached_vertices(m.host_vertex))
     eng = Engine(m, pc, cut, H)
@@ -160,7 +229,22 @@ def test_bridged_policy_exchanges_packets_in_shadows_round_loop():
         counts["egress"] += 1
         return h.harness_packet_event_new(e.time, e.src, e.dst, e.seq, e.pkt)
 
-    br = Bridge(ING(ingress), EGR(egress), None)
+    keep = {}
+
+    def touches_in(user, recs, n):   # the engine's first touches of the round -> the CPU side's cache
+        counts["engine_touches"] += n
+        cpu.defer_touches(np.ctypeslib.as_array(C.cast(recs, C.POINTER(C.c_uint8)), shape=(n * 56,))
+                          .view(S.PENDING_DTYPE).copy() if n else np.zeros(0, S.PENDING_DTYPE))
+
+    def touches_out(user, out):      # the CPU side's own, after the round's CPU events
+        keep["t"] = cpu.take_touches()
+        counts["cpu_touches"] += len(keep["t"])
+        out[0] = keep["t"].ctypes.data if len(keep["t"]) else None
+        return len(keep["t"])
+
+    counts.update(engine_touches=0, cpu_touches=0)
+    br = Bridge(ING(ingress), EGR(egress), None, TIN(touches_in) if one_cache else TIN(),
+                TOUT(touches_out) if one_cache else TOUT())
     pp = t.schedulerpolicygpurounds_new_bridged(eng.ptr.value, C.byref(br))
     assert pp
     pol = C.cast(pp, C.POINTER(B.Policy)).contents
@@ -189,7 +273,9 @@ def test_bridged_policy_exchanges_packets_in_shadows_round_loop():
         nxt = min(pol.getNextTime(pp), cpu.next_time())
     assert counts["ingress"] > 50 and counts["egress"] > 50 and counts["kept"] == 0
     assert rounds > 100
-    check_union(m, g, cut, eng.trace(), eng.digest(), cpu.trace(), cpu.digest())
+    if one_cache:
+        assert counts["engine_touches"] > 0 and counts["cpu_touches"] > 0
+    assert union_equal(m, g, cut, eng.trace(), eng.digest(), cpu.trace(), cpu.digest())
     pol.free(pp)
     cpu.close()
     eng.close()
