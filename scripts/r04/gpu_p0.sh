@@ -21,3 +21,18 @@ for v in A B; do
 done
 SHDGPU_LIB=shadow-1_amd/libshdgpu_tim.so timeout -k 10 200 python3 scripts/ps_timing.py > $O/timing_c3.txt 2>&1 || { tail -5 $O/timing_c3.txt; exit 4; }
 cat $O/timing_c3.txt
+# APSP: Gauss-Seidel sweeps (libshdgpu_pcvgs.so, -DSHD_SSSP_GS) against the product; parity of the variant
+for lib in libshdgpu.so libshdgpu_pcvgs.so; do
+  SHDGPU_LIB=shadow-1_amd/$lib timeout -k 10 120 python -u scripts/apsp_timing.py > $O/apsp_$lib.json 2> $O/apsp_$lib.err || { tail $O/apsp_$lib.err; exit 5; }
+  python3 -c "import json;d=json.load(open('$O/apsp_$lib.json'));print('$lib', {k:(v['ms'],v.get('sssp_ms'),v.get('iters')) for k,v in d.items()})"
+done
+SHDGPU_LIB=shadow-1_amd/libshdgpu_pcvgs.so timeout -k 10 300 python -u -m pytest tests/test_pathcache_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/pc_gs.log 2>&1; echo "pathcache gs rc=$?"; tail -3 $O/pc_gs.log
+# TCP: the mailbox part counters of round 3's 881351e (libshdgpu_tcpv.so, -DSHD_TCP_PARTS) against the
+# product, 65 536 hosts; per-dispatch k_tcp_round durations from a kernel trace of each
+timeout -k 10 300 python -u -m pytest tests/test_tcp_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tcp_tests.log 2>&1; echo "tcp tests rc=$?"; tail -2 $O/tcp_tests.log
+SHDGPU_LIB=shadow-1_amd/libshdgpu_tcpv.so timeout -k 10 300 python -u -m pytest tests/test_tcp_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/tcpv_tests.log 2>&1; echo "tcpv tests rc=$?"; tail -2 $O/tcpv_tests.log
+for v in A B; do
+  if [ $v = B ]; then L=shadow-1_amd/libshdgpu_tcpv.so; else L=shadow-1_amd/libshdgpu.so; fi
+  SHDGPU_LIB=$L timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/prof_tcp_$v -o tcp -- python3 bench.py --workload tcp --steps 1 --warmup 0 --no-cpu-baseline > $O/tcp_$v.json 2> $O/tcp_$v.err || { tail -5 $O/tcp_$v.err; exit 6; }
+  python3 -c "import json; d=json.loads(open('$O/tcp_$v.json').read().strip().splitlines()[-1]); print('tcp $v', round(d['value']/1e6,2), d.get('wall_inclusive'))"
+done

@@ -370,14 +370,19 @@ struct ProfAcc {
 #endif
 
 // --------------------------------------------------------------- RNG
+// glibc rand_r: three steps of x <- a x + c (mod 2^32), 11 + 10 + 10 bits of
+// their states.  The three states are taken from x directly (x_k = a^k x +
+// c (a^(k-1) + ... + 1)): three independent multiplies instead of a chain
+// of three, the same values
+constexpr uint32_t kLcgA = 1103515245u, kLcgC = 12345u;
+constexpr uint32_t kLcgA2 = kLcgA * kLcgA, kLcgC2 = kLcgA * kLcgC + kLcgC;
+constexpr uint32_t kLcgA3 = kLcgA * kLcgA2, kLcgC3 = kLcgA * kLcgC2 + kLcgC;
 __device__ __forceinline__ int32_t rand_r_dev(uint32_t& x) {
-    uint32_t r;
-    x = x * 1103515245u + 12345u;
-    r = (x >> 16) & 2047u;
-    x = x * 1103515245u + 12345u;
-    r = (r << 10) ^ ((x >> 16) & 1023u);
-    x = x * 1103515245u + 12345u;
-    r = (r << 10) ^ ((x >> 16) & 1023u);
+    const uint32_t x1 = x * kLcgA + kLcgC, x2 = x * kLcgA2 + kLcgC2, x3 = x * kLcgA3 + kLcgC3;
+    uint32_t r = (x1 >> 16) & 2047u;
+    r = (r << 10) ^ ((x2 >> 16) & 1023u);
+    r = (r << 10) ^ ((x3 >> 16) & 1023u);
+    x = x3;
     return (int32_t)r;
 }
 

@@ -125,7 +125,12 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         SST_T0(t_it)
         for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
             const int32_t v = c0 + lane;
+#ifdef SHD_SSSP_GS   // A/B: a vertex improved earlier in this sweep relaxes now too (and again next sweep)
+            const uint16_t uv = v < V ? upd[v] : 0xFFFF;
+            const bool fr = v < V && (uv == stamp || uv == (uint16_t)(stamp + 1));
+#else
             const bool fr = v < V && upd[v] == stamp;
+#endif
             uint64_t mask = __ballot(fr);
             if (!mask) continue;
             SST_T0(t_rx)

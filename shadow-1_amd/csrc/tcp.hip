@@ -66,6 +66,14 @@ constexpr uint32_t kCq = 4096;      // CoDel queue per host
 constexpr uint32_t kTr = 1u << 16;  // trace records per host
 constexpr uint32_t kTrSack = 1u << 20;
 constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 16 per host)
+#ifndef SHD_TCP_ONE_COUNTER   // (round 3's 881351e, measured in round 4: profiles/r04/tcp) a mailbox in 64
+                              // parts with a fill counter each (host h claims in part h % 64, 32 slots per
+                              // host), and each lane folds the earliest delivery it sent into its own next
+                              // time instead of one contended atomicMin; SHD_TCP_ONE_COUNTER: one counter
+constexpr uint32_t kMailSub = 64;
+#else
+constexpr uint32_t kMailSub = 1;
+#endif
 constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
 
 // ProtocolTCPFlags (protocol.h:23-31)
@@ -242,6 +250,7 @@ struct L {
     // the index of the next path query within it (first-query log)
     uint32_t ksrc, kq;
     uint64_t kseq;
+    uint64_t mail_min;      // the earliest delivery this lane sent this round (part counters)
 };
 __device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * c.g->pool_cap + i]; }
 __device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
@@ -1439,15 +1448,26 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
         const uint64_t seq = c.H->ev_seq++;   // event_new_ (the delivery's ID)
         if (t >= c.g->end_time) return;
         if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
+#ifndef SHD_TCP_ONE_COUNTER
+        const uint32_t part = (uint32_t)c.h % kMailSub, per = c.g->mail_cap / kMailSub;
+        const uint32_t kk = atomicAdd(c.g->n_out + part, 1u);
+        if (kk >= per) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+        const uint32_t slot = part * per + kk;
+#else
         const uint32_t slot = atomicAdd(c.g->n_out, 1u);
         if (slot >= c.g->mail_cap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+#endif
         Mail* m = &c.g->mail_out[slot];
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
         m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
         m->pkt.inq = 0;   // the copy is in no queue of the receiver
         c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
+#ifndef SHD_TCP_ONE_COUNTER
+        if (t < c.mail_min) c.mail_min = t;   // folded into next_time[h] at the round's end
+#else
         atomicMin((unsigned long long*)&c.g->next_time[c.g->H], (unsigned long long)t);
+#endif
     } else {
         pkt_status(c, pi, S_INET_DROPPED);
     }
@@ -1831,7 +1851,7 @@ __global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
     if (h >= g.H) return;
     Glob gl = g;
-    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0};
+    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
     sched_task(c, gl.hb, K_HEARTBEAT, -1);
     refill_cb(c);
     sched_task(c, kMs, K_REFILL_LO, -1);
@@ -1853,6 +1873,13 @@ __global__ void k_tcp_window(Glob g) {
     __shared__ uint64_t red[16];
     TCtl* ctl = g.ctl;
     if (ctl->halted) return;
+#ifndef SHD_TCP_ONE_COUNTER
+    {   // the next round's output mailbox starts empty (read before thread 0 moves rounds on)
+        const uint64_t k = ctl->rounds;
+        if (threadIdx.x < kMailSub) g.nmail[((k + 1) & 1) * kMailSub + threadIdx.x] = 0;
+    }
+    __syncthreads();
+#endif
     uint64_t t = ~0ull;
     for (int32_t i = (int32_t)threadIdx.x; i <= g.H; i += (int32_t)blockDim.x) {
         const uint64_t x = g.next_time[i];
@@ -1872,7 +1899,9 @@ __global__ void k_tcp_window(Glob g) {
             const uint64_t k = ctl->rounds;
             ctl->wend = t + g.W;
             ctl->rounds = k + 1;
+#ifdef SHD_TCP_ONE_COUNTER
             g.nmail[(k + 1) & 1] = 0;     // round k's output mailbox starts empty
+#endif
             g.next_time[g.H] = ~0ull;     // ... and so does its earliest delivery
         }
     }
@@ -1892,12 +1921,12 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
         gl = g;
         gl.mail_in = g.mail + (size_t)in * g.mail_cap; gl.mhead_in = g.mhead + (size_t)in * g.H;
         gl.mnext_in = g.mnext + (size_t)in * g.mail_cap;
-        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + out;
+        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + (size_t)out * kMailSub;
         gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * g.mail_cap;
     }
     __syncthreads();
     if (h >= g.H) return;
-    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0};
+    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
     // this host's deliveries (any order: the heap's key (time, src, seq) is unique)
     int32_t s = gl.mhead_in[h];
     gl.mhead_in[h] = -1;   // the list is empty again when this mailbox is next written
@@ -1923,6 +1952,9 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
     c.H->events += nev;
     // a host that stopped on an error leaves the run (the caller sees the bit)
     gl.next_time[h] = (c.H->nev && !c.H->err) ? gl.ev[(size_t)h * kEv].time : ~0ull;
+#ifndef SHD_TCP_ONE_COUNTER
+    if (c.mail_min < gl.next_time[h]) gl.next_time[h] = c.mail_min;   // its deliveries count either way
+#endif
 }
 
 #define HCHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "shd_tcp: %s: %s\n", #x, hipGetErrorString(e_)); rc = -5; goto done; } } while (0)
@@ -2099,10 +2131,11 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipGetLastError());
     HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
-    g.mail_cap = (uint32_t)H * 16u > kMailMin ? (uint32_t)H * 16u : kMailMin;
+    g.mail_cap = (uint32_t)H * 16u * (kMailSub > 1 ? 2u : 1u) > kMailMin ? (uint32_t)H * 16u * (kMailSub > 1 ? 2u : 1u)
+                                                                          : kMailMin;
     HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
-    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2));
-    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2));
+    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2 * kMailSub));
+    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * kMailSub));
     HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));

@@ -9,8 +9,8 @@ queries in ONE serial order (event_compare's key); the product cache gets the
 engine's touches of each window up front and the CPU side's queries one event
 at a time.  The CPU side's values must be the oracle's bit for bit, and the
 first touches it reports must be exactly the queries that ran a row in the
-oracle.  The grid graph (tests/test_ingress_gpu.py) is one where which
-endpoint ranks first decides a pair's value.
+oracle.  On the directed graph (tests/test_ingress_gpu.py) which endpoint
+ranks first decides a pair's value.
 """
 import ctypes as C
 
@@ -21,7 +21,7 @@ import oracle_ffi as O
 import shdgpu as S
 import workloads as W
 from sim import PathCache
-from test_ingress_gpu import grid_graph
+from test_ingress_gpu import directed_graph
 
 pytestmark = pytest.mark.gpu
 
@@ -43,7 +43,7 @@ def _records(rng, n, t0, hosts, T):
 
 @pytest.mark.parametrize("seed", [11, 12])
 def test_pc_touch_protocol_is_one_serial_cache(seed):
-    g = grid_graph()
+    g = directed_graph()
     rng = np.random.default_rng(seed)
     hv = np.sort(rng.integers(0, g.n_vertices, 40)).astype(np.int32)
     att = W.attached_vertices(hv)
