@@ -583,6 +583,13 @@ int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, c
  * from the cumulative interface counters snapshots[2k] (in), [2k+1] (out). */
 int shd_node_lines(const uint32_t* snapshots, uint64_t k, uint64_t interval_ns, uint32_t payload, uint32_t host,
                    shd_lines** out);
+/* The same lines from full tracker counters of each interval, [k][20]: the
+ * ten remote inbound counters then the ten remote outbound ones, in the
+ * counter string's order without its two totals (shdtcp.h's node_counters:
+ * control / data packets, first sent and retransmitted, and their header and
+ * payload bytes); the localhost counters are zero */
+int shd_tracker_node_lines(const uint64_t* counters, uint64_t k, uint64_t interval_ns, uint32_t host,
+                           shd_lines** out);
 /* The same from an engine: the [STATUS] lines of its whole trace (the model's
  * payload; ips / host_ids over all H hosts), and local host l's [node] lines
  * (its own heartbeat interval; heartbeats before end_time). */

@@ -48,6 +48,8 @@ typedef struct shd_tcp_model {
     uint32_t tcp_window;              /* --tcp-windows (options.c:79)                    */
     uint32_t packets_per_host;        /* packet pool per host (0: 8192); more live packets
                                          set SHD_TCP_ERR_POOL                             */
+    uint32_t qdisc;                   /* --interface-qdisc (options.c:162): 0 fifo, 1 rr
+                                         (network_interface.c:466-517)                    */
 } shd_tcp_model;
 
 /* the first path query a host made of a vertex pair (topology_isRoutable /
@@ -77,7 +79,21 @@ typedef struct shd_tcp_result {
                                          delivery events executed)                           */
     shd_tcp_query* queries;           /* each host's first query of each vertex pair      */
     uint64_t n_queries;
+    /* with SHD_TCP_TRACE_NODE: the tracker's node counters of every heartbeat
+     * interval (tracker.c:183-214, 566-611), [H][node_k][20]: inbound remote
+     * then outbound remote, each packets-control, bytes-control-header,
+     * packets-control-retrans, bytes-control-header-retrans, packets-data,
+     * bytes-data-header, bytes-data-payload, packets-data-retrans,
+     * bytes-data-header-retrans, bytes-data-payload-retrans (no TCP loopback:
+     * the localhost counters are zero); n_heartbeats[h] of them are host h's.
+     * shd_tracker_node_lines (shdgpu.h) makes the [node] lines of a host. */
+    uint64_t* node_counters;
+    uint32_t* n_heartbeats;
+    uint32_t node_k, _pad2;
 } shd_tcp_result;
+
+/* shd_tcp_run's `trace` bits */
+enum { SHD_TCP_TRACE_STATUS = 1, SHD_TCP_TRACE_NODE = 2 };
 
 enum {
     SHD_TCP_ERR_EVQ = 1, SHD_TCP_ERR_POOL = 2, SHD_TCP_ERR_QUEUE = 4, SHD_TCP_ERR_SOCKETS = 8,
@@ -85,8 +101,9 @@ enum {
     SHD_TCP_ERR_QLOG = 256
 };
 
-/* Run the model to end_time on the current HIP device.  trace != 0 writes the
- * [STATUS] lines (packet.c:647-659).  Returns 0 or a negative errno-style code:
+/* Run the model to end_time on the current HIP device.  trace & 1 writes the
+ * [STATUS] lines (packet.c:647-659); trace & 2 keeps the tracker's node
+ * counters per heartbeat (the [node] lines, tracker.c:419-465).  Returns 0 or a negative errno-style code:
  * -22 an invalid model, -113 a client whose server has no route in either
  * direction (the reference's connect fails with ECONNREFUSED there,
  * host.c:1224-1234; the device application has no such branch), -12 no device

@@ -265,6 +265,7 @@ struct o_topo {
      * NaN latency where computePathProperties fails; [V] pointers or NULL */
     double** row_lat;
     double** row_rel;
+    uint8_t* ran;   /* [V] a source row of this vertex has run */
 };
 
 static uint64_t hkey(int32_t s, int32_t d) { return ((uint64_t)(uint32_t)s << 32) | (uint32_t)d; }
@@ -309,9 +310,10 @@ o_topo* o_topo_new(const o_graph* g, const int32_t* attached, int32_t n_attached
     t->targets = malloc(sizeof(int32_t) * (n_attached + 1));
     memcpy(t->targets, attached, sizeof(int32_t) * n_attached);
     t->cap = 1024; t->tab = calloc(t->cap, sizeof(slot_t));
+    t->ran = calloc(g->V > 0 ? g->V : 1, 1);
     return t;
 }
-void o_topo_free(o_topo* t) { if (!t) return; free(t->targets); free(t->tab); free(t); }
+void o_topo_free(o_topo* t) { if (!t) return; free(t->targets); free(t->tab); free(t->ran); free(t); }
 
 static slot_t* from_cache(o_topo* t, int32_t s, int32_t d) { return tab_find(t, s, d); }
 
@@ -343,6 +345,7 @@ static int compute_source_paths(o_topo* t, int32_t s, int32_t d) {
         o_sssp_row(t->g, s, t->targets, t->nt, lat, rel, ok, NULL, NULL);
     }
     t->rows_run++;
+    t->ran[s] = 1;
     int all = 1;
     for (int32_t j = 0; j < t->nt; j++) {
         if (ok[j]) store(t, 0, s, t->targets[j], lat[j], rel[j]);
@@ -416,6 +419,9 @@ int o_topo_would_run(const o_topo* t, int32_t s, int32_t d) {
     if (tab_find((o_topo*)t, s, d)) return 0;
     if (!t->g->directed && tab_find((o_topo*)t, d, s)) return 0;
     if (t->props.is_complete || (t->g->prefer_direct && o_get_eid(t->g, s, d) >= 0)) return 0;
+    /* a directed rerun of a row that ran already (its reverse entry was stored
+     * first, topology.c:1987-1990) stores nothing new: not a first touch */
+    if (s != d && t->ran[s]) return 0;
     return 1;
 }
 void o_topo_touch(o_topo* t, int32_t s, int32_t d) { (void)get_path_entry(t, s, d); }
@@ -423,6 +429,8 @@ void o_topo_touch(o_topo* t, int32_t s, int32_t d) { (void)get_path_entry(t, s, 
 o_topo* o_topo_clone(const o_topo* t) {
     o_topo* c = malloc(sizeof(*c));
     *c = *t;
+    c->ran = malloc(t->g->V > 0 ? t->g->V : 1);
+    memcpy(c->ran, t->ran, t->g->V > 0 ? t->g->V : 1);
     c->targets = malloc(sizeof(int32_t) * (t->nt + 1));
     memcpy(c->targets, t->targets, sizeof(int32_t) * t->nt);
     c->tab = malloc(sizeof(slot_t) * t->cap);

@@ -371,6 +371,7 @@ typedef struct ohost_t {
     uint64_t rx_rem, rx_cap, rx_refill, tx_rem, tx_cap, tx_refill;
     int refill_pending;
     opq fifo;                            /* sockets wanting to send (network_interface.c:87-91) */
+    osock** rr; uint32_t rr_head, rr_n, rr_cap;   /* the same for the RR qdisc: a FIFO of sockets (rrQueue) */
     o_codel codel;
     int32_t next_handle;
 } ohost_t;
@@ -590,6 +591,28 @@ static opkt* sock_remove_input(osock* k) {   /* socket.c:345-372 */
     }
     return p;
 }
+/* the RR qdisc's GQueue of sockets (network_interface.c:58, 466-490, 586-591) */
+static void rr_push(ohost_t* H, osock* k) {
+    if (H->rr_n == H->rr_cap) {
+        const uint32_t nc = H->rr_cap ? 2 * H->rr_cap : 8;
+        osock** a = malloc(sizeof(osock*) * nc);
+        for (uint32_t i = 0; i < H->rr_n; i++) a[i] = H->rr[(H->rr_head + i) % H->rr_cap];
+        free(H->rr);
+        H->rr = a; H->rr_head = 0; H->rr_cap = nc;
+    }
+    H->rr[(H->rr_head + H->rr_n++) % H->rr_cap] = k;
+}
+static void rr_push_once(ohost_t* H, osock* k) {   /* g_queue_find, then push_tail */
+    for (uint32_t i = 0; i < H->rr_n; i++)
+        if (H->rr[(H->rr_head + i) % H->rr_cap] == k) return;
+    rr_push(H, k);
+}
+static osock* rr_pop(ohost_t* H) {
+    osock* k = H->rr[H->rr_head];
+    H->rr_head = (H->rr_head + 1) % H->rr_cap;
+    H->rr_n--;
+    return k;
+}
 static int sock_add_output(osock* k, opkt* p) {   /* socket_addToOutputBuffer (socket.c:385-424) */
     if (p->len > out_space(k)) return 0;
     if (p->prio == 0.0) fq_push(&k->outctl, p); else fq_push(&k->out, p);
@@ -597,7 +620,8 @@ static int sock_add_output(osock* k, opkt* p) {   /* socket_addToOutputBuffer (s
     pkt_status(p, S_SND_SOCKET_BUFFERED);
     if (space_out_incl_tcp(k) <= 0) sock_status(k, DS_WRITABLE, 0);
     /* networkinterface_wantsSend (network_interface.c:581-605): tracked once */
-    if (pq_index(&G->h[k->host].fifo, k) < 0) pq_push(&G->h[k->host].fifo, k);
+    if (G->cfg->qdisc_rr) rr_push_once(&G->h[k->host], k);
+    else if (pq_index(&G->h[k->host].fifo, k) < 0) pq_push(&G->h[k->host].fifo, k);
     if_send_packets(k->host);
     return 1;
 }
@@ -1339,10 +1363,18 @@ static void worker_send_packet(int32_t h, opkt* p) {   /* worker.c:260-321 */
         pkt_status(p, S_INET_DROPPED);
     }
 }
-static void if_send_packets(int32_t h) {   /* network_interface.c:519-579, FIFO qdisc */
+static void if_send_packets(int32_t h) {   /* network_interface.c:519-579 */
     ohost_t* H = &G->h[h];
     while (H->tx_rem >= MTU) {
         opkt* p = NULL;
+        if (G->cfg->qdisc_rr) {
+            while (!p && H->rr_n) {   /* _networkinterface_selectRoundRobin (:466-490) */
+                osock* k = rr_pop(H);
+                p = sock_remove_output(k);
+                if (p) tcp_about_to_send(k, p);
+                if (sock_peek_out(k)) rr_push(H, k);
+            }
+        }
         while (!p && H->fifo.n) {   /* _networkinterface_selectFirstInFirstOut (:492-517) */
             osock* k = pq_pop(&H->fifo);
             p = sock_remove_output(k);
@@ -1798,7 +1830,7 @@ int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out) {
         free(k->rtx.tally.marked.r); free(k->rtx.tally.sacked.r); free(k->rtx.tally.retx.r);
         free(k->rtx.tally.lost.r); free(k->rtx.tally.tmp.r);
     }
-    for (int32_t i = 0; i < H; i++) free(t.h[i].fifo.a);
+    for (int32_t i = 0; i < H; i++) { free(t.h[i].fifo.a); free(t.h[i].rr); }
     free(t.s); free(t.p); free(t.h); free(t.q); free(t.pool);
     G = NULL;
     return 0;

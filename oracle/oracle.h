@@ -223,7 +223,8 @@ typedef struct o_tcp_cfg {
     const int32_t* proc_peer;         /* [P] -1 server, else the server process */
     uint64_t end_time, heartbeat_interval;
     uint32_t tcp_bytes, recv_buf, send_buf, tcp_window;
-    uint32_t no_lines, _pad;          /* 1: keep the statuses, write no lines (bench.py's CPU baseline) */
+    uint32_t no_lines;                /* 1: keep the statuses, write no lines (bench.py's CPU baseline) */
+    uint32_t qdisc_rr;                /* 1: the round-robin qdisc (network_interface.c:466-490) */
 } o_tcp_cfg;
 typedef struct o_tcp_out {
     char* lines; size_t len; uint64_t n_lines;

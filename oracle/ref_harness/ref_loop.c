@@ -102,7 +102,10 @@ typedef struct ref_loop_cfg {
     /* 1: the default log level's work only -- debug records filtered (the
      * [STATUS] lines are not even formatted) and no line kept: for timing the
      * reference's loop (scripts/r04/ref_loop_timing.py) */
-    int32_t quiet, _pad4;
+    int32_t quiet;
+    /* 1: --interface-qdisc=rr (options.c:162; round-robin over the sockets
+     * that want to send, network_interface.c:466-490) instead of fifo */
+    int32_t qdisc_rr;
 } ref_loop_cfg;
 
 typedef struct ref_loop_out {
@@ -636,7 +639,8 @@ int ref_loop_run(const ref_loop_cfg* cfg, ref_loop_out* out) {
 
     /* the CLI defaults (options.c:60-240) with one config file argument */
     gchar* argv[] = {"shadow", "shadow.config.xml", NULL};
-    g_options = options_new(2, argv);
+    gchar* argv_rr[] = {"shadow", "--interface-qdisc=rr", "shadow.config.xml", NULL};
+    g_options = cfg->qdisc_rr ? options_new(3, argv_rr) : options_new(2, argv);
     if (!g_options) return -2;
     g_dns = dns_new();
     Scheduler* sched = scheduler_new(SP_SERIAL_GLOBAL, 0, &g_slave, 1, cfg->end_time);

@@ -75,6 +75,8 @@ constexpr uint32_t kMailSub = 64;
 constexpr uint32_t kMailSub = 1;
 #endif
 constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
+constexpr uint32_t kTrk = 10;       // tracker counters per direction (DHost::trk)
+constexpr uint32_t kXRetx = 1;      // DPkt::xflags: the packet was retransmitted (PDS_SND_TCP_RETRANSMITTED)
 
 // ProtocolTCPFlags (protocol.h:23-31)
 enum : uint32_t { F_RST = 1 << 1, F_SYN = 1 << 2, F_ACK = 1 << 3, F_SACK = 1 << 4, F_FIN = 1 << 5, F_DUPACK = 1 << 6 };
@@ -116,7 +118,7 @@ struct DPkt {
     uint64_t tsval, tsecho;
     double prio;
     uint32_t nsack, nst;
-    uint32_t inq, _pad;     // Q_THROTTLED / Q_UNORDERED: in its socket's heap (the reference's
+    uint32_t inq, xflags;   // Q_THROTTLED / Q_UNORDERED: in its socket's heap (the reference's
                             // priority_queue membership lookup, O(1) instead of a scan)
     uint8_t st[kSt];
     int32_t sacks[kPktSack];
@@ -190,13 +192,22 @@ struct DHost {
     uint64_t bw_down, bw_up;   // configured KiB/s (worker_getNodeBandwidth{Down,Up})
     int32_t refill_pending, nsock, next_handle;
     IHeap<2 * kSock> fifo;
+    Ring<2 * kSock> rrq;    // the RR qdisc's sockets wanting to send (rrQueue, network_interface.c:58)
     // CoDel (router_queue_codel.c)
     uint32_t cq_head, cq_n; uint64_t cq_total, cq_iexp, cq_next_drop; uint32_t cq_dc, cq_dc_last; int32_t cq_mode;
     uint32_t nfree, ntr, ntrs, nev;
     // the vertex pairs this host has queried (unordered, (min << 32) | max):
     // its first query of each goes to the run's first-query log (touch_log)
-    uint32_t npq, _pq_pad;
+    uint32_t npq, nhb;
     uint64_t pq[kPq];
+    // the tracker's interface counters of the running heartbeat interval
+    // (tracker.c:183-214; remote only: no TCP loopback here), inbound then
+    // outbound, each in the counter string's order (tracker.c:391-417 without
+    // the two totals): packets-control, bytes-control-header,
+    // packets-control-retrans, bytes-control-header-retrans, packets-data,
+    // bytes-data-header, bytes-data-payload, packets-data-retrans,
+    // bytes-data-header-retrans, bytes-data-payload-retrans
+    uint64_t trk[2 * kTrk];
 };
 struct CqEnt { uint64_t ts; uint32_t len; int32_t pkt; };
 
@@ -237,6 +248,8 @@ struct Glob {
     shd_tcp_query* qlog;    // [qlog_cap] each host's first query of each vertex pair (touch_log)
     uint32_t* nqlog;
     uint32_t qlog_cap, _pad3;
+    uint64_t* node;         // [H][node_k][2 * kTrk] tracker counters per heartbeat, or null
+    uint32_t node_k, qdisc_rr;
 };
 
 // ------------------------------------------------------------ per-lane context
@@ -396,6 +409,7 @@ __device__ bool sched_task(L& c, uint64_t delay, uint32_t kind, int32_t obj) {
 __device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDeliveryStatus (packet.c:647-659)
     DPkt* p = PK(c, pi);
     DHost* H = c.H;
+    if (st == S_SND_TCP_RETRANSMITTED) p->xflags |= kXRetx;   // packet_getDeliveryStatus's OR of every status
     if (p->nst < kSt) p->st[p->nst++] = st;
     else if (c.g->trace) H->err |= SHD_TCP_ERR_TRACE;   // a line would lose statuses: fail, never truncate
     if (!c.g->trace) return;
@@ -523,7 +537,14 @@ __device__ bool sock_add_output(L& c, DSock* k, int32_t pi) {   // socket.c:385-
     pkt_status(c, pi, S_SND_SOCKET_BUFFERED);
     if (space_out_incl_tcp(k) <= 0) sock_status(c, k, DS_WRITABLE, false);
     // networkinterface_wantsSend (network_interface.c:581-605): tracked once
-    if (ih_find(c.H->fifo, sidx(c, k)) < 0) ih_push(c.H->fifo, sidx(c, k), SockLess{&c}, c.H->err);
+    if (c.g->qdisc_rr) {
+        bool found = false;   // g_queue_find
+        for (uint32_t i = 0; i < c.H->rrq.n; i++)
+            found |= c.H->rrq.a[(c.H->rrq.head + i) % (2 * kSock)] == sidx(c, k);
+        if (!found) rg_push(c.H->rrq, sidx(c, k), c.H->err);
+    } else if (ih_find(c.H->fifo, sidx(c, k)) < 0) {
+        ih_push(c.H->fifo, sidx(c, k), SockLess{&c}, c.H->err);
+    }
     if_send_packets(c);
     return true;
 }
@@ -1415,6 +1436,22 @@ __device__ bool cq_dequeue(L& c, CqEnt& out) {
     out = e;
     return true;
 }
+// tracker_addInputBytes / tracker_addOutputBytes (tracker.c:216-276), the
+// node counters only (LOG_INFO_FLAGS_NODE); dir 0 in, 1 out
+__device__ void tracker_add(L& c, int32_t pi, int dir) {
+    if (!c.g->node) return;
+    const DPkt* p = PK(c, pi);
+    uint64_t* t = c.H->trk + kTrk * dir;
+    const uint64_t hdr = kHdr, pay = p->len;
+    const bool rx = (p->xflags & kXRetx) != 0;
+    if (pay > 0) {
+        if (rx) { t[7]++; t[8] += hdr; t[9] += pay; }
+        else { t[4]++; t[5] += hdr; t[6] += pay; }
+    } else {
+        if (rx) { t[2]++; t[3] += hdr; }
+        else { t[0]++; t[1] += hdr; }
+    }
+}
 __device__ void if_receive_packets(L& c) {   // :421-455
     DHost* H = c.H;
     while (H->rx_rem >= kMTU) {
@@ -1431,6 +1468,7 @@ __device__ void if_receive_packets(L& c) {   // :421-455
         } else {
             pkt_status(c, e.pkt, S_RCV_INTERFACE_DROPPED);
         }
+        tracker_add(c, e.pkt, 0);   // :415
         pkt_unref(c, e.pkt);
         consume(H->rx_rem, len);
         refill_if_needed(c);
@@ -1477,6 +1515,13 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
     const SockLess lt{&c};
     while (H->tx_rem >= kMTU) {
         int32_t pi = -1;
+        while (c.g->qdisc_rr && pi < 0 && H->rrq.n) {   // _networkinterface_selectRoundRobin (:466-490)
+            const int32_t si = rg_pop(H->rrq);
+            DSock* k = &c.g->sock[si];
+            pi = sock_remove_output(c, k);
+            if (pi >= 0) tcp_about_to_send(c, k, pi);
+            if (sock_peek_out(c, k) >= 0) rg_push(H->rrq, si, H->err);
+        }
         while (pi < 0 && H->fifo.n) {   // _networkinterface_selectFirstInFirstOut (:492-517)
             const int32_t si = ih_pop(H->fifo, lt);
             DSock* k = &c.g->sock[si];
@@ -1489,6 +1534,7 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
         worker_send_packet(c, pi);
         consume(H->tx_rem, (uint64_t)PK(c, pi)->len + kHdr);
         refill_if_needed(c);
+        tracker_add(c, pi, 1);   // :571
         pkt_unref(c, pi);
     }
 }
@@ -1759,7 +1805,20 @@ __device__ void app_run(L& c, DProc* pr) {
 // ------------------------------------------------------------ events
 __device__ void execute(L& c, const DEv& e) {
     switch (e.kind) {
-    case K_HEARTBEAT: sched_task(c, c.g->hb, K_HEARTBEAT, -1); break;   // tracker.c:607-610
+    case K_HEARTBEAT:   // tracker_heartbeat (tracker.c:566-611): the interval's counters, cleared
+        if (c.g->node) {
+            DHost* H = c.H;
+            if (H->nhb < c.g->node_k) {
+                uint64_t* o = c.g->node + ((size_t)c.h * c.g->node_k + H->nhb) * (2 * kTrk);
+                for (uint32_t j = 0; j < 2 * kTrk; j++) o[j] = H->trk[j];
+            } else {
+                H->err |= SHD_TCP_ERR_INTERNAL;
+            }
+            H->nhb++;
+            for (uint32_t j = 0; j < 2 * kTrk; j++) H->trk[j] = 0;
+        }
+        sched_task(c, c.g->hb, K_HEARTBEAT, -1);
+        break;
     case K_REFILL: refill_cb(c); break;
     case K_REFILL_LO: break;
     case K_PSTART: {   // the process's start task (process.c:1334-1357)
@@ -2108,8 +2167,10 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     std::sort(ipk.begin(), ipk.end());
     g.H = H; g.P = P; g.W = W;
     g.end_time = m->end_time; g.hb = m->heartbeat_interval ? m->heartbeat_interval : kSec;
-    g.tcp_bytes = m->tcp_bytes; g.trace = trace ? 1 : 0;
+    g.tcp_bytes = m->tcp_bytes; g.trace = (trace & SHD_TCP_TRACE_STATUS) ? 1 : 0;
     g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
+    if (m->qdisc > 1) { free(res); return -22; }
+    g.qdisc_rr = m->qdisc;
     HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)V * V));
     HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)V * V));
     HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
@@ -2144,7 +2205,16 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * (size_t)H));
     HCHECK(hipMemcpy(d_ipk, ipk.data(), sizeof(uint64_t) * (size_t)H, hipMemcpyHostToDevice));
     g.ip_key = d_ipk;
-    if (trace) {
+    if (trace & SHD_TCP_TRACE_NODE) {   // every heartbeat before the end, per host
+        g.node_k = (uint32_t)((m->end_time - 1) / g.hb) + 1;
+        if (hipMalloc(&g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k) != hipSuccess) {
+            (void)hipGetLastError();
+            fprintf(stderr, "shd_tcp_run: no device memory for the tracker counters\n");
+            rc = -12;
+            goto done;
+        }
+    }
+    if (g.trace) {
         // kTr records and kTrSack SACK words per host (about 16 MB): a traced
         // run of many hosts may not fit; say so instead of a bare -ENOMEM
         const size_t need = (sizeof(TRec) * (size_t)kTr + sizeof(int32_t) * (size_t)kTrSack) * (size_t)H;
@@ -2223,7 +2293,15 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         res->deliveries += hout[i].deliveries;
         res->error |= hout[i].err;
     }
-    if (trace) {
+    if (g.node) {
+        res->node_k = g.node_k;
+        res->n_heartbeats = (uint32_t*)calloc(H, sizeof(uint32_t));
+        res->node_counters = (uint64_t*)malloc(sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k);
+        HCHECK(hipMemcpy(res->node_counters, g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k,
+                         hipMemcpyDeviceToHost));
+        for (int32_t i = 0; i < H; i++) res->n_heartbeats[i] = hout[i].nhb < g.node_k ? hout[i].nhb : g.node_k;
+    }
+    if (g.trace) {
         std::string text;
         std::vector<TRec> recs;
         std::vector<int32_t> sk;
@@ -2253,7 +2331,7 @@ done:
     (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
     (void)hipFree(g.pool); (void)hipFree(g.freel); (void)hipFree(g.ev); (void)hipFree(g.cq);
     (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);
-    (void)hipFree(g.qlog); (void)hipFree(g.nqlog);
+    (void)hipFree(g.qlog); (void)hipFree(g.nqlog); (void)hipFree(g.node);
     if (rc) { shd_tcp_result_free(res); return rc; }
     *out = res;
     return 0;
@@ -2266,5 +2344,7 @@ extern "C" void shd_tcp_result_free(shd_tcp_result* r) {
     free(r->next_packet_id);
     free(r->rng_probe);
     free(r->queries);
+    free(r->node_counters);
+    free(r->n_heartbeats);
     free(r);
 }

@@ -417,3 +417,43 @@ int shd_node_lines(const uint32_t* snaps, uint64_t k, uint64_t interval_ns, uint
     }
     return lb_done(&b, out);
 }
+
+/* _tracker_getCounterString (tracker.c:399-417) from the ten counters of one
+ * direction (shdtcp.h's order): the totals, then the ten */
+static int counters_str(char* o, const uint64_t* t) {
+    const unsigned long long pk = t[0] + t[2] + t[4] + t[7], by = t[1] + t[3] + t[5] + t[6] + t[8] + t[9];
+    return sprintf(o, "%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu,%llu", pk, by,
+                   (unsigned long long)t[0], (unsigned long long)t[1], (unsigned long long)t[2],
+                   (unsigned long long)t[3], (unsigned long long)t[4], (unsigned long long)t[5],
+                   (unsigned long long)t[6], (unsigned long long)t[7], (unsigned long long)t[8],
+                   (unsigned long long)t[9]);
+}
+
+int shd_tracker_node_lines(const uint64_t* counters, uint64_t k, uint64_t interval_ns, uint32_t host,
+                           shd_lines** out) {
+    if (!out || (k && !counters) || !interval_ns) return SHD_EINVAL;
+    lbuf b;
+    int rc = lb_init(&b, out);
+    if (rc) return rc;
+    const unsigned secs = (unsigned)(interval_ns / 1000000000ull);
+    static const uint64_t kZero[10] = {0};
+    char zero[256], ci[256], co[256], line[1400];
+    counters_str(zero, kZero);
+    lb_add(&b, 0, host, kNodeHeader, sizeof(kNodeHeader) - 1);
+    int len = sprintf(line, "[shadow-heartbeat] [node] %u,%d,%d,%f,%d,%f;%s;%s;%s;%s", secs, 0, 0, 0.0, 0, 0.0, zero,
+                      zero, zero, zero);
+    lb_add(&b, 0, host, line, (size_t)len);
+    for (uint64_t j = 0; j < k; j++) {
+        const uint64_t* in = counters + 20 * j;
+        const uint64_t* ou = in + 10;
+        const unsigned long long rb = in[1] + in[3] + in[5] + in[6] + in[8] + in[9];
+        const unsigned long long sb = ou[1] + ou[3] + ou[5] + ou[6] + ou[8] + ou[9];
+        counters_str(ci, in);
+        counters_str(co, ou);
+        /* the CPU model is off (cpu-percent 0, no delays); no loopback TCP */
+        len = sprintf(line, "[shadow-heartbeat] [node] %u,%llu,%llu,%f,%d,%f;%s;%s;%s;%s", secs, rb, sb, 0.0, 0, 0.0,
+                      zero, zero, ci, co);
+        lb_add(&b, (j + 1) * interval_ns, host, line, (size_t)len);
+    }
+    return lb_done(&b, out);
+}

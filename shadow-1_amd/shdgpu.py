@@ -189,7 +189,7 @@ class TcpModel(C.Structure):
                 ("proc_host", P(C.c_int32)), ("proc_start", P(C.c_uint64)), ("proc_peer", P(C.c_int32)),
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
-                ("tcp_window", C.c_uint32), ("packets_per_host", C.c_uint32)]
+                ("tcp_window", C.c_uint32), ("packets_per_host", C.c_uint32), ("qdisc", C.c_uint32)]
 
 
 class TcpResult(C.Structure):
@@ -198,7 +198,12 @@ class TcpResult(C.Structure):
                 ("next_event_id", P(C.c_uint64)), ("next_packet_id", P(C.c_uint64)),
                 ("rng_probe", P(C.c_uint32)), ("rounds", C.c_uint64), ("events", C.c_uint64),
                 ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64),
-                ("queries", C.c_void_p), ("n_queries", C.c_uint64)]
+                ("queries", C.c_void_p), ("n_queries", C.c_uint64),
+                ("node_counters", P(C.c_uint64)), ("n_heartbeats", P(C.c_uint32)), ("node_k", C.c_uint32),
+                ("_pad2", C.c_uint32)]
+
+
+TCP_TRACE_STATUS, TCP_TRACE_NODE = 1, 2   # shd_tcp_run's trace bits
 
 
 TCP_QUERY_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("src", "<u4"), ("index", "<u4"),
@@ -215,6 +220,7 @@ class Lines(C.Structure):
 _SIGS = {
     "shd_tcp_run": (C.c_int, [P(TcpModel), C.c_int32, P(P(TcpResult))]),
     "shd_tcp_result_free": (None, [P(TcpResult)]),
+    "shd_tracker_node_lines": (C.c_int, [P(C.c_uint64), C.c_uint64, C.c_uint64, C.c_uint32, P(P(Lines))]),
     "shd_graph_check": (C.c_int, [P(Graph), P(GraphProps)]),
     "shd_graphml_load_file": (C.c_int, [C.c_char_p, P(P(GraphML))]),
     "shd_graphml_load_string": (C.c_int, [C.c_char_p, C.c_size_t, P(P(GraphML))]),

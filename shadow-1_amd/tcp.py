@@ -81,17 +81,20 @@ def serial_first_queries(queries: np.ndarray):
 
 
 def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000, trace=True,
-        recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0, guess_reversed=False):
+        recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0, guess_reversed=False,
+        node=False, qdisc=0):
     """Run the TCP echo model on the GPU: procs = [(host, start ns)], peers =
     [-1 | server process]; ips: host-order uint32 per host.  Returns
     dict(lines=[(t, h, line)] in each host's order, next_event_id,
-    next_packet_id, rng_probe, rounds, events, device_ms, first_touch_runs).
+    next_packet_id, rng_probe, rounds, events, device_ms, first_touch_runs;
+    with node: node_lines=[(t, h, line)], every host's tracker [node] lines by
+    (time, host), from the library's writer).
     guess_reversed: start from a wrong first-touch guess (tests)."""
     lat, rel, hvi, att = path_table(model, g, procs, peers, reverse=guess_reversed)
     V = lat.shape[0]
     for runs in range(1, 9):
         out = _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-                        packets_per_host)
+                        packets_per_host, node, qdisc)
         order, pairs = serial_first_queries(out.pop("queries"))
         lat2, rel2 = resolve(g, att, order, pairs, V)
         ij = tuple(np.array([(a, b) for a, b in pairs] + [(b, a) for a, b in pairs], dtype=np.int64).T) \
@@ -109,7 +112,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
 
 
 def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-              packets_per_host):
+              packets_per_host, node=False, qdisc=0):
     """one shd_tcp_run on the given path tables"""
     m = model.struct
     H = int(m.n_hosts)
@@ -139,8 +142,10 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
     tm.send_buf = send_buf
     tm.tcp_window = tcp_window
     tm.packets_per_host = packets_per_host
+    tm.qdisc = int(qdisc)   # --interface-qdisc: 0 fifo, 1 rr
     res = C.POINTER(S.TcpResult)()
-    S.check(S.lib().shd_tcp_run(C.byref(tm), 1 if trace else 0, C.byref(res)), "shd_tcp_run")
+    bits = (S.TCP_TRACE_STATUS if trace else 0) | (S.TCP_TRACE_NODE if node else 0)
+    S.check(S.lib().shd_tcp_run(C.byref(tm), bits, C.byref(res)), "shd_tcp_run")
     try:
         r = res.contents
         if r.error:
@@ -159,6 +164,19 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
                    queries=np.frombuffer(C.string_at(r.queries, int(r.n_queries) * S.TCP_QUERY_DTYPE.itemsize),
                                          dtype=S.TCP_QUERY_DTYPE).copy() if r.n_queries else
                    np.zeros(0, dtype=S.TCP_QUERY_DTYPE))
+        if node:
+            k = int(r.node_k)
+            cnt = np.ctypeslib.as_array(r.node_counters, shape=(H * k * 20,)).reshape(H, k, 20)
+            nhb = np.ctypeslib.as_array(r.n_heartbeats, shape=(H,))
+            hb = int(tm.heartbeat_interval) or S.SHD_SEC
+            nl = []
+            for h in range(H):
+                c = np.ascontiguousarray(cnt[h, :int(nhb[h])])
+                lp = C.POINTER(S.Lines)()
+                S.check(S.lib().shd_tracker_node_lines(c.ctypes.data_as(C.POINTER(C.c_uint64)), len(c), hb, h,
+                                                       C.byref(lp)), "shd_tracker_node_lines")
+                nl += S.take_lines(lp)
+            out["node_lines"] = sorted(nl, key=lambda x: (x[0], x[1]))
     finally:
         S.lib().shd_tcp_result_free(res)
     return out

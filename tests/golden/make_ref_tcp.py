@@ -4,7 +4,8 @@ oracle/_ref/libshdref_loop.so (the reference's tcp.c, tcp_cong_reno.c,
 tcp_retransmit_tally.cc, socket.c, network_interface.c, worker.c ... compiled
 unmodified; oracle/Makefile `ref`) and stores what a run must reproduce:
 the host IPs, the number and SHA-256 of the [STATUS] lines (in the serial
-order, and grouped by host in each host's order), and every host's
+order, and grouped by host in each host's order) and of the tracker's [node]
+lines (by time and host), and every host's
 next event ID, next packet ID and RNG draw at the end.
 
     python tests/golden/make_ref_tcp.py        # -> tests/golden/ref_tcp.json
@@ -24,9 +25,12 @@ def main():
     out = {}
     for name in TC.CASES:
         c, m = TC.build(name)
-        r = R.run(m, c["graph"], procs=c["procs"], tcp=dict(peers=c["peers"], nbytes=c["nbytes"]))
+        r = R.run(m, c["graph"], procs=c["procs"], tcp=dict(peers=c["peers"], nbytes=c["nbytes"],
+                                                            qdisc=c.get("qdisc", 0)))
         st = TC.status_lines(r["lines"])
+        hb = TC.node_lines(r["lines"])
         out[name] = dict(ips=r["ip"], n_status=len(st), status_sha256=TC.digest(st),
+                         n_heartbeat=len(hb), heartbeat_sha256=TC.digest(hb),
                          status_by_host_sha256=TC.digest(TC.by_host(st)),
                          next_event_id=[int(x) for x in r["next_event_id"]],
                          next_packet_id=[int(x) for x in r["next_packet_id"]],

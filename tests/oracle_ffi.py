@@ -329,7 +329,7 @@ class TcpCfg(C.Structure):
                 ("proc_peer", C.POINTER(C.c_int32)),
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
-                ("tcp_window", C.c_uint32), ("no_lines", C.c_uint32), ("_pad", C.c_uint32)]
+                ("tcp_window", C.c_uint32), ("no_lines", C.c_uint32), ("qdisc_rr", C.c_uint32)]
 
 
 class TcpOut(C.Structure):
@@ -339,7 +339,7 @@ class TcpOut(C.Structure):
 
 
 def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf=131072, tcp_window=10,
-            lines=True):
+            lines=True, qdisc=0):
     """The oracle's TCP echo run (o_tcp.c) on the model's hosts: procs = [(host,
     start)], peers = [-1 | server process]; ips: host-order uint32 per host.
     Returns dict(lines=[(t, h, line)], next_event_id, next_packet_id, rng_probe)
@@ -374,6 +374,7 @@ def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf
     cfg.send_buf = send_buf
     cfg.tcp_window = tcp_window
     cfg.no_lines = 0 if lines else 1
+    cfg.qdisc_rr = int(qdisc)
     out = TcpOut()
     l = lib()
     l.o_tcp_run.argtypes = [C.POINTER(TcpCfg), C.c_void_p, C.POINTER(TcpOut)]

@@ -36,7 +36,7 @@ class Cfg(C.Structure):
                 ("load", C.c_uint32), ("payload", C.c_uint32),
                 ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p),
                 ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32),
-                ("quiet", C.c_int32), ("_pad4", C.c_int32)]
+                ("quiet", C.c_int32), ("qdisc_rr", C.c_int32)]
 
 
 class Out(C.Structure):
@@ -123,6 +123,7 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
         keep.append(pp)
         cfg.proc_peer = _ptr(pp, C.c_int32)
         cfg.tcp_bytes = int(tcp.get("nbytes", 20000))
+        cfg.qdisc_rr = int(tcp.get("qdisc", 0))
     cfg.host_seed = m.host_rng
     cfg.host_vertex = m.host_vertex
     cfg.bw_down_kibps = m.bw_down_kibps

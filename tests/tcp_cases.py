@@ -58,6 +58,14 @@ def _server_first():
     return dict(graph=g, hv=[0, 17, 33], procs=procs, peers=[-1, -1, -1, 0, 1, 2], nbytes=50000, end=30, bw={})
 
 
+def _shared_hosts_rr():
+    """shared_hosts under --interface-qdisc=rr: a host's client sockets and its
+    server's child take turns at the interface (network_interface.c:466-490)"""
+    c = _shared_hosts()
+    c["qdisc"] = 1
+    return c
+
+
 CASES = {
     "ref_epoll_lossless": lambda: _pair(50.0, 0.0, 20000, 300),
     "ref_epoll_lossy": lambda: _pair(50.0, 0.25, 20000, 300),
@@ -68,6 +76,7 @@ CASES = {
     "geo_pairs": _geo_pairs,
     "shared_hosts": _shared_hosts,
     "server_first": _server_first,
+    "shared_hosts_rr": _shared_hosts_rr,
 }
 
 
@@ -81,6 +90,12 @@ def build(name):
 def status_lines(lines):
     """The [STATUS] lines (the tracker's heartbeat lines are not part of the TCP restatement)."""
     return [ln for ln in lines if not ln[2].startswith("[shadow-heartbeat]")]
+
+
+def node_lines(lines):
+    """The tracker's [shadow-heartbeat] lines (header, boot line, one per
+    heartbeat), by (time, host), each host's in its own order."""
+    return sorted((ln for ln in lines if ln[2].startswith("[shadow-heartbeat]")), key=lambda x: (x[0], x[1]))
 
 
 def digest(lines):

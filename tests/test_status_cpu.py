@@ -118,3 +118,30 @@ def test_c_writer_equals_the_python_restatement():
     for pl in (0, 1, 1500):
         assert S.tracker_node_lines(snaps, S.SHD_SEC, pl) == S.tracker_node_lines_py(snaps, S.SHD_SEC, pl)
         assert S.tracker_node_lines(snaps[:0], 2 * S.SHD_SEC, pl) == S.tracker_node_lines_py(snaps[:0], 2 * S.SHD_SEC, pl)
+
+
+def test_tracker_node_lines_from_full_counters():
+    """shd_tracker_node_lines (the TCP path's [node] lines): the header and the
+    boot line at t = 0, then per interval _tracker_logNode's line
+    (tracker.c:419-465) with _tracker_getCounterString's twelve fields
+    (tracker.c:399-417) for the remote counters, localhost all zero.  Checked
+    against the format written out here from those lines of the reference."""
+    import ctypes as C
+    cnt = np.zeros((2, 20), dtype=np.uint64)
+    # interval 1: in 3 control (66 B each), 2 data (66 + 1000), 1 data retransmit (66 + 500);
+    #             out 4 control, 1 control retransmit
+    cnt[0, :10] = [3, 198, 0, 0, 2, 132, 2000, 1, 66, 500]
+    cnt[0, 10:] = [4, 264, 1, 66, 0, 0, 0, 0, 0, 0]
+    lp = C.POINTER(S.Lines)()
+    S.check(S.lib().shd_tracker_node_lines(cnt.ctypes.data_as(C.POINTER(C.c_uint64)), 2, 2 * S.SHD_SEC, 7,
+                                           C.byref(lp)), "shd_tracker_node_lines")
+    lines = S.take_lines(lp)
+    assert [(t, h) for t, h, _ in lines] == [(0, 7), (0, 7), (2 * S.SHD_SEC, 7), (4 * S.SHD_SEC, 7)]
+    assert lines[0][2].startswith("[shadow-heartbeat] [node-header] interval-seconds,recv-bytes,")
+    z = ",".join(["0"] * 12)
+    assert lines[1][2] == f"[shadow-heartbeat] [node] 2,0,0,0.000000,0,0.000000;{z};{z};{z};{z}"
+    rin = 198 + 132 + 2000 + 66 + 500
+    rout = 264 + 66
+    assert lines[2][2] == (f"[shadow-heartbeat] [node] 2,{rin},{rout},0.000000,0,0.000000;{z};{z};"
+                           f"6,{rin},3,198,0,0,2,132,2000,1,66,500;5,{rout},4,264,1,66,0,0,0,0,0,0")
+    assert lines[3][2] == f"[shadow-heartbeat] [node] 2,0,0,0.000000,0,0.000000;{z};{z};{z};{z}"

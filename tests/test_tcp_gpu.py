@@ -25,10 +25,14 @@ def test_tcp_gpu_equals_reference(name):
     f = FIX[name]
     c, m = TC.build(name)
     ips = TC.ip_ints(f["ips"])
-    r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"])
+    r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], node=True, qdisc=c.get("qdisc", 0))
     got = r["lines"]
+    # the tracker's [node] lines: the library's writer over the device's counters
+    assert len(r["node_lines"]) == f["n_heartbeat"]
+    assert TC.digest(r["node_lines"]) == f["heartbeat_sha256"]
     if TC.digest(got) != f["status_by_host_sha256"]:
-        want = TC.by_host(O.tcp_run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"])["lines"])
+        want = TC.by_host(O.tcp_run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"],
+                                    qdisc=c.get("qdisc", 0))["lines"])
         for i, (x, y) in enumerate(zip(got, want)):
             assert x == y, (i, x, y)
         assert len(got) == len(want), (len(got), len(want))

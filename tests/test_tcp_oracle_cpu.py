@@ -26,7 +26,8 @@ FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
 
 def _oracle(name):
     c, m = TC.build(name)
-    return O.tcp_run(m, c["graph"], TC.ip_ints(FIX[name]["ips"]), c["procs"], c["peers"], nbytes=c["nbytes"])
+    return O.tcp_run(m, c["graph"], TC.ip_ints(FIX[name]["ips"]), c["procs"], c["peers"], nbytes=c["nbytes"],
+                     qdisc=c.get("qdisc", 0))
 
 
 @pytest.mark.parametrize("name", list(TC.CASES))
@@ -57,6 +58,12 @@ def test_tcp_fixture_cases_exercise_the_machinery():
     for need in ("SND_TCP_RETRANSMITTED", "INET_DROPPED", "RCV_TCP_ENQUEUE_UNORDERED", "RCV_SOCKET_DELIVERED",
                  "header=SYN ", "header=SYNACK", "header=FIN ", "header=FINACK", "DUPACK", "sack-ranges"):
         assert need in seen, need
+
+
+def test_rr_qdisc_changes_the_run():
+    """the round-robin fixture is not the FIFO one: its hosts' sockets take
+    turns at the interface in another order (network_interface.c:466-517)"""
+    assert FIX["shared_hosts_rr"]["status_sha256"] != FIX["shared_hosts"]["status_sha256"]
 
 
 @pytest.mark.skipif(not R.available(), reason="reference loop not built here (oracle/Makefile ref)")
