@@ -377,7 +377,7 @@ typedef struct ohost_t {
 } ohost_t;
 
 typedef struct tev { uint64_t time, seq; uint32_t dst, src, kind; int32_t obj; opkt* pkt; } tev;
-enum { K_HEARTBEAT, K_REFILL, K_REFILL_LO, K_PSTART, K_NOTIFY, K_DELIVER, K_DELACK, K_RTO, K_CLOSE, K_WINUPD };
+enum { K_HEARTBEAT, K_REFILL, K_REFILL_LO, K_PSTART, K_NOTIFY, K_DELIVER, K_DELACK, K_RTO, K_CLOSE, K_WINUPD, K_LOCAL };
 
 typedef struct {
     const o_tcp_cfg* cfg;
@@ -1383,7 +1383,12 @@ static void if_send_packets(int32_t h) {   /* network_interface.c:519-579 */
         }
         if (!p) break;
         pkt_status(p, S_SND_INTERFACE_SENT);
-        worker_send_packet(h, p);
+        if (p->dip == H->ip) {   /* our own interface (:548-555): a +1 ns task, no router, no bandwidth */
+            pkt_ref(p);
+            if (!push_ev(G, (uint32_t)h, (uint32_t)h, G->now + 1, K_LOCAL, -1, p)) pkt_unref(p);
+        } else {
+            worker_send_packet(h, p);
+        }
         consume(&H->tx_rem, (uint64_t)p->len + HDR_TCP);
         refill_if_needed(h);
         pkt_unref(p);
@@ -1724,6 +1729,12 @@ static void execute(const tev* e) {
         /* the task's reference goes after the event (host -1: no active host) */
         G->active = -1;
         pkt_unref(p);
+        break;
+    }
+    case K_LOCAL: {   /* _networkinterface_receivePacket as the loopback task (network_interface.c:551-554) */
+        if_receive_packet(h, e->pkt);
+        G->active = -1;   /* the task's reference goes after the event, as K_DELIVER's */
+        pkt_unref(e->pkt);
         break;
     }
     case K_DELACK: {   /* _tcp_sendACKTaskCallback (tcp.c:1767-1774) */

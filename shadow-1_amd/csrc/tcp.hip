@@ -105,7 +105,7 @@ enum : uint32_t { PF_PROCESSED = 1, PF_DATA_RECEIVED = 2, PF_DATA_ACKED = 4, PF_
 enum { E_WOULDBLOCK = 11, E_INPROGRESS = 115, E_ALREADY = 114, E_ISCONN = 106, E_NOTCONN = 107, E_PIPE = 32,
        E_CONNRESET = 104, E_CONNREFUSED = 111 };
 enum : uint32_t { K_HEARTBEAT, K_REFILL, K_REFILL_LO, K_PSTART, K_NOTIFY, K_DELIVER, K_DELACK, K_RTO, K_CLOSE,
-                  K_WINUPD };
+                  K_WINUPD, K_LOCAL };
 enum { T_SRV_START, T_SRV_ACCEPT, T_SRV_RECV, T_SRV_SEND, T_CLI_START, T_CLI_CONNECT, T_CLI_SEND, T_CLI_RECV,
        T_DONE };
 
@@ -1452,23 +1452,26 @@ __device__ void tracker_add(L& c, int32_t pi, int dir) {
         else { t[0]++; t[1] += hdr; }
     }
 }
+__device__ void if_receive_packet(L& c, int32_t pi) {   // _networkinterface_receivePacket (:375-419)
+    const DPkt* p = PK(c, pi);
+    pkt_status(c, pi, S_RCV_INTERFACE_RECEIVED);
+    DSock* k = lookup_socket(c, p->dport, p->sip, p->sport);
+    if (k) {
+        pkt_status(c, pi, S_RCV_SOCKET_PROCESSED);   // socket_pushInPacket
+        tcp_process(c, k, pi);
+    } else {
+        pkt_status(c, pi, S_RCV_INTERFACE_DROPPED);
+    }
+    tracker_add(c, pi, 0);   // :415
+}
 __device__ void if_receive_packets(L& c) {   // :421-455
     DHost* H = c.H;
     while (H->rx_rem >= kMTU) {
         CqEnt e;
         if (!cq_dequeue(c, e)) break;
         pkt_status(c, e.pkt, S_ROUTER_DEQUEUED);
-        DPkt* p = PK(c, e.pkt);
-        const uint64_t len = (uint64_t)p->len + kHdr;
-        pkt_status(c, e.pkt, S_RCV_INTERFACE_RECEIVED);   // _networkinterface_receivePacket (:375-419)
-        DSock* k = lookup_socket(c, p->dport, p->sip, p->sport);
-        if (k) {
-            pkt_status(c, e.pkt, S_RCV_SOCKET_PROCESSED);   // socket_pushInPacket
-            tcp_process(c, k, e.pkt);
-        } else {
-            pkt_status(c, e.pkt, S_RCV_INTERFACE_DROPPED);
-        }
-        tracker_add(c, e.pkt, 0);   // :415
+        const uint64_t len = (uint64_t)PK(c, e.pkt)->len + kHdr;
+        if_receive_packet(c, e.pkt);
         pkt_unref(c, e.pkt);
         consume(H->rx_rem, len);
         refill_if_needed(c);
@@ -1531,7 +1534,15 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
         }
         if (pi < 0) break;
         pkt_status(c, pi, S_SND_INTERFACE_SENT);
-        worker_send_packet(c, pi);
+        if (PK(c, pi)->dip == H->ip) {   // our own interface (:548-555): a +1 ns task, no router, no mailbox
+            pkt_ref(c, pi);
+            DEv e;
+            e.time = c.now + 1; e.seq = H->ev_seq++; e.src = (uint32_t)c.h; e.kind = K_LOCAL; e.obj = -1; e.pkt = pi;
+            if (e.time < c.g->end_time) evq_push(c, e);
+            else pkt_unref(c, pi);   // scheduler_push refused it: the task's reference goes now
+        } else {
+            worker_send_packet(c, pi);
+        }
         consume(H->tx_rem, (uint64_t)PK(c, pi)->len + kHdr);
         refill_if_needed(c);
         tracker_add(c, pi, 1);   // :571
@@ -1843,6 +1854,12 @@ __device__ void execute(L& c, const DEv& e) {
         pr->ep_notifying = 0;
         pr->ep_ready = watch_ready(c, pr);
         if (pr->ep_ready) ep_schedule(c, pr);
+        break;
+    }
+    case K_LOCAL: {   // the loopback task (network_interface.c:551-554)
+        if_receive_packet(c, e.pkt);
+        c.active = -1;   // the task's reference goes after event_execute cleared the host, as K_DELIVER's
+        pkt_unref(c, e.pkt);
         break;
     }
     case K_DELIVER: {   // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)

@@ -66,6 +66,21 @@ def _shared_hosts_rr():
     return c
 
 
+def _loopback_pair():
+    """a client of its own host's server: every packet goes out and comes back
+    through the host's own interface as a +1 ns task (network_interface.c:548-555)"""
+    return dict(graph=_one_vertex(50.0, 0.0), hv=[0], procs=[(0, SEC), (0, 2 * SEC)], peers=[-1, 0],
+                nbytes=300000, end=60, bw={})
+
+
+def _loopback_mixed():
+    """host 0 serves a local client and a remote one while its own client talks
+    to host 1: loopback and routed packets share host 0's interface and buckets"""
+    g = W.geometric_graph(10, seed=2, loss_max=0.02)
+    procs = [(0, SEC), (0, SEC), (1, SEC), (0, 2 * SEC), (1, 2 * SEC), (0, 2 * SEC + 7)]
+    return dict(graph=g, hv=[0, 3], procs=procs, peers=[-1, -1, -1, 0, 1, 2], nbytes=200000, end=60, bw={})
+
+
 CASES = {
     "ref_epoll_lossless": lambda: _pair(50.0, 0.0, 20000, 300),
     "ref_epoll_lossy": lambda: _pair(50.0, 0.25, 20000, 300),
@@ -77,6 +92,8 @@ CASES = {
     "shared_hosts": _shared_hosts,
     "server_first": _server_first,
     "shared_hosts_rr": _shared_hosts_rr,
+    "loopback_pair": _loopback_pair,
+    "loopback_mixed": _loopback_mixed,
 }
 
 
