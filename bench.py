@@ -471,7 +471,7 @@ def tcp_main(args):
     deliv = r["deliveries"] * len(runs)
     # algorithmic bytes per executed event: its 32-B record pushed and popped
     # once (64 B); per delivery the mailbox record written and read once
-    mail_b = 720   # sizeof(Mail) in csrc/tcp.hip (static_assert there)
+    mail_b = 216   # sizeof(Mail) in csrc/tcp.hip (static_assert there; SACK lists travel apart)
     alg = 64 * r["events"] + 2 * mail_b * r["deliveries"]
     per_round_us = r["device_ms"] * 1e3 / max(r["rounds"], 1)
     achieved = alg / (r["device_ms"] / 1e3) / 1e9

@@ -62,18 +62,21 @@ constexpr uint32_t kPoolDefault = 8192;   // packets per host (buffered, in flig
 constexpr uint32_t kPktSack = 128;  // SACK entries carried by one segment (the receive window's holes)
 constexpr uint32_t kSt = 96;        // delivery statuses a packet's line lists (each loss retransmission adds 6)
 constexpr uint32_t kEv = 8192;      // events per host
+constexpr uint32_t kEvStride = kEv + 4;   // a host's heap slots (evq_base: 3 before the root, lines of 4)
 constexpr uint32_t kCq = 4096;      // CoDel queue per host
 constexpr uint32_t kTr = 1u << 16;  // trace records per host
 constexpr uint32_t kTrSack = 1u << 20;
-constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 16 per host)
-#ifndef SHD_TCP_ONE_COUNTER   // (round 3's 881351e, measured in round 4: profiles/r04/tcp) a mailbox in 64
-                              // parts with a fill counter each (host h claims in part h % 64, 32 slots per
-                              // host), and each lane folds the earliest delivery it sent into its own next
-                              // time instead of one contended atomicMin; SHD_TCP_ONE_COUNTER: one counter
-constexpr uint32_t kMailSub = 64;
-#else
-constexpr uint32_t kMailSub = 1;
+#ifdef SHD_TCP_PROF
+constexpr uint32_t kProf = 20, kProfRounds = 4096;   // steps timed per lane, rounds kept
 #endif
+constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 16 per host)
+// the mailbox in 64 parts with a fill counter each (host h claims in part h % 64,
+// 32 slots per host), each lane folding the earliest delivery it sent into its
+// own next time (measured against one counter and one atomicMin in round 4:
+// profiles/r04/tcp)
+constexpr uint32_t kMailSub = 64;
+constexpr uint32_t kMailDst = 64;   // mails a destination finds by index per round (more: its list)
+constexpr uint32_t kMailSack = 8;   // SACK entries per mailbox slot on average (their own arena)
 constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
 constexpr uint32_t kTrk = 10;       // tracker counters per direction (DHost::trk)
 constexpr uint32_t kXRetx = 1;      // DPkt::xflags: the packet was retransmitted (PDS_SND_TCP_RETRANSMITTED)
@@ -121,11 +124,12 @@ struct DPkt {
     uint32_t inq, xflags;   // Q_THROTTLED / Q_UNORDERED: in its socket's heap (the reference's
                             // priority_queue membership lookup, O(1) instead of a scan)
     uint8_t st[kSt];
-    int32_t sacks[kPktSack];
+    // its SACK list (nsack entries) is out of line: Glob::psack at its pool slot,
+    // Glob::msack while it travels (a copy moves this record only)
 };
 struct DEv { uint64_t time, seq; uint32_t src, kind; int32_t obj, pkt; };
-struct Mail { uint32_t dst, src; uint64_t time, seq; DPkt pkt; };
-static_assert(sizeof(DEv) == 32 && sizeof(Mail) == 720, "bench.py's algorithmic bytes of the TCP rounds");
+struct Mail { uint32_t dst, src; uint64_t time, seq; uint32_t sack_off, _pad; DPkt pkt; };
+static_assert(sizeof(DEv) == 32 && sizeof(Mail) == 216, "bench.py's algorithmic bytes of the TCP rounds");
 struct TRec {
     uint64_t time; int32_t host; uint32_t status;
     uint32_t host_id, flags, sip, dip;
@@ -201,7 +205,7 @@ struct DHost {
     uint32_t npq, nhb;
     uint64_t pq[kPq];
     // the tracker's interface counters of the running heartbeat interval
-    // (tracker.c:183-214; remote only: no TCP loopback here), inbound then
+    // (tracker.c:183-214; the loopback task's packets included), inbound then
     // outbound, each in the counter string's order (tracker.c:391-417 without
     // the two totals): packets-control, bytes-control-header,
     // packets-control-retrans, bytes-control-header-retrans, packets-data,
@@ -228,20 +232,28 @@ struct Glob {
     DProc* proc;            // [P]
     int32_t* host_procs;    // [H][kProcs]
     DPkt* pool;             // [H][pool_cap]
+    int32_t* psack;         // [H][pool_cap][kPktSack] each pool slot's SACK list
     int32_t* freel;         // [H][pool_cap]
     const int32_t* hv;      // [H] host -> vertex (the path tables' index)
     int32_t V; uint32_t pool_cap;
-    DEv* ev;                // [H][kEv]
+    DEv* ev;                // [H][kEvStride] each host's event heap (evq_base)
     CqEnt* cq;              // [H][kCq]
     Mail* mail;             // [2][mail_cap] the two mailboxes (a round's input, its output)
-    uint32_t* nmail;        // [2] their fill counts
+    uint32_t* nmail;        // [2][kMailSub] their fill counts
+    int32_t* msack;         // [2][msack_cap] the SACK lists of the mails that carry one
+    uint32_t* nmsack;       // [2] their fill counts
+    uint32_t msack_cap, _pad4;
     int32_t* mhead;         // [2][H] each destination's list of mails (-1: none)
     int32_t* mnext;         // [2][mail_cap] the next mail of the same destination
+    int32_t* mbox;          // [2][H][kMailDst] each destination's first kMailDst mails of a round
+    uint32_t* mcnt;         // [2][H] how many mails it got (those past kMailDst are on its list)
     uint32_t mail_cap, _pad2;
     TCtl* ctl;
     const uint64_t* ip_key; // [H] (ip << 32 | host) ascending: host_of_ip's table
     Mail* mail_in; int32_t* mhead_in; int32_t* mnext_in;     // a lane's view of the round
     Mail* mail_out; uint32_t* n_out; int32_t* mhead_out; int32_t* mnext_out;
+    const int32_t* msack_in; int32_t* msack_out; uint32_t* nmsack_out;
+    int32_t* mbox_in; uint32_t* mcnt_in; int32_t* mbox_out; uint32_t* mcnt_out;
     TRec* tr;               // [H][kTr]
     int32_t* trs;           // [H][kTrSack]
     uint64_t* next_time;    // [H]
@@ -250,6 +262,8 @@ struct Glob {
     uint32_t qlog_cap, _pad3;
     uint64_t* node;         // [H][node_k][2 * kTrk] tracker counters per heartbeat, or null
     uint32_t node_k, qdisc_rr;
+    uint64_t* prof;         // SHD_TCP_PROF builds: [H][2 * kProf] cycles and counts per step
+    uint32_t* prof_round;   // [2][kProfRounds] per round: the most events and cycles of a lane
 };
 
 // ------------------------------------------------------------ per-lane context
@@ -266,6 +280,9 @@ struct L {
     uint64_t mail_min;      // the earliest delivery this lane sent this round (part counters)
 };
 __device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * c.g->pool_cap + i]; }
+__device__ __forceinline__ int32_t* PSK(const L& c, int32_t i) {
+    return c.g->psack + ((size_t)c.h * c.g->pool_cap + i) * kPktSack;
+}
 __device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
 
 __device__ int32_t rand_r_dev(uint32_t* state) {   // glibc rand_r (random.c's source)
@@ -365,13 +382,19 @@ __device__ __forceinline__ bool ev_less(const DEv& a, const DEv& b) {
     if (a.src != b.src) return a.src < b.src;
     return a.seq < b.seq;
 }
+// A 4-ary heap whose four children of a node share one 128-B line (node i at
+// slot i + 3 of the host's kEvStride, children 4i+1 .. 4i+4 at 4(i+1) ..): a
+// level is one line, and a host's push or pop half the binary heap's dependent
+// loads.  Keys (time, src, seq) are unique, so the pop order is the binary
+// heap's.
+__device__ __forceinline__ DEv* evq_base(const Glob* g, int32_t h) { return g->ev + (size_t)h * kEvStride + 3; }
 __device__ void evq_push(const L& c, const DEv& e) {
-    DEv* q = c.g->ev + (size_t)c.h * kEv;
+    DEv* q = evq_base(c.g, c.h);
     uint32_t& n = c.H->nev;
     if (n >= kEv) { c.H->err |= SHD_TCP_ERR_EVQ; return; }
     uint32_t i = n++;
     while (i > 0) {
-        const uint32_t p = (i - 1) / 2;
+        const uint32_t p = (i - 1) >> 2;
         if (!ev_less(e, q[p])) break;
         q[i] = q[p];
         i = p;
@@ -379,19 +402,25 @@ __device__ void evq_push(const L& c, const DEv& e) {
     q[i] = e;
 }
 __device__ DEv evq_pop(const L& c) {
-    DEv* q = c.g->ev + (size_t)c.h * kEv;
+    DEv* q = evq_base(c.g, c.h);
     uint32_t& n = c.H->nev;
     const DEv top = q[0], last = q[--n];
     uint32_t i = 0;
     for (;;) {
-        const uint32_t l = 2 * i + 1, r = l + 1;
-        uint32_t m = i;
-        const DEv* best = &last;
-        if (l < n && ev_less(q[l], *best)) { m = l; best = &q[l]; }
-        if (r < n && ev_less(q[r], *best)) { m = r; best = &q[r]; }
-        if (m == i) break;
-        q[i] = q[m];
-        i = m;
+        const uint32_t c0 = 4 * i + 1;
+        if (c0 >= n) break;
+        const uint32_t nc = n - c0 < 4u ? n - c0 : 4u;
+        DEv ch[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) if (j < nc) ch[j] = q[c0 + j];   // one line
+        uint32_t m = 0;
+        DEv best = ch[0];
+#pragma unroll
+        for (uint32_t j = 1; j < 4; j++)
+            if (j < nc && ev_less(ch[j], best)) { best = ch[j]; m = j; }
+        if (!ev_less(best, last)) break;
+        q[i] = best;
+        i = c0 + m;
     }
     if (n) q[i] = last;
     return top;
@@ -422,7 +451,8 @@ __device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDelive
     for (uint32_t i = 0; i < p->nst; i++) r->st[i] = p->st[i];
     r->sack_off = H->ntrs; r->nsack = p->nsack;
     if (H->ntrs + p->nsack > kTrSack) { H->err |= SHD_TCP_ERR_TRACE; r->nsack = 0; return; }
-    for (uint32_t i = 0; i < p->nsack; i++) c.g->trs[(size_t)c.h * kTrSack + H->ntrs + i] = p->sacks[i];
+    const int32_t* sk = PSK(c, pi);
+    for (uint32_t i = 0; i < p->nsack; i++) c.g->trs[(size_t)c.h * kTrSack + H->ntrs + i] = sk[i];
     H->ntrs += p->nsack;
 }
 __device__ int32_t pkt_alloc(L& c) {
@@ -434,7 +464,7 @@ __device__ int32_t pkt_new(L& c, uint32_t len) {   // packet_new (packet.c:74-95
     const int32_t i = pkt_alloc(c);
     if (i < 0) return -1;
     DPkt* p = PK(c, i);
-    memset(p, 0, sizeof(DPkt) - sizeof(p->sacks));
+    memset(p, 0, sizeof(DPkt));
     p->refs = 1;
     p->host_id = (uint32_t)c.h + 1;
     p->pid = c.H->pkt_seq++;
@@ -1007,7 +1037,8 @@ __device__ void tcp_about_to_send(L& c, DSock* k, int32_t pi) {
         if (k->nsack > kPktSack) c.H->err |= SHD_TCP_ERR_SACK;
         p->flags |= F_SACK;
         p->nsack = k->nsack < kPktSack ? k->nsack : kPktSack;
-        for (uint32_t i = 0; i < p->nsack; i++) p->sacks[i] = k->sacks[i];
+        int32_t* sk = PSK(c, pi);
+        for (uint32_t i = 0; i < p->nsack; i++) sk[i] = k->sacks[i];
     }
     p->ack = k->r_next;
     p->win = k->r_window;
@@ -1337,7 +1368,7 @@ __device__ void tcp_process(L& c, DSock* k, int32_t pi) {   // tcp.c:1777-2099
     if (p->len > 0 && !(k->error & TE_RECEIVE_EOF)) fl |= tcp_data_processing(c, k, pi);
     if (p->flags & F_ACK) fl |= tcp_ack_processing(c, k, pi);
     if (!(fl & PF_PROCESSED)) { pkt_status(c, pi, S_RCV_SOCKET_DROPPED); return; }
-    if (p->nsack) tally_mark_sacked(k->tally, p->sacks, p->nsack, c.H->err);
+    if (p->nsack) tally_mark_sacked(k->tally, PSK(c, pi), p->nsack, c.H->err);
     k->r_last_ts = p->tsval;
     if (p->tsecho && k->backoff == 0) tcp_update_rtt(c, k, p->tsecho);
     if (p->seq > k->r_next && p->seq < k->r_next + k->r_window) resp |= (F_ACK | F_DUPACK);
@@ -1489,26 +1520,27 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
         const uint64_t seq = c.H->ev_seq++;   // event_new_ (the delivery's ID)
         if (t >= c.g->end_time) return;
         if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
-#ifndef SHD_TCP_ONE_COUNTER
         const uint32_t part = (uint32_t)c.h % kMailSub, per = c.g->mail_cap / kMailSub;
         const uint32_t kk = atomicAdd(c.g->n_out + part, 1u);
         if (kk >= per) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
         const uint32_t slot = part * per + kk;
-#else
-        const uint32_t slot = atomicAdd(c.g->n_out, 1u);
-        if (slot >= c.g->mail_cap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
-#endif
         Mail* m = &c.g->mail_out[slot];
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
+        m->sack_off = 0;
+        if (p->nsack) {   // the SACK list travels in the mailbox's arena
+            const uint32_t off = atomicAdd(c.g->nmsack_out, p->nsack);
+            if (off + p->nsack > c.g->msack_cap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+            const int32_t* sk = PSK(c, pi);
+            for (uint32_t i = 0; i < p->nsack; i++) c.g->msack_out[off + i] = sk[i];
+            m->sack_off = off;
+        }
         m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
         m->pkt.inq = 0;   // the copy is in no queue of the receiver
-        c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
-#ifndef SHD_TCP_ONE_COUNTER
+        const uint32_t j = atomicAdd(&c.g->mcnt_out[d], 1u);   // the receiver's index, then its list
+        if (j < kMailDst) c.g->mbox_out[(size_t)d * kMailDst + j] = (int32_t)slot;
+        else c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);
         if (t < c.mail_min) c.mail_min = t;   // folded into next_time[h] at the round's end
-#else
-        atomicMin((unsigned long long*)&c.g->next_time[c.g->H], (unsigned long long)t);
-#endif
     } else {
         pkt_status(c, pi, S_INET_DROPPED);
     }
@@ -1938,7 +1970,7 @@ __global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
         sched_task(c, st > 0 ? st : 1, K_PSTART, pi);
     }
     const uint32_t n = c.H->nev;
-    gl.next_time[h] = n ? gl.ev[(size_t)h * kEv].time : ~0ull;
+    gl.next_time[h] = n ? evq_base(&gl, h)[0].time : ~0ull;
 }
 
 // the next round's window (worker.c:293's conservative width W past the
@@ -1949,13 +1981,12 @@ __global__ void k_tcp_window(Glob g) {
     __shared__ uint64_t red[16];
     TCtl* ctl = g.ctl;
     if (ctl->halted) return;
-#ifndef SHD_TCP_ONE_COUNTER
     {   // the next round's output mailbox starts empty (read before thread 0 moves rounds on)
         const uint64_t k = ctl->rounds;
         if (threadIdx.x < kMailSub) g.nmail[((k + 1) & 1) * kMailSub + threadIdx.x] = 0;
+        if (threadIdx.x == kMailSub) g.nmsack[(k + 1) & 1] = 0;
     }
     __syncthreads();
-#endif
     uint64_t t = ~0ull;
     for (int32_t i = (int32_t)threadIdx.x; i <= g.H; i += (int32_t)blockDim.x) {
         const uint64_t x = g.next_time[i];
@@ -1975,12 +2006,28 @@ __global__ void k_tcp_window(Glob g) {
             const uint64_t k = ctl->rounds;
             ctl->wend = t + g.W;
             ctl->rounds = k + 1;
-#ifdef SHD_TCP_ONE_COUNTER
-            g.nmail[(k + 1) & 1] = 0;     // round k's output mailbox starts empty
-#endif
             g.next_time[g.H] = ~0ull;     // ... and so does its earliest delivery
         }
     }
+}
+
+// a delivery from the round's input mailbox onto the host's heap (its packet
+// copied into the pool, its SACK list from the mailbox's arena)
+__device__ bool ingest_mail(L& c, int32_t s) {
+    const Glob& gl = *c.g;
+    const Mail* m = &gl.mail_in[s];
+    const int32_t pi = pkt_alloc(c);
+    if (pi < 0) return false;
+    *PK(c, pi) = m->pkt;
+    if (m->pkt.nsack) {
+        int32_t* sk = PSK(c, pi);
+        for (uint32_t i = 0; i < m->pkt.nsack; i++) sk[i] = gl.msack_in[m->sack_off + i];
+    }
+    DEv e;
+    e.time = m->time; e.seq = m->seq; e.src = m->src; e.kind = K_DELIVER; e.obj = -1; e.pkt = pi;
+    evq_push(c, e);
+    c.H->deliveries++;
+    return true;
 }
 
 // one conservative round: the mailbox's deliveries for this host, then every
@@ -1999,37 +2046,76 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
         gl.mnext_in = g.mnext + (size_t)in * g.mail_cap;
         gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + (size_t)out * kMailSub;
         gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * g.mail_cap;
+        gl.msack_in = g.msack + (size_t)in * g.msack_cap; gl.msack_out = g.msack + (size_t)out * g.msack_cap;
+        gl.nmsack_out = g.nmsack + out;
+        gl.mbox_in = g.mbox + (size_t)in * g.H * kMailDst; gl.mcnt_in = g.mcnt + (size_t)in * g.H;
+        gl.mbox_out = g.mbox + (size_t)out * g.H * kMailDst; gl.mcnt_out = g.mcnt + (size_t)out * g.H;
     }
     __syncthreads();
     if (h >= g.H) return;
+#ifndef SHD_TCP_GLOBAL_HOST
+    // the host's record lives in LDS for the round (every H-> access of its
+    // events at LDS latency instead of a cache's): other lanes read only its
+    // fixed fields (ip, bandwidths, refills) from the global copy
+    __shared__ DHost s_host[64];
+    s_host[threadIdx.x] = gl.host[h];
+    L c{&gl, h, &s_host[threadIdx.x], 0, h, 0, 0, 0, ~0ull};
+#else
     L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
-    // this host's deliveries (any order: the heap's key (time, src, seq) is unique)
-    int32_t s = gl.mhead_in[h];
-    gl.mhead_in[h] = -1;   // the list is empty again when this mailbox is next written
-    for (; s >= 0; s = gl.mnext_in[s]) {
-        const Mail* m = &gl.mail_in[s];
-        const int32_t pi = pkt_alloc(c);
-        if (pi < 0) break;
-        *PK(c, pi) = m->pkt;
-        DEv e;
-        e.time = m->time; e.seq = m->seq; e.src = m->src; e.kind = K_DELIVER; e.obj = -1; e.pkt = pi;
-        evq_push(c, e);
-        c.H->deliveries++;
+#endif
+#ifdef SHD_TCP_PROF
+    uint64_t* pf = gl.prof + (size_t)h * 2 * kProf;
+    const uint64_t t_lane = clock64();
+    uint64_t t_p = t_lane;
+#define TCP_PROF(slot) do { const uint64_t t_ = clock64(); pf[(slot)] += t_ - t_p; pf[kProf + (slot)]++; t_p = t_; } while (0)
+#else
+#define TCP_PROF(slot) do { } while (0)
+#endif
+    // this host's deliveries (any order: the heap's key (time, src, seq) is
+    // unique): the indexed ones four slot loads at a time, then its list
+    const uint32_t nm = gl.mcnt_in[h], nx = nm < kMailDst ? nm : kMailDst;
+    gl.mcnt_in[h] = 0;   // empty again when this mailbox is next written
+    int32_t s = nm > kMailDst ? gl.mhead_in[h] : -1;
+    if (s >= 0) gl.mhead_in[h] = -1;
+    bool full = false;
+    for (uint32_t b = 0; b < nx && !full; b += 4) {
+        int32_t sl[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) sl[j] = b + j < nx ? gl.mbox_in[(size_t)h * kMailDst + b + j] : -1;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++)
+            if (sl[j] >= 0 && !full) full = !ingest_mail(c, sl[j]);
     }
+    for (; s >= 0 && !full; s = gl.mnext_in[s]) full = !ingest_mail(c, s);
+    TCP_PROF(0);
     uint64_t nev = 0;
-    while (c.H->nev && gl.ev[(size_t)h * kEv].time < wend && !c.H->err) {
+    while (c.H->nev && evq_base(&gl, h)[0].time < wend && !c.H->err) {
         const DEv e = evq_pop(c);
+        TCP_PROF(1);
         c.now = e.time;
         c.active = h;
         c.ksrc = e.src; c.kseq = e.seq; c.kq = 0;
         execute(c, e);
+        TCP_PROF(2 + (e.kind < 12 ? e.kind : 12));
         if (++nev > (1u << 24)) c.H->err |= SHD_TCP_ERR_INTERNAL;   // a runaway round: stop, report
     }
+#ifdef SHD_TCP_PROF
+    {
+        const uint64_t cyc = clock64() - t_lane;
+        pf[14] += cyc; pf[kProf + 14]++;
+        if (nev > pf[15]) pf[15] = nev;
+        if (k < kProfRounds) {
+            atomicMax(gl.prof_round + k, (uint32_t)nev);
+            atomicMax(gl.prof_round + kProfRounds + k, (uint32_t)(cyc >> 10));
+        }
+    }
+#endif
     c.H->events += nev;
     // a host that stopped on an error leaves the run (the caller sees the bit)
-    gl.next_time[h] = (c.H->nev && !c.H->err) ? gl.ev[(size_t)h * kEv].time : ~0ull;
-#ifndef SHD_TCP_ONE_COUNTER
+    gl.next_time[h] = (c.H->nev && !c.H->err) ? evq_base(&gl, h)[0].time : ~0ull;
     if (c.mail_min < gl.next_time[h]) gl.next_time[h] = c.mail_min;   // its deliveries count either way
+#ifndef SHD_TCP_GLOBAL_HOST
+    gl.host[h] = *c.H;
 #endif
 }
 
@@ -2204,19 +2290,26 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMalloc(&g.host_procs, sizeof(int32_t) * hp.size()));
     HCHECK(hipMemcpy(g.host_procs, hp.data(), sizeof(int32_t) * hp.size(), hipMemcpyHostToDevice));
     HCHECK(hipMalloc(&g.pool, sizeof(DPkt) * (size_t)H * pool_cap));
+    HCHECK(hipMalloc(&g.psack, sizeof(int32_t) * kPktSack * (size_t)H * pool_cap));
     HCHECK(hipMalloc(&g.freel, sizeof(int32_t) * (size_t)H * pool_cap));
     k_tcp_free_init<<<(unsigned)(((size_t)H * pool_cap + 255) / 256), 256>>>(g.freel, (size_t)H * pool_cap, pool_cap);
     HCHECK(hipGetLastError());
-    HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
+    HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEvStride));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
-    g.mail_cap = (uint32_t)H * 16u * (kMailSub > 1 ? 2u : 1u) > kMailMin ? (uint32_t)H * 16u * (kMailSub > 1 ? 2u : 1u)
-                                                                          : kMailMin;
+    g.mail_cap = (uint32_t)H * 32u > kMailMin ? (uint32_t)H * 32u : kMailMin;
+    g.msack_cap = g.mail_cap * kMailSack;
+    HCHECK(hipMalloc(&g.msack, sizeof(int32_t) * 2 * (size_t)g.msack_cap));
+    HCHECK(hipMalloc(&g.nmsack, sizeof(uint32_t) * 2));
+    HCHECK(hipMemset(g.nmsack, 0, sizeof(uint32_t) * 2));
     HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
     HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2 * kMailSub));
     HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * kMailSub));
     HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
+    HCHECK(hipMalloc(&g.mbox, sizeof(int32_t) * 2 * kMailDst * (size_t)H));
+    HCHECK(hipMalloc(&g.mcnt, sizeof(uint32_t) * 2 * (size_t)H));
+    HCHECK(hipMemset(g.mcnt, 0, sizeof(uint32_t) * 2 * (size_t)H));
     HCHECK(hipMalloc(&g.ctl, sizeof(TCtl)));
     HCHECK(hipMemset(g.ctl, 0, sizeof(TCtl)));
     HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * (size_t)H));
@@ -2249,6 +2342,12 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     g.qlog_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);
     HCHECK(hipMalloc(&g.qlog, sizeof(shd_tcp_query) * (size_t)g.qlog_cap));
     HCHECK(hipMalloc(&g.nqlog, sizeof(uint32_t)));
+#ifdef SHD_TCP_PROF
+    HCHECK(hipMalloc(&g.prof, sizeof(uint64_t) * 2 * kProf * (size_t)H));
+    HCHECK(hipMemset(g.prof, 0, sizeof(uint64_t) * 2 * kProf * (size_t)H));
+    HCHECK(hipMalloc(&g.prof_round, sizeof(uint32_t) * 2 * kProfRounds));
+    HCHECK(hipMemset(g.prof_round, 0, sizeof(uint32_t) * 2 * kProfRounds));
+#endif
     HCHECK(hipMemset(g.nqlog, 0, sizeof(uint32_t)));
     HCHECK(hipEventCreate(&e0));
     HCHECK(hipEventCreate(&e1));
@@ -2337,6 +2436,31 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         res->lines[text.size()] = 0;
         res->len = text.size();
     }
+#ifdef SHD_TCP_PROF
+    {   // the steps' cycles summed over hosts, and per round the busiest lane
+        std::vector<uint64_t> pf(2 * kProf * (size_t)H);
+        std::vector<uint32_t> pr(2 * kProfRounds);
+        HCHECK(hipMemcpy(pf.data(), g.prof, sizeof(uint64_t) * pf.size(), hipMemcpyDeviceToHost));
+        HCHECK(hipMemcpy(pr.data(), g.prof_round, sizeof(uint32_t) * pr.size(), hipMemcpyDeviceToHost));
+        static const char* kName[kProf] = {"ingest", "evq_pop", "HEARTBEAT", "REFILL", "REFILL_LO", "PSTART",
+                                           "NOTIFY", "DELIVER", "DELACK", "RTO", "CLOSE", "WINUPD", "LOCAL",
+                                           "-", "lane_round", "max_ev", "-", "-", "-", "-"};
+        fprintf(stderr, "tcp_prof: step cycles_total count cycles_per\n");
+        for (uint32_t j = 0; j < kProf; j++) {
+            uint64_t cy = 0, n = 0;
+            for (int32_t i = 0; i < H; i++) {
+                const uint64_t* q = pf.data() + (size_t)i * 2 * kProf;
+                if (j == 15) { cy = std::max(cy, q[j]); continue; }
+                cy += q[j]; n += q[kProf + j];
+            }
+            if (cy || n) fprintf(stderr, "tcp_prof: %s %llu %llu %.1f\n", kName[j], (unsigned long long)cy,
+                                 (unsigned long long)n, n ? (double)cy / (double)n : 0.0);
+        }
+        const uint64_t nr = std::min<uint64_t>(hctl.rounds, kProfRounds);
+        for (uint64_t r = 0; r < nr; r++)
+            fprintf(stderr, "tcp_round: %llu max_ev %u max_kcyc %u\n", (unsigned long long)r, pr[r], pr[kProfRounds + r]);
+    }
+#endif
 done:
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -2345,10 +2469,13 @@ done:
     if (st) (void)hipStreamDestroy(st);
     (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_ipk); (void)hipFree(d_hv);
     (void)hipFree(g.mail); (void)hipFree(g.nmail); (void)hipFree(g.mhead); (void)hipFree(g.mnext); (void)hipFree(g.ctl);
+    (void)hipFree(g.mbox); (void)hipFree(g.mcnt);
     (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
-    (void)hipFree(g.pool); (void)hipFree(g.freel); (void)hipFree(g.ev); (void)hipFree(g.cq);
+    (void)hipFree(g.pool); (void)hipFree(g.psack); (void)hipFree(g.freel);
+    (void)hipFree(g.msack); (void)hipFree(g.nmsack); (void)hipFree(g.ev); (void)hipFree(g.cq);
     (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);
-    (void)hipFree(g.qlog); (void)hipFree(g.nqlog); (void)hipFree(g.node);
+    (void)hipFree(g.qlog); (void)hipFree(g.nqlog); (void)hipFree(g.node); (void)hipFree(g.prof);
+    (void)hipFree(g.prof_round);
     if (rc) { shd_tcp_result_free(res); return rc; }
     *out = res;
     return 0;
