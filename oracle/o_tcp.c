@@ -1156,7 +1156,7 @@ static void tcp_process(osock* k, opkt* p) {   /* tcp.c:1777-2099 */
         }
     }
     if (p->flags & F_RST) {
-        if (!(k->state & TS_LISTEN) && !(k->error & TE_CONNECTION_RESET)) {
+        if (k->state != TS_LISTEN && !(k->error & TE_CONNECTION_RESET)) {   /* TCPS_LISTEN is a bit there; a state here */
             k->error |= TE_CONNECTION_RESET;
             k->flags |= TF_REMOTE_CLOSED;
             tcp_set_state(k, TS_TIMEWAIT);
