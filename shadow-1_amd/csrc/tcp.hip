@@ -147,15 +147,13 @@ struct Rng64 { int64_t a, b; };
 struct RVec { uint32_t n; Rng64 r[kRanges]; };
 struct Tally { int64_t last_ack; uint64_t ndup; RVec marked, sacked, retx, lost, tmp; };
 
-struct DSock {
+struct DSock {   // every scalar first (a few lines per socket), then the containers
     int32_t used, host, proc;
     uint32_t status;
     int32_t bound; uint32_t bound_ip; uint16_t bound_port, peer_port;
     uint32_t peer_ip;
     int32_t assoc, assoc_general;
     uint64_t in_len, in_size, in_pending, out_len, out_size, out_pending;
-    Ring<kQ> in, out;
-    Ring<kQc> outctl;
     int32_t state, state_last;
     uint32_t flags, error;
     uint32_t r_start, r_next, r_window, r_end, r_last_window, r_last_ack, r_last_seq;
@@ -163,22 +161,29 @@ struct DSock {
     uint32_t s_unacked, s_next, s_window, s_end, s_last_ack, s_last_window, s_highest, s_packets_sent,
         s_quick_acks, s_delack_counter;
     int32_t s_delack_sched;
-    uint32_t nsack; int32_t sacks[kSacks];
+    uint32_t nsack;
     // the retransmit queue (tcp.c's GHashTable by sequence) as a sequence-sorted
     // window [rh, rh + nrtx) of rtx (packets) and rtxs (their sequences)
-    uint32_t nrtx, rh; int32_t rtx[kQ]; uint32_t rtxs[kQ]; uint64_t rtx_len; int32_t rto; THeap<kTimers> timers; uint64_t desired;
+    uint32_t nrtx, rh; uint64_t rtx_len; int32_t rto; uint64_t desired;
     uint32_t backoff;
-    Tally tally;
     int32_t at_did_init; uint64_t at_bytes, at_last_adjust, at_space;
     uint32_t cwnd; int32_t reno_state; uint64_t reno_ndup; uint32_t reno_nacked, reno_ssthresh;
     int32_t srtt, rttvar;
     uint64_t retx_count; uint32_t info_rtt;
-    IHeap<kQ> throttled; uint64_t throttled_len;
-    IHeap<kQ> unordered; uint64_t unordered_len;
+    uint64_t throttled_len, unordered_len;
     int32_t partial; uint32_t partial_off;
-    int32_t server; uint32_t nkids, npending; int32_t kids[kKids], pending[kKids];
+    int32_t server; uint32_t nkids, npending;
     uint32_t last_peer_ip, last_ip; uint16_t last_peer_port;
     int32_t child, parent, child_state;
+    int32_t kids[kKids], pending[kKids];
+    Ring<kQc> outctl;
+    THeap<kTimers> timers;
+    Tally tally;
+    IHeap<kQ> throttled;
+    IHeap<kQ> unordered;
+    Ring<kQ> in, out;
+    int32_t sacks[kSacks];
+    int32_t rtx[kQ]; uint32_t rtxs[kQ];
 };
 struct DProc {
     int32_t host, index, peer, running, step, fd, listenfd, wait_fd;
@@ -245,7 +250,8 @@ struct Glob {
     int32_t* mnext;         // [2][mail_cap] the next mail of the same destination
     uint32_t mail_cap, _pad2;
     TCtl* ctl;
-    const uint64_t* ip_key; // [H] (ip << 32 | host) ascending: host_of_ip's table
+    const uint64_t* ip_key; // [ip_mask + 1] (ip << 32 | host), open addressing: host_of_ip's table
+    uint32_t ip_mask, _pad5;
     Mail* mail_in; int32_t* mhead_in; int32_t* mnext_in;     // a lane's view of the round
     Mail* mail_out; uint32_t* n_out; int32_t* mhead_out; int32_t* mnext_out;
     const int32_t* msack_in; int32_t* msack_out; uint32_t* nmsack_out;
@@ -426,9 +432,9 @@ __device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDelive
     DPkt* p = PK(c, pi);
     DHost* H = c.H;
     if (st == S_SND_TCP_RETRANSMITTED) p->xflags |= kXRetx;   // packet_getDeliveryStatus's OR of every status
+    if (!c.g->trace) return;   // the list is read by the lines only
     if (p->nst < kSt) p->st[p->nst++] = st;
-    else if (c.g->trace) H->err |= SHD_TCP_ERR_TRACE;   // a line would lose statuses: fail, never truncate
-    if (!c.g->trace) return;
+    else H->err |= SHD_TCP_ERR_TRACE;   // a line would lose statuses: fail, never truncate
     if (H->ntr >= kTr) { H->err |= SHD_TCP_ERR_TRACE; return; }
     TRec* r = &c.g->tr[(size_t)c.h * kTr + H->ntr++];
     r->time = c.now; r->host = c.active; r->status = st;
@@ -451,7 +457,7 @@ __device__ int32_t pkt_new(L& c, uint32_t len) {   // packet_new (packet.c:74-95
     const int32_t i = pkt_alloc(c);
     if (i < 0) return -1;
     DPkt* p = PK(c, i);
-    memset(p, 0, sizeof(DPkt));
+    memset(p, 0, c.g->trace ? sizeof(DPkt) : offsetof(DPkt, st));
     p->refs = 1;
     p->host_id = (uint32_t)c.h + 1;
     p->pid = c.H->pkt_seq++;
@@ -460,6 +466,16 @@ __device__ int32_t pkt_new(L& c, uint32_t len) {   // packet_new (packet.c:74-95
     return i;
 }
 __device__ void pkt_ref(L& c, int32_t i) { PK(c, i)->refs++; }
+// a packet record copied: its status list only when lines are written (no
+// other reader)
+__device__ __forceinline__ void pkt_copy_rec(DPkt* d, const DPkt* p, bool st) {
+    if (st) { *d = *p; return; }
+    static_assert(offsetof(DPkt, st) % 8 == 0, "the record's head in 8-B words");
+    const uint64_t* a = (const uint64_t*)p;
+    uint64_t* b = (uint64_t*)d;
+#pragma unroll
+    for (uint32_t i = 0; i < offsetof(DPkt, st) / 8; i++) b[i] = a[i];
+}
 __device__ void pkt_unref(L& c, int32_t i) {   // packet.c:194-201
     DPkt* p = PK(c, i);
     if (--p->refs == 0) {
@@ -578,15 +594,19 @@ __device__ int32_t sock_remove_output(L& c, DSock* k) {   // socket.c:426-451
 // ------------------------------------------------------------ paths
 // the first host holding ip (dns.c: one address per host), by binary search
 // over the sorted (ip, host) keys
+// the host of an address: a hash table with linear probing, a lookup one
+// line in the common case (a binary search over the sorted addresses was 17
+// dependent loads at 65 536 hosts, on every packet sent)
+__host__ __device__ __forceinline__ uint32_t ip_slot(uint32_t ip, uint32_t mask) { return (ip * 0x9E3779B1u) >> 7 & mask; }
 __device__ int32_t host_of_ip(const L& c, uint32_t ip) {
     const uint64_t* k = c.g->ip_key;
-    uint32_t lo = 0, hi = (uint32_t)c.g->H;
-    const uint64_t x = (uint64_t)ip << 32;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (k[mid] < x) lo = mid + 1; else hi = mid;
+    const uint32_t mask = c.g->ip_mask;
+    for (uint32_t i = ip_slot(ip, mask), n = 0; n <= mask; i = (i + 1) & mask, n++) {
+        const uint64_t v = k[i];
+        if (v == ~0ull) return -1;
+        if ((uint32_t)(v >> 32) == ip) return (int32_t)(uint32_t)v;
     }
-    return (lo < (uint32_t)c.g->H && (uint32_t)(k[lo] >> 32) == ip) ? (int32_t)(uint32_t)k[lo] : -1;
+    return -1;
 }
 // A path query of the executing event (topology_isRoutable / getLatency /
 // getReliability, topology.c:2053-2092).  Which endpoint's Dijkstra row serves
@@ -870,7 +890,7 @@ __device__ int32_t sock_new(L& c) {   // host_createDescriptor + tcp_new (tcp.c:
     if (H->nsock >= kSock) { H->err |= SHD_TCP_ERR_SOCKETS; return -1; }
     const int32_t si = c.h * kSock + H->nsock++;
     DSock* k = &c.g->sock[si];
-    memset(k, 0, offsetof(DSock, in));
+    memset(k, 0, offsetof(DSock, outctl));   // the scalars
     k->used = 1; k->host = c.h; k->proc = -1; k->parent = -1; k->partial = -1;
     k->in.head = k->in.n = 0; k->out.head = k->out.n = 0; k->outctl.head = k->outctl.n = 0;
     k->state = TS_CLOSED; k->state_last = 0; k->flags = 0; k->error = 0;
@@ -1521,7 +1541,7 @@ __device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
             for (uint32_t i = 0; i < p->nsack; i++) c.g->msack_out[off + i] = sk[i];
             m->sack_off = off;
         }
-        m->pkt = *p;   // packet_copy: the copy starts with one reference (the task's)
+        pkt_copy_rec(&m->pkt, p, c.g->trace);   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
         m->pkt.inq = 0;   // the copy is in no queue of the receiver
         c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
@@ -2003,7 +2023,7 @@ __device__ bool ingest_mail(L& c, int32_t s) {
     const Mail* m = &gl.mail_in[s];
     const int32_t pi = pkt_alloc(c);
     if (pi < 0) return false;
-    *PK(c, pi) = m->pkt;
+    pkt_copy_rec(PK(c, pi), &m->pkt, gl.trace);
     if (m->pkt.nsack) {
         int32_t* sk = PSK(c, pi);
         for (uint32_t i = 0; i < m->pkt.nsack; i++) sk[i] = gl.msack_in[m->sack_off + i];
@@ -2210,7 +2230,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
     TCtl hctl;
-    std::vector<uint64_t> ipk(H);
+    std::vector<uint64_t> ipk;
     uint64_t rounds = 0;
     std::vector<uint64_t> nt(H + 1);
     std::vector<DHost> hout(H);
@@ -2240,8 +2260,18 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         slot[j] = k;
     }
 
-    for (int32_t i = 0; i < H; i++) ipk[i] = ((uint64_t)m->host_ip[i] << 32) | (uint32_t)i;
-    std::sort(ipk.begin(), ipk.end());
+    {   // host_of_ip's table: at most half full; an address's first host wins (host order)
+        uint32_t cap = 64;
+        while (cap < 2u * (uint32_t)H) cap <<= 1;
+        ipk.assign(cap, ~0ull);
+        g.ip_mask = cap - 1;
+        for (int32_t i = 0; i < H; i++) {
+            const uint32_t ip = m->host_ip[i];
+            uint32_t k = ip_slot(ip, g.ip_mask);
+            while (ipk[k] != ~0ull && (uint32_t)(ipk[k] >> 32) != ip) k = (k + 1) & g.ip_mask;
+            if (ipk[k] == ~0ull) ipk[k] = ((uint64_t)ip << 32) | (uint32_t)i;
+        }
+    }
     g.H = H; g.P = P; g.W = W;
     g.end_time = m->end_time; g.hb = m->heartbeat_interval ? m->heartbeat_interval : kSec;
     g.tcp_bytes = m->tcp_bytes; g.trace = (trace & SHD_TCP_TRACE_STATUS) ? 1 : 0;
@@ -2283,8 +2313,8 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
     HCHECK(hipMalloc(&g.ctl, sizeof(TCtl)));
     HCHECK(hipMemset(g.ctl, 0, sizeof(TCtl)));
-    HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * (size_t)H));
-    HCHECK(hipMemcpy(d_ipk, ipk.data(), sizeof(uint64_t) * (size_t)H, hipMemcpyHostToDevice));
+    HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * ipk.size()));
+    HCHECK(hipMemcpy(d_ipk, ipk.data(), sizeof(uint64_t) * ipk.size(), hipMemcpyHostToDevice));
     g.ip_key = d_ipk;
     if (trace & SHD_TCP_TRACE_NODE) {   // every heartbeat before the end, per host
         g.node_k = (uint32_t)((m->end_time - 1) / g.hb) + 1;
