@@ -175,6 +175,9 @@ struct DSock {   // every scalar first (a few lines per socket), then the contai
     int32_t server; uint32_t nkids, npending;
     uint32_t last_peer_ip, last_ip; uint16_t last_peer_port;
     int32_t child, parent, child_state;
+    // the path of this socket's last sent packet (host, vertex pair, latency,
+    // reliability: constant over a run), keyed by its destination address
+    uint32_t pc_ip; int32_t pc_host, pc_va, pc_vb; double pc_lat, pc_rel;
     int32_t kids[kKids], pending[kKids];
     Ring<kQc> outctl;
     THeap<kTimers> timers;
@@ -1515,11 +1518,22 @@ __device__ void if_receive_packets(L& c) {   // :421-455
         refill_if_needed(c);
     }
 }
-__device__ void worker_send_packet(L& c, int32_t pi) {   // worker.c:260-321
+__device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:260-321
     DPkt* p = PK(c, pi);
-    const int32_t d = host_of_ip(c, p->dip);
+    int32_t d;
     double lat, rel;
-    path(c, c.h, d, lat, rel);
+    if (ks->pc_ip != 0 && ks->pc_ip == p->dip) {   // the sending socket's path: no dependent loads
+        d = ks->pc_host;
+        touch_log(c, ks->pc_va, ks->pc_vb);
+        lat = ks->pc_lat; rel = ks->pc_rel;
+    } else {
+        d = host_of_ip(c, p->dip);
+        path(c, c.h, d, lat, rel);
+        if (d >= 0 && lat >= 0.0 && !c.H->err) {
+            ks->pc_ip = p->dip; ks->pc_host = d; ks->pc_va = c.g->hv[c.h]; ks->pc_vb = c.g->hv[d];
+            ks->pc_lat = lat; ks->pc_rel = rel;
+        }
+    }
     const double chance = next_double(&c.H->rng);
     if (chance <= rel || p->len == 0) {
         const uint64_t t = c.now + (uint64_t)ceil(lat * (double)kMs);
@@ -1555,9 +1569,11 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
     const SockLess lt{&c};
     while (H->tx_rem >= kMTU) {
         int32_t pi = -1;
+        DSock* ks = nullptr;   // the socket the packet came from
         while (c.g->qdisc_rr && pi < 0 && H->rrq.n) {   // _networkinterface_selectRoundRobin (:466-490)
             const int32_t si = rg_pop(H->rrq);
             DSock* k = &c.g->sock[si];
+            ks = k;
             pi = sock_remove_output(c, k);
             if (pi >= 0) tcp_about_to_send(c, k, pi);
             if (sock_peek_out(c, k) >= 0) rg_push(H->rrq, si, H->err);
@@ -1565,6 +1581,7 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
         while (pi < 0 && H->fifo.n) {   // _networkinterface_selectFirstInFirstOut (:492-517)
             const int32_t si = ih_pop(H->fifo, lt);
             DSock* k = &c.g->sock[si];
+            ks = k;
             pi = sock_remove_output(c, k);
             if (pi >= 0) tcp_about_to_send(c, k, pi);
             if (sock_peek_out(c, k) >= 0) ih_push(H->fifo, si, lt, H->err);
@@ -1578,7 +1595,7 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
             if (e.time < c.g->end_time) evq_push(c, e);
             else pkt_unref(c, pi);   // scheduler_push refused it: the task's reference goes now
         } else {
-            worker_send_packet(c, pi);
+            worker_send_packet(c, pi, ks);
         }
         consume(H->tx_rem, (uint64_t)PK(c, pi)->len + kHdr);
         refill_if_needed(c);

@@ -60,6 +60,25 @@ def test_tcp_gpu_scaled_model_equals_oracle(hosts, loss):
     assert r["events"] == o["events"] and r["deliveries"] > 0
 
 
+@pytest.mark.parametrize("hosts,loss", [(96, 0.02)])
+def test_tcp_gpu_untraced_run_equals_oracle(hosts, loss):
+    """The bench's mode: no lines written, so the device keeps no status list
+    and copies packet records without it -- the run's end state and event
+    count are still the oracle's, and the tracker's node lines the traced
+    run's."""
+    import workloads as W
+    g, m, ips, procs, peers, nb = W.tcp_echo_model(hosts, 40, end_s=12, nbytes=60000, loss_max=loss)
+    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, trace=False, node=True)
+    t = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, trace=True, node=True)
+    o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb)
+    assert r["lines"] == [] or all(ln[2].startswith("[shadow-heartbeat]") for ln in r["lines"])
+    assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
+    assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
+    assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
+    assert r["events"] == o["events"]
+    assert TC.node_lines(r["node_lines"]) == TC.node_lines(t["node_lines"]) and len(r["node_lines"]) > 0
+
+
 @pytest.mark.parametrize("name", ["geo_pairs", "shared_hosts", "server_first"])
 def test_tcp_gpu_first_touch_order_settles(name):
     """The path tables start from a wrong first-touch order (the clients
