@@ -142,6 +142,10 @@ template <uint32_t N> struct Ring {   // GQueue
     int32_t a[N];
 };
 template <uint32_t N> struct IHeap { uint32_t n; int32_t a[N]; };   // priority_queue.c over indices
+// the same heap over packets ordered by TCP sequence, each entry carrying its
+// key ((seq << 32) | pool index): a level is one load, not an index then the
+// packet's sequence (a packet's sequence does not change while it is queued)
+template <uint32_t N> struct KHeap { uint32_t n, _pad; uint64_t a[N]; };
 template <uint32_t N> struct THeap { uint32_t n; uint64_t a[N]; };  // timer expirations
 struct Rng64 { int64_t a, b; };
 struct RVec { uint32_t n; Rng64 r[kRanges]; };
@@ -182,8 +186,8 @@ struct DSock {   // every scalar first (a few lines per socket), then the contai
     Ring<kQc> outctl;
     THeap<kTimers> timers;
     Tally tally;
-    IHeap<kQ> throttled;
-    IHeap<kQ> unordered;
+    KHeap<kQ> throttled;
+    KHeap<kQ> unordered;
     Ring<kQ> in, out;
     int32_t sacks[kSacks];
     int32_t rtx[kQ]; uint32_t rtxs[kQ];
@@ -344,10 +348,36 @@ template <uint32_t N, class Less> __device__ int32_t ih_pop(IHeap<N>& q, Less lt
     ih_down(q, 0, lt);
     return x;
 }
-struct SeqLess {   // packet_compareTCPSequence (packet.c:207-221)
-    const DPkt* pool;
-    __device__ bool operator()(int32_t a, int32_t b) const { return pool[a].seq < pool[b].seq; }
-};
+// packet_compareTCPSequence (packet.c:207-221) on the entries' keys; the
+// swaps are ih_up's / ih_down's, so ties resolve as the reference heap's do
+__device__ __forceinline__ bool kh_less(uint64_t x, uint64_t y) { return (uint32_t)(x >> 32) < (uint32_t)(y >> 32); }
+template <uint32_t N> __device__ void kh_up(KHeap<N>& q, uint32_t i) {
+    while (i > 0 && kh_less(q.a[i], q.a[(i - 1) / 2])) {
+        const uint64_t t = q.a[i]; q.a[i] = q.a[(i - 1) / 2]; q.a[(i - 1) / 2] = t; i = (i - 1) / 2;
+    }
+}
+template <uint32_t N> __device__ void kh_down(KHeap<N>& q, uint32_t i) {
+    uint32_t ch;
+    while ((ch = 2 * i + 1) < q.n) {
+        if (ch + 1 < q.n && kh_less(q.a[ch + 1], q.a[ch])) ch = ch + 1;
+        if (kh_less(q.a[ch], q.a[i])) { const uint64_t t = q.a[i]; q.a[i] = q.a[ch]; q.a[ch] = t; i = ch; } else break;
+    }
+}
+template <uint32_t N> __device__ bool kh_push_new(KHeap<N>& q, int32_t x, uint32_t seq, uint32_t& err) {
+    if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return false; }
+    q.a[q.n++] = ((uint64_t)seq << 32) | (uint32_t)x;
+    kh_up(q, q.n - 1);
+    return true;
+}
+template <uint32_t N> __device__ __forceinline__ int32_t kh_top(const KHeap<N>& q) { return (int32_t)(uint32_t)q.a[0]; }
+template <uint32_t N> __device__ void kh_pop(KHeap<N>& q) {
+    if (!q.n) return;
+    const uint64_t x = q.a[0];
+    q.a[0] = q.a[q.n - 1];
+    q.a[q.n - 1] = x;
+    q.n--;
+    kh_down(q, 0);
+}
 template <uint32_t N> __device__ void th_push(THeap<N>& q, uint64_t x, uint32_t& err) {
     if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return; }
     uint32_t i = q.n++;
@@ -994,7 +1024,7 @@ __device__ void tcp_autotune_snd(L& c, DSock* k) {   // tcp.c:566-591
 __device__ void tcp_buffer_out(L& c, DSock* k, int32_t pi) {   // tcp.c:729-745
     DPkt* p = PK(c, pi);
     if (p->inq & Q_THROTTLED) return;   // already queued (priority_queue_push's lookup)
-    if (!ih_push_new(k->throttled, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err)) return;
+    if (!kh_push_new(k->throttled, pi, p->seq, c.H->err)) return;
     p->inq |= Q_THROTTLED;
     pkt_ref(c, pi);
     k->throttled_len += PK(c, pi)->len;
@@ -1004,7 +1034,7 @@ __device__ void tcp_buffer_out(L& c, DSock* k, int32_t pi) {   // tcp.c:729-745
 __device__ void tcp_buffer_in(L& c, DSock* k, int32_t pi) {   // tcp.c:747-760
     DPkt* p = PK(c, pi);
     if (p->inq & Q_UNORDERED) return;
-    if (!ih_push_new(k->unordered, pi, SeqLess{c.g->pool + (size_t)c.h * c.g->pool_cap}, c.H->err)) return;
+    if (!kh_push_new(k->unordered, pi, p->seq, c.H->err)) return;
     p->inq |= Q_UNORDERED;
     pkt_ref(c, pi);
     k->unordered_len += PK(c, pi)->len;
@@ -1093,9 +1123,8 @@ template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
             tally_compute_lost(k->tally, c.H->err);
         }
     }
-    const SeqLess lt{c.g->pool + (size_t)c.h * c.g->pool_cap};
     while (k->throttled.n) {
-        const int32_t pi = k->throttled.a[0];
+        const int32_t pi = kh_top(k->throttled);
         DPkt* p = PK(c, pi);
         const uint32_t len = p->len;
         if (len > 0) {
@@ -1103,7 +1132,7 @@ template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
             const bool in_buffer = len <= out_space(k);
             if (!in_buffer || !in_window) break;
         }
-        ih_pop(k->throttled, lt);
+        kh_pop(k->throttled);
         p->inq &= ~Q_THROTTLED;
         k->throttled_len -= len;
         sock_add_output(c, k, pi);
@@ -1111,11 +1140,11 @@ template <bool kOuter> __device__ void tcp_flush_body(L& c, DSock* k) {
         if (p->seq > k->s_highest) k->s_highest = p->seq;
     }
     while (k->unordered.n) {
-        const int32_t pi = k->unordered.a[0];
+        const int32_t pi = kh_top(k->unordered);
         DPkt* p = PK(c, pi);
         if (p->seq == k->r_next && sock_add_input(c, k, pi)) {
             k->r_last_seq = p->seq;
-            ih_pop(k->unordered, lt);
+            kh_pop(k->unordered);
             p->inq &= ~Q_UNORDERED;
             const uint32_t len = p->len;
             pkt_unref(c, pi);
