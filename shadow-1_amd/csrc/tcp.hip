@@ -145,7 +145,7 @@ template <uint32_t N> struct IHeap { uint32_t n; int32_t a[N]; };   // priority_
 // the same heap over packets ordered by TCP sequence, each entry carrying its
 // key ((seq << 32) | pool index): a level is one load, not an index then the
 // packet's sequence (a packet's sequence does not change while it is queued)
-template <uint32_t N> struct KHeap { uint32_t n, _pad; uint64_t a[N]; };
+template <uint32_t N> struct KHeap { uint32_t n, kmax; uint64_t a[N]; };   // kmax >= every key held
 template <uint32_t N> struct THeap { uint32_t n; uint64_t a[N]; };  // timer expirations
 struct Rng64 { int64_t a, b; };
 struct RVec { uint32_t n; Rng64 r[kRanges]; };
@@ -305,6 +305,17 @@ __device__ int32_t rand_r_dev(uint32_t* state) {   // glibc rand_r (random.c's s
     *state = next;
     return result;
 }
+// the state after n steps of rand_r's LCG (x -> 1103515245 x + 12345 mod 2^32)
+// in O(log n): powers of one affine map compose in any order
+__device__ uint32_t lcg_jump(uint32_t x, uint64_t n) {
+    uint32_t a = 1103515245u, b = 12345u, ra = 1u, rb = 0u;
+    for (; n; n >>= 1) {
+        if (n & 1) { ra = a * ra; rb = a * rb + b; }
+        b = a * b + b;
+        a = a * a;
+    }
+    return ra * x + rb;
+}
 __device__ double next_double(uint32_t* s) { return (double)(((double)rand_r_dev(s)) / ((double)2147483647)); }
 
 // ------------------------------------------------------------ heaps (priority_queue.c)
@@ -365,8 +376,10 @@ template <uint32_t N> __device__ void kh_down(KHeap<N>& q, uint32_t i) {
 }
 template <uint32_t N> __device__ bool kh_push_new(KHeap<N>& q, int32_t x, uint32_t seq, uint32_t& err) {
     if (q.n >= N) { err |= SHD_TCP_ERR_QUEUE; return false; }
+    const bool last = q.n == 0 || seq >= q.kmax;   // not below any key: no parent is greater (no swap)
     q.a[q.n++] = ((uint64_t)seq << 32) | (uint32_t)x;
-    kh_up(q, q.n - 1);
+    if (!last) kh_up(q, q.n - 1);
+    if (q.n == 1 || seq > q.kmax) q.kmax = seq;
     return true;
 }
 template <uint32_t N> __device__ __forceinline__ int32_t kh_top(const KHeap<N>& q) { return (int32_t)(uint32_t)q.a[0]; }
@@ -1853,7 +1866,9 @@ __device__ void app_run(L& c, DProc* pr) {
             break;
         }
         case T_CLI_START: {
-            for (uint32_t i = 0; i < N; i++) (void)rand_r_dev(&c.H->rng);   // _fillcharbuf: rand()
+            // _fillcharbuf: N rand() calls whose values nothing reads -- the
+            // state they leave, by a jump of 3N LCG steps (rand_r takes three)
+            c.H->rng = lcg_jump(c.H->rng, 3ull * N);
             const int32_t si = sock_new(c);
             if (si < 0) { pr->step = T_DONE; return; }
             sock_init_tcp(&c.g->sock[si], c.g->recv_buf, c.g->send_buf, c.g->tcp_window);
