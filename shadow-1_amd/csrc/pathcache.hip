@@ -96,14 +96,15 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              const int32_t* __restrict__ attached, const int32_t* __restrict__ self_eid,
                              shd_pv* __restrict__ out,
                              int64_t* __restrict__ stats, uint64_t* dist, int32_t* parent,
-                             uint16_t* upd, int* flags /* LDS int[4] */) {
+                             uint16_t* upd, int* flags /* LDS int[4] */,
+                             const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
     const int tid = threadIdx.x;
     for (int32_t v = tid; v < V; v += BLOCK) {
         dist[v] = kDistInf;
         parent[v] = -1;
         upd[v] = 0xFFFF;
     }
-    if (tid < 3) flags[tid] = 0;
+    if (tid < 4) flags[tid] = 0;
     __syncthreads();
     if (tid == 0) { dist[src] = 0; upd[src] = 0; }
     __syncthreads();
@@ -187,7 +188,11 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     // (Round 1 scanned every vertex's in-arcs, lane per vertex: uncoalesced,
     // 9.7 of the 29 ms of the 10 k-row table.)
     int64_t my_ties = 0;
-    {
+    if (fpar) {
+        // the row's parents given (k_sssp_tie_parents: igraph's first relaxer
+        // in its heap's pop order, for a row with equal-cost predecessors)
+        for (int32_t v = tid; v < V; v += BLOCK) parent[v] = fpar[v];
+    } else {
         uint32_t* cnt2 = (uint32_t*)upd;   // two 16-bit counts per word (the BF stamps are done with)
         for (int32_t w = tid; w < (V + 1) / 2; w += BLOCK) cnt2[w] = 0;
         __syncthreads();
@@ -239,9 +244,24 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             if (nbest > 1) my_ties++;
         }
     }
-    if (my_ties) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)my_ties);
-    if (tid == 0) atomicMax((unsigned long long*)&stats[2], (unsigned long long)it);
+    if (my_ties) {
+        atomicAdd((unsigned long long*)&stats[0], (unsigned long long)my_ties);
+        flags[3] = 1;
+    }
+    if (tid == 0 && !fpar) atomicMax((unsigned long long*)&stats[2], (unsigned long long)it);
     __syncthreads();
+    // A vertex with several exact predecessors at the same smallest d[u] (equal-
+    // cost paths, or parallel edges) takes its parent from the heap's pop order
+    // in igraph's Dijkstra, which the rule above does not see: the row is listed
+    // for k_sssp_tie_parents and finished by a second pass with those parents.
+    if (tie_rows) {
+        const bool tie_row = flags[3] != 0;
+        __syncthreads();
+        if (tie_row) {
+            if (tid == 0) tie_rows[atomicAdd((unsigned long long*)&stats[6], 1ull)] = row;
+            return;
+        }
+    }
 
 #if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 2
     return;
@@ -411,17 +431,21 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
-    int64_t* __restrict__ stats, int32_t row0, int32_t row1) {
+    int64_t* __restrict__ stats, int32_t row0, int32_t row1, const int32_t* __restrict__ row_list,
+    const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint64_t* dist = (uint64_t*)smem;
     int32_t* parent = (int32_t*)(smem + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(smem + (size_t)12 * V);
     int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
-    for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
+    // row_list: the second pass over listed rows [row0, row1) of it, parents from fpar
+    for (int32_t i = row0 + (int32_t)blockIdx.x; i < row1; i += gridDim.x) {
+        const int32_t row = row_list ? row_list[i] : i;
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
-                            parent, upd, flags);
+                            parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows);
+    }
 }
 
 template <int BLOCK>
@@ -434,18 +458,140 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     const double* __restrict__ eloss,
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
-    int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block, int32_t row0, int32_t row1) {
+    int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block, int32_t row0, int32_t row1,
+    const int32_t* __restrict__ row_list, const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
     __shared__ int flags[4];
     char* base = scratch + per_block * blockIdx.x;
     uint64_t* dist = (uint64_t*)base;
     int32_t* parent = (int32_t*)(base + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(base + (size_t)12 * V);
-    for (int32_t row = row0 + (int32_t)blockIdx.x; row < row1; row += gridDim.x)
+    for (int32_t i = row0 + (int32_t)blockIdx.x; i < row1; i += gridDim.x) {
+        const int32_t row = row_list ? row_list[i] : i;
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
-                            parent, upd, flags);
+                            parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows);
+    }
 }
+
+// ------------------------------------------------------------------ tie rows
+// igraph 0.7.1's igraph_get_shortest_paths_dijkstra, restated for the rows that
+// have equal-cost predecessors (o_pathcache.c:156-202 is the oracle's copy):
+// an indexed binary max-heap on -distance (igraph_2wheap_t), arcs relaxed in
+// igraph_incident(OUT) order (the CSR keeps it; self-loops, which never
+// improve a distance, are dropped), the first finite distance or a strictly
+// shorter one setting the parent.  So a vertex's parent is its first exact
+// predecessor in relaxation order, and among predecessors at one distance that
+// order is the heap's.  Every row runs to an empty heap (igraph stops once
+// every target is popped; the parents on a target's path are final by then
+// either way).  One lane per row, kTieLanes rows per wave (a wave per 16 rows:
+// more waves in flight for a latency-bound walk, less divergence per wave);
+// the lane's dist and heap live in global scratch with the lane as the
+// fastest index, so the heap's top levels, which every lane walks, share lines.  Sifts move a hole instead
+// of swapping: the same final arrangement as igraph_2wheap_switch steps.
+struct TieLane {
+    double* dist;      // [V] lane-strided, -1 = unreached
+    double* hdat;      // [V] heap values (-distance)
+    int32_t* hidx;     // [V] heap position -> vertex
+    int32_t* hidx2;    // [V] vertex -> heap position + 2
+};
+constexpr int kTieLanes = 16;
+#define TL(p, i) (p)[(size_t)(i) * kTieLanes]
+
+__device__ __forceinline__ void tie_shift_up(TieLane& h, int32_t elem, double val, int32_t id) {
+    while (elem != 0) {
+        const int32_t par = (elem + 1) / 2 - 1;
+        const double pv = TL(h.hdat, par);
+        if (val < pv) break;   // igraph_2wheap_shift_up: stop at the top or below a larger parent
+        const int32_t pid = TL(h.hidx, par);
+        TL(h.hdat, elem) = pv;
+        TL(h.hidx, elem) = pid;
+        TL(h.hidx2, pid) = elem + 2;
+        elem = par;
+    }
+    TL(h.hdat, elem) = val;
+    TL(h.hidx, elem) = id;
+    TL(h.hidx2, id) = elem + 2;
+}
+
+// igraph_2wheap_sink from `head` holding (val, id); returns its final position
+__device__ __forceinline__ int32_t tie_sink(TieLane& h, int32_t size, int32_t head, double val, int32_t id) {
+    for (;;) {
+        const int32_t l = 2 * head + 1, r = 2 * head + 2;
+        if (l >= size) break;
+        const double dl = TL(h.hdat, l);
+        int32_t c = l;
+        double dc = dl;
+        if (r != size) {
+            const double dr = TL(h.hdat, r);
+            if (!(dl >= dr)) { c = r; dc = dr; }
+        }
+        if (!(val < dc)) break;
+        const int32_t cid = TL(h.hidx, c);
+        TL(h.hdat, head) = dc;
+        TL(h.hidx, head) = cid;
+        TL(h.hidx2, cid) = head + 2;
+        head = c;
+    }
+    TL(h.hdat, head) = val;
+    TL(h.hidx, head) = id;
+    TL(h.hidx2, id) = head + 2;
+    return head;
+}
+
+__global__ __launch_bounds__(kTieLanes) void k_sssp_tie_parents(
+    int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
+    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, char* __restrict__ scratch) {
+    const int32_t slot = (int32_t)blockIdx.x * kTieLanes + (int32_t)threadIdx.x;
+    if (slot >= n) return;
+    char* wbase = scratch + (size_t)blockIdx.x * kTieLanes * (size_t)V * 24;
+    TieLane h;
+    h.dist = (double*)wbase + threadIdx.x;
+    h.hdat = (double*)(wbase + (size_t)kTieLanes * V * 8) + threadIdx.x;
+    h.hidx = (int32_t*)(wbase + (size_t)kTieLanes * V * 16) + threadIdx.x;
+    h.hidx2 = (int32_t*)(wbase + (size_t)kTieLanes * V * 20) + threadIdx.x;
+    int32_t* par = fpar + (size_t)slot * V;
+    for (int32_t v = 0; v < V; v++) {
+        TL(h.dist, v) = -1.0;
+        par[v] = -1;
+    }
+    const int32_t src = attached[rows[slot]];
+    TL(h.dist, src) = 0.0;
+    int32_t size = 1;
+    TL(h.hdat, 0) = 0.0;
+    TL(h.hidx, 0) = src;
+    TL(h.hidx2, src) = 2;
+    while (size > 0) {
+        // igraph_2wheap_max_index + igraph_2wheap_delete_max
+        const int32_t u = TL(h.hidx, 0);
+        const double mindist = -TL(h.hdat, 0);
+        size--;
+        if (size > 0) (void)tie_sink(h, size, 0, TL(h.hdat, size), TL(h.hidx, size));
+        const int32_t kb = arc_off[u], ke = arc_off[u + 1];
+        for (int32_t k = kb; k < ke; k++) {
+            const int32_t x = arc_dst[k];
+            const double alt = mindist + arc_w[k];
+            const double cur = TL(h.dist, x);
+            if (cur < 0) {                 // the first finite distance: push
+                TL(h.dist, x) = alt;
+                par[x] = arc_rin[k];
+                tie_shift_up(h, size, -alt, x);
+                size++;
+            } else if (alt < cur) {        // strictly shorter: igraph_2wheap_modify
+                TL(h.dist, x) = alt;
+                par[x] = arc_rin[k];
+                // data[pos] = -alt; sink(pos); shift_up(pos) -- the shift starts at
+                // pos again, with whatever the sink left there (the element itself:
+                // a larger value never sinks)
+                const int32_t pos = TL(h.hidx2, x) - 2;
+                (void)tie_sink(h, size, pos, -alt, x);
+                tie_shift_up(h, pos, TL(h.hdat, pos), TL(h.hidx, pos));
+            }
+        }
+    }
+}
+#undef TL
 
 // ------------------------------------------------------------------ direct
 // _topology_lookupDirectPath (topology.c:1877-1927) for every attached pair;
@@ -540,7 +686,7 @@ static void pc_free_device(shd_pc* pc) {
                     pc->d_rin_w, pc->d_rin_r, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
                     pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                     pc->d_dir, pc->d_self, pc->d_adj,
-                    pc->d_scratch, pc->d_stats};
+                    pc->d_scratch, pc->d_stats, pc->d_tie_rows, pc->d_tie_scratch};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -635,7 +781,8 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
         return SHD_ENOMEM;
     }
     if (pc->rows_mode) {
-        if (hipMalloc((void**)&pc->d_row, sizeof(shd_pv) * TT) != hipSuccess) {
+        if (hipMalloc((void**)&pc->d_row, sizeof(shd_pv) * TT) != hipSuccess ||
+            hipMalloc((void**)&pc->d_tie_rows, sizeof(int32_t) * T) != hipSuccess) {
             shd_pc_destroy(pc);
             return SHD_ENOMEM;
         }
@@ -655,6 +802,69 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
 constexpr int kRowBlock = SHD_ROW_BLOCK;   // workgroup of the LDS row kernel past 2 k vertices
 static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
 static constexpr size_t kLdsMax = 160 * 1024;
+
+// The rows the first pass listed (equal-cost predecessors somewhere in the
+// row): their parents from k_sssp_tie_parents, in chunks of rows whose heaps
+// fit a bounded scratch, then the row kernel again with those parents.
+static int finish_tie_rows(shd_pc* pc, int ncu) {
+    hipStream_t s = pc->stream;
+    const int32_t V = pc->V, T = pc->T;
+    int64_t n = 0;
+    SHD_HIP(hipMemcpyAsync(&n, pc->d_stats + 6, sizeof(n), hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    pc->info.n_tie_rows = (int32_t)n;
+    if (n <= 0) return SHD_OK;
+    if (n > T) return SHD_ERANGE;
+    // 24 B of lane scratch + 4 B of parents per vertex and row; <= 4 GiB a chunk
+    // (every row of a 10 k-vertex graph at once)
+    const size_t per_row = (size_t)V * 28;
+    int64_t chunk = std::max<int64_t>(kTieLanes, (int64_t)(((size_t)4 << 30) / per_row) / kTieLanes * kTieLanes);
+    chunk = std::min<int64_t>(chunk, (n + kTieLanes - 1) / kTieLanes * kTieLanes);
+    const size_t need_s = (size_t)chunk * V * 24, need_p = (size_t)chunk * V * 4;
+    if (!pc->d_tie_scratch || pc->tie_scratch_bytes < need_s + need_p) {
+        if (pc->d_tie_scratch) (void)hipFree(pc->d_tie_scratch);
+        pc->d_tie_scratch = nullptr;
+        pc->tie_scratch_bytes = 0;
+        SHD_HIP(hipMalloc(&pc->d_tie_scratch, need_s + need_p));
+        pc->tie_scratch_bytes = need_s + need_p;
+    }
+    char* scr = (char*)pc->d_tie_scratch;
+    int32_t* fpar = (int32_t*)(scr + need_s);
+    const size_t lds = lds_bytes_for(V);
+    for (int64_t c0 = 0; c0 < n; c0 += chunk) {
+        const int32_t cn = (int32_t)std::min<int64_t>(chunk, n - c0);
+        const int32_t* rows = pc->d_tie_rows + c0;
+        hipLaunchKernelGGL(k_sssp_tie_parents, dim3((cn + kTieLanes - 1) / kTieLanes), dim3(kTieLanes), 0, s, V, cn,
+                           rows, pc->d_attached,
+                           pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar, scr);
+        SHD_HIP(hipGetLastError());
+        if (lds <= kLdsMax && V <= 2048) {
+            const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, kLdsMax / lds));
+            const int grid = std::max(1, std::min(cn, ncu * per_cu));
+            hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
+                               pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
+                               pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
+                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr);
+        } else if (lds <= kLdsMax) {
+            const int grid = std::max(1, std::min(cn, ncu));
+            hipLaunchKernelGGL(k_sssp_rows_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds, s, V, T, pc->d_arc_off,
+                               pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
+                               pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
+                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr);
+        } else {
+            // the first pass sized d_scratch for ncu * 4 blocks
+            const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
+            const int grid = (int)std::max<size_t>(1, std::min<size_t>((size_t)cn, pc->scratch_bytes / per_block));
+            hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
+                               pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
+                               pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
+                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, (char*)pc->d_scratch, per_block,
+                               0, cn, rows, fpar, nullptr);
+        }
+        SHD_HIP(hipGetLastError());
+    }
+    return SHD_OK;
+}
 
 // the build; with a communicator this rank computes its block of source
 // rows and the blocks are all-gathered (shd_pc_build_sharded)
@@ -707,7 +917,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
-                                   pc->d_row, pc->d_stats, row0, row1);
+                                   pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows);
             } else {
                 int grid = std::max(1, std::min(row1 - row0, ncu));
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<kRowBlock>,
@@ -716,7 +926,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
-                                   pc->d_row, pc->d_stats, row0, row1);
+                                   pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows);
             }
         } else {
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -729,9 +939,12 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
             hipLaunchKernelGGL(k_sssp_rows_global<512>, dim3(grid), dim3(512), 0, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
                                pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
-                               pc->d_stats, (char*)pc->d_scratch, per_block, row0, row1);
+                               pc->d_stats, (char*)pc->d_scratch, per_block, row0, row1, nullptr, nullptr,
+                               pc->d_tie_rows);
         }
         SHD_HIP(hipGetLastError());
+        const int rc = finish_tie_rows(pc, ncu);
+        if (rc) { for (auto& e : ev) (void)hipEventDestroy(e); return rc; }
     }
     SHD_HIP(hipEventRecord(ev[2], s));
     if (comm && pc->rows_mode && W > 1) {
@@ -768,8 +981,10 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
             st[2] = std::max(st[2], o[2]);
             st[3] += o[3];
             st[4] += o[4];
+            st[6] += o[6];
         }
     }
+    pc->info.n_tie_rows = (int32_t)st[6];
     pc->info.rows_computed = pc->rows_mode ? T : 0;
     pc->info.n_ties = st[0];
     pc->info.max_hops = (int32_t)st[1];

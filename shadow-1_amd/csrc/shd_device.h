@@ -63,7 +63,10 @@ struct shd_pc {
     uint8_t* d_adj = nullptr;           // [T][T] 1 = adjacent (direct path exists)
     void* d_scratch = nullptr;          // global-memory SSSP scratch (large V)
     size_t scratch_bytes = 0;
-    int64_t* d_stats = nullptr;         // ties, max hops, max iters, unroutable, lat mismatch, minlat bits
+    int32_t* d_tie_rows = nullptr;      // [T] rows with equal-cost predecessors (first pass)
+    void* d_tie_scratch = nullptr;      // k_sssp_tie_parents: lane heaps + parents
+    size_t tie_scratch_bytes = 0;
+    int64_t* d_stats = nullptr;         // ties, max hops, max iters, unroutable, lat mismatch, minlat bits, tie rows
     bool built = false;
     shd_pc_info info{};
     // host lazy-cache adapter state (shd_pc_lookup)

@@ -50,8 +50,11 @@ def bundled_graph():
 
 def geometric_graph(n_vertices: int, seed: int = 1, radius_factor: float = 1.5,
                     loss_max: float = 0.01, self_loops: bool = True,
-                    vertex_loss: bool = False, max_tries: int = 20) -> S.GraphArrays:
-    """Random geometric graph in the unit square; connected (retries seeds)."""
+                    vertex_loss: bool = False, max_tries: int = 20,
+                    integer_latency: bool = False) -> S.GraphArrays:
+    """Random geometric graph in the unit square; connected (retries seeds).
+    integer_latency: whole milliseconds (ceil), as Shadow topologies usually
+    have them -- equal-cost paths everywhere."""
     rng = np.random.default_rng(seed)
     V = int(n_vertices)
     r = radius_factor * math.sqrt(math.log(max(V, 2)) / (math.pi * max(V, 2)))
@@ -104,12 +107,16 @@ def geometric_graph(n_vertices: int, seed: int = 1, radius_factor: float = 1.5,
         raise RuntimeError("could not generate a connected geometric graph")
     dist = np.hypot(pts[src, 0] - pts[dst, 0], pts[src, 1] - pts[dst, 1])
     lat = 1.0 + 50.0 * dist
+    if integer_latency:
+        lat = np.ceil(lat)
     loss = rng.random(len(src)) * loss_max
     # document order: shuffle edges so ids are not sorted by endpoint
     perm = rng.permutation(len(src))
     src, dst, lat, loss = src[perm], dst[perm], lat[perm], loss[perm]
     if self_loops:
         sl_lat = 1.0 + 50.0 * r * rng.random(V) + 0.5
+        if integer_latency:
+            sl_lat = np.ceil(sl_lat)
         sl_loss = rng.random(V) * loss_max
         src = np.concatenate([src, np.arange(V)])
         dst = np.concatenate([dst, np.arange(V)])
@@ -117,6 +124,33 @@ def geometric_graph(n_vertices: int, seed: int = 1, radius_factor: float = 1.5,
         loss = np.concatenate([loss, sl_loss])
     vl = rng.random(V) * 0.001 if vertex_loss else None
     return S.GraphArrays(V, src, dst, lat, loss, vl)
+
+
+def grid_graph(side: int = 6, seed: int = 5, loss_max: float = 0.05, directed: bool = False,
+               parallel: bool = False) -> S.GraphArrays:
+    """side x side grid, every edge (and self-loop) 1 ms: equal-cost paths
+    between almost every pair, edge loss U[0, loss_max], edges in a shuffled
+    document order.  directed: every edge both ways, each with its own loss;
+    parallel: a second copy of every tenth edge (equal latency, its own loss)."""
+    rng = np.random.default_rng(seed)
+    src, dst = [], []
+    for y in range(side):
+        for x in range(side):
+            v = y * side + x
+            if x + 1 < side:
+                src.append(v); dst.append(v + 1)
+            if y + 1 < side:
+                src.append(v); dst.append(v + side)
+    if directed:
+        src, dst = src + dst, dst + src
+    if parallel:
+        src += src[::10]; dst += dst[::10]
+    V = side * side
+    src += list(range(V))
+    dst += list(range(V))
+    perm = rng.permutation(len(src))
+    src, dst = np.array(src)[perm], np.array(dst)[perm]
+    return S.GraphArrays(V, src, dst, np.ones(len(src)), rng.random(len(src)) * loss_max, directed=directed)
 
 
 def seed_chain(n_hosts: int, options_seed: int = 1) -> np.ndarray:

@@ -25,7 +25,11 @@ order; its own first touches come back (o_state_take_touches), and the
 engine's resolution ranks both (shd_eng_resolve over the union).  On the
 directed graph below a pair's orientations are different paths with different
 latencies: without the protocol the co-simulation diverges from the serial run
-(checked).  (On an undirected tie-free graph the two rows of a pair differ in
+(checked).  The grid (workloads.grid_graph: every edge 1 ms) has equal-cost
+paths between almost every pair, so each endpoint's Dijkstra takes its own
+path, with its own reliability: there the path cache's tie rows
+(k_sssp_tie_parents, igraph's heap order) and the one-cache protocol are both
+on the line.  (On an undirected tie-free graph the two rows of a pair differ in
 the last bits of their folds only, which a PHOLD delivery almost never sees.)
 """
 import ctypes as C
@@ -59,7 +63,7 @@ def directed_graph(V=36, seed=5, loss_max=0.01):
 
 
 def model(n_hosts=300, seed=3, graph="bundled", **kw):
-    g = W.bundled_graph() if graph == "bundled" else directed_graph()
+    g = {"bundled": W.bundled_graph, "directed": directed_graph, "grid": W.grid_graph}[graph]()
     hv = np.sort(np.random.default_rng(seed).integers(0, g.n_vertices, n_hosts)).astype(np.int32)
     kw.setdefault("load", 8)
     m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, **kw)
@@ -127,12 +131,13 @@ def cosim(m, g, cut, one_cache=True):
 @pytest.mark.parametrize("graph,cut,kw", [("bundled", 120, {}), ("bundled", 1, {}), ("bundled", 299, {}),
                                           ("bundled", 70, dict(load=24, payload=1000, bw_down=200, bw_up=100000,
                                                                codelq_cap=256, queue_flags=S.SHD_QF_TRACE_STATUS)),
-                                          ("directed", 120, {}), ("directed", 1, {}), ("directed", 299, {})])
+                                          ("directed", 120, {}), ("directed", 1, {}), ("directed", 299, {}),
+                                          ("grid", 120, {}), ("grid", 1, {}), ("grid", 299, {})])
 def test_engine_exchanges_packets_with_cpu_side_hosts(graph, cut, kw):
     g, m = model(graph=graph, **kw)
     (gtr, gdg, ctr, cdg), n = cosim(m, g, cut)
     assert n["ingress"] > 50 and n["egress"] > 50 and n["rounds"] > 100
-    if graph == "directed":   # both sides touch first, on a graph where it matters
+    if graph != "bundled":   # both sides touch first, on a graph where it matters
         assert n["engine_touches"] > 0 and n["cpu_touches"] > 0
     assert union_equal(m, g, cut, gtr, gdg, ctr, cdg)
     if kw:
@@ -191,7 +196,7 @@ class Bridge(C.Structure):
                 ("touches_out", TOUT)]
 
 
-@pytest.mark.parametrize("graph,one_cache", [("bundled", False), ("directed", True)])
+@pytest.mark.parametrize("graph,one_cache", [("bundled", False), ("directed", True), ("grid", True)])
 def test_bridged_policy_exchanges_packets_in_shadows_round_loop(graph, one_cache):
     import test_boundary_gpu as B
     h, t = B.libs()

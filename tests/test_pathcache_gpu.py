@@ -76,7 +76,7 @@ def test_geometric_rows_bit_exact(V, seed, vloss):
     pc = PathCache(g, att)
     info = pc.info()
     assert info.is_complete == 0 and info.rows_computed == V
-    assert info.n_ties == 0
+    assert info.n_ties == 0 and info.n_tie_rows == 0   # tie-free: one pass, no heap rerun
     rows = list(range(0, V, max(1, V // 64))) + [V - 1]
     lat, rel = pc.rows()
     olat, orel, ties = oracle_rows(g, att, rows)
@@ -108,6 +108,67 @@ def test_lazy_lookup_first_touch_matches_reference_cache():
     rng = np.random.default_rng(1)
     for _ in range(3000):
         s, d = (int(x) for x in rng.integers(0, 400, 2))
+        a = pc.lookup(s, d)
+        b = ot.get(s, d)
+        assert np.array(a).view(np.uint64).tolist() == np.array(b).view(np.uint64).tolist(), (s, d)
+
+
+# Graphs with equal-cost paths (integer latencies, grids, parallel edges): a
+# vertex's parent is its first exact predecessor in the igraph heap's pop
+# order, which the row kernel's rule (smallest d[u], then lowest edge id) does
+# not see; such rows are rerun through k_sssp_tie_parents (the restated
+# igraph_2wheap Dijkstra) and must equal the oracle bit for bit.
+TIE_GRAPHS = {
+    "grid6": lambda: W.grid_graph(6),
+    "grid6_directed": lambda: W.grid_graph(6, directed=True),
+    "grid6_parallel": lambda: W.grid_graph(6, parallel=True),
+    "grid30": lambda: W.grid_graph(30, seed=2),
+    "geo_int_300": lambda: W.geometric_graph(300, seed=3, integer_latency=True),
+    "geo_int_2000_vloss": lambda: W.geometric_graph(2000, seed=4, integer_latency=True, vertex_loss=True),
+    "geo_int_5000": lambda: W.geometric_graph(5000, seed=6, integer_latency=True),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TIE_GRAPHS))
+def test_tie_rows_bit_exact(name):
+    g = TIE_GRAPHS[name]()
+    V = g.n_vertices
+    att = np.arange(V, dtype=np.int32)
+    pc = PathCache(g, att)
+    info = pc.info()
+    assert info.rows_computed == V and info.n_ties > 0 and info.n_tie_rows > 0
+    rows = list(range(V)) if V <= 1000 else list(range(0, V, max(1, V // 97))) + [V - 1]
+    lat, rel = pc.rows()
+    olat, orel, ties = oracle_rows(g, att, rows)
+    if len(rows) == V:
+        assert info.n_ties == ties
+    assert same_bits(lat[rows], olat) and same_bits(rel[rows], orel)
+
+
+def test_tie_rows_global_scratch_path_and_subset():
+    # V above the LDS capacity: both passes on the global-memory row kernel
+    V = 12500
+    g = W.geometric_graph(V, seed=8, integer_latency=True)
+    rng = np.random.default_rng(2)
+    att = np.sort(rng.choice(V, 240, replace=False)).astype(np.int32)
+    pc = PathCache(g, att)
+    info = pc.info()
+    assert info.n_tie_rows > 0
+    lat, rel = pc.rows()
+    rows = list(range(0, len(att), 7))
+    olat, orel, _ = oracle_rows(g, att, rows)
+    assert same_bits(lat[rows], olat) and same_bits(rel[rows], orel)
+
+
+def test_tie_graph_lazy_lookup_matches_reference_cache():
+    g = W.grid_graph(12, seed=4)
+    V = g.n_vertices
+    att = np.arange(V, dtype=np.int32)
+    pc = PathCache(g, att)
+    ot = O.OTopo(O.OGraph(g), att)
+    rng = np.random.default_rng(5)
+    for _ in range(2000):
+        s, d = (int(x) for x in rng.integers(0, V, 2))
         a = pc.lookup(s, d)
         b = ot.get(s, d)
         assert np.array(a).view(np.uint64).tolist() == np.array(b).view(np.uint64).tolist(), (s, d)

@@ -9,8 +9,9 @@ queries in ONE serial order (event_compare's key); the product cache gets the
 engine's touches of each window up front and the CPU side's queries one event
 at a time.  The CPU side's values must be the oracle's bit for bit, and the
 first touches it reports must be exactly the queries that ran a row in the
-oracle.  On the directed graph (tests/test_ingress_gpu.py) which endpoint
-ranks first decides a pair's value.
+oracle.  On the directed graph (tests/test_ingress_gpu.py) and on the grid
+(equal-cost paths: each endpoint's row takes its own, with its own
+reliability) which endpoint ranks first decides a pair's value.
 """
 import ctypes as C
 
@@ -41,9 +42,10 @@ def _records(rng, n, t0, hosts, T):
     return r
 
 
+@pytest.mark.parametrize("graph", ["directed", "grid"])
 @pytest.mark.parametrize("seed", [11, 12])
-def test_pc_touch_protocol_is_one_serial_cache(seed):
-    g = directed_graph()
+def test_pc_touch_protocol_is_one_serial_cache(seed, graph):
+    g = directed_graph() if graph == "directed" else W.grid_graph()
     rng = np.random.default_rng(seed)
     hv = np.sort(rng.integers(0, g.n_vertices, 40)).astype(np.int32)
     att = W.attached_vertices(hv)
