@@ -71,6 +71,10 @@ def parse():
     ap.add_argument("--relays", type=int, default=6500)
     ap.add_argument("--clients", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-reference-cpu", action="store_true",
+                    help="skip timing the reference's own serial loop (oracle/_ref/libshdref_loop.so)")
+    ap.add_argument("--reference-window-ms", type=int, nargs=2, default=[1100, 1200],
+                    help="the simulated window [t0, t1) over which the reference's own loop is timed")
     ap.add_argument("--cpu-sample-steps", type=int, default=0,
                     help="timed steps the CPU baseline runs (0 = all of them: the same window as value)")
     ap.add_argument("--exchange", choices=["p2p", "rccl", "torch"], default="p2p",
@@ -362,6 +366,8 @@ def main():
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_baseline = cpu_leg(args, S, W, g, model, step, value)
+        if args.workload == "c3" and not args.no_reference_cpu:
+            cpu_baseline["reference"] = reference_leg(args, S, W, g, host_vertex)
 
     if rank == 0:
         out = {
@@ -628,6 +634,58 @@ def cpu_leg(args, S, W, g, model, step, value):
             "gpu_over_cpu_parallel": round(value / par, 1) if par else None,
             "warmup_s": round((b["rows_ms"] + b["warmup_ms"]) * 1e-3, 2),
             "apsp_rows_all_cores_s": round(b["rows_ms"] * 1e-3, 2)}
+
+
+def reference_leg(args, S, W, g, host_vertex):
+    """The reference's OWN serial scheduler loop timed on this box's host cores
+    (BASELINE north_star: "the reference Shadow CPU scheduler timed on the box's
+    own host cores"): oracle/_ref/libshdref_loop.so is Shadow's worker.c,
+    scheduler.c (SP_SERIAL_GLOBAL, --workers 0, slave.c:415-428), host.c,
+    network_interface.c, router*.c, tracker.c, packet.c and the descriptors
+    compiled unmodified from the reference tree in the build container (it
+    travels prebuilt; test doubles only for what the image cannot compile,
+    oracle/ref_harness/ref_loop.c).  A bounded sample of the headline workload:
+    the same C3 model, its loop timed over the simulated window
+    --reference-window-ms (wall clock between the first sends at or after each
+    end), the path cache's rows computed on all cores beforehand (the lazy
+    cache's double serves them; Dijkstra is the APSP metric, timed apart).  The
+    port (oracle/o_engine.c) is timed on the same window beside it; the packet
+    events of the window are the port's count (the two loops' end states are
+    equal, tests/test_ref_loop_cpu.py and ref_loop.json)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    t0_ms, t1_ms = args.reference_window_ms
+    t0, t1 = t0_ms * S.SHD_MS, t1_ms * S.SHD_MS
+    res = {"value": None, "unit": "packet events/s", "cores": 1, "kind": "reference"}
+    try:
+        import oracle_ffi as O
+        import ref_loop_ffi as R
+        if not R.available():
+            res["sample"] = "oracle/_ref/libshdref_loop.so not built"
+            return res
+        m = W.phold_model(host_vertex, end_time=t1 + S.SHD_MS, seed=args.seed, load=args.load, payload=args.payload)
+        thr = cpu_threads()
+        tw = time.perf_counter()
+        r = R.run(m, g, quiet=True, marks=(t0, t1), row_threads=thr)
+        wall = time.perf_counter() - tw
+        ref_s = r["mark_wall_s"][1] - r["mark_wall_s"][0]
+        b = O.baseline(m, g, t0, t1, thr)
+    except Exception as ex:   # noqa: BLE001 -- reported, never substituted
+        res["sample"] = f"reference loop unavailable: {ex}"
+        return res
+    pkt = int(b["serial_pkt_events"])
+    port = pkt / (b["serial_ms"] * 1e-3) if b["serial_ms"] > 0 else None
+    res.update({
+        "value": round(pkt / ref_s, 1) if ref_s > 0 else None,
+        "sample": "the reference's own serial loop (oracle/_ref/libshdref_loop.so: worker.c, scheduler.c "
+                  "SP_SERIAL_GLOBAL, host.c, network_interface.c, router*.c, tracker.c, packet.c compiled "
+                  "unmodified; debug records filtered as at the default log level) on the bench's C3 model "
+                  "(%d hosts, %d-vertex graph, load %d), timed over simulated [%g s, %g s): %d packet events "
+                  "in %.2f s; path-cache rows precomputed on %d cores (%.1f s, not in the window)"
+                  % (len(host_vertex), g.n_vertices, args.load, t0 / 1e9, t1 / 1e9, pkt, ref_s, thr, r["rows_s"]),
+        "port_same_window": {"value": round(port, 1) if port else None, "cores": 1, "kind": "port"},
+        "reference_over_port": round((pkt / ref_s) / port, 4) if port and ref_s > 0 else None,
+        "run_s": round(wall, 1)})
+    return res
 
 
 if __name__ == "__main__":

@@ -87,6 +87,8 @@ o_topo* o_topo_new(const o_graph* g, const int32_t* attached, int32_t n_attached
 void o_topo_free(o_topo* t);
 /* precomputed rows by vertex ([V] pointers, NaN latency = no path) */
 void o_topo_set_row_cache(o_topo* t, double** row_lat, double** row_rel);
+/* every attached vertex's row on `threads` cores, owned by the cache */
+void o_topo_precompute_rows(o_topo* t, int threads);
 int32_t o_topo_n_targets(const o_topo* t);
 const int32_t* o_topo_targets(const o_topo* t);
 int o_topo_is_complete(const o_topo* t);

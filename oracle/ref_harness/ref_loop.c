@@ -53,6 +53,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <sys/epoll.h>
+#include <time.h>
 
 #include "main/core/logger/shadow_logger.h"
 #include "main/core/scheduler/scheduler.h"
@@ -106,6 +107,9 @@ typedef struct ref_loop_cfg {
     /* 1: --interface-qdisc=rr (options.c:162; round-robin over the sockets
      * that want to send, network_interface.c:466-490) instead of fifo */
     int32_t qdisc_rr;
+    /* wall-clock marks (bench.py's reference CPU baseline): the monotonic clock
+     * at the first path lookup (a send) at simulated time >= mark_time[k]; 0 = off */
+    uint64_t mark_time[2];
 } ref_loop_cfg;
 
 typedef struct ref_loop_out {
@@ -116,6 +120,7 @@ typedef struct ref_loop_out {
     uint64_t* next_event_id;      /* [H] host_getNewEventID at the end */
     uint64_t* next_packet_id;     /* [H] */
     uint32_t* rng_probe;          /* [H] random_rand of the host RNG at the end */
+    double mark_wall_s[2];        /* monotonic seconds at mark_time[k] (0 if never reached) */
 } ref_loop_out;
 
 static const ref_loop_cfg* g_cfg;
@@ -142,7 +147,18 @@ void slave_incrementPluginError(Slave* slave) {}
 
 static int32_t host_index_of(GQuark id) { return (int32_t)id - 1; }
 
+static void note_marks(void) {
+    for (int k = 0; k < 2; k++) {
+        if (!g_out || !g_cfg->mark_time[k] || g_out->mark_wall_s[k] != 0) continue;
+        if (worker_getCurrentTime() < g_cfg->mark_time[k]) continue;
+        struct timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        g_out->mark_wall_s[k] = (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+    }
+}
+
 static int path_of(Address* a, Address* b, double* lat, double* rel) {
+    note_marks();
     const int32_t ha = host_index_of((GQuark)address_getID(a)), hb = host_index_of((GQuark)address_getID(b));
     if (ha < 0 || hb < 0 || ha >= g_cfg->n_hosts || hb >= g_cfg->n_hosts) { *lat = -1; *rel = -1; return -1; }
     return g_cfg->path(g_cfg->path_ctx, g_cfg->host_vertex[ha], g_cfg->host_vertex[hb], lat, rel);

@@ -66,6 +66,7 @@ def lib():
         l.o_topo_new.restype = C.c_void_p
         l.o_topo_new.argtypes = [C.c_void_p, P(C.c_int32), C.c_int32, C.c_int32]
         l.o_topo_free.argtypes = [C.c_void_p]
+        l.o_topo_precompute_rows.argtypes = [C.c_void_p, C.c_int]
         l.o_topo_get.argtypes = [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double), P(C.c_double)]
         l.o_topo_would_run.argtypes = [C.c_void_p, C.c_int32, C.c_int32]
         l.o_topo_touch.argtypes = [C.c_void_p, C.c_int32, C.c_int32]

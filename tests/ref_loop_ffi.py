@@ -36,13 +36,13 @@ class Cfg(C.Structure):
                 ("load", C.c_uint32), ("payload", C.c_uint32),
                 ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p),
                 ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32),
-                ("quiet", C.c_int32), ("qdisc_rr", C.c_int32)]
+                ("quiet", C.c_int32), ("qdisc_rr", C.c_int32), ("mark_time", C.c_uint64 * 2)]
 
 
 class Out(C.Structure):
     _fields_ = [("lines", C.c_char_p), ("len", C.c_size_t), ("cap", C.c_size_t), ("n_lines", C.c_uint64),
                 ("ip", P(C.c_uint32)), ("next_event_id", P(C.c_uint64)), ("next_packet_id", P(C.c_uint64)),
-                ("rng_probe", P(C.c_uint32))]
+                ("rng_probe", P(C.c_uint32)), ("mark_wall_s", C.c_double * 2)]
 
 
 _lib = None
@@ -65,7 +65,8 @@ def _ptr(a, ct):
     return None if a is None else a.ctypes.data_as(P(ct))
 
 
-def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False, echo=None):
+def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False, echo=None,
+        marks=None, row_threads=0):
     """run_inproc in a forked child: the reference keeps process-wide state
     (the worker's thread-private object, glib quarks), so one run per process."""
     import multiprocessing as mp
@@ -74,7 +75,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp
 
     def child():
         try:
-            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp, quiet, echo)))
+            wr.send(("ok", run_inproc(model, g, host_start, procs, tcp, quiet, echo, marks, row_threads)))
         except BaseException as ex:   # noqa: BLE001 -- reported to the parent
             wr.send(("err", repr(ex)))
         wr.close()
@@ -93,7 +94,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp
 
 
 def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=None, tcp=None, quiet=False,
-               echo=None):
+               echo=None, marks=None, row_threads=0):
     """Run the model through the reference's loop; returns dict(lines=[(t, h, line)],
     ip=[str], next_event_id, next_packet_id, rng_probe (uint arrays)).
     host_start: [H] process start times (default: the model's app_start);
@@ -101,13 +102,23 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     and the engine's pushed SHD_EV_APP_START events, in push order);
     tcp: dict(peers=[-1 | server process index per process], nbytes=N) runs
     the TCP echo test (test_tcp.c) in those processes instead of PHOLD;
-    echo: [H] -1 | server host runs the UDP request/response echo instead."""
+    echo: [H] -1 | server host runs the UDP request/response echo instead;
+    marks: (t0, t1) simulated ns -> res["mark_wall_s"], the monotonic clock at
+    the first send at or after each (the reference's own loop timed over a
+    window); row_threads > 0: the path cache's rows computed on that many cores
+    before the run (o_topo_precompute_rows), so the loop's time is the loop's."""
     m = model.struct
     H = int(m.n_hosts)
     og = O.lib().o_graph_new(C.byref(g.struct))
     hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
     att = np.ascontiguousarray(np.unique(hv).astype(np.int32))
     topo = O.lib().o_topo_new(og, att.ctypes.data_as(P(C.c_int32)), len(att), 0)
+    rows_s = 0.0
+    if row_threads > 0:
+        import time
+        t0 = time.perf_counter()
+        O.lib().o_topo_precompute_rows(topo, int(row_threads))
+        rows_s = time.perf_counter() - t0
     keep = []
     cfg = Cfg()
     cfg.n_hosts = H
@@ -153,6 +164,8 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     cfg.path_ctx = topo
     tmp = tempfile.mkdtemp(prefix="shd_ref_loop_")
     cfg.root_dir = tmp.encode()
+    if marks is not None:
+        cfg.mark_time[0], cfg.mark_time[1] = int(marks[0]), int(marks[1])
     out = Out()
     try:
         import time
@@ -176,7 +189,8 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
         res = dict(lines=lines, ip=ips,
                    next_event_id=np.ctypeslib.as_array(out.next_event_id, shape=(H,)).copy(),
                    next_packet_id=np.ctypeslib.as_array(out.next_packet_id, shape=(H,)).copy(),
-                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy(), run_s=run_s)
+                   rng_probe=np.ctypeslib.as_array(out.rng_probe, shape=(H,)).copy(), run_s=run_s,
+                   mark_wall_s=(out.mark_wall_s[0], out.mark_wall_s[1]), rows_s=rows_s)
         lib().ref_loop_free(C.byref(out))
     finally:
         O.lib().o_topo_free(topo)
