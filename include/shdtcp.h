@@ -84,12 +84,17 @@ typedef struct shd_tcp_result {
      * then outbound remote, each packets-control, bytes-control-header,
      * packets-control-retrans, bytes-control-header-retrans, packets-data,
      * bytes-data-header, bytes-data-payload, packets-data-retrans,
-     * bytes-data-header-retrans, bytes-data-payload-retrans (no TCP loopback:
-     * the localhost counters are zero); n_heartbeats[h] of them are host h's.
+     * bytes-data-header-retrans, bytes-data-payload-retrans; a host's packets
+     * to its own address (the loopback task, network_interface.c:548-555) are
+     * counted here as the reference counts them: remote, since tracker.c:223
+     * and :255 call a packet local only when its address is 127.0.0.1, which
+     * no model's sockets use, so the localhost counters are zero.
+     * n_heartbeats[h] of them are host h's.
      * shd_tracker_node_lines (shdgpu.h) makes the [node] lines of a host. */
     uint64_t* node_counters;
     uint32_t* n_heartbeats;
     uint32_t node_k, _pad2;
+    uint64_t max_round_deliveries;    /* the most deliveries one round's mailbox took */
 } shd_tcp_result;
 
 /* shd_tcp_run's `trace` bits */

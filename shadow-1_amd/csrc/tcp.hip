@@ -72,7 +72,9 @@ constexpr uint32_t kMailMin = 1u << 16;   // mailbox slots per round: max(this, 
 // the mailbox in 64 parts with a fill counter each (host h claims in part h % 64,
 // 32 slots per host), each lane folding the earliest delivery it sent into its
 // own next time (measured against one counter and one atomicMin in round 4:
-// profiles/r04/tcp)
+// profiles/r04/tcp); a full part spills into a shared overflow range (half the
+// parts' size, its own counter), so one host with a wide window can send far
+// more than its part in a round (a few hosts at ~1 Gbit/s and 50 ms latency)
 constexpr uint32_t kMailSub = 64;
 constexpr uint32_t kMailSack = 8;   // SACK entries per mailbox slot on average (their own arena)
 constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
@@ -230,6 +232,7 @@ struct TCtl {
     uint64_t wend;       // the running round's window end
     uint64_t rounds;     // rounds started; round k reads mailbox k & 1 and writes the other
     uint32_t halted, _pad;
+    uint64_t max_mail;   // the most deliveries one round's mailbox took (shd_tcp_result)
 };
 
 struct Glob {
@@ -249,13 +252,13 @@ struct Glob {
     DEv* ev;                // [H][kEv] each host's event heap
     CqEnt* cq;              // [H][kCq]
     Mail* mail;             // [2][mail_cap] the two mailboxes (a round's input, its output)
-    uint32_t* nmail;        // [2][kMailSub] their fill counts
+    uint32_t* nmail;        // [2][kMailSub + 1] their fill counts (the parts', then the overflow's)
     int32_t* msack;         // [2][msack_cap] the SACK lists of the mails that carry one
     uint32_t* nmsack;       // [2] their fill counts
     uint32_t msack_cap, _pad4;
     int32_t* mhead;         // [2][H] each destination's list of mails (-1: none)
     int32_t* mnext;         // [2][mail_cap] the next mail of the same destination
-    uint32_t mail_cap, _pad2;
+    uint32_t mail_cap, mail_part;   // slots in all; slots per part (the overflow: the rest)
     TCtl* ctl;
     const uint64_t* ip_key; // [ip_mask + 1] (ip << 32 | host), open addressing: host_of_ip's table
     uint32_t ip_mask, _pad5;
@@ -1583,10 +1586,14 @@ __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:
         const uint64_t seq = c.H->ev_seq++;   // event_new_ (the delivery's ID)
         if (t >= c.g->end_time) return;
         if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
-        const uint32_t part = (uint32_t)c.h % kMailSub, per = c.g->mail_cap / kMailSub;
+        const uint32_t part = (uint32_t)c.h % kMailSub, per = c.g->mail_part;
         const uint32_t kk = atomicAdd(c.g->n_out + part, 1u);
-        if (kk >= per) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
-        const uint32_t slot = part * per + kk;
+        uint32_t slot = part * per + kk;
+        if (kk >= per) {   // the part is full: the shared overflow range
+            const uint32_t ko = atomicAdd(c.g->n_out + kMailSub, 1u);
+            if (ko >= c.g->mail_cap - per * kMailSub) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+            slot = per * kMailSub + ko;
+        }
         Mail* m = &c.g->mail_out[slot];
         m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
         m->sack_off = 0;
@@ -2047,12 +2054,23 @@ __global__ void k_tcp_window(Glob g) {
     __shared__ uint64_t red[16];
     TCtl* ctl = g.ctl;
     if (ctl->halted) return;
-    {   // the next round's output mailbox starts empty (read before thread 0 moves rounds on)
+    __shared__ uint32_t s_mail;
+    if (threadIdx.x == 0) s_mail = 0;
+    __syncthreads();
+    {   // the next round's output mailbox starts empty (read before thread 0 moves
+        // rounds on); what it took two rounds ago is counted first
         const uint64_t k = ctl->rounds;
-        if (threadIdx.x < kMailSub) g.nmail[((k + 1) & 1) * kMailSub + threadIdx.x] = 0;
-        if (threadIdx.x == kMailSub) g.nmsack[(k + 1) & 1] = 0;
+        if (threadIdx.x <= kMailSub) {
+            uint32_t* n = &g.nmail[((k + 1) & 1) * (kMailSub + 1) + threadIdx.x];
+            const uint32_t cap = threadIdx.x < kMailSub ? g.mail_part : g.mail_cap - g.mail_part * kMailSub;
+            const uint32_t v = *n;
+            if (v) atomicAdd(&s_mail, v < cap ? v : cap);
+            *n = 0;
+        }
+        if (threadIdx.x == kMailSub + 1) g.nmsack[(k + 1) & 1] = 0;
     }
     __syncthreads();
+    if (threadIdx.x == 0 && s_mail > ctl->max_mail) ctl->max_mail = s_mail;
     uint64_t t = ~0ull;
     for (int32_t i = (int32_t)threadIdx.x; i <= g.H; i += (int32_t)blockDim.x) {
         const uint64_t x = g.next_time[i];
@@ -2110,7 +2128,7 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
         gl = g;
         gl.mail_in = g.mail + (size_t)in * g.mail_cap; gl.mhead_in = g.mhead + (size_t)in * g.H;
         gl.mnext_in = g.mnext + (size_t)in * g.mail_cap;
-        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + (size_t)out * kMailSub;
+        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + (size_t)out * (kMailSub + 1);
         gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * g.mail_cap;
         gl.msack_in = g.msack + (size_t)in * g.msack_cap; gl.msack_out = g.msack + (size_t)out * g.msack_cap;
         gl.nmsack_out = g.nmsack + out;
@@ -2361,14 +2379,18 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     HCHECK(hipGetLastError());
     HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
     HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
-    g.mail_cap = (uint32_t)H * 32u > kMailMin ? (uint32_t)H * 32u : kMailMin;
+    {
+        const uint32_t parts = (uint32_t)H * 32u > kMailMin ? (uint32_t)H * 32u : kMailMin;
+        g.mail_part = parts / kMailSub;
+        g.mail_cap = g.mail_part * kMailSub + g.mail_part * kMailSub / 2;
+    }
     g.msack_cap = g.mail_cap * kMailSack;
     HCHECK(hipMalloc(&g.msack, sizeof(int32_t) * 2 * (size_t)g.msack_cap));
     HCHECK(hipMalloc(&g.nmsack, sizeof(uint32_t) * 2));
     HCHECK(hipMemset(g.nmsack, 0, sizeof(uint32_t) * 2));
     HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
-    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2 * kMailSub));
-    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * kMailSub));
+    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2 * (kMailSub + 1)));
+    HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * (kMailSub + 1)));
     HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
@@ -2401,7 +2423,8 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     }
     HCHECK(hipMalloc(&g.next_time, sizeof(uint64_t) * (H + 1)));
     HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (H + 1)));
-    g.qlog_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);
+    // every host can log kPq first queries (touch_log)
+    g.qlog_cap = (uint32_t)H * kPq > (1u << 16) ? (uint32_t)H * kPq : (1u << 16);
     HCHECK(hipMalloc(&g.qlog, sizeof(shd_tcp_query) * (size_t)g.qlog_cap));
     HCHECK(hipMalloc(&g.nqlog, sizeof(uint32_t)));
 #ifdef SHD_TCP_PROF
@@ -2462,6 +2485,22 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     res->next_packet_id = (uint64_t*)calloc(H, sizeof(uint64_t));
     res->rng_probe = (uint32_t*)calloc(H, sizeof(uint32_t));
     res->rounds = rounds;
+    {   // the last two rounds' mailboxes were never counted by k_tcp_window
+        std::vector<uint32_t> nm(2 * (kMailSub + 1));
+        HCHECK(hipMemcpy(nm.data(), g.nmail, sizeof(uint32_t) * nm.size(), hipMemcpyDeviceToHost));
+        TCtl cx;
+        HCHECK(hipMemcpy(&cx, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost));
+        res->max_round_deliveries = cx.max_mail;
+        for (int b = 0; b < 2; b++) {
+            uint64_t sum = 0;
+            for (uint32_t j = 0; j <= kMailSub; j++) {
+                const uint32_t cap = j < kMailSub ? g.mail_part : g.mail_cap - g.mail_part * kMailSub;
+                const uint32_t v = nm[b * (kMailSub + 1) + j];
+                sum += v < cap ? v : cap;
+            }
+            if (sum > res->max_round_deliveries) res->max_round_deliveries = sum;
+        }
+    }
     for (int32_t i = 0; i < H; i++) {
         res->next_event_id[i] = hout[i].ev_seq;
         res->next_packet_id[i] = hout[i].pkt_seq;

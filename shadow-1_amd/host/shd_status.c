@@ -263,8 +263,12 @@ int shd_status_lines(const shd_trace_rec* tr, uint64_t n, const uint32_t* ips, c
                      uint32_t n_hosts, uint32_t payload, uint32_t listen_port, const int32_t* app_peer,
                      shd_lines** out) {
     if (!out || (n && !tr) || !ips || !n_hosts) return SHD_EINVAL;
-    for (uint64_t i = 0; i < n; i++)
+    for (uint64_t i = 0; i < n; i++) {
         if (tr[i].host >= n_hosts || tr[i].kind < SHD_TR_SENT || tr[i].kind > SHD_TR_READ) return SHD_EINVAL;
+        /* every kind but the application's two names the other host in `peer`
+         * (the destination, or the datagram's source), which indexes ips[] */
+        if (tr[i].kind <= SHD_TR_LOCAL && tr[i].peer >= n_hosts) return SHD_EINVAL;
+    }
     lbuf b;
     int rc = lb_init(&b, out);
     if (rc) return rc;

@@ -17,7 +17,12 @@
  * superseded, unlinked and created afresh) and unlinks it at close; the other
  * ranks wait for rank 0's `ready` word, and drop a segment that is broken or
  * superseded and open the name again.  Callers still derive the name from a
- * random token, as RCCL's unique id.
+ * random token, as RCCL's unique id.  Joining is a handshake with a live rank
+ * 0: a joiner posts a fresh token of its own in its arrival slot and waits for
+ * rank 0 to echo it back, so a stale segment (whose rank 0 is gone, but which
+ * still reads ready and may hold a leftover barrier count) never lets a joiner
+ * through; it waits there until the new rank 0 marks that segment superseded,
+ * then opens the name again.
  */
 #include <errno.h>
 #include <fcntl.h>
@@ -40,8 +45,12 @@ struct shd_xhost_hdr {
     uint32_t broken;      /* set by a rank whose barrier timed out: every barrier fails */
     uint32_t ready;       /* kReady once rank 0 has initialised the segment */
     uint32_t superseded;  /* set by a rank 0 that replaced this (stale) segment */
+    uint32_t _pad[2];
+    uint64_t arrived[64]; /* joiner r's token (0: not yet), rank 0 echoes it in ack[r] */
+    uint64_t ack[64];
 };
 enum { kReady = 0x58484F53u };
+enum { kHdrBytes = (sizeof(struct shd_xhost_hdr) + 63) & ~63 };
 
 struct shd_xhost {
     char name[128];
@@ -52,7 +61,7 @@ struct shd_xhost {
     double timeout_s;
 };
 
-static char* slot_ptr(shd_xhost* x, int r) { return x->base + 64 + (size_t)r * x->slot; }
+static char* slot_ptr(shd_xhost* x, int r) { return x->base + kHdrBytes + (size_t)r * x->slot; }
 
 static double mono_s(void) {
     struct timespec t;
@@ -88,6 +97,24 @@ static int xhost_create(shd_xhost* x) {
     struct shd_xhost_hdr* h = (struct shd_xhost_hdr*)x->base;
     h->world = (uint32_t)x->world;
     __atomic_store_n(&h->ready, (uint32_t)kReady, __ATOMIC_RELEASE);
+    /* echo every joiner's token (this segment is fresh: only live joiners post) */
+    const double t0 = mono_s();
+    for (int r = 1; r < x->world; r++) {
+        uint64_t tok;
+        while ((tok = __atomic_load_n(&h->arrived[r], __ATOMIC_ACQUIRE)) == 0) {
+            if (mono_s() - t0 > x->timeout_s) {
+                fprintf(stderr, "libshdgpu: host transport %s: rank %d never joined in %.0f s\n", x->name, r,
+                        x->timeout_s);
+                __atomic_store_n(&h->broken, 1u, __ATOMIC_RELEASE);
+                munmap(x->base, x->map_bytes);
+                close(x->fd);
+                shm_unlink(x->name);
+                return SHD_ENODEV;
+            }
+            usleep(100);
+        }
+        __atomic_store_n(&h->ack[r], tok, __ATOMIC_RELEASE);
+    }
     return SHD_OK;
 }
 
@@ -121,7 +148,21 @@ static int xhost_join(shd_xhost* x) {
                             __atomic_load_n(&h->broken, __ATOMIC_ACQUIRE);
             if (!bad && __atomic_load_n(&h->ready, __ATOMIC_ACQUIRE) == (uint32_t)kReady) {
                 if (h->world != (uint32_t)x->world) { munmap(x->base, x->map_bytes); close(x->fd); return SHD_EINVAL; }
-                return SHD_OK;
+                /* the handshake: a token only this call knows, echoed by a live rank 0 */
+                struct timespec ts;
+                clock_gettime(CLOCK_MONOTONIC, &ts);
+                uint64_t tok = ((uint64_t)getpid() << 32) ^ (uint64_t)ts.tv_nsec ^ ((uint64_t)ts.tv_sec << 20) ^
+                               ((uint64_t)x->rank << 56);
+                if (!tok) tok = 1;
+                __atomic_store_n(&h->arrived[x->rank], tok, __ATOMIC_RELEASE);
+                for (;;) {
+                    if (__atomic_load_n(&h->ack[x->rank], __ATOMIC_ACQUIRE) == tok) return SHD_OK;
+                    if (__atomic_load_n(&h->superseded, __ATOMIC_ACQUIRE) ||
+                        __atomic_load_n(&h->broken, __ATOMIC_ACQUIRE) || mono_s() - t0 > x->timeout_s)
+                        break;
+                    usleep(100);
+                }
+                break;
             }
             if (bad || mono_s() - t0 > x->timeout_s) break;
             usleep(100);
@@ -142,7 +183,7 @@ int shd_xhost_open(const char* name, int world, int rank, size_t slot_bytes, shd
     x->world = world;
     x->rank = rank;
     x->slot = (slot_bytes + 63) & ~(size_t)63;
-    x->map_bytes = 64 + (size_t)world * x->slot;
+    x->map_bytes = kHdrBytes + (size_t)world * x->slot;
     const char* to = getenv("SHD_XHOST_TIMEOUT");
     x->timeout_s = to ? atof(to) : 300.0;
     const int rc = rank == 0 ? xhost_create(x) : xhost_join(x);

@@ -201,7 +201,7 @@ class TcpResult(C.Structure):
                 ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64),
                 ("queries", C.c_void_p), ("n_queries", C.c_uint64),
                 ("node_counters", P(C.c_uint64)), ("n_heartbeats", P(C.c_uint32)), ("node_k", C.c_uint32),
-                ("_pad2", C.c_uint32)]
+                ("_pad2", C.c_uint32), ("max_round_deliveries", C.c_uint64)]
 
 
 TCP_TRACE_STATUS, TCP_TRACE_NODE = 1, 2   # shd_tcp_run's trace bits

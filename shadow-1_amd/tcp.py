@@ -160,6 +160,7 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
                    next_packet_id=np.ctypeslib.as_array(r.next_packet_id, shape=(H,)).copy(),
                    rng_probe=np.ctypeslib.as_array(r.rng_probe, shape=(H,)).copy(),
                    rounds=int(r.rounds), events=int(r.events), deliveries=int(r.deliveries),
+                   max_round_deliveries=int(r.max_round_deliveries),
                    device_ms=float(r.device_ms),
                    queries=np.frombuffer(C.string_at(r.queries, int(r.n_queries) * S.TCP_QUERY_DTYPE.itemsize),
                                          dtype=S.TCP_QUERY_DTYPE).copy() if r.n_queries else

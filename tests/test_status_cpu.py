@@ -4,6 +4,7 @@ trace whose expected lines follow the reference's call chain, and on an
 oracle run (every datagram's statuses well formed).  The line format and each
 fate's lines are pinned to the reference's packet.c in test_ref_net_cpu.py."""
 import numpy as np
+import pytest
 
 import oracle_ffi as O
 import shdgpu as S
@@ -145,3 +146,23 @@ def test_tracker_node_lines_from_full_counters():
     assert lines[2][2] == (f"[shadow-heartbeat] [node] 2,{rin},{rout},0.000000,0,0.000000;{z};{z};"
                            f"6,{rin},3,198,0,0,2,132,2000,1,66,500;5,{rout},4,264,1,66,0,0,0,0,0,0")
     assert lines[3][2] == f"[shadow-heartbeat] [node] 2,0,0,0.000000,0,0.000000;{z};{z};{z};{z}"
+
+
+def test_status_writer_refuses_out_of_range_peers():
+    """shd_status_lines indexes ips[] with every record's peer (the sender's
+    destination, the receiver's source): a record naming a host past n_hosts
+    (or ~0) is refused with -EINVAL instead of read out of bounds."""
+    V = 12
+    g = W.geometric_graph(V, seed=3)
+    m = W.phold_model(W.hosts_on_vertices(V, 1), end_time=2 * S.SHD_SEC, trace=True, load=2,
+                      queue_flags=S.SHD_QF_TRACE_STATUS)
+    otr, _, _ = O.engine_run(m, g)
+    ips = ["10.0.0.%d" % (h + 1) for h in range(V)]
+    assert len(S.status_lines(otr, ips)) > 0
+    for kind in (S.TR_SENT, S.TR_ARRIVE, S.TR_RECV):
+        bad = otr.copy()
+        k = int(np.nonzero(bad["kind"] == kind)[0][0])
+        for peer in (V, 0xFFFFFFFF):
+            bad["peer"][k] = peer
+            with pytest.raises(S.ShdError):
+                S.status_lines(bad, ips)

@@ -102,3 +102,21 @@ def test_tcp_gpu_first_touch_order_settles(name):
     assert r["first_touch_runs"] == (2 if wrong else 1)
     if name == "server_first":
         assert wrong   # the case is built so that the order matters
+
+
+def test_tcp_gpu_wide_window_uses_the_mailbox_overflow():
+    """One fast, long connection (about 1 Gbit/s links, 20 MB): its window
+    grows past the 1024 mailbox slots a host's part holds per round (the
+    mailbox is split into 64 parts by host), so the sends spill into the
+    shared overflow range -- the run must neither fail with
+    SHD_TCP_ERR_MAILBOX nor differ from the oracle."""
+    import workloads as W
+    g, m, ips, procs, peers, nb = W.tcp_echo_model(2, 40, end_s=8, nbytes=20_000_000, bw_down=122070, bw_up=122070)
+    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, trace=False)
+    o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb, lines=False)
+    assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
+    assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
+    assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
+    assert r["events"] == o["events"]
+    # more deliveries than one part's 1024 slots in some round
+    assert r["max_round_deliveries"] > 1024
