@@ -343,7 +343,8 @@ def main():
     n_ps = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_persistent", 0))
     n_bat = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches", 0))
     n_sp = 0 if (world > 1 and not use_group) else int(getattr(st, "n_batches_sparse", 0))
-    kname = ("k_round_px" if fused else "k_round_xtl") if use_group else \
+    kname = (("k_round_spx" if n_bat and 2 * n_sp >= n_bat else "k_round_px") if fused else "k_round_xtl") \
+        if use_group else \
         ("k_round" if world > 1 else (("k_round_sp" if 2 * n_sp >= n_ps else "k_round_ps")
                                        if n_ps and 2 * n_ps >= n_bat else "k_round_tl"))
     wkey = "%s-%dh" % (args.workload, H // max(world, 1))
@@ -518,7 +519,9 @@ def tcp_main(args):
         # the per-host allocations and setup, the rounds, the copies back): the
         # rate a caller of shd_tcp_run sees end to end; `value` is device time
         "wall_inclusive": {"value": round(events / wall, 1), "unit": "events/s",
-                           "device_share": round(dev_s / wall, 3)},
+                           "device_share": round(dev_s / wall, 3),
+                           "host_ms_last_run": {k: round(v, 1) for k, v in r.get("host_ms", {}).items()}},
+        "first_touch": r.get("first_touch"),
         "rounds": r["rounds"], "events_per_run": r["events"], "deliveries_per_run": r["deliveries"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(achieved / 8000.0, 6), "traffic": None, "kernel": "k_tcp_round",

@@ -203,6 +203,12 @@ int shd_pc_copy_self(shd_pc* pc, double* lat, double* rel);
  * topology_getReliability (topology.c:2065-2087).  Returns latency -1 and
  * reliability -1 when the reference would (error path, topology.c:2040-2046). */
 int shd_pc_lookup(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex, double* lat, double* rel);
+/* n shd_pc_lookup calls in array order (the same first-touch semantics, ranks
+ * and minimumPathLatency), in one device round trip: the driver of the TCP
+ * path resolves its [V, V] path tables with it (shadow-1_amd/tcp.py).  Under
+ * shd_pc_defer_touches' protocol the queries run one by one. */
+int shd_pc_lookup_batch(shd_pc* pc, const int32_t* src_vertex, const int32_t* dst_vertex, uint64_t n,
+                        double* lat, double* rel);
 /* topology_incrementPathPacketCounter (topology.c:2053-2063) + read back */
 int shd_pc_count_packet(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex);
 int shd_pc_packet_count(shd_pc* pc, int32_t src_vertex, int32_t dst_vertex, uint64_t* count);

@@ -13,9 +13,11 @@
  *
  * The boundary is the same one shdgpu.h draws for the UDP path: plain
  * pointers and sizes, no torch types.  Path latency and reliability per host
- * pair come from the caller (Shadow's topology_getLatency /
- * topology_getReliability, topology.c:2053-2092, or shd_pc_lookup), resolved
- * in the order the serial loop touches them.
+ * pair come either from libshdgpu's path cache itself (path_cache set: the
+ * lazy cache's first-touch rule applied on the device, round by round, as the
+ * UDP engine does -- DESIGN.md §4), or from caller tables (Shadow's
+ * topology_getLatency / topology_getReliability, topology.c:2053-2092, or
+ * shd_pc_lookup), resolved in the order the serial loop touches them.
  */
 #ifndef SHD_TCP_H
 #define SHD_TCP_H
@@ -50,6 +52,22 @@ typedef struct shd_tcp_model {
                                          set SHD_TCP_ERR_POOL                             */
     uint32_t qdisc;                   /* --interface-qdisc (options.c:162): 0 fifo, 1 rr
                                          (network_interface.c:466-517)                    */
+    uint32_t _pad;
+    /* A built path cache of this model's graph (shdgpu.h shd_pc_create: an
+     * undirected graph, the hosts' vertices attached), or NULL.  Set: every
+     * path query of the run goes to the cache's device tables under the lazy
+     * cache's first-touch rule (topology.c:1969-2051): a pair with a ranked
+     * endpoint at the round's start takes the lower-ranked endpoint's row; a
+     * pair with none takes the querying source's row, the query logged with
+     * its event key, and between rounds the log is ranked in serial order
+     * (event_compare's key, then the query's index within its event), which
+     * both checks every such choice and ranks the rows that ran.  A choice the
+     * serial order contradicts (two unranked endpoints first touched from both
+     * sides within one window) ends the run with SHD_TCP_ERR_FIRST_TOUCH; the
+     * caller then runs the model on tables (the fields above).  The cache's
+     * ranks are left as the serial run leaves them.  host_vertex then holds
+     * graph vertex ids, and n_vertices / path_lat_ms / path_rel are unused. */
+    struct shd_pc* path_cache;
 } shd_tcp_model;
 
 /* the first path query a host made of a vertex pair (topology_isRoutable /
@@ -95,6 +113,10 @@ typedef struct shd_tcp_result {
     uint32_t* n_heartbeats;
     uint32_t node_k, _pad2;
     uint64_t max_round_deliveries;    /* the most deliveries one round's mailbox took */
+    uint64_t max_round_overflow;      /* ... and the most of them in its shared overflow range */
+    double setup_ms, results_ms, teardown_ms;   /* the call's host wall time around the rounds:
+                                                   allocation and upload, copies back and
+                                                   formatting, release */
 } shd_tcp_result;
 
 /* shd_tcp_run's `trace` bits */
@@ -103,7 +125,7 @@ enum { SHD_TCP_TRACE_STATUS = 1, SHD_TCP_TRACE_NODE = 2 };
 enum {
     SHD_TCP_ERR_EVQ = 1, SHD_TCP_ERR_POOL = 2, SHD_TCP_ERR_QUEUE = 4, SHD_TCP_ERR_SOCKETS = 8,
     SHD_TCP_ERR_MAILBOX = 16, SHD_TCP_ERR_TRACE = 32, SHD_TCP_ERR_SACK = 64, SHD_TCP_ERR_INTERNAL = 128,
-    SHD_TCP_ERR_QLOG = 256
+    SHD_TCP_ERR_QLOG = 256, SHD_TCP_ERR_FIRST_TOUCH = 512
 };
 
 /* Run the model to end_time on the current HIP device.  trace & 1 writes the

@@ -861,10 +861,240 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
             TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, nact};
 }
 
+// ---- sparse fused rounds (k_round_spx): the engine group at the north
+// star's shard (125 k hosts per GPU, a few percent of them with something due
+// in a window).  k_round_px gives every 64-host block a wave per round (1954
+// waves at 125 k hosts, against ~768 resident: three passes of blocks, each
+// taking the exchange's wait); here, as in the single engine's k_round_sp, a
+// block owns sph hosts (a multiple of 64, so its region blocks are whole),
+// takes what the peers stored for them into their calendars / inboxes, scans
+// their hand-off words, compacts the hosts with something due and runs them
+// 64 at a time.  Still one launch per round (the region take reads slots a
+// peer stored into over xGMI: a launch boundary between the peer's stores and
+// the take keeps every load of a slot off a stale line), with
+// k_round_px's fold / put / wait in front: blocks [0, world) fold round i - 1's
+// shares and put the headers, every block waits for every peer's header.
+// first: the batch's round 0 (the exchange before it is complete: its headers
+// read from xhdr, its regions taken by the last batch's k_xchg_px).
+__global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, DevSummary* __restrict__ prev,
+                                                       const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
+                                                       const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
+                                                       const shd_event* __restrict__ xhdr, shd_event* __restrict__ rgn,
+                                                       shd_event* const* __restrict__ peers,
+                                                       XHeader* __restrict__ halt_hdr, uint32_t* __restrict__ xerr,
+                                                       int world, int me, int wprev, const shd_event* __restrict__ xrep,
+                                                       uint64_t xhoff, int nrep, uint32_t sph, uint32_t nsp, int first) {
+    const DParams& P = *Pp;
+    const unsigned long long t_entry = wall_clock64();
+    const bool putter = !first && (int)blockIdx.x < world;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    uint32_t halt = *P.halt, bad = *xerr;
+    const uint64_t stop = ctl->stop, rbase = ctl->round_base, xtag = ctl->xtag, xpar = ctl->xpar;
+    const size_t stride = (size_t)P.xcap + 1;
+    uint64_t ws = kInf, pws = 0;
+    uint32_t fl = 0;
+    if (first) {   // as k_round_xtl: lane p reads peer p's header of the completed exchange
+        const XHeader hx = *(const XHeader*)(xhdr + (size_t)((int)threadIdx.x < world ? threadIdx.x : 0) * stride);
+        ws = (int)threadIdx.x < world ? hx.next_time : kInf;
+        fl = (int)threadIdx.x < world ? hx.flags : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(ws, off, 64);
+            ws = o < ws ? o : ws;
+            fl |= __shfl_xor(fl, off, 64);
+        }
+        if (blockIdx.x >= nsp) return;
+    } else {
+        pws = prev->ws;
+        const TlPart* pp = parts + (size_t)((i - 1) & 1) * nsp;
+        const uint32_t tag = (uint32_t)(xtag + (uint64_t)(i - 1));
+        if (putter) {
+            TlPart pv[4];
+            tl_issue(pp, nsp, 0, pv);
+            px_fold_put(P, prev, pv, pp, nsp, pws, prev->n_pending, prev->n_remote, prev->next_time, prev->error, stop,
+                        halt, bad, peers, world, me, wprev, tag, xhoff, nrep);
+        }
+        if (blockIdx.x >= nsp) return;   // a put block past the engine's blocks (grid = max(nsp, world))
+        if (px_wait(xhdr, stride, world, tag, bad, xerr, ws, fl, xrep, nrep, blockIdx.x)) {
+            if (threadIdx.x == 0) *P.halt = 1u;
+            if (lead) P.sum->flags = 2u;
+            return;
+        }
+    }
+    const int parity = (int)((rbase + (uint64_t)i) & 1);
+    const uint32_t hb = blockIdx.x * sph;   // the block's first host
+    const uint32_t nh = (uint32_t)P.nloc - hb < sph ? (uint32_t)P.nloc - hb : sph;
+    const uint32_t ngrp = (nh + 63u) >> 6;
+    uint32_t ierr = 0;
+    if (!first) {
+        // the peers' stores for this block's hosts (region blocks hb / 64 ...),
+        // into their calendars / inboxes, before the scan reads them
+        if (!halt && world > 1)
+            for (uint32_t gq = 0; gq < ngrp; gq++)
+                ierr |= xrgn_ingest_from(P, rgn, hb / 64u + gq, pws, parity, nullptr, nullptr, 0);
+        px_reset_counts(P, wprev, blockIdx.x, nsp);
+    }
+    if (halt) {
+        if (lead) P.sum->flags = 2u;
+        return;
+    }
+    if (fl) {   // flagged somewhere in the group: every engine halts here alike
+        if (blockIdx.x == 0) {
+            if ((int)threadIdx.x < world) {
+                const void* hp = xhdr + (size_t)threadIdx.x * stride;
+                XHeader h;
+                if (first) {
+                    h = *(const XHeader*)hp;
+                } else {
+                    const uint4 g0 = ld16_sys(hp), g1 = ld16_sys((const uint4*)hp + 1);
+                    h.next_time = ((uint64_t)g0.y << 32) | g0.x;
+                    h.flags = g0.z;
+                    h.tag = g0.w;
+                    h.n_pending = ((uint64_t)g1.y << 32) | g1.x;
+                    h.error = g1.z;
+                    h.count = g1.w;
+                }
+                halt_hdr[threadIdx.x] = h;
+            }
+            if (threadIdx.x == 0) {
+                *P.halt = 1u;
+                P.sum->flags = 1u;
+            }
+        }
+        return;
+    }
+    if (lead) {
+        atomicMin(&P.sum->t_first, t_entry);
+        *init = fresh_summary();
+        P.sum->ws = ws;
+    }
+    if (ws >= stop) return;   // only forwards the time (the next exchange packs it)
+    uint64_t we = ws + window;
+    if (we > stop || we < ws) we = stop;
+    if (threadIdx.x == 0) s_rsum = P.sum;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the take's stores, before the scan's loads
+    __syncthreads();
+    // ---- k_round_sp's round over this block's hosts
+    const uint32_t lane = threadIdx.x;
+    PsRsrc R;
+    R.bits = buf_rsrc(P.bin_bits ? P.bin_bits + (size_t)hb * kNBW : nullptr, (uint64_t)nh * kNBW * 4);
+    R.bins = buf_rsrc(P.bins ? P.bins + (size_t)hb * kNB * kBinCap : nullptr,
+                      (uint64_t)nh * kNB * kBinCap * sizeof(shd_event));
+    R.nin = buf_rsrc(P.inbox_n[parity] + hb, (uint64_t)nh * 4);
+    R.inbox = buf_rsrc(P.inbox[parity] + (size_t)hb * P.inbox_cap, (uint64_t)nh * P.inbox_cap * sizeof(shd_event));
+    HostCtx c;
+    hot_load(P, c);
+    c.l = P.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
+    c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
+    const uint32_t xwi = (uint32_t)((xpar + (uint64_t)i) & 1);
+    ps_round_reset(P, c, ws, we, parity, false);
+    c.xwi = xwi;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    uint64_t next = kInf;
+    uint32_t nact = 0;
+    for (uint32_t g0 = 0; g0 < ngrp; g0 += kSpScan) {
+        uint32_t nin4[kSpScan], w4[kSpScan][kNBW];
+        uint64_t t4[kSpScan];
+#pragma unroll
+        for (int q = 0; q < kSpScan; q++) {
+            const uint32_t lb = (g0 + q) * 64u + lane;
+            nin4[q] = 0; t4[q] = kInf;
+#pragma unroll
+            for (int j = 0; j < (int)kNBW; j++) w4[q][j] = 0;
+            if (g0 + q < ngrp && lb < nh) {
+                nin4[q] = ld4_sc1(R.nin, lb * 4u);
+                if (P.bins) {
+                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                    w4[q][0] = x.x; w4[q][1] = x.y; w4[q][2] = x.z; w4[q][3] = x.w;
+                    w4[q][4] = y.x; w4[q][5] = y.y; w4[q][6] = y.z; w4[q][7] = y.w;
+                }
+                t4[q] = P.hnext[hb + lb];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kSpScan; q++) {
+            const uint32_t lb = (g0 + q) * 64u + lane;
+            const bool has = g0 + q < ngrp && lb < nh;
+            const uint32_t wbits = ps_window_bits(P, c, w4[q], ws, we);
+            const bool act = has && !(nin4[q] == 0 && t4[q] >= we && wbits == 0);
+            if (has && !act) {
+                const uint64_t t = ps_idle_next(P, w4[q], t4[q], we);
+                next = t < next ? t : next;
+            }
+            const uint64_t m = __ballot(act);
+            if (act) {
+                const uint32_t k = nact + (uint32_t)__popcll(m & lt_mask);
+                s_act[k] = (uint16_t)lb;
+                if (k < (uint32_t)kBlock) {
+#pragma unroll
+                    for (int j = 0; j < (int)kNBW; j++) s_aw[j * kBlock + k] = w4[q][j];
+                    s_aw[kNBW * kBlock + k] = nin4[q];
+                }
+            }
+            nact += (uint32_t)__popcll(m);
+        }
+    }
+    __syncthreads();
+    uint32_t nev = 0, npkt = 0, err = c.err | ierr, nhost = 0;
+    for (uint32_t base = 0; base < nact; base += kBlock) {
+        const uint32_t k = base + lane;
+        const bool act = k < nact;
+        const uint32_t lb = act ? (uint32_t)s_act[k] : 0u;
+        const int32_t l = (int32_t)(hb + lb);
+        uint32_t nin = 0, w[kNBW];
+#pragma unroll
+        for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+        if (act) {
+            if (base == 0) {
+#pragma unroll
+                for (int j = 0; j < (int)kNBW; j++) w[j] = s_aw[j * kBlock + k];
+                nin = s_aw[kNBW * kBlock + k];
+            } else {
+                nin = ld4_sc1(R.nin, lb * 4u);
+                if (P.bins) {
+                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+                }
+            }
+        }
+        SpIn in;
+        in.l = l;
+        in.xwi = xwi;
+        if (act) {
+            in.rec = P.hs[l];
+            in.att = P.host_att[P.h0 + l];
+            in.st = P.self_thr[P.h0 + l];
+        }
+        const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
+        uint64_t hn = kInf;
+        ps_round_body<true>(P, c, act, lb, R, ws, we, parity, nin, w, wbits, hn, &in);
+        if (act) store_ctx(P, c);
+        next = hn < next ? hn : next;
+        nev += c.c_events; npkt += c.c_pkt;
+        err |= c.err;
+        nhost += (uint32_t)__popcll(__ballot(act && c.c_events != 0));
+        __syncthreads();   // (the next pass reuses the lanes' LDS slots)
+    }
+    // peer-to-peer: this block's stores into the peers' regions land before the
+    // round ends (the next launch's put block announces them)
+    if (P.xpeer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off, 64);
+        next = o < next ? o : next;
+        nev += __shfl_xor(nev, off, 64);
+        npkt += __shfl_xor(npkt, off, 64);
+        err |= __shfl_xor(err, off, 64);
+    }
+    if (threadIdx.x == 0)
+        parts[(size_t)(i & 1) * nsp + blockIdx.x] =
+            TlPart{next, (unsigned long long)wall_clock64(), (unsigned)nev, (unsigned)npkt, err, nhost};
+}
+
 // the exchange of a batch's last round i (P.sum: its summary): blocks
-// [0, world) fold and put, blocks [world, world + nblk) wait and ingest their
-// block's regions into the next round's calendar / inbox
-__global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __restrict__ parts, uint32_t nblk, int i,
+// [0, world) fold the round's nparts shares and put, blocks [world, world +
+// nblk) wait and ingest their 64-host block's regions into the next round's
+// calendar / inbox
+__global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __restrict__ parts, uint32_t nparts,
+                                                     uint32_t nblk, int i,
                                                      const DevCtl* __restrict__ ctl, shd_event* const* __restrict__ peers,
                                                      int world, int me, int wi, const shd_event* __restrict__ xhdr,
                                                      shd_event* __restrict__ rgn, uint32_t* __restrict__ xerr,
@@ -873,14 +1103,14 @@ __global__ __launch_bounds__(kBlock) void k_xchg_px(DParams P, const TlPart* __r
     uint32_t halt = *P.halt, bad = *xerr;
     uint64_t stop = ctl->stop, rbase = ctl->round_base, xtag = ctl->xtag, pws = sum->ws;
     const uint32_t tag = (uint32_t)(xtag + (uint64_t)i);
-    const TlPart* pp = parts + (size_t)(i & 1) * nblk;
+    const TlPart* pp = parts + (size_t)(i & 1) * nparts;
     if ((int)blockIdx.x < world) {
         TlPart pv[4];
-        tl_issue(pp, nblk, 0, pv);
+        tl_issue(pp, nparts, 0, pv);
         const uint64_t npend = sum->n_pending, nrem = sum->n_remote, pnext = sum->next_time;
         const uint32_t perr = sum->error;
-        px_fold_put(P, sum, pv, pp, nblk, pws, npend, nrem, pnext, perr, stop, halt, bad, peers, world, me, wi, tag, xhoff,
-                    nrep);
+        px_fold_put(P, sum, pv, pp, nparts, pws, npend, nrem, pnext, perr, stop, halt, bad, peers, world, me, wi, tag,
+                    xhoff, nrep);
         return;
     }
     const uint32_t blk = blockIdx.x - (uint32_t)world;

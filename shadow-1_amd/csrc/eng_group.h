@@ -47,8 +47,14 @@ struct shd_xgroup {
     int last_nb = shd_eng::kBatch;     // rounds in the last batch (its last summary is d_ring[last_nb])
     // full batches captured as HIP graphs (RCCL transport, one engine per
     // process), one per exchange parity at the batch start
-    hipGraphExec_t graph[2] = {nullptr, nullptr};
+    hipGraphExec_t graph[2][2] = {{nullptr, nullptr}, {nullptr, nullptr}};   // [sparse][parity]
     bool graph_failed = false;
+    // fused rounds over engines with more 64-host blocks than resident waves
+    // (the north star's 125 k-host shard): k_round_spx, blocks of sp_hosts
+    // hosts, while few hosts are active per round (sp_dense: the last batch
+    // had many, k_round_px instead -- the exchange is the same either way)
+    uint32_t sp_hosts = 0, sp_grid = 0;
+    bool sp_dense = false, sp_forced = false;
     // protected rounds (as for one engine): group-wide, so every rank decides alike
     bool logged_any = false;
     uint64_t last_logged = 0;          // first touches gathered from the whole group at the last log
@@ -446,11 +452,12 @@ extern "C" int shd_xgroup_unique_id(uint8_t id[SHD_XID_BYTES]) {
 }
 
 static void x_drop_graphs(shd_xgroup* g) {
-    for (auto& ge : g->graph)
-        if (ge) {
-            (void)hipGraphExecDestroy(ge);
-            ge = nullptr;
-        }
+    for (auto& gk : g->graph)
+        for (auto& ge : gk)
+            if (ge) {
+                (void)hipGraphExecDestroy(ge);
+                ge = nullptr;
+            }
 }
 
 static void x_free(shd_xgroup* g) {
@@ -556,6 +563,25 @@ static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p,
     // waited out their 30 s: the device did not run the three launches at once)
     g->fused = p2p && x_fuse_env() && (sharers <= 1 || shared_blocks <= (unsigned long long)ncu);
     g->end_time = e->P.end_time;
+    if (g->fused && !getenv("SHD_X_NO_SP")) {
+        // the sparse fused round (k_round_spx): blocks of sph hosts, about one
+        // per CU, when the engine has more 64-host blocks than two per CU
+        // (SHD_SP_HOSTS=<n>: n hosts per block whatever the size, as for one engine)
+        const char* sp_env = getenv("SHD_SP_HOSTS");
+        const uint32_t sp_force = sp_env ? (uint32_t)strtoul(sp_env, nullptr, 10) : 0u;
+        const uint64_t per = ((uint64_t)e->nloc + ncu - 1) / ncu;
+        const uint32_t sph = sp_force ? (sp_force + 63) / 64 * 64
+                                      : (uint32_t)std::max<uint64_t>(256, (per + 63) / 64 * 64);
+        const uint32_t grid = (uint32_t)(((uint64_t)e->nloc + sph - 1) / sph);
+        // (ranks sharing a GPU: every block of every sharer resident at once,
+        // one per CU, as for the fused schedule itself)
+        if ((sp_force || nblk > 2ull * (unsigned long long)ncu) && sph <= kSpMaxHosts && e->P.hpw == 64 &&
+            (sharers <= 1 || (uint64_t)sharers * std::max<uint32_t>(grid, (uint32_t)world) <= (uint64_t)ncu)) {
+            g->sp_hosts = sph;
+            g->sp_grid = grid;
+            g->sp_forced = sp_force != 0;
+        }
+    }
     g->xcap = block_events ? block_events : x_default_cap(e, world);
     g->fixed_cap = block_events != 0;
     if ((rc = x_alloc(g))) { x_free(g); return rc; }
@@ -603,13 +629,23 @@ extern "C" void shd_xgroup_destroy(shd_xgroup* g) { x_free(g); }
 
 // nb rounds of the engine group: per round, every engine's k_round_x, the
 // all-to-all, every engine's k_ingest_x
+static bool x_sparse(const shd_xgroup* g) { return g->sp_grid && !g->sp_dense; }
+
 static int x_enqueue_fused(shd_xgroup* g, int nb) {
     shd_eng* e = g->engs[0];
     shd_xgroup::Loc& L = g->loc[0];
     const uint32_t nblk = (uint32_t)((e->nloc + e->P.hpw - 1) / e->P.hpw);
+    const bool sp = x_sparse(g);
     for (int i = 0; i < nb; i++) {
         const int wp = (int)((g->xseq - 1) & 1);   // exchange i - 1 (for round 0: the one before the batch)
-        if (i == 0) {
+        if (sp) {
+            const uint32_t grid = std::max<uint32_t>(g->sp_grid, (uint32_t)g->world);
+            hipLaunchKernelGGL(k_round_spx, dim3(grid), dim3(kBlock), 0, e->stream, g->window, i, &e->d_ring[i],
+                               (const DevCtl*)e->d_ctl, L.parts, (const DParams*)(L.d_xpr + i + 1), &e->d_ring[i + 2],
+                               (const shd_event*)L.xrecv[wp], x_rgn(g, wp), (shd_event* const*)g->d_peers,
+                               L.halt_hdr, g->d_xerr, g->world, g->rank0, wp, x_rep(g, wp), x_hoff(g), kXReplMax,
+                               g->sp_hosts, g->sp_grid, i == 0 ? 1 : 0);
+        } else if (i == 0) {
             hipLaunchKernelGGL(k_round_xtl, dim3(nblk), dim3(kBlock), 0, e->stream, round_args(e->P),
                                (const DParams*)(L.d_xpr + 1), (const shd_event*)L.xrecv[wp], L.halt_hdr,
                                &e->d_ring[2], (const DevCtl*)e->d_ctl, 0, g->window, L.parts);
@@ -627,7 +663,8 @@ static int x_enqueue_fused(shd_xgroup* g, int nb) {
     const int wl = (int)((g->xseq - 1) & 1);
     const Params P = xparams(g, 0, &e->d_ring[nb]);
     hipLaunchKernelGGL(k_xchg_px, dim3((unsigned)g->world + nblk), dim3(kBlock), 0, e->stream, dp(P),
-                       (const TlPart*)L.parts, nblk, nb - 1, (const DevCtl*)e->d_ctl, (shd_event* const*)g->d_peers,
+                       (const TlPart*)L.parts, sp ? g->sp_grid : nblk, nblk, nb - 1, (const DevCtl*)e->d_ctl,
+                       (shd_event* const*)g->d_peers,
                        g->world, g->rank0, wl, (const shd_event*)L.xrecv[wl], x_rgn(g, wl), g->d_xerr, x_rep(g, wl),
                        x_hoff(g), kXReplMax);
     return SHD_OK;
@@ -685,7 +722,7 @@ static int x_launch_rounds(shd_xgroup* g, int nb) {
         return x_enqueue_rounds(g, nb);
     shd_eng* e = g->engs[0];
     const int par = (int)(g->xseq & 1);
-    hipGraphExec_t& ge = g->graph[par];
+    hipGraphExec_t& ge = g->graph[g->fused && x_sparse(g) ? 1 : 0][par];
     if (!ge) {
         const uint64_t xseq0 = g->xseq;
         hipGraph_t gr = nullptr;
@@ -772,8 +809,10 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             SHD_HIP(hipMemsetAsync(e->d_halt, 0, 4, e->stream));
         }
         SHD_HIP(hipEventRecord(g->engs[0]->bev[0], g->engs[0]->stream));
+        const bool sparse_batch = g->fused && x_sparse(g);
         if ((rc = x_launch_rounds(g, nb))) break;
         s.n_batches++;
+        if (sparse_batch) s.n_batches_sparse++;
         g->xepoch += (uint64_t)nb;
         SHD_HIP(hipGetLastError());
         SHD_HIP(hipEventRecord(g->engs[0]->bev[1], g->engs[0]->stream));
@@ -862,6 +901,17 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
                 e->round++;
                 e->parity = (int)(e->round & 1);
             }
+        }
+        if (g->sp_grid && !g->sp_forced && nl == 1) {   // the next batch's kernel, from this batch's activity
+            uint64_t br = 0, ba = 0;
+            const int upto = halted_at >= 0 ? halted_at : nb;
+            for (int i = 0; i < upto; i++) {
+                const DevSummary& r0 = g->engs[0]->h_ring[i + 1];
+                if (r0.flags != 0u || r0.ws >= stop) break;
+                br++;
+                ba += r0.n_active;
+            }
+            if (br) g->sp_dense = (double)ba > kSpDenseFrac * (double)br * (double)g->engs[0]->nloc;
         }
         if (done) break;
         if (halted_at < 0) {

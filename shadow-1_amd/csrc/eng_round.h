@@ -1008,6 +1008,7 @@ struct SpIn {
     int32_t att;
     int4 st;
     int32_t l;
+    uint32_t xwi;   // the engine group's exchange parity of the round (k_round_spx), else 0
 };
 template <bool SP>
 __device__ __forceinline__ void ps_prologue(const DParams& P, HostCtx& c, bool active, uint32_t lb, const PsRsrc& R,
@@ -1032,6 +1033,7 @@ __device__ __forceinline__ void ps_prologue(const DParams& P, HostCtx& c, bool a
     if (SP) {
         if (active) load_ctx(P, c, sp->l, sp->rec, sp->att, sp->st);
         ps_round_reset(P, c, ws, we, parity, false);
+        c.xwi = sp->xwi;
     }
     if (active) {
         if (nin) {   // inbound events of the previous round -> heap
@@ -1791,6 +1793,7 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
             }
             SpIn in;   // the record's loads go out with the bins' (ps_round_body<true>)
             in.l = l;
+            in.xwi = 0;
             if (act) {
                 in.rec = P.hs[l];
                 in.att = P.host_att[P.h0 + l];

@@ -65,7 +65,7 @@ __device__ __forceinline__ bool vrel(const double* vloss, int32_t v, double* r) 
 }
 
 #ifdef SHD_SSSP_TIMING   // measurement build (scripts/sssp_timing.py): cycles per phase per block
-__device__ unsigned long long g_sssp_tim[1024][8];
+__device__ unsigned long long g_sssp_tim[1024][16];
 extern "C" int shd_debug_sssp_timing(unsigned long long* out) {
     if (hipDeviceSynchronize() != hipSuccess) return SHD_ENODEV;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sssp_tim), sizeof(g_sssp_tim)) == hipSuccess ? SHD_OK : SHD_ENODEV;
@@ -97,7 +97,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              shd_pv* __restrict__ out,
                              int64_t* __restrict__ stats, uint64_t* dist, int32_t* parent,
                              uint16_t* upd, int* flags /* LDS int[4] */,
-                             const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
+                             const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows,
+                             int32_t* fl_pre, int32_t* fl_beg, uint64_t* fl_dv /* LDS [BLOCK] each */) {
     const int tid = threadIdx.x;
     for (int32_t v = tid; v < V; v += BLOCK) {
         dist[v] = kDistInf;
@@ -139,6 +140,68 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             int32_t beg = 0, end = 0;
             uint64_t dvb = 0;
             if (fr) { beg = arc_off[v]; end = arc_off[v + 1]; dvb = dist[v]; }
+#ifdef SHD_SSSP_FLAT
+            // A/B (measured and rejected): the chunk's frontier
+            // arcs flattened over the wave -- an exclusive scan of the frontier
+            // lanes' degrees in LDS, each lane up to four arcs per step (owner
+            // by binary search over the scan), every arc's loads out before any
+            // is consumed: one L2 round trip for a chunk's arcs however many
+            // frontier vertices it holds.  37.1 ms for the 10 k table against
+            // 24.5 ms with the half-wave pairs below (a chunk holds ~1.3
+            // frontier vertices in the graph's own order: the scan is overhead)
+            {
+                const int32_t deg = fr ? end - beg : 0;
+                int32_t inc = deg;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const int32_t y = __shfl_up(inc, off, 64);
+                    if (lane >= off) inc += y;
+                }
+                const int32_t total = __shfl(inc, 63, 64);
+                int32_t* pre = fl_pre + wv * 64;
+                fl_pre[wv * 64 + lane] = inc - deg;
+                fl_beg[wv * 64 + lane] = beg;
+                fl_dv[wv * 64 + lane] = dvb;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                for (int32_t k0 = 0; k0 < total; k0 += 256) {
+                    int32_t xs[4];
+                    double ws[4], dv4[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int32_t k = k0 + j * 64 + lane;
+                        xs[j] = -1;
+                        if (k < total) {
+                            int32_t lo = 0, hi = 64;   // the last lane whose exclusive prefix is <= k
+                            while (hi - lo > 1) {
+                                const int32_t mid = (lo + hi) >> 1;
+                                if (pre[mid] <= k) lo = mid; else hi = mid;
+                            }
+                            const int32_t a = fl_beg[wv * 64 + lo] + (k - pre[lo]);
+                            xs[j] = arc_dst[a];
+                            ws[j] = arc_w[a];
+                            dv4[j] = u2d(fl_dv[wv * 64 + lo]);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if (xs[j] < 0) continue;
+                        const int32_t x = xs[j];
+                        const uint64_t nb = d2u(dv4[j] + ws[j]);
+                        if (nb < dist[x]) {
+                            const uint64_t old = atomicMin((unsigned long long*)&dist[x], (unsigned long long)nb);
+                            if (nb < old) {
+                                upd[x] = (uint16_t)(it + 1);
+                                flags[it % 3] = 1;
+                            }
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();   // (the scan slots are rewritten by the wave's next chunk)
+                mask = 0;
+            }
+#endif
             while (mask) {
                 const int l0 = __ffsll((unsigned long long)mask) - 1;
                 mask &= mask - 1;
@@ -188,6 +251,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     // (Round 1 scanned every vertex's in-arcs, lane per vertex: uncoalesced,
     // 9.7 of the 29 ms of the 10 k-row table.)
     int64_t my_ties = 0;
+    SST_T0(t_par)
     if (fpar) {
         // the row's parents given (k_sssp_tie_parents: igraph's first relaxer
         // in its heap's pop order, for a row with equal-cost predecessors)
@@ -248,6 +312,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         atomicAdd((unsigned long long*)&stats[0], (unsigned long long)my_ties);
         flags[3] = 1;
     }
+    SST_ADD(8, t_par)
     if (tid == 0 && !fpar) atomicMax((unsigned long long*)&stats[2], (unsigned long long)it);
     __syncthreads();
     // A vertex with several exact predecessors at the same smallest d[u] (equal-
@@ -278,6 +343,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     const bool has_rsrc = vrel(vloss, src, &rsrc);
     int32_t my_maxhops = 0;
     int64_t my_unroutable = 0, my_mismatch = 0;
+    SST_T0(t_p1)
     // (1) special targets in full, lat half of the others
     for (int32_t j = tid; j < T; j += BLOCK) {
         const int32_t t = attached[j];
@@ -334,6 +400,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         out[(size_t)row * T + j] = shd_pv{lat, rel};
     }
     __syncthreads();
+    SST_ADD(9, t_p1)
+    SST_T0(t_p2)
 #if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 4   // phase ablation: targets' first pass only
     return;
 #endif
@@ -368,6 +436,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         }
     }
     __syncthreads();
+    SST_ADD(10, t_p2)
+    SST_T0(t_p3)
 #if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 3   // phase ablation: no level passes
     return;
 #endif
@@ -405,6 +475,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         }
     }
     __syncthreads();
+    SST_ADD(11, t_p3)
+    SST_T0(t_p4)
     // (4) rel half of the prefix targets
     for (int32_t j = tid; j < T; j += BLOCK) {
         const int32_t t = attached[j];
@@ -419,6 +491,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     if (my_unroutable) atomicAdd((unsigned long long*)&stats[3], (unsigned long long)my_unroutable);
     if (my_mismatch) atomicAdd((unsigned long long*)&stats[4], (unsigned long long)my_mismatch);
     __syncthreads();
+    SST_ADD(12, t_p4)
 }
 
 template <int BLOCK>
@@ -438,13 +511,21 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     int32_t* parent = (int32_t*)(smem + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(smem + (size_t)12 * V);
     int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
+#ifdef SHD_SSSP_FLAT
+    __shared__ int32_t fl_pre[BLOCK], fl_beg[BLOCK];
+    __shared__ uint64_t fl_dv[BLOCK];
+#else
+    int32_t *fl_pre = nullptr, *fl_beg = nullptr;
+    uint64_t* fl_dv = nullptr;
+#endif
     // row_list: the second pass over listed rows [row0, row1) of it, parents from fpar
     for (int32_t i = row0 + (int32_t)blockIdx.x; i < row1; i += gridDim.x) {
         const int32_t row = row_list ? row_list[i] : i;
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
-                            parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows);
+                            parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
+                            fl_beg, fl_dv);
     }
 }
 
@@ -461,6 +542,13 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block, int32_t row0, int32_t row1,
     const int32_t* __restrict__ row_list, const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
     __shared__ int flags[4];
+#ifdef SHD_SSSP_FLAT
+    __shared__ int32_t fl_pre[BLOCK], fl_beg[BLOCK];
+    __shared__ uint64_t fl_dv[BLOCK];
+#else
+    int32_t *fl_pre = nullptr, *fl_beg = nullptr;
+    uint64_t* fl_dv = nullptr;
+#endif
     char* base = scratch + per_block * blockIdx.x;
     uint64_t* dist = (uint64_t*)base;
     int32_t* parent = (int32_t*)(base + (size_t)8 * V);
@@ -470,7 +558,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
-                            parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows);
+                            parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
+                            fl_beg, fl_dv);
     }
 }
 
@@ -691,6 +780,126 @@ static void pc_free_device(shd_pc* pc) {
         if (p) (void)hipFree(p);
 }
 
+// ------------------------------------------------------------------ spatial relabelling
+// A/B, off unless SHD_PC_RELABEL is set (measured and rejected, DESIGN.md §6:
+// 27.7 ms for the 10 k table against 24.5 ms; a compact frontier lands in the
+// chunks of a few waves, which then hold the barrier for the rest).  A vertex
+// order from the graph alone (graphml topologies carry no coordinates):
+// recursive bisection by hop distance -- the subset's BFS distances from a far
+// vertex (the farthest from an arbitrary one), split at the median, until 64
+// vertices -- so that a chunk of 64 consecutive labels is a compact region and
+// a Bellman-Ford frontier (a shell around its source) meets few chunks.
+// perm[old] = new.
+struct PermCsr {
+    std::vector<int32_t> perm, inv;
+    std::vector<int32_t> inc_off, inc_eid, arc_off, arc_dst, arc_eid, rin_off, rin_src, rin_eid, nbr_off, nbr_v, nbr_eid;
+    std::vector<double> arc_w, rin_w;
+    shd_csr view{};
+};
+
+static void spatial_order(const shd_csr& c, std::vector<int32_t>& perm) {
+    const int32_t V = c.V;
+    perm.assign(V, 0);
+    if (!getenv("SHD_PC_RELABEL") || V <= 64) {
+        for (int32_t v = 0; v < V; v++) perm[v] = v;
+        return;
+    }
+    // undirected neighbour lists (both arc directions)
+    std::vector<int32_t> off(V + 1, 0), nb;
+    for (int32_t v = 0; v < V; v++) off[v + 1] = (c.arc_off[v + 1] - c.arc_off[v]) + (c.rin_off[v + 1] - c.rin_off[v]);
+    for (int32_t v = 0; v < V; v++) off[v + 1] += off[v];
+    nb.resize(off[V]);
+    for (int32_t v = 0; v < V; v++) {
+        int32_t k = off[v];
+        for (int32_t a = c.arc_off[v]; a < c.arc_off[v + 1]; a++) nb[k++] = c.arc_dst[a];
+        for (int32_t a = c.rin_off[v]; a < c.rin_off[v + 1]; a++) nb[k++] = c.rin_src[a];
+    }
+    std::vector<int32_t> order(V), dist(V, -1), mark(V, 0), q(V);
+    for (int32_t v = 0; v < V; v++) order[v] = v;
+    int32_t stamp = 0;
+    // BFS within order[lo, hi) (vertices marked `stamp`) from s: dist, the last vertex reached
+    auto bfs = [&](int32_t lo, int32_t hi, int32_t s) {
+        for (int32_t i = lo; i < hi; i++) dist[order[i]] = -1;
+        int32_t qh = 0, qt = 0, last = s;
+        dist[s] = 0;
+        q[qt++] = s;
+        while (qh < qt) {
+            const int32_t u = q[qh++];
+            last = u;
+            for (int32_t k = off[u]; k < off[u + 1]; k++) {
+                const int32_t x = nb[k];
+                if (mark[x] == stamp && dist[x] < 0) { dist[x] = dist[u] + 1; q[qt++] = x; }
+            }
+        }
+        return last;
+    };
+    struct Range { int32_t lo, hi; };
+    std::vector<Range> st{{0, V}};
+    while (!st.empty()) {
+        const Range r = st.back();
+        st.pop_back();
+        if (r.hi - r.lo <= 64) continue;
+        stamp++;
+        for (int32_t i = r.lo; i < r.hi; i++) mark[order[i]] = stamp;
+        const int32_t far = bfs(r.lo, r.hi, bfs(r.lo, r.hi, order[r.lo]));
+        (void)far;
+        // (the second BFS ran from the far vertex: dist holds its distances;
+        // vertices it did not reach sort last, in their current order)
+        std::stable_sort(order.begin() + r.lo, order.begin() + r.hi, [&](int32_t a, int32_t b) {
+            const uint32_t da = (uint32_t)dist[a], db = (uint32_t)dist[b];
+            return da < db;
+        });
+        const int32_t mid = r.lo + (((r.hi - r.lo) / 2 + 63) / 64) * 64;   // chunk-aligned halves
+        st.push_back({mid < r.hi ? mid : r.hi, r.hi});
+        st.push_back({r.lo, mid < r.hi ? mid : r.hi});
+    }
+    for (int32_t i = 0; i < V; i++) perm[order[i]] = i;
+}
+
+static void pc_relabel(const shd_csr& c, PermCsr& p) {
+    const int32_t V = c.V;
+    spatial_order(c, p.perm);
+    p.inv.assign(V, 0);
+    for (int32_t v = 0; v < V; v++) p.inv[p.perm[v]] = v;
+    const auto& perm = p.perm;
+    const auto& inv = p.inv;
+    auto lists = [&](const int32_t* off, std::vector<int32_t>& noff) {
+        noff.assign(V + 1, 0);
+        for (int32_t n = 0; n < V; n++) noff[n + 1] = noff[n] + (off[inv[n] + 1] - off[inv[n]]);
+    };
+    lists(c.inc_off, p.inc_off);
+    lists(c.arc_off, p.arc_off);
+    lists(c.rin_off, p.rin_off);
+    lists(c.nbr_off, p.nbr_off);
+    p.inc_eid.resize(p.inc_off[V] + 1);
+    p.arc_dst.resize(p.arc_off[V] + 1); p.arc_eid.resize(p.arc_off[V] + 1); p.arc_w.resize(p.arc_off[V] + 1);
+    p.rin_src.resize(p.rin_off[V] + 1); p.rin_eid.resize(p.rin_off[V] + 1); p.rin_w.resize(p.rin_off[V] + 1);
+    p.nbr_v.resize(p.nbr_off[V] + 1); p.nbr_eid.resize(p.nbr_off[V] + 1);
+    std::vector<std::pair<int32_t, int32_t>> tmp;
+    for (int32_t n = 0; n < V; n++) {
+        const int32_t o = inv[n];
+        for (int32_t k = c.inc_off[o], j = p.inc_off[n]; k < c.inc_off[o + 1]; k++, j++) p.inc_eid[j] = c.inc_eid[k];
+        for (int32_t k = c.arc_off[o], j = p.arc_off[n]; k < c.arc_off[o + 1]; k++, j++) {   // incidence order kept
+            p.arc_dst[j] = perm[c.arc_dst[k]]; p.arc_eid[j] = c.arc_eid[k]; p.arc_w[j] = c.arc_w[k];
+        }
+        for (int32_t k = c.rin_off[o], j = p.rin_off[n]; k < c.rin_off[o + 1]; k++, j++) {
+            p.rin_src[j] = perm[c.rin_src[k]]; p.rin_eid[j] = c.rin_eid[k]; p.rin_w[j] = c.rin_w[k];
+        }
+        // neighbour lists sorted again by (new neighbour label, eid): the lowest
+        // parallel eid stays first for get_eid
+        tmp.clear();
+        for (int32_t k = c.nbr_off[o]; k < c.nbr_off[o + 1]; k++) tmp.push_back({perm[c.nbr_v[k]], c.nbr_eid[k]});
+        std::sort(tmp.begin(), tmp.end());
+        for (size_t k = 0; k < tmp.size(); k++) { p.nbr_v[p.nbr_off[n] + k] = tmp[k].first; p.nbr_eid[p.nbr_off[n] + k] = tmp[k].second; }
+    }
+    shd_csr& w = p.view;
+    w.V = V; w.E = c.E; w.directed = c.directed; w.max_degree = c.max_degree;
+    w.inc_off = p.inc_off.data(); w.inc_eid = p.inc_eid.data();
+    w.arc_off = p.arc_off.data(); w.arc_dst = p.arc_dst.data(); w.arc_eid = p.arc_eid.data(); w.arc_w = p.arc_w.data();
+    w.rin_off = p.rin_off.data(); w.rin_src = p.rin_src.data(); w.rin_eid = p.rin_eid.data(); w.rin_w = p.rin_w.data();
+    w.nbr_off = p.nbr_off.data(); w.nbr_v = p.nbr_v.data(); w.nbr_eid = p.nbr_eid.data();
+}
+
 extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_t n_attached, uint32_t flags,
                              int device, shd_pc** out) {
     if (!g || !attached || n_attached <= 0 || !out) return SHD_EINVAL;
@@ -739,7 +948,15 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
         shd_pc_destroy(pc);
         return SHD_ENODEV;
     }
-    const shd_csr& c = pc->csr;
+    // the device's copy of the graph, relabelled in a spatial order when
+    // SHD_PC_RELABEL is set (pc_relabel; the identity otherwise).  Every rule
+    // that depends on order keeps the original one: each vertex's arcs stay in
+    // igraph incidence order (the tie rows' heap Dijkstra relaxes in it),
+    // parents break ties by original edge ids, and the neighbour lists keep the
+    // lowest parallel edge id first.
+    PermCsr pcsr;
+    pc_relabel(pc->csr, pcsr);
+    const shd_csr& c = pcsr.view;
     const int32_t na = c.arc_off[V];
     // per forward arc: its tail vertex and the index of the same arc among its
     // head's in-arcs (the parent pass streams the forward arcs, the tree walks
@@ -767,12 +984,21 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
         (rc = dalloc_copy(&pc->d_inc_eid, c.inc_eid, c.inc_off[V])) ||
         (rc = dalloc_copy(&pc->d_nbr_off, c.nbr_off, V + 1)) || (rc = dalloc_copy(&pc->d_nbr_v, c.nbr_v, c.nbr_off[V])) ||
         (rc = dalloc_copy(&pc->d_nbr_eid, c.nbr_eid, c.nbr_off[V])) || (rc = dalloc_copy(&pc->d_w, pc->h_w, E)) ||
-        (rc = dalloc_copy(&pc->d_eloss, pc->h_eloss, E)) || (rc = dalloc_copy(&pc->d_attached, pc->h_attached, T)) ||
-        (rc = dalloc_copy(&pc->d_self_eid, pc->h_self_eid, T))) {
+        (rc = dalloc_copy(&pc->d_eloss, pc->h_eloss, E)) || (rc = dalloc_copy(&pc->d_self_eid, pc->h_self_eid, T))) {
         shd_pc_destroy(pc);
         return rc;
     }
-    if (pc->has_vloss && (rc = dalloc_copy(&pc->d_vloss, pc->h_vloss, V))) { shd_pc_destroy(pc); return rc; }
+    {   // attached vertices and vertex loss factors in the device's labels
+        std::vector<int32_t> att_d(T);
+        for (int32_t i = 0; i < T; i++) att_d[i] = pcsr.perm[attached[i]];
+        std::vector<double> vl_d(V);
+        for (int32_t v = 0; v < V; v++) vl_d[pcsr.perm[v]] = pc->h_vloss[v];
+        if ((rc = dalloc_copy(&pc->d_attached, att_d.data(), T)) ||
+            (pc->has_vloss && (rc = dalloc_copy(&pc->d_vloss, vl_d.data(), V)))) {
+            shd_pc_destroy(pc);
+            return rc;
+        }
+    }
     const size_t TT = (size_t)T * T;
     if (hipMalloc((void**)&pc->d_dir, sizeof(shd_pv) * TT) != hipSuccess ||
         hipMalloc((void**)&pc->d_adj, TT) != hipSuccess || hipMalloc((void**)&pc->d_self, sizeof(shd_pv) * T) != hipSuccess ||
@@ -801,7 +1027,13 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
 #endif
 constexpr int kRowBlock = SHD_ROW_BLOCK;   // workgroup of the LDS row kernel past 2 k vertices
 static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
+// the dynamic row arrays' budget: 160 KiB less the kernels' static LDS (the
+// SHD_SSSP_FLAT A/B's scan slots, 16 B a thread of the 1024-thread block)
+#ifdef SHD_SSSP_FLAT
+static constexpr size_t kLdsMax = 160 * 1024 - 16 * 1024 - 64;
+#else
 static constexpr size_t kLdsMax = 160 * 1024;
+#endif
 
 // The rows the first pass listed (equal-cost predecessors somewhere in the
 // row): their parents from k_sssp_tie_parents, in chunks of rows whose heaps
@@ -1243,6 +1475,169 @@ static int pc_lookup_at(shd_pc* pc, int32_t a, int32_t b, double* lat, double* r
     if (ra != kNoRank && (rb == kNoRank || ra < rb))
         return fetch2(pc, pc->d_row, (size_t)a * T + b, lat, rel);
     return fetch2(pc, pc->d_row, (size_t)b * T + a, lat, rel);
+}
+
+// ------------------------------------------------------------------ batched lazy lookup
+// shd_pc_lookup over a list of queries in their order, with one upload, one
+// gather kernel and one download instead of a device round trip per query:
+// the rank rule (pc_lookup_at) runs on the host to name each query's table
+// entry, the entries are gathered on the device, and the rows the batch ranks
+// fold their newly stored entries into minimumPathLatency on the device
+// (run_row_for_min's rule, with "stored when the row ran" read off the final
+// ranks: a target stored before row a ran has a smaller rank than a's).
+enum : uint8_t { kPvDir = 0, kPvSelf = 1, kPvRow = 2, kPvFail = 3 };
+
+__global__ void k_pc_gather(const uint8_t* __restrict__ kind, const uint64_t* __restrict__ idx, uint64_t n,
+                            const shd_pv* __restrict__ dir, const shd_pv* __restrict__ self,
+                            const shd_pv* __restrict__ row, shd_pv* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t k = kind[i];
+        shd_pv v{-1.0, -1.0};
+        if (k == kPvDir) v = dir[idx[i]];
+        else if (k == kPvSelf) v = self[idx[i]];
+        else if (k == kPvRow) v = row[idx[i]];
+        out[i] = v;
+    }
+}
+
+// min over the entries each newly ranked row stored (rows[j] ranked rrank[j])
+__global__ void k_pc_newrow_min(const int32_t* __restrict__ rows, const int32_t* __restrict__ rrank, int32_t nr,
+                                int32_t T, const int32_t* __restrict__ rank, const int32_t* __restrict__ self_rank,
+                                const shd_pv* __restrict__ row, const uint8_t* __restrict__ adj, int prefer_direct,
+                                unsigned long long* __restrict__ out) {
+    __shared__ unsigned long long sm[256];
+    unsigned long long m = kDistInf;
+    const size_t n = (size_t)nr * T;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int32_t j = (int32_t)(i / T), t = (int32_t)(i % T), a = rows[j], R = rrank[j];
+        const bool stored = t == a ? self_rank[a] < R : rank[t] < R;
+        if (stored) continue;
+        if (prefer_direct && adj[(size_t)a * T + t]) continue;
+        const double lat = row[(size_t)a * T + t].lat;
+        if (!(lat >= 0.0)) continue;
+        const unsigned long long b = (unsigned long long)__double_as_longlong(lat);
+        m = b < m ? b : m;
+    }
+    sm[threadIdx.x] = m;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k && sm[threadIdx.x + k] < sm[threadIdx.x]) sm[threadIdx.x] = sm[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMin(out, sm[0]);
+}
+
+extern "C" int shd_pc_lookup_batch(shd_pc* pc, const int32_t* src_vertex, const int32_t* dst_vertex, uint64_t n,
+                                   double* lat, double* rel) {
+    if (!pc || !pc->built || (n && (!src_vertex || !dst_vertex || !lat || !rel))) return SHD_EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (src_vertex[i] < 0 || dst_vertex[i] < 0 || src_vertex[i] >= pc->V || dst_vertex[i] >= pc->V ||
+            pc->h_att_index[src_vertex[i]] < 0 || pc->h_att_index[dst_vertex[i]] < 0)
+            return SHD_EINVAL;
+    PcTouches* tch = (PcTouches*)pc->touches;
+    if ((tch && tch->on) || (!pc->complete && !pc->rows_mode)) {   // the co-simulation's protocol: query by query
+        for (uint64_t i = 0; i < n; i++) {
+            const int rc = shd_pc_lookup(pc, src_vertex[i], dst_vertex[i], &lat[i], &rel[i]);
+            if (rc) return rc;
+        }
+        return SHD_OK;
+    }
+    if (!n) return SHD_OK;
+    const int32_t T = pc->T;
+    std::vector<uint8_t> kind(n);
+    std::vector<uint64_t> idx(n);
+    std::vector<int32_t> nrow, nrank;
+    for (uint64_t i = 0; i < n; i++) {   // pc_lookup_at's rule, deciding the entry only
+        const int32_t a = pc->h_att_index[src_vertex[i]], b = pc->h_att_index[dst_vertex[i]];
+        const bool adj = pc->prefer_direct && !pc->complete &&
+                         shd_csr_get_eid(&pc->csr, pc->h_attached[a], pc->h_attached[b]) >= 0;
+        if (pc->complete || adj) { kind[i] = kPvDir; idx[i] = (uint64_t)a * T + b; continue; }
+        if (a == b) {
+            int32_t ra = pc->h_rank[a], rs = pc->h_self_rank[a];
+            if (ra == kNoRank && rs == kNoRank) pc->h_self_rank[a] = rs = pc->next_rank++;
+            if (rs < ra) { kind[i] = kPvSelf; idx[i] = (uint64_t)a; }
+            else { kind[i] = kPvRow; idx[i] = (uint64_t)a * T + a; }
+            continue;
+        }
+        int32_t ra = pc->h_rank[a], rb = pc->h_rank[b];
+        const bool hit = pc->directed ? (ra != kNoRank && ra < rb) : (ra != kNoRank || rb != kNoRank);
+        if (!hit) {
+            if (pc->h_rank[a] == kNoRank) {
+                pc->h_rank[a] = pc->next_rank++;
+                nrow.push_back(a);
+                nrank.push_back(pc->h_rank[a]);
+            }
+            ra = pc->h_rank[a];
+            if (pc->h_self_eid[a] < 0) { kind[i] = kPvFail; idx[i] = 0; continue; }
+        }
+        kind[i] = kPvRow;
+        idx[i] = (ra != kNoRank && (rb == kNoRank || ra < rb)) ? (uint64_t)a * T + b : (uint64_t)b * T + a;
+    }
+    SHD_HIP(hipSetDevice(pc->device));
+    hipStream_t s = pc->stream;
+    uint8_t* d_kind = nullptr;
+    uint64_t* d_idx = nullptr;
+    shd_pv* d_out = nullptr;
+    int32_t *d_rows = nullptr, *d_rrank = nullptr, *d_rank = nullptr, *d_srank = nullptr;
+    unsigned long long* d_min = nullptr;
+    std::vector<shd_pv> out(n);
+    unsigned long long mn = kDistInf;
+    int rc = SHD_OK;
+    const size_t nr = nrow.size();
+    if (hipMalloc(&d_kind, n) != hipSuccess || hipMalloc(&d_idx, 8 * n) != hipSuccess ||
+        hipMalloc(&d_out, sizeof(shd_pv) * n) != hipSuccess || hipMalloc(&d_min, 8) != hipSuccess ||
+        (nr && (hipMalloc(&d_rows, 4 * nr) != hipSuccess || hipMalloc(&d_rrank, 4 * nr) != hipSuccess ||
+                hipMalloc(&d_rank, 4 * (size_t)T) != hipSuccess || hipMalloc(&d_srank, 4 * (size_t)T) != hipSuccess))) {
+        rc = SHD_ENOMEM;
+        goto done;
+    }
+    if (hipMemcpyAsync(d_kind, kind.data(), n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_idx, idx.data(), 8 * n, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(d_min, &mn, 8, hipMemcpyHostToDevice, s) != hipSuccess) { rc = SHD_ENODEV; goto done; }
+    hipLaunchKernelGGL(k_pc_gather, dim3((unsigned)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s,
+                       d_kind, d_idx, n, pc->d_dir, pc->d_self, pc->d_row, d_out);
+    if (nr) {
+        if (hipMemcpyAsync(d_rows, nrow.data(), 4 * nr, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(d_rrank, nrank.data(), 4 * nr, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(d_rank, pc->h_rank, 4 * (size_t)T, hipMemcpyHostToDevice, s) != hipSuccess ||
+            hipMemcpyAsync(d_srank, pc->h_self_rank, 4 * (size_t)T, hipMemcpyHostToDevice, s) != hipSuccess) {
+            rc = SHD_ENODEV;
+            goto done;
+        }
+        const size_t tot = nr * (size_t)T;
+        hipLaunchKernelGGL(k_pc_newrow_min, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, s,
+                           d_rows, d_rrank, (int32_t)nr, T, d_rank, d_srank, pc->d_row, pc->d_adj,
+                           pc->prefer_direct, d_min);
+    }
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(out.data(), d_out, sizeof(shd_pv) * n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(&mn, d_min, 8, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        rc = SHD_ENODEV;
+        goto done;
+    }
+    // minimumPathLatency: the new rows' stored entries (in rank order, min is
+    // order-free), then the direct and self values as pc_lookup_at notes them
+    if (nr && mn != kDistInf) {
+        double m;
+        memcpy(&m, &mn, 8);
+        note_min(pc, m);
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        double l = out[i].lat, r = out[i].rel;
+        if (kind[i] == kPvDir) {
+            if (isnan(l)) { l = -1; r = -1; }
+            else note_min(pc, l);
+        } else if (kind[i] == kPvSelf) {
+            if (l >= 0) note_min(pc, l);
+        }
+        lat[i] = l;
+        rel[i] = r;
+    }
+done:
+    for (void* q : {(void*)d_kind, (void*)d_idx, (void*)d_out, (void*)d_rows, (void*)d_rrank, (void*)d_rank,
+                    (void*)d_srank, (void*)d_min})
+        if (q) (void)hipFree(q);
+    return rc;
 }
 
 extern "C" int shd_pc_count_packet(shd_pc* pc, int32_t sv, int32_t dv) {

@@ -40,10 +40,12 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
 #include "../../include/shdtcp.h"
+#include "shd_device.h"   // struct shd_pc: the path cache's device tables (shd_tcp_model.path_cache)
 
 namespace {
 
@@ -80,6 +82,9 @@ constexpr uint32_t kMailSack = 8;   // SACK entries per mailbox slot on average 
 constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
 constexpr uint32_t kTrk = 10;       // tracker counters per direction (DHost::trk)
 constexpr uint32_t kXRetx = 1;      // DPkt::xflags: the packet was retransmitted (PDS_SND_TCP_RETRANSMITTED)
+constexpr uint32_t kLocalRanks = 6;  // path_cache mode: rows a lane can run in one round (more: fall back)
+constexpr int32_t kLocalRank0 = 0x7FFF0000;   // pseudo-ranks of a lane's in-round rows: past every real rank
+enum : uint32_t { kFtRowA = 0, kFtRowB = 1, kFtSelf = 2 };
 
 // ProtocolTCPFlags (protocol.h:23-31)
 enum : uint32_t { F_RST = 1 << 1, F_SYN = 1 << 2, F_ACK = 1 << 3, F_SACK = 1 << 4, F_FIN = 1 << 5, F_DUPACK = 1 << 6 };
@@ -233,6 +238,8 @@ struct TCtl {
     uint64_t rounds;     // rounds started; round k reads mailbox k & 1 and writes the other
     uint32_t halted, _pad;
     uint64_t max_mail;   // the most deliveries one round's mailbox took (shd_tcp_result)
+    uint64_t max_ovf;    // ... and the most of them in its shared overflow range
+    uint32_t ft_bad, _pad2;   // path_cache mode: a round's first-touch choice the serial order contradicts
 };
 
 struct Glob {
@@ -275,6 +282,21 @@ struct Glob {
     uint32_t node_k, qdisc_rr;
     uint64_t* prof;         // SHD_TCP_PROF builds: [H][2 * kProf] cycles and counts per step
     uint32_t* prof_round;   // [2][kProfRounds] per round: the most events and cycles of a lane
+    // path_cache mode (shd_tcp_model.path_cache): the cache's device tables
+    // ([T][T] rows and direct values, [T] self values), the ranks as of the
+    // round's start (kNoRank: never), and the round's log of queries whose
+    // row depended on the order within the round (pc_query, k_tcp_window)
+    const shd_pv *prow, *pself, *pdir;
+    const uint8_t* padj;
+    const int32_t* pself_eid;
+    int32_t* rank;          // [T] row run order
+    int32_t* srank;         // [T] self-path store order
+    int32_t* next_rank;     // [1]
+    shd_tcp_query* ft;      // [ft_cap] (_pad: the choice, kFtRowA / kFtRowB / kFtSelf)
+    uint32_t* nft;
+    int32_t* ftord;         // [ft_cap] the log in serial order (scratch of k_tcp_window)
+    uint32_t ft_cap; int32_t pT;
+    uint32_t pcm, pc_complete, pc_prefer_direct, _pad6;
 };
 
 // ------------------------------------------------------------ per-lane context
@@ -289,6 +311,10 @@ struct L {
     uint32_t ksrc, kq;
     uint64_t kseq;
     uint64_t mail_min;      // the earliest delivery this lane sent this round (part counters)
+    // path_cache mode: the rows / self paths this lane's own queries ran in the
+    // round so far (vertex * 2 + kind), in order: its pseudo-ranks
+    uint32_t nlr;
+    int32_t lr[kLocalRanks];
 };
 __device__ __forceinline__ DPkt* PK(const L& c, int32_t i) { return &c.g->pool[(size_t)c.h * c.g->pool_cap + i]; }
 __device__ __forceinline__ int32_t* PSK(const L& c, int32_t i) {
@@ -686,16 +712,94 @@ __device__ void touch_log(L& c, int32_t va, int32_t vb) {
 // (latency < 0: shd_tcp_run refuses models whose connections have one, so
 // this is an internal error) fails the run instead of scheduling a delivery
 // at a negative delay
+// path_cache mode: the lazy cache's rule (pathcache.hip pc_lookup_at,
+// topology.c:1969-2051) on the device.  A pair with a ranked endpoint at the
+// round's start is decided: the lower-ranked endpoint's row (self pairs: the
+// self path or the row, by the same rule).  A pair with none depends on the
+// order of the round's first touches: the lane decides it as the serial loop
+// would if no other lane touched these vertices earlier in the window -- the
+// round-start ranks plus its own earlier rows of the round (pseudo-ranks) --
+// and logs the query with its key and choice; k_tcp_window replays the log in
+// serial order, ranks the rows that ran and checks every choice.
+__device__ int32_t eff_rank(const L& c, int32_t v, uint32_t kind) {
+    const int32_t r = kind ? c.g->srank[v] : c.g->rank[v];
+    if (r != kNoRank) return r;
+    const int32_t key = v * 2 + (int32_t)kind;
+    for (uint32_t p = 0; p < c.nlr && p < kLocalRanks; p++)
+        if (c.lr[p] == key) return kLocalRank0 + (int32_t)p;
+    return kNoRank;
+}
+__device__ void ft_log(L& c, int32_t va, int32_t vb, uint32_t choice) {
+    const uint32_t slot = atomicAdd(c.g->nft, 1u);
+    if (slot >= c.g->ft_cap) { c.H->err |= SHD_TCP_ERR_FIRST_TOUCH; return; }
+    shd_tcp_query r;
+    r.time = c.now; r.seq = c.kseq; r.host = (uint32_t)c.h; r.src = c.ksrc; r.index = c.kq - 1;
+    r.v_src = va; r.v_dst = vb; r._pad = choice;
+    c.g->ft[slot] = r;
+}
+__device__ void ft_run_local(L& c, int32_t v, uint32_t kind) {
+    if (c.nlr >= kLocalRanks) { c.H->err |= SHD_TCP_ERR_FIRST_TOUCH; return; }
+    c.lr[c.nlr++] = v * 2 + (int32_t)kind;
+}
+// the query of vertex pair (va, vb); want: the value is used (not only the
+// first touch of topology_isRoutable)
+__device__ void pc_query(L& c, int32_t va, int32_t vb, double& lat, double& rel) {
+    const Glob& g = *c.g;
+    const size_t T = (size_t)g.pT;
+    c.kq++;
+    shd_pv v{-1.0, -1.0};
+    if (g.pc_complete || (g.pc_prefer_direct && g.padj[(size_t)va * T + vb])) {
+        v = g.pdir[(size_t)va * T + vb];
+        if (isnan(v.lat)) v = shd_pv{-1.0, -1.0};
+    } else if (va == vb) {
+        const int32_t ra0 = g.rank[va], rs0 = g.srank[va];
+        bool self;
+        if (ra0 == kNoRank && rs0 == kNoRank) {
+            const int32_t ra = eff_rank(c, va, 0), rs = eff_rank(c, va, 1);
+            if (ra == kNoRank && rs == kNoRank) { ft_run_local(c, va, 1); self = true; }
+            else self = rs < ra;
+            ft_log(c, va, vb, self ? kFtSelf : kFtRowA);
+        } else {
+            self = rs0 < ra0;
+        }
+        v = self ? g.pself[va] : g.prow[(size_t)va * T + va];
+    } else {
+        const int32_t ra0 = g.rank[va], rb0 = g.rank[vb];
+        bool own;
+        bool fail = false;
+        if (ra0 == kNoRank && rb0 == kNoRank) {
+            const int32_t ra = eff_rank(c, va, 0), rb = eff_rank(c, vb, 0);
+            if (ra == kNoRank && rb == kNoRank) {   // a miss: va's row runs (and fails without a self-loop)
+                ft_run_local(c, va, 0);
+                own = true;
+                fail = g.pself_eid[va] < 0;
+            } else {
+                own = ra != kNoRank && (rb == kNoRank || ra < rb);
+            }
+            ft_log(c, va, vb, own ? kFtRowA : kFtRowB);
+        } else {
+            own = ra0 != kNoRank && (rb0 == kNoRank || ra0 < rb0);
+        }
+        if (!fail) v = own ? g.prow[(size_t)va * T + vb] : g.prow[(size_t)vb * T + va];
+    }
+    lat = v.lat;
+    rel = v.rel;
+}
+
 __device__ void path(L& c, int32_t a, int32_t b, double& lat, double& rel) {
     if (a < 0 || b < 0) {
         c.H->err |= SHD_TCP_ERR_INTERNAL;
         lat = 1.0; rel = 0.0;
         return;
     }
-    touch_log(c, c.g->hv[a], c.g->hv[b]);
-    const size_t i = (size_t)c.g->hv[a] * (size_t)c.g->V + (size_t)c.g->hv[b];
-    lat = c.g->lat[i];
-    rel = c.g->rel[i];
+    if (c.g->pcm) {
+        pc_query(c, c.g->hv[a], c.g->hv[b], lat, rel);
+    } else {
+        touch_log(c, c.g->hv[a], c.g->hv[b]);
+        const size_t i = (size_t)c.g->hv[a] * (size_t)c.g->V + (size_t)c.g->hv[b];
+        lat = c.g->lat[i];
+        rel = c.g->rel[i];
+    }
     if (!(lat >= 0.0)) {
         c.H->err |= SHD_TCP_ERR_INTERNAL;
         lat = 1.0; rel = 0.0;
@@ -1569,7 +1673,8 @@ __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:
     double lat, rel;
     if (ks->pc_ip != 0 && ks->pc_ip == p->dip) {   // the sending socket's path: no dependent loads
         d = ks->pc_host;
-        touch_log(c, ks->pc_va, ks->pc_vb);
+        if (c.g->pcm) c.kq++;   // the pair's value is stored: a repeat query changes nothing
+        else touch_log(c, ks->pc_va, ks->pc_vb);
         lat = ks->pc_lat; rel = ks->pc_rel;
     } else {
         d = host_of_ip(c, p->dip);
@@ -1889,7 +1994,14 @@ __device__ void app_run(L& c, DProc* pr) {
             const int32_t sh = sp->host;
             const uint32_t ip = c.g->host[sh].ip;
             const uint16_t port = c.g->sock[sp->listenfd].bound_port;
-            if (ip != c.H->ip) touch_log(c, c.g->hv[c.h], c.g->hv[sh]);   // topology_isRoutable (host.c:1224-1234)
+            if (ip != c.H->ip) {   // topology_isRoutable (host.c:1224-1234): a first touch, value unused
+                if (c.g->pcm) {
+                    double l_, r_;
+                    pc_query(c, c.g->hv[c.h], c.g->hv[sh], l_, r_);
+                } else {
+                    touch_log(c, c.g->hv[c.h], c.g->hv[sh]);
+                }
+            }
             DSock* k = &c.g->sock[pr->fd];
             if (!k->bound) {   // implicit bind to the default interface, peer-specific
                 const uint16_t bp = random_free_port(c);
@@ -2050,10 +2162,108 @@ __global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
 // earliest pending event of any host or mailbox); ends the run at end_time.
 // One block; launched before every round, so a batch of rounds runs without
 // the host.
+// path_cache mode: the last round's first-touch log in serial order
+// (event_compare's key, then the query's index in its event), replayed
+// against the ranks: each logged choice checked, the rows and self paths that
+// ran ranked (pc_lookup_at's rule).  One block; the log is small (a vertex is
+// first touched once per run).
+struct FtKey {
+    uint64_t time, seq;
+    uint32_t host, src, index, pad;
+};
+__device__ __forceinline__ bool ft_less(const FtKey& x, const FtKey& y) {
+    if (x.time != y.time) return x.time < y.time;
+    if (x.host != y.host) return x.host < y.host;
+    if (x.src != y.src) return x.src < y.src;
+    if (x.seq != y.seq) return x.seq < y.seq;
+    return x.index < y.index;
+}
+constexpr uint32_t kFtTile = 512;
+constexpr int32_t kFtLdsRanks = 4096;   // vertices whose ranks the replay keeps in LDS
+__device__ bool ft_replay(const Glob& g, uint32_t n) {
+    __shared__ FtKey tile[kFtTile];
+    __shared__ int32_t s_rank[kFtLdsRanks], s_srank[kFtLdsRanks];
+    __shared__ uint32_t s_bad;
+    const uint32_t tid = threadIdx.x, nt = blockDim.x;
+    // positions: the entries with a smaller key (the keys are distinct)
+    for (uint32_t base = 0; base < n; base += nt) {
+        const uint32_t i = base + tid;
+        const bool own = i < n;
+        FtKey a{};
+        if (own) { const shd_tcp_query& q = g.ft[i]; a = FtKey{q.time, q.seq, q.host, q.src, q.index, 0}; }
+        uint32_t pos = 0;
+        for (uint32_t t0 = 0; t0 < n; t0 += kFtTile) {
+            __syncthreads();
+            for (uint32_t j = tid; j < kFtTile && t0 + j < n; j += nt) {
+                const shd_tcp_query& q = g.ft[t0 + j];
+                tile[j] = FtKey{q.time, q.seq, q.host, q.src, q.index, 0};
+            }
+            __syncthreads();
+            const uint32_t m = n - t0 < kFtTile ? n - t0 : kFtTile;
+            if (own)
+                for (uint32_t j = 0; j < m; j++) pos += ft_less(tile[j], a) ? 1u : 0u;
+        }
+        if (own) g.ftord[pos] = (int32_t)i;
+    }
+    const bool lds = g.pT <= kFtLdsRanks;
+    if (lds)
+        for (int32_t v = (int32_t)tid; v < g.pT; v += (int32_t)nt) { s_rank[v] = g.rank[v]; s_srank[v] = g.srank[v]; }
+    if (tid == 0) s_bad = 0;
+    __syncthreads();
+    int32_t* rk = lds ? s_rank : g.rank;
+    int32_t* sk = lds ? s_srank : g.srank;
+    // the replay, in chunks of the sorted (source, destination, choice) staged in LDS
+    int32_t nr = *g.next_rank;
+    uint32_t* chunk = (uint32_t*)tile;   // 3 words an entry
+    constexpr uint32_t kChunk = sizeof(tile) / 12;
+    for (uint32_t c0 = 0; c0 < n; c0 += kChunk) {
+        const uint32_t m = n - c0 < kChunk ? n - c0 : kChunk;
+        __syncthreads();
+        for (uint32_t j = tid; j < m; j += nt) {
+            const shd_tcp_query& q = g.ft[g.ftord[c0 + j]];
+            chunk[3 * j] = (uint32_t)q.v_src; chunk[3 * j + 1] = (uint32_t)q.v_dst; chunk[3 * j + 2] = q._pad;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (uint32_t j = 0; j < m; j++) {
+                const int32_t a = (int32_t)chunk[3 * j], b = (int32_t)chunk[3 * j + 1];
+                const uint32_t choice = chunk[3 * j + 2];
+                uint32_t truth;
+                if (a == b) {
+                    const int32_t ra = rk[a], rs = sk[a];
+                    if (ra == kNoRank && rs == kNoRank) { sk[a] = nr++; truth = kFtSelf; }
+                    else truth = rs < ra ? kFtSelf : kFtRowA;
+                } else {
+                    const int32_t ra = rk[a], rb = rk[b];
+                    if (ra == kNoRank && rb == kNoRank) { rk[a] = nr++; truth = kFtRowA; }
+                    else truth = (ra != kNoRank && (rb == kNoRank || ra < rb)) ? kFtRowA : kFtRowB;
+                }
+                if (truth != choice) s_bad = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (lds)
+        for (int32_t v = (int32_t)tid; v < g.pT; v += (int32_t)nt) { g.rank[v] = s_rank[v]; g.srank[v] = s_srank[v]; }
+    if (tid == 0) { *g.next_rank = nr; *g.nft = 0; }
+    __syncthreads();
+    return s_bad != 0;
+}
+
 __global__ void k_tcp_window(Glob g) {
     __shared__ uint64_t red[16];
     TCtl* ctl = g.ctl;
     if (ctl->halted) return;
+    if (g.pcm) {
+        const uint32_t n = *g.nft;   // the last round's log (uniform)
+        if (n) {
+            const bool bad = n > g.ft_cap || ft_replay(g, n);
+            if (bad) {
+                if (threadIdx.x == 0) { ctl->ft_bad = 1; ctl->halted = 1; }
+                return;
+            }
+        }
+    }
     __shared__ uint32_t s_mail;
     if (threadIdx.x == 0) s_mail = 0;
     __syncthreads();
@@ -2065,6 +2275,7 @@ __global__ void k_tcp_window(Glob g) {
             const uint32_t cap = threadIdx.x < kMailSub ? g.mail_part : g.mail_cap - g.mail_part * kMailSub;
             const uint32_t v = *n;
             if (v) atomicAdd(&s_mail, v < cap ? v : cap);
+            if (threadIdx.x == kMailSub && v > ctl->max_ovf) ctl->max_ovf = v < cap ? v : cap;
             *n = 0;
         }
         if (threadIdx.x == kMailSub + 1) g.nmsack[(k + 1) & 1] = 0;
@@ -2252,44 +2463,138 @@ int32_t rand_r_host(uint32_t* state) {
 
 }  // namespace
 
+// path_cache mode's window and route check, from the cache's device tables:
+// the smallest ceil(latency) in ns over the connections' vertex pairs (hosts
+// that talk only to their peers: the same pairs the table path fills), in
+// both orientations' rows (either endpoint's may serve the pair; the window
+// only bounds the rounds), and whether some connection's pair has no route.
+// conn: (client vertex, server vertex, same host) triples.
+__global__ void k_tcp_pc_prep(const shd_pv* __restrict__ row, const shd_pv* __restrict__ self,
+                              const shd_pv* __restrict__ dir, const uint8_t* __restrict__ adj, int complete,
+                              int prefer_direct, int32_t T, const int32_t* __restrict__ conn, int32_t nconn,
+                              unsigned long long* __restrict__ out) {
+    auto lat_of = [&](int32_t u, int32_t v, double& l) {
+        if (complete || (prefer_direct && adj[(size_t)u * T + v])) { l = dir[(size_t)u * T + v].lat; return; }
+        if (u == v) {
+            const double a = self[u].lat, b = row[(size_t)u * T + u].lat;
+            l = (a >= 0 && (b < 0 || a < b)) ? a : b;
+            return;
+        }
+        const double a = row[(size_t)u * T + v].lat, b = row[(size_t)v * T + u].lat;
+        l = (a >= 0 && b >= 0) ? (a < b ? a : b) : -1.0;
+    };
+    unsigned long long w = ~0ull;
+    for (int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); k < nconn; k += (int32_t)(gridDim.x * blockDim.x)) {
+        const int32_t u = conn[3 * k], v = conn[3 * k + 1];
+        double l1, l2;
+        lat_of(u, v, l1);
+        lat_of(v, u, l2);
+        if (!(l1 >= 0) || !(l2 >= 0)) { atomicOr(out + 1, 1ull); continue; }
+        if (conn[3 * k + 2]) continue;   // a host's connection to itself: the loopback, no path
+        const double l = l1 < l2 ? l1 : l2;
+        const unsigned long long x = (unsigned long long)ceil(l * (double)kMs);
+        w = x < w ? x : w;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(w, o);
+        w = y < w ? y : w;
+    }
+    if ((threadIdx.x & 63) == 0 && w != ~0ull) atomicMin(out, w);
+}
+
+static int tcp_pc_prep(shd_pc* pc, const std::vector<int32_t>& conn, uint64_t* W) {
+    int32_t* d_conn = nullptr;
+    unsigned long long* d_out = nullptr;
+    unsigned long long h_out[2] = {~0ull, 0ull};
+    int rc = 0;
+    const int32_t T = pc->T;
+    const int32_t nconn = (int32_t)(conn.size() / 3);
+    if (hipSetDevice(pc->device) != hipSuccess || hipMalloc(&d_conn, sizeof(int32_t) * (conn.size() + 3)) != hipSuccess ||
+        hipMalloc(&d_out, 16) != hipSuccess ||
+        (nconn && hipMemcpy(d_conn, conn.data(), sizeof(int32_t) * conn.size(), hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(d_out, h_out, 16, hipMemcpyHostToDevice) != hipSuccess) {
+        rc = -5;
+    } else {
+        k_tcp_pc_prep<<<(unsigned)std::min<int32_t>((nconn + 255) / 256 + 1, 1024), 256>>>(
+            pc->d_row, pc->d_self, pc->d_dir, pc->d_adj, pc->complete, pc->prefer_direct, T, d_conn, nconn, d_out);
+        if (hipGetLastError() != hipSuccess || hipMemcpy(h_out, d_out, 16, hipMemcpyDeviceToHost) != hipSuccess) rc = -5;
+    }
+    (void)hipFree(d_conn); (void)hipFree(d_out);
+    if (rc) return rc;
+    if (h_out[1]) return -113;   // EHOSTUNREACH, as the table path
+    *W = h_out[0];
+    return 0;
+}
+
+static double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
 extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
+    const auto t_call = std::chrono::steady_clock::now();
+    auto t_results = t_call;
+    shd_pc* pc = m ? m->path_cache : nullptr;
     if (!m || !out || m->n_hosts <= 0 || m->n_hosts > (1 << 26) || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
-        !m->bw_up_kibps || !m->path_lat_ms || !m->path_rel || !m->host_vertex || m->n_vertices <= 0 ||
+        !m->bw_up_kibps || (!pc && (!m->path_lat_ms || !m->path_rel || m->n_vertices <= 0)) || !m->host_vertex ||
         (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
         return -22;
+    // path_cache mode: a built cache of an undirected graph (the directed
+    // lookup reruns rows, topology.c:1987-1990: not restated on the device)
+    if (pc && (!pc->built || pc->directed || (!pc->complete && !pc->d_row))) return -22;
     const int32_t H = m->n_hosts, P = m->n_procs;
     for (int32_t k = 0; k < P; k++) {
         if (m->proc_host[k] < 0 || m->proc_host[k] >= H) return -22;
         if (m->proc_peer[k] >= P || (m->proc_peer[k] >= 0 && m->proc_peer[m->proc_peer[k]] >= 0)) return -22;
     }
-    const int32_t V = m->n_vertices;
-    for (int32_t a = 0; a < H; a++)
-        if (m->host_vertex[a] < 0 || m->host_vertex[a] >= V) return -22;
-    // a client whose server is unreachable: the reference's connect fails with
-    // ECONNREFUSED (host.c:1224-1234, topology_isRoutable); the device
-    // application has no such branch, so the model is refused here
-    for (int32_t k = 0; k < P; k++) {
-        if (m->proc_peer[k] < 0) continue;
-        const size_t u = (size_t)m->host_vertex[m->proc_host[k]], v = (size_t)m->host_vertex[m->proc_host[m->proc_peer[k]]];
-        if (!(m->path_lat_ms[u * V + v] >= 0.0) || !(m->path_lat_ms[v * V + u] >= 0.0)) return -113;   // EHOSTUNREACH
+    const int32_t V = pc ? pc->T : m->n_vertices;
+    std::vector<int32_t> hvi(H);   // each host's table index: the given one, or its attached index in the cache
+    for (int32_t a = 0; a < H; a++) {
+        if (pc) {
+            if (m->host_vertex[a] < 0 || m->host_vertex[a] >= pc->V || pc->h_att_index[m->host_vertex[a]] < 0) return -22;
+            hvi[a] = pc->h_att_index[m->host_vertex[a]];
+        } else {
+            if (m->host_vertex[a] < 0 || m->host_vertex[a] >= V) return -22;
+            hvi[a] = m->host_vertex[a];
+        }
     }
     const uint32_t pool_cap = m->packets_per_host ? m->packets_per_host : kPoolDefault;
     if (pool_cap > (1u << 24)) return -22;
-    // the window: the smallest latency between two different hosts, in ns
-    // (ceil, worker.c:293), over the vertex pairs some pair of distinct hosts
-    // realizes (a vertex with itself only when two hosts share it)
     std::vector<int32_t> per_vertex(V, 0);
-    for (int32_t a = 0; a < H; a++) per_vertex[m->host_vertex[a]]++;
+    for (int32_t a = 0; a < H; a++) per_vertex[hvi[a]]++;
     uint64_t W = ~0ull;
-    for (int32_t u = 0; u < V; u++) {
-        if (!per_vertex[u]) continue;
-        for (int32_t v = 0; v < V; v++) {
-            if (!per_vertex[v] || (u == v && per_vertex[u] < 2)) continue;
-            const double l = m->path_lat_ms[(size_t)u * V + v];
-            if (l < 0) continue;
-            const uint64_t w = (uint64_t)ceil(l * (double)kMs);
-            if (w < W) W = w;
+    if (!pc) {
+        // a client whose server is unreachable: the reference's connect fails with
+        // ECONNREFUSED (host.c:1224-1234, topology_isRoutable); the device
+        // application has no such branch, so the model is refused here
+        for (int32_t k = 0; k < P; k++) {
+            if (m->proc_peer[k] < 0) continue;
+            const size_t u = (size_t)hvi[m->proc_host[k]], v = (size_t)hvi[m->proc_host[m->proc_peer[k]]];
+            if (!(m->path_lat_ms[u * V + v] >= 0.0) || !(m->path_lat_ms[v * V + u] >= 0.0)) return -113;   // EHOSTUNREACH
         }
+        // the window: the smallest latency between two different hosts, in ns
+        // (ceil, worker.c:293), over the vertex pairs some pair of distinct hosts
+        // realizes (a vertex with itself only when two hosts share it)
+        for (int32_t u = 0; u < V; u++) {
+            if (!per_vertex[u]) continue;
+            for (int32_t v = 0; v < V; v++) {
+                if (!per_vertex[v] || (u == v && per_vertex[u] < 2)) continue;
+                const double l = m->path_lat_ms[(size_t)u * V + v];
+                if (l < 0) continue;
+                const uint64_t w = (uint64_t)ceil(l * (double)kMs);
+                if (w < W) W = w;
+            }
+        }
+    } else {
+        // the same from the cache's device tables: either endpoint's row may
+        // serve a pair, so both count (the window only bounds the rounds)
+        std::vector<int32_t> conn;
+        for (int32_t k = 0; k < P; k++)
+            if (m->proc_peer[k] >= 0) {
+                const int32_t hc = m->proc_host[k], hs = m->proc_host[m->proc_peer[k]];
+                conn.push_back(hvi[hc]); conn.push_back(hvi[hs]); conn.push_back(hc == hs ? 1 : 0);
+            }
+        const int rr = tcp_pc_prep(pc, conn, &W);
+        if (rr) return rr;
     }
     if (W == 0) return -22;
     if (W == ~0ull) W = m->end_time ? m->end_time : 1;
@@ -2357,12 +2662,31 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
     if (m->qdisc > 1) { free(res); return -22; }
     g.qdisc_rr = m->qdisc;
-    HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)V * V));
-    HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)V * V));
-    HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
-    HCHECK(hipMemcpy(d_rel, m->path_rel, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
+    if (!pc) {
+        HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)V * V));
+        HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)V * V));
+        HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
+        HCHECK(hipMemcpy(d_rel, m->path_rel, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
+    } else {   // the cache's tables and ranks (copied back at the end)
+        g.pcm = 1;
+        g.pT = V;
+        g.pc_complete = pc->complete ? 1u : 0u;
+        g.pc_prefer_direct = pc->prefer_direct ? 1u : 0u;
+        g.prow = pc->d_row; g.pself = pc->d_self; g.pdir = pc->d_dir; g.padj = pc->d_adj; g.pself_eid = pc->d_self_eid;
+        HCHECK(hipMalloc(&g.rank, sizeof(int32_t) * (size_t)V));
+        HCHECK(hipMalloc(&g.srank, sizeof(int32_t) * (size_t)V));
+        HCHECK(hipMalloc(&g.next_rank, sizeof(int32_t)));
+        HCHECK(hipMemcpy(g.rank, pc->h_rank, sizeof(int32_t) * (size_t)V, hipMemcpyHostToDevice));
+        HCHECK(hipMemcpy(g.srank, pc->h_self_rank, sizeof(int32_t) * (size_t)V, hipMemcpyHostToDevice));
+        HCHECK(hipMemcpy(g.next_rank, &pc->next_rank, sizeof(int32_t), hipMemcpyHostToDevice));
+        g.ft_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);
+        HCHECK(hipMalloc(&g.ft, sizeof(shd_tcp_query) * (size_t)g.ft_cap));
+        HCHECK(hipMalloc(&g.ftord, sizeof(int32_t) * (size_t)g.ft_cap));
+        HCHECK(hipMalloc(&g.nft, sizeof(uint32_t)));
+        HCHECK(hipMemset(g.nft, 0, sizeof(uint32_t)));
+    }
     HCHECK(hipMalloc(&d_hv, sizeof(int32_t) * (size_t)H));
-    HCHECK(hipMemcpy(d_hv, m->host_vertex, sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(d_hv, hvi.data(), sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
     g.lat = d_lat; g.rel = d_rel; g.hv = d_hv; g.V = V; g.pool_cap = pool_cap;
     HCHECK(hipMalloc(&g.host, sizeof(DHost) * H));
     HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * H, hipMemcpyHostToDevice));
@@ -2440,6 +2764,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     // the initialisation above (k_tcp_free_init, the memsets) ran on the null
     // stream, which a non-blocking stream does not wait for: finish it first
     HCHECK(hipDeviceSynchronize());
+    res->setup_ms = ms_since(t_call);
     {
         // rounds run in batches of kBatch (window kernel, round kernel) pairs
         // captured once as a graph: no host round trip inside a batch; a
@@ -2472,6 +2797,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         HCHECK(hipEventElapsedTime(&ms, e0, e1));
         res->device_ms = ms;
     }
+    t_results = std::chrono::steady_clock::now();
     HCHECK(hipMemcpy(hout.data(), g.host, sizeof(DHost) * H, hipMemcpyDeviceToHost));
     {   // the first-query log
         uint32_t nq = 0;
@@ -2491,12 +2817,20 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         TCtl cx;
         HCHECK(hipMemcpy(&cx, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost));
         res->max_round_deliveries = cx.max_mail;
+        res->max_round_overflow = cx.max_ovf;
+        if (cx.ft_bad) res->error |= SHD_TCP_ERR_FIRST_TOUCH;
+        if (pc && !cx.ft_bad) {   // the cache's ranks as the serial run leaves them
+            HCHECK(hipMemcpy(pc->h_rank, g.rank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
+            HCHECK(hipMemcpy(pc->h_self_rank, g.srank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
+            HCHECK(hipMemcpy(&pc->next_rank, g.next_rank, sizeof(int32_t), hipMemcpyDeviceToHost));
+        }
         for (int b = 0; b < 2; b++) {
             uint64_t sum = 0;
             for (uint32_t j = 0; j <= kMailSub; j++) {
                 const uint32_t cap = j < kMailSub ? g.mail_part : g.mail_cap - g.mail_part * kMailSub;
                 const uint32_t v = nm[b * (kMailSub + 1) + j];
                 sum += v < cap ? v : cap;
+                if (j == kMailSub && (v < cap ? v : cap) > res->max_round_overflow) res->max_round_overflow = v < cap ? v : cap;
             }
             if (sum > res->max_round_deliveries) res->max_round_deliveries = sum;
         }
@@ -2562,7 +2896,9 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
             fprintf(stderr, "tcp_round: %llu max_ev %u max_kcyc %u\n", (unsigned long long)r, pr[r], pr[kProfRounds + r]);
     }
 #endif
+    res->results_ms = ms_since(t_results);
 done:
+    const auto t_free = std::chrono::steady_clock::now();
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -2576,7 +2912,10 @@ done:
     (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);
     (void)hipFree(g.qlog); (void)hipFree(g.nqlog); (void)hipFree(g.node); (void)hipFree(g.prof);
     (void)hipFree(g.prof_round);
+    (void)hipFree(g.rank); (void)hipFree(g.srank); (void)hipFree(g.next_rank);
+    (void)hipFree(g.ft); (void)hipFree(g.ftord); (void)hipFree(g.nft);
     if (rc) { shd_tcp_result_free(res); return rc; }
+    res->teardown_ms = ms_since(t_free);
     *out = res;
     return 0;
 }

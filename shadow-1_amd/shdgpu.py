@@ -190,7 +190,8 @@ class TcpModel(C.Structure):
                 ("proc_host", P(C.c_int32)), ("proc_start", P(C.c_uint64)), ("proc_peer", P(C.c_int32)),
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
-                ("tcp_window", C.c_uint32), ("packets_per_host", C.c_uint32), ("qdisc", C.c_uint32)]
+                ("tcp_window", C.c_uint32), ("packets_per_host", C.c_uint32), ("qdisc", C.c_uint32),
+                ("_pad", C.c_uint32), ("path_cache", C.c_void_p)]
 
 
 class TcpResult(C.Structure):
@@ -201,10 +202,12 @@ class TcpResult(C.Structure):
                 ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64),
                 ("queries", C.c_void_p), ("n_queries", C.c_uint64),
                 ("node_counters", P(C.c_uint64)), ("n_heartbeats", P(C.c_uint32)), ("node_k", C.c_uint32),
-                ("_pad2", C.c_uint32), ("max_round_deliveries", C.c_uint64)]
+                ("_pad2", C.c_uint32), ("max_round_deliveries", C.c_uint64), ("max_round_overflow", C.c_uint64),
+                ("setup_ms", C.c_double), ("results_ms", C.c_double), ("teardown_ms", C.c_double)]
 
 
 TCP_TRACE_STATUS, TCP_TRACE_NODE = 1, 2   # shd_tcp_run's trace bits
+TCP_ERR_FIRST_TOUCH = 512                  # SHD_TCP_ERR_FIRST_TOUCH (include/shdtcp.h)
 
 
 TCP_QUERY_DTYPE = np.dtype([("time", "<u8"), ("seq", "<u8"), ("host", "<u4"), ("src", "<u4"), ("index", "<u4"),
@@ -241,6 +244,8 @@ _SIGS = {
     "shd_pc_copy_self": (C.c_int, [C.c_void_p, P(C.c_double), P(C.c_double)]),
     "shd_pc_lookup": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_double),
                                 P(C.c_double)]),
+    "shd_pc_lookup_batch": (C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), C.c_uint64, P(C.c_double),
+                                      P(C.c_double)]),
     "shd_pc_count_packet": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     "shd_pc_packet_count": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_uint64)]),
     "shd_pc_min_time_jump": (C.c_int, [C.c_void_p, C.c_uint64, P(C.c_uint64)]),

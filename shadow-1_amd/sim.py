@@ -64,6 +64,16 @@ class PathCache:
         S.check(S.lib().shd_pc_lookup(self.ptr, int(s), int(d), C.byref(a), C.byref(b)), "lookup")
         return a.value, b.value
 
+    def lookup_batch(self, src, dst):
+        """shd_pc_lookup of every (src[i], dst[i]) in order, in one call
+        (shd_pc_lookup_batch): (lat, rel) arrays"""
+        s = np.ascontiguousarray(src, dtype=np.int32)
+        d = np.ascontiguousarray(dst, dtype=np.int32)
+        lat = np.empty(len(s)); rel = np.empty(len(s))
+        S.check(S.lib().shd_pc_lookup_batch(self.ptr, S.as_ptr(s, C.c_int32), S.as_ptr(d, C.c_int32), len(s),
+                                            S.as_ptr(lat, C.c_double), S.as_ptr(rel, C.c_double)), "lookup_batch")
+        return lat, rel
+
     def close(self):
         if self.ptr:
             S.lib().shd_pc_destroy(self.ptr)

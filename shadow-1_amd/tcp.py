@@ -2,14 +2,24 @@
 
 Mirrors what a Shadow build would do around shd_tcp_run: the hosts' addresses
 and RNG states come from the config front-end (dns.c's addresses, the seed
-chain after attach), and the path latency / reliability of every host pair is
-read from the product's lazy path cache (shd_pc_lookup, topology.c:2053-2092).
+chain after attach), and the path latency / reliability of every host pair
+comes from the product's lazy path cache (topology.c:2053-2092).
 
 Which endpoint's Dijkstra row serves a pair depends on the serial order of
-every pair's FIRST query (_topology_getPathEntry, topology.c:1969-2051):
-the tables passed to shd_tcp_run are resolved in a first-touch order, and the
-run logs each host's first query of each vertex pair with its event key
-(shd_tcp_result.queries).  The driver ranks the logged queries in serial
+every pair's FIRST query (_topology_getPathEntry, topology.c:1969-2051).  By
+default (mode "device") the run takes the cache itself (shd_tcp_model.
+path_cache): the device applies the first-touch rule round by round -- pairs
+with a ranked endpoint at a round's start decided, the others decided by the
+querying lane and logged, the log ranked in serial order between rounds
+(k_tcp_window) -- so one run, with no first-touch guess on the host.  A round
+whose lanes touched the same unranked vertices from both sides in a way the
+serial order contradicts ends the run with SHD_TCP_ERR_FIRST_TOUCH; the
+driver then takes the table path below.
+
+The table path (mode "tables", and the fallback): the tables passed to
+shd_tcp_run are resolved in a first-touch order (one shd_pc_lookup_batch call),
+and the run logs each host's first query of each vertex pair with its event
+key (shd_tcp_result.queries).  The driver ranks the logged queries in serial
 order (time, host, src, seq, index within the event), replays them through a
 fresh lazy cache and compares the values every logged pair gets with the ones
 the run used: equal, the run's order of first touches IS the serial one (the
@@ -17,8 +27,7 @@ run is a deterministic function of the values, so the serial loop with these
 values makes the same queries in the same order); otherwise the run is
 repeated with the new tables, until they agree (first_touch_runs in the
 result).  The first guess is a client's connect touching (client, server)
-first (topology_isRoutable, host.c:1224-1234), clients by start time: right
-for the echo application, so one run.
+first (topology_isRoutable, host.c:1224-1234), clients by start time.
 """
 from __future__ import annotations
 
@@ -41,15 +50,19 @@ def resolve(g: S.GraphArrays, att, first_queries, pairs, V):
     have run).  Pairs not listed stay -1."""
     lat = np.full((V, V), -1.0)
     rel = np.full((V, V), -1.0)
+    fq = np.asarray(first_queries, dtype=np.int64).reshape(-1, 2)
+    pq = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    both = np.stack([pq, pq[:, ::-1]], axis=1).reshape(-1, 2)   # each pair, then its reverse, after the first touches
+    q = np.concatenate([fq, both])
     pc = sim.PathCache(g, att)
     try:
-        for s, d in first_queries:
-            pc.lookup(att[s], att[d])
-        for s, d in pairs:
-            for x, y in ((s, d), (d, s)):
-                lat[x, y], rel[x, y] = pc.lookup(att[x], att[y])
+        # one shd_pc_lookup_batch call: the queries in order, one device round trip
+        lq, rq = pc.lookup_batch(att[q[:, 0]], att[q[:, 1]]) if len(q) else (np.zeros(0), np.zeros(0))
     finally:
         pc.close()
+    k = len(fq)
+    lat[both[:, 0], both[:, 1]] = lq[k:]
+    rel[both[:, 0], both[:, 1]] = rq[k:]
     return lat, rel
 
 
@@ -82,14 +95,31 @@ def serial_first_queries(queries: np.ndarray):
 
 def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000, trace=True,
         recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0, guess_reversed=False,
-        node=False, qdisc=0):
+        node=False, qdisc=0, mode="device"):
     """Run the TCP echo model on the GPU: procs = [(host, start ns)], peers =
     [-1 | server process]; ips: host-order uint32 per host.  Returns
     dict(lines=[(t, h, line)] in each host's order, next_event_id,
-    next_packet_id, rng_probe, rounds, events, device_ms, first_touch_runs;
-    with node: node_lines=[(t, h, line)], every host's tracker [node] lines by
-    (time, host), from the library's writer).
-    guess_reversed: start from a wrong first-touch guess (tests)."""
+    next_packet_id, rng_probe, rounds, events, device_ms, first_touch
+    ("device", or "tables" with first_touch_runs); with node:
+    node_lines=[(t, h, line)], every host's tracker [node] lines by (time,
+    host), from the library's writer).
+    mode "device": the path cache's first-touch rule on the device (falls back
+    to "tables" when a round's choice is contradicted, or on a directed graph);
+    guess_reversed: the table path from a wrong first-touch guess (tests)."""
+    if mode == "device" and not guess_reversed and not g.directed:
+        m = model.struct
+        H = int(m.n_hosts)
+        hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
+        pc = sim.PathCache(g, np.unique(hv))
+        try:
+            out = _run_once(model, ips, procs, peers, None, None, hv.astype(np.int32), nbytes, trace, recv_buf,
+                            send_buf, tcp_window, packets_per_host, node, qdisc, pc=pc)
+        finally:
+            pc.close()
+        if out is not None:
+            out.pop("queries")
+            out["first_touch"] = "device"
+            return out
     lat, rel, hvi, att = path_table(model, g, procs, peers, reverse=guess_reversed)
     V = lat.shape[0]
     for runs in range(1, 9):
@@ -102,6 +132,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
         same = np.array_equal(lat[ij].view(np.uint64), lat2[ij].view(np.uint64)) and \
             np.array_equal(rel[ij].view(np.uint64), rel2[ij].view(np.uint64))
         if same:
+            out["first_touch"] = "tables"
             out["first_touch_runs"] = runs
             out["first_touch_pairs"] = len(pairs)
             return out
@@ -112,12 +143,15 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
 
 
 def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-              packets_per_host, node=False, qdisc=0):
-    """one shd_tcp_run on the given path tables"""
+              packets_per_host, node=False, qdisc=0, pc=None):
+    """one shd_tcp_run on the given path tables, or with pc (sim.PathCache) on
+    the cache itself (hvi: graph vertices then); None when that run's
+    first-touch choices were contradicted (SHD_TCP_ERR_FIRST_TOUCH)"""
     m = model.struct
     H = int(m.n_hosts)
-    keep = dict(ip=np.ascontiguousarray(ips, dtype=np.uint32), hv=np.ascontiguousarray(hvi),
-                lat=np.ascontiguousarray(lat), rel=np.ascontiguousarray(rel),
+    keep = dict(ip=np.ascontiguousarray(ips, dtype=np.uint32), hv=np.ascontiguousarray(hvi, dtype=np.int32),
+                lat=np.ascontiguousarray(lat if lat is not None else np.zeros((1, 1))),
+                rel=np.ascontiguousarray(rel if rel is not None else np.zeros((1, 1))),
                 ph=np.ascontiguousarray([p[0] for p in procs], dtype=np.int32),
                 ps=np.ascontiguousarray([p[1] for p in procs], dtype=np.uint64),
                 pp=np.ascontiguousarray(peers, dtype=np.int32))
@@ -128,7 +162,7 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
     tm.host_seed = m.host_rng
     tm.bw_down_kibps = m.bw_down_kibps
     tm.bw_up_kibps = m.bw_up_kibps
-    tm.n_vertices = lat.shape[0]
+    tm.n_vertices = lat.shape[0] if lat is not None else 0
     tm.host_vertex = S.as_ptr(keep["hv"], C.c_int32)
     tm.path_lat_ms = S.as_ptr(keep["lat"], C.c_double)
     tm.path_rel = S.as_ptr(keep["rel"], C.c_double)
@@ -143,11 +177,15 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
     tm.tcp_window = tcp_window
     tm.packets_per_host = packets_per_host
     tm.qdisc = int(qdisc)   # --interface-qdisc: 0 fifo, 1 rr
+    if pc is not None:
+        tm.path_cache = pc.ptr.value
     res = C.POINTER(S.TcpResult)()
     bits = (S.TCP_TRACE_STATUS if trace else 0) | (S.TCP_TRACE_NODE if node else 0)
     S.check(S.lib().shd_tcp_run(C.byref(tm), bits, C.byref(res)), "shd_tcp_run")
     try:
         r = res.contents
+        if pc is not None and r.error == S.TCP_ERR_FIRST_TOUCH:
+            return None
         if r.error:
             raise S.ShdError(f"shd_tcp_run: error bits {r.error:#x}")
         text = C.string_at(r.lines, r.len).decode() if r.len else ""
@@ -160,7 +198,8 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
                    next_packet_id=np.ctypeslib.as_array(r.next_packet_id, shape=(H,)).copy(),
                    rng_probe=np.ctypeslib.as_array(r.rng_probe, shape=(H,)).copy(),
                    rounds=int(r.rounds), events=int(r.events), deliveries=int(r.deliveries),
-                   max_round_deliveries=int(r.max_round_deliveries),
+                   max_round_deliveries=int(r.max_round_deliveries), max_round_overflow=int(r.max_round_overflow),
+                   host_ms=dict(setup=float(r.setup_ms), results=float(r.results_ms), teardown=float(r.teardown_ms)),
                    device_ms=float(r.device_ms),
                    queries=np.frombuffer(C.string_at(r.queries, int(r.n_queries) * S.TCP_QUERY_DTYPE.itemsize),
                                          dtype=S.TCP_QUERY_DTYPE).copy() if r.n_queries else

@@ -80,9 +80,12 @@ def test_tcp_struct_layout_matches_the_header(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s/include/shdtcp.h"\n'
                    'int main(void){printf("%%zu %%zu %%zu %%zu %%zu\\n", sizeof(shd_tcp_model),'
                    ' offsetof(shd_tcp_model, host_vertex), offsetof(shd_tcp_model, packets_per_host),'
-                   ' sizeof(shd_tcp_result), offsetof(shd_tcp_result, deliveries));return 0;}\n' % REPO)
+                   ' sizeof(shd_tcp_result), offsetof(shd_tcp_result, deliveries));'
+                   'printf("%%zu %%zu\\n", offsetof(shd_tcp_model, path_cache),'
+                   ' offsetof(shd_tcp_result, max_round_deliveries));return 0;}\n' % REPO)
     exe = tmp_path / "l"
     subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     assert got == [C.sizeof(S.TcpModel), S.TcpModel.host_vertex.offset, S.TcpModel.packets_per_host.offset,
-                   C.sizeof(S.TcpResult), S.TcpResult.deliveries.offset]
+                   C.sizeof(S.TcpResult), S.TcpResult.deliveries.offset, S.TcpModel.path_cache.offset,
+                   S.TcpResult.max_round_deliveries.offset]

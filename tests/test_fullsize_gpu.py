@@ -173,3 +173,55 @@ def test_bench_workload_sharded_group_equals_single_engine(hosts, parts):
     assert np.array_equal(dg, d1)
     close_all(engines, grp)
     pc.close()
+
+
+def run_one_rank_p2p(m, pc):
+    """the engine group's fused peer-to-peer schedule with one rank (bench.py
+    --group): an RCCL communicator of one, the whole model on its engine"""
+    from sim import Comm
+    e = Engine(m, pc)
+    comm = Comm.rccl(XGroup.unique_id(), 1, 0, 0)
+    grp = XGroup.over(e, comm, p2p=True)
+    st = grp.run()
+    return st, e, grp, comm
+
+
+@pytest.mark.parametrize("sp", ["auto", "forced"])
+def test_c3_full_size_sparse_group_rounds_match_fixture(c3, sp, monkeypatch):
+    """k_round_spx (the sparse fused group round): C3 through a one-rank
+    peer-to-peer group with the sparse kernel forced (SHD_SP_HOSTS: blocks of
+    256 hosts) or as the group picks it (auto: 157 blocks of 64 hosts fit the
+    GPU, so k_round_px) -- the fixture's digests and traces either way"""
+    key, m, pc = c3
+    if sp == "forced":
+        monkeypatch.setenv("SHD_SP_HOSTS", "256")
+    fx = fixture(key)
+    st, e, grp, comm = run_one_rank_p2p(m, pc)
+    assert st.error == 0
+    tr = e.trace()
+    dg = e.digest()
+    n_ev, n_pkt, n_tr = (int(x) for x in fx["totals"])
+    assert (st.n_events, st.n_pkt_events, len(tr)) == (n_ev, n_pkt, n_tr)
+    assert np.array_equal(dg, fx["digest"])
+    th = FH.trace_host_hashes(tr, m.n_hosts)
+    assert np.array_equal(th, fx["trace_hash"])
+    grp.close(); e.close(); comm.close()
+
+
+def test_c5_codel_million_hosts_sparse_group_rounds_match_fixture():
+    """The north star's model through the one-rank fused group: 15 625 blocks
+    of 64 hosts, so k_round_spx runs the sparse rounds (blocks of ~4 k hosts,
+    one per CU) -- bit-exact against the full-size oracle fixture"""
+    cfg = CONFIGS["c5"]
+    fx = fixture("c5")
+    g, m, _ = build("c5")
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    st, e, grp, comm = run_one_rank_p2p(m, pc)
+    assert st.error == 0
+    dg = e.digest()
+    grp.close(); e.close(); comm.close()
+    pc.close()
+    n_ev, n_pkt, _ = (int(x) for x in fx["totals"])
+    assert (st.n_events, st.n_pkt_events) == (n_ev, n_pkt)
+    bh = FH.digest_block_hashes(dg, cfg["block"])
+    assert np.array_equal(bh, fx["block_hash"])

@@ -3,6 +3,8 @@
 Reference: src/main/routing/topology.c (rows 1655-1875 + 1407-1523, direct
 1877-1927, self 1545-1653, lazy selection 1969-2051).
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -172,3 +174,47 @@ def test_tie_graph_lazy_lookup_matches_reference_cache():
         a = pc.lookup(s, d)
         b = ot.get(s, d)
         assert np.array(a).view(np.uint64).tolist() == np.array(b).view(np.uint64).tolist(), (s, d)
+
+
+def _directed_geo(V, seed):
+    g0 = W.geometric_graph(V, seed=seed, loss_max=0.01)
+    src, dst = g0.src.astype(np.int64), g0.dst.astype(np.int64)
+    nsl = src != dst
+    rng = np.random.default_rng(seed)
+    return S.GraphArrays(V, np.concatenate([src, dst[nsl]]), np.concatenate([dst, src[nsl]]),
+                         np.concatenate([g0.latency, g0.latency[nsl] * (1.0 + rng.random(int(nsl.sum())))]),
+                         np.concatenate([g0.loss, g0.loss[nsl]]), directed=True)
+
+
+@pytest.mark.parametrize("name", ["geo", "grid", "directed", "bundled", "prefer_direct"])
+def test_lookup_batch_equals_sequential_lookups(name):
+    """shd_pc_lookup_batch: the same values, ranks and minimumPathLatency as
+    the same queries through shd_pc_lookup one by one (one device round trip
+    instead of one per query: the TCP driver's path tables)"""
+    if name == "geo":
+        g = W.geometric_graph(500, seed=4, vertex_loss=True)
+    elif name == "grid":
+        g = W.grid_graph(10, seed=3)
+    elif name == "directed":
+        g = _directed_geo(300, 6)
+    elif name == "bundled":
+        g = W.bundled_graph()
+    else:
+        g0 = W.geometric_graph(400, seed=8)
+        g = S.GraphArrays(g0.n_vertices, g0.src, g0.dst, g0.latency, g0.loss, prefer_direct=True)
+    rng = np.random.default_rng(11)
+    att = np.sort(rng.choice(g.n_vertices, min(g.n_vertices, 250), replace=False)).astype(np.int32)
+    q = att[rng.integers(0, len(att), (4000, 2))]
+    q[::37, 1] = q[::37, 0]   # self pairs among them
+    a = PathCache(g, att)
+    b = PathCache(g, att)
+    for part in (q[:1500], q[1500:]):   # two batches: the second starts from the first's ranks
+        lat, rel = a.lookup_batch(part[:, 0], part[:, 1])
+        want = np.array([b.lookup(int(s), int(d)) for s, d in part])
+        assert same_bits(lat, want[:, 0]) and same_bits(rel, want[:, 1])
+        ma, mb = C.c_double(), C.c_double()
+        S.check(S.lib().shd_pc_min_stored_latency(a.ptr, C.byref(ma)), "min")
+        S.check(S.lib().shd_pc_min_stored_latency(b.ptr, C.byref(mb)), "min")
+        assert ma.value == mb.value
+    a.close()
+    b.close()

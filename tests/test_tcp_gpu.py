@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import oracle_ffi as O
+import shdgpu as S
 import tcp as TCPGPU
 import tcp_cases as TC
 
@@ -20,12 +21,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
 
 
+@pytest.mark.parametrize("mode", ["device", "tables"])
 @pytest.mark.parametrize("name", list(TC.CASES))
-def test_tcp_gpu_equals_reference(name):
+def test_tcp_gpu_equals_reference(name, mode):
+    """mode "device": the path cache's first-touch rule applied on the device
+    (shd_tcp_model.path_cache); "tables": path tables resolved by the driver"""
     f = FIX[name]
     c, m = TC.build(name)
     ips = TC.ip_ints(f["ips"])
-    r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], node=True, qdisc=c.get("qdisc", 0))
+    r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], node=True, qdisc=c.get("qdisc", 0),
+                   mode=mode)
+    assert r["first_touch"] == mode
     got = r["lines"]
     # the tracker's [node] lines: the library's writer over the device's counters
     assert len(r["node_lines"]) == f["n_heartbeat"]
@@ -105,18 +111,48 @@ def test_tcp_gpu_first_touch_order_settles(name):
 
 
 def test_tcp_gpu_wide_window_uses_the_mailbox_overflow():
-    """One fast, long connection (about 1 Gbit/s links, 20 MB): its window
-    grows past the 1024 mailbox slots a host's part holds per round (the
-    mailbox is split into 64 parts by host), so the sends spill into the
-    shared overflow range -- the run must neither fail with
-    SHD_TCP_ERR_MAILBOX nor differ from the oracle."""
+    """Fast, long connections (about 1 Gbit/s links, 8 MB each way) whose
+    hosts share mailbox parts (the mailbox is split into 64 parts by host
+    index: hosts 1, 65 and 129 are clients in part 1, hosts 0, 64 and 128
+    servers in part 0): a part's 1024 slots per round are not enough, and the
+    sends spill into the shared overflow range -- the run must neither fail
+    with SHD_TCP_ERR_MAILBOX nor differ from the oracle."""
     import workloads as W
-    g, m, ips, procs, peers, nb = W.tcp_echo_model(2, 40, end_s=8, nbytes=20_000_000, bw_down=122070, bw_up=122070)
+    g, m, ips, procs, peers, nb = W.tcp_echo_model(130, 40, end_s=8, nbytes=8_000_000, bw_down=122070,
+                                                   bw_up=122070)
     r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, trace=False)
     o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb, lines=False)
     assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
     assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
     assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
     assert r["events"] == o["events"]
-    # more deliveries than one part's 1024 slots in some round
-    assert r["max_round_deliveries"] > 1024
+    assert r["max_round_overflow"] > 0, (r["max_round_deliveries"], r["max_round_overflow"])
+
+
+def test_tcp_gpu_device_first_touch_contradiction_falls_back():
+    """Two hosts each run a server and a client of the other's server, the
+    clients' connects (topology_isRoutable: a first touch) 10 us apart in one
+    window: each lane, seeing both vertices unranked, decides its own
+    vertex's row; in serial order host 1's touch comes first, so host 0's
+    query hits host 1's row.  The replay between rounds finds the
+    contradiction (SHD_TCP_ERR_FIRST_TOUCH) and the driver runs the model on
+    tables instead -- the result is the oracle's either way."""
+    import workloads as W
+    g, m, ips, _, _, nb = W.tcp_echo_model(2, 30, end_s=6, nbytes=30000)
+    if g.n_vertices and m.host_vertex[0] == m.host_vertex[1]:
+        pytest.skip("the two hosts share a vertex")
+    procs = [(0, S.SHD_SEC), (1, S.SHD_SEC), (0, 2 * S.SHD_SEC + 10000), (1, 2 * S.SHD_SEC)]
+    peers = [-1, -1, 1, 0]
+    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb)
+    o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb)
+    assert r["first_touch"] == "tables"
+    assert r["lines"] == TC.by_host(o["lines"])
+    assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
+    assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
+    # the same connects a window apart: no contradiction, the device decides
+    procs2 = [(0, S.SHD_SEC), (1, S.SHD_SEC), (0, 2 * S.SHD_SEC + 200 * S.SHD_MS), (1, 2 * S.SHD_SEC)]
+    r2 = TCPGPU.run(m, g, ips, procs2, peers, nbytes=nb)
+    o2 = O.tcp_run(m, g, ips, procs2, peers, nbytes=nb)
+    assert r2["first_touch"] == "device"
+    assert r2["lines"] == TC.by_host(o2["lines"])
+    assert r2["next_event_id"].tolist() == o2["next_event_id"].tolist()

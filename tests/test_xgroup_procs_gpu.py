@@ -103,6 +103,17 @@ def test_multiprocess_p2p_fused_rounds(world, hpv, tmp_path):
     assert len({int(r["stats"][3]) for r in res}) == 1
 
 
+@pytest.mark.parametrize("world,hpv", [(2, 1), (3, 3)])
+def test_multiprocess_p2p_sparse_rounds(world, hpv, tmp_path):
+    """k_round_spx, the sparse fused round, forced (SHD_SP_HOSTS=64: blocks of
+    64 hosts scanned and compacted): each round takes the peers' stores for its
+    blocks' hosts into their calendars / inboxes before the scan, and its own
+    sends for other ranks go into their regions as k_round_px's do"""
+    res = run_ranks(world, tmp_path, extra=["--p2p", "--hpv", str(hpv)], env_extra={"SHD_SP_HOSTS": "64"})
+    check_against_oracle(res, 240, hpv, 3.0, 0.01, 16)
+    assert len({int(r["stats"][3]) for r in res}) == 1
+
+
 @pytest.mark.parametrize("p2p", [False, True], ids=["alltoall", "p2p"])
 def test_multiprocess_group_tor_model(p2p, tmp_path):
     """BASELINE C4's relay/client model over 3 processes: per-class destination
