@@ -459,6 +459,9 @@ def tcp_main(args):
     mk = lambda n: W.tcp_echo_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,  # noqa: E731
                                     loss_max=args.edge_loss_max)
     g, m, ips, procs, peers, nb = mk(H)
+    # a caller running many models keeps the run's device buffers between
+    # calls (shdtcp.h shd_tcp_keep_workspace); the first call allocates them
+    S.lib().shd_tcp_keep_workspace(1)
     for _ in range(args.warmup):
         T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool)
     mark = Roctx()

@@ -139,6 +139,13 @@ enum {
 int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out);
 void shd_tcp_result_free(shd_tcp_result* r);
 
+/* keep != 0: shd_tcp_run keeps its device buffers (the per-host event queues,
+ * packet pools, sockets and mailboxes: tens of GB at 64 k hosts) for the next
+ * call on the same device instead of allocating and freeing them each call;
+ * 0 (the default): release them now and after every call.  A caller that runs
+ * many models in one process (a parameter sweep, the bench) sets 1. */
+void shd_tcp_keep_workspace(int32_t keep);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,7 +21,7 @@ g = W.geometric_graph(V, seed=1)
 pc = PathCache(g, np.arange(V, dtype=np.int32))
 pc.build()
 i = pc.info()
-out = np.zeros((1024, 8), dtype=np.uint64)
+out = np.zeros((1024, 16), dtype=np.uint64)
 f = S.lib().shd_debug_sssp_timing
 f.argtypes = [C.c_void_p]
 assert f(out.ctypes.data) == 0
@@ -34,3 +34,7 @@ tot = o[:, 0].sum() / waves
 for k, name in ((1, "iteration loop (scan + frontier)"), (2, "frontier work"), (3, "barrier wait")):
     print(f"{name:36s} {o[:, k].sum() / waves / tot * 100:5.1f} % of BF cycles (per-wave mean)")
 print(f"BF cycles per row per wave {tot / o[:, 7].sum():.0f}; per iteration {tot / o[:, 4].sum():.0f}")
+rows = o[:, 7].sum()
+for k, name in ((0, "Bellman-Ford"), (8, "parents"), (9, "targets, first pass"), (10, "tree arrays"),
+                (11, "tree prefix sweeps"), (12, "reliability pass")):
+    print(f"{name:36s} {o[:, k].sum() / waves / rows:10.0f} cycles per row per wave")

@@ -98,7 +98,9 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              int64_t* __restrict__ stats, uint64_t* dist, int32_t* parent,
                              uint16_t* upd, int* flags /* LDS int[4] */,
                              const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows,
-                             int32_t* fl_pre, int32_t* fl_beg, uint64_t* fl_dv /* LDS [BLOCK] each */) {
+                             int32_t* fl_pre, int32_t* fl_beg, uint64_t* fl_dv /* LDS [BLOCK] each */,
+                             const uint16_t* off16, const int32_t* cbase /* LDS arc offsets, or null */,
+                             bool bfq /* queued frontier: four vertices a wave in flight */) {
     const int tid = threadIdx.x;
     for (int32_t v = tid; v < V; v += BLOCK) {
         dist[v] = kDistInf;
@@ -125,6 +127,69 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         if (tid == 0) flags[(it + 1) % 3] = 0;
         const uint16_t stamp = (uint16_t)it;
         SST_T0(t_it)
+        if (bfq) {
+            // queued frontier: the wave's chunks are balloted as before, but
+            // frontier vertices go to a four-entry queue (uniform registers)
+            // and are relaxed four at a time -- each half-wave takes two, the
+            // first arc load of both issued before either relaxes -- so a wave
+            // keeps two vertices' loads in flight where the pairs below keep
+            // one (a chunk holds ~1.3 frontier vertices: the pairs mostly ran
+            // one half-wave on one vertex)
+            int32_t q0 = -1, q1 = -1, q2 = -1, q3 = -1;
+            int nq = 0;
+            auto arc_range = [&](int32_t v, int32_t& b, int32_t& e) {
+                if (off16) {
+                    b = cbase[v >> 6] + off16[v];
+                    e = v + 1 < V ? cbase[(v + 1) >> 6] + off16[v + 1] : cbase[(V + 63) >> 6];
+                } else {
+                    b = arc_off[v];
+                    e = arc_off[v + 1];
+                }
+            };
+            auto relax = [&](int32_t x, double cand) {
+                const uint64_t nb = d2u(cand);
+                if (nb < dist[x]) {
+                    const uint64_t old = atomicMin((unsigned long long*)&dist[x], (unsigned long long)nb);
+                    if (nb < old) {
+                        upd[x] = (uint16_t)(it + 1);
+                        flags[it % 3] = 1;
+                    }
+                }
+            };
+            auto run4 = [&]() {
+                const int32_t va = upper ? q1 : q0, vb = upper ? q3 : q2;
+                int32_t ba = 0, ea = 0, bb = 0, eb = 0;
+                double da = 0.0, db = 0.0;
+                if (va >= 0) { arc_range(va, ba, ea); da = u2d(dist[va]); }
+                if (vb >= 0) { arc_range(vb, bb, eb); db = u2d(dist[vb]); }
+                const int32_t ka = ba + hl, kb = bb + hl;
+                int32_t xa = -1, xb = -1;
+                double wa = 0.0, wb = 0.0;
+                if (ka < ea) { xa = arc_dst[ka]; wa = arc_w[ka]; }
+                if (kb < eb) { xb = arc_dst[kb]; wb = arc_w[kb]; }
+                if (xa >= 0) relax(xa, da + wa);
+                if (xb >= 0) relax(xb, db + wb);
+                for (int32_t k = ka + 32; k < ea; k += 32) relax(arc_dst[k], da + arc_w[k]);
+                for (int32_t k = kb + 32; k < eb; k += 32) relax(arc_dst[k], db + arc_w[k]);
+            };
+            for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
+                const int32_t v = c0 + lane;
+                uint64_t mask = __ballot(v < V && upd[v] == stamp);
+                while (mask) {
+                    const int32_t fv = c0 + __ffsll((unsigned long long)mask) - 1;
+                    mask &= mask - 1;
+                    q0 = q1; q1 = q2; q2 = q3; q3 = fv;
+                    if (++nq == 4) {
+                        run4();
+                        nq = 0;
+                    }
+                }
+            }
+            if (nq) {
+                while (nq < 4) { q0 = q1; q1 = q2; q2 = q3; q3 = -1; nq++; }
+                run4();
+            }
+        } else
         for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
             const int32_t v = c0 + lane;
 #ifdef SHD_SSSP_GS   // A/B: a vertex improved earlier in this sweep relaxes now too (and again next sweep)
@@ -139,7 +204,16 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             if (lane == 0) { SST_CNT(5, __popcll(mask)); }
             int32_t beg = 0, end = 0;
             uint64_t dvb = 0;
-            if (fr) { beg = arc_off[v]; end = arc_off[v + 1]; dvb = dist[v]; }
+            if (fr) {
+                if (off16) {   // the arc offsets from LDS: no L2 round trip before the arcs' loads
+                    beg = cbase[v >> 6] + off16[v];
+                    end = v + 1 < V ? cbase[(v + 1) >> 6] + off16[v + 1] : cbase[(V + 63) >> 6];
+                } else {
+                    beg = arc_off[v];
+                    end = arc_off[v + 1];
+                }
+                dvb = dist[v];
+            }
 #ifdef SHD_SSSP_FLAT
             // A/B (measured and rejected): the chunk's frontier
             // arcs flattened over the wave -- an exclusive scan of the frontier
@@ -505,12 +579,26 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, int32_t row0, int32_t row1, const int32_t* __restrict__ row_list,
-    const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
+    const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows, int mode /* bit 0 LDS offsets, 1 queued */) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int ldsoff = mode & 1;
     uint64_t* dist = (uint64_t*)smem;
     int32_t* parent = (int32_t*)(smem + (size_t)8 * V);
     uint16_t* upd = (uint16_t*)(smem + (size_t)12 * V);
     int* flags = (int*)(smem + (((size_t)14 * V + 15) & ~(size_t)15));
+    // ldsoff: the forward CSR's offsets kept in LDS for every row of the block
+    // (a 32-bit base per 64-vertex chunk, a 16-bit offset per vertex; the host
+    // checked that a chunk's arcs number below 65 536)
+    uint16_t* off16 = nullptr;
+    int32_t* cbase = nullptr;
+    if (ldsoff) {
+        off16 = (uint16_t*)(smem + (((size_t)14 * V + 15) & ~(size_t)15) + 16);
+        cbase = (int32_t*)(smem + (((size_t)14 * V + 15) & ~(size_t)15) + 16 + (((size_t)2 * V + 15) & ~(size_t)15));
+        const int32_t nch = (V + 63) >> 6;
+        for (int32_t v = (int32_t)threadIdx.x; v < V; v += BLOCK) off16[v] = (uint16_t)(arc_off[v] - arc_off[v & ~63]);
+        for (int32_t cix = (int32_t)threadIdx.x; cix <= nch; cix += BLOCK) cbase[cix] = arc_off[cix < nch ? cix << 6 : V];
+        __syncthreads();
+    }
 #ifdef SHD_SSSP_FLAT
     __shared__ int32_t fl_pre[BLOCK], fl_beg[BLOCK];
     __shared__ uint64_t fl_dv[BLOCK];
@@ -525,7 +613,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
-                            fl_beg, fl_dv);
+                            fl_beg, fl_dv, off16, cbase, (mode & 2) != 0);
     }
 }
 
@@ -540,7 +628,8 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, char* __restrict__ scratch, size_t per_block, int32_t row0, int32_t row1,
-    const int32_t* __restrict__ row_list, const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows) {
+    const int32_t* __restrict__ row_list, const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows,
+    int mode /* bit 1 queued */) {
     __shared__ int flags[4];
 #ifdef SHD_SSSP_FLAT
     __shared__ int32_t fl_pre[BLOCK], fl_beg[BLOCK];
@@ -559,7 +648,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_global(
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
-                            fl_beg, fl_dv);
+                            fl_beg, fl_dv, nullptr, nullptr, (mode & 2) != 0);
     }
 }
 
@@ -958,6 +1047,10 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
     pc_relabel(pc->csr, pcsr);
     const shd_csr& c = pcsr.view;
     const int32_t na = c.arc_off[V];
+    // the row kernel may keep the arc offsets in LDS (16 bits within a 64-vertex chunk)
+    pc->lds_off_ok = !getenv("SHD_PC_NO_LDS_OFF");
+    for (int32_t v0 = 0; v0 < V && pc->lds_off_ok; v0 += 64)
+        if (c.arc_off[std::min(V, v0 + 64)] - c.arc_off[v0] >= 65536) pc->lds_off_ok = false;
     // per forward arc: its tail vertex and the index of the same arc among its
     // head's in-arcs (the parent pass streams the forward arcs, the tree walks
     // use the in-arc indices)
@@ -1026,7 +1119,6 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
 #define SHD_ROW_BLOCK 1024
 #endif
 constexpr int kRowBlock = SHD_ROW_BLOCK;   // workgroup of the LDS row kernel past 2 k vertices
-static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
 // the dynamic row arrays' budget: 160 KiB less the kernels' static LDS (the
 // SHD_SSSP_FLAT A/B's scan slots, 16 B a thread of the 1024-thread block)
 #ifdef SHD_SSSP_FLAT
@@ -1034,6 +1126,24 @@ static constexpr size_t kLdsMax = 160 * 1024 - 16 * 1024 - 64;
 #else
 static constexpr size_t kLdsMax = 160 * 1024;
 #endif
+static size_t lds_bytes_for(int32_t V) { return (((size_t)14 * V + 15) & ~(size_t)15) + 16; }
+// the arc offsets in LDS (ldsoff): 16-bit per vertex, a 32-bit base per 64-vertex chunk
+// the row kernels' frontier: queued (default) or the half-wave pairs
+// (SHD_PC_BF_PAIRS, the A/B of DESIGN.md §6)
+static int bf_queue_bit() {
+    static const int b = getenv("SHD_PC_BF_PAIRS") ? 0 : 2;
+    return b;
+}
+static size_t lds_off_bytes(int32_t V) {
+    return (((size_t)2 * V + 15) & ~(size_t)15) + ((((size_t)(V + 63) / 64 + 1) * 4 + 15) & ~(size_t)15);
+}
+// the LDS layout of a row kernel launch: the row arrays, then (when they fit
+// and the graph allows, shd_pc::lds_off_ok) the arc offsets
+static size_t lds_launch_bytes(const shd_pc* pc, bool* ldsoff) {
+    const size_t rows = lds_bytes_for(pc->V);
+    *ldsoff = pc->lds_off_ok && rows + lds_off_bytes(pc->V) <= kLdsMax;
+    return rows + (*ldsoff ? lds_off_bytes(pc->V) : 0);
+}
 
 // The rows the first pass listed (equal-cost predecessors somewhere in the
 // row): their parents from k_sssp_tie_parents, in chunks of rows whose heaps
@@ -1062,7 +1172,8 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     }
     char* scr = (char*)pc->d_tie_scratch;
     int32_t* fpar = (int32_t*)(scr + need_s);
-    const size_t lds = lds_bytes_for(V);
+    bool lo = false;
+    const size_t lds_rows = lds_bytes_for(V), lds = lds_launch_bytes(pc, &lo);
     for (int64_t c0 = 0; c0 < n; c0 += chunk) {
         const int32_t cn = (int32_t)std::min<int64_t>(chunk, n - c0);
         const int32_t* rows = pc->d_tie_rows + c0;
@@ -1070,19 +1181,21 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
                            rows, pc->d_attached,
                            pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar, scr);
         SHD_HIP(hipGetLastError());
-        if (lds <= kLdsMax && V <= 2048) {
+        if (lds_rows <= kLdsMax && V <= 2048) {
             const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, kLdsMax / lds));
             const int grid = std::max(1, std::min(cn, ncu * per_cu));
             hipLaunchKernelGGL(k_sssp_rows_lds<256>, dim3(grid), dim3(256), lds, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
-                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr);
-        } else if (lds <= kLdsMax) {
+                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr,
+                               (lo ? 1 : 0) | bf_queue_bit());
+        } else if (lds_rows <= kLdsMax) {
             const int grid = std::max(1, std::min(cn, ncu));
             hipLaunchKernelGGL(k_sssp_rows_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
-                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr);
+                               pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr,
+                               (lo ? 1 : 0) | bf_queue_bit());
         } else {
             // the first pass sized d_scratch for ncu * 4 blocks
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -1091,7 +1204,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
                                pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, (char*)pc->d_scratch, per_block,
-                               0, cn, rows, fpar, nullptr);
+                               0, cn, rows, fpar, nullptr, bf_queue_bit());
         }
         SHD_HIP(hipGetLastError());
     }
@@ -1135,11 +1248,12 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
     }
     SHD_HIP(hipEventRecord(ev[1], s));
     if (pc->rows_mode) {
-        const size_t lds = lds_bytes_for(V);
+        bool lo = false;
+        const size_t lds_rows = lds_bytes_for(V), lds = lds_launch_bytes(pc, &lo);
         int ncu = 256;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, pc->device) == hipSuccess) ncu = prop.multiProcessorCount;
-        if (lds <= kLdsMax) {
+        if (lds_rows <= kLdsMax) {
             if (V <= 2048) {
                 int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, kLdsMax / lds));
                 int grid = std::max(1, std::min(row1 - row0, ncu * per_cu));
@@ -1149,7 +1263,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
-                                   pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows);
+                                   pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
+                                   (lo ? 1 : 0) | bf_queue_bit());
             } else {
                 int grid = std::max(1, std::min(row1 - row0, ncu));
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<kRowBlock>,
@@ -1158,7 +1273,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid,
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
-                                   pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows);
+                                   pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
+                                   (lo ? 1 : 0) | bf_queue_bit());
             }
         } else {
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -1172,7 +1288,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w,
                                pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                                pc->d_stats, (char*)pc->d_scratch, per_block, row0, row1, nullptr, nullptr,
-                               pc->d_tie_rows);
+                               pc->d_tie_rows, bf_queue_bit());
         }
         SHD_HIP(hipGetLastError());
         const int rc = finish_tie_rows(pc, ncu);

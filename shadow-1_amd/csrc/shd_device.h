@@ -63,6 +63,7 @@ struct shd_pc {
     uint8_t* d_adj = nullptr;           // [T][T] 1 = adjacent (direct path exists)
     void* d_scratch = nullptr;          // global-memory SSSP scratch (large V)
     size_t scratch_bytes = 0;
+    bool lds_off_ok = false;            // the row kernel may keep the CSR's arc offsets in LDS
     int32_t* d_tie_rows = nullptr;      // [T] rows with equal-cost predecessors (first pass)
     void* d_tie_scratch = nullptr;      // k_sssp_tie_parents: lane heaps + parents
     size_t tie_scratch_bytes = 0;

@@ -41,6 +41,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -2530,6 +2531,68 @@ static double ms_since(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
 
+// The run's device buffers come from a per-device workspace.  By default it
+// is released at the end of each call; after shd_tcp_keep_workspace(1) it
+// outlasts the call (grown when a run needs more) until
+// shd_tcp_keep_workspace(0): the per-host arenas of a large model are tens of
+// GB, and allocating and freeing them every call costs more wall time than
+// the rounds themselves.  One run at a time uses a device's
+// workspace (its lock is held for the call).
+enum WsSlot {
+    kWsLat, kWsRel, kWsRank, kWsSrank, kWsNextRank, kWsFt, kWsFtord, kWsNft, kWsHv, kWsHost, kWsSock, kWsProc,
+    kWsHostProcs, kWsPool, kWsPsack, kWsFreel, kWsEv, kWsCq, kWsMsack, kWsNmsack, kWsMail, kWsNmail, kWsMhead,
+    kWsMnext, kWsCtl, kWsIpk, kWsNode, kWsTr, kWsTrs, kWsNextTime, kWsQlog, kWsNqlog, kWsProf, kWsProfRound,
+    kWsSlots
+};
+struct TcpWs {
+    std::mutex mu;
+    void* p[kWsSlots] = {};
+    size_t n[kWsSlots] = {};
+};
+constexpr int kWsDevices = 64;
+static TcpWs g_ws[kWsDevices];
+
+static void ws_free_all(TcpWs& w) {
+    for (int i = 0; i < kWsSlots; i++) {
+        if (w.p[i]) (void)hipFree(w.p[i]);
+        w.p[i] = nullptr;
+        w.n[i] = 0;
+    }
+}
+
+template <class T>
+static hipError_t ws_alloc(TcpWs& w, int slot, T** out, size_t bytes) {
+    if (bytes == 0) bytes = 1;
+    if (w.n[slot] < bytes) {
+        if (w.p[slot]) (void)hipFree(w.p[slot]);
+        w.p[slot] = nullptr;
+        w.n[slot] = 0;
+        const hipError_t e = hipMalloc(&w.p[slot], bytes);
+        if (e != hipSuccess) return e;
+        w.n[slot] = bytes;
+    }
+    *out = (T*)w.p[slot];
+    return hipSuccess;
+}
+
+static bool g_ws_keep = false;
+
+extern "C" void shd_tcp_keep_workspace(int32_t keep) {
+    g_ws_keep = keep != 0;
+    if (keep) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int d = 0; d < kWsDevices; d++) {
+        std::lock_guard<std::mutex> lk(g_ws[d].mu);
+        bool any = false;
+        for (int i = 0; i < kWsSlots; i++) any |= g_ws[d].p[i] != nullptr;
+        if (!any) continue;
+        (void)hipSetDevice(d);
+        ws_free_all(g_ws[d]);
+    }
+    (void)hipSetDevice(cur);
+}
+
 extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
     const auto t_call = std::chrono::steady_clock::now();
     auto t_results = t_call;
@@ -2600,6 +2663,11 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     if (W == ~0ull) W = m->end_time ? m->end_time : 1;
 
     int rc = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kWsDevices) return -5;
+    TcpWs& ws = g_ws[dev];
+    std::unique_lock<std::mutex> ws_lock(ws.mu);
+    const bool ws_keep = g_ws_keep;
     Glob g;
     memset(&g, 0, sizeof(g));
     std::vector<DHost> hh(H);
@@ -2663,8 +2731,8 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     if (m->qdisc > 1) { free(res); return -22; }
     g.qdisc_rr = m->qdisc;
     if (!pc) {
-        HCHECK(hipMalloc(&d_lat, sizeof(double) * (size_t)V * V));
-        HCHECK(hipMalloc(&d_rel, sizeof(double) * (size_t)V * V));
+        HCHECK(ws_alloc(ws, kWsLat, &d_lat, sizeof(double) * (size_t)V * V));
+        HCHECK(ws_alloc(ws, kWsRel, &d_rel, sizeof(double) * (size_t)V * V));
         HCHECK(hipMemcpy(d_lat, m->path_lat_ms, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
         HCHECK(hipMemcpy(d_rel, m->path_rel, sizeof(double) * (size_t)V * V, hipMemcpyHostToDevice));
     } else {   // the cache's tables and ranks (copied back at the end)
@@ -2673,59 +2741,66 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         g.pc_complete = pc->complete ? 1u : 0u;
         g.pc_prefer_direct = pc->prefer_direct ? 1u : 0u;
         g.prow = pc->d_row; g.pself = pc->d_self; g.pdir = pc->d_dir; g.padj = pc->d_adj; g.pself_eid = pc->d_self_eid;
-        HCHECK(hipMalloc(&g.rank, sizeof(int32_t) * (size_t)V));
-        HCHECK(hipMalloc(&g.srank, sizeof(int32_t) * (size_t)V));
-        HCHECK(hipMalloc(&g.next_rank, sizeof(int32_t)));
+        HCHECK(ws_alloc(ws, kWsRank, &g.rank, sizeof(int32_t) * (size_t)V));
+        HCHECK(ws_alloc(ws, kWsSrank, &g.srank, sizeof(int32_t) * (size_t)V));
+        HCHECK(ws_alloc(ws, kWsNextRank, &g.next_rank, sizeof(int32_t)));
         HCHECK(hipMemcpy(g.rank, pc->h_rank, sizeof(int32_t) * (size_t)V, hipMemcpyHostToDevice));
         HCHECK(hipMemcpy(g.srank, pc->h_self_rank, sizeof(int32_t) * (size_t)V, hipMemcpyHostToDevice));
         HCHECK(hipMemcpy(g.next_rank, &pc->next_rank, sizeof(int32_t), hipMemcpyHostToDevice));
         g.ft_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);
-        HCHECK(hipMalloc(&g.ft, sizeof(shd_tcp_query) * (size_t)g.ft_cap));
-        HCHECK(hipMalloc(&g.ftord, sizeof(int32_t) * (size_t)g.ft_cap));
-        HCHECK(hipMalloc(&g.nft, sizeof(uint32_t)));
+        HCHECK(ws_alloc(ws, kWsFt, &g.ft, sizeof(shd_tcp_query) * (size_t)g.ft_cap));
+        HCHECK(ws_alloc(ws, kWsFtord, &g.ftord, sizeof(int32_t) * (size_t)g.ft_cap));
+        HCHECK(ws_alloc(ws, kWsNft, &g.nft, sizeof(uint32_t)));
         HCHECK(hipMemset(g.nft, 0, sizeof(uint32_t)));
     }
-    HCHECK(hipMalloc(&d_hv, sizeof(int32_t) * (size_t)H));
+    HCHECK(ws_alloc(ws, kWsHv, &d_hv, sizeof(int32_t) * (size_t)H));
     HCHECK(hipMemcpy(d_hv, hvi.data(), sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
     g.lat = d_lat; g.rel = d_rel; g.hv = d_hv; g.V = V; g.pool_cap = pool_cap;
-    HCHECK(hipMalloc(&g.host, sizeof(DHost) * H));
+    HCHECK(ws_alloc(ws, kWsHost, &g.host, sizeof(DHost) * H));
     HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * H, hipMemcpyHostToDevice));
-    HCHECK(hipMalloc(&g.sock, sizeof(DSock) * (size_t)H * kSock));
+    HCHECK(ws_alloc(ws, kWsSock, &g.sock, sizeof(DSock) * (size_t)H * kSock));
     HCHECK(hipMemset(g.sock, 0, sizeof(DSock) * (size_t)H * kSock));
-    HCHECK(hipMalloc(&g.proc, sizeof(DProc) * pp.size()));
+    HCHECK(ws_alloc(ws, kWsProc, &g.proc, sizeof(DProc) * pp.size()));
     HCHECK(hipMemcpy(g.proc, pp.data(), sizeof(DProc) * pp.size(), hipMemcpyHostToDevice));
-    HCHECK(hipMalloc(&g.host_procs, sizeof(int32_t) * hp.size()));
+    HCHECK(ws_alloc(ws, kWsHostProcs, &g.host_procs, sizeof(int32_t) * hp.size()));
     HCHECK(hipMemcpy(g.host_procs, hp.data(), sizeof(int32_t) * hp.size(), hipMemcpyHostToDevice));
-    HCHECK(hipMalloc(&g.pool, sizeof(DPkt) * (size_t)H * pool_cap));
-    HCHECK(hipMalloc(&g.psack, sizeof(int32_t) * kPktSack * (size_t)H * pool_cap));
-    HCHECK(hipMalloc(&g.freel, sizeof(int32_t) * (size_t)H * pool_cap));
+    HCHECK(ws_alloc(ws, kWsPool, &g.pool, sizeof(DPkt) * (size_t)H * pool_cap));
+    HCHECK(ws_alloc(ws, kWsPsack, &g.psack, sizeof(int32_t) * kPktSack * (size_t)H * pool_cap));
+    HCHECK(ws_alloc(ws, kWsFreel, &g.freel, sizeof(int32_t) * (size_t)H * pool_cap));
     k_tcp_free_init<<<(unsigned)(((size_t)H * pool_cap + 255) / 256), 256>>>(g.freel, (size_t)H * pool_cap, pool_cap);
     HCHECK(hipGetLastError());
-    HCHECK(hipMalloc(&g.ev, sizeof(DEv) * (size_t)H * kEv));
-    HCHECK(hipMalloc(&g.cq, sizeof(CqEnt) * (size_t)H * kCq));
+    HCHECK(ws_alloc(ws, kWsEv, &g.ev, sizeof(DEv) * (size_t)H * kEv));
+    HCHECK(ws_alloc(ws, kWsCq, &g.cq, sizeof(CqEnt) * (size_t)H * kCq));
     {
         const uint32_t parts = (uint32_t)H * 32u > kMailMin ? (uint32_t)H * 32u : kMailMin;
         g.mail_part = parts / kMailSub;
-        g.mail_cap = g.mail_part * kMailSub + g.mail_part * kMailSub / 2;
+        uint32_t ovf = g.mail_part * kMailSub / 2;
+        // SHD_TCP_MAIL_PART: smaller parts (the same overflow range), so that a
+        // test's model of a few hundred hosts exercises the overflow path
+        if (const char* e = getenv("SHD_TCP_MAIL_PART")) {
+            const long v = strtol(e, nullptr, 10);
+            if (v >= 1 && v < (long)g.mail_part) g.mail_part = (uint32_t)v;
+        }
+        g.mail_cap = g.mail_part * kMailSub + ovf;
     }
     g.msack_cap = g.mail_cap * kMailSack;
-    HCHECK(hipMalloc(&g.msack, sizeof(int32_t) * 2 * (size_t)g.msack_cap));
-    HCHECK(hipMalloc(&g.nmsack, sizeof(uint32_t) * 2));
+    HCHECK(ws_alloc(ws, kWsMsack, &g.msack, sizeof(int32_t) * 2 * (size_t)g.msack_cap));
+    HCHECK(ws_alloc(ws, kWsNmsack, &g.nmsack, sizeof(uint32_t) * 2));
     HCHECK(hipMemset(g.nmsack, 0, sizeof(uint32_t) * 2));
-    HCHECK(hipMalloc(&g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
-    HCHECK(hipMalloc(&g.nmail, sizeof(uint32_t) * 2 * (kMailSub + 1)));
+    HCHECK(ws_alloc(ws, kWsMail, &g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
+    HCHECK(ws_alloc(ws, kWsNmail, &g.nmail, sizeof(uint32_t) * 2 * (kMailSub + 1)));
     HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * (kMailSub + 1)));
-    HCHECK(hipMalloc(&g.mhead, sizeof(int32_t) * 2 * (size_t)H));
+    HCHECK(ws_alloc(ws, kWsMhead, &g.mhead, sizeof(int32_t) * 2 * (size_t)H));
     HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
-    HCHECK(hipMalloc(&g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
-    HCHECK(hipMalloc(&g.ctl, sizeof(TCtl)));
+    HCHECK(ws_alloc(ws, kWsMnext, &g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
+    HCHECK(ws_alloc(ws, kWsCtl, &g.ctl, sizeof(TCtl)));
     HCHECK(hipMemset(g.ctl, 0, sizeof(TCtl)));
-    HCHECK(hipMalloc(&d_ipk, sizeof(uint64_t) * ipk.size()));
+    HCHECK(ws_alloc(ws, kWsIpk, &d_ipk, sizeof(uint64_t) * ipk.size()));
     HCHECK(hipMemcpy(d_ipk, ipk.data(), sizeof(uint64_t) * ipk.size(), hipMemcpyHostToDevice));
     g.ip_key = d_ipk;
     if (trace & SHD_TCP_TRACE_NODE) {   // every heartbeat before the end, per host
         g.node_k = (uint32_t)((m->end_time - 1) / g.hb) + 1;
-        if (hipMalloc(&g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k) != hipSuccess) {
+        if (ws_alloc(ws, kWsNode, &g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k) != hipSuccess) {
             (void)hipGetLastError();
             fprintf(stderr, "shd_tcp_run: no device memory for the tracker counters\n");
             rc = -12;
@@ -2736,8 +2811,8 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         // kTr records and kTrSack SACK words per host (about 16 MB): a traced
         // run of many hosts may not fit; say so instead of a bare -ENOMEM
         const size_t need = (sizeof(TRec) * (size_t)kTr + sizeof(int32_t) * (size_t)kTrSack) * (size_t)H;
-        if (hipMalloc(&g.tr, sizeof(TRec) * (size_t)H * kTr) != hipSuccess ||
-            hipMalloc(&g.trs, sizeof(int32_t) * (size_t)H * kTrSack) != hipSuccess) {
+        if (ws_alloc(ws, kWsTr, &g.tr, sizeof(TRec) * (size_t)H * kTr) != hipSuccess ||
+            ws_alloc(ws, kWsTrs, &g.trs, sizeof(int32_t) * (size_t)H * kTrSack) != hipSuccess) {
             (void)hipGetLastError();
             fprintf(stderr, "shd_tcp_run: no device memory for the status trace of %d hosts (%.1f GB); "
                             "run without trace\n", H, need / 1e9);
@@ -2745,16 +2820,16 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
             goto done;
         }
     }
-    HCHECK(hipMalloc(&g.next_time, sizeof(uint64_t) * (H + 1)));
+    HCHECK(ws_alloc(ws, kWsNextTime, &g.next_time, sizeof(uint64_t) * (H + 1)));
     HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (H + 1)));
     // every host can log kPq first queries (touch_log)
     g.qlog_cap = (uint32_t)H * kPq > (1u << 16) ? (uint32_t)H * kPq : (1u << 16);
-    HCHECK(hipMalloc(&g.qlog, sizeof(shd_tcp_query) * (size_t)g.qlog_cap));
-    HCHECK(hipMalloc(&g.nqlog, sizeof(uint32_t)));
+    HCHECK(ws_alloc(ws, kWsQlog, &g.qlog, sizeof(shd_tcp_query) * (size_t)g.qlog_cap));
+    HCHECK(ws_alloc(ws, kWsNqlog, &g.nqlog, sizeof(uint32_t)));
 #ifdef SHD_TCP_PROF
-    HCHECK(hipMalloc(&g.prof, sizeof(uint64_t) * 2 * kProf * (size_t)H));
+    HCHECK(ws_alloc(ws, kWsProf, &g.prof, sizeof(uint64_t) * 2 * kProf * (size_t)H));
     HCHECK(hipMemset(g.prof, 0, sizeof(uint64_t) * 2 * kProf * (size_t)H));
-    HCHECK(hipMalloc(&g.prof_round, sizeof(uint32_t) * 2 * kProfRounds));
+    HCHECK(ws_alloc(ws, kWsProfRound, &g.prof_round, sizeof(uint32_t) * 2 * kProfRounds));
     HCHECK(hipMemset(g.prof_round, 0, sizeof(uint32_t) * 2 * kProfRounds));
 #endif
     HCHECK(hipMemset(g.nqlog, 0, sizeof(uint32_t)));
@@ -2904,16 +2979,8 @@ done:
     if (gexec) (void)hipGraphExecDestroy(gexec);
     if (graph) (void)hipGraphDestroy(graph);
     if (st) (void)hipStreamDestroy(st);
-    (void)hipFree(d_lat); (void)hipFree(d_rel); (void)hipFree(d_ipk); (void)hipFree(d_hv);
-    (void)hipFree(g.mail); (void)hipFree(g.nmail); (void)hipFree(g.mhead); (void)hipFree(g.mnext); (void)hipFree(g.ctl);
-    (void)hipFree(g.host); (void)hipFree(g.sock); (void)hipFree(g.proc); (void)hipFree(g.host_procs);
-    (void)hipFree(g.pool); (void)hipFree(g.psack); (void)hipFree(g.freel);
-    (void)hipFree(g.msack); (void)hipFree(g.nmsack); (void)hipFree(g.ev); (void)hipFree(g.cq);
-    (void)hipFree(g.tr); (void)hipFree(g.trs); (void)hipFree(g.next_time);
-    (void)hipFree(g.qlog); (void)hipFree(g.nqlog); (void)hipFree(g.node); (void)hipFree(g.prof);
-    (void)hipFree(g.prof_round);
-    (void)hipFree(g.rank); (void)hipFree(g.srank); (void)hipFree(g.next_rank);
-    (void)hipFree(g.ft); (void)hipFree(g.ftord); (void)hipFree(g.nft);
+    if (!ws_keep || rc) ws_free_all(ws);   // a failed run leaves no workspace behind
+    ws_lock.unlock();
     if (rc) { shd_tcp_result_free(res); return rc; }
     res->teardown_ms = ms_since(t_free);
     *out = res;

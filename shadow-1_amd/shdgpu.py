@@ -224,6 +224,7 @@ class Lines(C.Structure):
 _SIGS = {
     "shd_tcp_run": (C.c_int, [P(TcpModel), C.c_int32, P(P(TcpResult))]),
     "shd_tcp_result_free": (None, [P(TcpResult)]),
+    "shd_tcp_keep_workspace": (None, [C.c_int32]),
     "shd_tracker_node_lines": (C.c_int, [P(C.c_uint64), C.c_uint64, C.c_uint64, C.c_uint32, P(P(Lines))]),
     "shd_graph_check": (C.c_int, [P(Graph), P(GraphProps)]),
     "shd_graphml_load_file": (C.c_int, [C.c_char_p, P(P(GraphML))]),

@@ -33,6 +33,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import time
+
 import numpy as np
 
 import shdgpu as S
@@ -110,7 +112,9 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
         m = model.struct
         H = int(m.n_hosts)
         hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
+        t_pc = time.perf_counter()
         pc = sim.PathCache(g, np.unique(hv))
+        pc_ms = (time.perf_counter() - t_pc) * 1e3
         try:
             out = _run_once(model, ips, procs, peers, None, None, hv.astype(np.int32), nbytes, trace, recv_buf,
                             send_buf, tcp_window, packets_per_host, node, qdisc, pc=pc)
@@ -119,6 +123,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
         if out is not None:
             out.pop("queries")
             out["first_touch"] = "device"
+            out["host_ms"]["path_cache"] = pc_ms
             return out
     lat, rel, hvi, att = path_table(model, g, procs, peers, reverse=guess_reversed)
     V = lat.shape[0]

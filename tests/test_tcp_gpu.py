@@ -21,6 +21,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
 
 
+# cases whose first touches contradict a lane's choice within one window, so
+# that the device run stops with SHD_TCP_ERR_FIRST_TOUCH and the driver runs
+# the tables: shared_hosts(_rr) connect 0->1, 1->2, 2->0 at the same instant
+# (serially, host 2's query of (vertex 7, vertex 0) finds vertex 0 ranked by
+# host 0's touch; its lane saw both unranked and chose vertex 7's row);
+# loopback_mixed's host 0 ranks its own vertex (a self path) in the round in
+# which host 1 first queries (3, 0)
+DEVICE_FALLS_BACK = {"shared_hosts", "shared_hosts_rr", "loopback_mixed"}
+
+
 @pytest.mark.parametrize("mode", ["device", "tables"])
 @pytest.mark.parametrize("name", list(TC.CASES))
 def test_tcp_gpu_equals_reference(name, mode):
@@ -31,7 +41,7 @@ def test_tcp_gpu_equals_reference(name, mode):
     ips = TC.ip_ints(f["ips"])
     r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], node=True, qdisc=c.get("qdisc", 0),
                    mode=mode)
-    assert r["first_touch"] == mode
+    assert r["first_touch"] == ("tables" if mode == "device" and name in DEVICE_FALLS_BACK else mode)
     got = r["lines"]
     # the tracker's [node] lines: the library's writer over the device's counters
     assert len(r["node_lines"]) == f["n_heartbeat"]
@@ -110,17 +120,21 @@ def test_tcp_gpu_first_touch_order_settles(name):
         assert wrong   # the case is built so that the order matters
 
 
-def test_tcp_gpu_wide_window_uses_the_mailbox_overflow():
+def test_tcp_gpu_wide_window_uses_the_mailbox_overflow(monkeypatch):
     """Fast, long connections (about 1 Gbit/s links, 8 MB each way) whose
     hosts share mailbox parts (the mailbox is split into 64 parts by host
     index: hosts 1, 65 and 129 are clients in part 1, hosts 0, 64 and 128
-    servers in part 0): a part's 1024 slots per round are not enough, and the
-    sends spill into the shared overflow range -- the run must neither fail
-    with SHD_TCP_ERR_MAILBOX nor differ from the oracle."""
+    servers in part 0).  The model's busiest round takes a few thousand
+    deliveries, tens per part; with the parts cut to 8 slots
+    (SHD_TCP_MAIL_PART, the overflow range left at its size) the sends spill
+    into the shared overflow range -- the run must neither fail with
+    SHD_TCP_ERR_MAILBOX nor differ from the oracle."""
     import workloads as W
     g, m, ips, procs, peers, nb = W.tcp_echo_model(130, 40, end_s=8, nbytes=8_000_000, bw_down=122070,
                                                    bw_up=122070)
+    monkeypatch.setenv("SHD_TCP_MAIL_PART", "8")
     r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, trace=False)
+    monkeypatch.delenv("SHD_TCP_MAIL_PART")
     o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb, lines=False)
     assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
     assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
