@@ -440,6 +440,9 @@ typedef struct shd_run_stats {
                                        (k_round_ps: the round grid fits the GPU;
                                        k_round_sp: more hosts, blocks of many) */
     uint64_t n_batches_sparse;      /* ... of them, sparse (k_round_sp)           */
+    uint64_t n_rounds_replayed;     /* rounds run again from the last state copy to recover
+                                       an unprotected round whose first-touch drop decision
+                                       was ambiguous (shd_eng_run_until) */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

@@ -787,6 +787,7 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             for (int k = 0; k < nl && !rc; k++) {
                 round0[k] = g->engs[k]->round;
                 SHD_HIP(hipSetDevice(g->engs[k]->device));
+                g->engs[k]->snap_valid = false;   // the group's copy, not a run_until restore point
                 rc = snapshot_state(g->engs[k], false);
             }
             if (rc) break;

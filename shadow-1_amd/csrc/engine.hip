@@ -83,6 +83,19 @@ struct shd_eng {
     // drop decisions turns out ambiguous, then the round reruns with the ranks
     std::vector<void*> snap;
     bool snap_failed = false;
+    // the copy as a restore point (shd_eng_run_until): `snap` holds the state
+    // at the start of round snap_round, window start snap_next, and nothing
+    // outside the rounds has changed the state since (push_events, ingest and
+    // the host-driven co-simulation rounds clear snap_valid)
+    bool snap_valid = false;
+    bool in_replay = false;
+    int snap_parity = 0;
+    uint64_t snap_round = 0, snap_next = 0;
+    DevSummary snap_sum{};
+    // the stops of the run_until calls since the copy: a round's window ends at
+    // min(start + W, stop), so a replay stops at each of them again to run the
+    // same windows (the same rounds resolve the same first-touch logs)
+    std::vector<uint64_t> snap_stops;
     // shd_eng_round_begin's state copy, for shd_eng_round_retry
     bool rb_snap = false;
     int rb_parity = 0;
@@ -603,6 +616,7 @@ extern "C" int shd_eng_boot(shd_eng* e) {
     if ((rc = read_summary(e))) return rc;
     e->parity = 0;
     e->booted = true;
+    e->snap_valid = false;
     if (e->h_sum->error) return SHD_EOVERFLOW;
     return SHD_OK;
 }
@@ -611,6 +625,7 @@ extern "C" int shd_eng_push_events(shd_eng* e, const shd_event* ev, uint64_t n) 
     if (!e || (n && !ev)) return SHD_EINVAL;
     if (!e->booted) return SHD_EINVAL;
     if (!n) return SHD_OK;
+    e->snap_valid = false;   // a replay from the copy would miss these events
     if (n > (1u << 30)) return SHD_ERANGE;
     // two kinds: application starts of this engine's hosts (each consumes its
     // host's next event ID here), and packet deliveries from hosts outside this
@@ -942,6 +957,21 @@ static int snapshot_state(shd_eng* e, bool restore) {
     return SHD_OK;
 }
 
+// a state copy at the start of the round about to run from window start `next`
+static int take_restore_point(shd_eng* e, uint64_t next) {
+    const int rc = snapshot_state(e, false);
+    if (rc) { e->snap_valid = false; return rc; }
+    e->snap_valid = true;
+    e->snap_round = e->round;
+    e->snap_parity = e->parity;
+    e->snap_sum = *e->h_sum;
+    e->snap_next = next;
+    e->snap_stops.clear();
+    return SHD_OK;
+}
+
+static bool replay_off() { return getenv("SHD_NO_REPLAY") != nullptr; }
+
 static bool want_protect(const shd_eng* e) {
     if (protect_off() || e->snap_failed) return false;
     // complete graphs serve the direct value, which does not depend on which
@@ -952,7 +982,7 @@ static bool want_protect(const shd_eng* e) {
 
 // one protected round [ws, we) (host-driven, k_round); returns its summary
 static int protected_round(shd_eng* e, uint64_t ws, uint64_t we, shd_round_summary* out, uint32_t* reruns) {
-    int rc = snapshot_state(e, false);
+    int rc = take_restore_point(e, ws);
     if (rc == SHD_ENOMEM) return shd_eng_run_round(e, ws, we, out);
     if (rc) return rc;
     const int parity0 = e->parity;
@@ -996,6 +1026,7 @@ extern "C" int shd_eng_round_begin(shd_eng* e, uint64_t ws, uint64_t we, shd_rou
     if (!e || !e->booted || we <= ws || we - ws > e->window) return SHD_EINVAL;
     SHD_HIP(hipSetDevice(e->device));
     e->rb_snap = false;
+    e->snap_valid = false;   // the co-simulation's rounds: the copy is the retry's only
     if (want_protect(e)) {
         const int rc = snapshot_state(e, false);
         if (rc == SHD_OK) {
@@ -1037,6 +1068,66 @@ extern "C" int shd_eng_round_retry(shd_eng* e, const shd_pending* all, uint64_t 
     return SHD_OK;
 }
 
+// An unprotected round (a batch round) logged a first touch whose drop
+// decision differs under the two candidate rows: nothing of it can be kept.
+// Go back to the last restore point, run the rounds from there to the
+// ambiguous round's start again, and run that round protected (rolled back to
+// its own copy, its log ranked, run again).  None of the replayed rounds can
+// be ambiguous: they make the same sends with the same draws, and every
+// vertex ranked in the first run is ranked now (the ranks assigned since the
+// copy are restored with it and assigned again in the same serial order), so
+// a send is undecided in the replay only if it was undecided and decidable
+// the first time.  No snapshot of the round itself is needed.
+static int replay_ambiguous(shd_eng* e, uint64_t ws, uint64_t stop, shd_round_summary* r, shd_run_stats* s) {
+    if (!e->snap_valid || e->in_replay) return SHD_EAMBIG;
+    int rc = snapshot_state(e, true);
+    if (rc) return rc;
+    e->round = e->snap_round;
+    e->parity = e->snap_parity;
+    *e->h_sum = e->snap_sum;
+    e->h_sum->next_time = e->snap_next;
+    e->tl_ready = false;
+    SHD_HIP(hipStreamSynchronize(e->stream));
+    const uint64_t round0 = e->round;
+    const double kms = e->kernel_ms_total;
+    std::vector<uint64_t> stops = e->snap_stops;   // (a protected round of the replay takes a new copy)
+    // the restore point's own round runs protected again: it may be the
+    // protected round that took the copy and was ambiguous itself (rolled back
+    // and rerun from its log), which unprotected would be ambiguous again
+    if (e->snap_next < ws) {
+        uint64_t we0 = e->snap_next + e->window;
+        const uint64_t stop0 = stops.empty() ? stop : stops.front();
+        if (we0 > stop0 || we0 < e->snap_next) we0 = stop0;
+        shd_round_summary r0{};
+        e->in_replay = true;
+        rc = protected_round(e, e->snap_next, we0, &r0, &s->n_rounds_rerun);
+        e->in_replay = false;
+        if (rc) return rc;
+        e->h_sum->next_time = r0.next_time;
+    }
+    stops.push_back(ws);
+    e->in_replay = true;
+    double sub_ms = 0;
+    for (const uint64_t b : stops) {
+        if (b <= e->h_sum->next_time || b > ws) continue;
+        shd_run_stats sub{};
+        rc = shd_eng_run_until(e, b, &sub);
+        sub_ms += sub.device_ms_round_kernel;
+        s->n_rounds_rerun += sub.n_rounds_rerun;
+        if (rc) break;
+    }
+    e->in_replay = false;
+    e->kernel_ms_total = kms + sub_ms;
+    if (rc) return rc;
+    if (e->h_sum->next_time != ws) return SHD_EAMBIG;   // (the replay did not reach the round: cannot happen)
+    s->n_rounds_replayed += e->round - round0;
+    uint64_t we = ws + e->window;
+    if (we > stop || we < ws) we = stop;
+    rc = protected_round(e, ws, we, r, &s->n_rounds_rerun);
+    s->n_rounds_protected++;
+    return rc;
+}
+
 extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st) {
     if (!e) return SHD_EINVAL;
     // a partial engine's sends to hosts outside it leave by rounds
@@ -1050,8 +1141,14 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     s.window_ns = e->window;
     const uint64_t stop = std::min<uint64_t>(t_stop, e->P.end_time);
     uint64_t next = e->h_sum->next_time;
-    e->kernel_ms_total = 0;
+    if (!e->in_replay) e->kernel_ms_total = 0;
     const uint64_t pend0 = e->pending_resolved;
+    // a restore point for an ambiguous unprotected round (replay_ambiguous);
+    // complete graphs never log a first touch
+    if (!e->snap_valid && !e->snap_failed && !e->P.complete && !replay_off() && next < stop && !want_protect(e)) {
+        const int rc0 = take_restore_point(e, next);
+        if (rc0 && rc0 != SHD_ENOMEM) return rc0;
+    }
     constexpr int B = shd_eng::kBatch, R = shd_eng::kRing;
     static_assert(R >= B + 2, "summary ring");
     while (next < stop && rc == SHD_OK) {
@@ -1121,6 +1218,8 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         // late, rare logs cost one halt each); after more, it is ticketed.
         uint32_t n_logs = 0;
         uint64_t b_rounds = 0, b_active = 0;
+        bool amb = false;
+        uint64_t amb_ws = 0;
         for (int i = 0; i < nb; i++) {
             const DevSummary& r = e->h_ring[i + 1];
             const uint64_t ws = e->h_ring[i].next_time;
@@ -1128,6 +1227,12 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             const double ms = round_kernel_ms(e, r);
             e->kernel_ms_total += ms;
             e->last_kernel_ms = ms;
+            if ((r.error & SHD_ERR_AMBIGUOUS) && !(r.error & ~(uint32_t)SHD_ERR_AMBIGUOUS) && e->snap_valid &&
+                !e->in_replay && !replay_off()) {
+                amb = true;   // this round and the batch's later ones are dropped: replay_ambiguous
+                amb_ws = ws;
+                break;
+            }
             if (r.n_pending) n_logs++;
             const bool halted_here = halt && r.n_pending > (tl ? 0ull : (unsigned long long)kResolveMax);
             s.n_rounds++;
@@ -1160,7 +1265,10 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
                 e->last_logged = r.n_pending;
                 e->logged_any = true;
                 next = e->h_sum->next_time;
-                if (e->h_sum->error) { s.error = e->h_sum->error; rc = SHD_EOVERFLOW; }
+                if (e->h_sum->error) {
+                    s.error = e->h_sum->error;
+                    rc = (e->h_sum->error & SHD_ERR_AMBIGUOUS) ? SHD_EAMBIG : SHD_EOVERFLOW;
+                }
                 break;
             }
             if (r.n_pending) e->pending_resolved += r.n_pending;
@@ -1175,10 +1283,31 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         }
         e->tl_ready = n_logs <= 1;
         if (b_rounds && tl && !e->sp_forced) e->sp_dense = (double)b_active > kSpDenseFrac * (double)b_rounds * (double)e->nloc;
+        if (amb) {
+            uint64_t we = amb_ws + e->window;
+            if (we > stop || we < amb_ws) we = stop;
+            shd_round_summary r{};
+            const uint64_t pend_before = e->pending_resolved;
+            rc = replay_ambiguous(e, amb_ws, stop, &r, &s);
+            if (rc && !(rc == SHD_EOVERFLOW && r.error)) break;
+            s.n_rounds++;
+            s.n_events += r.n_events;
+            s.n_pkt_events += r.n_pkt_events;
+            s.n_host_rounds += e->round_active;
+            s.final_time = we;
+            if (r.error) { s.error = r.error; rc = rc ? rc : SHD_EOVERFLOW; break; }
+            e->last_logged = e->pending_resolved - pend_before;
+            if (e->last_logged) e->logged_any = true;
+            e->tl_ready = e->last_logged == 0;
+            next = r.next_time;
+        }
     }
     e->h_sum->next_time = next;
     // every event before `stop` has run: the engine's clock stands at stop
     if (rc == SHD_OK) e->t_done = std::max<uint64_t>(e->t_done, std::min<uint64_t>(stop, next));
+    if (rc == SHD_OK && e->snap_valid && !e->in_replay && stop > e->snap_next &&
+        (e->snap_stops.empty() || e->snap_stops.back() != stop))
+        e->snap_stops.push_back(stop);
     s.n_pending_resolved = e->pending_resolved - pend0;
     s.device_ms_round_kernel = e->kernel_ms_total;
     s.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1257,6 +1386,7 @@ extern "C" int shd_eng_remote_copy(shd_eng* e, void* dev_dst, uint64_t cap, uint
 extern "C" int shd_eng_ingest(shd_eng* e, const void* ev, uint64_t n) {
     if (!e || (n && !ev)) return SHD_EINVAL;
     if (!n) return SHD_OK;
+    e->snap_valid = false;
     SHD_HIP(hipSetDevice(e->device));
     hipLaunchKernelGGL(k_ingest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, e->stream, dp(e->P),
                        (const shd_event*)ev, n, e->parity);

@@ -83,6 +83,9 @@ extern "C" int shd_debug_sssp_timing(unsigned long long* out) {
 // Per-row working set: dist u64[V], parent i32[V] (index into the rin_* arcs),
 // upd u16[V] (iteration at which the vertex last improved = frontier stamp).
 constexpr int kChunk = 32;   // edges folded per pass of the forward chain walk
+#ifndef SHD_SSSP_BFQ
+#define SHD_SSSP_BFQ 2   // queued frontier: vertices per half-wave relaxed together
+#endif
 
 template <int BLOCK>
 __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
@@ -135,7 +138,10 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             // keeps two vertices' loads in flight where the pairs below keep
             // one (a chunk holds ~1.3 frontier vertices: the pairs mostly ran
             // one half-wave on one vertex)
-            int32_t q0 = -1, q1 = -1, q2 = -1, q3 = -1;
+            constexpr int Q = SHD_SSSP_BFQ;   // vertices per half-wave in flight
+            int32_t q[2 * Q];
+#pragma unroll
+            for (int j = 0; j < 2 * Q; j++) q[j] = -1;
             int nq = 0;
             auto arc_range = [&](int32_t v, int32_t& b, int32_t& e) {
                 if (off16) {
@@ -156,21 +162,32 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                     }
                 }
             };
-            auto run4 = [&]() {
-                const int32_t va = upper ? q1 : q0, vb = upper ? q3 : q2;
-                int32_t ba = 0, ea = 0, bb = 0, eb = 0;
-                double da = 0.0, db = 0.0;
-                if (va >= 0) { arc_range(va, ba, ea); da = u2d(dist[va]); }
-                if (vb >= 0) { arc_range(vb, bb, eb); db = u2d(dist[vb]); }
-                const int32_t ka = ba + hl, kb = bb + hl;
-                int32_t xa = -1, xb = -1;
-                double wa = 0.0, wb = 0.0;
-                if (ka < ea) { xa = arc_dst[ka]; wa = arc_w[ka]; }
-                if (kb < eb) { xb = arc_dst[kb]; wb = arc_w[kb]; }
-                if (xa >= 0) relax(xa, da + wa);
-                if (xb >= 0) relax(xb, db + wb);
-                for (int32_t k = ka + 32; k < ea; k += 32) relax(arc_dst[k], da + arc_w[k]);
-                for (int32_t k = kb + 32; k < eb; k += 32) relax(arc_dst[k], db + arc_w[k]);
+            auto run_q = [&]() {
+                int32_t bq[Q], eq[Q], xq[Q];
+                double dq[Q], wq[Q];
+#pragma unroll
+                for (int j = 0; j < Q; j++) {
+                    const int32_t v = upper ? q[2 * j + 1] : q[2 * j];
+                    bq[j] = 0; eq[j] = 0; dq[j] = 0.0;
+                    if (v >= 0) { arc_range(v, bq[j], eq[j]); dq[j] = u2d(dist[v]); }
+                }
+#pragma unroll
+                for (int j = 0; j < Q; j++) {
+                    const int32_t k = bq[j] + hl;
+                    xq[j] = -1; wq[j] = 0.0;
+                    if (k < eq[j]) { xq[j] = arc_dst[k]; wq[j] = arc_w[k]; }
+                }
+#pragma unroll
+                for (int j = 0; j < Q; j++)
+                    if (xq[j] >= 0) relax(xq[j], dq[j] + wq[j]);
+#pragma unroll
+                for (int j = 0; j < Q; j++)
+                    for (int32_t k = bq[j] + hl + 32; k < eq[j]; k += 32) relax(arc_dst[k], dq[j] + arc_w[k]);
+            };
+            auto push = [&](int32_t fv) {
+#pragma unroll
+                for (int j = 0; j < 2 * Q - 1; j++) q[j] = q[j + 1];
+                q[2 * Q - 1] = fv;
             };
             for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
                 const int32_t v = c0 + lane;
@@ -178,16 +195,16 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                 while (mask) {
                     const int32_t fv = c0 + __ffsll((unsigned long long)mask) - 1;
                     mask &= mask - 1;
-                    q0 = q1; q1 = q2; q2 = q3; q3 = fv;
-                    if (++nq == 4) {
-                        run4();
+                    push(fv);
+                    if (++nq == 2 * Q) {
+                        run_q();
                         nq = 0;
                     }
                 }
             }
             if (nq) {
-                while (nq < 4) { q0 = q1; q1 = q2; q2 = q3; q3 = -1; nq++; }
-                run4();
+                while (nq < 2 * Q) { push(-1); nq++; }
+                run_q();
             }
         } else
         for (int32_t c0 = wv * 64; c0 < V; c0 += BLOCK) {
@@ -1048,7 +1065,7 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
     const shd_csr& c = pcsr.view;
     const int32_t na = c.arc_off[V];
     // the row kernel may keep the arc offsets in LDS (16 bits within a 64-vertex chunk)
-    pc->lds_off_ok = !getenv("SHD_PC_NO_LDS_OFF");
+    pc->lds_off_ok = getenv("SHD_PC_LDS_OFF") != nullptr;   // opt-in: neutral to slower
     for (int32_t v0 = 0; v0 < V && pc->lds_off_ok; v0 += 64)
         if (c.arc_off[std::min(V, v0 + 64)] - c.arc_off[v0] >= 65536) pc->lds_off_ok = false;
     // per forward arc: its tail vertex and the index of the same arc among its

@@ -65,7 +65,38 @@ def group_rollback(parts):
     return dict(rerun=rerun, protected=prot, rounds=rounds)
 
 
-SCENARIOS = {"engine_rollback": engine_rollback, "group_rollback": group_rollback}
+def engine_replay(steps):
+    """SHD_FORCE_AMBIG with SHD_NO_PROTECT: no round runs behind a copy of its
+    own, so every round that logs an undecided first-touch send is an
+    ambiguous unprotected round; each is recovered by replaying from the last
+    restore point (shd_eng_run_until) and must leave the run the oracle's.
+    steps > 1: the run is split into that many run_until calls."""
+    import oracle_ffi as O
+    import workloads as W
+    import shdgpu as S
+    from sim import Engine, PathCache, sort_trace
+    g = W.geometric_graph(200, seed=4)
+    m = W.phold_model(W.hosts_on_vertices(200, 2), end_time=3 * S.SHD_SEC, trace=True)
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    eng = Engine(m, pc)
+    end = m.params["end_time"]
+    tot = dict(replayed=0, rerun=0, protected=0, rounds=0, pkt=0, events=0)
+    for k in range(1, steps + 1):
+        st = eng.run_until(end * k // steps)
+        tot["replayed"] += st.n_rounds_replayed
+        tot["rerun"] += st.n_rounds_rerun
+        tot["protected"] += st.n_rounds_protected
+        tot["rounds"] += st.n_rounds
+        tot["pkt"] += st.n_pkt_events
+        tot["events"] += st.n_events
+    otr, odg, ost = O.engine_run(m, g)
+    assert tot["events"] == ost["n_events"] and tot["pkt"] == ost["n_pkt_events"], (tot, ost)
+    assert np.array_equal(sort_trace(eng.trace()), sort_trace(otr))
+    assert np.array_equal(eng.digest(), odg)
+    return tot
+
+
+SCENARIOS = {"engine_rollback": engine_rollback, "group_rollback": group_rollback, "engine_replay": engine_replay}
 
 
 def main():

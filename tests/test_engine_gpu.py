@@ -56,7 +56,7 @@ def test_geometric_one_host_per_vertex(queue_flags, closed, monkeypatch):
     assert np.count_nonzero(gpu[0]["kind"] == S.TR_INET_DROP) > 0  # reliability drops
 
 
-def run_hooked(scenario, arg, timeout=300):
+def run_hooked(scenario, arg, timeout=300, **env_over):
     """A scenario of tests/hook_worker.py in a child process on the test build
     (libshdgpu_th.so: the semantics-changing hooks exist only there), with
     SHD_FORCE_AMBIG and SHD_PROTECT_ALL set; the child checks the run against
@@ -68,6 +68,11 @@ def run_hooked(scenario, arg, timeout=300):
     here = os.path.dirname(os.path.abspath(__file__))
     env = dict(os.environ, SHD_FORCE_AMBIG="1", SHD_PROTECT_ALL="1",
                SHDGPU_LIB=os.path.join(os.path.dirname(here), "shadow-1_amd", "libshdgpu_th.so"))
+    for k, v in env_over.items():
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
     p = subprocess.run([sys.executable, "-u", os.path.join(here, "hook_worker.py"), scenario, str(arg)],
                        env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=timeout)
     out = p.stdout.decode(errors="replace")
@@ -83,6 +88,17 @@ def test_ambiguous_first_touch_rounds_roll_back(hpv):
     # run must still be the serial oracle's, bit for bit (checked in the child)
     st = run_hooked("engine_rollback", hpv)
     assert st["rerun"] > 0 and st["protected"] == st["rounds"]
+
+
+@pytest.mark.parametrize("steps", [1, 3])
+def test_ambiguous_unprotected_rounds_replay(steps):
+    # protection off (SHD_NO_PROTECT) with every undecided first-touch send
+    # forced ambiguous: an unprotected batch round that logs one cannot be
+    # kept, so shd_eng_run_until goes back to its last restore point, runs to
+    # the round's start again and runs the round protected; the run is the
+    # serial oracle's, bit for bit (checked in the child)
+    st = run_hooked("engine_replay", steps, SHD_PROTECT_ALL=None, SHD_NO_PROTECT="1")
+    assert st["replayed"] > 0 and st["rerun"] > 0 and st["protected"] < st["rounds"], st
 
 
 def test_product_library_ignores_the_test_hooks(monkeypatch):
