@@ -566,16 +566,23 @@ def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, t
 
 def pmc_traffic(workload, kernel):
     """HBM bytes per round of the round kernel from the committed rocprofv3
-    PMC passes of THIS workload and kernel (profiles/r04/pmc_traffic.json,
+    PMC passes of THIS workload and kernel (profiles/r05 or r04/pmc_traffic.json,
     scripts/pmc_traffic.py: FETCH_SIZE x the calibrated read correction +
     WRITE_SIZE, over the timed region's dispatches), used only when they were
     taken of the engine source being run; else None (no inherited numbers)."""
     try:
         import shdgpu as S
-        prof = json.load(open(os.path.join(REPO, "profiles", "r04", "pmc_traffic.json")))
         sha = S.engine_source_sha1()
     except (OSError, ValueError):
         return None
+    prof = {}
+    for rnd in ("r05", "r04"):   # the newest round's passes of this source
+        try:
+            prof = json.load(open(os.path.join(REPO, "profiles", rnd, "pmc_traffic.json")))
+        except (OSError, ValueError):
+            continue
+        if prof.get("engine_source_sha1") == sha:
+            break
     if prof.get("engine_source_sha1") != sha:
         return None
     ent = prof.get("entries", {}).get(workload + "/" + kernel)

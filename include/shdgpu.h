@@ -298,10 +298,46 @@ typedef struct shd_model {
      *                     first sendto binds it: one random port). */
     uint32_t app;                   /* SHD_APP_*                               */
     int32_t _pad2;
-    const int32_t* app_peer;        /* [H] (SHD_APP_UDP_ECHO) or NULL          */
+    const int32_t* app_peer;        /* [H] (SHD_APP_UDP_ECHO; SHD_APP_UDP's SHD_DEST_PEER
+                                       hosts: the host sent to) or NULL          */
+    /*   SHD_APP_UDP       a datagram application per host: host h runs
+     *                     app_spec[host_app[h]] (shd_udp_app below); PHOLD is
+     *                     {SHD_SEND_EACH, SHD_DEST_WEIGHTED, load, 1}, the echo's
+     *                     server {SHD_SEND_LISTENER, SHD_DEST_REPLY, 0, 1} and
+     *                     client {SHD_SEND_ONCE, SHD_DEST_PEER, load, 1}. */
+    const struct shd_udp_app* app_spec;   /* [n_app_specs] (SHD_APP_UDP) or NULL */
+    const uint8_t* host_app;        /* [H] (SHD_APP_UDP) or NULL               */
+    uint32_t n_app_specs;           /* <= 256                                  */
+    uint32_t _pad3;
 } shd_model;
 
-enum { SHD_APP_PHOLD = 0, SHD_APP_UDP_ECHO = 1 };
+enum { SHD_APP_PHOLD = 0, SHD_APP_UDP_ECHO = 1, SHD_APP_UDP = 2 };
+
+/* SHD_APP_UDP: what a host's process does at its start and with each datagram
+ * it reads, over the calls test_phold.c makes (socket, bind, sendto, recvfrom,
+ * close; udp.c:75-142).  Every datagram carries the model's `payload` bytes.
+ *   send  SHD_SEND_EACH      listen on PHOLD's port; each datagram from a new
+ *                            socket (an implicit bind: one port draw each,
+ *                            host.c:1514-1525), closed after the sendto;
+ *         SHD_SEND_LISTENER  listen on PHOLD's port and send from that socket;
+ *         SHD_SEND_ONCE      no listener: one socket, bound by its first sendto
+ *                            (one port draw); replies are read on it.
+ *   dest  SHD_DEST_WEIGHTED  _phold_chooseNode over the host's dest_cum row (no
+ *                            host drawn: nothing sent), to PHOLD's port;
+ *         SHD_DEST_PEER      app_peer[h], to PHOLD's port;
+ *         SHD_DEST_REPLY     the source address and port of the datagram just
+ *                            read (n_start must be 0).
+ *   n_start   datagrams sent when the process starts;
+ *   per_read  1: one datagram per datagram read (PHOLD's rule); 0: read only.
+ * shd_eng_create refuses (SHD_EINVAL) a model whose datagrams could reach a
+ * port no socket listens on: a weighted or peer destination that does not
+ * listen (SHD_SEND_ONCE), a replying host that an SHD_SEND_EACH host can send
+ * to, or SHD_SEND_EACH with SHD_DEST_REPLY. */
+typedef struct shd_udp_app {
+    uint32_t send, dest, n_start, per_read;
+} shd_udp_app;
+enum { SHD_SEND_EACH = 0, SHD_SEND_ONCE = 1, SHD_SEND_LISTENER = 2 };
+enum { SHD_DEST_WEIGHTED = 0, SHD_DEST_PEER = 1, SHD_DEST_REPLY = 2 };
 
 /* queue_flags: SHD_QF_NO_CALENDAR routes every inter-host event through the
  * per-host inbox and heap (the calendar's fallback path), for testing */

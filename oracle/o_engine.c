@@ -83,8 +83,9 @@ typedef struct {
      * in (_networkinterface_receivePacket) and out (_networkinterface_sendPackets);
      * cumulative here, differenced per heartbeat by the reader */
     uint32_t if_in, if_out;
-    /* SHD_APP_UDP_ECHO: the sources of the datagrams the socket holds, in
-     * arrival order (recvfrom's address); a client's implicitly bound port */
+    /* a replying host (SHD_DEST_REPLY): the sources of the datagrams its
+     * socket holds, in arrival order (recvfrom's address); an SHD_SEND_ONCE
+     * host's implicitly bound port */
     uint32_t* rxq; uint32_t rxq_head, rxq_count, rxq_cap;
     int bound; uint16_t port;
 } ohost;
@@ -190,6 +191,24 @@ static void refill_if_needed(ctx_t* c, uint32_t h) {
 }
 static inline void consume(uint64_t* rem, uint64_t n) { *rem = (n >= *rem) ? 0 : *rem - n; }
 
+/* the datagram application host h runs (shdgpu.h shd_udp_app): PHOLD's
+ * (test_phold.c), the UDP echo's server or client (ref_loop.c app 2), or the
+ * model's own per-host spec (SHD_APP_UDP, ref_loop.c app 3); *peer: the
+ * SHD_DEST_PEER host */
+static shd_udp_app app_of(const ctx_t* c, uint32_t h, int32_t* peer) {
+    shd_udp_app a = {SHD_SEND_EACH, SHD_DEST_WEIGHTED, c->m->load, 1};
+    *peer = -1;
+    if (c->m->app == SHD_APP_UDP_ECHO) {
+        *peer = c->m->app_peer[h];
+        if (*peer < 0) a = (shd_udp_app){SHD_SEND_LISTENER, SHD_DEST_REPLY, 0, 1};
+        else a = (shd_udp_app){SHD_SEND_ONCE, SHD_DEST_PEER, c->m->load, 1};
+    } else if (c->m->app == SHD_APP_UDP) {
+        a = c->m->app_spec[c->m->host_app[h]];
+        if (a.dest == SHD_DEST_PEER) *peer = c->m->app_peer[h];
+    }
+    return a;
+}
+
 /* _networkinterface_receivePacket (network_interface.c:375-419): hand the
  * datagram to the bound UDP socket (PHOLD listener on 8998) or drop it */
 static void if_receive_packet(ctx_t* c, uint32_t h, uint32_t src, uint32_t pkt) {
@@ -199,7 +218,8 @@ static void if_receive_packet(ctx_t* c, uint32_t h, uint32_t src, uint32_t pkt) 
         trace(c, c->now, 0, h, src, pkt, SHD_TR_RECV);
         H->n_recv++;
         H->unread++;
-        if (c->m->app == SHD_APP_UDP_ECHO) {   /* the socket keeps the datagram's source */
+        int32_t pr;
+        if (app_of(c, h, &pr).dest == SHD_DEST_REPLY) {   /* the socket keeps the datagram's source */
             if (H->rxq_count == H->rxq_cap) {
                 uint32_t ncap = H->rxq_cap ? 2 * H->rxq_cap : 16;
                 uint32_t* nq = malloc(sizeof(uint32_t) * ncap);
@@ -403,49 +423,41 @@ static uint16_t random_free_port(ohost* H) {
     return 0;
 }
 
-/* _phold_sendNewMessage (test_phold.c:218-230): chooseNode with random()
- * (process_emu_random -> host RNG, process.c:4790-4795), then socket +
- * sendto (implicit bind: one random port, host.c:1514-1525), UDP packet,
- * networkinterface_wantsSend -> sendPackets */
-static void send_new_message(ctx_t* c, uint32_t h) {
+/* one datagram of host h's application (app_of), `payload` bytes:
+ *   the destination: SHD_DEST_WEIGHTED _phold_sendNewMessage's chooseNode
+ *     (test_phold.c:160-178, 218-230) with random() (process_emu_random -> host
+ *     RNG, process.c:4790-4795) over the host's own weights (each process reads
+ *     its weights file, test_phold.c:341-356), no host drawn: nothing sent;
+ *     SHD_DEST_PEER the peer; SHD_DEST_REPLY `src`, the datagram just read;
+ *   the source port: SHD_SEND_EACH a new socket whose sendto binds it
+ *     implicitly (one random port, host.c:1514-1525), closed after;
+ *     SHD_SEND_ONCE the host's one socket, bound by its first sendto;
+ *     SHD_SEND_LISTENER the listener (PHOLD's port, no draw);
+ * then the UDP packet, networkinterface_wantsSend -> sendPackets */
+static void app_send(ctx_t* c, uint32_t h, const shd_udp_app* a, int32_t peer, uint32_t src) {
     ohost* H = &c->hosts[h];
-    double r = ((double)o_rand_r(&H->rng)) / RAND_MAX_D;
-    /* first i with cumulative >= r (test_phold.c:165-176), over this host's
-     * own weights (each process reads its weights file, test_phold.c:341-356) */
-    const double* cum = c->m->dest_cum;
-    if (c->m->host_class && c->m->n_classes > 1)
-        cum += (size_t)c->m->host_class[h] * (size_t)c->m->n_hosts;
-    int32_t lo = 0, hi = c->m->n_hosts;   /* search [lo,hi) */
-    while (lo < hi) { int32_t mid = lo + (hi - lo) / 2; if (cum[mid] >= r) hi = mid; else lo = mid + 1; }
-    if (lo >= c->m->n_hosts) return;      /* NULL node: nothing sent */
-    uint32_t dst = (uint32_t)lo;
-    const uint16_t port = random_free_port(H);
-    uint32_t pkt = H->pkt_seq++;
-    /* packet_new + PDS_SND_CREATED (udp.c:116), PDS_SND_SOCKET_BUFFERED (socket.c:405) */
-    if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, port, h, ~0u, pkt, SHD_TR_CREATED);
-    if (H->txq_count == H->txq_cap) {
-        uint32_t ncap = H->txq_cap * 2;
-        txent* nq = malloc(sizeof(txent) * ncap);
-        for (uint32_t i = 0; i < H->txq_count; i++) nq[i] = H->txq[(H->txq_head + i) % H->txq_cap];
-        free(H->txq); H->txq = nq; H->txq_cap = ncap; H->txq_head = 0;
+    uint32_t dst;
+    if (a->dest == SHD_DEST_WEIGHTED) {
+        double r = ((double)o_rand_r(&H->rng)) / RAND_MAX_D;
+        const double* cum = c->m->dest_cum;
+        if (c->m->host_class && c->m->n_classes > 1)
+            cum += (size_t)c->m->host_class[h] * (size_t)c->m->n_hosts;
+        int32_t lo = 0, hi = c->m->n_hosts;   /* first i with cumulative >= r, in [lo,hi) */
+        while (lo < hi) { int32_t mid = lo + (hi - lo) / 2; if (cum[mid] >= r) hi = mid; else lo = mid + 1; }
+        if (lo >= c->m->n_hosts) return;      /* NULL node: nothing sent */
+        dst = (uint32_t)lo;
+    } else {
+        dst = a->dest == SHD_DEST_REPLY ? src : (uint32_t)peer;
     }
-    H->txq[(H->txq_head + H->txq_count) % H->txq_cap] = (txent){dst, pkt};
-    H->txq_count++;
-    if_send_packets(c, h);
-}
-
-/* SHD_APP_UDP_ECHO (ref_loop.c app 2): one datagram of `payload` bytes to
- * dst from the host's one socket -- a server's bound listener (PHOLD's port,
- * no draw), a client's socket, bound by its first sendto (one random port,
- * host.c:1514-1525); then as send_new_message */
-static void echo_send(ctx_t* c, uint32_t h, uint32_t dst) {
-    ohost* H = &c->hosts[h];
     uint16_t port = SHD_PHOLD_LISTEN_PORT;
-    if (c->m->app_peer[h] >= 0) {
+    if (a->send == SHD_SEND_EACH) {
+        port = random_free_port(H);
+    } else if (a->send == SHD_SEND_ONCE) {
         if (!H->bound) { H->port = random_free_port(H); H->bound = 1; }
         port = H->port;
     }
     uint32_t pkt = H->pkt_seq++;
+    /* packet_new + PDS_SND_CREATED (udp.c:116), PDS_SND_SOCKET_BUFFERED (socket.c:405) */
     if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, port, h, ~0u, pkt, SHD_TR_CREATED);
     if (H->txq_count == H->txq_cap) {
         uint32_t ncap = H->txq_cap * 2;
@@ -501,15 +513,13 @@ static void execute(ctx_t* c, const shd_event* e) {
     case SHD_EV_REFILL_LO:
         /* loopback interface: buckets reach capacity, nothing to send or receive */
         break;
-    case SHD_EV_APP_START:
+    case SHD_EV_APP_START: {
         H->listening = 1;
-        if (c->m->app == SHD_APP_UDP_ECHO) {   /* a client sends `load` requests; a server waits */
-            if (c->m->app_peer[h] >= 0)
-                for (uint32_t i = 0; i < c->m->load; i++) echo_send(c, h, (uint32_t)c->m->app_peer[h]);
-            break;
-        }
-        for (uint32_t i = 0; i < c->m->load; i++) send_new_message(c, h);
+        int32_t peer;
+        const shd_udp_app a = app_of(c, h, &peer);
+        for (uint32_t i = 0; i < a.n_start; i++) app_send(c, h, &a, peer, 0);   /* _phold_bootstrapMessages */
         break;
+    }
     case SHD_EV_PACKET: {
         /* _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122) */
         H->n_pkt_events++;
@@ -528,16 +538,17 @@ static void execute(ctx_t* c, const shd_event* e) {
         H->unread = 0;
         /* _phold_wait_and_process_events (test_phold.c:287-315): each recvfrom
          * (PDS_RCV_SOCKET_DELIVERED, udp.c:158) answered by one new message */
+        int32_t peer;
+        const shd_udp_app a = app_of(c, h, &peer);
         for (uint32_t i = 0; i < n; i++) {
             if (c->m->queue_flags & SHD_QF_TRACE_STATUS) trace(c, c->now, 0, h, ~0u, ~0u, SHD_TR_READ);
-            if (c->m->app == SHD_APP_UDP_ECHO) {   /* the reply to the sender, or the next request */
-                const uint32_t src = H->rxq[H->rxq_head];
+            uint32_t src = 0;
+            if (a.dest == SHD_DEST_REPLY) {   /* recvfrom's address: the datagram's source */
+                src = H->rxq[H->rxq_head];
                 H->rxq_head = (H->rxq_head + 1) % H->rxq_cap;
                 H->rxq_count--;
-                echo_send(c, h, c->m->app_peer[h] < 0 ? src : (uint32_t)c->m->app_peer[h]);
-            } else {
-                send_new_message(c, h);
             }
+            if (a.per_read) app_send(c, h, &a, peer, src);
         }
         break;
     }

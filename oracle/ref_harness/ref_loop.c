@@ -79,7 +79,8 @@ typedef int (*ref_path_fn)(void* ctx, int32_t src_vertex, int32_t dst_vertex, do
 
 typedef struct ref_loop_cfg {
     int32_t n_hosts;
-    int32_t app;                  /* 0 = PHOLD-UDP (test_phold.c), 1 = TCP echo, 2 = UDP echo */
+    int32_t app;                  /* 0 = PHOLD-UDP (test_phold.c), 1 = TCP echo, 2 = UDP echo,
+                                     3 = a datagram application per host (app_spec below) */
     const uint32_t* host_seed;    /* [H] host RNG state after attach (the model's host_rng) */
     const int32_t* host_vertex;   /* [H] */
     const uint64_t* bw_down_kibps, *bw_up_kibps;   /* [H] */
@@ -110,6 +111,11 @@ typedef struct ref_loop_cfg {
     /* wall-clock marks (bench.py's reference CPU baseline): the monotonic clock
      * at the first path lookup (a send) at simulated time >= mark_time[k]; 0 = off */
     uint64_t mark_time[2];
+    /* app 3 (shdgpu.h shd_udp_app): host h runs app_spec[4 * host_app[h] ..]
+     * = {send, dest, n_start, per_read}; app_peer[h]: its SHD_DEST_PEER host */
+    const uint32_t* app_spec;
+    const uint8_t* host_app;
+    const int32_t* app_peer;
 } ref_loop_cfg;
 
 typedef struct ref_loop_out {
@@ -448,6 +454,96 @@ static void echo_continue(Process* proc) {
     }
 }
 
+/* ---- app 3: a datagram application per host (shdgpu.h shd_udp_app, the
+ * device application hook's general form) over the same host_* calls as
+ * test_phold.c.  send: 0 (EACH) listen on PHOLD's port, each datagram from a
+ * new socket (socket, sendto -- its implicit bind draws a port --, close), as
+ * _phold_sendToNode; 1 (ONCE) no listener, one socket whose first sendto binds
+ * it, replies read on it; 2 (LISTENER) listen on PHOLD's port and send from it.
+ * dest: 0 (WEIGHTED) _phold_chooseNode over the host's weights row, to PHOLD's
+ * port (none drawn: nothing sent); 1 (PEER) app_peer[h]'s PHOLD port; 2 (REPLY)
+ * the address and port recvfrom gave.  n_start datagrams when the process
+ * starts; per_read: one datagram per datagram read, else none. */
+static const uint32_t* udp_spec(int32_t h) { return g_cfg->app_spec + 4u * g_cfg->host_app[h]; }
+
+static void udp_send(Process* proc, in_addr_t rip, in_port_t rport) {
+    Host* host = proc->host;
+    const int32_t h = host_index_of(host_getID(host));
+    const uint32_t* a = udp_spec(h);
+    in_addr_t ip;
+    in_port_t port = htons(PHOLD_LISTEN_PORT);
+    if (a[1] == 0) {
+        const double r = ((double)random_rand(host_getRandom(host))) / ((double)RAND_MAX);
+        const double* cum = g_cfg->dest_cum;
+        if (g_cfg->host_class && g_cfg->n_classes > 1) cum += (size_t)g_cfg->host_class[h] * (size_t)g_cfg->n_hosts;
+        int32_t chosen = -1;
+        for (int32_t i = 0; i < g_cfg->n_hosts; i++)
+            if (cum[i] >= r) { chosen = i; break; }
+        if (chosen < 0) return;
+        ip = host_getDefaultIP(g_hosts[chosen]);
+    } else if (a[1] == 1) {
+        ip = host_getDefaultIP(g_hosts[g_cfg->app_peer[h]]);
+    } else {
+        ip = rip;
+        port = rport;
+    }
+    gsize bytes = 0;
+    const gsize n = g_cfg->payload ? g_cfg->payload : 1;
+    if (a[0] == 0) {
+        gint fd = host_createDescriptor(host, DT_UDPSOCKET);
+        Descriptor* desc = host_lookupDescriptor(host, fd);
+        descriptor_setFlags(desc, descriptor_getFlags(desc) | O_NONBLOCK);
+        (void)host_sendUserData(host, fd, (gpointer)g_echo_buf, n, ip, (in_addr_t)port, &bytes);
+        (void)host_closeUser(host, fd);
+    } else {
+        (void)host_sendUserData(host, proc->listenfd, (gpointer)g_echo_buf, n, ip, (in_addr_t)port, &bytes);
+    }
+}
+
+static void udp_start(Process* proc) {
+    Host* host = proc->host;
+    const uint32_t* a = udp_spec(host_index_of(host_getID(host)));
+    proc->listenfd = host_createDescriptor(host, DT_UDPSOCKET);
+    Descriptor* desc = host_lookupDescriptor(host, proc->listenfd);
+    descriptor_setFlags(desc, descriptor_getFlags(desc) | O_NONBLOCK);
+    if (a[0] != 1) {
+        struct sockaddr_in bindAddr;
+        memset(&bindAddr, 0, sizeof(bindAddr));
+        bindAddr.sin_family = AF_INET;
+        bindAddr.sin_addr.s_addr = htonl(INADDR_ANY);
+        bindAddr.sin_port = htons(PHOLD_LISTEN_PORT);
+        (void)host_bindToInterface(host, proc->listenfd, (struct sockaddr*)&bindAddr);
+    }
+    proc->epollfd = host_createDescriptor(host, DT_EPOLL);
+    struct epoll_event ev;
+    memset(&ev, 0, sizeof(ev));
+    ev.events = EPOLLIN;
+    ev.data.fd = proc->listenfd;
+    (void)host_epollControl(host, proc->epollfd, EPOLL_CTL_ADD, proc->listenfd, &ev);
+    for (uint32_t i = 0; i < a[2]; i++) udp_send(proc, 0, 0);
+}
+
+static void udp_continue(Process* proc) {
+    Host* host = proc->host;
+    const uint32_t* a = udp_spec(host_index_of(host_getID(host)));
+    for (;;) {
+        struct epoll_event evs[10];
+        gint nfds = 0;
+        if (host_epollGetEvents(host, proc->epollfd, evs, 10, &nfds) != 0 || nfds <= 0) break;
+        for (gint i = 0; i < nfds; i++) {
+            for (;;) {
+                gchar buffer[65536];
+                in_addr_t ip = 0;
+                in_port_t port = 0;
+                gsize nBytes = 0;
+                gint rc = host_receiveUserData(host, proc->listenfd, buffer, sizeof(buffer), &ip, &port, &nBytes);
+                if (rc != 0 || nBytes == 0) break;
+                if (a[3]) udp_send(proc, ip, port);
+            }
+        }
+    }
+}
+
 /* ---- app 1: src/test/tcp/test_tcp.c's echo test in its nonblocking-epoll
  * mode (_run_server / _run_client, test_tcp.c:713-810), restated over the
  * host_* calls the syscall handlers make.  The client fills its buffer with
@@ -609,6 +705,7 @@ static void process_start_task(Process* proc, gpointer nothing) {
     if (g_cfg->app == 0) phold_start(proc);
     else if (g_cfg->app == 1) tcp_start(proc);
     else if (g_cfg->app == 2) echo_start(proc);
+    else if (g_cfg->app == 3) udp_start(proc);
     worker_setActiveProcess(NULL);
 }
 static void process_stop_task(Process* proc, gpointer nothing) { process_stop(proc); }
@@ -638,6 +735,7 @@ void process_continue(Process* proc) {
     if (g_cfg->app == 0) phold_continue(proc);
     else if (g_cfg->app == 1) tcp_continue(proc);
     else if (g_cfg->app == 2) echo_continue(proc);
+    else if (g_cfg->app == 3) udp_continue(proc);
     worker_setActiveProcess(NULL);
 }
 

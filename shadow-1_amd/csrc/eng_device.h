@@ -8,7 +8,13 @@
 
 constexpr uint64_t kInf = 0xFFFFFFFFFFFFFFFFull;
 constexpr uint32_t F_REFILL_PENDING = 1u, F_NOTIFY_PENDING = 2u, F_LISTENING = 4u, F_CODEL_DROP_MODE = 8u,
-                   F_BOUND = 16u;   // a UDP echo client's socket is bound (its first sendto drew the port)
+                   F_BOUND = 16u;   // an SHD_SEND_ONCE socket is bound (its first sendto drew the port)
+// the host's datagram application (F_APP: not PHOLD), in the flags word from
+// boot on: bits 8-9 shd_udp_app::send, 10-11 dest, 12 per_read
+constexpr uint32_t kAppShift = 8u;
+__device__ __forceinline__ uint32_t app_send(uint32_t flags) { return (flags >> kAppShift) & 3u; }
+__device__ __forceinline__ uint32_t app_dest(uint32_t flags) { return (flags >> (kAppShift + 2)) & 3u; }
+__device__ __forceinline__ bool app_per_read(uint32_t flags) { return ((flags >> (kAppShift + 4)) & 1u) != 0; }
 // a send's destination draw (TxEnt::r, SendRec::r): a rand_r value (PHOLD's
 // destination pick, resolved at the flush), or a host named by the
 // application (the UDP echo's server or the sender being answered)
@@ -83,8 +89,8 @@ struct alignas(128) HostRec {
     uint16_t cq_head, cq_count, tq_head, tq_count;   // FIFO heads / lengths
     uint32_t evq_n;
     uint32_t if_in, if_out;                // tracker node counters: interface packets in / out (cumulative)
-    uint16_t rq_head;                      // UDP echo: the head of the socket's source ring (its length is unread)
-    uint16_t port;                         // UDP echo client: its socket's port (F_BOUND)
+    uint16_t rq_head;                      // SHD_DEST_REPLY: the head of the socket's source ring (its length is unread)
+    uint16_t port;                         // SHD_SEND_ONCE: its socket's port (F_BOUND)
 };
 static_assert(sizeof(HostRec) == 128, "host record: one 128-B line, 8 x 16 B");
 
@@ -172,7 +178,7 @@ static_assert(sizeof(DestGuide) == 48, "guide entry: three 16-B loads");
 constexpr int kDestExc = 16;   // closed-form destination exceptions (ParamsT::exc_x)
 // ParamsT::feat: the model's optional features (all off on the bench's models)
 constexpr uint32_t F_TRACE = 1u, F_HB = 2u, F_PCOUNT = 4u, F_HOSTHB = 8u, F_AMBIG = 16u, F_STATUS = 64u,
-                   F_ECHO = 128u;   // the application is SHD_APP_UDP_ECHO
+                   F_APP = 128u;    // the application is not PHOLD: per-host modes (app_send / app_dest)
 
 template <template <class> class Ptr>
 struct ParamsT {
@@ -219,11 +225,16 @@ struct ParamsT {
     // are self_thr[h].x <= x <= self_thr[h].y (precomputed, exact); .w = class
     Ptr<const int4> self_thr;
     Ptr<const uint64_t> host_hb;     // per-host heartbeat interval [H] (null: `heartbeat`)
-    // the application (shd_model::app): SHD_APP_PHOLD, or SHD_APP_UDP_ECHO with
-    // app_peer[h] = -1 (server) | the server host, and per host a ring of the
-    // sources of the datagrams its socket holds ([nloc][rq_cap], recvfrom's address)
+    // the application (shd_model::app): SHD_APP_PHOLD, or a datagram
+    // application per host (SHD_APP_UDP_ECHO / SHD_APP_UDP): app_mode[h]
+    // (send | dest << 2 | per_read << 4, copied into the flags word at boot),
+    // app_nstart[h] its start datagrams, app_peer[h] its SHD_DEST_PEER host; a
+    // replying host keeps a ring of the sources of the datagrams its socket
+    // holds ([nloc][rq_cap], recvfrom's address)
     uint32_t app, rq_cap;
     Ptr<const int32_t> app_peer;
+    Ptr<const uint8_t> app_mode;
+    Ptr<const uint32_t> app_nstart;
     Ptr<uint32_t> rq;
     int32_t no_app_start;            // SHD_QF_NO_APP_START: boot schedules no application start
     // closed-form destinations (dest_closed): even weights, host h attached
@@ -791,7 +802,7 @@ __device__ void if_receive_packet(const DParams& P, HostCtx& c, uint32_t src, ui
         trace(P, c, c.now, 0, c.h, src, pkt, SHD_TR_RECV);
         c.c_recv++;
         c.unread++;
-        if (c.k.feat & F_ECHO) rq_push(P, c, src);
+        if ((c.k.feat & F_APP) && app_dest(c.flags) == SHD_DEST_REPLY) rq_push(P, c, src);
         if (!(c.flags & F_NOTIFY_PENDING)) {   // epoll.c:345-365, +1 ns
             schedule_self(P, c, SHD_EV_NOTIFY, 1, 0);
             c.flags |= F_NOTIFY_PENDING;
@@ -1365,26 +1376,42 @@ __device__ __forceinline__ void app_read(const DParams& P, HostCtx& c) {
 //   PHOLD (_phold_sendNewMessage, test_phold.c:218-230): the destination draw,
 //     resolved at the flush (no destination: nothing sent), the implicit
 //     bind's port draw, SND_CREATED;
-//   UDP echo (oracle/ref_harness/ref_loop.c app 2): the datagram read leaves
-//     the socket (its source: the ring); a server answers that source from
-//     its bound listener, a client asks its server again from its one socket,
-//     bound by its first sendto (one port draw, host.c:1514-1525).
+//   a datagram application (F_APP: SHD_APP_UDP, SHD_APP_UDP_ECHO, shdgpu.h
+//     shd_udp_app; oracle/ref_harness/ref_loop.c apps 2 and 3): a replying
+//     host takes the read datagram's source off its ring; a read-only host
+//     sends nothing for it; the destination is the weighted draw (as PHOLD's),
+//     the peer or that source; the source port is a new socket's (a port draw
+//     per datagram), the one socket's (bound by its first sendto: one draw,
+//     host.c:1514-1525) or the listener's.
 __device__ __forceinline__ bool app_message(const DParams& P, HostCtx& c, bool reading, uint32_t& rv,
                                             uint32_t& pkt) {
-    if (!(c.k.feat & F_ECHO)) {
+    if (!(c.k.feat & F_APP)) {
         rv = (uint32_t)rand_r_dev(c.rng);
         if ((int32_t)rv > c.dst_thr) return false;   // no i with dest_cum[i] >= r
         bind_and_create(P, c, c.pkt_seq);
         pkt = c.pkt_seq++;
         return true;
     }
-    uint32_t dst = (uint32_t)c.peer, sport = SHD_PHOLD_LISTEN_PORT;
-    if (reading) {
-        const uint32_t src = P.rq[(size_t)c.l * P.rq_cap + c.rq_head];
+    const uint32_t send = app_send(c.flags), dest = app_dest(c.flags);
+    uint32_t src = 0;
+    if (reading && dest == SHD_DEST_REPLY) {   // the datagram read leaves the socket (its source: the ring)
+        src = P.rq[(size_t)c.l * P.rq_cap + c.rq_head];
         c.rq_head = c.rq_head + 1 == P.rq_cap ? 0u : c.rq_head + 1;
-        if (c.peer < 0) dst = src;
     }
-    if (c.peer >= 0) {
+    if (reading && !app_per_read(c.flags)) return false;
+    if (dest == SHD_DEST_WEIGHTED) {
+        rv = (uint32_t)rand_r_dev(c.rng);
+        if ((int32_t)rv > c.dst_thr) return false;
+    } else {
+        rv = (dest == SHD_DEST_REPLY ? src : (uint32_t)c.peer) | kDstHost;
+    }
+    if (send == SHD_SEND_EACH) {
+        bind_and_create(P, c, c.pkt_seq);
+        pkt = c.pkt_seq++;
+        return true;
+    }
+    uint32_t sport = SHD_PHOLD_LISTEN_PORT;
+    if (send == SHD_SEND_ONCE) {
         if (!(c.flags & F_BOUND)) {
             c.port = random_free_port_value(c);
             c.flags |= F_BOUND;
@@ -1392,7 +1419,6 @@ __device__ __forceinline__ bool app_message(const DParams& P, HostCtx& c, bool r
         sport = c.port;
     }
     if (c.k.feat & F_STATUS) trace(P, c, c.now, sport, c.h, ~0u, c.pkt_seq, SHD_TR_CREATED);
-    rv = dst | kDstHost;
     pkt = c.pkt_seq++;
     return true;
 }
@@ -1507,7 +1533,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         c.c_recv++;
         c.if_in++;
         c.unread++;
-        if (c.k.feat & F_ECHO) rq_push(P, c, e.src);
+        if ((c.k.feat & F_APP) && app_dest(c.flags) == SHD_DEST_REPLY) rq_push(P, c, e.src);
         c.cq_head = (c.cq_head + 1 == c.k.cq_cap) ? 0 : c.cq_head + 1;
         c.cq_iexp = 0;
         const bool nt = !(c.flags & F_NOTIFY_PENDING);
@@ -1564,7 +1590,7 @@ __device__ void begin_event(const DParams& P, HostCtx& c, const shd_event& e) {
         break;
     case SHD_EV_APP_START:
         c.flags |= F_LISTENING;
-        c.w_msgs = ((c.k.feat & F_ECHO) && c.peer < 0) ? 0u : P.load;   // a UDP echo server waits
+        c.w_msgs = (c.k.feat & F_APP) ? P.app_nstart[c.h] : P.load;   // (a replying host: 0)
         break;
     case SHD_EV_PACKET: {
         // _worker_runDeliverPacketTask -> router_enqueue (router.c:104-122)
@@ -1687,7 +1713,7 @@ __device__ __forceinline__ void load_ctx(const DParams& P, HostCtx& c, int32_t l
     c.tq_head = launder(r.tq_head); c.tq_count = launder(r.tq_count);
     c.if_in = launder(r.if_in); c.if_out = launder(r.if_out);
     c.rq_head = launder((uint32_t)r.rq_head); c.port = launder((uint32_t)r.port);
-    c.peer = (c.k.feat & F_ECHO) ? launder(P.app_peer[P.h0 + l]) : -1;
+    c.peer = (c.k.feat & F_APP) ? launder(P.app_peer[P.h0 + l]) : -1;
     c.evq_n = launder(r.evq_n);
     if (r.evq_n) {
         const shd_event t = P.evq[(size_t)l * P.evq_stride + 3];

@@ -26,7 +26,8 @@ __global__ __launch_bounds__(kBlock) void k_boot(DParams P, const uint32_t* __re
         for (int k = 0; k < 3; k++) { r.tt[k] = kInf; r.ts_back[k] = 0; }
         P.hc[l] = HostCnt{0, 0, 0, 0, 0, 0};
         r.rng = rng0[h]; r.pkt_seq = 0; r.rx_refill = (uint32_t)rxr; r.tx_refill = (uint32_t)txr;
-        r.flags = 0; r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
+        r.flags = P.app_mode ? (uint32_t)P.app_mode[h] << kAppShift : 0u;   // (F_APP: the host's application)
+        r.unread = 0; r.cq_dc = 0; r.cq_dcl = 0; r.cq_head = 0; r.cq_count = 0;
         r.tq_head = 0; r.tq_count = 0; r.evq_n = 0; r.if_in = 0; r.if_out = 0; r.rq_head = 0; r.port = 0;
         P.hs[l] = r;
         P.inbox_n[0][l] = 0; P.inbox_n[1][l] = 0;

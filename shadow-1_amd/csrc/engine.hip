@@ -75,7 +75,9 @@ struct shd_eng {
     bool booted = false;
     bool heartbeats = false;    // SHD_QF_HEARTBEATS: snapshots in P.hb
     std::vector<uint64_t> host_hb;   // <host heartbeatfrequency> per host (empty: P.heartbeat)
-    std::vector<int32_t> app_peer;   // SHD_APP_UDP_ECHO roles (empty: PHOLD)
+    std::vector<int32_t> app_peer_dev;   // per host: the SHD_DEST_PEER host (device copy), else -1
+    std::vector<int32_t> app_peer;   // per host: >= 0 where it reads on the socket it sends from
+                                     // (SHD_SEND_ONCE; the status writer's port rule), empty: PHOLD
     std::vector<void*> allocs;
     std::vector<size_t> alloc_bytes;
     // protected rounds (DESIGN.md "First-touch rule"): device state copied
@@ -113,6 +115,8 @@ struct shd_eng {
     int4* d_self_thr = nullptr;
     uint64_t* d_host_hb = nullptr;
     int32_t* d_app_peer = nullptr;
+    uint8_t* d_app_mode = nullptr;
+    uint32_t* d_app_nstart = nullptr;
     int32_t n_cls = 1;
     uint64_t t_done = 0;                    // end of the last executed round's window (push_events floor)
     int32_t* d_rank = nullptr;
@@ -192,6 +196,108 @@ static int ealloc(shd_eng* e, T** p, size_t n, bool zero = true) {
         if (rc_) { shd_eng_destroy(e); return rc_; } \
     } while (0)
 
+// The datagram application of every host (shd_model::app other than PHOLD),
+// checked so that no datagram can reach a port nobody listens on (the device
+// hands every datagram that reaches a started host to its application):
+// mode[h] = send | dest << 2 | per_read << 4, nstart[h] its start count,
+// peer[h] its SHD_DEST_PEER host (else -1).  *rq_cap: the per-host ring of
+// the sources of unread datagrams (replying hosts only; 0: none), bounded by
+// the datagrams that can be in flight at once.
+static int resolve_apps(const shd_model* m, int32_t n_cls, std::vector<uint8_t>& mode, std::vector<uint32_t>& nstart,
+                        std::vector<int32_t>& peer, uint32_t* rq_cap, uint64_t* max_start) {
+    const int32_t H = m->n_hosts;
+    mode.assign(H, 0);
+    nstart.assign(H, 0);
+    peer.assign(H, -1);
+    *rq_cap = 0;
+    *max_start = 0;
+    if (m->app == SHD_APP_UDP_ECHO) {
+        // the UDP echo's roles: every client's server is a server host; a
+        // socket holds at most the requests in flight to it (its clients' loads)
+        if (!m->app_peer) return SHD_EINVAL;
+        std::vector<uint64_t> held(H, m->load);
+        for (int32_t h = 0; h < H; h++) {
+            const int32_t s = m->app_peer[h];
+            if (s < -1 || s >= H || s == h || (s >= 0 && m->app_peer[s] != -1)) return SHD_EINVAL;
+            if (s >= 0) held[s] += m->load;
+            mode[h] = s < 0 ? (uint8_t)(SHD_SEND_LISTENER | SHD_DEST_REPLY << 2 | 1u << 4)
+                            : (uint8_t)(SHD_SEND_ONCE | SHD_DEST_PEER << 2 | 1u << 4);
+            nstart[h] = s < 0 ? 0u : m->load;
+            peer[h] = s;
+        }
+        uint64_t cap = 16;
+        for (int32_t h = 0; h < H; h++) cap = std::max<uint64_t>(cap, held[h]);
+        if (cap > 65535) return SHD_ERANGE;   // (a 16-bit ring head in the record)
+        *rq_cap = (uint32_t)cap;
+        *max_start = m->load;
+        return SHD_OK;
+    }
+    // SHD_APP_UDP
+    auto refuse = [](const char* why, long a, long b) {
+        fprintf(stderr, "shd_eng_create: SHD_APP_UDP: %s (%ld, %ld)\n", why, a, b);
+        return SHD_EINVAL;
+    };
+    if (!m->app_spec || !m->host_app || m->n_app_specs == 0 || m->n_app_specs > 256)
+        return refuse("no specs, or more than 256", (long)m->n_app_specs, 0);
+    for (uint32_t k = 0; k < m->n_app_specs; k++) {
+        const shd_udp_app& a = m->app_spec[k];
+        if (a.send > SHD_SEND_LISTENER || a.dest > SHD_DEST_REPLY || a.per_read > 1)
+            return refuse("spec out of range", (long)k, 0);
+        if (a.dest == SHD_DEST_REPLY && (a.n_start || a.send == SHD_SEND_EACH))
+            return refuse("a replying spec that starts or sends from new sockets", (long)k, 0);
+    }
+    bool any_reply = false;
+    uint64_t total = 0;
+    for (int32_t h = 0; h < H; h++) {
+        if (m->host_app[h] >= m->n_app_specs) return refuse("host_app out of range", (long)h, m->host_app[h]);
+        const shd_udp_app& a = m->app_spec[m->host_app[h]];
+        mode[h] = (uint8_t)(a.send | a.dest << 2 | a.per_read << 4);
+        nstart[h] = a.n_start;
+        total += a.n_start;
+        *max_start = std::max<uint64_t>(*max_start, a.n_start);
+        any_reply |= a.dest == SHD_DEST_REPLY;
+    }
+    auto listens = [&](int32_t x) { return (mode[x] & 3u) != SHD_SEND_ONCE; };
+    auto replies = [&](int32_t x) { return ((mode[x] >> 2) & 3u) == SHD_DEST_REPLY; };
+    // the weighted rows: a host with positive weight is a destination of the
+    // row's hosts, so it must listen; and, if any of them sends from a new
+    // socket each time, must not reply (the reply would go to a closed port)
+    std::vector<uint8_t> row_used(n_cls, 0), row_each(n_cls, 0);
+    for (int32_t h = 0; h < H; h++) {
+        if (((mode[h] >> 2) & 3u) != SHD_DEST_WEIGHTED) continue;
+        const int32_t cl = m->host_class ? m->host_class[h] : 0;
+        row_used[cl] = 1;
+        if ((mode[h] & 3u) == SHD_SEND_EACH) row_each[cl] = 1;
+    }
+    for (int32_t cl = 0; cl < n_cls; cl++) {
+        if (!row_used[cl]) continue;
+        const double* cum = m->dest_cum + (size_t)cl * H;
+        for (int32_t i = 0; i < H; i++) {
+            const bool pos = i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1];
+            if (!pos) continue;
+            if (!listens(i)) return refuse("a weighted destination does not listen (class, host)", cl, i);
+            if (row_each[cl] && replies(i))
+                return refuse("a replying host is a weighted destination of new-socket senders (class, host)", cl, i);
+        }
+    }
+    for (int32_t h = 0; h < H; h++) {
+        if (((mode[h] >> 2) & 3u) != SHD_DEST_PEER) continue;
+        const int32_t s = m->app_peer ? m->app_peer[h] : -1;
+        if (s < 0 || s >= H || s == h || !listens(s)) return refuse("a peer that does not listen (host, peer)", h, s);
+        if ((mode[h] & 3u) == SHD_SEND_EACH && replies(s))
+            return refuse("a replying peer of a new-socket sender (host, peer)", h, s);
+        peer[h] = s;
+    }
+    if (any_reply) {
+        // every datagram in flight started as some host's start datagram
+        // (one read answers with at most one): a socket holds at most them all
+        const uint64_t cap = std::max<uint64_t>(16, total);
+        if (cap > 65535) return SHD_ERANGE;   // (a 16-bit ring head in the record)
+        *rq_cap = (uint32_t)cap;
+    }
+    return SHD_OK;
+}
+
 extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin, int32_t host_end, int device,
                               shd_eng** out) {
     if (!m || !pc || !out || !pc->built || m->n_hosts <= 0) return SHD_EINVAL;
@@ -251,21 +357,19 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         return SHD_EINVAL;
     }
     if (m->host_heartbeat) e->host_hb.assign(m->host_heartbeat, m->host_heartbeat + H);
-    if (m->app == SHD_APP_UDP_ECHO) {
-        // the UDP echo's roles: every client's server is a server host; a
-        // socket holds at most the requests in flight to it (its clients' loads)
-        if (!m->app_peer) { shd_eng_destroy(e); return SHD_EINVAL; }
-        std::vector<uint64_t> held(H, m->load);
-        for (int32_t h = 0; h < H; h++) {
-            const int32_t s = m->app_peer[h];
-            if (s < -1 || s >= H || s == h || (s >= 0 && m->app_peer[s] != -1)) { shd_eng_destroy(e); return SHD_EINVAL; }
-            if (s >= 0) held[s] += m->load;
-        }
-        uint64_t cap = 16;
-        for (int32_t h = 0; h < H; h++) cap = std::max<uint64_t>(cap, held[h]);
-        if (cap > 65535) { shd_eng_destroy(e); return SHD_ERANGE; }   // (a 16-bit ring head in the record)
-        P.rq_cap = (uint32_t)cap;
-        e->app_peer.assign(m->app_peer, m->app_peer + H);
+    // the applications other than PHOLD: every host's datagram application as
+    // a mode byte (send | dest << 2 | per_read << 4) and its start count
+    std::vector<uint8_t> app_mode;
+    std::vector<uint32_t> app_nstart;
+    uint64_t max_start = m->load;
+    if (m->app == SHD_APP_UDP_ECHO || m->app == SHD_APP_UDP) {
+        std::vector<int32_t> peer(H, -1);
+        const int rc0 = resolve_apps(m, n_cls, app_mode, app_nstart, peer, &P.rq_cap, &max_start);
+        if (rc0) { shd_eng_destroy(e); return rc0; }
+        e->app_peer.assign(H, -1);   // the status writer: hosts that read on their sending socket
+        for (int32_t h = 0; h < H; h++)
+            if ((app_mode[h] & 3u) == SHD_SEND_ONCE) e->app_peer[h] = 0;
+        e->app_peer_dev = peer;
     } else if (m->app != SHD_APP_PHOLD) {
         shd_eng_destroy(e);
         return SHD_EINVAL;
@@ -300,9 +404,11 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     EALLOC(e->d_guide, HC);
     EALLOC(e->d_self_thr, H);
     if (m->host_heartbeat) EALLOC(e->d_host_hb, H);
-    if (P.app == SHD_APP_UDP_ECHO) {
+    if (!app_mode.empty()) {
         EALLOC(e->d_app_peer, H);
-        EALLOC(P.rq, n * P.rq_cap);
+        EALLOC(e->d_app_mode, H);
+        EALLOC(e->d_app_nstart, H);
+        if (P.rq_cap) EALLOC(P.rq, n * P.rq_cap);
     }
     // destination guide table per class: guide[k] = first i with cum[i] >= k / H (H if none)
     std::vector<DestGuide> guide(HC);
@@ -344,7 +450,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     }
     for (auto& ev : e->bev) (void)hipEventCreate(&ev);
     P.halt = e->d_halt; P.next_rank = e->d_next_rank; P.trace_n = e->d_trace_n;
-    P.pend_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 16, (uint64_t)n * (m->load + 4)), 1u << 30);
+    P.pend_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(1u << 16, (uint64_t)n * (max_start + 4)), 1u << 30);
     P.remote_cap = (uint32_t)std::min<uint64_t>((uint64_t)n * P.inbox_cap, 1u << 30);
     {
         int rc;
@@ -367,7 +473,9 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         (m->host_heartbeat &&
          hipMemcpyAsync(e->d_host_hb, m->host_heartbeat, 8 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess) ||
         (e->d_app_peer &&
-         hipMemcpyAsync(e->d_app_peer, m->app_peer, 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess)) {
+         (hipMemcpyAsync(e->d_app_peer, e->app_peer_dev.data(), 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipMemcpyAsync(e->d_app_mode, app_mode.data(), (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess ||
+          hipMemcpyAsync(e->d_app_nstart, app_nstart.data(), 4 * (size_t)H, hipMemcpyHostToDevice, s) != hipSuccess))) {
         shd_eng_destroy(e);
         return SHD_ENODEV;
     }
@@ -384,6 +492,8 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.dest_guide = e->d_guide;
     P.host_hb = e->d_host_hb;
     P.app_peer = e->d_app_peer;
+    P.app_mode = e->d_app_mode;
+    P.app_nstart = e->d_app_nstart;
     P.no_app_start = (m->queue_flags & SHD_QF_NO_APP_START) ? 1 : 0;
     // draw thresholds: x / RAND_MAX <= c  <=>  x <= draw_threshold(c)
     {
@@ -394,8 +504,11 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         for (int32_t h = 0; h < H; h++) {
             const int32_t cl = m->host_class ? (int32_t)m->host_class[h] : 0;
             const double* cum = m->dest_cum + (size_t)cl * H;
-            thr[h].x = h ? draw_threshold(cum[h - 1]) + 1 : 0;
-            thr[h].y = draw_threshold(cum[h]);
+            // (a host after every draw -- its predecessor's cumulative weight
+            // already 1: no draw of its own; the empty range, not INT32_MAX + 1)
+            const int64_t lo = h ? (int64_t)draw_threshold(cum[h - 1]) + 1 : 0;
+            thr[h].x = lo > INT32_MAX ? 1 : (int32_t)lo;
+            thr[h].y = lo > INT32_MAX ? 0 : draw_threshold(cum[h]);
             thr[h].z = cls_dst_thr[cl];
             thr[h].w = cl;
         }
@@ -409,7 +522,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             bool ok = getenv("SHD_NO_DEST_CLOSED") == nullptr && n_cls == 1;
             for (int32_t h = 0; h < H && ok; h++) ok = host_att[h] == h;
             std::vector<int32_t> ty(H);
-            for (int32_t i = 0; i < H; i++) ty[i] = thr[i].y;
+            for (int32_t i = 0; i < H && ok; i++) ty[i] = draw_threshold(m->dest_cum[i]);   // (monotone; thr.y may be emptied)
             auto f = [&](int32_t i) { return (int64_t)(((uint64_t)(i + 1) * R) / (uint64_t)H); };
             auto pick_true = [&](int64_t x) {   // first i with thr[i] >= x
                 return (int32_t)(std::lower_bound(ty.begin(), ty.end(), (int32_t)x) - ty.begin());
@@ -472,7 +585,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
     P.feat = (m->trace ? F_TRACE : 0u) | (P.hb ? F_HB : 0u) | (P.pcount ? F_PCOUNT : 0u) |
              (P.host_hb ? F_HOSTHB : 0u) | (P.force_ambig ? F_AMBIG : 0u) |
              ((m->trace && (m->queue_flags & SHD_QF_TRACE_STATUS)) ? F_STATUS : 0u) |
-             (P.app == SHD_APP_UDP_ECHO ? F_ECHO : 0u);
+             (P.app != SHD_APP_PHOLD ? F_APP : 0u);
     P.sum = e->d_sum;
     // the serial-equivalent window W: min over every latency a send can be
     // served (rows, direct values, self values) -> ceil(lat * 1e6) ns

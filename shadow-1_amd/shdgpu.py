@@ -100,6 +100,11 @@ class PcInfo(C.Structure):
     ]
 
 
+class UdpApp(C.Structure):
+    """shd_udp_app (include/shdgpu.h): one host's datagram application."""
+    _fields_ = [("send", C.c_uint32), ("dest", C.c_uint32), ("n_start", C.c_uint32), ("per_read", C.c_uint32)]
+
+
 class Model(C.Structure):
     _fields_ = [
         ("n_hosts", C.c_int32), ("_pad0", C.c_int32),
@@ -114,10 +119,13 @@ class Model(C.Structure):
         ("host_class", P(C.c_uint8)), ("n_classes", C.c_int32), ("_pad1", C.c_int32),
         ("host_heartbeat", P(C.c_uint64)),
         ("app", C.c_uint32), ("_pad2", C.c_int32), ("app_peer", P(C.c_int32)),
+        ("app_spec", P(UdpApp)), ("host_app", P(C.c_uint8)), ("n_app_specs", C.c_uint32), ("_pad3", C.c_uint32),
     ]
 
 
-SHD_APP_PHOLD, SHD_APP_UDP_ECHO = 0, 1
+SHD_APP_PHOLD, SHD_APP_UDP_ECHO, SHD_APP_UDP = 0, 1, 2
+SHD_SEND_EACH, SHD_SEND_ONCE, SHD_SEND_LISTENER = 0, 1, 2
+SHD_DEST_WEIGHTED, SHD_DEST_PEER, SHD_DEST_REPLY = 0, 1, 2
 
 
 class Event(C.Structure):
@@ -432,11 +440,15 @@ class ModelArrays:
     def __init__(self, host_vertex, host_rng, bw_down, bw_up, dest_cum, *, end_time,
                  app_start=1 * SHD_SEC, load=16, payload=1, heartbeat_interval=SHD_SEC,
                  bootstrap_end=0, trace=False, evq_cap=0, inbox_cap=0, codelq_cap=0,
-                 txq_cap=0, queue_flags=0, host_class=None, host_heartbeat=None, app_peer=None):
+                 txq_cap=0, queue_flags=0, host_class=None, host_heartbeat=None, app_peer=None,
+                 app_specs=None, host_app=None):
         """dest_cum: [H] (one weights row for every host) or [n_classes, H] with
         host_class [H] picking each host's row; host_heartbeat: [H] ns or None;
         app_peer: None (every host runs PHOLD) or [H] -1 | server host (every
-        host runs the UDP request/response echo, SHD_APP_UDP_ECHO)."""
+        host runs the UDP request/response echo, SHD_APP_UDP_ECHO);
+        app_specs: [(send, dest, n_start, per_read)] with host_app [H] picking
+        each host's (SHD_APP_UDP, include/shdgpu.h shd_udp_app; app_peer then
+        names the SHD_DEST_PEER hosts' peers)."""
         self.host_vertex = np.ascontiguousarray(host_vertex, dtype=np.int32)
         self.host_rng = np.ascontiguousarray(host_rng, dtype=np.uint32)
         self.bw_down = np.ascontiguousarray(bw_down, dtype=np.uint64)
@@ -454,6 +466,18 @@ class ModelArrays:
         self.app_peer = None if app_peer is None else np.ascontiguousarray(app_peer, dtype=np.int32)
         assert self.app_peer is None or len(self.app_peer) == H
         self.app = SHD_APP_PHOLD if self.app_peer is None else SHD_APP_UDP_ECHO
+        self.app_specs = None
+        self.host_app = None
+        # the status writer's port rule: >= 0 for a host that reads on the
+        # socket it sends from (the echo's clients, SHD_SEND_ONCE), else -1
+        self.status_peer = self.app_peer
+        if app_specs is not None:
+            assert host_app is not None and len(host_app) == H and 0 < len(app_specs) <= 256
+            self.app = SHD_APP_UDP
+            self.app_specs = (UdpApp * len(app_specs))(*[UdpApp(*map(int, a)) for a in app_specs])
+            self.host_app = np.ascontiguousarray(host_app, dtype=np.uint8)
+            once = np.array([int(a[0]) == SHD_SEND_ONCE for a in app_specs], dtype=bool)
+            self.status_peer = np.where(once[self.host_app], 0, -1).astype(np.int32)
         self.params = dict(end_time=int(end_time), app_start=int(app_start), load=int(load),
                            payload=int(payload), heartbeat_interval=int(heartbeat_interval),
                            bootstrap_end=int(bootstrap_end), trace=int(bool(trace)),
@@ -466,7 +490,10 @@ class ModelArrays:
             int(evq_cap), int(inbox_cap), int(codelq_cap), int(txq_cap), int(queue_flags),
             None if self.host_class is None else as_ptr(self.host_class, C.c_uint8), int(n_classes), 0,
             None if self.host_heartbeat is None else as_ptr(self.host_heartbeat, C.c_uint64),
-            self.app, 0, None if self.app_peer is None else as_ptr(self.app_peer, C.c_int32))
+            self.app, 0, None if self.app_peer is None else as_ptr(self.app_peer, C.c_int32),
+            None if self.app_specs is None else C.cast(self.app_specs, P(UdpApp)),
+            None if self.host_app is None else as_ptr(self.host_app, C.c_uint8),
+            0 if self.app_specs is None else len(self.app_specs), 0)
 
     @property
     def n_hosts(self):

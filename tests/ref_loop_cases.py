@@ -129,6 +129,40 @@ def _udp_echo_codel():
     return dict(model=m, graph=g)
 
 
+def _udp_mix(payload=1, bw_server=10240, client_load=2):
+    """The general datagram application (SHD_APP_UDP, ref_loop.c app 3): five
+    kinds of host on one 60-vertex geometric graph, edge loss U[0, 0.02]:
+    20 PHOLD hosts (new socket per datagram, weighted destinations over
+    themselves and the sinks, 3 each at the start, one per read), 10 servers
+    (reply from the listener to whatever they read), 15 clients (one socket,
+    weighted over the servers, 2 requests in flight each), 5 one-way senders
+    (4 datagrams from the listener to one sink each, nothing per read) and 10
+    sinks (read only)."""
+    V = 60
+    g = W.geometric_graph(V, seed=31, loss_max=0.02)
+    m0 = W.phold_model(W.hosts_on_vertices(V, 1), end_time=3 * S.SHD_SEC, trace=True)
+    kind = np.array([0] * 20 + [1] * 10 + [2] * 15 + [3] * 5 + [4] * 10, dtype=np.uint8)
+    specs = [(S.SHD_SEND_EACH, S.SHD_DEST_WEIGHTED, 3, 1),      # PHOLD
+             (S.SHD_SEND_LISTENER, S.SHD_DEST_REPLY, 0, 1),     # server
+             (S.SHD_SEND_ONCE, S.SHD_DEST_WEIGHTED, client_load, 1),   # client
+             (S.SHD_SEND_LISTENER, S.SHD_DEST_PEER, 4, 0),      # one-way sender
+             (S.SHD_SEND_LISTENER, S.SHD_DEST_WEIGHTED, 0, 0)]  # sink
+    w = np.zeros((2, V))
+    w[0, (kind == 0) | (kind == 4)] = 1.0      # class 0: PHOLD hosts and sinks
+    w[1, kind == 1] = 1.0                      # class 1 (clients): the servers
+    cum = np.cumsum(w / w.sum(axis=1, keepdims=True), axis=1)
+    for r in range(2):   # exactly 1 from each row's last weighted host on (the rest stay unweighted)
+        cum[r, np.flatnonzero(w[r])[-1]:] = 1.0
+    cls = (kind == 2).astype(np.uint8)
+    peer = np.full(V, -1, dtype=np.int32)
+    peer[kind == 3] = np.flatnonzero(kind == 4)[:5]
+    bw = np.where(kind == 1, bw_server, 10240).astype(np.uint64)
+    m = S.ModelArrays(m0.host_vertex, m0.host_rng, bw, m0.bw_up, cum, end_time=3 * S.SHD_SEC, trace=True,
+                      payload=payload, codelq_cap=512, queue_flags=TS, host_class=cls, app_peer=peer,
+                      app_specs=specs, host_app=kind)
+    return dict(model=m, graph=g)
+
+
 CASES = {
     "phold_v100": _phold_v100,
     "codel": _codel,
@@ -140,6 +174,10 @@ CASES = {
     "c1": _c1,
     "udp_echo": _udp_echo,
     "udp_echo_codel": _udp_echo_codel,
+    "udp_mix": _udp_mix,
+    # 1500-B datagrams into 256 KiB/s receive buckets at the servers, 24
+    # requests in flight per client: the servers' CoDel queues build and drop
+    "udp_mix_codel": lambda: _udp_mix(payload=1500, bw_server=256, client_load=24),
 }
 
 

@@ -36,7 +36,8 @@ class Cfg(C.Structure):
                 ("load", C.c_uint32), ("payload", C.c_uint32),
                 ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p),
                 ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32),
-                ("quiet", C.c_int32), ("qdisc_rr", C.c_int32), ("mark_time", C.c_uint64 * 2)]
+                ("quiet", C.c_int32), ("qdisc_rr", C.c_int32), ("mark_time", C.c_uint64 * 2),
+                ("app_spec", P(C.c_uint32)), ("host_app", P(C.c_uint8)), ("app_peer", P(C.c_int32))]
 
 
 class Out(C.Structure):
@@ -124,7 +125,16 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     cfg.n_hosts = H
     cfg.quiet = 1 if quiet else 0
     cfg.app = 0 if tcp is None else 1
-    if echo is not None:   # the UDP echo application: echo[h] = -1 (server) or h's server host
+    if getattr(model, "app_specs", None) is not None:   # app 3: the model's per-host datagram applications
+        cfg.app = 3
+        sp = np.ascontiguousarray([[a.send, a.dest, a.n_start, a.per_read] for a in model.app_specs],
+                                  dtype=np.uint32).ravel()
+        keep.append(sp)
+        cfg.app_spec = _ptr(sp, C.c_uint32)
+        cfg.host_app = _ptr(model.host_app, C.c_uint8)
+        if model.app_peer is not None:
+            cfg.app_peer = _ptr(model.app_peer, C.c_int32)
+    elif echo is not None:   # the UDP echo application: echo[h] = -1 (server) or h's server host
         cfg.app = 2
         ep = np.ascontiguousarray(echo, dtype=np.int32)
         keep.append(ep)

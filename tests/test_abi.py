@@ -89,3 +89,20 @@ def test_tcp_struct_layout_matches_the_header(tmp_path):
     assert got == [C.sizeof(S.TcpModel), S.TcpModel.host_vertex.offset, S.TcpModel.packets_per_host.offset,
                    C.sizeof(S.TcpResult), S.TcpResult.deliveries.offset, S.TcpModel.path_cache.offset,
                    S.TcpResult.max_round_deliveries.offset]
+
+
+def test_model_struct_layout_matches_the_header(tmp_path):
+    # the ctypes mirrors of shd_model / shd_udp_app / shd_run_stats against gcc's layout
+    import ctypes as C
+    src = tmp_path / "m.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s/include/shdgpu.h"\n'
+                   'int main(void){printf("%%zu %%zu %%zu %%zu %%zu %%zu %%zu\\n", sizeof(shd_model),'
+                   ' offsetof(shd_model, app_peer), offsetof(shd_model, app_spec), offsetof(shd_model, host_app),'
+                   ' offsetof(shd_model, n_app_specs), sizeof(shd_udp_app), sizeof(shd_run_stats));'
+                   'printf("%%zu\\n", offsetof(shd_run_stats, n_rounds_replayed));return 0;}\n' % REPO)
+    exe = tmp_path / "m"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [C.sizeof(S.Model), S.Model.app_peer.offset, S.Model.app_spec.offset, S.Model.host_app.offset,
+                   S.Model.n_app_specs.offset, C.sizeof(S.UdpApp), C.sizeof(S.RunStats),
+                   S.RunStats.n_rounds_replayed.offset]

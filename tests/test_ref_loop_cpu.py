@@ -38,7 +38,7 @@ def oracle_lines(case, fx):
     K = hb_k(case)
     hb = np.zeros((m.n_hosts, K, 2), dtype=np.uint32)
     tr, dg, _ = O.engine_run(m, g, pushes=case.get("pushes"), heartbeats=hb)
-    st = S.status_lines(tr, fx["ips"], payload=int(m.struct.payload), app_peer=m.app_peer)
+    st = S.status_lines(tr, fx["ips"], payload=int(m.struct.payload), app_peer=m.status_peer)
     st = sorted(st, key=lambda x: (x[0], x[1]))
     return st, RC.heartbeat_lines(m, hb, K), dg
 
