@@ -86,6 +86,9 @@ constexpr int kChunk = 32;   // edges folded per pass of the forward chain walk
 #ifndef SHD_SSSP_BFQ
 #define SHD_SSSP_BFQ 2   // queued frontier: vertices per half-wave relaxed together
 #endif
+#ifndef SHD_SSSP_BFQ2
+#define SHD_SSSP_BFQ2 1  // ... in the two-row kernel
+#endif
 
 template <int BLOCK>
 __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
@@ -103,8 +106,18 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows,
                              int32_t* fl_pre, int32_t* fl_beg, uint64_t* fl_dv /* LDS [BLOCK] each */,
                              const uint16_t* off16, const int32_t* cbase /* LDS arc offsets, or null */,
-                             bool bfq /* queued frontier: four vertices a wave in flight */) {
+                             bool bfq /* queued frontier: four vertices a wave in flight */,
+                             int bf_it = -1 /* >= 0: dist holds the row's converged distances (sssp_bf2) */) {
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6, hl = lane & 31;
+    const bool upper = lane >= 32;
+    int it = 0;
+    if (bf_it >= 0) {   // the distances came from the two-row Bellman-Ford
+        for (int32_t v = tid; v < V; v += BLOCK) parent[v] = -1;
+        if (tid < 4) flags[tid] = 0;
+        it = bf_it;
+        __syncthreads();
+    } else {
     for (int32_t v = tid; v < V; v += BLOCK) {
         dist[v] = kDistInf;
         parent[v] = -1;
@@ -122,9 +135,6 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     // instead of one lane walking ~20 arcs with a dependent L2 load per arc.
     // Any relaxation order reaches the same fixpoint: d[x] = min over paths of
     // the left-folded sum (fl(a + w) is monotone in a).
-    const int lane = tid & 63, wv = tid >> 6, hl = lane & 31;
-    const bool upper = lane >= 32;
-    int it = 0;
     SST_T0(t_bf)
     for (;;) {
         if (tid == 0) flags[(it + 1) % 3] = 0;
@@ -327,6 +337,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     }
     SST_ADD(0, t_bf)
     if (tid == 0) { SST_CNT(4, it); SST_CNT(7, 1); }
+    }   // (bf_it < 0)
 
 #if defined(SHD_SSSP_STOP_AFTER) && SHD_SSSP_STOP_AFTER == 1   // phase ablation (scripts/apsp_phases.sh)
     __syncthreads();
@@ -458,7 +469,16 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
             if (has_rsrc) rel *= rsrc;
             rel *= rt;
             int32_t k = 0;
-            for (int32_t v = t; v != src; v = rin_src[parent[v]]) k++;
+            bool broken = false;   // (a parent chain that does not reach the source: counted, never followed)
+            for (int32_t v = t; v != src; v = rin_src[parent[v]]) {
+                if (parent[v] < 0 || k >= V) { broken = true; break; }
+                k++;
+            }
+            if (broken) {
+                my_mismatch++;
+                out[(size_t)row * T + j] = shd_pv{-1.0, -1.0};
+                continue;
+            }
             if (k > my_maxhops) my_maxhops = k;
             lat = 0.0;
             int32_t eid_buf[kChunk];
@@ -631,6 +651,203 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
                             fl_beg, fl_dv, off16, cbase, (mode & 2) != 0);
+    }
+}
+
+// ---- two rows per workgroup (k_sssp_rows2_lds, the default where both
+// rows' distances fit the LDS: 10 080 vertices).  A row's Bellman-Ford is a
+// chain of ~50 dependent frontier iterations, each the slowest wave's chunk
+// scan and relaxations and a workgroup barrier: latency, not throughput.  Two
+// rows in one loop give every wave two independent chains between the same
+// barriers.  Their distances fill the LDS (8 B a vertex each), so the 16-bit
+// stamps give way to one bit a vertex per row: a relaxation that improves x
+// sets x's bit (an LDS atomic or); right after the barrier each wave takes
+// (atomic exchange with 0) the bit words of its own chunks, one word per lane,
+// and relaxes the vertices they name.  A bit set in an iteration after its
+// word was taken waits for the next one (as the stamps did); one set before
+// (a faster wave's relaxation) is taken at once -- any order reaches the same
+// fixpoint (fl(a + w) is monotone), and a vertex still relaxes once per
+// improvement.  The rows' properties then run one at a time through
+// sssp_one_row's phases (bf_it), row B's distances parked in global scratch.
+template <int BLOCK, int NCH>
+__device__ void sssp_bf2(int32_t srcA, int32_t srcB /* -1: none */, int32_t V, const int32_t* __restrict__ arc_off,
+                         const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w, uint64_t* dA,
+                         uint64_t* dB, uint32_t* bA, uint32_t* bB /* [ceil(V / 32)] each */,
+                         int* flags /* LDS int[8]: A's at 0..2, B's at 4..6 */, int* itA, int* itB) {
+    constexpr int NW = BLOCK / 64;
+    static_assert(2 * NCH <= 32, "a wave's bit words of both rows in one lane each");
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hl = lane & 31;
+    const bool upper = lane >= 32;
+    const int32_t nw32 = (V + 31) >> 5;
+    for (int32_t v = tid; v < V; v += BLOCK) { dA[v] = kDistInf; dB[v] = kDistInf; }
+    for (int32_t k = tid; k < nw32; k += BLOCK) { bA[k] = 0; bB[k] = 0; }
+    if (tid < 8) flags[tid] = 0;
+    __syncthreads();
+    if (tid == 0) {
+        dA[srcA] = 0;
+        bA[srcA >> 5] = 1u << (srcA & 31);
+        if (srcB >= 0) {
+            dB[srcB] = 0;
+            bB[srcB >> 5] = 1u << (srcB & 31);
+        }
+    }
+    __syncthreads();
+    bool liveA = true, liveB = srcB >= 0;
+    int it = 0;
+    *itA = 0;
+    *itB = 0;
+    for (;;) {
+        if (tid == 0) { flags[(it + 1) % 3] = 0; flags[4 + (it + 1) % 3] = 0; }
+        // the wave's bit words: lane 2c + h holds row A's word h of chunk c,
+        // lane 32 + 2c + h row B's
+        uint32_t wbits = 0;
+        {
+            const int r = lane >> 5, j = lane & 31, c = j >> 1;
+            const int32_t k = (wv + c * NW) * 2 + (j & 1);   // word index: chunk (wv + c NW), half j & 1
+            if (j < 2 * NCH && k < nw32 && (r == 0 ? liveA : liveB)) wbits = atomicExch(r == 0 ? &bA[k] : &bB[k], 0u);
+        }
+        constexpr int Q = SHD_SSSP_BFQ2;
+        int32_t qa[2 * Q], qb[2 * Q];
+#pragma unroll
+        for (int j = 0; j < 2 * Q; j++) { qa[j] = -1; qb[j] = -1; }
+        int na = 0, nb = 0;
+        auto relax = [&](uint64_t* d, uint32_t* b, int* fl, int32_t x, double cand) {
+            const uint64_t nbv = d2u(cand);
+            if (nbv < d[x]) {
+                const uint64_t old = atomicMin((unsigned long long*)&d[x], (unsigned long long)nbv);
+                if (nbv < old) {
+                    atomicOr(&b[x >> 5], 1u << (x & 31));
+                    fl[it % 3] = 1;
+                }
+            }
+        };
+        auto run_q = [&](uint64_t* d, uint32_t* b, int* fl, int32_t (&q)[2 * Q]) {
+            int32_t bq[Q], eq[Q], xq[Q];
+            double dq[Q], wq[Q];
+#pragma unroll
+            for (int j = 0; j < Q; j++) {
+                const int32_t v = upper ? q[2 * j + 1] : q[2 * j];
+                bq[j] = 0; eq[j] = 0; dq[j] = 0.0;
+                if (v >= 0 && v < V) { bq[j] = arc_off[v]; eq[j] = arc_off[v + 1]; dq[j] = u2d(d[v]); }
+            }
+#pragma unroll
+            for (int j = 0; j < Q; j++) {
+                const int32_t k = bq[j] + hl;
+                xq[j] = -1; wq[j] = 0.0;
+                if (k < eq[j]) { xq[j] = arc_dst[k]; wq[j] = arc_w[k]; }
+            }
+#pragma unroll
+            for (int j = 0; j < Q; j++)
+                if (xq[j] >= 0) relax(d, b, fl, xq[j], dq[j] + wq[j]);
+#pragma unroll
+            for (int j = 0; j < Q; j++)
+                for (int32_t k = bq[j] + hl + 32; k < eq[j]; k += 32) relax(d, b, fl, arc_dst[k], dq[j] + arc_w[k]);
+        };
+        auto push = [&](int32_t (&q)[2 * Q], int32_t fv) {
+#pragma unroll
+            for (int j = 0; j < 2 * Q - 1; j++) q[j] = q[j + 1];
+            q[2 * Q - 1] = fv;
+        };
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const int32_t c0 = (wv + c * NW) * 64;
+            uint64_t mA = (uint64_t)(uint32_t)__shfl((int)wbits, 2 * c) |
+                          ((uint64_t)(uint32_t)__shfl((int)wbits, 2 * c + 1) << 32);
+            uint64_t mB = (uint64_t)(uint32_t)__shfl((int)wbits, 32 + 2 * c) |
+                          ((uint64_t)(uint32_t)__shfl((int)wbits, 32 + 2 * c + 1) << 32);
+            // (uniform; each half widened from uint32_t: an int would sign-extend)
+            mA = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mA) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mA >> 32)) << 32);
+            mB = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mB) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mB >> 32)) << 32);
+            while (mA) {
+                const int32_t fv = c0 + __ffsll((unsigned long long)mA) - 1;
+                mA &= mA - 1;
+                push(qa, fv);
+                if (++na == 2 * Q) { run_q(dA, bA, flags, qa); na = 0; }
+            }
+            while (mB) {
+                const int32_t fv = c0 + __ffsll((unsigned long long)mB) - 1;
+                mB &= mB - 1;
+                push(qb, fv);
+                if (++nb == 2 * Q) { run_q(dB, bB, flags + 4, qb); nb = 0; }
+            }
+        }
+        if (na) {
+            while (na < 2 * Q) { push(qa, -1); na++; }
+            run_q(dA, bA, flags, qa);
+        }
+        if (nb) {
+            while (nb < 2 * Q) { push(qb, -1); nb++; }
+            run_q(dB, bB, flags + 4, qb);
+        }
+        __syncthreads();
+        const bool moreA = liveA && flags[it % 3] != 0, moreB = liveB && flags[4 + it % 3] != 0;
+        it++;
+        if (liveA && !moreA) *itA = it;
+        if (liveB && !moreB) *itB = it;
+        liveA = moreA;
+        liveB = moreB;
+        if ((!liveA && !liveB) || it >= 0xFFFE) break;
+    }
+}
+
+// a row's properties after sssp_bf2 (sssp_one_row's phases from its parents on)
+template <int BLOCK>
+__device__ __forceinline__ void sssp_post_row(
+    int32_t row, int32_t V, int32_t T, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
+    const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src, const int32_t* __restrict__ arc_rin,
+    const int32_t* __restrict__ rin_off, const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
+    const double* __restrict__ rin_w, const double* __restrict__ rin_r, const double* __restrict__ w_e,
+    const double* __restrict__ eloss, const double* __restrict__ vloss, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out, int64_t* __restrict__ stats, uint64_t* dist,
+    int32_t* parent, uint16_t* upd, int* flags, int32_t* __restrict__ tie_rows, int bf_it) {
+    sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src, rin_eid,
+                        rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist, parent, upd, flags,
+                        nullptr, tie_rows, nullptr, nullptr, nullptr, nullptr, nullptr, false, bf_it);
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_sssp_rows2_lds(
+    int32_t V, int32_t T, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst,
+    const double* __restrict__ arc_w, const int32_t* __restrict__ arc_src, const int32_t* __restrict__ arc_rin,
+    const int32_t* __restrict__ rin_off,
+    const int32_t* __restrict__ rin_src, const int32_t* __restrict__ rin_eid,
+    const double* __restrict__ rin_w, const double* __restrict__ rin_r, const double* __restrict__ w_e,
+    const double* __restrict__ eloss,
+    const double* __restrict__ vloss, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
+    int64_t* __restrict__ stats, int32_t row0, int32_t row1, int32_t* __restrict__ tie_rows,
+    uint64_t* __restrict__ park /* [grid][V]: row B's distances while row A's properties run */) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint64_t* rA = (uint64_t*)smem;
+    uint64_t* rB = (uint64_t*)(smem + (size_t)8 * V);
+    const size_t nbw = (size_t)((V + 31) >> 5);
+    uint32_t* bA = (uint32_t*)(smem + (size_t)16 * V);
+    uint32_t* bB = bA + nbw;
+    int* flags = (int*)(bB + nbw);
+    uint64_t* pk = park + (size_t)blockIdx.x * V;
+    const int tid = threadIdx.x;
+    for (int32_t p = row0 + 2 * (int32_t)blockIdx.x; p < row1; p += 2 * (int32_t)gridDim.x) {
+        const int32_t ra = p, rb = p + 1 < row1 ? p + 1 : -1;
+        int itA = 0, itB = 0;
+        sssp_bf2<BLOCK, 10>(attached[ra], rb >= 0 ? attached[rb] : -1, V, arc_off, arc_dst, arc_w, rA, rB, bA, bB,
+                            flags, &itA, &itB);
+        if (rb >= 0)
+            for (int32_t v = tid; v < V; v += BLOCK) pk[v] = rB[v];
+        __syncthreads();
+        // row A: its distances in rA, parents and stamps in rB's space
+        sssp_post_row<BLOCK>(ra, V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src, rin_eid, rin_w,
+                             rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, rA, (int32_t*)rB,
+                             (uint16_t*)(smem + (size_t)12 * V), flags, tie_rows, itA);
+        __syncthreads();
+        if (rb < 0) continue;
+        for (int32_t v = tid; v < V; v += BLOCK) rA[v] = pk[v];
+        __syncthreads();
+        sssp_post_row<BLOCK>(rb, V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src, rin_eid, rin_w,
+                             rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, rA, (int32_t*)rB,
+                             (uint16_t*)(smem + (size_t)12 * V), flags, tie_rows, itB);
+        __syncthreads();
     }
 }
 
@@ -1151,6 +1368,14 @@ static int bf_queue_bit() {
     static const int b = getenv("SHD_PC_BF_PAIRS") ? 0 : 2;
     return b;
 }
+// the two-row kernel: both rows' distances (16 B a vertex), their frontier
+// bits and the flags; its
+// waves scan ten 64-vertex chunks each at most (sssp_bf2<1024, 10>)
+static size_t two_row_lds(int32_t V) { return (size_t)16 * V + (size_t)8 * ((V + 31) / 32) + 32; }
+static bool two_row_ok(const shd_pc* pc) {
+    static const bool off = getenv("SHD_PC_ONE_ROW") != nullptr;   // A/B: one row per workgroup
+    return !off && kRowBlock == 1024 && pc->V <= 10 * 1024 && two_row_lds(pc->V) <= kLdsMax;
+}
 static size_t lds_off_bytes(int32_t V) {
     return (((size_t)2 * V + 15) & ~(size_t)15) + ((((size_t)(V + 63) / 64 + 1) * 4 + 15) & ~(size_t)15);
 }
@@ -1282,6 +1507,25 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
                                    (lo ? 1 : 0) | bf_queue_bit());
+            } else if (two_row_ok(pc)) {
+                // two rows per workgroup (sssp_bf2), row B parked in d_scratch
+                const size_t lds2 = two_row_lds(V);
+                const int grid = std::max(1, std::min((row1 - row0 + 1) / 2, ncu));
+                const size_t park = (size_t)grid * V * sizeof(uint64_t);
+                if (!pc->d_scratch || pc->scratch_bytes < park) {
+                    if (pc->d_scratch) (void)hipFree(pc->d_scratch);
+                    pc->d_scratch = nullptr;
+                    pc->scratch_bytes = 0;
+                    SHD_HIP(hipMalloc(&pc->d_scratch, park));
+                    pc->scratch_bytes = park;
+                }
+                SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows2_lds<kRowBlock>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+                hipLaunchKernelGGL(k_sssp_rows2_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds2, s, V, T,
+                                   pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin,
+                                   pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w,
+                                   pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats,
+                                   row0, row1, pc->d_tie_rows, (uint64_t*)pc->d_scratch);
             } else {
                 int grid = std::max(1, std::min(row1 - row0, ncu));
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<kRowBlock>,
