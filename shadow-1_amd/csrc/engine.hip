@@ -1622,6 +1622,7 @@ extern "C" void shd_eng_destroy(shd_eng* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) (void)hipFree(p);
+    for (void* p : e->snap) (void)hipFree(p);   // the protected rounds' / restore point's state copy
     if (e->h_sum) (void)hipHostFree(e->h_sum);
     if (e->h_ring) (void)hipHostFree(e->h_ring);
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);
