@@ -6,7 +6,6 @@
 #   pmc_calibration.json    FETCH_SIZE / WRITE_SIZE against known bytes (scripts/microbench/pmc_calib.hip)
 #   pmc_traffic.json        FETCH_SIZE x correction + WRITE_SIZE per round over the timed region (separate passes)
 #   sq_counters.txt         SQ counters of k_round_ps (two passes; per dispatch = one persistent batch)
-#   ps_timing.txt           phase stamps of the persistent round (timing build)
 #   barrier.txt, launch.txt the seam microbenchmarks
 set -o pipefail
 export TMPDIR=/tmp
@@ -40,7 +39,9 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_
 done
 python3 scripts/pmc_summary.py $O/pmc1 $O/pmc2 --kernel k_round_ps > $O/sq_counters.txt && rm -rf $O/pmc1 $O/pmc2 || exit 9
 echo sq ok
-SHD_TIMING_LIGHT=1 SHDGPU_LIB=shadow-1_amd/libshdgpu_tim.so timeout -k 10 200 python3 scripts/ps_timing.py > $O/ps_timing.txt 2>&1 || { tail $O/ps_timing.txt; exit 10; }
+# (round 5: no phase stamps -- the SHD_TIMING build of this engine stops in the
+# compiler's back end, "illegal VGPR to SGPR copy"; profiles/r04/ps_timing.txt
+# holds round 4's)
 timeout -k 10 60 ./scripts/microbench/barrier > $O/barrier.txt 2>&1 || exit 11
 timeout -k 10 60 ./scripts/microbench/launch > $O/launch.txt 2>&1 || exit 12
 rm -f $O/*.err
