@@ -86,6 +86,9 @@ constexpr int kChunk = 32;   // edges folded per pass of the forward chain walk
 #ifndef SHD_SSSP_BFQ
 #define SHD_SSSP_BFQ 2   // queued frontier: vertices per half-wave relaxed together
 #endif
+#ifndef SHD_SSSP_MIXQ
+#define SHD_SSSP_MIXQ 0  // 1: the two-row kernel's rows share one queue (21.35 against 20.28 ms: not kept)
+#endif
 #ifndef SHD_SSSP_BFQ2
 #define SHD_SSSP_BFQ2 2  // ... in the two-row kernel (1: 21.6 ms, 2: 20.3 ms on the 10 k table)
 #endif
@@ -748,6 +751,44 @@ __device__ void sssp_bf2(int32_t srcA, int32_t srcB /* -1: none */, int32_t V, c
             for (int j = 0; j < 2 * Q - 1; j++) q[j] = q[j + 1];
             q[2 * Q - 1] = fv;
         };
+#if SHD_SSSP_MIXQ
+        // one queue for both rows (an entry: the vertex | row << 30): a
+        // half-wave's vertex of row A and the other's of row B relax together,
+        // both rows' loads in flight at once
+        int32_t qm[2 * Q];
+#pragma unroll
+        for (int j = 0; j < 2 * Q; j++) qm[j] = -1;
+        int nm = 0;
+        auto run_qm = [&]() {
+            int32_t bq[Q], eq[Q], xq[Q], rq[Q];
+            double dq[Q], wq[Q];
+#pragma unroll
+            for (int j = 0; j < Q; j++) {
+                const int32_t e = upper ? qm[2 * j + 1] : qm[2 * j];
+                const int32_t v = e & 0x3FFFFFFF;
+                rq[j] = e >= 0 ? (e >> 30) : 0;
+                bq[j] = 0; eq[j] = 0; dq[j] = 0.0;
+                if (e >= 0 && v < V) {
+                    bq[j] = arc_off[v]; eq[j] = arc_off[v + 1];
+                    dq[j] = u2d(rq[j] ? dB[v] : dA[v]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < Q; j++) {
+                const int32_t k = bq[j] + hl;
+                xq[j] = -1; wq[j] = 0.0;
+                if (k < eq[j]) { xq[j] = arc_dst[k]; wq[j] = arc_w[k]; }
+            }
+#pragma unroll
+            for (int j = 0; j < Q; j++)
+                if (xq[j] >= 0) relax(rq[j] ? dB : dA, rq[j] ? bB : bA, rq[j] ? flags + 4 : flags, xq[j], dq[j] + wq[j]);
+#pragma unroll
+            for (int j = 0; j < Q; j++)
+                for (int32_t k = bq[j] + hl + 32; k < eq[j]; k += 32)
+                    relax(rq[j] ? dB : dA, rq[j] ? bB : bA, rq[j] ? flags + 4 : flags, arc_dst[k], dq[j] + arc_w[k]);
+        };
+        (void)na; (void)nb; (void)run_q;
+#endif
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int32_t c0 = (wv + c * NW) * 64;
@@ -760,6 +801,25 @@ __device__ void sssp_bf2(int32_t srcA, int32_t srcB /* -1: none */, int32_t V, c
                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mA >> 32)) << 32);
             mB = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mB) |
                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mB >> 32)) << 32);
+#if SHD_SSSP_MIXQ
+            while (mA | mB) {
+                int32_t fv;
+                if (mA) {
+                    fv = c0 + __ffsll((unsigned long long)mA) - 1;
+                    mA &= mA - 1;
+                } else {
+                    fv = (c0 + __ffsll((unsigned long long)mB) - 1) | (1 << 30);
+                    mB &= mB - 1;
+                }
+                push(qm, fv);
+                if (++nm == 2 * Q) { run_qm(); nm = 0; }
+            }
+        }
+        if (nm) {
+            while (nm < 2 * Q) { push(qm, -1); nm++; }
+            run_qm();
+        }
+#else
             while (mA) {
                 const int32_t fv = c0 + __ffsll((unsigned long long)mA) - 1;
                 mA &= mA - 1;
@@ -781,6 +841,7 @@ __device__ void sssp_bf2(int32_t srcA, int32_t srcB /* -1: none */, int32_t V, c
             while (nb < 2 * Q) { push(qb, -1); nb++; }
             run_q(dB, bB, flags + 4, qb);
         }
+#endif
         __syncthreads();
         const bool moreA = liveA && flags[it % 3] != 0, moreB = liveB && flags[4 + it % 3] != 0;
         it++;
