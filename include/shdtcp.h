@@ -68,6 +68,26 @@ typedef struct shd_tcp_model {
      * ranks are left as the serial run leaves them.  host_vertex then holds
      * graph vertex ids, and n_vertices / path_lat_ms / path_rel are unused. */
     struct shd_pc* path_cache;
+    /* Datagram processes beside the echo ones: both transports in one model,
+     * on each host's one interface (qdisc, token buckets, CoDel queue) --
+     * network_interface.c:519-579 serves TCP and UDP sockets alike.
+     * proc_app[k] >= 0: process k runs the datagram application
+     * app_spec[4 * proc_app[k] ..] = shd_udp_app's {send, dest, n_start,
+     * per_read} (shdgpu.h; PHOLD's port 8998) instead of the echo, with
+     * proc_peer[k] = -1; at most one such process per host.  NULL proc_app:
+     * every process runs the echo.  udp_payload: bytes per datagram (1 ..
+     * 65507); app_peer [H]: the SHD_DEST_PEER host of each host; dest_cum
+     * [n_classes][H] / host_class [H]: SHD_DEST_WEIGHTED's cumulative weights
+     * (host_class NULL: row 0).  A host then holds up to 16 sockets at once
+     * (8 otherwise): more set SHD_TCP_ERR_SOCKETS. */
+    const int32_t* proc_app;
+    const uint32_t* app_spec;
+    int32_t n_app_specs;
+    uint32_t udp_payload;
+    const int32_t* app_peer;
+    const double* dest_cum;
+    const uint8_t* host_class;
+    int32_t n_classes, _pad2;
 } shd_tcp_model;
 
 /* the first path query a host made of a vertex pair (topology_isRoutable /
@@ -128,7 +148,8 @@ enum {
     SHD_TCP_ERR_QLOG = 256, SHD_TCP_ERR_FIRST_TOUCH = 512
 };
 
-/* Run the model to end_time on the current HIP device.  trace & 1 writes the
+/* Run the model to end_time on the current HIP device (the reference's
+ * src/main/core/worker.c loop for these processes; see the file comment).  trace & 1 writes the
  * [STATUS] lines (packet.c:647-659); trace & 2 keeps the tracker's node
  * counters per heartbeat (the [node] lines, tracker.c:419-465).  Returns 0 or a negative errno-style code:
  * -22 an invalid model, -113 a client whose server has no route in either

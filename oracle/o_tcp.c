@@ -44,6 +44,8 @@
 #define SEC 1000000000ull
 #define MTU 1500u
 #define HDR_TCP 66u
+#define HDR_UDP 42u          /* CONFIG_HEADER_SIZE_UDPIPETH (definitions.h:176) */
+#define UDP_PORT 8998        /* the datagram applications' port (test_phold.c's) */
 #define MSS (MTU - HDR_TCP)
 
 /* ProtocolTCPFlags (protocol.h:23-31) */
@@ -91,7 +93,9 @@ typedef struct opkt {
     double prio;
     uint8_t st[128]; uint32_t nst;
     int32_t owner;               /* host whose active events print its lines (-2: none) */
+    int udp;                     /* a datagram (PUDP) */
 } opkt;
+static uint32_t hdr_of(const opkt* p) { return p->udp ? HDR_UDP : HDR_TCP; }   /* packet.c:318-323 */
 
 typedef struct { char* s; size_t len, cap; uint64_t n; } obuf;
 static void ob_put(obuf* b, const char* s, size_t n) {
@@ -324,6 +328,7 @@ static opkt* fq_pop(pqueue* q) {
 
 typedef struct osock {
     int32_t host, handle, proc;          /* proc: the process whose epoll watches it (-1) */
+    int udp, used;                       /* a datagram socket (udp.c); used: not released */
     uint32_t status;
     int bound; uint32_t bound_ip; uint16_t bound_port;
     uint32_t peer_ip; uint16_t peer_port;
@@ -361,6 +366,7 @@ typedef struct oproc {
     uint32_t wait_events, done;
     /* the process's epoll (epoll.c): one watch at a time */
     int ep_ready, ep_readable, ep_scheduled, ep_notifying;
+    int32_t app;                         /* >= 0: the datagram application cfg->app_spec[4 * app ..] */
 } oproc;
 
 typedef struct ohost_t {
@@ -445,6 +451,15 @@ static void ip_str(uint32_t ip, char* buf) {
 static void pkt_string(const opkt* p, obuf* b) {
     char s[20], d[20];
     ip_str(p->sip, s); ip_str(p->dip, d);
+    if (p->udp) {   /* PUDP (packet.c:535-548) */
+        ob_printf(b, "packetID=%u:%llu %s:%u -> %s:%u bytes=%u", p->host_id, (unsigned long long)p->pid, s, p->sport,
+                  d, p->dport, p->len);
+        if (p->nst) {
+            ob_printf(b, " status=");
+            for (uint32_t i = 0; i < p->nst; i++) ob_printf(b, i + 1 < p->nst ? "%s," : "%s", k_status_name[p->st[i]]);
+        }
+        return;
+    }
     ob_printf(b, "packetID=%u:%llu %s:%u -> %s:%u seq=%u ack=%u sack=", p->host_id, (unsigned long long)p->pid, s,
               p->sport, d, p->dport, p->seq, p->ack);
     int32_t first = -1, last = -1;
@@ -510,6 +525,7 @@ static void tcp_flush(osock* k);
 static void if_send_packets(int32_t h);
 static void sock_status(osock* k, uint32_t bits, int set);
 static void tcp_process(osock* k, opkt* p);
+static void udp_release(osock* k);
 
 static int32_t sidx(const osock* k) { return (int32_t)(k - G->s); }
 
@@ -774,9 +790,15 @@ static void reno_timeout(osock* k) {   /* :150-161 */
 
 /* ------------------------------------------------------------ the TCP socket */
 static int32_t sock_new(int32_t h) {   /* tcp_new (tcp.c:2452-2512) */
-    if (G->ns == G->caps) { fprintf(stderr, "o_tcp: socket table full\n"); abort(); }   /* never moves */
-    osock* k = &G->s[G->ns];
+    uint32_t si = 0;   /* a released datagram socket's slot first */
+    while (si < G->ns && G->s[si].used) si++;
+    if (si == G->ns) {
+        if (G->ns == G->caps) { fprintf(stderr, "o_tcp: socket table full\n"); abort(); }   /* never moves */
+        G->ns++;
+    }
+    osock* k = &G->s[si];
     memset(k, 0, sizeof(*k));
+    k->used = 1;
     k->host = h;
     k->handle = G->h[h].next_handle++;
     k->proc = -1;
@@ -796,7 +818,7 @@ static int32_t sock_new(int32_t h) {   /* tcp_new (tcp.c:2452-2512) */
     k->rtx.timers.cmp = cmp_time;
     k->rtx.tally.last_ack = -1;
     tcp_set_rto(k, 1000);
-    return (int32_t)G->ns++;
+    return (int32_t)si;
 }
 static uint32_t tcp_get_ip(osock* k) {   /* tcp.c:335-353 */
     if (k->server) return k->bound ? k->bound_ip : k->last_ip;
@@ -1300,27 +1322,31 @@ static void refill_if_needed(int32_t h) {   /* network_interface.c:130-161 (star
     }
 }
 static void consume(uint64_t* rem, uint64_t n) { *rem = (n >= *rem) ? 0 : *rem - n; }
-static osock* lookup_socket(int32_t h, uint16_t port, uint32_t peer_ip, uint16_t peer_port) {
+static osock* lookup_socket(int32_t h, int udp, uint16_t port, uint32_t peer_ip, uint16_t peer_port) {
     /* the general key (listeners) first, then the destination-specific one
-     * (network_interface.c:385-403) */
+     * (network_interface.c:385-403); keys are per protocol */
     for (uint32_t i = 0; i < G->ns; i++) {
         osock* k = &G->s[i];
-        if (k->host == h && k->assoc && k->assoc_general && k->bound_port == port) return k;
+        if (k->used && k->host == h && k->assoc && k->assoc_general && k->udp == udp && k->bound_port == port) return k;
     }
     for (uint32_t i = 0; i < G->ns; i++) {
         osock* k = &G->s[i];
-        if (k->host == h && k->assoc && !k->assoc_general && k->bound_port == port && k->peer_ip == peer_ip &&
-            k->peer_port == peer_port)
+        if (k->used && k->host == h && k->assoc && !k->assoc_general && k->udp == udp && k->bound_port == port &&
+            k->peer_ip == peer_ip && k->peer_port == peer_port)
             return k;
     }
     return NULL;
 }
 static void if_receive_packet(int32_t h, opkt* p) {   /* network_interface.c:375-419 */
     pkt_status(p, S_RCV_INTERFACE_RECEIVED);
-    osock* k = lookup_socket(h, p->dport, p->sip, p->sport);
+    osock* k = lookup_socket(h, p->udp, p->dport, p->sip, p->sport);
     if (k) {
         pkt_status(p, S_RCV_SOCKET_PROCESSED);   /* socket_pushInPacket (socket.c:140-145) */
-        tcp_process(k, p);
+        if (k->udp) {   /* udp_processPacket (udp.c:52-61) */
+            if (p->len > 0 && !sock_add_input(k, p)) pkt_status(p, S_RCV_SOCKET_DROPPED);
+        } else {
+            tcp_process(k, p);
+        }
     } else {
         pkt_status(p, S_RCV_INTERFACE_DROPPED);
     }
@@ -1340,7 +1366,7 @@ static void if_receive_packets(int32_t h) {   /* network_interface.c:421-455 */
         if (!have) break;
         opkt* p = G->pool[e.id];
         pkt_status(p, S_ROUTER_DEQUEUED);   /* router_dequeue (router.c:125-133) */
-        const uint64_t len = (uint64_t)p->len + HDR_TCP;
+        const uint64_t len = (uint64_t)p->len + hdr_of(p);
         if_receive_packet(h, p);
         pkt_unref(p);
         consume(&H->rx_rem, len);
@@ -1367,21 +1393,27 @@ static void if_send_packets(int32_t h) {   /* network_interface.c:519-579 */
     ohost_t* H = &G->h[h];
     while (H->tx_rem >= MTU) {
         opkt* p = NULL;
+        osock* drained = NULL;   /* left the sendable queue: a closed datagram socket is released after */
         if (G->cfg->qdisc_rr) {
             while (!p && H->rr_n) {   /* _networkinterface_selectRoundRobin (:466-490) */
                 osock* k = rr_pop(H);
                 p = sock_remove_output(k);
-                if (p) tcp_about_to_send(k, p);
+                if (p && !k->udp) tcp_about_to_send(k, p);   /* _networkinterface_updatePacketHeader */
                 if (sock_peek_out(k)) rr_push(H, k);
+                else drained = k;
             }
         }
         while (!p && H->fifo.n) {   /* _networkinterface_selectFirstInFirstOut (:492-517) */
             osock* k = pq_pop(&H->fifo);
             p = sock_remove_output(k);
-            if (p) tcp_about_to_send(k, p);
+            if (p && !k->udp) tcp_about_to_send(k, p);
             if (sock_peek_out(k)) pq_push(&H->fifo, k);
+            else drained = k;
         }
-        if (!p) break;
+        if (!p) {
+            if (drained) udp_release(drained);
+            break;
+        }
         pkt_status(p, S_SND_INTERFACE_SENT);
         if (p->dip == H->ip) {   /* our own interface (:548-555): a +1 ns task, no router, no bandwidth */
             pkt_ref(p);
@@ -1389,9 +1421,10 @@ static void if_send_packets(int32_t h) {   /* network_interface.c:519-579 */
         } else {
             worker_send_packet(h, p);
         }
-        consume(&H->tx_rem, (uint64_t)p->len + HDR_TCP);
+        consume(&H->tx_rem, (uint64_t)p->len + hdr_of(p));
         refill_if_needed(h);
         pkt_unref(p);
+        if (drained) udp_release(drained);
     }
 }
 static void refill_cb(int32_t h) {   /* network_interface.c:163-183 */
@@ -1411,16 +1444,26 @@ static uint16_t random_port(ohost_t* H) {   /* host.c:1058-1070 */
     uint16_t p = (uint16_t)pick;
     return (uint16_t)(p + 10000);
 }
-static int port_free(int32_t h, uint16_t port) {
-    for (uint32_t i = 0; i < G->ns; i++) if (G->s[i].host == h && G->s[i].assoc && G->s[i].bound_port == port) return 0;
+/* _host_isInterfaceAvailable (host.c:1029-1056) -> networkinterface_isAssociated
+ * (network_interface.c:279-301): the port is taken by a socket associated with
+ * no peer (the general key) or with this peer */
+static int port_free(int32_t h, int udp, uint16_t port, uint32_t pip, uint16_t pport) {
+    for (uint32_t i = 0; i < G->ns; i++) {
+        const osock* k = &G->s[i];
+        if (!k->used || k->host != h || !k->assoc || k->udp != udp || k->bound_port != port) continue;
+        if (k->assoc_general || (k->peer_ip == pip && k->peer_port == pport)) return 0;
+    }
     return 1;
 }
-static uint16_t random_free_port(int32_t h) {   /* host.c:1072-1110 */
+static uint16_t random_free_port(int32_t h, int udp, uint32_t pip, uint16_t pport) {   /* host.c:1072-1110 */
     ohost_t* H = &G->h[h];
-    for (int i = 0; i < 10; i++) { uint16_t p = random_port(H); if (port_free(h, p)) return p; }
+    for (int i = 0; i < 10; i++) { uint16_t p = random_port(H); if (port_free(h, udp, p, pip, pport)) return p; }
     const uint16_t start = random_port(H);
     uint16_t next = start == 65535 ? 10000 : (uint16_t)(start + 1);
-    while (next != start) { if (port_free(h, next)) return next; next = next == 65535 ? 10000 : (uint16_t)(next + 1); }
+    while (next != start) {
+        if (port_free(h, udp, next, pip, pport)) return next;
+        next = next == 65535 ? 10000 : (uint16_t)(next + 1);
+    }
     return 0;
 }
 static int tcp_connect_error(osock* k) {   /* tcp.c:1367-1390 */
@@ -1440,7 +1483,7 @@ static int host_connect(int32_t h, osock* k, uint32_t ip, uint16_t port) {   /* 
     double lat, rel;
     path(h, host_of_ip(ip), &lat, &rel);   /* topology_isRoutable */
     if (!k->bound) {
-        const uint16_t bp = random_free_port(h);
+        const uint16_t bp = random_free_port(h, 0, ip, port);
         k->bound = 1; k->bound_ip = G->h[h].ip; k->bound_port = bp;
         k->peer_ip = ip; k->peer_port = port;
         k->assoc = 1; k->assoc_general = 0;
@@ -1588,7 +1631,7 @@ static void app_run(oproc* pr) {
             osock* l = &G->s[li];
             pr->listenfd = li;
             /* bind INADDR_ANY:0 (host.c:1111-1189): a random free port */
-            l->bound = 1; l->bound_ip = 0; l->bound_port = random_free_port(h);
+            l->bound = 1; l->bound_ip = 0; l->bound_port = random_free_port(h, 0, 0, 0);
             l->assoc = 1; l->assoc_general = 1;
             /* listen (host.c:1284-1335, tcp.c:1486-1494) */
             l->server = 1;
@@ -1681,6 +1724,105 @@ static void app_continue(oproc* pr) {   /* process_continue on an epoll notifica
     app_run(pr);
 }
 
+/* ------------------------------------------------------------ datagram sockets (udp.c, host.c) */
+static int32_t udp_sock_new(int32_t h) {   /* host_createDescriptor(DT_UDPSOCKET) -> udp_new (udp.c:211-223) */
+    const int32_t si = sock_new(h);
+    osock* k = &G->s[si];
+    k->udp = 1;
+    k->status = DS_ACTIVE | DS_WRITABLE;
+    return si;
+}
+/* host_sendUserData (host.c:1466-1555): the implicit bind (:1514-1525), then
+ * udp_sendUserData (udp.c:75-142): one packet into the output buffer */
+static int udp_send_user(int32_t h, int32_t si, uint32_t n, uint32_t ip, uint16_t port) {
+    osock* k = &G->s[si];
+    if (k->status & DS_CLOSED) return 9;
+    if (!k->bound) {
+        const uint16_t bp = random_free_port(h, 1, 0, 0);
+        k->bound = 1; k->bound_ip = G->h[h].ip; k->bound_port = bp;
+        k->peer_ip = 0; k->peer_port = 0;
+        k->assoc = 1; k->assoc_general = 1;
+    }
+    if (out_space(k) < n) return ERR_EWOULDBLOCK;
+    opkt* p = pkt_new((uint32_t)h, n);
+    p->udp = 1;
+    p->sip = k->bound_ip ? k->bound_ip : G->h[h].ip;
+    p->sport = k->bound_port; p->dip = ip; p->dport = port;
+    pkt_status(p, S_SND_CREATED);
+    sock_add_output(k, p);
+    return 0;
+}
+/* a closed datagram socket with nothing left to send: released */
+static void udp_release(osock* k) {
+    if (!k->udp || !(k->status & DS_CLOSED) || k->out.n || k->outctl.n) return;
+    while (k->in.n) pkt_unref(fq_pop(&k->in));
+    free(k->in.p); free(k->out.p); free(k->outctl.p);
+    memset(k, 0, sizeof(*k));   /* used = 0 */
+}
+static void udp_close(int32_t si) {   /* descriptor_close -> udp_close -> host_closeDescriptor (host.c:768-771) */
+    osock* k = &G->s[si];
+    sock_status(k, DS_CLOSED, 1);
+    k->assoc = 0; k->assoc_general = 0;
+    udp_release(k);
+}
+/* the datagram application (oracle/ref_harness/ref_loop.c udp_send / udp_start /
+ * udp_continue, over test_phold.c's calls) */
+static void udp_app_send(oproc* pr, uint32_t rip, uint16_t rport) {
+    const int32_t h = pr->host;
+    const uint32_t* a = G->cfg->app_spec + 4u * (uint32_t)pr->app;
+    uint32_t ip;
+    uint16_t port = UDP_PORT;
+    if (a[1] == 0) {   /* _phold_chooseNode (test_phold.c:160-178): the first host whose weight reaches the draw */
+        const double r = o_next_double(&G->h[h].rng);
+        const double* cum = G->cfg->dest_cum;
+        if (G->cfg->host_class && G->cfg->n_classes > 1) cum += (size_t)G->cfg->host_class[h] * (size_t)G->cfg->n_hosts;
+        int32_t chosen = -1;
+        for (int32_t i = 0; i < G->cfg->n_hosts; i++)
+            if (cum[i] >= r) { chosen = i; break; }
+        if (chosen < 0) return;
+        ip = G->h[chosen].ip;
+    } else if (a[1] == 1) {
+        ip = G->h[G->cfg->app_peer[h]].ip;
+    } else {
+        ip = rip;
+        port = rport;
+    }
+    if (a[0] == 0) {   /* a socket per datagram: socket, sendto, close */
+        const int32_t si = udp_sock_new(h);
+        (void)udp_send_user(h, si, G->cfg->udp_payload, ip, port);
+        udp_close(si);
+    } else {
+        (void)udp_send_user(h, pr->listenfd, G->cfg->udp_payload, ip, port);
+    }
+}
+static void udp_app_start(oproc* pr) {
+    const int32_t h = pr->host;
+    const uint32_t* a = G->cfg->app_spec + 4u * (uint32_t)pr->app;
+    const int32_t li = udp_sock_new(h);
+    pr->listenfd = li;
+    if (a[0] != 1 && port_free(h, 1, UDP_PORT, 0, 0)) {   /* bind INADDR_ANY:8998 */
+        osock* l = &G->s[li];
+        l->bound = 1; l->bound_ip = 0; l->bound_port = UDP_PORT;
+        l->assoc = 1; l->assoc_general = 1;
+    }
+    app_wait(pr, li, 1);   /* epoll_ctl ADD, EPOLLIN: kept for the process's life */
+    for (uint32_t i = 0; i < a[2]; i++) udp_app_send(pr, 0, 0);
+}
+static void udp_app_continue(oproc* pr) {   /* every datagram, while epoll_wait reports the socket readable */
+    const uint32_t* a = G->cfg->app_spec + 4u * (uint32_t)pr->app;
+    while (watch_ready(pr)) {
+        for (;;) {
+            opkt* p = sock_remove_input(&G->s[pr->listenfd]);   /* udp_receiveUserData (udp.c:144-178) */
+            if (!p) break;
+            pkt_status(p, S_RCV_SOCKET_DELIVERED);
+            const uint32_t ip = p->sip;
+            const uint16_t port = p->sport;
+            pkt_unref(p);
+            if (a[3]) udp_app_send(pr, ip, port);
+        }
+    }
+}
+
 /* ------------------------------------------------------------ events */
 static void execute(const tev* e) {
     const int32_t h = (int32_t)e->dst;
@@ -1697,6 +1839,7 @@ static void execute(const tev* e) {
         oproc* pr = &G->p[e->obj];
         if (pr->running) break;
         pr->running = 1;
+        if (pr->app >= 0) { udp_app_start(pr); break; }
         pr->step = pr->peer < 0 ? T_SRV_START : T_CLI_START;
         app_run(pr);
         break;
@@ -1707,7 +1850,11 @@ static void execute(const tev* e) {
         if (!pr->running) break;
         if (pr->ep_ready) {
             pr->ep_notifying = 1;
-            app_continue(pr);
+            if (pr->app >= 0) {   /* the datagram application keeps its watch */
+                if (watch_ready(pr)) { pr->ep_ready = 0; pr->ep_readable = 0; udp_app_continue(pr); }
+            } else {
+                app_continue(pr);
+            }
             pr->ep_notifying = 0;
             pr->ep_ready = watch_ready(pr);
             pr->ep_readable = pr->ep_ready;
@@ -1722,7 +1869,7 @@ static void execute(const tev* e) {
         if (G->npool == G->cappool) { G->cappool = G->cappool ? 2 * G->cappool : 1024; G->pool = realloc(G->pool, G->cappool * sizeof(opkt*)); }
         const uint32_t id = G->npool++;
         G->pool[id] = p;
-        o_codel_enqueue(&H->codel, G->now, p->len + HDR_TCP, id, e->src);
+        o_codel_enqueue(&H->codel, G->now, p->len + hdr_of(p), id, e->src);
         pkt_ref(p);
         pkt_status(p, S_ROUTER_ENQUEUED);
         if (was_empty) if_receive_packets(h);
@@ -1782,7 +1929,7 @@ int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out) {
     const int32_t H = cfg->n_hosts;
     t.h = calloc((size_t)H, sizeof(ohost_t));
     t.p = calloc((size_t)(cfg->n_procs > 0 ? cfg->n_procs : 1), sizeof(oproc));
-    t.caps = (uint32_t)(4 * (cfg->n_procs > 0 ? cfg->n_procs : 1) + 16);
+    t.caps = (uint32_t)(4 * (cfg->n_procs > 0 ? cfg->n_procs : 1) + 16 + (cfg->proc_app ? 32 * H : 0));
     t.s = calloc(t.caps, sizeof(osock));
     for (int32_t i = 0; i < H; i++) {
         ohost_t* h = &t.h[i];
@@ -1802,6 +1949,7 @@ int o_tcp_run(const o_tcp_cfg* cfg, o_topo* topo, o_tcp_out* out) {
         oproc* pr = &t.p[k];
         pr->host = cfg->proc_host[k]; pr->index = k; pr->peer = cfg->proc_peer[k]; pr->start = cfg->proc_start[k];
         pr->fd = pr->listenfd = pr->wait_fd = -1;
+        pr->app = cfg->proc_app ? cfg->proc_app[k] : -1;
     }
     /* host_boot (host.c:372-390), every host at t = 0 in order */
     for (int32_t i = 0; i < H; i++) {

@@ -227,6 +227,14 @@ typedef struct o_tcp_cfg {
     uint32_t tcp_bytes, recv_buf, send_buf, tcp_window;
     uint32_t no_lines;                /* 1: keep the statuses, write no lines (bench.py's CPU baseline) */
     uint32_t qdisc_rr;                /* 1: the round-robin qdisc (network_interface.c:466-490) */
+    /* datagram processes beside the echo ones (shdtcp.h's shd_tcp_model fields) */
+    const int32_t* proc_app;          /* [P] -1 echo, else the application's index; NULL: none */
+    const uint32_t* app_spec;         /* [n][4] {send, dest, n_start, per_read} */
+    uint32_t udp_payload, _pad;
+    const int32_t* app_peer;          /* [H] */
+    const double* dest_cum;           /* [n_classes][H] */
+    const uint8_t* host_class;        /* [H] or NULL */
+    int32_t n_classes, _pad2;
 } o_tcp_cfg;
 typedef struct o_tcp_out {
     char* lines; size_t len; uint64_t n_lines;

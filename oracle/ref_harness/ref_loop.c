@@ -116,6 +116,11 @@ typedef struct ref_loop_cfg {
     const uint32_t* app_spec;
     const uint8_t* host_app;
     const int32_t* app_peer;
+    /* app 1 with datagram processes beside the TCP echo ones (one model, both
+     * transports on each host's interface): proc_app[k] >= 0 runs
+     * app_spec[4 * proc_app[k] ..] in process k instead of the echo (at most
+     * one such process per host: they share PHOLD's port); NULL: all echo */
+    const int32_t* proc_app;
 } ref_loop_cfg;
 
 typedef struct ref_loop_out {
@@ -275,6 +280,8 @@ struct _Process {
     gint listenfd;
     /* app 1 (TCP echo) */
     gint index, step, fd, wait_fd;
+    /* apps 3 and 1's datagram processes: {send, dest, n_start, per_read} */
+    const uint32_t* spec;
     guint32 done;
     gchar* buf;
 };
@@ -469,7 +476,7 @@ static const uint32_t* udp_spec(int32_t h) { return g_cfg->app_spec + 4u * g_cfg
 static void udp_send(Process* proc, in_addr_t rip, in_port_t rport) {
     Host* host = proc->host;
     const int32_t h = host_index_of(host_getID(host));
-    const uint32_t* a = udp_spec(h);
+    const uint32_t* a = proc->spec;
     in_addr_t ip;
     in_port_t port = htons(PHOLD_LISTEN_PORT);
     if (a[1] == 0) {
@@ -502,7 +509,7 @@ static void udp_send(Process* proc, in_addr_t rip, in_port_t rport) {
 
 static void udp_start(Process* proc) {
     Host* host = proc->host;
-    const uint32_t* a = udp_spec(host_index_of(host_getID(host)));
+    const uint32_t* a = proc->spec;
     proc->listenfd = host_createDescriptor(host, DT_UDPSOCKET);
     Descriptor* desc = host_lookupDescriptor(host, proc->listenfd);
     descriptor_setFlags(desc, descriptor_getFlags(desc) | O_NONBLOCK);
@@ -525,7 +532,7 @@ static void udp_start(Process* proc) {
 
 static void udp_continue(Process* proc) {
     Host* host = proc->host;
-    const uint32_t* a = udp_spec(host_index_of(host_getID(host)));
+    const uint32_t* a = proc->spec;
     for (;;) {
         struct epoll_event evs[10];
         gint nfds = 0;
@@ -702,10 +709,14 @@ static void process_start_task(Process* proc, gpointer nothing) {
     if (proc->running) return;
     worker_setActiveProcess(proc);
     proc->running = TRUE;
+    if (g_cfg->app == 1 && g_cfg->proc_app && proc->index >= 0 && g_cfg->proc_app[proc->index] >= 0)
+        proc->spec = g_cfg->app_spec + 4u * (uint32_t)g_cfg->proc_app[proc->index];
+    else if (g_cfg->app == 3)
+        proc->spec = udp_spec(host_index_of(host_getID(proc->host)));
     if (g_cfg->app == 0) phold_start(proc);
+    else if (proc->spec) udp_start(proc);
     else if (g_cfg->app == 1) tcp_start(proc);
     else if (g_cfg->app == 2) echo_start(proc);
-    else if (g_cfg->app == 3) udp_start(proc);
     worker_setActiveProcess(NULL);
 }
 static void process_stop_task(Process* proc, gpointer nothing) { process_stop(proc); }
@@ -733,9 +744,9 @@ void process_continue(Process* proc) {
     if (!process_isRunning(proc)) return;
     worker_setActiveProcess(proc);
     if (g_cfg->app == 0) phold_continue(proc);
+    else if (proc->spec) udp_continue(proc);
     else if (g_cfg->app == 1) tcp_continue(proc);
     else if (g_cfg->app == 2) echo_continue(proc);
-    else if (g_cfg->app == 3) udp_continue(proc);
     worker_setActiveProcess(NULL);
 }
 

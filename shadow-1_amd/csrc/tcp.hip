@@ -53,7 +53,12 @@ namespace {
 constexpr uint64_t kMs = 1000000ull;
 constexpr uint64_t kSec = 1000000000ull;
 constexpr uint32_t kMTU = 1500, kHdr = 66, kMSS = kMTU - kHdr;
-constexpr int kSock = 8;            // sockets per host (a listener, its children, clients)
+constexpr uint32_t kHdrUdp = 42;    // CONFIG_HEADER_SIZE_UDPIPETH (definitions.h:176)
+constexpr uint16_t kUdpPort = 8998; // the datagram applications' port (test_phold.c's PHOLD_LISTEN_PORT)
+constexpr uint32_t kDgramMax = 65507;   // CONFIG_DATAGRAM_MAX_SIZE (definitions.h:193)
+constexpr int kSock = 8;            // sockets per host (a listener, its children, clients); a model with
+                                    // datagram processes gets 2 * kSock (their per-datagram sockets wait at the
+                                    // interface): Glob::spk, never more than the qdisc queues hold
 constexpr int kProcs = 8;           // processes per host
 constexpr uint32_t kQ = 4096;       // per-socket packet queues
 constexpr uint32_t kQc = 256;       // control-packet queue
@@ -83,6 +88,8 @@ constexpr uint32_t kMailSack = 8;   // SACK entries per mailbox slot on average 
 constexpr uint32_t kPq = 8;         // vertex pairs a host remembers having queried (first-query log)
 constexpr uint32_t kTrk = 10;       // tracker counters per direction (DHost::trk)
 constexpr uint32_t kXRetx = 1;      // DPkt::xflags: the packet was retransmitted (PDS_SND_TCP_RETRANSMITTED)
+constexpr uint32_t kXUdp = 2;       // DPkt::xflags: a datagram (PUDP, packet.c:320-321)
+constexpr uint32_t kTrUdp = 1u << 31;   // TRec::flags: the record is a datagram's (packet_toString's PUDP form)
 constexpr uint32_t kLocalRanks = 6;  // path_cache mode: rows a lane can run in one round (more: fall back)
 constexpr int32_t kLocalRank0 = 0x7FFF0000;   // pseudo-ranks of a lane's in-round rows: past every real rank
 enum : uint32_t { kFtRowA = 0, kFtRowB = 1, kFtSelf = 2 };
@@ -160,7 +167,7 @@ struct RVec { uint32_t n; Rng64 r[kRanges]; };
 struct Tally { int64_t last_ack; uint64_t ndup; RVec marked, sacked, retx, lost, tmp; };
 
 struct DSock {   // every scalar first (a few lines per socket), then the containers
-    int32_t used, host, proc;
+    int32_t used, host, proc, udp;   // udp: a datagram socket (udp.c), else TCP
     uint32_t status;
     int32_t bound; uint32_t bound_ip; uint16_t bound_port, peer_port;
     uint32_t peer_ip;
@@ -202,6 +209,7 @@ struct DSock {   // every scalar first (a few lines per socket), then the contai
 };
 struct DProc {
     int32_t host, index, peer, running, step, fd, listenfd, wait_fd;
+    int32_t app, _pad;   // >= 0: the datagram application app_spec[4 * app ..] (else the TCP echo)
     uint32_t wait_events, done;
     int32_t ep_ready, ep_scheduled, ep_notifying;
     uint64_t start;
@@ -249,7 +257,7 @@ struct Glob {
     uint64_t end_time, hb, W, now_dummy;
     uint32_t tcp_bytes, trace, recv_buf, send_buf, tcp_window, _pad;
     DHost* host;
-    DSock* sock;            // [H][kSock]
+    DSock* sock;            // [H][spk]
     DProc* proc;            // [P]
     int32_t* host_procs;    // [H][kProcs]
     DPkt* pool;             // [H][pool_cap]
@@ -298,6 +306,15 @@ struct Glob {
     int32_t* ftord;         // [ft_cap] the log in serial order (scratch of k_tcp_window)
     uint32_t ft_cap; int32_t pT;
     uint32_t pcm, pc_complete, pc_prefer_direct, _pad6;
+    // the datagram processes (shd_tcp_model.proc_app): their applications
+    // {send, dest, n_start, per_read}, each host's SHD_DEST_PEER host, the
+    // SHD_DEST_WEIGHTED rows ([n_classes][H] cumulative) and class per host
+    const uint32_t* app_spec;
+    const int32_t* app_peer;
+    const double* dest_cum;
+    const uint8_t* host_class;
+    int32_t n_classes; uint32_t udp_payload;
+    int32_t spk, _pad7;     // sockets per host
 };
 
 // ------------------------------------------------------------ per-lane context
@@ -322,6 +339,9 @@ __device__ __forceinline__ int32_t* PSK(const L& c, int32_t i) {
     return c.g->psack + ((size_t)c.h * c.g->pool_cap + i) * kPktSack;
 }
 __device__ __forceinline__ int32_t sidx(const L& c, const DSock* k) { return (int32_t)(k - c.g->sock); }
+__device__ __forceinline__ DSock* SK(const L& c, int32_t j) { return &c.g->sock[(size_t)c.h * c.g->spk + j]; }
+// packet_getHeaderSize (packet.c:318-323)
+__device__ __forceinline__ uint32_t hdr_of(const DPkt* p) { return (p->xflags & kXUdp) ? kHdrUdp : kHdr; }
 
 __device__ int32_t rand_r_dev(uint32_t* state) {   // glibc rand_r (random.c's source)
     uint32_t next = *state;
@@ -514,7 +534,8 @@ __device__ void pkt_status(L& c, int32_t pi, uint8_t st) {   // packet_addDelive
     if (H->ntr >= kTr) { H->err |= SHD_TCP_ERR_TRACE; return; }
     TRec* r = &c.g->tr[(size_t)c.h * kTr + H->ntr++];
     r->time = c.now; r->host = c.active; r->status = st;
-    r->host_id = p->host_id; r->pid = p->pid; r->flags = p->flags; r->sip = p->sip; r->dip = p->dip;
+    r->host_id = p->host_id; r->pid = p->pid; r->flags = p->flags | ((p->xflags & kXUdp) ? kTrUdp : 0u);
+    r->sip = p->sip; r->dip = p->dip;
     r->sport = p->sport; r->dport = p->dport; r->seq = p->seq; r->ack = p->ack; r->win = p->win; r->len = p->len;
     r->tsval = p->tsval; r->tsecho = p->tsecho; r->nst = p->nst;
     for (uint32_t i = 0; i < p->nst; i++) r->st[i] = p->st[i];
@@ -619,6 +640,7 @@ struct SockLess {   // _networkinterface_compareSocket: never equal
 };
 
 __device__ void if_send_packets(L& c);
+__device__ void udp_release(L& c, DSock* k);
 __device__ bool sock_add_input(L& c, DSock* k, int32_t pi) {   // socket.c:319-343
     DPkt* p = PK(c, pi);
     if (p->len > in_space(k)) return false;
@@ -1041,9 +1063,14 @@ __device__ void reno_timeout(DSock* k) {
 // ------------------------------------------------------------ TCP
 __device__ int32_t sock_new(L& c) {   // host_createDescriptor + tcp_new (tcp.c:2452-2512)
     DHost* H = c.H;
-    if (H->nsock >= kSock) { H->err |= SHD_TCP_ERR_SOCKETS; return -1; }
-    const int32_t si = c.h * kSock + H->nsock++;
-    DSock* k = &c.g->sock[si];
+    int32_t j = 0;   // a released datagram socket's slot first (udp_release)
+    while (j < H->nsock && SK(c, j)->used) j++;
+    if (j == H->nsock) {
+        if (H->nsock >= c.g->spk) { H->err |= SHD_TCP_ERR_SOCKETS; return -1; }
+        H->nsock++;
+    }
+    DSock* k = SK(c, j);
+    const int32_t si = sidx(c, k);
     memset(k, 0, offsetof(DSock, outctl));   // the scalars
     k->used = 1; k->host = c.h; k->proc = -1; k->parent = -1; k->partial = -1;
     k->in.head = k->in.n = 0; k->out.head = k->out.n = 0; k->outctl.head = k->outctl.n = 0;
@@ -1559,14 +1586,16 @@ __device__ void refill_if_needed(L& c) {   // :130-161, started at t = 0
     }
 }
 __device__ __forceinline__ void consume(uint64_t& rem, uint64_t n) { rem = (n >= rem) ? 0 : rem - n; }
-__device__ DSock* lookup_socket(L& c, uint16_t port, uint32_t peer_ip, uint16_t peer_port) {   // :385-403
+// the association keys are (protocol, port, peer); general: peer 0:0
+__device__ DSock* lookup_socket(L& c, int32_t udp, uint16_t port, uint32_t peer_ip, uint16_t peer_port) {   // :385-403
     for (int32_t j = 0; j < c.H->nsock; j++) {
-        DSock* k = &c.g->sock[c.h * kSock + j];
-        if (k->assoc && k->assoc_general && k->bound_port == port) return k;
+        DSock* k = SK(c, j);
+        if (k->assoc && k->assoc_general && k->udp == udp && k->bound_port == port) return k;
     }
     for (int32_t j = 0; j < c.H->nsock; j++) {
-        DSock* k = &c.g->sock[c.h * kSock + j];
-        if (k->assoc && !k->assoc_general && k->bound_port == port && k->peer_ip == peer_ip && k->peer_port == peer_port)
+        DSock* k = SK(c, j);
+        if (k->assoc && !k->assoc_general && k->udp == udp && k->bound_port == port && k->peer_ip == peer_ip &&
+            k->peer_port == peer_port)
             return k;
     }
     return nullptr;
@@ -1633,7 +1662,7 @@ __device__ void tracker_add(L& c, int32_t pi, int dir) {
     if (!c.g->node) return;
     const DPkt* p = PK(c, pi);
     uint64_t* t = c.H->trk + kTrk * dir;
-    const uint64_t hdr = kHdr, pay = p->len;
+    const uint64_t hdr = hdr_of(p), pay = p->len;
     const bool rx = (p->xflags & kXRetx) != 0;
     if (pay > 0) {
         if (rx) { t[7]++; t[8] += hdr; t[9] += pay; }
@@ -1646,10 +1675,14 @@ __device__ void tracker_add(L& c, int32_t pi, int dir) {
 __device__ void if_receive_packet(L& c, int32_t pi) {   // _networkinterface_receivePacket (:375-419)
     const DPkt* p = PK(c, pi);
     pkt_status(c, pi, S_RCV_INTERFACE_RECEIVED);
-    DSock* k = lookup_socket(c, p->dport, p->sip, p->sport);
+    DSock* k = lookup_socket(c, (p->xflags & kXUdp) ? 1 : 0, p->dport, p->sip, p->sport);
     if (k) {
         pkt_status(c, pi, S_RCV_SOCKET_PROCESSED);   // socket_pushInPacket
-        tcp_process(c, k, pi);
+        if (k->udp) {   // udp_processPacket (udp.c:52-61)
+            if (p->len > 0 && !sock_add_input(c, k, pi)) pkt_status(c, pi, S_RCV_SOCKET_DROPPED);
+        } else {
+            tcp_process(c, k, pi);
+        }
     } else {
         pkt_status(c, pi, S_RCV_INTERFACE_DROPPED);
     }
@@ -1661,7 +1694,7 @@ __device__ void if_receive_packets(L& c) {   // :421-455
         CqEnt e;
         if (!cq_dequeue(c, e)) break;
         pkt_status(c, e.pkt, S_ROUTER_DEQUEUED);
-        const uint64_t len = (uint64_t)PK(c, e.pkt)->len + kHdr;
+        const uint64_t len = (uint64_t)PK(c, e.pkt)->len + hdr_of(PK(c, e.pkt));
         if_receive_packet(c, e.pkt);
         pkt_unref(c, e.pkt);
         consume(H->rx_rem, len);
@@ -1725,23 +1758,29 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
     while (H->tx_rem >= kMTU) {
         int32_t pi = -1;
         DSock* ks = nullptr;   // the socket the packet came from
+        DSock* drained = nullptr;   // ... left the sendable queue (a closed datagram socket is released after)
         while (c.g->qdisc_rr && pi < 0 && H->rrq.n) {   // _networkinterface_selectRoundRobin (:466-490)
             const int32_t si = rg_pop(H->rrq);
             DSock* k = &c.g->sock[si];
             ks = k;
             pi = sock_remove_output(c, k);
-            if (pi >= 0) tcp_about_to_send(c, k, pi);
+            if (pi >= 0 && !k->udp) tcp_about_to_send(c, k, pi);   // _networkinterface_updatePacketHeader (:457-463)
             if (sock_peek_out(c, k) >= 0) rg_push(H->rrq, si, H->err);
+            else drained = k;
         }
         while (pi < 0 && H->fifo.n) {   // _networkinterface_selectFirstInFirstOut (:492-517)
             const int32_t si = ih_pop(H->fifo, lt);
             DSock* k = &c.g->sock[si];
             ks = k;
             pi = sock_remove_output(c, k);
-            if (pi >= 0) tcp_about_to_send(c, k, pi);
+            if (pi >= 0 && !k->udp) tcp_about_to_send(c, k, pi);
             if (sock_peek_out(c, k) >= 0) ih_push(H->fifo, si, lt, H->err);
+            else drained = k;
         }
-        if (pi < 0) break;
+        if (pi < 0) {
+            if (drained) udp_release(c, drained);
+            break;
+        }
         pkt_status(c, pi, S_SND_INTERFACE_SENT);
         if (PK(c, pi)->dip == H->ip) {   // our own interface (:548-555): a +1 ns task, no router, no mailbox
             pkt_ref(c, pi);
@@ -1752,10 +1791,11 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
         } else {
             worker_send_packet(c, pi, ks);
         }
-        consume(H->tx_rem, (uint64_t)PK(c, pi)->len + kHdr);
+        consume(H->tx_rem, (uint64_t)PK(c, pi)->len + hdr_of(PK(c, pi)));
         refill_if_needed(c);
         tracker_add(c, pi, 1);   // :571
         pkt_unref(c, pi);
+        if (drained) udp_release(c, drained);
     }
 }
 __device__ void refill_cb(L& c) {   // :163-183
@@ -1774,18 +1814,25 @@ __device__ uint16_t random_port(L& c) {   // :1058-1070
     const double pick = round(f * (double)(65535 - 10000));
     return (uint16_t)((uint16_t)pick + 10000);
 }
-__device__ bool port_free(L& c, uint16_t port) {
+// _host_isInterfaceAvailable (host.c:1029-1056) -> networkinterface_isAssociated
+// (network_interface.c:279-301): the protocol's port is taken by a socket
+// associated with no peer (the general key) or with this peer
+__device__ bool port_free(L& c, int32_t udp, uint16_t port, uint32_t peer_ip, uint16_t peer_port) {
     for (int32_t j = 0; j < c.H->nsock; j++) {
-        const DSock* k = &c.g->sock[c.h * kSock + j];
-        if (k->assoc && k->bound_port == port) return false;
+        const DSock* k = SK(c, j);
+        if (!k->assoc || k->udp != udp || k->bound_port != port) continue;
+        if (k->assoc_general || (k->peer_ip == peer_ip && k->peer_port == peer_port)) return false;
     }
     return true;
 }
-__device__ uint16_t random_free_port(L& c) {   // :1072-1110
-    for (int i = 0; i < 10; i++) { const uint16_t p = random_port(c); if (port_free(c, p)) return p; }
+__device__ uint16_t random_free_port(L& c, int32_t udp, uint32_t pip, uint16_t pport) {   // :1072-1110
+    for (int i = 0; i < 10; i++) { const uint16_t p = random_port(c); if (port_free(c, udp, p, pip, pport)) return p; }
     const uint16_t start = random_port(c);
     uint16_t next = start == 65535 ? 10000 : (uint16_t)(start + 1);
-    while (next != start) { if (port_free(c, next)) return next; next = next == 65535 ? 10000 : (uint16_t)(next + 1); }
+    while (next != start) {
+        if (port_free(c, udp, next, pip, pport)) return next;
+        next = next == 65535 ? 10000 : (uint16_t)(next + 1);
+    }
     return 0;
 }
 __device__ int tcp_connect_error(DSock* k) {   // tcp.c:1367-1390
@@ -1903,12 +1950,143 @@ __device__ void tcp_close(L& c, DSock* k) {   // descriptor_close + tcp_close (t
     }
 }
 
+// ------------------------------------------------------------ datagram sockets (udp.c, host.c)
+// host_createDescriptor(DT_UDPSOCKET) -> udp_new (udp.c:211-223): active and
+// writable at once, the host's socket buffer sizes
+__device__ int32_t udp_sock_new(L& c) {
+    const int32_t si = sock_new(c);
+    if (si < 0) return -1;
+    DSock* k = &c.g->sock[si];
+    k->udp = 1;
+    k->in_size = c.g->recv_buf;
+    k->out_size = c.g->send_buf;
+    k->status = DS_ACTIVE | DS_WRITABLE;
+    return si;
+}
+// host_sendUserData (host.c:1466-1555) for a datagram socket: the implicit
+// bind of an unbound socket (a random free port on the default interface,
+// no peer: :1514-1525), then udp_sendUserData (udp.c:75-142): one packet of
+// n <= CONFIG_DATAGRAM_MAX_SIZE bytes into the socket's output buffer
+__device__ int udp_send_user(L& c, DSock* k, uint32_t n, uint32_t ip, uint16_t port) {
+    if (k->status & DS_CLOSED) return 9;   // EBADF
+    if (!k->bound) {
+        const uint16_t bp = random_free_port(c, 1, 0, 0);
+        if (!bp) return 99;   // EADDRNOTAVAIL
+        k->bound = 1; k->bound_ip = c.H->ip; k->bound_port = bp;
+        k->peer_ip = 0; k->peer_port = 0;
+        k->assoc = 1; k->assoc_general = 1;
+    }
+    if (out_space(k) < n) return E_WOULDBLOCK;
+    const int32_t pi = pkt_new(c, n);
+    if (pi < 0) return E_WOULDBLOCK;
+    DPkt* p = PK(c, pi);
+    p->xflags |= kXUdp;   // packet_setUDP (PUDP_NONE)
+    p->sip = k->bound_ip ? k->bound_ip : c.H->ip;   // INADDR_ANY: the default address
+    p->sport = k->bound_port; p->dip = ip; p->dport = port;
+    pkt_status(c, pi, S_SND_CREATED);
+    sock_add_output(c, k, pi);   // the buffer holds the packet's reference (space checked above)
+    return 0;
+}
+// host_receiveUserData -> udp_receiveUserData (udp.c:144-178): the next
+// datagram, its source address
+__device__ int udp_recv_user(L& c, DSock* k, uint32_t& sip, uint16_t& sport, uint32_t& n) {
+    const int32_t pi = sock_remove_input(c, k);
+    if (pi < 0) return E_WOULDBLOCK;
+    const DPkt* p = PK(c, pi);
+    n = p->len < 65536u ? p->len : 65536u;
+    pkt_status(c, pi, S_RCV_SOCKET_DELIVERED);
+    sip = p->sip; sport = p->sport;
+    pkt_unref(c, pi);
+    return 0;
+}
+// a closed datagram socket's last reference goes when it is neither in the
+// host's descriptors nor in the interface's sendable queue: its slot is
+// released (socket_free drops what its buffers still hold, socket.c:36-56)
+__device__ void udp_release(L& c, DSock* k) {
+    if (!k->udp || !(k->status & DS_CLOSED) || k->out.n || k->outctl.n) return;
+    while (k->in.n) pkt_unref(c, rg_pop(k->in));
+    k->used = 0;
+}
+// host_closeUser -> descriptor_close -> udp_close -> host_closeDescriptor
+// (host.c:768-771, 571-583): closed, no longer associated
+__device__ void udp_close(L& c, DSock* k) {
+    sock_status(c, k, DS_CLOSED, true);
+    k->assoc = 0; k->assoc_general = 0;
+    udp_release(c, k);
+}
+
 // ------------------------------------------------------------ the echo application (test_tcp.c:713-810)
 __device__ void app_wait(L& c, DProc* pr, int32_t fd, uint32_t events) {   // epoll_ctl ADD (epoll.c:411-433)
     pr->wait_fd = fd;
     pr->wait_events = events;
     c.g->sock[fd].proc = pr->index;
     ep_status_changed(c, pr);
+}
+
+// ------------------------------------------------------------ the datagram application
+// shd_udp_app (shdgpu.h) in a process, as the reference's loop runs it
+// (oracle/ref_harness/ref_loop.c udp_start / udp_send / udp_continue, over
+// test_phold.c's calls): a socket listening on PHOLD's port (SHD_SEND_EACH,
+// SHD_SEND_LISTENER) or bound by its first sendto (SHD_SEND_ONCE), one epoll
+// watch for reading it for the process's life; n_start datagrams at start,
+// one per datagram read when per_read
+__device__ void udp_app_send(L& c, DProc* pr, uint32_t rip, uint16_t rport) {
+    const uint32_t* a = c.g->app_spec + 4u * (uint32_t)pr->app;
+    uint32_t ip;
+    uint16_t port = kUdpPort;
+    if (a[1] == 0) {   // SHD_DEST_WEIGHTED: _phold_chooseNode (test_phold.c:160-178), the first
+                       // host whose cumulative weight reaches the draw (a lower bound: the rows ascend)
+        const double r = next_double(&c.H->rng);
+        const double* cum = c.g->dest_cum;
+        if (c.g->host_class && c.g->n_classes > 1) cum += (size_t)c.g->host_class[c.h] * (size_t)c.g->H;
+        int32_t lo = 0, hi = c.g->H;
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if (cum[mid] >= r) hi = mid; else lo = mid + 1;
+        }
+        if (lo >= c.g->H) return;   // none: _phold_sendToNode sends nothing
+        ip = c.g->host[lo].ip;
+    } else if (a[1] == 1) {   // SHD_DEST_PEER
+        ip = c.g->host[c.g->app_peer[c.h]].ip;
+    } else {                  // SHD_DEST_REPLY: recvfrom's address
+        ip = rip;
+        port = rport;
+    }
+    if (a[0] == 0) {   // SHD_SEND_EACH: socket, sendto (its implicit bind draws a port), close
+        const int32_t si = udp_sock_new(c);
+        if (si < 0) return;
+        DSock* k = &c.g->sock[si];
+        (void)udp_send_user(c, k, c.g->udp_payload, ip, port);
+        udp_close(c, k);
+    } else {
+        (void)udp_send_user(c, &c.g->sock[pr->listenfd], c.g->udp_payload, ip, port);
+    }
+}
+__device__ void udp_app_start(L& c, DProc* pr) {
+    const uint32_t* a = c.g->app_spec + 4u * (uint32_t)pr->app;
+    const int32_t li = udp_sock_new(c);
+    if (li < 0) { pr->step = T_DONE; return; }
+    pr->listenfd = li;
+    DSock* l = &c.g->sock[li];
+    if (a[0] != 1 && port_free(c, 1, kUdpPort, 0, 0)) {   // bind INADDR_ANY:8998 (host.c:1111-1189)
+        l->bound = 1; l->bound_ip = 0; l->bound_port = kUdpPort;
+        l->assoc = 1; l->assoc_general = 1;
+    }
+    app_wait(c, pr, li, 1);   // epoll_ctl ADD, EPOLLIN
+    for (uint32_t i = 0; i < a[2]; i++) udp_app_send(c, pr, 0, 0);
+}
+// every datagram the socket holds, while epoll_wait reports it readable
+__device__ void udp_app_continue(L& c, DProc* pr) {
+    const uint32_t* a = c.g->app_spec + 4u * (uint32_t)pr->app;
+    DSock* k = &c.g->sock[pr->listenfd];
+    for (int guard = 0; watch_ready(c, pr) && guard < (1 << 20); guard++) {
+        for (;;) {
+            uint32_t ip = 0, n = 0;
+            uint16_t port = 0;
+            if (udp_recv_user(c, k, ip, port, n) != 0 || n == 0) break;
+            if (a[3]) udp_app_send(c, pr, ip, port);
+        }
+    }
 }
 __device__ void app_run(L& c, DProc* pr) {
     const uint32_t N = c.g->tcp_bytes;
@@ -1920,7 +2098,7 @@ __device__ void app_run(L& c, DProc* pr) {
             DSock* l = &c.g->sock[li];
             sock_init_tcp(l, c.g->recv_buf, c.g->send_buf, c.g->tcp_window);
             pr->listenfd = li;
-            l->bound = 1; l->bound_ip = 0; l->bound_port = random_free_port(c);   // bind INADDR_ANY:0
+            l->bound = 1; l->bound_ip = 0; l->bound_port = random_free_port(c, 0, 0, 0);   // bind INADDR_ANY:0
             l->assoc = 1; l->assoc_general = 1;
             l->server = 1;   // listen (tcp.c:1486-1494)
             tcp_set_state(c, l, TS_LISTEN);
@@ -2005,7 +2183,7 @@ __device__ void app_run(L& c, DProc* pr) {
             }
             DSock* k = &c.g->sock[pr->fd];
             if (!k->bound) {   // implicit bind to the default interface, peer-specific
-                const uint16_t bp = random_free_port(c);
+                const uint16_t bp = random_free_port(c, 0, ip, port);
                 k->bound = 1; k->bound_ip = c.H->ip; k->bound_port = bp;
                 k->peer_ip = ip; k->peer_port = port;
                 k->assoc = 1; k->assoc_general = 0;
@@ -2054,6 +2232,7 @@ __device__ void execute(L& c, const DEv& e) {
         DProc* pr = &c.g->proc[e.obj];
         if (pr->running) break;
         pr->running = 1;
+        if (pr->app >= 0) { udp_app_start(c, pr); break; }
         pr->step = pr->peer < 0 ? T_SRV_START : T_CLI_START;
         app_run(c, pr);
         break;
@@ -2063,11 +2242,16 @@ __device__ void execute(L& c, const DEv& e) {
         pr->ep_scheduled = 0;
         if (!pr->running || !pr->ep_ready) break;
         pr->ep_notifying = 1;
-        if (watch_ready(c, pr)) {   // epoll_wait collects the event, then EPOLL_CTL_DEL
-            if (pr->wait_fd >= 0) c.g->sock[pr->wait_fd].proc = -1;
-            pr->wait_fd = -1;
-            pr->ep_ready = 0;
-            app_run(c, pr);
+        if (watch_ready(c, pr)) {
+            if (pr->app >= 0) {   // the datagram application keeps its watch
+                pr->ep_ready = 0;
+                udp_app_continue(c, pr);
+            } else {   // epoll_wait collects the event, then EPOLL_CTL_DEL
+                if (pr->wait_fd >= 0) c.g->sock[pr->wait_fd].proc = -1;
+                pr->wait_fd = -1;
+                pr->ep_ready = 0;
+                app_run(c, pr);
+            }
         }
         pr->ep_notifying = 0;
         pr->ep_ready = watch_ready(c, pr);
@@ -2085,7 +2269,7 @@ __device__ void execute(L& c, const DEv& e) {
         const bool was_empty = H->cq_n == 0;
         if (H->cq_n >= kCq) { H->err |= SHD_TCP_ERR_QUEUE; break; }
         CqEnt* q = &c.g->cq[(size_t)c.h * kCq + (H->cq_head + H->cq_n) % kCq];
-        q->ts = c.now; q->len = PK(c, e.pkt)->len + kHdr; q->pkt = e.pkt;
+        q->ts = c.now; q->len = PK(c, e.pkt)->len + hdr_of(PK(c, e.pkt)); q->pkt = e.pkt;
         H->cq_n++;
         H->cq_total += q->len;
         pkt_ref(c, e.pkt);
@@ -2413,6 +2597,20 @@ void format_line(std::string& o, const TRec& r, const int32_t* sacks, int32_t ho
     char buf[512], s[20], d[20];
     ip_str(r.sip, s);
     ip_str(r.dip, d);
+    if (r.flags & kTrUdp) {   // PUDP (packet.c:535-548)
+        snprintf(buf, sizeof(buf), "%llu\t%d\t[%s] packetID=%u:%llu %s:%u -> %s:%u bytes=%u", (unsigned long long)r.time,
+                 host, kStatusName[r.status], r.host_id, (unsigned long long)r.pid, s, r.sport, d, r.dport, r.len);
+        o += buf;
+        if (r.nst) {
+            o += " status=";
+            for (uint32_t i = 0; i < r.nst && i < kSt; i++) {
+                o += kStatusName[r.st[i]];
+                if (i + 1 < r.nst) o += ",";
+            }
+        }
+        o += "\n";
+        return;
+    }
     snprintf(buf, sizeof(buf), "%llu\t%d\t[%s] packetID=%u:%llu %s:%u -> %s:%u seq=%u ack=%u sack=",
              (unsigned long long)r.time, host, kStatusName[r.status], r.host_id, (unsigned long long)r.pid, s, r.sport, d,
              r.dport, r.seq, r.ack);
@@ -2469,7 +2667,7 @@ int32_t rand_r_host(uint32_t* state) {
 // that talk only to their peers: the same pairs the table path fills), in
 // both orientations' rows (either endpoint's may serve the pair; the window
 // only bounds the rounds), and whether some connection's pair has no route.
-// conn: (client vertex, server vertex, same host) triples.
+// conn: (client vertex, server vertex, same host, route required) quads.
 __global__ void k_tcp_pc_prep(const shd_pv* __restrict__ row, const shd_pv* __restrict__ self,
                               const shd_pv* __restrict__ dir, const uint8_t* __restrict__ adj, int complete,
                               int prefer_direct, int32_t T, const int32_t* __restrict__ conn, int32_t nconn,
@@ -2486,12 +2684,15 @@ __global__ void k_tcp_pc_prep(const shd_pv* __restrict__ row, const shd_pv* __re
     };
     unsigned long long w = ~0ull;
     for (int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x); k < nconn; k += (int32_t)(gridDim.x * blockDim.x)) {
-        const int32_t u = conn[3 * k], v = conn[3 * k + 1];
+        const int32_t u = conn[4 * k], v = conn[4 * k + 1];
         double l1, l2;
         lat_of(u, v, l1);
         lat_of(v, u, l2);
-        if (!(l1 >= 0) || !(l2 >= 0)) { atomicOr(out + 1, 1ull); continue; }
-        if (conn[3 * k + 2]) continue;   // a host's connection to itself: the loopback, no path
+        if (!(l1 >= 0) || !(l2 >= 0)) {
+            if (conn[4 * k + 3]) atomicOr(out + 1, 1ull);   // a connection's pair without a route
+            continue;
+        }
+        if (conn[4 * k + 2]) continue;   // a host's connection to itself: the loopback, no path
         const double l = l1 < l2 ? l1 : l2;
         const unsigned long long x = (unsigned long long)ceil(l * (double)kMs);
         w = x < w ? x : w;
@@ -2509,8 +2710,8 @@ static int tcp_pc_prep(shd_pc* pc, const std::vector<int32_t>& conn, uint64_t* W
     unsigned long long h_out[2] = {~0ull, 0ull};
     int rc = 0;
     const int32_t T = pc->T;
-    const int32_t nconn = (int32_t)(conn.size() / 3);
-    if (hipSetDevice(pc->device) != hipSuccess || hipMalloc(&d_conn, sizeof(int32_t) * (conn.size() + 3)) != hipSuccess ||
+    const int32_t nconn = (int32_t)(conn.size() / 4);
+    if (hipSetDevice(pc->device) != hipSuccess || hipMalloc(&d_conn, sizeof(int32_t) * (conn.size() + 4)) != hipSuccess ||
         hipMalloc(&d_out, 16) != hipSuccess ||
         (nconn && hipMemcpy(d_conn, conn.data(), sizeof(int32_t) * conn.size(), hipMemcpyHostToDevice) != hipSuccess) ||
         hipMemcpy(d_out, h_out, 16, hipMemcpyHostToDevice) != hipSuccess) {
@@ -2542,7 +2743,7 @@ enum WsSlot {
     kWsLat, kWsRel, kWsRank, kWsSrank, kWsNextRank, kWsFt, kWsFtord, kWsNft, kWsHv, kWsHost, kWsSock, kWsProc,
     kWsHostProcs, kWsPool, kWsPsack, kWsFreel, kWsEv, kWsCq, kWsMsack, kWsNmsack, kWsMail, kWsNmail, kWsMhead,
     kWsMnext, kWsCtl, kWsIpk, kWsNode, kWsTr, kWsTrs, kWsNextTime, kWsQlog, kWsNqlog, kWsProf, kWsProfRound,
-    kWsSlots
+    kWsAppSpec, kWsAppPeer, kWsDestCum, kWsHostClass, kWsSlots
 };
 struct TcpWs {
     std::mutex mu;
@@ -2605,9 +2806,31 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     // lookup reruns rows, topology.c:1987-1990: not restated on the device)
     if (pc && (!pc->built || pc->directed || (!pc->complete && !pc->d_row))) return -22;
     const int32_t H = m->n_hosts, P = m->n_procs;
+    auto app_of = [&](int32_t k) { return m->proc_app ? m->proc_app[k] : -1; };
+    bool any_udp = false;
     for (int32_t k = 0; k < P; k++) {
         if (m->proc_host[k] < 0 || m->proc_host[k] >= H) return -22;
         if (m->proc_peer[k] >= P || (m->proc_peer[k] >= 0 && m->proc_peer[m->proc_peer[k]] >= 0)) return -22;
+        // a client's server runs the echo; a datagram process has no echo peer
+        if (m->proc_peer[k] >= 0 && app_of(m->proc_peer[k]) >= 0) return -22;
+        if (app_of(k) >= 0 && m->proc_peer[k] >= 0) return -22;
+        any_udp |= app_of(k) >= 0;
+    }
+    if (any_udp) {   // the datagram processes' applications (shd_tcp_model's comment)
+        if (!m->app_spec || m->n_app_specs <= 0 || m->udp_payload < 1 || m->udp_payload > kDgramMax) return -22;
+        std::vector<uint8_t> seen(H, 0);
+        for (int32_t k = 0; k < P; k++) {
+            const int32_t a = app_of(k);
+            if (a < 0) continue;
+            if (a >= m->n_app_specs || seen[m->proc_host[k]]++) return -22;
+            const uint32_t* s = m->app_spec + 4 * (size_t)a;
+            if (s[0] > 2 || s[1] > 2 || s[3] > 1) return -22;
+            if (s[1] == 0 && !m->dest_cum) return -22;
+            if (s[1] == 1 && (!m->app_peer || m->app_peer[m->proc_host[k]] < 0 || m->app_peer[m->proc_host[k]] >= H))
+                return -22;
+        }
+        if (m->host_class && m->n_classes > 1)
+            for (int32_t a = 0; a < H; a++) if (m->host_class[a] >= m->n_classes) return -22;
     }
     const int32_t V = pc ? pc->T : m->n_vertices;
     std::vector<int32_t> hvi(H);   // each host's table index: the given one, or its attached index in the cache
@@ -2650,12 +2873,21 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     } else {
         // the same from the cache's device tables: either endpoint's row may
         // serve a pair, so both count (the window only bounds the rounds)
-        std::vector<int32_t> conn;
+        std::vector<int32_t> conn;   // (client vertex, server vertex, same host, route required)
         for (int32_t k = 0; k < P; k++)
             if (m->proc_peer[k] >= 0) {
                 const int32_t hc = m->proc_host[k], hs = m->proc_host[m->proc_peer[k]];
-                conn.push_back(hvi[hc]); conn.push_back(hvi[hs]); conn.push_back(hc == hs ? 1 : 0);
+                conn.push_back(hvi[hc]); conn.push_back(hvi[hs]); conn.push_back(hc == hs ? 1 : 0); conn.push_back(1);
             }
+        if (any_udp) {   // datagrams may go between any two hosts: every pair of their vertices bounds the window
+            for (int32_t u = 0; u < V; u++) {
+                if (!per_vertex[u]) continue;
+                for (int32_t v = u; v < V; v++) {
+                    if (!per_vertex[v] || (u == v && per_vertex[u] < 2)) continue;
+                    conn.push_back(u); conn.push_back(v); conn.push_back(0); conn.push_back(0);
+                }
+            }
+        }
         const int rr = tcp_pc_prep(pc, conn, &W);
         if (rr) return rr;
     }
@@ -2675,6 +2907,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     std::vector<int32_t> hp((size_t)H * kProcs, -1);
     shd_tcp_result* res = (shd_tcp_result*)calloc(1, sizeof(shd_tcp_result));
     double* d_lat = nullptr; double* d_rel = nullptr;
+    uint32_t* d_spec = nullptr; int32_t* d_apeer = nullptr; double* d_cum = nullptr; uint8_t* d_cls = nullptr;
     int32_t* d_hv = nullptr;
     uint64_t* d_ipk = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -2705,6 +2938,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         memset(&pr, 0, sizeof(pr));
         pr.host = m->proc_host[k]; pr.index = k; pr.peer = m->proc_peer[k]; pr.start = m->proc_start[k];
         pr.fd = pr.listenfd = pr.wait_fd = -1;
+        pr.app = app_of(k);
         int32_t* slot = &hp[(size_t)pr.host * kProcs];
         int j = 0;
         while (j < kProcs && slot[j] >= 0) j++;
@@ -2730,6 +2964,30 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
     if (m->qdisc > 1) { free(res); return -22; }
     g.qdisc_rr = m->qdisc;
+    g.spk = any_udp ? 2 * kSock : kSock;   // (the qdisc queues hold 2 * kSock sockets)
+    if (any_udp) {
+        g.udp_payload = m->udp_payload;
+        g.n_classes = m->n_classes;
+        const size_t ncum = (size_t)(m->host_class && m->n_classes > 1 ? m->n_classes : 1) * (size_t)H;
+        HCHECK(ws_alloc(ws, kWsAppSpec, &d_spec, sizeof(uint32_t) * 4 * (size_t)m->n_app_specs));
+        HCHECK(hipMemcpy(d_spec, m->app_spec, sizeof(uint32_t) * 4 * (size_t)m->n_app_specs, hipMemcpyHostToDevice));
+        g.app_spec = d_spec;
+        if (m->app_peer) {
+            HCHECK(ws_alloc(ws, kWsAppPeer, &d_apeer, sizeof(int32_t) * (size_t)H));
+            HCHECK(hipMemcpy(d_apeer, m->app_peer, sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
+            g.app_peer = d_apeer;
+        }
+        if (m->dest_cum) {
+            HCHECK(ws_alloc(ws, kWsDestCum, &d_cum, sizeof(double) * ncum));
+            HCHECK(hipMemcpy(d_cum, m->dest_cum, sizeof(double) * ncum, hipMemcpyHostToDevice));
+            g.dest_cum = d_cum;
+        }
+        if (m->host_class && m->n_classes > 1) {
+            HCHECK(ws_alloc(ws, kWsHostClass, &d_cls, (size_t)H));
+            HCHECK(hipMemcpy(d_cls, m->host_class, (size_t)H, hipMemcpyHostToDevice));
+            g.host_class = d_cls;
+        }
+    }
     if (!pc) {
         HCHECK(ws_alloc(ws, kWsLat, &d_lat, sizeof(double) * (size_t)V * V));
         HCHECK(ws_alloc(ws, kWsRel, &d_rel, sizeof(double) * (size_t)V * V));
@@ -2758,8 +3016,8 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     g.lat = d_lat; g.rel = d_rel; g.hv = d_hv; g.V = V; g.pool_cap = pool_cap;
     HCHECK(ws_alloc(ws, kWsHost, &g.host, sizeof(DHost) * H));
     HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * H, hipMemcpyHostToDevice));
-    HCHECK(ws_alloc(ws, kWsSock, &g.sock, sizeof(DSock) * (size_t)H * kSock));
-    HCHECK(hipMemset(g.sock, 0, sizeof(DSock) * (size_t)H * kSock));
+    HCHECK(ws_alloc(ws, kWsSock, &g.sock, sizeof(DSock) * (size_t)H * g.spk));
+    HCHECK(hipMemset(g.sock, 0, sizeof(DSock) * (size_t)H * g.spk));
     HCHECK(ws_alloc(ws, kWsProc, &g.proc, sizeof(DProc) * pp.size()));
     HCHECK(hipMemcpy(g.proc, pp.data(), sizeof(DProc) * pp.size(), hipMemcpyHostToDevice));
     HCHECK(ws_alloc(ws, kWsHostProcs, &g.host_procs, sizeof(int32_t) * hp.size()));

@@ -199,7 +199,10 @@ class TcpModel(C.Structure):
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
                 ("tcp_window", C.c_uint32), ("packets_per_host", C.c_uint32), ("qdisc", C.c_uint32),
-                ("_pad", C.c_uint32), ("path_cache", C.c_void_p)]
+                ("_pad", C.c_uint32), ("path_cache", C.c_void_p),
+                ("proc_app", P(C.c_int32)), ("app_spec", P(C.c_uint32)), ("n_app_specs", C.c_int32),
+                ("udp_payload", C.c_uint32), ("app_peer", P(C.c_int32)), ("dest_cum", P(C.c_double)),
+                ("host_class", P(C.c_uint8)), ("n_classes", C.c_int32), ("_pad2", C.c_int32)]
 
 
 class TcpResult(C.Structure):

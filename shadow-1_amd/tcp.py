@@ -68,12 +68,13 @@ def resolve(g: S.GraphArrays, att, first_queries, pairs, V):
     return lat, rel
 
 
-def path_table(model: S.ModelArrays, g: S.GraphArrays, procs, peers, reverse=False):
+def path_table(model: S.ModelArrays, g: S.GraphArrays, procs, peers, reverse=False, all_pairs=False):
     """Latency (ms) and reliability per pair of attached vertices ([V, V],
     V = the distinct vertices the hosts sit on) from the path cache, pairs
     resolved in the first guess of the first-touch order (clients by start
     time, each touching (client, server) first); pairs no connection uses stay
-    -1; reverse: the clients in reverse order (a wrong guess, for tests).
+    -1 (all_pairs: every pair is filled, for datagrams that may go anywhere);
+    reverse: the clients in reverse order (a wrong guess, for tests).
     Returns (lat, rel, host -> vertex index, attached vertices)."""
     m = model.struct
     H = int(m.n_hosts)
@@ -81,7 +82,9 @@ def path_table(model: S.ModelArrays, g: S.GraphArrays, procs, peers, reverse=Fal
     att, hvi = np.unique(hv, return_inverse=True)
     order = sorted(((p[1], k) for k, p in enumerate(procs) if peers[k] >= 0), reverse=reverse)
     q = [(hvi[procs[k][0]], hvi[procs[peers[k]][0]]) for _, k in order]
-    lat, rel = resolve(g, att, q, q, len(att))
+    V = len(att)
+    pairs = q + [(a, b) for a in range(V) for b in range(a, V)] if all_pairs else q
+    lat, rel = resolve(g, att, q, pairs, V)
     return lat, rel, hvi.astype(np.int32), att
 
 
@@ -97,7 +100,7 @@ def serial_first_queries(queries: np.ndarray):
 
 def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000, trace=True,
         recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0, guess_reversed=False,
-        node=False, qdisc=0, mode="device"):
+        node=False, qdisc=0, mode="device", udp=None):
     """Run the TCP echo model on the GPU: procs = [(host, start ns)], peers =
     [-1 | server process]; ips: host-order uint32 per host.  Returns
     dict(lines=[(t, h, line)] in each host's order, next_event_id,
@@ -107,7 +110,12 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
     host), from the library's writer).
     mode "device": the path cache's first-touch rule on the device (falls back
     to "tables" when a round's choice is contradicted, or on a directed graph);
-    guess_reversed: the table path from a wrong first-touch guess (tests)."""
+    guess_reversed: the table path from a wrong first-touch guess (tests).
+    udp: dict(apps=[-1 | spec index per process], specs=[(send, dest,
+    n_start, per_read)], app_peer=[H], payload=bytes) -- the processes with
+    an index run that datagram application (shd_tcp_model.proc_app) instead
+    of the echo; the model's dest_cum / host_class give SHD_DEST_WEIGHTED's
+    weights."""
     if mode == "device" and not guess_reversed and not g.directed:
         m = model.struct
         H = int(m.n_hosts)
@@ -117,7 +125,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
         pc_ms = (time.perf_counter() - t_pc) * 1e3
         try:
             out = _run_once(model, ips, procs, peers, None, None, hv.astype(np.int32), nbytes, trace, recv_buf,
-                            send_buf, tcp_window, packets_per_host, node, qdisc, pc=pc)
+                            send_buf, tcp_window, packets_per_host, node, qdisc, pc=pc, udp=udp)
         finally:
             pc.close()
         if out is not None:
@@ -125,11 +133,11 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
             out["first_touch"] = "device"
             out["host_ms"]["path_cache"] = pc_ms
             return out
-    lat, rel, hvi, att = path_table(model, g, procs, peers, reverse=guess_reversed)
+    lat, rel, hvi, att = path_table(model, g, procs, peers, reverse=guess_reversed, all_pairs=udp is not None)
     V = lat.shape[0]
     for runs in range(1, 9):
         out = _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-                        packets_per_host, node, qdisc)
+                        packets_per_host, node, qdisc, udp=udp)
         order, pairs = serial_first_queries(out.pop("queries"))
         lat2, rel2 = resolve(g, att, order, pairs, V)
         ij = tuple(np.array([(a, b) for a, b in pairs] + [(b, a) for a, b in pairs], dtype=np.int64).T) \
@@ -148,7 +156,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
 
 
 def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-              packets_per_host, node=False, qdisc=0, pc=None):
+              packets_per_host, node=False, qdisc=0, pc=None, udp=None):
     """one shd_tcp_run on the given path tables, or with pc (sim.PathCache) on
     the cache itself (hvi: graph vertices then); None when that run's
     first-touch choices were contradicted (SHD_TCP_ERR_FIRST_TOUCH)"""
@@ -184,6 +192,18 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
     tm.qdisc = int(qdisc)   # --interface-qdisc: 0 fifo, 1 rr
     if pc is not None:
         tm.path_cache = pc.ptr.value
+    if udp is not None:
+        keep["pa"] = np.ascontiguousarray(udp["apps"], dtype=np.int32)
+        keep["sp"] = np.ascontiguousarray([[int(x) for x in a] for a in udp["specs"]], dtype=np.uint32).ravel()
+        keep["ap"] = np.ascontiguousarray(udp.get("app_peer", [-1] * H), dtype=np.int32)
+        tm.proc_app = S.as_ptr(keep["pa"], C.c_int32)
+        tm.app_spec = S.as_ptr(keep["sp"], C.c_uint32)
+        tm.n_app_specs = len(udp["specs"])
+        tm.udp_payload = int(udp.get("payload", m.payload or 1))
+        tm.app_peer = S.as_ptr(keep["ap"], C.c_int32)
+        tm.dest_cum = m.dest_cum
+        tm.host_class = m.host_class
+        tm.n_classes = m.n_classes
     res = C.POINTER(S.TcpResult)()
     bits = (S.TCP_TRACE_STATUS if trace else 0) | (S.TCP_TRACE_NODE if node else 0)
     S.check(S.lib().shd_tcp_run(C.byref(tm), bits, C.byref(res)), "shd_tcp_run")

@@ -357,3 +357,38 @@ def tcp_echo_model(n_hosts: int, n_vertices: int, *, seed: int = 1, end_s: int =
     procs = [(2 * i, S.SHD_SEC) for i in range(n)] + [(2 * i + 1, 2 * S.SHD_SEC + i * 1000) for i in range(n)]
     peers = [-1] * n + [(i + n // 2) % n for i in range(n)]
     return g, m, ips, procs, peers, nbytes
+
+
+def mixed_transport_model(n_hosts: int, n_vertices: int, *, seed: int = 1, end_s: int = 12, nbytes: int = 60000,
+                          loss_max: float = 0.0, payload: int = 512, bw_down=10240, bw_up=10240):
+    """tcp_echo_model's echo pairs plus one datagram process per host
+    (shd_tcp_model.proc_app, shdgpu.h shd_udp_app), from 1 s + h us, by h % 4:
+    0 PHOLD-like (a socket per datagram to a weighted host's listener, 2 at
+    start, one per datagram read), 1 a listener sending to its peer h + 1 (2 at
+    start, one per read), 2 a listener answering each datagram to its sender,
+    3 a connected-style client (one implicitly bound socket) of host h - 1's
+    listener.  Both transports share each host's interface.  Returns (graph,
+    model, ips, procs, peers, nbytes, udp) with udp as shadow-1_amd/tcp.py's
+    run() takes it."""
+    g, _, ips, procs, peers, nb = tcp_echo_model(n_hosts, n_vertices, seed=seed, end_s=end_s, nbytes=nbytes,
+                                                 loss_max=loss_max, bw_down=bw_down, bw_up=bw_up)
+    H = len(ips)
+    hv = (np.arange(H, dtype=np.int64) * n_vertices // H).astype(np.int32)
+    m = phold_model(hv, end_time=end_s * S.SHD_SEC, seed=seed, load=0, payload=payload, bw_down=bw_down, bw_up=bw_up)
+    specs = [(S.SHD_SEND_EACH, S.SHD_DEST_WEIGHTED, 2, 1), (S.SHD_SEND_LISTENER, S.SHD_DEST_PEER, 2, 1),
+             (S.SHD_SEND_LISTENER, S.SHD_DEST_REPLY, 0, 1), (S.SHD_SEND_ONCE, S.SHD_DEST_PEER, 1, 1)]
+    app_peer = [-1] * H
+    apps = [-1] * len(procs)
+    for h in range(H):
+        k = h % 4
+        if k == 1 and h + 1 < H:
+            app_peer[h] = h + 1
+        elif k == 3:
+            app_peer[h] = h - 1
+        elif k == 1:
+            k = 2   # the last host has no peer after it: it answers instead
+        procs = procs + [(h, S.SHD_SEC + h * 1000)]
+        peers = peers + [-1]
+        apps.append(k)
+    udp = dict(apps=apps, specs=specs, app_peer=app_peer, payload=payload)
+    return g, m, ips, procs, peers, nb, udp

@@ -22,11 +22,12 @@ import tcp_cases as TC  # noqa: E402
 
 
 def main():
-    out = {}
-    for name in TC.CASES:
+    path = os.path.join(HERE, "ref_tcp.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    names = sys.argv[1:] or list(TC.CASES)
+    for name in names:
         c, m = TC.build(name)
-        r = R.run(m, c["graph"], procs=c["procs"], tcp=dict(peers=c["peers"], nbytes=c["nbytes"],
-                                                            qdisc=c.get("qdisc", 0)))
+        r = R.run(m, c["graph"], procs=c["procs"], tcp=TC.tcp_arg(c))
         st = TC.status_lines(r["lines"])
         hb = TC.node_lines(r["lines"])
         out[name] = dict(ips=r["ip"], n_status=len(st), status_sha256=TC.digest(st),
@@ -36,7 +37,7 @@ def main():
                          next_packet_id=[int(x) for x in r["next_packet_id"]],
                          rng_probe=[int(x) for x in r["rng_probe"]])
         print(name, len(st), flush=True)
-    with open(os.path.join(HERE, "ref_tcp.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -330,7 +330,11 @@ class TcpCfg(C.Structure):
                 ("proc_peer", C.POINTER(C.c_int32)),
                 ("end_time", C.c_uint64), ("heartbeat_interval", C.c_uint64),
                 ("tcp_bytes", C.c_uint32), ("recv_buf", C.c_uint32), ("send_buf", C.c_uint32),
-                ("tcp_window", C.c_uint32), ("no_lines", C.c_uint32), ("qdisc_rr", C.c_uint32)]
+                ("tcp_window", C.c_uint32), ("no_lines", C.c_uint32), ("qdisc_rr", C.c_uint32),
+                ("proc_app", C.POINTER(C.c_int32)), ("app_spec", C.POINTER(C.c_uint32)),
+                ("udp_payload", C.c_uint32), ("_pad", C.c_uint32), ("app_peer", C.POINTER(C.c_int32)),
+                ("dest_cum", C.POINTER(C.c_double)), ("host_class", C.POINTER(C.c_uint8)),
+                ("n_classes", C.c_int32), ("_pad2", C.c_int32)]
 
 
 class TcpOut(C.Structure):
@@ -340,12 +344,13 @@ class TcpOut(C.Structure):
 
 
 def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf=131072, tcp_window=10,
-            lines=True, qdisc=0):
+            lines=True, qdisc=0, udp=None):
     """The oracle's TCP echo run (o_tcp.c) on the model's hosts: procs = [(host,
     start)], peers = [-1 | server process]; ips: host-order uint32 per host.
     Returns dict(lines=[(t, h, line)], next_event_id, next_packet_id, rng_probe)
     with a delivery copy's release (host -1) put on its receiver, as the
-    reference-loop binding does."""
+    reference-loop binding does.  udp: as shadow-1_amd/tcp.py's (datagram
+    processes beside the echo ones)."""
     import numpy as np
     m = model.struct
     H = int(m.n_hosts)
@@ -376,6 +381,17 @@ def tcp_run(model, g, ips, procs, peers, nbytes=20000, recv_buf=174760, send_buf
     cfg.tcp_window = tcp_window
     cfg.no_lines = 0 if lines else 1
     cfg.qdisc_rr = int(qdisc)
+    if udp is not None:
+        pa = np.ascontiguousarray(udp["apps"], dtype=np.int32)
+        sp = np.ascontiguousarray([[int(x) for x in a] for a in udp["specs"]], dtype=np.uint32).ravel()
+        ap = np.ascontiguousarray(udp.get("app_peer", [-1] * H), dtype=np.int32)
+        cfg.proc_app = pa.ctypes.data_as(C.POINTER(C.c_int32))
+        cfg.app_spec = sp.ctypes.data_as(C.POINTER(C.c_uint32))
+        cfg.app_peer = ap.ctypes.data_as(C.POINTER(C.c_int32))
+        cfg.udp_payload = int(udp.get("payload", m.payload or 1))
+        cfg.dest_cum = m.dest_cum
+        cfg.host_class = m.host_class
+        cfg.n_classes = m.n_classes
     out = TcpOut()
     l = lib()
     l.o_tcp_run.argtypes = [C.POINTER(TcpCfg), C.c_void_p, C.POINTER(TcpOut)]

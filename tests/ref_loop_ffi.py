@@ -37,7 +37,8 @@ class Cfg(C.Structure):
                 ("path", C.c_void_p), ("path_ctx", C.c_void_p), ("root_dir", C.c_char_p),
                 ("proc_peer", P(C.c_int32)), ("tcp_bytes", C.c_uint32), ("_pad3", C.c_uint32),
                 ("quiet", C.c_int32), ("qdisc_rr", C.c_int32), ("mark_time", C.c_uint64 * 2),
-                ("app_spec", P(C.c_uint32)), ("host_app", P(C.c_uint8)), ("app_peer", P(C.c_int32))]
+                ("app_spec", P(C.c_uint32)), ("host_app", P(C.c_uint8)), ("app_peer", P(C.c_int32)),
+                ("proc_app", P(C.c_int32))]
 
 
 class Out(C.Structure):
@@ -102,7 +103,10 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
     procs: [(host, start)] processes in <process> order instead (the oracle's
     and the engine's pushed SHD_EV_APP_START events, in push order);
     tcp: dict(peers=[-1 | server process index per process], nbytes=N) runs
-    the TCP echo test (test_tcp.c) in those processes instead of PHOLD;
+    the TCP echo test (test_tcp.c) in those processes instead of PHOLD; with
+    apps=[-1 | index into specs per process], specs=[shd_udp_app-like
+    (send, dest, n_start, per_read)] and app_peer=[H] the processes with an
+    index run that datagram application instead (both transports in one model);
     echo: [H] -1 | server host runs the UDP request/response echo instead;
     marks: (t0, t1) simulated ns -> res["mark_wall_s"], the monotonic clock at
     the first send at or after each (the reference's own loop timed over a
@@ -145,6 +149,14 @@ def run_inproc(model: S.ModelArrays, g: S.GraphArrays, host_start=None, procs=No
         cfg.proc_peer = _ptr(pp, C.c_int32)
         cfg.tcp_bytes = int(tcp.get("nbytes", 20000))
         cfg.qdisc_rr = int(tcp.get("qdisc", 0))
+        if tcp.get("apps") is not None:
+            pa = np.ascontiguousarray(tcp["apps"], dtype=np.int32)
+            sp = np.ascontiguousarray([[int(x) for x in a] for a in tcp["specs"]], dtype=np.uint32).ravel()
+            ap = np.ascontiguousarray(tcp["app_peer"], dtype=np.int32)
+            keep += [pa, sp, ap]
+            cfg.proc_app = _ptr(pa, C.c_int32)
+            cfg.app_spec = _ptr(sp, C.c_uint32)
+            cfg.app_peer = _ptr(ap, C.c_int32)
     cfg.host_seed = m.host_rng
     cfg.host_vertex = m.host_vertex
     cfg.bw_down_kibps = m.bw_down_kibps

@@ -11,6 +11,14 @@ autotuning), 2 % loss on 500 kB (fast retransmit, SACK ranges), slow links
 (CoDel queues at the receiver), heavy loss (RTO backoff), ten pairs on a lossy
 geometric graph, hosts running several servers and clients at once, and a
 pair whose first touch comes from the server's side.
+
+The mixed_* cases put both transports in one model: besides the echo
+processes, processes running a datagram application (shdgpu.h shd_udp_app:
+send socket, destination rule, datagrams at start, one answer per datagram
+read) share the hosts' interfaces, qdiscs, buckets and CoDel queues with the
+TCP sockets (network_interface.c:519-579) -- run by the reference's loop with
+the same per-process applications (oracle/ref_harness/ref_loop.c, app 1 with
+proc_app).
 """
 import hashlib
 
@@ -81,6 +89,49 @@ def _loopback_mixed():
     return dict(graph=g, hv=[0, 3], procs=procs, peers=[-1, -1, -1, 0, 1, 2], nbytes=200000, end=60, bw={})
 
 
+EACH, ONCE, LISTENER = S.SHD_SEND_EACH, S.SHD_SEND_ONCE, S.SHD_SEND_LISTENER
+WEIGHTED, PEER, REPLY = S.SHD_DEST_WEIGHTED, S.SHD_DEST_PEER, S.SHD_DEST_REPLY
+
+
+def _mixed_hosts():
+    """five hosts on a lossy geometric graph: an echo pair (server on host 0,
+    client on host 1) and datagram processes -- host 0 PHOLD-like (a socket per
+    datagram to a weighted host's listener, one per datagram read: it shares
+    host 0's interface with the TCP server's child), hosts 2 and 3 a
+    listener pair (2 sends to its peer 3, 3 answers each datagram to its
+    sender), host 1 a connected-style client (one implicitly bound socket,
+    beside its TCP client: both draw ports from host 1's RNG), host 4 no
+    listener (datagrams for it are dropped at its interface)"""
+    g = W.geometric_graph(12, seed=5, loss_max=0.02)
+    procs = [(0, SEC), (1, 2 * SEC), (0, SEC + 500), (2, SEC), (3, SEC), (1, SEC + 300)]
+    peers = [-1, 0, -1, -1, -1, -1]
+    apps = [-1, -1, 0, 1, 2, 3]
+    specs = [(EACH, WEIGHTED, 3, 1), (LISTENER, PEER, 4, 1), (LISTENER, REPLY, 0, 1), (ONCE, PEER, 2, 1)]
+    return dict(graph=g, hv=[0, 4, 8, 11, 2], procs=procs, peers=peers, nbytes=300000, end=40, bw={},
+                apps=apps, specs=specs, app_peer=[-1, 0, 3, -1, -1], payload=700)
+
+
+def _mixed_slow_rr():
+    """mixed_hosts on slow links (256 KiB/s down, 512 up: the receivers' CoDel
+    queues fill) under the round-robin qdisc: the datagram sockets and the
+    TCP sockets take turns at each interface"""
+    c = _mixed_hosts()
+    c["bw"] = dict(bw_down=256, bw_up=512)
+    c["qdisc"] = 1
+    c["payload"] = 1200
+    return c
+
+
+def _mixed_loopback():
+    """one host with a loopback echo pair and a datagram listener sending to
+    its own address (the +1 ns loopback task for UDP too), a second host
+    PHOLD-like to both"""
+    procs = [(0, SEC), (0, 2 * SEC), (0, SEC + 10), (1, SEC)]
+    return dict(graph=_one_vertex(25.0, 0.0), hv=[0, 0], procs=procs, peers=[-1, 0, -1, -1], nbytes=100000, end=30,
+                bw={}, apps=[-1, -1, 0, 1], specs=[(LISTENER, PEER, 3, 0), (EACH, WEIGHTED, 2, 1)], app_peer=[0, -1],
+                payload=300)
+
+
 CASES = {
     "ref_epoll_lossless": lambda: _pair(50.0, 0.0, 20000, 300),
     "ref_epoll_lossy": lambda: _pair(50.0, 0.25, 20000, 300),
@@ -94,14 +145,35 @@ CASES = {
     "shared_hosts_rr": _shared_hosts_rr,
     "loopback_pair": _loopback_pair,
     "loopback_mixed": _loopback_mixed,
+    "mixed_hosts": _mixed_hosts,
+    "mixed_slow_rr": _mixed_slow_rr,
+    "mixed_loopback": _mixed_loopback,
 }
+
+# the cases with echo processes only (oracle/o_tcp.c restates TCP alone)
+ECHO_CASES = [n for n in CASES if not n.startswith("mixed_")]
 
 
 def build(name):
     c = CASES[name]()
     m = W.phold_model(np.asarray(c["hv"], dtype=np.int32), end_time=c["end"] * SEC, trace=True,
-                      queue_flags=S.SHD_QF_TRACE_STATUS, load=0, **c["bw"])
+                      queue_flags=S.SHD_QF_TRACE_STATUS, load=0, payload=c.get("payload", 1), **c["bw"])
     return c, m
+
+
+def udp_arg(c):
+    """tcp.run's udp argument of a case (None: echo processes only)"""
+    if "apps" not in c:
+        return None
+    return dict(apps=c["apps"], specs=c["specs"], app_peer=c["app_peer"], payload=c.get("payload", 1))
+
+
+def tcp_arg(c):
+    """ref_loop_ffi.run's tcp argument of a case"""
+    t = dict(peers=c["peers"], nbytes=c["nbytes"], qdisc=c.get("qdisc", 0))
+    if "apps" in c:
+        t.update(apps=c["apps"], specs=c["specs"], app_peer=c["app_peer"])
+    return t
 
 
 def status_lines(lines):

@@ -40,9 +40,18 @@ def test_tcp_gpu_equals_reference(name, mode):
     c, m = TC.build(name)
     ips = TC.ip_ints(f["ips"])
     r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], node=True, qdisc=c.get("qdisc", 0),
-                   mode=mode)
+                   mode=mode, udp=TC.udp_arg(c))
     assert r["first_touch"] == ("tables" if mode == "device" and name in DEVICE_FALLS_BACK else mode)
     got = r["lines"]
+    if "apps" in c and TC.digest(got) != f["status_by_host_sha256"]:
+        # both transports: the reference's loop itself locates the first difference where it was built
+        import ref_loop_ffi as R
+        if R.available():
+            want = TC.by_host(TC.status_lines(R.run(m, c["graph"], procs=c["procs"], tcp=TC.tcp_arg(c))["lines"]))
+            for i, (x, y) in enumerate(zip(got, want)):
+                assert x == y, (i, x, y)
+        assert len(got) == f["n_status"], (len(got), f["n_status"])
+        assert TC.digest(got) == f["status_by_host_sha256"]
     # the tracker's [node] lines: the library's writer over the device's counters
     assert len(r["node_lines"]) == f["n_heartbeat"]
     assert TC.digest(r["node_lines"]) == f["heartbeat_sha256"]
@@ -74,6 +83,28 @@ def test_tcp_gpu_scaled_model_equals_oracle(hosts, loss):
     assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
     assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
     assert r["events"] == o["events"] and r["deliveries"] > 0
+
+
+@pytest.mark.parametrize("hosts,loss,qdisc", [(96, 0.02, 0), (128, 0.01, 1)])
+def test_tcp_gpu_mixed_transports_equal_oracle(hosts, loss, qdisc):
+    """Both transports at a few hundred processes (workloads.
+    mixed_transport_model: the echo pairs plus a datagram process on every
+    host, four kinds of application): every host's [STATUS] lines and end
+    state equal the oracle's (oracle/o_tcp.c, pinned to the reference's loop
+    on the mixed_* fixtures), with the path cache on the device and on
+    tables."""
+    import workloads as W
+    g, m, ips, procs, peers, nb, udp = W.mixed_transport_model(hosts, 40, end_s=10, nbytes=60000, loss_max=loss)
+    o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb, qdisc=qdisc, udp=udp)
+    want = TC.by_host(o["lines"])
+    assert sum(" bytes=" in ln[2] and " seq=" not in ln[2] for ln in want) > 1000   # datagrams' lines
+    for mode in ("device", "tables"):
+        r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, qdisc=qdisc, udp=udp, mode=mode)
+        assert len(r["lines"]) == len(want) and r["lines"] == want, mode
+        assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
+        assert r["next_packet_id"].tolist() == o["next_packet_id"].tolist()
+        assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
+        assert r["events"] == o["events"]
 
 
 @pytest.mark.parametrize("hosts,loss", [(96, 0.02)])

@@ -27,7 +27,7 @@ FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
 def _oracle(name):
     c, m = TC.build(name)
     return O.tcp_run(m, c["graph"], TC.ip_ints(FIX[name]["ips"]), c["procs"], c["peers"], nbytes=c["nbytes"],
-                     qdisc=c.get("qdisc", 0))
+                     qdisc=c.get("qdisc", 0), udp=TC.udp_arg(c))
 
 
 @pytest.mark.parametrize("name", list(TC.CASES))
