@@ -137,6 +137,12 @@ typedef struct shd_tcp_result {
     double setup_ms, results_ms, teardown_ms;   /* the call's host wall time around the rounds:
                                                    allocation and upload, copies back and
                                                    formatting, release */
+    /* the hosts this result covers: [first_host, first_host + n_local_hosts)
+     * (shd_tcp_run: all of them; shd_tcp_run_group: this engine's share) --
+     * the per-host arrays above (next_event_id, next_packet_id, rng_probe,
+     * node_counters, n_heartbeats) and the lines are these hosts'; the lines
+     * carry the model's host index.  queries: every engine's. */
+    int32_t first_host, n_local_hosts;
 } shd_tcp_result;
 
 /* shd_tcp_run's `trace` bits */
@@ -159,6 +165,25 @@ enum {
  * and released by shd_tcp_result_free. */
 int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out);
 void shd_tcp_result_free(shd_tcp_result* r);
+
+/* The same model on a group of engines, one per process and GPU (shdgpu.h
+ * shd_comm: RCCL, or the host-memory transport for several processes on one
+ * GPU), every rank calling with the same model: rank r runs hosts
+ * [r * H / world, (r + 1) * H / world) -- the reference's rounds across
+ * workers (slave.c:437-462) with its hosts' events, both transports, the
+ * qdisc, buckets and CoDel queue on the engine that owns the host.  Each
+ * round's window starts at the earliest pending event over the group (an
+ * all-gather of one word per engine); after the round the deliveries for
+ * other engines' hosts go to them in one all-to-all of fixed segments
+ * (SHD_TCP_XCAP deliveries per engine pair and round, 4096 by default; more
+ * set SHD_TCP_ERR_MAILBOX), and the servers' listening ports their clients
+ * connect to are published to every engine.  Results equal shd_tcp_run's on
+ * the same model, host by host.  Tables only (path_cache NULL; -22 otherwise):
+ * the queries every engine logged come back in each rank's result, for the
+ * caller's first-touch ranking as on one engine.  Returns as shd_tcp_run, -5
+ * also when the group's communication fails. */
+struct shd_comm;
+int shd_tcp_run_group(const shd_tcp_model* m, struct shd_comm* comm, int32_t trace, shd_tcp_result** out);
 
 /* keep != 0: shd_tcp_run keeps its device buffers (the per-host event queues,
  * packet pools, sockets and mailboxes: tens of GB at 64 k hosts) for the next

@@ -249,6 +249,8 @@ struct TCtl {
     uint64_t max_mail;   // the most deliveries one round's mailbox took (shd_tcp_result)
     uint64_t max_ovf;    // ... and the most of them in its shared overflow range
     uint32_t ft_bad, _pad2;   // path_cache mode: a round's first-touch choice the serial order contradicts
+    uint64_t tmin;       // a group's round: this engine's earliest pending event (k_tcp_window, local)
+    uint32_t xerr, _pad3;   // a group's exchange failed: SHD_TCP_ERR_MAILBOX / _INTERNAL bits
 };
 
 struct Glob {
@@ -275,6 +277,7 @@ struct Glob {
     int32_t* mhead;         // [2][H] each destination's list of mails (-1: none)
     int32_t* mnext;         // [2][mail_cap] the next mail of the same destination
     uint32_t mail_cap, mail_part;   // slots in all; slots per part (the overflow: the rest)
+    uint32_t mail_stride, _pad8;    // a mailbox's slots: mail_cap, then a group's world * xcap from the others
     TCtl* ctl;
     const uint64_t* ip_key; // [ip_mask + 1] (ip << 32 | host), open addressing: host_of_ip's table
     uint32_t ip_mask, _pad5;
@@ -315,12 +318,33 @@ struct Glob {
     const uint8_t* host_class;
     int32_t n_classes; uint32_t udp_payload;
     int32_t spk, _pad7;     // sockets per host
+    // a run sharded over a group (shd_tcp_run_group): this engine's hosts
+    // [h0, h0 + nloc) of the model's H (the per-host arrays hold these; one
+    // engine: h0 = 0, nloc = H), every host's address and bandwidths, each
+    // process's listening port (its owner publishes it: port_new), and the
+    // round's deliveries for the other engines (per engine a segment: XSegHead,
+    // xcap mails, xsack_cap SACK words)
+    int32_t h0, nloc;
+    const uint32_t* ip_all;
+    const uint64_t* bwu_all;
+    const uint64_t* bwd_all;
+    uint32_t* proc_port;    // [P] 0: not listening (yet)
+    uint32_t* nport_new;    // [1] this round's publications ...
+    uint64_t* port_new;     // [kPortNew] ... (process << 32 | port)
+    char* xsend;            // [world] segments
+    int32_t world, me;
+    uint32_t xcap, xsack_cap;
+    size_t xseg;            // bytes per segment
 };
+constexpr uint32_t kPortNew = 256;   // listening ports one engine publishes in one round, at most
+struct XSegHead { uint32_t n, nsack, err, _pad[13]; };   // 64 B, then xcap Mails, then xsack_cap SACK words
+static_assert(sizeof(XSegHead) == 64, "segment header");
 
 // ------------------------------------------------------------ per-lane context
 struct L {
     const Glob* g;
-    int32_t h;
+    int32_t h;              // the lane's host: its index in this engine's per-host arrays
+    int32_t gh;             // ... and in the model (h0 + h): event keys, packet IDs, paths, logs
     DHost* H;
     uint64_t now;
     int32_t active;
@@ -517,7 +541,7 @@ __device__ DEv evq_pop(const L& c) {
 // event_new_ consumes the source's ID; scheduler_push drops past the end (scheduler.c:342-357)
 __device__ bool sched_task(L& c, uint64_t delay, uint32_t kind, int32_t obj) {
     DEv e;
-    e.time = c.now + delay; e.seq = c.H->ev_seq++; e.src = (uint32_t)c.h; e.kind = kind; e.obj = obj; e.pkt = -1;
+    e.time = c.now + delay; e.seq = c.H->ev_seq++; e.src = (uint32_t)c.gh; e.kind = kind; e.obj = obj; e.pkt = -1;
     if (e.time >= c.g->end_time) return false;
     evq_push(c, e);
     return true;
@@ -556,7 +580,7 @@ __device__ int32_t pkt_new(L& c, uint32_t len) {   // packet_new (packet.c:74-95
     DPkt* p = PK(c, i);
     memset(p, 0, c.g->trace ? sizeof(DPkt) : offsetof(DPkt, st));
     p->refs = 1;
-    p->host_id = (uint32_t)c.h + 1;
+    p->host_id = (uint32_t)c.gh + 1;
     p->pid = c.H->pkt_seq++;
     p->len = len;
     if (len > 0) p->prio = ++c.H->prio;   // host_getNextPacketPriority (host.c:1663-1666)
@@ -726,7 +750,7 @@ __device__ void touch_log(L& c, int32_t va, int32_t vb) {
     const uint32_t slot = atomicAdd(c.g->nqlog, 1u);
     if (slot >= c.g->qlog_cap) { H->err |= SHD_TCP_ERR_QLOG; return; }
     shd_tcp_query r;
-    r.time = c.now; r.seq = c.kseq; r.host = (uint32_t)c.h; r.src = c.ksrc; r.index = q;
+    r.time = c.now; r.seq = c.kseq; r.host = (uint32_t)c.gh; r.src = c.ksrc; r.index = q;
     r.v_src = va; r.v_dst = vb; r._pad = 0;
     c.g->qlog[slot] = r;
 }
@@ -756,7 +780,7 @@ __device__ void ft_log(L& c, int32_t va, int32_t vb, uint32_t choice) {
     const uint32_t slot = atomicAdd(c.g->nft, 1u);
     if (slot >= c.g->ft_cap) { c.H->err |= SHD_TCP_ERR_FIRST_TOUCH; return; }
     shd_tcp_query r;
-    r.time = c.now; r.seq = c.kseq; r.host = (uint32_t)c.h; r.src = c.ksrc; r.index = c.kq - 1;
+    r.time = c.now; r.seq = c.kseq; r.host = (uint32_t)c.gh; r.src = c.ksrc; r.index = c.kq - 1;
     r.v_src = va; r.v_dst = vb; r._pad = choice;
     c.g->ft[slot] = r;
 }
@@ -1107,7 +1131,7 @@ __device__ uint32_t tcp_get_peer_ip(const DSock* k) {
 }
 __device__ uint32_t src_ip_for(const L& c, const DSock* k, uint32_t dst) {
     uint32_t ip = tcp_get_ip(c, k);
-    if (ip == 0) ip = (dst == 0x7f000001u) ? 0x7f000001u : c.g->host[k->host].ip;
+    if (ip == 0) ip = (dst == 0x7f000001u) ? 0x7f000001u : c.g->ip_all[c.gh];
     return ip;
 }
 __device__ void tcp_update_rcv_window(DSock* k) { k->r_window = (uint32_t)(in_space(k) / kMSS); }   // tcp.c:762-782
@@ -1126,10 +1150,10 @@ __device__ void tcp_tune_initial_buffers(L& c, DSock* k) {   // tcp.c:441-533
     path(c, a, b, l1, r);   // _tcp_calculateRTT (tcp.c:363-405)
     path(c, b, a, l2, r);
     const uint32_t rtt = (uint32_t)ceil(l1) + (uint32_t)ceil(l2);
-    const DHost* A = &c.g->host[a];
-    const DHost* B = &c.g->host[b];
-    const uint32_t sbw = (uint32_t)A->bw_up < (uint32_t)B->bw_down ? (uint32_t)A->bw_up : (uint32_t)B->bw_down;
-    const uint32_t rbw = (uint32_t)A->bw_down < (uint32_t)B->bw_up ? (uint32_t)A->bw_down : (uint32_t)B->bw_up;
+    const uint32_t au = (uint32_t)c.g->bwu_all[a], ad = (uint32_t)c.g->bwd_all[a];
+    const uint32_t bu = (uint32_t)c.g->bwu_all[b], bd = (uint32_t)c.g->bwd_all[b];
+    const uint32_t sbw = au < bd ? au : bd;
+    const uint32_t rbw = ad < bu ? ad : bu;
     // float arithmetic as the reference writes it (tcp.c:504, 514)
     uint64_t sendbuf = (uint64_t)(((float)(rtt * sbw) * 1024.0f * 1.25f) / 1000.0f);
     uint64_t recvbuf = (uint64_t)(((float)(rtt * rbw) * 1024.0f * 1.25f) / 1000.0f);
@@ -1701,6 +1725,42 @@ __device__ void if_receive_packets(L& c) {   // :421-455
         refill_if_needed(c);
     }
 }
+// a delivery for another engine's host: its record (and SACK list) into that
+// engine's segment of the round's exchange (shd_tcp_run_group), taken by the
+// receiver before the next round (k_tcp_xingest)
+__device__ void xsend_mail(L& c, int32_t pi, int32_t d, uint64_t t, uint64_t seq) {
+    const Glob& g = *c.g;
+    const DPkt* p = PK(c, pi);
+    int32_t r = 0;   // the engine of host d: the contiguous split of shd_tcp_run_group
+    while (r + 1 < g.world && (int64_t)d >= ((int64_t)(r + 1) * g.H) / g.world) r++;
+    char* seg = g.xsend + (size_t)r * g.xseg;
+    XSegHead* hd = (XSegHead*)seg;
+    uint32_t off = 0;
+    if (p->nsack) {   // the SACK list's space first: a claimed mail slot is always written whole
+        off = atomicAdd(&hd->nsack, p->nsack);
+        if (off + p->nsack > g.xsack_cap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+        int32_t* dst = (int32_t*)(seg + sizeof(XSegHead) + (size_t)g.xcap * sizeof(Mail)) + off;
+        const int32_t* sk = PSK(c, pi);
+        for (uint32_t i = 0; i < p->nsack; i++) dst[i] = sk[i];
+    }
+    const uint32_t k = atomicAdd(&hd->n, 1u);
+    if (k >= g.xcap) { c.H->err |= SHD_TCP_ERR_MAILBOX; return; }
+    Mail* m = (Mail*)(seg + sizeof(XSegHead)) + k;
+    m->dst = (uint32_t)d; m->src = (uint32_t)c.gh; m->time = t; m->seq = seq;
+    m->sack_off = off;
+    pkt_copy_rec(&m->pkt, p, g.trace);
+    m->pkt.refs = 1;
+    m->pkt.inq = 0;
+}
+// a server's listening port, for its clients (DProc::peer) on any engine
+__device__ void publish_port(L& c, int32_t proc, uint16_t port) {
+    c.g->proc_port[proc] = port;
+    if (c.g->world > 1) {
+        const uint32_t k = atomicAdd(c.g->nport_new, 1u);
+        if (k >= kPortNew) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
+        c.g->port_new[k] = ((uint64_t)(uint32_t)proc << 32) | port;
+    }
+}
 __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:260-321
     DPkt* p = PK(c, pi);
     int32_t d;
@@ -1712,9 +1772,9 @@ __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:
         lat = ks->pc_lat; rel = ks->pc_rel;
     } else {
         d = host_of_ip(c, p->dip);
-        path(c, c.h, d, lat, rel);
+        path(c, c.gh, d, lat, rel);
         if (d >= 0 && lat >= 0.0 && !c.H->err) {
-            ks->pc_ip = p->dip; ks->pc_host = d; ks->pc_va = c.g->hv[c.h]; ks->pc_vb = c.g->hv[d];
+            ks->pc_ip = p->dip; ks->pc_host = d; ks->pc_va = c.g->hv[c.gh]; ks->pc_vb = c.g->hv[d];
             ks->pc_lat = lat; ks->pc_rel = rel;
         }
     }
@@ -1724,7 +1784,13 @@ __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:
         pkt_status(c, pi, S_INET_SENT);
         const uint64_t seq = c.H->ev_seq++;   // event_new_ (the delivery's ID)
         if (t >= c.g->end_time) return;
-        if (d == c.h) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
+        if (d == c.gh) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
+        if (t < c.mail_min) c.mail_min = t;   // folded into next_time[h] at the round's end
+        const int32_t dl = d - c.g->h0;
+        if (dl < 0 || dl >= c.g->nloc) {   // another engine's host: its segment of the round's exchange
+            xsend_mail(c, pi, d, t, seq);
+            return;
+        }
         const uint32_t part = (uint32_t)c.h % kMailSub, per = c.g->mail_part;
         const uint32_t kk = atomicAdd(c.g->n_out + part, 1u);
         uint32_t slot = part * per + kk;
@@ -1734,7 +1800,7 @@ __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:
             slot = per * kMailSub + ko;
         }
         Mail* m = &c.g->mail_out[slot];
-        m->dst = (uint32_t)d; m->src = (uint32_t)c.h; m->time = t; m->seq = seq;
+        m->dst = (uint32_t)dl; m->src = (uint32_t)c.gh; m->time = t; m->seq = seq;
         m->sack_off = 0;
         if (p->nsack) {   // the SACK list travels in the mailbox's arena
             const uint32_t off = atomicAdd(c.g->nmsack_out, p->nsack);
@@ -1746,8 +1812,7 @@ __device__ void worker_send_packet(L& c, int32_t pi, DSock* ks) {   // worker.c:
         pkt_copy_rec(&m->pkt, p, c.g->trace);   // packet_copy: the copy starts with one reference (the task's)
         m->pkt.refs = 1;
         m->pkt.inq = 0;   // the copy is in no queue of the receiver
-        c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[d], (int32_t)slot);   // the receiver's list
-        if (t < c.mail_min) c.mail_min = t;   // folded into next_time[h] at the round's end
+        c.g->mnext_out[slot] = atomicExch(&c.g->mhead_out[dl], (int32_t)slot);   // the receiver's list
     } else {
         pkt_status(c, pi, S_INET_DROPPED);
     }
@@ -1785,7 +1850,7 @@ __device__ void if_send_packets(L& c) {   // :519-579, FIFO qdisc
         if (PK(c, pi)->dip == H->ip) {   // our own interface (:548-555): a +1 ns task, no router, no mailbox
             pkt_ref(c, pi);
             DEv e;
-            e.time = c.now + 1; e.seq = H->ev_seq++; e.src = (uint32_t)c.h; e.kind = K_LOCAL; e.obj = -1; e.pkt = pi;
+            e.time = c.now + 1; e.seq = H->ev_seq++; e.src = (uint32_t)c.gh; e.kind = K_LOCAL; e.obj = -1; e.pkt = pi;
             if (e.time < c.g->end_time) evq_push(c, e);
             else pkt_unref(c, pi);   // scheduler_push refused it: the task's reference goes now
         } else {
@@ -2038,16 +2103,16 @@ __device__ void udp_app_send(L& c, DProc* pr, uint32_t rip, uint16_t rport) {
                        // host whose cumulative weight reaches the draw (a lower bound: the rows ascend)
         const double r = next_double(&c.H->rng);
         const double* cum = c.g->dest_cum;
-        if (c.g->host_class && c.g->n_classes > 1) cum += (size_t)c.g->host_class[c.h] * (size_t)c.g->H;
+        if (c.g->host_class && c.g->n_classes > 1) cum += (size_t)c.g->host_class[c.gh] * (size_t)c.g->H;
         int32_t lo = 0, hi = c.g->H;
         while (lo < hi) {
             const int32_t mid = (lo + hi) >> 1;
             if (cum[mid] >= r) hi = mid; else lo = mid + 1;
         }
         if (lo >= c.g->H) return;   // none: _phold_sendToNode sends nothing
-        ip = c.g->host[lo].ip;
+        ip = c.g->ip_all[lo];
     } else if (a[1] == 1) {   // SHD_DEST_PEER
-        ip = c.g->host[c.g->app_peer[c.h]].ip;
+        ip = c.g->ip_all[c.g->app_peer[c.gh]];
     } else {                  // SHD_DEST_REPLY: recvfrom's address
         ip = rip;
         port = rport;
@@ -2099,6 +2164,7 @@ __device__ void app_run(L& c, DProc* pr) {
             sock_init_tcp(l, c.g->recv_buf, c.g->send_buf, c.g->tcp_window);
             pr->listenfd = li;
             l->bound = 1; l->bound_ip = 0; l->bound_port = random_free_port(c, 0, 0, 0);   // bind INADDR_ANY:0
+            publish_port(c, pr->index, l->bound_port);
             l->assoc = 1; l->assoc_general = 1;
             l->server = 1;   // listen (tcp.c:1486-1494)
             tcp_set_state(c, l, TS_LISTEN);
@@ -2168,17 +2234,18 @@ __device__ void app_run(L& c, DProc* pr) {
             break;
         }
         case T_CLI_CONNECT: {   // host_connectToPeer (host.c:1191-1282), tcp_connectToPeer (tcp.c:1462-1484)
-            const DProc* sp = &c.g->proc[pr->peer];
-            if (sp->listenfd < 0) { pr->step = T_DONE; return; }
-            const int32_t sh = sp->host;
-            const uint32_t ip = c.g->host[sh].ip;
-            const uint16_t port = c.g->sock[sp->listenfd].bound_port;
+            // the server's port as test_tcp.c's message queue hands it over (its
+            // owner publishes it when it binds; none yet: the client gives up)
+            const uint32_t port = c.g->proc_port[pr->peer];
+            if (port == 0) { pr->step = T_DONE; return; }
+            const int32_t sh = c.g->proc[pr->peer].host;
+            const uint32_t ip = c.g->ip_all[sh];
             if (ip != c.H->ip) {   // topology_isRoutable (host.c:1224-1234): a first touch, value unused
                 if (c.g->pcm) {
                     double l_, r_;
-                    pc_query(c, c.g->hv[c.h], c.g->hv[sh], l_, r_);
+                    pc_query(c, c.g->hv[c.gh], c.g->hv[sh], l_, r_);
                 } else {
-                    touch_log(c, c.g->hv[c.h], c.g->hv[sh]);
+                    touch_log(c, c.g->hv[c.gh], c.g->hv[sh]);
                 }
             }
             DSock* k = &c.g->sock[pr->fd];
@@ -2327,9 +2394,9 @@ __global__ void k_tcp_free_init(int32_t* freel, size_t n, uint32_t cap) {
 // the loopback refill at +1 ms, then each process's start task
 __global__ void __launch_bounds__(64) k_tcp_boot(Glob g) {
     const int32_t h = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
-    if (h >= g.H) return;
+    if (h >= g.nloc) return;
     Glob gl = g;
-    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
+    L c{&gl, h, gl.h0 + h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
     sched_task(c, gl.hb, K_HEARTBEAT, -1);
     refill_cb(c);
     sched_task(c, kMs, K_REFILL_LO, -1);
@@ -2435,7 +2502,9 @@ __device__ bool ft_replay(const Glob& g, uint32_t n) {
     return s_bad != 0;
 }
 
-__global__ void k_tcp_window(Glob g) {
+// local: a group's round -- this engine's earliest pending event goes to
+// ctl->tmin and the host decides the window over the group (k_tcp_decide)
+__global__ void k_tcp_window(Glob g, int local) {
     __shared__ uint64_t red[16];
     TCtl* ctl = g.ctl;
     if (ctl->halted) return;
@@ -2468,7 +2537,7 @@ __global__ void k_tcp_window(Glob g) {
     __syncthreads();
     if (threadIdx.x == 0 && s_mail > ctl->max_mail) ctl->max_mail = s_mail;
     uint64_t t = ~0ull;
-    for (int32_t i = (int32_t)threadIdx.x; i <= g.H; i += (int32_t)blockDim.x) {
+    for (int32_t i = (int32_t)threadIdx.x; i <= g.nloc; i += (int32_t)blockDim.x) {
         const uint64_t x = g.next_time[i];
         t = x < t ? x : t;
     }
@@ -2480,15 +2549,94 @@ __global__ void k_tcp_window(Glob g) {
     __syncthreads();
     if (threadIdx.x == 0) {
         for (uint32_t w = 1; w < blockDim.x / 64; w++) t = red[w] < t ? red[w] : t;
-        if (t == ~0ull || t >= g.end_time) {
+        if (local) {
+            ctl->tmin = t;
+            g.next_time[g.nloc] = ~0ull;
+        } else if (t == ~0ull || t >= g.end_time) {
             ctl->halted = 1;
         } else {
             const uint64_t k = ctl->rounds;
             ctl->wend = t + g.W;
             ctl->rounds = k + 1;
-            g.next_time[g.H] = ~0ull;     // ... and so does its earliest delivery
+            g.next_time[g.nloc] = ~0ull;  // ... and so does its earliest delivery
         }
     }
+}
+
+// ---- a group's exchange (shd_tcp_run_group)
+// the window over the group: t (the min of the engines' ctl->tmin); the
+// segments and publications of the round start empty
+__global__ void k_tcp_decide(Glob g, uint64_t t) {
+    TCtl* ctl = g.ctl;
+    if (threadIdx.x == 0) {
+        if (ctl->halted) return;
+        if (t == ~0ull || t >= g.end_time) {
+            ctl->halted = 1;
+        } else {
+            ctl->wend = t + g.W;
+            ctl->rounds++;
+        }
+        *g.nport_new = 0;
+    }
+    if ((int)threadIdx.x < g.world) {
+        XSegHead* hd = (XSegHead*)(g.xsend + (size_t)threadIdx.x * g.xseg);
+        hd->n = 0; hd->nsack = 0; hd->err = 0;
+    }
+}
+// the deliveries the other engines sent this engine in the round just run:
+// into the round's output mailbox after its own slots (slot mail_cap + r *
+// xcap + i), each linked into its host's list, its SACK list into the arena
+__global__ void k_tcp_xingest(Glob g, const char* __restrict__ xrecv) {
+    const int32_t r = (int32_t)blockIdx.x;
+    if (r == g.me) return;
+    const TCtl* ctl = g.ctl;
+    const uint64_t k = ctl->rounds - 1;
+    const uint32_t out = (uint32_t)(k & 1) ^ 1u;
+    const char* seg = xrecv + (size_t)r * g.xseg;
+    const XSegHead* hd = (const XSegHead*)seg;
+    const uint32_t n = hd->n < g.xcap ? hd->n : g.xcap;
+    const Mail* src = (const Mail*)(seg + sizeof(XSegHead));
+    const int32_t* sks = (const int32_t*)(seg + sizeof(XSegHead) + (size_t)g.xcap * sizeof(Mail));
+    Mail* mail = g.mail + (size_t)out * g.mail_stride;
+    int32_t* mhead = g.mhead + (size_t)out * g.nloc;
+    int32_t* mnext = g.mnext + (size_t)out * g.mail_stride;
+    int32_t* msack = g.msack + (size_t)out * g.msack_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        Mail m = src[i];
+        const int32_t dl = (int32_t)m.dst - g.h0;
+        if (dl < 0 || dl >= g.nloc) { atomicOr(&g.ctl->xerr, (uint32_t)SHD_TCP_ERR_INTERNAL); continue; }
+        if (m.pkt.nsack) {
+            if (m.pkt.nsack > kPktSack || m.sack_off + m.pkt.nsack > g.xsack_cap) {
+                atomicOr(&g.ctl->xerr, (uint32_t)SHD_TCP_ERR_INTERNAL);
+                continue;
+            }
+            const uint32_t off = atomicAdd(g.nmsack + out, m.pkt.nsack);
+            if (off + m.pkt.nsack > g.msack_cap) { atomicOr(&g.ctl->xerr, (uint32_t)SHD_TCP_ERR_MAILBOX); continue; }
+            for (uint32_t j = 0; j < m.pkt.nsack; j++) msack[off + j] = sks[m.sack_off + j];
+            m.sack_off = off;
+        }
+        m.dst = (uint32_t)dl;
+        const uint32_t slot = g.mail_cap + (uint32_t)r * g.xcap + i;
+        mail[slot] = m;
+        mnext[slot] = atomicExch(&mhead[dl], (int32_t)slot);
+    }
+}
+// the listening ports the group's engines published in the last round
+// ([world][1 + kPortNew]: the count, then process << 32 | port)
+__global__ void k_tcp_ports(Glob g, const uint64_t* __restrict__ all) {
+    const int32_t r = (int32_t)blockIdx.x;
+    const uint64_t* a = all + (size_t)r * (1 + kPortNew);
+    const uint32_t n = (uint32_t)a[0] < kPortNew ? (uint32_t)a[0] : kPortNew;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t v = a[1 + i];
+        g.proc_port[(uint32_t)(v >> 32)] = (uint32_t)v;
+    }
+}
+// this engine's publications of the round, packed for the all-gather
+__global__ void k_tcp_ports_pack(Glob g, uint64_t* __restrict__ mine) {
+    const uint32_t n = *g.nport_new;
+    if (threadIdx.x == 0) mine[0] = n;
+    for (uint32_t i = threadIdx.x; i < n && i < kPortNew; i += blockDim.x) mine[1 + i] = g.port_new[i];
 }
 
 // a delivery from the round's input mailbox onto the host's heap (its packet
@@ -2522,24 +2670,24 @@ __global__ void __launch_bounds__(64) k_tcp_round(Glob g) {
     const uint32_t in = (uint32_t)(k & 1), out = in ^ 1u;
     if (threadIdx.x == 0) {
         gl = g;
-        gl.mail_in = g.mail + (size_t)in * g.mail_cap; gl.mhead_in = g.mhead + (size_t)in * g.H;
-        gl.mnext_in = g.mnext + (size_t)in * g.mail_cap;
-        gl.mail_out = g.mail + (size_t)out * g.mail_cap; gl.n_out = g.nmail + (size_t)out * (kMailSub + 1);
-        gl.mhead_out = g.mhead + (size_t)out * g.H; gl.mnext_out = g.mnext + (size_t)out * g.mail_cap;
+        gl.mail_in = g.mail + (size_t)in * g.mail_stride; gl.mhead_in = g.mhead + (size_t)in * g.nloc;
+        gl.mnext_in = g.mnext + (size_t)in * g.mail_stride;
+        gl.mail_out = g.mail + (size_t)out * g.mail_stride; gl.n_out = g.nmail + (size_t)out * (kMailSub + 1);
+        gl.mhead_out = g.mhead + (size_t)out * g.nloc; gl.mnext_out = g.mnext + (size_t)out * g.mail_stride;
         gl.msack_in = g.msack + (size_t)in * g.msack_cap; gl.msack_out = g.msack + (size_t)out * g.msack_cap;
         gl.nmsack_out = g.nmsack + out;
     }
     __syncthreads();
-    if (h >= g.H) return;
+    if (h >= g.nloc) return;
 #ifndef SHD_TCP_GLOBAL_HOST
     // the host's record lives in LDS for the round (every H-> access of its
     // events at LDS latency instead of a cache's): other lanes read only its
     // fixed fields (ip, bandwidths, refills) from the global copy
     __shared__ DHost s_host[64];
     s_host[threadIdx.x] = gl.host[h];
-    L c{&gl, h, &s_host[threadIdx.x], 0, h, 0, 0, 0, ~0ull};
+    L c{&gl, h, gl.h0 + h, &s_host[threadIdx.x], 0, h, 0, 0, 0, ~0ull};
 #else
-    L c{&gl, h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
+    L c{&gl, h, gl.h0 + h, &gl.host[h], 0, h, 0, 0, 0, ~0ull};
 #endif
 #ifdef SHD_TCP_PROF
     uint64_t* pf = gl.prof + (size_t)h * 2 * kProf;
@@ -2743,7 +2891,8 @@ enum WsSlot {
     kWsLat, kWsRel, kWsRank, kWsSrank, kWsNextRank, kWsFt, kWsFtord, kWsNft, kWsHv, kWsHost, kWsSock, kWsProc,
     kWsHostProcs, kWsPool, kWsPsack, kWsFreel, kWsEv, kWsCq, kWsMsack, kWsNmsack, kWsMail, kWsNmail, kWsMhead,
     kWsMnext, kWsCtl, kWsIpk, kWsNode, kWsTr, kWsTrs, kWsNextTime, kWsQlog, kWsNqlog, kWsProf, kWsProfRound,
-    kWsAppSpec, kWsAppPeer, kWsDestCum, kWsHostClass, kWsSlots
+    kWsAppSpec, kWsAppPeer, kWsDestCum, kWsHostClass, kWsIpAll, kWsBwu, kWsBwd, kWsProcPort, kWsPortNew, kWsXsend,
+    kWsXrecv, kWsPmine, kWsPall, kWsSlots
 };
 struct TcpWs {
     std::mutex mu;
@@ -2794,10 +2943,16 @@ extern "C" void shd_tcp_keep_workspace(int32_t keep) {
     (void)hipSetDevice(cur);
 }
 
-extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
+// shd_tcp_run on one engine (comm null) or on this engine's share of a group
+// (shd_tcp_run_group: hosts [h0, h0 + nloc), the round's window agreed over
+// the group, deliveries between engines exchanged after every round)
+static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, shd_tcp_result** out) {
     const auto t_call = std::chrono::steady_clock::now();
     auto t_results = t_call;
     shd_pc* pc = m ? m->path_cache : nullptr;
+    const int32_t world = comm ? comm->world : 1, me = comm ? comm->rank : 0;
+    // a group runs on tables (the device first-touch replay ranks one engine's log)
+    if (comm && pc) return -22;
     if (!m || !out || m->n_hosts <= 0 || m->n_hosts > (1 << 26) || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
         !m->bw_up_kibps || (!pc && (!m->path_lat_ms || !m->path_rel || m->n_vertices <= 0)) || !m->host_vertex ||
         (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
@@ -2806,6 +2961,9 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     // lookup reruns rows, topology.c:1987-1990: not restated on the device)
     if (pc && (!pc->built || pc->directed || (!pc->complete && !pc->d_row))) return -22;
     const int32_t H = m->n_hosts, P = m->n_procs;
+    if (world > H) return -22;
+    const int32_t h0 = (int32_t)(((int64_t)me * H) / world);
+    const int32_t nloc = (int32_t)(((int64_t)(me + 1) * H) / world) - h0;
     auto app_of = [&](int32_t k) { return m->proc_app ? m->proc_app[k] : -1; };
     bool any_udp = false;
     for (int32_t k = 0; k < P; k++) {
@@ -2902,9 +3060,9 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     const bool ws_keep = g_ws_keep;
     Glob g;
     memset(&g, 0, sizeof(g));
-    std::vector<DHost> hh(H);
+    std::vector<DHost> hh(nloc);
     std::vector<DProc> pp(P > 0 ? P : 1);
-    std::vector<int32_t> hp((size_t)H * kProcs, -1);
+    std::vector<int32_t> hp((size_t)nloc * kProcs, -1);
     shd_tcp_result* res = (shd_tcp_result*)calloc(1, sizeof(shd_tcp_result));
     double* d_lat = nullptr; double* d_rel = nullptr;
     uint32_t* d_spec = nullptr; int32_t* d_apeer = nullptr; double* d_cum = nullptr; uint8_t* d_cls = nullptr;
@@ -2917,17 +3075,19 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     TCtl hctl;
     std::vector<uint64_t> ipk;
     uint64_t rounds = 0;
-    std::vector<uint64_t> nt(H + 1);
-    std::vector<DHost> hout(H);
-    for (int32_t i = 0; i < H; i++) {
+    std::vector<DHost> hout(nloc);
+    uint32_t* d_ipall = nullptr; uint64_t* d_bwu = nullptr; uint64_t* d_bwd = nullptr;
+    char* d_xrecv = nullptr; uint64_t* d_pmine = nullptr; uint64_t* d_pall = nullptr;
+    for (int32_t i = 0; i < nloc; i++) {
         DHost& x = hh[i];
+        const int32_t gi = h0 + i;
         memset(&x, 0, sizeof(x));
-        x.ip = m->host_ip[i];
-        x.rng = m->host_seed[i];
-        x.bw_down = m->bw_down_kibps[i];
-        x.bw_up = m->bw_up_kibps[i];
-        x.tx_refill = m->bw_up_kibps[i] * 1024 / 1000;   // _networkinterface_setupTokenBuckets (:192-226)
-        x.rx_refill = m->bw_down_kibps[i] * 1024 / 1000;
+        x.ip = m->host_ip[gi];
+        x.rng = m->host_seed[gi];
+        x.bw_down = m->bw_down_kibps[gi];
+        x.bw_up = m->bw_up_kibps[gi];
+        x.tx_refill = m->bw_up_kibps[gi] * 1024 / 1000;   // _networkinterface_setupTokenBuckets (:192-226)
+        x.rx_refill = m->bw_down_kibps[gi] * 1024 / 1000;
         x.tx_cap = x.tx_refill + kMTU;
         x.rx_cap = x.rx_refill + kMTU;
         x.nfree = pool_cap;
@@ -2939,7 +3099,8 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         pr.host = m->proc_host[k]; pr.index = k; pr.peer = m->proc_peer[k]; pr.start = m->proc_start[k];
         pr.fd = pr.listenfd = pr.wait_fd = -1;
         pr.app = app_of(k);
-        int32_t* slot = &hp[(size_t)pr.host * kProcs];
+        if (pr.host < h0 || pr.host >= h0 + nloc) continue;   // another engine's
+        int32_t* slot = &hp[(size_t)(pr.host - h0) * kProcs];
         int j = 0;
         while (j < kProcs && slot[j] >= 0) j++;
         if (j == kProcs) { free(res); return -22; }
@@ -2959,6 +3120,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         }
     }
     g.H = H; g.P = P; g.W = W;
+    g.h0 = h0; g.nloc = nloc; g.world = world; g.me = me;
     g.end_time = m->end_time; g.hb = m->heartbeat_interval ? m->heartbeat_interval : kSec;
     g.tcp_bytes = m->tcp_bytes; g.trace = (trace & SHD_TCP_TRACE_STATUS) ? 1 : 0;
     g.recv_buf = m->recv_buf; g.send_buf = m->send_buf; g.tcp_window = m->tcp_window;
@@ -3011,26 +3173,53 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         HCHECK(ws_alloc(ws, kWsNft, &g.nft, sizeof(uint32_t)));
         HCHECK(hipMemset(g.nft, 0, sizeof(uint32_t)));
     }
+    HCHECK(ws_alloc(ws, kWsIpAll, &d_ipall, sizeof(uint32_t) * (size_t)H));
+    HCHECK(hipMemcpy(d_ipall, m->host_ip, sizeof(uint32_t) * (size_t)H, hipMemcpyHostToDevice));
+    HCHECK(ws_alloc(ws, kWsBwu, &d_bwu, sizeof(uint64_t) * (size_t)H));
+    HCHECK(hipMemcpy(d_bwu, m->bw_up_kibps, sizeof(uint64_t) * (size_t)H, hipMemcpyHostToDevice));
+    HCHECK(ws_alloc(ws, kWsBwd, &d_bwd, sizeof(uint64_t) * (size_t)H));
+    HCHECK(hipMemcpy(d_bwd, m->bw_down_kibps, sizeof(uint64_t) * (size_t)H, hipMemcpyHostToDevice));
+    g.ip_all = d_ipall; g.bwu_all = d_bwu; g.bwd_all = d_bwd;
+    HCHECK(ws_alloc(ws, kWsProcPort, &g.proc_port, sizeof(uint32_t) * pp.size()));
+    HCHECK(hipMemset(g.proc_port, 0, sizeof(uint32_t) * pp.size()));
+    HCHECK(ws_alloc(ws, kWsPortNew, &g.port_new, sizeof(uint64_t) * (kPortNew + 1)));
+    g.nport_new = (uint32_t*)(g.port_new + kPortNew);
+    HCHECK(hipMemset(g.port_new, 0, sizeof(uint64_t) * (kPortNew + 1)));
+    if (world > 1) {   // the exchange's segments (SHD_TCP_XCAP: deliveries per engine pair and round)
+        g.xcap = 4096;
+        if (const char* e = getenv("SHD_TCP_XCAP")) {
+            const long v = strtol(e, nullptr, 10);
+            if (v >= 16 && v <= (1l << 22)) g.xcap = (uint32_t)v;
+        }
+        g.xsack_cap = g.xcap * kMailSack;
+        g.xseg = sizeof(XSegHead) + (size_t)g.xcap * sizeof(Mail) + (size_t)g.xsack_cap * sizeof(int32_t);
+        g.xseg = (g.xseg + 255) & ~(size_t)255;
+        HCHECK(ws_alloc(ws, kWsXsend, &g.xsend, g.xseg * (size_t)world));
+        HCHECK(ws_alloc(ws, kWsXrecv, &d_xrecv, g.xseg * (size_t)world));
+        HCHECK(hipMemset(g.xsend, 0, g.xseg * (size_t)world));
+        HCHECK(ws_alloc(ws, kWsPmine, &d_pmine, sizeof(uint64_t) * (1 + kPortNew)));
+        HCHECK(ws_alloc(ws, kWsPall, &d_pall, sizeof(uint64_t) * (1 + kPortNew) * (size_t)world));
+    }
     HCHECK(ws_alloc(ws, kWsHv, &d_hv, sizeof(int32_t) * (size_t)H));
     HCHECK(hipMemcpy(d_hv, hvi.data(), sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
     g.lat = d_lat; g.rel = d_rel; g.hv = d_hv; g.V = V; g.pool_cap = pool_cap;
-    HCHECK(ws_alloc(ws, kWsHost, &g.host, sizeof(DHost) * H));
-    HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * H, hipMemcpyHostToDevice));
-    HCHECK(ws_alloc(ws, kWsSock, &g.sock, sizeof(DSock) * (size_t)H * g.spk));
-    HCHECK(hipMemset(g.sock, 0, sizeof(DSock) * (size_t)H * g.spk));
+    HCHECK(ws_alloc(ws, kWsHost, &g.host, sizeof(DHost) * nloc));
+    HCHECK(hipMemcpy(g.host, hh.data(), sizeof(DHost) * nloc, hipMemcpyHostToDevice));
+    HCHECK(ws_alloc(ws, kWsSock, &g.sock, sizeof(DSock) * (size_t)nloc * g.spk));
+    HCHECK(hipMemset(g.sock, 0, sizeof(DSock) * (size_t)nloc * g.spk));
     HCHECK(ws_alloc(ws, kWsProc, &g.proc, sizeof(DProc) * pp.size()));
     HCHECK(hipMemcpy(g.proc, pp.data(), sizeof(DProc) * pp.size(), hipMemcpyHostToDevice));
     HCHECK(ws_alloc(ws, kWsHostProcs, &g.host_procs, sizeof(int32_t) * hp.size()));
     HCHECK(hipMemcpy(g.host_procs, hp.data(), sizeof(int32_t) * hp.size(), hipMemcpyHostToDevice));
-    HCHECK(ws_alloc(ws, kWsPool, &g.pool, sizeof(DPkt) * (size_t)H * pool_cap));
-    HCHECK(ws_alloc(ws, kWsPsack, &g.psack, sizeof(int32_t) * kPktSack * (size_t)H * pool_cap));
-    HCHECK(ws_alloc(ws, kWsFreel, &g.freel, sizeof(int32_t) * (size_t)H * pool_cap));
-    k_tcp_free_init<<<(unsigned)(((size_t)H * pool_cap + 255) / 256), 256>>>(g.freel, (size_t)H * pool_cap, pool_cap);
+    HCHECK(ws_alloc(ws, kWsPool, &g.pool, sizeof(DPkt) * (size_t)nloc * pool_cap));
+    HCHECK(ws_alloc(ws, kWsPsack, &g.psack, sizeof(int32_t) * kPktSack * (size_t)nloc * pool_cap));
+    HCHECK(ws_alloc(ws, kWsFreel, &g.freel, sizeof(int32_t) * (size_t)nloc * pool_cap));
+    k_tcp_free_init<<<(unsigned)(((size_t)nloc * pool_cap + 255) / 256), 256>>>(g.freel, (size_t)nloc * pool_cap, pool_cap);
     HCHECK(hipGetLastError());
-    HCHECK(ws_alloc(ws, kWsEv, &g.ev, sizeof(DEv) * (size_t)H * kEv));
-    HCHECK(ws_alloc(ws, kWsCq, &g.cq, sizeof(CqEnt) * (size_t)H * kCq));
+    HCHECK(ws_alloc(ws, kWsEv, &g.ev, sizeof(DEv) * (size_t)nloc * kEv));
+    HCHECK(ws_alloc(ws, kWsCq, &g.cq, sizeof(CqEnt) * (size_t)nloc * kCq));
     {
-        const uint32_t parts = (uint32_t)H * 32u > kMailMin ? (uint32_t)H * 32u : kMailMin;
+        const uint32_t parts = (uint32_t)nloc * 32u > kMailMin ? (uint32_t)nloc * 32u : kMailMin;
         g.mail_part = parts / kMailSub;
         uint32_t ovf = g.mail_part * kMailSub / 2;
         // SHD_TCP_MAIL_PART: smaller parts (the same overflow range), so that a
@@ -3040,17 +3229,18 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
             if (v >= 1 && v < (long)g.mail_part) g.mail_part = (uint32_t)v;
         }
         g.mail_cap = g.mail_part * kMailSub + ovf;
+        g.mail_stride = g.mail_cap + (world > 1 ? (uint32_t)world * g.xcap : 0u);
     }
     g.msack_cap = g.mail_cap * kMailSack;
     HCHECK(ws_alloc(ws, kWsMsack, &g.msack, sizeof(int32_t) * 2 * (size_t)g.msack_cap));
     HCHECK(ws_alloc(ws, kWsNmsack, &g.nmsack, sizeof(uint32_t) * 2));
     HCHECK(hipMemset(g.nmsack, 0, sizeof(uint32_t) * 2));
-    HCHECK(ws_alloc(ws, kWsMail, &g.mail, sizeof(Mail) * 2 * (size_t)g.mail_cap));
+    HCHECK(ws_alloc(ws, kWsMail, &g.mail, sizeof(Mail) * 2 * (size_t)g.mail_stride));
     HCHECK(ws_alloc(ws, kWsNmail, &g.nmail, sizeof(uint32_t) * 2 * (kMailSub + 1)));
     HCHECK(hipMemset(g.nmail, 0, sizeof(uint32_t) * 2 * (kMailSub + 1)));
-    HCHECK(ws_alloc(ws, kWsMhead, &g.mhead, sizeof(int32_t) * 2 * (size_t)H));
-    HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)H));
-    HCHECK(ws_alloc(ws, kWsMnext, &g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_cap));
+    HCHECK(ws_alloc(ws, kWsMhead, &g.mhead, sizeof(int32_t) * 2 * (size_t)nloc));
+    HCHECK(hipMemset(g.mhead, 0xff, sizeof(int32_t) * 2 * (size_t)nloc));
+    HCHECK(ws_alloc(ws, kWsMnext, &g.mnext, sizeof(int32_t) * 2 * (size_t)g.mail_stride));
     HCHECK(ws_alloc(ws, kWsCtl, &g.ctl, sizeof(TCtl)));
     HCHECK(hipMemset(g.ctl, 0, sizeof(TCtl)));
     HCHECK(ws_alloc(ws, kWsIpk, &d_ipk, sizeof(uint64_t) * ipk.size()));
@@ -3058,7 +3248,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     g.ip_key = d_ipk;
     if (trace & SHD_TCP_TRACE_NODE) {   // every heartbeat before the end, per host
         g.node_k = (uint32_t)((m->end_time - 1) / g.hb) + 1;
-        if (ws_alloc(ws, kWsNode, &g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k) != hipSuccess) {
+        if (ws_alloc(ws, kWsNode, &g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)nloc * g.node_k) != hipSuccess) {
             (void)hipGetLastError();
             fprintf(stderr, "shd_tcp_run: no device memory for the tracker counters\n");
             rc = -12;
@@ -3068,25 +3258,25 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     if (g.trace) {
         // kTr records and kTrSack SACK words per host (about 16 MB): a traced
         // run of many hosts may not fit; say so instead of a bare -ENOMEM
-        const size_t need = (sizeof(TRec) * (size_t)kTr + sizeof(int32_t) * (size_t)kTrSack) * (size_t)H;
-        if (ws_alloc(ws, kWsTr, &g.tr, sizeof(TRec) * (size_t)H * kTr) != hipSuccess ||
-            ws_alloc(ws, kWsTrs, &g.trs, sizeof(int32_t) * (size_t)H * kTrSack) != hipSuccess) {
+        const size_t need = (sizeof(TRec) * (size_t)kTr + sizeof(int32_t) * (size_t)kTrSack) * (size_t)nloc;
+        if (ws_alloc(ws, kWsTr, &g.tr, sizeof(TRec) * (size_t)nloc * kTr) != hipSuccess ||
+            ws_alloc(ws, kWsTrs, &g.trs, sizeof(int32_t) * (size_t)nloc * kTrSack) != hipSuccess) {
             (void)hipGetLastError();
             fprintf(stderr, "shd_tcp_run: no device memory for the status trace of %d hosts (%.1f GB); "
-                            "run without trace\n", H, need / 1e9);
+                            "run without trace\n", nloc, need / 1e9);
             rc = -12;
             goto done;
         }
     }
-    HCHECK(ws_alloc(ws, kWsNextTime, &g.next_time, sizeof(uint64_t) * (H + 1)));
-    HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (H + 1)));
+    HCHECK(ws_alloc(ws, kWsNextTime, &g.next_time, sizeof(uint64_t) * (nloc + 1)));
+    HCHECK(hipMemset(g.next_time, 0xff, sizeof(uint64_t) * (nloc + 1)));
     // every host can log kPq first queries (touch_log)
-    g.qlog_cap = (uint32_t)H * kPq > (1u << 16) ? (uint32_t)H * kPq : (1u << 16);
+    g.qlog_cap = (uint32_t)nloc * kPq > (1u << 16) ? (uint32_t)nloc * kPq : (1u << 16);
     HCHECK(ws_alloc(ws, kWsQlog, &g.qlog, sizeof(shd_tcp_query) * (size_t)g.qlog_cap));
     HCHECK(ws_alloc(ws, kWsNqlog, &g.nqlog, sizeof(uint32_t)));
 #ifdef SHD_TCP_PROF
-    HCHECK(ws_alloc(ws, kWsProf, &g.prof, sizeof(uint64_t) * 2 * kProf * (size_t)H));
-    HCHECK(hipMemset(g.prof, 0, sizeof(uint64_t) * 2 * kProf * (size_t)H));
+    HCHECK(ws_alloc(ws, kWsProf, &g.prof, sizeof(uint64_t) * 2 * kProf * (size_t)nloc));
+    HCHECK(hipMemset(g.prof, 0, sizeof(uint64_t) * 2 * kProf * (size_t)nloc));
     HCHECK(ws_alloc(ws, kWsProfRound, &g.prof_round, sizeof(uint32_t) * 2 * kProfRounds));
     HCHECK(hipMemset(g.prof_round, 0, sizeof(uint32_t) * 2 * kProfRounds));
 #endif
@@ -3104,22 +3294,69 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         // halted run turns the batch's remaining kernels into no-ops
         // one host per lane, 64 per wave (16 per wave measured +4 % at 16 k
         // hosts, DESIGN.md §6: not kept)
-        const int threads = 64, blocks = (H + threads - 1) / threads;
+        const int threads = 64, blocks = (nloc + threads - 1) / threads;
         constexpr int kBatch = 64;
-        HCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-        for (int i = 0; i < kBatch; i++) {
-            k_tcp_window<<<1, 1024, 0, st>>>(g);
-            k_tcp_round<<<blocks, threads, 0, st>>>(g);
+        if (world == 1) {
+            HCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            for (int i = 0; i < kBatch; i++) {
+                k_tcp_window<<<1, 1024, 0, st>>>(g, 0);
+                k_tcp_round<<<blocks, threads, 0, st>>>(g);
+            }
+            HCHECK(hipStreamEndCapture(st, &graph));
+            HCHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
         }
-        HCHECK(hipStreamEndCapture(st, &graph));
-        HCHECK(hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0));
         HCHECK(hipEventRecord(e0, st));
         k_tcp_boot<<<blocks, threads, 0, st>>>(g);
         HCHECK(hipGetLastError());
         for (;;) {
-            HCHECK(hipGraphLaunch(gexec, st));
-            HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
-            HCHECK(hipStreamSynchronize(st));
+            if (world == 1) {
+                HCHECK(hipGraphLaunch(gexec, st));
+                HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
+                HCHECK(hipStreamSynchronize(st));
+            } else {
+                // a group's round (slave.c:437-462 across engines): the earliest
+                // event over the group opens the window; the round's ports and
+                // deliveries for the other engines are exchanged after it
+                k_tcp_window<<<1, 1024, 0, st>>>(g, 1);
+                k_tcp_ports_pack<<<1, 256, 0, st>>>(g, d_pmine);
+                HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
+                HCHECK(hipStreamSynchronize(st));
+                struct { uint64_t tmin; uint32_t nport, halted; } mine{hctl.tmin, 0, hctl.halted}, all[64];
+                {
+                    uint64_t np = 0;
+                    HCHECK(hipMemcpy(&np, d_pmine, sizeof(uint64_t), hipMemcpyDeviceToHost));
+                    mine.nport = (uint32_t)np;
+                }
+                if (shd_comm_allgather_host(comm, &mine, sizeof(mine), all)) { rc = -5; goto done; }
+                uint64_t t = ~0ull;
+                uint32_t anyport = 0, halted = 0;
+                for (int r = 0; r < world; r++) {
+                    t = all[r].tmin < t ? all[r].tmin : t;
+                    anyport |= all[r].nport;
+                    halted |= all[r].halted;
+                }
+                if (anyport) {
+                    if (shd_comm_allgather_dev(comm, d_pmine, d_pall, sizeof(uint64_t) * (1 + kPortNew), st)) {
+                        rc = -5;
+                        goto done;
+                    }
+                    k_tcp_ports<<<world, 256, 0, st>>>(g, d_pall);
+                }
+                if (halted) t = ~0ull;   // an engine stopped: every engine ends at the same round
+                k_tcp_decide<<<1, 64, 0, st>>>(g, t);
+                if (t == ~0ull || t >= g.end_time) {
+                    HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
+                    HCHECK(hipStreamSynchronize(st));
+                    break;
+                }
+                k_tcp_round<<<blocks, threads, 0, st>>>(g);
+                HCHECK(hipGetLastError());
+                if (shd_comm_alltoall_dev(comm, g.xsend, d_xrecv, g.xseg, st)) { rc = -5; goto done; }
+                k_tcp_xingest<<<world, 256, 0, st>>>(g, d_xrecv);
+                HCHECK(hipGetLastError());
+                HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
+                HCHECK(hipStreamSynchronize(st));
+            }
             if (hctl.halted) break;
             if (hctl.rounds > (1ull << 26)) { res->error |= SHD_TCP_ERR_INTERNAL; break; }
         }
@@ -3131,18 +3368,37 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         res->device_ms = ms;
     }
     t_results = std::chrono::steady_clock::now();
-    HCHECK(hipMemcpy(hout.data(), g.host, sizeof(DHost) * H, hipMemcpyDeviceToHost));
-    {   // the first-query log
+    HCHECK(hipMemcpy(hout.data(), g.host, sizeof(DHost) * nloc, hipMemcpyDeviceToHost));
+    {   // the first-query log (a group's: every engine's, so that each ranks the run's first touches alike)
         uint32_t nq = 0;
         HCHECK(hipMemcpy(&nq, g.nqlog, sizeof(uint32_t), hipMemcpyDeviceToHost));
         if (nq > g.qlog_cap) nq = g.qlog_cap;   // (the run's error bits say so)
-        res->queries = (shd_tcp_query*)malloc(sizeof(shd_tcp_query) * (nq ? nq : 1));
-        res->n_queries = nq;
-        if (nq) HCHECK(hipMemcpy(res->queries, g.qlog, sizeof(shd_tcp_query) * nq, hipMemcpyDeviceToHost));
+        std::vector<shd_tcp_query> mine(nq ? nq : 1);
+        if (nq) HCHECK(hipMemcpy(mine.data(), g.qlog, sizeof(shd_tcp_query) * nq, hipMemcpyDeviceToHost));
+        if (world == 1) {
+            res->queries = (shd_tcp_query*)malloc(sizeof(shd_tcp_query) * (nq ? nq : 1));
+            memcpy(res->queries, mine.data(), sizeof(shd_tcp_query) * (nq ? nq : 1));
+            res->n_queries = nq;
+        } else {
+            std::vector<uint32_t> counts(world);
+            if (shd_comm_allgather_host(comm, &nq, sizeof(nq), counts.data())) { rc = -5; goto done; }
+            uint32_t mx = 1, tot = 0;
+            for (uint32_t c : counts) { mx = c > mx ? c : mx; tot += c; }
+            mine.resize(mx);
+            std::vector<shd_tcp_query> all((size_t)mx * world);
+            if (shd_comm_allgather_host(comm, mine.data(), sizeof(shd_tcp_query) * mx, all.data())) { rc = -5; goto done; }
+            res->queries = (shd_tcp_query*)malloc(sizeof(shd_tcp_query) * (tot ? tot : 1));
+            res->n_queries = tot;
+            size_t o = 0;
+            for (int r = 0; r < world; r++)
+                for (uint32_t j = 0; j < counts[r]; j++) res->queries[o++] = all[(size_t)r * mx + j];
+        }
     }
-    res->next_event_id = (uint64_t*)calloc(H, sizeof(uint64_t));
-    res->next_packet_id = (uint64_t*)calloc(H, sizeof(uint64_t));
-    res->rng_probe = (uint32_t*)calloc(H, sizeof(uint32_t));
+    res->first_host = h0;
+    res->n_local_hosts = nloc;
+    res->next_event_id = (uint64_t*)calloc(nloc, sizeof(uint64_t));
+    res->next_packet_id = (uint64_t*)calloc(nloc, sizeof(uint64_t));
+    res->rng_probe = (uint32_t*)calloc(nloc, sizeof(uint32_t));
     res->rounds = rounds;
     {   // the last two rounds' mailboxes were never counted by k_tcp_window
         std::vector<uint32_t> nm(2 * (kMailSub + 1));
@@ -3152,6 +3408,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         res->max_round_deliveries = cx.max_mail;
         res->max_round_overflow = cx.max_ovf;
         if (cx.ft_bad) res->error |= SHD_TCP_ERR_FIRST_TOUCH;
+        res->error |= cx.xerr;
         if (pc && !cx.ft_bad) {   // the cache's ranks as the serial run leaves them
             HCHECK(hipMemcpy(pc->h_rank, g.rank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
             HCHECK(hipMemcpy(pc->h_self_rank, g.srank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
@@ -3168,7 +3425,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
             if (sum > res->max_round_deliveries) res->max_round_deliveries = sum;
         }
     }
-    for (int32_t i = 0; i < H; i++) {
+    for (int32_t i = 0; i < nloc; i++) {
         res->next_event_id[i] = hout[i].ev_seq;
         res->next_packet_id[i] = hout[i].pkt_seq;
         uint32_t st = hout[i].rng;
@@ -3179,24 +3436,24 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     }
     if (g.node) {
         res->node_k = g.node_k;
-        res->n_heartbeats = (uint32_t*)calloc(H, sizeof(uint32_t));
-        res->node_counters = (uint64_t*)malloc(sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k);
-        HCHECK(hipMemcpy(res->node_counters, g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)H * g.node_k,
+        res->n_heartbeats = (uint32_t*)calloc(nloc, sizeof(uint32_t));
+        res->node_counters = (uint64_t*)malloc(sizeof(uint64_t) * 2 * kTrk * (size_t)nloc * g.node_k);
+        HCHECK(hipMemcpy(res->node_counters, g.node, sizeof(uint64_t) * 2 * kTrk * (size_t)nloc * g.node_k,
                          hipMemcpyDeviceToHost));
-        for (int32_t i = 0; i < H; i++) res->n_heartbeats[i] = hout[i].nhb < g.node_k ? hout[i].nhb : g.node_k;
+        for (int32_t i = 0; i < nloc; i++) res->n_heartbeats[i] = hout[i].nhb < g.node_k ? hout[i].nhb : g.node_k;
     }
     if (g.trace) {
         std::string text;
         std::vector<TRec> recs;
         std::vector<int32_t> sk;
-        for (int32_t i = 0; i < H; i++) {
+        for (int32_t i = 0; i < nloc; i++) {
             recs.resize(hout[i].ntr);
             sk.resize(hout[i].ntrs + 1);
             if (hout[i].ntr)
                 HCHECK(hipMemcpy(recs.data(), g.tr + (size_t)i * kTr, sizeof(TRec) * hout[i].ntr, hipMemcpyDeviceToHost));
             if (hout[i].ntrs)
                 HCHECK(hipMemcpy(sk.data(), g.trs + (size_t)i * kTrSack, sizeof(int32_t) * hout[i].ntrs, hipMemcpyDeviceToHost));
-            for (const TRec& r : recs) format_line(text, r, sk.data() + r.sack_off, i);
+            for (const TRec& r : recs) format_line(text, r, sk.data() + r.sack_off, h0 + i);
             res->n_lines += hout[i].ntr;
         }
         res->lines = (char*)malloc(text.size() + 1);
@@ -3206,7 +3463,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
     }
 #ifdef SHD_TCP_PROF
     {   // the steps' cycles summed over hosts, and per round the busiest lane
-        std::vector<uint64_t> pf(2 * kProf * (size_t)H);
+        std::vector<uint64_t> pf(2 * kProf * (size_t)nloc);
         std::vector<uint32_t> pr(2 * kProfRounds);
         HCHECK(hipMemcpy(pf.data(), g.prof, sizeof(uint64_t) * pf.size(), hipMemcpyDeviceToHost));
         HCHECK(hipMemcpy(pr.data(), g.prof_round, sizeof(uint32_t) * pr.size(), hipMemcpyDeviceToHost));
@@ -3216,7 +3473,7 @@ extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result
         fprintf(stderr, "tcp_prof: step cycles_total count cycles_per\n");
         for (uint32_t j = 0; j < kProf; j++) {
             uint64_t cy = 0, n = 0;
-            for (int32_t i = 0; i < H; i++) {
+            for (int32_t i = 0; i < nloc; i++) {
                 const uint64_t* q = pf.data() + (size_t)i * 2 * kProf;
                 if (j == 15) { cy = std::max(cy, q[j]); continue; }
                 cy += q[j]; n += q[kProf + j];
@@ -3243,6 +3500,16 @@ done:
     res->teardown_ms = ms_since(t_free);
     *out = res;
     return 0;
+}
+
+extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
+    return tcp_run_impl(m, nullptr, trace, out);
+}
+
+extern "C" int shd_tcp_run_group(const shd_tcp_model* m, shd_comm* comm, int32_t trace, shd_tcp_result** out) {
+    if (!comm) return -22;
+    if (hipSetDevice(comm->device) != hipSuccess) return -5;
+    return tcp_run_impl(m, comm, trace, out);
 }
 
 extern "C" void shd_tcp_result_free(shd_tcp_result* r) {

@@ -214,7 +214,8 @@ class TcpResult(C.Structure):
                 ("queries", C.c_void_p), ("n_queries", C.c_uint64),
                 ("node_counters", P(C.c_uint64)), ("n_heartbeats", P(C.c_uint32)), ("node_k", C.c_uint32),
                 ("_pad2", C.c_uint32), ("max_round_deliveries", C.c_uint64), ("max_round_overflow", C.c_uint64),
-                ("setup_ms", C.c_double), ("results_ms", C.c_double), ("teardown_ms", C.c_double)]
+                ("setup_ms", C.c_double), ("results_ms", C.c_double), ("teardown_ms", C.c_double),
+                ("first_host", C.c_int32), ("n_local_hosts", C.c_int32)]
 
 
 TCP_TRACE_STATUS, TCP_TRACE_NODE = 1, 2   # shd_tcp_run's trace bits
@@ -234,6 +235,7 @@ class Lines(C.Structure):
 
 _SIGS = {
     "shd_tcp_run": (C.c_int, [P(TcpModel), C.c_int32, P(P(TcpResult))]),
+    "shd_tcp_run_group": (C.c_int, [P(TcpModel), C.c_void_p, C.c_int32, P(P(TcpResult))]),
     "shd_tcp_result_free": (None, [P(TcpResult)]),
     "shd_tcp_keep_workspace": (None, [C.c_int32]),
     "shd_tracker_node_lines": (C.c_int, [P(C.c_uint64), C.c_uint64, C.c_uint64, C.c_uint32, P(P(Lines))]),

@@ -100,7 +100,7 @@ def serial_first_queries(queries: np.ndarray):
 
 def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000, trace=True,
         recv_buf=RECV_BUF, send_buf=SEND_BUF, tcp_window=TCP_WINDOW, packets_per_host=0, guess_reversed=False,
-        node=False, qdisc=0, mode="device", udp=None):
+        node=False, qdisc=0, mode="device", udp=None, comm=None):
     """Run the TCP echo model on the GPU: procs = [(host, start ns)], peers =
     [-1 | server process]; ips: host-order uint32 per host.  Returns
     dict(lines=[(t, h, line)] in each host's order, next_event_id,
@@ -115,8 +115,12 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
     n_start, per_read)], app_peer=[H], payload=bytes) -- the processes with
     an index run that datagram application (shd_tcp_model.proc_app) instead
     of the echo; the model's dest_cum / host_class give SHD_DEST_WEIGHTED's
-    weights."""
-    if mode == "device" and not guess_reversed and not g.directed:
+    weights.
+    comm (sim.Comm): this rank's share of a group run (shd_tcp_run_group: every
+    rank calls with the same model; the result covers hosts [first_host,
+    first_host + n_local_hosts), the lines carry the model's host index); a
+    group runs on tables, the first-touch ranking over every rank's log."""
+    if mode == "device" and not guess_reversed and not g.directed and comm is None:
         m = model.struct
         H = int(m.n_hosts)
         hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
@@ -137,7 +141,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
     V = lat.shape[0]
     for runs in range(1, 9):
         out = _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-                        packets_per_host, node, qdisc, udp=udp)
+                        packets_per_host, node, qdisc, udp=udp, comm=comm)
         order, pairs = serial_first_queries(out.pop("queries"))
         lat2, rel2 = resolve(g, att, order, pairs, V)
         ij = tuple(np.array([(a, b) for a, b in pairs] + [(b, a) for a, b in pairs], dtype=np.int64).T) \
@@ -156,7 +160,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
 
 
 def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, send_buf, tcp_window,
-              packets_per_host, node=False, qdisc=0, pc=None, udp=None):
+              packets_per_host, node=False, qdisc=0, pc=None, udp=None, comm=None):
     """one shd_tcp_run on the given path tables, or with pc (sim.PathCache) on
     the cache itself (hvi: graph vertices then); None when that run's
     first-touch choices were contradicted (SHD_TCP_ERR_FIRST_TOUCH)"""
@@ -206,9 +210,13 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
         tm.n_classes = m.n_classes
     res = C.POINTER(S.TcpResult)()
     bits = (S.TCP_TRACE_STATUS if trace else 0) | (S.TCP_TRACE_NODE if node else 0)
-    S.check(S.lib().shd_tcp_run(C.byref(tm), bits, C.byref(res)), "shd_tcp_run")
+    if comm is not None:
+        S.check(S.lib().shd_tcp_run_group(C.byref(tm), comm.ptr, bits, C.byref(res)), "shd_tcp_run_group")
+    else:
+        S.check(S.lib().shd_tcp_run(C.byref(tm), bits, C.byref(res)), "shd_tcp_run")
     try:
         r = res.contents
+        h0, HL = int(r.first_host), int(r.n_local_hosts)
         if pc is not None and r.error == S.TCP_ERR_FIRST_TOUCH:
             return None
         if r.error:
@@ -218,10 +226,10 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
         for ln in text.splitlines():
             t, h, body = ln.split("\t", 2)
             lines.append((int(t), int(h), body))
-        out = dict(lines=lines,
-                   next_event_id=np.ctypeslib.as_array(r.next_event_id, shape=(H,)).copy(),
-                   next_packet_id=np.ctypeslib.as_array(r.next_packet_id, shape=(H,)).copy(),
-                   rng_probe=np.ctypeslib.as_array(r.rng_probe, shape=(H,)).copy(),
+        out = dict(lines=lines, first_host=h0, n_local_hosts=HL,
+                   next_event_id=np.ctypeslib.as_array(r.next_event_id, shape=(HL,)).copy(),
+                   next_packet_id=np.ctypeslib.as_array(r.next_packet_id, shape=(HL,)).copy(),
+                   rng_probe=np.ctypeslib.as_array(r.rng_probe, shape=(HL,)).copy(),
                    rounds=int(r.rounds), events=int(r.events), deliveries=int(r.deliveries),
                    max_round_deliveries=int(r.max_round_deliveries), max_round_overflow=int(r.max_round_overflow),
                    host_ms=dict(setup=float(r.setup_ms), results=float(r.results_ms), teardown=float(r.teardown_ms)),
@@ -231,14 +239,14 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
                    np.zeros(0, dtype=S.TCP_QUERY_DTYPE))
         if node:
             k = int(r.node_k)
-            cnt = np.ctypeslib.as_array(r.node_counters, shape=(H * k * 20,)).reshape(H, k, 20)
-            nhb = np.ctypeslib.as_array(r.n_heartbeats, shape=(H,))
+            cnt = np.ctypeslib.as_array(r.node_counters, shape=(HL * k * 20,)).reshape(HL, k, 20)
+            nhb = np.ctypeslib.as_array(r.n_heartbeats, shape=(HL,))
             hb = int(tm.heartbeat_interval) or S.SHD_SEC
             nl = []
-            for h in range(H):
-                c = np.ascontiguousarray(cnt[h, :int(nhb[h])])
+            for i in range(HL):
+                c = np.ascontiguousarray(cnt[i, :int(nhb[i])])
                 lp = C.POINTER(S.Lines)()
-                S.check(S.lib().shd_tracker_node_lines(c.ctypes.data_as(C.POINTER(C.c_uint64)), len(c), hb, h,
+                S.check(S.lib().shd_tracker_node_lines(c.ctypes.data_as(C.POINTER(C.c_uint64)), len(c), hb, h0 + i,
                                                        C.byref(lp)), "shd_tracker_node_lines")
                 nl += S.take_lines(lp)
             out["node_lines"] = sorted(nl, key=lambda x: (x[0], x[1]))
