@@ -445,15 +445,39 @@ def tcp_main(args):
     """The TCP path measured like the headline: a step is one
     whole shd_tcp_run of workloads.tcp_echo_model (hosts resident in HBM from
     the call's upload on; the value is device time of the rounds, HIP events on
-    the run's stream).  Replicas only: the TCP path runs on one GPU."""
+    the run's stream).  At N > 1 (torch.distributed.run) the hosts are
+    --hosts-per-gpu per GPU, sharded over the ranks by shd_tcp_run_group
+    (weak scaling; RCCL, or --comm host: every rank on one GPU over the
+    host-memory transport, a rehearsal); the value is every rank's events over
+    the slowest rank's device time."""
     import torch
     import shdgpu as S
     import workloads as W
     import tcp as T
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        raise SystemExit("--workload tcp runs on one GPU (replicas only)")
-    torch.cuda.set_device(0)
-    H = args.hosts_per_gpu or 65536
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = args.comm == "host" and world > 1
+    dist = comm = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(0 if rehearsal else local_rank)
+        dist.init_process_group("gloo" if rehearsal else "nccl")
+        from sim import Comm, XGroup
+        tdev = "cpu" if rehearsal else "cuda"
+        uid = torch.zeros(S.SHD_XID_BYTES, dtype=torch.uint8, device=tdev)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(XGroup.unique_id() if not rehearsal else os.urandom(S.SHD_XID_BYTES)),
+                                       dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        dev = 0 if rehearsal else local_rank
+        if rehearsal:
+            comm = Comm.host("shdtcp_" + bytes(uid.cpu().numpy().tobytes())[:8].hex(), world, rank, dev)
+        else:
+            comm = Comm.rccl(bytes(uid.cpu().numpy().tobytes()), world, rank, dev)
+    else:
+        torch.cuda.set_device(0)
+    H = (args.hosts_per_gpu or 65536) * max(world, 1)
     pool = args.tcp_pool
     V = min(args.vertices, 1000)
     mk = lambda n: W.tcp_echo_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,  # noqa: E731
@@ -462,16 +486,22 @@ def tcp_main(args):
     # a caller running many models keeps the run's device buffers between
     # calls (shdtcp.h shd_tcp_keep_workspace); the first call allocates them
     S.lib().shd_tcp_keep_workspace(1)
+    run1 = lambda: T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool,  # noqa: E731
+                         comm=comm, mode="tables" if comm is not None else "device")
     for _ in range(args.warmup):
-        T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool)
+        run1()
     mark = Roctx()
     runs = []
+    if dist is not None:
+        dist.barrier()
     torch.cuda.synchronize()
     mark.push("shd_timed_region")
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        runs.append(T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool))
+        runs.append(run1())
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     wall = time.perf_counter() - t0
     mark.pop()
     r = runs[-1]
@@ -479,6 +509,17 @@ def tcp_main(args):
     dev_s = sum(x["device_ms"] for x in runs) / 1e3
     events = r["events"] * len(runs)
     deliv = r["deliveries"] * len(runs)
+    if dist is not None:   # every rank's events over the slowest rank's time
+        red = torch.tensor([float(events), float(deliv)], dtype=torch.float64, device="cpu" if rehearsal else "cuda")
+        dist.all_reduce(red)
+        mx = torch.tensor([dev_s, wall], dtype=torch.float64, device=red.device)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        events, deliv = int(red[0].item()), int(red[1].item())
+        dev_s, wall = float(mx[0].item()), float(mx[1].item())
+        comm.close()
+        if rank != 0:
+            dist.destroy_process_group()
+            return
     # algorithmic bytes per executed event: its 32-B record pushed and popped
     # once (64 B); per delivery the mailbox record written and read once
     mail_b = 216   # sizeof(Mail) in csrc/tcp.hip (static_assert there; SACK lists travel apart)
@@ -486,7 +527,7 @@ def tcp_main(args):
     per_round_us = r["device_ms"] * 1e3 / max(r["rounds"], 1)
     achieved = alg / (r["device_ms"] / 1e3) / 1e9
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:
         # bounded sample: the same model at min(H, 4096) hosts (the same
         # per-pair work); the GPU runs that sample too, and the end states of
         # every host must agree
@@ -508,15 +549,17 @@ def tcp_main(args):
                "same_end_state_as_gpu": bool(same)}
     out = {
         "metric": "simulated TCP events/sec", "value": round(events / dev_s, 1), "unit": "events/s",
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(dev_s * 1e3 / len(runs), 3), "higher_is_better": True, "scaling": "replicas only",
+        "n_gpus": max(world, 1), "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dev_s * 1e3 / len(runs), 3), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (random geometric topology + TCP echo pairs, seed %d)"
         % args.seed,
         "config": {"workload": "TCP echo (src/test/tcp/test_tcp.c, nonblocking-epoll), %d hosts / %d pairs, "
                                "%d-vertex geometric topology, %d B each way, %d s simulated"
                                % (H, H // 2, V, nb, args.tcp_end_s),
                    "hosts": H, "vertices": V, "packets_per_host": pool,
-                   "parallelism": "one lane per host, 1 GPU"},
+                   "parallelism": "one lane per host, %s" % (
+                       "1 GPU" if world <= 1 else "hosts sharded over %d ranks (shd_tcp_run_group, %s)"
+                       % (world, "host-memory transport, one GPU: rehearsal" if rehearsal else "RCCL"))},
         "packet_deliveries_per_s": round(deliv / dev_s, 1), "wall_s": round(wall, 3),
         # the same events over the whole calls' wall time (the model's upload,
         # the per-host allocations and setup, the rounds, the copies back): the
@@ -534,6 +577,8 @@ def tcp_main(args):
     }
     os.dup2(_STDOUT_FD, 1)
     print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, torch):

@@ -13,6 +13,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "shd_device.h"
@@ -91,6 +92,47 @@ int shd_comm_alltoall_dev(shd_comm* c, const void* d_send, void* d_recv, size_t 
     SHD_HIP(hipStreamSynchronize(s));
     if ((rc = shd_xhost_alltoall(c->hx, hs, bytes, hs + all))) return rc;
     SHD_HIP(hipMemcpyAsync(d_recv, hs + all, all, hipMemcpyHostToDevice, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    return SHD_OK;
+}
+
+int shd_comm_alltoallv_dev(shd_comm* c, const char* d_send, const size_t* send_off, const size_t* send_bytes,
+                           char* d_recv, const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) {
+    const int W = c->world;
+    if (c->kind == SHD_COMM_RCCL) {
+        if (ncclGroupStart() != ncclSuccess) return SHD_ENODEV;
+        int rc = SHD_OK;
+        for (int p = 0; p < W && !rc; p++) {
+            if (send_bytes[p] &&
+                ncclSend(d_send + send_off[p], send_bytes[p], ncclUint8, p, c->nccl, s) != ncclSuccess)
+                rc = SHD_ENODEV;
+            if (!rc && recv_bytes[p] &&
+                ncclRecv(d_recv + recv_off[p], recv_bytes[p], ncclUint8, p, c->nccl, s) != ncclSuccess)
+                rc = SHD_ENODEV;
+        }
+        if (ncclGroupEnd() != ncclSuccess) rc = SHD_ENODEV;
+        return rc;
+    }
+    size_t blk = 0;   // every rank's largest block (each rank passes the same sizes' maximum: both directions)
+    for (int p = 0; p < W; p++) blk = std::max(blk, std::max(send_bytes[p], recv_bytes[p]));
+    unsigned long long mine = blk;
+    std::vector<unsigned long long> all(W);
+    int rc = shd_xhost_allgather(c->hx, &mine, sizeof(mine), all.data());
+    if (rc) return rc;
+    blk = 0;
+    for (unsigned long long v : all) blk = std::max(blk, (size_t)v);
+    if (blk == 0) return SHD_OK;
+    const size_t tot = blk * (size_t)W;
+    if ((rc = stage(c, 2 * tot))) return rc;
+    char* hs = (char*)c->h_stage;
+    for (int p = 0; p < W; p++)
+        if (send_bytes[p]) SHD_HIP(hipMemcpyAsync(hs + (size_t)p * blk, d_send + send_off[p], send_bytes[p],
+                                                  hipMemcpyDeviceToHost, s));
+    SHD_HIP(hipStreamSynchronize(s));
+    if ((rc = shd_xhost_alltoall(c->hx, hs, blk, hs + tot))) return rc;
+    for (int p = 0; p < W; p++)
+        if (recv_bytes[p]) SHD_HIP(hipMemcpyAsync(d_recv + recv_off[p], hs + tot + (size_t)p * blk, recv_bytes[p],
+                                                  hipMemcpyHostToDevice, s));
     SHD_HIP(hipStreamSynchronize(s));
     return SHD_OK;
 }

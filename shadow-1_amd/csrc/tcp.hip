@@ -167,7 +167,8 @@ struct RVec { uint32_t n; Rng64 r[kRanges]; };
 struct Tally { int64_t last_ack; uint64_t ndup; RVec marked, sacked, retx, lost, tmp; };
 
 struct DSock {   // every scalar first (a few lines per socket), then the containers
-    int32_t used, host, proc, udp;   // udp: a datagram socket (udp.c), else TCP
+    int16_t used, udp;      // udp: a datagram socket (udp.c), else TCP (the scalars' layout as before it)
+    int32_t host, proc;
     uint32_t status;
     int32_t bound; uint32_t bound_ip; uint16_t bound_port, peer_port;
     uint32_t peer_ip;
@@ -330,13 +331,13 @@ struct Glob {
     const uint64_t* bwd_all;
     uint32_t* proc_port;    // [P] 0: not listening (yet)
     uint32_t* nport_new;    // [1] this round's publications ...
-    uint64_t* port_new;     // [kPortNew] ... (process << 32 | port)
+    uint64_t* port_new;     // [pcap] ... (process << 32 | port)
+    uint32_t pcap, _pad9;   // publications per engine and round at most: the most processes one engine has
     char* xsend;            // [world] segments
     int32_t world, me;
     uint32_t xcap, xsack_cap;
     size_t xseg;            // bytes per segment
 };
-constexpr uint32_t kPortNew = 256;   // listening ports one engine publishes in one round, at most
 struct XSegHead { uint32_t n, nsack, err, _pad[13]; };   // 64 B, then xcap Mails, then xsack_cap SACK words
 static_assert(sizeof(XSegHead) == 64, "segment header");
 
@@ -1757,7 +1758,7 @@ __device__ void publish_port(L& c, int32_t proc, uint16_t port) {
     c.g->proc_port[proc] = port;
     if (c.g->world > 1) {
         const uint32_t k = atomicAdd(c.g->nport_new, 1u);
-        if (k >= kPortNew) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
+        if (k >= c.g->pcap) { c.H->err |= SHD_TCP_ERR_INTERNAL; return; }
         c.g->port_new[k] = ((uint64_t)(uint32_t)proc << 32) | port;
     }
 }
@@ -2586,15 +2587,15 @@ __global__ void k_tcp_decide(Glob g, uint64_t t) {
 // the deliveries the other engines sent this engine in the round just run:
 // into the round's output mailbox after its own slots (slot mail_cap + r *
 // xcap + i), each linked into its host's list, its SACK list into the arena
-__global__ void k_tcp_xingest(Glob g, const char* __restrict__ xrecv) {
+// cnt: [world][2] the mails and SACK words each engine sent this one
+__global__ void k_tcp_xingest(Glob g, const char* __restrict__ xrecv, const uint32_t* __restrict__ cnt) {
     const int32_t r = (int32_t)blockIdx.x;
     if (r == g.me) return;
     const TCtl* ctl = g.ctl;
     const uint64_t k = ctl->rounds - 1;
     const uint32_t out = (uint32_t)(k & 1) ^ 1u;
     const char* seg = xrecv + (size_t)r * g.xseg;
-    const XSegHead* hd = (const XSegHead*)seg;
-    const uint32_t n = hd->n < g.xcap ? hd->n : g.xcap;
+    const uint32_t n = cnt[2 * r] < g.xcap ? cnt[2 * r] : g.xcap;
     const Mail* src = (const Mail*)(seg + sizeof(XSegHead));
     const int32_t* sks = (const int32_t*)(seg + sizeof(XSegHead) + (size_t)g.xcap * sizeof(Mail));
     Mail* mail = g.mail + (size_t)out * g.mail_stride;
@@ -2621,12 +2622,20 @@ __global__ void k_tcp_xingest(Glob g, const char* __restrict__ xrecv) {
         mnext[slot] = atomicExch(&mhead[dl], (int32_t)slot);
     }
 }
+// what this engine's segments hold after the round ([world][2]: mails, SACK words)
+__global__ void k_tcp_xheads(Glob g, uint32_t* __restrict__ heads) {
+    const int32_t p = (int32_t)threadIdx.x;
+    if (p >= g.world) return;
+    const XSegHead* hd = (const XSegHead*)(g.xsend + (size_t)p * g.xseg);
+    heads[2 * p] = hd->n < g.xcap ? hd->n : g.xcap;
+    heads[2 * p + 1] = hd->nsack < g.xsack_cap ? hd->nsack : g.xsack_cap;
+}
 // the listening ports the group's engines published in the last round
-// ([world][1 + kPortNew]: the count, then process << 32 | port)
+// ([world][1 + pcap]: the count, then process << 32 | port)
 __global__ void k_tcp_ports(Glob g, const uint64_t* __restrict__ all) {
     const int32_t r = (int32_t)blockIdx.x;
-    const uint64_t* a = all + (size_t)r * (1 + kPortNew);
-    const uint32_t n = (uint32_t)a[0] < kPortNew ? (uint32_t)a[0] : kPortNew;
+    const uint64_t* a = all + (size_t)r * (1 + g.pcap);
+    const uint32_t n = (uint32_t)a[0] < g.pcap ? (uint32_t)a[0] : g.pcap;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         const uint64_t v = a[1 + i];
         g.proc_port[(uint32_t)(v >> 32)] = (uint32_t)v;
@@ -2636,7 +2645,7 @@ __global__ void k_tcp_ports(Glob g, const uint64_t* __restrict__ all) {
 __global__ void k_tcp_ports_pack(Glob g, uint64_t* __restrict__ mine) {
     const uint32_t n = *g.nport_new;
     if (threadIdx.x == 0) mine[0] = n;
-    for (uint32_t i = threadIdx.x; i < n && i < kPortNew; i += blockDim.x) mine[1 + i] = g.port_new[i];
+    for (uint32_t i = threadIdx.x; i < n && i < g.pcap; i += blockDim.x) mine[1 + i] = g.port_new[i];
 }
 
 // a delivery from the round's input mailbox onto the host's heap (its packet
@@ -2892,7 +2901,7 @@ enum WsSlot {
     kWsHostProcs, kWsPool, kWsPsack, kWsFreel, kWsEv, kWsCq, kWsMsack, kWsNmsack, kWsMail, kWsNmail, kWsMhead,
     kWsMnext, kWsCtl, kWsIpk, kWsNode, kWsTr, kWsTrs, kWsNextTime, kWsQlog, kWsNqlog, kWsProf, kWsProfRound,
     kWsAppSpec, kWsAppPeer, kWsDestCum, kWsHostClass, kWsIpAll, kWsBwu, kWsBwd, kWsProcPort, kWsPortNew, kWsXsend,
-    kWsXrecv, kWsPmine, kWsPall, kWsSlots
+    kWsXrecv, kWsPmine, kWsPall, kWsXcnt, kWsSlots
 };
 struct TcpWs {
     std::mutex mu;
@@ -3077,7 +3086,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     uint64_t rounds = 0;
     std::vector<DHost> hout(nloc);
     uint32_t* d_ipall = nullptr; uint64_t* d_bwu = nullptr; uint64_t* d_bwd = nullptr;
-    char* d_xrecv = nullptr; uint64_t* d_pmine = nullptr; uint64_t* d_pall = nullptr;
+    char* d_xrecv = nullptr; uint64_t* d_pmine = nullptr; uint64_t* d_pall = nullptr; uint32_t* d_xcnt = nullptr;
     for (int32_t i = 0; i < nloc; i++) {
         DHost& x = hh[i];
         const int32_t gi = h0 + i;
@@ -3182,11 +3191,21 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     g.ip_all = d_ipall; g.bwu_all = d_bwu; g.bwd_all = d_bwd;
     HCHECK(ws_alloc(ws, kWsProcPort, &g.proc_port, sizeof(uint32_t) * pp.size()));
     HCHECK(hipMemset(g.proc_port, 0, sizeof(uint32_t) * pp.size()));
-    HCHECK(ws_alloc(ws, kWsPortNew, &g.port_new, sizeof(uint64_t) * (kPortNew + 1)));
-    g.nport_new = (uint32_t*)(g.port_new + kPortNew);
-    HCHECK(hipMemset(g.port_new, 0, sizeof(uint64_t) * (kPortNew + 1)));
+    {   // every engine sizes the publications alike: the most processes any engine's hosts run
+        std::vector<uint32_t> per(world, 0);
+        for (int32_t k = 0; k < P; k++) {
+            int32_t r = 0;
+            while (r + 1 < world && (int64_t)m->proc_host[k] >= ((int64_t)(r + 1) * H) / world) r++;
+            per[r]++;
+        }
+        g.pcap = 1;
+        for (uint32_t v : per) g.pcap = v > g.pcap ? v : g.pcap;
+    }
+    HCHECK(ws_alloc(ws, kWsPortNew, &g.port_new, sizeof(uint64_t) * (g.pcap + 1)));
+    g.nport_new = (uint32_t*)(g.port_new + g.pcap);
+    HCHECK(hipMemset(g.port_new, 0, sizeof(uint64_t) * (g.pcap + 1)));
     if (world > 1) {   // the exchange's segments (SHD_TCP_XCAP: deliveries per engine pair and round)
-        g.xcap = 4096;
+        g.xcap = (uint32_t)std::max<int64_t>(16384, 8 * (int64_t)nloc);
         if (const char* e = getenv("SHD_TCP_XCAP")) {
             const long v = strtol(e, nullptr, 10);
             if (v >= 16 && v <= (1l << 22)) g.xcap = (uint32_t)v;
@@ -3197,8 +3216,9 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         HCHECK(ws_alloc(ws, kWsXsend, &g.xsend, g.xseg * (size_t)world));
         HCHECK(ws_alloc(ws, kWsXrecv, &d_xrecv, g.xseg * (size_t)world));
         HCHECK(hipMemset(g.xsend, 0, g.xseg * (size_t)world));
-        HCHECK(ws_alloc(ws, kWsPmine, &d_pmine, sizeof(uint64_t) * (1 + kPortNew)));
-        HCHECK(ws_alloc(ws, kWsPall, &d_pall, sizeof(uint64_t) * (1 + kPortNew) * (size_t)world));
+        HCHECK(ws_alloc(ws, kWsPmine, &d_pmine, sizeof(uint64_t) * (1 + g.pcap)));
+        HCHECK(ws_alloc(ws, kWsPall, &d_pall, sizeof(uint64_t) * (1 + g.pcap) * (size_t)world));
+        HCHECK(ws_alloc(ws, kWsXcnt, &d_xcnt, sizeof(uint32_t) * 4 * (size_t)world));
     }
     HCHECK(ws_alloc(ws, kWsHv, &d_hv, sizeof(int32_t) * (size_t)H));
     HCHECK(hipMemcpy(d_hv, hvi.data(), sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
@@ -3336,7 +3356,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                     halted |= all[r].halted;
                 }
                 if (anyport) {
-                    if (shd_comm_allgather_dev(comm, d_pmine, d_pall, sizeof(uint64_t) * (1 + kPortNew), st)) {
+                    if (shd_comm_allgather_dev(comm, d_pmine, d_pall, sizeof(uint64_t) * (1 + g.pcap), st)) {
                         rc = -5;
                         goto done;
                     }
@@ -3351,8 +3371,36 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                 }
                 k_tcp_round<<<blocks, threads, 0, st>>>(g);
                 HCHECK(hipGetLastError());
-                if (shd_comm_alltoall_dev(comm, g.xsend, d_xrecv, g.xseg, st)) { rc = -5; goto done; }
-                k_tcp_xingest<<<world, 256, 0, st>>>(g, d_xrecv);
+                {   // the segments' used parts only: the counts first (one all-gather), then an all-to-all-v
+                    uint32_t heads[128], allh[64 * 128];
+                    k_tcp_xheads<<<1, 64, 0, st>>>(g, d_xcnt);
+                    HCHECK(hipMemcpyAsync(heads, d_xcnt, sizeof(uint32_t) * 2 * world, hipMemcpyDeviceToHost, st));
+                    HCHECK(hipStreamSynchronize(st));
+                    if (shd_comm_allgather_host(comm, heads, sizeof(uint32_t) * 2 * world, allh)) { rc = -5; goto done; }
+                    size_t so[64], sb[64], ro[64], rb[64], so2[64], sb2[64], ro2[64], rb2[64];
+                    uint32_t mine_in[128];
+                    const size_t sack_at = sizeof(XSegHead) + (size_t)g.xcap * sizeof(Mail);
+                    for (int p = 0; p < world; p++) {
+                        const bool self = p == me;
+                        so[p] = ro[p] = (size_t)p * g.xseg + sizeof(XSegHead);
+                        so2[p] = ro2[p] = (size_t)p * g.xseg + sack_at;
+                        sb[p] = self ? 0 : (size_t)heads[2 * p] * sizeof(Mail);
+                        sb2[p] = self ? 0 : (size_t)heads[2 * p + 1] * sizeof(int32_t);
+                        const uint32_t* from = allh + (size_t)p * 2 * world + 2 * me;   // what p sent this engine
+                        mine_in[2 * p] = self ? 0 : from[0];
+                        mine_in[2 * p + 1] = self ? 0 : from[1];
+                        rb[p] = (size_t)mine_in[2 * p] * sizeof(Mail);
+                        rb2[p] = (size_t)mine_in[2 * p + 1] * sizeof(int32_t);
+                    }
+                    if (shd_comm_alltoallv_dev(comm, g.xsend, so, sb, d_xrecv, ro, rb, st) ||
+                        shd_comm_alltoallv_dev(comm, g.xsend, so2, sb2, d_xrecv, ro2, rb2, st)) {
+                        rc = -5;
+                        goto done;
+                    }
+                    // (blocking: the counts leave this stack frame; the last round's ingest has finished)
+                    HCHECK(hipMemcpy(d_xcnt + 2 * world, mine_in, sizeof(uint32_t) * 2 * world, hipMemcpyHostToDevice));
+                    k_tcp_xingest<<<world, 256, 0, st>>>(g, d_xrecv, d_xcnt + 2 * world);
+                }
                 HCHECK(hipGetLastError());
                 HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));
                 HCHECK(hipStreamSynchronize(st));
