@@ -96,7 +96,8 @@ int shd_comm_alltoall_dev(shd_comm* c, const void* d_send, void* d_recv, size_t 
     return SHD_OK;
 }
 
-int shd_comm_alltoallv_dev(shd_comm* c, const char* d_send, const size_t* send_off, const size_t* send_bytes,
+// (declared where it is used: csrc/tcp.hip)
+__attribute__((visibility("hidden"))) int shd_comm_alltoallv_dev(shd_comm* c, const char* d_send, const size_t* send_off, const size_t* send_bytes,
                            char* d_recv, const size_t* recv_off, const size_t* recv_bytes, hipStream_t s) {
     const int W = c->world;
     if (c->kind == SHD_COMM_RCCL) {

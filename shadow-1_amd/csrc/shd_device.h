@@ -101,15 +101,6 @@ __attribute__((visibility("hidden"))) int shd_comm_alltoall_dev(shd_comm* c, con
                                                                 size_t bytes_per_peer, hipStream_t s);
 __attribute__((visibility("hidden"))) int shd_comm_allgather_dev(shd_comm* c, const void* d_send, void* d_recv,
                                                                  size_t bytes, hipStream_t s);
-// device buffers of per-peer sizes: peer p gets send_bytes[p] from
-// d_send + send_off[p], this rank recv_bytes[p] from peer p into d_recv +
-// recv_off[p] (the sizes agreed beforehand: recv_bytes[p] = what p sends here);
-// RCCL: grouped send / receive on `s`; host transport: fixed blocks of the
-// largest size through host memory (synchronizes `s`)
-__attribute__((visibility("hidden"))) int shd_comm_alltoallv_dev(shd_comm* c, const char* d_send,
-                                                                 const size_t* send_off, const size_t* send_bytes,
-                                                                 char* d_recv, const size_t* recv_off,
-                                                                 const size_t* recv_bytes, hipStream_t s);
 // host buffers, blocking: out[r * bytes ...] = rank r's `bytes`
 __attribute__((visibility("hidden"))) int shd_comm_allgather_host(shd_comm* c, const void* mine, size_t bytes,
                                                                   void* out);

@@ -47,6 +47,14 @@
 
 #include "../../include/shdtcp.h"
 #include "shd_device.h"   // struct shd_pc: the path cache's device tables (shd_tcp_model.path_cache)
+// comm.hip: device buffers of per-peer sizes -- peer p gets send_bytes[p] from d_send +
+// send_off[p], this rank recv_bytes[p] from peer p into d_recv + recv_off[p] (the sizes
+// agreed beforehand); RCCL: grouped send / receive on `s`; the host transport: fixed
+// blocks of the largest size through host memory (synchronizes `s`)
+__attribute__((visibility("hidden"))) int shd_comm_alltoallv_dev(shd_comm* c, const char* d_send,
+                                                                 const size_t* send_off, const size_t* send_bytes,
+                                                                 char* d_recv, const size_t* recv_off,
+                                                                 const size_t* recv_bytes, hipStream_t s);
 
 namespace {
 
