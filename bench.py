@@ -66,6 +66,9 @@ def parse():
                          "TCP path (include/shdtcp.h) on workloads.tcp_echo_model, one run per step")
     ap.add_argument("--tcp-bytes", type=int, default=500000, help="tcp: bytes each client echoes")
     ap.add_argument("--tcp-end-s", type=int, default=20, help="tcp: simulated seconds")
+    ap.add_argument("--tcp-udp", action="store_true",
+                    help="tcp: both transports -- workloads.mixed_transport_model (a datagram process on every "
+                         "host beside the echo pairs)")
     ap.add_argument("--tcp-pool", type=int, default=2048,
                     help="tcp: packet pool per host (shd_tcp_model.packets_per_host; overflow fails the run)")
     ap.add_argument("--relays", type=int, default=6500)
@@ -480,14 +483,18 @@ def tcp_main(args):
     H = (args.hosts_per_gpu or 65536) * max(world, 1)
     pool = args.tcp_pool
     V = min(args.vertices, 1000)
-    mk = lambda n: W.tcp_echo_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,  # noqa: E731
-                                    loss_max=args.edge_loss_max)
-    g, m, ips, procs, peers, nb = mk(H)
+    def mk(n):
+        if args.tcp_udp:
+            return W.mixed_transport_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,
+                                           loss_max=args.edge_loss_max)
+        return W.tcp_echo_model(n, V, seed=args.seed, end_s=args.tcp_end_s, nbytes=args.tcp_bytes,
+                                loss_max=args.edge_loss_max) + (None,)
+    g, m, ips, procs, peers, nb, udp = mk(H)
     # a caller running many models keeps the run's device buffers between
     # calls (shdtcp.h shd_tcp_keep_workspace); the first call allocates them
     S.lib().shd_tcp_keep_workspace(1)
     run1 = lambda: T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool,  # noqa: E731
-                         comm=comm, mode="tables" if comm is not None else "device")
+                         comm=comm, mode="tables" if comm is not None else "device", udp=udp)
     for _ in range(args.warmup):
         run1()
     mark = Roctx()
@@ -534,10 +541,10 @@ def tcp_main(args):
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests"))
         import oracle_ffi as O
         hs = min(H, 4096)
-        gs, ms, ipss, pss, prs, _ = mk(hs) if hs != H else (g, m, ips, procs, peers, nb)
-        rs = T.run(ms, gs, ipss, pss, prs, nbytes=nb, trace=False, packets_per_host=pool) if hs != H else r
+        gs, ms, ipss, pss, prs, _, us = mk(hs) if hs != H else (g, m, ips, procs, peers, nb, udp)
+        rs = T.run(ms, gs, ipss, pss, prs, nbytes=nb, trace=False, packets_per_host=pool, udp=us) if hs != H else r
         tc = time.perf_counter()
-        o = O.tcp_run(ms, gs, ipss, pss, prs, nbytes=nb, lines=False)
+        o = O.tcp_run(ms, gs, ipss, pss, prs, nbytes=nb, lines=False, udp=us)
         cs = time.perf_counter() - tc
         same = (o["events"] == rs["events"] and o["next_event_id"].tolist() == rs["next_event_id"].tolist()
                 and o["next_packet_id"].tolist() == rs["next_packet_id"].tolist()
@@ -554,8 +561,10 @@ def tcp_main(args):
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (random geometric topology + TCP echo pairs, seed %d)"
         % args.seed,
         "config": {"workload": "TCP echo (src/test/tcp/test_tcp.c, nonblocking-epoll), %d hosts / %d pairs, "
-                               "%d-vertex geometric topology, %d B each way, %d s simulated"
-                               % (H, H // 2, V, nb, args.tcp_end_s),
+                               "%d-vertex geometric topology, %d B each way, %d s simulated%s"
+                               % (H, H // 2, V, nb, args.tcp_end_s,
+                                  "; and a datagram process per host (workloads.mixed_transport_model)"
+                                  if args.tcp_udp else ""),
                    "hosts": H, "vertices": V, "packets_per_host": pool,
                    "parallelism": "one lane per host, %s" % (
                        "1 GPU" if world <= 1 else "hosts sharded over %d ranks (shd_tcp_run_group, %s)"
