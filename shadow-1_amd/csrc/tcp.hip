@@ -2893,6 +2893,18 @@ static int tcp_pc_prep(shd_pc* pc, const std::vector<int32_t>& conn, uint64_t* W
     return 0;
 }
 
+// a group's small all-gather of host words through two kept device buffers (one
+// RCCL all-gather on the run's stream, or the host transport's): shd_comm_
+// allgather_host would allocate and free device memory every call, twice a round
+static int group_allgather(shd_comm* comm, char* d_mine, char* d_all, const void* mine, void* all, size_t bytes,
+                           hipStream_t st) {
+    if (comm->kind == SHD_COMM_HOST) return shd_comm_allgather_host(comm, mine, bytes, all) ? -5 : 0;
+    if (hipMemcpyAsync(d_mine, mine, bytes, hipMemcpyHostToDevice, st) != hipSuccess) return -5;
+    if (shd_comm_allgather_dev(comm, d_mine, d_all, bytes, st)) return -5;
+    if (hipMemcpyAsync(all, d_all, bytes * (size_t)comm->world, hipMemcpyDeviceToHost, st) != hipSuccess) return -5;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : -5;
+}
+
 static double ms_since(std::chrono::steady_clock::time_point t) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
 }
@@ -2909,7 +2921,7 @@ enum WsSlot {
     kWsHostProcs, kWsPool, kWsPsack, kWsFreel, kWsEv, kWsCq, kWsMsack, kWsNmsack, kWsMail, kWsNmail, kWsMhead,
     kWsMnext, kWsCtl, kWsIpk, kWsNode, kWsTr, kWsTrs, kWsNextTime, kWsQlog, kWsNqlog, kWsProf, kWsProfRound,
     kWsAppSpec, kWsAppPeer, kWsDestCum, kWsHostClass, kWsIpAll, kWsBwu, kWsBwd, kWsProcPort, kWsPortNew, kWsXsend,
-    kWsXrecv, kWsPmine, kWsPall, kWsXcnt, kWsSlots
+    kWsXrecv, kWsPmine, kWsPall, kWsXcnt, kWsGmine, kWsGall, kWsSlots
 };
 struct TcpWs {
     std::mutex mu;
@@ -3095,6 +3107,8 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     std::vector<DHost> hout(nloc);
     uint32_t* d_ipall = nullptr; uint64_t* d_bwu = nullptr; uint64_t* d_bwd = nullptr;
     char* d_xrecv = nullptr; uint64_t* d_pmine = nullptr; uint64_t* d_pall = nullptr; uint32_t* d_xcnt = nullptr;
+    char* d_gmine = nullptr; char* d_gall = nullptr;
+    constexpr size_t kGatherMax = 1024;   // bytes one rank contributes to a control all-gather (<= 64 engines)
     for (int32_t i = 0; i < nloc; i++) {
         DHost& x = hh[i];
         const int32_t gi = h0 + i;
@@ -3227,6 +3241,8 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         HCHECK(ws_alloc(ws, kWsPmine, &d_pmine, sizeof(uint64_t) * (1 + g.pcap)));
         HCHECK(ws_alloc(ws, kWsPall, &d_pall, sizeof(uint64_t) * (1 + g.pcap) * (size_t)world));
         HCHECK(ws_alloc(ws, kWsXcnt, &d_xcnt, sizeof(uint32_t) * 4 * (size_t)world));
+        HCHECK(ws_alloc(ws, kWsGmine, &d_gmine, kGatherMax));
+        HCHECK(ws_alloc(ws, kWsGall, &d_gall, kGatherMax * (size_t)world));
     }
     HCHECK(ws_alloc(ws, kWsHv, &d_hv, sizeof(int32_t) * (size_t)H));
     HCHECK(hipMemcpy(d_hv, hvi.data(), sizeof(int32_t) * (size_t)H, hipMemcpyHostToDevice));
@@ -3355,7 +3371,8 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                     HCHECK(hipMemcpy(&np, d_pmine, sizeof(uint64_t), hipMemcpyDeviceToHost));
                     mine.nport = (uint32_t)np;
                 }
-                if (shd_comm_allgather_host(comm, &mine, sizeof(mine), all)) { rc = -5; goto done; }
+                static_assert(sizeof(mine) <= 1024, "control word");
+                if (group_allgather(comm, d_gmine, d_gall, &mine, all, sizeof(mine), st)) { rc = -5; goto done; }
                 uint64_t t = ~0ull;
                 uint32_t anyport = 0, halted = 0;
                 for (int r = 0; r < world; r++) {
@@ -3384,7 +3401,10 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                     k_tcp_xheads<<<1, 64, 0, st>>>(g, d_xcnt);
                     HCHECK(hipMemcpyAsync(heads, d_xcnt, sizeof(uint32_t) * 2 * world, hipMemcpyDeviceToHost, st));
                     HCHECK(hipStreamSynchronize(st));
-                    if (shd_comm_allgather_host(comm, heads, sizeof(uint32_t) * 2 * world, allh)) { rc = -5; goto done; }
+                    if (group_allgather(comm, d_gmine, d_gall, heads, allh, sizeof(uint32_t) * 2 * world, st)) {
+                        rc = -5;
+                        goto done;
+                    }
                     size_t so[64], sb[64], ro[64], rb[64], so2[64], sb2[64], ro2[64], rb2[64];
                     uint32_t mine_in[128];
                     const size_t sack_at = sizeof(XSegHead) + (size_t)g.xcap * sizeof(Mail);

@@ -82,3 +82,25 @@ def test_tcp_group_scaled_equals_oracle(case, world, tmp_path):
     assert cat["next_packet_id"] == o["next_packet_id"].tolist()
     assert cat["rng_probe"] == o["rng_probe"].tolist()
     assert sum(int(r["events"]) for r in res) == o["events"]
+
+
+def test_tcp_group_rccl_one_rank_equals_one_engine():
+    """The RCCL communicator's calls of the group run (all-gathers, the grouped
+    send / receive of the all-to-all-v) on a one-rank group: RCCL refuses two
+    ranks on one GPU, so the multi-rank path is tested over the host-memory
+    transport above and this runs RCCL's side alone -- equal to shd_tcp_run."""
+    import sim
+    import tcp as TCPGPU
+    f = FIX["mixed_hosts"]
+    c, m = TC.build("mixed_hosts")
+    ips = TC.ip_ints(f["ips"])
+    comm = sim.Comm.rccl(sim.XGroup.unique_id(), 1, 0, 0)
+    try:
+        r = TCPGPU.run(m, c["graph"], ips, c["procs"], c["peers"], nbytes=c["nbytes"], node=True,
+                       udp=TC.udp_arg(c), comm=comm, mode="tables")
+    finally:
+        comm.close()
+    assert r["first_host"] == 0 and r["n_local_hosts"] == len(ips)
+    assert TC.digest(r["lines"]) == f["status_by_host_sha256"]
+    assert r["next_event_id"].tolist() == f["next_event_id"]
+    assert r["rng_probe"].tolist() == f["rng_probe"]
