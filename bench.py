@@ -494,7 +494,7 @@ def tcp_main(args):
     # calls (shdtcp.h shd_tcp_keep_workspace); the first call allocates them
     S.lib().shd_tcp_keep_workspace(1)
     run1 = lambda: T.run(m, g, ips, procs, peers, nbytes=nb, trace=False, packets_per_host=pool,  # noqa: E731
-                         comm=comm, mode="tables" if comm is not None else "device", udp=udp)
+                         comm=comm, udp=udp)
     for _ in range(args.warmup):
         run1()
     mark = Roctx()

@@ -178,10 +178,13 @@ void shd_tcp_result_free(shd_tcp_result* r);
  * (SHD_TCP_XCAP deliveries per engine pair and round, 4096 by default; more
  * set SHD_TCP_ERR_MAILBOX), and the servers' listening ports their clients
  * connect to are published to every engine.  Results equal shd_tcp_run's on
- * the same model, host by host.  Tables only (path_cache NULL; -22 otherwise):
- * the queries every engine logged come back in each rank's result, for the
- * caller's first-touch ranking as on one engine.  Returns as shd_tcp_run, -5
- * also when the group's communication fails. */
+ * the same model, host by host.  Paths: with path_cache (every rank's own
+ * cache of the same graph, built alike) each round's first-touch log of every
+ * engine is gathered and replayed alike on every rank, so the ranks stay
+ * equal and a contradicted choice stops every rank at the same round
+ * (SHD_TCP_ERR_FIRST_TOUCH); with tables the queries every engine logged come
+ * back in each rank's result, for the caller's ranking as on one engine.
+ * Returns as shd_tcp_run, -5 also when the group's communication fails. */
 struct shd_comm;
 int shd_tcp_run_group(const shd_tcp_model* m, struct shd_comm* comm, int32_t trace, shd_tcp_result** out);
 

@@ -2630,9 +2630,11 @@ __global__ void k_tcp_xingest(Glob g, const char* __restrict__ xrecv, const uint
         mnext[slot] = atomicExch(&mhead[dl], (int32_t)slot);
     }
 }
-// what this engine's segments hold after the round ([world][2]: mails, SACK words)
+// what this engine's segments hold after the round ([world][2]: mails, SACK
+// words), then the round's first-touch log entries (path_cache mode)
 __global__ void k_tcp_xheads(Glob g, uint32_t* __restrict__ heads) {
     const int32_t p = (int32_t)threadIdx.x;
+    if (p == 0) heads[2 * g.world] = g.pcm ? *g.nft : 0u;
     if (p >= g.world) return;
     const XSegHead* hd = (const XSegHead*)(g.xsend + (size_t)p * g.xseg);
     heads[2 * p] = hd->n < g.xcap ? hd->n : g.xcap;
@@ -2980,8 +2982,6 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     auto t_results = t_call;
     shd_pc* pc = m ? m->path_cache : nullptr;
     const int32_t world = comm ? comm->world : 1, me = comm ? comm->rank : 0;
-    // a group runs on tables (the device first-touch replay ranks one engine's log)
-    if (comm && pc) return -22;
     if (!m || !out || m->n_hosts <= 0 || m->n_hosts > (1 << 26) || m->n_procs < 0 || !m->host_ip || !m->host_seed || !m->bw_down_kibps ||
         !m->bw_up_kibps || (!pc && (!m->path_lat_ms || !m->path_rel || m->n_vertices <= 0)) || !m->host_vertex ||
         (m->n_procs && (!m->proc_host || !m->proc_start || !m->proc_peer)))
@@ -3198,7 +3198,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         HCHECK(hipMemcpy(g.rank, pc->h_rank, sizeof(int32_t) * (size_t)V, hipMemcpyHostToDevice));
         HCHECK(hipMemcpy(g.srank, pc->h_self_rank, sizeof(int32_t) * (size_t)V, hipMemcpyHostToDevice));
         HCHECK(hipMemcpy(g.next_rank, &pc->next_rank, sizeof(int32_t), hipMemcpyHostToDevice));
-        g.ft_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);
+        g.ft_cap = (uint32_t)H * 4u > (1u << 16) ? (uint32_t)H * 4u : (1u << 16);   // (a group's: every engine's log)
         HCHECK(ws_alloc(ws, kWsFt, &g.ft, sizeof(shd_tcp_query) * (size_t)g.ft_cap));
         HCHECK(ws_alloc(ws, kWsFtord, &g.ftord, sizeof(int32_t) * (size_t)g.ft_cap));
         HCHECK(ws_alloc(ws, kWsNft, &g.nft, sizeof(uint32_t)));
@@ -3240,7 +3240,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         HCHECK(hipMemset(g.xsend, 0, g.xseg * (size_t)world));
         HCHECK(ws_alloc(ws, kWsPmine, &d_pmine, sizeof(uint64_t) * (1 + g.pcap)));
         HCHECK(ws_alloc(ws, kWsPall, &d_pall, sizeof(uint64_t) * (1 + g.pcap) * (size_t)world));
-        HCHECK(ws_alloc(ws, kWsXcnt, &d_xcnt, sizeof(uint32_t) * 4 * (size_t)world));
+        HCHECK(ws_alloc(ws, kWsXcnt, &d_xcnt, sizeof(uint32_t) * (4 * (size_t)world + 2)));
         HCHECK(ws_alloc(ws, kWsGmine, &d_gmine, kGatherMax));
         HCHECK(ws_alloc(ws, kWsGall, &d_gall, kGatherMax * (size_t)world));
     }
@@ -3397,13 +3397,39 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                 k_tcp_round<<<blocks, threads, 0, st>>>(g);
                 HCHECK(hipGetLastError());
                 {   // the segments' used parts only: the counts first (one all-gather), then an all-to-all-v
-                    uint32_t heads[128], allh[64 * 128];
+                    uint32_t heads[129], allh[64 * 129];
+                    const size_t hs = 2 * (size_t)world + 1;   // per engine: its segments' counts, its log entries
                     k_tcp_xheads<<<1, 64, 0, st>>>(g, d_xcnt);
-                    HCHECK(hipMemcpyAsync(heads, d_xcnt, sizeof(uint32_t) * 2 * world, hipMemcpyDeviceToHost, st));
+                    HCHECK(hipMemcpyAsync(heads, d_xcnt, sizeof(uint32_t) * hs, hipMemcpyDeviceToHost, st));
                     HCHECK(hipStreamSynchronize(st));
-                    if (group_allgather(comm, d_gmine, d_gall, heads, allh, sizeof(uint32_t) * 2 * world, st)) {
+                    if (group_allgather(comm, d_gmine, d_gall, heads, allh, sizeof(uint32_t) * hs, st)) {
                         rc = -5;
                         goto done;
+                    }
+                    if (g.pcm) {   // the round's first touches: every engine's log replayed alike (k_tcp_window)
+                        uint32_t mx = 0, tot = 0;
+                        for (int r = 0; r < world; r++) {
+                            const uint32_t n = allh[(size_t)r * hs + 2 * world];
+                            mx = n > mx ? n : mx;
+                            tot += n;
+                        }
+                        if (mx) {
+                            if (mx > g.ft_cap || tot > g.ft_cap) { res->error |= SHD_TCP_ERR_FIRST_TOUCH; break; }
+                            std::vector<shd_tcp_query> mine_q(mx), all_q((size_t)mx * world);
+                            const uint32_t nme = allh[(size_t)me * hs + 2 * world];
+                            if (nme) HCHECK(hipMemcpy(mine_q.data(), g.ft, sizeof(shd_tcp_query) * nme, hipMemcpyDeviceToHost));
+                            if (shd_comm_allgather_host(comm, mine_q.data(), sizeof(shd_tcp_query) * mx, all_q.data())) {
+                                rc = -5;
+                                goto done;
+                            }
+                            std::vector<shd_tcp_query> uni;
+                            uni.reserve(tot);
+                            for (int r = 0; r < world; r++)
+                                for (uint32_t j = 0; j < allh[(size_t)r * hs + 2 * world]; j++)
+                                    uni.push_back(all_q[(size_t)r * mx + j]);
+                            HCHECK(hipMemcpy(g.ft, uni.data(), sizeof(shd_tcp_query) * tot, hipMemcpyHostToDevice));
+                            HCHECK(hipMemcpy(g.nft, &tot, sizeof(uint32_t), hipMemcpyHostToDevice));
+                        }
                     }
                     size_t so[64], sb[64], ro[64], rb[64], so2[64], sb2[64], ro2[64], rb2[64];
                     uint32_t mine_in[128];
@@ -3414,7 +3440,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                         so2[p] = ro2[p] = (size_t)p * g.xseg + sack_at;
                         sb[p] = self ? 0 : (size_t)heads[2 * p] * sizeof(Mail);
                         sb2[p] = self ? 0 : (size_t)heads[2 * p + 1] * sizeof(int32_t);
-                        const uint32_t* from = allh + (size_t)p * 2 * world + 2 * me;   // what p sent this engine
+                        const uint32_t* from = allh + (size_t)p * hs + 2 * me;   // what p sent this engine
                         mine_in[2 * p] = self ? 0 : from[0];
                         mine_in[2 * p + 1] = self ? 0 : from[1];
                         rb[p] = (size_t)mine_in[2 * p] * sizeof(Mail);
@@ -3426,8 +3452,8 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                         goto done;
                     }
                     // (blocking: the counts leave this stack frame; the last round's ingest has finished)
-                    HCHECK(hipMemcpy(d_xcnt + 2 * world, mine_in, sizeof(uint32_t) * 2 * world, hipMemcpyHostToDevice));
-                    k_tcp_xingest<<<world, 256, 0, st>>>(g, d_xrecv, d_xcnt + 2 * world);
+                    HCHECK(hipMemcpy(d_xcnt + hs, mine_in, sizeof(uint32_t) * 2 * world, hipMemcpyHostToDevice));
+                    k_tcp_xingest<<<world, 256, 0, st>>>(g, d_xrecv, d_xcnt + hs);
                 }
                 HCHECK(hipGetLastError());
                 HCHECK(hipMemcpyAsync(&hctl, g.ctl, sizeof(TCtl), hipMemcpyDeviceToHost, st));

@@ -118,9 +118,10 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
     weights.
     comm (sim.Comm): this rank's share of a group run (shd_tcp_run_group: every
     rank calls with the same model; the result covers hosts [first_host,
-    first_host + n_local_hosts), the lines carry the model's host index); a
-    group runs on tables, the first-touch ranking over every rank's log."""
-    if mode == "device" and not guess_reversed and not g.directed and comm is None:
+    first_host + n_local_hosts), the lines carry the model's host index); every
+    rank's first touches are ranked together, on the device (each round's logs
+    gathered) or over the tables' query logs."""
+    if mode == "device" and not guess_reversed and not g.directed:
         m = model.struct
         H = int(m.n_hosts)
         hv = np.ctypeslib.as_array(m.host_vertex, shape=(H,)).copy()
@@ -129,7 +130,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
         pc_ms = (time.perf_counter() - t_pc) * 1e3
         try:
             out = _run_once(model, ips, procs, peers, None, None, hv.astype(np.int32), nbytes, trace, recv_buf,
-                            send_buf, tcp_window, packets_per_host, node, qdisc, pc=pc, udp=udp)
+                            send_buf, tcp_window, packets_per_host, node, qdisc, pc=pc, udp=udp, comm=comm)
         finally:
             pc.close()
         if out is not None:

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--name", required=True)
     ap.add_argument("--out", required=True)
     ap.add_argument("--case", required=True, help="a tcp_cases name, or mixed:H:loss:qdisc, or echo:H:loss")
+    ap.add_argument("--mode", default="tables", choices=["tables", "device"])
     a = ap.parse_args()
     import sim
     import tcp as TCPGPU
@@ -46,13 +47,13 @@ def main():
         g, ips, procs, peers, nb = c["graph"], TC.ip_ints(fix["ips"]), c["procs"], c["peers"], c["nbytes"]
         udp, qdisc = TC.udp_arg(c), c.get("qdisc", 0)
     comm = sim.Comm.host(a.name, a.world, a.rank, 0)
-    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, node=True, qdisc=qdisc, udp=udp, comm=comm, mode="tables")
+    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, node=True, qdisc=qdisc, udp=udp, comm=comm, mode=a.mode)
     comm.close()
     np.savez(os.path.join(a.out, f"rank{a.rank}.npz"), lines=json.dumps(r["lines"]),
              node_lines=json.dumps(r["node_lines"]), next_event_id=r["next_event_id"],
              next_packet_id=r["next_packet_id"], rng_probe=r["rng_probe"], first_host=r["first_host"],
              n_local_hosts=r["n_local_hosts"], rounds=r["rounds"], events=r["events"],
-             first_touch_runs=r.get("first_touch_runs", 0))
+             first_touch_runs=r.get("first_touch_runs", 0), first_touch=r["first_touch"])
     print(f"rank {a.rank}: hosts [{r['first_host']}, {r['first_host'] + r['n_local_hosts']}) rounds {r['rounds']} "
           f"events {r['events']}", flush=True)
 

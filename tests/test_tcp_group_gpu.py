@@ -23,10 +23,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
 
 
-def run_ranks(world, case, tmp_path, timeout=240):
+def run_ranks(world, case, tmp_path, timeout=240, mode="tables"):
     name = "shdtcp_" + uuid.uuid4().hex[:16]
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "tcp_group_worker.py"), "--rank", str(r),
-                               "--world", str(world), "--name", name, "--out", str(tmp_path), "--case", case],
+                               "--world", str(world), "--name", name, "--out", str(tmp_path), "--case", case,
+                               "--mode", mode],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
              for r in range(world)]
     outs = []
@@ -51,9 +52,19 @@ def run_ranks(world, case, tmp_path, timeout=240):
 
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("name", ["mixed_hosts", "mixed_slow_rr", "geo_pairs", "shared_hosts"])
-def test_tcp_group_equals_reference(name, world, tmp_path):
+@pytest.mark.parametrize("mode", ["tables", "device"])
+def test_tcp_group_equals_reference(name, world, mode, tmp_path):
+    """mode "device": the path cache's first-touch rule on the device, every
+    engine's log of a round gathered and replayed alike (a contradicted choice:
+    every rank falls back to tables together, as shared_hosts does on one engine)"""
     f = FIX[name]
-    lines, node, cat, res = run_ranks(world, name, tmp_path)
+    lines, node, cat, res = run_ranks(world, name, tmp_path, mode=mode)
+    modes = {str(r["first_touch"]) for r in res}
+    assert len(modes) == 1   # every rank alike
+    if mode == "device" and name in ("geo_pairs", "mixed_hosts"):
+        assert modes == {"device"}
+    if name == "shared_hosts":
+        assert modes == {"tables"}
     assert len(lines) == f["n_status"]
     assert TC.digest(lines) == f["status_by_host_sha256"]
     assert len(node) == f["n_heartbeat"] and TC.digest(node) == f["heartbeat_sha256"]
