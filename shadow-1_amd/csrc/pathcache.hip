@@ -89,6 +89,11 @@ constexpr int kChunk = 32;   // edges folded per pass of the forward chain walk
 #ifndef SHD_SSSP_MIXQ
 #define SHD_SSSP_MIXQ 0  // 1: the two-row kernel's rows share one queue (21.35 against 20.28 ms: not kept)
 #endif
+#ifndef SHD_SSSP_BALLOT
+#define SHD_SSSP_BALLOT 0  // 1: the two-row kernel walks only its non-empty bit words (a ballot, one readlane
+                           // each) instead of every chunk's four shuffles: 22.1-22.4 against 21.4 ms on the
+                           // 10 k table (scripts/r05/gpu_apsp_ballot.sh, profiles/r05/apsp_ballot/): not kept
+#endif
 #ifndef SHD_SSSP_BFQ2
 #define SHD_SSSP_BFQ2 2  // ... in the two-row kernel (1: 21.6 ms, 2: 20.3 ms on the 10 k table)
 #endif
@@ -789,6 +794,32 @@ __device__ void sssp_bf2(int32_t srcA, int32_t srcB /* -1: none */, int32_t V, c
         };
         (void)na; (void)nb; (void)run_q;
 #endif
+#if SHD_SSSP_BALLOT && !SHD_SSSP_MIXQ
+        {   // the wave's non-empty words, lane by lane: row A's (lanes 0-19) then row B's (32-51);
+            // any order reaches the same fixpoint (as the bits taken early above)
+            uint64_t nz = __ballot(wbits != 0u);
+            while (nz) {
+                const int ln = __ffsll((unsigned long long)nz) - 1;
+                nz &= nz - 1;
+                uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)wbits, ln);
+                const int j = ln & 31;
+                const int32_t base = (wv + (j >> 1) * NW) * 64 + (j & 1) * 32;
+                if (ln < 32) {
+                    while (m) {
+                        push(qa, base + __builtin_ctz(m));
+                        m &= m - 1;
+                        if (++na == 2 * Q) { run_q(dA, bA, flags, qa); na = 0; }
+                    }
+                } else {
+                    while (m) {
+                        push(qb, base + __builtin_ctz(m));
+                        m &= m - 1;
+                        if (++nb == 2 * Q) { run_q(dB, bB, flags + 4, qb); nb = 0; }
+                    }
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             const int32_t c0 = (wv + c * NW) * 64;
@@ -833,6 +864,9 @@ __device__ void sssp_bf2(int32_t srcA, int32_t srcB /* -1: none */, int32_t V, c
                 if (++nb == 2 * Q) { run_q(dB, bB, flags + 4, qb); nb = 0; }
             }
         }
+#endif
+#endif
+#if !SHD_SSSP_MIXQ
         if (na) {
             while (na < 2 * Q) { push(qa, -1); na++; }
             run_q(dA, bA, flags, qa);
