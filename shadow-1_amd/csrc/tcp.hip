@@ -2439,6 +2439,22 @@ __device__ __forceinline__ bool ft_less(const FtKey& x, const FtKey& y) {
     if (x.seq != y.seq) return x.seq < y.seq;
     return x.index < y.index;
 }
+// a logged choice the serial order contradicts is harmless when both
+// candidates give the pair the same bits (latency and reliability): the lane
+// computed exactly what the serial loop computes, and the replay ranks the
+// rows as the serial order does (every later choice of that lane that its
+// in-round pseudo-ranks decided is logged and checked on its own).  Not
+// where a row's run can fail (a vertex without a self-loop: pc_query's miss)
+__device__ __forceinline__ bool pv_same(const shd_pv& x, const shd_pv& y) {
+    return __double_as_longlong(x.lat) == __double_as_longlong(y.lat) &&
+           __double_as_longlong(x.rel) == __double_as_longlong(y.rel);
+}
+__device__ bool ft_same_value(const Glob& g, int32_t a, int32_t b) {
+    if (g.pself_eid[a] < 0 || g.pself_eid[b] < 0) return false;
+    const size_t T = (size_t)g.pT;
+    if (a == b) return pv_same(g.pself[a], g.prow[(size_t)a * T + a]);
+    return pv_same(g.prow[(size_t)a * T + b], g.prow[(size_t)b * T + a]);
+}
 constexpr uint32_t kFtTile = 512;
 constexpr int32_t kFtLdsRanks = 4096;   // vertices whose ranks the replay keeps in LDS
 __device__ bool ft_replay(const Glob& g, uint32_t n) {
@@ -2499,7 +2515,7 @@ __device__ bool ft_replay(const Glob& g, uint32_t n) {
                     if (ra == kNoRank && rb == kNoRank) { rk[a] = nr++; truth = kFtRowA; }
                     else truth = (ra != kNoRank && (rb == kNoRank || ra < rb)) ? kFtRowA : kFtRowB;
                 }
-                if (truth != choice) s_bad = 1;
+                if (truth != choice && !ft_same_value(g, a, b)) s_bad = 1;
             }
         }
     }
