@@ -3006,7 +3006,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     // lookup reruns rows, topology.c:1987-1990: not restated on the device)
     if (pc && (!pc->built || pc->directed || (!pc->complete && !pc->d_row))) return -22;
     const int32_t H = m->n_hosts, P = m->n_procs;
-    if (world > H) return -22;
+    if (world > H || world > 64) return -22;   // (the group's per-engine tables below hold 64)
     const int32_t h0 = (int32_t)(((int64_t)me * H) / world);
     const int32_t nloc = (int32_t)(((int64_t)(me + 1) * H) / world) - h0;
     auto app_of = [&](int32_t k) { return m->proc_app ? m->proc_app[k] : -1; };
