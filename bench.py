@@ -354,7 +354,8 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(wkey, kname),
                 "traffic_key": wkey + "/" + kname,
-                "kernel": kname, "avg_launch_us": round(avg_launch_ms * 1e3, 3),
+                "kernel": kname, "batches": {"all": n_bat, "persistent": n_ps, "sparse": n_sp},
+                "avg_launch_us": round(avg_launch_ms * 1e3, 3),
                 "avg_round_us": round(avg_launch_ms * 1e3, 3),
                 "rounds_per_launch": round(rounds / max(n_bat, 1), 1) if n_bat else None,
                 "avg_in_kernel_us": round(kms_all / max(launches, 1) * 1e3, 3),

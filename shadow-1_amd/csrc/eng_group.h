@@ -564,12 +564,15 @@ static int x_create(shd_eng* e, shd_comm* comm, uint32_t block_events, bool p2p,
     g->fused = p2p && x_fuse_env() && (sharers <= 1 || shared_blocks <= (unsigned long long)ncu);
     g->end_time = e->P.end_time;
     if (g->fused && !getenv("SHD_X_NO_SP")) {
-        // the sparse fused round (k_round_spx): blocks of sph hosts, about one
+        // the sparse fused round (k_round_spx): blocks of sph hosts, about two
         // per CU, when the engine has more 64-host blocks than two per CU
         // (SHD_SP_HOSTS=<n>: n hosts per block whatever the size, as for one engine)
         const char* sp_env = getenv("SHD_SP_HOSTS");
         const uint32_t sp_force = sp_env ? (uint32_t)strtoul(sp_env, nullptr, 10) : 0u;
-        const uint64_t per = ((uint64_t)e->nloc + ncu - 1) / ncu;
+        // (about two blocks per CU with one rank per GPU, as for one engine; one per CU when
+        // ranks share the GPU)
+        const uint64_t bpc = sharers <= 1 ? 2 : 1;
+        const uint64_t per = ((uint64_t)e->nloc + bpc * ncu - 1) / (bpc * ncu);
         const uint32_t sph = sp_force ? (sp_force + 63) / 64 * 64
                                       : (uint32_t)std::max<uint64_t>(256, (per + 63) / 64 * 64);
         const uint32_t grid = (uint32_t)(((uint64_t)e->nloc + sph - 1) / sph);
@@ -904,15 +907,16 @@ extern "C" int shd_xgroup_run_until(shd_xgroup* g, uint64_t t_stop, shd_run_stat
             }
         }
         if (g->sp_grid && !g->sp_forced && nl == 1) {   // the next batch's kernel, from this batch's activity
-            uint64_t br = 0, ba = 0;
+            uint64_t br = 0, ba = 0, bp = 0;
             const int upto = halted_at >= 0 ? halted_at : nb;
             for (int i = 0; i < upto; i++) {
                 const DevSummary& r0 = g->engs[0]->h_ring[i + 1];
                 if (r0.flags != 0u || r0.ws >= stop) break;
                 br++;
                 ba += r0.n_active;
+                bp += r0.n_pkt_events;
             }
-            if (br) g->sp_dense = (double)ba > kSpDenseFrac * (double)br * (double)g->engs[0]->nloc;
+            if (br) g->sp_dense = sp_dense_batch(br, ba, bp, (uint64_t)g->engs[0]->nloc);
         }
         if (done) break;
         if (halted_at < 0) {

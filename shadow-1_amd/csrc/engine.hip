@@ -651,17 +651,24 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         e->ps_ok = e->h0 == 0 && e->nloc == H && ncu > 0 && per_cu >= 2 && grid <= 2 * ncu && !sp_force;
         size_t nshare = e->ps_ok ? (size_t)grid : 0;
         if (!e->ps_ok && e->h0 == 0 && e->nloc == H && ncu > 0) {
-            // too many hosts for a resident wave each: blocks of sph hosts, one per CU
+            // too many hosts for a resident wave each: blocks of sph hosts, about two per CU
             int per_cu_sp = 0;
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_sp, reinterpret_cast<const void*>(&k_round_sp),
                                                              kBlock, 0) != hipSuccess)
                 per_cu_sp = 0;
             (void)hipGetLastError();
-            const uint64_t per = ((uint64_t)e->nloc + ncu - 1) / ncu;
+            // about two blocks per CU (where occupancy admits two): at the C5 shard 256 hosts a
+            // block ran 23.6 ms a step against 26.2 ms at one block of 512 per CU, and 250 k hosts
+            // 28.5 ms at 512 against 38.7 ms at 1024 (profiles/r05/sph); three per CU lost again
+            const uint64_t bpc = per_cu_sp >= 2 ? 2 : 1;
+            const uint64_t per = ((uint64_t)e->nloc + bpc * ncu - 1) / (bpc * ncu);
             const uint32_t sph = sp_force ? (sp_force + 63) / 64 * 64
                                           : (uint32_t)std::max<uint64_t>(256, (per + 63) / 64 * 64);
             const uint32_t g = (uint32_t)(((uint64_t)e->nloc + sph - 1) / sph);
             const bool no_sp = getenv("SHD_NO_SP") != nullptr;   // perf knob: k_round_tl batches instead
+            if (getenv("SHD_SP_VERBOSE"))
+                fprintf(stderr, "shd: sparse rounds: %d CUs, %d blocks per CU resident, %u hosts per block, %u blocks\n",
+                        ncu, per_cu_sp, sph, g);
             if (!no_sp && per_cu_sp >= 1 && sph <= kSpMaxHosts && g <= (uint32_t)(ncu * per_cu_sp)) {
                 e->sp_ok = true;
                 e->sp_forced = sp_force != 0;
@@ -1012,8 +1019,23 @@ static int launch_batch(shd_eng* e, bool tl) {
 
 // a persistent batch: nb rounds in one launch (k_round_ps); the shares' tags
 // advance past the batch whatever it ran
-// active hosts per round above which launch-per-round batches beat k_round_sp
-static constexpr double kSpDenseFrac = 0.08;
+// when launch-per-round batches beat k_round_sp: the last batch's packet events per host-round
+// above 0.08, or its active hosts above 30 % of the hosts (several passes a block).  Measured
+// per batch kind over whole runs (profiles/r05/sph/spverb/): C5's shard decays from 90 % active
+// hosts at 0.35 events per active host, where the sparse round loses up to 46 % (0.67: 82 against
+// 60 µs a round), through a tie at 0.09 events per host-round (46 against 47 µs) to 4 % active,
+// where it wins by a third (23 against 33 µs); C4 at 14 % active hosts but 1.4 events each
+// (0.2 per host-round) runs 226 µs sparse against 128 µs; C3 at 100 k hosts (0.3 per host-round)
+// 45 against 43 µs.  (SHD_SP_DENSE_FRAC / SHD_SP_DENSE_PKT: other thresholds, for measurements)
+static double env_or(const char* name, double dflt) {
+    const char* v = getenv(name);
+    return v ? strtod(v, nullptr) : dflt;
+}
+static bool sp_dense_batch(uint64_t rounds, uint64_t active, uint64_t pkt, uint64_t nloc) {
+    static const double f_act = env_or("SHD_SP_DENSE_FRAC", 0.3), f_pkt = env_or("SHD_SP_DENSE_PKT", 0.08);
+    const double hr = (double)rounds * (double)nloc;
+    return (double)active > f_act * hr || (double)pkt > f_pkt * hr;
+}
 
 static int launch_batch_ps(shd_eng* e, int nb) {
     const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
@@ -1336,7 +1358,8 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
         // with at most one logging round the next batch is ticketless (the
         // late, rare logs cost one halt each); after more, it is ticketed.
         uint32_t n_logs = 0;
-        uint64_t b_rounds = 0, b_active = 0;
+        uint64_t b_rounds = 0, b_active = 0, b_pkt = 0;
+        double b_ms = 0;
         bool amb = false;
         uint64_t amb_ws = 0;
         for (int i = 0; i < nb; i++) {
@@ -1360,6 +1383,8 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             s.n_host_rounds += r.n_active;
             b_rounds++;
             b_active += r.n_active;
+            b_pkt += r.n_pkt_events;
+            b_ms += ms;
             uint64_t we = ws + e->window;
             if (we > stop || we < ws) we = stop;
             s.final_time = we;
@@ -1401,7 +1426,12 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             next = r.next_time;
         }
         e->tl_ready = n_logs <= 1;
-        if (b_rounds && tl && !e->sp_forced) e->sp_dense = (double)b_active > kSpDenseFrac * (double)b_rounds * (double)e->nloc;
+        if (b_rounds && tl && getenv("SHD_SP_VERBOSE"))
+            fprintf(stderr, "shd: batch %s rounds %llu active/round %.4f pkt/round %.1f us/round %.2f\n",
+                    e->sp_ok && !e->sp_dense ? "sp" : "tl", (unsigned long long)b_rounds,
+                    (double)b_active / ((double)b_rounds * (double)e->nloc), (double)b_pkt / (double)b_rounds,
+                    b_ms * 1e3 / (double)b_rounds);
+        if (b_rounds && tl && !e->sp_forced) e->sp_dense = sp_dense_batch(b_rounds, b_active, b_pkt, (uint64_t)e->nloc);
         if (amb) {
             uint64_t we = amb_ws + e->window;
             if (we > stop || we < amb_ws) we = stop;
