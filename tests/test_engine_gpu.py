@@ -212,14 +212,19 @@ def test_run_to_run_determinism():
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
 
 
-@pytest.mark.parametrize("sph,kind", [(256, "geo"), (64, "geo"), (1024, "codel"), (192, "complete")])
+@pytest.mark.parametrize("sph,kind", [(256, "geo"), (64, "geo"), (1024, "codel"), (192, "complete"), (64, "wide")])
 def test_sparse_persistent_rounds_match_oracle(sph, kind, monkeypatch):
     """k_round_sp (the engines with more hosts than resident waves: the C5
     shard) forced on small models with SHD_SP_HOSTS: blocks of `sph` hosts scan
     their hosts, compact the active ones and run them 64 at a time (several
-    passes a round at 1024 hosts per block); the result is the serial run's."""
+    passes a round at 1024 hosts per block); the result is the serial run's.
+    "wide": 33 600 hosts in 525 blocks, more shares than one round trip of the
+    gather polls (512)."""
     monkeypatch.setenv("SHD_SP_HOSTS", str(sph))
-    if kind == "complete":
+    if kind == "wide":
+        g = W.geometric_graph(400, seed=2)
+        m = W.phold_model(W.hosts_on_vertices(400, 84), end_time=int(1.3 * S.SHD_SEC), trace=True, load=2)
+    elif kind == "complete":
         g = W.bundled_graph()
         hv = np.sort(np.random.default_rng(2).integers(0, g.n_vertices, 700)).astype(np.int32)
         m = W.phold_model(hv, end_time=3 * S.SHD_SEC, trace=True, load=8)
