@@ -74,6 +74,8 @@ def parse():
     ap.add_argument("--relays", type=int, default=6500)
     ap.add_argument("--clients", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip the end-state check against one engine over all hosts on rank 0")
     ap.add_argument("--no-reference-cpu", action="store_true",
                     help="skip timing the reference's own serial loop (oracle/_ref/libshdref_loop.so)")
     ap.add_argument("--reference-window-ms", type=int, nargs=2, default=[1100, 1200],
@@ -239,7 +241,9 @@ def main():
               f"apsp={min(builds):.1f}ms iters={info.sssp_iterations_max} hops={info.max_hops}")
 
     exchange = "none (single engine)"
+    transport = "none" if world <= 1 and not use_group else "torch.distributed"
     if use_group:
+        transport = "host-memory all-to-all" if args.comm == "host" else "rccl"
         exchange = "shd_xgroup/%s all-to-all" % ("host-memory" if args.comm == "host" else "RCCL")
         grp = None
         if args.exchange == "p2p":
@@ -249,11 +253,13 @@ def main():
                 two_launch = os.environ.get("SHD_X_UNFUSED") or (
                     rehearsal and world * -(-(pb[rank + 1] - pb[rank]) // 64) >
                     torch.cuda.get_device_properties(dev).multi_processor_count)
+                transport = "p2p"
                 exchange = ("shd_xgroup/peer-to-peer (IPC-mapped receive blocks, xGMI stores, "
                             + ("a separate exchange launch per round)" if two_launch else
                                "each round's launch completes the previous round's exchange)"))
             except S.ShdError as ex:
                 log(rank, f"peer-to-peer transport unavailable ({ex}); RCCL all-to-all instead")
+                transport += "-after-p2p-map-or-self-check-failed"
         if grp is None:
             grp = XGroup.over(eng, comm)
         run = lambda t: grp.run_until(t)  # noqa: E731
@@ -289,6 +295,7 @@ def main():
             grp = XGroup.over(eng, comm)
             exchange = ("shd_xgroup/%s all-to-all (peer-to-peer warm-up failed)"
                         % ("host-memory" if args.comm == "host" else "RCCL"))
+            transport = ("host-memory all-to-all" if args.comm == "host" else "rccl") + "-after-p2p-timeout"
             run = lambda t: grp.run_until(t)  # noqa: E731
             wst = run(args.warmup * step)
     torch.cuda.synchronize()
@@ -364,6 +371,11 @@ def main():
                 "packet_events_per_launch": round(pkt_all / max(launches, 1), 1),
                 "active_hosts_per_launch": round(hr_all / max(launches, 1), 1)}
 
+    parity = None
+    if world > 1 and not args.no_parity:
+        parity = parity_leg(args, S, g, att, model, eng, pb, rank, world, dev, end_time, dist, torch, tdev,
+                            int(getattr(wst, "n_pkt_events", getattr(wst, "pkt_events", 0))) + int(pkt))
+
     lossy = None
     if world == 1 and args.lossy_edge_loss_max > 0 and not use_group and args.workload == "c3":
         lossy = lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, torch)
@@ -411,6 +423,8 @@ def main():
                                       "hosts sharded over %d GPU" % max(world, 1),
                        "exchange": (exchange if use_group else
                                     "torch.distributed" if world > 1 else "none (single engine)")},
+            "transport": transport,
+            "parity": parity,
             "all_events_per_s": round(ev_all / elapsed, 1),
             # the same events over the timed region plus the one-time host->device
             # upload of the boundary's host buffers (engine + path-cache creation)
@@ -652,6 +666,52 @@ def cpu_threads():
     except ValueError:
         n = 0
     return max(1, n or min(len(os.sched_getaffinity(0)), 16))
+
+
+def parity_leg(args, S, g, att, model, eng, pb, rank, world, dev, end_time, dist, torch, tdev, pkt_local):
+    """N > 1: the run checked against the same model on ONE engine.  After the
+    timed region every rank hashes its hosts' end states (shd_eng_digest:
+    event-ID counter, RNG, queues, CoDel state and counters of each host,
+    SHA-256 over the rank's slice) and its packet-event count; rank 0 runs the
+    whole model, all H hosts, on one engine of its own GPU over the same
+    [0, end) on a path cache built afresh, and compares slice by slice.  The
+    line says whether the transport that ran (`transport`) left every rank's
+    hosts exactly where the single engine leaves them.  Untimed."""
+    import hashlib
+    from sim import Engine, PathCache
+    t0 = time.perf_counter()
+    mine = np.frombuffer(hashlib.sha256(eng.digest().tobytes()).digest(), dtype=np.uint8).astype(np.int64)
+    mine = np.concatenate([mine, [pkt_local]])
+    t = torch.tensor(mine, dtype=torch.int64, device=tdev)
+    got = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(got, t)
+    got = [x.cpu().numpy() for x in got]
+    res = torch.zeros(2 + world, dtype=torch.int64, device=tdev)
+    if rank == 0:
+        pc1 = PathCache(g, att, device=dev)
+        ref = Engine(model, pc1, 0, model.n_hosts, device=dev)
+        ref.boot()
+        rst = ref.run_until(end_time)
+        dg = ref.digest()
+        ref.close()
+        pc1.close()
+        ok = []
+        for r in range(world):
+            h = hashlib.sha256(dg[pb[r]:pb[r + 1]].tobytes()).digest()
+            ok.append(int(bytes(got[r][:32].astype(np.uint8).tobytes()) == h))
+        pkt_group = int(sum(int(x[32]) for x in got))
+        res[0] = int(all(ok) and pkt_group == int(rst.n_pkt_events))
+        res[1] = int(rst.n_pkt_events)
+        res[2:] = torch.tensor(ok, dtype=torch.int64)
+    dist.broadcast(res, 0)
+    r = res.cpu().numpy()
+    return {"ok": bool(r[0]), "ranks_ok": [bool(x) for x in r[2:]],
+            "pkt_events_single_engine": int(r[1]),
+            "pkt_events_group": int(sum(int(x[32]) for x in got)),
+            "reference": "one engine over all %d hosts on rank 0's GPU, same model, [0, %.3f s), fresh path cache; "
+                         "per-rank SHA-256 of the hosts' end-state digests (shd_eng_digest)" %
+                         (model.n_hosts, end_time / 1e9),
+            "ms": round((time.perf_counter() - t0) * 1e3, 1)}
 
 
 def cpu_leg(args, S, W, g, model, step, value):

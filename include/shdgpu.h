@@ -479,6 +479,8 @@ typedef struct shd_run_stats {
     uint64_t n_rounds_replayed;     /* rounds run again from the last state copy to recover
                                        an unprotected round whose first-touch drop decision
                                        was ambiguous (shd_eng_run_until) */
+    uint64_t n_restore_points;      /* restore points renewed between the batches of this call
+                                       (a point older than 2^16 rounds) */
 } shd_run_stats;
 
 typedef struct shd_eng shd_eng;

@@ -161,7 +161,10 @@ enum {
  * -22 an invalid model, -113 a client whose server has no route in either
  * direction (the reference's connect fails with ECONNREFUSED there,
  * host.c:1224-1234; the device application has no such branch), -12 no device
- * memory for the trace buffers, -5 a HIP error.  *out is allocated by the call
+ * memory for the trace buffers, -5 a HIP error.  A client on another host than
+ * its server that starts less than one window W (the smallest path latency)
+ * after it is refused (-22): it could connect in the round its server binds,
+ * and the port it reads would depend on the lanes' timing.  *out is allocated by the call
  * and released by shd_tcp_result_free. */
 int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out);
 void shd_tcp_result_free(shd_tcp_result* r);
@@ -173,18 +176,28 @@ void shd_tcp_result_free(shd_tcp_result* r);
  * workers (slave.c:437-462) with its hosts' events, both transports, the
  * qdisc, buckets and CoDel queue on the engine that owns the host.  Each
  * round's window starts at the earliest pending event over the group (an
- * all-gather of one word per engine); after the round the deliveries for
- * other engines' hosts go to them in one all-to-all of fixed segments
- * (SHD_TCP_XCAP deliveries per engine pair and round, 4096 by default; more
- * set SHD_TCP_ERR_MAILBOX), and the servers' listening ports their clients
- * connect to are published to every engine.  Results equal shd_tcp_run's on
- * the same model, host by host.  Paths: with path_cache (every rank's own
+ * all-gather of a few words per engine); after the round the deliveries for
+ * other engines' hosts go to them: every engine writes them into one segment
+ * per destination engine (SHD_TCP_XCAP deliveries per engine pair and round,
+ * max(16384, 8 x the engine's hosts) by default; more set
+ * SHD_TCP_ERR_MAILBOX), the segments' counts go round in one all-gather and
+ * only their used parts in an all-to-all-v (grouped send / receive on RCCL),
+ * and the servers' listening ports their clients connect to are published to
+ * every engine.  Results equal shd_tcp_run's on the same model, host by host
+ * (a client on another host than its server must start at least one window
+ * after it, or the model is refused with -22, as on one engine).  Paths: with path_cache (every rank's own
  * cache of the same graph, built alike) each round's first-touch log of every
  * engine is gathered and replayed alike on every rank, so the ranks stay
  * equal and a contradicted choice stops every rank at the same round
  * (SHD_TCP_ERR_FIRST_TOUCH); with tables the queries every engine logged come
  * back in each rank's result, for the caller's ranking as on one engine.
- * Returns as shd_tcp_run, -5 also when the group's communication fails. */
+ * Returns as shd_tcp_run, -5 also when the group's communication fails.
+ * Failure is collective only where every rank sees it: an error bit of the
+ * run, a halted engine (every engine ends at that round) and a first-touch
+ * log too long for the device end every rank at the same round; a HIP error
+ * local to one rank ends that rank's call, and the others stay in their next
+ * collective until the transport gives up (the host transport after its
+ * 300-s barrier timeout; RCCL does not time out). */
 struct shd_comm;
 int shd_tcp_run_group(const shd_tcp_model* m, struct shd_comm* comm, int32_t trace, shd_tcp_result** out);
 

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--vertices", type=int, default=10000)
     ap.add_argument("--hosts", type=int, default=10000)
     ap.add_argument("--load", type=int, default=None)
+    ap.add_argument("--at", type=float, default=2.0, help="simulated seconds before the measured rounds")
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3",
                     help="c5: bench.py's C5 model at --hosts hosts (the per-GPU shard: 125000; k_round_sp)")
     a = ap.parse_args()
@@ -43,25 +44,37 @@ def main():
     hv = (np.arange(a.hosts, dtype=np.int64) * a.vertices // a.hosts).astype(np.int32)
     if a.workload == "c5":
         g = W.geometric_graph(a.vertices, seed=1, loss_max=0.01)
-        m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 32, payload=1500, bw_down=512,
+        m = W.phold_model(hv, end_time=int((a.at + 2) * S.SHD_SEC), seed=1, load=a.load or 32, payload=1500, bw_down=512,
                           bw_up=10240, codelq_cap=256)
     else:
         g = W.geometric_graph(a.vertices, seed=1, loss_max=0.0)
-        m = W.phold_model(hv, end_time=4 * S.SHD_SEC, seed=1, load=a.load or 16, payload=1)
+        m = W.phold_model(hv, end_time=int((a.at + 2) * S.SHD_SEC), seed=1, load=a.load or 16, payload=1)
     pc = PathCache(g, W.attached_vertices(hv), device=0)
     pc.build()
     eng = Engine(m, pc, 0, a.hosts, device=0)
     eng.boot()
-    eng.run_until(2 * S.SHD_SEC)
-    buf0 = np.zeros(64 * 2048 * 20, dtype=np.uint64)
+    eng.run_until(int(a.at * S.SHD_SEC))
+    buf0 = np.zeros(64 * 2048 * 24, dtype=np.uint64)
     f(buf0.ctypes.data_as(C.POINTER(C.c_uint64)))   # the stamps before the measured rounds
-    st = eng.run_until(2 * S.SHD_SEC + 60 * eng.window)   # under one persistent batch: its rounds leave their stamps
+    fc = lib.shd_debug_counts
+    fc.restype = C.c_int
+    fc.argtypes = [C.POINTER(C.c_uint64), C.c_int]
+    cn = np.zeros(8, dtype=np.uint64)
+    fc(cn.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
+    st = eng.run_until(int(a.at * S.SHD_SEC) + 60 * eng.window)   # under one persistent batch: its rounds leave their stamps
     print(f"persistent batches {st.n_batches_persistent} of {st.n_batches}, rounds {st.n_rounds}, "
           f"{st.device_ms_launches / max(st.n_rounds, 1) * 1e3:.2f} us/round (HIP events)")
-    buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
+    fc(cn.ctypes.data_as(C.POINTER(C.c_uint64)), 1)
+    if cn.any():   # a -DSHD_TCNT build: event-path counters over the measured rounds
+        nr = max(st.n_rounds, 1)
+        names_c = ["cq loads", "tq loads", "heap pushes", "heap pops", "inbox merged", "events", "flushes",
+                   "suspended lanes"]
+        print("counters per round: " + ", ".join(f"{n} {int(v) / nr:.1f}" for n, v in zip(names_c, cn)) +
+              f"; packet events {st.n_pkt_events / nr:.1f}, events {st.n_events / nr:.1f}")
+    buf = np.zeros(64 * 2048 * 24, dtype=np.uint64)
     f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
-    t = buf.reshape(64, 2048, 20).astype(np.int64)
-    t_before = buf0.reshape(64, 2048, 20).astype(np.int64)
+    t = buf.reshape(64, 2048, 24).astype(np.int64)
+    t_before = buf0.reshape(64, 2048, 24).astype(np.int64)
     # the measured launch's blocks (k_round_ps: one per 64 hosts; k_round_sp: fewer) and its rounds' slots
     fresh = t[:, :, 0] != t_before[:, :, 0]
     grid = int(np.count_nonzero(fresh.any(axis=0)))
@@ -119,6 +132,31 @@ def main():
                   f"(take+begin {seg[sel, 0].mean():.2f} = take_next {seg[sel, 3].mean():.2f} + begin_event "
                   f"{seg[sel, 4].mean():.2f} + notify {seg[sel, 5].mean():.2f} + rest; run_work "
                   f"{seg[sel, 1].mean():.2f}, early flushes {seg[sel, 2].mean():.2f}), flushes {nfl[sel].mean():.2f}")
+    # k_round_sp: active hosts (20) and passes (21) per block and round
+    na, npas = [], []
+    for r in range(64):
+        x = t_all[r]
+        t0 = x[:, 0].min()
+        ok = (t0 > 0) & (x[:, 1] >= t0) & (x[:, 20] < 100000)
+        na += list(x[ok, 20]); npas += list(x[ok, 21])
+    if na and max(npas) > 0:
+        na, npas = np.array(na), np.array(npas)
+        print(f"  sparse: active hosts per block-round mean {na.mean():.2f} max {na.max()}; passes mean "
+              f"{npas.mean():.2f} max {npas.max()}; blocks with none {np.mean(na == 0) * 100:.1f} %")
+    # k_round_sp's scan: its first batch's words landed (22), the compaction done (23), from the round start
+    sl, sc = [], []
+    for r in range(64):
+        x = t_all[r]
+        t0 = x[:, 0].min()
+        ok = (t0 > 0) & (x[:, 22] >= x[:, 0]) & (x[:, 23] >= x[:, 22]) & (x[:, 0] > 0)
+        sl += list((x[ok, 22] - x[ok, 0]) / 100.0); sc += list((x[ok, 23] - x[ok, 22]) / 100.0)
+    if sl:
+        print(f"  sparse scan: block start -> words landed {np.mean(sl):.2f} us (max {np.max(sl):.2f}), "
+              f"-> compaction done {np.mean(sc):.2f} us (max {np.max(sc):.2f})")
+    # phase durations (mean over rounds of the mean over blocks)
+    d = np.diff(rows, axis=2)
+    print("  phase durations, mean over blocks: " + ", ".join(
+        f"{names[k]}<-{names[k - 1]} {np.nanmean(d[:, :, k - 1]):.2f}" for k in range(1, 8)))
     per = np.diff(np.nanmax(rows[:, :, 7], axis=1))
     print(f"  round period (max 'all seen' to the next) {np.mean(per[per > 0]):.2f} us")
 

@@ -61,9 +61,9 @@ def main():
     names = ["cq HBM loads", "tq HBM loads", "heap pushes", "heap pops", "inbox merged", "events", "flushes (waves)",
              "suspended lanes"]
     print("per round: " + ", ".join(f"{names[i]} {cn[i] / nr:.1f}" for i in range(8)))
-    buf = np.zeros(64 * 2048 * 20, dtype=np.uint64)
+    buf = np.zeros(64 * 2048 * 24, dtype=np.uint64)
     f(buf.ctypes.data_as(C.POINTER(C.c_uint64)))
-    t = buf.reshape(64, 2048, 20).astype(np.int64)
+    t = buf.reshape(64, 2048, 24).astype(np.int64)
     hpw = int(os.environ.get("SHD_HPW", "64"))
     grid = (a.hosts + hpw - 1) // hpw
     t = t[:, :grid, :]

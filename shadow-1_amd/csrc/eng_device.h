@@ -321,7 +321,7 @@ enum {
 // -DSHD_TIMING (make timing -> libshdgpu_tim.so, scripts/round_timing.py):
 // wall-clock stamps per block at the round's phase boundaries, 64 round slots
 // keyed by the summary address x 2048 blocks x 8 stamps
-__device__ unsigned long long g_tim[64][2048][20];
+__device__ unsigned long long g_tim[64][2048][24];
 // per event class, over iterations in which every lane that starts an event
 // starts one of that class: {iterations, cycles, of which take_next, of which
 // begin_event}.  Class = kind (1..7), 8 = a packet on the general path
@@ -329,7 +329,7 @@ __device__ unsigned long long g_kc[10][4];
 // event-path counters (timing build): cq / tq entries loaded from HBM, heap
 // pushes / pops, inbox events merged, events, flushes, suspended lanes
 __device__ unsigned long long g_cnt[8];
-#ifdef SHD_TIMING_LIGHT   // phase stamps only: no per-event counters either
+#if defined(SHD_TIMING_LIGHT) && !defined(SHD_TCNT)   // phase stamps only: no per-event counters either
 #define TCNT(i)
 #else
 #define TCNT(i) atomicAdd(&g_cnt[i], 1ull)
@@ -340,28 +340,55 @@ __shared__ unsigned long long s_kc[10][4];
 #else
 #define TIM_WAIT() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory")
 #endif
+// SHD_TIMING_P0: the persistent kernels keep their one parameter copy (as the
+// product does; a copy per round costs scalar-cache misses every round and
+// doubled the sparse round's time in round 5's stamps) and name the round's
+// slot in LDS instead (s_tslot, valid while s_tslot_key holds the key; the
+// persistent kernels clear it on exit)
+#define TIM_SLOT() (uint32_t)(((uintptr_t)P.sum / sizeof(DevSummary)) & 63)
+#ifdef SHD_TIMING_P0
+__shared__ uint32_t s_tslot;
+#define PS_TIM_SLOT() (s_tslot & 63u)
+#else
+#define PS_TIM_SLOT() TIM_SLOT()
+#endif
 #define TIM(k)                                                                                         \
     do {                                                                                               \
         TIM_WAIT();                                                                                    \
         if (threadIdx.x == 0 && blockIdx.x < 2048)                                                     \
-            g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = wall_clock64();       \
+            g_tim[TIM_SLOT()][blockIdx.x][k] = wall_clock64();                                         \
+    } while (0)
+// in the persistent rounds' code (k_round_ps / _sp / _spx): the slot from LDS
+// under SHD_TIMING_P0
+#define TIMP(k)                                                                                        \
+    do {                                                                                               \
+        TIM_WAIT();                                                                                    \
+        if (threadIdx.x == 0 && blockIdx.x < 2048)                                                     \
+            g_tim[PS_TIM_SLOT()][blockIdx.x][k] = wall_clock64();                                      \
+    } while (0)
+#define TIMVP(k, v)                                                                                    \
+    do {                                                                                               \
+        if ((int)threadIdx.x == __ffsll((unsigned long long)__ballot(1)) - 1 && blockIdx.x < 2048)     \
+            g_tim[PS_TIM_SLOT()][blockIdx.x][k] = (v);                                                 \
     } while (0)
 // inside a divergent region: the first active lane stamps
 #define TIMA(k)                                                                                        \
     do {                                                                                               \
         TIM_WAIT();                                                                                    \
         if ((int)threadIdx.x == __ffsll((unsigned long long)__ballot(1)) - 1 && blockIdx.x < 2048)     \
-            g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = wall_clock64();       \
+            g_tim[TIM_SLOT()][blockIdx.x][k] = wall_clock64();                                         \
     } while (0)
 #define TIMV(k, v)                                                                                     \
     do {                                                                                               \
         if ((int)threadIdx.x == __ffsll((unsigned long long)__ballot(1)) - 1 && blockIdx.x < 2048)     \
-            g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][k] = (v);                  \
+            g_tim[TIM_SLOT()][blockIdx.x][k] = (v);                                                    \
     } while (0)
 #else
 #define TIM(k)
+#define TIMP(k)
 #define TIMA(k)
 #define TIMV(k, v)
+#define TIMVP(k, v)
 #define TCNT(i)
 #endif
 #ifdef SHD_PROF
@@ -1142,7 +1169,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     s_cls[lane] = c.cls;
     __syncthreads();
 #ifdef SHD_TIMING_LIGHT
-    TIM(12);
+    TIMP(12);
 #endif
     uint32_t err = 0;
     for (uint32_t base = 0; base < total; base += kBlock) {
@@ -1204,7 +1231,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     }
     __syncthreads();
 #ifdef SHD_TIMING_LIGHT
-    TIM(13);
+    TIMP(13);
 #endif
     // per host, in send order (worker.c:286-320).  Timers scheduled since the
     // last flush hold provisional IDs: an ID x loses the dropped sends issued
@@ -1256,7 +1283,7 @@ __device__ __forceinline__ void flush_wave(const DParams& P, HostCtx& c, bool de
     __syncthreads();
     if (lane == 0) s_pool_n = 0;   // (every lane read it above, before the barrier)
 #ifdef SHD_TIMING_LIGHT
-    TIM(14);
+    TIMP(14);
 #endif
     // deliveries: calendar claims for 64 events at a time, then the stores.
     // The round's last flush (one batch) only issues the claims; the stores

@@ -435,6 +435,45 @@ __device__ __forceinline__ uint4 ld16_sys(const void* p) {
     return make_uint4(x[0], x[1], x[2], x[3]);
 }
 
+// The mapping's self-check (round 6: the transport had never crossed a
+// device when the group was created).  Lane p < W stores a known 16-B granule
+// into peer p's receive block, at this rank's header slot of parity 0, with the
+// same system-scope store the exchange uses, and drains it; after a barrier
+// over the communicator each rank reads every sender's granule from its own
+// block with the exchange's system-scope load and checks it (bad: the senders
+// whose granule was missing or wrong, one bit each).  The slots are zeroed
+// again before the group's first exchange.
+constexpr uint32_t kProbeMagic = 0x5ad0c0deu;
+__global__ void k_p2p_probe_put(shd_event* const* __restrict__ peers, int world, int me, size_t stride, uint32_t gen,
+                                int corrupt) {
+    const int p = (int)threadIdx.x;
+    if (p < world) {
+        const uint4 v = make_uint4(kProbeMagic, (uint32_t)me, (uint32_t)p, gen + (uint32_t)corrupt);
+        st16_sys(peers[p] + (size_t)me * stride, v);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__global__ void k_p2p_probe_check(const shd_event* __restrict__ mine, int world, int me, size_t stride, uint32_t gen,
+                                  unsigned long long* __restrict__ bad) {
+    const int p = (int)threadIdx.x;
+    const bool ok = p >= world || [&] {
+        const uint4 v = ld16_sys(mine + (size_t)p * stride);
+        return v.x == kProbeMagic && v.y == (uint32_t)p && v.z == (uint32_t)me && v.w == gen;
+    }();
+    const unsigned long long m = __ballot(!ok);
+    if (p == 0) *bad = m;
+}
+
+#ifdef SHD_TEST_HOOKS
+// test build: exchanged events to lose on taking them (SHD_TEST_XDROP), so
+// that a check of a group's end state against one engine can be seen to fail
+__device__ int g_test_xdrop;
+__device__ __forceinline__ bool test_xdrop() { return g_test_xdrop > 0 && atomicSub(&g_test_xdrop, 1) > 0; }
+#define TEST_XDROP() if (test_xdrop()) continue
+#else
+#define TEST_XDROP()
+#endif
+
 // the events of the regions [p][blk] (p != xme) of one parity -> calendar /
 // inbox[parity] of the block's hosts; s_n / s_w (or null): what each lane's
 // host received, for the lane (inbox count, calendar bins).  Returns error bits.
@@ -467,6 +506,7 @@ __device__ uint32_t xrgn_ingest_from(const DParams& P, shd_event* __restrict__ r
             // this CU) before this block's next share lets the peer store there again
             __hip_atomic_store((unsigned long long*)(rgn + ((size_t)(p0 + k) * P.xnbx + blk) * kXSlots + threadIdx.x),
                                0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            TEST_XDROP();
             const int32_t dl = (int32_t)e.dst - P.h0;
             const int32_t j = dl - (int32_t)blk * P.hpw;
             if (dl < 0 || dl >= P.nloc || j < 0 || j >= P.hpw) {
@@ -540,6 +580,7 @@ __device__ __forceinline__ uint32_t xrgn_take(const DParams& P, shd_event* __res
         }
         __hip_atomic_store((unsigned long long*)(rgn + ((size_t)k * P.xnbx + blk) * kXSlots + threadIdx.x), 0ull,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // taken (system scope: as above)
+        TEST_XDROP();
         const int32_t dl = (int32_t)e.dst - P.h0;
         const int32_t j = dl - (int32_t)blk * P.hpw;
         if (dl < 0 || dl >= P.nloc || j < 0 || j >= P.hpw) {
@@ -971,10 +1012,12 @@ __global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, De
     uint64_t we = ws + window;
     if (we > stop || we < ws) we = stop;
     if (threadIdx.x == 0) s_rsum = P.sum;
+#ifdef SHD_TIMING_P0
+    if (threadIdx.x == 0) s_tslot = TIM_SLOT();
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the take's stores, before the scan's loads
     __syncthreads();
     // ---- k_round_sp's round over this block's hosts
-    const uint32_t lane = threadIdx.x;
     PsRsrc R;
     R.bits = buf_rsrc(P.bin_bits ? P.bin_bits + (size_t)hb * kNBW : nullptr, (uint64_t)nh * kNBW * 4);
     R.bins = buf_rsrc(P.bins ? P.bins + (size_t)hb * kNB * kBinCap : nullptr,
@@ -988,92 +1031,12 @@ __global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, De
     const uint32_t xwi = (uint32_t)((xpar + (uint64_t)i) & 1);
     ps_round_reset(P, c, ws, we, parity, false);
     c.xwi = xwi;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
-    uint64_t next = kInf;
-    uint32_t nact = 0;
-    for (uint32_t g0 = 0; g0 < ngrp; g0 += kSpScan) {
-        uint32_t nin4[kSpScan], w4[kSpScan][kNBW];
-        uint64_t t4[kSpScan];
-#pragma unroll
-        for (int q = 0; q < kSpScan; q++) {
-            const uint32_t lb = (g0 + q) * 64u + lane;
-            nin4[q] = 0; t4[q] = kInf;
-#pragma unroll
-            for (int j = 0; j < (int)kNBW; j++) w4[q][j] = 0;
-            if (g0 + q < ngrp && lb < nh) {
-                nin4[q] = ld4_sc1(R.nin, lb * 4u);
-                if (P.bins) {
-                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
-                    w4[q][0] = x.x; w4[q][1] = x.y; w4[q][2] = x.z; w4[q][3] = x.w;
-                    w4[q][4] = y.x; w4[q][5] = y.y; w4[q][6] = y.z; w4[q][7] = y.w;
-                }
-                t4[q] = P.hnext[hb + lb];
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kSpScan; q++) {
-            const uint32_t lb = (g0 + q) * 64u + lane;
-            const bool has = g0 + q < ngrp && lb < nh;
-            const uint32_t wbits = ps_window_bits(P, c, w4[q], ws, we);
-            const bool act = has && !(nin4[q] == 0 && t4[q] >= we && wbits == 0);
-            if (has && !act) {
-                const uint64_t t = ps_idle_next(P, w4[q], t4[q], we);
-                next = t < next ? t : next;
-            }
-            const uint64_t m = __ballot(act);
-            if (act) {
-                const uint32_t k = nact + (uint32_t)__popcll(m & lt_mask);
-                s_act[k] = (uint16_t)lb;
-                if (k < (uint32_t)kBlock) {
-#pragma unroll
-                    for (int j = 0; j < (int)kNBW; j++) s_aw[j * kBlock + k] = w4[q][j];
-                    s_aw[kNBW * kBlock + k] = nin4[q];
-                }
-            }
-            nact += (uint32_t)__popcll(m);
-        }
-    }
+    uint64_t next;
+    uint32_t nact;
+    sp_scan(P, R, hb, nh, ngrp, ws, we, next, nact);
     __syncthreads();
     uint32_t nev = 0, npkt = 0, err = c.err | ierr, nhost = 0;
-    for (uint32_t base = 0; base < nact; base += kBlock) {
-        const uint32_t k = base + lane;
-        const bool act = k < nact;
-        const uint32_t lb = act ? (uint32_t)s_act[k] : 0u;
-        const int32_t l = (int32_t)(hb + lb);
-        uint32_t nin = 0, w[kNBW];
-#pragma unroll
-        for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
-        if (act) {
-            if (base == 0) {
-#pragma unroll
-                for (int j = 0; j < (int)kNBW; j++) w[j] = s_aw[j * kBlock + k];
-                nin = s_aw[kNBW * kBlock + k];
-            } else {
-                nin = ld4_sc1(R.nin, lb * 4u);
-                if (P.bins) {
-                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
-                    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-                }
-            }
-        }
-        SpIn in;
-        in.l = l;
-        in.xwi = xwi;
-        if (act) {
-            in.rec = P.hs[l];
-            in.att = P.host_att[P.h0 + l];
-            in.st = P.self_thr[P.h0 + l];
-        }
-        const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
-        uint64_t hn = kInf;
-        ps_round_body<true>(P, c, act, lb, R, ws, we, parity, nin, w, wbits, hn, &in);
-        if (act) store_ctx(P, c);
-        next = hn < next ? hn : next;
-        nev += c.c_events; npkt += c.c_pkt;
-        err |= c.err;
-        nhost += (uint32_t)__popcll(__ballot(act && c.c_events != 0));
-        __syncthreads();   // (the next pass reuses the lanes' LDS slots)
-    }
+    sp_passes<false>(P, c, R, hb, nact, ws, we, parity, xwi, next, nev, npkt, err, nhost);
     // peer-to-peer: this block's stores into the peers' regions land before the
     // round ends (the next launch's put block announces them)
     if (P.xpeer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -336,6 +336,64 @@ static void x_p2p_unmap(shd_xgroup* g) {
     g->p2p_base = nullptr;
 }
 
+// x_p2p_map's self-check (k_p2p_probe_put / _check); every step collective
+static int x_p2p_probe(shd_xgroup* g) {
+    shd_eng* e = g->engs[0];
+    const int W = g->world, me = g->rank0;
+    if (W > 64) return SHD_EINVAL;
+    // a generation all ranks agree on (rank 0's clock), so that a granule left
+    // by an earlier mapping at the same address never passes
+    uint32_t gen = (uint32_t)std::chrono::steady_clock::now().time_since_epoch().count() | 1u;
+    std::vector<uint32_t> gens(W);
+    int rc = shd_comm_allgather_host(g->comm, &gen, 4, gens.data());
+    if (rc) return rc;
+    gen = gens[0];
+    int corrupt = 0;
+#ifdef SHD_TEST_HOOKS   // test build: exchanged events this rank loses on taking them
+    if (const char* f = getenv("SHD_TEST_XDROP")) {
+        const int n = atoi(f);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_test_xdrop), &n, sizeof(n));
+    }
+#endif
+#ifdef SHD_TEST_HOOKS   // test build: this rank puts a wrong granule (every rank must then fail alike)
+    if (const char* f = getenv("SHD_P2P_PROBE_CORRUPT"))
+        if (atoi(f) == me) corrupt = 1;
+#endif
+    uint32_t ok = 1;
+    unsigned long long* d_bad = nullptr;
+    unsigned long long bad = ~0ull;
+    if (hipMalloc((void**)&d_bad, sizeof(*d_bad)) != hipSuccess) ok = 0;
+    if (ok) {
+        hipLaunchKernelGGL(k_p2p_probe_put, dim3(1), dim3(64), 0, e->stream, g->d_peers, W, me, g->stride, gen, corrupt);
+        if (hipStreamSynchronize(e->stream) != hipSuccess) ok = 0;
+    }
+    std::vector<uint32_t> oks(W);
+    if ((rc = shd_comm_allgather_host(g->comm, &ok, 4, oks.data()))) { (void)hipFree(d_bad); return rc; }
+    for (uint32_t x : oks) ok &= x;
+    if (ok) {   // every rank's puts have drained
+        hipLaunchKernelGGL(k_p2p_probe_check, dim3(1), dim3(64), 0, e->stream, g->p2p_base, W, me, g->stride, gen,
+                           d_bad);
+        if (hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, e->stream) != hipSuccess ||
+            hipStreamSynchronize(e->stream) != hipSuccess)
+            ok = 0;
+        if (bad) {
+            fprintf(stderr, "shd_xgroup: peer-to-peer self-check failed on rank %d: granules from senders %#llx "
+                            "missing or wrong\n", me, bad);
+            ok = 0;
+        }
+        // the probe's slots back to "no exchange yet" before any rank's first put
+        for (int p = 0; p < W && ok; p++)
+            if (hipMemsetAsync(g->p2p_base + (size_t)p * g->stride, 0, sizeof(shd_event), e->stream) != hipSuccess)
+                ok = 0;
+        if (hipStreamSynchronize(e->stream) != hipSuccess) ok = 0;
+    }
+    (void)hipGetLastError();
+    (void)hipFree(d_bad);
+    if ((rc = shd_comm_allgather_host(g->comm, &ok, 4, oks.data()))) return rc;
+    for (uint32_t x : oks) ok &= x;
+    return ok ? SHD_OK : SHD_ENODEV;
+}
+
 // the peer-to-peer receive blocks: allocated uncached (a peer's stores land
 // in memory, no L2 of this GPU holds a stale copy), exported by IPC handle,
 // every rank's handle all-gathered and mapped.  The handle exchange is also
@@ -396,6 +454,15 @@ static int x_p2p_map(shd_xgroup* g) {
     if (!ok) {
         x_p2p_unmap(g);
         return SHD_ENODEV;
+    }
+    // the self-check: one known granule from every rank into every peer's
+    // block over the mapping, read back by the receiver; a transport that
+    // loses or garbles it fails the group's creation on every rank alike
+    // (SHD_ENODEV, the caller falls back to the all-to-all) instead of
+    // silently wrong rounds
+    if ((rc = x_p2p_probe(g))) {
+        x_p2p_unmap(g);
+        return rc;
     }
     g->loc[0].xrecv[0] = g->p2p_base;
     g->loc[0].xrecv[1] = g->p2p_base + (size_t)W * g->stride;

@@ -1041,6 +1041,7 @@ __device__ __forceinline__ void ps_prologue(const DParams& P, HostCtx& c, bool a
             const uint32_t n = nin < P.inbox_cap ? nin : P.inbox_cap;
             for (uint32_t i = 0; i < n; i++) {
                 const uint32_t off = (lb * P.inbox_cap + i) * 32u;
+                TCNT(4);
                 heap_push(P, c, evv_event(EvV{ld16_sc1(R.inbox, off), ld16_sc1(R.inbox, off + 16)}));
             }
             __hip_atomic_store(&P.inbox_n[parity][c.l], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1086,7 +1087,7 @@ __device__ __forceinline__ void ps_prologue(const DParams& P, HostCtx& c, bool a
             }
         }
     }
-    TIM(2);
+    TIMP(2);
 }
 
 // k_round_ps, a round whose window the previous round loaded ahead (every
@@ -1120,7 +1121,7 @@ __device__ __forceinline__ void ps_prologue_pf(const DParams& P, HostCtx& c, boo
             }
         }
     }
-    TIM(2);
+    TIMP(2);
 }
 
 // the next window's first kPfBins bins (from bin b on), loaded before the
@@ -1283,7 +1284,7 @@ __device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool
             }
             const bool last = __ballot(st == 2u) == 0;
 #ifdef SHD_TIMING
-            if (last) TIM(3);   // the round's last flush starts
+            if (last) TIMP(3);   // the round's last flush starts
 #endif
 #ifdef SHD_TIMING_LIGHT
             n_fl++;
@@ -1297,17 +1298,17 @@ __device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool
             if (st == 2u) st = 1u;
         }
     }
-    TIM(4);
+    TIMP(4);
 #ifdef SHD_TIMING_LIGHT
-    TIMV(16, (uint64_t)n_it);   // loop iterations of the wave
-    TIMV(17, (uint64_t)n_fl);   // flushes
-    TIMV(18, (uint64_t)__popcll(__ballot(active)));
-    TIMV(8, t_take);    // in take_next + begin_event (+ the fused notification / refill)
-    TIMV(9, t_work);    // in run_work
-    TIMV(10, t_fl);     // in the flushes before the last
-    TIMV(11, t_q[0]);   // of 8: take_next
-    TIMV(15, t_q[1]);   //       begin_event
-    TIMV(19, t_q[2]);   //       the fused notification (the rest: the fused refill, the loop's own)
+    TIMVP(16, (uint64_t)n_it);   // loop iterations of the wave
+    TIMVP(17, (uint64_t)n_fl);   // flushes
+    TIMVP(18, (uint64_t)__popcll(__ballot(active)));
+    TIMVP(8, t_take);    // in take_next + begin_event (+ the fused notification / refill)
+    TIMVP(9, t_work);    // in run_work
+    TIMVP(10, t_fl);     // in the flushes before the last
+    TIMVP(11, t_q[0]);   // of 8: take_next
+    TIMVP(15, t_q[1]);   //       begin_event
+    TIMVP(19, t_q[2]);   //       the fused notification (the rest: the fused refill, the loop's own)
 #endif
 #pragma unroll
     for (int k = 0; k < (int)kNBW; k++) w[k] &= ~cm[k];
@@ -1323,7 +1324,7 @@ __device__ __forceinline__ void ps_loop_close(const DParams& P, HostCtx& c, bool
         next = ps_idle_next(P, w, host_next(c), we);
     }
     flush_finish(P, c, pd);
-    TIM(5);
+    TIMP(5);
 }
 
 // k_round_sp's round of an active host (ps_prologue + ps_loop_close)
@@ -1470,7 +1471,14 @@ __device__ __forceinline__ void ps_fresh(DevSummary* s) {
 // first read of each field a scalar-cache miss; the round's summary is
 // s_rsum.  (Timing builds keep the copy per round: the stamps' slot follows
 // P.sum.  SHD_PS_PR: the same, for an A/B.)
-#if defined(SHD_TIMING) || defined(SHD_PS_PR)
+#if defined(SHD_TIMING_P0)
+#define PS_PARAMS(i)                                                                          \
+    const DParams& P = P0;                                                                    \
+    if (threadIdx.x == 0) {                                                                   \
+        s_rsum = &ring[(i) + 1];                                                              \
+        s_tslot = (uint32_t)(((uintptr_t)&ring[(i) + 1] / sizeof(DevSummary)) & 63);          \
+    }
+#elif defined(SHD_TIMING) || defined(SHD_PS_PR)
 #define PS_PARAMS(i)                                    \
     const DParams& P = Pr[(i) + 1];                     \
     if (threadIdx.x == 0) s_rsum = &ring[(i) + 1]
@@ -1479,6 +1487,7 @@ __device__ __forceinline__ void ps_fresh(DevSummary* s) {
     const DParams& P = P0;                              \
     if (threadIdx.x == 0) s_rsum = &ring[(i) + 1]
 #endif
+
 
 #ifndef SHD_NO_PF
 constexpr bool kPsPf = true;
@@ -1536,7 +1545,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         PS_PARAMS(i);
         const unsigned long long t_start = wall_clock64();
 #ifdef SHD_TIMING
-        if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = t_start;
+        if (threadIdx.x == 0 && blockIdx.x < 2048) g_tim[PS_TIM_SLOT()][blockIdx.x][0] = t_start;
 #endif
         if (lead) ps_fresh(&ring[i + 2]);   // the next round's summary (this round's: ring[i + 1])
         const int parity = (int)((rbase + (uint64_t)i) & 1);
@@ -1560,7 +1569,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
                 w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
             }
             const uint32_t wbits = ps_window_bits(P, c, pw, ws, we);
-            TIM(1);
+            TIMP(1);
             active = has && !(host_next(c) >= we && wbits == 0);   // (no inbox: it would have been named)
             ps_prologue_pf(P, c, active, ws, we, pnd, wbits, cm);
         } else {
@@ -1574,7 +1583,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
                 }
             }
             const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
-            TIM(1);
+            TIMP(1);
             active = has && !(nin == 0 && host_next(c) >= we && wbits == 0);
             ps_prologue<false>(P, c, active, lb, R, ws, we, parity, nin, w, wbits);
         }
@@ -1597,7 +1606,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         const uint32_t tag = tag0 + (uint32_t)i;
         const uint32_t base = (uint32_t)(i & 1) * nblk;
         ps_publish(rs, base + blockIdx.x, next, fl, nev, npkt, nact, tag, ps_noted(pfm));
-        TIM(6);
+        TIMP(6);
         if (pfm) {   // the next window's events, staged while the other blocks finish
             const uint64_t b1 = we >> P.bin_shift;
             pnd = pf_stage(pb, we, (b1 + kPfBins) << P.bin_shift);
@@ -1610,7 +1619,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         bool dall = false;
         const bool ok_v = ps_gather<kPsPf>(rs, base, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt,
                                            f_nact, hb, (uint32_t)P.hpw, &dm, &dall);
-        TIM(7);
+        TIMP(7);
         // the folds are wave-uniform: said so to the compiler, so that the
         // round loop and the parity branch stay scalar (with a vector exit
         // condition the host context would be merged through divergent flow)
@@ -1677,6 +1686,151 @@ constexpr int kSpScan = SHD_SP_SCAN;
 __shared__ uint16_t s_act[kSpMaxHosts];  // the round's active hosts (index in the block)
 __shared__ uint32_t s_aw[(kNBW + 1) * kBlock];   // the first pass's hand-off words: bitmap, inbox count
 
+// k_round_sp / k_round_spx: the round's scan of a block's hosts [hb, hb + nh)
+// (ngrp groups of 64): the hosts with something due in [ws, we) go to s_act
+// (their words to s_aw for the first pass), nact counts them; next: the least
+// next time of the lane's idle hosts
+__device__ __forceinline__ void sp_scan(const DParams& P, const PsRsrc& R, uint32_t hb, uint32_t nh, uint32_t ngrp,
+                                        uint64_t ws, uint64_t we, uint64_t& next, uint32_t& nact) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    next = kInf;
+    nact = 0;
+    // the scan: every host's words and own next time, kSpScan groups per
+    // round trip.  The window's bins sit at the same ring positions for
+    // every host (b0 is the round's), so each host's window bits are two
+    // words picked by a uniform index and one shift; and an idle host's
+    // calendar bound is not worked out per host: the first non-empty bin
+    // from we's on, in ring order, of the OR of the idle hosts' bitmaps is
+    // the least of theirs (bits_first_from is a min over set bits), so the
+    // block ORs them and takes one bound for the lot (round 6: the per-host
+    // bound was 3/4 of the scan, ~3.5 us a round at the C5 shard); each
+    // lane ORs its own groups' idle hosts, and the fold of the lanes' next
+    // times takes the least
+    uint32_t orw[kNBW];
+#pragma unroll
+    for (int j = 0; j < (int)kNBW; j++) orw[j] = 0;
+    const uint32_t p0 = (uint32_t)(ws >> P.bin_shift) & (kNB - 1);
+    const uint32_t nbin = P.bins ? (uint32_t)(((we - 1) >> P.bin_shift) - (ws >> P.bin_shift)) + 1u : 0u;
+    const uint32_t wi0 = p0 >> 5, wi1 = (wi0 + 1u) & (kNBW - 1), wsh = p0 & 31u;
+    const uint32_t wmask = nbin >= 3 ? 7u : (1u << nbin) - 1u;
+    for (uint32_t g0 = 0; g0 < ngrp; g0 += kSpScan) {
+        uint32_t nin4[kSpScan], w4[kSpScan][kNBW];
+        uint64_t t4[kSpScan];
+#pragma unroll
+        for (int q = 0; q < kSpScan; q++) {
+            const uint32_t lb = (g0 + q) * 64u + lane;
+            nin4[q] = 0; t4[q] = kInf;
+#pragma unroll
+            for (int j = 0; j < (int)kNBW; j++) w4[q][j] = 0;
+            if (g0 + q < ngrp && lb < nh) {
+                nin4[q] = ld4_sc1(R.nin, lb * 4u);
+                if (P.bins) {
+                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                    w4[q][0] = x.x; w4[q][1] = x.y; w4[q][2] = x.z; w4[q][3] = x.w;
+                    w4[q][4] = y.x; w4[q][5] = y.y; w4[q][6] = y.z; w4[q][7] = y.w;
+                }
+                t4[q] = P.hnext[hb + lb];
+            }
+        }
+#ifdef SHD_TIMING
+        if (g0 == 0) {   // the first scan batch's words have landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            TIMVP(22, wall_clock64());
+        }
+#endif
+#pragma unroll
+        for (int q = 0; q < kSpScan; q++) {
+            if (g0 + q >= ngrp) break;   // (uniform)
+            const uint32_t lb = (g0 + q) * 64u + lane;
+            const bool has = lb < nh;
+            uint32_t lo = w4[q][0], hi = w4[q][1];
+#pragma unroll
+            for (int j = 1; j < (int)kNBW; j++) {   // uniform picks: v_cndmask on a scalar condition
+                lo = wi0 == (uint32_t)j ? w4[q][j] : lo;
+                hi = wi1 == (uint32_t)j ? w4[q][j] : hi;
+            }
+            hi = wi1 == 0u ? w4[q][0] : hi;
+            const uint32_t wbits = (uint32_t)(((((uint64_t)hi) << 32) | lo) >> wsh) & wmask;
+            const bool act = has && !(nin4[q] == 0 && t4[q] >= we && wbits == 0);
+            if (has && !act) {
+                next = t4[q] < next ? t4[q] : next;
+#pragma unroll
+                for (int j = 0; j < (int)kNBW; j++) orw[j] |= w4[q][j];
+            }
+            const uint64_t m = __ballot(act);
+            if (act) {
+                const uint32_t k = nact + (uint32_t)__popcll(m & lt_mask);
+                s_act[k] = (uint16_t)lb;
+                if (k < (uint32_t)kBlock) {
+#pragma unroll
+                    for (int j = 0; j < (int)kNBW; j++) s_aw[j * kBlock + k] = w4[q][j];
+                    s_aw[kNBW * kBlock + k] = nin4[q];
+                }
+            }
+            nact += (uint32_t)__popcll(m);
+        }
+    }
+    if (P.bins) {   // the lane's idle hosts' calendar bound: one, from their bitmaps' OR (the
+                    // block's min over the lanes comes with the round's fold below)
+        const uint64_t cb = cal_lower_bound(P, orw, we);
+        next = cb < next ? cb : next;
+    }
+#ifdef SHD_TIMING
+    TIMVP(23, wall_clock64());   // the compaction done (before the barrier)
+#endif
+}
+
+// k_round_sp / k_round_spx: the scan's active hosts, 64 at a time: each pass
+// loads its hosts' records (with the bins' loads, ps_round_body<true>), runs
+// their round and stores them; next / nev / npkt / fl / nhost accumulate the
+// lane's share (PEND: a logged first touch flags kPsPend)
+template <bool PEND>
+__device__ __forceinline__ void sp_passes(const DParams& P, HostCtx& c, const PsRsrc& R, uint32_t hb, uint32_t nact,
+                                          uint64_t ws, uint64_t we, int parity, uint32_t xwi, uint64_t& next,
+                                          uint32_t& nev, uint32_t& npkt, uint32_t& fl, uint32_t& nhost) {
+    const uint32_t lane = threadIdx.x;
+    for (uint32_t base = 0; base < nact; base += kBlock) {
+        const uint32_t k = base + lane;
+        const bool act = k < nact;
+        const uint32_t lb = act ? (uint32_t)s_act[k] : 0u;
+        const int32_t l = (int32_t)(hb + lb);
+        uint32_t nin = 0, w[kNBW];
+#pragma unroll
+        for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
+        if (act) {
+            if (base == 0) {
+#pragma unroll
+                for (int j = 0; j < (int)kNBW; j++) w[j] = s_aw[j * kBlock + k];
+                nin = s_aw[kNBW * kBlock + k];
+            } else {   // later passes (more than 64 active hosts): the words again
+                nin = ld4_sc1(R.nin, lb * 4u);
+                if (P.bins) {
+                    const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
+                    w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+                }
+            }
+        }
+        SpIn in;   // the record's loads go out with the bins' (ps_round_body<true>)
+        in.l = l;
+        in.xwi = xwi;
+        if (act) {
+            in.rec = P.hs[l];
+            in.att = P.host_att[P.h0 + l];
+            in.st = P.self_thr[P.h0 + l];
+        }
+        const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
+        uint64_t hn = kInf;
+        ps_round_body<true>(P, c, act, lb, R, ws, we, parity, nin, w, wbits, hn, &in);
+        if (act) store_ctx(P, c);
+        next = hn < next ? hn : next;
+        nev += c.c_events; npkt += c.c_pkt;
+        fl |= c.err | (PEND && c.n_pend ? kPsPend : 0u);
+        nhost += (uint32_t)__popcll(__ballot(act && c.c_events != 0));
+        __syncthreads();   // (the next pass reuses the lanes' LDS slots)
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, DevSummary* __restrict__ ring,
                                                       const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
                                                       const DParams* __restrict__ Pr, uint64_t ticks, uint32_t sph) {
@@ -1707,12 +1861,11 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
     const uint64_t stop = ctl->stop, rbase = ctl->round_base;
     const uint32_t tag0 = (uint32_t)ctl->xtag;
     const bool lead = blockIdx.x == 0 && lane == 0;
-    const uint64_t lt_mask = (1ull << lane) - 1ull;
     for (int i = 0; i < nb; i++) {
         PS_PARAMS(i);
         const unsigned long long t_start = wall_clock64();
 #ifdef SHD_TIMING
-        if (lane == 0 && blockIdx.x < 2048) g_tim[((uintptr_t)P.sum / sizeof(DevSummary)) & 63][blockIdx.x][0] = t_start;
+        if (lane == 0 && blockIdx.x < 2048) g_tim[PS_TIM_SLOT()][blockIdx.x][0] = t_start;
 #endif
         if (lead) ps_fresh(&ring[i + 2]);
         const int parity = (int)((rbase + (uint64_t)i) & 1);
@@ -1722,94 +1875,16 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         R.nin = parity ? R1.nin : R0.nin;
         R.inbox = parity ? R1.inbox : R0.inbox;
         ps_round_reset(P, c, ws, we, parity, false);
-        // the scan: every host's words and own next time, four groups per round trip
-        uint64_t next = kInf;
-        uint32_t nact = 0;
-        for (uint32_t g0 = 0; g0 < ngrp; g0 += kSpScan) {
-            uint32_t nin4[kSpScan], w4[kSpScan][kNBW];
-            uint64_t t4[kSpScan];
-#pragma unroll
-            for (int q = 0; q < kSpScan; q++) {
-                const uint32_t lb = (g0 + q) * 64u + lane;
-                nin4[q] = 0; t4[q] = kInf;
-#pragma unroll
-                for (int j = 0; j < (int)kNBW; j++) w4[q][j] = 0;
-                if (g0 + q < ngrp && lb < nh) {
-                    nin4[q] = ld4_sc1(R.nin, lb * 4u);
-                    if (P.bins) {
-                        const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
-                        w4[q][0] = x.x; w4[q][1] = x.y; w4[q][2] = x.z; w4[q][3] = x.w;
-                        w4[q][4] = y.x; w4[q][5] = y.y; w4[q][6] = y.z; w4[q][7] = y.w;
-                    }
-                    t4[q] = P.hnext[hb + lb];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < kSpScan; q++) {
-                const uint32_t lb = (g0 + q) * 64u + lane;
-                const bool has = g0 + q < ngrp && lb < nh;
-                const uint32_t wbits = ps_window_bits(P, c, w4[q], ws, we);
-                const bool act = has && !(nin4[q] == 0 && t4[q] >= we && wbits == 0);
-                if (has && !act) {
-                    const uint64_t t = ps_idle_next(P, w4[q], t4[q], we);
-                    next = t < next ? t : next;
-                }
-                const uint64_t m = __ballot(act);
-                if (act) {
-                    const uint32_t k = nact + (uint32_t)__popcll(m & lt_mask);
-                    s_act[k] = (uint16_t)lb;
-                    if (k < (uint32_t)kBlock) {
-#pragma unroll
-                        for (int j = 0; j < (int)kNBW; j++) s_aw[j * kBlock + k] = w4[q][j];
-                        s_aw[kNBW * kBlock + k] = nin4[q];
-                    }
-                }
-                nact += (uint32_t)__popcll(m);
-            }
-        }
+        uint64_t next;
+        uint32_t nact;
+        sp_scan(P, R, hb, nh, ngrp, ws, we, next, nact);
         __syncthreads();
-        TIM(1);
+        TIMP(1);
+        TIMVP(20, (uint64_t)nact);   // the block's active hosts this round
+        TIMVP(21, (uint64_t)((nact + kBlock - 1) / kBlock));   // passes
         // the active hosts, 64 at a time
         uint32_t nev = 0, npkt = 0, fl = 0, nhost = 0;
-        for (uint32_t base = 0; base < nact; base += kBlock) {
-            const uint32_t k = base + lane;
-            const bool act = k < nact;
-            const uint32_t lb = act ? (uint32_t)s_act[k] : 0u;
-            const int32_t l = (int32_t)(hb + lb);
-            uint32_t nin = 0, w[kNBW];
-#pragma unroll
-            for (int j = 0; j < (int)kNBW; j++) w[j] = 0;
-            if (act) {
-                if (base == 0) {
-#pragma unroll
-                    for (int j = 0; j < (int)kNBW; j++) w[j] = s_aw[j * kBlock + k];
-                    nin = s_aw[kNBW * kBlock + k];
-                } else {   // later passes (more than 64 active hosts): the words again
-                    nin = ld4_sc1(R.nin, lb * 4u);
-                    if (P.bins) {
-                        const uint4 x = ld16_sc1(R.bits, lb * 32u), y = ld16_sc1(R.bits, lb * 32u + 16u);
-                        w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
-                    }
-                }
-            }
-            SpIn in;   // the record's loads go out with the bins' (ps_round_body<true>)
-            in.l = l;
-            in.xwi = 0;
-            if (act) {
-                in.rec = P.hs[l];
-                in.att = P.host_att[P.h0 + l];
-                in.st = P.self_thr[P.h0 + l];
-            }
-            const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
-            uint64_t hn = kInf;
-            ps_round_body<true>(P, c, act, lb, R, ws, we, parity, nin, w, wbits, hn, &in);
-            if (act) store_ctx(P, c);
-            next = hn < next ? hn : next;
-            nev += c.c_events; npkt += c.c_pkt;
-            fl |= c.err | (c.n_pend ? kPsPend : 0u);
-            nhost += (uint32_t)__popcll(__ballot(act && c.c_events != 0));
-            __syncthreads();   // (the next pass reuses the lanes' LDS slots)
-        }
+        sp_passes<true>(P, c, R, hb, nact, ws, we, parity, 0u, next, nev, npkt, fl, nhost);
         for (int off = 32; off > 0; off >>= 1) {
             const uint64_t o = __shfl_xor(next, off, 64);
             next = o < next ? o : next;
@@ -1820,11 +1895,11 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         const uint32_t tag = tag0 + (uint32_t)i;
         const uint32_t sbase = (uint32_t)(i & 1) * nblk;
         ps_publish(rs, sbase + blockIdx.x, next, fl, nev, npkt, nhost, tag, ps_noted(false));
-        TIM(6);
+        TIMP(6);
         uint64_t f_next;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
         const bool ok_v = ps_gather<false>(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
-        TIM(7);
+        TIMP(7);
         const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;
         f_fl = __builtin_amdgcn_readfirstlane(f_fl);
         f_next = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(f_next >> 32)) << 32) |

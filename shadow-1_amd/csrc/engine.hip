@@ -1106,6 +1106,13 @@ static int take_restore_point(shd_eng* e, uint64_t next) {
 }
 
 static bool replay_off() { return getenv("SHD_NO_REPLAY") != nullptr; }
+// rounds after which a restore point is renewed (the test build: SHD_RESTORE_EVERY)
+static uint64_t restore_every() {
+#ifdef SHD_TEST_HOOKS
+    if (const char* v = getenv("SHD_RESTORE_EVERY")) return strtoull(v, nullptr, 10);
+#endif
+    return 1ull << 16;
+}
 
 static bool want_protect(const shd_eng* e) {
     if (protect_off() || e->snap_failed) return false;
@@ -1279,12 +1286,13 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
     if (!e->in_replay) e->kernel_ms_total = 0;
     const uint64_t pend0 = e->pending_resolved;
     // a restore point for an ambiguous unprotected round (replay_ambiguous);
-    // complete graphs never log a first touch.  A point more than kRestoreEvery
-    // rounds old is renewed, so that a replay never reruns more than that (a
-    // copy of the state every 2^16 rounds: 0.01 % of C3's run, 0.6 % of the
-    // 1 M-host shard's)
-    constexpr uint64_t kRestoreEvery = 1ull << 16;
-    const bool stale = e->snap_valid && e->round - e->snap_round > kRestoreEvery;
+    // complete graphs never log a first touch.  A point more than
+    // restore_every() rounds old is renewed -- here and between the batches of
+    // this call, after a batch that ended cleanly -- so that a replay never
+    // reruns more than that plus one batch (a copy of the state every 2^16
+    // rounds: 0.01 % of C3's run, 0.6 % of the 1 M-host shard's)
+    const uint64_t every = restore_every();
+    const bool stale = e->snap_valid && e->round - e->snap_round > every;
     if ((!e->snap_valid || stale) && !e->snap_failed && !e->P.complete && !replay_off() && next < stop &&
         !want_protect(e)) {
         const int rc0 = take_restore_point(e, next);
@@ -1312,6 +1320,16 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
             e->tl_ready = e->last_logged == 0;
             next = r.next_time;
             continue;
+        }
+        // a stale restore point renewed between batches (the state is at a
+        // round start, window start `next`, as at a call's entry), so that the
+        // rounds a replay reruns stay bounded within one long call too
+        if (e->snap_valid && !e->in_replay && e->round - e->snap_round > every && !e->snap_failed &&
+            !replay_off()) {
+            e->h_sum->next_time = next;
+            const int rc0 = take_restore_point(e, next);
+            if (rc0 && rc0 != SHD_ENOMEM) { rc = rc0; break; }
+            s.n_restore_points++;
         }
         // slot 0 carries the window start; rounds use slots 1..B
         e->h_seed[0] = host_fresh_summary();
@@ -1465,7 +1483,7 @@ extern "C" int shd_eng_run_until(shd_eng* e, uint64_t t_stop, shd_run_stats* st)
 }
 
 #ifdef SHD_TIMING
-extern "C" int shd_debug_timing(uint64_t* out) {   // 64 x 2048 x 20
+extern "C" int shd_debug_timing(uint64_t* out) {   // 64 x 2048 x 24
     SHD_HIP(hipDeviceSynchronize());
     SHD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tim), sizeof(g_tim)));
     return SHD_OK;

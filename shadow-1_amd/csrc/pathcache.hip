@@ -2146,6 +2146,68 @@ extern "C" int shd_pc_min_time_jump(shd_pc* pc, uint64_t runahead_ns, uint64_t* 
     return SHD_OK;
 }
 
+// minimumPathLatency after a run that ranked rows on the device (shd_tcp_run's
+// path_cache mode, pc->h_rank / h_self_rank holding the run's final ranks,
+// old_rank / old_self the ranks before it): the entries each newly ranked row
+// stored (k_pc_newrow_min, run_row_for_min's rule) and each newly stored self
+// path (pc_lookup_at's self branch) are folded in.  The direct entries of a
+// complete graph, which pc_lookup_at notes on every lookup, are not: the
+// device path keeps no list of the pairs it queried
+__attribute__((visibility("hidden"))) int shd_pc_fold_ranked(shd_pc* pc, const int32_t* old_rank,
+                                                             const int32_t* old_self) {
+    if (!pc || pc->complete || !pc->d_row) return SHD_OK;
+    const int32_t T = pc->T;
+    std::vector<int32_t> nrow, nrank;
+    bool new_self = false;
+    for (int32_t a = 0; a < T; a++) {
+        if (old_rank[a] == kNoRank && pc->h_rank[a] != kNoRank) { nrow.push_back(a); nrank.push_back(pc->h_rank[a]); }
+        new_self |= old_self[a] == kNoRank && pc->h_self_rank[a] != kNoRank;
+    }
+    SHD_HIP(hipSetDevice(pc->device));
+    if (new_self) {
+        std::vector<shd_pv> sv(T);
+        SHD_HIP(hipMemcpy(sv.data(), pc->d_self, sizeof(shd_pv) * (size_t)T, hipMemcpyDeviceToHost));
+        for (int32_t a = 0; a < T; a++)
+            if (old_self[a] == kNoRank && pc->h_self_rank[a] != kNoRank && pc->h_self_rank[a] < pc->h_rank[a] &&
+                sv[a].lat >= 0)
+                note_min(pc, sv[a].lat);
+    }
+    if (nrow.empty()) return SHD_OK;
+    const size_t nr = nrow.size();
+    int32_t *d_rows = nullptr, *d_rrank = nullptr, *d_rank = nullptr, *d_srank = nullptr;
+    unsigned long long* d_min = nullptr;
+    unsigned long long mn = kDistInf;
+    int rc = SHD_OK;
+    hipStream_t s = pc->stream;
+    if (hipMalloc(&d_rows, 4 * nr) != hipSuccess || hipMalloc(&d_rrank, 4 * nr) != hipSuccess ||
+        hipMalloc(&d_rank, 4 * (size_t)T) != hipSuccess || hipMalloc(&d_srank, 4 * (size_t)T) != hipSuccess ||
+        hipMalloc(&d_min, 8) != hipSuccess) {
+        rc = SHD_ENOMEM;
+    } else if (hipMemcpyAsync(d_rows, nrow.data(), 4 * nr, hipMemcpyHostToDevice, s) != hipSuccess ||
+               hipMemcpyAsync(d_rrank, nrank.data(), 4 * nr, hipMemcpyHostToDevice, s) != hipSuccess ||
+               hipMemcpyAsync(d_rank, pc->h_rank, 4 * (size_t)T, hipMemcpyHostToDevice, s) != hipSuccess ||
+               hipMemcpyAsync(d_srank, pc->h_self_rank, 4 * (size_t)T, hipMemcpyHostToDevice, s) != hipSuccess ||
+               hipMemcpyAsync(d_min, &mn, 8, hipMemcpyHostToDevice, s) != hipSuccess) {
+        rc = SHD_ENODEV;
+    } else {
+        const size_t tot = nr * (size_t)T;
+        hipLaunchKernelGGL(k_pc_newrow_min, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 2048)), dim3(256), 0, s,
+                           d_rows, d_rrank, (int32_t)nr, T, d_rank, d_srank, pc->d_row, pc->d_adj, pc->prefer_direct,
+                           d_min);
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(&mn, d_min, 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            rc = SHD_ENODEV;
+        else if (mn != kDistInf) {
+            double m;
+            memcpy(&m, &mn, 8);
+            note_min(pc, m);
+        }
+    }
+    for (void* q : {(void*)d_rows, (void*)d_rrank, (void*)d_rank, (void*)d_srank, (void*)d_min})
+        if (q) (void)hipFree(q);
+    return rc;
+}
+
 extern "C" int shd_pc_min_stored_latency(shd_pc* pc, double* ms) {
     if (!pc || !ms) return SHD_EINVAL;
     *ms = pc->min_stored_latency;

@@ -51,6 +51,8 @@
 // send_off[p], this rank recv_bytes[p] from peer p into d_recv + recv_off[p] (the sizes
 // agreed beforehand); RCCL: grouped send / receive on `s`; the host transport: fixed
 // blocks of the largest size through host memory (synchronizes `s`)
+__attribute__((visibility("hidden"))) int shd_pc_fold_ranked(shd_pc* pc, const int32_t* old_rank,
+                                                             const int32_t* old_self);
 __attribute__((visibility("hidden"))) int shd_comm_alltoallv_dev(shd_comm* c, const char* d_send,
                                                                  const size_t* send_off, const size_t* send_bytes,
                                                                  char* d_recv, const size_t* recv_off,
@@ -3096,6 +3098,21 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     }
     if (W == 0) return -22;
     if (W == ~0ull) W = m->end_time ? m->end_time : 1;
+    // test_tcp.c's client takes its server's listening port when it connects
+    // (its message queue); the device publishes a port where the server's bind
+    // runs, and another lane -- or, on a group, another engine -- sees it from
+    // the next round on.  A client on another host that starts within
+    // [server start, server start + W) could connect in the server's own round,
+    // and what it read would depend on the lanes' timing (one engine) or
+    // differ from the one-engine run (a group): such a model is refused, on
+    // one engine and on a group alike.  W later the port is always there; a
+    // client that starts before its server finds none on every path, as in
+    // the serial loop
+    for (int32_t k = 0; k < P; k++) {
+        const int32_t s = m->proc_peer[k];
+        if (s < 0 || m->proc_host[k] == m->proc_host[s]) continue;
+        if (m->proc_start[k] >= m->proc_start[s] && m->proc_start[k] - m->proc_start[s] < W) return -22;
+    }
 
     int rc = 0;
     int dev = 0;
@@ -3528,9 +3545,12 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         if (cx.ft_bad) res->error |= SHD_TCP_ERR_FIRST_TOUCH;
         res->error |= cx.xerr;
         if (pc && !cx.ft_bad) {   // the cache's ranks as the serial run leaves them
+            std::vector<int32_t> old_rank(pc->h_rank, pc->h_rank + V), old_self(pc->h_self_rank, pc->h_self_rank + V);
             HCHECK(hipMemcpy(pc->h_rank, g.rank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
             HCHECK(hipMemcpy(pc->h_self_rank, g.srank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
             HCHECK(hipMemcpy(&pc->next_rank, g.next_rank, sizeof(int32_t), hipMemcpyDeviceToHost));
+            // and minimumPathLatency with the entries those rows stored
+            if (const int fr = shd_pc_fold_ranked(pc, old_rank.data(), old_self.data())) { rc = fr; goto done; }
         }
         for (int b = 0; b < 2; b++) {
             uint64_t sum = 0;

@@ -184,7 +184,8 @@ class RunStats(C.Structure):
                           ("n_batches_ticketless", C.c_uint32), ("n_rounds_protected", C.c_uint32),
                           ("n_rounds_rerun", C.c_uint32), ("n_host_rounds", C.c_uint64),
                           ("n_batches", C.c_uint64), ("n_batches_persistent", C.c_uint64),
-                          ("n_batches_sparse", C.c_uint64), ("n_rounds_replayed", C.c_uint64)]
+                          ("n_batches_sparse", C.c_uint64), ("n_rounds_replayed", C.c_uint64),
+                         ("n_restore_points", C.c_uint64)]
 
 
 # exported symbols (checked by tests/test_abi.py against include/shdgpu.h)

@@ -153,6 +153,7 @@ def run(model: S.ModelArrays, g: S.GraphArrays, ips, procs, peers, nbytes=20000,
             out["first_touch"] = "tables"
             out["first_touch_runs"] = runs
             out["first_touch_pairs"] = len(pairs)
+            out["first_touch_order"] = [(int(att[a]), int(att[b])) for a, b in order]   # graph vertices
             return out
         # the serial order of this run's first touches: run again on it
         lat, rel = lat.copy(), rel.copy()

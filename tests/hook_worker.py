@@ -80,10 +80,11 @@ def engine_replay(steps):
     pc = PathCache(g, W.attached_vertices(m.host_vertex))
     eng = Engine(m, pc)
     end = m.params["end_time"]
-    tot = dict(replayed=0, rerun=0, protected=0, rounds=0, pkt=0, events=0)
+    tot = dict(replayed=0, rerun=0, protected=0, rounds=0, pkt=0, events=0, renewed=0, max_replay=0)
     for k in range(1, steps + 1):
         st = eng.run_until(end * k // steps)
         tot["replayed"] += st.n_rounds_replayed
+        tot["renewed"] += st.n_restore_points
         tot["rerun"] += st.n_rounds_rerun
         tot["protected"] += st.n_rounds_protected
         tot["rounds"] += st.n_rounds

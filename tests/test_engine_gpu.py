@@ -101,6 +101,19 @@ def test_ambiguous_unprotected_rounds_replay(steps):
     assert st["replayed"] > 0 and st["rerun"] > 0 and st["protected"] < st["rounds"], st
 
 
+def test_restore_point_renewed_between_batches():
+    # a restore point older than the renewal interval is renewed
+    # between the batches of one call too (not only at a call's entry), so an
+    # ambiguous round late in a long call replays a bounded number of rounds.
+    # With the interval at 8 rounds (test build) the one-call run renews it,
+    # stays the oracle's bit for bit, and replays fewer rounds than with the
+    # default interval
+    far = run_hooked("engine_replay", 1, SHD_PROTECT_ALL=None, SHD_NO_PROTECT="1")
+    near = run_hooked("engine_replay", 1, SHD_PROTECT_ALL=None, SHD_NO_PROTECT="1", SHD_RESTORE_EVERY="8")
+    assert far["renewed"] == 0 and near["renewed"] > 0, (far, near)
+    assert near["rerun"] > 0 and near["replayed"] <= far["replayed"], (far, near)
+
+
 def test_product_library_ignores_the_test_hooks(monkeypatch):
     # the product build has no hooks: with the variables set, nothing is forced
     monkeypatch.setenv("SHD_FORCE_AMBIG", "1")

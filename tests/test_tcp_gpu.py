@@ -204,3 +204,49 @@ def test_tcp_gpu_device_first_touch_contradiction_falls_back():
     assert r2["first_touch"] == "device"
     assert r2["lines"] == TC.by_host(o2["lines"])
     assert r2["next_event_id"].tolist() == o2["next_event_id"].tolist()
+
+
+def test_tcp_gpu_refuses_a_connect_in_its_servers_window():
+    """a client reads its server's listening port when it
+    connects, and the device publishes that port in the round the server
+    binds; a client on another host starting less than one window W after its
+    server could connect in that same round and read the port or not by the
+    lanes' timing (on a group: differently from one engine).  Such a model is
+    refused; the same client a window later runs and equals the oracle."""
+    import workloads as W
+    g, m, ips, _, _, nb = W.tcp_echo_model(2, 30, end_s=4, nbytes=20000)
+    procs = [(0, S.SHD_SEC), (1, S.SHD_SEC + 1000)]
+    peers = [-1, 0]
+    with pytest.raises(S.ShdError):
+        TCPGPU.run(m, g, ips, procs, peers, nbytes=nb)
+    procs2 = [(0, S.SHD_SEC), (1, S.SHD_SEC + 300 * S.SHD_MS)]
+    r = TCPGPU.run(m, g, ips, procs2, peers, nbytes=nb)
+    o = O.tcp_run(m, g, ips, procs2, peers, nbytes=nb)
+    assert r["lines"] == TC.by_host(o["lines"])
+    assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
+
+
+def test_tcp_gpu_path_cache_min_latency_follows_the_run():
+    """after a run on the path cache itself, the cache's
+    minimumPathLatency (shd_pc_min_stored_latency, which topology_shd.c reads
+    for the min time jump) includes the entries of the rows the run ranked, as
+    if the run's first touches had gone through shd_pc_lookup in serial order:
+    a fresh cache replaying the settled first-touch order of the tables path
+    ends with the same value."""
+    import ctypes as C
+    import sim
+    import workloads as W
+    g, m, ips, procs, peers, nb = W.tcp_echo_model(24, 30, end_s=4, nbytes=20000)
+    hv = np.asarray(m.host_vertex, dtype=np.int32)
+    pc = sim.PathCache(g, np.unique(hv))
+    out = TCPGPU._run_once(m, ips, procs, peers, None, None, hv, nb, False, TCPGPU.RECV_BUF, TCPGPU.SEND_BUF,
+                           TCPGPU.TCP_WINDOW, 0, pc=pc)
+    assert out is not None   # the device's first touches held
+    r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb, trace=False, mode="tables")
+    pc2 = sim.PathCache(g, np.unique(hv))
+    for a, b in r["first_touch_order"]:
+        pc2.lookup(a, b)
+    m1, m2 = C.c_double(), C.c_double()
+    S.check(S.lib().shd_pc_min_stored_latency(pc.ptr, C.byref(m1)), "min")
+    S.check(S.lib().shd_pc_min_stored_latency(pc2.ptr, C.byref(m2)), "min")
+    assert m1.value == m2.value > 0, (m1.value, m2.value)

@@ -145,6 +145,18 @@ def test_multiprocess_group_rolls_back_ambiguous_rounds(p2p, tmp_path):
     assert all(int(r["stats"][5]) > 0 for r in res)            # reruns happened on every rank
 
 
+def test_p2p_self_check_failure_fails_every_rank_alike(tmp_path):
+    """The peer-to-peer mapping's self-check (round 6): every rank puts a known
+    granule into every peer's receive block over the mapping and each receiver
+    checks what came.  A rank that puts a wrong one (test hook) fails the
+    check at its peers: every rank gets SHD_ENODEV from
+    shd_xgroup_create_p2p alike, falls back to the all-to-all transport, and
+    the run still matches the oracle."""
+    res = run_ranks(2, tmp_path, extra=["--p2p"], env_extra={"SHD_P2P_PROBE_CORRUPT": "1", "SHDGPU_LIB": TH_LIB})
+    check_against_oracle(res, 240, 1, 3.0, 0.01, 16)
+    assert all(int(r["stats"][6]) == 1 for r in res)
+
+
 def test_p2p_mapping_failure_on_one_rank_fails_every_rank_alike(tmp_path):
     """A rank that cannot map its peers' receive blocks (test hook) takes part
     in both all-gathers of the mapping: every rank gets SHD_ENODEV from
