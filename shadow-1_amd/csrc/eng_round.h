@@ -1363,11 +1363,12 @@ __device__ __forceinline__ uint4 ps_noted(bool pf) {
     return d;
 }
 
-// every block's share of round i (slots [base, base + nblk)): poll until all
+// every block's share of round i (slots [base, base + nblk)), K per lane per
+// poll (64 K blocks a chunk, the chunks one after the other): poll until all
 // carry `tag`, folding them; block 0 also folds the counts.  DIRTY: the noted
 // destinations too -- bit k of `dmask`: host hb + k of this block was named,
 // `dall`: some block noted more than it could name.  False on timeout
-template <bool DIRTY>
+template <bool DIRTY, int K = 4>
 __device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nblk, uint32_t tag, bool counts,
                           uint64_t ticks, uint64_t& next, uint32_t& flags, uint32_t& nev, uint32_t& npkt,
                           uint32_t& nact, uint32_t hb = 0, uint32_t hpw = 0, uint64_t* dmask = nullptr,
@@ -1376,15 +1377,15 @@ __device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t ba
     uint64_t dm = 0;
     uint32_t da = 0;
     const unsigned long long t0 = wall_clock64();
-    for (uint32_t c0 = 0; c0 < nblk; c0 += 256) {
+    for (uint32_t c0 = 0; c0 < nblk; c0 += 64u * K) {
         uint32_t need = 0;
 #pragma unroll
-        for (int k = 0; k < 4; k++)
+        for (int k = 0; k < K; k++)
             if (c0 + 64u * k + threadIdx.x < nblk) need |= 1u << k;
         while (__ballot(need != 0)) {
-            uint4 a[4], b[4], d[4];
+            uint4 a[K], b[K], d[K];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < K; k++) {
                 const uint32_t off = (base + c0 + 64u * k + threadIdx.x) * 48u;
                 a[k] = make_uint4(0, 0, 0, 0);
                 b[k] = a[k];
@@ -1396,7 +1397,7 @@ __device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t ba
                 }
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < K; k++) {
                 if (!((need >> k) & 1u) || a[k].w != tag || (counts && b[k].w != tag) || (DIRTY && d[k].w != tag))
                     continue;
                 const uint64_t t = ((uint64_t)a[k].y << 32) | a[k].x;
@@ -1683,6 +1684,10 @@ constexpr uint32_t kSpMaxHosts = 4096;   // hosts per block at most (64 groups o
 #define SHD_SP_SCAN 8
 #endif
 constexpr int kSpScan = SHD_SP_SCAN;
+#ifndef SHD_SP_GATHER_K
+#define SHD_SP_GATHER_K 8
+#endif
+constexpr int kSpGatherK = SHD_SP_GATHER_K;   // shares per lane per poll of the sparse round's barrier
 __shared__ uint16_t s_act[kSpMaxHosts];  // the round's active hosts (index in the block)
 __shared__ uint32_t s_aw[(kNBW + 1) * kBlock];   // the first pass's hand-off words: bitmap, inbox count
 
@@ -1898,7 +1903,10 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         TIMP(6);
         uint64_t f_next;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
-        const bool ok_v = ps_gather<false>(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt, f_nact);
+        // (K = 8: the C5 shard's ~490 blocks in one chunk, so that the shares
+        // published last are polled once, not after the first chunk's wait)
+        const bool ok_v = ps_gather<false, kSpGatherK>(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl,
+                                                       f_nev, f_npkt, f_nact);
         TIMP(7);
         const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;
         f_fl = __builtin_amdgcn_readfirstlane(f_fl);
