@@ -635,7 +635,7 @@ def lossy_leg(args, S, W, Engine, PathCache, host_vertex, step, end_time, dev, t
 
 def pmc_traffic(workload, kernel):
     """HBM bytes per round of the round kernel from the committed rocprofv3
-    PMC passes of THIS workload and kernel (profiles/r05 or r04/pmc_traffic.json,
+    PMC passes of THIS workload and kernel (profiles/r06, r05 or r04/pmc_traffic.json,
     scripts/pmc_traffic.py: FETCH_SIZE x the calibrated read correction +
     WRITE_SIZE, over the timed region's dispatches), used only when they were
     taken of the engine source being run; else None (no inherited numbers)."""
@@ -645,7 +645,7 @@ def pmc_traffic(workload, kernel):
     except (OSError, ValueError):
         return None
     prof = {}
-    for rnd in ("r05", "r04"):   # the newest round's passes of this source
+    for rnd in ("r06", "r05", "r04"):   # the newest round's passes of this source
         try:
             prof = json.load(open(os.path.join(REPO, "profiles", rnd, "pmc_traffic.json")))
         except (OSError, ValueError):

@@ -1684,10 +1684,13 @@ constexpr uint32_t kSpMaxHosts = 4096;   // hosts per block at most (64 groups o
 #define SHD_SP_SCAN 8
 #endif
 constexpr int kSpScan = SHD_SP_SCAN;
+// shares per lane per poll of the sparse round's barrier: 4 (chunks of 256
+// blocks, one after the other) measured faster than 8 at the C5 shard's 489
+// blocks, 76.7 against 75.6 M (round 6, profiles/r06/sp3)
 #ifndef SHD_SP_GATHER_K
-#define SHD_SP_GATHER_K 8
+#define SHD_SP_GATHER_K 4
 #endif
-constexpr int kSpGatherK = SHD_SP_GATHER_K;   // shares per lane per poll of the sparse round's barrier
+constexpr int kSpGatherK = SHD_SP_GATHER_K;
 __shared__ uint16_t s_act[kSpMaxHosts];  // the round's active hosts (index in the block)
 __shared__ uint32_t s_aw[(kNBW + 1) * kBlock];   // the first pass's hand-off words: bitmap, inbox count
 
@@ -1903,8 +1906,6 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         TIMP(6);
         uint64_t f_next;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
-        // (K = 8: the C5 shard's ~490 blocks in one chunk, so that the shares
-        // published last are polled once, not after the first chunk's wait)
         const bool ok_v = ps_gather<false, kSpGatherK>(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl,
                                                        f_nev, f_npkt, f_nact);
         TIMP(7);

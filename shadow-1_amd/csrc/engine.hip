@@ -84,6 +84,7 @@ struct shd_eng {
     // before a round that may log many first touches, restored when one of its
     // drop decisions turns out ambiguous, then the round reruns with the ranks
     std::vector<void*> snap;
+    std::vector<uint8_t> snap_kind;   // per entry: 0 device, 1 pinned host, 2 pageable host
     bool snap_failed = false;
     // the copy as a restore point (shd_eng_run_until): `snap` holds the state
     // at the start of round snap_round, window start snap_next, and nothing
@@ -1068,27 +1069,63 @@ static constexpr uint64_t kProtectMin = 64;
 static bool protect_all() { return test_hook("SHD_PROTECT_ALL"); }
 static bool protect_off() { return getenv("SHD_NO_PROTECT") != nullptr; }
 
+// the state copy's memory: device memory, or where that is exhausted (round 6:
+// a 1 M-host engine beside its state copy on a full device) pinned host memory,
+// else pageable host memory -- the copy then crosses PCIe and a protected round
+// costs more, but the rounds stay protected and ambiguous first touches stay
+// recoverable instead of failing the run
+static void snap_free(shd_eng* e) {
+    for (size_t i = 0; i < e->snap.size(); i++) {
+        if (!e->snap[i]) continue;
+        const uint8_t k = i < e->snap_kind.size() ? e->snap_kind[i] : 0;
+        if (k == 0) (void)hipFree(e->snap[i]);
+        else if (k == 1) (void)hipHostFree(e->snap[i]);
+        else free(e->snap[i]);
+    }
+    e->snap.clear();
+    e->snap_kind.clear();
+}
 static int snapshot_state(shd_eng* e, bool restore) {
     if (!restore && e->snap.size() != e->allocs.size()) {
+        bool warned = false;
         for (size_t i = e->snap.size(); i < e->allocs.size(); i++) {
+            const size_t bytes = e->alloc_bytes[i];
             void* q = nullptr;
-            if (hipMalloc(&q, e->alloc_bytes[i]) != hipSuccess) {
+            uint8_t kind = 0;
+            if (test_hook("SHD_SNAP_NO_DEVICE") || hipMalloc(&q, bytes) != hipSuccess) {
                 (void)hipGetLastError();
-                for (void* p : e->snap) (void)hipFree(p);
-                e->snap.clear();
-                e->snap_failed = true;
-                fprintf(stderr, "libshdgpu: no memory for the protected-round state copy; "
-                                "rounds run unprotected (an ambiguous first touch fails the run)\n");
-                return SHD_ENOMEM;
+                q = nullptr;
+                kind = 1;
+                if (hipHostMalloc(&q, bytes, hipHostMallocDefault) != hipSuccess) {
+                    (void)hipGetLastError();
+                    kind = 2;
+                    q = malloc(bytes);
+                }
+                if (!q) {
+                    snap_free(e);
+                    e->snap_failed = true;
+                    fprintf(stderr, "libshdgpu: no memory for the protected-round state copy; "
+                                    "rounds run unprotected (an ambiguous first touch fails the run)\n");
+                    return SHD_ENOMEM;
+                }
+                if (!warned && getenv("SHD_VERBOSE"))
+                    fprintf(stderr, "libshdgpu: the protected-round state copy in host memory (%s)\n",
+                            kind == 1 ? "pinned" : "pageable");
+                warned = true;
             }
             e->snap.push_back(q);
+            e->snap_kind.push_back(kind);
         }
     }
     for (size_t i = 0; i < e->allocs.size(); i++) {
         void* dst = restore ? e->allocs[i] : e->snap[i];
         const void* src = restore ? e->snap[i] : e->allocs[i];
-        SHD_HIP(hipMemcpyAsync(dst, src, e->alloc_bytes[i], hipMemcpyDeviceToDevice, e->stream));
+        const hipMemcpyKind k = e->snap_kind[i] == 0 ? hipMemcpyDeviceToDevice
+                                : restore ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+        SHD_HIP(hipMemcpyAsync(dst, src, e->alloc_bytes[i], k, e->stream));
     }
+    if (std::any_of(e->snap_kind.begin(), e->snap_kind.end(), [](uint8_t k) { return k == 2; }))
+        SHD_HIP(hipStreamSynchronize(e->stream));   // (pageable copies: done before the host moves on)
     return SHD_OK;
 }
 
@@ -1676,7 +1713,7 @@ extern "C" void shd_eng_destroy(shd_eng* e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     for (void* p : e->allocs) (void)hipFree(p);
-    for (void* p : e->snap) (void)hipFree(p);   // the protected rounds' / restore point's state copy
+    snap_free(e);   // the protected rounds' / restore point's state copy
     if (e->h_sum) (void)hipHostFree(e->h_sum);
     if (e->h_ring) (void)hipHostFree(e->h_ring);
     if (e->h_ctl) (void)hipHostFree(e->h_ctl);

@@ -97,7 +97,33 @@ def engine_replay(steps):
     return tot
 
 
-SCENARIOS = {"engine_rollback": engine_rollback, "group_rollback": group_rollback, "engine_replay": engine_replay}
+def c5_snap_host(_):
+    """SHD_SNAP_NO_DEVICE: the protected-round state copy cannot take device
+    memory (as on a full device), so it goes to host memory; the 1 M-host C5
+    model with CoDel queues building, its first-touch rounds protected behind
+    that copy, must still equal the committed oracle fixture."""
+    import fixture_hash as FH
+    import workloads as W
+    from fullsize_configs import CONFIGS, build
+    from sim import Engine, PathCache
+    cfg = CONFIGS["c5"]
+    fx = np.load(os.path.join(HERE, "golden", cfg["file"]))
+    g, m, _ = build("c5")
+    pc = PathCache(g, W.attached_vertices(m.host_vertex))
+    eng = Engine(m, pc)
+    st = eng.run()
+    assert st.error == 0
+    dg = eng.digest()
+    n_ev, n_pkt, _ = (int(x) for x in fx["totals"])
+    assert (st.n_events, st.n_pkt_events) == (n_ev, n_pkt), (st.n_events, st.n_pkt_events, n_ev, n_pkt)
+    bh = FH.digest_block_hashes(dg, cfg["block"])
+    bad = np.nonzero(bh != fx["block_hash"])[0]
+    assert len(bad) == 0, f"{len(bad)} host blocks differ, first {bad[:8]}"
+    return dict(protected=int(st.n_rounds_protected), rerun=int(st.n_rounds_rerun), rounds=int(st.n_rounds))
+
+
+SCENARIOS = {"engine_rollback": engine_rollback, "group_rollback": group_rollback, "engine_replay": engine_replay,
+             "c5_snap_host": c5_snap_host}
 
 
 def main():

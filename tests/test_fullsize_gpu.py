@@ -225,3 +225,24 @@ def test_c5_codel_million_hosts_sparse_group_rounds_match_fixture():
     assert (st.n_events, st.n_pkt_events) == (n_ev, n_pkt)
     bh = FH.digest_block_hashes(dg, cfg["block"])
     assert np.array_equal(bh, fx["block_hash"])
+
+
+def test_c5_protected_rounds_with_the_state_copy_in_host_memory():
+    """The protected rounds' state copy falls back to host memory when device
+    memory is exhausted (test build: SHD_SNAP_NO_DEVICE makes every device
+    allocation of the copy fail): the 1 M-host C5 run keeps its protected
+    rounds and still equals the oracle fixture bit for bit (checked in the
+    child, tests/hook_worker.py c5_snap_host)."""
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, SHD_SNAP_NO_DEVICE="1", SHD_VERBOSE="1",
+               SHDGPU_LIB=os.path.join(os.path.dirname(here), "shadow-1_amd", "libshdgpu_th.so"))
+    p = subprocess.run([sys.executable, "-u", os.path.join(here, "hook_worker.py"), "c5_snap_host", "0"], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=900)
+    out = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, out[-3000:]
+    assert "state copy in host memory" in out, out[-2000:]
+    st = json.loads(out.strip().splitlines()[-1])
+    assert st["protected"] > 0, st
