@@ -1100,6 +1100,155 @@ __global__ __launch_bounds__(kTieLanes) void k_sssp_tie_parents(
 }
 #undef TL
 
+// The same Dijkstra, one row per one-wave block with the row's state in LDS
+// (round 6: k_sssp_tie_parents' lane heaps in global scratch -- 240 KB a row at
+// 10 k vertices, every tied row in flight at once -- made each of a row's ~35
+// dependent heap steps per pop an HBM round trip: 490 ms for the 10 k
+// all-tied build).  Here the row keeps
+//   st[V]   uint16: 0 unreached, 1 popped, heap position + 2 (igraph's index2)
+//   hv[hc]  the heap's values (-distance), hi[hc] its vertices (uint16)
+// in LDS, and no distance array: an unreached vertex's is none, a heap
+// member's is -hv[pos] (exact), and a popped vertex is never relaxed (alt =
+// d(u) + w >= d(u) >= its distance: igraph's "strictly shorter" never holds).
+// A pop's arcs are loaded by the wave's lanes at once, each with its target's
+// state and value (only a target that an earlier arc of the same pop touched
+// can have changed since -- the same vertex again, a parallel edge: re-read),
+// and lane 0 runs the heap steps igraph takes, in arc order, only for the
+// arcs that push or decrease.  A row whose heap outgrows hc is left to
+// k_sssp_tie_parents (listed in ovf).  Same parents as k_sssp_tie_parents.
+__device__ __forceinline__ void tlds_shift_up(double* hv, uint16_t* hi, uint16_t* st, int32_t elem, double val,
+                                              int32_t id) {
+    while (elem != 0) {
+        const int32_t par = (elem + 1) / 2 - 1;
+        const double pv = hv[par];
+        if (val < pv) break;
+        const int32_t pid = hi[par];
+        hv[elem] = pv;
+        hi[elem] = (uint16_t)pid;
+        st[pid] = (uint16_t)(elem + 2);
+        elem = par;
+    }
+    hv[elem] = val;
+    hi[elem] = (uint16_t)id;
+    st[id] = (uint16_t)(elem + 2);
+}
+__device__ __forceinline__ void tlds_sink(double* hv, uint16_t* hi, uint16_t* st, int32_t size, int32_t head,
+                                          double val, int32_t id) {
+    for (;;) {
+        const int32_t l = 2 * head + 1, r = 2 * head + 2;
+        if (l >= size) break;
+        const double dl = hv[l];
+        const double dr = r != size ? hv[r] : 0.0;
+        const int32_t il = hi[l], ir = r != size ? hi[r] : 0;
+        int32_t c = l, cid = il;
+        double dc = dl;
+        if (r != size && !(dl >= dr)) { c = r; dc = dr; cid = ir; }
+        if (!(val < dc)) break;
+        hv[head] = dc;
+        hi[head] = (uint16_t)cid;
+        st[cid] = (uint16_t)(head + 2);
+        head = c;
+    }
+    hv[head] = val;
+    hi[head] = (uint16_t)id;
+    st[id] = (uint16_t)(head + 2);
+}
+__device__ __forceinline__ double bcast_d(double v, int lane) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__global__ __launch_bounds__(64) void k_sssp_tie_lds(
+    int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
+    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf_n) {
+    extern __shared__ __align__(16) char tsm[];
+    uint16_t* st = (uint16_t*)tsm;
+    double* hv = (double*)(tsm + (((size_t)2 * V + 15) & ~(size_t)15));
+    uint16_t* hi = (uint16_t*)(hv + hc);
+    const int lane = (int)threadIdx.x;
+    for (int32_t slot = (int32_t)blockIdx.x; slot < n; slot += (int32_t)gridDim.x) {
+        int32_t* par = fpar + (size_t)slot * V;
+        for (int32_t v = lane; v < V; v += 64) {
+            st[v] = 0;
+            par[v] = -1;
+        }
+        __syncthreads();
+        const int32_t src = attached[rows[slot]];
+        int32_t size = 1;
+        if (lane == 0) {
+            hv[0] = 0.0;
+            hi[0] = (uint16_t)src;
+            st[src] = 2;
+        }
+        int ovf = 0;
+        while (size > 0 && !ovf) {
+            // the pop (igraph_2wheap_max_index + delete_max), by lane 0
+            int32_t u0 = 0;
+            double md0 = 0.0;
+            if (lane == 0) {
+                u0 = hi[0];
+                md0 = -hv[0];
+                size--;
+                if (size > 0) tlds_sink(hv, hi, st, size, 0, hv[size], hi[size]);
+                st[u0] = 1;
+            }
+            const int32_t u = __builtin_amdgcn_readfirstlane(u0);
+            const double md = bcast_d(md0, 0);
+            size = __builtin_amdgcn_readfirstlane(size);
+            __syncthreads();
+            const int32_t kb = arc_off[u], ke = arc_off[u + 1];
+            for (int32_t c0 = kb; c0 < ke && !ovf; c0 += 64) {
+                const int32_t k = c0 + lane;
+                const bool valid = k < ke;
+                int32_t x = -1, rin = 0;
+                double alt = 0.0, cur = 0.0;
+                uint32_t sx = 1;
+                if (valid) {
+                    x = arc_dst[k];
+                    alt = md + arc_w[k];
+                    rin = arc_rin[k];
+                    sx = st[x];
+                    if (sx >= 2) cur = -hv[sx - 2];
+                }
+                const int32_t cnt = ke - c0 < 64 ? ke - c0 : 64;
+                bool dup = false;   // an earlier arc of this chunk to the same vertex
+                for (int32_t i = 0; i < cnt; i++) dup |= i < lane && __builtin_amdgcn_readlane(x, i) == x;
+                uint64_t m = __ballot(valid && (dup || sx == 0 || (sx >= 2 && alt < cur)));
+                if (lane == 0) {
+                    while (m) {
+                        const int j = __builtin_ctzll(m);
+                        m &= m - 1;
+                        const int32_t xj = __builtin_amdgcn_readlane(x, j);
+                        const double aj = bcast_d(alt, j);
+                        const int32_t rj = __builtin_amdgcn_readlane(rin, j);
+                        const uint32_t sj = st[xj];
+                        if (sj == 0) {   // the first finite distance: push
+                            if (size >= hc) { ovf = 1; break; }
+                            par[xj] = rj;
+                            tlds_shift_up(hv, hi, st, size, -aj, xj);
+                            size++;
+                        } else if (sj >= 2) {   // strictly shorter: igraph_2wheap_modify
+                            const int32_t pos = (int32_t)sj - 2;
+                            if (aj < -hv[pos]) {
+                                par[xj] = rj;
+                                tlds_sink(hv, hi, st, size, pos, -aj, xj);
+                                tlds_shift_up(hv, hi, st, pos, hv[pos], hi[pos]);
+                            }
+                        }
+                    }
+                }
+                size = __builtin_amdgcn_readfirstlane(size);
+                ovf = __builtin_amdgcn_readfirstlane(ovf);
+                __syncthreads();
+            }
+        }
+        if (ovf && lane == 0) atomicAdd(ovf_n, 1);
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ direct
 // _topology_lookupDirectPath (topology.c:1877-1927) for every attached pair;
 // igraph_get_eid through the (neighbour, eid)-sorted lists (lowest parallel eid)
@@ -1492,32 +1641,79 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     SHD_HIP(hipMemcpyAsync(&n, pc->d_stats + 6, sizeof(n), hipMemcpyDeviceToHost, s));
     SHD_HIP(hipStreamSynchronize(s));
     pc->info.n_tie_rows = (int32_t)n;
+    pc->info.n_tie_rows_global = 0;
     if (n <= 0) return SHD_OK;
     if (n > T) return SHD_ERANGE;
-    // 24 B of lane scratch + 4 B of parents per vertex and row; <= 4 GiB a chunk
-    // (every row of a 10 k-vertex graph at once)
+    // k_sssp_tie_lds where a row's state fits LDS beside a heap of >= 256
+    // entries (as many blocks per CU as fit, up to 4); else, and for its rows
+    // whose heap outgrows that, k_sssp_tie_parents (SHD_PC_TIE_GLOBAL: always)
+    const size_t st_bytes = ((size_t)2 * V + 15) & ~(size_t)15;
+    int hc = 0, bpc = 0;
+    if (V <= 65533 && !getenv("SHD_PC_TIE_GLOBAL"))
+        for (int b = 4; b >= 1 && !hc; b--) {
+            const size_t budget = (kLdsMax / b) & ~(size_t)15;
+            if (budget <= st_bytes) continue;
+            const size_t h = std::min<size_t>({(budget - st_bytes) / 10, (size_t)V, (size_t)65533});
+            if (h >= 256) { hc = (int)h; bpc = b; }
+        }
+    const size_t tl_lds = st_bytes + (size_t)hc * 10;
+    // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
+    // scratch per vertex and row; <= 4 GiB a chunk (every row of a 10 k-vertex
+    // graph at once)
     const size_t per_row = (size_t)V * 28;
     int64_t chunk = std::max<int64_t>(kTieLanes, (int64_t)(((size_t)4 << 30) / per_row) / kTieLanes * kTieLanes);
     chunk = std::min<int64_t>(chunk, (n + kTieLanes - 1) / kTieLanes * kTieLanes);
     const size_t need_s = (size_t)chunk * V * 24, need_p = (size_t)chunk * V * 4;
-    if (!pc->d_tie_scratch || pc->tie_scratch_bytes < need_s + need_p) {
+    const size_t need = (hc ? 0 : need_s) + need_p;
+    if (!pc->d_tie_scratch || pc->tie_scratch_bytes < need) {
         if (pc->d_tie_scratch) (void)hipFree(pc->d_tie_scratch);
         pc->d_tie_scratch = nullptr;
         pc->tie_scratch_bytes = 0;
-        SHD_HIP(hipMalloc(&pc->d_tie_scratch, need_s + need_p));
-        pc->tie_scratch_bytes = need_s + need_p;
+        SHD_HIP(hipMalloc(&pc->d_tie_scratch, need));
+        pc->tie_scratch_bytes = need;
+    }
+    int32_t* d_ovf = nullptr;
+    if (hc) {
+        SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t)));
+        SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_tie_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)tl_lds));
     }
     char* scr = (char*)pc->d_tie_scratch;
-    int32_t* fpar = (int32_t*)(scr + need_s);
+    int32_t* fpar = (int32_t*)(scr + (hc ? 0 : need_s));
     bool lo = false;
     const size_t lds_rows = lds_bytes_for(V), lds = lds_launch_bytes(pc, &lo);
     for (int64_t c0 = 0; c0 < n; c0 += chunk) {
         const int32_t cn = (int32_t)std::min<int64_t>(chunk, n - c0);
         const int32_t* rows = pc->d_tie_rows + c0;
-        hipLaunchKernelGGL(k_sssp_tie_parents, dim3((cn + kTieLanes - 1) / kTieLanes), dim3(kTieLanes), 0, s, V, cn,
-                           rows, pc->d_attached,
-                           pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar, scr);
-        SHD_HIP(hipGetLastError());
+        int32_t ovf = hc ? 0 : 1;
+        if (hc) {
+            SHD_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), s));
+            const int grid = std::max(1, std::min(cn, ncu * bpc));
+            hipLaunchKernelGGL(k_sssp_tie_lds, dim3(grid), dim3(64), tl_lds, s, V, cn, rows, pc->d_attached,
+                               pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar, (int32_t)hc, d_ovf);
+            SHD_HIP(hipGetLastError());
+            SHD_HIP(hipMemcpyAsync(&ovf, d_ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            SHD_HIP(hipStreamSynchronize(s));
+            pc->info.n_tie_rows_global += ovf;
+        }
+        if (ovf) {   // (a heap past hc: the chunk again through lane heaps in global scratch)
+            if (hc && pc->tie_scratch_bytes < need_s + need_p) {
+                void* q = nullptr;
+                SHD_HIP(hipMalloc(&q, need_s + need_p));
+                SHD_HIP(hipMemcpyAsync((char*)q + need_s, fpar, need_p, hipMemcpyDeviceToDevice, s));
+                SHD_HIP(hipStreamSynchronize(s));
+                (void)hipFree(pc->d_tie_scratch);
+                pc->d_tie_scratch = q;
+                pc->tie_scratch_bytes = need_s + need_p;
+                scr = (char*)q;
+                fpar = (int32_t*)(scr + need_s);
+                hc = 0;   // (the later chunks go straight to the lane heaps)
+            }
+            hipLaunchKernelGGL(k_sssp_tie_parents, dim3((cn + kTieLanes - 1) / kTieLanes), dim3(kTieLanes), 0, s, V,
+                               cn, rows, pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin,
+                               fpar, scr);
+            SHD_HIP(hipGetLastError());
+        }
         if (lds_rows <= kLdsMax && V <= 2048) {
             const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(8, kLdsMax / lds));
             const int grid = std::max(1, std::min(cn, ncu * per_cu));
@@ -1545,6 +1741,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         }
         SHD_HIP(hipGetLastError());
     }
+    if (d_ovf) (void)hipFree(d_ovf);
     return SHD_OK;
 }
 

@@ -96,7 +96,7 @@ class PcInfo(C.Structure):
         ("n_unroutable", C.c_int32), ("min_latency_ms", C.c_double),
         ("build_ms_device", C.c_double), ("build_ms_sssp", C.c_double),
         ("build_ms_props", C.c_double), ("build_ms_direct", C.c_double),
-        ("n_tie_rows", C.c_int32),
+        ("n_tie_rows", C.c_int32), ("n_tie_rows_global", C.c_int32),
     ]
 
 

@@ -147,6 +147,36 @@ def test_tie_rows_bit_exact(name):
     assert same_bits(lat[rows], olat) and same_bits(rel[rows], orel)
 
 
+@pytest.mark.parametrize("name", ["grid30", "geo_int_2000_vloss"])
+def test_tie_rows_bit_exact_on_the_lane_heap_kernel(name, monkeypatch):
+    # round 6 moved tied rows to k_sssp_tie_lds (one row per wave, its heap in
+    # LDS); SHD_PC_TIE_GLOBAL keeps k_sssp_tie_parents (lane heaps in global
+    # scratch), which the LDS kernel still falls back to: both stay exact
+    monkeypatch.setenv("SHD_PC_TIE_GLOBAL", "1")
+    test_tie_rows_bit_exact(name)
+
+
+def test_tie_rows_heap_past_lds_falls_back_bit_exact():
+    # two hubs joined to every leaf at one whole millisecond: from a leaf, the
+    # other leaves tie (both hubs are exact predecessors) and the heap holds
+    # every leaf at once -- past the LDS heap at 5000 vertices, so each row is
+    # run again through the lane heaps in global scratch; still the oracle's
+    V = 5000
+    leaves = np.arange(2, V, dtype=np.int64)
+    src = np.concatenate([np.zeros(V - 2, np.int64), np.ones(V - 2, np.int64), [0]])
+    dst = np.concatenate([leaves, leaves, [1]])
+    rng = np.random.default_rng(3)
+    g = S.GraphArrays(V, src, dst, np.full(len(src), 1.0), rng.uniform(0.0, 0.01, len(src)))
+    att = np.arange(V, dtype=np.int32)
+    pc = PathCache(g, att)
+    info = pc.info()
+    assert info.n_tie_rows > 0 and info.n_tie_rows_global > 0, (info.n_tie_rows, info.n_tie_rows_global)
+    lat, rel = pc.rows()
+    rows = [0, 1, 2, 3, 777, V - 1]
+    olat, orel, _ = oracle_rows(g, att, rows)
+    assert same_bits(lat[rows], olat) and same_bits(rel[rows], orel)
+
+
 def test_tie_rows_global_scratch_path_and_subset():
     # V above the LDS capacity: both passes on the global-memory row kernel
     V = 12500
