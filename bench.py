@@ -591,7 +591,7 @@ def tcp_main(args):
         "wall_inclusive": {"value": round(events / wall, 1), "unit": "events/s",
                            "device_share": round(dev_s / wall, 3),
                            "host_ms_last_run": {k: round(v, 1) for k, v in r.get("host_ms", {}).items()}},
-        "first_touch": r.get("first_touch"),
+        "first_touch": r.get("first_touch"), "first_touch_reruns": r.get("first_touch_reruns"),
         "rounds": r["rounds"], "events_per_run": r["events"], "deliveries_per_run": r["deliveries"],
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": 8000.0, "unit": "GB/s",
                      "frac": round(achieved / 8000.0, 6), "traffic": None, "kernel": "k_tcp_round",

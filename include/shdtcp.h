@@ -131,7 +131,11 @@ typedef struct shd_tcp_result {
      * shd_tracker_node_lines (shdgpu.h) makes the [node] lines of a host. */
     uint64_t* node_counters;
     uint32_t* n_heartbeats;
-    uint32_t node_k, _pad2;
+    uint32_t node_k;
+    uint32_t first_touch_reruns;      /* path_cache mode: runs this call made again from the start,
+                                         each with one more round's first touches ranked in
+                                         serial order before it runs (a contradicted device
+                                         choice that changed a value) */
     uint64_t max_round_deliveries;    /* the most deliveries one round's mailbox took */
     uint64_t max_round_overflow;      /* ... and the most of them in its shared overflow range */
     double setup_ms, results_ms, teardown_ms;   /* the call's host wall time around the rounds:

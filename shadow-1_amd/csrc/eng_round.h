@@ -179,7 +179,12 @@ __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
 
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
 // window, run events < we
-template <bool RX = false>   // RX: the fused peer-to-peer round's received window events (s_rx)
+// RX: the fused peer-to-peer round's received window events (s_rx).  LEAN
+// (round 6): the model uses none of the optional features (ParamsT::feat == 0,
+// the bench's models): the context's feature word is the constant 0, so the
+// trace, status, heartbeat, path-counter and datagram-application paths fold
+// away (registers and issue the PHOLD path does not need)
+template <bool RX = false, bool LEAN = false>
 __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, uint64_t ws, uint64_t we, int parity,
                                            uint64_t& next_out, uint64_t& nev_out, uint64_t& npkt_out,
                                            uint32_t& err_out, uint32_t xwi = 0) {
@@ -249,6 +254,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #endif
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
     hot_load(P, c);
+    if (LEAN) c.k.feat = 0;
     PendDel pd;
     send_pool_reset(c); c.att = 0; c.cls = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0; c.pf_lim = 0;
@@ -814,6 +820,7 @@ __device__ __forceinline__ void tl_publish(DevSummary* s, const TlPart& f, uint3
 // round i of a ticketless batch: shares of round i go to parts[i & 1]
 // (argument order: what the first memory round trip needs comes first, so
 // that one scalar load batch brings all of it)
+template <bool LEAN>
 __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, DevSummary* __restrict__ prev,
                                                       const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
                                                       const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
@@ -880,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tl(uint64_t window, int i, Dev
     if (we > stop || we < ws) we = stop;
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body(P, in, ws, we, parity, next, nev, npkt, err);
+    round_body<false, LEAN>(P, in, ws, we, parity, next, nev, npkt, err);
     TIM(4);
     const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));   // hosts that executed an event
     for (int off = 32; off > 0; off >>= 1) {
@@ -1496,6 +1503,7 @@ constexpr bool kPsPf = true;
 constexpr bool kPsPf = false;
 #endif
 
+template <bool LEAN>
 __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, DevSummary* __restrict__ ring,
                                                       const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
                                                       const DParams* __restrict__ Pr, uint64_t ticks) {
@@ -1521,6 +1529,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
     HostCtx c;
     hot_load(P0, c);
+    if (LEAN) c.k.feat = 0;
     if (has) {
         load_ctx(P0, c, l, P0.hs[l], P0.host_att[P0.h0 + l], P0.self_thr[P0.h0 + l]);
     } else {
@@ -1839,6 +1848,7 @@ __device__ __forceinline__ void sp_passes(const DParams& P, HostCtx& c, const Ps
     }
 }
 
+template <bool LEAN>
 __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, DevSummary* __restrict__ ring,
                                                       const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
                                                       const DParams* __restrict__ Pr, uint64_t ticks, uint32_t sph) {
@@ -1863,6 +1873,7 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
     HostCtx c;
     hot_load(P0, c);
+    if (LEAN) c.k.feat = 0;
     c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
     c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
     uint64_t ws = ring[0].next_time;

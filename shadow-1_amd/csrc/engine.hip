@@ -58,6 +58,11 @@ namespace {
 // every round protected, a failing peer mapping) exist only in the test build
 // (make testhooks -> libshdgpu_th.so, -DSHD_TEST_HOOKS), which the tests that
 // need them load in a child process; the product library ignores these names.
+#ifdef SHD_NO_LEAN   // A/B build: the general instantiations for every model
+static constexpr bool kNoLean = true;
+#else
+static constexpr bool kNoLean = false;
+#endif
 #ifdef SHD_TEST_HOOKS
 static bool test_hook(const char* name) { return getenv(name) != nullptr; }
 #else
@@ -640,8 +645,10 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         const int grid = (e->nloc + P.hpw - 1) / P.hpw;
         int ncu = 0, per_cu = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_round_ps), kBlock,
-                                                         0) != hipSuccess)
+        const bool lean = P.feat == 0 && !kNoLean;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lean ? reinterpret_cast<const void*>(&k_round_ps<true>)
+                                                                       : reinterpret_cast<const void*>(&k_round_ps<false>),
+                                                         kBlock, 0) != hipSuccess)
             per_cu = 0;
         (void)hipGetLastError();
         // (blocks of one wave: up to two per CU, below what LDS and registers admit)
@@ -654,7 +661,9 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         if (!e->ps_ok && e->h0 == 0 && e->nloc == H && ncu > 0) {
             // too many hosts for a resident wave each: blocks of sph hosts, about two per CU
             int per_cu_sp = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_sp, reinterpret_cast<const void*>(&k_round_sp),
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_sp,
+                                                             lean ? reinterpret_cast<const void*>(&k_round_sp<true>)
+                                                                  : reinterpret_cast<const void*>(&k_round_sp<false>),
                                                              kBlock, 0) != hipSuccess)
                 per_cu_sp = 0;
             (void)hipGetLastError();
@@ -989,9 +998,15 @@ static int enqueue_batch_tl(shd_eng* e) {
     constexpr int B = shd_eng::kBatch;
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     for (int i = 0; i < B; i++) {
-        hipLaunchKernelGGL(k_round_tl, dim3(grid), dim3(kBlock), 0, e->stream, e->window, i, &e->d_ring[i],
-                           (const DevCtl*)e->d_ctl, e->d_tpart, (const DParams*)(e->d_pr + i + 1), &e->d_ring[i + 2],
-                           round_args(e->P));
+        // (the lean instantiation for models with no optional feature: ParamsT::feat == 0)
+        if (e->P.feat == 0 && !kNoLean)
+            hipLaunchKernelGGL(k_round_tl<true>, dim3(grid), dim3(kBlock), 0, e->stream, e->window, i, &e->d_ring[i],
+                               (const DevCtl*)e->d_ctl, e->d_tpart, (const DParams*)(e->d_pr + i + 1),
+                               &e->d_ring[i + 2], round_args(e->P));
+        else
+            hipLaunchKernelGGL(k_round_tl<false>, dim3(grid), dim3(kBlock), 0, e->stream, e->window, i, &e->d_ring[i],
+                               (const DevCtl*)e->d_ctl, e->d_tpart, (const DParams*)(e->d_pr + i + 1),
+                               &e->d_ring[i + 2], round_args(e->P));
     }
     hipLaunchKernelGGL(k_fold_tl, dim3(1), dim3(64), 0, e->stream, (const TlPart*)e->d_tpart, (uint32_t)grid, B - 1,
                        &e->d_ring[B], e->d_halt);
@@ -1040,13 +1055,16 @@ static bool sp_dense_batch(uint64_t rounds, uint64_t active, uint64_t pkt, uint6
 
 static int launch_batch_ps(shd_eng* e, int nb) {
     const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
+    const bool lean = e->P.feat == 0 && !kNoLean;   // (no optional feature: the lean instantiations)
     if (e->sp_ok) {
-        hipLaunchKernelGGL(k_round_sp, dim3(e->sp_grid), dim3(kBlock), 0, e->stream, e->window, nb, e->d_ring,
-                           (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr, ticks, e->sp_hosts);
+        hipLaunchKernelGGL(lean ? k_round_sp<true> : k_round_sp<false>, dim3(e->sp_grid), dim3(kBlock), 0, e->stream,
+                           e->window, nb, e->d_ring, (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr,
+                           ticks, e->sp_hosts);
     } else {
         const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
-        hipLaunchKernelGGL(k_round_ps, dim3(grid), dim3(kBlock), 0, e->stream, e->window, nb, e->d_ring,
-                           (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr, ticks);
+        hipLaunchKernelGGL(lean ? k_round_ps<true> : k_round_ps<false>, dim3(grid), dim3(kBlock), 0, e->stream,
+                           e->window, nb, e->d_ring, (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr,
+                           ticks);
     }
     SHD_HIP(hipGetLastError());
     e->ps_epoch += (uint32_t)nb;

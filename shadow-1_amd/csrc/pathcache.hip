@@ -1049,9 +1049,11 @@ __device__ __forceinline__ int32_t tie_sink(TieLane& h, int32_t size, int32_t he
 __global__ __launch_bounds__(kTieLanes) void k_sssp_tie_parents(
     int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
-    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, char* __restrict__ scratch) {
-    const int32_t slot = (int32_t)blockIdx.x * kTieLanes + (int32_t)threadIdx.x;
-    if (slot >= n) return;
+    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, char* __restrict__ scratch,
+    const int32_t* __restrict__ slots) {   // slots: the chunk's slots to run (null: [0, n))
+    const int32_t i = (int32_t)blockIdx.x * kTieLanes + (int32_t)threadIdx.x;
+    if (i >= n) return;
+    const int32_t slot = slots ? slots[i] : i;
     char* wbase = scratch + (size_t)blockIdx.x * kTieLanes * (size_t)V * 24;
     TieLane h;
     h.dist = (double*)wbase + threadIdx.x;
@@ -1162,7 +1164,7 @@ __device__ __forceinline__ double bcast_d(double v, int lane) {
 __global__ __launch_bounds__(64) void k_sssp_tie_lds(
     int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
-    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf_n) {
+    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf) {
     extern __shared__ __align__(16) char tsm[];
     uint16_t* st = (uint16_t*)tsm;
     double* hv = (double*)(tsm + (((size_t)2 * V + 15) & ~(size_t)15));
@@ -1182,8 +1184,8 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
             hi[0] = (uint16_t)src;
             st[src] = 2;
         }
-        int ovf = 0;
-        while (size > 0 && !ovf) {
+        int ovfl = 0;
+        while (size > 0 && !ovfl) {
             // the pop (igraph_2wheap_max_index + delete_max), by lane 0
             int32_t u0 = 0;
             double md0 = 0.0;
@@ -1199,7 +1201,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
             size = __builtin_amdgcn_readfirstlane(size);
             __syncthreads();
             const int32_t kb = arc_off[u], ke = arc_off[u + 1];
-            for (int32_t c0 = kb; c0 < ke && !ovf; c0 += 64) {
+            for (int32_t c0 = kb; c0 < ke && !ovfl; c0 += 64) {
                 const int32_t k = c0 + lane;
                 const bool valid = k < ke;
                 int32_t x = -1, rin = 0;
@@ -1225,7 +1227,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                         const int32_t rj = __builtin_amdgcn_readlane(rin, j);
                         const uint32_t sj = st[xj];
                         if (sj == 0) {   // the first finite distance: push
-                            if (size >= hc) { ovf = 1; break; }
+                            if (size >= hc) { ovfl = 1; break; }
                             par[xj] = rj;
                             tlds_shift_up(hv, hi, st, size, -aj, xj);
                             size++;
@@ -1240,11 +1242,11 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                     }
                 }
                 size = __builtin_amdgcn_readfirstlane(size);
-                ovf = __builtin_amdgcn_readfirstlane(ovf);
+                ovfl = __builtin_amdgcn_readfirstlane(ovfl);
                 __syncthreads();
             }
         }
-        if (ovf && lane == 0) atomicAdd(ovf_n, 1);
+        if (ovfl && lane == 0) ovf[1 + atomicAdd(ovf, 1)] = slot;
         __syncthreads();
     }
 }
@@ -1342,7 +1344,7 @@ static void pc_free_device(shd_pc* pc) {
                     pc->d_rin_w, pc->d_rin_r, pc->d_inc_off, pc->d_inc_eid, pc->d_nbr_off, pc->d_nbr_v, pc->d_nbr_eid,
                     pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row,
                     pc->d_dir, pc->d_self, pc->d_adj,
-                    pc->d_scratch, pc->d_stats, pc->d_tie_rows, pc->d_tie_scratch};
+                    pc->d_scratch, pc->d_stats, pc->d_tie_rows, pc->d_tie_scratch, pc->d_tie_lane};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
 }
@@ -1663,8 +1665,8 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     const size_t per_row = (size_t)V * 28;
     int64_t chunk = std::max<int64_t>(kTieLanes, (int64_t)(((size_t)4 << 30) / per_row) / kTieLanes * kTieLanes);
     chunk = std::min<int64_t>(chunk, (n + kTieLanes - 1) / kTieLanes * kTieLanes);
-    const size_t need_s = (size_t)chunk * V * 24, need_p = (size_t)chunk * V * 4;
-    const size_t need = (hc ? 0 : need_s) + need_p;
+    const size_t need_p = (size_t)chunk * V * 4;
+    const size_t need = need_p;
     if (!pc->d_tie_scratch || pc->tie_scratch_bytes < need) {
         if (pc->d_tie_scratch) (void)hipFree(pc->d_tie_scratch);
         pc->d_tie_scratch = nullptr;
@@ -1673,45 +1675,40 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         pc->tie_scratch_bytes = need;
     }
     int32_t* d_ovf = nullptr;
-    if (hc) {
-        SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t)));
+    if (hc) {   // [0]: the count, then the slots of the rows whose heap outgrew hc
+        SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t) * (1 + (size_t)chunk)));
         SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_tie_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)tl_lds));
     }
-    char* scr = (char*)pc->d_tie_scratch;
-    int32_t* fpar = (int32_t*)(scr + (hc ? 0 : need_s));
+    int32_t* fpar = (int32_t*)pc->d_tie_scratch;
     bool lo = false;
     const size_t lds_rows = lds_bytes_for(V), lds = lds_launch_bytes(pc, &lo);
     for (int64_t c0 = 0; c0 < n; c0 += chunk) {
         const int32_t cn = (int32_t)std::min<int64_t>(chunk, n - c0);
         const int32_t* rows = pc->d_tie_rows + c0;
-        int32_t ovf = hc ? 0 : 1;
+        int32_t nov = hc ? 0 : cn;   // rows for the lane heaps (all of them without k_sssp_tie_lds)
         if (hc) {
             SHD_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), s));
             const int grid = std::max(1, std::min(cn, ncu * bpc));
             hipLaunchKernelGGL(k_sssp_tie_lds, dim3(grid), dim3(64), tl_lds, s, V, cn, rows, pc->d_attached,
                                pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar, (int32_t)hc, d_ovf);
             SHD_HIP(hipGetLastError());
-            SHD_HIP(hipMemcpyAsync(&ovf, d_ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            SHD_HIP(hipMemcpyAsync(&nov, d_ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
             SHD_HIP(hipStreamSynchronize(s));
-            pc->info.n_tie_rows_global += ovf;
+            pc->info.n_tie_rows_global += nov;
         }
-        if (ovf) {   // (a heap past hc: the chunk again through lane heaps in global scratch)
-            if (hc && pc->tie_scratch_bytes < need_s + need_p) {
-                void* q = nullptr;
-                SHD_HIP(hipMalloc(&q, need_s + need_p));
-                SHD_HIP(hipMemcpyAsync((char*)q + need_s, fpar, need_p, hipMemcpyDeviceToDevice, s));
-                SHD_HIP(hipStreamSynchronize(s));
-                (void)hipFree(pc->d_tie_scratch);
-                pc->d_tie_scratch = q;
-                pc->tie_scratch_bytes = need_s + need_p;
-                scr = (char*)q;
-                fpar = (int32_t*)(scr + need_s);
-                hc = 0;   // (the later chunks go straight to the lane heaps)
+        if (nov) {   // (a heap past hc: those rows again through lane heaps in global scratch)
+            const size_t ns = (size_t)((nov + kTieLanes - 1) / kTieLanes) * kTieLanes * V * 24;
+            if (!pc->d_tie_lane || pc->tie_lane_bytes < ns) {
+                if (pc->d_tie_lane) (void)hipFree(pc->d_tie_lane);
+                pc->d_tie_lane = nullptr;
+                pc->tie_lane_bytes = 0;
+                SHD_HIP(hipMalloc(&pc->d_tie_lane, ns));
+                pc->tie_lane_bytes = ns;
             }
-            hipLaunchKernelGGL(k_sssp_tie_parents, dim3((cn + kTieLanes - 1) / kTieLanes), dim3(kTieLanes), 0, s, V,
-                               cn, rows, pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin,
-                               fpar, scr);
+            hipLaunchKernelGGL(k_sssp_tie_parents, dim3((nov + kTieLanes - 1) / kTieLanes), dim3(kTieLanes), 0, s, V,
+                               nov, rows, pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin,
+                               fpar, (char*)pc->d_tie_lane, hc ? (const int32_t*)(d_ovf + 1) : nullptr);
             SHD_HIP(hipGetLastError());
         }
         if (lds_rows <= kLdsMax && V <= 2048) {

@@ -65,8 +65,10 @@ struct shd_pc {
     size_t scratch_bytes = 0;
     bool lds_off_ok = false;            // the row kernel may keep the CSR's arc offsets in LDS
     int32_t* d_tie_rows = nullptr;      // [T] rows with equal-cost predecessors (first pass)
-    void* d_tie_scratch = nullptr;      // k_sssp_tie_parents: lane heaps + parents
+    void* d_tie_scratch = nullptr;      // tied rows' parents (k_sssp_tie_lds / k_sssp_tie_parents)
     size_t tie_scratch_bytes = 0;
+    void* d_tie_lane = nullptr;         // k_sssp_tie_parents' lane heaps (rows whose heap outgrew LDS)
+    size_t tie_lane_bytes = 0;
     int64_t* d_stats = nullptr;         // ties, max hops, max iters, unroutable, lat mismatch, minlat bits, tie rows
     bool built = false;
     shd_pc_info info{};

@@ -256,10 +256,11 @@ struct CqEnt { uint64_t ts; uint32_t len; int32_t pkt; };
 struct TCtl {
     uint64_t wend;       // the running round's window end
     uint64_t rounds;     // rounds started; round k reads mailbox k & 1 and writes the other
-    uint32_t halted, _pad;
+    uint32_t halted, sched_i;   // sched_i: the next entry of the first-touch schedule (Glob::sched_*)
     uint64_t max_mail;   // the most deliveries one round's mailbox took (shd_tcp_result)
     uint64_t max_ovf;    // ... and the most of them in its shared overflow range
-    uint32_t ft_bad, _pad2;   // path_cache mode: a round's first-touch choice the serial order contradicts
+    uint32_t ft_bad, ft_nr0;   // path_cache mode: a round's first-touch choice the serial order contradicts;
+                               // next_rank before that round's replay
     uint64_t tmin;       // a group's round: this engine's earliest pending event (k_tcp_window, local)
     uint32_t xerr, _pad3;   // a group's exchange failed: SHD_TCP_ERR_MAILBOX / _INTERNAL bits
 };
@@ -319,7 +320,13 @@ struct Glob {
     uint32_t* nft;
     int32_t* ftord;         // [ft_cap] the log in serial order (scratch of k_tcp_window)
     uint32_t ft_cap; int32_t pT;
-    uint32_t pcm, pc_complete, pc_prefer_direct, _pad6;
+    uint32_t pcm, pc_complete, pc_prefer_direct, sched_n;
+    // the first-touch schedule (one engine): entry i ranks sched_v[sched_off[i],
+    // sched_off[i + 1]) (v: a row, ~v: a self path) in that order when round
+    // sched_round[i] opens, before it runs (tcp_run_impl's reruns)
+    const uint32_t* sched_round;
+    const uint32_t* sched_off;
+    const int32_t* sched_v;
     // the datagram processes (shd_tcp_model.proc_app): their applications
     // {send, dest, n_start, per_read}, each host's SHD_DEST_PEER host, the
     // SHD_DEST_WEIGHTED rows ([n_classes][H] cumulative) and class per host
@@ -2538,11 +2545,27 @@ __global__ void k_tcp_window(Glob g, int local) {
     if (g.pcm) {
         const uint32_t n = *g.nft;   // the last round's log (uniform)
         if (n) {
+            const int32_t nr0 = *g.next_rank;
             const bool bad = n > g.ft_cap || ft_replay(g, n);
             if (bad) {
-                if (threadIdx.x == 0) { ctl->ft_bad = 1; ctl->halted = 1; }
+                if (threadIdx.x == 0) { ctl->ft_bad = 1; ctl->ft_nr0 = (uint32_t)nr0; ctl->halted = 1; }
                 return;
             }
+        }
+        // the schedule's entry for the round this window opens: its first
+        // touches ranked, in the serial order an earlier run of the same
+        // model found for them, before any lane queries (one engine)
+        if (!local && threadIdx.x == 0 && ctl->sched_i < g.sched_n &&
+            g.sched_round[ctl->sched_i] == (uint32_t)(ctl->rounds + 1)) {
+            const uint32_t i = ctl->sched_i;
+            int32_t nr = *g.next_rank;
+            for (uint32_t j = g.sched_off[i]; j < g.sched_off[i + 1]; j++) {
+                const int32_t v = g.sched_v[j];
+                if (v >= 0) g.rank[v] = nr++;
+                else g.srank[~v] = nr++;
+            }
+            *g.next_rank = nr;
+            ctl->sched_i = i + 1;
         }
     }
     __shared__ uint32_t s_mail;
@@ -2995,7 +3018,20 @@ extern "C" void shd_tcp_keep_workspace(int32_t keep) {
 // shd_tcp_run on one engine (comm null) or on this engine's share of a group
 // (shd_tcp_run_group: hosts [h0, h0 + nloc), the round's window agreed over
 // the group, deliveries between engines exchanged after every round)
-static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, shd_tcp_result** out) {
+// one engine's first-touch schedule across the reruns of one shd_tcp_run call
+// (Glob::sched_*): a run whose round R contradicts a device choice that changes
+// a value stops there; the ranks that round's replay assigned, in serial order,
+// are added for round R and the model runs again from the start -- the rounds
+// before R are the same rounds, and in round R every such pair then has a
+// ranked endpoint at the round's start, which is the serial loop's value
+constexpr size_t kFtReruns = 256;   // schedule entries (reruns) one call makes at most
+struct TcpSched {
+    std::vector<uint32_t> round, off{0};
+    std::vector<int32_t> v;
+    bool extended = false;
+};
+static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, shd_tcp_result** out,
+                        TcpSched* sch = nullptr) {
     const auto t_call = std::chrono::steady_clock::now();
     auto t_results = t_call;
     shd_pc* pc = m ? m->path_cache : nullptr;
@@ -3139,6 +3175,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     uint64_t rounds = 0;
     std::vector<DHost> hout(nloc);
     uint32_t* d_ipall = nullptr; uint64_t* d_bwu = nullptr; uint64_t* d_bwd = nullptr;
+    uint32_t* d_sched = nullptr;   // the first-touch schedule (TcpSched), when it has entries
     char* d_xrecv = nullptr; uint64_t* d_pmine = nullptr; uint64_t* d_pall = nullptr; uint32_t* d_xcnt = nullptr;
     char* d_gmine = nullptr; char* d_gall = nullptr;
     constexpr size_t kGatherMax = 1024;   // bytes one rank contributes to a control all-gather (<= 64 engines)
@@ -3236,6 +3273,17 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         HCHECK(ws_alloc(ws, kWsFtord, &g.ftord, sizeof(int32_t) * (size_t)g.ft_cap));
         HCHECK(ws_alloc(ws, kWsNft, &g.nft, sizeof(uint32_t)));
         HCHECK(hipMemset(g.nft, 0, sizeof(uint32_t)));
+        if (sch && !sch->round.empty() && world == 1) {
+            const size_t nr = sch->round.size(), nv = sch->v.size();
+            HCHECK(hipMalloc((void**)&d_sched, sizeof(uint32_t) * (2 * nr + 1) + sizeof(int32_t) * (nv ? nv : 1)));
+            HCHECK(hipMemcpy(d_sched, sch->round.data(), sizeof(uint32_t) * nr, hipMemcpyHostToDevice));
+            HCHECK(hipMemcpy(d_sched + nr, sch->off.data(), sizeof(uint32_t) * (nr + 1), hipMemcpyHostToDevice));
+            if (nv) HCHECK(hipMemcpy(d_sched + 2 * nr + 1, sch->v.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice));
+            g.sched_round = d_sched;
+            g.sched_off = d_sched + nr;
+            g.sched_v = (const int32_t*)(d_sched + 2 * nr + 1);
+            g.sched_n = (uint32_t)nr;
+        }
     }
     HCHECK(ws_alloc(ws, kWsIpAll, &d_ipall, sizeof(uint32_t) * (size_t)H));
     HCHECK(hipMemcpy(d_ipall, m->host_ip, sizeof(uint32_t) * (size_t)H, hipMemcpyHostToDevice));
@@ -3543,6 +3591,29 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
         res->max_round_deliveries = cx.max_mail;
         res->max_round_overflow = cx.max_ovf;
         if (cx.ft_bad) res->error |= SHD_TCP_ERR_FIRST_TOUCH;
+        if (cx.ft_bad && sch && pc && world == 1 && sch->round.size() < kFtReruns) {
+            // the contradicted round's first touches in serial order: the
+            // ranks its replay assigned, [ft_nr0, next_rank)
+            std::vector<int32_t> rk(V), sk(V);
+            int32_t nr1 = 0;
+            HCHECK(hipMemcpy(rk.data(), g.rank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
+            HCHECK(hipMemcpy(sk.data(), g.srank, sizeof(int32_t) * (size_t)V, hipMemcpyDeviceToHost));
+            HCHECK(hipMemcpy(&nr1, g.next_rank, sizeof(int32_t), hipMemcpyDeviceToHost));
+            const int32_t nr0 = (int32_t)cx.ft_nr0;
+            std::vector<int32_t> ord(nr1 > nr0 ? nr1 - nr0 : 0, INT32_MIN);
+            for (int32_t v = 0; v < V; v++) {
+                if (rk[v] != kNoRank && rk[v] >= nr0 && rk[v] < nr1) ord[rk[v] - nr0] = v;
+                if (sk[v] != kNoRank && sk[v] >= nr0 && sk[v] < nr1) ord[sk[v] - nr0] = ~v;
+            }
+            bool ok = !ord.empty();
+            for (int32_t x : ord) ok &= x != INT32_MIN;
+            if (ok) {
+                sch->round.push_back((uint32_t)cx.rounds);
+                sch->v.insert(sch->v.end(), ord.begin(), ord.end());
+                sch->off.push_back((uint32_t)sch->v.size());
+                sch->extended = true;
+            }
+        }
         res->error |= cx.xerr;
         if (pc && !cx.ft_bad) {   // the cache's ranks as the serial run leaves them
             std::vector<int32_t> old_rank(pc->h_rank, pc->h_rank + V), old_self(pc->h_self_rank, pc->h_self_rank + V);
@@ -3627,6 +3698,7 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
     res->results_ms = ms_since(t_results);
 done:
     const auto t_free = std::chrono::steady_clock::now();
+    if (d_sched) (void)hipFree(d_sched);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -3641,7 +3713,22 @@ done:
 }
 
 extern "C" int shd_tcp_run(const shd_tcp_model* m, int32_t trace, shd_tcp_result** out) {
-    return tcp_run_impl(m, nullptr, trace, out);
+    // path_cache mode: a contradicted round makes the next run rank that
+    // round's first touches before it runs (TcpSched); every round before it
+    // runs again the same, so the reruns cost the rounds up to each
+    // contradiction.  Past kFtReruns the contradiction stands
+    // (SHD_TCP_ERR_FIRST_TOUCH: the caller's tables)
+    TcpSched sch;
+    for (uint32_t k = 0;; k++) {
+        sch.extended = false;
+        const int rc = tcp_run_impl(m, nullptr, trace, out, &sch);
+        if (rc || !sch.extended) {
+            if (!rc && *out) (*out)->first_touch_reruns = k;
+            return rc;
+        }
+        shd_tcp_result_free(*out);
+        *out = nullptr;
+    }
 }
 
 extern "C" int shd_tcp_run_group(const shd_tcp_model* m, shd_comm* comm, int32_t trace, shd_tcp_result** out) {

@@ -214,7 +214,7 @@ class TcpResult(C.Structure):
                 ("device_ms", C.c_double), ("error", C.c_uint32), ("deliveries", C.c_uint64),
                 ("queries", C.c_void_p), ("n_queries", C.c_uint64),
                 ("node_counters", P(C.c_uint64)), ("n_heartbeats", P(C.c_uint32)), ("node_k", C.c_uint32),
-                ("_pad2", C.c_uint32), ("max_round_deliveries", C.c_uint64), ("max_round_overflow", C.c_uint64),
+                ("first_touch_reruns", C.c_uint32), ("max_round_deliveries", C.c_uint64), ("max_round_overflow", C.c_uint64),
                 ("setup_ms", C.c_double), ("results_ms", C.c_double), ("teardown_ms", C.c_double),
                 ("first_host", C.c_int32), ("n_local_hosts", C.c_int32)]
 

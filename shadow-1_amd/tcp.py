@@ -235,6 +235,7 @@ def _run_once(model, ips, procs, peers, lat, rel, hvi, nbytes, trace, recv_buf, 
                    rounds=int(r.rounds), events=int(r.events), deliveries=int(r.deliveries),
                    max_round_deliveries=int(r.max_round_deliveries), max_round_overflow=int(r.max_round_overflow),
                    host_ms=dict(setup=float(r.setup_ms), results=float(r.results_ms), teardown=float(r.teardown_ms)),
+                   first_touch_reruns=int(r.first_touch_reruns),
                    device_ms=float(r.device_ms),
                    queries=np.frombuffer(C.string_at(r.queries, int(r.n_queries) * S.TCP_QUERY_DTYPE.itemsize),
                                          dtype=S.TCP_QUERY_DTYPE).copy() if r.n_queries else

@@ -29,8 +29,8 @@ FIX = json.load(open(os.path.join(HERE, "golden", "ref_tcp.json")))
 # same instant: host 2's lane chose vertex 7's row where the serial order
 # takes vertex 0's) and loopback_mixed (a self path ranked in the round in
 # which host 1 first queries (3, 0)) contradict only such choices;
-# test_tcp_gpu_device_first_touch_contradiction_falls_back keeps one that
-# does not
+# test_tcp_gpu_device_first_touch_contradiction_reruns_on_the_device keeps one that
+# does not (since round 6 one engine reruns it on the device, ranked)
 DEVICE_FALLS_BACK = set()
 
 
@@ -177,14 +177,15 @@ def test_tcp_gpu_wide_window_uses_the_mailbox_overflow(monkeypatch):
     assert r["max_round_overflow"] > 0, (r["max_round_deliveries"], r["max_round_overflow"])
 
 
-def test_tcp_gpu_device_first_touch_contradiction_falls_back():
+def test_tcp_gpu_device_first_touch_contradiction_reruns_on_the_device():
     """Two hosts each run a server and a client of the other's server, the
     clients' connects (topology_isRoutable: a first touch) 10 us apart in one
     window: each lane, seeing both vertices unranked, decides its own
     vertex's row; in serial order host 1's touch comes first, so host 0's
     query hits host 1's row.  The replay between rounds finds the
-    contradiction (SHD_TCP_ERR_FIRST_TOUCH) and the driver runs the model on
-    tables instead -- the result is the oracle's either way."""
+    contradiction; since round 6 shd_tcp_run runs the model again with that
+    round's first touches ranked in serial order before it runs (no table
+    fallback) -- the result is the oracle's."""
     import workloads as W
     g, m, ips, _, _, nb = W.tcp_echo_model(2, 30, end_s=6, nbytes=30000)
     if g.n_vertices and m.host_vertex[0] == m.host_vertex[1]:
@@ -193,7 +194,7 @@ def test_tcp_gpu_device_first_touch_contradiction_falls_back():
     peers = [-1, -1, 1, 0]
     r = TCPGPU.run(m, g, ips, procs, peers, nbytes=nb)
     o = O.tcp_run(m, g, ips, procs, peers, nbytes=nb)
-    assert r["first_touch"] == "tables"
+    assert r["first_touch"] == "device" and r["first_touch_reruns"] >= 1, (r["first_touch"], r["first_touch_reruns"])
     assert r["lines"] == TC.by_host(o["lines"])
     assert r["next_event_id"].tolist() == o["next_event_id"].tolist()
     assert r["rng_probe"].tolist() == o["rng_probe"].tolist()
