@@ -772,6 +772,7 @@ __device__ __forceinline__ void px_reset_counts(const DParams& P, int wi, uint32
         __hip_atomic_store(&c[j], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+template <bool LEAN>   // LEAN: ParamsT::feat == 0 (round_body)
 __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, DevSummary* __restrict__ prev,
                                                       const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
                                                       const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
@@ -886,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
     }
     uint64_t next, nev, npkt;
     uint32_t err;
-    round_body<true>(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((xpar + (uint64_t)i) & 1));
+    round_body<true, LEAN>(P, in, ws, we, parity, next, nev, npkt, err, (uint32_t)((xpar + (uint64_t)i) & 1));
     if (dm) ierr |= xrgn_store(P, s_def, sl, dm, parity ^ 1);
     err |= ierr;
     const uint32_t nact = (uint32_t)__popcll(__ballot(nev != 0));
@@ -917,6 +918,7 @@ __global__ __launch_bounds__(kBlock) void k_round_px(uint64_t window, int i, Dev
 // shares and put the headers, every block waits for every peer's header.
 // first: the batch's round 0 (the exchange before it is complete: its headers
 // read from xhdr, its regions taken by the last batch's k_xchg_px).
+template <bool LEAN>   // LEAN: ParamsT::feat == 0 (round_body)
 __global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, DevSummary* __restrict__ prev,
                                                        const DevCtl* __restrict__ ctl, TlPart* __restrict__ parts,
                                                        const DParams* __restrict__ Pp, DevSummary* __restrict__ init,
@@ -1026,6 +1028,7 @@ __global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, De
     R.inbox = buf_rsrc(P.inbox[parity] + (size_t)hb * P.inbox_cap, (uint64_t)nh * P.inbox_cap * sizeof(shd_event));
     HostCtx c;
     hot_load(P, c);
+    if (LEAN) c.k.feat = 0;
     c.l = P.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
     c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
     const uint32_t xwi = (uint32_t)((xpar + (uint64_t)i) & 1);

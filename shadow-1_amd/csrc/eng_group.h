@@ -706,11 +706,13 @@ static int x_enqueue_fused(shd_xgroup* g, int nb) {
     shd_xgroup::Loc& L = g->loc[0];
     const uint32_t nblk = (uint32_t)((e->nloc + e->P.hpw - 1) / e->P.hpw);
     const bool sp = x_sparse(g);
+    const bool lean = e->P.feat == 0 && !kNoLean;   // (no optional feature: the lean instantiations)
     for (int i = 0; i < nb; i++) {
         const int wp = (int)((g->xseq - 1) & 1);   // exchange i - 1 (for round 0: the one before the batch)
         if (sp) {
             const uint32_t grid = std::max<uint32_t>(g->sp_grid, (uint32_t)g->world);
-            hipLaunchKernelGGL(k_round_spx, dim3(grid), dim3(kBlock), 0, e->stream, g->window, i, &e->d_ring[i],
+            hipLaunchKernelGGL(lean ? k_round_spx<true> : k_round_spx<false>, dim3(grid), dim3(kBlock), 0, e->stream,
+                               g->window, i, &e->d_ring[i],
                                (const DevCtl*)e->d_ctl, L.parts, (const DParams*)(L.d_xpr + i + 1), &e->d_ring[i + 2],
                                (const shd_event*)L.xrecv[wp], x_rgn(g, wp), (shd_event* const*)g->d_peers,
                                L.halt_hdr, g->d_xerr, g->world, g->rank0, wp, x_rep(g, wp), x_hoff(g), kXReplMax,
@@ -722,7 +724,8 @@ static int x_enqueue_fused(shd_xgroup* g, int nb) {
         } else {
             // every peer's header needs its put block, also when the engine has fewer blocks of hosts
             const uint32_t grid = std::max<uint32_t>(nblk, (uint32_t)g->world);
-            hipLaunchKernelGGL(k_round_px, dim3(grid), dim3(kBlock), 0, e->stream, g->window, i, &e->d_ring[i],
+            hipLaunchKernelGGL(lean ? k_round_px<true> : k_round_px<false>, dim3(grid), dim3(kBlock), 0, e->stream,
+                               g->window, i, &e->d_ring[i],
                                (const DevCtl*)e->d_ctl, L.parts, (const DParams*)(L.d_xpr + i + 1), &e->d_ring[i + 2],
                                round_args(e->P), (const shd_event*)L.xrecv[wp], x_rgn(g, wp),
                                (shd_event* const*)g->d_peers, L.halt_hdr, g->d_xerr, g->world, g->rank0, wp,

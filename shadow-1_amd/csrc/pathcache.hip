@@ -1651,13 +1651,20 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     // whose heap outgrows that, k_sssp_tie_parents (SHD_PC_TIE_GLOBAL: always)
     const size_t st_bytes = ((size_t)2 * V + 15) & ~(size_t)15;
     int hc = 0, bpc = 0;
-    if (V <= 65533 && !getenv("SHD_PC_TIE_GLOBAL"))
+    const char* hc_env = getenv("SHD_PC_TIE_HC");   // a heap capacity to try (measurements): blocks per CU follow
+    if (V <= 65533 && !getenv("SHD_PC_TIE_GLOBAL")) {
+        if (hc_env) {
+            hc = std::max(64, std::min(atoi(hc_env), std::min(V, 65533)));
+            bpc = (int)std::max<size_t>(1, kLdsMax / (st_bytes + (size_t)hc * 10));
+            if (st_bytes + (size_t)hc * 10 > kLdsMax) hc = bpc = 0;
+        }
         for (int b = 4; b >= 1 && !hc; b--) {
             const size_t budget = (kLdsMax / b) & ~(size_t)15;
             if (budget <= st_bytes) continue;
             const size_t h = std::min<size_t>({(budget - st_bytes) / 10, (size_t)V, (size_t)65533});
             if (h >= 256) { hc = (int)h; bpc = b; }
         }
+    }
     const size_t tl_lds = st_bytes + (size_t)hc * 10;
     // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
     // scratch per vertex and row; <= 4 GiB a chunk (every row of a 10 k-vertex

@@ -2912,7 +2912,46 @@ __global__ void k_tcp_pc_prep(const shd_pv* __restrict__ row, const shd_pv* __re
     if ((threadIdx.x & 63) == 0 && w != ~0ull) atomicMin(out, w);
 }
 
-static int tcp_pc_prep(shd_pc* pc, const std::vector<int32_t>& conn, uint64_t* W) {
+// the datagram processes' share of the window (any two hosts may exchange a
+// datagram): the least latency over every pair of vertices hosts occupy (occ:
+// 0 none, 1 one host, 2 several; a vertex with itself only when two hosts
+// share it), straight from the occupancy on the device -- no host-side list of
+// pairs (O(V^2) of them once hosts sit on ~10 k vertices)
+__global__ void k_tcp_pc_prep_occ(const shd_pv* __restrict__ row, const shd_pv* __restrict__ self,
+                                  const shd_pv* __restrict__ dir, const uint8_t* __restrict__ adj, int complete,
+                                  int prefer_direct, int32_t T, const uint8_t* __restrict__ occ,
+                                  unsigned long long* __restrict__ out) {
+    auto lat_of = [&](int32_t u, int32_t v, double& l) {
+        if (complete || (prefer_direct && adj[(size_t)u * T + v])) { l = dir[(size_t)u * T + v].lat; return; }
+        if (u == v) {
+            const double a = self[u].lat, b = row[(size_t)u * T + u].lat;
+            l = (a >= 0 && (b < 0 || a < b)) ? a : b;
+            return;
+        }
+        const double a = row[(size_t)u * T + v].lat, b = row[(size_t)v * T + u].lat;
+        l = (a >= 0 && b >= 0) ? (a < b ? a : b) : -1.0;
+    };
+    unsigned long long w = ~0ull;
+    const uint64_t n = (uint64_t)T * (uint64_t)T;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+        const int32_t u = (int32_t)(k / (uint64_t)T), v = (int32_t)(k % (uint64_t)T);
+        if (v < u || !occ[u] || !occ[v] || (u == v && occ[u] < 2)) continue;
+        double l1, l2;
+        lat_of(u, v, l1);
+        lat_of(v, u, l2);
+        if (!(l1 >= 0) || !(l2 >= 0)) continue;   // (no route: the datagram is never sent)
+        const double l = l1 < l2 ? l1 : l2;
+        const unsigned long long x = (unsigned long long)ceil(l * (double)kMs);
+        w = x < w ? x : w;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(w, o);
+        w = y < w ? y : w;
+    }
+    if ((threadIdx.x & 63) == 0 && w != ~0ull) atomicMin(out, w);
+}
+
+static int tcp_pc_prep(shd_pc* pc, const std::vector<int32_t>& conn, const std::vector<uint8_t>& occ, uint64_t* W) {
     int32_t* d_conn = nullptr;
     unsigned long long* d_out = nullptr;
     unsigned long long h_out[2] = {~0ull, 0ull};
@@ -2927,7 +2966,20 @@ static int tcp_pc_prep(shd_pc* pc, const std::vector<int32_t>& conn, uint64_t* W
     } else {
         k_tcp_pc_prep<<<(unsigned)std::min<int32_t>((nconn + 255) / 256 + 1, 1024), 256>>>(
             pc->d_row, pc->d_self, pc->d_dir, pc->d_adj, pc->complete, pc->prefer_direct, T, d_conn, nconn, d_out);
-        if (hipGetLastError() != hipSuccess || hipMemcpy(h_out, d_out, 16, hipMemcpyDeviceToHost) != hipSuccess) rc = -5;
+        if (!occ.empty()) {
+            uint8_t* d_occ = nullptr;
+            if (hipMalloc(&d_occ, occ.size()) != hipSuccess ||
+                hipMemcpy(d_occ, occ.data(), occ.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                rc = -5;
+            } else {
+                const uint64_t n = (uint64_t)T * (uint64_t)T;
+                k_tcp_pc_prep_occ<<<(unsigned)std::min<uint64_t>((n + 255) / 256, 4096), 256>>>(
+                    pc->d_row, pc->d_self, pc->d_dir, pc->d_adj, pc->complete, pc->prefer_direct, T, d_occ, d_out);
+            }
+            (void)hipFree(d_occ);   // (hipFree waits for the kernel)
+        }
+        if (rc || hipGetLastError() != hipSuccess || hipMemcpy(h_out, d_out, 16, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = -5;
     }
     (void)hipFree(d_conn); (void)hipFree(d_out);
     if (rc) return rc;
@@ -3120,16 +3172,12 @@ static int tcp_run_impl(const shd_tcp_model* m, shd_comm* comm, int32_t trace, s
                 const int32_t hc = m->proc_host[k], hs = m->proc_host[m->proc_peer[k]];
                 conn.push_back(hvi[hc]); conn.push_back(hvi[hs]); conn.push_back(hc == hs ? 1 : 0); conn.push_back(1);
             }
-        if (any_udp) {   // datagrams may go between any two hosts: every pair of their vertices bounds the window
-            for (int32_t u = 0; u < V; u++) {
-                if (!per_vertex[u]) continue;
-                for (int32_t v = u; v < V; v++) {
-                    if (!per_vertex[v] || (u == v && per_vertex[u] < 2)) continue;
-                    conn.push_back(u); conn.push_back(v); conn.push_back(0); conn.push_back(0);
-                }
-            }
+        std::vector<uint8_t> occ;   // datagrams may go between any two hosts: every pair of their vertices bounds it
+        if (any_udp) {
+            occ.resize(V);
+            for (int32_t u = 0; u < V; u++) occ[u] = (uint8_t)std::min<int32_t>(per_vertex[u], 2);
         }
-        const int rr = tcp_pc_prep(pc, conn, &W);
+        const int rr = tcp_pc_prep(pc, conn, occ, &W);
         if (rr) return rr;
     }
     if (W == 0) return -22;
