@@ -1347,15 +1347,26 @@ __device__ __forceinline__ void ps_round_body(const DParams& P, HostCtx& c, bool
     ps_loop_close<false>(P, c, active, active, R, lb, we, w, cm, next, nullptr);
 }
 
+// The shares' granules are stored in three planes (round 6): granule g of slot
+// s at (g * nsl + s) * 16, nsl = the slots of both parities -- so a wave's poll
+// of 64 blocks' first granules reads 1 KB of consecutive lines instead of 64
+// sectors 48 B apart (every block polls every share every round: at the C5
+// shard 489 x 489 of them); SHD_PS_AOS keeps the 48-B records for an A/B
+#ifdef SHD_PS_AOS
+__device__ __forceinline__ uint32_t ps_goff(uint32_t nsl, uint32_t slot, uint32_t g) { return slot * 48u + g * 16u; }
+#else
+__device__ __forceinline__ uint32_t ps_goff(uint32_t nsl, uint32_t slot, uint32_t g) { return (g * nsl + slot) * 16u; }
+#endif
 // the share of round i: its three granules tagged, stored write-through after
 // the wave's hand-off stores drained; d: the noted destinations
-__device__ __forceinline__ void ps_publish(__amdgpu_buffer_rsrc_t rs, uint32_t slot, uint64_t next, uint32_t flags,
-                                           uint32_t nev, uint32_t npkt, uint32_t nact, uint32_t tag, uint4 d) {
+__device__ __forceinline__ void ps_publish(__amdgpu_buffer_rsrc_t rs, uint32_t nsl, uint32_t slot, uint64_t next,
+                                           uint32_t flags, uint32_t nev, uint32_t npkt, uint32_t nact, uint32_t tag,
+                                           uint4 d) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every store of this wave has landed
     if (threadIdx.x == 0) {
-        st16_sc1(rs, slot * 48u, make_uint4((uint32_t)next, (uint32_t)(next >> 32), flags, tag));
-        st16_sc1(rs, slot * 48u + 16u, make_uint4(nev, npkt, nact, tag));
-        st16_sc1(rs, slot * 48u + 32u, make_uint4(d.x, d.y, d.z, tag));
+        st16_sc1(rs, ps_goff(nsl, slot, 0), make_uint4((uint32_t)next, (uint32_t)(next >> 32), flags, tag));
+        st16_sc1(rs, ps_goff(nsl, slot, 1), make_uint4(nev, npkt, nact, tag));
+        st16_sc1(rs, ps_goff(nsl, slot, 2), make_uint4(d.x, d.y, d.z, tag));
     }
 }
 // the block's noted destinations for its share (after its last flush)
@@ -1376,7 +1387,8 @@ __device__ __forceinline__ uint4 ps_noted(bool pf) {
 // destinations too -- bit k of `dmask`: host hb + k of this block was named,
 // `dall`: some block noted more than it could name.  False on timeout
 template <bool DIRTY, int K = 4>
-__device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t base, uint32_t nblk, uint32_t tag, bool counts,
+__device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t nsl, uint32_t base, uint32_t nblk, uint32_t tag,
+                                          bool counts,
                           uint64_t ticks, uint64_t& next, uint32_t& flags, uint32_t& nev, uint32_t& npkt,
                           uint32_t& nact, uint32_t hb = 0, uint32_t hpw = 0, uint64_t* dmask = nullptr,
                           bool* dall = nullptr) {
@@ -1393,14 +1405,14 @@ __device__ __forceinline__ bool ps_gather(__amdgpu_buffer_rsrc_t rs, uint32_t ba
             uint4 a[K], b[K], d[K];
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                const uint32_t off = (base + c0 + 64u * k + threadIdx.x) * 48u;
+                const uint32_t sl = base + c0 + 64u * k + threadIdx.x;
                 a[k] = make_uint4(0, 0, 0, 0);
                 b[k] = a[k];
                 d[k] = a[k];
                 if ((need >> k) & 1u) {
-                    a[k] = ld16_sc1(rs, off);
-                    if (counts) b[k] = ld16_sc1(rs, off + 16u);
-                    if (DIRTY) d[k] = ld16_sc1(rs, off + 32u);
+                    a[k] = ld16_sc1(rs, ps_goff(nsl, sl, 0));
+                    if (counts) b[k] = ld16_sc1(rs, ps_goff(nsl, sl, 1));
+                    if (DIRTY) d[k] = ld16_sc1(rs, ps_goff(nsl, sl, 2));
                 }
             }
 #pragma unroll
@@ -1615,7 +1627,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         }
         const uint32_t tag = tag0 + (uint32_t)i;
         const uint32_t base = (uint32_t)(i & 1) * nblk;
-        ps_publish(rs, base + blockIdx.x, next, fl, nev, npkt, nact, tag, ps_noted(pfm));
+        ps_publish(rs, 2 * nblk, base + blockIdx.x, next, fl, nev, npkt, nact, tag, ps_noted(pfm));
         TIMP(6);
         if (pfm) {   // the next window's events, staged while the other blocks finish
             const uint64_t b1 = we >> P.bin_shift;
@@ -1627,7 +1639,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
         uint64_t f_next, dm = 0;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
         bool dall = false;
-        const bool ok_v = ps_gather<kPsPf>(rs, base, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt,
+        const bool ok_v = ps_gather<kPsPf>(rs, 2 * nblk, base, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl, f_nev, f_npkt,
                                            f_nact, hb, (uint32_t)P.hpw, &dm, &dall);
         TIMP(7);
         // the folds are wave-uniform: said so to the compiler, so that the
@@ -1913,11 +1925,11 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         }
         const uint32_t tag = tag0 + (uint32_t)i;
         const uint32_t sbase = (uint32_t)(i & 1) * nblk;
-        ps_publish(rs, sbase + blockIdx.x, next, fl, nev, npkt, nhost, tag, ps_noted(false));
+        ps_publish(rs, 2 * nblk, sbase + blockIdx.x, next, fl, nev, npkt, nhost, tag, ps_noted(false));
         TIMP(6);
         uint64_t f_next;
         uint32_t f_fl, f_nev, f_npkt, f_nact;
-        const bool ok_v = ps_gather<false, kSpGatherK>(rs, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl,
+        const bool ok_v = ps_gather<false, kSpGatherK>(rs, 2 * nblk, sbase, nblk, tag, blockIdx.x == 0, ticks, f_next, f_fl,
                                                        f_nev, f_npkt, f_nact);
         TIMP(7);
         const bool ok = __builtin_amdgcn_readfirstlane((int)ok_v) != 0;

@@ -1650,20 +1650,20 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     // entries (as many blocks per CU as fit, up to 4); else, and for its rows
     // whose heap outgrows that, k_sssp_tie_parents (SHD_PC_TIE_GLOBAL: always)
     const size_t st_bytes = ((size_t)2 * V + 15) & ~(size_t)15;
+    // A heap of 1024 entries (the rows of the 10 k whole-millisecond graph peak
+    // between 600 and 1024: at 600, 503 of 10 000 rows outgrew it) beside the
+    // row's 2-B vertex states, as many blocks per CU as LDS holds: the build
+    // ran 439 ms at the largest heap that fits four per CU, 365 ms at 1024
+    // (five per CU), 534 / 642 ms at 600 / 400 (rows falling back); round 5's
+    // lane heaps 480-490 ms (profiles/r06/tiehc).  SHD_PC_TIE_HC: another
+    // capacity (measurements)
     int hc = 0, bpc = 0;
-    const char* hc_env = getenv("SHD_PC_TIE_HC");   // a heap capacity to try (measurements): blocks per CU follow
     if (V <= 65533 && !getenv("SHD_PC_TIE_GLOBAL")) {
-        if (hc_env) {
-            hc = std::max(64, std::min(atoi(hc_env), std::min(V, 65533)));
-            bpc = (int)std::max<size_t>(1, kLdsMax / (st_bytes + (size_t)hc * 10));
-            if (st_bytes + (size_t)hc * 10 > kLdsMax) hc = bpc = 0;
-        }
-        for (int b = 4; b >= 1 && !hc; b--) {
-            const size_t budget = (kLdsMax / b) & ~(size_t)15;
-            if (budget <= st_bytes) continue;
-            const size_t h = std::min<size_t>({(budget - st_bytes) / 10, (size_t)V, (size_t)65533});
-            if (h >= 256) { hc = (int)h; bpc = b; }
-        }
+        const char* hc_env = getenv("SHD_PC_TIE_HC");
+        hc = std::max(64, std::min(hc_env ? atoi(hc_env) : 1024, std::min(V, 65533)));
+        if (st_bytes + (size_t)hc * 10 > kLdsMax) hc = (int)std::min<size_t>(std::min(V, 65533), (kLdsMax - std::min(kLdsMax, st_bytes)) / 10);
+        bpc = hc >= 64 ? (int)std::min<size_t>(8, std::max<size_t>(1, kLdsMax / (st_bytes + (size_t)hc * 10))) : 0;
+        if (!bpc) hc = 0;
     }
     const size_t tl_lds = st_bytes + (size_t)hc * 10;
     // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
