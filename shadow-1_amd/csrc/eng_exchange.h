@@ -1028,7 +1028,7 @@ __global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, De
     R.inbox = buf_rsrc(P.inbox[parity] + (size_t)hb * P.inbox_cap, (uint64_t)nh * P.inbox_cap * sizeof(shd_event));
     HostCtx c;
     hot_load(P, c);
-    if (LEAN) c.k.feat = 0;
+    if (LEAN) { c.k.feat = 0; c.k.boot_end = 0; }
     c.l = P.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
     c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
     const uint32_t xwi = (uint32_t)((xpar + (uint64_t)i) & 1);

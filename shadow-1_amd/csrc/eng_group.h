@@ -706,7 +706,7 @@ static int x_enqueue_fused(shd_xgroup* g, int nb) {
     shd_xgroup::Loc& L = g->loc[0];
     const uint32_t nblk = (uint32_t)((e->nloc + e->P.hpw - 1) / e->P.hpw);
     const bool sp = x_sparse(g);
-    const bool lean = e->P.feat == 0 && !kNoLean;   // (no optional feature: the lean instantiations)
+    const bool lean = lean_model(e->P);   // (the lean instantiations)
     for (int i = 0; i < nb; i++) {
         const int wp = (int)((g->xseq - 1) & 1);   // exchange i - 1 (for round 0: the one before the batch)
         if (sp) {

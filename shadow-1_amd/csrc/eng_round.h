@@ -180,9 +180,10 @@ __device__ __forceinline__ void host_in_load(const DRoundArgs& a, HostIn& in) {
 // one round [ws, we): merge inbox[parity] and the calendar bins of the
 // window, run events < we
 // RX: the fused peer-to-peer round's received window events (s_rx).  LEAN
-// (round 6): the model uses none of the optional features (ParamsT::feat == 0,
-// the bench's models): the context's feature word is the constant 0, so the
-// trace, status, heartbeat, path-counter and datagram-application paths fold
+// (round 6): the model uses none of the optional features (ParamsT::feat == 0)
+// and has no bootstrap period -- the bench's models: the context's feature
+// word and bootstrap end are the constant 0, so the trace, status, heartbeat,
+// path-counter and datagram-application paths and the bootstrapping tests fold
 // away (registers and issue the PHOLD path does not need)
 template <bool RX = false, bool LEAN = false>
 __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, uint64_t ws, uint64_t we, int parity,
@@ -254,7 +255,7 @@ __device__ __forceinline__ void round_body(const DParams& P, const HostIn& in, u
 #endif
     HostCtx c;   // idle lanes take part in the wave's flushes with no sends
     hot_load(P, c);
-    if (LEAN) c.k.feat = 0;
+    if (LEAN) { c.k.feat = 0; c.k.boot_end = 0; }
     PendDel pd;
     send_pool_reset(c); c.att = 0; c.cls = 0; c.err = 0;
     c.ws = ws; c.ws_mod = (uint32_t)(ws % SHD_MS); c.np = parity ^ 1; c.xwi = xwi; c.xput = 0; c.pf_lim = 0;
@@ -1541,7 +1542,7 @@ __global__ __launch_bounds__(kBlock) void k_round_ps(uint64_t window, int nb, De
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
     HostCtx c;
     hot_load(P0, c);
-    if (LEAN) c.k.feat = 0;
+    if (LEAN) { c.k.feat = 0; c.k.boot_end = 0; }
     if (has) {
         load_ctx(P0, c, l, P0.hs[l], P0.host_att[P0.h0 + l], P0.self_thr[P0.h0 + l]);
     } else {
@@ -1885,7 +1886,7 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(shares, (uint64_t)2 * nblk * sizeof(PsShare));
     HostCtx c;
     hot_load(P0, c);
-    if (LEAN) c.k.feat = 0;
+    if (LEAN) { c.k.feat = 0; c.k.boot_end = 0; }
     c.l = P0.nloc; c.h = 0; c.att = 0; c.cls = 0; c.evq_n = 0; c.top_time = kInf; c.peer = -1; c.rq_head = 0;
     c.tt0 = c.tt1 = c.tt2 = kInf; c.ev_seq = 0; c.cq_hv = false; c.tq_hv = false;
     uint64_t ws = ring[0].next_time;

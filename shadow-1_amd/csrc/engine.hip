@@ -63,6 +63,10 @@ static constexpr bool kNoLean = true;
 #else
 static constexpr bool kNoLean = false;
 #endif
+// the lean round kernels (LEAN: no optional feature, no bootstrap period --
+// every bench model): their feature word and bootstrap end are constants
+template <class PT>
+static bool lean_model(const PT& P) { return !kNoLean && P.feat == 0 && P.bootstrap_end == 0; }
 #ifdef SHD_TEST_HOOKS
 static bool test_hook(const char* name) { return getenv(name) != nullptr; }
 #else
@@ -645,7 +649,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
         const int grid = (e->nloc + P.hpw - 1) / P.hpw;
         int ncu = 0, per_cu = 0;
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
-        const bool lean = P.feat == 0 && !kNoLean;
+        const bool lean = lean_model(P);
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lean ? reinterpret_cast<const void*>(&k_round_ps<true>)
                                                                        : reinterpret_cast<const void*>(&k_round_ps<false>),
                                                          kBlock, 0) != hipSuccess)
@@ -999,7 +1003,7 @@ static int enqueue_batch_tl(shd_eng* e) {
     const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
     for (int i = 0; i < B; i++) {
         // (the lean instantiation for models with no optional feature: ParamsT::feat == 0)
-        if (e->P.feat == 0 && !kNoLean)
+        if (lean_model(e->P))
             hipLaunchKernelGGL(k_round_tl<true>, dim3(grid), dim3(kBlock), 0, e->stream, e->window, i, &e->d_ring[i],
                                (const DevCtl*)e->d_ctl, e->d_tpart, (const DParams*)(e->d_pr + i + 1),
                                &e->d_ring[i + 2], round_args(e->P));
@@ -1055,7 +1059,7 @@ static bool sp_dense_batch(uint64_t rounds, uint64_t active, uint64_t pkt, uint6
 
 static int launch_batch_ps(shd_eng* e, int nb) {
     const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
-    const bool lean = e->P.feat == 0 && !kNoLean;   // (no optional feature: the lean instantiations)
+    const bool lean = lean_model(e->P);   // (the lean instantiations)
     if (e->sp_ok) {
         hipLaunchKernelGGL(lean ? k_round_sp<true> : k_round_sp<false>, dim3(e->sp_grid), dim3(kBlock), 0, e->stream,
                            e->window, nb, e->d_ring, (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr,

@@ -1161,6 +1161,16 @@ __device__ __forceinline__ double bcast_d(double v, int lane) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), lane);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+// (one wave per block: the lanes' LDS accesses are ordered by the wave's own
+// instruction order, so no __syncthreads -- whose workgroup fence would drain
+// every outstanding global store and load, the parents' stores and the next
+// pop's arc loads, twice a pop -- only a compiler fence)
+#define TIE_WAVE_SYNC()                                              \
+    do {                                                             \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       \
+        __builtin_amdgcn_wave_barrier();                             \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       \
+    } while (0)
 __global__ __launch_bounds__(64) void k_sssp_tie_lds(
     int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
@@ -1176,7 +1186,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
             st[v] = 0;
             par[v] = -1;
         }
-        __syncthreads();
+        TIE_WAVE_SYNC();
         const int32_t src = attached[rows[slot]];
         int32_t size = 1;
         if (lane == 0) {
@@ -1185,6 +1195,16 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
             st[src] = 2;
         }
         int ovfl = 0;
+        // the next pop's first chunk of arcs, loaded while lane 0 sinks: the
+        // heap top after a pop's relaxations is the next pop's vertex
+        int32_t pkb = arc_off[src], pke = arc_off[src + 1];
+        int32_t px = -1, prin = 0;
+        double pw = 0.0;
+        if (pkb + lane < pke) {
+            px = arc_dst[pkb + lane];
+            pw = arc_w[pkb + lane];
+            prin = arc_rin[pkb + lane];
+        }
         while (size > 0 && !ovfl) {
             // the pop (igraph_2wheap_max_index + delete_max), by lane 0
             int32_t u0 = 0;
@@ -1196,21 +1216,22 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                 if (size > 0) tlds_sink(hv, hi, st, size, 0, hv[size], hi[size]);
                 st[u0] = 1;
             }
-            const int32_t u = __builtin_amdgcn_readfirstlane(u0);
             const double md = bcast_d(md0, 0);
             size = __builtin_amdgcn_readfirstlane(size);
-            __syncthreads();
-            const int32_t kb = arc_off[u], ke = arc_off[u + 1];
+            TIE_WAVE_SYNC();
+            const int32_t kb = pkb, ke = pke;
+            int32_t top = -1;
             for (int32_t c0 = kb; c0 < ke && !ovfl; c0 += 64) {
                 const int32_t k = c0 + lane;
                 const bool valid = k < ke;
                 int32_t x = -1, rin = 0;
-                double alt = 0.0, cur = 0.0;
+                double w = 0.0;
+                if (c0 == kb) { x = px; w = pw; rin = prin; }
+                else if (valid) { x = arc_dst[k]; w = arc_w[k]; rin = arc_rin[k]; }
+                const double alt = md + w;
+                double cur = 0.0;
                 uint32_t sx = 1;
                 if (valid) {
-                    x = arc_dst[k];
-                    alt = md + arc_w[k];
-                    rin = arc_rin[k];
                     sx = st[x];
                     if (sx >= 2) cur = -hv[sx - 2];
                 }
@@ -1243,13 +1264,29 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                 }
                 size = __builtin_amdgcn_readfirstlane(size);
                 ovfl = __builtin_amdgcn_readfirstlane(ovfl);
-                __syncthreads();
+                TIE_WAVE_SYNC();
+            }
+            // the next pop's vertex (the top now) and its first chunk of arcs,
+            // issued before its sink
+            int32_t t0 = -1;
+            if (lane == 0 && size > 0) t0 = hi[0];
+            top = __builtin_amdgcn_readfirstlane(t0);
+            if (top >= 0 && !ovfl) {
+                pkb = arc_off[top];
+                pke = arc_off[top + 1];
+                px = -1;
+                if (pkb + lane < pke) {
+                    px = arc_dst[pkb + lane];
+                    pw = arc_w[pkb + lane];
+                    prin = arc_rin[pkb + lane];
+                }
             }
         }
         if (ovfl && lane == 0) ovf[1 + atomicAdd(ovf, 1)] = slot;
-        __syncthreads();
+        TIE_WAVE_SYNC();
     }
 }
+#undef TIE_WAVE_SYNC
 
 // ------------------------------------------------------------------ direct
 // _topology_lookupDirectPath (topology.c:1877-1927) for every attached pair;
