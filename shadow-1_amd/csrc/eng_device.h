@@ -1886,7 +1886,10 @@ __device__ __forceinline__ uint64_t cal_lower_bound(const DParams& P, const uint
     return t > we ? t : we;
 }
 
-__device__ __forceinline__ void store_ctx(const DParams& P, HostCtx& c) {
+// rec / hn: where the record and the next time go (default: the host's
+// global ones; k_round_sp with LDS-resident records: the block's LDS copies)
+__device__ __forceinline__ void store_ctx(const DParams& P, HostCtx& c, HostRec* rec = nullptr,
+                                          uint64_t* hn = nullptr) {
     const int32_t l = c.l;
     HostRec r;
     r.ev_seq = c.ev_seq; r.cq_total = (uint32_t)c.cq_total; r.cq_iexp = c.cq_iexp; r.cq_ndrop = c.cq_ndrop;
@@ -1908,7 +1911,8 @@ __device__ __forceinline__ void store_ctx(const DParams& P, HostCtx& c) {
     r.tq_head = (uint16_t)c.tq_head; r.tq_count = (uint16_t)c.tq_count; r.evq_n = c.evq_n;
     r.if_in = c.if_in; r.if_out = c.if_out;
     r.rq_head = (uint16_t)c.rq_head; r.port = (uint16_t)c.port;
-    P.hs[l] = r;
+    if (rec) *rec = r;
+    else P.hs[l] = r;
     if (c.cq_hv) P.cq[(size_t)l * c.k.cq_cap + c.cq_head] = s_cqh[threadIdx.x];
     if (c.tq_hv) P.tq[(size_t)l * c.k.tq_cap + c.tq_head] = s_tqh[threadIdx.x];
     HostCnt* hc = P.hc + l;   // counter deltas: fire-and-forget atomics
@@ -1918,7 +1922,8 @@ __device__ __forceinline__ void store_ctx(const DParams& P, HostCtx& c) {
     if (c.c_idrop) atomicAdd(&hc->idrop, (unsigned long long)c.c_idrop);
     if (c.c_cdrop) atomicAdd(&hc->cdrop, (unsigned long long)c.c_cdrop);
     if (c.c_recv) atomicAdd(&hc->recv, (unsigned long long)c.c_recv);
-    P.hnext[l] = host_next(c);
+    if (hn) *hn = host_next(c);
+    else P.hnext[l] = host_next(c);
 }
 
 template <int BLOCK>

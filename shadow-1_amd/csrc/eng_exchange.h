@@ -1036,10 +1036,10 @@ __global__ __launch_bounds__(kBlock) void k_round_spx(uint64_t window, int i, De
     c.xwi = xwi;
     uint64_t next;
     uint32_t nact;
-    sp_scan(P, R, hb, nh, ngrp, ws, we, next, nact);
+    sp_scan(P, R, hb, nh, ngrp, ws, we, next, nact, s_act, nullptr);
     __syncthreads();
     uint32_t nev = 0, npkt = 0, err = c.err | ierr, nhost = 0;
-    sp_passes<false>(P, c, R, hb, nact, ws, we, parity, xwi, next, nev, npkt, err, nhost);
+    sp_passes<false>(P, c, R, hb, nact, ws, we, parity, xwi, next, nev, npkt, err, nhost, s_act, nullptr, nullptr);
     // peer-to-peer: this block's stores into the peers' regions land before the
     // round ends (the next launch's put block announces them)
     if (P.xpeer) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

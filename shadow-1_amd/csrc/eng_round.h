@@ -1720,8 +1720,11 @@ __shared__ uint32_t s_aw[(kNBW + 1) * kBlock];   // the first pass's hand-off wo
 // (ngrp groups of 64): the hosts with something due in [ws, we) go to s_act
 // (their words to s_aw for the first pass), nact counts them; next: the least
 // next time of the lane's idle hosts
+// (alist: the list's LDS array; lhn: the block's hosts' next times in LDS, or
+// null: the global hnext)
 __device__ __forceinline__ void sp_scan(const DParams& P, const PsRsrc& R, uint32_t hb, uint32_t nh, uint32_t ngrp,
-                                        uint64_t ws, uint64_t we, uint64_t& next, uint32_t& nact) {
+                                        uint64_t ws, uint64_t we, uint64_t& next, uint32_t& nact, uint16_t* alist,
+                                        const uint64_t* lhn) {
     const uint32_t lane = threadIdx.x;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
     next = kInf;
@@ -1760,7 +1763,7 @@ __device__ __forceinline__ void sp_scan(const DParams& P, const PsRsrc& R, uint3
                     w4[q][0] = x.x; w4[q][1] = x.y; w4[q][2] = x.z; w4[q][3] = x.w;
                     w4[q][4] = y.x; w4[q][5] = y.y; w4[q][6] = y.z; w4[q][7] = y.w;
                 }
-                t4[q] = P.hnext[hb + lb];
+                t4[q] = lhn ? lhn[lb] : P.hnext[hb + lb];
             }
         }
 #ifdef SHD_TIMING
@@ -1791,7 +1794,7 @@ __device__ __forceinline__ void sp_scan(const DParams& P, const PsRsrc& R, uint3
             const uint64_t m = __ballot(act);
             if (act) {
                 const uint32_t k = nact + (uint32_t)__popcll(m & lt_mask);
-                s_act[k] = (uint16_t)lb;
+                alist[k] = (uint16_t)lb;
                 if (k < (uint32_t)kBlock) {
 #pragma unroll
                     for (int j = 0; j < (int)kNBW; j++) s_aw[j * kBlock + k] = w4[q][j];
@@ -1815,15 +1818,18 @@ __device__ __forceinline__ void sp_scan(const DParams& P, const PsRsrc& R, uint3
 // loads its hosts' records (with the bins' loads, ps_round_body<true>), runs
 // their round and stores them; next / nev / npkt / fl / nhost accumulate the
 // lane's share (PEND: a logged first touch flags kPsPend)
+// (alist: the scan's list; lrec / lhn: the block's hosts' records and next
+// times in LDS, or null: the global ones)
 template <bool PEND>
 __device__ __forceinline__ void sp_passes(const DParams& P, HostCtx& c, const PsRsrc& R, uint32_t hb, uint32_t nact,
                                           uint64_t ws, uint64_t we, int parity, uint32_t xwi, uint64_t& next,
-                                          uint32_t& nev, uint32_t& npkt, uint32_t& fl, uint32_t& nhost) {
+                                          uint32_t& nev, uint32_t& npkt, uint32_t& fl, uint32_t& nhost,
+                                          const uint16_t* alist, HostRec* lrec, uint64_t* lhn) {
     const uint32_t lane = threadIdx.x;
     for (uint32_t base = 0; base < nact; base += kBlock) {
         const uint32_t k = base + lane;
         const bool act = k < nact;
-        const uint32_t lb = act ? (uint32_t)s_act[k] : 0u;
+        const uint32_t lb = act ? (uint32_t)alist[k] : 0u;
         const int32_t l = (int32_t)(hb + lb);
         uint32_t nin = 0, w[kNBW];
 #pragma unroll
@@ -1845,14 +1851,17 @@ __device__ __forceinline__ void sp_passes(const DParams& P, HostCtx& c, const Ps
         in.l = l;
         in.xwi = xwi;
         if (act) {
-            in.rec = P.hs[l];
+            in.rec = lrec ? lrec[lb] : P.hs[l];
             in.att = P.host_att[P.h0 + l];
             in.st = P.self_thr[P.h0 + l];
         }
         const uint32_t wbits = ps_window_bits(P, c, w, ws, we);
         uint64_t hn = kInf;
         ps_round_body<true>(P, c, act, lb, R, ws, we, parity, nin, w, wbits, hn, &in);
-        if (act) store_ctx(P, c);
+        if (act) {
+            if (lrec) store_ctx(P, c, &lrec[lb], &lhn[lb]);
+            else store_ctx(P, c);
+        }
         next = hn < next ? hn : next;
         nev += c.c_events; npkt += c.c_pkt;
         fl |= c.err | (PEND && c.n_pend ? kPsPend : 0u);
@@ -1861,10 +1870,19 @@ __device__ __forceinline__ void sp_passes(const DParams& P, HostCtx& c, const Ps
     }
 }
 
+// k_round_sp's dynamic LDS: the scan's list (sph 2-B entries), then, with lrec
+// (round 6: where two blocks per CU still fit), the block's hosts' records and
+// next times for the whole batch -- loaded at its start, stored at its end, so
+// a pass neither loads a record from HBM nor stores one before the share's drain
+extern __shared__ __align__(16) char s_spdyn[];
+__host__ __device__ constexpr size_t sp_dyn_bytes(uint32_t sph, bool lrec) {
+    return (((size_t)2 * sph + 127) & ~(size_t)127) + (lrec ? (size_t)sph * (sizeof(HostRec) + 8) : 0);
+}
 template <bool LEAN>
 __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, DevSummary* __restrict__ ring,
                                                       const DevCtl* __restrict__ ctl, PsShare* __restrict__ shares,
-                                                      const DParams* __restrict__ Pr, uint64_t ticks, uint32_t sph) {
+                                                      const DParams* __restrict__ Pr, uint64_t ticks, uint32_t sph,
+                                                      int lrec_on) {
     const DParams& P0 = Pr[1];
     const uint32_t nblk = gridDim.x;
     const uint32_t lane = threadIdx.x;
@@ -1893,6 +1911,16 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
     const uint64_t stop = ctl->stop, rbase = ctl->round_base;
     const uint32_t tag0 = (uint32_t)ctl->xtag;
     const bool lead = blockIdx.x == 0 && lane == 0;
+    uint16_t* alist = (uint16_t*)s_spdyn;
+    HostRec* lrec = lrec_on ? (HostRec*)(s_spdyn + sp_dyn_bytes(sph, false)) : nullptr;
+    uint64_t* lhn = lrec_on ? (uint64_t*)(lrec + sph) : nullptr;
+    if (lrec) {   // the block's hosts' records and next times, for the batch
+        for (uint32_t j = lane; j < nh; j += kBlock) {
+            lrec[j] = P0.hs[hb + j];
+            lhn[j] = P0.hnext[hb + j];
+        }
+        __syncthreads();
+    }
     for (int i = 0; i < nb; i++) {
         PS_PARAMS(i);
         const unsigned long long t_start = wall_clock64();
@@ -1909,14 +1937,14 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         ps_round_reset(P, c, ws, we, parity, false);
         uint64_t next;
         uint32_t nact;
-        sp_scan(P, R, hb, nh, ngrp, ws, we, next, nact);
+        sp_scan(P, R, hb, nh, ngrp, ws, we, next, nact, alist, lhn);
         __syncthreads();
         TIMP(1);
         TIMVP(20, (uint64_t)nact);   // the block's active hosts this round
         TIMVP(21, (uint64_t)((nact + kBlock - 1) / kBlock));   // passes
         // the active hosts, 64 at a time
         uint32_t nev = 0, npkt = 0, fl = 0, nhost = 0;
-        sp_passes<true>(P, c, R, hb, nact, ws, we, parity, 0u, next, nev, npkt, fl, nhost);
+        sp_passes<true>(P, c, R, hb, nact, ws, we, parity, 0u, next, nev, npkt, fl, nhost, alist, lrec, lhn);
         for (int off = 32; off > 0; off >>= 1) {
             const uint64_t o = __shfl_xor(next, off, 64);
             next = o < next ? o : next;
@@ -1959,6 +1987,13 @@ __global__ __launch_bounds__(kBlock) void k_round_sp(uint64_t window, int nb, De
         if (f_fl) break;
         ws = f_next;
         if (ws >= stop) break;
+    }
+    if (lrec) {   // the records and next times back, once for the batch
+        __syncthreads();
+        for (uint32_t j = lane; j < nh; j += kBlock) {
+            P0.hs[hb + j] = lrec[j];
+            P0.hnext[hb + j] = lhn[j];
+        }
     }
 }
 

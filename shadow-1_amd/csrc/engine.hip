@@ -165,6 +165,8 @@ struct shd_eng {
     // fits the GPU one block per CU and the engine holds every host
     bool ps_ok = false;
     bool sp_ok = false;                     // the sparse persistent kernel (k_round_sp) instead
+    bool sp_lrec = false;                   // its hosts' records resident in LDS for a batch
+    size_t sp_dyn = 0;                      // its dynamic LDS bytes
     bool sp_dense = false;                  // the last batch had many active hosts: launch-per-round batches
     bool sp_forced = false;                 // SHD_SP_HOSTS: the sparse kernel whatever the density
     uint32_t sp_hosts = 0;                  // ... its hosts per block
@@ -668,7 +670,7 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_sp,
                                                              lean ? reinterpret_cast<const void*>(&k_round_sp<true>)
                                                                   : reinterpret_cast<const void*>(&k_round_sp<false>),
-                                                             kBlock, 0) != hipSuccess)
+                                                             kBlock, sp_dyn_bytes(kSpMaxHosts, false)) != hipSuccess)
                 per_cu_sp = 0;
             (void)hipGetLastError();
             // about two blocks per CU (where occupancy admits two): at the C5 shard 256 hosts a
@@ -683,8 +685,24 @@ extern "C" int shd_eng_create(const shd_model* m, shd_pc* pc, int32_t host_begin
             if (getenv("SHD_SP_VERBOSE"))
                 fprintf(stderr, "shd: sparse rounds: %d CUs, %d blocks per CU resident, %u hosts per block, %u blocks\n",
                         ncu, per_cu_sp, sph, g);
+            // the block's records resident in LDS for the batch where the grid still fits resident
+            // with them (SHD_SP_NO_LREC: records in HBM, the A/B knob)
+            int per_cu_lrec = 0;
+            if (!getenv("SHD_SP_NO_LREC") && sph <= kSpMaxHosts &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_lrec,
+                                                             lean ? reinterpret_cast<const void*>(&k_round_sp<true>)
+                                                                  : reinterpret_cast<const void*>(&k_round_sp<false>),
+                                                             kBlock, sp_dyn_bytes(sph, true)) != hipSuccess)
+                per_cu_lrec = 0;
+            (void)hipGetLastError();
+            const bool lrec = per_cu_lrec >= 1 && g <= (uint32_t)(ncu * per_cu_lrec);
+            if (getenv("SHD_SP_VERBOSE"))
+                fprintf(stderr, "shd: sparse rounds: records in %s (%d blocks per CU with them)\n",
+                        lrec ? "LDS" : "HBM", per_cu_lrec);
             if (!no_sp && per_cu_sp >= 1 && sph <= kSpMaxHosts && g <= (uint32_t)(ncu * per_cu_sp)) {
                 e->sp_ok = true;
+                e->sp_lrec = lrec;
+                e->sp_dyn = sp_dyn_bytes(lrec ? sph : kSpMaxHosts, lrec);
                 e->sp_forced = sp_force != 0;
                 e->sp_hosts = sph;
                 e->sp_grid = g;
@@ -1061,9 +1079,9 @@ static int launch_batch_ps(shd_eng* e, int nb) {
     const uint64_t ticks = (uint64_t)(2.0 * e->wall_khz * 1000.0);   // 2 s: a block that never comes
     const bool lean = lean_model(e->P);   // (the lean instantiations)
     if (e->sp_ok) {
-        hipLaunchKernelGGL(lean ? k_round_sp<true> : k_round_sp<false>, dim3(e->sp_grid), dim3(kBlock), 0, e->stream,
-                           e->window, nb, e->d_ring, (const DevCtl*)e->d_ctl, e->d_pshare, (const DParams*)e->d_pr,
-                           ticks, e->sp_hosts);
+        hipLaunchKernelGGL(lean ? k_round_sp<true> : k_round_sp<false>, dim3(e->sp_grid), dim3(kBlock), e->sp_dyn,
+                           e->stream, e->window, nb, e->d_ring, (const DevCtl*)e->d_ctl, e->d_pshare,
+                           (const DParams*)e->d_pr, ticks, e->sp_hosts, (int)e->sp_lrec);
     } else {
         const int grid = (e->nloc + e->P.hpw - 1) / e->P.hpw;
         hipLaunchKernelGGL(lean ? k_round_ps<true> : k_round_ps<false>, dim3(grid), dim3(kBlock), 0, e->stream,
