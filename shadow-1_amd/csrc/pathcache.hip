@@ -1165,19 +1165,34 @@ __device__ __forceinline__ double bcast_d(double v, int lane) {
 // instruction order, so no __syncthreads -- whose workgroup fence would drain
 // every outstanding global store and load, the parents' stores and the next
 // pop's arc loads, twice a pop -- only a compiler fence)
+// STG (round 6): the vertex states in the block's slice of global scratch
+// (L2-resident) instead of LDS, so LDS holds the heap only -- 10 KB a row at
+// 1024 entries, 16 rows per CU against 5 with 20 KB of states beside it (10 k
+// vertices).  Every state store is lane 0's; the other lanes read states only
+// in the arcs' parallel loads, behind a workgroup-scope fence (a wait for lane
+// 0's stores); lane 0 re-reads a state only for a decrease (its heap position
+// moves with other vertices' steps) or a repeated target.
 #define TIE_WAVE_SYNC()                                              \
     do {                                                             \
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");       \
-        __builtin_amdgcn_wave_barrier();                             \
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");       \
+        if (STG) {                                                   \
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   \
+            __builtin_amdgcn_wave_barrier();                         \
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   \
+        } else {                                                     \
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+            __builtin_amdgcn_wave_barrier();                         \
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+        }                                                            \
     } while (0)
+template <bool STG>
 __global__ __launch_bounds__(64) void k_sssp_tie_lds(
     int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
-    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf) {
+    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf,
+    uint16_t* __restrict__ stg) {
     extern __shared__ __align__(16) char tsm[];
-    uint16_t* st = (uint16_t*)tsm;
-    double* hv = (double*)(tsm + (((size_t)2 * V + 15) & ~(size_t)15));
+    uint16_t* st = STG ? stg + (size_t)blockIdx.x * V : (uint16_t*)tsm;
+    double* hv = (double*)(tsm + (STG ? 0 : (((size_t)2 * V + 15) & ~(size_t)15)));
     uint16_t* hi = (uint16_t*)(hv + hc);
     const int lane = (int)threadIdx.x;
     for (int32_t slot = (int32_t)blockIdx.x; slot < n; slot += (int32_t)gridDim.x) {
@@ -1239,6 +1254,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                 bool dup = false;   // an earlier arc of this chunk to the same vertex
                 for (int32_t i = 0; i < cnt; i++) dup |= i < lane && __builtin_amdgcn_readlane(x, i) == x;
                 uint64_t m = __ballot(valid && (dup || sx == 0 || (sx >= 2 && alt < cur)));
+                const uint64_t mdup = STG ? __ballot(dup) : 0ull;
                 if (lane == 0) {
                     while (m) {
                         const int j = __builtin_ctzll(m);
@@ -1246,7 +1262,10 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                         const int32_t xj = __builtin_amdgcn_readlane(x, j);
                         const double aj = bcast_d(alt, j);
                         const int32_t rj = __builtin_amdgcn_readlane(rin, j);
-                        const uint32_t sj = st[xj];
+                        // (STG: an unreached target of a first visit is still
+                        // unreached -- no other arc of the chunk reaches it)
+                        const uint32_t s0 = STG ? (uint32_t)__builtin_amdgcn_readlane((int)sx, j) : 1u;
+                        const uint32_t sj = (STG && s0 == 0u && !((mdup >> j) & 1ull)) ? 0u : (uint32_t)st[xj];
                         if (sj == 0) {   // the first finite distance: push
                             if (size >= hc) { ovfl = 1; break; }
                             par[xj] = rj;
@@ -1694,15 +1713,29 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     // (five per CU), 534 / 642 ms at 600 / 400 (rows falling back); round 5's
     // lane heaps 480-490 ms (profiles/r06/tiehc).  SHD_PC_TIE_HC: another
     // capacity (measurements)
+    // STG: the states in global scratch and LDS for the heap only, where that
+    // puts more rows on a CU (SHD_PC_TIE_STG=0 / 1 forces either)
     int hc = 0, bpc = 0;
+    bool stg = false;
     if (V <= 65533 && !getenv("SHD_PC_TIE_GLOBAL")) {
         const char* hc_env = getenv("SHD_PC_TIE_HC");
+        const char* stg_env = getenv("SHD_PC_TIE_STG");
         hc = std::max(64, std::min(hc_env ? atoi(hc_env) : 1024, std::min(V, 65533)));
-        if (st_bytes + (size_t)hc * 10 > kLdsMax) hc = (int)std::min<size_t>(std::min(V, 65533), (kLdsMax - std::min(kLdsMax, st_bytes)) / 10);
-        bpc = hc >= 64 ? (int)std::min<size_t>(8, std::max<size_t>(1, kLdsMax / (st_bytes + (size_t)hc * 10))) : 0;
+        const int bpc_g = (int)std::min<size_t>(16, std::max<size_t>(1, kLdsMax / ((size_t)hc * 10)));
+        int hc_l = hc;
+        if (st_bytes + (size_t)hc_l * 10 > kLdsMax)
+            hc_l = (int)std::min<size_t>(std::min(V, 65533), (kLdsMax - std::min(kLdsMax, st_bytes)) / 10);
+        const int bpc_l = hc_l >= 64 ? (int)std::min<size_t>(8, std::max<size_t>(1, kLdsMax / (st_bytes + (size_t)hc_l * 10))) : 0;
+        stg = stg_env ? atoi(stg_env) != 0 : (bpc_g > bpc_l || hc_l < hc);
+        if (stg) {
+            bpc = bpc_g;
+        } else {
+            hc = hc_l;
+            bpc = bpc_l;
+        }
         if (!bpc) hc = 0;
     }
-    const size_t tl_lds = st_bytes + (size_t)hc * 10;
+    const size_t tl_lds = (stg ? 0 : st_bytes) + (size_t)hc * 10;
     // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
     // scratch per vertex and row; <= 4 GiB a chunk (every row of a 10 k-vertex
     // graph at once)
@@ -1721,8 +1754,13 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     int32_t* d_ovf = nullptr;
     if (hc) {   // [0]: the count, then the slots of the rows whose heap outgrew hc
         SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t) * (1 + (size_t)chunk)));
-        SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_tie_lds, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)tl_lds));
+        SHD_HIP(hipFuncSetAttribute(stg ? (const void*)k_sssp_tie_lds<true> : (const void*)k_sssp_tie_lds<false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl_lds));
+    }
+    uint16_t* d_stg = nullptr;   // (STG: V states per block of the grid)
+    if (hc && stg) {
+        const size_t g = (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(chunk, n), (int64_t)ncu * bpc));
+        SHD_HIP(hipMalloc(&d_stg, g * (size_t)V * sizeof(uint16_t)));
     }
     int32_t* fpar = (int32_t*)pc->d_tie_scratch;
     bool lo = false;
@@ -1734,8 +1772,9 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         if (hc) {
             SHD_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), s));
             const int grid = std::max(1, std::min(cn, ncu * bpc));
-            hipLaunchKernelGGL(k_sssp_tie_lds, dim3(grid), dim3(64), tl_lds, s, V, cn, rows, pc->d_attached,
-                               pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar, (int32_t)hc, d_ovf);
+            hipLaunchKernelGGL(stg ? k_sssp_tie_lds<true> : k_sssp_tie_lds<false>, dim3(grid), dim3(64), tl_lds, s, V,
+                               cn, rows, pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                               (int32_t)hc, d_ovf, d_stg);
             SHD_HIP(hipGetLastError());
             SHD_HIP(hipMemcpyAsync(&nov, d_ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
             SHD_HIP(hipStreamSynchronize(s));
@@ -1783,6 +1822,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         SHD_HIP(hipGetLastError());
     }
     if (d_ovf) (void)hipFree(d_ovf);
+    if (d_stg) (void)hipFree(d_stg);
     return SHD_OK;
 }
 
