@@ -1118,11 +1118,12 @@ __global__ __launch_bounds__(kTieLanes) void k_sssp_tie_parents(
 // and lane 0 runs the heap steps igraph takes, in arc order, only for the
 // arcs that push or decrease.  A row whose heap outgrows hc is left to
 // k_sssp_tie_parents (listed in ovf).  Same parents as k_sssp_tie_parents.
-__device__ __forceinline__ void tlds_shift_up(double* hv, uint16_t* hi, uint16_t* st, int32_t elem, double val,
+template <typename HV>
+__device__ __forceinline__ void tlds_shift_up(HV* hv, uint16_t* hi, uint16_t* st, int32_t elem, HV val,
                                               int32_t id) {
     while (elem != 0) {
         const int32_t par = (elem + 1) / 2 - 1;
-        const double pv = hv[par];
+        const HV pv = hv[par];
         if (val < pv) break;
         const int32_t pid = hi[par];
         hv[elem] = pv;
@@ -1134,16 +1135,17 @@ __device__ __forceinline__ void tlds_shift_up(double* hv, uint16_t* hi, uint16_t
     hi[elem] = (uint16_t)id;
     st[id] = (uint16_t)(elem + 2);
 }
-__device__ __forceinline__ void tlds_sink(double* hv, uint16_t* hi, uint16_t* st, int32_t size, int32_t head,
-                                          double val, int32_t id) {
+template <typename HV>
+__device__ __forceinline__ void tlds_sink(HV* hv, uint16_t* hi, uint16_t* st, int32_t size, int32_t head, HV val,
+                                          int32_t id) {
     for (;;) {
         const int32_t l = 2 * head + 1, r = 2 * head + 2;
         if (l >= size) break;
-        const double dl = hv[l];
-        const double dr = r != size ? hv[r] : 0.0;
+        const HV dl = hv[l];
+        const HV dr = r != size ? hv[r] : (HV)0;
         const int32_t il = hi[l], ir = r != size ? hi[r] : 0;
         int32_t c = l, cid = il;
-        double dc = dl;
+        HV dc = dl;
         if (r != size && !(dl >= dr)) { c = r; dc = dr; cid = ir; }
         if (!(val < dc)) break;
         hv[head] = dc;
@@ -1184,7 +1186,11 @@ __device__ __forceinline__ double bcast_d(double v, int lane) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
         }                                                            \
     } while (0)
-template <bool STG>
+// HV: the heap's values (-distance): double, or int32_t where every arc weight
+// is a whole number and V x the largest stays below 2^30 (shd_pc::w_int) --
+// then every distance igraph's doubles hold is an exact integer of that range,
+// the same order and ties, and a heap entry takes 6 B instead of 10
+template <bool STG, typename HV>
 __global__ __launch_bounds__(64) void k_sssp_tie_lds(
     int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
@@ -1192,7 +1198,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
     uint16_t* __restrict__ stg) {
     extern __shared__ __align__(16) char tsm[];
     uint16_t* st = STG ? stg + (size_t)blockIdx.x * V : (uint16_t*)tsm;
-    double* hv = (double*)(tsm + (STG ? 0 : (((size_t)2 * V + 15) & ~(size_t)15)));
+    HV* hv = (HV*)(tsm + (STG ? 0 : (((size_t)2 * V + 15) & ~(size_t)15)));
     uint16_t* hi = (uint16_t*)(hv + hc);
     const int lane = (int)threadIdx.x;
     for (int32_t slot = (int32_t)blockIdx.x; slot < n; slot += (int32_t)gridDim.x) {
@@ -1205,7 +1211,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
         const int32_t src = attached[rows[slot]];
         int32_t size = 1;
         if (lane == 0) {
-            hv[0] = 0.0;
+            hv[0] = (HV)0;
             hi[0] = (uint16_t)src;
             st[src] = 2;
         }
@@ -1226,7 +1232,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
             double md0 = 0.0;
             if (lane == 0) {
                 u0 = hi[0];
-                md0 = -hv[0];
+                md0 = -(double)hv[0];
                 size--;
                 if (size > 0) tlds_sink(hv, hi, st, size, 0, hv[size], hi[size]);
                 st[u0] = 1;
@@ -1248,7 +1254,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                 uint32_t sx = 1;
                 if (valid) {
                     sx = st[x];
-                    if (sx >= 2) cur = -hv[sx - 2];
+                    if (sx >= 2) cur = -(double)hv[sx - 2];
                 }
                 const int32_t cnt = ke - c0 < 64 ? ke - c0 : 64;
                 bool dup = false;   // an earlier arc of this chunk to the same vertex
@@ -1269,13 +1275,13 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
                         if (sj == 0) {   // the first finite distance: push
                             if (size >= hc) { ovfl = 1; break; }
                             par[xj] = rj;
-                            tlds_shift_up(hv, hi, st, size, -aj, xj);
+                            tlds_shift_up(hv, hi, st, size, (HV)(-aj), xj);
                             size++;
                         } else if (sj >= 2) {   // strictly shorter: igraph_2wheap_modify
                             const int32_t pos = (int32_t)sj - 2;
-                            if (aj < -hv[pos]) {
+                            if (aj < -(double)hv[pos]) {
                                 par[xj] = rj;
-                                tlds_sink(hv, hi, st, size, pos, -aj, xj);
+                                tlds_sink(hv, hi, st, size, pos, (HV)(-aj), xj);
                                 tlds_shift_up(hv, hi, st, pos, hv[pos], hi[pos]);
                             }
                         }
@@ -1604,6 +1610,16 @@ extern "C" int shd_pc_create(const shd_graph* g, const int32_t* attached, int32_
     // per in-arc: the edge's reliability factor 1 - loss ((double)1.0f - loss, topology.c:437)
     std::vector<double> rin_r((size_t)na + 1);
     for (int32_t a = 0; a < na; a++) rin_r[a] = (double)1.0f - g->edge_loss[c.rin_eid[a]];
+    {   // whole-number weights with V x the largest below 2^30: the tie kernel's 4-B heap values
+        double wmax = 0.0;
+        bool wi = true;
+        for (int32_t k = 0; k < na && wi; k++) {
+            const double w = c.arc_w[k];
+            wi = std::isfinite(w) && w >= 0.0 && w == std::floor(w);
+            wmax = w > wmax ? w : wmax;
+        }
+        pc->w_int = wi && wmax * (double)V < (double)(1 << 30);
+    }
     if ((rc = dalloc_copy(&pc->d_arc_off, c.arc_off, V + 1)) || (rc = dalloc_copy(&pc->d_arc_dst, c.arc_dst, na)) ||
         (rc = dalloc_copy(&pc->d_arc_w, c.arc_w, na)) || (rc = dalloc_copy(&pc->d_rin_off, c.rin_off, V + 1)) ||
         (rc = dalloc_copy(&pc->d_rin_src, c.rin_src, na)) || (rc = dalloc_copy(&pc->d_rin_eid, c.rin_eid, na)) ||
@@ -1716,12 +1732,13 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     // STG: the states in global scratch and LDS for the heap only, where that
     // puts more rows on a CU (SHD_PC_TIE_STG=0 / 1 forces either)
     int hc = 0, bpc = 0;
-    bool stg = false;
+    bool stg = false, hv4 = false;
     if (V <= 65533 && !getenv("SHD_PC_TIE_GLOBAL")) {
         const char* hc_env = getenv("SHD_PC_TIE_HC");
         const char* stg_env = getenv("SHD_PC_TIE_STG");
         hc = std::max(64, std::min(hc_env ? atoi(hc_env) : 1024, std::min(V, 65533)));
-        const int bpc_g = (int)std::min<size_t>(16, std::max<size_t>(1, kLdsMax / ((size_t)hc * 10)));
+        hv4 = pc->w_int && !getenv("SHD_PC_TIE_HV8");   // (4-B heap values with STG only)
+        const int bpc_g = (int)std::min<size_t>(32, std::max<size_t>(1, kLdsMax / ((size_t)hc * (hv4 ? 6 : 10))));
         int hc_l = hc;
         if (st_bytes + (size_t)hc_l * 10 > kLdsMax)
             hc_l = (int)std::min<size_t>(std::min(V, 65533), (kLdsMax - std::min(kLdsMax, st_bytes)) / 10);
@@ -1732,10 +1749,13 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         } else {
             hc = hc_l;
             bpc = bpc_l;
+            hv4 = false;
         }
         if (!bpc) hc = 0;
     }
-    const size_t tl_lds = (stg ? 0 : st_bytes) + (size_t)hc * 10;
+    const size_t tl_lds = (stg ? 0 : st_bytes) + (size_t)hc * (hv4 ? 6 : 10);
+    const void* tie_fn = stg ? (hv4 ? (const void*)k_sssp_tie_lds<true, int32_t> : (const void*)k_sssp_tie_lds<true, double>)
+                             : (const void*)k_sssp_tie_lds<false, double>;
     // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
     // scratch per vertex and row; <= 4 GiB a chunk (every row of a 10 k-vertex
     // graph at once)
@@ -1754,8 +1774,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     int32_t* d_ovf = nullptr;
     if (hc) {   // [0]: the count, then the slots of the rows whose heap outgrew hc
         SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t) * (1 + (size_t)chunk)));
-        SHD_HIP(hipFuncSetAttribute(stg ? (const void*)k_sssp_tie_lds<true> : (const void*)k_sssp_tie_lds<false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl_lds));
+        SHD_HIP(hipFuncSetAttribute(tie_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl_lds));
     }
     uint16_t* d_stg = nullptr;   // (STG: V states per block of the grid)
     if (hc && stg) {
@@ -1771,10 +1790,23 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         int32_t nov = hc ? 0 : cn;   // rows for the lane heaps (all of them without k_sssp_tie_lds)
         if (hc) {
             SHD_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), s));
-            const int grid = std::max(1, std::min(cn, ncu * bpc));
-            hipLaunchKernelGGL(stg ? k_sssp_tie_lds<true> : k_sssp_tie_lds<false>, dim3(grid), dim3(64), tl_lds, s, V,
-                               cn, rows, pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
-                               (int32_t)hc, d_ovf, d_stg);
+            // as many rows for every block (the grid strides over the rows): 10 000 rows
+            // on 6 656 slots ran as a full pass and a half-empty one (SHD_PC_TIE_FILL: all slots)
+            const int cap = std::max(1, std::min(cn, ncu * bpc));
+            const int per = (cn + cap - 1) / cap;
+            const int grid = getenv("SHD_PC_TIE_FILL") ? cap : (cn + per - 1) / per;
+            if (stg && hv4)
+                hipLaunchKernelGGL((k_sssp_tie_lds<true, int32_t>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, d_stg);
+            else if (stg)
+                hipLaunchKernelGGL((k_sssp_tie_lds<true, double>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, d_stg);
+            else
+                hipLaunchKernelGGL((k_sssp_tie_lds<false, double>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, d_stg);
             SHD_HIP(hipGetLastError());
             SHD_HIP(hipMemcpyAsync(&nov, d_ovf, sizeof(int32_t), hipMemcpyDeviceToHost, s));
             SHD_HIP(hipStreamSynchronize(s));

@@ -69,6 +69,7 @@ struct shd_pc {
     size_t tie_scratch_bytes = 0;
     void* d_tie_lane = nullptr;         // k_sssp_tie_parents' lane heaps (rows whose heap outgrew LDS)
     size_t tie_lane_bytes = 0;
+    bool w_int = false;                 // whole-number arc weights, V x the largest < 2^30 (4-B tie heap values)
     int64_t* d_stats = nullptr;         // ties, max hops, max iters, unroutable, lat mismatch, minlat bits, tie rows
     bool built = false;
     shd_pc_info info{};
