@@ -1790,11 +1790,11 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         int32_t nov = hc ? 0 : cn;   // rows for the lane heaps (all of them without k_sssp_tie_lds)
         if (hc) {
             SHD_HIP(hipMemsetAsync(d_ovf, 0, sizeof(int32_t), s));
-            // as many rows for every block (the grid strides over the rows): 10 000 rows
-            // on 6 656 slots ran as a full pass and a half-empty one (SHD_PC_TIE_FILL: all slots)
-            const int cap = std::max(1, std::min(cn, ncu * bpc));
-            const int per = (cn + cap - 1) / cap;
-            const int grid = getenv("SHD_PC_TIE_FILL") ? cap : (cn + per - 1) / per;
+            // every slot filled (the grid strides over the rows): as many rows for every
+            // block instead (10 000 rows on 5 000 blocks, not 6 656) ran 186 against 168 ms
+            // -- a row's time grows little with the rows beside it on the CU
+            // (profiles/r06/tiefill)
+            const int grid = std::max(1, std::min(cn, ncu * bpc));
             if (stg && hv4)
                 hipLaunchKernelGGL((k_sssp_tie_lds<true, int32_t>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
                                    pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
