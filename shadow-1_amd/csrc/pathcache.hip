@@ -1313,6 +1313,232 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
 }
 #undef TIE_WAVE_SYNC
 
+// The same Dijkstra with no vertex -> heap position map at all (round 6,
+// SHD_PC_TIE_KIND=g; k_sssp_tie_lds<true> kept that map in global scratch and
+// stored a vertex's new position at every step of every sift, then waited for
+// those stores before the next pop's arcs could read it).  Per vertex, in the
+// block's slice of global scratch, only what changes at a push or a decrease:
+// its state (0 unreached, 2 reached) and its heap value (-distance).  A popped
+// vertex keeps state 2 and its final value: an arc from the popped vertex u
+// (d(u) >= every popped distance) gives alt = d(u) + w >= that value, never
+// igraph's "strictly shorter", exactly as the popped state did.  So the sifts
+// touch LDS only, a pop's arcs and their targets' entries are loaded before
+// the pop's sink (nothing in them changes at a pop), and a decrease finds its
+// vertex's heap position by a search of the heap's vertex array by the whole
+// wave (<= hc / 64 LDS reads a lane).  Same parents as k_sssp_tie_lds.
+template <typename HV>
+struct TieG {
+    HV negd;       // the heap value (-distance) at its last push / decrease
+    uint32_t st;   // 0 unreached, 2 reached
+};
+template <typename HV>
+__device__ __forceinline__ void tg_shift_up(HV* hv, uint16_t* hi, int32_t elem, HV val, int32_t id) {
+    while (elem != 0) {
+        const int32_t par = (elem + 1) / 2 - 1;
+        const HV pv = hv[par];
+        if (val < pv) break;
+        hv[elem] = pv;
+        hi[elem] = hi[par];
+        elem = par;
+    }
+    hv[elem] = val;
+    hi[elem] = (uint16_t)id;
+}
+template <typename HV>
+__device__ __forceinline__ void tg_sink(HV* hv, uint16_t* hi, int32_t size, int32_t head, HV val, int32_t id) {
+    for (;;) {
+        const int32_t l = 2 * head + 1, r = 2 * head + 2;
+        if (l >= size) break;
+        const HV dl = hv[l];
+        const HV dr = r != size ? hv[r] : (HV)0;
+        int32_t c = l;
+        HV dc = dl;
+        if (r != size && !(dl >= dr)) { c = r; dc = dr; }
+        if (!(val < dc)) break;
+        hv[head] = dc;
+        hi[head] = hi[c];
+        head = c;
+    }
+    hv[head] = val;
+    hi[head] = (uint16_t)id;
+}
+template <typename HV>
+__device__ __forceinline__ TieG<HV> tg_load(const TieG<HV>* g, int32_t x) {
+    return g[x];
+}
+#define TG_WG_SYNC()                                             \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   \
+    } while (0)
+#define TG_WAVE_SYNC()                                           \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
+    } while (0)
+// per arc: does an earlier arc of its source's list, in the same 64-arc chunk
+// (chunks from the list's start), go to the same vertex (a parallel edge the
+// tie kernel's chunk must take in order); computed once per tied build
+__global__ void k_arc_dup(int32_t na, const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_src,
+                          const int32_t* __restrict__ arc_dst, uint8_t* __restrict__ dup) {
+    const int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k >= na) return;
+    const int32_t kb = arc_off[arc_src[k]];
+    const int32_t c0 = kb + ((k - kb) & ~63);
+    const int32_t x = arc_dst[k];
+    uint8_t d = 0;
+    for (int32_t j = c0; j < k; j++) d |= arc_dst[j] == x ? 1 : 0;
+    dup[k] = d;
+}
+template <typename HV>
+__global__ __launch_bounds__(64) void k_sssp_tie_g(
+    int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
+    const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
+    const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf,
+    TieG<HV>* __restrict__ gsc, const uint8_t* __restrict__ arc_dup) {
+    extern __shared__ __align__(16) char tsm[];
+    TieG<HV>* g = gsc + (size_t)blockIdx.x * V;
+    HV* hv = (HV*)tsm;
+    uint16_t* hi = (uint16_t*)(hv + hc);
+    const int lane = (int)threadIdx.x;
+    for (int32_t slot = (int32_t)blockIdx.x; slot < n; slot += (int32_t)gridDim.x) {
+        int32_t* par = fpar + (size_t)slot * V;
+        for (int32_t v = lane; v < V; v += 64) {
+            g[v].st = 0u;
+            par[v] = -1;
+        }
+        const int32_t src = attached[rows[slot]];
+        int32_t size = 1;
+        if (lane == 0) {
+            hv[0] = (HV)0;
+            hi[0] = (uint16_t)src;
+        }
+        TG_WG_SYNC();
+        if (lane == 0) g[src] = TieG<HV>{(HV)0, 2u};
+        TG_WG_SYNC();
+        int ovfl = 0;
+        // the next pop's first chunk of arcs and their targets' entries
+        int32_t pkb = arc_off[src], pke = arc_off[src + 1];
+        int32_t px = -1, prin = 0, pdup = 0;
+        double pw = 0.0;
+        TieG<HV> pg{(HV)0, 1u};
+        if (pkb + lane < pke) {
+            px = arc_dst[pkb + lane];
+            pw = arc_w[pkb + lane];
+            prin = arc_rin[pkb + lane];
+            pdup = arc_dup[pkb + lane];
+            pg = tg_load(g, px);
+        }
+        while (size > 0 && !ovfl) {
+            // the pop (igraph_2wheap_max_index + delete_max), by lane 0
+            double md0 = 0.0;
+            if (lane == 0) {
+                md0 = -(double)hv[0];
+                size--;
+                if (size > 0) tg_sink(hv, hi, size, 0, hv[size], (int32_t)hi[size]);
+            }
+            const double md = bcast_d(md0, 0);
+            size = __builtin_amdgcn_readfirstlane(size);
+            TG_WAVE_SYNC();
+            const int32_t kb = pkb, ke = pke;
+            for (int32_t c0 = kb; c0 < ke && !ovfl; c0 += 64) {
+                const int32_t k = c0 + lane;
+                const bool valid = k < ke;
+                int32_t x = -1, rin = 0, xd = 0;
+                double w = 0.0;
+                TieG<HV> gx{(HV)0, 1u};
+                if (c0 == kb) { x = px; w = pw; rin = prin; gx = pg; xd = pdup; }
+                else if (valid) { x = arc_dst[k]; w = arc_w[k]; rin = arc_rin[k]; xd = arc_dup[k]; gx = tg_load(g, x); }
+                const double alt = md + w;
+                const bool dup = valid && xd != 0;   // an earlier arc of this chunk to the same vertex (k_arc_dup)
+                uint64_t m = __ballot(valid && (dup || gx.st == 0u || (gx.st == 2u && alt < -(double)gx.negd)));
+                const uint64_t mdup = __ballot(dup);
+                // every lane runs the candidates (uniform: m), lane 0 the heap steps
+                while (m) {
+                    const int j = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int32_t xj = __builtin_amdgcn_readlane(x, j);
+                    const double aj = bcast_d(alt, j);
+                    const int32_t rj = __builtin_amdgcn_readlane(rin, j);
+                    uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)gx.st, j);
+                    double cj = -(double)(HV)0;
+                    {
+                        HV nj;
+                        if (sizeof(HV) == 4) {
+                            nj = (HV)__builtin_amdgcn_readlane((int)gx.negd, j);
+                        } else {
+                            nj = (HV)bcast_d((double)gx.negd, j);
+                        }
+                        cj = -(double)nj;
+                    }
+                    if ((mdup >> j) & 1ull) {   // a target an earlier arc of this chunk changed: lane 0's own stores
+                        uint32_t s0 = 0u;
+                        double c0v = 0.0;
+                        if (lane == 0) {
+                            const TieG<HV> e = g[xj];
+                            s0 = e.st;
+                            c0v = -(double)e.negd;
+                        }
+                        sj = (uint32_t)__builtin_amdgcn_readfirstlane((int)s0);
+                        cj = bcast_d(c0v, 0);
+                    }
+                    if (sj == 0u) {   // the first finite distance: push
+                        if (size >= hc) { ovfl = 1; break; }
+                        if (lane == 0) {
+                            par[xj] = rj;
+                            tg_shift_up(hv, hi, size, (HV)(-aj), xj);
+                            g[xj] = TieG<HV>{(HV)(-aj), 2u};
+                        }
+                        size++;
+                        TG_WAVE_SYNC();
+                    } else if (aj < cj) {   // strictly shorter: igraph_2wheap_modify
+                        // its heap position: the wave searches the heap's vertices
+                        int32_t f = -1;
+                        for (int32_t i = lane; i < size; i += 64)
+                            if ((int32_t)hi[i] == xj) f = i;
+                        const uint64_t fm = __ballot(f >= 0);
+                        const int32_t pos = fm ? __builtin_amdgcn_readlane(f, __builtin_ctzll(fm)) : -1;
+                        if (lane == 0 && pos >= 0) {
+                            par[xj] = rj;
+                            tg_sink(hv, hi, size, pos, (HV)(-aj), xj);
+                            tg_shift_up(hv, hi, pos, hv[pos], (int32_t)hi[pos]);
+                            g[xj].negd = (HV)(-aj);
+                        }
+                        if (pos < 0) ovfl = 2;   // (never: a reached vertex with a larger value is in the heap)
+                        TG_WAVE_SYNC();
+                    }
+                }
+                ovfl = __builtin_amdgcn_readfirstlane(ovfl);
+                TG_WG_SYNC();   // the chunk's stores before the next loads of the entries
+            }
+            // the next pop's vertex (the top now), its first chunk of arcs and their
+            // entries, issued before its sink
+            int32_t t0 = -1;
+            if (lane == 0 && size > 0) t0 = hi[0];
+            const int32_t top = __builtin_amdgcn_readfirstlane(t0);
+            if (top >= 0 && !ovfl) {
+                pkb = arc_off[top];
+                pke = arc_off[top + 1];
+                px = -1;
+                pg = TieG<HV>{(HV)0, 1u};
+                if (pkb + lane < pke) {
+                    px = arc_dst[pkb + lane];
+                    pw = arc_w[pkb + lane];
+                    prin = arc_rin[pkb + lane];
+                    pdup = arc_dup[pkb + lane];
+                    pg = tg_load(g, px);
+                }
+            }
+        }
+        if (ovfl && lane == 0) ovf[1 + atomicAdd(ovf, 1)] = slot;
+        TG_WG_SYNC();
+    }
+}
+#undef TG_WG_SYNC
+#undef TG_WAVE_SYNC
+
 // ------------------------------------------------------------------ direct
 // _topology_lookupDirectPath (topology.c:1877-1927) for every attached pair;
 // igraph_get_eid through the (neighbour, eid)-sorted lists (lowest parallel eid)
@@ -1754,7 +1980,12 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         if (!bpc) hc = 0;
     }
     const size_t tl_lds = (stg ? 0 : st_bytes) + (size_t)hc * (hv4 ? 6 : 10);
-    const void* tie_fn = stg ? (hv4 ? (const void*)k_sssp_tie_lds<true, int32_t> : (const void*)k_sssp_tie_lds<true, double>)
+    // with the states out of LDS: k_sssp_tie_g (no position map) unless
+    // SHD_PC_TIE_KIND=st (k_sssp_tie_lds<true>: the position map in global scratch)
+    const char* kind_env = getenv("SHD_PC_TIE_KIND");
+    const bool tg = stg && !(kind_env && strcmp(kind_env, "st") == 0);
+    const void* tie_fn = tg ? (hv4 ? (const void*)k_sssp_tie_g<int32_t> : (const void*)k_sssp_tie_g<double>)
+                       : stg ? (hv4 ? (const void*)k_sssp_tie_lds<true, int32_t> : (const void*)k_sssp_tie_lds<true, double>)
                              : (const void*)k_sssp_tie_lds<false, double>;
     // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
     // scratch per vertex and row; <= 4 GiB a chunk (every row of a 10 k-vertex
@@ -1779,7 +2010,20 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     uint16_t* d_stg = nullptr;   // (STG: V states per block of the grid)
     if (hc && stg) {
         const size_t g = (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(chunk, n), (int64_t)ncu * bpc));
-        SHD_HIP(hipMalloc(&d_stg, g * (size_t)V * sizeof(uint16_t)));
+        SHD_HIP(hipMalloc(&d_stg, g * (size_t)V * (tg ? (hv4 ? sizeof(TieG<int32_t>) : sizeof(TieG<double>))
+                                                     : sizeof(uint16_t))));
+    }
+    uint8_t* d_dup = nullptr;   // (k_sssp_tie_g: the arcs' repeated-target flags)
+    if (hc && tg) {
+        int32_t na = 0;
+        SHD_HIP(hipMemcpyAsync(&na, pc->d_arc_off + V, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        SHD_HIP(hipStreamSynchronize(s));
+        SHD_HIP(hipMalloc(&d_dup, (size_t)na + 1));
+        if (na > 0) {
+            hipLaunchKernelGGL(k_arc_dup, dim3((na + 255) / 256), dim3(256), 0, s, na, pc->d_arc_off, pc->d_arc_src,
+                               pc->d_arc_dst, d_dup);
+            SHD_HIP(hipGetLastError());
+        }
     }
     int32_t* fpar = (int32_t*)pc->d_tie_scratch;
     bool lo = false;
@@ -1795,7 +2039,15 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
             // -- a row's time grows little with the rows beside it on the CU
             // (profiles/r06/tiefill)
             const int grid = std::max(1, std::min(cn, ncu * bpc));
-            if (stg && hv4)
+            if (tg && hv4)
+                hipLaunchKernelGGL((k_sssp_tie_g<int32_t>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, (TieG<int32_t>*)d_stg, d_dup);
+            else if (tg)
+                hipLaunchKernelGGL((k_sssp_tie_g<double>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, (TieG<double>*)d_stg, d_dup);
+            else if (stg && hv4)
                 hipLaunchKernelGGL((k_sssp_tie_lds<true, int32_t>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
                                    pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
                                    (int32_t)hc, d_ovf, d_stg);
@@ -1855,6 +2107,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     }
     if (d_ovf) (void)hipFree(d_ovf);
     if (d_stg) (void)hipFree(d_stg);
+    if (d_dup) (void)hipFree(d_dup);
     return SHD_OK;
 }
 
