@@ -1331,14 +1331,19 @@ struct TieG {
     HV negd;       // the heap value (-distance) at its last push / decrease
     uint32_t st;   // 0 unreached, 2 reached
 };
+// (a level's reads go out together -- both children's values and vertices,
+// the right child's even where it is past the end: k_sssp_tie_g holds at most
+// hc - 1 entries, so that slot is still the heap's -- so a level costs one LDS
+// round trip, not three)
 template <typename HV>
 __device__ __forceinline__ void tg_shift_up(HV* hv, uint16_t* hi, int32_t elem, HV val, int32_t id) {
     while (elem != 0) {
         const int32_t par = (elem + 1) / 2 - 1;
         const HV pv = hv[par];
+        const uint16_t pid = hi[par];
         if (val < pv) break;
         hv[elem] = pv;
-        hi[elem] = hi[par];
+        hi[elem] = pid;
         elem = par;
     }
     hv[elem] = val;
@@ -1349,14 +1354,14 @@ __device__ __forceinline__ void tg_sink(HV* hv, uint16_t* hi, int32_t size, int3
     for (;;) {
         const int32_t l = 2 * head + 1, r = 2 * head + 2;
         if (l >= size) break;
-        const HV dl = hv[l];
-        const HV dr = r != size ? hv[r] : (HV)0;
-        int32_t c = l;
-        HV dc = dl;
-        if (r != size && !(dl >= dr)) { c = r; dc = dr; }
+        const HV dl = hv[l], dr = hv[r];
+        const uint16_t il = hi[l], ir = hi[r];
+        const bool right = r != size && !(dl >= dr);
+        const int32_t c = right ? r : l;
+        const HV dc = right ? dr : dl;
         if (!(val < dc)) break;
         hv[head] = dc;
-        hi[head] = hi[c];
+        hi[head] = right ? ir : il;
         head = c;
     }
     hv[head] = val;
@@ -1485,7 +1490,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
                         cj = bcast_d(c0v, 0);
                     }
                     if (sj == 0u) {   // the first finite distance: push
-                        if (size >= hc) { ovfl = 1; break; }
+                        if (size >= hc - 1) { ovfl = 1; break; }   // (hc - 1: tg_sink's read of a right child)
                         if (lane == 0) {
                             par[xj] = rj;
                             tg_shift_up(hv, hi, size, (HV)(-aj), xj);
@@ -1521,8 +1526,8 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
             if (top >= 0 && !ovfl) {
                 pkb = arc_off[top];
                 pke = arc_off[top + 1];
-                px = -1;
-                pg = TieG<HV>{(HV)0, 1u};
+                // (no defaults for the lanes past the list: `valid` masks them, and a
+                // register reset here would wait for every store of the pop first)
                 if (pkb + lane < pke) {
                     px = arc_dst[pkb + lane];
                     pw = arc_w[pkb + lane];
