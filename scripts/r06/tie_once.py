@@ -1,0 +1,17 @@
+"""One path-cache build of the 10 k whole-millisecond geometric graph (every row ties): the
+tie kernel's profiling target (rocprofv3 --pmc / --kernel-trace)."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(REPO, "shadow-1_amd"))
+import numpy as np  # noqa: E402
+
+import workloads as W  # noqa: E402
+from sim import PathCache  # noqa: E402
+
+g = W.geometric_graph(10000, seed=1, integer_latency=True)
+pc = PathCache(g, np.arange(10000, dtype=np.int32))
+i = pc.info()
+print("build_ms", round(i.build_ms_device, 3), "tie_rows", i.n_tie_rows, flush=True)
+pc.close()
