@@ -53,6 +53,12 @@ extern "C" int shd_device_count(int* n) {
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ double u2d(uint64_t u) { return __longlong_as_double((long long)u); }
 __device__ __forceinline__ uint64_t d2u(double d) { return (uint64_t)__double_as_longlong(d); }
+// k_sssp_tie_g's per-vertex entry of a row (there: why no heap position)
+template <typename HV>
+struct TieG {
+    HV negd;       // the heap value (-distance) at its last push / decrease
+    uint32_t st;   // 0 unreached, 2 reached
+};
 
 // reliability factor of a vertex whose packetloss attribute is present
 // (_topology_findVertexAttributeDouble: NaN means absent, topology.c:330-347)
@@ -624,7 +630,11 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const double* __restrict__ vloss, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, int32_t row0, int32_t row1, const int32_t* __restrict__ row_list,
-    const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows, int mode /* bit 0 LDS offsets, 1 queued */) {
+    const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows, int mode /* bit 0 LDS offsets, 1 queued */,
+    const char* __restrict__ gdist, int gkind, const uint8_t* __restrict__ gok) {
+    // gdist (round 6): the tied rows' distances from k_sssp_tie_g's per-row entries
+    // (gkind 4: TieG<int32_t>, 8: TieG<double>), for the rows gok marks complete --
+    // no Bellman-Ford again for them, only the properties over the given parents
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int ldsoff = mode & 1;
     uint64_t* dist = (uint64_t*)smem;
@@ -654,11 +664,28 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     // row_list: the second pass over listed rows [row0, row1) of it, parents from fpar
     for (int32_t i = row0 + (int32_t)blockIdx.x; i < row1; i += gridDim.x) {
         const int32_t row = row_list ? row_list[i] : i;
+        int bf_it = -1;
+        if (gdist && gok[i - row0]) {   // (0.0 - value: +0.0 at the source, as the Bellman-Ford's)
+            const size_t r = (size_t)(i - row0) * V;
+            for (int32_t v = (int32_t)threadIdx.x; v < V; v += BLOCK) {
+                uint64_t d = kDistInf;
+                if (gkind == 4) {
+                    const TieG<int32_t> e = ((const TieG<int32_t>*)gdist)[r + v];
+                    if (e.st == 2u) d = d2u(0.0 - (double)e.negd);
+                } else {
+                    const TieG<double> e = ((const TieG<double>*)gdist)[r + v];
+                    if (e.st == 2u) d = d2u(0.0 - e.negd);
+                }
+                dist[v] = d;
+            }
+            bf_it = 0;
+            __syncthreads();
+        }
         sssp_one_row<BLOCK>(row, attached[row], V, T, arc_off, arc_dst, arc_w, arc_src, arc_rin, rin_off, rin_src,
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
-                            fl_beg, fl_dv, off16, cbase, (mode & 2) != 0);
+                            fl_beg, fl_dv, off16, cbase, (mode & 2) != 0, bf_it);
     }
 }
 
@@ -1326,15 +1353,19 @@ __global__ __launch_bounds__(64) void k_sssp_tie_lds(
 // the pop's sink (nothing in them changes at a pop), and a decrease finds its
 // vertex's heap position by a search of the heap's vertex array by the whole
 // wave (<= hc / 64 LDS reads a lane).  Same parents as k_sssp_tie_lds.
-template <typename HV>
-struct TieG {
-    HV negd;       // the heap value (-distance) at its last push / decrease
-    uint32_t st;   // 0 unreached, 2 reached
-};
 // (a level's reads go out together -- both children's values and vertices,
 // the right child's even where it is past the end: k_sssp_tie_g holds at most
 // hc - 1 entries, so that slot is still the heap's -- so a level costs one LDS
 // round trip, not three)
+// (dz: a zero the compiler cannot see through -- a VGPR from inline asm -- so
+// that the index arithmetic of lane 0's sifts stays in VALU instead of being
+// scalarized: the one scalar unit of a CU serialised the sifts of all 26
+// rows on it (SQ_ACTIVE_INST_SCA ~ 68 % of the CU's cycles, profiles/r06/tiepmc))
+__device__ __forceinline__ int32_t tg_vzero() {
+    int32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
 template <typename HV>
 __device__ __forceinline__ void tg_shift_up(HV* hv, uint16_t* hi, int32_t elem, HV val, int32_t id) {
     while (elem != 0) {
@@ -1363,6 +1394,43 @@ __device__ __forceinline__ void tg_sink(HV* hv, uint16_t* hi, int32_t size, int3
         hv[head] = dc;
         hi[head] = right ? ir : il;
         head = c;
+    }
+    hv[head] = val;
+    hi[head] = (uint16_t)id;
+}
+// The same sifts for VH: the index arithmetic in VALU (the positions come in
+// derived from tg_vzero), and every exit test made uniform by reading lane 0's
+// outcome into a scalar (readfirstlane) -- a divergent loop would spend as
+// many scalar instructions on its exec masks as the scalarized one spends on
+// the arithmetic
+template <typename HV>
+__device__ __forceinline__ void tg_shift_up_v(HV* hv, uint16_t* hi, int32_t elem, HV val, int32_t id) {
+    for (;;) {
+        if (!__builtin_amdgcn_readfirstlane((int)(elem != 0))) break;
+        const int32_t par = (elem + 1) / 2 - 1;
+        const HV pv = hv[par];
+        const uint16_t pid = hi[par];
+        if (__builtin_amdgcn_readfirstlane((int)(val < pv))) break;
+        hv[elem] = pv;
+        hi[elem] = pid;
+        elem = par;
+    }
+    hv[elem] = val;
+    hi[elem] = (uint16_t)id;
+}
+template <typename HV>
+__device__ __forceinline__ void tg_sink_v(HV* hv, uint16_t* hi, int32_t size, int32_t head, HV val, int32_t id) {
+    for (;;) {
+        const int32_t l = 2 * head + 1, r = 2 * head + 2;
+        if (!__builtin_amdgcn_readfirstlane((int)(l < size))) break;
+        const HV dl = hv[l], dr = hv[r];
+        const uint16_t il = hi[l], ir = hi[r];
+        const bool right = r != size && !(dl >= dr);
+        const HV dc = right ? dr : dl;
+        if (!__builtin_amdgcn_readfirstlane((int)(val < dc))) break;
+        hv[head] = dc;
+        hi[head] = right ? ir : il;
+        head = right ? r : l;
     }
     hv[head] = val;
     hi[head] = (uint16_t)id;
@@ -1397,19 +1465,21 @@ __global__ void k_arc_dup(int32_t na, const int32_t* __restrict__ arc_off, const
     for (int32_t j = c0; j < k; j++) d |= arc_dst[j] == x ? 1 : 0;
     dup[k] = d;
 }
-template <typename HV>
+template <typename HV, bool VH>
 __global__ __launch_bounds__(64) void k_sssp_tie_g(
     int32_t V, int32_t n, const int32_t* __restrict__ rows, const int32_t* __restrict__ attached,
     const int32_t* __restrict__ arc_off, const int32_t* __restrict__ arc_dst, const double* __restrict__ arc_w,
     const int32_t* __restrict__ arc_rin, int32_t* __restrict__ fpar, int32_t hc, int32_t* __restrict__ ovf,
-    TieG<HV>* __restrict__ gsc, const uint8_t* __restrict__ arc_dup) {
+    TieG<HV>* __restrict__ gsc, const uint8_t* __restrict__ arc_dup, uint8_t* __restrict__ gok) {
+    // gsc: V entries per ROW of the chunk (they are the row's distances for the
+    // second pass, k_sssp_rows_lds's gdist); gok[slot]: the row ran to its end
     extern __shared__ __align__(16) char tsm[];
-    TieG<HV>* g = gsc + (size_t)blockIdx.x * V;
     HV* hv = (HV*)tsm;
     uint16_t* hi = (uint16_t*)(hv + hc);
     const int lane = (int)threadIdx.x;
     for (int32_t slot = (int32_t)blockIdx.x; slot < n; slot += (int32_t)gridDim.x) {
         int32_t* par = fpar + (size_t)slot * V;
+        TieG<HV>* g = gsc + (size_t)slot * V;
         for (int32_t v = lane; v < V; v += 64) {
             g[v].st = 0u;
             par[v] = -1;
@@ -1442,24 +1512,48 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
             if (lane == 0) {
                 md0 = -(double)hv[0];
                 size--;
-                if (size > 0) tg_sink(hv, hi, size, 0, hv[size], (int32_t)hi[size]);
+                const int32_t dz = VH ? tg_vzero() : 0;
+                if (size > 0) {
+                    if (VH) tg_sink_v(hv, hi, size, dz, hv[size + dz], (int32_t)hi[size + dz]);
+                    else tg_sink(hv, hi, size, 0, hv[size], (int32_t)hi[size]);
+                }
             }
             const double md = bcast_d(md0, 0);
             size = __builtin_amdgcn_readfirstlane(size);
             TG_WAVE_SYNC();
             const int32_t kb = pkb, ke = pke;
+            // (every chunk's arcs and entries come through the same registers, p*: a
+            // later chunk's are loaded after the previous chunk's stores, as the next
+            // pop's are -- one set of load targets, so no wait for them lands in the
+            // sifts)
             for (int32_t c0 = kb; c0 < ke && !ovfl; c0 += 64) {
-                const int32_t k = c0 + lane;
-                const bool valid = k < ke;
-                int32_t x = -1, rin = 0, xd = 0;
-                double w = 0.0;
-                TieG<HV> gx{(HV)0, 1u};
-                if (c0 == kb) { x = px; w = pw; rin = prin; gx = pg; xd = pdup; }
-                else if (valid) { x = arc_dst[k]; w = arc_w[k]; rin = arc_rin[k]; xd = arc_dup[k]; gx = tg_load(g, x); }
+                if (c0 != kb && c0 + lane < ke) {   // a later chunk's, after the previous chunk's stores
+                    const int32_t k = c0 + lane;
+                    px = arc_dst[k];
+                    pw = arc_w[k];
+                    prin = arc_rin[k];
+                    pdup = arc_dup[k];
+                    pg = tg_load(g, px);
+                }
+                const bool valid = c0 + lane < ke;
+                const int32_t x = px, rin = prin, xd = pdup;
+                const double w = pw;
+                const TieG<HV> gx = pg;
                 const double alt = md + w;
                 const bool dup = valid && xd != 0;   // an earlier arc of this chunk to the same vertex (k_arc_dup)
                 uint64_t m = __ballot(valid && (dup || gx.st == 0u || (gx.st == 2u && alt < -(double)gx.negd)));
                 const uint64_t mdup = __ballot(dup);
+                // the entry's words copied out of the load's target registers (an asm
+                // move), so that reading them in the loop below waits for nothing --
+                // a wait there would also wait for the loop's own stores
+                uint32_t gst, gng;
+                {
+                    const uint32_t s0 = gx.st;
+                    uint32_t n0;
+                    if (sizeof(HV) == 4) n0 = (uint32_t)(int32_t)gx.negd; else n0 = 0u;
+                    asm volatile("v_mov_b32 %0, %1" : "=v"(gst) : "v"(s0));
+                    asm volatile("v_mov_b32 %0, %1" : "=v"(gng) : "v"(n0));
+                }
                 // every lane runs the candidates (uniform: m), lane 0 the heap steps
                 while (m) {
                     const int j = __builtin_ctzll(m);
@@ -1467,12 +1561,12 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
                     const int32_t xj = __builtin_amdgcn_readlane(x, j);
                     const double aj = bcast_d(alt, j);
                     const int32_t rj = __builtin_amdgcn_readlane(rin, j);
-                    uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)gx.st, j);
+                    uint32_t sj = (uint32_t)__builtin_amdgcn_readlane((int)gst, j);
                     double cj = -(double)(HV)0;
                     {
                         HV nj;
                         if (sizeof(HV) == 4) {
-                            nj = (HV)__builtin_amdgcn_readlane((int)gx.negd, j);
+                            nj = (HV)(int32_t)__builtin_amdgcn_readlane((int)gng, j);
                         } else {
                             nj = (HV)bcast_d((double)gx.negd, j);
                         }
@@ -1493,7 +1587,9 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
                         if (size >= hc - 1) { ovfl = 1; break; }   // (hc - 1: tg_sink's read of a right child)
                         if (lane == 0) {
                             par[xj] = rj;
-                            tg_shift_up(hv, hi, size, (HV)(-aj), xj);
+                            const int32_t dz = VH ? tg_vzero() : 0;
+                            if (VH) tg_shift_up_v(hv, hi, size + dz, (HV)(-aj), xj);
+                            else tg_shift_up(hv, hi, size, (HV)(-aj), xj);
                             g[xj] = TieG<HV>{(HV)(-aj), 2u};
                         }
                         size++;
@@ -1507,8 +1603,14 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
                         const int32_t pos = fm ? __builtin_amdgcn_readlane(f, __builtin_ctzll(fm)) : -1;
                         if (lane == 0 && pos >= 0) {
                             par[xj] = rj;
-                            tg_sink(hv, hi, size, pos, (HV)(-aj), xj);
-                            tg_shift_up(hv, hi, pos, hv[pos], (int32_t)hi[pos]);
+                            const int32_t dz = VH ? tg_vzero() : 0;
+                            if (VH) {
+                                tg_sink_v(hv, hi, size, pos + dz, (HV)(-aj), xj);
+                                tg_shift_up_v(hv, hi, pos + dz, hv[pos + dz], (int32_t)hi[pos + dz]);
+                            } else {
+                                tg_sink(hv, hi, size, pos, (HV)(-aj), xj);
+                                tg_shift_up(hv, hi, pos, hv[pos], (int32_t)hi[pos]);
+                            }
                             g[xj].negd = (HV)(-aj);
                         }
                         if (pos < 0) ovfl = 2;   // (never: a reached vertex with a larger value is in the heap)
@@ -1538,6 +1640,7 @@ __global__ __launch_bounds__(64) void k_sssp_tie_g(
             }
         }
         if (ovfl && lane == 0) ovf[1 + atomicAdd(ovf, 1)] = slot;
+        if (lane == 0) gok[slot] = ovfl ? 0 : 1;
         TG_WG_SYNC();
     }
 }
@@ -1989,13 +2092,16 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     // SHD_PC_TIE_KIND=st (k_sssp_tie_lds<true>: the position map in global scratch)
     const char* kind_env = getenv("SHD_PC_TIE_KIND");
     const bool tg = stg && !(kind_env && strcmp(kind_env, "st") == 0);
-    const void* tie_fn = tg ? (hv4 ? (const void*)k_sssp_tie_g<int32_t> : (const void*)k_sssp_tie_g<double>)
+    const bool vh = !getenv("SHD_PC_TIE_SHEAP");   // (the sifts in VALU; SHD_PC_TIE_SHEAP: scalarized)
+    const void* tie_fn = tg ? (hv4 ? (vh ? (const void*)k_sssp_tie_g<int32_t, true> : (const void*)k_sssp_tie_g<int32_t, false>)
+                                   : (vh ? (const void*)k_sssp_tie_g<double, true> : (const void*)k_sssp_tie_g<double, false>))
                        : stg ? (hv4 ? (const void*)k_sssp_tie_lds<true, int32_t> : (const void*)k_sssp_tie_lds<true, double>)
                              : (const void*)k_sssp_tie_lds<false, double>;
     // parents (4 B per vertex and row), and for k_sssp_tie_parents 24 B of lane
     // scratch per vertex and row; <= 4 GiB a chunk (every row of a 10 k-vertex
     // graph at once)
-    const size_t per_row = (size_t)V * 28;
+    const size_t g_entry = tg ? (hv4 ? sizeof(TieG<int32_t>) : sizeof(TieG<double>)) : 0;
+    const size_t per_row = (size_t)V * (28 + g_entry);   // (+ k_sssp_tie_g's per-row entries)
     int64_t chunk = std::max<int64_t>(kTieLanes, (int64_t)(((size_t)4 << 30) / per_row) / kTieLanes * kTieLanes);
     chunk = std::min<int64_t>(chunk, (n + kTieLanes - 1) / kTieLanes * kTieLanes);
     const size_t need_p = (size_t)chunk * V * 4;
@@ -2012,12 +2118,20 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
         SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t) * (1 + (size_t)chunk)));
         SHD_HIP(hipFuncSetAttribute(tie_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl_lds));
     }
-    uint16_t* d_stg = nullptr;   // (STG: V states per block of the grid)
+    // STG: V states per block of the grid; k_sssp_tie_g: V entries per row of a
+    // chunk, which the second pass reads as the rows' distances (d_gd; its
+    // Bellman-Ford again was 22 of the 10 k all-tied build's 105 ms;
+    // SHD_PC_TIE_NOGD: the Bellman-Ford again)
+    uint16_t* d_stg = nullptr;
+    uint8_t* d_gok = nullptr;
     if (hc && stg) {
-        const size_t g = (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(chunk, n), (int64_t)ncu * bpc));
-        SHD_HIP(hipMalloc(&d_stg, g * (size_t)V * (tg ? (hv4 ? sizeof(TieG<int32_t>) : sizeof(TieG<double>))
-                                                     : sizeof(uint16_t))));
+        const size_t g = tg ? (size_t)std::min<int64_t>(chunk, n)
+                            : (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(chunk, n), (int64_t)ncu * bpc));
+        SHD_HIP(hipMalloc(&d_stg, g * (size_t)V * (tg ? g_entry : sizeof(uint16_t))));
+        if (tg) SHD_HIP(hipMalloc(&d_gok, g));
     }
+    const char* d_gd = (tg && !getenv("SHD_PC_TIE_NOGD")) ? (const char*)d_stg : nullptr;
+    const int gkind = d_gd ? (hv4 ? 4 : 8) : 0;
     uint8_t* d_dup = nullptr;   // (k_sssp_tie_g: the arcs' repeated-target flags)
     if (hc && tg) {
         int32_t na = 0;
@@ -2044,14 +2158,22 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
             // -- a row's time grows little with the rows beside it on the CU
             // (profiles/r06/tiefill)
             const int grid = std::max(1, std::min(cn, ncu * bpc));
-            if (tg && hv4)
-                hipLaunchKernelGGL((k_sssp_tie_g<int32_t>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+            if (tg && hv4 && vh)
+                hipLaunchKernelGGL((k_sssp_tie_g<int32_t, true>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
                                    pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
-                                   (int32_t)hc, d_ovf, (TieG<int32_t>*)d_stg, d_dup);
+                                   (int32_t)hc, d_ovf, (TieG<int32_t>*)d_stg, d_dup, d_gok);
+            else if (tg && hv4)
+                hipLaunchKernelGGL((k_sssp_tie_g<int32_t, false>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, (TieG<int32_t>*)d_stg, d_dup, d_gok);
+            else if (tg && vh)
+                hipLaunchKernelGGL((k_sssp_tie_g<double, true>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                                   pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
+                                   (int32_t)hc, d_ovf, (TieG<double>*)d_stg, d_dup, d_gok);
             else if (tg)
-                hipLaunchKernelGGL((k_sssp_tie_g<double>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
+                hipLaunchKernelGGL((k_sssp_tie_g<double, false>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
                                    pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
-                                   (int32_t)hc, d_ovf, (TieG<double>*)d_stg, d_dup);
+                                   (int32_t)hc, d_ovf, (TieG<double>*)d_stg, d_dup, d_gok);
             else if (stg && hv4)
                 hipLaunchKernelGGL((k_sssp_tie_lds<true, int32_t>), dim3(grid), dim3(64), tl_lds, s, V, cn, rows,
                                    pc->d_attached, pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_rin, fpar,
@@ -2090,14 +2212,16 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
                                pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr,
-                               (lo ? 1 : 0) | bf_queue_bit());
+                               (lo ? 1 : 0) | bf_queue_bit(),
+                               (const char*)d_gd, gkind, d_gok);
         } else if (lds_rows <= kLdsMax) {
             const int grid = std::max(1, std::min(cn, ncu));
             hipLaunchKernelGGL(k_sssp_rows_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds, s, V, T, pc->d_arc_off,
                                pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin, pc->d_rin_off, pc->d_rin_src,
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
                                pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr,
-                               (lo ? 1 : 0) | bf_queue_bit());
+                               (lo ? 1 : 0) | bf_queue_bit(),
+                               (const char*)d_gd, gkind, d_gok);
         } else {
             // the first pass sized d_scratch for ncu * 4 blocks
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -2113,6 +2237,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
     if (d_ovf) (void)hipFree(d_ovf);
     if (d_stg) (void)hipFree(d_stg);
     if (d_dup) (void)hipFree(d_dup);
+    if (d_gok) (void)hipFree(d_gok);
     return SHD_OK;
 }
 
@@ -2169,7 +2294,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
-                                   (lo ? 1 : 0) | bf_queue_bit());
+                                   (lo ? 1 : 0) | bf_queue_bit(),
+                               (const char*)nullptr, 0, (const uint8_t*)nullptr);
             } else if (two_row_ok(pc)) {
                 // two rows per workgroup (sssp_bf2), row B parked in d_scratch
                 const size_t lds2 = two_row_lds(V);
@@ -2198,7 +2324,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached,
                                    pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
-                                   (lo ? 1 : 0) | bf_queue_bit());
+                                   (lo ? 1 : 0) | bf_queue_bit(),
+                               (const char*)nullptr, 0, (const uint8_t*)nullptr);
             }
         } else {
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
