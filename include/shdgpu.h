@@ -188,6 +188,11 @@ typedef struct shd_pc_info {
                                        predecessors) */
     int32_t n_tie_rows_global;      /* ... of them run again through lane heaps in global
                                        scratch (k_sssp_tie_parents: a heap past the LDS one) */
+    int32_t n_tie_rows_predicted;   /* ... of them listed without a first pass: a build on
+                                       whole-number weights whose probe rows (2 x CUs) were
+                                       90 % tied (round 6; their ties counted in the second
+                                       pass, sssp_iterations_max over the probe only) */
+    int32_t _pad0;
 } shd_pc_info;
 
 /* attached: vertex ids with >=1 attached host (topology.c:2393, verticesWithAttachedHosts) */

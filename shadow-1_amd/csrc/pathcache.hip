@@ -121,7 +121,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                              int32_t* fl_pre, int32_t* fl_beg, uint64_t* fl_dv /* LDS [BLOCK] each */,
                              const uint16_t* off16, const int32_t* cbase /* LDS arc offsets, or null */,
                              bool bfq /* queued frontier: four vertices a wave in flight */,
-                             int bf_it = -1 /* >= 0: dist holds the row's converged distances (sssp_bf2) */) {
+                             int bf_it = -1 /* >= 0: dist holds the row's converged distances (sssp_bf2) */,
+                             bool count_ties = false /* with fpar: count the row's ties all the same */) {
     const int tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6, hl = lane & 31;
     const bool upper = lane >= 32;
@@ -368,11 +369,13 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
     // 9.7 of the 29 ms of the 10 k-row table.)
     int64_t my_ties = 0;
     SST_T0(t_par)
-    if (fpar) {
+    if (fpar && !count_ties) {
         // the row's parents given (k_sssp_tie_parents: igraph's first relaxer
         // in its heap's pop order, for a row with equal-cost predecessors)
         for (int32_t v = tid; v < V; v += BLOCK) parent[v] = fpar[v];
     } else {
+        // (count_ties: a row sent to the tie kernel without a first pass -- its
+        // ties counted here, its parents the given ones, set below)
         uint32_t* cnt2 = (uint32_t*)upd;   // two 16-bit counts per word (the BF stamps are done with)
         for (int32_t w = tid; w < (V + 1) / 2; w += BLOCK) cnt2[w] = 0;
         __syncthreads();
@@ -397,7 +400,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                 if (dub == kDistInf) continue;
                 if (u2d(dub) + ww[j] == u2d(dist[x])) {
                     atomicAdd(&cnt2[x >> 1], 1u << ((x & 1) * 16));
-                    parent[x] = arc_rin[k];
+                    if (!fpar) parent[x] = arc_rin[k];
                 }
             }
         }
@@ -420,8 +423,12 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                     }
                 }
             }
-            parent[v] = best;
+            if (!fpar) parent[v] = best;
             if (nbest > 1) my_ties++;
+        }
+        if (fpar) {
+            __syncthreads();
+            for (int32_t v = tid; v < V; v += BLOCK) parent[v] = fpar[v];
         }
     }
     if (my_ties) {
@@ -631,7 +638,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
     const int32_t* __restrict__ self_eid, shd_pv* __restrict__ out,
     int64_t* __restrict__ stats, int32_t row0, int32_t row1, const int32_t* __restrict__ row_list,
     const int32_t* __restrict__ fpar, int32_t* __restrict__ tie_rows, int mode /* bit 0 LDS offsets, 1 queued */,
-    const char* __restrict__ gdist, int gkind, const uint8_t* __restrict__ gok) {
+    const char* __restrict__ gdist, int gkind, const uint8_t* __restrict__ gok, int32_t cnt_from) {
     // gdist (round 6): the tied rows' distances from k_sssp_tie_g's per-row entries
     // (gkind 4: TieG<int32_t>, 8: TieG<double>), for the rows gok marks complete --
     // no Bellman-Ford again for them, only the properties over the given parents
@@ -685,7 +692,7 @@ __global__ __launch_bounds__(BLOCK) void k_sssp_rows_lds(
                             rin_eid,
                             rin_w, rin_r, w_e, eloss, vloss, attached, self_eid, out, stats, dist,
                             parent, upd, flags, fpar ? fpar + (size_t)(i - row0) * V : nullptr, tie_rows, fl_pre,
-                            fl_beg, fl_dv, off16, cbase, (mode & 2) != 0, bf_it);
+                            fl_beg, fl_dv, off16, cbase, (mode & 2) != 0, bf_it, fpar && i - row0 >= cnt_from);
     }
 }
 
@@ -1451,6 +1458,10 @@ __device__ __forceinline__ TieG<HV> tg_load(const TieG<HV>* g, int32_t x) {
         __builtin_amdgcn_wave_barrier();                         \
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   \
     } while (0)
+__global__ void k_iota(int32_t* __restrict__ out, int32_t n, int32_t base) {
+    const int32_t k = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (k < n) out[k] = base + k;
+}
 // per arc: does an earlier arc of its source's list, in the same 64-arc chunk
 // (chunks from the list's start), go to the same vertex (a parallel edge the
 // tie kernel's chunk must take in order); computed once per tied build
@@ -2042,7 +2053,9 @@ static size_t lds_launch_bytes(const shd_pc* pc, bool* ldsoff) {
 // The rows the first pass listed (equal-cost predecessors somewhere in the
 // row): their parents from k_sssp_tie_parents, in chunks of rows whose heaps
 // fit a bounded scratch, then the row kernel again with those parents.
-static int finish_tie_rows(shd_pc* pc, int ncu) {
+// cnt_from: tie-list entries from this index on were listed without a first
+// pass (a predicted all-tied build): the second pass counts their ties
+static int finish_tie_rows(shd_pc* pc, int ncu, int64_t cnt_from) {
     hipStream_t s = pc->stream;
     const int32_t V = pc->V, T = pc->T;
     int64_t n = 0;
@@ -2213,7 +2226,8 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
                                pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr,
                                (lo ? 1 : 0) | bf_queue_bit(),
-                               (const char*)d_gd, gkind, d_gok);
+                               (const char*)d_gd, gkind, d_gok,
+                               (int32_t)std::min<int64_t>(INT32_MAX, std::max<int64_t>(-1, cnt_from - c0)));
         } else if (lds_rows <= kLdsMax) {
             const int grid = std::max(1, std::min(cn, ncu));
             hipLaunchKernelGGL(k_sssp_rows_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds, s, V, T, pc->d_arc_off,
@@ -2221,7 +2235,8 @@ static int finish_tie_rows(shd_pc* pc, int ncu) {
                                pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w, pc->d_eloss, pc->d_vloss,
                                pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats, 0, cn, rows, fpar, nullptr,
                                (lo ? 1 : 0) | bf_queue_bit(),
-                               (const char*)d_gd, gkind, d_gok);
+                               (const char*)d_gd, gkind, d_gok,
+                               (int32_t)std::min<int64_t>(INT32_MAX, std::max<int64_t>(-1, cnt_from - c0)));
         } else {
             // the first pass sized d_scratch for ncu * 4 blocks
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -2279,6 +2294,8 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
     SHD_HIP(hipEventRecord(ev[1], s));
     if (pc->rows_mode) {
         bool lo = false;
+        int64_t cnt_from = INT64_MAX;   // (a predicted all-tied build: the tie list's unprobed rows)
+        pc->info.n_tie_rows_predicted = 0;
         const size_t lds_rows = lds_bytes_for(V), lds = lds_launch_bytes(pc, &lo);
         int ncu = 256;
         hipDeviceProp_t prop;
@@ -2295,12 +2312,20 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
                                    (lo ? 1 : 0) | bf_queue_bit(),
-                               (const char*)nullptr, 0, (const uint8_t*)nullptr);
+                               (const char*)nullptr, 0, (const uint8_t*)nullptr, 0);
             } else if (two_row_ok(pc)) {
                 // two rows per workgroup (sssp_bf2), row B parked in d_scratch
                 const size_t lds2 = two_row_lds(V);
                 const int grid = std::max(1, std::min((row1 - row0 + 1) / 2, ncu));
                 const size_t park = (size_t)grid * V * sizeof(uint64_t);
+                // A predicted all-tied build (round 6): on whole-number weights the first
+                // pass runs one probe of 2 x CUs rows; when 90 % of them tie, the other
+                // rows go to the tie kernel without a first pass (whose Bellman-Ford a
+                // tied row only used to be listed), and the second pass counts their
+                // ties (SHD_PC_NO_TIE_PREDICT: the first pass over every row)
+                const bool predict = pc->w_int && W == 1 && !getenv("SHD_PC_NO_TIE_PREDICT") &&
+                                     row1 - row0 > 8 * grid;
+                const int32_t prow1 = predict ? row0 + 2 * grid : row1;
                 if (!pc->d_scratch || pc->scratch_bytes < park) {
                     if (pc->d_scratch) (void)hipFree(pc->d_scratch);
                     pc->d_scratch = nullptr;
@@ -2314,7 +2339,29 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin,
                                    pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r, pc->d_w,
                                    pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid, pc->d_row, pc->d_stats,
-                                   row0, row1, pc->d_tie_rows, (uint64_t*)pc->d_scratch);
+                                   row0, prow1, pc->d_tie_rows, (uint64_t*)pc->d_scratch);
+                if (predict) {
+                    SHD_HIP(hipGetLastError());
+                    int64_t nt = 0;
+                    SHD_HIP(hipMemcpyAsync(&nt, pc->d_stats + 6, sizeof(nt), hipMemcpyDeviceToHost, s));
+                    SHD_HIP(hipStreamSynchronize(s));
+                    if (nt * 10 >= (int64_t)(prow1 - row0) * 9) {
+                        const int32_t nr = row1 - prow1;
+                        hipLaunchKernelGGL(k_iota, dim3((nr + 255) / 256), dim3(256), 0, s, pc->d_tie_rows + nt, nr,
+                                           prow1);
+                        const int64_t tot = nt + nr;
+                        SHD_HIP(hipMemcpyAsync(pc->d_stats + 6, &tot, sizeof(tot), hipMemcpyHostToDevice, s));
+                        cnt_from = nt;
+                        pc->info.n_tie_rows_predicted = nr;
+                    } else {
+                        hipLaunchKernelGGL(k_sssp_rows2_lds<kRowBlock>, dim3(grid), dim3(kRowBlock), lds2, s, V, T,
+                                           pc->d_arc_off, pc->d_arc_dst, pc->d_arc_w, pc->d_arc_src, pc->d_arc_rin,
+                                           pc->d_rin_off, pc->d_rin_src, pc->d_rin_eid, pc->d_rin_w, pc->d_rin_r,
+                                           pc->d_w, pc->d_eloss, pc->d_vloss, pc->d_attached, pc->d_self_eid,
+                                           pc->d_row, pc->d_stats, prow1, row1, pc->d_tie_rows,
+                                           (uint64_t*)pc->d_scratch);
+                    }
+                }
             } else {
                 int grid = std::max(1, std::min(row1 - row0, ncu));
                 SHD_HIP(hipFuncSetAttribute((const void*)k_sssp_rows_lds<kRowBlock>,
@@ -2325,7 +2372,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                    pc->d_self_eid,
                                    pc->d_row, pc->d_stats, row0, row1, nullptr, nullptr, pc->d_tie_rows,
                                    (lo ? 1 : 0) | bf_queue_bit(),
-                               (const char*)nullptr, 0, (const uint8_t*)nullptr);
+                               (const char*)nullptr, 0, (const uint8_t*)nullptr, 0);
             }
         } else {
             const size_t per_block = ((size_t)14 * V + 255) & ~(size_t)255;
@@ -2342,7 +2389,7 @@ static int pc_build(shd_pc* pc, shd_comm* comm) {
                                pc->d_tie_rows, bf_queue_bit());
         }
         SHD_HIP(hipGetLastError());
-        const int rc = finish_tie_rows(pc, ncu);
+        const int rc = finish_tie_rows(pc, ncu, cnt_from);
         if (rc) { for (auto& e : ev) (void)hipEventDestroy(e); return rc; }
     }
     SHD_HIP(hipEventRecord(ev[2], s));

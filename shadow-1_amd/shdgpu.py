@@ -97,6 +97,7 @@ class PcInfo(C.Structure):
         ("build_ms_device", C.c_double), ("build_ms_sssp", C.c_double),
         ("build_ms_props", C.c_double), ("build_ms_direct", C.c_double),
         ("n_tie_rows", C.c_int32), ("n_tie_rows_global", C.c_int32),
+        ("n_tie_rows_predicted", C.c_int32), ("_pad0", C.c_int32),
     ]
 
 

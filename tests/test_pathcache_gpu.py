@@ -156,6 +156,25 @@ def test_tie_rows_bit_exact_on_the_lane_heap_kernel(name, monkeypatch):
     test_tie_rows_bit_exact(name)
 
 
+def test_predicted_all_tied_build_equals_the_first_pass_over_every_row(monkeypatch):
+    # round 6: on whole-number weights a probe of 2 x CUs rows runs the first
+    # pass; when 90 % tie, the other rows go to the tie kernel without one and
+    # the second pass counts their ties.  Same table, same tie count as the
+    # first pass over every row (SHD_PC_NO_TIE_PREDICT)
+    g = W.geometric_graph(5000, seed=6, integer_latency=True)
+    att = np.arange(g.n_vertices, dtype=np.int32)
+    pc = PathCache(g, att)
+    a = pc.info()
+    lat, rel = pc.rows()
+    monkeypatch.setenv("SHD_PC_NO_TIE_PREDICT", "1")
+    pc2 = PathCache(g, att)
+    b = pc2.info()
+    lat2, rel2 = pc2.rows()
+    assert a.n_tie_rows_predicted > 0 and b.n_tie_rows_predicted == 0
+    assert a.n_ties == b.n_ties and a.max_hops == b.max_hops and a.n_unroutable == b.n_unroutable
+    assert same_bits(lat, lat2) and same_bits(rel, rel2)
+
+
 def test_tie_rows_heap_past_lds_falls_back_bit_exact():
     # two hubs joined to every leaf at one whole millisecond: from a leaf, the
     # other leaves tie (both hubs are exact predecessors) and the heap holds
