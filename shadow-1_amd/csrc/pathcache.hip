@@ -373,9 +373,52 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
         // the row's parents given (k_sssp_tie_parents: igraph's first relaxer
         // in its heap's pop order, for a row with equal-cost predecessors)
         for (int32_t v = tid; v < V; v += BLOCK) parent[v] = fpar[v];
+    } else if (fpar) {
+        // count_ties: a row sent to the tie kernel without a first pass (a
+        // predicted all-tied build, on whole-number weights: every distance an
+        // exact integer below 2^30) -- its ties counted, its parents the given
+        // ones.  A tie: two or more exact predecessors at the least exact
+        // predecessor distance; per vertex that least distance (32-bit atomicMin
+        // in parent[]), then the exact predecessors at it (16-bit counts in upd):
+        // two streaming passes over the arcs instead of an in-arc walk per vertex
+        uint32_t* mind = (uint32_t*)parent;
+        uint32_t* cnt2 = (uint32_t*)upd;
+        for (int32_t v = tid; v < V; v += BLOCK) mind[v] = 0xFFFFFFFFu;
+        for (int32_t w = tid; w < (V + 1) / 2; w += BLOCK) cnt2[w] = 0;
+        __syncthreads();
+        const int32_t na = arc_off[V];
+        for (int pass = 0; pass < 2; pass++) {
+            for (int32_t k0 = tid; k0 < na; k0 += 4 * BLOCK) {
+                int32_t uu[4], xx[4];
+                double ww[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int32_t k = min(k0 + j * BLOCK, na - 1);
+                    uu[j] = arc_src[k];
+                    xx[j] = arc_dst[k];
+                    ww[j] = arc_w[k];
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int32_t k = k0 + j * BLOCK;
+                    if (k >= na) break;
+                    const int32_t x = xx[j];
+                    if (x == src) continue;
+                    const uint64_t dub = dist[uu[j]];
+                    if (dub == kDistInf) continue;
+                    if (u2d(dub) + ww[j] != u2d(dist[x])) continue;
+                    const uint32_t du = (uint32_t)u2d(dub);
+                    if (pass == 0) atomicMin(&mind[x], du);
+                    else if (du == mind[x]) atomicAdd(&cnt2[x >> 1], 1u << ((x & 1) * 16));
+                }
+            }
+            __syncthreads();
+        }
+        for (int32_t v = tid; v < V; v += BLOCK)
+            if (upd[v] > 1) my_ties++;
+        __syncthreads();
+        for (int32_t v = tid; v < V; v += BLOCK) parent[v] = fpar[v];
     } else {
-        // (count_ties: a row sent to the tie kernel without a first pass -- its
-        // ties counted here, its parents the given ones, set below)
         uint32_t* cnt2 = (uint32_t*)upd;   // two 16-bit counts per word (the BF stamps are done with)
         for (int32_t w = tid; w < (V + 1) / 2; w += BLOCK) cnt2[w] = 0;
         __syncthreads();
@@ -400,7 +443,7 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                 if (dub == kDistInf) continue;
                 if (u2d(dub) + ww[j] == u2d(dist[x])) {
                     atomicAdd(&cnt2[x >> 1], 1u << ((x & 1) * 16));
-                    if (!fpar) parent[x] = arc_rin[k];
+                    parent[x] = arc_rin[k];
                 }
             }
         }
@@ -423,12 +466,8 @@ __device__ void sssp_one_row(int32_t row, int32_t src, int32_t V, int32_t T,
                     }
                 }
             }
-            if (!fpar) parent[v] = best;
+            parent[v] = best;
             if (nbest > 1) my_ties++;
-        }
-        if (fpar) {
-            __syncthreads();
-            for (int32_t v = tid; v < V; v += BLOCK) parent[v] = fpar[v];
         }
     }
     if (my_ties) {
