@@ -184,7 +184,7 @@ typedef struct shd_pc_info {
     double build_ms_props;          /* device time of the path-properties kernel */
     double build_ms_direct;         /* device time of the direct-table kernel   */
     int32_t n_tie_rows;             /* rows whose parents came from the restated igraph heap
-                                       (k_sssp_tie_lds / k_sssp_tie_parents: equal-cost
+                                       (k_sssp_tie_g / k_sssp_tie_parents: equal-cost
                                        predecessors) */
     int32_t n_tie_rows_global;      /* ... of them run again through lane heaps in global
                                        scratch (k_sssp_tie_parents: a heap past the LDS one) */
