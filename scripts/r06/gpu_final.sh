@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 6, final tree: the whole GPU suite, smoke(), then the driver's default bench line (C3 headline)
 set -o pipefail
-O=gpurun_out/r06_final
+O=${O:-gpurun_out/r06_final}
 rm -rf $O; mkdir -p $O
 timeout -k 10 1100 python3 -u -m pytest tests -x -q -m gpu --timeout 600 --timeout-method thread \
     > $O/tests.log 2>&1; rc=$?; echo "pytest rc=$rc" >> $O/tests.log
