@@ -106,3 +106,18 @@ def test_model_struct_layout_matches_the_header(tmp_path):
     assert got == [C.sizeof(S.Model), S.Model.app_peer.offset, S.Model.app_spec.offset, S.Model.host_app.offset,
                    S.Model.n_app_specs.offset, C.sizeof(S.UdpApp), C.sizeof(S.RunStats),
                    S.RunStats.n_rounds_replayed.offset]
+
+
+def test_pc_info_layout_matches_the_header(tmp_path):
+    # the ctypes mirror of shd_pc_info (round 6 added n_tie_rows_predicted) against gcc's layout
+    import ctypes as C
+    src = tmp_path / "p.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "%s/include/shdgpu.h"\n'
+                   'int main(void){printf("%%zu %%zu %%zu %%zu\\n", sizeof(shd_pc_info),'
+                   ' offsetof(shd_pc_info, n_tie_rows), offsetof(shd_pc_info, n_tie_rows_global),'
+                   ' offsetof(shd_pc_info, n_tie_rows_predicted));return 0;}\n' % REPO)
+    exe = tmp_path / "p"
+    subprocess.run(["gcc", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [C.sizeof(S.PcInfo), S.PcInfo.n_tie_rows.offset, S.PcInfo.n_tie_rows_global.offset,
+                   S.PcInfo.n_tie_rows_predicted.offset]
