@@ -2165,9 +2165,19 @@ static int finish_tie_rows(shd_pc* pc, int ncu, int64_t cnt_from) {
         SHD_HIP(hipMalloc(&pc->d_tie_scratch, need));
         pc->tie_scratch_bytes = need;
     }
+    // the call's temporary device buffers, freed on every return (an error return
+    // too; hipFree waits for the device, so no kernel of the call still uses them)
+    struct TmpBufs {
+        void* p[4] = {nullptr, nullptr, nullptr, nullptr};
+        ~TmpBufs() {
+            for (void* q : p)
+                if (q) (void)hipFree(q);
+        }
+    } tmp;
     int32_t* d_ovf = nullptr;
     if (hc) {   // [0]: the count, then the slots of the rows whose heap outgrew hc
         SHD_HIP(hipMalloc(&d_ovf, sizeof(int32_t) * (1 + (size_t)chunk)));
+        tmp.p[0] = d_ovf;
         SHD_HIP(hipFuncSetAttribute(tie_fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tl_lds));
     }
     // STG: V states per block of the grid; k_sssp_tie_g: V entries per row of a
@@ -2180,7 +2190,11 @@ static int finish_tie_rows(shd_pc* pc, int ncu, int64_t cnt_from) {
         const size_t g = tg ? (size_t)std::min<int64_t>(chunk, n)
                             : (size_t)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(chunk, n), (int64_t)ncu * bpc));
         SHD_HIP(hipMalloc(&d_stg, g * (size_t)V * (tg ? g_entry : sizeof(uint16_t))));
-        if (tg) SHD_HIP(hipMalloc(&d_gok, g));
+        tmp.p[1] = d_stg;
+        if (tg) {
+            SHD_HIP(hipMalloc(&d_gok, g));
+            tmp.p[2] = d_gok;
+        }
     }
     const char* d_gd = (tg && !getenv("SHD_PC_TIE_NOGD")) ? (const char*)d_stg : nullptr;
     const int gkind = d_gd ? (hv4 ? 4 : 8) : 0;
@@ -2190,6 +2204,7 @@ static int finish_tie_rows(shd_pc* pc, int ncu, int64_t cnt_from) {
         SHD_HIP(hipMemcpyAsync(&na, pc->d_arc_off + V, sizeof(int32_t), hipMemcpyDeviceToHost, s));
         SHD_HIP(hipStreamSynchronize(s));
         SHD_HIP(hipMalloc(&d_dup, (size_t)na + 1));
+        tmp.p[3] = d_dup;
         if (na > 0) {
             hipLaunchKernelGGL(k_arc_dup, dim3((na + 255) / 256), dim3(256), 0, s, na, pc->d_arc_off, pc->d_arc_src,
                                pc->d_arc_dst, d_dup);
@@ -2288,10 +2303,6 @@ static int finish_tie_rows(shd_pc* pc, int ncu, int64_t cnt_from) {
         }
         SHD_HIP(hipGetLastError());
     }
-    if (d_ovf) (void)hipFree(d_ovf);
-    if (d_stg) (void)hipFree(d_stg);
-    if (d_dup) (void)hipFree(d_dup);
-    if (d_gok) (void)hipFree(d_gok);
     return SHD_OK;
 }
 
