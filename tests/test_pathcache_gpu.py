@@ -120,8 +120,16 @@ def test_lazy_lookup_first_touch_matches_reference_cache():
 # order, which the row kernel's rule (smallest d[u], then lowest edge id) does
 # not see; such rows are rerun through k_sssp_tie_parents (the restated
 # igraph_2wheap Dijkstra) and must equal the oracle bit for bit.
+def _half_ms(g):
+    # the same graph at half the latencies: ties kept (k / 2 is exact), the weights no
+    # longer whole numbers -- the tie kernel's 8-B heap values, no predicted build
+    return S.GraphArrays(g.n_vertices, g.src, g.dst, g.latency * 0.5, g.loss, g.vertex_loss, directed=g.directed)
+
+
 TIE_GRAPHS = {
     "grid6": lambda: W.grid_graph(6),
+    "grid6_half_ms": lambda: _half_ms(W.grid_graph(6)),
+    "geo_half_ms_300": lambda: _half_ms(W.geometric_graph(300, seed=3, integer_latency=True)),
     "grid6_directed": lambda: W.grid_graph(6, directed=True),
     "grid6_parallel": lambda: W.grid_graph(6, parallel=True),
     "grid30": lambda: W.grid_graph(30, seed=2),
